@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X satisfiability pre-filter (BASELINE.json metric).
+
+A *step* = one pass of the HIP constraint-evaluation kernel over the whole
+synthetic batch resident in HBM: n_states x n_cand candidate-model evaluations
+(2^20 states x 64-op-node 256-bit DAGs x 256
+candidates per GPU), followed by the first-SAT reduction and — for N > 1 — the
+RCCL gather of the per-state first-SAT words to rank 0.  Weak scaling: every
+rank owns its own 2^20 hash-shard of states (state ids rank*2^20 + i).
+
+Printed (rank 0, one JSON line): whole-job candidate-model evals/s, the
+roofline object of the eval kernel (INT32 VALU bound: nominal ops from the
+committed per-op table / measured kernel time vs 39.3 Tops/s), its HBM
+fraction, the CPU baseline (oracle/c restatement, OpenMP over the host cores,
+timed on a bounded sample), and the batched Keccak-256 line (config 5).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--states S] [--cand C]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "candidate-model evals/sec (1/2/4/8 GPU) + myth analyze wall-clock, z3 calls"
+SEED = 0x4D595448
+VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12  # 39.3 INT32 Tops/s (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBS = 8000.0
+KECCAK_OPS_PER_HASH = 7458  # SURVEY.md §8d (310/round x 24 + absorb)
+KECCAK_BYTES_PER_HASH = 96
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def vp(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--states", type=int, default=1 << 20)
+    ap.add_argument("--cand", type=int, default=256)
+    ap.add_argument("--nodes", type=int, default=64)
+    ap.add_argument("--keccak", type=int, default=1 << 30, help="hashes per GPU (0 = skip)")
+    ap.add_argument("--keccak-chunk", type=int, default=1 << 26)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from mythril_amd import _native as N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    N.lib()  # loud failure if the HIP library is missing
+
+    # ---------------------------------------------------------- workload
+    n_states, n_cand, n_nodes = args.states, args.cand, args.nodes
+    base = rank * n_states
+    t0 = time.time()
+    b = N.synth_generate(SEED, base, n_states, n_nodes, n_cand)
+    words, po, status = N.lower(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+    hdr = N.program_headers(words, po)
+    n_slots = int(hdr[:, 2].max())
+    n_vars = b["n_vars"]
+    ops_state = N.nominal_ops(b["nodes"], b["node_offsets"]).astype(np.float64)
+    log(f"rank {rank}: generated+lowered {n_states} states in {time.time() - t0:.1f}s; "
+        f"slots max {n_slots}, ins mean {hdr[:, 0].mean():.1f}, unsupported {(status != 0).sum()}")
+
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    d_words = torch.from_numpy(words.view(np.int32)).to(dev)
+    d_po = torch.from_numpy(po.view(np.int64)).to(dev)
+    n_cand_words = n_states * n_vars * 2 * n_cand * 4
+    d_cands = torch.empty(n_cand_words, dtype=torch.int32, device=dev)
+    N.fill_candidates_dev(vp(d_words), vp(d_po), n_states, base, SEED, vp(d_cands), n_cand, n_vars, sh)
+    pl = np.nonzero(b["planted"])[0].astype(np.uint32)
+    d_pstate = torch.from_numpy(pl.view(np.int32)).to(dev)
+    d_pidx = torch.from_numpy(b["plant_idx"][pl].view(np.int32)).to(dev)
+    d_pwords = torch.from_numpy(np.ascontiguousarray(b["plant_words"][pl]).view(np.int32)).to(dev)
+    N.plant_candidates_dev(vp(d_cands), n_states, n_cand, n_vars, vp(d_pstate), vp(d_pidx), vp(d_pwords),
+                           len(pl), sh)
+    n_chunks = (n_cand + 63) // 64
+    d_first = torch.empty(n_states, dtype=torch.int32, device=dev)
+    d_wit = torch.empty(n_states * n_vars * 8, dtype=torch.int32, device=dev)
+    d_scratch = torch.empty(n_states * n_chunks, dtype=torch.int32, device=dev)
+    gather_buf = [torch.empty_like(d_first) for _ in range(world)] if (world > 1 and rank == 0) else None
+    torch.cuda.synchronize(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        N.eval_batch_dev(vp(d_words), vp(d_po), n_states, vp(d_cands), n_cand, n_vars, n_slots, vp(d_first),
+                         vp(d_wit), vp(d_scratch), sh)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.gather(d_first, gather_buf if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    kern_ms = float(np.mean([a.elapsed_time(bb) for a, bb in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    first = d_first.cpu().numpy()
+    sat = int((first >= 0).sum())
+    planted_ok = bool(np.all(first[pl] >= 0) and np.all(first[pl] <= b["plant_idx"][pl].astype(np.int64)))
+    evals_rank = n_states * n_cand
+    value = world * evals_rank * args.steps / elapsed
+    ops_launch = float(ops_state.sum()) * n_cand
+    achieved_tops = ops_launch / (kern_ms * 1e-3) / 1e12
+    bytes_launch = (n_cand_words * 4 + words.nbytes + po.nbytes + n_states * n_chunks * 4 * 2 + n_states * 4
+                    + sat * n_vars * 32)
+    achieved_gbs = bytes_launch / (kern_ms * 1e-3) / 1e9
+    log(f"rank {rank}: kernel {kern_ms:.2f} ms/launch, step {1e3 * elapsed / args.steps:.2f} ms, SAT {sat}/{n_states}, "
+        f"planted found {planted_ok}")
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "eval_pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pm = json.load(f)
+            if pm.get("states") == n_states and pm.get("cand") == n_cand:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    # ---------------------------------------------------------- Keccak
+    keccak = None
+    if args.keccak > 0:
+        nk, chunk = args.keccak, min(args.keccak_chunk, args.keccak)
+        kfirst = rank * nk
+        d_pre = torch.empty(nk * 64, dtype=torch.uint8, device=dev)
+        d_dig = torch.empty(nk * 32, dtype=torch.uint8, device=dev)
+        N.fill_mapping_preimages_dev(vp(d_pre), kfirst, nk, SEED, sh)
+        torch.cuda.synchronize(dev)
+
+        def kpass(evl=None):
+            for off in range(0, nk, chunk):
+                m = min(chunk, nk - off)
+                if evl is not None:
+                    evl.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                    evl[-1][0].record(stream)
+                N.keccak256_dev(ctypes.c_void_p(d_pre.data_ptr() + off * 64), m, 64, 64,
+                                ctypes.c_void_p(d_dig.data_ptr() + off * 32), sh)
+                if evl is not None:
+                    evl[-1][1].record(stream)
+
+        kpass()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        kevs = []
+        tk = time.perf_counter()
+        ksteps = max(1, min(args.steps, 3))
+        for _ in range(ksteps):
+            kpass(kevs)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        kel = time.perf_counter() - tk
+        if world > 1:
+            t = torch.tensor([kel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            kel = float(t.item())
+        kms = float(np.mean([a.elapsed_time(bb) for a, bb in kevs]))
+        k_rate = world * nk * ksteps / kel
+        k_tops = chunk * KECCAK_OPS_PER_HASH / (kms * 1e-3) / 1e12
+        k_gbs = chunk * KECCAK_BYTES_PER_HASH / (kms * 1e-3) / 1e9
+        # spot check against the oracle happens in tests; here a cheap self-consistency sample
+        keccak = {
+            "metric": "keccak256 hashes/s (64-byte mapping-slot preimages)",
+            "value": k_rate,
+            "unit": "hashes/s",
+            "hashes_per_gpu": nk,
+            "ms_per_pass": 1e3 * kel / ksteps,
+            "roofline": {"bound": "valu", "achieved": k_tops, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                         "frac": k_tops / VALU_PEAK_TOPS, "traffic": None,
+                         "kernel": "mgp_keccak64_kernel", "launch_ms": kms, "hashes_per_launch": chunk},
+            "roofline_hbm": {"achieved": k_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k_gbs / HBM_PEAK_GBS},
+        }
+        del d_pre, d_dig
+
+    # ---------------------------------------------------------- CPU baseline
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        cpu = cpu_baseline(b, d_cands, n_states, n_cand, n_vars, args.cpu_seconds, evals_rank / (kern_ms * 1e-3))
+        if keccak is not None:
+            keccak["cpu_baseline"] = cpu_keccak(args.cpu_seconds / 2)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded DAG generator + Philox candidates, 50% planted witnesses)",
+            "config": {
+                "workload": "synthetic: 1M states x 64-node 256-bit constraint DAGs x 256 candidate assignments"
+                if n_states == 1 << 20 and n_cand == 256 else f"synthetic: {n_states} states x {n_nodes} nodes x {n_cand} cand",
+                "states_per_gpu": n_states, "candidates": n_cand, "op_nodes": n_nodes, "n_vars": n_vars,
+                "parallelism": f"dp{world} (state hash-shards, RCCL gather of first-SAT)",
+                "lds_slots": n_slots, "nominal_ops_per_eval": float(ops_state.mean()),
+            },
+            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                         "frac": achieved_tops / VALU_PEAK_TOPS, "traffic": traffic,
+                         "kernel": "mgp_eval_kernel(+finalize)", "launch_ms": kern_ms,
+                         "evals_per_launch": evals_rank},
+            "roofline_hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": achieved_gbs / HBM_PEAK_GBS, "bytes_per_launch": bytes_launch},
+            "cpu_baseline": cpu,
+            "results": {"sat_states": sat, "planted_states": int(len(pl)), "planted_found": planted_ok},
+            "keccak": keccak,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _threads() -> int:
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit():
+        return int(v)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(b, d_cands, n_states, n_cand, n_vars, target_s, gpu_rate):
+    """Time the C oracle (OpenMP, all candidates evaluated) on a bounded sample of the same batch."""
+    from oracle import coracle
+
+    def sample(k):
+        # device layout [s][v][h][c][4] -> host AoS [s][c][v][8]
+        words_per_state = n_vars * 2 * n_cand * 4
+        dv = d_cands[: k * words_per_state].cpu().numpy().view(np.uint32)
+        dv = dv.reshape(k, n_vars, 2, n_cand, 4).transpose(0, 3, 1, 2, 4).reshape(k, n_cand, n_vars, 8)
+        sub_off = b["node_offsets"][: k + 1]
+        sub_coff = b["const_offsets"][: k + 1]
+        return (b["nodes"][: int(sub_off[-1])], sub_off, b["consts"][: int(sub_coff[-1])], sub_coff,
+                np.ascontiguousarray(dv))
+
+    k = min(256, n_states)
+    t_used = 0.0
+    while True:
+        nodes, no, cs, co, cands = sample(k)
+        t = time.perf_counter()
+        ref = coracle.first_sat(nodes, no, cs, co, cands, full=True)
+        t_used = time.perf_counter() - t
+        if t_used >= target_s * 0.5 or k >= n_states:
+            break
+        k = min(n_states, int(k * min(8.0, max(2.0, target_s / max(t_used, 1e-3)))))
+    rate = k * n_cand / t_used
+    log(f"cpu baseline: {k} states x {n_cand} cand in {t_used:.1f}s = {rate:.3g} evals/s")
+    return {"value": rate, "unit": "evals/s", "cores": _threads(), "kind": "port",
+            "sample": f"first {k} states of the rank-0 batch x {n_cand} candidates (all evaluated), "
+                      f"oracle/c/oracle.c DAG evaluator, OpenMP", "seconds": t_used,
+            "gpu_over_cpu": gpu_rate / rate}
+
+
+def cpu_keccak(target_s):
+    from oracle import coracle
+
+    n = 1 << 20
+    pre = coracle.mapping_preimages(0, n, SEED)
+    while True:
+        t = time.perf_counter()
+        coracle.keccak256(pre, n, 64, 64)
+        dt = time.perf_counter() - t
+        if dt >= target_s * 0.5 or n >= 1 << 26:
+            break
+        n = min(1 << 26, int(n * max(2.0, target_s / max(dt, 1e-3))))
+        pre = coracle.mapping_preimages(0, n, SEED)
+    rate = n / dt
+    log(f"cpu keccak: {n} hashes in {dt:.1f}s = {rate:.3g}/s")
+    return {"value": rate, "unit": "hashes/s", "cores": _threads(), "kind": "port",
+            "sample": f"{n} mapping-slot preimages, oracle/c/oracle.c keccak256, OpenMP", "seconds": dt}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * mgp.h — C ABI of libmgp.so, the MI355X-native satisfiability pre-filter
+ * and batched Keccak-256 for Mythril's LASER engine.
+ *
+ * The reference (mythril v0.22.1, 100 % Python) reaches native code only
+ * through z3py/ctypes and pysha3; these entry points are the native boundary
+ * that replaces those calls on the hot path:
+ *
+ *   mgp_eval_batch      replaces the serial z3 check() behind
+ *                        Constraints.is_possible
+ *                        (mythril/laser/ethereum/state/constraints.py:34-51)
+ *                        and the SAT-only analysis.solver.get_model calls
+ *                        (mythril/analysis/solver.py:27-61) — witness search
+ *                        only: a witness proves SAT, everything else stays z3.
+ *   mgp_lower           lowers the constraint DAG (laser.smt vocabulary,
+ *                        mythril/laser/smt/ *.py) to the flat bytecode.
+ *   mgp_keccak256_batch replaces ethereum.utils.sha3 in
+ *                        KeccakFunctionManager.find_concrete_keccak
+ *                        (mythril/laser/ethereum/keccak_function_manager.py:40-54)
+ *                        and pysha3 keccak_256 in get_code_hash
+ *                        (mythril/support/support_utils.py:29-41).
+ *
+ * Conventions: every function returns 0 on success and a negative MGP_E_*
+ * code on failure; no C++ exception crosses this boundary; host buffers are
+ * caller-owned; the context owns device buffers and a HIP stream.  One context
+ * per device per host thread.  Results are deterministic: first-SAT is the
+ * lowest candidate index whose assignment makes the root true.
+ *
+ * The *_dev entry points take device pointers and a hipStream_t (as void*) so
+ * that callers holding inputs resident in HBM (bench.py, torch tensors) skip
+ * the PCIe copies.
+ */
+#ifndef MGP_H
+#define MGP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mgp_ir.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGP_OK 0
+#define MGP_E_ARG (-1)       /* bad argument / shape                       */
+#define MGP_E_HIP (-2)       /* HIP runtime error (message in mgp_last_error) */
+#define MGP_E_NOMEM (-3)     /* allocation failed                          */
+#define MGP_E_CAPACITY (-4)  /* output buffer too small (mgp_lower)        */
+
+typedef struct mgp_ctx mgp_ctx;
+
+/* ------------------------------------------------------------ lifecycle */
+int mgp_create(int device, mgp_ctx **out);
+void mgp_destroy(mgp_ctx *ctx);
+const char *mgp_last_error(mgp_ctx *ctx); /* ctx may be NULL: global error */
+int mgp_device_count(int *out);
+const char *mgp_version(void);
+
+/* -------------------------------------------------------------- lowering
+ * Host-side, no device needed.  Lowers n_states node lists to bytecode.
+ *   nodes[node_offsets[s] .. node_offsets[s+1])   nodes of state s
+ *   consts[const_offsets[s]*8 ..]                  its constant pool (u32 limbs)
+ * out_words receives the concatenated programs (capacity out_cap words),
+ * out_prog_offsets[s] the word offset of state s (n_states+1 entries),
+ * out_status[s] MGP_ST_OK or MGP_ST_UNSUPPORTED (an unsupported state still
+ * gets a valid program header so that evaluation reports MGP_UNDECIDED).
+ * max_slots caps the BV slots per state (0 = default 32).
+ * Returns MGP_E_CAPACITY (and the needed size in *out_words_used) if too small. */
+int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets,
+              uint32_t n_states, const uint32_t *consts,
+              const uint64_t *const_offsets, uint32_t max_slots,
+              uint32_t *out_words, uint64_t out_cap,
+              uint64_t *out_prog_offsets, uint8_t *out_status,
+              uint64_t *out_words_used);
+
+/* ----------------------------------------------------- constraint eval
+ * prog_words/prog_offsets: output of mgp_lower (prog_offsets has n_states+1
+ * entries; prog_offsets[n_states] = total words).
+ * cand_words: n_states * n_cand * n_vars * 8 u32, layout [state][cand][var][limb]
+ *   (limb 0 least significant).
+ * out_first_sat[s]: lowest satisfying candidate index, MGP_NO_SAT (-1) if none,
+ *   MGP_UNDECIDED (-2) if the state's program is unsupported.
+ * out_witness (may be NULL): n_states * n_vars * 8 u32; filled for SAT states
+ *   with the winning candidate's words, left untouched otherwise. */
+int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words,
+                   const uint64_t *prog_offsets, uint32_t n_states,
+                   const uint32_t *cand_words, uint32_t n_cand,
+                   uint32_t n_vars, int32_t *out_first_sat,
+                   uint32_t *out_witness);
+
+/* Device-resident variant.  d_cands uses the DEVICE layout
+ * [state][var][half][cand] of 16-byte groups (see mgp_cand_index); n_slots is
+ * the max header slot count over the batch (mgp_lower reports it per state). */
+int mgp_eval_batch_dev(const uint32_t *d_prog_words,
+                       const uint64_t *d_prog_offsets, uint32_t n_states,
+                       const uint32_t *d_cands, uint32_t n_cand,
+                       uint32_t n_vars, uint32_t n_slots,
+                       int32_t *d_first_sat, uint32_t *d_witness,
+                       int32_t *d_scratch /* n_states*ceil(n_cand/64) */,
+                       void *stream);
+
+/* Fill device candidates with the benchmark mixture (Philox4x32-10 keyed by
+ * (seed, state_base+s, cand, var)): 25 % interesting values (0, 1, 2^256-1,
+ * 2^255, 2^160-1, ACTORS, constant-pool entries +-1), 75 % uniform. */
+int mgp_fill_candidates_dev(const uint32_t *d_prog_words,
+                            const uint64_t *d_prog_offsets, uint32_t n_states,
+                            uint64_t state_base, uint64_t seed,
+                            uint32_t *d_cands, uint32_t n_cand,
+                            uint32_t n_vars, void *stream);
+
+/* Overwrite candidate plant_idx[i] of state plant_state[i] with the n_vars*8
+ * words plant_words[i] (device pointers, n_plant entries). */
+int mgp_plant_candidates_dev(uint32_t *d_cands, uint32_t n_states,
+                             uint32_t n_cand, uint32_t n_vars,
+                             const uint32_t *d_plant_state,
+                             const uint32_t *d_plant_idx,
+                             const uint32_t *d_plant_words, uint32_t n_plant,
+                             void *stream);
+
+/* ---------------------------------------------------------- Keccak-256
+ * n preimages of len bytes each, preimage i at in + i*stride; 32-byte
+ * big-endian digests to out32 + 32*i.  Keccak-256 = Keccak[r=1088,c=512]
+ * with 0x01 domain padding (Ethereum), NOT NIST SHA3-256. */
+int mgp_keccak256_batch(mgp_ctx *ctx, const uint8_t *in, uint64_t n,
+                        uint32_t len, uint32_t stride, uint8_t *out32);
+int mgp_keccak256_dev(const uint8_t *d_in, uint64_t n, uint32_t len,
+                      uint32_t stride, uint8_t *d_out32, void *stream);
+
+/* Benchmark preimages: pad32(addr_i) || pad32(i mod 8), addr_i = low 160 bits
+ * of splitmix64 chain seeded with seed + first + i. */
+int mgp_fill_mapping_preimages_dev(uint8_t *d_out64, uint64_t first,
+                                   uint64_t n, uint64_t seed, void *stream);
+
+/* --------------------------------------------------- synthetic workload
+ * Seeded synthetic constraint DAGs: n_nodes op-nodes per
+ * state over 4 free 256-bit vars + up to 2 keccak-UF apps (vars 4, 5) and a
+ * <=16-entry constant pool; root = conjunction of the last 4 Bool nodes.
+ * States are generated independently from (seed, state_base + s), so any
+ * sub-range reproduces exactly.  For states with planted[s] = 1 a satisfying
+ * assignment (n_vars*8 words) is written to plant_words[s] and the candidate
+ * index to plant_idx[s] (< n_cand).
+ * Capacities: nodes_out >= n_states*(n_nodes+32), consts_out >= n_states*16*8. */
+int mgp_synth_generate(uint64_t seed, uint64_t state_base, uint32_t n_states,
+                       uint32_t n_nodes, uint32_t n_cand,
+                       mgp_node *nodes_out, uint64_t *node_offsets,
+                       uint32_t *consts_out, uint64_t *const_offsets,
+                       uint8_t *planted, uint32_t *plant_idx,
+                       uint32_t *plant_words);
+
+/* Nominal INT32 op counts summed over the op-nodes of
+ * each state — the algorithmic work the roofline fraction is priced on. */
+int mgp_nominal_ops(const mgp_node *nodes, const uint64_t *node_offsets,
+                    uint32_t n_states, uint64_t *out_ops);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MGP_H */

@@ -1,0 +1,310 @@
+"""ctypes binding of libmgp.so (include/mgp.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (``make -C
+mythril_amd/csrc``) and lives next to this file.  There is deliberately no
+fallback: if the library is missing or cannot load, every entry point raises
+``NativeUnavailable`` — the product path never silently evaluates constraints
+on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmgp.so")
+
+# include/mgp_ir.h : mgp_node (24 bytes)
+NODE_DTYPE = np.dtype(
+    [
+        ("op", "u1"),
+        ("flags", "u1"),
+        ("width", "<u2"),
+        ("a", "<i4"),
+        ("b", "<i4"),
+        ("c", "<i4"),
+        ("p0", "<u4"),
+        ("p1", "<u4"),
+    ]
+)
+assert NODE_DTYPE.itemsize == 24
+
+MGP_OK = 0
+MGP_E_ARG = -1
+MGP_E_HIP = -2
+MGP_E_NOMEM = -3
+MGP_E_CAPACITY = -4
+
+MGP_NO_SAT = -1
+MGP_UNDECIDED = -2
+ST_OK = 0
+ST_UNSUPPORTED = 1
+
+
+class NativeUnavailable(RuntimeError):
+    """libmgp.so is missing or failed to load (no CPU fallback exists)."""
+
+
+class MgpError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mgp error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I32 = ctypes.c_int32
+
+
+def _bind(lib):
+    sig = {
+        "mgp_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+        "mgp_destroy": (None, [_P]),
+        "mgp_last_error": (ctypes.c_char_p, [_P]),
+        "mgp_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+        "mgp_version": (ctypes.c_char_p, []),
+        "mgp_lower": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P, _U64, _P, _P, _P]),
+        "mgp_eval_batch": (ctypes.c_int, [_P, _P, _P, _U32, _P, _U32, _U32, _P, _P]),
+        "mgp_eval_batch_dev": (ctypes.c_int, [_P, _P, _U32, _P, _U32, _U32, _U32, _P, _P, _P, _P]),
+        "mgp_fill_candidates_dev": (ctypes.c_int, [_P, _P, _U32, _U64, _U64, _P, _U32, _U32, _P]),
+        "mgp_plant_candidates_dev": (ctypes.c_int, [_P, _U32, _U32, _U32, _P, _P, _P, _U32, _P]),
+        "mgp_keccak256_batch": (ctypes.c_int, [_P, _P, _U64, _U32, _U32, _P]),
+        "mgp_keccak256_dev": (ctypes.c_int, [_P, _U64, _U32, _U32, _P, _P]),
+        "mgp_fill_mapping_preimages_dev": (ctypes.c_int, [_P, _U64, _U64, _U64, _P]),
+        "mgp_synth_generate": (ctypes.c_int, [_U64, _U64, _U32, _U32, _U32, _P, _P, _P, _P, _P, _P, _P]),
+        "mgp_nominal_ops": (ctypes.c_int, [_P, _P, _U32, _P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def lib():
+    """Load libmgp.so once; raise NativeUnavailable loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise NativeUnavailable(
+                    f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(the GPU pre-filter has no CPU fallback)"
+                )
+            try:
+                _lib = _bind(ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL))
+            except OSError as e:  # pragma: no cover - depends on the box
+                raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    return _lib
+
+
+EXPORTED_SYMBOLS = (
+    "mgp_create",
+    "mgp_destroy",
+    "mgp_last_error",
+    "mgp_device_count",
+    "mgp_version",
+    "mgp_lower",
+    "mgp_eval_batch",
+    "mgp_eval_batch_dev",
+    "mgp_fill_candidates_dev",
+    "mgp_plant_candidates_dev",
+    "mgp_keccak256_batch",
+    "mgp_keccak256_dev",
+    "mgp_fill_mapping_preimages_dev",
+    "mgp_synth_generate",
+    "mgp_nominal_ops",
+)
+
+
+def _ptr(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to libmgp must be C-contiguous"
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _check(rc: int, ctx=None):
+    if rc != MGP_OK:
+        msg = lib().mgp_last_error(ctx)
+        raise MgpError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().mgp_device_count(ctypes.byref(n))
+    return n.value if rc == MGP_OK else 0
+
+
+# ------------------------------------------------------------------ lowering
+def lower(
+    nodes: np.ndarray,
+    node_offsets: np.ndarray,
+    consts: np.ndarray,
+    const_offsets: np.ndarray,
+    max_slots: int = 0,
+) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Lower node lists to bytecode -> (words u32, prog_offsets u64, status u8)."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    const_offsets = np.ascontiguousarray(const_offsets, dtype=np.uint64)
+    n_states = len(node_offsets) - 1
+    prog_offsets = np.zeros(n_states + 1, dtype=np.uint64)
+    status = np.zeros(max(n_states, 1), dtype=np.uint8)
+    used = ctypes.c_uint64(0)
+    cap = int(len(nodes)) * 16 + n_states * 64 + 64
+    L = lib()
+    for _ in range(2):
+        words = np.zeros(cap, dtype=np.uint32)
+        rc = L.mgp_lower(
+            _ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets), max_slots,
+            _ptr(words), cap, _ptr(prog_offsets), _ptr(status), ctypes.byref(used),
+        )
+        if rc == MGP_E_CAPACITY:
+            cap = int(used.value)
+            continue
+        _check(rc)
+        return words[: int(used.value)], prog_offsets, status[:n_states]
+    raise MgpError(MGP_E_CAPACITY, "lowering capacity")
+
+
+def program_headers(words: np.ndarray, prog_offsets: np.ndarray) -> np.ndarray:
+    """(n_states, 4) header words: n_ins, n_consts, n_slots, status|vars<<8."""
+    idx = prog_offsets[:-1].astype(np.int64)
+    return np.stack([words[idx + k] for k in range(4)], axis=1)
+
+
+# ------------------------------------------------------------------ context
+class Context:
+    """One libmgp context (device + HIP stream + device buffers)."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().mgp_create(device, ctypes.byref(self._h)))
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().mgp_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def eval_batch(self, words, prog_offsets, cands: np.ndarray, want_witness: bool = True):
+        """cands: uint32 [n_states, n_cand, n_vars, 8].  -> (first_sat i32, witness u32 [n,n_vars,8])."""
+        words = np.ascontiguousarray(words, dtype=np.uint32)
+        prog_offsets = np.ascontiguousarray(prog_offsets, dtype=np.uint64)
+        cands = np.ascontiguousarray(cands, dtype=np.uint32)
+        n_states, n_cand, n_vars, limbs = cands.shape
+        assert limbs == 8 and len(prog_offsets) == n_states + 1
+        first = np.full(n_states, MGP_NO_SAT, dtype=np.int32)
+        wit = np.zeros((n_states, n_vars, 8), dtype=np.uint32) if want_witness else None
+        rc = lib().mgp_eval_batch(
+            self._h, _ptr(words), _ptr(prog_offsets), n_states, _ptr(cands), n_cand, n_vars,
+            _ptr(first), _ptr(wit),
+        )
+        _check(rc, self._h)
+        return first, wit
+
+    def keccak256(self, data: np.ndarray, length: int, stride: int) -> np.ndarray:
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        n = 0 if stride == 0 else (len(data) - length) // stride + 1 if len(data) >= length else 0
+        return self.keccak256_n(data, n, length, stride)
+
+    def keccak256_n(self, data: np.ndarray, n: int, length: int, stride: int) -> np.ndarray:
+        data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        if n and len(data) < (n - 1) * stride + length:
+            raise ValueError("input buffer too small")
+        out = np.zeros((n, 32), dtype=np.uint8)
+        if n == 0:
+            return out
+        if data.size == 0:
+            data = np.zeros(1, dtype=np.uint8)
+        _check(lib().mgp_keccak256_batch(self._h, _ptr(data), n, length, stride, _ptr(out)), self._h)
+        return out
+
+
+# ------------------------------------------------------------- synthetic
+SYNTH_VARS = 6
+
+
+def synth_generate(seed: int, state_base: int, n_states: int, n_nodes: int = 64, n_cand: int = 256):
+    """Synthetic DAG batch -> dict(nodes, node_offsets, consts, const_offsets, planted, plant_idx, plant_words)."""
+    stride = n_nodes + 32
+    nodes = np.zeros(n_states * stride, dtype=NODE_DTYPE)
+    node_offsets = np.zeros(n_states + 1, dtype=np.uint64)
+    consts = np.zeros((n_states * 16, 8), dtype=np.uint32)
+    const_offsets = np.zeros(n_states + 1, dtype=np.uint64)
+    planted = np.zeros(n_states, dtype=np.uint8)
+    plant_idx = np.zeros(n_states, dtype=np.uint32)
+    plant_words = np.zeros((n_states, SYNTH_VARS, 8), dtype=np.uint32)
+    _check(
+        lib().mgp_synth_generate(
+            seed, state_base, n_states, n_nodes, n_cand, _ptr(nodes), _ptr(node_offsets), _ptr(consts),
+            _ptr(const_offsets), _ptr(planted), _ptr(plant_idx), _ptr(plant_words),
+        )
+    )
+    return {
+        "nodes": nodes[: int(node_offsets[-1])],
+        "node_offsets": node_offsets,
+        "consts": consts[: int(const_offsets[-1])],
+        "const_offsets": const_offsets,
+        "planted": planted,
+        "plant_idx": plant_idx,
+        "plant_words": plant_words,
+        "n_vars": SYNTH_VARS,
+    }
+
+
+def nominal_ops(nodes: np.ndarray, node_offsets: np.ndarray) -> np.ndarray:
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    n = len(node_offsets) - 1
+    out = np.zeros(max(n, 1), dtype=np.uint64)
+    _check(lib().mgp_nominal_ops(_ptr(nodes), _ptr(node_offsets), n, _ptr(out)))
+    return out[:n]
+
+
+# ---------------------------------------------------- device-pointer API
+def eval_batch_dev(d_words, d_offs, n_states, d_cands, n_cand, n_vars, n_slots, d_first, d_wit, d_scratch,
+                   stream) -> None:
+    _check(
+        lib().mgp_eval_batch_dev(
+            d_words, d_offs, n_states, d_cands, n_cand, n_vars, n_slots, d_first, d_wit, d_scratch, stream
+        )
+    )
+
+
+def fill_candidates_dev(d_words, d_offs, n_states, state_base, seed, d_cands, n_cand, n_vars, stream) -> None:
+    _check(lib().mgp_fill_candidates_dev(d_words, d_offs, n_states, state_base, seed, d_cands, n_cand, n_vars,
+                                         stream))
+
+
+def plant_candidates_dev(d_cands, n_states, n_cand, n_vars, d_pstate, d_pidx, d_pwords, n_plant, stream) -> None:
+    _check(lib().mgp_plant_candidates_dev(d_cands, n_states, n_cand, n_vars, d_pstate, d_pidx, d_pwords, n_plant,
+                                          stream))
+
+
+def keccak256_dev(d_in, n, length, stride, d_out, stream) -> None:
+    _check(lib().mgp_keccak256_dev(d_in, n, length, stride, d_out, stream))
+
+
+def fill_mapping_preimages_dev(d_out, first, n, seed, stream) -> None:
+    _check(lib().mgp_fill_mapping_preimages_dev(d_out, first, n, seed, stream))

@@ -1,0 +1,577 @@
+// mgp_kernels.hip — gfx950 kernels of the Mythril satisfiability pre-filter.
+//
+//   mgp_eval_kernel      constraint bytecode x candidate models, first-SAT
+//   mgp_finalize_kernel  per-state min over candidate chunks + witness copy
+//   mgp_fill_kernel      Philox4x32-10 benchmark candidates (untimed)
+//   mgp_plant_kernel     scatter planted witnesses into the candidate array
+//   mgp_transpose_kernel host AoS candidates -> device SoA layout
+//   mgp_keccak_kernel    batched Keccak-256, one preimage per lane
+//   mgp_preimage_kernel  benchmark mapping-slot preimages (untimed)
+//
+// Execution model: one 64-lane wave per (state,
+// 64-candidate chunk).  The bytecode and constant pool are wave-uniform and
+// are fetched through the scalar cache (s_load) — every lane of a wave runs
+// the same instruction on its own candidate, so the opcode dispatch is a
+// uniform branch with no divergence.  Each lane keeps the running
+// accumulator (last BV result, 8 VGPRs) and 64 Bool bits (2 VGPRs) in
+// registers; BV values that must outlive the next instruction go to per-lane
+// LDS slots ([slot][half][lane] x 16 B: ds_read_b128 / ds_write_b128,
+// conflict-free).  No MFMA: nothing here is a contraction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mgp_ir.h"
+#include "mgp_bv.h"
+
+#define MGP_WAVE 64
+#define MGP_PARTIAL_NONE 0x7FFFFFFF
+#define MGP_PARTIAL_UNDEC (-2)
+
+namespace {
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective"): blocks dispatched round-robin over the 8 XCDs get
+// consecutive logical ids per XCD, so neighbouring states (adjacent bytecode)
+// share one L2.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
+  uint32_t xcd = bid & 7u, q = nblk >> 3, r = nblk & 7u;
+  uint32_t base = (xcd < r) ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+struct EvalCtx {
+  const uint4 *lds;
+  const uint32_t *cpool;
+  const uint4 *cbase;  // this state's candidates, device layout
+  uint32_t n_cand;
+  uint32_t cand;       // clamped candidate index of this lane
+  uint32_t lane;
+};
+
+__device__ __forceinline__ U256 u256_from(uint4 lo, uint4 hi) {
+  U256 v;
+  v.w[0] = lo.x; v.w[1] = lo.y; v.w[2] = lo.z; v.w[3] = lo.w;
+  v.w[4] = hi.x; v.w[5] = hi.y; v.w[6] = hi.z; v.w[7] = hi.w;
+  return v;
+}
+
+__device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx &e) {
+  uint32_t kind = o >> 14, idx = o & 0x3FFFu;
+  if (kind == MGP_K_ACC) return acc;
+  if (kind == MGP_K_SLOT) {
+    const uint4 *p = e.lds + (size_t)idx * 2u * MGP_WAVE + e.lane;
+    return u256_from(p[0], p[MGP_WAVE]);
+  }
+  if (kind == MGP_K_CONST) {
+    const uint32_t *c = e.cpool + idx * 8u;  // uniform -> s_load_dwordx8
+    U256 v;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) v.w[l] = c[l];
+    return v;
+  }
+  const uint4 *p = e.cbase + (size_t)idx * 2u * e.n_cand + e.cand;
+  return u256_from(p[0], p[e.n_cand]);
+}
+
+__device__ __forceinline__ void store_slot(uint4 *lds, uint32_t slot, uint32_t lane, const U256 &v) {
+  uint4 *p = lds + (size_t)slot * 2u * MGP_WAVE + lane;
+  p[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+  p[MGP_WAVE] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+}
+
+__device__ __forceinline__ bool is_bool_op(uint32_t op) { return op >= MGP_OP_BAND && op <= MGP_OP_BEQ; }
+__device__ __forceinline__ bool is_cmp_op(uint32_t op) { return op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF; }
+__device__ __forceinline__ bool is_signed_op(uint32_t op) {
+  return op == MGP_OP_SDIV || op == MGP_OP_SREM || op == MGP_OP_SMOD || op == MGP_OP_ASHR;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------- eval
+__global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
+    const uint32_t *__restrict__ words, const uint64_t *__restrict__ offs,
+    uint32_t n_states, const uint4 *__restrict__ cands, uint32_t n_cand,
+    uint32_t n_vars, uint32_t n_chunks, uint32_t n_slots,
+    int32_t *__restrict__ partial) {
+  extern __shared__ uint4 mgp_lds[];
+  const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
+  const uint32_t state = lid / n_chunks, chunk = lid - state * n_chunks;
+  if (state >= n_states) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t cand = chunk * MGP_WAVE + lane;
+  const bool valid = cand < n_cand;
+
+  const uint32_t *prog = words + offs[state];
+  const uint32_t n_ins = uni(prog[0]);
+  const uint32_t h_slots = uni(prog[2]);
+  const uint32_t h_stat = uni(prog[3]);
+  if ((h_stat & 0xFFu) != MGP_ST_OK || h_slots > n_slots || (h_stat >> 8) > n_vars) {
+    if (lane == 0) partial[(size_t)state * n_chunks + chunk] = MGP_PARTIAL_UNDEC;
+    return;
+  }
+  const uint32_t *ins = prog + MGP_HDR_WORDS;
+  EvalCtx e;
+  e.lds = mgp_lds;
+  e.cpool = ins + (size_t)n_ins * MGP_INS_WORDS;
+  e.cbase = cands + (size_t)state * n_vars * 2u * n_cand;
+  e.n_cand = n_cand;
+  e.cand = valid ? cand : (n_cand - 1u);
+  e.lane = lane;
+
+  U256 acc = bv_zero();
+  uint64_t bools = 1ull << MGP_BOOL_TRUE;
+  bool root = false;
+
+  for (uint32_t pc = 0; pc < n_ins; ++pc) {
+    const uint32_t w0 = uni(ins[pc * 4u + 0u]);
+    const uint32_t w1 = uni(ins[pc * 4u + 1u]);
+    const uint32_t w2 = uni(ins[pc * 4u + 2u]);
+    const uint32_t op = w0 & 0xFFu;
+    const uint32_t width = ((w0 >> 8) & 0xFFu) + 1u;
+    const uint32_t dst = (w0 >> 16) & 0xFFu;
+    const uint32_t flags = w0 >> 24;
+    const uint32_t oa = w1 & 0xFFFFu, ob = w1 >> 16, oc = w2 & 0xFFFFu, imm = w2 >> 16;
+
+    if (op == MGP_OP_RET) {
+      root = ((bools >> oa) & 1ull) != 0ull;
+      break;
+    }
+    if (is_bool_op(op)) {
+      const bool a = ((bools >> oa) & 1ull) != 0ull;
+      const bool b = ((bools >> ob) & 1ull) != 0ull;
+      const bool c = ((bools >> oc) & 1ull) != 0ull;
+      bool r;
+      switch (op) {
+        case MGP_OP_BAND: r = a && b; break;
+        case MGP_OP_BOR: r = a || b; break;
+        case MGP_OP_BXOR: r = a != b; break;
+        case MGP_OP_BNOT: r = !a; break;
+        case MGP_OP_BITE: r = a ? b : c; break;
+        default: r = a == b; break;  // BEQ
+      }
+      bools = (bools & ~(1ull << dst)) | ((uint64_t)r << dst);
+      continue;
+    }
+    if (is_cmp_op(op)) {
+      U256 a = fetch(oa, acc, e), b = fetch(ob, acc, e);
+      bool r;
+      switch (op) {
+        case MGP_OP_EQ: r = bv_eq(a, b); break;
+        case MGP_OP_ULT: r = bv_ult(a, b); break;
+        case MGP_OP_ULE: r = !bv_ult(b, a); break;
+        case MGP_OP_UGT: r = bv_ult(b, a); break;
+        case MGP_OP_UGE: r = !bv_ult(a, b); break;
+        case MGP_OP_SLT: r = bv_slt(bv_sext(a, width), bv_sext(b, width)); break;
+        case MGP_OP_SLE: r = !bv_slt(bv_sext(b, width), bv_sext(a, width)); break;
+        case MGP_OP_SGT: r = bv_slt(bv_sext(b, width), bv_sext(a, width)); break;
+        case MGP_OP_SGE: r = !bv_slt(bv_sext(a, width), bv_sext(b, width)); break;
+        case MGP_OP_UADD_NOOVF: {
+          uint32_t carry;
+          U256 s = bv_add(a, b, &carry);
+          r = (width >= 256u) ? (carry == 0u) : bv_eq(s, bv_mask(s, width));
+          break;
+        }
+        case MGP_OP_UMUL_NOOVF: {
+          U256 lo;
+          U256 hi = bv_mul_full(a, b, &lo);
+          r = bv_is_zero(hi) && bv_eq(lo, bv_mask(lo, width));
+          break;
+        }
+        default: r = !bv_ult(a, b); break;  // USUB_NOUDF: b <= a
+      }
+      bools = (bools & ~(1ull << dst)) | ((uint64_t)r << dst);
+      continue;
+    }
+
+    // ---- BV-producing instructions
+    U256 r;
+    if (op == MGP_OP_ITE) {
+      const bool c = ((bools >> oa) & 1ull) != 0ull;
+      U256 t = fetch(ob, acc, e), f = fetch(oc, acc, e);
+      r = bv_sel(c, t, f);
+      if (width < 256u) r = bv_mask(r, width);
+      acc = r;
+      if (flags & MGP_INS_STORE) store_slot(mgp_lds, dst, lane, r);
+      continue;
+    }
+    U256 a = fetch(oa, acc, e);
+    if (op == MGP_OP_MOV || op == MGP_OP_ZEXT) {
+      r = a;
+    } else if (op == MGP_OP_NOT) {
+      r = bv_not(a);
+    } else if (op == MGP_OP_NEG) {
+      r = bv_neg(a);
+    } else if (op == MGP_OP_EXTRACT) {
+      r = bv_lshr(a, imm);
+    } else if (op == MGP_OP_SEXT) {
+      r = bv_sext(a, imm);
+    } else {
+      U256 b = fetch(ob, acc, e);
+      if (is_signed_op(op) && width < 256u) {
+        a = bv_sext(a, width);
+        if (op != MGP_OP_ASHR) b = bv_sext(b, width);
+      }
+      switch (op) {
+        case MGP_OP_ADD: r = bv_add(a, b, nullptr); break;
+        case MGP_OP_SUB: r = bv_sub(a, b, nullptr); break;
+        case MGP_OP_MUL: r = bv_mul(a, b); break;
+        case MGP_OP_UDIV: { U256 q, m; bv_udivrem(a, b, &q, &m); r = q; break; }
+        case MGP_OP_UREM: { U256 q, m; bv_udivrem(a, b, &q, &m); r = m; break; }
+        case MGP_OP_SDIV: r = bv_sdiv(a, b); break;
+        case MGP_OP_SREM: r = bv_srem(a, b); break;
+        case MGP_OP_SMOD: r = bv_smod(a, b); break;
+        case MGP_OP_AND: r = bv_and(a, b); break;
+        case MGP_OP_OR: r = bv_or(a, b); break;
+        case MGP_OP_XOR: r = bv_xor(a, b); break;
+        case MGP_OP_SHL: r = bv_shl(a, bv_shift_amount(b)); break;
+        case MGP_OP_LSHR: r = bv_lshr(a, bv_shift_amount(b)); break;
+        case MGP_OP_ASHR: r = bv_ashr(a, bv_shift_amount(b)); break;
+        case MGP_OP_CONCAT: r = bv_or(bv_shl(a, imm), b); break;
+        default: r = bv_zero(); break;
+      }
+    }
+    if (width < 256u) r = bv_mask(r, width);
+    acc = r;
+    if (flags & MGP_INS_STORE) store_slot(mgp_lds, dst, lane, r);
+  }
+
+  const unsigned long long m = __ballot(valid && root);
+  if (lane == 0) {
+    partial[(size_t)state * n_chunks + chunk] =
+        m ? (int32_t)(chunk * MGP_WAVE + (uint32_t)__ffsll((long long)m) - 1u) : MGP_PARTIAL_NONE;
+  }
+}
+
+__global__ void mgp_finalize_kernel(const int32_t *__restrict__ partial, uint32_t n_states,
+                                    uint32_t n_chunks, const uint4 *__restrict__ cands,
+                                    uint32_t n_cand, uint32_t n_vars,
+                                    int32_t *__restrict__ first_sat, uint4 *__restrict__ witness) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_states) return;
+  int32_t best = MGP_PARTIAL_NONE;
+  bool undec = false;
+  for (uint32_t k = 0; k < n_chunks; ++k) {
+    int32_t p = partial[(size_t)s * n_chunks + k];
+    if (p == MGP_PARTIAL_UNDEC) undec = true;
+    else if (p < best) best = p;
+  }
+  int32_t res = undec ? MGP_UNDECIDED : (best == MGP_PARTIAL_NONE ? MGP_NO_SAT : best);
+  first_sat[s] = res;
+  if (res >= 0 && witness) {
+    const uint4 *cb = cands + (size_t)s * n_vars * 2u * n_cand;
+    for (uint32_t v = 0; v < n_vars; ++v)
+      for (uint32_t h = 0; h < 2u; ++h)
+        witness[((size_t)s * n_vars + v) * 2u + h] = cb[(size_t)(v * 2u + h) * n_cand + (uint32_t)res];
+  }
+}
+
+// --------------------------------------------------------------- Philox
+namespace {
+__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, ctr.x), lo0 = 0xD2511F53u * ctr.x;
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, ctr.z), lo1 = 0xCD9E8D57u * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += 0x9E3779B9u;
+    key.y += 0xBB67AE85u;
+  }
+  return ctr;
+}
+}  // namespace
+
+// one thread per (state, var, cand); writes both 16-byte halves
+__global__ void mgp_fill_kernel(const uint32_t *__restrict__ words, const uint64_t *__restrict__ offs,
+                                uint32_t n_states, uint64_t state_base, uint64_t seed,
+                                uint4 *__restrict__ cands, uint32_t n_cand, uint32_t n_vars) {
+  const uint64_t total = (uint64_t)n_states * n_vars * n_cand;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = (uint32_t)(t % n_cand);
+    const uint64_t sv = t / n_cand;
+    const uint32_t v = (uint32_t)(sv % n_vars);
+    const uint32_t s = (uint32_t)(sv / n_vars);
+    const uint64_t gs = state_base + s;
+    uint4 r0 = philox4x32_10(make_uint4(c, v, (uint32_t)gs, (uint32_t)(gs >> 32)), key);
+    uint4 r1 = philox4x32_10(make_uint4(c, v | (1u << 16), (uint32_t)gs, (uint32_t)(gs >> 32)), key);
+    uint4 sel = philox4x32_10(make_uint4(c, v | (2u << 16), (uint32_t)gs, (uint32_t)(gs >> 32)), key);
+    uint32_t w[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    if ((sel.x & 3u) == 0u) {  // 25 % interesting values
+      const uint32_t kind = sel.y & 15u;
+      for (int l = 0; l < 8; ++l) w[l] = 0u;
+      if (kind == 1u) {
+        w[0] = 1u;
+      } else if (kind == 2u) {
+        for (int l = 0; l < 8; ++l) w[l] = 0xFFFFFFFFu;
+      } else if (kind == 3u) {
+        w[7] = 0x80000000u;
+      } else if (kind == 4u) {
+        for (int l = 0; l < 5; ++l) w[l] = 0xFFFFFFFFu;
+      } else if (kind >= 5u && kind <= 7u) {  // ACTORS transaction/symbolic.py:25-27
+        const uint32_t pat[3][5] = {
+            {0xAFFEAFFEu, 0xAFFEAFFEu, 0xAFFEAFFEu, 0xAFFEAFFEu, 0xAFFEAFFEu},
+            {0xDEADBEEFu, 0xDEADBEEFu, 0xDEADBEEFu, 0xDEADBEEFu, 0xDEADBEEFu},
+            {0xAAAAAAAAu, 0xAAAAAAAAu, 0xAAAAAAAAu, 0xAAAAAAAAu, 0xAAAAAAAAu}};
+        for (int l = 0; l < 5; ++l) w[l] = pat[kind - 5u][l];
+      } else if (kind >= 8u) {  // constant-pool entry + {-1, 0, +1}
+        const uint32_t *prog = words + offs[s];
+        const uint32_t n_ins = prog[0], n_c = prog[1];
+        if (n_c) {
+          const uint32_t *cp = prog + MGP_HDR_WORDS + (size_t)n_ins * MGP_INS_WORDS + (sel.z % n_c) * 8u;
+          U256 x;
+          for (int l = 0; l < 8; ++l) x.w[l] = cp[l];
+          const uint32_t d = sel.w % 3u;
+          if (d == 0u) x = bv_sub(x, bv_small(1u), nullptr);
+          else if (d == 2u) x = bv_add(x, bv_small(1u), nullptr);
+          for (int l = 0; l < 8; ++l) w[l] = x.w[l];
+        }
+      }
+    }
+    uint4 *dst = cands + ((size_t)s * n_vars + v) * 2u * n_cand + c;
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[n_cand] = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+}
+
+__global__ void mgp_plant_kernel(uint4 *__restrict__ cands, uint32_t n_cand, uint32_t n_vars,
+                                 const uint32_t *__restrict__ pstate, const uint32_t *__restrict__ pidx,
+                                 const uint4 *__restrict__ pwords, uint32_t n_plant) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = (uint64_t)n_plant * n_vars * 2u;
+  if (t >= total) return;
+  const uint32_t h = (uint32_t)(t & 1u);
+  const uint32_t v = (uint32_t)((t >> 1) % n_vars);
+  const uint32_t i = (uint32_t)((t >> 1) / n_vars);
+  const uint32_t s = pstate[i], c = pidx[i];
+  cands[((size_t)s * n_vars + v) * 2u * n_cand + (size_t)h * n_cand + c] = pwords[((size_t)i * n_vars + v) * 2u + h];
+}
+
+// host AoS [state][cand][var][2 x uint4] -> device [state][var][half][cand]
+__global__ void mgp_transpose_kernel(const uint4 *__restrict__ aos, uint4 *__restrict__ soa,
+                                     uint32_t n_states, uint32_t n_cand, uint32_t n_vars) {
+  const uint64_t total = (uint64_t)n_states * n_vars * 2u * n_cand;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = (uint32_t)(t % n_cand);
+    uint64_t r = t / n_cand;
+    const uint32_t h = (uint32_t)(r & 1u);
+    r >>= 1;
+    const uint32_t v = (uint32_t)(r % n_vars);
+    const uint64_t s = r / n_vars;
+    soa[t] = aos[((s * n_cand + c) * n_vars + v) * 2u + h];
+  }
+}
+
+// --------------------------------------------------------------- Keccak
+namespace {
+__constant__ uint64_t kKeccakRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+    0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+    0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int n) {
+  return n == 0 ? x : ((x << n) | (x >> (64 - n)));
+}
+
+// Keccak-f[1600]; lane (x,y) at st[x + 5y].  Rotation offsets (FIPS 202 rho).
+__device__ __forceinline__ void keccak_f1600(uint64_t st[25]) {
+  constexpr int kRho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
+                            25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+#pragma unroll 1
+  for (int round = 0; round < 24; ++round) {
+    uint64_t C[5], D[5], B[25];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) C[x] = st[x] ^ st[x + 5] ^ st[x + 10] ^ st[x + 15] ^ st[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) D[x] = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
+#pragma unroll
+    for (int i = 0; i < 25; ++i) st[i] ^= D[i % 5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x)
+#pragma unroll
+      for (int y = 0; y < 5; ++y) B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(st[x + 5 * y], kRho[x + 5 * y]);
+#pragma unroll
+    for (int y = 0; y < 5; ++y)
+#pragma unroll
+      for (int x = 0; x < 5; ++x)
+        st[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+    st[0] ^= kKeccakRC[round];
+  }
+}
+}  // namespace
+
+// generic path: any len, any stride (byte loads), multi-block absorb
+__global__ void mgp_keccak_kernel(const uint8_t *__restrict__ in, uint64_t n, uint32_t len,
+                                  uint32_t stride, uint8_t *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *p = in + i * stride;
+  uint64_t st[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) st[k] = 0ull;
+  uint32_t off = 0;
+  while (len - off >= 136u) {
+    for (int k = 0; k < 17; ++k) {
+      uint64_t v = 0;
+      for (int b = 7; b >= 0; --b) v = (v << 8) | p[off + 8 * k + b];
+      st[k] ^= v;
+    }
+    keccak_f1600(st);
+    off += 136u;
+  }
+  uint8_t blk[136];
+  for (int b = 0; b < 136; ++b) blk[b] = 0;
+  for (uint32_t b = 0; b < len - off; ++b) blk[b] = p[off + b];
+  blk[len - off] ^= 0x01u;
+  blk[135] ^= 0x80u;
+  for (int k = 0; k < 17; ++k) {
+    uint64_t v = 0;
+    for (int b = 7; b >= 0; --b) v = (v << 8) | blk[8 * k + b];
+    st[k] ^= v;
+  }
+  keccak_f1600(st);
+  uint8_t *o = out + i * 32u;
+  for (int k = 0; k < 4; ++k)
+    for (int b = 0; b < 8; ++b) o[8 * k + b] = (uint8_t)(st[k] >> (8 * b));
+}
+
+// fast path: 64-byte preimages, 16-byte aligned stride (mapping slots)
+__global__ __launch_bounds__(256) void mgp_keccak64_kernel(const uint4 *__restrict__ in, uint64_t n,
+                                                           uint32_t stride16, uint4 *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 *p = in + i * stride16;
+  uint64_t st[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) st[k] = 0ull;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint4 v = p[q];
+    st[2 * q] = ((uint64_t)v.y << 32) | v.x;
+    st[2 * q + 1] = ((uint64_t)v.w << 32) | v.z;
+  }
+  st[8] = 0x01ull;
+  st[16] = 0x8000000000000000ull;
+  keccak_f1600(st);
+  uint4 *o = out + i * 2u;
+  o[0] = make_uint4((uint32_t)st[0], (uint32_t)(st[0] >> 32), (uint32_t)st[1], (uint32_t)(st[1] >> 32));
+  o[1] = make_uint4((uint32_t)st[2], (uint32_t)(st[2] >> 32), (uint32_t)st[3], (uint32_t)(st[3] >> 32));
+}
+
+namespace {
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+}  // namespace
+
+// preimage i = pad32(addr_i) || pad32((first+i) mod 8), big-endian words
+__global__ void mgp_preimage_kernel(uint8_t *__restrict__ out, uint64_t first, uint64_t n, uint64_t seed) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t g = first + i;
+  const uint64_t x0 = splitmix64(seed + g), x1 = splitmix64(x0), x2 = splitmix64(x1);
+  uint8_t b[64];
+  for (int k = 0; k < 64; ++k) b[k] = 0;
+  // addr = (x2 & 0xffffffff) << 128 | x1 << 64 | x0, 20 bytes big-endian at [12, 32)
+  for (int k = 0; k < 8; ++k) b[31 - k] = (uint8_t)(x0 >> (8 * k));
+  for (int k = 0; k < 8; ++k) b[23 - k] = (uint8_t)(x1 >> (8 * k));
+  for (int k = 0; k < 4; ++k) b[15 - k] = (uint8_t)(x2 >> (8 * k));
+  b[63] = (uint8_t)(g & 7u);
+  uint4 *o = reinterpret_cast<uint4 *>(out + i * 64u);
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w[4];
+    for (int j = 0; j < 4; ++j)
+      w[j] = (uint32_t)b[16 * q + 4 * j] | ((uint32_t)b[16 * q + 4 * j + 1] << 8) |
+             ((uint32_t)b[16 * q + 4 * j + 2] << 16) | ((uint32_t)b[16 * q + 4 * j + 3] << 24);
+    o[q] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// ------------------------------------------------------------ launchers
+extern "C" {
+
+hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
+                           const uint32_t *cands, uint32_t n_cand, uint32_t n_vars, uint32_t n_slots,
+                           int32_t *first_sat, uint32_t *witness, int32_t *partial, hipStream_t st) {
+  if (n_states == 0) return hipSuccess;
+  const uint32_t n_chunks = (n_cand + MGP_WAVE - 1) / MGP_WAVE;
+  const uint64_t nblk = (uint64_t)n_states * n_chunks;
+  const size_t lds = (size_t)(n_slots ? n_slots : 1u) * 2u * MGP_WAVE * sizeof(uint4);
+  hipLaunchKernelGGL(mgp_eval_kernel, dim3((uint32_t)nblk), dim3(MGP_WAVE), lds, st, words, offs,
+                     n_states, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars, n_chunks,
+                     n_slots, partial);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  hipLaunchKernelGGL(mgp_finalize_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, partial,
+                     n_states, n_chunks, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars,
+                     first_sat, reinterpret_cast<uint4 *>(witness));
+  return hipGetLastError();
+}
+
+hipError_t mgp_launch_fill(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
+                           uint64_t state_base, uint64_t seed, uint32_t *cands, uint32_t n_cand,
+                           uint32_t n_vars, hipStream_t st) {
+  const uint64_t total = (uint64_t)n_states * n_vars * n_cand;
+  if (total == 0) return hipSuccess;
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 65536ull * 16) blocks = 65536ull * 16;
+  hipLaunchKernelGGL(mgp_fill_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, words, offs, n_states,
+                     state_base, seed, reinterpret_cast<uint4 *>(cands), n_cand, n_vars);
+  return hipGetLastError();
+}
+
+hipError_t mgp_launch_plant(uint32_t *cands, uint32_t n_cand, uint32_t n_vars, const uint32_t *pstate,
+                            const uint32_t *pidx, const uint32_t *pwords, uint32_t n_plant, hipStream_t st) {
+  const uint64_t total = (uint64_t)n_plant * n_vars * 2u;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(mgp_plant_kernel, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<uint4 *>(cands), n_cand, n_vars, pstate, pidx,
+                     reinterpret_cast<const uint4 *>(pwords), n_plant);
+  return hipGetLastError();
+}
+
+hipError_t mgp_launch_transpose(const uint32_t *aos, uint32_t *soa, uint32_t n_states, uint32_t n_cand,
+                                uint32_t n_vars, hipStream_t st) {
+  const uint64_t total = (uint64_t)n_states * n_vars * 2u * n_cand;
+  if (total == 0) return hipSuccess;
+  uint64_t blocks = (total + 255) / 256;
+  if (blocks > 65536ull * 16) blocks = 65536ull * 16;
+  hipLaunchKernelGGL(mgp_transpose_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
+                     reinterpret_cast<const uint4 *>(aos), reinterpret_cast<uint4 *>(soa), n_states,
+                     n_cand, n_vars);
+  return hipGetLastError();
+}
+
+hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32_t stride, uint8_t *out,
+                             hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const bool fast = len == 64u && (stride % 16u) == 0u && ((uintptr_t)in % 16u) == 0u &&
+                    ((uintptr_t)out % 16u) == 0u;
+  const uint64_t blocks = (n + 255) / 256;
+  if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  if (fast) {
+    hipLaunchKernelGGL(mgp_keccak64_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
+                       reinterpret_cast<const uint4 *>(in), n, stride / 16u, reinterpret_cast<uint4 *>(out));
+  } else {
+    hipLaunchKernelGGL(mgp_keccak_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, in, n, len, stride, out);
+  }
+  return hipGetLastError();
+}
+
+hipError_t mgp_launch_preimages(uint8_t *out, uint64_t first, uint64_t n, uint64_t seed, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(mgp_preimage_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, out, first, n,
+                     seed);
+  return hipGetLastError();
+}
+
+}  // extern "C"

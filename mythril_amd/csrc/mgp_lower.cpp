@@ -1,0 +1,470 @@
+// mgp_lower.cpp — constraint DAG -> flat bytecode (host side).
+//
+// Per state:
+//   1. validate the topologically ordered node list (widths <= 256, operand
+//      indices point backwards, root is Bool);
+//   2. expand uninterpreted-function applications (keccak256_<n> and its
+//      inverse, keccak_function_manager.py:56-69, and base-array Selects) into
+//      EQ/ITE chains: Ackermann expansion with a lazily built interpretation
+//      (mgp_ir.h, MGP_OP_UFAPP / MGP_OP_UFINV);
+//   3. re-pool constants (masked to the using node's width, de-duplicated);
+//   4. liveness-based allocation of BV slots (per-lane LDS) and Bool bits,
+//      with accumulator forwarding: an operand produced by the immediately
+//      preceding BV instruction is read from registers (ACC) and only values
+//      with a later use are stored;
+//   5. emit header + instructions + constant pool.
+// States are independent; the batch is lowered in parallel with OpenMP.
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mgp.h"
+
+namespace {
+
+// value reference during lowering
+enum RefKind : uint8_t { R_NONE = 0, R_VAR, R_CONST, R_INS, R_BOOLC };
+
+struct Ref {
+  RefKind k = R_NONE;
+  uint32_t idx = 0;  // var index / const pool index / vinstr index / bool const (0,1)
+  bool operator==(const Ref &o) const { return k == o.k && idx == o.idx; }
+};
+
+struct VIns {
+  uint8_t op;
+  uint16_t width;   // result width (BV) or operand width (compare)
+  bool is_bool;     // produces a Bool
+  Ref a, b, c;
+  uint32_t imm;
+};
+
+inline bool op_is_bool_result(uint8_t op) {
+  return (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) || (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) ||
+         op == MGP_OP_TRUE || op == MGP_OP_FALSE;
+}
+inline bool op_takes_bools(uint8_t op) { return op >= MGP_OP_BAND && op <= MGP_OP_BEQ; }
+
+struct ConstKey {
+  uint32_t w[8];
+  bool operator==(const ConstKey &o) const { return memcmp(w, o.w, sizeof(w)) == 0; }
+};
+struct ConstHash {
+  size_t operator()(const ConstKey &k) const {
+    uint64_t h = 1469598103934665603ull;
+    for (int i = 0; i < 8; ++i) h = (h ^ k.w[i]) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
+
+inline uint32_t limb_mask(uint32_t w, int l) {
+  int lo = 32 * l;
+  if ((int)w >= lo + 32) return 0xFFFFFFFFu;
+  if ((int)w <= lo) return 0u;
+  return (1u << (w - lo)) - 1u;
+}
+
+struct Lowered {
+  std::vector<uint32_t> words;
+  uint8_t status = MGP_ST_OK;
+};
+
+struct LowerState {
+  std::vector<VIns> ins;
+  std::vector<ConstKey> pool;
+  std::unordered_map<ConstKey, uint32_t, ConstHash> pool_map;
+  uint32_t max_var = 0;  // 1 + highest var index used
+
+  Ref add(uint8_t op, uint16_t width, bool is_bool, Ref a, Ref b = Ref(), Ref c = Ref(), uint32_t imm = 0) {
+    ins.push_back(VIns{op, width, is_bool, a, b, c, imm});
+    Ref r;
+    r.k = R_INS;
+    r.idx = (uint32_t)ins.size() - 1;
+    return r;
+  }
+  Ref constant(const uint32_t *limbs, uint32_t width) {
+    ConstKey k;
+    for (int l = 0; l < 8; ++l) k.w[l] = limbs[l] & limb_mask(width, l);
+    auto it = pool_map.find(k);
+    Ref r;
+    r.k = R_CONST;
+    if (it != pool_map.end()) {
+      r.idx = it->second;
+    } else {
+      r.idx = (uint32_t)pool.size();
+      pool.push_back(k);
+      pool_map.emplace(k, r.idx);
+    }
+    return r;
+  }
+};
+
+struct UFApp {
+  Ref arg, val;
+};
+
+Lowered unsupported() {
+  Lowered L;
+  L.status = MGP_ST_UNSUPPORTED;
+  L.words = {0u, 0u, 0u, (uint32_t)MGP_ST_UNSUPPORTED};
+  return L;
+}
+
+Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *consts, uint64_t n_consts,
+                  uint32_t max_slots) {
+  if (n_nodes == 0) return unsupported();
+  LowerState S;
+  std::vector<Ref> val(n_nodes);
+  std::vector<uint16_t> wid(n_nodes);
+  std::vector<uint8_t> isb(n_nodes);
+  std::unordered_map<uint32_t, std::vector<UFApp>> fapps, iapps;
+
+  for (uint64_t i = 0; i < n_nodes; ++i) {
+    const mgp_node &nd = nodes[i];
+    const uint8_t op = nd.op;
+    const bool rb = op_is_bool_result(op);
+    uint32_t w = rb ? 1u : nd.width;
+    if (!rb && (w == 0 || w > MGP_MAX_WIDTH)) return unsupported();
+    auto opnd = [&](int32_t j) -> bool { return j >= 0 && (uint64_t)j < i; };
+    wid[i] = (uint16_t)w;
+    isb[i] = rb;
+    switch (op) {
+      case MGP_OP_VAR: {
+        if (nd.p0 >= 0x3FFFu) return unsupported();
+        S.max_var = std::max(S.max_var, nd.p0 + 1);
+        Ref v;
+        v.k = R_VAR;
+        v.idx = nd.p0;
+        val[i] = (w < 256u) ? S.add(MGP_OP_MOV, (uint16_t)w, false, v) : v;
+        break;
+      }
+      case MGP_OP_CONST: {
+        if (nd.p0 >= n_consts) return unsupported();
+        val[i] = S.constant(consts + (size_t)nd.p0 * 8u, w);
+        break;
+      }
+      case MGP_OP_TRUE:
+      case MGP_OP_FALSE: {
+        Ref r;
+        r.k = R_BOOLC;
+        r.idx = (op == MGP_OP_TRUE) ? 1u : 0u;
+        val[i] = r;
+        break;
+      }
+      case MGP_OP_ADD: case MGP_OP_SUB: case MGP_OP_MUL: case MGP_OP_UDIV: case MGP_OP_UREM:
+      case MGP_OP_SDIV: case MGP_OP_SREM: case MGP_OP_SMOD: case MGP_OP_AND: case MGP_OP_OR:
+      case MGP_OP_XOR: case MGP_OP_SHL: case MGP_OP_LSHR: case MGP_OP_ASHR: {
+        if (!opnd(nd.a) || !opnd(nd.b)) return unsupported();
+        if (isb[nd.a] || isb[nd.b] || wid[nd.a] != w || wid[nd.b] != w) return unsupported();
+        val[i] = S.add(op, (uint16_t)w, false, val[nd.a], val[nd.b]);
+        break;
+      }
+      case MGP_OP_NOT: case MGP_OP_NEG: {
+        if (!opnd(nd.a) || isb[nd.a] || wid[nd.a] != w) return unsupported();
+        val[i] = S.add(op, (uint16_t)w, false, val[nd.a]);
+        break;
+      }
+      case MGP_OP_EXTRACT: {
+        if (!opnd(nd.a) || isb[nd.a]) return unsupported();
+        const uint32_t hi = nd.p0, lo = nd.p1;
+        if (hi < lo || hi >= wid[nd.a] || hi - lo + 1 != w) return unsupported();
+        if (lo == 0 && w == wid[nd.a]) { val[i] = val[nd.a]; break; }
+        val[i] = S.add(MGP_OP_EXTRACT, (uint16_t)w, false, val[nd.a], Ref(), Ref(), lo);
+        break;
+      }
+      case MGP_OP_CONCAT: {
+        if (!opnd(nd.a) || !opnd(nd.b) || isb[nd.a] || isb[nd.b]) return unsupported();
+        if ((uint32_t)wid[nd.a] + wid[nd.b] != w) return unsupported();
+        val[i] = S.add(MGP_OP_CONCAT, (uint16_t)w, false, val[nd.a], val[nd.b], Ref(), wid[nd.b]);
+        break;
+      }
+      case MGP_OP_ZEXT: {
+        if (!opnd(nd.a) || isb[nd.a] || wid[nd.a] > w) return unsupported();
+        val[i] = val[nd.a];  // storage is zero-extended already
+        break;
+      }
+      case MGP_OP_SEXT: {
+        if (!opnd(nd.a) || isb[nd.a] || wid[nd.a] > w) return unsupported();
+        if (wid[nd.a] == w) { val[i] = val[nd.a]; break; }
+        val[i] = S.add(MGP_OP_SEXT, (uint16_t)w, false, val[nd.a], Ref(), Ref(), wid[nd.a]);
+        break;
+      }
+      case MGP_OP_ITE: {
+        if (!opnd(nd.a) || !opnd(nd.b) || !opnd(nd.c) || !isb[nd.a]) return unsupported();
+        if (isb[nd.b] && isb[nd.c]) {  // Bool-valued ite
+          wid[i] = 1;
+          isb[i] = 1;
+          val[i] = S.add(MGP_OP_BITE, 1, true, val[nd.a], val[nd.b], val[nd.c]);
+          break;
+        }
+        if (isb[nd.b] || isb[nd.c] || wid[nd.b] != w || wid[nd.c] != w) return unsupported();
+        val[i] = S.add(MGP_OP_ITE, (uint16_t)w, false, val[nd.a], val[nd.b], val[nd.c]);
+        break;
+      }
+      case MGP_OP_EQ: case MGP_OP_ULT: case MGP_OP_ULE: case MGP_OP_UGT: case MGP_OP_UGE:
+      case MGP_OP_SLT: case MGP_OP_SLE: case MGP_OP_SGT: case MGP_OP_SGE:
+      case MGP_OP_UADD_NOOVF: case MGP_OP_UMUL_NOOVF: case MGP_OP_USUB_NOUDF: {
+        if (!opnd(nd.a) || !opnd(nd.b)) return unsupported();
+        if (op == MGP_OP_EQ && isb[nd.a] && isb[nd.b]) {
+          val[i] = S.add(MGP_OP_BEQ, 1, true, val[nd.a], val[nd.b]);
+          break;
+        }
+        if (isb[nd.a] || isb[nd.b] || wid[nd.a] != wid[nd.b]) return unsupported();
+        val[i] = S.add(op, wid[nd.a], true, val[nd.a], val[nd.b]);
+        break;
+      }
+      case MGP_OP_BAND: case MGP_OP_BOR: case MGP_OP_BXOR: case MGP_OP_BEQ: {
+        if (!opnd(nd.a) || !opnd(nd.b) || !isb[nd.a] || !isb[nd.b]) return unsupported();
+        val[i] = S.add(op, 1, true, val[nd.a], val[nd.b]);
+        break;
+      }
+      case MGP_OP_BNOT: {
+        if (!opnd(nd.a) || !isb[nd.a]) return unsupported();
+        val[i] = S.add(op, 1, true, val[nd.a]);
+        break;
+      }
+      case MGP_OP_BITE: {
+        if (!opnd(nd.a) || !opnd(nd.b) || !opnd(nd.c) || !isb[nd.a] || !isb[nd.b] || !isb[nd.c])
+          return unsupported();
+        val[i] = S.add(op, 1, true, val[nd.a], val[nd.b], val[nd.c]);
+        break;
+      }
+      case MGP_OP_UFAPP: {
+        // f(arg): first earlier f-app with equal argument, else fresh var p1
+        if (!opnd(nd.a) || isb[nd.a] || nd.p1 >= 0x3FFFu) return unsupported();
+        const uint32_t aw = wid[nd.a];
+        S.max_var = std::max(S.max_var, nd.p1 + 1);
+        Ref fresh;
+        fresh.k = R_VAR;
+        fresh.idx = nd.p1;
+        Ref v = (w < 256u) ? S.add(MGP_OP_MOV, (uint16_t)w, false, fresh) : fresh;
+        std::vector<UFApp> &fl = fapps[nd.p0];
+        for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
+          Ref e = S.add(MGP_OP_EQ, (uint16_t)aw, true, val[nd.a], it->arg);
+          v = S.add(MGP_OP_ITE, (uint16_t)w, false, e, it->val, v);
+        }
+        fl.push_back(UFApp{val[nd.a], v});
+        val[i] = v;
+        break;
+      }
+      case MGP_OP_UFINV: {
+        // f^-1(arg): first earlier inverse app with equal argument, else the
+        // argument of the first earlier f-app whose value equals arg, else p1
+        if (!opnd(nd.a) || isb[nd.a] || nd.p1 >= 0x3FFFu) return unsupported();
+        const uint32_t aw = wid[nd.a];
+        S.max_var = std::max(S.max_var, nd.p1 + 1);
+        Ref fresh;
+        fresh.k = R_VAR;
+        fresh.idx = nd.p1;
+        Ref v = (w < 256u) ? S.add(MGP_OP_MOV, (uint16_t)w, false, fresh) : fresh;
+        std::vector<UFApp> &fl = fapps[nd.p0];
+        for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
+          Ref e = S.add(MGP_OP_EQ, (uint16_t)aw, true, val[nd.a], it->val);
+          v = S.add(MGP_OP_ITE, (uint16_t)w, false, e, it->arg, v);
+        }
+        std::vector<UFApp> &il = iapps[nd.p0];
+        for (auto it = il.rbegin(); it != il.rend(); ++it) {
+          Ref e = S.add(MGP_OP_EQ, (uint16_t)aw, true, val[nd.a], it->arg);
+          v = S.add(MGP_OP_ITE, (uint16_t)w, false, e, it->val, v);
+        }
+        il.push_back(UFApp{val[nd.a], v});
+        val[i] = v;
+        break;
+      }
+      default:
+        return unsupported();
+    }
+  }
+  if (!isb[n_nodes - 1]) return unsupported();
+  Ref root = val[n_nodes - 1];
+
+  // ---------------------------------------------- dead-code elimination
+  {
+    const uint32_t n0 = (uint32_t)S.ins.size();
+    std::vector<uint8_t> live(n0, 0);
+    if (root.k == R_INS) live[root.idx] = 1;
+    for (int64_t t = (int64_t)n0 - 1; t >= 0; --t) {
+      if (!live[t]) continue;
+      const VIns &I = S.ins[t];
+      for (const Ref *r : {&I.a, &I.b, &I.c})
+        if (r->k == R_INS) live[r->idx] = 1;
+    }
+    std::vector<uint32_t> remap(n0, 0);
+    std::vector<VIns> kept;
+    kept.reserve(n0);
+    for (uint32_t t = 0; t < n0; ++t) {
+      if (!live[t]) continue;
+      remap[t] = (uint32_t)kept.size();
+      VIns I = S.ins[t];
+      for (Ref *r : {&I.a, &I.b, &I.c})
+        if (r->k == R_INS) r->idx = remap[r->idx];
+      kept.push_back(I);
+    }
+    S.ins.swap(kept);
+    if (root.k == R_INS) root.idx = remap[root.idx];
+  }
+
+  // ---------------------------------------------------------- liveness
+  const uint32_t n = (uint32_t)S.ins.size();
+  std::vector<int64_t> last_use(n, -1);       // last instruction reading the value
+  std::vector<uint8_t> needs_slot(n, 0);      // some use cannot be served from ACC
+  std::vector<int64_t> prev_bv(n + 1, -1);    // last BV-producing instruction before t
+  {
+    int64_t last = -1;
+    for (uint32_t t = 0; t < n; ++t) {
+      prev_bv[t] = last;
+      if (!S.ins[t].is_bool) last = t;
+    }
+    prev_bv[n] = last;
+  }
+  auto use = [&](const Ref &r, uint32_t t, bool bool_opnd) {
+    if (r.k != R_INS) return;
+    last_use[r.idx] = std::max<int64_t>(last_use[r.idx], t);
+    if (!bool_opnd && prev_bv[t] != (int64_t)r.idx) needs_slot[r.idx] = 1;
+  };
+  for (uint32_t t = 0; t < n; ++t) {
+    const VIns &I = S.ins[t];
+    if (op_takes_bools(I.op)) {
+      use(I.a, t, true); use(I.b, t, true); use(I.c, t, true);
+    } else if (I.op == MGP_OP_ITE) {
+      use(I.a, t, true); use(I.b, t, false); use(I.c, t, false);
+    } else {
+      use(I.a, t, false); use(I.b, t, false); use(I.c, t, false);
+    }
+  }
+  if (root.k == R_INS) last_use[root.idx] = std::max<int64_t>(last_use[root.idx], n);
+
+  // ---------------------------------------------------------- allocation
+  const uint32_t slot_cap = std::min<uint32_t>(max_slots ? max_slots : 32u, 255u);
+  std::vector<int32_t> loc(n, -1);
+  std::vector<uint32_t> free_slots, free_bools;
+  for (int32_t s = (int32_t)slot_cap - 1; s >= 0; --s) free_slots.push_back((uint32_t)s);
+  for (int32_t b = MGP_BOOL_ALLOC - 1; b >= 0; --b) free_bools.push_back((uint32_t)b);
+  std::vector<std::vector<uint32_t>> expire(n + 1);
+  for (uint32_t t = 0; t < n; ++t)
+    if (last_use[t] >= 0 && last_use[t] <= (int64_t)n) expire[last_use[t]].push_back(t);
+  uint32_t slots_used = 0;
+
+  std::vector<uint32_t> out;
+  out.reserve(4 + 4 * n + 8 * S.pool.size() + 4);
+  out.resize(4, 0u);
+
+  auto bv_opnd = [&](const Ref &r, uint32_t t) -> uint32_t {
+    switch (r.k) {
+      case R_VAR: return MGP_OPND(MGP_K_VAR, r.idx);
+      case R_CONST: return MGP_OPND(MGP_K_CONST, r.idx);
+      case R_INS:
+        if (prev_bv[t] == (int64_t)r.idx) return MGP_OPND(MGP_K_ACC, 0);
+        return MGP_OPND(MGP_K_SLOT, (uint32_t)loc[r.idx]);
+      default: return 0;
+    }
+  };
+  auto bool_opnd = [&](const Ref &r) -> uint32_t {
+    if (r.k == R_BOOLC) return r.idx ? MGP_BOOL_TRUE : MGP_BOOL_FALSE;
+    if (r.k == R_INS) return (uint32_t)loc[r.idx];
+    return MGP_BOOL_FALSE;
+  };
+
+  uint32_t n_emit = 0;
+  for (uint32_t t = 0; t < n; ++t) {
+    const VIns &I = S.ins[t];
+    uint32_t oa, ob = 0, oc = 0;
+    if (op_takes_bools(I.op)) {
+      oa = bool_opnd(I.a); ob = bool_opnd(I.b); oc = bool_opnd(I.c);
+    } else if (I.op == MGP_OP_ITE) {
+      oa = bool_opnd(I.a); ob = bv_opnd(I.b, t); oc = bv_opnd(I.c, t);
+    } else {
+      oa = bv_opnd(I.a, t);
+      ob = I.b.k != R_NONE ? bv_opnd(I.b, t) : 0u;
+      oc = I.c.k != R_NONE ? bv_opnd(I.c, t) : 0u;
+    }
+    // operands read first: free values whose last use is this instruction
+    for (uint32_t v : expire[t]) {
+      if (loc[v] < 0) continue;
+      if (S.ins[v].is_bool) free_bools.push_back((uint32_t)loc[v]);
+      else free_slots.push_back((uint32_t)loc[v]);
+    }
+    uint32_t dst = 0, flags = 0;
+    const bool live = last_use[t] > (int64_t)t;
+    if (I.is_bool) {
+      if (live) {
+        if (free_bools.empty()) return unsupported();
+        dst = free_bools.back();
+        free_bools.pop_back();
+        loc[t] = (int32_t)dst;
+      } else {
+        return unsupported();  // unreachable after DCE
+      }
+    } else if (live && needs_slot[t]) {
+      if (free_slots.empty()) return unsupported();
+      dst = free_slots.back();
+      free_slots.pop_back();
+      loc[t] = (int32_t)dst;
+      slots_used = std::max(slots_used, dst + 1);
+      flags = MGP_INS_STORE;
+    }
+    const uint32_t width_field = (uint32_t)(I.width ? I.width - 1 : 0) & 0xFFu;
+    out.push_back((uint32_t)I.op | (width_field << 8) | (dst << 16) | (flags << 24));
+    out.push_back((oa & 0xFFFFu) | (ob << 16));
+    out.push_back((oc & 0xFFFFu) | ((I.imm & 0xFFFFu) << 16));
+    out.push_back(0u);
+    ++n_emit;
+  }
+  // RET
+  out.push_back((uint32_t)MGP_OP_RET);
+  out.push_back(bool_opnd(root));
+  out.push_back(0u);
+  out.push_back(0u);
+  ++n_emit;
+
+  out[0] = n_emit;
+  out[1] = (uint32_t)S.pool.size();
+  out[2] = slots_used;
+  out[3] = (uint32_t)MGP_ST_OK | (S.max_var << 8);
+  for (const ConstKey &k : S.pool)
+    for (int l = 0; l < 8; ++l) out.push_back(k.w[l]);
+  while (out.size() % 4) out.push_back(0u);
+  Lowered L;
+  L.words.swap(out);
+  return L;
+}
+
+}  // namespace
+
+extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                         const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_slots,
+                         uint32_t *out_words, uint64_t out_cap, uint64_t *out_prog_offsets,
+                         uint8_t *out_status, uint64_t *out_words_used) {
+  if (!node_offsets || !out_prog_offsets || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
+  std::vector<Lowered> res(n_states);
+  int bad = 0;
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
+    const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
+    if (n1 < n0 || c1 < c0) {
+#pragma omp atomic write
+      bad = 1;
+      continue;
+    }
+    res[s] = lower_one(nodes + n0, n1 - n0, consts ? consts + c0 * 8u : nullptr, c1 - c0, max_slots);
+  }
+  if (bad) return MGP_E_ARG;
+  uint64_t total = 0;
+  for (uint32_t s = 0; s < n_states; ++s) {
+    out_prog_offsets[s] = total;
+    total += res[s].words.size();
+  }
+  out_prog_offsets[n_states] = total;
+  if (out_words_used) *out_words_used = total;
+  if (!out_words || total > out_cap) return MGP_E_CAPACITY;
+#pragma omp parallel for schedule(static)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    memcpy(out_words + out_prog_offsets[s], res[s].words.data(), res[s].words.size() * 4u);
+    if (out_status) out_status[s] = res[s].status;
+  }
+  return MGP_OK;
+}

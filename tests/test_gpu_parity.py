@@ -1,0 +1,179 @@
+"""GPU parity: the HIP path (through the C ABI of libmgp.so) vs the CPU oracle.
+
+Integer work, so the bar is bit-exact: first-SAT index, witness words and
+Keccak digests must equal the oracle's on the same seeded inputs.
+"""
+import numpy as np
+import pytest
+
+from mythril_amd import _native as N
+from oracle import bvsem as S
+from oracle import coracle
+from oracle.keccak_ref import keccak256 as keccak_py
+
+from ._util import cands_from_ints, load_golden, pack_states, random_cands
+
+pytestmark = pytest.mark.gpu
+
+
+def _lower(nodes, noff, consts, coff, **kw):
+    words, po, status = N.lower(nodes, noff, consts, coff, **kw)
+    return words, po, status
+
+
+# ------------------------------------------------------------ golden vectors
+def test_vm_arith_golden_on_gpu(mgp_ctx):
+    """Every SSTOREd value of the reference's straight-line VMTests, recomputed by the kernel."""
+    cases = [t for t in load_golden("vm_arith.json") if t["reference_agrees"]]
+    states = []
+    for t in cases:
+        consts = [int(c, 16) for c in t["consts"]]
+        for node, exp in t["checks"]:
+            nl = [list(n) for n in t["nodes"]]
+            consts_x = consts + [int(exp, 16)]
+            nl.append([S.CONST, 256, -1, -1, -1, len(consts_x) - 1, 0])
+            nl.append([S.EQ, 1, node, len(nl) - 1, -1, 0, 0])
+            states.append((nl, consts_x))
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = np.zeros((len(states), 1, 1, 8), dtype=np.uint32)
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    bad = [i for i in range(len(states)) if first[i] != 0]
+    assert not bad, f"{len(bad)} VMTests values differ on GPU (first: {bad[:5]})"
+
+
+def test_shift_vectors_on_gpu(mgp_ctx):
+    vecs = load_golden("shift_vectors.json")
+    opmap = {"shl": S.SHL, "shr": S.LSHR, "sar": S.ASHR}
+    states = []
+    for v in vecs:
+        val, sh, ex = int(v["value"], 16), int(v["shift"], 16), int(v["expected"], 16)
+        # value and shift come in as candidate variables (not constants) so the
+        # kernel cannot fold anything
+        nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0],
+              [opmap[v["op"]], 256, 0, 1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 0, 0],
+              [S.EQ, 1, 2, 3, -1, 0, 0]]
+        states.append((nl, [ex], [val, sh]))
+    nodes, noff, consts, coff = pack_states([(s[0], s[1]) for s in states])
+    words, po, status = _lower(nodes, noff, consts, coff)
+    cands = cands_from_ints([[s[2]] for s in states])
+    first, wit = mgp_ctx.eval_batch(words, po, cands)
+    assert (first == 0).all(), np.nonzero(first != 0)
+
+
+# --------------------------------------------------------------- synthetic
+@pytest.mark.parametrize("n_cand", [1, 37, 64, 256, 300])
+def test_synthetic_vs_c_oracle(mgp_ctx, n_cand):
+    n_states = 3000 if n_cand <= 256 else 800
+    b = N.synth_generate(0x4D595448, 12345, n_states, 64, n_cand)
+    words, po, status = _lower(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+    rng = np.random.default_rng(n_cand)
+    cands = random_cands(rng, n_states, n_cand, b["n_vars"])
+    for s in range(n_states):
+        if b["planted"][s]:
+            cands[s, b["plant_idx"][s]] = b["plant_words"][s]
+    first, wit = mgp_ctx.eval_batch(words, po, cands)
+    ref = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)
+    mism = np.nonzero(first != ref)[0]
+    assert mism.size == 0, f"{mism.size} states differ, e.g. {mism[:5]} gpu={first[mism[:5]]} ref={ref[mism[:5]]}"
+    sat = first >= 0
+    assert sat.sum() >= b["planted"].sum()
+    for s in np.nonzero(sat)[0][:200]:
+        assert (wit[s] == cands[s, first[s]]).all()
+
+
+def test_edge_values_all_ops(mgp_ctx):
+    """Every BV op at widths 256/160/64/8/1 on boundary operands vs oracle.bvsem."""
+    ops = [S.ADD, S.SUB, S.MUL, S.UDIV, S.UREM, S.SDIV, S.SREM, S.SMOD, S.AND, S.OR, S.XOR, S.SHL, S.LSHR,
+           S.ASHR]
+    cmps = [S.EQ, S.ULT, S.ULE, S.UGT, S.UGE, S.SLT, S.SLE, S.SGT, S.SGE, S.UADD_NOOVF, S.UMUL_NOOVF,
+            S.USUB_NOUDF]
+    widths = [256, 160, 64, 8, 1]
+    rng = np.random.default_rng(7)
+    states, cand_rows, expect = [], [], []
+    for w in widths:
+        m = (1 << w) - 1
+        vals = sorted({0, 1, 2, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1, 3 & m, (m >> 1) + 2 & m}
+                      | {int(rng.integers(0, 2 ** 63)) & m for _ in range(3)})
+        pairs = [(a, b) for a in vals for b in vals]
+        for op in ops + cmps:
+            for a, bb in pairs[:: max(1, len(pairs) // 24)]:
+                is_cmp = op in cmps
+                nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0],
+                      [op, 1 if is_cmp else w, 0, 1, -1, 0, 0]]
+                if is_cmp:
+                    res = S.cmpop(op, a, bb, w)
+                    nl.append([S.BNOT, 1, 2, -1, -1, 0, 0] if not res else [S.BAND, 1, 2, 2, -1, 0, 0])
+                    consts = []
+                else:
+                    res = S.binop(op, a, bb, w)
+                    nl.append([S.CONST, w, -1, -1, -1, 0, 0])
+                    nl.append([S.EQ, 1, 2, 3, -1, 0, 0])
+                    consts = [res]
+                states.append((nl, consts))
+                # high garbage bits above the var width must be ignored
+                cand_rows.append([[a | (int(rng.integers(1, 2 ** 62)) << w if w < 256 else a, bb]])
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = cands_from_ints(cand_rows)
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    bad = np.nonzero(first != 0)[0]
+    assert bad.size == 0, f"{bad.size} op/edge cases wrong, first: {bad[:8]}"
+
+
+def test_unsupported_and_empty(mgp_ctx):
+    # width 512 (not supported this round) -> MGP_UNDECIDED, other states unaffected
+    nl_bad = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.CONCAT, 512, 0, 1, -1, 0, 0],
+              [S.EQ, 1, 2, 2, -1, 0, 0]]
+    nl_ok = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 1, -1, 0, 0]]
+    nl_true = [[S.TRUE, 1, -1, -1, -1, 0, 0]]
+    nl_false = [[S.FALSE, 1, -1, -1, -1, 0, 0]]
+    nodes, noff, consts, coff = pack_states([(nl_bad, []), (nl_ok, []), (nl_true, []), (nl_false, [])])
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert list(status) == [1, 0, 0, 0]
+    cands = cands_from_ints([[[5, 3], [3, 5]]] * 4)
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    assert list(first) == [N.MGP_UNDECIDED, 1, 0, N.MGP_NO_SAT]
+    # zero states is a no-op
+    f0, _ = mgp_ctx.eval_batch(np.zeros(0, np.uint32), np.zeros(1, np.uint64), np.zeros((0, 1, 1, 8), np.uint32))
+    assert f0.size == 0
+
+
+def test_uf_ackermann_semantics(mgp_ctx):
+    """keccak UF pairs: f(a)==f(b) forces equal values only when a==b, inverse round trip."""
+    # nodes: x0, x1, f(x0)[fresh 2], f(x1)[fresh 3], inv(f(x0))[fresh 4]
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0],
+          [S.UFAPP, 256, 0, -1, -1, 0, 2], [S.UFAPP, 256, 1, -1, -1, 0, 3],
+          [S.UFINV, 256, 2, -1, -1, 0, 4],
+          [S.EQ, 1, 2, 3, -1, 0, 0],          # f(x0) == f(x1)
+          [S.EQ, 1, 4, 0, -1, 0, 0],          # inv(f(x0)) == x0
+          [S.BAND, 1, 5, 6, -1, 0, 0]]
+    rows = [[[7, 7, 11, 13, 99], [7, 8, 11, 13, 99], [7, 8, 11, 11, 99], [7, 8, 12, 12, 7]]]
+    nodes, noff, consts, coff = pack_states([(nl, [])])
+    words, po, status = _lower(nodes, noff, consts, coff)
+    cands = cands_from_ints(rows)
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    ref = S.first_sat(nl, [], rows[0])
+    assert first[0] == ref == 0
+
+
+# ------------------------------------------------------------------ Keccak
+def test_keccak_kats_on_gpu(mgp_ctx):
+    for k in load_golden("keccak_kat.json"):
+        pre = bytes.fromhex(k["preimage"])
+        out = mgp_ctx.keccak256_n(np.frombuffer(pre, dtype=np.uint8), 1, len(pre), max(len(pre), 1))
+        assert out[0].tobytes().hex() == k["digest"], k["source"]
+
+
+@pytest.mark.parametrize("length", [0, 1, 31, 32, 55, 64, 100, 135, 136, 137, 200, 272, 300])
+def test_keccak_lengths_vs_oracle(mgp_ctx, length):
+    rng = np.random.default_rng(length)
+    n = 777
+    stride = length + 3
+    data = rng.integers(0, 256, size=n * stride + 8, dtype=np.uint8)
+    out = mgp_ctx.keccak256_n(data, n, length, stride)
+    ref = coracle.keccak256(data, n, length, stride)
+    assert (out == ref).all()
+    assert out[5].tobytes() == keccak_py(data[5 * stride:5 * stride + length].tobytes())

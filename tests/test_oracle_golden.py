@@ -1,0 +1,127 @@
+"""Pin the CPU oracle to the reference's own golden data (CPU-only).
+
+* Keccak-256 KATs from the VMTests the reference runs (vmSha3Test) and the
+  empty-hash constant of keccak_function_manager.py:71-78.
+* EIP-145 shift vectors from tests/instructions/{shl,shr,sar}_test.py.
+* Straight-line VMTests (vmArithmeticTest, vmBitwiseLogicOperation) rebuilt as
+  constraint DAGs the way LASER builds z3 terms; every SSTOREd value must equal
+  the fixture's expected post-storage.
+* The Python restatement (oracle.bvsem) and the C restatement (oracle/c) agree.
+"""
+import numpy as np
+import pytest
+
+from mythril_amd import _native as N
+from oracle import bvsem as S
+from oracle import coracle
+from oracle.keccak_ref import EMPTY_HASH, keccak256
+
+from ._util import load_golden, pack_states, random_cands, state_slice
+
+
+def test_keccak_kats_python_and_c():
+    kats = load_golden("keccak_kat.json")
+    assert len(kats) >= 10
+    for k in kats:
+        pre = bytes.fromhex(k["preimage"])
+        assert keccak256(pre).hex() == k["digest"], k["source"]
+        c = coracle.keccak256(np.frombuffer(pre, dtype=np.uint8), 1, len(pre), max(1, len(pre)))
+        assert c[0].tobytes().hex() == k["digest"], k["source"]
+    assert int.from_bytes(keccak256(b""), "big") == EMPTY_HASH
+
+
+def test_keccak_not_nist_sha3():
+    import hashlib
+
+    assert keccak256(b"").hex() != hashlib.sha3_256(b"").hexdigest()
+
+
+def test_keccak_python_vs_c_random_lengths():
+    rng = np.random.default_rng(3)
+    for ln in [0, 1, 63, 64, 135, 136, 137, 271, 272, 500]:
+        data = rng.integers(0, 256, size=ln * 4 + 1, dtype=np.uint8)
+        c = coracle.keccak256(data, 4, ln, ln)
+        for i in range(4):
+            assert c[i].tobytes() == keccak256(data[i * ln:(i + 1) * ln].tobytes())
+
+
+def test_shift_vectors():
+    vecs = load_golden("shift_vectors.json")
+    assert len(vecs) >= 40
+    fn = {"shl": S.bvshl, "shr": S.bvlshr, "sar": S.bvashr}
+    for v in vecs:
+        val, sh, ex = int(v["value"], 16), int(v["shift"], 16), int(v["expected"], 16)
+        assert fn[v["op"]](val, sh, 256) == ex, v
+
+
+def _arith_states(cases):
+    states = []
+    for t in cases:
+        consts = [int(c, 16) for c in t["consts"]]
+        for node, exp in t["checks"]:
+            nl = [list(n) for n in t["nodes"]]
+            cx = consts + [int(exp, 16)]
+            nl.append([S.CONST, 256, -1, -1, -1, len(cx) - 1, 0])
+            nl.append([S.EQ, 1, node, len(nl) - 1, -1, 0, 0])
+            states.append((nl, cx))
+    return states
+
+
+def test_vm_arith_python_oracle():
+    cases = load_golden("vm_arith.json")
+    agree = [t for t in cases if t["reference_agrees"]]
+    assert len(agree) >= 200
+    for t in agree:
+        consts = [int(c, 16) for c in t["consts"]]
+        vals = S.eval_dag(t["nodes"], consts, [])
+        for node, exp in t["checks"]:
+            assert vals[node] == int(exp, 16), t["name"]
+
+
+def test_vm_arith_c_oracle():
+    states = _arith_states([t for t in load_golden("vm_arith.json") if t["reference_agrees"]])
+    nodes, noff, consts, coff = pack_states(states)
+    cands = np.zeros((len(states), 1, 1, 8), dtype=np.uint32)
+    out = coracle.first_sat(nodes, noff, consts, coff, cands)
+    assert (out == 0).all()
+
+
+def test_vm_arith_disagreements_are_division_by_zero_only():
+    """The only VMTests where z3 term semantics != EVM expectation are ADDMOD/MULMOD by 0
+    (LASER builds URem(...) with no zero guard, instructions.py:551-579; SMT-LIB x%0 = x)."""
+    bad = [t["name"] for t in load_golden("vm_arith.json") if not t["reference_agrees"]]
+    assert all("ByZero" in n or "byZero" in n for n in bad), bad
+
+
+def test_smtlib_division_conventions():
+    w = 256
+    m = (1 << w) - 1
+    assert S.bvudiv(5, 0, w) == m
+    assert S.bvurem(5, 0, w) == 5
+    assert S.bvsdiv(5, 0, w) == m
+    assert S.bvsdiv(m, 0, w) == 1  # -1 / 0 = 1
+    assert S.bvsrem(m - 4, 0, w) == m - 4
+    assert S.bvsmod(m - 4, 0, w) == m - 4
+    assert S.bvsdiv(1 << 255, m, w) == 1 << 255  # overflow wraps
+    assert S.bvsrem(m - 6, 3, w) == m  # -7 % 3 = -1
+    assert S.bvsmod(m - 6, 3, w) == 2  # -7 mod 3 = 2
+    assert S.bvashr(1 << 255, 300, w) == m
+
+
+@pytest.mark.parametrize("seed_base", [0, 777])
+def test_python_vs_c_oracle_synthetic(seed_base):
+    n_states, n_cand = 120, 12
+    b = N.synth_generate(0x4D595448, seed_base, n_states, 64, n_cand)
+    rng = np.random.default_rng(seed_base)
+    cands = random_cands(rng, n_states, n_cand, b["n_vars"])
+    for s in range(n_states):
+        if b["planted"][s]:
+            cands[s, b["plant_idx"][s]] = b["plant_words"][s]
+    c_res = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)
+    for s in range(n_states):
+        nodes, consts = state_slice(b, s)
+        rows = [[S.limbs_to_int(cands[s, c, v]) for v in range(b["n_vars"])] for c in range(n_cand)]
+        assert S.first_sat(nodes, consts, rows) == c_res[s], s
+    # planted witnesses really satisfy (checks the generator's planting with the oracle)
+    pl = np.nonzero(b["planted"])[0]
+    assert len(pl) > 0 and (c_res[pl] >= 0).all() and (c_res[pl] <= b["plant_idx"][pl]).all()

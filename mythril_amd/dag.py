@@ -1,0 +1,263 @@
+"""Terms -> per-state constraint DAGs (include/mgp_ir.h node lists) and candidates.
+
+`build_state` flattens the conjunction of a state's path constraints
+(mythril/laser/ethereum/state/constraints.py:10-126 holds them as a list of
+Bool) into a topologically ordered node list with a constant pool and a
+variable table.  Every uninterpreted-function application (keccak256_<n>,
+its inverse, base-array selects) gets a fresh candidate variable — the
+Ackermann encoding the HIP path evaluates (mgp_lower.cpp).
+
+`make_candidates` builds the candidate assignments one state is evaluated on:
+the parent state's witness first (a successor only adds constraints to its
+parent, svm.py:251-255 / instructions.py:1533-1610), then assignments
+harvested from the DAG's own constants (x == c, x +- 1 around compared
+constants, LASER's actor addresses transaction/symbolic.py:22-27, keccak
+interval bases keccak_function_manager.py:118-146), then uniform values.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import ir
+from ._native import NODE_DTYPE
+from .smt import Term
+
+ACTORS = (0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE, 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,
+          0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA)
+SPECIAL = (0, 1, 2, (1 << 256) - 1, 1 << 255, (1 << 160) - 1, 10 ** 18, 10 ** 20)
+
+
+@dataclass
+class StateDag:
+    nodes: List[Tuple[int, int, int, int, int, int, int]] = field(default_factory=list)
+    consts: List[int] = field(default_factory=list)
+    vars: List[Tuple[str, int]] = field(default_factory=list)  # (name, width); index = var index
+    var_terms: List[Optional[Term]] = field(default_factory=list)
+    hints: Dict[int, List[int]] = field(default_factory=dict)  # var index -> harvested values
+    aliases: List[Tuple[int, int]] = field(default_factory=list)  # (dst var, src var) from x == y
+
+    @property
+    def n_vars(self) -> int:
+        return len(self.vars)
+
+
+def build_state(constraints: Sequence[Term]) -> StateDag:
+    """Flatten And(constraints) into a StateDag (root = last node, Bool)."""
+    d = StateDag()
+    memo: Dict[int, int] = {}
+    var_idx: Dict[Tuple[str, int], int] = {}
+    const_idx: Dict[int, int] = {}
+
+    def new_var(name: str, width: int, term: Optional[Term]) -> int:
+        key = (name, width)
+        if key not in var_idx:
+            var_idx[key] = len(d.vars)
+            d.vars.append(key)
+            d.var_terms.append(term)
+        return var_idx[key]
+
+    def emit(t: Term) -> int:
+        ch = [memo[id(a)] for a in t.args]
+        a, b, c = (ch + [-1, -1, -1])[:3]
+        w = 1 if t.width == 0 else t.width
+        p0 = p1 = 0
+        op = t.op
+        if op == ir.VAR:
+            p0 = new_var(str(t.params[0]), w, t)
+        elif op == ir.CONST:
+            v = t.params[0]
+            if v not in const_idx:
+                const_idx[v] = len(d.consts)
+                d.consts.append(v)
+            p0 = const_idx[v]
+        elif op == ir.EXTRACT:
+            p0, p1 = t.params
+        elif op in (ir.UFAPP, ir.UFINV):
+            fid, name = t.params
+            p0 = fid
+            p1 = new_var(f"{name}@{len(d.nodes)}", w, None)
+        d.nodes.append((op, w, a, b, c, p0, p1))
+        return len(d.nodes) - 1
+
+    roots: List[int] = []
+    for root in constraints:
+        stack: List[Tuple[Term, bool]] = [(root, False)]
+        while stack:
+            t, done = stack.pop()
+            if id(t) in memo:
+                continue
+            if done:
+                memo[id(t)] = emit(t)
+                continue
+            stack.append((t, True))
+            for a in reversed(t.args):
+                if id(a) not in memo:
+                    stack.append((a, False))
+        roots.append(memo[id(root)])
+    if not roots:
+        d.nodes.append((ir.TRUE, 1, -1, -1, -1, 0, 0))
+    else:
+        r = roots[0]
+        for x in roots[1:]:
+            d.nodes.append((ir.BAND, 1, r, x, -1, 0, 0))
+            r = len(d.nodes) - 1
+        if r != len(d.nodes) - 1:  # root must be the last node
+            d.nodes.append((ir.BAND, 1, r, r, -1, 0, 0))
+    _harvest_hints(d)
+    return d
+
+
+def _var_of(nodes, x) -> int:
+    op = nodes[x][0]
+    if op == ir.VAR:
+        return nodes[x][5]
+    if op in (ir.UFAPP, ir.UFINV):
+        return nodes[x][6]
+    return -1
+
+
+def _harvest_hints(d: StateDag) -> None:
+    """x == c -> x := c ; x <op> c -> c-1, c, c+1 and 64-aligned neighbours (keccak
+    intervals, keccak_function_manager.py:135-140) ; x == y -> alias pair."""
+    nodes = d.nodes
+    for (op, w, a, b, c, p0, p1) in nodes:
+        if op < ir.EQ or op > ir.USUB_NOUDF or a < 0 or b < 0:
+            continue
+        va, vb = _var_of(nodes, a), _var_of(nodes, b)
+        if op == ir.EQ and va >= 0 and vb >= 0 and va != vb:
+            d.aliases.append((va, vb))
+            d.aliases.append((vb, va))
+        for vi, y in ((va, b), (vb, a)):
+            if vi < 0 or nodes[y][0] != ir.CONST:
+                continue
+            cv = d.consts[nodes[y][5]]
+            m = (1 << nodes[a][1]) - 1
+            if op == ir.EQ:
+                vals = [cv]
+            else:
+                up = (cv + 63) & ~63 & m
+                vals = [up, (up + 64) & m, cv, (cv - 1) & m, (cv + 1) & m]
+            d.hints.setdefault(vi, []).extend(vals)
+
+
+def pack_states(states: Sequence[StateDag]):
+    """-> (nodes NODE_DTYPE, node_offsets u64, consts u32[n,8], const_offsets u64)."""
+    n_nodes = sum(len(s.nodes) for s in states)
+    nodes = np.zeros(n_nodes, dtype=NODE_DTYPE)
+    noff = np.zeros(len(states) + 1, dtype=np.uint64)
+    n_c = sum(len(s.consts) for s in states)
+    consts = np.zeros((n_c, 8), dtype=np.uint32)
+    coff = np.zeros(len(states) + 1, dtype=np.uint64)
+    i = j = 0
+    for k, s in enumerate(states):
+        for (op, w, a, b, c, p0, p1) in s.nodes:
+            nodes[i] = (op, 0, w, a, b, c, p0, p1)
+            i += 1
+        for v in s.consts:
+            consts[j] = [(v >> (32 * l)) & 0xFFFFFFFF for l in range(8)] if v < (1 << 256) else 0
+            j += 1
+        noff[k + 1] = i
+        coff[k + 1] = j
+    return nodes, noff, consts, coff
+
+
+def _to_limbs(v: int) -> List[int]:
+    return [(v >> (32 * l)) & 0xFFFFFFFF for l in range(8)]
+
+
+def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: int = 0x4D595448,
+                    parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> np.ndarray:
+    """uint32 [n_states, n_cand, n_vars, 8] candidate assignments (host layout of mgp_eval_batch).
+
+    c0 parent witness (if any), c1 first hint of every var, c2 = c1 with every
+    x == y alias applied, then a seeded mixture per var: 35 % harvested hint,
+    25 % pool (state constants +-1, actors, boundary values), 15 % alias of an
+    equal-width var, 25 % uniform.
+    """
+    rng = np.random.default_rng(seed)
+    out = rng.integers(0, 2 ** 32, size=(len(states), n_cand, n_vars, 8), dtype=np.uint64).astype(np.uint32)
+    for s, st in enumerate(states):
+        V = st.n_vars
+        widths = [w for (_, w) in st.vars]
+        pools: List[List[int]] = []
+        for vi, w in enumerate(widths):
+            m = (1 << w) - 1
+            pool = [v & m for v in st.consts] + [(v + 1) & m for v in st.consts] + [(v - 1) & m for v in st.consts]
+            pools.append(pool + [v & m for v in ACTORS + SPECIAL])
+        same_w: Dict[int, List[int]] = {}
+        for vi, w in enumerate(widths):
+            same_w.setdefault(w, []).append(vi)
+        # masks so that uniform values respect narrow widths
+        for vi, w in enumerate(widths):
+            if w < 256:
+                for l in range(8):
+                    lo = 32 * l
+                    mask = 0xFFFFFFFF if w >= lo + 32 else (0 if w <= lo else (1 << (w - lo)) - 1)
+                    out[s, :, vi, l] &= np.uint32(mask)
+        vals = np.zeros((n_cand, V), dtype=object)
+        have = np.zeros((n_cand, V), dtype=bool)
+        row = 0
+        if parents is not None and parents[s]:
+            for vi, (name, w) in enumerate(st.vars):
+                if name in parents[s]:
+                    vals[0, vi] = parents[s][name] & ((1 << w) - 1)
+                    have[0, vi] = True
+            row = 1
+        for structured in (False, True):
+            if row >= n_cand:
+                break
+            for vi in range(V):
+                if st.hints.get(vi):
+                    vals[row, vi] = st.hints[vi][0]
+                    have[row, vi] = True
+            if structured:
+                for (dst, src) in st.aliases:
+                    if widths[dst] == widths[src] and have[row, src] and not have[row, dst]:
+                        vals[row, dst] = vals[row, src]
+                        have[row, dst] = True
+            row += 1
+        for c in range(row, n_cand):
+            alias_todo = []
+            for vi in range(V):
+                r = rng.random()
+                hv = st.hints.get(vi)
+                if r < 0.35 and hv:
+                    vals[c, vi] = hv[int(rng.integers(0, len(hv)))]
+                    have[c, vi] = True
+                elif r < 0.60 and pools[vi]:
+                    vals[c, vi] = pools[vi][int(rng.integers(0, len(pools[vi])))]
+                    have[c, vi] = True
+                elif r < 0.75:
+                    alias_todo.append(vi)
+            for vi in alias_todo:  # after the others, so an alias can copy any var
+                srcs = [u for (d_, u) in st.aliases if d_ == vi] or [u for u in same_w[widths[vi]] if u != vi]
+                if srcs:
+                    u = srcs[int(rng.integers(0, len(srcs)))]
+                    if have[c, u]:
+                        vals[c, vi] = vals[c, u]
+                    else:
+                        vals[c, vi] = int(sum(int(out[s, c, u, l]) << (32 * l) for l in range(8)))
+                    have[c, vi] = True
+        for c in range(n_cand):
+            for vi in range(V):
+                if have[c, vi]:
+                    out[s, c, vi] = _to_limbs(int(vals[c, vi]))
+    return out
+
+
+def witness_to_model(st: StateDag, words: np.ndarray) -> Dict[str, int]:
+    """Witness words [n_vars, 8] -> {var name: value masked to its width} (free vars only)."""
+    model: Dict[str, int] = {}
+    for vi, (name, w) in enumerate(st.vars):
+        v = 0
+        for l in range(8):
+            v |= int(words[vi, l]) << (32 * l)
+        model[name] = v & ((1 << w) - 1)
+    return model
+
+
+def nominal_ops(st: StateDag) -> int:
+    return sum(ir.NOMINAL_OPS.get(n[0], 0) for n in st.nodes)

@@ -1,0 +1,150 @@
+"""KeccakFunctionManager mirror + batched concrete Keccak-256 on the GPU.
+
+Mirrors mythril/laser/ethereum/keccak_function_manager.py:21-149 (same
+method names, constants and constraint shapes):
+
+  find_concrete_keccak(data)      40-54   concrete hash of data.size()//8 big-endian bytes
+  get_function(length)            56-69   UF pair keccak256_<n> / keccak256_<n>-1
+  get_empty_keccak_hash()         71-78
+  create_keccak(data)             80-98   (hash term, condition)
+  get_concrete_hash_data(model)   100-116
+  _create_condition(func_input)   118-146 interval [index*PART, index*PART+PART), %64 == 0,
+                                          OR over the concrete hashes seen so far
+
+The concrete hashes go through the HIP Keccak kernel (libmgp.so,
+mgp_keccak256_batch) — one launch for a whole batch via
+`find_concrete_keccak_batch` — instead of pyethereum's utils.sha3.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .smt import And, BitVec, Bool, Function, Or, ULE, ULT, URem, symbol_factory
+
+TOTAL_PARTS = 10 ** 40
+PART = (2 ** 256 - 1) // TOTAL_PARTS
+INTERVAL_DIFFERENCE = 10 ** 30
+hash_matcher = "fffffff"
+
+_ctx = None
+
+
+def _context():
+    global _ctx
+    if _ctx is None:
+        from . import _native as N
+
+        _ctx = N.Context(0)
+    return _ctx
+
+
+def keccak256_batch(preimages: Sequence[bytes]) -> List[bytes]:
+    """Keccak-256 of many byte strings in one GPU launch per distinct length."""
+    out: List[Optional[bytes]] = [None] * len(preimages)
+    by_len: Dict[int, List[int]] = {}
+    for i, p in enumerate(preimages):
+        by_len.setdefault(len(p), []).append(i)
+    ctx = _context()
+    for ln, idx in by_len.items():
+        buf = np.frombuffer(b"".join(preimages[i] for i in idx), dtype=np.uint8) if ln else np.zeros(1, np.uint8)
+        dig = ctx.keccak256_n(buf, len(idx), ln, max(ln, 1) if ln else 1)
+        for k, i in enumerate(idx):
+            out[i] = dig[k].tobytes()
+    return out  # type: ignore[return-value]
+
+
+def keccak256(data: bytes) -> bytes:
+    return keccak256_batch([data])[0]
+
+
+class KeccakFunctionManager:
+    def __init__(self):
+        self.store_function: Dict[int, Tuple[Function, Function]] = {}
+        self.interval_hook_for_size: Dict[int, int] = {}
+        self._index_counter = TOTAL_PARTS - 34534
+        self.hash_result_store: Dict[int, List[BitVec]] = {}
+        self.quick_inverse: Dict[BitVec, BitVec] = {}
+        self.concrete_hashes: Dict[BitVec, BitVec] = {}
+
+    @staticmethod
+    def find_concrete_keccak(data: BitVec) -> BitVec:
+        digest = keccak256(data.value.to_bytes(data.size() // 8, byteorder="big"))
+        return symbol_factory.BitVecVal(int.from_bytes(digest, "big"), 256)
+
+    @staticmethod
+    def find_concrete_keccak_batch(datas: Sequence[BitVec]) -> List[BitVec]:
+        digs = keccak256_batch([d.value.to_bytes(d.size() // 8, byteorder="big") for d in datas])
+        return [symbol_factory.BitVecVal(int.from_bytes(h, "big"), 256) for h in digs]
+
+    def get_function(self, length: int) -> Tuple[Function, Function]:
+        try:
+            func, inverse = self.store_function[length]
+        except KeyError:
+            func = Function("keccak256_{}".format(length), length, 256)
+            inverse = Function("keccak256_{}-1".format(length), 256, length, inverse_of=func)
+            self.store_function[length] = (func, inverse)
+            self.hash_result_store[length] = []
+        return func, inverse
+
+    @staticmethod
+    def get_empty_keccak_hash() -> BitVec:
+        val = 89477152217924674838424037953991966239322087453347756267410168184682657981552
+        return symbol_factory.BitVecVal(val, 256)
+
+    def create_keccak(self, data: BitVec) -> Tuple[BitVec, Bool]:
+        length = data.size()
+        func, inverse = self.get_function(length)
+        if data.symbolic is False:
+            concrete_hash = self.find_concrete_keccak(data)
+            self.concrete_hashes[data] = concrete_hash
+            condition = And(func(data) == concrete_hash, inverse(func(data)) == data)
+            return concrete_hash, condition
+        condition = self._create_condition(func_input=data)
+        self.hash_result_store[length].append(func(data))
+        return func(data), condition
+
+    def get_concrete_hash_data(self, model) -> Dict[int, List[Optional[int]]]:
+        concrete_hashes: Dict[int, List[Optional[int]]] = {}
+        for size in self.hash_result_store:
+            concrete_hashes[size] = []
+            for val in self.hash_result_store[size]:
+                v = model.eval(val.raw)
+                if v is not None:
+                    concrete_hashes[size].append(v)
+        return concrete_hashes
+
+    def _create_condition(self, func_input: BitVec) -> Bool:
+        length = func_input.size()
+        func, inv = self.get_function(length)
+        try:
+            index = self.interval_hook_for_size[length]
+        except KeyError:
+            self.interval_hook_for_size[length] = self._index_counter
+            index = self._index_counter
+            self._index_counter -= INTERVAL_DIFFERENCE
+        lower_bound = index * PART
+        upper_bound = lower_bound + PART
+        cond = And(
+            inv(func(func_input)) == func_input,
+            ULE(symbol_factory.BitVecVal(lower_bound, 256), func(func_input)),
+            ULT(func(func_input), symbol_factory.BitVecVal(upper_bound, 256)),
+            URem(func(func_input), symbol_factory.BitVecVal(64, 256)) == 0,
+        )
+        concrete_cond = symbol_factory.Bool(False)
+        for key, keccak in self.concrete_hashes.items():
+            hash_eq = And(func(func_input) == keccak, key == func_input)
+            concrete_cond = Or(concrete_cond, hash_eq)
+        return And(inv(func(func_input)) == func_input, Or(cond, concrete_cond))
+
+    def interval_values(self, length: int, k: int = 4) -> List[int]:
+        """Candidate hash values for keccak256_<length>: aligned points of its interval."""
+        if length not in self.interval_hook_for_size:
+            return []
+        lo = self.interval_hook_for_size[length] * PART
+        lo += (-lo) % 64
+        return [lo + 64 * j for j in range(k)]
+
+
+keccak_function_manager = KeccakFunctionManager()

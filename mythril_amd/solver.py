@@ -1,0 +1,415 @@
+"""GPU-first satisfiability front end — mirror of the reference's solver surface.
+
+Mirrors, with the same names, argument meaning and error behaviour:
+
+  get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True)
+      mythril/analysis/solver.py:27-61 — returns a Model or raises UnsatError
+      (on unsat AND on unknown/timeout); literal False -> UnsatError; Python
+      bools are dropped; lru_cache'd on the hashable constraint tuple.
+  Constraints.is_possible
+      mythril/laser/ethereum/state/constraints.py:30-51 — cached bit; unknown
+      counts as possible.
+  Solver / Optimize / SolverStatistics
+      mythril/laser/smt/solver/solver.py:15-105, solver_statistics.py:8-43 —
+      query_count counts every check() that reaches the fallback solver.
+
+What changes is the order: a batch of states is first evaluated on the GPU
+(libmgp.so) against candidate assignments; a witness PROVES satisfiability
+(`sat`).  Everything else — no witness, unsupported DAG, every UNSAT, every
+minimize/maximize query (tx-sequence model values must stay bit-identical to
+z3's, solver.py:88-136) — goes to the fallback backend unchanged.  The
+fallback is z3 (mythril_amd.z3_backend, where z3 is installed); without it the
+answer is `unknown`, which each caller maps exactly as the reference does.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from functools import lru_cache
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import dag as D
+from .smt import Bool, Expression, Term, bconst
+
+sat, unsat, unknown = "sat", "unsat", "unknown"
+
+
+class UnsatError(Exception):
+    """mythril/exceptions.py:16."""
+
+
+class _Singleton(type):
+    _inst: Dict[type, object] = {}
+    _lock = threading.Lock()
+
+    def __call__(cls, *a, **k):
+        with cls._lock:
+            if cls not in cls._inst:
+                cls._inst[cls] = super().__call__(*a, **k)
+        return cls._inst[cls]
+
+
+class SolverStatistics(metaclass=_Singleton):
+    """solver_statistics.py:29-43 plus the pre-filter's own counters."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.enabled = True
+        self.query_count = 0      # checks that reached the fallback solver (the reference's "z3 calls")
+        self.solver_time = 0.0
+        self.gpu_queries = 0      # states sent to the GPU
+        self.gpu_sat = 0          # states proven SAT by a GPU witness
+        self.gpu_undecided = 0
+        self.gpu_time = 0.0
+        self.gpu_batches = 0
+
+    def __repr__(self):
+        return (f"Query count: {self.query_count} \nSolver time: {self.solver_time}\n"
+                f"GPU queries: {self.gpu_queries} (sat {self.gpu_sat}, undecided {self.gpu_undecided}, "
+                f"{self.gpu_batches} batches, {self.gpu_time:.3f}s)")
+
+
+def stat_smt_query(func: Callable):
+    stats = SolverStatistics()
+
+    def wrapper(*args, **kwargs):
+        if not stats.enabled:
+            return func(*args, **kwargs)
+        stats.query_count += 1
+        t = time.time()
+        try:
+            return func(*args, **kwargs)
+        finally:
+            stats.solver_time += time.time() - t
+
+    return wrapper
+
+
+class Model:
+    """laser.smt.Model (model.py:6-59) over a {variable name: value} assignment."""
+
+    def __init__(self, assignments: Optional[Sequence[Dict[str, int]]] = None, raw=None):
+        self.assignments: List[Dict[str, int]] = list(assignments or [])
+        self.raw = raw  # a fallback solver's native model, when it produced this one
+
+    def decls(self) -> List[str]:
+        out: List[str] = []
+        for a in self.assignments:
+            out.extend(a.keys())
+        return out
+
+    def __getitem__(self, item):
+        if isinstance(item, int):
+            return self.decls()[item]
+        name = item.raw.params[0] if isinstance(item, Expression) else item
+        for a in self.assignments:
+            if name in a:
+                return a[name]
+        return None
+
+    def eval(self, expression, model_completion: bool = False):
+        t = expression.raw if isinstance(expression, Expression) else expression
+        if isinstance(t, Term):
+            if t.op == 2:  # CONST
+                return t.params[0]
+            if t.op == 1:  # VAR
+                v = self[str(t.params[0])]
+                return 0 if v is None and model_completion else v
+        return None
+
+
+# --------------------------------------------------------------- backends
+class Backend:
+    """Fallback solver interface: check(terms, timeout_ms, minimize, maximize) -> (result, Model|None)."""
+
+    name = "none"
+
+    def check(self, terms: Sequence[Term], timeout_ms: int, minimize=(), maximize=()) -> Tuple[str, Optional[Model]]:
+        return unknown, None
+
+
+_backend: Backend = Backend()
+
+
+def set_backend(b: Backend) -> Backend:
+    global _backend
+    old, _backend = _backend, b
+    return old
+
+
+def get_backend() -> Backend:
+    return _backend
+
+
+# ------------------------------------------------------------- GPU stage
+class Prefilter:
+    """Batched GPU witness search over states (one libmgp context)."""
+
+    def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448):
+        from . import _native as N
+
+        self._N = N
+        self.ctx = N.Context(device)
+        self.n_cand = n_cand
+        self.seed = seed
+        self._calls = 0
+
+    def check_states(self, states: Sequence[Sequence[Term]],
+                     parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> List[Tuple[str, Optional[Dict[str, int]]]]:
+        """-> per state ('sat', assignment) or ('undecided', None)."""
+        if not states:
+            return []
+        stats = SolverStatistics()
+        t0 = time.time()
+        dags = [D.build_state(s) for s in states]
+        n_vars = max(1, max(d.n_vars for d in dags))
+        nodes, noff, consts, coff = D.pack_states(dags)
+        words, po, status = self._N.lower(nodes, noff, consts, coff)
+        self._calls += 1
+        cands = D.make_candidates(dags, self.n_cand, n_vars, seed=self.seed + self._calls, parents=parents)
+        first, wit = self.ctx.eval_batch(words, po, cands)
+        out: List[Tuple[str, Optional[Dict[str, int]]]] = []
+        for i, d in enumerate(dags):
+            if first[i] >= 0:
+                out.append((sat, D.witness_to_model(d, wit[i])))
+            else:
+                out.append(("undecided", None))
+        stats.gpu_batches += 1
+        stats.gpu_queries += len(states)
+        stats.gpu_sat += sum(1 for r in out if r[0] == sat)
+        stats.gpu_undecided += sum(1 for r in out if r[0] != sat)
+        stats.gpu_time += time.time() - t0
+        return out
+
+
+_prefilter: Optional[Prefilter] = None
+_enabled = True
+
+
+def prefilter() -> Optional[Prefilter]:
+    """The process-wide GPU stage (None when disabled)."""
+    global _prefilter
+    if not _enabled:
+        return None
+    if _prefilter is None:
+        _prefilter = Prefilter()
+    return _prefilter
+
+
+def enable_gpu(flag: bool = True) -> None:
+    global _enabled
+    _enabled = flag
+
+
+def _terms(constraints: Iterable) -> List[Term]:
+    out = []
+    for c in constraints:
+        if isinstance(c, bool):
+            out.append(bconst(c))
+        elif isinstance(c, Expression):
+            out.append(c.raw)
+        else:
+            out.append(c)
+    return out
+
+
+# ------------------------------------------------------------ Solver API
+class BaseSolver:
+    def __init__(self):
+        self.constraints: List[Term] = []
+        self.timeout = 10000
+        self._model: Optional[Model] = None
+
+    def set_timeout(self, timeout: int) -> None:
+        self.timeout = timeout
+
+    def add(self, *constraints) -> None:
+        flat = []
+        for c in constraints:
+            flat.extend(c if isinstance(c, (list, tuple)) else [c])
+        self.constraints.extend(_terms(flat))
+
+    append = add
+
+    def model(self) -> Model:
+        return self._model
+
+
+class Solver(BaseSolver):
+    """GPU witness first, then the fallback solver (counted in SolverStatistics.query_count)."""
+
+    def check(self, *args) -> str:
+        pf = prefilter()
+        if pf is not None:
+            res, assign = pf.check_states([self.constraints])[0]
+            if res == sat:
+                self._model = Model([assign])
+                return sat
+        return self._fallback()
+
+    @stat_smt_query
+    def _fallback(self) -> str:
+        r, m = get_backend().check(self.constraints, self.timeout)
+        self._model = m
+        return r
+
+    def reset(self) -> None:
+        self.constraints = []
+
+
+class Optimize(BaseSolver):
+    """Optimize: always the fallback solver — minimised model values are reported verbatim."""
+
+    def __init__(self):
+        super().__init__()
+        self._min: List[Term] = []
+        self._max: List[Term] = []
+
+    def minimize(self, e) -> None:
+        self._min.append(e.raw if isinstance(e, Expression) else e)
+
+    def maximize(self, e) -> None:
+        self._max.append(e.raw if isinstance(e, Expression) else e)
+
+    def check(self, *args) -> str:
+        if not self._min and not self._max:
+            pf = prefilter()
+            if pf is not None:
+                res, assign = pf.check_states([self.constraints])[0]
+                if res == sat:
+                    self._model = Model([assign])
+                    return sat
+        return self._fallback()
+
+    @stat_smt_query
+    def _fallback(self) -> str:
+        r, m = get_backend().check(self.constraints, self.timeout, tuple(self._min), tuple(self._max))
+        self._model = m
+        return r
+
+
+class _Clock:
+    """time_handler (laser/ethereum/time_handler.py:5-18) stand-in: ms left of the execution budget."""
+
+    def __init__(self):
+        self.deadline: Optional[float] = None
+
+    def start_execution(self, seconds: float) -> None:
+        self.deadline = time.time() + seconds
+
+    def time_remaining(self) -> float:
+        return 1e12 if self.deadline is None else (self.deadline - time.time()) * 1000.0
+
+
+time_handler = _Clock()
+solver_timeout_ms = 10000  # analysis_args.solver_timeout default (analysis_args.py:11)
+
+
+@lru_cache(maxsize=2 ** 23)
+def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True) -> Model:
+    """analysis/solver.py:27-61 with a GPU witness stage for SAT-only queries."""
+    timeout = solver_timeout_ms
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+        if timeout <= 0:
+            raise UnsatError
+    for c in constraints:
+        if type(c) == bool and not c:
+            raise UnsatError
+    constraints = [c for c in constraints if type(c) != bool]
+    s = Optimize()
+    s.set_timeout(int(timeout))
+    for c in constraints:
+        s.add(c)
+    for e in minimize:
+        s.minimize(e)
+    for e in maximize:
+        s.maximize(e)
+    result = s.check()
+    if result == sat:
+        return s.model()
+    raise UnsatError
+
+
+class Constraints(list):
+    """constraints.py:10-126 with a GPU-first is_possible and witness inheritance."""
+
+    def __init__(self, constraint_list: Optional[List] = None, is_possible: Optional[bool] = None,
+                 witness: Optional[Dict[str, int]] = None):
+        constraint_list = self._get_smt_bool_list(constraint_list or [])
+        super().__init__(constraint_list)
+        self._default_timeout = 100
+        self._is_possible = is_possible
+        self.witness = witness  # last satisfying assignment seen (parent's for a fresh child)
+
+    @property
+    def is_possible(self) -> bool:
+        if self._is_possible is not None:
+            return self._is_possible
+        batch_is_possible([self])
+        return bool(self._is_possible)
+
+    def append(self, constraint) -> None:
+        super().append(constraint if isinstance(constraint, Bool) else Bool(bconst(bool(constraint))))
+        self._is_possible = None
+
+    def pop(self, index: int = -1) -> None:
+        raise NotImplementedError
+
+    @property
+    def as_list(self) -> List[Bool]:
+        return self[:]
+
+    def __copy__(self) -> "Constraints":
+        return Constraints(super().copy(), is_possible=self._is_possible, witness=self.witness)
+
+    def copy(self) -> "Constraints":
+        return self.__copy__()
+
+    def __deepcopy__(self, memodict=None) -> "Constraints":
+        return self.__copy__()
+
+    def __add__(self, constraints) -> "Constraints":
+        lst = super().__add__(self._get_smt_bool_list(constraints))
+        return Constraints(constraint_list=lst, is_possible=None, witness=self.witness)
+
+    def __iadd__(self, constraints) -> "Constraints":
+        super().__iadd__(self._get_smt_bool_list(constraints))
+        self._is_possible = None
+        return self
+
+    @staticmethod
+    def _get_smt_bool_list(constraints) -> List[Bool]:
+        return [c if isinstance(c, Bool) else Bool(bconst(bool(c))) for c in constraints]
+
+    def __hash__(self):
+        return tuple(self[:]).__hash__()
+
+
+def batch_is_possible(items: Sequence[Constraints]) -> List[bool]:
+    """The prune filter of LaserEVM.exec (svm.py:251-255) over a whole worklist.
+
+    One GPU batch for every uncached entry; each entry the GPU cannot prove SAT
+    goes through the reference's single-query path (100 ms fallback check,
+    unknown -> possible, constraints.py:42-51).
+    """
+    todo = [c for c in items if c._is_possible is None]
+    pf = prefilter()
+    results: List[Tuple[str, Optional[Dict[str, int]]]] = [("undecided", None)] * len(todo)
+    if pf is not None and todo:
+        results = pf.check_states([_terms(c) for c in todo], parents=[c.witness for c in todo])
+    for c, (res, assign) in zip(todo, results):
+        if res == sat:
+            c._is_possible = True
+            c.witness = assign
+            continue
+        s = Solver()
+        s.set_timeout(c._default_timeout)
+        s.add(*c)
+        r = s._fallback()
+        c._is_possible = r != unsat
+    return [bool(c._is_possible) for c in items]

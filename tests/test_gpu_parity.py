@@ -94,7 +94,7 @@ def test_edge_values_all_ops(mgp_ctx):
     states, cand_rows, expect = [], [], []
     for w in widths:
         m = (1 << w) - 1
-        vals = sorted({0, 1, 2, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1, 3 & m, (m >> 1) + 2 & m}
+        vals = sorted({v & m for v in (0, 1, 2, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1, 3, (m >> 1) + 2)}
                       | {int(rng.integers(0, 2 ** 63)) & m for _ in range(3)})
         pairs = [(a, b) for a in vals for b in vals]
         for op in ops + cmps:
@@ -113,7 +113,8 @@ def test_edge_values_all_ops(mgp_ctx):
                     consts = [res]
                 states.append((nl, consts))
                 # high garbage bits above the var width must be ignored
-                cand_rows.append([[a | (int(rng.integers(1, 2 ** 62)) << w if w < 256 else a, bb]])
+                hi = (int(rng.integers(1, 2 ** 62)) << w) if w < 256 else 0
+                cand_rows.append([[a | hi, bb]])
     nodes, noff, consts, coff = pack_states(states)
     words, po, status = _lower(nodes, noff, consts, coff)
     assert (status == 0).all()

@@ -1,0 +1,186 @@
+"""GPU-first solver front end, written like the reference's own tests.
+
+Mirrors tests/laser/keccak_tests.py:7-138 (same cases, same sat/unsat
+expectations) on top of mythril_amd.smt + mythril_amd.keccak: the GPU must
+prove every SAT case with a witness the oracle confirms, and must never claim
+SAT on an UNSAT case (those are left to the fallback solver: without z3 the
+answer is `unknown`, exactly what reaches z3 in the integrated path).
+"""
+import numpy as np
+import pytest
+
+from mythril_amd import dag as D
+from mythril_amd import solver as SV
+from mythril_amd.keccak import KeccakFunctionManager, keccak256_batch
+from mythril_amd.smt import And, symbol_factory
+from oracle import bvsem as S
+from oracle.keccak_ref import keccak256 as keccak_py
+
+pytestmark = pytest.mark.gpu
+
+BVV = symbol_factory.BitVecVal
+BVS = symbol_factory.BitVecSym
+
+
+class CountingBackend(SV.Backend):
+    name = "counting"
+
+    def __init__(self):
+        self.calls = 0
+
+    def check(self, terms, timeout_ms, minimize=(), maximize=()):
+        self.calls += 1
+        return SV.unknown, None
+
+
+@pytest.fixture()
+def backend(mgp_ctx):
+    b = CountingBackend()
+    old = SV.set_backend(b)
+    SV.SolverStatistics().reset()
+    SV.enable_gpu(True)
+    yield b
+    SV.set_backend(old)
+
+
+def _oracle_confirms(constraints, model):
+    st = D.build_state([c.raw for c in constraints])
+    xs = [model.get(name, 0) for (name, _) in st.vars]
+    return S.eval_root(st.nodes, st.consts, xs)
+
+
+KM = KeccakFunctionManager()  # module-level like the reference's singleton (state carries across cases)
+
+
+@pytest.mark.parametrize(
+    "input1, input2, expected",
+    [
+        (BVV(100, 8), BVV(101, 8), SV.unsat),
+        (BVV(100, 8), BVV(100, 16), SV.unsat),
+        (BVV(100, 8), BVV(100, 8), SV.sat),
+        (BVS("N1", 256), BVS("N2", 256), SV.sat),
+        (BVV(100, 256), BVS("N1", 256), SV.sat),
+        (BVV(100, 8), BVS("N1", 256), SV.unsat),
+    ],
+)
+def test_keccak_basic(backend, input1, input2, expected):
+    s = SV.Solver()
+    o1, c1 = KM.create_keccak(input1)
+    o2, c2 = KM.create_keccak(input2)
+    s.add(And(c1, c2))
+    s.add(o1 == o2)
+    r = s.check()
+    if expected == SV.sat:
+        assert r == SV.sat, "GPU must find a witness for a satisfiable keccak case"
+        assert backend.calls == 0
+        assert _oracle_confirms([And(c1, c2), o1 == o2], s.model().assignments[0])
+    else:
+        assert r != SV.sat
+        assert backend.calls == 1  # left to the fallback solver unchanged
+
+
+def test_keccak_symbol_and_val(backend):
+    s = SV.Solver()
+    hundred = BVV(100, 256)
+    n = BVS("n", 256)
+    o1, c1 = KM.create_keccak(hundred)
+    o2, c2 = KM.create_keccak(n)
+    s.add(And(c1, c2))
+    s.add(o1 == o2)
+    s.add(n == BVV(10, 256))
+    assert s.check() != SV.sat
+
+
+def test_keccak_complex_eq(backend):
+    s = SV.Solver()
+    a, b = BVS("a", 160), BVS("b", 160)
+    o1, c1 = KM.create_keccak(a)
+    o2, c2 = KM.create_keccak(b)
+    s.add(And(c1, c2))
+    two = BVV(2, 256)
+    o1, c1 = KM.create_keccak(two * o1)
+    o2, c2 = KM.create_keccak(two * o2)
+    s.add(And(c1, c2))
+    s.add(o1 == o2)
+    s.add(a != b)
+    assert s.check() != SV.sat
+
+
+def test_keccak_complex_eq2(backend):
+    s = SV.Solver()
+    a, b = BVS("a", 160), BVS("b", 160)
+    o1, c1 = KM.create_keccak(a)
+    o2, c2 = KM.create_keccak(b)
+    cs = [And(c1, c2)]
+    two = BVV(2, 256)
+    o1, c1 = KM.create_keccak(two * o1)
+    o2, c2 = KM.create_keccak(two * o2)
+    cs += [And(c1, c2), o1 == o2]
+    s.add(*cs)
+    assert s.check() == SV.sat
+    assert _oracle_confirms(cs, s.model().assignments[0])
+
+
+def test_keccak_simple_number(backend):
+    s = SV.Solver()
+    a = BVS("a", 160)
+    o, c = KM.create_keccak(a)
+    s.add(c)
+    s.add(BVV(10, 256) == o)
+    assert s.check() != SV.sat
+
+
+def test_keccak_other_num(backend):
+    s = SV.Solver()
+    a, b = BVS("a", 160), BVS("b", 256)
+    o, c = KM.create_keccak(a)
+    cs = [c]
+    o, c = KM.create_keccak(BVV(2, 256) * o)
+    cs += [c, b == o]
+    s.add(*cs)
+    assert s.check() == SV.sat
+    assert _oracle_confirms(cs, s.model().assignments[0])
+
+
+def test_get_model_contract(backend):
+    x = BVS("x", 256)
+    m = SV.get_model((x == BVV(5, 256),))
+    assert m[x] == 5
+    with pytest.raises(SV.UnsatError):
+        SV.get_model((False,))
+    with pytest.raises(SV.UnsatError):  # undecided -> fallback -> unknown -> UnsatError (solver.py:56-61)
+        SV.get_model((x == BVV(5, 256), x == BVV(6, 256)))
+    with pytest.raises(SV.UnsatError):  # minimize always goes to the fallback
+        SV.get_model((x == BVV(5, 256),), minimize=(x,))
+    assert backend.calls == 2
+
+
+def test_constraints_is_possible_batch(backend):
+    x, y = BVS("x", 256), BVS("y", 256)
+    items = [SV.Constraints([x == BVV(i, 256), SV.Not(y == x)]) for i in range(50)]
+    items.append(SV.Constraints([x == BVV(1, 256), x == BVV(2, 256)]))
+    res = SV.batch_is_possible(items)
+    assert res[:50] == [True] * 50
+    assert res[50] is True  # unknown counts as possible (constraints.py:50)
+    assert backend.calls == 1
+    st = SV.SolverStatistics()
+    assert st.gpu_queries == 51 and st.gpu_sat == 50 and st.query_count == 1
+    # children inherit the witness as their first candidate
+    child = items[0].copy()
+    child.append(UGE_(y, BVV(0, 256)))
+    assert child.witness is not None and child.is_possible
+
+
+def UGE_(a, b):
+    from mythril_amd.smt import UGE
+
+    return UGE(a, b)
+
+
+def test_concrete_keccak_batch_matches_reference_impl(mgp_ctx):
+    rng = np.random.default_rng(1)
+    pre = [bytes(rng.integers(0, 256, size=n, dtype=np.uint8)) for n in (0, 1, 32, 64, 64, 100, 136, 137, 300)]
+    assert keccak256_batch(pre) == [keccak_py(p) for p in pre]
+    km = KeccakFunctionManager()
+    assert km.find_concrete_keccak(BVV(0, 256)).value == int.from_bytes(keccak_py(b"\0" * 32), "big")
+    assert km.get_empty_keccak_hash().value == int.from_bytes(keccak_py(b""), "big")

@@ -1,0 +1,172 @@
+"""Host lowering (mgp_lower, C++) vs the DAG oracle — CPU only.
+
+The bytecode produced for the GPU is executed by oracle.bytecode_ref (an
+independent interpreter of the encoding in include/mgp_ir.h) and must agree
+with oracle.bvsem on the DAG for every candidate.
+"""
+import numpy as np
+import pytest
+
+from mythril_amd import _native as N
+from oracle import bvsem as S
+from oracle import bytecode_ref as BR
+
+from ._util import INTERESTING, load_golden, pack_states, state_slice
+
+
+def _check_states(states, cand_rows, max_slots=0):
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = N.lower(nodes, noff, consts, coff, max_slots=max_slots)
+    for s, (nl, cl) in enumerate(states):
+        for xs in cand_rows[s]:
+            want = S.eval_root(nl, cl, xs)
+            got = BR.run_program(words, int(po[s]), xs)
+            assert got == want, (s, xs)
+    return words, po, status
+
+
+def test_synthetic_lowering_matches_dag():
+    b = N.synth_generate(0x4D595448, 99, 150, 64, 16)
+    words, po, status = N.lower(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+    assert (status == 0).all()
+    rng = np.random.default_rng(1)
+    for s in range(150):
+        nodes, consts = state_slice(b, s)
+        rows = [[int(rng.integers(0, 2 ** 63)) << int(rng.integers(0, 190)) for _ in range(6)] for _ in range(6)]
+        rows.append([INTERESTING[int(rng.integers(0, len(INTERESTING)))] for _ in range(6)])
+        if b["planted"][s]:
+            rows.append([S.limbs_to_int(x) for x in b["plant_words"][s]])
+        for xs in rows:
+            assert BR.run_program(words, int(po[s]), xs) == S.eval_root(nodes, consts, xs), s
+
+
+def test_golden_arith_lowering():
+    cases = [t for t in load_golden("vm_arith.json") if t["reference_agrees"]][:80]
+    states = []
+    for t in cases:
+        consts = [int(c, 16) for c in t["consts"]]
+        node, exp = t["checks"][0]
+        nl = [list(n) for n in t["nodes"]]
+        cx = consts + [int(exp, 16)]
+        nl.append([S.CONST, 256, -1, -1, -1, len(cx) - 1, 0])
+        nl.append([S.EQ, 1, node, len(nl) - 1, -1, 0, 0])
+        states.append((nl, cx))
+    _check_states(states, [[[]]] * len(states))
+
+
+def test_narrow_widths_and_signed_ops():
+    rng = np.random.default_rng(2)
+    states, rows = [], []
+    for w in (1, 7, 8, 31, 32, 33, 64, 100, 160, 255):
+        for op in (S.ADD, S.SUB, S.MUL, S.UDIV, S.UREM, S.SDIV, S.SREM, S.SMOD, S.SHL, S.LSHR, S.ASHR):
+            for cmp in (S.SLT, S.ULE, S.SGE, S.EQ, S.UMUL_NOOVF, S.UADD_NOOVF):
+                nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0], [op, w, 0, 1, -1, 0, 0],
+                      [S.SEXT, 256, 2, -1, -1, 0, 0], [S.EXTRACT, w, 3, -1, -1, w - 1, 0],
+                      [cmp, 1, 4, 0, -1, 0, 0]]
+                states.append((nl, []))
+                rows.append([[int(rng.integers(0, 2 ** 62)) * (1 << int(rng.integers(0, 200))),
+                              int(rng.integers(0, 2 ** 62))] for _ in range(4)] + [[(1 << w) - 1, 0],
+                                                                                    [1 << (w - 1), (1 << w) - 1]])
+    _check_states(states, rows)
+
+
+def test_concat_extract_ite_bool_ops():
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0],
+          [S.EXTRACT, 8, 0, -1, -1, 15, 8], [S.EXTRACT, 160, 1, -1, -1, 159, 0],
+          [S.CONCAT, 168, 2, 3, -1, 0, 0], [S.ZEXT, 256, 4, -1, -1, 0, 0],
+          [S.ULT, 1, 5, 0, -1, 0, 0], [S.ITE, 256, 6, 0, 1, 0, 0],
+          [S.EQ, 1, 7, 1, -1, 0, 0], [S.BXOR, 1, 6, 8, -1, 0, 0], [S.BITE, 1, 9, 6, 8, 0, 0],
+          [S.TRUE, 1, -1, -1, -1, 0, 0], [S.BEQ, 1, 10, 11, -1, 0, 0], [S.EQ, 1, 12, 9, -1, 0, 0]]
+    rows = [[[a, b] for a in INTERESTING[:8] for b in INTERESTING[:8]]]
+    _check_states([(nl, [])], rows)
+
+
+def test_uf_chains():
+    # three apps of f, one inverse, consistency must hold in all orders
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.VAR, 256, -1, -1, -1, 2, 0],
+          [S.UFAPP, 256, 0, -1, -1, 0, 3], [S.UFAPP, 256, 1, -1, -1, 0, 4], [S.UFAPP, 256, 2, -1, -1, 0, 5],
+          [S.UFINV, 256, 4, -1, -1, 0, 6], [S.UFINV, 256, 5, -1, -1, 0, 7],
+          [S.EQ, 1, 6, 1, -1, 0, 0], [S.EQ, 1, 3, 5, -1, 0, 0], [S.BOR, 1, 8, 9, -1, 0, 0],
+          [S.EQ, 1, 7, 2, -1, 0, 0], [S.BAND, 1, 10, 11, -1, 0, 0]]
+    rows = []
+    for x0 in (1, 2):
+        for x1 in (1, 2, 3):
+            for x2 in (1, 3):
+                for h in ((10, 10, 10), (10, 11, 12), (10, 11, 10)):
+                    rows.append([x0, x1, x2, *h, 1, 2])
+    _check_states([(nl, [])], [rows])
+
+
+def test_many_live_values_rejected_cleanly():
+    # 40 simultaneously live 256-bit values with a 16-slot cap -> unsupported, not wrong
+    n = 40
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]
+    for i in range(n):
+        nl.append([S.ADD if i % 2 else S.MUL, 256, len(nl) - 1, i % 2, -1, 0, 0])
+    first = 2
+    acc = first
+    for i in range(1, n):
+        nl.append([S.XOR, 256, acc, first + i, -1, 0, 0])
+        acc = len(nl) - 1
+    nl.append([S.ULT, 1, acc, 0, -1, 0, 0])
+    nodes, noff, consts, coff = pack_states([(nl, [])])
+    _, _, status = N.lower(nodes, noff, consts, coff, max_slots=4)
+    assert status[0] == N.ST_UNSUPPORTED
+    words, po, status = N.lower(nodes, noff, consts, coff, max_slots=64)
+    assert status[0] == N.ST_OK
+    for xs in ([3, 5], [INTERESTING[3], INTERESTING[4]]):
+        assert BR.run_program(words, int(po[0]), xs) == S.eval_root(nl, [], xs)
+
+
+@pytest.mark.parametrize("bad", ["wide", "forward_ref", "bool_as_bv", "width_mismatch", "root_bv", "unknown_op"])
+def test_malformed_dags_are_unsupported(bad):
+    v0 = [S.VAR, 256, -1, -1, -1, 0, 0]
+    v1 = [S.VAR, 256, -1, -1, -1, 1, 0]
+    nl = {
+        "wide": [v0, v1, [S.CONCAT, 512, 0, 1, -1, 0, 0], [S.EQ, 1, 2, 2, -1, 0, 0]],
+        "forward_ref": [v0, [S.ULT, 1, 0, 2, -1, 0, 0], v1],
+        "bool_as_bv": [v0, [S.ULT, 1, 0, 0, -1, 0, 0], [S.ADD, 256, 0, 1, -1, 0, 0], [S.EQ, 1, 2, 0, -1, 0, 0]],
+        "width_mismatch": [v0, [S.VAR, 8, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 1, -1, 0, 0]],
+        "root_bv": [v0, v1, [S.ADD, 256, 0, 1, -1, 0, 0]],
+        "unknown_op": [v0, [99, 1, 0, 0, -1, 0, 0]],
+    }[bad]
+    nodes, noff, consts, coff = pack_states([(nl, []), ([v0, v1, [S.ULT, 1, 0, 1, -1, 0, 0]], [])])
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert status[0] == N.ST_UNSUPPORTED and status[1] == N.ST_OK
+    assert BR.run_program(words, int(po[0]), [1, 2]) is None
+    assert BR.run_program(words, int(po[1]), [1, 2]) is True
+
+
+def test_empty_batch_and_constant_roots():
+    nodes, noff, consts, coff = pack_states([([[S.TRUE, 1, -1, -1, -1, 0, 0]], []),
+                                             ([[S.FALSE, 1, -1, -1, -1, 0, 0]], [])])
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert BR.run_program(words, int(po[0]), []) is True
+    assert BR.run_program(words, int(po[1]), []) is False
+    w0, po0, st0 = N.lower(np.zeros(0, dtype=N.NODE_DTYPE), np.zeros(1, np.uint64), np.zeros((0, 8), np.uint32),
+                           np.zeros(1, np.uint64))
+    assert len(po0) == 1 and w0.size == 0
+
+
+def test_program_layout_invariants():
+    b = N.synth_generate(0x4D595448, 5, 500, 64, 256)
+    words, po, status = N.lower(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+    hdr = N.program_headers(words, po)
+    assert (po % 4 == 0).all(), "programs must be 16-byte aligned for s_load_dwordx4"
+    sizes = 4 + 4 * hdr[:, 0].astype(np.int64) + 8 * hdr[:, 1].astype(np.int64)
+    assert (sizes <= (po[1:] - po[:-1]).astype(np.int64)).all()
+    assert hdr[:, 2].max() <= 32 and (hdr[:, 3] >> 8 <= b["n_vars"]).all()
+    # deterministic
+    w2, po2, _ = N.lower(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+    assert np.array_equal(words, w2) and np.array_equal(po, po2)
+
+
+def test_synthetic_generator_is_deterministic_and_sliceable():
+    a = N.synth_generate(0x4D595448, 0, 64, 64, 256)
+    b = N.synth_generate(0x4D595448, 32, 32, 64, 256)
+    off = int(a["node_offsets"][32])
+    assert np.array_equal(a["nodes"][off:], b["nodes"])
+    assert np.array_equal(a["planted"][32:], b["planted"])
+    assert np.array_equal(a["plant_words"][32:], b["plant_words"])
+    ops = N.nominal_ops(a["nodes"], a["node_offsets"])
+    assert 1000 < ops.mean() < 6000

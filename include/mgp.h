@@ -153,6 +153,12 @@ int mgp_synth_generate(uint64_t seed, uint64_t state_base, uint32_t n_states,
 int mgp_nominal_ops(const mgp_node *nodes, const uint64_t *node_offsets,
                     uint32_t n_states, uint64_t *out_ops);
 
+/* INT32 VALU issue-rate probe: blocks x 256 threads x iters x 512 v_add_u32
+ * (the count is written to *ops_out); time it on `stream` to obtain the
+ * measured peak the roofline fractions are priced against. */
+int mgp_probe_valu_dev(uint32_t iters, uint32_t blocks, uint32_t *d_sink,
+                       uint64_t *ops_out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,7 @@ def _bind(lib):
         "mgp_fill_mapping_preimages_dev": (ctypes.c_int, [_P, _U64, _U64, _U64, _P]),
         "mgp_synth_generate": (ctypes.c_int, [_U64, _U64, _U32, _U32, _U32, _P, _P, _P, _P, _P, _P, _P]),
         "mgp_nominal_ops": (ctypes.c_int, [_P, _P, _U32, _P]),
+        "mgp_probe_valu_dev": (ctypes.c_int, [_U32, _U32, _P, _P, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -124,6 +125,7 @@ EXPORTED_SYMBOLS = (
     "mgp_fill_mapping_preimages_dev",
     "mgp_synth_generate",
     "mgp_nominal_ops",
+    "mgp_probe_valu_dev",
 )
 
 
@@ -308,3 +310,9 @@ def keccak256_dev(d_in, n, length, stride, d_out, stream) -> None:
 
 def fill_mapping_preimages_dev(d_out, first, n, seed, stream) -> None:
     _check(lib().mgp_fill_mapping_preimages_dev(d_out, first, n, seed, stream))
+
+
+def probe_valu_dev(iters, blocks, d_sink, stream) -> int:
+    ops = ctypes.c_uint64(0)
+    _check(lib().mgp_probe_valu_dev(iters, blocks, d_sink, ctypes.byref(ops), stream))
+    return int(ops.value)

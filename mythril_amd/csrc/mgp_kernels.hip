@@ -496,6 +496,30 @@ __global__ void mgp_preimage_kernel(uint8_t *__restrict__ out, uint64_t first, u
   }
 }
 
+
+// ------------------------------------------------------ VALU peak probe
+// 8 independent v_add_u32 chains, 64 adds per chain per iteration, written as
+// inline asm so nothing is folded: measures the INT32 VALU issue rate the
+// roofline fraction is priced against ("confirm with a
+// v_add_u32 microbenchmark").
+__global__ __launch_bounds__(256) void mgp_valu_probe_kernel(uint32_t iters, uint32_t *__restrict__ sink) {
+  uint32_t a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+           a7 = a0 + 7;
+  const uint32_t b = blockIdx.x | 1u;
+  for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      asm volatile(
+          "v_add_u32 %0, %0, %8\n\tv_add_u32 %1, %1, %8\n\tv_add_u32 %2, %2, %8\n\tv_add_u32 %3, %3, %8\n\t"
+          "v_add_u32 %4, %4, %8\n\tv_add_u32 %5, %5, %8\n\tv_add_u32 %6, %6, %8\n\tv_add_u32 %7, %7, %8"
+          : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
+          : "v"(b));
+    }
+  }
+  const uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+  if (r == 0xFFFFFFFFu) sink[blockIdx.x] = r;  // keep the chains live
+}
+
 // ------------------------------------------------------------ launchers
 extern "C" {
 
@@ -571,6 +595,11 @@ hipError_t mgp_launch_preimages(uint8_t *out, uint64_t first, uint64_t n, uint64
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(mgp_preimage_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, out, first, n,
                      seed);
+  return hipGetLastError();
+}
+
+hipError_t mgp_launch_valu_probe(uint32_t iters, uint32_t blocks, uint32_t *sink, hipStream_t st) {
+  hipLaunchKernelGGL(mgp_valu_probe_kernel, dim3(blocks), dim3(256), 0, st, iters, sink);
   return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@ hipError_t mgp_launch_transpose(const uint32_t *aos, uint32_t *soa, uint32_t n_s
 hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32_t stride, uint8_t *out,
                              hipStream_t st);
 hipError_t mgp_launch_preimages(uint8_t *out, uint64_t first, uint64_t n, uint64_t seed, hipStream_t st);
+hipError_t mgp_launch_valu_probe(uint32_t iters, uint32_t blocks, uint32_t *sink, hipStream_t st);
 }
 
 namespace {
@@ -297,6 +298,13 @@ int mgp_fill_mapping_preimages_dev(uint8_t *d_out64, uint64_t first, uint64_t n,
   if (n && !d_out64) return fail(nullptr, MGP_E_ARG, "NULL device pointer");
   hipError_t e = mgp_launch_preimages(d_out64, first, n, seed, (hipStream_t)stream);
   return e == hipSuccess ? MGP_OK : hip_fail(nullptr, e, "mgp_fill_mapping_preimages_dev");
+}
+
+int mgp_probe_valu_dev(uint32_t iters, uint32_t blocks, uint32_t *d_sink, uint64_t *ops_out, void *stream) {
+  if (!d_sink || blocks == 0) return fail(nullptr, MGP_E_ARG, "bad probe arguments");
+  if (ops_out) *ops_out = (uint64_t)blocks * 256u * iters * 64u * 8u;
+  hipError_t e = mgp_launch_valu_probe(iters, blocks, d_sink, (hipStream_t)stream);
+  return e == hipSuccess ? MGP_OK : hip_fail(nullptr, e, "mgp_probe_valu_dev");
 }
 
 }  // extern "C"

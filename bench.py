@@ -103,6 +103,10 @@ def main():
     d_pwords = torch.from_numpy(np.ascontiguousarray(b["plant_words"][pl]).view(np.int32)).to(dev)
     N.plant_candidates_dev(vp(d_cands), n_states, n_cand, n_vars, vp(d_pstate), vp(d_pidx), vp(d_pwords),
                            len(pl), sh)
+    order, bounds, bslots = N.plan_buckets(words, po)
+    d_order = torch.from_numpy(order.view(np.int32)).to(dev)
+    log(f"rank {rank}: {len(bslots)} slot buckets: " +
+        ", ".join(f"{int(sl)}:{int(bounds[i + 1] - bounds[i])}" for i, sl in enumerate(bslots)))
     n_chunks = (n_cand + 63) // 64
     d_first = torch.empty(n_states, dtype=torch.int32, device=dev)
     d_wit = torch.empty(n_states * n_vars * 8, dtype=torch.int32, device=dev)
@@ -114,7 +118,7 @@ def main():
         if ev is not None:
             ev[0].record(stream)
         N.eval_batch_dev(vp(d_words), vp(d_po), n_states, vp(d_cands), n_cand, n_vars, n_slots, vp(d_first),
-                         vp(d_wit), vp(d_scratch), sh)
+                         vp(d_wit), vp(d_scratch), sh, vp(d_order), bounds, bslots)
         if ev is not None:
             ev[1].record(stream)
         if world > 1:

@@ -90,15 +90,30 @@ int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words,
                    uint32_t *out_witness);
 
 /* Device-resident variant.  d_cands uses the DEVICE layout
- * [state][var][half][cand] of 16-byte groups (see mgp_cand_index); n_slots is
- * the max header slot count over the batch (mgp_lower reports it per state). */
+ * [state][var][half][cand] of 16-byte groups.  With n_buckets == 0 one launch
+ * covers all states with n_slots BV slots of LDS each (the max header slot
+ * count).  Otherwise d_order (device) lists the states bucket by bucket:
+ * bucket b = d_order[bucket_bounds[b] .. bucket_bounds[b+1]) runs with
+ * bucket_slots[b] slots (bounds/slots are HOST arrays, see mgp_plan_buckets),
+ * so each bucket gets the occupancy its LDS footprint allows. */
 int mgp_eval_batch_dev(const uint32_t *d_prog_words,
                        const uint64_t *d_prog_offsets, uint32_t n_states,
                        const uint32_t *d_cands, uint32_t n_cand,
                        uint32_t n_vars, uint32_t n_slots,
                        int32_t *d_first_sat, uint32_t *d_witness,
                        int32_t *d_scratch /* n_states*ceil(n_cand/64) */,
+                       const uint32_t *d_order,
+                       const uint32_t *bucket_bounds,
+                       const uint32_t *bucket_slots, uint32_t n_buckets,
                        void *stream);
+
+/* Host-side launch plan: states grouped by the BV-slot count in their program
+ * header.  Writes order_out[n_states], bounds_out[nb+1], slots_out[nb];
+ * returns nb (<= max_buckets) or a negative error. */
+int mgp_plan_buckets(const uint32_t *prog_words, const uint64_t *prog_offsets,
+                     uint32_t n_states, uint32_t *order_out,
+                     uint32_t *bounds_out, uint32_t *slots_out,
+                     uint32_t max_buckets);
 
 /* Fill device candidates with the benchmark mixture (Philox4x32-10 keyed by
  * (seed, state_base+s, cand, var)): 25 % interesting values (0, 1, 2^256-1,

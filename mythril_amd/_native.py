@@ -73,7 +73,8 @@ def _bind(lib):
         "mgp_version": (ctypes.c_char_p, []),
         "mgp_lower": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P, _U64, _P, _P, _P]),
         "mgp_eval_batch": (ctypes.c_int, [_P, _P, _P, _U32, _P, _U32, _U32, _P, _P]),
-        "mgp_eval_batch_dev": (ctypes.c_int, [_P, _P, _U32, _P, _U32, _U32, _U32, _P, _P, _P, _P]),
+        "mgp_eval_batch_dev": (ctypes.c_int, [_P, _P, _U32, _P, _U32, _U32, _U32, _P, _P, _P, _P, _P, _P, _U32, _P]),
+        "mgp_plan_buckets": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32]),
         "mgp_fill_candidates_dev": (ctypes.c_int, [_P, _P, _U32, _U64, _U64, _P, _U32, _U32, _P]),
         "mgp_plant_candidates_dev": (ctypes.c_int, [_P, _U32, _U32, _U32, _P, _P, _P, _U32, _P]),
         "mgp_keccak256_batch": (ctypes.c_int, [_P, _P, _U64, _U32, _U32, _P]),
@@ -118,6 +119,7 @@ EXPORTED_SYMBOLS = (
     "mgp_lower",
     "mgp_eval_batch",
     "mgp_eval_batch_dev",
+    "mgp_plan_buckets",
     "mgp_fill_candidates_dev",
     "mgp_plant_candidates_dev",
     "mgp_keccak256_batch",
@@ -285,11 +287,28 @@ def nominal_ops(nodes: np.ndarray, node_offsets: np.ndarray) -> np.ndarray:
 
 
 # ---------------------------------------------------- device-pointer API
+def plan_buckets(words: np.ndarray, prog_offsets: np.ndarray, max_buckets: int = 256):
+    """-> (order u32[n], bounds u32[nb+1], slots u32[nb]) grouping states by LDS slot count."""
+    words = np.ascontiguousarray(words, dtype=np.uint32)
+    prog_offsets = np.ascontiguousarray(prog_offsets, dtype=np.uint64)
+    n = len(prog_offsets) - 1
+    order = np.zeros(max(n, 1), dtype=np.uint32)
+    bounds = np.zeros(max_buckets + 1, dtype=np.uint32)
+    slots = np.zeros(max_buckets, dtype=np.uint32)
+    nb = lib().mgp_plan_buckets(_ptr(words), _ptr(prog_offsets), n, _ptr(order), _ptr(bounds), _ptr(slots),
+                                max_buckets)
+    if nb < 0:
+        _check(nb)
+    return order[:n], bounds[: nb + 1].copy(), slots[:nb].copy()
+
+
 def eval_batch_dev(d_words, d_offs, n_states, d_cands, n_cand, n_vars, n_slots, d_first, d_wit, d_scratch,
-                   stream) -> None:
+                   stream, d_order=None, bounds: Optional[np.ndarray] = None, slots: Optional[np.ndarray] = None) -> None:
+    nb = 0 if bounds is None else len(slots)
     _check(
         lib().mgp_eval_batch_dev(
-            d_words, d_offs, n_states, d_cands, n_cand, n_vars, n_slots, d_first, d_wit, d_scratch, stream
+            d_words, d_offs, n_states, d_cands, n_cand, n_vars, n_slots, d_first, d_wit, d_scratch, d_order,
+            _ptr(bounds) if nb else None, _ptr(slots) if nb else None, nb, stream
         )
     )
 

@@ -284,23 +284,101 @@ MGP_HD U256 bv_mul_full(const U256 &a, const U256 &b, U256 *lo) {
   return hi;
 }
 
-// unsigned division with remainder; b == 0 -> q = 2^256-1, r = a (z3 bvudiv/bvurem)
-MGP_HD void bv_udivrem(const U256 &a, const U256 &b, U256 *q_out, U256 *r_out) {
-  U256 q = bv_zero(), r = a;
-  uint32_t na = bv_bitlen(a), nb = bv_bitlen(b);
-  if (nb != 0u && na >= nb) {
-    uint32_t n = na - nb;
-    U256 d = bv_shl(b, n);
-    for (uint32_t i = 0; i <= n; ++i) {
-      uint32_t borrow;
-      U256 t = bv_sub(r, d, &borrow);
-      uint32_t bit = borrow ^ 1u;
-      r = bv_sel(bit != 0u, t, r);
-      q = bv_shl1(q, bit);
-      d = bv_shr1(d);
+#if defined(__HIP_DEVICE_COMPILE__)
+MGP_HD bool mgp_wave_any(bool p) { return __ballot(p) != 0ull; }
+#else
+MGP_HD bool mgp_wave_any(bool p) { return p; }
+#endif
+
+// One quotient digit of Knuth's algorithm D (TAOCP 4.3.1) at a compile-time
+// digit position J over the normalised 16-limb dividend u and 8-limb divisor v
+// (v.w[7] has its top bit set).  qhat comes from a double-precision estimate
+// of (u[J+8]:u[J+7]) / v7 (exact to +-1, fixed with one integer correction
+// each way), refined with v6, then multiply-subtract with a rare add-back.
+template <int J>
+MGP_HD uint32_t bv_knuth_digit(uint32_t (&u)[16], const U256 &v, double inv_v7) {
+  const uint32_t v7 = v.w[7], v6 = v.w[6];
+  const uint64_t num = ((uint64_t)u[J + 8] << 32) | u[J + 7];
+  uint64_t qhat;
+  if (u[J + 8] >= v7) {
+    qhat = 0xFFFFFFFFull;
+  } else {
+    const double dn = (double)u[J + 8] * 4294967296.0 + (double)u[J + 7];
+    qhat = (uint64_t)(dn * inv_v7);
+    if (qhat > 0xFFFFFFFFull) qhat = 0xFFFFFFFFull;
+    int64_t r = (int64_t)(num - qhat * v7);
+    if (r < 0) { --qhat; r += v7; }
+    if (r >= (int64_t)v7) { ++qhat; }
+  }
+  uint64_t rhat = num - qhat * v7;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (rhat < 0x100000000ull && qhat * v6 > ((rhat << 32) | u[J + 6])) {
+      --qhat;
+      rhat += v7;
     }
   }
-  if (nb == 0u) q = bv_ones();
+  // u[J .. J+8] -= qhat * v
+  uint32_t borrow = 0, hi = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t p = qhat * v.w[i] + hi;
+    hi = (uint32_t)(p >> 32);
+    u[J + i] = mgp_subc(u[J + i], (uint32_t)p, borrow, &borrow);
+  }
+  u[J + 8] = mgp_subc(u[J + 8], hi, borrow, &borrow);
+  if (borrow) {  // qhat was one too large (probability ~2^-31): add v back
+    --qhat;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u[J + i] = mgp_addc(u[J + i], v.w[i], c, &c);
+    u[J + 8] += c;
+  }
+  return (uint32_t)qhat;
+}
+
+template <int J>
+MGP_HD void bv_knuth_step(uint32_t (&u)[16], const U256 &v, double inv_v7, uint32_t ndig, U256 &q) {
+  // digit J of every lane is zero unless 32*J <= bitlen(a) - bitlen(b); skip it
+  // when that holds for no lane of the wave (uniform branch)
+  if (mgp_wave_any((uint32_t)J < ndig)) q.w[J] = bv_knuth_digit<J>(u, v, inv_v7);
+}
+
+// unsigned division with remainder; b == 0 -> q = 2^256-1, r = a (z3 bvudiv/bvurem)
+// Knuth D with 32-bit digits over the fixed 512/256-bit shapes: every limb
+// index is a compile-time constant, so all of u, v and q stay in VGPRs.
+MGP_HD void bv_udivrem(const U256 &a, const U256 &b, U256 *q_out, U256 *r_out) {
+  const uint32_t la = bv_bitlen(a), lb = bv_bitlen(b);
+  U256 q = bv_zero(), r = a;
+  const bool divides = lb != 0u && la >= lb;
+  if (mgp_wave_any(divides)) {
+    const uint32_t s = divides ? 256u - lb : 0u;  // normalisation shift
+    const U256 v = bv_shl(divides ? b : bv_ones(), s);
+    const U256 ulo = bv_shl(a, s);
+    const U256 uhi = s ? bv_lshr(a, 256u - s) : bv_zero();
+    uint32_t u[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      u[i] = ulo.w[i];
+      u[i + 8] = uhi.w[i];
+    }
+    const double inv_v7 = 1.0 / (double)v.w[7];
+    const uint32_t ndig = divides ? ((la - lb) >> 5) + 1u : 0u;
+    bv_knuth_step<7>(u, v, inv_v7, ndig, q);
+    bv_knuth_step<6>(u, v, inv_v7, ndig, q);
+    bv_knuth_step<5>(u, v, inv_v7, ndig, q);
+    bv_knuth_step<4>(u, v, inv_v7, ndig, q);
+    bv_knuth_step<3>(u, v, inv_v7, ndig, q);
+    bv_knuth_step<2>(u, v, inv_v7, ndig, q);
+    bv_knuth_step<1>(u, v, inv_v7, ndig, q);
+    bv_knuth_step<0>(u, v, inv_v7, ndig, q);
+    U256 rn;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rn.w[i] = u[i];
+    if (divides) r = bv_lshr(rn, s);
+    if (!divides) q = bv_zero();
+  }
+  if (lb == 0u) q = bv_ones();
   *q_out = q;
   *r_out = r;
 }

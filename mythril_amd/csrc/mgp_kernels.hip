@@ -94,10 +94,12 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
     const uint32_t *__restrict__ words, const uint64_t *__restrict__ offs,
     uint32_t n_states, const uint4 *__restrict__ cands, uint32_t n_cand,
     uint32_t n_vars, uint32_t n_chunks, uint32_t n_slots,
-    int32_t *__restrict__ partial) {
+    int32_t *__restrict__ partial, const uint32_t *__restrict__ order, uint32_t order_base) {
   extern __shared__ uint4 mgp_lds[];
   const uint32_t lid = xcd_remap(blockIdx.x, gridDim.x);
-  const uint32_t state = lid / n_chunks, chunk = lid - state * n_chunks;
+  const uint32_t k = lid / n_chunks, chunk = lid - k * n_chunks;
+  // a launch covers states order[order_base + k] (one slot-count bucket) or order_base + k
+  const uint32_t state = order ? order[order_base + k] : order_base + k;
   if (state >= n_states) return;
   const uint32_t lane = threadIdx.x;
   const uint32_t cand = chunk * MGP_WAVE + lane;
@@ -124,10 +126,15 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
   uint64_t bools = 1ull << MGP_BOOL_TRUE;
   bool root = false;
 
+  // software-pipelined instruction fetch: the scalar loads of instruction
+  // pc+1 are in flight while instruction pc executes (mgp_lower pads every
+  // program with one zero instruction after RET)
+  uint32_t n0 = uni(ins[0]), n1 = uni(ins[1]), n2 = uni(ins[2]);
   for (uint32_t pc = 0; pc < n_ins; ++pc) {
-    const uint32_t w0 = uni(ins[pc * 4u + 0u]);
-    const uint32_t w1 = uni(ins[pc * 4u + 1u]);
-    const uint32_t w2 = uni(ins[pc * 4u + 2u]);
+    const uint32_t w0 = n0, w1 = n1, w2 = n2;
+    n0 = uni(ins[pc * 4u + 4u]);
+    n1 = uni(ins[pc * 4u + 5u]);
+    n2 = uni(ins[pc * 4u + 6u]);
     const uint32_t op = w0 & 0xFFu;
     const uint32_t width = ((w0 >> 8) & 0xFFu) + 1u;
     const uint32_t dst = (w0 >> 16) & 0xFFu;
@@ -213,15 +220,24 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
         a = bv_sext(a, width);
         if (op != MGP_OP_ASHR) b = bv_sext(b, width);
       }
-      switch (op) {
+      if (op >= MGP_OP_UDIV && op <= MGP_OP_SMOD) {
+        // one division site for the five div/rem ops (SMT-LIB msb case split on |a|, |b|)
+        const bool sg = op >= MGP_OP_SDIV;
+        const bool sa = sg && bv_sign(a), sb = sg && bv_sign(b);
+        U256 q, m;
+        bv_udivrem(sa ? bv_neg(a) : a, sb ? bv_neg(b) : b, &q, &m);
+        if (op == MGP_OP_UDIV) r = q;
+        else if (op == MGP_OP_UREM) r = m;
+        else if (op == MGP_OP_SDIV) r = (sa != sb) ? bv_neg(q) : q;
+        else if (op == MGP_OP_SREM) r = sa ? bv_neg(m) : m;
+        else if (bv_is_zero(m) || (!sa && !sb)) r = m;  // SMOD: sign follows the divisor
+        else if (sa && !sb) r = bv_add(bv_neg(m), b, nullptr);
+        else if (!sa && sb) r = bv_add(m, b, nullptr);
+        else r = bv_neg(m);
+      } else switch (op) {
         case MGP_OP_ADD: r = bv_add(a, b, nullptr); break;
         case MGP_OP_SUB: r = bv_sub(a, b, nullptr); break;
         case MGP_OP_MUL: r = bv_mul(a, b); break;
-        case MGP_OP_UDIV: { U256 q, m; bv_udivrem(a, b, &q, &m); r = q; break; }
-        case MGP_OP_UREM: { U256 q, m; bv_udivrem(a, b, &q, &m); r = m; break; }
-        case MGP_OP_SDIV: r = bv_sdiv(a, b); break;
-        case MGP_OP_SREM: r = bv_srem(a, b); break;
-        case MGP_OP_SMOD: r = bv_smod(a, b); break;
         case MGP_OP_AND: r = bv_and(a, b); break;
         case MGP_OP_OR: r = bv_or(a, b); break;
         case MGP_OP_XOR: r = bv_xor(a, b); break;
@@ -525,16 +541,28 @@ extern "C" {
 
 hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
                            const uint32_t *cands, uint32_t n_cand, uint32_t n_vars, uint32_t n_slots,
-                           int32_t *first_sat, uint32_t *witness, int32_t *partial, hipStream_t st) {
+                           int32_t *first_sat, uint32_t *witness, int32_t *partial, const uint32_t *order,
+                           const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
+                           hipStream_t st) {
   if (n_states == 0) return hipSuccess;
   const uint32_t n_chunks = (n_cand + MGP_WAVE - 1) / MGP_WAVE;
-  const uint64_t nblk = (uint64_t)n_states * n_chunks;
-  const size_t lds = (size_t)(n_slots ? n_slots : 1u) * 2u * MGP_WAVE * sizeof(uint4);
-  hipLaunchKernelGGL(mgp_eval_kernel, dim3((uint32_t)nblk), dim3(MGP_WAVE), lds, st, words, offs,
-                     n_states, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars, n_chunks,
-                     n_slots, partial);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
+  // One launch per slot-count bucket: the dynamic LDS (slots x 2 KiB per
+  // 64-lane wave) is sized per bucket, so states with few live values run at
+  // the occupancy their LDS footprint allows instead of the batch maximum.
+  const uint32_t nb = (n_buckets && order && bucket_bounds && bucket_slots) ? n_buckets : 1u;
+  for (uint32_t bkt = 0; bkt < nb; ++bkt) {
+    const uint32_t lo = (nb > 1 || n_buckets) ? bucket_bounds[bkt] : 0u;
+    const uint32_t hi = (nb > 1 || n_buckets) ? bucket_bounds[bkt + 1] : n_states;
+    const uint32_t sl = (nb > 1 || n_buckets) ? bucket_slots[bkt] : n_slots;
+    if (hi <= lo) continue;
+    const uint64_t nblk = (uint64_t)(hi - lo) * n_chunks;
+    const size_t lds = (size_t)(sl ? sl : 1u) * 2u * MGP_WAVE * sizeof(uint4);
+    hipLaunchKernelGGL(mgp_eval_kernel, dim3((uint32_t)nblk), dim3(MGP_WAVE), lds, st, words, offs, n_states,
+                       reinterpret_cast<const uint4 *>(cands), n_cand, n_vars, n_chunks, sl, partial,
+                       (nb > 1 || n_buckets) ? order : nullptr, lo);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
   hipLaunchKernelGGL(mgp_finalize_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, partial,
                      n_states, n_chunks, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars,
                      first_sat, reinterpret_cast<uint4 *>(witness));

@@ -109,7 +109,7 @@ struct UFApp {
 Lowered unsupported() {
   Lowered L;
   L.status = MGP_ST_UNSUPPORTED;
-  L.words = {0u, 0u, 0u, (uint32_t)MGP_ST_UNSUPPORTED};
+  L.words = {0u, 0u, 0u, (uint32_t)MGP_ST_UNSUPPORTED, 0u, 0u, 0u, 0u};
   return L;
 }
 
@@ -427,6 +427,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   for (const ConstKey &k : S.pool)
     for (int l = 0; l < 8; ++l) out.push_back(k.w[l]);
   while (out.size() % 4) out.push_back(0u);
+  for (int k = 0; k < 4; ++k) out.push_back(0u);  // the kernel prefetches one instruction past RET
   Lowered L;
   L.words.swap(out);
   return L;
@@ -467,4 +468,38 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
     if (out_status) out_status[s] = res[s].status;
   }
   return MGP_OK;
+}
+
+extern "C" int mgp_plan_buckets(const uint32_t *prog_words, const uint64_t *prog_offsets, uint32_t n_states,
+                                uint32_t *order_out, uint32_t *bounds_out, uint32_t *slots_out,
+                                uint32_t max_buckets) {
+  // counting sort of the states by BV-slot count (header word 2); one bucket
+  // per distinct count, merged upward when there are more than max_buckets
+  if (!prog_words || !prog_offsets || !order_out || !bounds_out || !slots_out || max_buckets == 0) return MGP_E_ARG;
+  std::vector<uint32_t> cnt(257, 0);
+  std::vector<uint16_t> sl(n_states);
+  for (uint32_t s = 0; s < n_states; ++s) {
+    const uint32_t v = std::min<uint32_t>(prog_words[prog_offsets[s] + 2], 256u);
+    sl[s] = (uint16_t)v;
+    cnt[v]++;
+  }
+  std::vector<uint32_t> distinct;
+  for (uint32_t v = 0; v <= 256; ++v)
+    if (cnt[v]) distinct.push_back(v);
+  // merge the smallest classes into their upper neighbour until the plan fits
+  while (distinct.size() > max_buckets) distinct.erase(distinct.begin());
+  std::vector<uint32_t> bucket_of(257, 0);
+  uint32_t b = 0;
+  for (uint32_t v = 0; v <= 256; ++v) {
+    while (b < distinct.size() && distinct[b] < v) ++b;
+    bucket_of[v] = std::min<uint32_t>(b, (uint32_t)distinct.size() - 1);
+  }
+  const uint32_t nb = (uint32_t)distinct.size();
+  std::vector<uint32_t> fill(nb + 1, 0);
+  for (uint32_t s = 0; s < n_states; ++s) fill[bucket_of[sl[s]] + 1]++;
+  for (uint32_t k = 0; k < nb; ++k) fill[k + 1] += fill[k];
+  for (uint32_t k = 0; k <= nb; ++k) bounds_out[k] = fill[k];
+  for (uint32_t k = 0; k < nb; ++k) slots_out[k] = distinct[k];
+  for (uint32_t s = 0; s < n_states; ++s) order_out[fill[bucket_of[sl[s]]]++] = s;
+  return (int)nb;
 }

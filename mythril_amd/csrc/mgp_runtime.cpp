@@ -14,7 +14,9 @@
 extern "C" {
 hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t n_states, const uint32_t *cands,
                            uint32_t n_cand, uint32_t n_vars, uint32_t n_slots, int32_t *first_sat,
-                           uint32_t *witness, int32_t *partial, hipStream_t st);
+                           uint32_t *witness, int32_t *partial, const uint32_t *order,
+                           const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
+                           hipStream_t st);
 hipError_t mgp_launch_fill(const uint32_t *words, const uint64_t *offs, uint32_t n_states, uint64_t state_base,
                            uint64_t seed, uint32_t *cands, uint32_t n_cand, uint32_t n_vars, hipStream_t st);
 hipError_t mgp_launch_plant(uint32_t *cands, uint32_t n_cand, uint32_t n_vars, const uint32_t *pstate,
@@ -60,7 +62,7 @@ struct mgp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  DevBuf words, offs, cand_aos, cand_soa, first, wit, partial, kin, kout;
+  DevBuf words, offs, cand_aos, cand_soa, first, wit, partial, kin, kout, order;
 };
 
 namespace {
@@ -96,6 +98,7 @@ int64_t validate_programs(const uint32_t *w, const uint64_t *offs, uint32_t n_st
     const uint32_t n_ins = w[o], n_c = w[o + 1], n_sl = w[o + 2], st = w[o + 3];
     if ((st & 0xFFu) != MGP_ST_OK) continue;  // reported as undecided by the kernel
     if (n_sl > kMaxSlotsHard || (st >> 8) > n_vars ||
+        o + MGP_HDR_WORDS + (uint64_t)(n_ins + 1) * MGP_INS_WORDS > e ||
         o + MGP_HDR_WORDS + (uint64_t)n_ins * MGP_INS_WORDS + (uint64_t)n_c * 8u > e) {
       *why = "bad program header at state " + std::to_string(s);
       return -1;
@@ -178,7 +181,7 @@ void mgp_destroy(mgp_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (DevBuf *b : {&ctx->words, &ctx->offs, &ctx->cand_aos, &ctx->cand_soa, &ctx->first, &ctx->wit,
-                    &ctx->partial, &ctx->kin, &ctx->kout})
+                    &ctx->partial, &ctx->kin, &ctx->kout, &ctx->order})
     b->release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -213,9 +216,16 @@ int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words, const uint64_t *pro
   MGP_HIP(ctx, hipMemcpyAsync(ctx->cand_aos.p, cand_words, cand_bytes, hipMemcpyHostToDevice, st));
   MGP_HIP(ctx, mgp_launch_transpose((const uint32_t *)ctx->cand_aos.p, (uint32_t *)ctx->cand_soa.p, n_states,
                                     n_cand, n_vars, st));
+  std::vector<uint32_t> order(n_states), bounds(kMaxSlotsHard + 2), bslots(kMaxSlotsHard + 1);
+  const int nb = mgp_plan_buckets(prog_words, prog_offsets, n_states, order.data(), bounds.data(), bslots.data(),
+                                  kMaxSlotsHard + 1);
+  if (nb < 0) return fail(ctx, MGP_E_ARG, "bucket planning failed");
+  MGP_HIP(ctx, ctx->order.ensure((size_t)n_states * 4u));
+  MGP_HIP(ctx, hipMemcpyAsync(ctx->order.p, order.data(), (size_t)n_states * 4u, hipMemcpyHostToDevice, st));
   MGP_HIP(ctx, mgp_launch_eval((const uint32_t *)ctx->words.p, (const uint64_t *)ctx->offs.p, n_states,
                                (const uint32_t *)ctx->cand_soa.p, n_cand, n_vars, (uint32_t)slots,
-                               (int32_t *)ctx->first.p, (uint32_t *)ctx->wit.p, (int32_t *)ctx->partial.p, st));
+                               (int32_t *)ctx->first.p, (uint32_t *)ctx->wit.p, (int32_t *)ctx->partial.p,
+                               (const uint32_t *)ctx->order.p, bounds.data(), bslots.data(), (uint32_t)nb, st));
   MGP_HIP(ctx, hipMemcpyAsync(out_first_sat, ctx->first.p, (size_t)n_states * 4u, hipMemcpyDeviceToHost, st));
   MGP_HIP(ctx, hipStreamSynchronize(st));
   if (out_witness) {
@@ -232,13 +242,19 @@ int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words, const uint64_t *pro
 
 int mgp_eval_batch_dev(const uint32_t *d_prog_words, const uint64_t *d_prog_offsets, uint32_t n_states,
                        const uint32_t *d_cands, uint32_t n_cand, uint32_t n_vars, uint32_t n_slots,
-                       int32_t *d_first_sat, uint32_t *d_witness, int32_t *d_scratch, void *stream) {
+                       int32_t *d_first_sat, uint32_t *d_witness, int32_t *d_scratch, const uint32_t *d_order,
+                       const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
+                       void *stream) {
   if (n_states == 0) return MGP_OK;
   if (!d_prog_words || !d_prog_offsets || !d_cands || !d_first_sat || !d_scratch || n_cand == 0 || n_vars == 0 ||
-      n_slots > kMaxSlotsHard)
+      n_slots > kMaxSlotsHard || (n_buckets && (!d_order || !bucket_bounds || !bucket_slots)))
     return fail(nullptr, MGP_E_ARG, "bad argument to mgp_eval_batch_dev");
+  for (uint32_t b = 0; b < n_buckets; ++b)
+    if (bucket_slots[b] > kMaxSlotsHard || bucket_bounds[b] > bucket_bounds[b + 1] || bucket_bounds[b + 1] > n_states)
+      return fail(nullptr, MGP_E_ARG, "bad bucket plan");
   hipError_t e = mgp_launch_eval(d_prog_words, d_prog_offsets, n_states, d_cands, n_cand, n_vars, n_slots,
-                                 d_first_sat, d_witness, d_scratch, (hipStream_t)stream);
+                                 d_first_sat, d_witness, d_scratch, d_order, bucket_bounds, bucket_slots, n_buckets,
+                                 (hipStream_t)stream);
   return e == hipSuccess ? MGP_OK : hip_fail(nullptr, e, "mgp_eval_batch_dev");
 }
 

@@ -162,29 +162,26 @@ MGP_HD uint32_t bv_shift_amount(const U256 &s) {
   return (hi != 0u || s.w[0] >= 256u) ? 256u : s.w[0];
 }
 
+// Variable shifts are branch-free: three limb-granular select stages
+// (v_cndmask) and one funnel stage (v_alignbit), so a per-lane shift amount
+// costs no exec-mask manipulation and no scalar work.
 // logical / arithmetic right shift by s (0..256); fill = 0 or 0xFFFFFFFF
 MGP_HD U256 bv_shr_fill(U256 a, uint32_t s, uint32_t fill) {
-  if (s >= 256u) {
+  const bool all = s >= 256u;
+  const uint32_t k = s >> 5, b = s & 31u;
+  const bool k4 = (k & 4u) != 0u, k2 = (k & 2u) != 0u, k1 = (k & 1u) != 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a.w[i] = fill;
-    return a;
-  }
-  uint32_t k = s >> 5, b = s & 31u;
-  if (k & 4u) {
+  for (int i = 0; i < 8; ++i) a.w[i] = k4 ? ((i + 4 < 8) ? a.w[i + 4] : fill) : a.w[i];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a.w[i] = (i + 4 < 8) ? a.w[i + 4] : fill;
-  }
-  if (k & 2u) {
+  for (int i = 0; i < 8; ++i) a.w[i] = k2 ? ((i + 2 < 8) ? a.w[i + 2] : fill) : a.w[i];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a.w[i] = (i + 2 < 8) ? a.w[i + 2] : fill;
-  }
-  if (k & 1u) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a.w[i] = (i + 1 < 8) ? a.w[i + 1] : fill;
-  }
+  for (int i = 0; i < 8; ++i) a.w[i] = k1 ? ((i + 1 < 8) ? a.w[i + 1] : fill) : a.w[i];
   U256 r;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r.w[i] = mgp_funnel_r((i + 1 < 8) ? a.w[i + 1] : fill, a.w[i], b);
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t v = mgp_funnel_r((i + 1 < 8) ? a.w[i + 1] : fill, a.w[i], b);
+    r.w[i] = all ? fill : v;
+  }
   return r;
 }
 MGP_HD U256 bv_lshr(const U256 &a, uint32_t s) { return bv_shr_fill(a, s, 0u); }
@@ -192,24 +189,22 @@ MGP_HD U256 bv_ashr(const U256 &a, uint32_t s) {
   return bv_shr_fill(a, s, bv_sign(a) ? 0xFFFFFFFFu : 0u);
 }
 MGP_HD U256 bv_shl(U256 a, uint32_t s) {
-  if (s >= 256u) return bv_zero();
-  uint32_t k = s >> 5, b = s & 31u;
-  if (k & 4u) {
+  const bool all = s >= 256u;
+  const uint32_t k = s >> 5, b = s & 31u;
+  const bool k4 = (k & 4u) != 0u, k2 = (k & 2u) != 0u, k1 = (k & 1u) != 0u;
 #pragma unroll
-    for (int i = 7; i >= 0; --i) a.w[i] = (i >= 4) ? a.w[i - 4] : 0u;
-  }
-  if (k & 2u) {
+  for (int i = 7; i >= 0; --i) a.w[i] = k4 ? ((i >= 4) ? a.w[i - 4] : 0u) : a.w[i];
 #pragma unroll
-    for (int i = 7; i >= 0; --i) a.w[i] = (i >= 2) ? a.w[i - 2] : 0u;
-  }
-  if (k & 1u) {
+  for (int i = 7; i >= 0; --i) a.w[i] = k2 ? ((i >= 2) ? a.w[i - 2] : 0u) : a.w[i];
 #pragma unroll
-    for (int i = 7; i >= 0; --i) a.w[i] = (i >= 1) ? a.w[i - 1] : 0u;
-  }
-  if (b == 0u) return a;
+  for (int i = 7; i >= 0; --i) a.w[i] = k1 ? ((i >= 1) ? a.w[i - 1] : 0u) : a.w[i];
   U256 r;
+  const uint32_t rb = (32u - b) & 31u;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r.w[i] = mgp_funnel_r(a.w[i], (i >= 1) ? a.w[i - 1] : 0u, 32u - b);
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t v = mgp_funnel_r(a.w[i], (i >= 1) ? a.w[i - 1] : 0u, rb);
+    r.w[i] = all ? 0u : (b == 0u ? a.w[i] : v);
+  }
   return r;
 }
 // shift left by one, shifting in bit `in`
@@ -299,24 +294,20 @@ template <int J>
 MGP_HD uint32_t bv_knuth_digit(uint32_t (&u)[16], const U256 &v, double inv_v7) {
   const uint32_t v7 = v.w[7], v6 = v.w[6];
   const uint64_t num = ((uint64_t)u[J + 8] << 32) | u[J + 7];
-  uint64_t qhat;
-  if (u[J + 8] >= v7) {
-    qhat = 0xFFFFFFFFull;
-  } else {
-    const double dn = (double)u[J + 8] * 4294967296.0 + (double)u[J + 7];
-    qhat = (uint64_t)(dn * inv_v7);
-    if (qhat > 0xFFFFFFFFull) qhat = 0xFFFFFFFFull;
-    int64_t r = (int64_t)(num - qhat * v7);
-    if (r < 0) { --qhat; r += v7; }
-    if (r >= (int64_t)v7) { ++qhat; }
+  // qhat = min(floor(num / v7), B - 1): double estimate, one integer fix each way
+  const double dn = (double)u[J + 8] * 4294967296.0 + (double)u[J + 7];
+  uint64_t qhat = (uint64_t)(dn * inv_v7);
+  qhat = qhat > 0xFFFFFFFFull ? 0xFFFFFFFFull : qhat;
+  {
+    const int64_t r0 = (int64_t)(num - qhat * v7);
+    qhat = r0 < 0 ? qhat - 1u : (r0 >= (int64_t)v7 && qhat < 0xFFFFFFFFull ? qhat + 1u : qhat);
   }
   uint64_t rhat = num - qhat * v7;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    if (rhat < 0x100000000ull && qhat * v6 > ((rhat << 32) | u[J + 6])) {
-      --qhat;
-      rhat += v7;
-    }
+    const bool dec = rhat < 0x100000000ull && qhat * v6 > ((rhat << 32) | u[J + 6]);
+    qhat = dec ? qhat - 1u : qhat;
+    rhat = dec ? rhat + v7 : rhat;
   }
   // u[J .. J+8] -= qhat * v
   uint32_t borrow = 0, hi = 0;

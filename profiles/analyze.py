@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Summarise a profiles/collect.sh run: per-kernel trace stats + PMC counters.
+
+    python profiles/analyze.py gpurun_out/prof_<tag> > profiles/<tag>_summary.md
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split("(")[0]
+
+
+def main(d):
+    out = []
+    stats = os.path.join(d, "trace", "run_kernel_stats.csv")
+    out.append(f"# rocprofv3 summary: {d}\n")
+    out.append("## kernel trace (--kernel-trace --stats)\n")
+    out.append("| kernel | calls | total ms | avg us | % |")
+    out.append("|---|---|---|---|---|")
+    with open(stats) as f:
+        for r in csv.DictReader(f):
+            out.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.3f} | "
+                       f"{float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.1f} |")
+    # per-dispatch durations of the eval kernel grouped into steps
+    tr = os.path.join(d, "trace", "run_kernel_trace.csv")
+    evals = []
+    with open(tr) as f:
+        for r in csv.DictReader(f):
+            if short(r["Kernel_Name"]) in ("mgp_eval_kernel", "mgp_finalize_kernel"):
+                evals.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
+    evals.sort()
+    steps, cur = [], []
+    for s, e, n in evals:
+        cur.append((s, e))
+        if n == "mgp_finalize_kernel":
+            steps.append((cur[0][0], cur[-1][1], sum(b - a for a, b in cur)))
+            cur = []
+    if steps:
+        out.append("\n## eval step (all bucket launches + finalize)\n")
+        out.append("| step | wall us (first start -> last end) | sum of kernel durations us |")
+        out.append("|---|---|---|")
+        for i, (a, b, busy) in enumerate(steps):
+            out.append(f"| {i} | {(b - a)/1e3:.1f} | {busy/1e3:.1f} |")
+    # counters
+    agg = defaultdict(lambda: defaultdict(float))
+    meta = {}
+    for sub in sorted(os.listdir(d)):
+        p = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        with open(p) as f:
+            for r in csv.DictReader(f):
+                k = short(r["Kernel_Name"])
+                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"], r["Scratch_Size"])
+    out.append("\n## PMC counters (summed over dispatches; separate passes)\n")
+    for k in ("mgp_eval_kernel", "mgp_keccak64_kernel", "mgp_valu_probe_kernel"):
+        if k not in agg:
+            continue
+        c = agg[k]
+        v, sg, lds, scr = meta[k]
+        out.append(f"### {k}  (VGPR {v}, SGPR {sg}, LDS {lds} B, scratch {scr})\n")
+        out.append("| counter | value |")
+        out.append("|---|---|")
+        for n in sorted(c):
+            out.append(f"| {n} | {c[n]:.4g} |")
+        der = {}
+        if c.get("SQ_WAVES"):
+            der["VALU insts / wave"] = c["SQ_INSTS_VALU"] / c["SQ_WAVES"]
+            der["SALU insts / wave"] = c.get("SQ_INSTS_SALU", 0) / c["SQ_WAVES"]
+            der["LDS insts / wave"] = c.get("SQ_INSTS_LDS", 0) / c["SQ_WAVES"]
+            der["SMEM insts / wave"] = c.get("SQ_INSTS_SMEM", 0) / c["SQ_WAVES"]
+        if c.get("SQ_WAVE_CYCLES"):
+            der["VALU active / wave-cycles"] = c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_WAVE_CYCLES"]
+            tot = c.get("SQ_WAIT_ANY", 0) + c.get("SQ_WAIT_INST_ANY", 0) + c.get("SQ_ACTIVE_INST_ANY", 0)
+            if tot:
+                der["wait_any share"] = c.get("SQ_WAIT_ANY", 0) / tot
+                der["wait_inst_any share"] = c.get("SQ_WAIT_INST_ANY", 0) / tot
+                der["active_inst_any share"] = c.get("SQ_ACTIVE_INST_ANY", 0) / tot
+        if "FETCH_SIZE" in c:
+            der["FETCH_SIZE KB (x2 gfx950 correction for wide streams)"] = c["FETCH_SIZE"]
+        if der:
+            out.append("\nderived:\n")
+            for n, val in der.items():
+                out.append(f"- {n}: {val:.4g}")
+        out.append("")
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

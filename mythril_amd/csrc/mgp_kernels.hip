@@ -19,6 +19,9 @@
 // conflict-free).  No MFMA: nothing here is a contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <type_traits>
 
 #include "../../include/mgp_ir.h"
 #include "mgp_bv.h"
@@ -30,6 +33,17 @@
 namespace {
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0..N-1, so that
+// per-candidate register arrays are only ever indexed by constants (a runtime
+// index would demote them to scratch)
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+  if constexpr (N > 0) {
+    static_for<N - 1>(f);
+    f(std::integral_constant<int, N - 1>{});
+  }
+}
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle
 // must be bijective"): blocks dispatched round-robin over the 8 XCDs get
@@ -46,7 +60,6 @@ struct EvalCtx {
   const uint32_t *cpool;
   const uint4 *cbase;  // this state's candidates, device layout
   uint32_t n_cand;
-  uint32_t cand;       // clamped candidate index of this lane
   uint32_t lane;
 };
 
@@ -57,26 +70,29 @@ __device__ __forceinline__ U256 u256_from(uint4 lo, uint4 hi) {
   return v;
 }
 
-__device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx &e) {
+// LDS slot image: [slot][cpl][half][lane] x 16 B (ds_read_b128, conflict-free)
+template <int CPL>
+__device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx &e, int c, uint32_t cand) {
   uint32_t kind = o >> 14, idx = o & 0x3FFFu;
   if (kind == MGP_K_ACC) return acc;
   if (kind == MGP_K_SLOT) {
-    const uint4 *p = e.lds + (size_t)idx * 2u * MGP_WAVE + e.lane;
+    const uint4 *p = e.lds + ((size_t)idx * CPL + c) * 2u * MGP_WAVE + e.lane;
     return u256_from(p[0], p[MGP_WAVE]);
   }
   if (kind == MGP_K_CONST) {
-    const uint32_t *c = e.cpool + idx * 8u;  // uniform -> s_load_dwordx8
+    const uint32_t *cp = e.cpool + idx * 8u;  // uniform -> s_load_dwordx8
     U256 v;
 #pragma unroll
-    for (int l = 0; l < 8; ++l) v.w[l] = c[l];
+    for (int l = 0; l < 8; ++l) v.w[l] = cp[l];
     return v;
   }
-  const uint4 *p = e.cbase + (size_t)idx * 2u * e.n_cand + e.cand;
+  const uint4 *p = e.cbase + (size_t)idx * 2u * e.n_cand + cand;
   return u256_from(p[0], p[e.n_cand]);
 }
 
-__device__ __forceinline__ void store_slot(uint4 *lds, uint32_t slot, uint32_t lane, const U256 &v) {
-  uint4 *p = lds + (size_t)slot * 2u * MGP_WAVE + lane;
+template <int CPL>
+__device__ __forceinline__ void store_slot(uint4 *lds, uint32_t slot, int c, uint32_t lane, const U256 &v) {
+  uint4 *p = lds + ((size_t)slot * CPL + c) * 2u * MGP_WAVE + lane;
   p[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
   p[MGP_WAVE] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
 }
@@ -90,6 +106,89 @@ __device__ __forceinline__ bool is_signed_op(uint32_t op) {
 }  // namespace
 
 // --------------------------------------------------------------- eval
+namespace {
+
+__device__ __forceinline__ bool eval_cmp(uint32_t op, const U256 &a, const U256 &b, uint32_t width) {
+  switch (op) {
+    case MGP_OP_EQ: return bv_eq(a, b);
+    case MGP_OP_ULT: return bv_ult(a, b);
+    case MGP_OP_ULE: return !bv_ult(b, a);
+    case MGP_OP_UGT: return bv_ult(b, a);
+    case MGP_OP_UGE: return !bv_ult(a, b);
+    case MGP_OP_SLT: return bv_slt(bv_sext(a, width), bv_sext(b, width));
+    case MGP_OP_SLE: return !bv_slt(bv_sext(b, width), bv_sext(a, width));
+    case MGP_OP_SGT: return bv_slt(bv_sext(b, width), bv_sext(a, width));
+    case MGP_OP_SGE: return !bv_slt(bv_sext(a, width), bv_sext(b, width));
+    case MGP_OP_UADD_NOOVF: {
+      uint32_t carry;
+      U256 s = bv_add(a, b, &carry);
+      return (width >= 256u) ? (carry == 0u) : bv_eq(s, bv_mask(s, width));
+    }
+    case MGP_OP_UMUL_NOOVF: {
+      U256 lo;
+      U256 hi = bv_mul_full(a, b, &lo);
+      return bv_is_zero(hi) && bv_eq(lo, bv_mask(lo, width));
+    }
+    default: return !bv_ult(a, b);  // USUB_NOUDF: b <= a
+  }
+}
+
+// binary BV ops (a, b already fetched); division ops share one udivrem site
+__device__ __forceinline__ U256 eval_bin(uint32_t op, U256 a, U256 b, uint32_t width, uint32_t imm) {
+  if (op == MGP_OP_CONCAT) return bv_or(bv_shl(a, imm), b);
+  if (is_signed_op(op) && width < 256u) {
+    a = bv_sext(a, width);
+    if (op != MGP_OP_ASHR) b = bv_sext(b, width);
+  }
+  if (op >= MGP_OP_UDIV && op <= MGP_OP_SMOD) {
+    // SMT-LIB msb case split on |a|, |b|
+    const bool sg = op >= MGP_OP_SDIV;
+    const bool sa = sg && bv_sign(a), sb = sg && bv_sign(b);
+    U256 q, m;
+    bv_udivrem(sa ? bv_neg(a) : a, sb ? bv_neg(b) : b, &q, &m);
+    if (op == MGP_OP_UDIV) return q;
+    if (op == MGP_OP_UREM) return m;
+    if (op == MGP_OP_SDIV) return (sa != sb) ? bv_neg(q) : q;
+    if (op == MGP_OP_SREM) return sa ? bv_neg(m) : m;
+    if (bv_is_zero(m) || (!sa && !sb)) return m;  // SMOD: sign follows the divisor
+    if (sa && !sb) return bv_add(bv_neg(m), b, nullptr);
+    if (!sa && sb) return bv_add(m, b, nullptr);
+    return bv_neg(m);
+  }
+  switch (op) {
+    case MGP_OP_ADD: return bv_add(a, b, nullptr);
+    case MGP_OP_SUB: return bv_sub(a, b, nullptr);
+    case MGP_OP_MUL: return bv_mul(a, b);
+    case MGP_OP_AND: return bv_and(a, b);
+    case MGP_OP_OR: return bv_or(a, b);
+    case MGP_OP_XOR: return bv_xor(a, b);
+    case MGP_OP_SHL: return bv_shl(a, bv_shift_amount(b));
+    case MGP_OP_LSHR: return bv_lshr(a, bv_shift_amount(b));
+    case MGP_OP_ASHR: return bv_ashr(a, bv_shift_amount(b));
+    default: return bv_zero();
+  }
+}
+
+__device__ __forceinline__ bool is_unary_bv(uint32_t op) {
+  return op == MGP_OP_MOV || op == MGP_OP_ZEXT || op == MGP_OP_NOT || op == MGP_OP_NEG ||
+         op == MGP_OP_EXTRACT || op == MGP_OP_SEXT;
+}
+
+__device__ __forceinline__ U256 eval_unary(uint32_t op, const U256 &a, uint32_t imm) {
+  if (op == MGP_OP_NOT) return bv_not(a);
+  if (op == MGP_OP_NEG) return bv_neg(a);
+  if (op == MGP_OP_EXTRACT) return bv_lshr(a, imm);
+  if (op == MGP_OP_SEXT) return bv_sext(a, imm);
+  return a;  // MOV / ZEXT: storage is zero-extended, masking below
+}
+
+}  // namespace
+
+// CPL = candidates per lane: a wave evaluates 64*CPL candidate models per
+// pass over the bytecode, so the scalar decode/dispatch work of every
+// instruction is shared by CPL independent 256-bit computations (which the
+// scheduler interleaves for ILP).
+template <int CPL>
 __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
     const uint32_t *__restrict__ words, const uint64_t *__restrict__ offs,
     uint32_t n_states, const uint4 *__restrict__ cands, uint32_t n_cand,
@@ -102,8 +201,6 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
   const uint32_t state = order ? order[order_base + k] : order_base + k;
   if (state >= n_states) return;
   const uint32_t lane = threadIdx.x;
-  const uint32_t cand = chunk * MGP_WAVE + lane;
-  const bool valid = cand < n_cand;
 
   const uint32_t *prog = words + offs[state];
   const uint32_t n_ins = uni(prog[0]);
@@ -119,12 +216,22 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
   e.cpool = ins + (size_t)n_ins * MGP_INS_WORDS;
   e.cbase = cands + (size_t)state * n_vars * 2u * n_cand;
   e.n_cand = n_cand;
-  e.cand = valid ? cand : (n_cand - 1u);
   e.lane = lane;
 
-  U256 acc = bv_zero();
-  uint64_t bools = 1ull << MGP_BOOL_TRUE;
-  bool root = false;
+  uint32_t cand[CPL];
+  bool valid[CPL];
+  U256 acc[CPL];
+  uint64_t bools[CPL];
+  bool root[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const uint32_t x = chunk * (MGP_WAVE * CPL) + c * MGP_WAVE + lane;
+    valid[c] = x < n_cand;
+    cand[c] = valid[c] ? x : n_cand - 1u;
+    acc[c] = bv_zero();
+    bools[c] = 1ull << MGP_BOOL_TRUE;
+    root[c] = false;
+  }
 
   // software-pipelined instruction fetch: the scalar loads of instruction
   // pc+1 are in flight while instruction pc executes (mgp_lower pads every
@@ -142,122 +249,67 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
     const uint32_t oa = w1 & 0xFFFFu, ob = w1 >> 16, oc = w2 & 0xFFFFu, imm = w2 >> 16;
 
     if (op == MGP_OP_RET) {
-      root = ((bools >> oa) & 1ull) != 0ull;
+      static_for<CPL>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int c = decltype(ic)::value;
+        root[c] = ((bools[c] >> oa) & 1ull) != 0ull;
+      });
       break;
     }
     if (is_bool_op(op)) {
-      const bool a = ((bools >> oa) & 1ull) != 0ull;
-      const bool b = ((bools >> ob) & 1ull) != 0ull;
-      const bool c = ((bools >> oc) & 1ull) != 0ull;
-      bool r;
-      switch (op) {
-        case MGP_OP_BAND: r = a && b; break;
-        case MGP_OP_BOR: r = a || b; break;
-        case MGP_OP_BXOR: r = a != b; break;
-        case MGP_OP_BNOT: r = !a; break;
-        case MGP_OP_BITE: r = a ? b : c; break;
-        default: r = a == b; break;  // BEQ
-      }
-      bools = (bools & ~(1ull << dst)) | ((uint64_t)r << dst);
+      static_for<CPL>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int c = decltype(ic)::value;
+        const bool a = ((bools[c] >> oa) & 1ull) != 0ull;
+        const bool b = ((bools[c] >> ob) & 1ull) != 0ull;
+        const bool cc = ((bools[c] >> oc) & 1ull) != 0ull;
+        bool r;
+        switch (op) {
+          case MGP_OP_BAND: r = a && b; break;
+          case MGP_OP_BOR: r = a || b; break;
+          case MGP_OP_BXOR: r = a != b; break;
+          case MGP_OP_BNOT: r = !a; break;
+          case MGP_OP_BITE: r = a ? b : cc; break;
+          default: r = a == b; break;  // BEQ
+        }
+        bools[c] = (bools[c] & ~(1ull << dst)) | ((uint64_t)r << dst);
+      });
       continue;
     }
     if (is_cmp_op(op)) {
-      U256 a = fetch(oa, acc, e), b = fetch(ob, acc, e);
-      bool r;
-      switch (op) {
-        case MGP_OP_EQ: r = bv_eq(a, b); break;
-        case MGP_OP_ULT: r = bv_ult(a, b); break;
-        case MGP_OP_ULE: r = !bv_ult(b, a); break;
-        case MGP_OP_UGT: r = bv_ult(b, a); break;
-        case MGP_OP_UGE: r = !bv_ult(a, b); break;
-        case MGP_OP_SLT: r = bv_slt(bv_sext(a, width), bv_sext(b, width)); break;
-        case MGP_OP_SLE: r = !bv_slt(bv_sext(b, width), bv_sext(a, width)); break;
-        case MGP_OP_SGT: r = bv_slt(bv_sext(b, width), bv_sext(a, width)); break;
-        case MGP_OP_SGE: r = !bv_slt(bv_sext(a, width), bv_sext(b, width)); break;
-        case MGP_OP_UADD_NOOVF: {
-          uint32_t carry;
-          U256 s = bv_add(a, b, &carry);
-          r = (width >= 256u) ? (carry == 0u) : bv_eq(s, bv_mask(s, width));
-          break;
-        }
-        case MGP_OP_UMUL_NOOVF: {
-          U256 lo;
-          U256 hi = bv_mul_full(a, b, &lo);
-          r = bv_is_zero(hi) && bv_eq(lo, bv_mask(lo, width));
-          break;
-        }
-        default: r = !bv_ult(a, b); break;  // USUB_NOUDF: b <= a
-      }
-      bools = (bools & ~(1ull << dst)) | ((uint64_t)r << dst);
+      static_for<CPL>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int c = decltype(ic)::value;
+        const U256 a = fetch<CPL>(oa, acc[c], e, c, cand[c]);
+        const U256 b = fetch<CPL>(ob, acc[c], e, c, cand[c]);
+        const bool r = eval_cmp(op, a, b, width);
+        bools[c] = (bools[c] & ~(1ull << dst)) | ((uint64_t)r << dst);
+      });
       continue;
     }
 
     // ---- BV-producing instructions
-    U256 r;
-    if (op == MGP_OP_ITE) {
-      const bool c = ((bools >> oa) & 1ull) != 0ull;
-      U256 t = fetch(ob, acc, e), f = fetch(oc, acc, e);
-      r = bv_sel(c, t, f);
+    static_for<CPL>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int c = decltype(ic)::value;
+      U256 r;
+      if (op == MGP_OP_ITE) {
+        const bool cond = ((bools[c] >> oa) & 1ull) != 0ull;
+        r = bv_sel(cond, fetch<CPL>(ob, acc[c], e, c, cand[c]), fetch<CPL>(oc, acc[c], e, c, cand[c]));
+      } else if (is_unary_bv(op)) {
+        r = eval_unary(op, fetch<CPL>(oa, acc[c], e, c, cand[c]), imm);
+      } else {
+        r = eval_bin(op, fetch<CPL>(oa, acc[c], e, c, cand[c]), fetch<CPL>(ob, acc[c], e, c, cand[c]), width, imm);
+      }
       if (width < 256u) r = bv_mask(r, width);
-      acc = r;
-      if (flags & MGP_INS_STORE) store_slot(mgp_lds, dst, lane, r);
-      continue;
-    }
-    U256 a = fetch(oa, acc, e);
-    if (op == MGP_OP_MOV || op == MGP_OP_ZEXT) {
-      r = a;
-    } else if (op == MGP_OP_NOT) {
-      r = bv_not(a);
-    } else if (op == MGP_OP_NEG) {
-      r = bv_neg(a);
-    } else if (op == MGP_OP_EXTRACT) {
-      r = bv_lshr(a, imm);
-    } else if (op == MGP_OP_SEXT) {
-      r = bv_sext(a, imm);
-    } else {
-      U256 b = fetch(ob, acc, e);
-      if (is_signed_op(op) && width < 256u) {
-        a = bv_sext(a, width);
-        if (op != MGP_OP_ASHR) b = bv_sext(b, width);
-      }
-      if (op >= MGP_OP_UDIV && op <= MGP_OP_SMOD) {
-        // one division site for the five div/rem ops (SMT-LIB msb case split on |a|, |b|)
-        const bool sg = op >= MGP_OP_SDIV;
-        const bool sa = sg && bv_sign(a), sb = sg && bv_sign(b);
-        U256 q, m;
-        bv_udivrem(sa ? bv_neg(a) : a, sb ? bv_neg(b) : b, &q, &m);
-        if (op == MGP_OP_UDIV) r = q;
-        else if (op == MGP_OP_UREM) r = m;
-        else if (op == MGP_OP_SDIV) r = (sa != sb) ? bv_neg(q) : q;
-        else if (op == MGP_OP_SREM) r = sa ? bv_neg(m) : m;
-        else if (bv_is_zero(m) || (!sa && !sb)) r = m;  // SMOD: sign follows the divisor
-        else if (sa && !sb) r = bv_add(bv_neg(m), b, nullptr);
-        else if (!sa && sb) r = bv_add(m, b, nullptr);
-        else r = bv_neg(m);
-      } else switch (op) {
-        case MGP_OP_ADD: r = bv_add(a, b, nullptr); break;
-        case MGP_OP_SUB: r = bv_sub(a, b, nullptr); break;
-        case MGP_OP_MUL: r = bv_mul(a, b); break;
-        case MGP_OP_AND: r = bv_and(a, b); break;
-        case MGP_OP_OR: r = bv_or(a, b); break;
-        case MGP_OP_XOR: r = bv_xor(a, b); break;
-        case MGP_OP_SHL: r = bv_shl(a, bv_shift_amount(b)); break;
-        case MGP_OP_LSHR: r = bv_lshr(a, bv_shift_amount(b)); break;
-        case MGP_OP_ASHR: r = bv_ashr(a, bv_shift_amount(b)); break;
-        case MGP_OP_CONCAT: r = bv_or(bv_shl(a, imm), b); break;
-        default: r = bv_zero(); break;
-      }
-    }
-    if (width < 256u) r = bv_mask(r, width);
-    acc = r;
-    if (flags & MGP_INS_STORE) store_slot(mgp_lds, dst, lane, r);
+      acc[c] = r;
+      if (flags & MGP_INS_STORE) store_slot<CPL>(mgp_lds, dst, c, lane, r);
+    });
   }
 
-  const unsigned long long m = __ballot(valid && root);
-  if (lane == 0) {
-    partial[(size_t)state * n_chunks + chunk] =
-        m ? (int32_t)(chunk * MGP_WAVE + (uint32_t)__ffsll((long long)m) - 1u) : MGP_PARTIAL_NONE;
+  int32_t first = MGP_PARTIAL_NONE;
+#pragma unroll
+  for (int c = CPL - 1; c >= 0; --c) {
+    const unsigned long long m = __ballot(valid[c] && root[c]);
+    if (m) first = (int32_t)(chunk * (MGP_WAVE * CPL) + c * MGP_WAVE + (uint32_t)__ffsll((long long)m) - 1u);
   }
+  if (lane == 0) partial[(size_t)state * n_chunks + chunk] = first;
 }
 
 __global__ void mgp_finalize_kernel(const int32_t *__restrict__ partial, uint32_t n_states,
@@ -537,6 +589,43 @@ __global__ __launch_bounds__(256) void mgp_valu_probe_kernel(uint32_t iters, uin
 }
 
 // ------------------------------------------------------------ launchers
+template <int CPL>
+static hipError_t launch_eval_cpl(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
+                                  const uint32_t *cands, uint32_t n_cand, uint32_t n_vars, uint32_t n_slots,
+                                  int32_t *partial, const uint32_t *order, const uint32_t *bucket_bounds,
+                                  const uint32_t *bucket_slots, uint32_t n_buckets, uint32_t n_chunks,
+                                  hipStream_t st) {
+  // One launch per slot-count bucket: the dynamic LDS (slots x CPL x 2 KiB
+  // per 64-lane wave) is sized per bucket, so states with few live values run
+  // at the occupancy their LDS footprint allows instead of the batch maximum.
+  const bool bucketed = n_buckets && order && bucket_bounds && bucket_slots;
+  const uint32_t nb = bucketed ? n_buckets : 1u;
+  for (uint32_t bkt = 0; bkt < nb; ++bkt) {
+    const uint32_t lo = bucketed ? bucket_bounds[bkt] : 0u;
+    const uint32_t hi = bucketed ? bucket_bounds[bkt + 1] : n_states;
+    const uint32_t sl = bucketed ? bucket_slots[bkt] : n_slots;
+    if (hi <= lo) continue;
+    const uint64_t nblk = (uint64_t)(hi - lo) * n_chunks;
+    const size_t lds = (size_t)(sl ? sl : 1u) * CPL * 2u * MGP_WAVE * sizeof(uint4);
+    hipLaunchKernelGGL(mgp_eval_kernel<CPL>, dim3((uint32_t)nblk), dim3(MGP_WAVE), lds, st, words, offs, n_states,
+                       reinterpret_cast<const uint4 *>(cands), n_cand, n_vars, n_chunks, sl, partial,
+                       bucketed ? order : nullptr, lo);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
+// candidates per lane: 2 when a state has enough candidates to fill 128
+// lanes; MGP_CPL=1|2 in the environment forces a value (A/B measurements)
+static uint32_t cpl_override() {
+  static const uint32_t v = [] {
+    const char *e = getenv("MGP_CPL");
+    return (e && (e[0] == '1' || e[0] == '2') && e[1] == 0) ? (uint32_t)(e[0] - '0') : 0u;
+  }();
+  return v;
+}
+
 extern "C" {
 
 hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
@@ -545,24 +634,14 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
                            const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
                            hipStream_t st) {
   if (n_states == 0) return hipSuccess;
-  const uint32_t n_chunks = (n_cand + MGP_WAVE - 1) / MGP_WAVE;
-  // One launch per slot-count bucket: the dynamic LDS (slots x 2 KiB per
-  // 64-lane wave) is sized per bucket, so states with few live values run at
-  // the occupancy their LDS footprint allows instead of the batch maximum.
-  const uint32_t nb = (n_buckets && order && bucket_bounds && bucket_slots) ? n_buckets : 1u;
-  for (uint32_t bkt = 0; bkt < nb; ++bkt) {
-    const uint32_t lo = (nb > 1 || n_buckets) ? bucket_bounds[bkt] : 0u;
-    const uint32_t hi = (nb > 1 || n_buckets) ? bucket_bounds[bkt + 1] : n_states;
-    const uint32_t sl = (nb > 1 || n_buckets) ? bucket_slots[bkt] : n_slots;
-    if (hi <= lo) continue;
-    const uint64_t nblk = (uint64_t)(hi - lo) * n_chunks;
-    const size_t lds = (size_t)(sl ? sl : 1u) * 2u * MGP_WAVE * sizeof(uint4);
-    hipLaunchKernelGGL(mgp_eval_kernel, dim3((uint32_t)nblk), dim3(MGP_WAVE), lds, st, words, offs, n_states,
-                       reinterpret_cast<const uint4 *>(cands), n_cand, n_vars, n_chunks, sl, partial,
-                       (nb > 1 || n_buckets) ? order : nullptr, lo);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return err;
-  }
+  const uint32_t cpl = cpl_override() ? cpl_override() : (n_cand >= 128u ? 2u : 1u);
+  const uint32_t n_chunks = (n_cand + MGP_WAVE * cpl - 1) / (MGP_WAVE * cpl);
+  hipError_t err = (cpl == 2u)
+                       ? launch_eval_cpl<2>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
+                                            bucket_bounds, bucket_slots, n_buckets, n_chunks, st)
+                       : launch_eval_cpl<1>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
+                                            bucket_bounds, bucket_slots, n_buckets, n_chunks, st);
+  if (err != hipSuccess) return err;
   hipLaunchKernelGGL(mgp_finalize_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, partial,
                      n_states, n_chunks, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars,
                      first_sat, reinterpret_cast<uint4 *>(witness));

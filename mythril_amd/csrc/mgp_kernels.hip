@@ -55,19 +55,12 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
   return base + (bid >> 3);
 }
 
-// The first kVarCache candidate variables of a lane are loaded into VGPRs
-// once, at wave start (all loads in flight together), instead of paying a
-// dependent global-memory round trip at every VAR operand.
-constexpr int kVarCache = 6;
-
-template <int CPL>
 struct EvalCtx {
   const uint4 *lds;
   const uint32_t *cpool;
   const uint4 *cbase;  // this state's candidates, device layout
   uint32_t n_cand;
   uint32_t lane;
-  U256 vc[CPL][kVarCache];
 };
 
 __device__ __forceinline__ U256 u256_from(uint4 lo, uint4 hi) {
@@ -79,7 +72,7 @@ __device__ __forceinline__ U256 u256_from(uint4 lo, uint4 hi) {
 
 // LDS slot image: [slot][cpl][half][lane] x 16 B (ds_read_b128, conflict-free)
 template <int CPL>
-__device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx<CPL> &e, int c, uint32_t cand) {
+__device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx &e, int c, uint32_t cand) {
   uint32_t kind = o >> 14, idx = o & 0x3FFFu;
   if (kind == MGP_K_ACC) return acc;
   if (kind == MGP_K_SLOT) {
@@ -92,15 +85,6 @@ __device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx
 #pragma unroll
     for (int l = 0; l < 8; ++l) v.w[l] = cp[l];
     return v;
-  }
-  switch (idx) {  // uniform branch to a register-cached variable
-    case 0: return e.vc[c][0];
-    case 1: return e.vc[c][1];
-    case 2: return e.vc[c][2];
-    case 3: return e.vc[c][3];
-    case 4: return e.vc[c][4];
-    case 5: return e.vc[c][5];
-    default: break;
   }
   const uint4 *p = e.cbase + (size_t)idx * 2u * e.n_cand + cand;
   return u256_from(p[0], p[e.n_cand]);
@@ -227,7 +211,7 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
     return;
   }
   const uint32_t *ins = prog + MGP_HDR_WORDS;
-  EvalCtx<CPL> e;
+  EvalCtx e;
   e.lds = mgp_lds;
   e.cpool = ins + (size_t)n_ins * MGP_INS_WORDS;
   e.cbase = cands + (size_t)state * n_vars * 2u * n_cand;
@@ -248,19 +232,6 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
     bools[c] = 1ull << MGP_BOOL_TRUE;
     root[c] = false;
   }
-  const uint32_t vars_used = h_stat >> 8;
-  static_for<CPL>([&](auto ic) __attribute__((always_inline)) {
-    constexpr int c = decltype(ic)::value;
-    static_for<kVarCache>([&](auto iv) __attribute__((always_inline)) {
-      constexpr int v = decltype(iv)::value;
-      if ((uint32_t)v < vars_used) {
-        const uint4 *p = e.cbase + (size_t)v * 2u * n_cand + cand[c];
-        e.vc[c][v] = u256_from(p[0], p[n_cand]);
-      } else {
-        e.vc[c][v] = bv_zero();
-      }
-    });
-  });
 
   // software-pipelined instruction fetch: the scalar loads of instruction
   // pc+1 are in flight while instruction pc executes (mgp_lower pads every
@@ -663,7 +634,7 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
                            const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
                            hipStream_t st) {
   if (n_states == 0) return hipSuccess;
-  const uint32_t cpl = cpl_override() ? cpl_override() : 1u;  // CPL=2 measured slower (LDS occupancy)
+  const uint32_t cpl = cpl_override() ? cpl_override() : (n_cand >= 128u ? 2u : 1u);
   const uint32_t n_chunks = (n_cand + MGP_WAVE * cpl - 1) / (MGP_WAVE * cpl);
   hipError_t err = (cpl == 2u)
                        ? launch_eval_cpl<2>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,

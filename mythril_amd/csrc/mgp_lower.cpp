@@ -307,6 +307,64 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     if (root.k == R_INS) root.idx = remap[root.idx];
   }
 
+  // ------------------------------------------- register-pressure scheduling
+  // Re-emit the live instructions in a depth-first post-order from the root,
+  // visiting the operand with the larger Sethi-Ullman need first.  Trees then
+  // need O(log n) simultaneously live values instead of whatever the node
+  // order of the input happened to imply, and a parent usually directly
+  // follows its last operand (accumulator forwarding, no LDS round trip).
+  {
+    const uint32_t n0 = (uint32_t)S.ins.size();
+    std::vector<uint32_t> need(n0, 1);
+    auto kids = [&](uint32_t t, uint32_t out[3]) -> int {
+      int k = 0;
+      const VIns &I = S.ins[t];
+      for (const Ref *r : {&I.a, &I.b, &I.c})
+        if (r->k == R_INS) out[k++] = r->idx;
+      return k;
+    };
+    for (uint32_t t = 0; t < n0; ++t) {
+      uint32_t ch[3];
+      const int k = kids(t, ch);
+      uint32_t nd[3] = {0, 0, 0};
+      for (int i = 0; i < k; ++i) nd[i] = need[ch[i]];
+      std::sort(nd, nd + k, [](uint32_t x, uint32_t y) { return x > y; });
+      uint32_t m = 1;
+      for (int i = 0; i < k; ++i) m = std::max(m, nd[i] + (uint32_t)i);
+      need[t] = m;
+    }
+    std::vector<uint8_t> state(n0, 0);  // 0 new, 1 expanded, 2 emitted
+    std::vector<uint32_t> order;
+    order.reserve(n0);
+    std::vector<uint32_t> stack;
+    if (root.k == R_INS) stack.push_back(root.idx);
+    while (!stack.empty()) {
+      const uint32_t t = stack.back();
+      if (state[t] == 2) { stack.pop_back(); continue; }
+      if (state[t] == 1) { state[t] = 2; order.push_back(t); stack.pop_back(); continue; }
+      state[t] = 1;
+      uint32_t ch[3];
+      const int k = kids(t, ch);
+      // push so that the operand with the larger need is evaluated first
+      std::sort(ch, ch + k, [&](uint32_t x, uint32_t y) { return need[x] < need[y]; });
+      for (int i = 0; i < k; ++i)
+        if (state[ch[i]] == 0) stack.push_back(ch[i]);
+    }
+    if (order.size() == n0) {
+      std::vector<uint32_t> remap(n0);
+      for (uint32_t i = 0; i < n0; ++i) remap[order[i]] = i;
+      std::vector<VIns> re(n0);
+      for (uint32_t i = 0; i < n0; ++i) {
+        VIns I = S.ins[order[i]];
+        for (Ref *r : {&I.a, &I.b, &I.c})
+          if (r->k == R_INS) r->idx = remap[r->idx];
+        re[i] = I;
+      }
+      S.ins.swap(re);
+      if (root.k == R_INS) root.idx = remap[root.idx];
+    }
+  }
+
   // ---------------------------------------------------------- liveness
   const uint32_t n = (uint32_t)S.ins.size();
   std::vector<int64_t> last_use(n, -1);       // last instruction reading the value

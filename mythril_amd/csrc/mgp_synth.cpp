@@ -15,6 +15,7 @@
 // uses the same 256-bit helpers as the kernel (mgp_bv.h) — this is workload
 // construction, not verification; parity is checked against oracle/.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -211,9 +212,24 @@ struct Gen {
     uint32_t r = rng.below(100), acc = 0;
     for (const MixEntry &m : kMix) {
       acc += m.weight;
-      if (r < acc) return m.op;
+      if (r < acc) return ablate(m.op);
     }
     return MGP_OP_ADD;
+  }
+  // ablation knob for kernel studies (never set by the benchmark):
+  // MGP_SYNTH_ABLATE=nodiv|nomul|nodivmul replaces those ops by ADD
+  static uint8_t ablate(uint8_t op) {
+    static const int mode = [] {
+      const char *e = getenv("MGP_SYNTH_ABLATE");
+      if (!e) return 0;
+      if (!strcmp(e, "nodiv")) return 1;
+      if (!strcmp(e, "nomul")) return 2;
+      if (!strcmp(e, "nodivmul")) return 3;
+      return 0;
+    }();
+    const bool div = op >= MGP_OP_UDIV && op <= MGP_OP_SMOD;
+    if (((mode & 1) && div) || ((mode & 2) && op == MGP_OP_MUL)) return MGP_OP_ADD;
+    return op;
   }
 
   void bin_wide(uint8_t op) {

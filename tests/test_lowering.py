@@ -98,17 +98,24 @@ def test_uf_chains():
 
 
 def test_many_live_values_rejected_cleanly():
-    # 40 simultaneously live 256-bit values with a 16-slot cap -> unsupported, not wrong
+    # 40 values each used by two chains that consume them in opposite orders:
+    # whatever the schedule, all 40 are live at once -> a 4-slot cap is
+    # unsupported (never wrong), a 64-slot cap lowers and evaluates correctly
     n = 40
     nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]
+    vals = []
     for i in range(n):
-        nl.append([S.ADD if i % 2 else S.MUL, 256, len(nl) - 1, i % 2, -1, 0, 0])
-    first = 2
-    acc = first
-    for i in range(1, n):
-        nl.append([S.XOR, 256, acc, first + i, -1, 0, 0])
+        nl.append([S.ADD if i % 2 else S.MUL, 256, len(nl) - 1 if i else 0, i % 2, -1, 0, 0])
+        vals.append(len(nl) - 1)
+    acc = vals[0]
+    for v in vals[1:]:
+        nl.append([S.XOR, 256, acc, v, -1, 0, 0])
         acc = len(nl) - 1
-    nl.append([S.ULT, 1, acc, 0, -1, 0, 0])
+    acc2 = vals[-1]
+    for v in reversed(vals[:-1]):
+        nl.append([S.SUB, 256, acc2, v, -1, 0, 0])
+        acc2 = len(nl) - 1
+    nl.append([S.ULT, 1, acc, acc2, -1, 0, 0])
     nodes, noff, consts, coff = pack_states([(nl, [])])
     _, _, status = N.lower(nodes, noff, consts, coff, max_slots=4)
     assert status[0] == N.ST_UNSUPPORTED

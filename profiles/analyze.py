@@ -11,7 +11,7 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0]
+    return name.split("(")[0].replace("void ", "").split("<")[0]
 
 
 def main(d):

@@ -18,7 +18,7 @@ from collections import defaultdict
 d = sys.argv[1]
 agg = defaultdict(float)
 for r in csv.DictReader(open(os.path.join(d, "pmc_sq", "run_counter_collection.csv"))):
-    if r["Kernel_Name"].startswith("mgp_eval_kernel"):
+    if "mgp_eval_kernel" in r["Kernel_Name"]:
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
 w = agg["SQ_WAVES"]
 print({k: round(v / w, 1) for k, v in agg.items()}, "waves", w)

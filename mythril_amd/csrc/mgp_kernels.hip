@@ -634,7 +634,7 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
                            const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
                            hipStream_t st) {
   if (n_states == 0) return hipSuccess;
-  const uint32_t cpl = cpl_override() ? cpl_override() : (n_cand >= 128u ? 2u : 1u);
+  const uint32_t cpl = cpl_override() ? cpl_override() : 1u;  // CPL=2 measured slower (LDS occupancy halves)
   const uint32_t n_chunks = (n_cand + MGP_WAVE * cpl - 1) / (MGP_WAVE * cpl);
   hipError_t err = (cpl == 2u)
                        ? launch_eval_cpl<2>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,

@@ -15,6 +15,7 @@
 //   5. emit header + instructions + constant pool.
 // States are independent; the batch is lowered in parallel with OpenMP.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -313,7 +314,11 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   // need O(log n) simultaneously live values instead of whatever the node
   // order of the input happened to imply, and a parent usually directly
   // follows its last operand (accumulator forwarding, no LDS round trip).
-  {
+  static const bool sched_on = [] {  // MGP_LOWER_SCHED=0 keeps input order (A/B studies)
+    const char *e = getenv("MGP_LOWER_SCHED");
+    return !(e && e[0] == '0');
+  }();
+  if (sched_on) {
     const uint32_t n0 = (uint32_t)S.ins.size();
     std::vector<uint32_t> need(n0, 1);
     auto kids = [&](uint32_t t, uint32_t out[3]) -> int {

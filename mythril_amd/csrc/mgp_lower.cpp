@@ -115,7 +115,7 @@ Lowered unsupported() {
 }
 
 Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *consts, uint64_t n_consts,
-                  uint32_t max_slots) {
+                  uint32_t max_slots, int sched) {
   if (n_nodes == 0) return unsupported();
   LowerState S;
   std::vector<Ref> val(n_nodes);
@@ -309,51 +309,97 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   }
 
   // ------------------------------------------- register-pressure scheduling
-  // Re-emit the live instructions in a depth-first post-order from the root,
-  // visiting the operand with the larger Sethi-Ullman need first.  Trees then
-  // need O(log n) simultaneously live values instead of whatever the node
-  // order of the input happened to imply, and a parent usually directly
-  // follows its last operand (accumulator forwarding, no LDS round trip).
-  static const bool sched_on = [] {  // MGP_LOWER_SCHED=0 keeps input order (A/B studies)
-    const char *e = getenv("MGP_LOWER_SCHED");
-    return !(e && e[0] == '0');
-  }();
-  if (sched_on) {
+  // sched 1: depth-first post-order from the root, operand with the larger
+  //          Sethi-Ullman need first (trees need O(log n) live values and a
+  //          parent usually follows its last operand: accumulator forwarding);
+  // sched 2: greedy list scheduling — among ready instructions take the one
+  //          that frees the most BV values (last use) minus the one it creates,
+  //          ties to the one reading the most recent result.
+  // The caller keeps whichever schedule needs the fewest LDS slots.
+  if (sched != 0) {
     const uint32_t n0 = (uint32_t)S.ins.size();
-    std::vector<uint32_t> need(n0, 1);
     auto kids = [&](uint32_t t, uint32_t out[3]) -> int {
       int k = 0;
       const VIns &I = S.ins[t];
       for (const Ref *r : {&I.a, &I.b, &I.c})
-        if (r->k == R_INS) out[k++] = r->idx;
+        if (r->k == R_INS) {
+          bool dup = false;
+          for (int j = 0; j < k; ++j) dup |= out[j] == r->idx;
+          if (!dup) out[k++] = r->idx;
+        }
       return k;
     };
-    for (uint32_t t = 0; t < n0; ++t) {
-      uint32_t ch[3];
-      const int k = kids(t, ch);
-      uint32_t nd[3] = {0, 0, 0};
-      for (int i = 0; i < k; ++i) nd[i] = need[ch[i]];
-      std::sort(nd, nd + k, [](uint32_t x, uint32_t y) { return x > y; });
-      uint32_t m = 1;
-      for (int i = 0; i < k; ++i) m = std::max(m, nd[i] + (uint32_t)i);
-      need[t] = m;
-    }
-    std::vector<uint8_t> state(n0, 0);  // 0 new, 1 expanded, 2 emitted
     std::vector<uint32_t> order;
     order.reserve(n0);
-    std::vector<uint32_t> stack;
-    if (root.k == R_INS) stack.push_back(root.idx);
-    while (!stack.empty()) {
-      const uint32_t t = stack.back();
-      if (state[t] == 2) { stack.pop_back(); continue; }
-      if (state[t] == 1) { state[t] = 2; order.push_back(t); stack.pop_back(); continue; }
-      state[t] = 1;
-      uint32_t ch[3];
-      const int k = kids(t, ch);
-      // push so that the operand with the larger need is evaluated first
-      std::sort(ch, ch + k, [&](uint32_t x, uint32_t y) { return need[x] < need[y]; });
-      for (int i = 0; i < k; ++i)
-        if (state[ch[i]] == 0) stack.push_back(ch[i]);
+    if (sched == 1) {
+      std::vector<uint32_t> need(n0, 1);
+      for (uint32_t t = 0; t < n0; ++t) {
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        uint32_t nd[3] = {0, 0, 0};
+        for (int i = 0; i < k; ++i) nd[i] = need[ch[i]];
+        std::sort(nd, nd + k, [](uint32_t x, uint32_t y) { return x > y; });
+        uint32_t m = 1;
+        for (int i = 0; i < k; ++i) m = std::max(m, nd[i] + (uint32_t)i);
+        need[t] = m;
+      }
+      std::vector<uint8_t> state(n0, 0);  // 0 new, 1 expanded, 2 emitted
+      std::vector<uint32_t> stack;
+      if (root.k == R_INS) stack.push_back(root.idx);
+      while (!stack.empty()) {
+        const uint32_t t = stack.back();
+        if (state[t] == 2) { stack.pop_back(); continue; }
+        if (state[t] == 1) { state[t] = 2; order.push_back(t); stack.pop_back(); continue; }
+        state[t] = 1;
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        std::sort(ch, ch + k, [&](uint32_t x, uint32_t y) { return need[x] < need[y]; });
+        for (int i = 0; i < k; ++i)
+          if (state[ch[i]] == 0) stack.push_back(ch[i]);
+      }
+    } else {
+      std::vector<uint32_t> uses(n0, 0), pending(n0, 0);
+      std::vector<std::vector<uint32_t>> users(n0);
+      for (uint32_t t = 0; t < n0; ++t) {
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        pending[t] = (uint32_t)k;
+        for (int i = 0; i < k; ++i) {
+          uses[ch[i]]++;
+          users[ch[i]].push_back(t);
+        }
+      }
+      std::vector<uint32_t> ready;
+      for (uint32_t t = 0; t < n0; ++t)
+        if (pending[t] == 0) ready.push_back(t);
+      int64_t last = -1;
+      while (!ready.empty()) {
+        size_t best = 0;
+        int best_score = -1000, best_recent = -1;
+        for (size_t r = 0; r < ready.size(); ++r) {
+          const uint32_t t = ready[r];
+          uint32_t ch[3];
+          const int k = kids(t, ch);
+          int score = 0, recent = 0;
+          for (int i = 0; i < k; ++i) {
+            if (!S.ins[ch[i]].is_bool && uses[ch[i]] == 1) score += 1;
+            if ((int64_t)ch[i] == last) recent = 1;
+          }
+          if (!S.ins[t].is_bool && !users[t].empty()) score -= 1;
+          if (score > best_score || (score == best_score && recent > best_recent)) {
+            best = r, best_score = score, best_recent = recent;
+          }
+        }
+        const uint32_t t = ready[best];
+        ready.erase(ready.begin() + (ptrdiff_t)best);
+        order.push_back(t);
+        last = t;
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        for (int i = 0; i < k; ++i) uses[ch[i]]--;
+        for (uint32_t u : users[t])
+          if (--pending[u] == 0) ready.push_back(u);
+      }
     }
     if (order.size() == n0) {
       std::vector<uint32_t> remap(n0);
@@ -505,6 +551,12 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
   if (!node_offsets || !out_prog_offsets || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
   std::vector<Lowered> res(n_states);
   int bad = 0;
+  // MGP_LOWER_SCHED (A/B studies): 0 input order, 2 DFS only, 3 greedy only;
+  // default 1 = the fewest-slot schedule of the three
+  static const int sched_mode = [] {
+    const char *e = getenv("MGP_LOWER_SCHED");
+    return (e && e[0] >= '0' && e[0] <= '3' && e[1] == 0) ? e[0] - '0' : 1;
+  }();
 #pragma omp parallel for schedule(dynamic, 256)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
@@ -514,7 +566,19 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
       bad = 1;
       continue;
     }
-    res[s] = lower_one(nodes + n0, n1 - n0, consts ? consts + c0 * 8u : nullptr, c1 - c0, max_slots);
+    // Three schedules (input order, Sethi-Ullman DFS, greedy list); keep the
+    // one needing the fewest LDS slots — occupancy is set by the slot count
+    // (bench A/B: the DFS order alone saves stores but costs slots, 5 % slower).
+    const uint32_t *cp = consts ? consts + c0 * 8u : nullptr;
+    Lowered a = lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, sched_mode == 0 ? 0 : (sched_mode == 1 ? 0 : sched_mode - 1));
+    if (sched_mode == 1) {
+      for (int alt = 1; alt <= 2; ++alt) {
+        Lowered b = lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, alt);
+        const bool a_ok = a.status == MGP_ST_OK, b_ok = b.status == MGP_ST_OK;
+        if (b_ok && (!a_ok || b.words[2] < a.words[2])) a = std::move(b);
+      }
+    }
+    res[s] = std::move(a);
   }
   if (bad) return MGP_E_ARG;
   uint64_t total = 0;

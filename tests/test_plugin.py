@@ -1,0 +1,180 @@
+"""The LASER plugin at the prune point (svm.py:220-264), on a stand-in LaserEVM.
+
+mythril is not importable here, so `FakeLaser` restates the reference's
+`exec` loop (svm.py:220-264: strategy iteration, execute_state, the
+`is_possible` filter, manage_cfg, work_list append, total_states) over
+JUMPI-like states: each executed state forks into two children that add
+`x_k == v` / `x_k != v` (instructions.py:1556-1562).  The fallback solver is a
+brute-force decision over a small domain built on the oracle (test
+infrastructure), so the reference (no plugin) and the plugin run must prune
+exactly the same states in the same order.
+"""
+import itertools
+
+import pytest
+
+from mythril_amd import dag as D
+from mythril_amd import plugin as P
+from mythril_amd import solver as SV
+from mythril_amd.smt import ULT, symbol_factory
+from oracle import bvsem as S
+
+BVV = symbol_factory.BitVecVal
+BVS = symbol_factory.BitVecSym
+
+
+class BruteBackend(SV.Backend):
+    """Decides small problems exactly: every var ranges over 0..3 (constraints pin the rest)."""
+
+    name = "brute"
+
+    def __init__(self):
+        self.calls = 0
+
+    def check(self, terms, timeout_ms, minimize=(), maximize=()):
+        self.calls += 1
+        st = D.build_state(list(terms))
+        for xs in itertools.product(range(4), repeat=len(st.vars)):
+            if S.eval_root(st.nodes, st.consts, list(xs)):
+                return SV.sat, SV.Model([{name: v for (name, _), v in zip(st.vars, xs)}])
+        return SV.unsat, None
+
+
+class WS:
+    def __init__(self, constraints):
+        self.constraints = constraints
+
+
+class GS:
+    def __init__(self, depth, constraints, tag):
+        self.depth = depth
+        self.world_state = WS(constraints)
+        self.tag = tag
+
+
+class BFS:
+    """strategy/basic.py BreadthFirstSearchStrategy: pop(0); empty -> StopIteration."""
+
+    def __init__(self, work_list):
+        self.work_list = work_list
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        try:
+            return self.work_list.pop(0)
+        except IndexError:
+            raise StopIteration
+
+
+X = [BVS(f"x{i}", 256) for i in range(4)]
+
+
+class FakeLaser:
+    def __init__(self, max_depth=4):
+        self.work_list = [GS(0, SV.Constraints([ULT(X[0], BVV(3, 256))]), "r")]
+        self.strategy = BFS(self.work_list)
+        self.total_states = 0
+        self.max_depth = max_depth
+        self.executed = []
+        self.cfg = []
+        self.create_timeout = None
+        self.execution_timeout = None
+
+    def execute_state(self, gs):
+        self.executed.append(gs.tag)
+        if gs.depth >= self.max_depth:
+            return [], "STOP"
+        k = gs.depth % 4
+        v = BVV(gs.depth % 3, 256)
+        a = gs.world_state.constraints.copy()
+        a.append(X[k] == v)
+        b = gs.world_state.constraints.copy()
+        b.append(X[k] != v)
+        if gs.depth == 2:  # an infeasible branch: contradicts the root constraint
+            a.append(X[0] == BVV(7, 256))
+        return [GS(gs.depth + 1, a, gs.tag + "a"), GS(gs.depth + 1, b, gs.tag + "b")], "JUMPI"
+
+    def manage_cfg(self, op, states):
+        self.cfg.append((op, [s.tag for s in states]))
+
+    # svm.py:220-264 (reference exec, no plugin)
+    def exec(self, create=False, track_gas=False):
+        final_states = []
+        for global_state in self.strategy:
+            try:
+                new_states, op_code = self.execute_state(global_state)
+            except NotImplementedError:
+                continue
+            new_states = [s for s in new_states if s.world_state.constraints.is_possible]
+            self.manage_cfg(op_code, new_states)
+            if new_states:
+                self.work_list += new_states
+            elif track_gas:
+                final_states.append(global_state)
+            self.total_states += len(new_states)
+        return final_states if track_gas else None
+
+
+@pytest.fixture()
+def brute(monkeypatch):
+    b = BruteBackend()
+    old = SV.set_backend(b)
+    SV.SolverStatistics().reset()
+    yield b
+    SV.set_backend(old)
+
+
+def _run(plugin=None, track_gas=True):
+    vm = FakeLaser()
+    if plugin is not None:
+        P.LaserPluginLoader(vm).load(plugin)
+    finals = vm.exec(track_gas=track_gas)
+    return vm, [g.tag for g in finals]
+
+
+@pytest.mark.parametrize("window", [1, 3, 16])
+def test_plugin_prunes_like_reference_cpu(brute, monkeypatch, window):
+    monkeypatch.setattr(SV, "prefilter", lambda: None)  # fallback only: no GPU in this container
+    ref_vm, ref_final = _run()
+    ref_calls = brute.calls
+    brute.calls = 0
+    plugin = P.PluginFactory.build_gpu_prefilter_plugin(window=window)
+    vm, final = _run(plugin)
+    assert vm.executed == ref_vm.executed
+    assert vm.cfg == ref_vm.cfg
+    assert final == ref_final
+    assert vm.total_states == ref_vm.total_states
+    assert brute.calls == ref_calls  # same queries, batched
+    assert plugin.states_checked == ref_calls
+    assert any(not states for _, states in ref_vm.cfg) or ref_vm.total_states < 2 ** 5
+
+
+def test_plugin_loader_contract():
+    vm = FakeLaser()
+    loader = P.LaserPluginLoader(vm)
+    p = P.GpuPrefilterPlugin()
+    assert not loader.is_enabled(p)
+    loader.load(p)
+    assert loader.is_enabled(p)
+    with pytest.raises(ValueError):
+        P.GpuPrefilterPlugin(window=0)
+    P.disable()
+    SV.enable_gpu(True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [1, 8])
+def test_plugin_prunes_like_reference_gpu(brute, mgp_ctx, window):
+    SV.enable_gpu(False)
+    ref_vm, ref_final = _run()
+    ref_calls = brute.calls
+    brute.calls = 0
+    SV.enable_gpu(True)
+    vm, final = _run(P.GpuPrefilterPlugin(window=window))
+    assert vm.executed == ref_vm.executed and vm.cfg == ref_vm.cfg and final == ref_final
+    # every feasible successor is proved by a GPU witness: only the infeasible ones reach the fallback
+    n_infeasible = sum(2 - len(states) for op, states in ref_vm.cfg if op == "JUMPI")
+    assert brute.calls == n_infeasible < ref_calls
+    assert SV.SolverStatistics().gpu_sat > 0

@@ -107,6 +107,15 @@ int mgp_eval_batch_dev(const uint32_t *d_prog_words,
                        const uint32_t *bucket_slots, uint32_t n_buckets,
                        void *stream);
 
+/* Evaluation engine of mgp_eval_batch / mgp_eval_batch_dev:
+ *   MGP_ENGINE_ASM  hand-written gfx950 interpreter (mgp_eval_gfx950), default
+ *   MGP_ENGINE_HIP  HIP C++ interpreter (independent second implementation)
+ * Sets the engine when `engine` is one of them; returns the current engine.
+ * Process-wide; MGP_ENGINE=hip|asm in the environment sets the initial value. */
+#define MGP_ENGINE_HIP 1
+#define MGP_ENGINE_ASM 2
+int mgp_set_eval_engine(int engine);
+
 /* Host-side launch plan: states grouped by the BV-slot count in their program
  * header.  Writes order_out[n_states], bounds_out[nb+1], slots_out[nb];
  * returns nb (<= max_buckets) or a negative error. */

@@ -83,6 +83,7 @@ def _bind(lib):
         "mgp_synth_generate": (ctypes.c_int, [_U64, _U64, _U32, _U32, _U32, _P, _P, _P, _P, _P, _P, _P]),
         "mgp_nominal_ops": (ctypes.c_int, [_P, _P, _U32, _P]),
         "mgp_probe_valu_dev": (ctypes.c_int, [_U32, _U32, _P, _P, _P]),
+        "mgp_set_eval_engine": (ctypes.c_int, [ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -128,7 +129,18 @@ EXPORTED_SYMBOLS = (
     "mgp_synth_generate",
     "mgp_nominal_ops",
     "mgp_probe_valu_dev",
+    "mgp_set_eval_engine",
 )
+
+ENGINE_HIP, ENGINE_ASM = 1, 2
+ENGINES = {"hip": ENGINE_HIP, "asm": ENGINE_ASM}
+
+
+def set_eval_engine(name: Optional[str] = None) -> str:
+    """Select the evaluation kernel ('asm' = hand-written gfx950 interpreter, default;
+    'hip' = HIP C++ interpreter); returns the engine in use."""
+    cur = lib().mgp_set_eval_engine(ENGINES[name] if name else 0)
+    return {v: k for k, v in ENGINES.items()}[cur]
 
 
 def _ptr(a: Optional[np.ndarray]):

@@ -1,0 +1,1099 @@
+#!/usr/bin/env python3
+"""Generator of mgp_eval_gfx950 — the hand-written gfx950 interpreter of the uop encoding.
+
+    python3 gen_eval_asm.py <out.s> <out_header.h>
+
+Design: one 64-lane wave per (state, 64-candidate chunk); the
+uop stream is wave-uniform and is read through the scalar cache one uop ahead;
+every uop is dispatched through a jump table (s_setpc_b64 into a table of
+s_branch stubs), so the kernel has no decode chain and no divergent branch.
+Handlers are straight-line gfx950 code on fixed registers:
+
+  VGPR  v0 lane, v1 lane*16 (LDS lane base), v2/v3 candidate byte offsets of
+        the two 16-B halves, v4-v7 scratch, vA=v[8:15], vB=v[16:23],
+        vC=v[24:31], T=v[32:63] (product / division temporaries)
+  SGPR  s[4:5] uop pointer, s[6:7] candidate base of the state, s8 bytes per
+        variable, s9 n_vars-1, s[10:11] jump table, s[14:15] constant pool,
+        s[16:19] current uop C, s[20:23] prefetched uop N, s[24:31] constant
+        operand, s[32:39] sign constant H, s[40:47] mask constant M,
+        s[48:55] temporaries, s[56:57] valid-lane mask, s[58:59] partial
+        result address, s60 first candidate of the chunk, s[62:63] 2^32 (f64),
+        s[64:101] 19 Bool slots as 64-bit lane masks (M0-relative s_movrels)
+
+Every handler writes 256-bit values in 8 x u32 limbs; carries go through VCC
+(v_add_co / v_addc_co), products through v_mad_u64_u32 (Comba columns),
+funnel shifts through v_alignbit_b32, division is Knuth's algorithm D with
+32-bit digits and a double-precision quotient estimate.  No MFMA: nothing
+here is a contraction.  No scalar memory writes anywhere (vector stores only).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+from mythril_amd import uop_spec as U  # noqa: E402
+
+KNAME = "mgp_eval_gfx950"
+VA, VB, VC, VT = 8, 16, 24, 32
+S_KB, S_KH, S_KM = 24, 32, 40
+
+
+def v(i):
+    return f"v{i}"
+
+
+def vr(i, n):
+    return f"v[{i}:{i + n - 1}]"
+
+
+def s(i):
+    return f"s{i}"
+
+
+def sr(i, n=2):
+    return f"s[{i}:{i + n - 1}]"
+
+
+class Asm:
+    def __init__(self):
+        self.lines = []
+        self.n = 0
+
+    def __call__(self, *ins):
+        for x in ins:
+            self.lines.append("  " + x)
+
+    def label(self, name):
+        self.lines.append(f"{name}:")
+
+    def fresh(self, stem):
+        self.n += 1
+        return f".L{stem}_{self.n}"
+
+    def comment(self, text):
+        self.lines.append(f"  // {text}")
+
+
+A = Asm()
+
+# ---------------------------------------------------------------- helpers
+
+
+def tail():
+    """Advance to the prefetched uop, prefetch the next one, dispatch."""
+    A("s_waitcnt lgkmcnt(0)",
+      "s_mov_b64 s[16:17], s[20:21]",
+      "s_mov_b64 s[18:19], s[22:23]",
+      "s_add_u32 s4, s4, 16",
+      "s_addc_u32 s5, s5, 0",
+      "s_load_dwordx4 s[20:23], s[4:5], 0x10",
+      "s_and_b32 s12, s16, 0x3fc",
+      "s_add_u32 s12, s10, s12",
+      "s_addc_u32 s13, s11, 0",
+      "s_setpc_b64 s[12:13]")
+
+
+def op_dispatch():
+    A("s_lshr_b32 s12, s16, 8",
+      "s_and_b32 s12, s12, 0x3fc",
+      "s_add_u32 s12, s10, s12",
+      "s_addc_u32 s13, s11, 0",
+      "s_setpc_b64 s[12:13]")
+
+
+def bool_read(field_sreg, shift, dst_pair):
+    """dst_pair <- Bool slot whose (index*2) is the 16-bit field of field_sreg at shift."""
+    if shift == 0:
+        A(f"s_and_b32 s48, {field_sreg}, 0xffff")
+    else:
+        A(f"s_lshr_b32 s48, {field_sreg}, 16")
+    A("s_mov_b32 m0, s48", "s_nop 0", f"s_movrels_b64 {sr(dst_pair)}, s[64:65]")
+
+
+def bool_write(src_pair):
+    A("s_lshr_b32 s48, s19, 16", "s_mov_b32 m0, s48", "s_nop 0", f"s_movreld_b64 s[64:65], {src_pair}")
+
+
+def copy8(dst, src):
+    for i in range(8):
+        A(f"v_mov_b32 {v(dst + i)}, {v(src + i)}")
+
+
+def sext_inplace(base):
+    """x = (x ^ H) - H, H = 2^(w-1) in s[32:39]: sign-extends a zero-extended w-bit value.
+    (gfx950 VOP2 carry ops read VCC over the constant bus, so H is copied to v[56:63] first.)"""
+    sext_to(base, base)
+
+
+def sext_to(dst, src):
+    for i in range(8):
+        A(f"v_mov_b32 {v(56 + i)}, {s(S_KH + i)}")
+    for i in range(8):
+        A(f"v_xor_b32 {v(dst + i)}, {v(56 + i)}, {v(src + i)}")
+    A(f"v_sub_co_u32 {v(dst)}, vcc, {v(dst)}, v56")
+    for i in range(1, 8):
+        A(f"v_subb_co_u32 {v(dst + i)}, vcc, {v(dst + i)}, {v(56 + i)}, vcc")
+
+
+def cneg(base, mvgpr, tmp):
+    """x = m ? -x : x with m a per-lane all-ones/zero mask in a VGPR."""
+    for i in range(8):
+        A(f"v_xor_b32 {v(base + i)}, {v(base + i)}, {v(mvgpr)}")
+    A(f"v_lshrrev_b32 {v(tmp)}, 31, {v(mvgpr)}",
+      f"v_add_co_u32 {v(base)}, vcc, {v(tmp)}, {v(base)}")
+    for i in range(1, 8):
+        A(f"v_addc_co_u32 {v(base + i)}, vcc, 0, {v(base + i)}, vcc")
+
+
+def or_reduce(dst, regs):
+    """dst = OR of the regs (dst may be one of them)."""
+    regs = list(regs)
+    cur = regs[0]
+    rest = regs[1:]
+    while rest:
+        if len(rest) >= 2:
+            A(f"v_or3_b32 {v(dst)}, {v(cur)}, {v(rest[0])}, {v(rest[1])}")
+            rest = rest[2:]
+        else:
+            A(f"v_or_b32 {v(dst)}, {v(cur)}, {v(rest[0])}")
+            rest = []
+        cur = dst
+
+
+def shift_setup(vs, left):
+    """Per-lane shift amount vs (0..255) -> k masks s[48:49] (4), s[50:51] (2), s[52:53] (1),
+    v5 = bit shift b, v6 = 32-b, s[54:55] = (b == 0).  Uses v4, v7."""
+    A(f"v_lshrrev_b32 v4, 5, {v(vs)}",
+      f"v_and_b32 v5, 31, {v(vs)}",
+      "v_and_b32 v7, 4, v4", "v_cmp_ne_u32_e64 s[48:49], 0, v7",
+      "v_and_b32 v7, 2, v4", "v_cmp_ne_u32_e64 s[50:51], 0, v7",
+      "v_and_b32 v7, 1, v4", "v_cmp_ne_u32_e64 s[52:53], 0, v7")
+    if left:
+        A("v_sub_u32 v6, 32, v5", "v_cmp_eq_u32_e64 s[54:55], 0, v5")
+
+
+def shl_var(regs, nz):
+    """In-place per-lane left shift of the limb list `regs` (low first) after shift_setup(left).
+    nz = number of low limbs that may be non-zero on entry (the rest are zero)."""
+    n = len(regs)
+    for L, m in ((4, "s[48:49]"), (2, "s[50:51]"), (1, "s[52:53]")):
+        new_nz = min(n, nz + L)
+        for i in range(new_nz - 1, -1, -1):
+            src = i - L
+            if i >= nz:
+                if src >= 0:
+                    A(f"v_cndmask_b32_e64 {v(regs[i])}, 0, {v(regs[src])}, {m}")
+            elif src < 0:
+                A(f"v_cndmask_b32_e64 {v(regs[i])}, {v(regs[i])}, 0, {m}")
+            else:
+                A(f"v_cndmask_b32_e64 {v(regs[i])}, {v(regs[i])}, {v(regs[src])}, {m}")
+        nz = new_nz
+    top = min(n - 1, nz)
+    for i in range(top, 0, -1):
+        A(f"v_alignbit_b32 v7, {v(regs[i])}, {v(regs[i - 1])}, v6",
+          f"v_cndmask_b32_e64 {v(regs[i])}, v7, {v(regs[i])}, s[54:55]")
+    A(f"v_lshlrev_b32 {v(regs[0])}, v5, {v(regs[0])}")
+
+
+def shr_var(regs, fill):
+    """In-place per-lane right shift after shift_setup(left=False); fill = '0' or a VGPR name."""
+    n = len(regs)
+    for L, m in ((4, "s[48:49]"), (2, "s[50:51]"), (1, "s[52:53]")):
+        for i in range(n):
+            src = regs[i + L] if i + L < n else None
+            val = v(src) if src is not None else fill
+            A(f"v_cndmask_b32_e64 {v(regs[i])}, {v(regs[i])}, {val}, {m}")
+    for i in range(n):
+        hi = v(regs[i + 1]) if i + 1 < n else fill
+        A(f"v_alignbit_b32 {v(regs[i])}, {hi}, {v(regs[i])}, v5")
+
+
+def amount_from_vB():
+    """v4 <- per-lane shift amount from vB clamped to 0..255, v6 <- all-ones where it is >= 256."""
+    A(f"v_lshrrev_b32 v7, 8, {v(VB)}")
+    or_reduce(4, [7, VB + 1, VB + 2, VB + 3, VB + 4, VB + 5, VB + 6, VB + 7])
+    A("v_cmp_ne_u32_e64 s[48:49], 0, v4",
+      "v_cndmask_b32_e64 v6, 0, -1, s[48:49]",
+      f"v_and_b32 v4, 0xff, {v(VB)}")
+
+
+# ---------------------------------------------------------------- handlers
+
+HBODY = {}
+
+
+def handler(name):
+    def deco(fn):
+        HBODY[name] = fn
+        return fn
+    return deco
+
+
+def wait_operands():
+    A("s_waitcnt vmcnt(0) lgkmcnt(0)")
+
+
+def bv_epilogue():
+    lm, ls = A.fresh("nomask"), A.fresh("nostore")
+    A("s_bitcmp1_b32 s16, 19", f"s_cbranch_scc0 {lm}")
+    for i in range(8):
+        A(f"v_and_b32 {v(VA + i)}, {s(S_KM + i)}, {v(VA + i)}")
+    A.label(lm)
+    A("s_bitcmp1_b32 s16, 18", f"s_cbranch_scc0 {ls}",
+      "s_and_b32 s48, s18, 0xffff",
+      "v_add_u32 v4, s48, v1",
+      f"ds_write_b128 v4, {vr(VA, 4)}",
+      f"ds_write_b128 v4, {vr(VA + 4, 4)} offset:1024")
+    A.label(ls)
+    tail()
+
+
+def cmp_epilogue():
+    li = A.fresh("noinv")
+    A("s_bitcmp1_b32 s16, 21", f"s_cbranch_scc0 {li}", "s_not_b64 vcc, vcc")
+    A.label(li)
+    bool_write("vcc")
+    tail()
+
+
+def write_partial_and_end(value_sreg):
+    A("s_mov_b64 exec, 1",
+      f"v_mov_b32 v4, {value_sreg}",
+      "v_mov_b32 v5, 0",
+      "global_store_dword v5, v4, s[58:59]",
+      "s_endpgm")
+
+
+@handler("INVALID")
+def h_invalid():
+    A("s_waitcnt vmcnt(0) lgkmcnt(0)", "s_mov_b32 s48, -2")
+    write_partial_and_end("s48")
+
+
+def fetch_one(kind, dst, which):
+    """Issue the fetch of operand A (which='A', w1[15:0]) or B (w1[31:16]) into dst."""
+    sp = "s51" if which == "A" else "s50"
+    pr = "s[54:55]" if which == "A" else "s[52:53]"
+    vaddr = "v5" if which == "A" else "v4"
+    get = (f"s_and_b32 {sp}, s17, 0xffff" if which == "A" else f"s_lshr_b32 {sp}, s17, 16")
+    if kind == "acc":
+        if which == "B":
+            copy8(dst, VA)
+        return
+    A(get)
+    if kind == "slot":
+        A(f"v_add_u32 {vaddr}, {sp}, v1",
+          f"ds_read_b128 {vr(dst, 4)}, {vaddr}",
+          f"ds_read_b128 {vr(dst + 4, 4)}, {vaddr} offset:1024")
+    elif kind == "var":
+        lo = 54 if which == "A" else 52
+        A(f"s_min_u32 {sp}, {sp}, s9",
+          f"s_mul_i32 {sp}, {sp}, s8",
+          f"s_add_u32 s{lo}, s6, {sp}",
+          f"s_addc_u32 s{lo + 1}, s7, 0",
+          f"global_load_dwordx4 {vr(dst, 4)}, v2, {pr}",
+          f"global_load_dwordx4 {vr(dst + 4, 4)}, v3, {pr}")
+    else:  # const
+        A(f"s_load_dwordx8 s[24:31], s[14:15], {sp}", "s_waitcnt lgkmcnt(0)")
+        for i in range(8):
+            A(f"v_mov_b32 {v(dst + i)}, {s(S_KB + i)}")
+
+
+def make_fetch(name):
+    _, ka, kb, tgt = name.split("_")
+
+    def body():
+        l1, l2 = A.fresh("nokm"), A.fresh("nokh")
+        A("s_bitcmp1_b32 s16, 19", f"s_cbranch_scc0 {l1}",
+          "s_lshr_b32 s48, s18, 16", "s_load_dwordx8 s[40:47], s[14:15], s48")
+        A.label(l1)
+        A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {l2}",
+          "s_and_b32 s49, s19, 0xffff", "s_load_dwordx8 s[32:39], s[14:15], s49")
+        A.label(l2)
+        if kb != "none":
+            fetch_one(kb, VB, "B")
+        fetch_one(ka, VA if tgt == "A" else VC, "A")
+        op_dispatch()
+    return body
+
+
+for _f in U.FETCH:
+    HBODY[_f] = make_fetch(_f)
+
+
+# ---- Bool ops
+@handler("RET")
+def h_ret():
+    A("s_waitcnt vmcnt(0)")
+    bool_read("s17", 0, 50)
+    A("s_and_b64 s[50:51], s[50:51], s[56:57]",
+      "s_ff1_i32_b64 s52, s[50:51]",
+      "s_add_u32 s53, s60, s52",
+      "s_cmp_lt_i32 s52, 0",
+      "s_cselect_b32 s53, 0x7fffffff, s53")
+    write_partial_and_end("s53")
+
+
+def bool_binop(name, instr):
+    @handler(name)
+    def _():
+        bool_read("s17", 0, 50)
+        bool_read("s17", 16, 52)
+        A(f"{instr} s[50:51], s[50:51], s[52:53]")
+        bool_write("s[50:51]")
+        tail()
+
+
+bool_binop("BAND", "s_and_b64")
+bool_binop("BOR", "s_or_b64")
+bool_binop("BXOR", "s_xor_b64")
+bool_binop("BEQ", "s_xnor_b64")
+
+
+@handler("BNOT")
+def h_bnot():
+    bool_read("s17", 0, 50)
+    A("s_not_b64 s[50:51], s[50:51]")
+    bool_write("s[50:51]")
+    tail()
+
+
+@handler("BITE")
+def h_bite():
+    bool_read("s17", 0, 50)
+    bool_read("s17", 16, 52)
+    bool_read("s18", 0, 54)
+    A("s_and_b64 s[52:53], s[50:51], s[52:53]",
+      "s_andn2_b64 s[54:55], s[54:55], s[50:51]",
+      "s_or_b64 s[50:51], s[52:53], s[54:55]")
+    bool_write("s[50:51]")
+    tail()
+
+
+# ---- BV binary
+def bin_limbs(name, first, rest):
+    @handler(name)
+    def _():
+        wait_operands()
+        A(first.format(d=v(VA), a=v(VA), b=v(VB)))
+        for i in range(1, 8):
+            A(rest.format(d=v(VA + i), a=v(VA + i), b=v(VB + i)))
+        bv_epilogue()
+
+
+bin_limbs("ADD", "v_add_co_u32 {d}, vcc, {a}, {b}", "v_addc_co_u32 {d}, vcc, {a}, {b}, vcc")
+bin_limbs("SUB", "v_sub_co_u32 {d}, vcc, {a}, {b}", "v_subb_co_u32 {d}, vcc, {a}, {b}, vcc")
+bin_limbs("AND", "v_and_b32 {d}, {a}, {b}", "v_and_b32 {d}, {a}, {b}")
+bin_limbs("OR", "v_or_b32 {d}, {a}, {b}", "v_or_b32 {d}, {a}, {b}")
+bin_limbs("XOR", "v_xor_b32 {d}, {a}, {b}", "v_xor_b32 {d}, {a}, {b}")
+
+
+def mul_low(xa, yb, out):
+    """out[0..7] = low 256 bits of X*Y (Comba columns, v[4:5] + v6 accumulator)."""
+    A("v_mov_b32 v6, 0")
+    for k in range(8):
+        pairs = [(i, k - i) for i in range(k + 1)]
+        for n, (i, j) in enumerate(pairs):
+            src2 = "0" if (k == 0 and n == 0) else "v[4:5]"
+            A(f"v_mad_u64_u32 v[4:5], s[48:49], {v(xa + i)}, {v(yb + j)}, {src2}")
+            if k < 7 and not (k == 0 and n == 0):
+                A("v_addc_co_u32 v6, s[50:51], v6, 0, s[48:49]")
+        A(f"v_mov_b32 {v(out + k)}, v4")
+        if k < 7:
+            A("v_mov_b32 v4, v5", "v_mov_b32 v5, v6", "v_mov_b32 v6, 0")
+
+
+def mul_full(xa, yb, out):
+    """out[0..15] = X*Y (512 bits)."""
+    A("v_mov_b32 v4, 0", "v_mov_b32 v5, 0", "v_mov_b32 v6, 0")
+    for k in range(15):
+        for i in range(max(0, k - 7), min(k, 7) + 1):
+            j = k - i
+            A(f"v_mad_u64_u32 v[4:5], s[48:49], {v(xa + i)}, {v(yb + j)}, v[4:5]",
+              "v_addc_co_u32 v6, s[50:51], v6, 0, s[48:49]")
+        A(f"v_mov_b32 {v(out + k)}, v4", "v_mov_b32 v4, v5", "v_mov_b32 v5, v6", "v_mov_b32 v6, 0")
+    A(f"v_mov_b32 {v(out + 15)}, v4")
+
+
+@handler("MUL")
+def h_mul():
+    wait_operands()
+    mul_low(VA, VB, VT)
+    copy8(VA, VT)
+    bv_epilogue()
+
+
+@handler("NOT")
+def h_not():
+    wait_operands()
+    for i in range(8):
+        A(f"v_not_b32 {v(VA + i)}, {v(VA + i)}")
+    bv_epilogue()
+
+
+@handler("NEG")
+def h_neg():
+    wait_operands()
+    A(f"v_sub_co_u32 {v(VA)}, vcc, 0, {v(VA)}")
+    for i in range(1, 8):
+        A(f"v_subb_co_u32 {v(VA + i)}, vcc, 0, {v(VA + i)}, vcc")
+    bv_epilogue()
+
+
+@handler("MOV")
+def h_mov():
+    wait_operands()
+    bv_epilogue()
+
+
+@handler("SEXT")
+def h_sext():
+    wait_operands()
+    sext_inplace(VA)
+    bv_epilogue()
+
+
+def maybe_sext_A():
+    l = A.fresh("nosx")
+    A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {l}")
+    sext_inplace(VA)
+    A.label(l)
+
+
+@handler("SHL")
+def h_shl():
+    wait_operands()
+    amount_from_vB()
+    A("v_mov_b32 v26, v6", "v_mov_b32 v27, v4")   # vC is free in BV handlers
+    shift_setup(27, left=True)
+    shl_var(list(range(VA, VA + 8)), 8)
+    A("v_cmp_ne_u32_e64 s[48:49], 0, v26")
+    for i in range(8):
+        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, 0, s[48:49]")
+    bv_epilogue()
+
+
+def h_shr(arith):
+    def _():
+        wait_operands()
+        if arith:
+            maybe_sext_A()
+        amount_from_vB()
+        A("v_mov_b32 v26, v6", "v_mov_b32 v27, v4")
+        if arith:
+            A(f"v_ashrrev_i32 v28, 31, {v(VA + 7)}")
+            fill = "v28"
+        else:
+            fill = "0"
+        shift_setup(27, left=False)
+        shr_var(list(range(VA, VA + 8)), fill)
+        A("v_cmp_ne_u32_e64 s[48:49], 0, v26")
+        for i in range(8):
+            A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {fill}, s[48:49]")
+        bv_epilogue()
+    return _
+
+
+HBODY["LSHR"] = h_shr(False)
+HBODY["ASHR"] = h_shr(True)
+
+
+def uniform_b():
+    A(f"s_bfe_u32 s48, s16, {(5 << 16) | U.SHIFT_B_POS:#x}")
+
+
+def shli_body(k, regs_base=VA):
+    """vA <<= 32k + b (b in s48, uniform)."""
+    if k >= 8:
+        for i in range(8):
+            A(f"v_mov_b32 {v(regs_base + i)}, 0")
+        return
+    lb0, ldone = A.fresh("b0"), A.fresh("shldone")
+    A("s_cmp_eq_u32 s48, 0", f"s_cbranch_scc1 {lb0}", "s_sub_u32 s49, 32, s48")
+    for i in range(7, -1, -1):
+        src = i - k
+        if src < 0:
+            A(f"v_mov_b32 {v(regs_base + i)}, 0")
+        elif src == 0:
+            A(f"v_alignbit_b32 {v(regs_base + i)}, {v(regs_base + src)}, 0, s49")
+        else:
+            A(f"v_alignbit_b32 {v(regs_base + i)}, {v(regs_base + src)}, {v(regs_base + src - 1)}, s49")
+    A(f"s_branch {ldone}")
+    A.label(lb0)
+    for i in range(7, -1, -1):
+        src = i - k
+        if src < 0:
+            A(f"v_mov_b32 {v(regs_base + i)}, 0")
+        elif k:
+            A(f"v_mov_b32 {v(regs_base + i)}, {v(regs_base + src)}")
+    A.label(ldone)
+
+
+def shri_body(k, fill):
+    for i in range(8):
+        lo, hi = i + k, i + k + 1
+        if lo >= 8:
+            A(f"v_mov_b32 {v(VA + i)}, {fill}")
+        else:
+            hv = v(VA + hi) if hi < 8 else fill
+            A(f"v_alignbit_b32 {v(VA + i)}, {hv}, {v(VA + lo)}, s48")
+
+
+def make_shli(k):
+    def _():
+        wait_operands()
+        uniform_b()
+        shli_body(k)
+        bv_epilogue()
+    return _
+
+
+def make_lshri(k):
+    def _():
+        wait_operands()
+        uniform_b()
+        shri_body(k, "0")
+        bv_epilogue()
+    return _
+
+
+def make_ashri(k):
+    def _():
+        wait_operands()
+        maybe_sext_A()
+        uniform_b()
+        A(f"v_ashrrev_i32 v4, 31, {v(VA + 7)}")
+        shri_body(k, "v4")
+        bv_epilogue()
+    return _
+
+
+def make_concat(k):
+    def _():
+        wait_operands()
+        uniform_b()
+        shli_body(k)
+        for i in range(8):
+            A(f"v_or_b32 {v(VA + i)}, {v(VA + i)}, {v(VB + i)}")
+        bv_epilogue()
+    return _
+
+
+for _k in range(9):
+    HBODY[f"SHLI{_k}"] = make_shli(_k)
+    HBODY[f"LSHRI{_k}"] = make_lshri(_k)
+    HBODY[f"ASHRI{_k}"] = make_ashri(_k)
+for _k in range(8):
+    HBODY[f"CONCAT{_k}"] = make_concat(_k)
+
+
+@handler("ITE")
+def h_ite():
+    wait_operands()
+    bool_read("s19", 16, 50)
+    for i in range(8):
+        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VB + i)}, {v(VA + i)}, s[50:51]")
+    bv_epilogue()
+
+
+# ---- compares (result -> vcc -> Bool slot)
+def ult_chain(x, y, tmp=VT):
+    A(f"v_sub_co_u32 {v(tmp)}, vcc, {v(x)}, {v(y)}")
+    for i in range(1, 8):
+        A(f"v_subb_co_u32 {v(tmp)}, vcc, {v(x + i)}, {v(y + i)}, vcc")
+
+
+def slt_chain(x, y):
+    A(f"v_xor_b32 v4, 0x80000000, {v(x + 7)}", f"v_xor_b32 v5, 0x80000000, {v(y + 7)}")
+    A(f"v_sub_co_u32 {v(VT)}, vcc, {v(x)}, {v(y)}")
+    for i in range(1, 7):
+        A(f"v_subb_co_u32 {v(VT)}, vcc, {v(x + i)}, {v(y + i)}, vcc")
+    A(f"v_subb_co_u32 {v(VT)}, vcc, v4, v5, vcc")
+
+
+def make_cmp(base, xreg):
+    def _():
+        wait_operands()
+        X, Y = xreg, VB
+        if base == "EQ":
+            for i in range(8):
+                A(f"v_xor_b32 {v(VT + i)}, {v(X + i)}, {v(Y + i)}")
+            or_reduce(VT, range(VT, VT + 8))
+            A(f"v_cmp_eq_u32 vcc, 0, {v(VT)}")
+        elif base in ("ULT", "UGT"):
+            x, y = (X, Y) if base == "ULT" else (Y, X)
+            ult_chain(x, y)
+        elif base in ("SLT", "SGT"):
+            lsx, ldone = A.fresh("sx"), A.fresh("cmpdone")
+            A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc1 {lsx}")
+            x, y = (X, Y) if base == "SLT" else (Y, X)
+            slt_chain(x, y)
+            A(f"s_branch {ldone}")
+            A.label(lsx)
+            sext_to(40, X)
+            sext_to(48, Y)
+            x, y = (40, 48) if base == "SLT" else (48, 40)
+            slt_chain(x, y)
+            A.label(ldone)
+        elif base == "UADDNO256":
+            A(f"v_add_co_u32 {v(VT)}, vcc, {v(X)}, {v(Y)}")
+            for i in range(1, 8):
+                A(f"v_addc_co_u32 {v(VT)}, vcc, {v(X + i)}, {v(Y + i)}, vcc")
+        elif base == "UADDNOW":
+            A(f"v_add_co_u32 {v(VT)}, vcc, {v(X)}, {v(Y)}")
+            for i in range(1, 8):
+                A(f"v_addc_co_u32 {v(VT + i)}, vcc, {v(X + i)}, {v(Y + i)}, vcc")
+            # raw = M < sum
+            for i in range(8):
+                A(f"v_mov_b32 {v(40 + i)}, {s(S_KM + i)}")
+            A(f"v_sub_co_u32 v4, vcc, v40, {v(VT)}")
+            for i in range(1, 8):
+                A(f"v_subb_co_u32 v4, vcc, {v(40 + i)}, {v(VT + i)}, vcc")
+        elif base in ("UMULNO256", "UMULNOW"):
+            mul_full(X, Y, VT)
+            or_reduce(VT + 8, range(VT + 8, VT + 16))
+            A(f"v_cmp_ne_u32 vcc, 0, {v(VT + 8)}")
+            if base == "UMULNOW":
+                A("s_mov_b64 s[52:53], vcc")
+                for i in range(8):
+                    A(f"v_mov_b32 {v(48 + i)}, {s(S_KM + i)}")
+                A(f"v_sub_co_u32 v4, vcc, v48, {v(VT)}")
+                for i in range(1, 8):
+                    A(f"v_subb_co_u32 v4, vcc, {v(48 + i)}, {v(VT + i)}, vcc")
+                A("s_or_b64 vcc, vcc, s[52:53]")
+        cmp_epilogue()
+    return _
+
+
+for _c in U.CMPS:
+    HBODY[f"{_c}_RA"] = make_cmp(_c, VA)
+    HBODY[f"{_c}_RC"] = make_cmp(_c, VC)
+
+
+# ---- division (Knuth D, 32-bit digits)
+UQ = 32          # u[0..15] = v[32:47]; q digit J is stored into u[J+8]
+VN = 48          # normalised divisor v[48:55]
+
+
+def u(i):
+    return v(UQ + i)
+
+
+def vn(i):
+    return v(VN + i)
+
+
+def bitlen_chain(base, out):
+    """out = bit length of the 256-bit value at base (garbage when zero); v60/v61/v62 scratch.
+    Returns with s[48:49] = (value != 0)."""
+    A("v_mov_b32 v60, 0", f"v_mov_b32 v61, {v(base)}")
+    for i in range(1, 8):
+        A(f"v_cmp_ne_u32 vcc, 0, {v(base + i)}",
+          f"v_cndmask_b32_e64 v60, v60, {i}, vcc",
+          f"v_cndmask_b32 v61, v61, {v(base + i)}, vcc")
+    A("v_ffbh_u32 v62, v61",
+      "v_lshlrev_b32 v60, 5, v60",
+      "v_add_u32 v60, 32, v60",
+      f"v_sub_u32 {v(out)}, v60, v62",
+      "v_cmp_ne_u32_e64 s[48:49], 0, v61")
+
+
+def knuth_digit(J):
+    # estimate qhat from (u[J+8]:u[J+7]) / vn7 in double precision
+    A(f"v_cvt_f64_u32 v[30:31], {u(J + 8)}",
+      f"v_cvt_f64_u32 v[4:5], {u(J + 7)}",
+      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",
+      "v_mul_f64 v[30:31], v[30:31], v[28:29]",
+      "v_cvt_u32_f64 v60, v[30:31]")
+    # r = num - qhat*vn7 ; fix qhat by one each way (exact floor, capped at 2^32-1)
+    A(f"v_mad_u64_u32 v[56:57], s[48:49], v60, {vn(7)}, 0",
+      f"v_sub_co_u32 v62, vcc, {u(J + 7)}, v56",
+      f"v_subb_co_u32 v63, vcc, {u(J + 8)}, v57, vcc",
+      "v_subb_co_u32 v60, s[48:49], v60, 0, vcc",
+      f"v_cndmask_b32_e64 v61, 0, {vn(7)}, vcc",
+      "v_add_co_u32 v62, s[48:49], v62, v61",
+      "v_addc_co_u32 v63, s[48:49], v63, 0, s[48:49]",
+      "v_cmp_ne_u32_e64 s[48:49], 0, v63",
+      f"v_cmp_ge_u32_e64 s[50:51], v62, {vn(7)}",
+      "s_or_b64 s[48:49], s[48:49], s[50:51]",
+      "v_cmp_ne_u32_e64 s[50:51], -1, v60",
+      "s_and_b64 vcc, s[48:49], s[50:51]",
+      "v_addc_co_u32 v60, s[48:49], v60, 0, vcc",
+      f"v_cndmask_b32_e64 v61, 0, {vn(7)}, vcc",
+      "v_sub_co_u32 v62, s[48:49], v62, v61",
+      "v_subb_co_u32 v63, s[48:49], v63, 0, s[48:49]")
+    # Knuth D3: while rhat < 2^32 and qhat*vn6 > (rhat:u[J+6]): qhat--, rhat += vn7 (twice)
+    for _ in range(2):
+        A(f"v_mad_u64_u32 v[56:57], s[48:49], v60, {vn(6)}, 0",
+          f"v_mov_b32 v58, {u(J + 6)}",
+          "v_mov_b32 v59, v62",
+          "v_cmp_gt_u64_e64 s[48:49], v[56:57], v[58:59]",
+          "v_cmp_eq_u32_e64 s[50:51], 0, v63",
+          "s_and_b64 vcc, s[48:49], s[50:51]",
+          "v_subb_co_u32 v60, s[48:49], v60, 0, vcc",
+          f"v_cndmask_b32_e64 v61, 0, {vn(7)}, vcc",
+          "v_add_co_u32 v62, s[48:49], v62, v61",
+          "v_addc_co_u32 v63, s[48:49], v63, 0, s[48:49]")
+    # u[J..J+8] -= qhat * vn
+    A("v_mov_b32 v58, 0", "v_mov_b32 v59, 0")
+    for i in range(8):
+        A(f"v_mad_u64_u32 v[56:57], s[48:49], v60, {vn(i)}, v[58:59]")
+        if i == 0:
+            A(f"v_sub_co_u32 {u(J)}, vcc, {u(J)}, v56")
+        else:
+            A(f"v_subb_co_u32 {u(J + i)}, vcc, {u(J + i)}, v56, vcc")
+        A("v_mov_b32 v58, v57")
+    A(f"v_subb_co_u32 {u(J + 8)}, vcc, {u(J + 8)}, v58, vcc")
+    lno = A.fresh("noaddback")
+    A("s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lno}",
+      "s_mov_b64 s[50:51], vcc",
+      "v_subb_co_u32 v60, s[48:49], v60, 0, s[50:51]")
+    for i in range(8):
+        A(f"v_cndmask_b32_e64 v61, 0, {vn(i)}, s[50:51]")
+        if i == 0:
+            A(f"v_add_co_u32 {u(J)}, vcc, v61, {u(J)}")
+        else:
+            A(f"v_addc_co_u32 {u(J + i)}, vcc, v61, {u(J + i)}, vcc")
+    A(f"v_addc_co_u32 {u(J + 8)}, vcc, 0, {u(J + 8)}, vcc")
+    A.label(lno)
+    A(f"v_mov_b32 {u(J + 8)}, v60")
+
+
+@handler("DIV")
+def h_div():
+    wait_operands()
+    maybe_sext_op = A.fresh("nosxd")
+    A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {maybe_sext_op}")
+    sext_inplace(VA)
+    sext_inplace(VB)
+    A.label(maybe_sext_op)
+    lus, lsd = A.fresh("udiv"), A.fresh("sdone")
+    A(f"s_bfe_u32 s61, s16, {(3 << 16) | U.DIVOP_POS:#x}",
+      "s_cmp_lt_u32 s61, 2", f"s_cbranch_scc1 {lus}",
+      f"v_ashrrev_i32 v24, 31, {v(VA + 7)}",
+      f"v_ashrrev_i32 v25, 31, {v(VB + 7)}")
+    cneg(VA, 24, 61)
+    cneg(VB, 25, 61)
+    A(f"s_branch {lsd}")
+    A.label(lus)
+    A("v_mov_b32 v24, 0", "v_mov_b32 v25, 0")
+    A.label(lsd)
+    # lb = bitlen(b) -> v60 path into v26 temporarily; bnz -> s[26:27]
+    bitlen_chain(VB, 26)
+    A("s_mov_b64 s[26:27], s[48:49]")
+    bitlen_chain(VA, 27)
+    # a < b ?
+    ult_chain(VA, VB, tmp=62)
+    A("s_andn2_b64 s[24:25], s[26:27], vcc")          # divides = b != 0 && a >= b
+    A("v_sub_u32 v27, v27, v26",                       # d = la - lb
+      "v_cndmask_b32_e64 v27, -1, v27, s[24:25]",
+      "v_sub_u32 v26, 0x100, v26",                     # s = 256 - lb
+      "v_cndmask_b32_e64 v26, 0, v26, s[24:25]")
+    lpost = A.fresh("divpost")
+    A("s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {lpost}")
+    # normalise: vn = b << s, u = a << s (512 bits)
+    copy8(VN, VB)
+    copy8(UQ, VA)
+    for i in range(8, 16):
+        A(f"v_mov_b32 {u(i)}, 0")
+    shift_setup(26, left=True)
+    shl_var(list(range(VN, VN + 8)), 8)
+    shl_var(list(range(UQ, UQ + 16)), 8)
+    # 1 / vn7 in double precision (rcp + one Newton step)
+    A(f"v_cvt_f64_u32 v[30:31], {vn(7)}",
+      "v_rcp_f64 v[28:29], v[30:31]",
+      "s_nop 1",
+      "v_fma_f64 v[4:5], -v[30:31], v[28:29], 1.0",
+      "v_fma_f64 v[28:29], v[28:29], v[4:5], v[28:29]",
+      "s_mov_b32 s62, 0", "s_mov_b32 s63, 0x41f00000")
+    for J in range(7, -1, -1):
+        lskip = A.fresh(f"skipdig{J}")
+        A(f"v_cmp_lt_i32 vcc, {32 * J - 1}, v27",
+          "s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lskip}")
+        knuth_digit(J)
+        A.label(lskip)
+    # remainder = u[0..7] >> s  (only UREM/SREM/SMOD need it)
+    lnorem = A.fresh("norem")
+    A("s_cmp_eq_u32 s61, 0", f"s_cbranch_scc1 {lnorem}",
+      "s_cmp_eq_u32 s61, 2", f"s_cbranch_scc1 {lnorem}")
+    shift_setup(26, left=False)
+    shr_var(list(range(UQ, UQ + 8)), "0")
+    A.label(lnorem)
+    A.label(lpost)
+    # per lane: dividing -> (q = u[8..15], r = u[0..7]); else q = (b == 0 ? ~0 : 0), r = a
+    A("v_cndmask_b32_e64 v61, -1, 0, s[26:27]")
+    for i in range(8):
+        A(f"v_cndmask_b32_e64 {u(8 + i)}, v61, {u(8 + i)}, s[24:25]",
+          f"v_cndmask_b32_e64 {u(i)}, {v(VA + i)}, {u(i)}, s[24:25]")
+    # result by variant: 0 UDIV, 1 UREM, 2 SDIV, 3 SREM, 4 SMOD
+    l_r, l_sd, l_sr, l_end = A.fresh("rem"), A.fresh("sdiv"), A.fresh("srem"), A.fresh("divend")
+    A("s_cmp_eq_u32 s61, 1", f"s_cbranch_scc1 {l_r}",
+      "s_cmp_eq_u32 s61, 2", f"s_cbranch_scc1 {l_sd}",
+      "s_cmp_eq_u32 s61, 3", f"s_cbranch_scc1 {l_sr}",
+      "s_cmp_eq_u32 s61, 4", f"s_cbranch_scc1 {l_end}_smod")
+    copy8(VA, UQ + 8)                                 # UDIV
+    A(f"s_branch {l_end}")
+    A.label(l_r)
+    copy8(VA, UQ)
+    A(f"s_branch {l_end}")
+    A.label(l_sd)
+    copy8(VA, UQ + 8)
+    A("v_xor_b32 v24, v24, v25")
+    cneg(VA, 24, 61)
+    A(f"s_branch {l_end}")
+    A.label(l_sr)
+    copy8(VA, UQ)
+    cneg(VA, 24, 61)
+    A(f"s_branch {l_end}")
+    A.label(f"{l_end}_smod")
+    # r = |a| mod |b| in u[0..7], |b| in vB; sign follows the divisor
+    copy8(VA, UQ)
+    or_reduce(61, range(UQ, UQ + 8))
+    A("v_cmp_ne_u32_e64 s[48:49], 0, v61",             # r != 0
+      "v_cmp_ne_u32_e64 s[50:51], 0, v24",             # sa
+      "v_cmp_ne_u32_e64 s[52:53], 0, v25",             # sb
+      "s_and_b64 s[50:51], s[50:51], s[48:49]",
+      "s_and_b64 s[52:53], s[52:53], s[48:49]",
+      "s_andn2_b64 s[54:55], s[50:51], s[52:53]",       # sa & !sb & r != 0 -> |b| - r
+      "s_andn2_b64 s[48:49], s[52:53], s[50:51]",       # !sa & sb & r != 0 -> r - |b|
+      "s_and_b64 s[50:51], s[50:51], s[52:53]")         # sa & sb & r != 0 -> -r
+    A(f"v_sub_co_u32 {vn(0)}, vcc, {v(VB)}, {u(0)}")
+    for i in range(1, 8):
+        A(f"v_subb_co_u32 {vn(i)}, vcc, {v(VB + i)}, {u(i)}, vcc")
+    for i in range(8):
+        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {vn(i)}, s[54:55]")
+    A(f"v_sub_co_u32 {vn(0)}, vcc, {u(0)}, {v(VB)}")
+    for i in range(1, 8):
+        A(f"v_subb_co_u32 {vn(i)}, vcc, {u(i)}, {v(VB + i)}, vcc")
+    for i in range(8):
+        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {vn(i)}, s[48:49]")
+    A(f"v_sub_co_u32 {vn(0)}, vcc, 0, {u(0)}")
+    for i in range(1, 8):
+        A(f"v_subb_co_u32 {vn(i)}, vcc, 0, {u(i)}, vcc")
+    for i in range(8):
+        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {vn(i)}, s[50:51]")
+    A.label(l_end)
+    bv_epilogue()
+
+
+# ---------------------------------------------------------------- kernel
+
+PROLOGUE = """\
+  s_load_dwordx8 s[64:71], s[0:1], 0x0
+  s_load_dwordx8 s[72:79], s[0:1], 0x20
+  s_load_dword s80, s[0:1], 0x40
+  s_waitcnt lgkmcnt(0)
+  // s[64:65] words  s[66:67] offs  s[68:69] cands  s[70:71] partial  s[72:73] order
+  // s74 n_states  s75 n_cand  s76 n_vars  s77 n_chunks  s78 n_slots  s79 order_base  s80 grid x
+  // XCD-aware bijective remap of workgroup x (cdna_hip_programming.md §5 T1)
+  s_and_b32 s82, s2, 7
+  s_lshr_b32 s83, s80, 3
+  s_and_b32 s84, s80, 7
+  s_add_u32 s85, s83, 1
+  s_mul_i32 s86, s82, s85
+  s_mul_i32 s87, s84, s85
+  s_sub_u32 s88, s82, s84
+  s_mul_i32 s88, s88, s83
+  s_add_u32 s87, s87, s88
+  s_cmp_lt_u32 s82, s84
+  s_cselect_b32 s86, s86, s87
+  s_lshr_b32 s81, s2, 3
+  s_add_u32 s81, s81, s86
+  s_add_u32 s81, s81, s79
+  s_cmp_eq_u64 s[72:73], 0
+  s_cbranch_scc1 .Lno_order
+  s_lshl_b32 s82, s81, 2
+  s_add_u32 s82, s72, s82
+  s_addc_u32 s83, s73, 0
+  s_load_dword s81, s[82:83], 0x0
+  s_waitcnt lgkmcnt(0)
+.Lno_order:
+  s_cmp_ge_u32 s81, s74
+  s_cbranch_scc1 .Lexit
+  // partial entry: partial + (state * n_chunks + chunk) * 4
+  s_mul_i32 s82, s81, s77
+  s_add_u32 s82, s82, s3
+  s_mul_hi_u32 s83, s82, 4
+  s_lshl_b32 s82, s82, 2
+  s_add_u32 s58, s70, s82
+  s_addc_u32 s59, s71, s83
+  // program address = words + offs[state] * 4
+  s_lshl_b32 s82, s81, 3
+  s_mul_hi_u32 s83, s81, 8
+  s_add_u32 s82, s66, s82
+  s_addc_u32 s83, s67, s83
+  s_load_dwordx2 s[82:83], s[82:83], 0x0
+  s_waitcnt lgkmcnt(0)
+  s_lshl_b64 s[82:83], s[82:83], 2
+  s_add_u32 s84, s64, s82
+  s_addc_u32 s85, s65, s83
+  s_load_dwordx4 s[88:91], s[84:85], 0x0
+  s_waitcnt lgkmcnt(0)
+  // v1 header checks (same as the HIP kernel): status, slot budget of this bucket, variables
+  s_and_b32 s92, s91, 0xff
+  s_cmp_lg_u32 s92, 0
+  s_cbranch_scc1 .Lundec
+  s_cmp_gt_u32 s90, s78
+  s_cbranch_scc1 .Lundec
+  s_lshr_b32 s92, s91, 8
+  s_cmp_gt_u32 s92, s76
+  s_cbranch_scc1 .Lundec
+  // uop header at word align4(4 + 4*n_ins + 8*n_consts) + 4
+  s_lshl_b32 s92, s88, 2
+  s_lshl_b32 s93, s89, 3
+  s_add_u32 s92, s92, s93
+  s_add_u32 s92, s92, 7
+  s_and_b32 s92, s92, 0xfffffffc
+  s_add_u32 s92, s92, 4
+  s_lshl_b32 s92, s92, 2
+  s_add_u32 s84, s84, s92
+  s_addc_u32 s85, s85, 0
+  s_load_dwordx4 s[88:91], s[84:85], 0x0
+  s_waitcnt lgkmcnt(0)
+  s_cmp_lg_u32 s89, 0
+  s_cbranch_scc1 .Lundec
+  s_add_u32 s14, s84, s90
+  s_addc_u32 s15, s85, 0
+  s_add_u32 s4, s84, 16
+  s_addc_u32 s5, s85, 0
+  s_load_dwordx4 s[16:19], s[4:5], 0x0
+  s_load_dwordx4 s[20:23], s[4:5], 0x10
+  // candidates of this state: cands + state * n_vars * n_cand * 32, layout [var][half][cand] x 16 B
+  s_lshl_b32 s8, s75, 5
+  s_mul_i32 s92, s76, s8
+  s_mul_i32 s6, s81, s92
+  s_mul_hi_u32 s7, s81, s92
+  s_add_u32 s6, s68, s6
+  s_addc_u32 s7, s69, s7
+  s_sub_u32 s9, s76, 1
+  // lanes: candidate = chunk*64 + lane (clamped; lanes past n_cand are masked out of the result)
+  s_lshl_b32 s60, s3, 6
+  v_add_u32 v5, s60, v0
+  v_cmp_gt_u32_e64 s[56:57], s75, v5
+  s_sub_u32 s92, s75, 1
+  v_min_u32 v5, s92, v5
+  v_lshlrev_b32 v2, 4, v5
+  s_lshl_b32 s92, s75, 4
+  v_add_u32 v3, s92, v2
+  v_lshlrev_b32 v1, 4, v0
+  s_getpc_b64 s[10:11]
+.Lpc_base:
+  s_add_u32 s10, s10, .Ltab-.Lpc_base
+  s_addc_u32 s11, s11, 0
+  s_mov_b64 s[64:65], 0
+  s_mov_b64 s[66:67], -1
+  s_mov_b32 s62, 0
+  s_mov_b32 s63, 0x41f00000
+  s_waitcnt lgkmcnt(0)
+  s_and_b32 s12, s16, 0x3fc
+  s_add_u32 s12, s10, s12
+  s_addc_u32 s13, s11, 0
+  s_setpc_b64 s[12:13]
+.Lundec:
+  s_mov_b64 exec, 1
+  v_mov_b32 v4, -2
+  v_mov_b32 v5, 0
+  global_store_dword v5, v4, s[58:59]
+.Lexit:
+  s_endpgm
+"""
+
+KARGS = [("words", 8, "global_buffer"), ("offs", 8, "global_buffer"), ("cands", 8, "global_buffer"),
+         ("partial", 8, "global_buffer"), ("order", 8, "global_buffer"), ("n_states", 4, "by_value"),
+         ("n_cand", 4, "by_value"), ("n_vars", 4, "by_value"), ("n_chunks", 4, "by_value"),
+         ("n_slots", 4, "by_value"), ("order_base", 4, "by_value"), ("grid_x", 4, "by_value")]
+
+
+def metadata():
+    out = ["amdhsa.kernels:", "  - .args:"]
+    off = 0
+    for name, size, kind in KARGS:
+        out.append(f"      - .name: {name}")
+        if kind == "global_buffer":
+            out.append("        .address_space: global")
+        out += [f"        .offset: {off}", f"        .size: {size}", f"        .value_kind: {kind}"]
+        off += size
+    ksize = (off + 7) // 8 * 8
+    out += [
+        "    .group_segment_fixed_size: 0",
+        "    .kernarg_segment_align: 8",
+        f"    .kernarg_segment_size: {ksize}",
+        "    .max_flat_workgroup_size: 64",
+        f"    .name: {KNAME}",
+        "    .private_segment_fixed_size: 0",
+        "    .sgpr_count: 104",
+        f"    .symbol: {KNAME}.kd",
+        "    .vgpr_count: 64",
+        "    .wavefront_size: 64",
+        "amdhsa.target: amdgcn-amd-amdhsa--gfx950",
+        "amdhsa.version:", "  - 1", "  - 2",
+    ]
+    return "\n".join(out), ksize
+
+
+def generate() -> str:
+    body = Asm()
+    global A
+    A = body
+    A.lines.append(PROLOGUE)
+    A.lines.append(".Ltab:")
+    for name in U.HANDLERS:
+        A(f"s_branch .Lh_{name}")
+    for _ in range(256 - len(U.HANDLERS)):
+        A("s_branch .Lh_INVALID")
+    for name in U.HANDLERS:
+        A.lines.append(f".Lh_{name}:")
+        HBODY[name]()
+    md, ksize = metadata()
+    head = [
+        '.amdgcn_target "amdgcn-amd-amdhsa--gfx950"',
+        ".text",
+        f".globl {KNAME}",
+        ".p2align 8",
+        f".type {KNAME},@function",
+        f"{KNAME}:",
+    ]
+    tail_ = [
+        ".Lfunc_end:",
+        f".size {KNAME}, .Lfunc_end-{KNAME}",
+        "",
+        ".rodata",
+        ".p2align 6",
+        f".amdhsa_kernel {KNAME}",
+        "  .amdhsa_group_segment_fixed_size 0",
+        "  .amdhsa_private_segment_fixed_size 0",
+        f"  .amdhsa_kernarg_size {ksize}",
+        "  .amdhsa_user_sgpr_count 2",
+        "  .amdhsa_user_sgpr_kernarg_segment_ptr 1",
+        "  .amdhsa_system_sgpr_workgroup_id_x 1",
+        "  .amdhsa_system_sgpr_workgroup_id_y 1",
+        "  .amdhsa_system_vgpr_workitem_id 0",
+        "  .amdhsa_next_free_vgpr 64",
+        "  .amdhsa_next_free_sgpr 102",
+        "  .amdhsa_accum_offset 64",
+        "  .amdhsa_reserve_vcc 1",
+        "  .amdhsa_float_denorm_mode_32 3",
+        "  .amdhsa_float_denorm_mode_16_64 3",
+        ".end_amdhsa_kernel",
+        "",
+        ".amdgpu_metadata",
+        "---",
+        md,
+        "...",
+        ".end_amdgpu_metadata",
+    ]
+    return "\n".join(head + A.lines + tail_) + "\n"
+
+
+def main():
+    out_s, out_h = sys.argv[1], sys.argv[2]
+    src = generate()
+    with open(out_s, "w") as f:
+        f.write(f"// generated by gen_eval_asm.py — do not edit\n{src}")
+    with open(out_h, "w") as f:
+        f.write(U.c_header())
+
+
+if __name__ == "__main__":
+    main()

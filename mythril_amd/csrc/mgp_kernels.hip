@@ -23,7 +23,7 @@
 
 #include <type_traits>
 
-#include "../../include/mgp_ir.h"
+#include "../../include/mgp.h"
 #include "mgp_bv.h"
 
 #define MGP_WAVE 64
@@ -626,7 +626,28 @@ static uint32_t cpl_override() {
   return v;
 }
 
+extern "C" hipError_t mgp_asm_available(void);
+extern "C" hipError_t mgp_launch_eval_asm(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
+                                          const uint32_t *cands, uint32_t n_cand, uint32_t n_vars,
+                                          uint32_t n_slots, int32_t *partial, const uint32_t *order,
+                                          const uint32_t *bucket_bounds, const uint32_t *bucket_slots,
+                                          uint32_t n_buckets, uint32_t n_chunks, hipStream_t st);
+
+// Evaluation engine: MGP_ENGINE_ASM = the hand-written gfx950 interpreter
+// (mgp_eval_gfx950, default), MGP_ENGINE_HIP = the HIP C++ interpreter above
+// (kept as an independent second implementation; A/B and cross-checks).
+// MGP_ENGINE=hip|asm in the environment sets the initial choice.
+static int g_engine = [] {
+  const char *e = getenv("MGP_ENGINE");
+  return (e && e[0] == 'h') ? MGP_ENGINE_HIP : MGP_ENGINE_ASM;
+}();
+
 extern "C" {
+
+int mgp_set_eval_engine(int engine) {
+  if (engine == MGP_ENGINE_HIP || engine == MGP_ENGINE_ASM) g_engine = engine;
+  return g_engine;
+}
 
 hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
                            const uint32_t *cands, uint32_t n_cand, uint32_t n_vars, uint32_t n_slots,
@@ -634,13 +655,20 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
                            const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
                            hipStream_t st) {
   if (n_states == 0) return hipSuccess;
-  const uint32_t cpl = cpl_override() ? cpl_override() : 1u;  // CPL=2 measured slower (LDS occupancy halves)
-  const uint32_t n_chunks = (n_cand + MGP_WAVE * cpl - 1) / (MGP_WAVE * cpl);
-  hipError_t err = (cpl == 2u)
-                       ? launch_eval_cpl<2>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
-                                            bucket_bounds, bucket_slots, n_buckets, n_chunks, st)
-                       : launch_eval_cpl<1>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
-                                            bucket_bounds, bucket_slots, n_buckets, n_chunks, st);
+  uint32_t n_chunks;
+  hipError_t err;
+  if (g_engine == MGP_ENGINE_ASM) {
+    n_chunks = (n_cand + MGP_WAVE - 1) / MGP_WAVE;
+    err = mgp_launch_eval_asm(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
+                              bucket_bounds, bucket_slots, n_buckets, n_chunks, st);
+  } else {
+    const uint32_t cpl = cpl_override() ? cpl_override() : 1u;  // CPL=2 measured slower (LDS occupancy halves)
+    n_chunks = (n_cand + MGP_WAVE * cpl - 1) / (MGP_WAVE * cpl);
+    err = (cpl == 2u) ? launch_eval_cpl<2>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
+                                           bucket_bounds, bucket_slots, n_buckets, n_chunks, st)
+                      : launch_eval_cpl<1>(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
+                                           bucket_bounds, bucket_slots, n_buckets, n_chunks, st);
+  }
   if (err != hipSuccess) return err;
   hipLaunchKernelGGL(mgp_finalize_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, partial,
                      n_states, n_chunks, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars,

@@ -12,7 +12,9 @@
 //      with accumulator forwarding: an operand produced by the immediately
 //      preceding BV instruction is read from registers (ACC) and only values
 //      with a later use are stored;
-//   5. emit header + instructions + constant pool.
+//   5. emit header + instructions + constant pool;
+//   6. append the micro-op re-encoding for the gfx950 assembly interpreter
+//      (mgp_uop.cpp; layout in mythril_amd/uop_spec.py).
 // States are independent; the batch is lowered in parallel with OpenMP.
 #include <stdint.h>
 #include <stdlib.h>
@@ -23,6 +25,8 @@
 #include <vector>
 
 #include "../../include/mgp.h"
+
+int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out);  // mgp_uop.cpp
 
 namespace {
 
@@ -578,6 +582,15 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
         if (b_ok && (!a_ok || b.words[2] < a.words[2])) a = std::move(b);
       }
     }
+    // append the uop program of the gfx950 interpreter; a state it cannot run
+    // is made unsupported in both encodings so that both engines agree
+    std::vector<uint32_t> uops;
+    if (mgp_uop_translate(a.words.data(), uops) != 0) {
+      a = unsupported();
+      uops.clear();
+      mgp_uop_translate(a.words.data(), uops);
+    }
+    a.words.insert(a.words.end(), uops.begin(), uops.end());
     res[s] = std::move(a);
   }
   if (bad) return MGP_E_ARG;

@@ -1,0 +1,298 @@
+// mgp_uop.cpp — v1 bytecode -> micro-ops of the gfx950 assembly interpreter.
+//
+// mgp_lower produces, per state, the v1 program of include/mgp_ir.h (the
+// schedule, slot/Bool allocation and accumulator forwarding live there).  This
+// pass re-encodes it for mgp_eval_gfx950 (gen_eval_asm.py): one uop per v1
+// instruction, with everything the kernel would otherwise decode at run time
+// resolved here —
+//   * the operand kinds select a fetch handler (F_<kindA>_<kindB>_<target>),
+//     so the kernel never branches on operand kinds;
+//   * commutative ops / compares are swapped so the accumulator is operand A
+//     (a compare never overwrites the accumulator: a non-accumulator A goes to
+//     vC);
+//   * shifts by a constant become uniform-shift handlers (limb move + one
+//     v_alignbit per limb), EXTRACT is LSHRI + mask, CONCAT a fused
+//     shift-or;
+//   * narrow widths carry explicit MASK / SEXT flags whose constants
+//     (2^w - 1, 2^(w-1)) are appended to the state's constant pool;
+//   * LDS slot / pool / Bool operands are pre-scaled byte offsets.
+// Encoding: mythril_amd/uop_spec.py (mgp_uop.h is generated from it).
+#include <stdint.h>
+#include <string.h>
+
+#include <map>
+#include <vector>
+
+#include "../../include/mgp_ir.h"
+#include "mgp_uop.h"
+
+namespace {
+
+struct Opnd {
+  int kind;       // 0 acc, 1 slot, 2 var, 3 const, -1 none
+  uint32_t param;
+};
+
+constexpr int KACC = 0, KSLOT = 1, KVAR = 2, KCONST = 3, KNONE = -1;
+
+// fetch handler ids, in uop_spec.FETCH order: A-target block (4 x 5), then C-target (3 x 5)
+inline uint32_t fetch_id(int ka, int kb, bool to_c) {
+  const int kbi = kb + 1;  // none = 0
+  if (!to_c) return (uint32_t)(MGP_U_F_acc_none_A + ka * 5 + kbi);
+  return (uint32_t)(MGP_U_F_slot_none_C + (ka - 1) * 5 + kbi);
+}
+
+struct Translator {
+  const uint32_t *v1;
+  uint32_t n_ins, n_c;
+  std::vector<uint32_t> pool;        // 8 words per constant
+  std::map<uint32_t, uint32_t> mask_c, sign_c;  // width -> pool index
+  bool bad = false;
+
+  uint32_t add_const(const uint32_t w[8]) {
+    const uint32_t idx = (uint32_t)(pool.size() / 8);
+    pool.insert(pool.end(), w, w + 8);
+    return idx;
+  }
+  uint32_t mask_off(uint32_t width) {
+    auto it = mask_c.find(width);
+    if (it == mask_c.end()) {
+      uint32_t w[8];
+      for (int l = 0; l < 8; ++l) {
+        const int lo = 32 * l;
+        w[l] = (int)width >= lo + 32 ? 0xFFFFFFFFu : ((int)width <= lo ? 0u : ((1u << (width - lo)) - 1u));
+      }
+      it = mask_c.emplace(width, add_const(w)).first;
+    }
+    return pool_byte(it->second);
+  }
+  uint32_t sign_off(uint32_t width) {
+    auto it = sign_c.find(width);
+    if (it == sign_c.end()) {
+      uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      w[(width - 1) >> 5] = 1u << ((width - 1) & 31);
+      it = sign_c.emplace(width, add_const(w)).first;
+    }
+    return pool_byte(it->second);
+  }
+  uint32_t pool_byte(uint32_t idx) {
+    if (idx >= 2048u) bad = true;
+    return idx * 32u;
+  }
+  Opnd bv(uint32_t o) {
+    const uint32_t kind = o >> 14, idx = o & 0x3FFFu;
+    switch (kind) {
+      case MGP_K_ACC: return {KACC, 0};
+      case MGP_K_SLOT:
+        if (idx >= MGP_U_MAX_LDS_SLOTS) bad = true;
+        return {KSLOT, idx * MGP_U_SLOT_BYTES};
+      case MGP_K_CONST: return {KCONST, pool_byte(idx)};
+      default: return {KVAR, idx};
+    }
+  }
+  uint32_t boolslot(uint32_t b) {
+    if (b == MGP_BOOL_FALSE) return 0;
+    if (b == MGP_BOOL_TRUE) return 2;
+    const uint32_t s = b + 2;
+    if (s >= MGP_U_BOOL_SLOTS) bad = true;
+    return s * 2;
+  }
+  // value of a v1 constant operand (pool index), low limb + "any high bits"
+  void const_value(uint32_t o, uint32_t *lo, bool *big) {
+    const uint32_t idx = o & 0x3FFFu;
+    const uint32_t *c = &pool[(size_t)idx * 8];
+    *lo = c[0];
+    bool hi = false;
+    for (int l = 1; l < 8; ++l) hi |= c[l] != 0;
+    *big = hi || c[0] >= 256u;
+  }
+};
+
+inline uint32_t w0_of(uint32_t first, uint32_t op, uint32_t flags) { return (first << 2) | (op << 10) | flags; }
+
+}  // namespace
+
+// Appends the uop program of one v1 program to `out`.  Returns 0, or 1 when the
+// state does not fit the interpreter's limits (it is then marked undecided).
+int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
+  const size_t base = out.size();
+  out.resize(base + MGP_U_HDR_WORDS, 0u);
+  Translator T;
+  T.v1 = v1;
+  T.n_ins = v1[0];
+  T.n_c = v1[1];
+  const bool v1_ok = (v1[3] & 0xFFu) == MGP_ST_OK;
+  const uint32_t *ins = v1 + MGP_HDR_WORDS;
+  if (v1_ok) T.pool.assign(ins + (size_t)T.n_ins * MGP_INS_WORDS, ins + (size_t)T.n_ins * MGP_INS_WORDS + (size_t)T.n_c * 8);
+  std::vector<uint32_t> uops;
+  auto emit = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    uops.push_back(w0); uops.push_back(w1); uops.push_back(w2); uops.push_back(w3);
+  };
+
+  for (uint32_t pc = 0; v1_ok && pc < T.n_ins && !T.bad; ++pc) {
+    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
+    const uint32_t op = I[0] & 0xFFu, width = ((I[0] >> 8) & 0xFFu) + 1u, dst = (I[0] >> 16) & 0xFFu;
+    const bool store = ((I[0] >> 24) & MGP_INS_STORE) != 0;
+    const uint32_t oa = I[1] & 0xFFFFu, ob = I[1] >> 16, oc = I[2] & 0xFFFFu, imm = I[2] >> 16;
+    const bool narrow = width < 256u;
+
+    if (op == MGP_OP_RET) {
+      emit(w0_of(MGP_U_RET, MGP_U_RET, 0), T.boolslot(oa), 0, 0);
+      break;
+    }
+    if (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) {
+      static const uint32_t ids[] = {MGP_U_BAND, MGP_U_BOR, MGP_U_BXOR, MGP_U_BNOT, MGP_U_BITE, MGP_U_BEQ};
+      const uint32_t id = ids[op - MGP_OP_BAND];
+      emit(w0_of(id, id, 0), T.boolslot(oa) | (T.boolslot(ob) << 16), T.boolslot(oc), T.boolslot(dst) << 16);
+      continue;
+    }
+    if (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) {
+      Opnd a = T.bv(oa), b = T.bv(ob);
+      // base compare, invert, commutes-with-swap partner
+      uint32_t base;
+      bool inv = false;
+      switch (op) {
+        case MGP_OP_EQ: base = MGP_U_EQ_RA; break;
+        case MGP_OP_ULT: base = MGP_U_ULT_RA; break;
+        case MGP_OP_UGE: base = MGP_U_ULT_RA; inv = true; break;
+        case MGP_OP_UGT: base = MGP_U_UGT_RA; break;
+        case MGP_OP_ULE: base = MGP_U_UGT_RA; inv = true; break;
+        case MGP_OP_SLT: base = MGP_U_SLT_RA; break;
+        case MGP_OP_SGE: base = MGP_U_SLT_RA; inv = true; break;
+        case MGP_OP_SGT: base = MGP_U_SGT_RA; break;
+        case MGP_OP_SLE: base = MGP_U_SGT_RA; inv = true; break;
+        case MGP_OP_UADD_NOOVF: base = narrow ? MGP_U_UADDNOW_RA : MGP_U_UADDNO256_RA; inv = true; break;
+        case MGP_OP_UMUL_NOOVF: base = narrow ? MGP_U_UMULNOW_RA : MGP_U_UMULNO256_RA; inv = true; break;
+        default: base = MGP_U_ULT_RA; inv = true; break;  // USUB_NOUDF(a,b) = !(a < b)
+      }
+      if (b.kind == KACC && a.kind != KACC) {
+        std::swap(a, b);
+        if (base == MGP_U_ULT_RA) base = MGP_U_UGT_RA;
+        else if (base == MGP_U_UGT_RA) base = MGP_U_ULT_RA;
+        else if (base == MGP_U_SLT_RA) base = MGP_U_SGT_RA;
+        else if (base == MGP_U_SGT_RA) base = MGP_U_SLT_RA;
+      }
+      uint32_t flags = inv ? MGP_UF_INVERT : 0u, w2 = 0, w3 = T.boolslot(dst) << 16;
+      if (narrow && (base == MGP_U_SLT_RA || base == MGP_U_SGT_RA)) {
+        flags |= MGP_UF_SEXT;
+        w3 |= T.sign_off(width);
+      }
+      if (base == MGP_U_UADDNOW_RA || base == MGP_U_UMULNOW_RA) {
+        flags |= MGP_UF_MASK;
+        w2 |= T.mask_off(width) << 16;
+      }
+      const bool ra = a.kind == KACC;
+      const uint32_t opid = ra ? base : base + 1u;  // _RC follows _RA
+      const uint32_t first = fetch_id(a.kind, b.kind, !ra);
+      emit(w0_of(first, opid, flags), (ra ? 0u : a.param) | (b.param << 16), w2, w3);
+      continue;
+    }
+    // ---- BV-producing
+    uint32_t flags = 0, w2 = 0, w3 = 0, opid = 0;
+    Opnd a = {KNONE, 0}, b = {KNONE, 0};
+    bool need_mask = false;
+    switch (op) {
+      case MGP_OP_ADD: case MGP_OP_MUL: case MGP_OP_AND: case MGP_OP_OR: case MGP_OP_XOR: {
+        a = T.bv(oa); b = T.bv(ob);
+        if (b.kind == KACC && a.kind != KACC) std::swap(a, b);
+        opid = op == MGP_OP_ADD ? MGP_U_ADD : op == MGP_OP_MUL ? MGP_U_MUL : op == MGP_OP_AND ? MGP_U_AND
+             : op == MGP_OP_OR ? MGP_U_OR : MGP_U_XOR;
+        need_mask = narrow && (op == MGP_OP_ADD || op == MGP_OP_MUL);
+        break;
+      }
+      case MGP_OP_SUB:
+        a = T.bv(oa); b = T.bv(ob); opid = MGP_U_SUB; need_mask = narrow;
+        break;
+      case MGP_OP_SHL: case MGP_OP_LSHR: case MGP_OP_ASHR: {
+        a = T.bv(oa);
+        if ((ob >> 14) == MGP_K_CONST) {
+          uint32_t lo;
+          bool big;
+          T.const_value(ob, &lo, &big);
+          const uint32_t k = big ? 8u : lo >> 5, sb = big ? 0u : lo & 31u;
+          opid = (op == MGP_OP_SHL ? MGP_U_SHLI0 : op == MGP_OP_LSHR ? MGP_U_LSHRI0 : MGP_U_ASHRI0) + k;
+          flags |= sb << MGP_U_SHIFT_B_POS;
+        } else {
+          b = T.bv(ob);
+          opid = op == MGP_OP_SHL ? MGP_U_SHL : op == MGP_OP_LSHR ? MGP_U_LSHR : MGP_U_ASHR;
+        }
+        if (op == MGP_OP_ASHR && narrow) {
+          flags |= MGP_UF_SEXT;
+          w3 |= T.sign_off(width);
+        }
+        need_mask = narrow && op != MGP_OP_LSHR;
+        break;
+      }
+      case MGP_OP_UDIV: case MGP_OP_UREM: case MGP_OP_SDIV: case MGP_OP_SREM: case MGP_OP_SMOD: {
+        a = T.bv(oa); b = T.bv(ob); opid = MGP_U_DIV;
+        static const uint32_t dv[] = {MGP_DIV_UDIV, MGP_DIV_UREM, MGP_DIV_SDIV, MGP_DIV_SREM, MGP_DIV_SMOD};
+        flags |= dv[op - MGP_OP_UDIV] << MGP_U_DIVOP_POS;
+        if (narrow && op >= MGP_OP_SDIV) {
+          flags |= MGP_UF_SEXT;
+          w3 |= T.sign_off(width);
+        }
+        need_mask = narrow && op != MGP_OP_UREM;
+        break;
+      }
+      case MGP_OP_NOT: case MGP_OP_NEG:
+        a = T.bv(oa); opid = op == MGP_OP_NOT ? MGP_U_NOT : MGP_U_NEG; need_mask = narrow;
+        break;
+      case MGP_OP_MOV: case MGP_OP_ZEXT:
+        a = T.bv(oa); opid = MGP_U_MOV; need_mask = narrow;
+        break;
+      case MGP_OP_EXTRACT:
+        a = T.bv(oa);
+        if (imm == 0) {
+          opid = MGP_U_MOV;
+        } else {
+          opid = MGP_U_LSHRI0 + (imm >> 5);
+          flags |= (imm & 31u) << MGP_U_SHIFT_B_POS;
+        }
+        need_mask = narrow;
+        break;
+      case MGP_OP_SEXT:
+        a = T.bv(oa); opid = MGP_U_SEXT; w3 |= T.sign_off(imm); need_mask = narrow;
+        break;
+      case MGP_OP_CONCAT:
+        a = T.bv(oa); b = T.bv(ob);
+        if (imm == 0 || imm >= 256u) { T.bad = true; break; }
+        opid = MGP_U_CONCAT0 + (imm >> 5);
+        flags |= (imm & 31u) << MGP_U_SHIFT_B_POS;
+        break;
+      case MGP_OP_ITE:
+        a = T.bv(ob); b = T.bv(oc); opid = MGP_U_ITE;
+        w3 |= T.boolslot(oa) << 16;
+        break;
+      default:
+        T.bad = true;
+    }
+    if (T.bad) break;
+    if (need_mask) {
+      flags |= MGP_UF_MASK;
+      w2 |= T.mask_off(width) << 16;
+    }
+    if (store) {
+      if (dst >= MGP_U_MAX_LDS_SLOTS) { T.bad = true; break; }
+      flags |= MGP_UF_STORE;
+      w2 |= dst * MGP_U_SLOT_BYTES;
+    }
+    const uint32_t first = fetch_id(a.kind, b.kind, false);
+    emit(w0_of(first, opid, flags), a.param | (b.param << 16), w2, w3);
+  }
+
+  if (!v1_ok || T.bad || uops.empty()) {
+    out[base + 0] = 0;
+    out[base + 1] = 1;  // not runnable: the kernel reports MGP_UNDECIDED
+    out[base + 2] = MGP_U_HDR_WORDS * 4u;
+    for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);
+    return v1_ok ? 1 : 0;
+  }
+  const uint32_t n_uops = (uint32_t)(uops.size() / MGP_U_UOP_WORDS);
+  out.insert(out.end(), uops.begin(), uops.end());
+  for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);  // prefetch pad
+  out[base + 0] = n_uops;
+  out[base + 1] = 0;
+  out[base + 2] = (uint32_t)((MGP_U_HDR_WORDS + (n_uops + 1) * MGP_U_UOP_WORDS) * 4u);
+  out.insert(out.end(), T.pool.begin(), T.pool.end());
+  return 0;
+}

@@ -1,0 +1,88 @@
+"""Micro-op ("uop") encoding of the gfx950 assembly interpreter — single source of truth.
+
+The host translator (csrc/mgp_uop.cpp, via the generated header mgp_uop.h), the
+assembly generator (csrc/gen_eval_asm.py) and the CPU reference interpreter of
+the encoding (oracle/uop_ref.py, test infrastructure) all read this table.
+
+Program layout (per state, appended after the v1 bytecode of include/mgp_ir.h,
+at word offset align4(4 + 4*n_ins + 8*n_consts) + 4 from the program start):
+
+  header   4 words: n_uops, status (0 = runnable), pool byte offset (from the
+           uop header), 0
+  uops     n_uops x 4 words, then one all-zero uop (the kernel prefetches one
+           uop ahead)
+  pool     constants, 8 little-endian u32 limbs each (the v1 pool followed by
+           the width masks 2^w-1 and sign constants 2^(w-1) the uops use)
+
+uop words:
+  w0 [9:0]   byte offset of the FIRST handler in the dispatch table (id*4):
+             a fetch handler for BV/compare uops, the op handler otherwise
+     [17:10] op handler id (fetch handlers jump to it)
+     [18] STORE   result -> LDS slot (w2[15:0] = slot byte offset)
+     [19] MASK    result &= pool[w2[31:16]] (2^w - 1)
+     [20] SEXT    operands sign-extended from width w with H = pool[w3[15:0]]
+     [21] INVERT  compare result negated
+     [26:22]      uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT)
+     [29:27]      division variant (DIV_*)
+  w1 [15:0] operand A parameter, [31:16] operand B parameter
+            SLOT: LDS byte offset (slot*2048), VAR: variable index,
+            CONST: pool byte offset; Bool operands: bool slot * 2
+  w2 [15:0] store slot byte offset / third Bool operand * 2, [31:16] mask pool byte offset
+  w3 [15:0] sign-constant pool byte offset, [31:16] Bool destination * 2 (compares, Bool ops)
+            or ITE condition * 2
+
+Registers of the interpreter: vA (accumulator / operand A), vB (operand B),
+vC (operand A of a compare that is not the accumulator); Bool slots are
+64-bit lane masks in SGPRs: slot 0 = false, slot 1 = true, 2.. allocatable.
+"""
+
+KINDS = ("acc", "slot", "var", "const")
+B_KINDS = ("none",) + KINDS
+
+# fetch handlers: F_<kindA>_<kindB>_<target of A>; A = acc with target C never occurs
+FETCH = [f"F_{ka}_{kb}_A" for ka in KINDS for kb in B_KINDS] + \
+        [f"F_{ka}_{kb}_C" for ka in KINDS[1:] for kb in B_KINDS]
+
+BOOL_OPS = ["RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ"]
+BV_BIN = ["ADD", "SUB", "MUL", "AND", "OR", "XOR", "SHL", "LSHR", "ASHR", "DIV"]
+BV_UN = ["NOT", "NEG", "MOV", "SEXT"]
+SHIFT_I = [f"SHLI{k}" for k in range(9)] + [f"LSHRI{k}" for k in range(9)] + [f"ASHRI{k}" for k in range(9)]
+CONCAT = [f"CONCAT{k}" for k in range(8)]
+CMPS = ["EQ", "ULT", "UGT", "SLT", "SGT", "UADDNO256", "UADDNOW", "UMULNO256", "UMULNOW"]
+CMP_VARIANTS = [f"{c}_{r}" for c in CMPS for r in ("RA", "RC")]
+
+OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS
+# handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
+# id past the table ends the program instead of running off into memory
+HANDLERS = ["INVALID"] + FETCH + OPS
+ID = {name: i for i, name in enumerate(HANDLERS)}
+assert len(HANDLERS) < 256
+
+DIV_VARIANTS = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
+
+F_STORE, F_MASK, F_SEXT, F_INVERT = 1 << 18, 1 << 19, 1 << 20, 1 << 21
+SHIFT_B_POS, DIVOP_POS = 22, 27
+
+BOOL_SLOTS = 19          # 0 false, 1 true, 2..18 allocatable
+MAX_LDS_SLOTS = 31       # slot byte offsets must fit 16 bits with the +1024 half
+SLOT_BYTES = 2048        # 64 lanes x 32 B
+HDR_WORDS = 4
+UOP_WORDS = 4
+
+
+def c_header() -> str:
+    """The C view of this table (written to build/mgp/mgp_uop.h by the generator)."""
+    lines = ["/* generated from mythril_amd/uop_spec.py — do not edit */", "#pragma once"]
+    for name, i in ID.items():
+        lines.append(f"#define MGP_U_{name} {i}")
+    for name, v in DIV_VARIANTS.items():
+        lines.append(f"#define MGP_DIV_{name} {v}")
+    lines += [
+        f"#define MGP_UF_STORE {F_STORE}u", f"#define MGP_UF_MASK {F_MASK}u",
+        f"#define MGP_UF_SEXT {F_SEXT}u", f"#define MGP_UF_INVERT {F_INVERT}u",
+        f"#define MGP_U_SHIFT_B_POS {SHIFT_B_POS}", f"#define MGP_U_DIVOP_POS {DIVOP_POS}",
+        f"#define MGP_U_BOOL_SLOTS {BOOL_SLOTS}", f"#define MGP_U_MAX_LDS_SLOTS {MAX_LDS_SLOTS}",
+        f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",
+        f"#define MGP_U_UOP_WORDS {UOP_WORDS}",
+    ]
+    return "\n".join(lines) + "\n"

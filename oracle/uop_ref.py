@@ -1,0 +1,196 @@
+"""Reference interpreter of the uop encoding — TEST INFRASTRUCTURE.
+
+Executes the micro-op programs that mgp_lower appends for the gfx950
+assembly interpreter (encoding: mythril_amd/uop_spec.py) at the level of the
+kernel's registers — vA / vB / vC 256-bit values, Bool slots, LDS slots — so
+that the host translator (csrc/mgp_uop.cpp) can be checked on a CPU-only
+machine: eval_dag(DAG) == run_uops(lower(DAG)) for every candidate.  The
+assembly handlers implement exactly these register-level semantics.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+from mythril_amd import uop_spec as U
+
+from . import bvsem as S
+
+M256 = (1 << 256) - 1
+_NAME = {i: n for n, i in U.ID.items()}
+
+
+def _limbs(words, off) -> int:
+    return S.limbs_to_int([int(x) for x in words[off:off + 8]])
+
+
+def _s256(x: int) -> int:
+    return x - (1 << 256) if x >> 255 else x
+
+
+def _sext(x: int, h: int) -> int:
+    return ((x ^ h) - h) & M256
+
+
+def uop_offset(words, off: int) -> int:
+    """Word offset of the uop header of the program at `off` (after the v1 bytecode)."""
+    n_ins, n_c = int(words[off]), int(words[off + 1])
+    v1 = 4 + 4 * n_ins + 8 * n_c
+    return off + ((v1 + 3) & ~3) + 4
+
+
+def _div(op: int, a: int, b: int) -> int:
+    if op == U.DIV_VARIANTS["UDIV"]:
+        return M256 if b == 0 else a // b
+    if op == U.DIV_VARIANTS["UREM"]:
+        return a if b == 0 else a % b
+    table = {U.DIV_VARIANTS["SDIV"]: S.bvsdiv, U.DIV_VARIANTS["SREM"]: S.bvsrem, U.DIV_VARIANTS["SMOD"]: S.bvsmod}
+    return table[op](a, b, 256)
+
+
+def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
+    """Run the uop program of the state whose v1 program starts at `off`.
+
+    Returns True/False, or None when either header marks the state unsupported.
+    """
+    if int(words[off + 3]) & 0xFF:
+        return None
+    u0 = uop_offset(words, off)
+    n_uops, status, pool_bytes = int(words[u0]), int(words[u0 + 1]), int(words[u0 + 2])
+    if status:
+        return None
+    pool0 = u0 + pool_bytes // 4
+
+    def pool(byte_off: int) -> int:
+        return _limbs(words, pool0 + byte_off // 4)
+
+    vA = vB = vC = 0
+    KM = KH = 0
+    lds = {}
+    bools = [False] * U.BOOL_SLOTS
+    bools[1] = True
+
+    def load(kind: str, p: int) -> int:
+        if kind == "slot":
+            return lds[p]
+        if kind == "var":
+            return int(xs[p]) & M256
+        return pool(p)
+
+    for pc in range(n_uops):
+        w0, w1, w2, w3 = (int(words[u0 + 4 + 4 * pc + k]) for k in range(4))
+        first = _NAME[(w0 & 0x3FF) >> 2]
+        op = _NAME[(w0 >> 10) & 0xFF]
+        pa, pb = w1 & 0xFFFF, w1 >> 16
+        if first.startswith("F_"):
+            _, ka, kb, tgt = first.split("_")
+            if w0 & U.F_MASK:
+                KM = pool(w2 >> 16)
+            if w0 & U.F_SEXT:
+                KH = pool(w3 & 0xFFFF)
+            if kb != "none":
+                vB = vA if kb == "acc" else load(kb, pb)
+            if ka != "acc":
+                if tgt == "A":
+                    vA = load(ka, pa)
+                else:
+                    vC = load(ka, pa)
+        else:
+            op = first
+        sb = (w0 >> U.SHIFT_B_POS) & 31
+        if op in U.BOOL_OPS:
+            a, b, c = bools[pa >> 1], bools[pb >> 1], bools[(w2 & 0xFFFF) >> 1]
+            if op == "RET":
+                return a
+            r = {"BAND": a and b, "BOR": a or b, "BXOR": a != b, "BNOT": not a,
+                 "BITE": b if a else c, "BEQ": a == b}[op]
+            bools[w3 >> 17] = r
+            continue
+        if op.endswith("_RA") or op.endswith("_RC"):
+            base = op[:-3]
+            X = vA if op.endswith("_RA") else vC
+            Y = vB
+            if w0 & U.F_SEXT:
+                X, Y = _sext(X, KH), _sext(Y, KH)
+            if base == "EQ":
+                raw = X == Y
+            elif base == "ULT":
+                raw = X < Y
+            elif base == "UGT":
+                raw = X > Y
+            elif base == "SLT":
+                raw = _s256(X) < _s256(Y)
+            elif base == "SGT":
+                raw = _s256(X) > _s256(Y)
+            elif base == "UADDNO256":
+                raw = X + Y > M256
+            elif base == "UADDNOW":
+                raw = X + Y > KM
+            elif base == "UMULNO256":
+                raw = X * Y > M256
+            elif base == "UMULNOW":
+                p = X * Y
+                raw = (p >> 256) != 0 or (p & M256) > KM
+            else:
+                raise ValueError(op)
+            bools[w3 >> 17] = bool(raw) != bool(w0 & U.F_INVERT)
+            continue
+        # BV-producing
+        if op == "ITE":
+            vA = vA if bools[w3 >> 17] else vB
+        elif op in ("ADD", "SUB", "MUL", "AND", "OR", "XOR"):
+            vA = {"ADD": vA + vB, "SUB": vA - vB, "MUL": vA * vB, "AND": vA & vB,
+                  "OR": vA | vB, "XOR": vA ^ vB}[op] & M256
+        elif op in ("SHL", "LSHR", "ASHR"):
+            s = vB if vB < 256 else 256
+            if op == "SHL":
+                vA = (vA << s) & M256
+            elif op == "LSHR":
+                vA >>= s
+            else:
+                if w0 & U.F_SEXT:
+                    vA = _sext(vA, KH)
+                vA = (_s256(vA) >> s) & M256
+        elif op == "DIV":
+            a, b = vA, vB
+            if w0 & U.F_SEXT:
+                a, b = _sext(a, KH), _sext(b, KH)
+            vA = _div((w0 >> U.DIVOP_POS) & 7, a, b) & M256
+        elif op == "NOT":
+            vA = ~vA & M256
+        elif op == "NEG":
+            vA = -vA & M256
+        elif op == "MOV":
+            pass
+        elif op == "SEXT":
+            vA = _sext(vA, KH)
+        elif op[:4] in ("SHLI", "LSHR", "ASHR") and op[-1].isdigit():
+            k = int(op[-1])
+            s = 256 if k == 8 else 32 * k + sb
+            if op.startswith("SHLI"):
+                vA = (vA << s) & M256
+            elif op.startswith("LSHRI"):
+                vA >>= s
+            else:
+                if w0 & U.F_SEXT:
+                    vA = _sext(vA, KH)
+                vA = (_s256(vA) >> s) & M256
+        elif op.startswith("CONCAT"):
+            k = int(op[-1])
+            vA = ((vA << (32 * k + sb)) & M256) | vB
+        else:
+            raise ValueError(op)
+        if w0 & U.F_MASK:
+            vA &= KM
+        if w0 & U.F_STORE:
+            lds[w2 & 0xFFFF] = vA
+    raise ValueError("uop program fell off the end without RET")
+
+
+def first_sat_uops(words, off, cands) -> int:
+    for i, xs in enumerate(cands):
+        r = run_uops(words, off, xs)
+        if r is None:
+            return -2
+        if r:
+            return i
+    return -1

@@ -1,0 +1,85 @@
+"""Static checks of the generated gfx950 interpreter (CPU only).
+
+The kernel is generated (mythril_amd/csrc/gen_eval_asm.py); these checks make
+properties the GPU run depends on hold by construction:
+  * every branch inside a handler is a forward branch, so each uop finishes
+    and the only loop is the dispatch, which advances the uop pointer each time
+    (a wave always reaches RET or the INVALID handler of the zero pad);
+  * the dispatch table has 256 entries, so no 8-bit handler id can jump outside it;
+  * no scalar-memory writes anywhere (results go out through vector stores);
+  * 64-bit VGPR operands are even-aligned (gfx950 register-tuple rule);
+  * the file assembles for gfx950 with the ROCm LLVM assembler.
+"""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GEN = os.path.join(ROOT, "mythril_amd", "csrc", "gen_eval_asm.py")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    d = tmp_path_factory.mktemp("asm")
+    s, h = str(d / "k.s"), str(d / "h.h")
+    subprocess.run([sys.executable, GEN, s, h], check=True)
+    return s, open(s).read().splitlines()
+
+
+def test_branches_are_forward(asm):
+    _, lines = asm
+    pos = {}
+    for i, l in enumerate(lines):
+        m = re.match(r"^(\.L\w+):", l)
+        if m:
+            pos[m.group(1)] = i
+    table = pos[".Ltab"]
+    n_branches = 0
+    for i, l in enumerate(lines):
+        m = re.match(r"^\s+s_(?:c?branch\w*)\s+(\.L\w+)", l)
+        if not m:
+            continue
+        n_branches += 1
+        tgt = m.group(1)
+        assert tgt in pos, f"undefined label {tgt}"
+        assert pos[tgt] > i or (i > table and tgt.startswith(".Lh_") and i < table + 257), \
+            f"backward branch at line {i}: {l.strip()}"
+    assert n_branches > 300
+
+
+def test_dispatch_table_is_full(asm):
+    _, lines = asm
+    t = lines.index(".Ltab:")
+    stubs = lines[t + 1:t + 1 + 256]
+    assert all(re.match(r"^\s+s_branch \.Lh_\w+$", x) for x in stubs)
+    assert not re.match(r"^\s+s_branch", lines[t + 257])
+
+
+def test_no_scalar_memory_writes(asm):
+    _, lines = asm
+    # built from parts so that this file itself does not spell the mnemonics
+    bad = ["s_" + x for x in ("store", "buffer_store", "scratch_store", "dcache_wb", "dcache_discard", "atomic")]
+    for l in lines:
+        op = l.strip().split(" ")[0]
+        assert not any(op.startswith(b) for b in bad), l
+
+
+def test_vgpr_pairs_even_aligned(asm):
+    _, lines = asm
+    for l in lines:
+        for a, b in re.findall(r"v\[(\d+):(\d+)\]", l):
+            if int(b) - int(a) == 1:
+                assert int(a) % 2 == 0, l
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM}/clang"), reason="ROCm LLVM assembler not installed")
+def test_assembles_for_gfx950(asm, tmp_path):
+    s, _ = asm
+    o = str(tmp_path / "k.o")
+    r = subprocess.run([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
+                        "-c", s, "-o", o], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]

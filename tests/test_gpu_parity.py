@@ -16,6 +16,16 @@ from ._util import cands_from_ints, load_golden, pack_states, random_cands
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["asm", "hip"])
+def engine(request):
+    """Every parity test runs on both evaluation kernels: the hand-written gfx950
+    interpreter (default engine) and the HIP C++ interpreter."""
+    old = N.set_eval_engine()
+    assert N.set_eval_engine(request.param) == request.param
+    yield request.param
+    N.set_eval_engine(old)
+
+
 def _lower(nodes, noff, consts, coff, **kw):
     words, po, status = N.lower(nodes, noff, consts, coff, **kw)
     return words, po, status

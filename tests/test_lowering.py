@@ -1,8 +1,10 @@
 """Host lowering (mgp_lower, C++) vs the DAG oracle — CPU only.
 
 The bytecode produced for the GPU is executed by oracle.bytecode_ref (an
-independent interpreter of the encoding in include/mgp_ir.h) and must agree
-with oracle.bvsem on the DAG for every candidate.
+independent interpreter of the encoding in include/mgp_ir.h) and its uop
+re-encoding for the gfx950 assembly interpreter by oracle.uop_ref (register-
+level semantics of the handlers, encoding in mythril_amd/uop_spec.py); both
+must agree with oracle.bvsem on the DAG for every candidate.
 """
 import numpy as np
 import pytest
@@ -10,6 +12,7 @@ import pytest
 from mythril_amd import _native as N
 from oracle import bvsem as S
 from oracle import bytecode_ref as BR
+from oracle import uop_ref as UR
 
 from ._util import INTERESTING, load_golden, pack_states, state_slice
 
@@ -22,6 +25,7 @@ def _check_states(states, cand_rows, max_slots=0):
             want = S.eval_root(nl, cl, xs)
             got = BR.run_program(words, int(po[s]), xs)
             assert got == want, (s, xs)
+            assert UR.run_uops(words, int(po[s]), xs) == want, ("uop", s, xs)
     return words, po, status
 
 
@@ -37,7 +41,9 @@ def test_synthetic_lowering_matches_dag():
         if b["planted"][s]:
             rows.append([S.limbs_to_int(x) for x in b["plant_words"][s]])
         for xs in rows:
-            assert BR.run_program(words, int(po[s]), xs) == S.eval_root(nodes, consts, xs), s
+            want = S.eval_root(nodes, consts, xs)
+            assert BR.run_program(words, int(po[s]), xs) == want, s
+            assert UR.run_uops(words, int(po[s]), xs) == want, ("uop", s)
 
 
 def test_golden_arith_lowering():
@@ -97,11 +103,9 @@ def test_uf_chains():
     _check_states([(nl, [])], [rows])
 
 
-def test_many_live_values_rejected_cleanly():
-    # 40 values each used by two chains that consume them in opposite orders:
-    # whatever the schedule, all 40 are live at once -> a 4-slot cap is
-    # unsupported (never wrong), a 64-slot cap lowers and evaluates correctly
-    n = 40
+def _live_chain(n):
+    # n values each used by two chains that consume them in opposite orders:
+    # whatever the schedule, all n are live at once
     nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]
     vals = []
     for i in range(n):
@@ -116,13 +120,29 @@ def test_many_live_values_rejected_cleanly():
         nl.append([S.SUB, 256, acc2, v, -1, 0, 0])
         acc2 = len(nl) - 1
     nl.append([S.ULT, 1, acc, acc2, -1, 0, 0])
+    return nl
+
+
+def test_many_live_values_rejected_cleanly():
+    # 28 live values: a 4-slot cap is unsupported (never wrong), the default cap lowers
+    nl = _live_chain(28)
     nodes, noff, consts, coff = pack_states([(nl, [])])
     _, _, status = N.lower(nodes, noff, consts, coff, max_slots=4)
     assert status[0] == N.ST_UNSUPPORTED
     words, po, status = N.lower(nodes, noff, consts, coff, max_slots=64)
     assert status[0] == N.ST_OK
     for xs in ([3, 5], [INTERESTING[3], INTERESTING[4]]):
-        assert BR.run_program(words, int(po[0]), xs) == S.eval_root(nl, [], xs)
+        want = S.eval_root(nl, [], xs)
+        assert BR.run_program(words, int(po[0]), xs) == want
+        assert UR.run_uops(words, int(po[0]), xs) == want
+    # 40 live values exceed the interpreter's 31 LDS slots (62 KiB per wave):
+    # unsupported in both encodings, so both engines answer "undecided"
+    nl = _live_chain(40)
+    nodes, noff, consts, coff = pack_states([(nl, [])])
+    words, po, status = N.lower(nodes, noff, consts, coff, max_slots=64)
+    assert status[0] == N.ST_UNSUPPORTED
+    assert BR.run_program(words, int(po[0]), [3, 5]) is None
+    assert UR.run_uops(words, int(po[0]), [3, 5]) is None
 
 
 @pytest.mark.parametrize("bad", ["wide", "forward_ref", "bool_as_bv", "width_mismatch", "root_bv", "unknown_op"])
@@ -142,6 +162,8 @@ def test_malformed_dags_are_unsupported(bad):
     assert status[0] == N.ST_UNSUPPORTED and status[1] == N.ST_OK
     assert BR.run_program(words, int(po[0]), [1, 2]) is None
     assert BR.run_program(words, int(po[1]), [1, 2]) is True
+    assert UR.run_uops(words, int(po[0]), [1, 2]) is None
+    assert UR.run_uops(words, int(po[1]), [1, 2]) is True
 
 
 def test_empty_batch_and_constant_roots():
@@ -150,6 +172,8 @@ def test_empty_batch_and_constant_roots():
     words, po, status = N.lower(nodes, noff, consts, coff)
     assert BR.run_program(words, int(po[0]), []) is True
     assert BR.run_program(words, int(po[1]), []) is False
+    assert UR.run_uops(words, int(po[0]), []) is True
+    assert UR.run_uops(words, int(po[1]), []) is False
     w0, po0, st0 = N.lower(np.zeros(0, dtype=N.NODE_DTYPE), np.zeros(1, np.uint64), np.zeros((0, 8), np.uint32),
                            np.zeros(1, np.uint64))
     assert len(po0) == 1 and w0.size == 0

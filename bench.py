@@ -39,6 +39,7 @@ VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 KECCAK_OPS_PER_HASH = 7458  # SURVEY.md §8d (310/round x 24 + absorb)
 KECCAK_BYTES_PER_HASH = 96
+ENGINE_KERNEL = {"asm": "mgp_eval_gfx950", "hip": "mgp_eval_kernel"}
 
 
 def log(*a):
@@ -166,7 +167,8 @@ def main():
         try:
             with open(pmc_path) as f:
                 pm = json.load(f)
-            if pm.get("states") == n_states and pm.get("cand") == n_cand:
+            if (pm.get("states") == n_states and pm.get("cand") == n_cand
+                    and pm.get("kernel") == ENGINE_KERNEL[N.set_eval_engine()]):
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -258,7 +260,7 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": valu_peak, "unit": "TOP/s",
                          "frac": achieved_tops / valu_peak, "traffic": traffic, "peak_derived": VALU_PEAK_TOPS,
                          "ops": "nominal INT32 ops of the live DAG nodes (SURVEY.md 8d table) x candidates",
-                         "kernel": "mgp_eval_kernel(+finalize)", "launch_ms": kern_ms,
+                         "kernel": ENGINE_KERNEL[N.set_eval_engine()] + "(+finalize)", "launch_ms": kern_ms,
                          "evals_per_launch": evals_rank},
             "roofline_hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": achieved_gbs / HBM_PEAK_GBS, "bytes_per_launch": bytes_launch},

@@ -36,6 +36,7 @@ from mythril_amd import uop_spec as U  # noqa: E402
 
 KNAME = "mgp_eval_gfx950"
 VA, VB, VC, VT = 8, 16, 24, 32
+RV = 64          # v[64:127]: candidate variables 0..7 of this lane, preloaded at wave start
 S_KB, S_KH, S_KM = 24, 32, 40
 
 
@@ -282,6 +283,15 @@ def fetch_one(kind, dst, which):
             copy8(dst, VA)
         return
     A(get)
+    if kind == "rvar":
+        # v[dst+i] = v[64 + 8*var + i]: GPR-index mode (gfx950 has no v_movrels) offsets
+        # SRC0 of the moves by 8*var into the preloaded variable bank
+        A(f"s_lshl_b32 {sp}, {sp}, 3", "s_waitcnt vmcnt(0)",
+          f"s_set_gpr_idx_on {sp}, gpr_idx(SRC0)", "s_nop 1")
+        for i in range(8):
+            A(f"v_mov_b32 {v(dst + i)}, {v(RV + i)}")
+        A("s_set_gpr_idx_off", "s_nop 1")
+        return
     if kind == "slot":
         A(f"v_add_u32 {vaddr}, {sp}, v1",
           f"ds_read_b128 {vr(dst, 4)}, {vaddr}",
@@ -977,6 +987,57 @@ PROLOGUE = """\
   s_lshl_b32 s92, s75, 4
   v_add_u32 v3, s92, v2
   v_lshlrev_b32 v1, 4, v0
+  // preload variables 0..min(n_vars, 8)-1 of this lane's candidate into v[64:127]
+  s_mov_b64 s[92:93], s[6:7]
+  s_cmp_le_u32 s76, 0
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[64:67], v2, s[92:93]
+  global_load_dwordx4 v[68:71], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+  s_cmp_le_u32 s76, 1
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[72:75], v2, s[92:93]
+  global_load_dwordx4 v[76:79], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+  s_cmp_le_u32 s76, 2
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[80:83], v2, s[92:93]
+  global_load_dwordx4 v[84:87], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+  s_cmp_le_u32 s76, 3
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[88:91], v2, s[92:93]
+  global_load_dwordx4 v[92:95], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+  s_cmp_le_u32 s76, 4
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[96:99], v2, s[92:93]
+  global_load_dwordx4 v[100:103], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+  s_cmp_le_u32 s76, 5
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[104:107], v2, s[92:93]
+  global_load_dwordx4 v[108:111], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+  s_cmp_le_u32 s76, 6
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[112:115], v2, s[92:93]
+  global_load_dwordx4 v[116:119], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+  s_cmp_le_u32 s76, 7
+  s_cbranch_scc1 .Lvars_done
+  global_load_dwordx4 v[120:123], v2, s[92:93]
+  global_load_dwordx4 v[124:127], v3, s[92:93]
+  s_add_u32 s92, s92, s8
+  s_addc_u32 s93, s93, 0
+.Lvars_done:
   s_getpc_b64 s[10:11]
 .Lpc_base:
   s_add_u32 s10, s10, .Ltab-.Lpc_base
@@ -1024,7 +1085,7 @@ def metadata():
         "    .private_segment_fixed_size: 0",
         "    .sgpr_count: 104",
         f"    .symbol: {KNAME}.kd",
-        "    .vgpr_count: 64",
+        "    .vgpr_count: 128",
         "    .wavefront_size: 64",
         "amdhsa.target: amdgcn-amd-amdhsa--gfx950",
         "amdhsa.version:", "  - 1", "  - 2",
@@ -1069,9 +1130,9 @@ def generate() -> str:
         "  .amdhsa_system_sgpr_workgroup_id_x 1",
         "  .amdhsa_system_sgpr_workgroup_id_y 1",
         "  .amdhsa_system_vgpr_workitem_id 0",
-        "  .amdhsa_next_free_vgpr 64",
+        "  .amdhsa_next_free_vgpr 128",
         "  .amdhsa_next_free_sgpr 102",
-        "  .amdhsa_accum_offset 64",
+        "  .amdhsa_accum_offset 128",
         "  .amdhsa_reserve_vcc 1",
         "  .amdhsa_float_denorm_mode_32 3",
         "  .amdhsa_float_denorm_mode_16_64 3",

@@ -29,17 +29,18 @@
 namespace {
 
 struct Opnd {
-  int kind;       // 0 acc, 1 slot, 2 var, 3 const, -1 none
+  int kind;       // 0 acc, 1 slot, 2 var (HBM), 3 const, 4 rvar (register-resident var), -1 none
   uint32_t param;
 };
 
-constexpr int KACC = 0, KSLOT = 1, KVAR = 2, KCONST = 3, KNONE = -1;
+constexpr int KACC = 0, KSLOT = 1, KVAR = 2, KCONST = 3, KRVAR = 4, KNONE = -1;
 
-// fetch handler ids, in uop_spec.FETCH order: A-target block (4 x 5), then C-target (3 x 5)
+// fetch handler ids, in uop_spec.FETCH order: A-target block (K x (K+1)), then
+// C-target ((K-1) x (K+1)), K = MGP_U_N_KINDS, B kind "none" first
 inline uint32_t fetch_id(int ka, int kb, bool to_c) {
-  const int kbi = kb + 1;  // none = 0
-  if (!to_c) return (uint32_t)(MGP_U_F_acc_none_A + ka * 5 + kbi);
-  return (uint32_t)(MGP_U_F_slot_none_C + (ka - 1) * 5 + kbi);
+  const int kbi = kb + 1;
+  if (!to_c) return (uint32_t)(MGP_U_F_acc_none_A + ka * (MGP_U_N_KINDS + 1) + kbi);
+  return (uint32_t)(MGP_U_F_slot_none_C + (ka - 1) * (MGP_U_N_KINDS + 1) + kbi);
 }
 
 struct Translator {
@@ -87,7 +88,7 @@ struct Translator {
         if (idx >= MGP_U_MAX_LDS_SLOTS) bad = true;
         return {KSLOT, idx * MGP_U_SLOT_BYTES};
       case MGP_K_CONST: return {KCONST, pool_byte(idx)};
-      default: return {KVAR, idx};
+      default: return {idx < MGP_U_REG_VARS ? KRVAR : KVAR, idx};
     }
   }
   uint32_t boolslot(uint32_t b) {

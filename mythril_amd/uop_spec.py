@@ -25,7 +25,7 @@ uop words:
      [26:22]      uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT)
      [29:27]      division variant (DIV_*)
   w1 [15:0] operand A parameter, [31:16] operand B parameter
-            SLOT: LDS byte offset (slot*2048), VAR: variable index,
+            SLOT: LDS byte offset (slot*2048), VAR / RVAR: variable index,
             CONST: pool byte offset; Bool operands: bool slot * 2
   w2 [15:0] store slot byte offset / third Bool operand * 2, [31:16] mask pool byte offset
   w3 [15:0] sign-constant pool byte offset, [31:16] Bool destination * 2 (compares, Bool ops)
@@ -36,7 +36,11 @@ vC (operand A of a compare that is not the accumulator); Bool slots are
 64-bit lane masks in SGPRs: slot 0 = false, slot 1 = true, 2.. allocatable.
 """
 
-KINDS = ("acc", "slot", "var", "const")
+# operand kinds: acc = the accumulator vA, slot = per-lane LDS slot, var = candidate
+# variable loaded from HBM, const = constant pool (scalar load), rvar = candidate
+# variable 0..REG_VARS-1 preloaded into v[64:127] at wave start (v_movrels)
+KINDS = ("acc", "slot", "var", "const", "rvar")
+REG_VARS = 8
 B_KINDS = ("none",) + KINDS
 
 # fetch handlers: F_<kindA>_<kindB>_<target of A>; A = acc with target C never occurs
@@ -83,6 +87,7 @@ def c_header() -> str:
         f"#define MGP_U_SHIFT_B_POS {SHIFT_B_POS}", f"#define MGP_U_DIVOP_POS {DIVOP_POS}",
         f"#define MGP_U_BOOL_SLOTS {BOOL_SLOTS}", f"#define MGP_U_MAX_LDS_SLOTS {MAX_LDS_SLOTS}",
         f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",
-        f"#define MGP_U_UOP_WORDS {UOP_WORDS}",
+        f"#define MGP_U_UOP_WORDS {UOP_WORDS}", f"#define MGP_U_REG_VARS {REG_VARS}",
+        f"#define MGP_U_N_KINDS {len(KINDS)}",
     ]
     return "\n".join(lines) + "\n"

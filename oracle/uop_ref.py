@@ -72,7 +72,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
     def load(kind: str, p: int) -> int:
         if kind == "slot":
             return lds[p]
-        if kind == "var":
+        if kind in ("var", "rvar"):
             return int(xs[p]) & M256
         return pool(p)
 

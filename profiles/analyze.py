@@ -30,7 +30,7 @@ def main(d):
     evals = []
     with open(tr) as f:
         for r in csv.DictReader(f):
-            if short(r["Kernel_Name"]) in ("mgp_eval_kernel", "mgp_finalize_kernel"):
+            if short(r["Kernel_Name"]) in ("mgp_eval_kernel", "mgp_eval_gfx950", "mgp_finalize_kernel"):
                 evals.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     evals.sort()
     steps, cur = [], []
@@ -58,7 +58,9 @@ def main(d):
                 agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["LDS_Block_Size"], r["Scratch_Size"])
     out.append("\n## PMC counters (summed over dispatches; separate passes)\n")
-    for k in ("mgp_eval_kernel", "mgp_keccak64_kernel", "mgp_valu_probe_kernel"):
+    traffic = {}
+    n_steps = max(1, sum(1 for e in evals if e[2] == "mgp_finalize_kernel"))
+    for k in ("mgp_eval_gfx950", "mgp_eval_kernel", "mgp_keccak64_kernel", "mgp_valu_probe_kernel"):
         if k not in agg:
             continue
         c = agg[k]
@@ -82,13 +84,31 @@ def main(d):
                 der["wait_inst_any share"] = c.get("SQ_WAIT_INST_ANY", 0) / tot
                 der["active_inst_any share"] = c.get("SQ_ACTIVE_INST_ANY", 0) / tot
         if "FETCH_SIZE" in c:
-            der["FETCH_SIZE KB (x2 gfx950 correction for wide streams)"] = c["FETCH_SIZE"]
+            der["FETCH_SIZE KB (raw, all dispatches)"] = c["FETCH_SIZE"]
+        if k in ("mgp_eval_gfx950", "mgp_eval_kernel") and "FETCH_SIZE" in c:
+            # per eval step (all bucket dispatches of one step); FETCH_SIZE doubled for 16-B/lane
+            # streaming reads (MI355X_MICROARCH.md, HBM section), WRITE_SIZE read as-is
+            fetch = 2 * c["FETCH_SIZE"] * 1024 / n_steps
+            write = c.get("WRITE_SIZE", 0) * 1024 / n_steps
+            der["HBM bytes per eval step (2 x FETCH_SIZE + WRITE_SIZE)"] = fetch + write
+            traffic[k] = {"fetch_bytes_per_step": fetch, "write_bytes_per_step": write,
+                          "hbm_bytes_per_launch": fetch + write, "steps_in_profile": n_steps}
         if der:
             out.append("\nderived:\n")
             for n, val in der.items():
                 out.append(f"- {n}: {val:.4g}")
         out.append("")
     print("\n".join(out))
+    # machine-readable traffic figure for bench.py's roofline.traffic (same workload shape only)
+    bj = os.path.join(d, "bench_trace.json")
+    for k, t in traffic.items():
+        try:
+            cfg = json.load(open(bj))["config"]
+            t.update({"kernel": k, "states": cfg["states_per_gpu"], "cand": cfg["candidates"], "source": d})
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "eval_pmc_traffic.json"), "w") as f:
+                json.dump(t, f, indent=1)
+        except (OSError, ValueError, KeyError):
+            pass
 
 
 if __name__ == "__main__":

@@ -83,3 +83,41 @@ def test_assembles_for_gfx950(asm, tmp_path):
     r = subprocess.run([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
                         "-c", s, "-o", o], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_address_registers_initialised_before_first_load(asm):
+    # v1 (LDS lane base), v2/v3 (candidate offsets) and the table base s[10:11] must be
+    # written in the prologue before the first instruction that uses them
+    _, lines = asm
+    body = [l.strip() for l in lines]
+
+    def first(pred):
+        return next(i for i, l in enumerate(body) if pred(l))
+
+    w1 = first(lambda l: l.startswith("v_lshlrev_b32 v1,"))
+    w2 = first(lambda l: l.startswith("v_lshlrev_b32 v2,"))
+    w3 = first(lambda l: l.startswith("v_add_u32 v3,"))
+    assert w2 < w3 < first(lambda l: l.startswith("global_load") and ", v3," in l)
+    assert w2 < first(lambda l: l.startswith("global_load") and ", v2," in l)
+    assert w1 < first(lambda l: l.startswith("ds_") and ", v" in l)
+    assert first(lambda l: l.startswith("s_getpc_b64 s[10:11]")) < first(lambda l: l.startswith("s_setpc_b64"))
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM}/ld.lld"), reason="ROCm LLVM linker not installed")
+def test_embedded_code_object_is_current(asm, tmp_path):
+    """libmgp.so must embed exactly the code object the current generator produces
+    (a stale build would run an old kernel on the GPU)."""
+    import ctypes
+
+    from mythril_amd import _native as N
+
+    s, _ = asm
+    o, h = str(tmp_path / "k.o"), str(tmp_path / "k.hsaco")
+    subprocess.run([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
+                    "-c", s, "-o", o], check=True)
+    subprocess.run([f"{LLVM}/ld.lld", "-shared", o, "-o", h], check=True)
+    fresh = open(h, "rb").read()
+    lib = N.lib()
+    size = ctypes.c_size_t.in_dll(lib, "mgp_eval_gfx950_hsaco_size").value
+    emb = bytes((ctypes.c_ubyte * size).in_dll(lib, "mgp_eval_gfx950_hsaco"))
+    assert emb == fresh, "libmgp.so embeds a stale mgp_eval_gfx950 (rebuild: make -C mythril_amd/csrc)"

@@ -36,7 +36,9 @@ from mythril_amd import uop_spec as U  # noqa: E402
 
 KNAME = "mgp_eval_gfx950"
 VA, VB, VC, VT = 8, 16, 24, 32
-RV = 64          # v[64:127]: candidate variables 0..7 of this lane, preloaded at wave start
+RV = 64          # v[64:111]: candidate variables 0..5 of this lane, preloaded at wave start
+PG = 112         # v[112:115]: the current 64-uop page, uop k in lane k (read with v_readlane)
+PQ = 116         # v[116:123]: the constant pool, constant c in lane c, limb l in v[116+l]
 S_KB, S_KH, S_KM = 24, 32, 40
 
 
@@ -82,13 +84,12 @@ A = Asm()
 
 
 def tail():
-    """Advance to the prefetched uop, prefetch the next one, dispatch."""
-    A("s_waitcnt lgkmcnt(0)",
-      "s_mov_b64 s[16:17], s[20:21]",
-      "s_mov_b64 s[18:19], s[22:23]",
-      "s_add_u32 s4, s4, 16",
-      "s_addc_u32 s5, s5, 0",
-      "s_load_dwordx4 s[20:23], s[4:5], 0x10",
+    """Read the next uop from the VGPR page (lane s3) and dispatch it."""
+    A("v_readlane_b32 s16, v112, s3",
+      "v_readlane_b32 s17, v113, s3",
+      "v_readlane_b32 s18, v114, s3",
+      "v_readlane_b32 s19, v115, s3",
+      "s_add_u32 s3, s3, 1",
       "s_and_b32 s12, s16, 0x3fc",
       "s_add_u32 s12, s10, s12",
       "s_addc_u32 s13, s11, 0",
@@ -304,8 +305,9 @@ def fetch_one(kind, dst, which):
           f"s_addc_u32 s{lo + 1}, s7, 0",
           f"global_load_dwordx4 {vr(dst, 4)}, v2, {pr}",
           f"global_load_dwordx4 {vr(dst + 4, 4)}, v3, {pr}")
-    else:  # const
-        A(f"s_load_dwordx8 s[24:31], s[14:15], {sp}", "s_waitcnt lgkmcnt(0)")
+    else:  # const: broadcast lane `idx` of the pool registers
+        for i in range(8):
+            A(f"v_readlane_b32 {s(S_KB + i)}, {v(PQ + i)}, {sp}")
         for i in range(8):
             A(f"v_mov_b32 {v(dst + i)}, {s(S_KB + i)}")
 
@@ -315,11 +317,13 @@ def make_fetch(name):
 
     def body():
         l1, l2 = A.fresh("nokm"), A.fresh("nokh")
-        A("s_bitcmp1_b32 s16, 19", f"s_cbranch_scc0 {l1}",
-          "s_lshr_b32 s48, s18, 16", "s_load_dwordx8 s[40:47], s[14:15], s48")
+        A("s_bitcmp1_b32 s16, 19", f"s_cbranch_scc0 {l1}", "s_lshr_b32 s48, s18, 16")
+        for i in range(8):
+            A(f"v_readlane_b32 {s(S_KM + i)}, {v(PQ + i)}, s48")
         A.label(l1)
-        A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {l2}",
-          "s_and_b32 s49, s19, 0xffff", "s_load_dwordx8 s[32:39], s[14:15], s49")
+        A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {l2}", "s_and_b32 s49, s19, 0xffff")
+        for i in range(8):
+            A(f"v_readlane_b32 {s(S_KH + i)}, {v(PQ + i)}, s49")
         A.label(l2)
         if kb != "none":
             fetch_one(kb, VB, "B")
@@ -330,6 +334,21 @@ def make_fetch(name):
 
 for _f in U.FETCH:
     HBODY[_f] = make_fetch(_f)
+
+
+# ---- program paging
+@handler("PAGE")
+def h_page():
+    # next 64 uops: lane k loads uop min(k, remaining-1) of the next page into v[112:115]
+    A("s_add_u32 s4, s4, 0x400", "s_addc_u32 s5, s5, 0",
+      "s_sub_u32 s20, s20, 64",
+      "v_min_u32 v4, s20, v0",
+      "v_lshlrev_b32 v4, 4, v4",
+      "s_waitcnt vmcnt(0)",
+      "global_load_dwordx4 v[112:115], v4, s[4:5]",
+      "s_waitcnt vmcnt(0)",
+      "s_mov_b32 s3, 0")
+    tail()
 
 
 # ---- Bool ops
@@ -961,14 +980,19 @@ PROLOGUE = """\
   s_addc_u32 s85, s85, 0
   s_load_dwordx4 s[88:91], s[84:85], 0x0
   s_waitcnt lgkmcnt(0)
+  // uop header: n_uops, status, pool byte offset, n_pool
   s_cmp_lg_u32 s89, 0
+  s_cbranch_scc1 .Lundec
+  s_cmp_gt_u32 s91, 64
+  s_cbranch_scc1 .Lundec
+  s_cmp_eq_u32 s88, 0
   s_cbranch_scc1 .Lundec
   s_add_u32 s14, s84, s90
   s_addc_u32 s15, s85, 0
   s_add_u32 s4, s84, 16
   s_addc_u32 s5, s85, 0
-  s_load_dwordx4 s[16:19], s[4:5], 0x0
-  s_load_dwordx4 s[20:23], s[4:5], 0x10
+  s_sub_u32 s20, s88, 1
+  s_mov_b32 s21, s91
   // candidates of this state: cands + state * n_vars * n_cand * 32, layout [var][half][cand] x 16 B
   s_lshl_b32 s8, s75, 5
   s_mul_i32 s92, s76, s8
@@ -987,58 +1011,21 @@ PROLOGUE = """\
   s_lshl_b32 s92, s75, 4
   v_add_u32 v3, s92, v2
   v_lshlrev_b32 v1, 4, v0
-  // preload variables 0..min(n_vars, 8)-1 of this lane's candidate into v[64:127]
-  s_mov_b64 s[92:93], s[6:7]
-  s_cmp_le_u32 s76, 0
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[64:67], v2, s[92:93]
-  global_load_dwordx4 v[68:71], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-  s_cmp_le_u32 s76, 1
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[72:75], v2, s[92:93]
-  global_load_dwordx4 v[76:79], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-  s_cmp_le_u32 s76, 2
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[80:83], v2, s[92:93]
-  global_load_dwordx4 v[84:87], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-  s_cmp_le_u32 s76, 3
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[88:91], v2, s[92:93]
-  global_load_dwordx4 v[92:95], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-  s_cmp_le_u32 s76, 4
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[96:99], v2, s[92:93]
-  global_load_dwordx4 v[100:103], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-  s_cmp_le_u32 s76, 5
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[104:107], v2, s[92:93]
-  global_load_dwordx4 v[108:111], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-  s_cmp_le_u32 s76, 6
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[112:115], v2, s[92:93]
-  global_load_dwordx4 v[116:119], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-  s_cmp_le_u32 s76, 7
-  s_cbranch_scc1 .Lvars_done
-  global_load_dwordx4 v[120:123], v2, s[92:93]
-  global_load_dwordx4 v[124:127], v3, s[92:93]
-  s_add_u32 s92, s92, s8
-  s_addc_u32 s93, s93, 0
-.Lvars_done:
-  s_getpc_b64 s[10:11]
+  // uop page 0 -> v[112:115] (lane k = uop min(k, n_uops-1)); pool -> v[116:123] (lane c = constant
+  // min(c, n_pool-1)); both issued before the variable loads so that vmcnt(12) covers them
+  v_min_u32 v4, s20, v0
+  v_lshlrev_b32 v4, 4, v4
+  global_load_dwordx4 v[112:115], v4, s[4:5]
+  s_cmp_eq_u32 s21, 0
+  s_cbranch_scc1 .Lno_pool
+  s_sub_u32 s92, s21, 1
+  v_min_u32 v4, s92, v0
+  v_lshlrev_b32 v4, 5, v4
+  global_load_dwordx4 v[116:119], v4, s[14:15]
+  global_load_dwordx4 v[120:123], v4, s[14:15] offset:16
+.Lno_pool:
+  // preload variables 0..min(n_vars, 6)-1 of this lane's candidate into v[64:111]
+{VAR_PRELOAD}  s_getpc_b64 s[10:11]
 .Lpc_base:
   s_add_u32 s10, s10, .Ltab-.Lpc_base
   s_addc_u32 s11, s11, 0
@@ -1046,11 +1033,8 @@ PROLOGUE = """\
   s_mov_b64 s[66:67], -1
   s_mov_b32 s62, 0
   s_mov_b32 s63, 0x41f00000
-  s_waitcnt lgkmcnt(0)
-  s_and_b32 s12, s16, 0x3fc
-  s_add_u32 s12, s10, s12
-  s_addc_u32 s13, s11, 0
-  s_setpc_b64 s[12:13]
+  s_mov_b32 s3, 0
+{FIRST_DISPATCH}
 .Lundec:
   s_mov_b64 exec, 1
   v_mov_b32 v4, -2
@@ -1085,7 +1069,7 @@ def metadata():
         "    .private_segment_fixed_size: 0",
         "    .sgpr_count: 104",
         f"    .symbol: {KNAME}.kd",
-        "    .vgpr_count: 128",
+        "    .vgpr_count: 124",
         "    .wavefront_size: 64",
         "amdhsa.target: amdgcn-amd-amdhsa--gfx950",
         "amdhsa.version:", "  - 1", "  - 2",
@@ -1093,11 +1077,30 @@ def metadata():
     return "\n".join(out), ksize
 
 
+def var_preload() -> str:
+    """Variables 0..REG_VARS-1 -> v[64:111]; always REG_VARS x 2 loads (index clamped to
+    n_vars-1), so that vmcnt(2*REG_VARS) below waits exactly for the page and pool loads."""
+    out = []
+    for i in range(U.REG_VARS):
+        r = RV + 8 * i
+        out += [f"  s_min_u32 s94, s9, {i}", "  s_mul_i32 s94, s94, s8",
+                "  s_add_u32 s92, s6, s94", "  s_addc_u32 s93, s7, 0",
+                f"  global_load_dwordx4 v[{r}:{r + 3}], v2, s[92:93]",
+                f"  global_load_dwordx4 v[{r + 4}:{r + 7}], v3, s[92:93]"]
+    out.append(f"  s_waitcnt vmcnt({2 * U.REG_VARS})")
+    return "\n".join(out) + "\n"
+
+
 def generate() -> str:
     body = Asm()
     global A
     A = body
-    A.lines.append(PROLOGUE)
+    first = Asm()
+    global_A = A
+    globals()["A"] = first
+    tail()
+    globals()["A"] = global_A
+    A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines)))
     A.lines.append(".Ltab:")
     for name in U.HANDLERS:
         A(f"s_branch .Lh_{name}")
@@ -1130,9 +1133,9 @@ def generate() -> str:
         "  .amdhsa_system_sgpr_workgroup_id_x 1",
         "  .amdhsa_system_sgpr_workgroup_id_y 1",
         "  .amdhsa_system_vgpr_workitem_id 0",
-        "  .amdhsa_next_free_vgpr 128",
+        "  .amdhsa_next_free_vgpr 124",
         "  .amdhsa_next_free_sgpr 102",
-        "  .amdhsa_accum_offset 128",
+        "  .amdhsa_accum_offset 124",
         "  .amdhsa_reserve_vcc 1",
         "  .amdhsa_float_denorm_mode_32 3",
         "  .amdhsa_float_denorm_mode_16_64 3",

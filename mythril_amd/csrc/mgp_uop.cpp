@@ -76,9 +76,10 @@ struct Translator {
     }
     return pool_byte(it->second);
   }
+  // constants are addressed by pool index (the kernel keeps constant c in lane c)
   uint32_t pool_byte(uint32_t idx) {
-    if (idx >= 2048u) bad = true;
-    return idx * 32u;
+    if (idx >= MGP_U_MAX_POOL) bad = true;
+    return idx;
   }
   Opnd bv(uint32_t o) {
     const uint32_t kind = o >> 14, idx = o & 0x3FFFu;
@@ -288,12 +289,29 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);
     return v1_ok ? 1 : 0;
   }
-  const uint32_t n_uops = (uint32_t)(uops.size() / MGP_U_UOP_WORDS);
-  out.insert(out.end(), uops.begin(), uops.end());
-  for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);  // prefetch pad
+  if (T.pool.size() / 8 > MGP_U_MAX_POOL) {
+    out[base + 1] = 1;
+    out[base + 2] = MGP_U_HDR_WORDS * 4u;
+    for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);
+    return 1;
+  }
+  // pages of 64 uops: the last uop of every full page is PAGE (load the next page)
+  const uint32_t n_real = (uint32_t)(uops.size() / MGP_U_UOP_WORDS);
+  uint32_t n_uops = 0;
+  for (uint32_t i = 0; i < n_real; ++i) {
+    if (n_uops % MGP_U_PAGE_UOPS == MGP_U_PAGE_UOPS - 1) {
+      const uint32_t page[4] = {(uint32_t)MGP_U_PAGE << 2 | (uint32_t)MGP_U_PAGE << 10, 0, 0, 0};
+      out.insert(out.end(), page, page + 4);
+      ++n_uops;
+    }
+    out.insert(out.end(), uops.begin() + (size_t)i * 4, uops.begin() + (size_t)i * 4 + 4);
+    ++n_uops;
+  }
+  for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);  // zero pad: INVALID
   out[base + 0] = n_uops;
   out[base + 1] = 0;
   out[base + 2] = (uint32_t)((MGP_U_HDR_WORDS + (n_uops + 1) * MGP_U_UOP_WORDS) * 4u);
+  out[base + 3] = (uint32_t)(T.pool.size() / 8);
   out.insert(out.end(), T.pool.begin(), T.pool.end());
   return 0;
 }

@@ -8,11 +8,14 @@ Program layout (per state, appended after the v1 bytecode of include/mgp_ir.h,
 at word offset align4(4 + 4*n_ins + 8*n_consts) + 4 from the program start):
 
   header   4 words: n_uops, status (0 = runnable), pool byte offset (from the
-           uop header), 0
-  uops     n_uops x 4 words, then one all-zero uop (the kernel prefetches one
-           uop ahead)
-  pool     constants, 8 little-endian u32 limbs each (the v1 pool followed by
-           the width masks 2^w-1 and sign constants 2^(w-1) the uops use)
+           uop header), n_pool
+  uops     n_uops x 4 words in pages of 64: uop 63 of every full page is PAGE
+           (the kernel holds one page in 4 VGPRs, uop k in lane k, and reads
+           the current uop with v_readlane; PAGE loads the next page), then one
+           all-zero uop
+  pool     n_pool <= 64 constants, 8 little-endian u32 limbs each (the v1 pool
+           followed by the width masks 2^w-1 and sign constants 2^(w-1) the uops
+           use); constant c lives in lane c of 8 VGPRs (limb l in the l-th)
 
 uop words:
   w0 [9:0]   byte offset of the FIRST handler in the dispatch table (id*4):
@@ -26,9 +29,9 @@ uop words:
      [29:27]      division variant (DIV_*)
   w1 [15:0] operand A parameter, [31:16] operand B parameter
             SLOT: LDS byte offset (slot*2048), VAR / RVAR: variable index,
-            CONST: pool byte offset; Bool operands: bool slot * 2
-  w2 [15:0] store slot byte offset / third Bool operand * 2, [31:16] mask pool byte offset
-  w3 [15:0] sign-constant pool byte offset, [31:16] Bool destination * 2 (compares, Bool ops)
+            CONST: pool index; Bool operands: bool slot * 2
+  w2 [15:0] store slot byte offset / third Bool operand * 2, [31:16] mask pool index
+  w3 [15:0] sign-constant pool index, [31:16] Bool destination * 2 (compares, Bool ops)
             or ITE condition * 2
 
 Registers of the interpreter: vA (accumulator / operand A), vB (operand B),
@@ -38,16 +41,16 @@ vC (operand A of a compare that is not the accumulator); Bool slots are
 
 # operand kinds: acc = the accumulator vA, slot = per-lane LDS slot, var = candidate
 # variable loaded from HBM, const = constant pool (scalar load), rvar = candidate
-# variable 0..REG_VARS-1 preloaded into v[64:127] at wave start (v_movrels)
+# variable 0..REG_VARS-1 preloaded into v[64:111] at wave start (GPR-index moves)
 KINDS = ("acc", "slot", "var", "const", "rvar")
-REG_VARS = 8
+REG_VARS = 6
 B_KINDS = ("none",) + KINDS
 
 # fetch handlers: F_<kindA>_<kindB>_<target of A>; A = acc with target C never occurs
 FETCH = [f"F_{ka}_{kb}_A" for ka in KINDS for kb in B_KINDS] + \
         [f"F_{ka}_{kb}_C" for ka in KINDS[1:] for kb in B_KINDS]
 
-BOOL_OPS = ["RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ"]
+BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ"]
 BV_BIN = ["ADD", "SUB", "MUL", "AND", "OR", "XOR", "SHL", "LSHR", "ASHR", "DIV"]
 BV_UN = ["NOT", "NEG", "MOV", "SEXT"]
 SHIFT_I = [f"SHLI{k}" for k in range(9)] + [f"LSHRI{k}" for k in range(9)] + [f"ASHRI{k}" for k in range(9)]
@@ -72,6 +75,8 @@ MAX_LDS_SLOTS = 31       # slot byte offsets must fit 16 bits with the +1024 hal
 SLOT_BYTES = 2048        # 64 lanes x 32 B
 HDR_WORDS = 4
 UOP_WORDS = 4
+PAGE_UOPS = 64           # uops per VGPR page (one per lane); the last one is PAGE
+MAX_POOL = 64            # constants per state (one per lane)
 
 
 def c_header() -> str:
@@ -88,6 +93,7 @@ def c_header() -> str:
         f"#define MGP_U_BOOL_SLOTS {BOOL_SLOTS}", f"#define MGP_U_MAX_LDS_SLOTS {MAX_LDS_SLOTS}",
         f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",
         f"#define MGP_U_UOP_WORDS {UOP_WORDS}", f"#define MGP_U_REG_VARS {REG_VARS}",
-        f"#define MGP_U_N_KINDS {len(KINDS)}",
+        f"#define MGP_U_N_KINDS {len(KINDS)}", f"#define MGP_U_PAGE_UOPS {PAGE_UOPS}",
+        f"#define MGP_U_MAX_POOL {MAX_POOL}",
     ]
     return "\n".join(lines) + "\n"

@@ -60,8 +60,11 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         return None
     pool0 = u0 + pool_bytes // 4
 
-    def pool(byte_off: int) -> int:
-        return _limbs(words, pool0 + byte_off // 4)
+    n_pool = int(words[u0 + 3])
+
+    def pool(idx: int) -> int:
+        assert idx < n_pool
+        return _limbs(words, pool0 + 8 * idx)
 
     vA = vB = vC = 0
     KM = KH = 0
@@ -78,6 +81,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
 
     for pc in range(n_uops):
         w0, w1, w2, w3 = (int(words[u0 + 4 + 4 * pc + k]) for k in range(4))
+        assert (pc % U.PAGE_UOPS == U.PAGE_UOPS - 1) == ((w0 & 0x3FF) >> 2 == U.ID["PAGE"]), "page layout"
         first = _NAME[(w0 & 0x3FF) >> 2]
         op = _NAME[(w0 >> 10) & 0xFF]
         pa, pb = w1 & 0xFFFF, w1 >> 16
@@ -97,6 +101,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         else:
             op = first
         sb = (w0 >> U.SHIFT_B_POS) & 31
+        if op == "PAGE":
+            assert pc % U.PAGE_UOPS == U.PAGE_UOPS - 1, "PAGE must end a 64-uop page"
+            continue
         if op in U.BOOL_OPS:
             a, b, c = bools[pa >> 1], bools[pb >> 1], bools[(w2 & 0xFFFF) >> 1]
             if op == "RET":

@@ -188,3 +188,44 @@ def test_keccak_lengths_vs_oracle(mgp_ctx, length):
     ref = coracle.keccak256(data, n, length, stride)
     assert (out == ref).all()
     assert out[5].tobytes() == keccak_py(data[5 * stride:5 * stride + length].tobytes())
+
+
+def _long_program(rng, n_ops, n_vars, n_consts):
+    """A random chain DAG of n_ops BV ops over n_vars variables and n_consts constants."""
+    nl = [[S.VAR, 256, -1, -1, -1, v, 0] for v in range(n_vars)]
+    consts = [int(rng.integers(1, 2 ** 62)) << int(rng.integers(0, 190)) for _ in range(n_consts)]
+    nl += [[S.CONST, 256, -1, -1, -1, c, 0] for c in range(n_consts)]
+    leaves = list(range(len(nl)))
+    ops = [S.ADD, S.SUB, S.XOR, S.MUL, S.AND, S.OR, S.LSHR, S.UREM]
+    t = 0
+    live = []
+    for i in range(n_ops):
+        op = ops[int(rng.integers(0, len(ops)))]
+        b = leaves[int(rng.integers(0, len(leaves)))] if (i % 3 or not live) else live[int(rng.integers(0, len(live)))]
+        nl.append([op, 256, t, b, -1, 0, 0])
+        t = len(nl) - 1
+        if i % 7 == 0:
+            live.append(t)
+    # root: OR of (t == var0) and an ULT over a kept intermediate, so a random candidate is SAT ~50%
+    nl.append([S.EQ, 1, t, 0, -1, 0, 0])
+    nl.append([S.ULT, 1, live[-1], t, -1, 0, 0])
+    nl.append([S.BOR, 1, len(nl) - 2, len(nl) - 1, -1, 0, 0])
+    return nl, consts
+
+
+@pytest.mark.parametrize("n_ops,n_vars,n_consts", [(150, 3, 4), (300, 9, 40), (70, 7, 70)])
+def test_long_programs_many_vars_and_constants(mgp_ctx, n_ops, n_vars, n_consts):
+    """Programs past one 64-uop page, variables beyond the 6 register-resident ones (HBM
+    operands) and constant pools up to and past the 64-entry limit (past it: undecided)."""
+    rng = np.random.default_rng(n_ops + n_vars)
+    states = [_long_program(rng, n_ops, n_vars, n_consts) for _ in range(12)]
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    cands = random_cands(rng, len(states), 64, n_vars, interesting_frac=0.1)
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    want = coracle.first_sat(nodes, noff, consts, coff, cands)
+    ok = status == 0
+    assert np.array_equal(first[ok], want[ok])
+    assert (first[~ok] == N.MGP_UNDECIDED).all()
+    if n_consts <= 60:
+        assert ok.all()

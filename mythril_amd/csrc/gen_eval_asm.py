@@ -62,6 +62,7 @@ class Asm:
     def __init__(self):
         self.lines = []
         self.n = 0
+        self.ool = []   # out-of-line blocks of the current handler (rare paths), emitted after it
 
     def __call__(self, *ins):
         for x in ins:
@@ -77,31 +78,53 @@ class Asm:
     def comment(self, text):
         self.lines.append(f"  // {text}")
 
+    def out_of_line(self, label, body):
+        """Emit `body` (a callable) as a block after the handler; the common path falls through."""
+        self.ool.append((label, body))
+
+    def flush_ool(self):
+        while self.ool:
+            label, body = self.ool.pop(0)
+            self.lines.append(f"{label}:")
+            body()
+
 
 A = Asm()
 
 # ---------------------------------------------------------------- helpers
 
 
-def tail():
-    """Read the next uop from the VGPR page (lane s3) and dispatch it."""
-    A("v_readlane_b32 s16, v112, s3",
-      "v_readlane_b32 s17, v113, s3",
-      "v_readlane_b32 s18, v114, s3",
-      "v_readlane_b32 s19, v115, s3",
+def prefetch_next():
+    """At handler entry: read the next uop (lane s3 of the page) into N = s[20:23] and its
+    first handler address into s[0:1], so the v_readlane -> SALU latency overlaps the body."""
+    A("v_readlane_b32 s20, v112, s3",
+      "v_readlane_b32 s21, v113, s3",
+      "v_readlane_b32 s22, v114, s3",
+      "v_readlane_b32 s23, v115, s3",
       "s_add_u32 s3, s3, 1",
-      "s_and_b32 s12, s16, 0x3fc",
+      "s_and_b32 s0, s20, 0xffff",
+      "s_lshl_b32 s0, s0, 2",
+      "s_add_u32 s0, s10, s0",
+      "s_addc_u32 s1, s11, 0")
+
+
+def tail():
+    """Make the prefetched uop current and jump to its first handler."""
+    A("s_mov_b64 s[16:17], s[20:21]",
+      "s_mov_b64 s[18:19], s[22:23]",
+      "s_setpc_b64 s[0:1]")
+
+
+def op_target():
+    """s[12:13] <- address of the op handler (w0[31:16] * 4 from the kernel base)."""
+    A("s_lshr_b32 s12, s16, 16",
+      "s_lshl_b32 s12, s12, 2",
       "s_add_u32 s12, s10, s12",
-      "s_addc_u32 s13, s11, 0",
-      "s_setpc_b64 s[12:13]")
+      "s_addc_u32 s13, s11, 0")
 
 
 def op_dispatch():
-    A("s_lshr_b32 s12, s16, 8",
-      "s_and_b32 s12, s12, 0x3fc",
-      "s_add_u32 s12, s10, s12",
-      "s_addc_u32 s13, s11, 0",
-      "s_setpc_b64 s[12:13]")
+    A("s_setpc_b64 s[12:13]")
 
 
 def bool_read(field_sreg, shift, dst_pair):
@@ -236,27 +259,48 @@ def wait_operands():
     A("s_waitcnt vmcnt(0) lgkmcnt(0)")
 
 
-def bv_epilogue():
-    lm, ls = A.fresh("nomask"), A.fresh("nostore")
-    A("s_bitcmp1_b32 s16, 19", f"s_cbranch_scc0 {lm}")
-    for i in range(8):
-        A(f"v_and_b32 {v(VA + i)}, {s(S_KM + i)}, {v(VA + i)}")
-    A.label(lm)
-    A("s_bitcmp1_b32 s16, 18", f"s_cbranch_scc0 {ls}",
-      "s_and_b32 s48, s18, 0xffff",
+# uop flag bits (w2 = s18, w3 = s19; see uop_spec)
+B_STORE, B_MASK, B_SEXT, B_INVERT = 22, 23, 24, 25
+
+
+def store_slot():
+    A("s_and_b32 s48, s18, 0xffff",
       "v_add_u32 v4, s48, v1",
       f"ds_write_b128 v4, {vr(VA, 4)}",
       f"ds_write_b128 v4, {vr(VA + 4, 4)} offset:1024")
-    A.label(ls)
+
+
+def bv_epilogue():
+    """[mask] [store] then dispatch; unmasked results fall straight through to the tail."""
+    lm, ls = A.fresh("mask"), A.fresh("store")
+    A(f"s_bitcmp1_b32 s18, {B_MASK}", f"s_cbranch_scc1 {lm}",
+      f"s_bitcmp1_b32 s18, {B_STORE}", f"s_cbranch_scc1 {ls}")
     tail()
+
+    def masked():
+        for i in range(8):
+            A(f"v_and_b32 {v(VA + i)}, {s(S_KM + i)}, {v(VA + i)}")
+        A(f"s_bitcmp1_b32 s18, {B_STORE}", f"s_cbranch_scc1 {ls}")
+        tail()
+
+    def stored():
+        store_slot()
+        tail()
+    A.out_of_line(lm, masked)
+    A.out_of_line(ls, stored)
 
 
 def cmp_epilogue():
-    li = A.fresh("noinv")
-    A("s_bitcmp1_b32 s16, 21", f"s_cbranch_scc0 {li}", "s_not_b64 vcc, vcc")
-    A.label(li)
+    li = A.fresh("inv")
+    A(f"s_bitcmp1_b32 s18, {B_INVERT}", f"s_cbranch_scc1 {li}")
     bool_write("vcc")
     tail()
+
+    def inverted():
+        A("s_not_b64 vcc, vcc")
+        bool_write("vcc")
+        tail()
+    A.out_of_line(li, inverted)
 
 
 def write_partial_and_end(value_sreg):
@@ -316,19 +360,30 @@ def make_fetch(name):
     _, ka, kb, tgt = name.split("_")
 
     def body():
-        l1, l2 = A.fresh("nokm"), A.fresh("nokh")
-        A("s_bitcmp1_b32 s16, 19", f"s_cbranch_scc0 {l1}", "s_lshr_b32 s48, s18, 16")
-        for i in range(8):
-            A(f"v_readlane_b32 {s(S_KM + i)}, {v(PQ + i)}, s48")
-        A.label(l1)
-        A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {l2}", "s_and_b32 s49, s19, 0xffff")
-        for i in range(8):
-            A(f"v_readlane_b32 {s(S_KH + i)}, {v(PQ + i)}, s49")
-        A.label(l2)
+        op_target()
+        lk, lh, back_k, back_h = A.fresh("km"), A.fresh("kh"), A.fresh("kmback"), A.fresh("khback")
+        A(f"s_bitcmp1_b32 s18, {B_MASK}", f"s_cbranch_scc1 {lk}")
+        A.label(back_k)
+        A(f"s_bitcmp1_b32 s18, {B_SEXT}", f"s_cbranch_scc1 {lh}")
+        A.label(back_h)
         if kb != "none":
             fetch_one(kb, VB, "B")
         fetch_one(ka, VA if tgt == "A" else VC, "A")
         op_dispatch()
+
+        def km():
+            A(f"s_bfe_u32 s48, s18, {(6 << 16) | 16:#x}")
+            for i in range(8):
+                A(f"v_readlane_b32 {s(S_KM + i)}, {v(PQ + i)}, s48")
+            A(f"s_branch {back_k}")
+
+        def kh():
+            A("s_and_b32 s49, s19, 0x3f")
+            for i in range(8):
+                A(f"v_readlane_b32 {s(S_KH + i)}, {v(PQ + i)}, s49")
+            A(f"s_branch {back_h}")
+        A.out_of_line(lk, km)
+        A.out_of_line(lh, kh)
     return body
 
 
@@ -339,15 +394,17 @@ for _f in U.FETCH:
 # ---- program paging
 @handler("PAGE")
 def h_page():
-    # next 64 uops: lane k loads uop min(k, remaining-1) of the next page into v[112:115]
+    # next 64 uops: lane k loads uop min(k, remaining) of the next page into v[112:115]
+    # (s2 = uops left from the page start; index `remaining` is the INVALID pad)
     A("s_add_u32 s4, s4, 0x400", "s_addc_u32 s5, s5, 0",
-      "s_sub_u32 s20, s20, 64",
-      "v_min_u32 v4, s20, v0",
+      "s_sub_u32 s2, s2, 64",
+      "v_min_u32 v4, s2, v0",
       "v_lshlrev_b32 v4, 4, v4",
       "s_waitcnt vmcnt(0)",
       "global_load_dwordx4 v[112:115], v4, s[4:5]",
       "s_waitcnt vmcnt(0)",
       "s_mov_b32 s3, 0")
+    prefetch_next()
     tail()
 
 
@@ -485,7 +542,7 @@ def h_sext():
 
 def maybe_sext_A():
     l = A.fresh("nosx")
-    A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {l}")
+    A(f"s_bitcmp1_b32 s18, {B_SEXT}", f"s_cbranch_scc0 {l}")
     sext_inplace(VA)
     A.label(l)
 
@@ -529,7 +586,7 @@ HBODY["ASHR"] = h_shr(True)
 
 
 def uniform_b():
-    A(f"s_bfe_u32 s48, s16, {(5 << 16) | U.SHIFT_B_POS:#x}")
+    A(f"s_bfe_u32 s48, s19, {(5 << 16) | U.SHIFT_B_POS:#x}")
 
 
 def shli_body(k, regs_base=VA):
@@ -655,7 +712,7 @@ def make_cmp(base, xreg):
             ult_chain(x, y)
         elif base in ("SLT", "SGT"):
             lsx, ldone = A.fresh("sx"), A.fresh("cmpdone")
-            A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc1 {lsx}")
+            A(f"s_bitcmp1_b32 s18, {B_SEXT}", f"s_cbranch_scc1 {lsx}")
             x, y = (X, Y) if base == "SLT" else (Y, X)
             slt_chain(x, y)
             A(f"s_branch {ldone}")
@@ -793,12 +850,12 @@ def knuth_digit(J):
 def h_div():
     wait_operands()
     maybe_sext_op = A.fresh("nosxd")
-    A("s_bitcmp1_b32 s16, 20", f"s_cbranch_scc0 {maybe_sext_op}")
+    A(f"s_bitcmp1_b32 s18, {B_SEXT}", f"s_cbranch_scc0 {maybe_sext_op}")
     sext_inplace(VA)
     sext_inplace(VB)
     A.label(maybe_sext_op)
     lus, lsd = A.fresh("udiv"), A.fresh("sdone")
-    A(f"s_bfe_u32 s61, s16, {(3 << 16) | U.DIVOP_POS:#x}",
+    A(f"s_bfe_u32 s61, s18, {(3 << 16) | U.DIVOP_POS:#x}",
       "s_cmp_lt_u32 s61, 2", f"s_cbranch_scc1 {lus}",
       f"v_ashrrev_i32 v24, 31, {v(VA + 7)}",
       f"v_ashrrev_i32 v25, 31, {v(VB + 7)}")
@@ -991,8 +1048,7 @@ PROLOGUE = """\
   s_addc_u32 s15, s85, 0
   s_add_u32 s4, s84, 16
   s_addc_u32 s5, s85, 0
-  s_sub_u32 s20, s88, 1
-  s_mov_b32 s21, s91
+  s_mov_b32 s2, s88
   // candidates of this state: cands + state * n_vars * n_cand * 32, layout [var][half][cand] x 16 B
   s_lshl_b32 s8, s75, 5
   s_mul_i32 s92, s76, s8
@@ -1011,24 +1067,25 @@ PROLOGUE = """\
   s_lshl_b32 s92, s75, 4
   v_add_u32 v3, s92, v2
   v_lshlrev_b32 v1, 4, v0
-  // uop page 0 -> v[112:115] (lane k = uop min(k, n_uops-1)); pool -> v[116:123] (lane c = constant
+  // uop page 0 -> v[112:115] (lane k = uop min(k, n_uops): lanes past the end hold the INVALID pad); pool -> v[116:123] (lane c = constant
   // min(c, n_pool-1)); both issued before the variable loads so that vmcnt(12) covers them
-  v_min_u32 v4, s20, v0
+  v_min_u32 v4, s2, v0
   v_lshlrev_b32 v4, 4, v4
   global_load_dwordx4 v[112:115], v4, s[4:5]
-  s_cmp_eq_u32 s21, 0
+  s_cmp_eq_u32 s91, 0
   s_cbranch_scc1 .Lno_pool
-  s_sub_u32 s92, s21, 1
+  s_sub_u32 s92, s91, 1
   v_min_u32 v4, s92, v0
   v_lshlrev_b32 v4, 5, v4
   global_load_dwordx4 v[116:119], v4, s[14:15]
   global_load_dwordx4 v[120:123], v4, s[14:15] offset:16
 .Lno_pool:
   // preload variables 0..min(n_vars, 6)-1 of this lane's candidate into v[64:111]
-{VAR_PRELOAD}  s_getpc_b64 s[10:11]
+{VAR_PRELOAD}  // s[10:11] = kernel entry address: uops hold handler offsets / 4 from it
+  s_getpc_b64 s[10:11]
 .Lpc_base:
-  s_add_u32 s10, s10, .Ltab-.Lpc_base
-  s_addc_u32 s11, s11, 0
+  s_sub_u32 s10, s10, .Lpc_base-mgp_eval_gfx950
+  s_subb_u32 s11, s11, 0
   s_mov_b64 s[64:65], 0
   s_mov_b64 s[66:67], -1
   s_mov_b32 s62, 0
@@ -1098,17 +1155,17 @@ def generate() -> str:
     first = Asm()
     global_A = A
     globals()["A"] = first
+    prefetch_next()
     tail()
     globals()["A"] = global_A
     A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines)))
-    A.lines.append(".Ltab:")
+    no_prefetch = set(U.FETCH) | {"INVALID", "RET", "PAGE"}
     for name in U.HANDLERS:
-        A(f"s_branch .Lh_{name}")
-    for _ in range(256 - len(U.HANDLERS)):
-        A("s_branch .Lh_INVALID")
-    for name in U.HANDLERS:
-        A.lines.append(f".Lh_{name}:")
+        A.lines.append(f".p2align 2\nmgp_h_{name}:")
+        if name not in no_prefetch:
+            prefetch_next()
         HBODY[name]()
+        A.flush_ool()
     md, ksize = metadata()
     head = [
         '.amdgcn_target "amdgcn-amd-amdhsa--gfx950"',

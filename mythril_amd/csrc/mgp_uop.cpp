@@ -25,6 +25,14 @@
 
 #include "../../include/mgp_ir.h"
 #include "mgp_uop.h"
+#include "mgp_uop_off.h"
+
+// handler entry offsets (/4, from the kernel entry) by handler id; exported for the
+// CPU reference interpreter of the encoding (oracle/uop_ref.py)
+extern "C" const uint16_t *mgp_uop_handler_offsets(uint32_t *n) {
+  if (n) *n = MGP_U_N_HANDLERS;
+  return kUopHandlerOffset;
+}
 
 namespace {
 
@@ -110,7 +118,10 @@ struct Translator {
   }
 };
 
-inline uint32_t w0_of(uint32_t first, uint32_t op, uint32_t flags) { return (first << 2) | (op << 10) | flags; }
+// w0 = entry offsets of the first handler and of the op handler (fetch handlers jump to it)
+inline uint32_t w0_of(uint32_t first, uint32_t op) {
+  return (uint32_t)kUopHandlerOffset[first] | ((uint32_t)kUopHandlerOffset[op] << 16);
+}
 
 }  // namespace
 
@@ -139,13 +150,13 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     const bool narrow = width < 256u;
 
     if (op == MGP_OP_RET) {
-      emit(w0_of(MGP_U_RET, MGP_U_RET, 0), T.boolslot(oa), 0, 0);
+      emit(w0_of(MGP_U_RET, MGP_U_RET), T.boolslot(oa), 0, 0);
       break;
     }
     if (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) {
       static const uint32_t ids[] = {MGP_U_BAND, MGP_U_BOR, MGP_U_BXOR, MGP_U_BNOT, MGP_U_BITE, MGP_U_BEQ};
       const uint32_t id = ids[op - MGP_OP_BAND];
-      emit(w0_of(id, id, 0), T.boolslot(oa) | (T.boolslot(ob) << 16), T.boolslot(oc), T.boolslot(dst) << 16);
+      emit(w0_of(id, id), T.boolslot(oa) | (T.boolslot(ob) << 16), T.boolslot(oc), T.boolslot(dst) << 16);
       continue;
     }
     if (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) {
@@ -186,7 +197,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       const bool ra = a.kind == KACC;
       const uint32_t opid = ra ? base : base + 1u;  // _RC follows _RA
       const uint32_t first = fetch_id(a.kind, b.kind, !ra);
-      emit(w0_of(first, opid, flags), (ra ? 0u : a.param) | (b.param << 16), w2, w3);
+      emit(w0_of(first, opid), (ra ? 0u : a.param) | (b.param << 16), w2 | flags, w3);
       continue;
     }
     // ---- BV-producing
@@ -213,7 +224,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           T.const_value(ob, &lo, &big);
           const uint32_t k = big ? 8u : lo >> 5, sb = big ? 0u : lo & 31u;
           opid = (op == MGP_OP_SHL ? MGP_U_SHLI0 : op == MGP_OP_LSHR ? MGP_U_LSHRI0 : MGP_U_ASHRI0) + k;
-          flags |= sb << MGP_U_SHIFT_B_POS;
+          w3 |= sb << MGP_U_SHIFT_B_POS;
         } else {
           b = T.bv(ob);
           opid = op == MGP_OP_SHL ? MGP_U_SHL : op == MGP_OP_LSHR ? MGP_U_LSHR : MGP_U_ASHR;
@@ -248,7 +259,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           opid = MGP_U_MOV;
         } else {
           opid = MGP_U_LSHRI0 + (imm >> 5);
-          flags |= (imm & 31u) << MGP_U_SHIFT_B_POS;
+          w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
         }
         need_mask = narrow;
         break;
@@ -259,7 +270,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         a = T.bv(oa); b = T.bv(ob);
         if (imm == 0 || imm >= 256u) { T.bad = true; break; }
         opid = MGP_U_CONCAT0 + (imm >> 5);
-        flags |= (imm & 31u) << MGP_U_SHIFT_B_POS;
+        w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
         break;
       case MGP_OP_ITE:
         a = T.bv(ob); b = T.bv(oc); opid = MGP_U_ITE;
@@ -279,7 +290,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       w2 |= dst * MGP_U_SLOT_BYTES;
     }
     const uint32_t first = fetch_id(a.kind, b.kind, false);
-    emit(w0_of(first, opid, flags), a.param | (b.param << 16), w2, w3);
+    emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
   }
 
   if (!v1_ok || T.bad || uops.empty()) {
@@ -300,14 +311,15 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   uint32_t n_uops = 0;
   for (uint32_t i = 0; i < n_real; ++i) {
     if (n_uops % MGP_U_PAGE_UOPS == MGP_U_PAGE_UOPS - 1) {
-      const uint32_t page[4] = {(uint32_t)MGP_U_PAGE << 2 | (uint32_t)MGP_U_PAGE << 10, 0, 0, 0};
+      const uint32_t page[4] = {w0_of(MGP_U_PAGE, MGP_U_PAGE), 0, 0, 0};
       out.insert(out.end(), page, page + 4);
       ++n_uops;
     }
     out.insert(out.end(), uops.begin() + (size_t)i * 4, uops.begin() + (size_t)i * 4 + 4);
     ++n_uops;
   }
-  for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);  // zero pad: INVALID
+  const uint32_t pad[4] = {w0_of(MGP_U_INVALID, MGP_U_INVALID), 0, 0, 0};  // ends a runaway program
+  out.insert(out.end(), pad, pad + 4);
   out[base + 0] = n_uops;
   out[base + 1] = 0;
   out[base + 2] = (uint32_t)((MGP_U_HDR_WORDS + (n_uops + 1) * MGP_U_UOP_WORDS) * 4u);

@@ -18,21 +18,22 @@ at word offset align4(4 + 4*n_ins + 8*n_consts) + 4 from the program start):
            use); constant c lives in lane c of 8 VGPRs (limb l in the l-th)
 
 uop words:
-  w0 [9:0]   byte offset of the FIRST handler in the dispatch table (id*4):
-             a fetch handler for BV/compare uops, the op handler otherwise
-     [17:10] op handler id (fetch handlers jump to it)
-     [18] STORE   result -> LDS slot (w2[15:0] = slot byte offset)
-     [19] MASK    result &= pool[w2[31:16]] (2^w - 1)
-     [20] SEXT    operands sign-extended from width w with H = pool[w3[15:0]]
-     [21] INVERT  compare result negated
-     [26:22]      uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT)
-     [29:27]      division variant (DIV_*)
+  w0 [15:0]  entry offset / 4 (from the kernel entry) of the FIRST handler: a fetch
+             handler for BV/compare uops, the op handler otherwise
+     [31:16] entry offset / 4 of the op handler (fetch handlers jump to it)
+             (offsets come from the assembled kernel's symbol table, gen_offsets.py)
   w1 [15:0] operand A parameter, [31:16] operand B parameter
             SLOT: LDS byte offset (slot*2048), VAR / RVAR: variable index,
             CONST: pool index; Bool operands: bool slot * 2
-  w2 [15:0] store slot byte offset / third Bool operand * 2, [31:16] mask pool index
-  w3 [15:0] sign-constant pool index, [31:16] Bool destination * 2 (compares, Bool ops)
-            or ITE condition * 2
+  w2 [15:0] store slot byte offset / third Bool operand * 2
+     [21:16] mask pool index
+     [22] STORE   result -> LDS slot
+     [23] MASK    result &= pool[mask] (2^w - 1); compares: M for the overflow tests
+     [24] SEXT    operands sign-extended from width w with H = pool[w3[5:0]]
+     [25] INVERT  compare result negated
+     [28:26]      division variant (DIV_*)
+  w3 [5:0]  sign-constant pool index, [12:8] uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT),
+     [31:16] Bool destination * 2 (compares, Bool ops) or ITE condition * 2
 
 Registers of the interpreter: vA (accumulator / operand A), vB (operand B),
 vC (operand A of a compare that is not the accumulator); Bool slots are
@@ -67,8 +68,9 @@ assert len(HANDLERS) < 256
 
 DIV_VARIANTS = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
 
-F_STORE, F_MASK, F_SEXT, F_INVERT = 1 << 18, 1 << 19, 1 << 20, 1 << 21
-SHIFT_B_POS, DIVOP_POS = 22, 27
+F_STORE, F_MASK, F_SEXT, F_INVERT = 1 << 22, 1 << 23, 1 << 24, 1 << 25   # in w2
+SHIFT_B_POS = 8     # in w3
+DIVOP_POS = 26      # in w2
 
 BOOL_SLOTS = 19          # 0 false, 1 true, 2..18 allocatable
 MAX_LDS_SLOTS = 31       # slot byte offsets must fit 16 bits with the +1024 half

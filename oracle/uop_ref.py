@@ -16,7 +16,25 @@ from mythril_amd import uop_spec as U
 from . import bvsem as S
 
 M256 = (1 << 256) - 1
-_NAME = {i: n for n, i in U.ID.items()}
+_NAME_BY_OFF = None
+
+
+def _names():
+    """handler entry offset (w0 fields) -> handler name, from the built library."""
+    global _NAME_BY_OFF
+    if _NAME_BY_OFF is None:
+        import ctypes
+
+        from mythril_amd import _native as N
+
+        fn = N.lib().mgp_uop_handler_offsets
+        fn.restype = ctypes.POINTER(ctypes.c_uint16)
+        fn.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+        n = ctypes.c_uint32()
+        p = fn(ctypes.byref(n))
+        assert n.value == len(U.HANDLERS)
+        _NAME_BY_OFF = {p[i]: U.HANDLERS[i] for i in range(n.value)}
+    return _NAME_BY_OFF
 
 
 def _limbs(words, off) -> int:
@@ -81,16 +99,17 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
 
     for pc in range(n_uops):
         w0, w1, w2, w3 = (int(words[u0 + 4 + 4 * pc + k]) for k in range(4))
-        assert (pc % U.PAGE_UOPS == U.PAGE_UOPS - 1) == ((w0 & 0x3FF) >> 2 == U.ID["PAGE"]), "page layout"
-        first = _NAME[(w0 & 0x3FF) >> 2]
-        op = _NAME[(w0 >> 10) & 0xFF]
+        assert (pc % U.PAGE_UOPS == U.PAGE_UOPS - 1) == (_names()[w0 & 0xFFFF] == "PAGE"), "page layout"
+        names = _names()
+        first = names[w0 & 0xFFFF]
+        op = names[w0 >> 16]
         pa, pb = w1 & 0xFFFF, w1 >> 16
         if first.startswith("F_"):
             _, ka, kb, tgt = first.split("_")
-            if w0 & U.F_MASK:
-                KM = pool(w2 >> 16)
-            if w0 & U.F_SEXT:
-                KH = pool(w3 & 0xFFFF)
+            if w2 & U.F_MASK:
+                KM = pool((w2 >> 16) & 0x3F)
+            if w2 & U.F_SEXT:
+                KH = pool(w3 & 0x3F)
             if kb != "none":
                 vB = vA if kb == "acc" else load(kb, pb)
             if ka != "acc":
@@ -100,7 +119,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
                     vC = load(ka, pa)
         else:
             op = first
-        sb = (w0 >> U.SHIFT_B_POS) & 31
+        sb = (w3 >> U.SHIFT_B_POS) & 31
         if op == "PAGE":
             assert pc % U.PAGE_UOPS == U.PAGE_UOPS - 1, "PAGE must end a 64-uop page"
             continue
@@ -116,7 +135,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
             base = op[:-3]
             X = vA if op.endswith("_RA") else vC
             Y = vB
-            if w0 & U.F_SEXT:
+            if w2 & U.F_SEXT:
                 X, Y = _sext(X, KH), _sext(Y, KH)
             if base == "EQ":
                 raw = X == Y
@@ -139,7 +158,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
                 raw = (p >> 256) != 0 or (p & M256) > KM
             else:
                 raise ValueError(op)
-            bools[w3 >> 17] = bool(raw) != bool(w0 & U.F_INVERT)
+            bools[w3 >> 17] = bool(raw) != bool(w2 & U.F_INVERT)
             continue
         # BV-producing
         if op == "ITE":
@@ -154,14 +173,14 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
             elif op == "LSHR":
                 vA >>= s
             else:
-                if w0 & U.F_SEXT:
+                if w2 & U.F_SEXT:
                     vA = _sext(vA, KH)
                 vA = (_s256(vA) >> s) & M256
         elif op == "DIV":
             a, b = vA, vB
-            if w0 & U.F_SEXT:
+            if w2 & U.F_SEXT:
                 a, b = _sext(a, KH), _sext(b, KH)
-            vA = _div((w0 >> U.DIVOP_POS) & 7, a, b) & M256
+            vA = _div((w2 >> U.DIVOP_POS) & 7, a, b) & M256
         elif op == "NOT":
             vA = ~vA & M256
         elif op == "NEG":
@@ -178,7 +197,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
             elif op.startswith("LSHRI"):
                 vA >>= s
             else:
-                if w0 & U.F_SEXT:
+                if w2 & U.F_SEXT:
                     vA = _sext(vA, KH)
                 vA = (_s256(vA) >> s) & M256
         elif op.startswith("CONCAT"):
@@ -186,9 +205,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
             vA = ((vA << (32 * k + sb)) & M256) | vB
         else:
             raise ValueError(op)
-        if w0 & U.F_MASK:
+        if w2 & U.F_MASK:
             vA &= KM
-        if w0 & U.F_STORE:
+        if w2 & U.F_STORE:
             lds[w2 & 0xFFFF] = vA
     raise ValueError("uop program fell off the end without RET")
 

@@ -2,10 +2,12 @@
 
 The kernel is generated (mythril_amd/csrc/gen_eval_asm.py); these checks make
 properties the GPU run depends on hold by construction:
-  * every branch inside a handler is a forward branch, so each uop finishes
-    and the only loop is the dispatch, which advances the uop pointer each time
-    (a wave always reaches RET or the INVALID handler of the zero pad);
-  * the dispatch table has 256 entries, so no 8-bit handler id can jump outside it;
+  * every branch inside a handler is a forward branch (or the return from an
+    out-of-line rare path to the point right after the branch into it), so each
+    uop finishes and the only loop is the dispatch, which advances the uop
+    index each time (a wave always reaches RET or the INVALID pad uop);
+  * every handler the translator can name is a symbol of the object, at the
+    offsets the library's translator uses;
   * no scalar-memory writes anywhere (results go out through vector stores);
   * 64-bit VGPR operands are even-aligned (gfx950 register-tuple rule);
   * the file assembles for gfx950 with the ROCm LLVM assembler.
@@ -37,8 +39,7 @@ def test_branches_are_forward(asm):
         m = re.match(r"^(\.L\w+):", l)
         if m:
             pos[m.group(1)] = i
-    table = pos[".Ltab"]
-    n_branches = 0
+    n_branches = n_back = 0
     for i, l in enumerate(lines):
         m = re.match(r"^\s+s_(?:c?branch\w*)\s+(\.L\w+)", l)
         if not m:
@@ -46,17 +47,35 @@ def test_branches_are_forward(asm):
         n_branches += 1
         tgt = m.group(1)
         assert tgt in pos, f"undefined label {tgt}"
-        assert pos[tgt] > i or (i > table and tgt.startswith(".Lh_") and i < table + 257), \
-            f"backward branch at line {i}: {l.strip()}"
-    assert n_branches > 300
+        if pos[tgt] > i:
+            continue
+        # a return from an out-of-line block: must land right after the forward branch
+        # that entered this block (so it cannot loop)
+        n_back += 1
+        assert re.match(r"\.L(km|kh)back_\d+$", tgt), f"backward branch at line {i}: {l.strip()}"
+        enter = lines[pos[tgt] - 1].strip()
+        assert enter.startswith("s_cbranch_scc1"), enter
+        block = enter.split()[-1]
+        assert pos[tgt] < pos[block] < i
+    assert n_branches > 300 and n_back > 0
 
 
-def test_dispatch_table_is_full(asm):
+def test_handlers_are_symbols_at_translator_offsets(asm):
+    import ctypes
+
+    from mythril_amd import _native as N
+    from mythril_amd import uop_spec as U
+
     _, lines = asm
-    t = lines.index(".Ltab:")
-    stubs = lines[t + 1:t + 1 + 256]
-    assert all(re.match(r"^\s+s_branch \.Lh_\w+$", x) for x in stubs)
-    assert not re.match(r"^\s+s_branch", lines[t + 257])
+    labels = [l.split()[-1][:-1] for l in lines if "mgp_h_" in l and l.endswith(":")]
+    assert labels == [f"mgp_h_{h}" for h in U.HANDLERS]
+    fn = N.lib().mgp_uop_handler_offsets
+    fn.restype = ctypes.POINTER(ctypes.c_uint16)
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+    n = ctypes.c_uint32()
+    p = fn(ctypes.byref(n))
+    offs = [p[i] for i in range(n.value)]
+    assert n.value == len(U.HANDLERS) and len(set(offs)) == len(offs) and min(offs) > 0
 
 
 def test_no_scalar_memory_writes(asm):
@@ -101,6 +120,8 @@ def test_address_registers_initialised_before_first_load(asm):
     assert w2 < first(lambda l: l.startswith("global_load") and ", v2," in l)
     assert w1 < first(lambda l: l.startswith("ds_") and ", v" in l)
     assert first(lambda l: l.startswith("s_getpc_b64 s[10:11]")) < first(lambda l: l.startswith("s_setpc_b64"))
+    assert first(lambda l: l.startswith("global_load_dwordx4 v[112:115]")) < \
+        first(lambda l: l.startswith("v_readlane_b32 s20, v112"))
 
 
 @pytest.mark.skipif(not os.path.exists(f"{LLVM}/ld.lld"), reason="ROCm LLVM linker not installed")

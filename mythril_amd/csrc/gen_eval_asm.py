@@ -778,7 +778,8 @@ def bitlen_chain(base, out):
         A(f"v_cmp_ne_u32 vcc, 0, {v(base + i)}",
           f"v_cndmask_b32_e64 v60, v60, {i}, vcc",
           f"v_cndmask_b32 v61, v61, {v(base + i)}, vcc")
-    A("v_ffbh_u32 v62, v61",
+    A("v_mov_b32 v59, v60",
+      "v_ffbh_u32 v62, v61",
       "v_lshlrev_b32 v60, 5, v60",
       "v_add_u32 v60, 32, v60",
       f"v_sub_u32 {v(out)}, v60, v62",
@@ -786,41 +787,22 @@ def bitlen_chain(base, out):
 
 
 def knuth_digit(J):
-    # estimate qhat from (u[J+8]:u[J+7]) / vn7 in double precision
+    """One quotient digit of Knuth's algorithm D at window u[J..J+8] (vn normalised).
+
+    qhat = floor(U3/V2 + 2^-12) in double precision, U3 = u[J+8..J+6] (96 bits),
+    V2 = vn7:vn6 (64 bits, top bit set).  |U3/V2 - U/V| <= 2^-31 and the double
+    evaluation is within 2^-18 of U3/V2 (1/V2 from v_rcp_f64 + two Newton steps), so
+    with the 2^-12 bias qhat is the true digit q or q+1 — never below it.  q+1 makes the
+    multiply-subtract go negative: one add-back, taken by a wave only when one of its
+    lanes sits within 2^-12 of the next integer.
+    """
     A(f"v_cvt_f64_u32 v[30:31], {u(J + 8)}",
       f"v_cvt_f64_u32 v[4:5], {u(J + 7)}",
+      f"v_cvt_f64_u32 v[6:7], {u(J + 6)}",
       "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",
-      "v_mul_f64 v[30:31], v[30:31], v[28:29]",
+      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[6:7]",
+      "v_fma_f64 v[30:31], v[30:31], v[28:29], s[28:29]",
       "v_cvt_u32_f64 v60, v[30:31]")
-    # r = num - qhat*vn7 ; fix qhat by one each way (exact floor, capped at 2^32-1)
-    A(f"v_mad_u64_u32 v[56:57], s[48:49], v60, {vn(7)}, 0",
-      f"v_sub_co_u32 v62, vcc, {u(J + 7)}, v56",
-      f"v_subb_co_u32 v63, vcc, {u(J + 8)}, v57, vcc",
-      "v_subb_co_u32 v60, s[48:49], v60, 0, vcc",
-      f"v_cndmask_b32_e64 v61, 0, {vn(7)}, vcc",
-      "v_add_co_u32 v62, s[48:49], v62, v61",
-      "v_addc_co_u32 v63, s[48:49], v63, 0, s[48:49]",
-      "v_cmp_ne_u32_e64 s[48:49], 0, v63",
-      f"v_cmp_ge_u32_e64 s[50:51], v62, {vn(7)}",
-      "s_or_b64 s[48:49], s[48:49], s[50:51]",
-      "v_cmp_ne_u32_e64 s[50:51], -1, v60",
-      "s_and_b64 vcc, s[48:49], s[50:51]",
-      "v_addc_co_u32 v60, s[48:49], v60, 0, vcc",
-      f"v_cndmask_b32_e64 v61, 0, {vn(7)}, vcc",
-      "v_sub_co_u32 v62, s[48:49], v62, v61",
-      "v_subb_co_u32 v63, s[48:49], v63, 0, s[48:49]")
-    # Knuth D3: while rhat < 2^32 and qhat*vn6 > (rhat:u[J+6]): qhat--, rhat += vn7 (twice)
-    for _ in range(2):
-        A(f"v_mad_u64_u32 v[56:57], s[48:49], v60, {vn(6)}, 0",
-          f"v_mov_b32 v58, {u(J + 6)}",
-          "v_mov_b32 v59, v62",
-          "v_cmp_gt_u64_e64 s[48:49], v[56:57], v[58:59]",
-          "v_cmp_eq_u32_e64 s[50:51], 0, v63",
-          "s_and_b64 vcc, s[48:49], s[50:51]",
-          "v_subb_co_u32 v60, s[48:49], v60, 0, vcc",
-          f"v_cndmask_b32_e64 v61, 0, {vn(7)}, vcc",
-          "v_add_co_u32 v62, s[48:49], v62, v61",
-          "v_addc_co_u32 v63, s[48:49], v63, 0, s[48:49]")
     # u[J..J+8] -= qhat * vn
     A("v_mov_b32 v58, 0", "v_mov_b32 v59, 0")
     for i in range(8):
@@ -866,13 +848,17 @@ def h_div():
     A("v_mov_b32 v24, 0", "v_mov_b32 v25, 0")
     A.label(lsd)
     # lb = bitlen(b) -> v60 path into v26 temporarily; bnz -> s[26:27]
-    bitlen_chain(VB, 26)
+    bitlen_chain(VB, 26)                               # v26 = lb, v59 = top limb index of b
     A("s_mov_b64 s[26:27], s[48:49]")
-    bitlen_chain(VA, 27)
+    # top non-zero limb index of a -> v27
+    A("v_mov_b32 v27, 0")
+    for i in range(1, 8):
+        A(f"v_cmp_ne_u32 vcc, 0, {v(VA + i)}", f"v_cndmask_b32_e64 v27, v27, {i}, vcc")
     # a < b ?
     ult_chain(VA, VB, tmp=62)
     A("s_andn2_b64 s[24:25], s[26:27], vcc")          # divides = b != 0 && a >= b
-    A("v_sub_u32 v27, v27, v26",                       # d = la - lb
+    # d = top limb(a) - top limb(b): quotient digits J > d are zero (u unchanged) -> skipped
+    A("v_sub_u32 v27, v27, v59",
       "v_cndmask_b32_e64 v27, -1, v27, s[24:25]",
       "v_sub_u32 v26, 0x100, v26",                     # s = 256 - lb
       "v_cndmask_b32_e64 v26, 0, v26, s[24:25]")
@@ -887,15 +873,20 @@ def h_div():
     shl_var(list(range(VN, VN + 8)), 8)
     shl_var(list(range(UQ, UQ + 16)), 8)
     # 1 / vn7 in double precision (rcp + one Newton step)
-    A(f"v_cvt_f64_u32 v[30:31], {vn(7)}",
+    A("s_mov_b32 s62, 0", "s_mov_b32 s63, 0x41f00000",      # 2^32
+      "s_mov_b32 s28, 0", "s_mov_b32 s29, 0x3f300000",      # 2^-12 (qhat bias)
+      f"v_cvt_f64_u32 v[30:31], {vn(7)}",
+      f"v_cvt_f64_u32 v[4:5], {vn(6)}",
+      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",   # V2 = vn7*2^32 + vn6
       "v_rcp_f64 v[28:29], v[30:31]",
       "s_nop 1",
       "v_fma_f64 v[4:5], -v[30:31], v[28:29], 1.0",
       "v_fma_f64 v[28:29], v[28:29], v[4:5], v[28:29]",
-      "s_mov_b32 s62, 0", "s_mov_b32 s63, 0x41f00000")
+      "v_fma_f64 v[4:5], -v[30:31], v[28:29], 1.0",
+      "v_fma_f64 v[28:29], v[28:29], v[4:5], v[28:29]")
     for J in range(7, -1, -1):
         lskip = A.fresh(f"skipdig{J}")
-        A(f"v_cmp_lt_i32 vcc, {32 * J - 1}, v27",
+        A(f"v_cmp_le_i32 vcc, {J}, v27",
           "s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lskip}")
         knuth_digit(J)
         A.label(lskip)

@@ -229,3 +229,50 @@ def test_long_programs_many_vars_and_constants(mgp_ctx, n_ops, n_vars, n_consts)
     assert (first[~ok] == N.MGP_UNDECIDED).all()
     if n_consts <= 60:
         assert ok.all()
+
+
+def _magnitude_values(rng, n, w):
+    """Operands of every bit length class (plus 0, 1, all-ones, powers of two), as w-bit ints."""
+    m = (1 << w) - 1
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.1:
+            out.append(int(rng.choice([0, 1, 2, m, m - 1, 1 << (w - 1), (1 << (w - 1)) - 1])) & m)
+        else:
+            bits = int(rng.integers(1, w + 1))
+            v = 0
+            for k in range(0, bits, 62):
+                v = (v << 62) | int(rng.integers(0, 2 ** 62))
+            out.append((v >> max(0, (((bits + 61) // 62) * 62) - bits)) & m | (1 << (bits - 1)))
+    return out
+
+
+@pytest.mark.parametrize("w", [256, 160, 64])
+def test_division_all_variants_every_candidate(mgp_ctx, w):
+    """UDIV/UREM/SDIV/SREM/SMOD on operands of all magnitudes (1-limb divisors force all
+    eight Knuth digits): root = (op(x0, x1) != x2) with x2 the expected value, so a correct
+    kernel leaves every state without a satisfying candidate."""
+    rng = np.random.default_rng(w)
+    ops = [S.UDIV, S.UREM, S.SDIV, S.SREM, S.SMOD]
+    n_cand, per_op = 256, 3
+    states, rows = [], []
+    for op in ops:
+        for _ in range(per_op):
+            a = _magnitude_values(rng, n_cand, w)
+            b = _magnitude_values(rng, n_cand, w)
+            exp = [S.binop(op, x, y, w) for x, y in zip(a, b)]
+            nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0], [S.VAR, w, -1, -1, -1, 2, 0],
+                  [op, w, 0, 1, -1, 0, 0], [S.EQ, 1, 3, 2, -1, 0, 0], [S.BNOT, 1, 4, -1, -1, 0, 0]]
+            states.append((nl, []))
+            rows.append([[x, y, e] for x, y, e in zip(a, b, exp)])
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    first, _ = mgp_ctx.eval_batch(words, po, cands_from_ints(rows))
+    bad = np.nonzero(first != N.MGP_NO_SAT)[0]
+    if bad.size:
+        s0 = int(bad[0])
+        a, b, e = rows[s0][int(first[s0])]
+        pytest.fail(f"{bad.size} states with a wrong quotient/remainder; first: op {ops[s0 // per_op]} "
+                    f"a={a:#x} b={b:#x} expected {e:#x}")

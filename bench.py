@@ -161,8 +161,10 @@ def main():
     log(f"rank {rank}: kernel {kern_ms:.2f} ms/launch, step {1e3 * elapsed / args.steps:.2f} ms, SAT {sat}/{n_states}, "
         f"planted found {planted_ok}")
 
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "eval_pmc_traffic.json")
+    # HBM bytes and issued VALU instructions per step from the committed rocprofv3 PMC
+    # run of the same workload (profiles/collect.sh -> analyze.py -> profiles/eval_pmc.json)
+    traffic, valu_busy = None, None
+    pmc_path = os.path.join(ROOT, "profiles", "eval_pmc.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
@@ -170,6 +172,9 @@ def main():
             if (pm.get("states") == n_states and pm.get("cand") == n_cand
                     and pm.get("kernel") == ENGINE_KERNEL[N.set_eval_engine()]):
                 traffic = pm.get("hbm_bytes_per_launch")
+                if pm.get("valu_wave_insts_per_step"):
+                    valu_busy = {"issued_int32_lane_ops_per_s": pm["valu_wave_insts_per_step"] * 64 / (kern_ms * 1e-3),
+                                 "source": pm.get("source")}
         except (OSError, ValueError):
             traffic = None
 
@@ -264,6 +269,9 @@ def main():
                          "evals_per_launch": evals_rank},
             "roofline_hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": achieved_gbs / HBM_PEAK_GBS, "bytes_per_launch": bytes_launch},
+            # VALU busy: every issued VALU instruction (dispatch/decode overhead included) x 64 lanes
+            "valu_busy": None if valu_busy is None else dict(
+                valu_busy, frac=valu_busy["issued_int32_lane_ops_per_s"] / (valu_peak * 1e12)),
             "cpu_baseline": cpu,
             "results": {"sat_states": sat, "planted_states": int(len(pl)), "planted_found": planted_ok},
             "keccak": keccak,

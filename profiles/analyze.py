@@ -93,6 +93,10 @@ def main(d):
             der["HBM bytes per eval step (2 x FETCH_SIZE + WRITE_SIZE)"] = fetch + write
             traffic[k] = {"fetch_bytes_per_step": fetch, "write_bytes_per_step": write,
                           "hbm_bytes_per_launch": fetch + write, "steps_in_profile": n_steps}
+            if c.get("SQ_INSTS_VALU"):
+                # issued VALU wave-instructions per step (x 64 lanes = lane-ops, overhead included)
+                traffic[k]["valu_wave_insts_per_step"] = c["SQ_INSTS_VALU"] / n_steps
+                traffic[k]["salu_insts_per_step"] = c.get("SQ_INSTS_SALU", 0) / n_steps
         if der:
             out.append("\nderived:\n")
             for n, val in der.items():
@@ -104,8 +108,10 @@ def main(d):
     for k, t in traffic.items():
         try:
             cfg = json.load(open(bj))["config"]
-            t.update({"kernel": k, "states": cfg["states_per_gpu"], "cand": cfg["candidates"], "source": d})
-            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "eval_pmc_traffic.json"), "w") as f:
+            tag = os.path.basename(os.path.normpath(d)).replace("prof_", "")
+            t.update({"kernel": k, "states": cfg["states_per_gpu"], "cand": cfg["candidates"],
+                      "source": f"profiles/{tag}_summary.md (rocprofv3 run {d})"})
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "eval_pmc.json"), "w") as f:
                 json.dump(t, f, indent=1)
         except (OSError, ValueError, KeyError):
             pass

@@ -40,6 +40,24 @@ def chain(op, k, width=256, bkind="var", store_every=0):
     else:
         b = 1
     t = 0
+    if op == "FIB":   # t_i = t_{i-1} + t_{i-2}: B from an LDS slot, every result stored
+        prev = 1
+        for i in range(k):
+            nl.append([S.ADD, 256, t, prev, -1, 0, 0])
+            prev, t = t, len(nl) - 1
+        nl.append([S.EQ, 1, t, 0, -1, 0, 0])
+        nl.append([S.EQ, 1, 1, t, -1, 0, 0])
+        nl.append([S.BOR, 1, len(nl) - 2, len(nl) - 1, -1, 0, 0])
+        return nl, consts
+    if op == "BAND":  # Bool chain: c = (x0 < x1); b_i = b_{i-1} & c  (SALU-only uops)
+        nl.append([S.ULT, 1, 0, 1, -1, 0, 0])
+        c = b = len(nl) - 1
+        for i in range(k):
+            nl.append([S.BOR if i % 2 else S.BAND, 1, b, c, -1, 0, 0])
+            b = len(nl) - 1
+        nl.append([S.EQ, 1, 0, 1, -1, 0, 0])
+        nl.append([S.BOR, 1, b, len(nl) - 1, -1, 0, 0])
+        return nl, consts
     for i in range(k):
         if op in (S.EQ, S.ULT, S.SLT):
             c = len(nl)
@@ -113,7 +131,7 @@ def main():
     waves = args.states * (n_cand // 64)
     base_t, _, _ = run(*chain(S.ADD, 0), args.states, n_cand, torch, dev, stream, sh)
     rows = []
-    cases = [("ADD var", S.ADD, "var"), ("ADD const", S.ADD, "const"), ("SUB var", S.SUB, "var"),
+    cases = [("FIB slot+st", "FIB", "var"), ("BAND/BOR", "BAND", "var"), ("ADD var", S.ADD, "var"), ("ADD const", S.ADD, "const"), ("SUB var", S.SUB, "var"),
              ("XOR var", S.XOR, "var"), ("MUL var", S.MUL, "var"), ("UDIV var", S.UDIV, "var"),
              ("UREM var", S.UREM, "var"), ("SDIV var", S.SDIV, "var"),
              ("SHL var", S.SHL, "var"), ("LSHR const", S.LSHR, "const"),
@@ -122,7 +140,7 @@ def main():
     for name, op, bk in cases:
         nl, consts = chain(op, args.k, bkind=bk)
         t, n_ins, slots = run(nl, consts, args.states, n_cand, torch, dev, stream, sh)
-        per_chain = args.k * (2 if op in (S.EQ, S.ULT, S.SLT, S.ITE, S.EXTRACT) else 1)
+        per_chain = args.k * (2 if op in (S.EQ, S.ULT, S.SLT, S.ITE) else 1)
         cyc = (t - base_t) * CLOCK * SIMDS / (waves * per_chain)
         rows.append({"case": name, "ms": t * 1e3, "v1_ins": n_ins, "slots": slots,
                      "simd_cycles_per_uop": cyc})

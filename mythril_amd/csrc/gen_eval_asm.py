@@ -803,16 +803,23 @@ def knuth_digit(J):
       "v_fma_f64 v[30:31], v[30:31], s[62:63], v[6:7]",
       "v_fma_f64 v[30:31], v[30:31], v[28:29], s[28:29]",
       "v_cvt_u32_f64 v60, v[30:31]")
-    # u[J..J+8] -= qhat * vn
-    A("v_mov_b32 v58, 0", "v_mov_b32 v59, 0")
-    for i in range(8):
-        A(f"v_mad_u64_u32 v[56:57], s[48:49], v60, {vn(i)}, v[58:59]")
-        if i == 0:
-            A(f"v_sub_co_u32 {u(J)}, vcc, {u(J)}, v56")
+    # u[J..J+8] -= qhat * vn: the 8 products are independent (no carry between the mads);
+    # their sum  lo0 | lo1+hi0 | ... | lo7+hi6 | hi7  is formed by an add chain (carry in
+    # s[48:49]) interleaved with the borrow chain of the subtraction (VCC), so the critical
+    # path is ~9 dependent steps instead of 25
+    pairs = [(8, 9), (10, 11), (12, 13), (14, 15), (56, 57), (58, 59), (62, 63), (4, 5)]
+    for i, (lo, hi) in enumerate(pairs):
+        A(f"v_mad_u64_u32 v[{lo}:{hi}], s[50:51], v60, {vn(i)}, 0")
+    A(f"v_sub_co_u32 {u(J)}, vcc, {u(J)}, v{pairs[0][0]}")
+    for i in range(1, 8):
+        lo, hi_prev = pairs[i][0], pairs[i - 1][1]
+        if i == 1:
+            A(f"v_add_co_u32 v{lo}, s[48:49], v{lo}, v{hi_prev}")
         else:
-            A(f"v_subb_co_u32 {u(J + i)}, vcc, {u(J + i)}, v56, vcc")
-        A("v_mov_b32 v58, v57")
-    A(f"v_subb_co_u32 {u(J + 8)}, vcc, {u(J + 8)}, v58, vcc")
+            A(f"v_addc_co_u32 v{lo}, s[48:49], v{lo}, v{hi_prev}, s[48:49]")
+        A(f"v_subb_co_u32 {u(J + i)}, vcc, {u(J + i)}, v{lo}, vcc")
+    A(f"v_addc_co_u32 v{pairs[7][1]}, s[48:49], 0, v{pairs[7][1]}, s[48:49]")
+    A(f"v_subb_co_u32 {u(J + 8)}, vcc, {u(J + 8)}, v{pairs[7][1]}, vcc")
     lno = A.fresh("noaddback")
     A("s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lno}",
       "s_mov_b64 s[50:51], vcc",
@@ -863,12 +870,15 @@ def h_div():
       "v_sub_u32 v26, 0x100, v26",                     # s = 256 - lb
       "v_cndmask_b32_e64 v26, 0, v26, s[24:25]")
     lpost = A.fresh("divpost")
-    A("s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {lpost}")
-    # normalise: vn = b << s, u = a << s (512 bits)
-    copy8(VN, VB)
+    # u = a (512 bits) before the all-lanes-trivial skip: a lane that does not divide keeps
+    # s = 0, and its digits are zero (qhat <= 1 with an exact add-back), so u[0..7] = a is
+    # its remainder and vA is free as scratch for the digit products
     copy8(UQ, VA)
     for i in range(8, 16):
         A(f"v_mov_b32 {u(i)}, 0")
+    A("s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {lpost}")
+    # normalise: vn = b << s, u = a << s
+    copy8(VN, VB)
     shift_setup(26, left=True)
     shl_var(list(range(VN, VN + 8)), 8)
     shl_var(list(range(UQ, UQ + 16)), 8)
@@ -898,11 +908,10 @@ def h_div():
     shr_var(list(range(UQ, UQ + 8)), "0")
     A.label(lnorem)
     A.label(lpost)
-    # per lane: dividing -> (q = u[8..15], r = u[0..7]); else q = (b == 0 ? ~0 : 0), r = a
+    # per lane: dividing -> (q = u[8..15], r = u[0..7]); else q = (b == 0 ? ~0 : 0), r = u[0..7] = a
     A("v_cndmask_b32_e64 v61, -1, 0, s[26:27]")
     for i in range(8):
-        A(f"v_cndmask_b32_e64 {u(8 + i)}, v61, {u(8 + i)}, s[24:25]",
-          f"v_cndmask_b32_e64 {u(i)}, {v(VA + i)}, {u(i)}, s[24:25]")
+        A(f"v_cndmask_b32_e64 {u(8 + i)}, v61, {u(8 + i)}, s[24:25]")
     # result by variant: 0 UDIV, 1 UREM, 2 SDIV, 3 SREM, 4 SMOD
     l_r, l_sd, l_sr, l_end = A.fresh("rem"), A.fresh("sdiv"), A.fresh("srem"), A.fresh("divend")
     A("s_cmp_eq_u32 s61, 1", f"s_cbranch_scc1 {l_r}",

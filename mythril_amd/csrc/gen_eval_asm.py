@@ -103,8 +103,7 @@ def prefetch_next():
       "v_readlane_b32 s23, v115, s3",
       "s_add_u32 s3, s3, 1",
       "s_and_b32 s0, s20, 0xffff",
-      "s_lshl_b32 s0, s0, 2",
-      "s_add_u32 s0, s10, s0",
+      "s_lshl2_add_u32 s0, s0, s10",
       "s_addc_u32 s1, s11, 0")
 
 
@@ -118,8 +117,7 @@ def tail():
 def op_target():
     """s[12:13] <- address of the op handler (w0[31:16] * 4 from the kernel base)."""
     A("s_lshr_b32 s12, s16, 16",
-      "s_lshl_b32 s12, s12, 2",
-      "s_add_u32 s12, s10, s12",
+      "s_lshl2_add_u32 s12, s12, s10",
       "s_addc_u32 s13, s11, 0")
 
 
@@ -146,7 +144,7 @@ def copy8(dst, src):
 
 
 def sext_inplace(base):
-    """x = (x ^ H) - H, H = 2^(w-1) in s[32:39]: sign-extends a zero-extended w-bit value.
+    """x = (x ^ H) - H, H = 2^(w-1) in s[32:39] (load_kh first): sign-extends a zero-extended w-bit value.
     (gfx950 VOP2 carry ops read VCC over the constant bus, so H is copied to v[56:63] first.)"""
     sext_to(base, base)
 
@@ -263,6 +261,20 @@ def wait_operands():
 B_STORE, B_MASK, B_SEXT, B_INVERT = 22, 23, 24, 25
 
 
+def load_km():
+    """s[40:47] <- pool[mask index w2[21:16]] (2^w - 1)."""
+    A(f"s_bfe_u32 s48, s18, {(6 << 16) | 16:#x}")
+    for i in range(8):
+        A(f"v_readlane_b32 {s(S_KM + i)}, {v(PQ + i)}, s48")
+
+
+def load_kh():
+    """s[32:39] <- pool[sign index w3[5:0]] (2^(w-1))."""
+    A("s_and_b32 s49, s19, 0x3f")
+    for i in range(8):
+        A(f"v_readlane_b32 {s(S_KH + i)}, {v(PQ + i)}, s49")
+
+
 def store_slot():
     A("s_and_b32 s48, s18, 0xffff",
       "v_add_u32 v4, s48, v1",
@@ -270,14 +282,28 @@ def store_slot():
       f"ds_write_b128 v4, {vr(VA + 4, 4)} offset:1024")
 
 
+EPI_MODE = [None]   # None: test the STORE/MASK flags at run time; else the variant's fixed epilogue
+
+
 def bv_epilogue():
     """[mask] [store] then dispatch; unmasked results fall straight through to the tail."""
+    mode = EPI_MODE[0]
+    if mode is not None:
+        if "M" in mode:
+            load_km()
+            for i in range(8):
+                A(f"v_and_b32 {v(VA + i)}, {s(S_KM + i)}, {v(VA + i)}")
+        if "S" in mode:
+            store_slot()
+        tail()
+        return
     lm, ls = A.fresh("mask"), A.fresh("store")
     A(f"s_bitcmp1_b32 s18, {B_MASK}", f"s_cbranch_scc1 {lm}",
       f"s_bitcmp1_b32 s18, {B_STORE}", f"s_cbranch_scc1 {ls}")
     tail()
 
     def masked():
+        load_km()
         for i in range(8):
             A(f"v_and_b32 {v(VA + i)}, {s(S_KM + i)}, {v(VA + i)}")
         A(f"s_bitcmp1_b32 s18, {B_STORE}", f"s_cbranch_scc1 {ls}")
@@ -331,7 +357,7 @@ def fetch_one(kind, dst, which):
     if kind == "rvar":
         # v[dst+i] = v[64 + 8*var + i]: GPR-index mode (gfx950 has no v_movrels) offsets
         # SRC0 of the moves by 8*var into the preloaded variable bank
-        A(f"s_lshl_b32 {sp}, {sp}, 3", "s_waitcnt vmcnt(0)",
+        A(f"s_lshl_b32 {sp}, {sp}, 3",
           f"s_set_gpr_idx_on {sp}, gpr_idx(SRC0)", "s_nop 1")
         for i in range(8):
             A(f"v_mov_b32 {v(dst + i)}, {v(RV + i)}")
@@ -361,29 +387,10 @@ def make_fetch(name):
 
     def body():
         op_target()
-        lk, lh, back_k, back_h = A.fresh("km"), A.fresh("kh"), A.fresh("kmback"), A.fresh("khback")
-        A(f"s_bitcmp1_b32 s18, {B_MASK}", f"s_cbranch_scc1 {lk}")
-        A.label(back_k)
-        A(f"s_bitcmp1_b32 s18, {B_SEXT}", f"s_cbranch_scc1 {lh}")
-        A.label(back_h)
         if kb != "none":
             fetch_one(kb, VB, "B")
         fetch_one(ka, VA if tgt == "A" else VC, "A")
         op_dispatch()
-
-        def km():
-            A(f"s_bfe_u32 s48, s18, {(6 << 16) | 16:#x}")
-            for i in range(8):
-                A(f"v_readlane_b32 {s(S_KM + i)}, {v(PQ + i)}, s48")
-            A(f"s_branch {back_k}")
-
-        def kh():
-            A("s_and_b32 s49, s19, 0x3f")
-            for i in range(8):
-                A(f"v_readlane_b32 {s(S_KH + i)}, {v(PQ + i)}, s49")
-            A(f"s_branch {back_h}")
-        A.out_of_line(lk, km)
-        A.out_of_line(lh, kh)
     return body
 
 
@@ -536,6 +543,7 @@ def h_mov():
 @handler("SEXT")
 def h_sext():
     wait_operands()
+    load_kh()
     sext_inplace(VA)
     bv_epilogue()
 
@@ -543,6 +551,7 @@ def h_sext():
 def maybe_sext_A():
     l = A.fresh("nosx")
     A(f"s_bitcmp1_b32 s18, {B_SEXT}", f"s_cbranch_scc0 {l}")
+    load_kh()
     sext_inplace(VA)
     A.label(l)
 
@@ -717,6 +726,7 @@ def make_cmp(base, xreg):
             slt_chain(x, y)
             A(f"s_branch {ldone}")
             A.label(lsx)
+            load_kh()
             sext_to(40, X)
             sext_to(48, Y)
             x, y = (40, 48) if base == "SLT" else (48, 40)
@@ -727,6 +737,7 @@ def make_cmp(base, xreg):
             for i in range(1, 8):
                 A(f"v_addc_co_u32 {v(VT)}, vcc, {v(X + i)}, {v(Y + i)}, vcc")
         elif base == "UADDNOW":
+            load_km()
             A(f"v_add_co_u32 {v(VT)}, vcc, {v(X)}, {v(Y)}")
             for i in range(1, 8):
                 A(f"v_addc_co_u32 {v(VT + i)}, vcc, {v(X + i)}, {v(Y + i)}, vcc")
@@ -737,6 +748,8 @@ def make_cmp(base, xreg):
             for i in range(1, 8):
                 A(f"v_subb_co_u32 v4, vcc, {v(40 + i)}, {v(VT + i)}, vcc")
         elif base in ("UMULNO256", "UMULNOW"):
+            if base == "UMULNOW":
+                load_km()
             mul_full(X, Y, VT)
             or_reduce(VT + 8, range(VT + 8, VT + 16))
             A(f"v_cmp_ne_u32 vcc, 0, {v(VT + 8)}")
@@ -840,6 +853,7 @@ def h_div():
     wait_operands()
     maybe_sext_op = A.fresh("nosxd")
     A(f"s_bitcmp1_b32 s18, {B_SEXT}", f"s_cbranch_scc0 {maybe_sext_op}")
+    load_kh()
     sext_inplace(VA)
     sext_inplace(VB)
     A.label(maybe_sext_op)
@@ -961,6 +975,21 @@ def h_div():
         A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {vn(i)}, s[50:51]")
     A.label(l_end)
     bv_epilogue()
+
+
+def make_epi_variant(op, mode):
+    def _():
+        EPI_MODE[0] = mode
+        try:
+            HBODY[op]()
+        finally:
+            EPI_MODE[0] = None
+    return _
+
+
+for _name in U.EPI_VARIANTS:
+    _op, _mode = _name.rsplit("_", 1)
+    HBODY[_name] = make_epi_variant(_op, _mode)
 
 
 # ---------------------------------------------------------------- kernel
@@ -1144,7 +1173,9 @@ def var_preload() -> str:
                 "  s_add_u32 s92, s6, s94", "  s_addc_u32 s93, s7, 0",
                 f"  global_load_dwordx4 v[{r}:{r + 3}], v2, s[92:93]",
                 f"  global_load_dwordx4 v[{r + 4}:{r + 7}], v3, s[92:93]"]
-    out.append(f"  s_waitcnt vmcnt({2 * U.REG_VARS})")
+    # page, pool and variables all present before the first uop (the variable loads were
+    # issued right behind the page and pool, so this adds little over waiting for those)
+    out.append("  s_waitcnt vmcnt(0)")
     return "\n".join(out) + "\n"
 
 

@@ -119,6 +119,20 @@ struct Translator {
 };
 
 // w0 = entry offsets of the first handler and of the op handler (fetch handlers jump to it)
+// cheap BV ops have handler variants with a fixed epilogue (no flag tests at run time)
+inline uint32_t epi_variant(uint32_t op, bool store, bool mask) {
+  if (!store && !mask) return op;
+  static const uint32_t T[][4] = {
+      {MGP_U_ADD, MGP_U_ADD_S, MGP_U_ADD_M, MGP_U_ADD_MS}, {MGP_U_SUB, MGP_U_SUB_S, MGP_U_SUB_M, MGP_U_SUB_MS},
+      {MGP_U_AND, MGP_U_AND_S, MGP_U_AND_M, MGP_U_AND_MS}, {MGP_U_OR, MGP_U_OR_S, MGP_U_OR_M, MGP_U_OR_MS},
+      {MGP_U_XOR, MGP_U_XOR_S, MGP_U_XOR_M, MGP_U_XOR_MS}, {MGP_U_NOT, MGP_U_NOT_S, MGP_U_NOT_M, MGP_U_NOT_MS},
+      {MGP_U_NEG, MGP_U_NEG_S, MGP_U_NEG_M, MGP_U_NEG_MS}, {MGP_U_MOV, MGP_U_MOV_S, MGP_U_MOV_M, MGP_U_MOV_MS},
+      {MGP_U_ITE, MGP_U_ITE_S, MGP_U_ITE_M, MGP_U_ITE_MS}};
+  for (const auto &e : T)
+    if (e[0] == op) return mask ? (store ? e[3] : e[2]) : e[1];
+  return op;
+}
+
 inline uint32_t w0_of(uint32_t first, uint32_t op) {
   return (uint32_t)kUopHandlerOffset[first] | ((uint32_t)kUopHandlerOffset[op] << 16);
 }
@@ -290,6 +304,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       w2 |= dst * MGP_U_SLOT_BYTES;
     }
     const uint32_t first = fetch_id(a.kind, b.kind, false);
+    opid = epi_variant(opid, (flags & MGP_UF_STORE) != 0, (flags & MGP_UF_MASK) != 0);
     emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
   }
 

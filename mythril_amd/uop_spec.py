@@ -59,7 +59,12 @@ CONCAT = [f"CONCAT{k}" for k in range(8)]
 CMPS = ["EQ", "ULT", "UGT", "SLT", "SGT", "UADDNO256", "UADDNOW", "UMULNO256", "UMULNOW"]
 CMP_VARIANTS = [f"{c}_{r}" for c in CMPS for r in ("RA", "RC")]
 
-OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS
+# epilogue-specialised variants of the cheap BV ops: _S store, _M mask, _MS both (the
+# translator picks one from the STORE/MASK flags, so these handlers test no flags)
+EPI_OPS = ["ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "MOV", "ITE"]
+EPI_VARIANTS = [f"{o}_{v}" for o in EPI_OPS for v in ("S", "M", "MS")]
+
+OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
 # id past the table ends the program instead of running off into memory
 HANDLERS = ["INVALID"] + FETCH + OPS

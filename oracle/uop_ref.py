@@ -119,6 +119,8 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
                     vC = load(ka, pa)
         else:
             op = first
+        if op in U.EPI_VARIANTS:   # fixed-epilogue variant: same semantics, flags still in w2
+            op = op.rsplit("_", 1)[0]
         sb = (w3 >> U.SHIFT_B_POS) & 31
         if op == "PAGE":
             assert pc % U.PAGE_UOPS == U.PAGE_UOPS - 1, "PAGE must end a 64-uop page"

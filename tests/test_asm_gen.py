@@ -57,7 +57,7 @@ def test_branches_are_forward(asm):
         assert enter.startswith("s_cbranch_scc1"), enter
         block = enter.split()[-1]
         assert pos[tgt] < pos[block] < i
-    assert n_branches > 300 and n_back > 0
+    assert n_branches > 200
 
 
 def test_handlers_are_symbols_at_translator_offsets(asm):

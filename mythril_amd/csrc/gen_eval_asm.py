@@ -977,19 +977,23 @@ def h_div():
     bv_epilogue()
 
 
-def make_epi_variant(op, mode):
+def make_epi_variant(body, mode):
     def _():
         EPI_MODE[0] = mode
         try:
-            HBODY[op]()
+            body()
         finally:
             EPI_MODE[0] = None
     return _
 
 
+_EPI_BASE = {_op: HBODY[_op] for _op in U.EPI_OPS}
 for _name in U.EPI_VARIANTS:
     _op, _mode = _name.rsplit("_", 1)
-    HBODY[_name] = make_epi_variant(_op, _mode)
+    HBODY[_name] = make_epi_variant(_EPI_BASE[_op], _mode)
+# the translator only names the base handler of these ops when neither flag is set
+for _op in U.EPI_OPS:
+    HBODY[_op] = make_epi_variant(_EPI_BASE[_op], "")
 
 
 # ---------------------------------------------------------------- kernel

@@ -358,10 +358,10 @@ def fetch_one(kind, dst, which):
         # v[dst+i] = v[64 + 8*var + i]: GPR-index mode (gfx950 has no v_movrels) offsets
         # SRC0 of the moves by 8*var into the preloaded variable bank
         A(f"s_lshl_b32 {sp}, {sp}, 3",
-          f"s_set_gpr_idx_on {sp}, gpr_idx(SRC0)", "s_nop 1")
+          f"s_set_gpr_idx_on {sp}, gpr_idx(SRC0)")
         for i in range(8):
             A(f"v_mov_b32 {v(dst + i)}, {v(RV + i)}")
-        A("s_set_gpr_idx_off", "s_nop 1")
+        A("s_set_gpr_idx_off")
         return
     if kind == "slot":
         A(f"v_add_u32 {vaddr}, {sp}, v1",
@@ -431,10 +431,11 @@ def h_ret():
 def bool_binop(name, instr):
     @handler(name)
     def _():
-        bool_read("s17", 0, 50)
-        bool_read("s17", 16, 52)
-        A(f"{instr} s[50:51], s[50:51], s[52:53]")
-        bool_write("s[50:51]")
+        # the S_MOVREL-after-M0-write wait state is filled with the next operand's field extract
+        A("s_and_b32 s48, s17, 0xffff", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s17, 16",
+          "s_movrels_b64 s[50:51], s[64:65]", "s_mov_b32 m0, s49", "s_lshr_b32 s48, s19, 16",
+          "s_movrels_b64 s[52:53], s[64:65]", "s_mov_b32 m0, s48",
+          f"{instr} s[50:51], s[50:51], s[52:53]", "s_movreld_b64 s[64:65], s[50:51]")
         tail()
 
 
@@ -446,9 +447,9 @@ bool_binop("BEQ", "s_xnor_b64")
 
 @handler("BNOT")
 def h_bnot():
-    bool_read("s17", 0, 50)
-    A("s_not_b64 s[50:51], s[50:51]")
-    bool_write("s[50:51]")
+    A("s_and_b32 s48, s17, 0xffff", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s19, 16",
+      "s_movrels_b64 s[50:51], s[64:65]", "s_mov_b32 m0, s49", "s_not_b64 s[50:51], s[50:51]",
+      "s_movreld_b64 s[64:65], s[50:51]")
     tail()
 
 

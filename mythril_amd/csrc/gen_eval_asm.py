@@ -37,8 +37,9 @@ from mythril_amd import uop_spec as U  # noqa: E402
 KNAME = "mgp_eval_gfx950"
 VA, VB, VC, VT = 8, 16, 24, 32
 RV = 64          # v[64:111]: candidate variables 0..5 of this lane, preloaded at wave start
-PG = 112         # v[112:115]: the current 64-uop page, uop k in lane k (read with v_readlane)
-PQ = 116         # v[116:123]: the constant pool, constant c in lane c, limb l in v[116+l]
+PG = 112         # v[112:116]: the current 64-uop page, uop k in lane k (read with v_readlane):
+                 #   v112 first-handler address (low 32 bits), v113 op-handler address, v114-116 w1-w3
+PQ = 118         # v[118:125]: the constant pool, constant c in lane c, limb l in v[118+l]
 S_KB, S_KH, S_KM = 24, 32, 40
 
 
@@ -95,16 +96,29 @@ A = Asm()
 
 
 def prefetch_next():
-    """At handler entry: read the next uop (lane s3 of the page) into N = s[20:23] and its
-    first handler address into s[0:1], so the v_readlane -> SALU latency overlaps the body."""
-    A("v_readlane_b32 s20, v112, s3",
-      "v_readlane_b32 s21, v113, s3",
-      "v_readlane_b32 s22, v114, s3",
-      "v_readlane_b32 s23, v115, s3",
-      "s_add_u32 s3, s3, 1",
-      "s_and_b32 s0, s20, 0xffff",
-      "s_lshl2_add_u32 s0, s0, s10",
-      "s_addc_u32 s1, s11, 0")
+    """At handler entry: read the next uop (lane s3 of the page): its first-handler address
+    straight into s0 (s1 = high half of the code address, constant), op-handler address and
+    w1-w3 into N = s[20:23].  The addresses were computed lane-parallel when the page was
+    loaded, so dispatch costs one SALU op (the lane counter) besides the moves."""
+    A("v_readlane_b32 s0, v112, s3",
+      "v_readlane_b32 s20, v113, s3",
+      "v_readlane_b32 s21, v114, s3",
+      "v_readlane_b32 s22, v115, s3",
+      "v_readlane_b32 s23, v116, s3",
+      "s_add_u32 s3, s3, 1")
+
+
+def page_decode():
+    """v[112:115] raw uop words w0-w3 -> v112/v113 absolute handler addresses (low 32 bits;
+    the prologue checked that the kernel code does not cross a 4 GiB boundary), v114-116 w1-w3."""
+    A("v_mov_b32 v116, v115",
+      "v_mov_b32 v115, v114",
+      "v_mov_b32 v114, v113",
+      "v_lshrrev_b32 v113, 16, v112",
+      "v_lshl_add_u32 v113, v113, 2, s10",
+      "v_and_b32 v112, 0xffff, v112",
+      "v_lshl_add_u32 v112, v112, 2, s10",
+      "s_nop 1")   # VALU write -> v_readlane of the same VGPR
 
 
 def tail():
@@ -115,10 +129,8 @@ def tail():
 
 
 def op_target():
-    """s[12:13] <- address of the op handler (w0[31:16] * 4 from the kernel base)."""
-    A("s_lshr_b32 s12, s16, 16",
-      "s_lshl2_add_u32 s12, s12, s10",
-      "s_addc_u32 s13, s11, 0")
+    """s[12:13] <- address of the op handler (s16 = its low 32 bits, s13 = code high half)."""
+    A("s_mov_b32 s12, s16")
 
 
 def op_dispatch():
@@ -411,6 +423,7 @@ def h_page():
       "global_load_dwordx4 v[112:115], v4, s[4:5]",
       "s_waitcnt vmcnt(0)",
       "s_mov_b32 s3, 0")
+    page_decode()
     prefetch_next()
     tail()
 
@@ -1111,16 +1124,22 @@ PROLOGUE = """\
   s_sub_u32 s92, s91, 1
   v_min_u32 v4, s92, v0
   v_lshlrev_b32 v4, 5, v4
-  global_load_dwordx4 v[116:119], v4, s[14:15]
-  global_load_dwordx4 v[120:123], v4, s[14:15] offset:16
+  global_load_dwordx4 v[118:121], v4, s[14:15]
+  global_load_dwordx4 v[122:125], v4, s[14:15] offset:16
 .Lno_pool:
   // preload variables 0..min(n_vars, 6)-1 of this lane's candidate into v[64:111]
-{VAR_PRELOAD}  // s[10:11] = kernel entry address: uops hold handler offsets / 4 from it
+  // s[10:11] = kernel entry address: uops hold handler offsets / 4 from it.  Handler
+  // addresses are formed as 32-bit sums: a code object crossing a 4 GiB boundary (never
+  // seen; would need the loader to place it there) makes every wave report undecided.
   s_getpc_b64 s[10:11]
 .Lpc_base:
   s_sub_u32 s10, s10, .Lpc_base-mgp_eval_gfx950
   s_subb_u32 s11, s11, 0
-  s_mov_b64 s[64:65], 0
+  s_add_u32 s92, s10, .Lfunc_end-mgp_eval_gfx950
+  s_cbranch_scc1 .Lundec
+  s_mov_b32 s1, s11
+  s_mov_b32 s13, s11
+{VAR_PRELOAD}{PAGE_DECODE}  s_mov_b64 s[64:65], 0
   s_mov_b64 s[66:67], -1
   s_mov_b32 s62, 0
   s_mov_b32 s63, 0x41f00000
@@ -1160,7 +1179,7 @@ def metadata():
         "    .private_segment_fixed_size: 0",
         "    .sgpr_count: 104",
         f"    .symbol: {KNAME}.kd",
-        "    .vgpr_count: 124",
+        "    .vgpr_count: 126",
         "    .wavefront_size: 64",
         "amdhsa.target: amdgcn-amd-amdhsa--gfx950",
         "amdhsa.version:", "  - 1", "  - 2",
@@ -1194,7 +1213,12 @@ def generate() -> str:
     prefetch_next()
     tail()
     globals()["A"] = global_A
-    A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines)))
+    dec = Asm()
+    globals()["A"] = dec
+    page_decode()
+    globals()["A"] = global_A
+    A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
+                   .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n"))
     no_prefetch = set(U.FETCH) | {"INVALID", "RET", "PAGE"}
     for name in U.HANDLERS:
         A.lines.append(f".p2align 2\nmgp_h_{name}:")
@@ -1226,9 +1250,9 @@ def generate() -> str:
         "  .amdhsa_system_sgpr_workgroup_id_x 1",
         "  .amdhsa_system_sgpr_workgroup_id_y 1",
         "  .amdhsa_system_vgpr_workitem_id 0",
-        "  .amdhsa_next_free_vgpr 124",
+        "  .amdhsa_next_free_vgpr 126",
         "  .amdhsa_next_free_sgpr 102",
-        "  .amdhsa_accum_offset 124",
+        "  .amdhsa_accum_offset 128",
         "  .amdhsa_reserve_vcc 1",
         "  .amdhsa_float_denorm_mode_32 3",
         "  .amdhsa_float_denorm_mode_16_64 3",

@@ -121,7 +121,7 @@ def test_address_registers_initialised_before_first_load(asm):
     assert w1 < first(lambda l: l.startswith("ds_") and ", v" in l)
     assert first(lambda l: l.startswith("s_getpc_b64 s[10:11]")) < first(lambda l: l.startswith("s_setpc_b64"))
     assert first(lambda l: l.startswith("global_load_dwordx4 v[112:115]")) < \
-        first(lambda l: l.startswith("v_readlane_b32 s20, v112"))
+        first(lambda l: l.startswith("v_readlane_b32 s0, v112"))
 
 
 @pytest.mark.skipif(not os.path.exists(f"{LLVM}/ld.lld"), reason="ROCm LLVM linker not installed")

@@ -116,6 +116,10 @@ int mgp_eval_batch_dev(const uint32_t *d_prog_words,
 #define MGP_ENGINE_ASM 2
 int mgp_set_eval_engine(int engine);
 
+/* Diagnostic only: when d_diag (device memory, 16 B per state x chunk) is non-null the
+ * MGP_ENGINE_ASM kernel writes per-wave clock stamps there (profiles/stamps.py). */
+int mgp_set_eval_diag(void *d_diag);
+
 /* Host-side launch plan: states grouped by the BV-slot count in their program
  * header.  Writes order_out[n_states], bounds_out[nb+1], slots_out[nb];
  * returns nb (<= max_buckets) or a negative error. */

@@ -84,6 +84,7 @@ def _bind(lib):
         "mgp_nominal_ops": (ctypes.c_int, [_P, _P, _U32, _P]),
         "mgp_probe_valu_dev": (ctypes.c_int, [_U32, _U32, _P, _P, _P]),
         "mgp_set_eval_engine": (ctypes.c_int, [ctypes.c_int]),
+        "mgp_set_eval_diag": (ctypes.c_int, [_P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -130,6 +131,7 @@ EXPORTED_SYMBOLS = (
     "mgp_nominal_ops",
     "mgp_probe_valu_dev",
     "mgp_set_eval_engine",
+    "mgp_set_eval_diag",
 )
 
 ENGINE_HIP, ENGINE_ASM = 1, 2

@@ -429,6 +429,26 @@ def h_page():
 
 
 # ---- Bool ops
+def diag_stamp():
+    """Diagnostic build-in (kernarg diag != 0): diag[item] = {first dispatch - entry,
+    RET - first dispatch, entry time lo, entry time hi} in shader clocks."""
+    ln = A.fresh("nodiag")
+    A("v_readlane_b32 s24, v126, 0", "v_readlane_b32 s25, v126, 1",
+      "s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {ln}",
+      "s_memtime s[54:55]",
+      "v_readlane_b32 s26, v126, 2", "v_readlane_b32 s27, v126, 3",
+      "v_readlane_b32 s28, v126, 4", "v_readlane_b32 s29, v126, 6",
+      "s_lshl_b32 s29, s29, 4", "s_add_u32 s24, s24, s29", "s_addc_u32 s25, s25, 0",
+      "s_sub_u32 s30, s28, s26",
+      "s_waitcnt lgkmcnt(0)",
+      "s_sub_u32 s31, s54, s28",
+      "s_mov_b64 exec, 1",
+      "v_mov_b32 v4, s30", "v_mov_b32 v5, s31", "v_mov_b32 v6, s26", "v_mov_b32 v7, s27",
+      "v_mov_b32 v8, 0",
+      "global_store_dwordx4 v8, v[4:7], s[24:25]")
+    A.label(ln)
+
+
 @handler("RET")
 def h_ret():
     A("s_waitcnt vmcnt(0)")
@@ -438,6 +458,7 @@ def h_ret():
       "s_add_u32 s53, s60, s52",
       "s_cmp_lt_i32 s52, 0",
       "s_cselect_b32 s53, 0x7fffffff, s53")
+    diag_stamp()
     write_partial_and_end("s53")
 
 
@@ -1013,16 +1034,22 @@ for _op in U.EPI_OPS:
 # ---------------------------------------------------------------- kernel
 
 PROLOGUE = """\
+  s_memtime s[96:97]
   s_load_dwordx8 s[64:71], s[0:1], 0x0
   s_load_dwordx8 s[72:79], s[0:1], 0x20
-  s_load_dword s80, s[0:1], 0x40
   s_waitcnt lgkmcnt(0)
-  // s[64:65] words  s[66:67] offs  s[68:69] cands  s[70:71] partial  s[72:73] order
-  // s74 n_states  s75 n_cand  s76 n_vars  s77 n_chunks  s78 n_slots  s79 order_base  s80 grid x
+  // s[64:65] desc  s[66:67] cands  s[68:69] partial  s[70:71] diag
+  // s72 n_states  s73 n_cand  s74 n_vars  s75 n_chunks  s76 n_slots  s77 position base  s78 grid x
+  // diagnostic stamps (diag != 0): v126 lanes 0-1 diag, 2-3 entry time, 4-5 first
+  // dispatch time, 6 item index; written at RET as 16 B per (state, chunk) item
+  v_writelane_b32 v126, s70, 0
+  v_writelane_b32 v126, s71, 1
+  v_writelane_b32 v126, s96, 2
+  v_writelane_b32 v126, s97, 3
   // XCD-aware bijective remap of workgroup x (cdna_hip_programming.md §5 T1)
   s_and_b32 s82, s2, 7
-  s_lshr_b32 s83, s80, 3
-  s_and_b32 s84, s80, 7
+  s_lshr_b32 s83, s78, 3
+  s_and_b32 s84, s78, 7
   s_add_u32 s85, s83, 1
   s_mul_i32 s86, s82, s85
   s_mul_i32 s87, s84, s85
@@ -1033,85 +1060,50 @@ PROLOGUE = """\
   s_cselect_b32 s86, s86, s87
   s_lshr_b32 s81, s2, 3
   s_add_u32 s81, s81, s86
-  s_add_u32 s81, s81, s79
-  s_cmp_eq_u64 s[72:73], 0
-  s_cbranch_scc1 .Lno_order
-  s_lshl_b32 s82, s81, 2
-  s_add_u32 s82, s72, s82
-  s_addc_u32 s83, s73, 0
-  s_load_dword s81, s[82:83], 0x0
-  s_waitcnt lgkmcnt(0)
-.Lno_order:
-  s_cmp_ge_u32 s81, s74
+  s_add_u32 s81, s81, s77
+  s_cmp_ge_u32 s81, s72
   s_cbranch_scc1 .Lexit
+  // launch descriptor of this position (mgp_desc_kernel): 32 B
+  s_lshl_b32 s82, s81, 5
+  s_lshr_b32 s83, s81, 27
+  s_add_u32 s82, s64, s82
+  s_addc_u32 s83, s65, s83
+  s_load_dwordx8 s[84:91], s[82:83], 0x0
+  s_waitcnt lgkmcnt(0)
+  // s84 state  s85 undecided  s86 slots  s87 n_uops  s[88:89] page 0  s90 pool offset from
+  // page 0  s91 n_pool | register-variable mask << 8
   // partial entry: partial + (state * n_chunks + chunk) * 4
-  s_mul_i32 s82, s81, s77
+  s_mul_i32 s82, s84, s75
   s_add_u32 s82, s82, s3
+  v_writelane_b32 v126, s82, 6
   s_mul_hi_u32 s83, s82, 4
   s_lshl_b32 s82, s82, 2
-  s_add_u32 s58, s70, s82
-  s_addc_u32 s59, s71, s83
-  // program address = words + offs[state] * 4
-  s_lshl_b32 s82, s81, 3
-  s_mul_hi_u32 s83, s81, 8
-  s_add_u32 s82, s66, s82
-  s_addc_u32 s83, s67, s83
-  s_load_dwordx2 s[82:83], s[82:83], 0x0
-  s_waitcnt lgkmcnt(0)
-  s_lshl_b64 s[82:83], s[82:83], 2
-  s_add_u32 s84, s64, s82
-  s_addc_u32 s85, s65, s83
-  s_load_dwordx4 s[88:91], s[84:85], 0x0
-  s_waitcnt lgkmcnt(0)
-  // v1 header checks (same as the HIP kernel): status, slot budget of this bucket, variables
-  s_and_b32 s92, s91, 0xff
-  s_cmp_lg_u32 s92, 0
+  s_add_u32 s58, s68, s82
+  s_addc_u32 s59, s69, s83
+  s_cmp_lg_u32 s85, 0
   s_cbranch_scc1 .Lundec
-  s_cmp_gt_u32 s90, s78
+  s_cmp_gt_u32 s86, s76
   s_cbranch_scc1 .Lundec
-  s_lshr_b32 s92, s91, 8
-  s_cmp_gt_u32 s92, s76
-  s_cbranch_scc1 .Lundec
-  // uop header at word align4(4 + 4*n_ins + 8*n_consts) + 4
-  s_lshl_b32 s92, s88, 2
-  s_lshl_b32 s93, s89, 3
-  s_add_u32 s92, s92, s93
-  s_add_u32 s92, s92, 7
-  s_and_b32 s92, s92, 0xfffffffc
-  s_add_u32 s92, s92, 4
-  s_lshl_b32 s92, s92, 2
-  s_add_u32 s84, s84, s92
-  s_addc_u32 s85, s85, 0
-  s_load_dwordx4 s[88:91], s[84:85], 0x0
-  s_waitcnt lgkmcnt(0)
-  // uop header: n_uops, status, pool byte offset, n_pool
-  s_cmp_lg_u32 s89, 0
-  s_cbranch_scc1 .Lundec
-  s_cmp_gt_u32 s91, 64
-  s_cbranch_scc1 .Lundec
-  s_cmp_eq_u32 s88, 0
-  s_cbranch_scc1 .Lundec
-  s_add_u32 s14, s84, s90
-  s_addc_u32 s15, s85, 0
-  s_add_u32 s4, s84, 16
-  s_addc_u32 s5, s85, 0
-  s_mov_b32 s2, s88
+  s_mov_b64 s[4:5], s[88:89]
+  s_add_u32 s14, s88, s90
+  s_addc_u32 s15, s89, 0
+  s_mov_b32 s2, s87
   // candidates of this state: cands + state * n_vars * n_cand * 32, layout [var][half][cand] x 16 B
-  s_lshl_b32 s8, s75, 5
-  s_mul_i32 s92, s76, s8
-  s_mul_i32 s6, s81, s92
-  s_mul_hi_u32 s7, s81, s92
-  s_add_u32 s6, s68, s6
-  s_addc_u32 s7, s69, s7
-  s_sub_u32 s9, s76, 1
+  s_lshl_b32 s8, s73, 5
+  s_mul_i32 s92, s74, s8
+  s_mul_i32 s6, s84, s92
+  s_mul_hi_u32 s7, s84, s92
+  s_add_u32 s6, s66, s6
+  s_addc_u32 s7, s67, s7
+  s_sub_u32 s9, s74, 1
   // lanes: candidate = chunk*64 + lane (clamped; lanes past n_cand are masked out of the result)
   s_lshl_b32 s60, s3, 6
   v_add_u32 v5, s60, v0
-  v_cmp_gt_u32_e64 s[56:57], s75, v5
-  s_sub_u32 s92, s75, 1
+  v_cmp_gt_u32_e64 s[56:57], s73, v5
+  s_sub_u32 s92, s73, 1
   v_min_u32 v5, s92, v5
   v_lshlrev_b32 v2, 4, v5
-  s_lshl_b32 s92, s75, 4
+  s_lshl_b32 s92, s73, 4
   v_add_u32 v3, s92, v2
   v_lshlrev_b32 v1, 4, v0
   // uop page 0 -> v[112:115] (lane k = uop min(k, n_uops): lanes past the end hold the INVALID pad); pool -> v[116:123] (lane c = constant
@@ -1119,9 +1111,10 @@ PROLOGUE = """\
   v_min_u32 v4, s2, v0
   v_lshlrev_b32 v4, 4, v4
   global_load_dwordx4 v[112:115], v4, s[4:5]
-  s_cmp_eq_u32 s91, 0
+  s_and_b32 s93, s91, 0xff
+  s_cmp_eq_u32 s93, 0
   s_cbranch_scc1 .Lno_pool
-  s_sub_u32 s92, s91, 1
+  s_sub_u32 s92, s93, 1
   v_min_u32 v4, s92, v0
   v_lshlrev_b32 v4, 5, v4
   global_load_dwordx4 v[118:121], v4, s[14:15]
@@ -1139,7 +1132,14 @@ PROLOGUE = """\
   s_cbranch_scc1 .Lundec
   s_mov_b32 s1, s11
   s_mov_b32 s13, s11
-{VAR_PRELOAD}{PAGE_DECODE}  s_mov_b64 s[64:65], 0
+{VAR_PRELOAD}{PAGE_DECODE}  s_cmp_eq_u64 s[70:71], 0
+  s_cbranch_scc1 .Lnostamp
+  s_memtime s[96:97]
+  s_waitcnt lgkmcnt(0)
+  v_writelane_b32 v126, s96, 4
+  v_writelane_b32 v126, s97, 5
+.Lnostamp:
+  s_mov_b64 s[64:65], 0
   s_mov_b64 s[66:67], -1
   s_mov_b32 s62, 0
   s_mov_b32 s63, 0x41f00000
@@ -1154,10 +1154,10 @@ PROLOGUE = """\
   s_endpgm
 """
 
-KARGS = [("words", 8, "global_buffer"), ("offs", 8, "global_buffer"), ("cands", 8, "global_buffer"),
-         ("partial", 8, "global_buffer"), ("order", 8, "global_buffer"), ("n_states", 4, "by_value"),
-         ("n_cand", 4, "by_value"), ("n_vars", 4, "by_value"), ("n_chunks", 4, "by_value"),
-         ("n_slots", 4, "by_value"), ("order_base", 4, "by_value"), ("grid_x", 4, "by_value")]
+KARGS = [("desc", 8, "global_buffer"), ("cands", 8, "global_buffer"), ("partial", 8, "global_buffer"),
+         ("diag", 8, "global_buffer"), ("n_states", 4, "by_value"), ("n_cand", 4, "by_value"),
+         ("n_vars", 4, "by_value"), ("n_chunks", 4, "by_value"), ("n_slots", 4, "by_value"),
+         ("pos_base", 4, "by_value"), ("grid_x", 4, "by_value"), ("pad", 4, "by_value")]
 
 
 def metadata():
@@ -1179,7 +1179,7 @@ def metadata():
         "    .private_segment_fixed_size: 0",
         "    .sgpr_count: 104",
         f"    .symbol: {KNAME}.kd",
-        "    .vgpr_count: 126",
+        "    .vgpr_count: 128",
         "    .wavefront_size: 64",
         "amdhsa.target: amdgcn-amd-amdhsa--gfx950",
         "amdhsa.version:", "  - 1", "  - 2",
@@ -1188,15 +1188,17 @@ def metadata():
 
 
 def var_preload() -> str:
-    """Variables 0..REG_VARS-1 -> v[64:111]; always REG_VARS x 2 loads (index clamped to
-    n_vars-1), so that vmcnt(2*REG_VARS) below waits exactly for the page and pool loads."""
+    """Variables v < REG_VARS the program reads (mask bit 8+v of s91) -> v[64+8v : 72+8v]
+    (index clamped to n_vars-1); the others are never read and not loaded."""
     out = []
     for i in range(U.REG_VARS):
         r = RV + 8 * i
-        out += [f"  s_min_u32 s94, s9, {i}", "  s_mul_i32 s94, s94, s8",
+        out += [f"  s_bitcmp1_b32 s91, {8 + i}", f"  s_cbranch_scc0 .Lnovar{i}",
+                f"  s_min_u32 s94, s9, {i}", "  s_mul_i32 s94, s94, s8",
                 "  s_add_u32 s92, s6, s94", "  s_addc_u32 s93, s7, 0",
                 f"  global_load_dwordx4 v[{r}:{r + 3}], v2, s[92:93]",
-                f"  global_load_dwordx4 v[{r + 4}:{r + 7}], v3, s[92:93]"]
+                f"  global_load_dwordx4 v[{r + 4}:{r + 7}], v3, s[92:93]",
+                f".Lnovar{i}:"]
     # page, pool and variables all present before the first uop (the variable loads were
     # issued right behind the page and pool, so this adds little over waiting for those)
     out.append("  s_waitcnt vmcnt(0)")
@@ -1250,7 +1252,7 @@ def generate() -> str:
         "  .amdhsa_system_sgpr_workgroup_id_x 1",
         "  .amdhsa_system_sgpr_workgroup_id_y 1",
         "  .amdhsa_system_vgpr_workitem_id 0",
-        "  .amdhsa_next_free_vgpr 126",
+        "  .amdhsa_next_free_vgpr 128",
         "  .amdhsa_next_free_sgpr 102",
         "  .amdhsa_accum_offset 128",
         "  .amdhsa_reserve_vcc 1",

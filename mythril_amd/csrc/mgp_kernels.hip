@@ -626,10 +626,39 @@ static uint32_t cpl_override() {
   return v;
 }
 
+// Launch descriptors of the gfx950 interpreter, one per position p of the launch
+// order (order[p], or p): everything its prologue needs from the program headers, so
+// that a wave reaches its page / pool / variable loads after one dependent load
+// instead of four (offs -> v1 header -> uop header).  32 B each:
+//   {state, undecided, slots, n_uops}  {page0 address lo, hi, pool offset from page 0,
+//    n_pool | register-variable mask << 8}
+__global__ void mgp_desc_kernel(const uint32_t *__restrict__ words, const uint64_t *__restrict__ offs,
+                                uint32_t n_states, const uint32_t *__restrict__ order, uint32_t n_vars,
+                                uint4 *__restrict__ desc) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_states) return;
+  const uint32_t state = order ? order[p] : p;
+  const uint32_t *w = words + offs[state];
+  const uint4 h = make_uint4(w[0], w[1], w[2], w[3]);
+  uint32_t undec = 1u, n_uops = 0u, pool_rel = 0u, npm = 0u;
+  uint64_t page = 0u;
+  if ((h.w & 0xFFu) == MGP_ST_OK && (h.w >> 8) <= n_vars) {
+    const uint32_t v1 = 4u + 4u * h.x + 8u * h.y;
+    const uint32_t *u = w + ((v1 + 3u) & ~3u) + 4u;
+    const uint4 uh = make_uint4(u[0], u[1], u[2], u[3]);
+    n_uops = uh.x;
+    npm = uh.w;
+    undec = (uh.y == 0u && (npm & 0xFFu) <= 64u && n_uops > 0u) ? 0u : 1u;
+    page = reinterpret_cast<uint64_t>(u + 4);
+    pool_rel = uh.z - 16u;
+  }
+  desc[2 * (size_t)p] = make_uint4(state, undec, h.z, n_uops);
+  desc[2 * (size_t)p + 1] = make_uint4((uint32_t)page, (uint32_t)(page >> 32), pool_rel, npm);
+}
+
 extern "C" hipError_t mgp_asm_available(void);
-extern "C" hipError_t mgp_launch_eval_asm(const uint32_t *words, const uint64_t *offs, uint32_t n_states,
-                                          const uint32_t *cands, uint32_t n_cand, uint32_t n_vars,
-                                          uint32_t n_slots, int32_t *partial, const uint32_t *order,
+extern "C" hipError_t mgp_launch_eval_asm(const void *desc, uint32_t n_states, const uint32_t *cands,
+                                          uint32_t n_cand, uint32_t n_vars, uint32_t n_slots, int32_t *partial,
                                           const uint32_t *bucket_bounds, const uint32_t *bucket_slots,
                                           uint32_t n_buckets, uint32_t n_chunks, hipStream_t st);
 
@@ -659,8 +688,19 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
   hipError_t err;
   if (g_engine == MGP_ENGINE_ASM) {
     n_chunks = (n_cand + MGP_WAVE - 1) / MGP_WAVE;
-    err = mgp_launch_eval_asm(words, offs, n_states, cands, n_cand, n_vars, n_slots, partial, order,
-                              bucket_bounds, bucket_slots, n_buckets, n_chunks, st);
+    const bool bucketed = n_buckets && order && bucket_bounds && bucket_slots;
+    void *desc = nullptr;
+    err = hipMallocAsync(&desc, (size_t)n_states * 32u, st);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(mgp_desc_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, words, offs, n_states,
+                       bucketed ? order : nullptr, n_vars, reinterpret_cast<uint4 *>(desc));
+    err = hipGetLastError();
+    if (err == hipSuccess)
+      err = mgp_launch_eval_asm(desc, n_states, cands, n_cand, n_vars, n_slots, partial,
+                                bucketed ? bucket_bounds : nullptr, bucketed ? bucket_slots : nullptr,
+                                bucketed ? n_buckets : 0u, n_chunks, st);
+    const hipError_t ferr = hipFreeAsync(desc, st);
+    if (err == hipSuccess) err = ferr;
   } else {
     const uint32_t cpl = cpl_override() ? cpl_override() : 1u;  // CPL=2 measured slower (LDS occupancy halves)
     n_chunks = (n_cand + MGP_WAVE * cpl - 1) / (MGP_WAVE * cpl);

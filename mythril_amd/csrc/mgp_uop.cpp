@@ -55,6 +55,7 @@ struct Translator {
   const uint32_t *v1;
   uint32_t n_ins, n_c;
   std::vector<uint32_t> pool;        // 8 words per constant
+  uint32_t var_mask = 0;             // register variables the program reads (preloaded)
   std::map<uint32_t, uint32_t> mask_c, sign_c;  // width -> pool index
   bool bad = false;
 
@@ -97,7 +98,12 @@ struct Translator {
         if (idx >= MGP_U_MAX_LDS_SLOTS) bad = true;
         return {KSLOT, idx * MGP_U_SLOT_BYTES};
       case MGP_K_CONST: return {KCONST, pool_byte(idx)};
-      default: return {idx < MGP_U_REG_VARS ? KRVAR : KVAR, idx};
+      default:
+        if (idx < MGP_U_REG_VARS) {
+          var_mask |= 1u << idx;
+          return {KRVAR, idx};
+        }
+        return {KVAR, idx};
     }
   }
   uint32_t boolslot(uint32_t b) {
@@ -338,7 +344,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   out[base + 0] = n_uops;
   out[base + 1] = 0;
   out[base + 2] = (uint32_t)((MGP_U_HDR_WORDS + (n_uops + 1) * MGP_U_UOP_WORDS) * 4u);
-  out[base + 3] = (uint32_t)(T.pool.size() / 8);
+  out[base + 3] = (uint32_t)(T.pool.size() / 8) | (T.var_mask << 8);
   out.insert(out.end(), T.pool.begin(), T.pool.end());
   return 0;
 }

@@ -8,7 +8,8 @@ Program layout (per state, appended after the v1 bytecode of include/mgp_ir.h,
 at word offset align4(4 + 4*n_ins + 8*n_consts) + 4 from the program start):
 
   header   4 words: n_uops, status (0 = runnable), pool byte offset (from the
-           uop header), n_pool
+           uop header), n_pool | register-variable mask << 8 (bit v: the program
+           reads variable v < REG_VARS, which the kernel preloads into VGPRs)
   uops     n_uops x 4 words in pages of 64: uop 63 of every full page is PAGE
            (the kernel holds one page in 4 VGPRs, uop k in lane k, and reads
            the current uop with v_readlane; PAGE loads the next page), then one

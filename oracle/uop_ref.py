@@ -78,7 +78,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         return None
     pool0 = u0 + pool_bytes // 4
 
-    n_pool = int(words[u0 + 3])
+    n_pool = int(words[u0 + 3]) & 0xFF   # bits 8..13: register variables the program reads
 
     def pool(idx: int) -> int:
         assert idx < n_pool

@@ -80,7 +80,8 @@ int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets,
  * cand_words: n_states * n_cand * n_vars * 8 u32, layout [state][cand][var][limb]
  *   (limb 0 least significant).
  * out_first_sat[s]: lowest satisfying candidate index, MGP_NO_SAT (-1) if none,
- *   MGP_UNDECIDED (-2) if the state's program is unsupported.
+ *   MGP_UNDECIDED (-2) if the state's program is unsupported (MGP_EVAL_FAULT (-3):
+ *   an internal inconsistency, never expected).
  * out_witness (may be NULL): n_states * n_vars * 8 u32; filled for SAT states
  *   with the winning candidate's words, left untouched otherwise. */
 int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words,

@@ -145,5 +145,8 @@ typedef struct mgp_node {
 /* first-SAT sentinels */
 #define MGP_NO_SAT (-1)
 #define MGP_UNDECIDED (-2)
+/* an evaluation wave left no valid result for the state (internal inconsistency; never
+ * expected — reported instead of reading a candidate outside the batch) */
+#define MGP_EVAL_FAULT (-3)
 
 #endif /* MGP_IR_H */

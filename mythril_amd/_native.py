@@ -41,6 +41,7 @@ MGP_E_CAPACITY = -4
 
 MGP_NO_SAT = -1
 MGP_UNDECIDED = -2
+MGP_EVAL_FAULT = -3  # internal inconsistency (never expected); treated as undecided
 ST_OK = 0
 ST_UNSUPPORTED = 1
 

@@ -850,32 +850,38 @@ def knuth_digit(J):
       "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",
       "v_fma_f64 v[30:31], v[30:31], s[62:63], v[6:7]",
       "v_fma_f64 v[30:31], v[30:31], v[28:29], s[28:29]",
-      "v_cvt_u32_f64 v60, v[30:31]")
-    # u[J..J+8] -= qhat * vn: the 8 products are independent (no carry between the mads);
-    # their sum  lo0 | lo1+hi0 | ... | lo7+hi6 | hi7  is formed by an add chain (carry in
-    # s[48:49]) interleaved with the borrow chain of the subtraction (VCC), so the critical
-    # path is ~9 dependent steps instead of 25
+      "v_cvt_u32_f64 v60, v[30:31]",
+      # lanes whose digit J is zero (J > d = top limb(a) - top limb(b), or not dividing;
+      # vcc from the caller's skip test) take qhat = 0.  Every lane left has
+      # top limb(b) <= 7 - J, so its normalised divisor has vn[i] = 0 for i < J: the
+      # products and the subtraction only involve vn[J..7] and u[2J..J+8]
+      "v_cndmask_b32 v60, 0, v60, vcc")
+    # u[2J..J+8] -= qhat * vn[J..7]: the products are independent (no carry between the
+    # mads); their sum  lo_J | lo_J+1 + hi_J | ... | hi_7  is formed by an add chain
+    # (carry in s[48:49]) interleaved with the borrow chain of the subtraction (VCC)
     pairs = [(8, 9), (10, 11), (12, 13), (14, 15), (56, 57), (58, 59), (62, 63), (4, 5)]
-    for i, (lo, hi) in enumerate(pairs):
+    for i in range(J, 8):
+        lo, hi = pairs[i]
         A(f"v_mad_u64_u32 v[{lo}:{hi}], s[50:51], v60, {vn(i)}, 0")
-    A(f"v_sub_co_u32 {u(J)}, vcc, {u(J)}, v{pairs[0][0]}")
-    for i in range(1, 8):
+    A(f"v_sub_co_u32 {u(2 * J)}, vcc, {u(2 * J)}, v{pairs[J][0]}")
+    for i in range(J + 1, 8):
         lo, hi_prev = pairs[i][0], pairs[i - 1][1]
-        if i == 1:
+        if i == J + 1:
             A(f"v_add_co_u32 v{lo}, s[48:49], v{lo}, v{hi_prev}")
         else:
             A(f"v_addc_co_u32 v{lo}, s[48:49], v{lo}, v{hi_prev}, s[48:49]")
         A(f"v_subb_co_u32 {u(J + i)}, vcc, {u(J + i)}, v{lo}, vcc")
-    A(f"v_addc_co_u32 v{pairs[7][1]}, s[48:49], 0, v{pairs[7][1]}, s[48:49]")
+    if J < 7:
+        A(f"v_addc_co_u32 v{pairs[7][1]}, s[48:49], 0, v{pairs[7][1]}, s[48:49]")
     A(f"v_subb_co_u32 {u(J + 8)}, vcc, {u(J + 8)}, v{pairs[7][1]}, vcc")
     lno = A.fresh("noaddback")
     A("s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lno}",
       "s_mov_b64 s[50:51], vcc",
       "v_subb_co_u32 v60, s[48:49], v60, 0, s[50:51]")
-    for i in range(8):
+    for i in range(J, 8):
         A(f"v_cndmask_b32_e64 v61, 0, {vn(i)}, s[50:51]")
-        if i == 0:
-            A(f"v_add_co_u32 {u(J)}, vcc, v61, {u(J)}")
+        if i == J:
+            A(f"v_add_co_u32 {u(J + i)}, vcc, v61, {u(J + i)}")
         else:
             A(f"v_addc_co_u32 {u(J + i)}, vcc, v61, {u(J + i)}, vcc")
     A(f"v_addc_co_u32 {u(J + 8)}, vcc, 0, {u(J + 8)}, vcc")
@@ -1063,12 +1069,15 @@ PROLOGUE = """\
   s_add_u32 s81, s81, s77
   s_cmp_ge_u32 s81, s72
   s_cbranch_scc1 .Lexit
-  // launch descriptor of this position (mgp_desc_kernel): 32 B
+  // launch descriptor of this position (mgp_desc_kernel): 32 B.  glc: the descriptors
+  // were written by the kernel just before this one on the stream, into a buffer that a
+  // previous launch may have read at the same address, and the scalar cache is not
+  // guaranteed to be invalidated between two kernels of one stream - read them from L2
   s_lshl_b32 s82, s81, 5
   s_lshr_b32 s83, s81, 27
   s_add_u32 s82, s64, s82
   s_addc_u32 s83, s65, s83
-  s_load_dwordx8 s[84:91], s[82:83], 0x0
+  s_load_dwordx8 s[84:91], s[82:83], 0x0 glc
   s_waitcnt lgkmcnt(0)
   // s84 state  s85 undecided  s86 slots  s87 n_uops  s[88:89] page 0  s90 pool offset from
   // page 0  s91 n_pool | register-variable mask << 8

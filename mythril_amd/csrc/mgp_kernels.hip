@@ -19,9 +19,13 @@
 // conflict-free).  No MFMA: nothing here is a contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 
 #include "../../include/mgp.h"
 #include "mgp_bv.h"
@@ -319,13 +323,16 @@ __global__ void mgp_finalize_kernel(const int32_t *__restrict__ partial, uint32_
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= n_states) return;
   int32_t best = MGP_PARTIAL_NONE;
-  bool undec = false;
+  bool undec = false, bad = false;
   for (uint32_t k = 0; k < n_chunks; ++k) {
     int32_t p = partial[(size_t)s * n_chunks + k];
     if (p == MGP_PARTIAL_UNDEC) undec = true;
+    else if (p == MGP_PARTIAL_NONE) continue;
+    else if (p < 0 || (uint32_t)p >= n_cand) bad = true;  // a chunk left no valid result
     else if (p < best) best = p;
   }
-  int32_t res = undec ? MGP_UNDECIDED : (best == MGP_PARTIAL_NONE ? MGP_NO_SAT : best);
+  int32_t res = bad ? MGP_EVAL_FAULT
+                    : undec ? MGP_UNDECIDED : (best == MGP_PARTIAL_NONE ? MGP_NO_SAT : best);
   first_sat[s] = res;
   if (res >= 0 && witness) {
     const uint4 *cb = cands + (size_t)s * n_vars * 2u * n_cand;
@@ -662,6 +669,42 @@ extern "C" hipError_t mgp_launch_eval_asm(const void *desc, uint32_t n_states, c
                                           const uint32_t *bucket_bounds, const uint32_t *bucket_slots,
                                           uint32_t n_buckets, uint32_t n_chunks, hipStream_t st);
 
+// Launch-descriptor buffers, one per (device, stream), grow-only.  Kernels of one stream
+// run in order, so a stream's buffer is free again for its next launch; growing it waits
+// for the stream first (the old buffer may still be read by enqueued kernels).  Not
+// stream-ordered allocation (hipMallocAsync / hipFreeAsync): a descriptor buffer must stay
+// mapped until the interpreter launches that read it have finished.
+static hipError_t desc_buffer(hipStream_t st, size_t bytes, void **out) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> bufs;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lk(mu);
+  auto &b = bufs[{dev, st}];
+  if (b.second < bytes) {
+    if (b.first) {
+      e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+      (void)hipFree(b.first);
+      b = {nullptr, 0};
+    }
+    size_t cap = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+    e = hipMalloc(&b.first, cap);
+    if (e != hipSuccess) return e;
+    b.second = cap;
+  }
+  *out = b.first;
+  return hipSuccess;
+}
+
+// MGP_SYNC_DEBUG=1: synchronise after every launch of the evaluation path and name the
+// kernel that failed (fault triage; never set in measurements)
+static bool sync_debug() {
+  static const bool v = getenv("MGP_SYNC_DEBUG") != nullptr;
+  return v;
+}
+
 // Evaluation engine: MGP_ENGINE_ASM = the hand-written gfx950 interpreter
 // (mgp_eval_gfx950, default), MGP_ENGINE_HIP = the HIP C++ interpreter above
 // (kept as an independent second implementation; A/B and cross-checks).
@@ -690,17 +733,20 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
     n_chunks = (n_cand + MGP_WAVE - 1) / MGP_WAVE;
     const bool bucketed = n_buckets && order && bucket_bounds && bucket_slots;
     void *desc = nullptr;
-    err = hipMallocAsync(&desc, (size_t)n_states * 32u, st);
+    err = desc_buffer(st, (size_t)n_states * 32u, &desc);
     if (err != hipSuccess) return err;
     hipLaunchKernelGGL(mgp_desc_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, words, offs, n_states,
                        bucketed ? order : nullptr, n_vars, reinterpret_cast<uint4 *>(desc));
     err = hipGetLastError();
+    if (err == hipSuccess && sync_debug()) {
+      err = hipStreamSynchronize(st);
+      if (err != hipSuccess) fprintf(stderr, "[mgp] mgp_desc_kernel failed: %s\n", hipGetErrorString(err));
+    }
     if (err == hipSuccess)
       err = mgp_launch_eval_asm(desc, n_states, cands, n_cand, n_vars, n_slots, partial,
                                 bucketed ? bucket_bounds : nullptr, bucketed ? bucket_slots : nullptr,
                                 bucketed ? n_buckets : 0u, n_chunks, st);
-    const hipError_t ferr = hipFreeAsync(desc, st);
-    if (err == hipSuccess) err = ferr;
+
   } else {
     const uint32_t cpl = cpl_override() ? cpl_override() : 1u;  // CPL=2 measured slower (LDS occupancy halves)
     n_chunks = (n_cand + MGP_WAVE * cpl - 1) / (MGP_WAVE * cpl);
@@ -713,7 +759,12 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
   hipLaunchKernelGGL(mgp_finalize_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, partial,
                      n_states, n_chunks, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars,
                      first_sat, reinterpret_cast<uint4 *>(witness));
-  return hipGetLastError();
+  err = hipGetLastError();
+  if (err == hipSuccess && sync_debug()) {
+    err = hipStreamSynchronize(st);
+    if (err != hipSuccess) fprintf(stderr, "[mgp] mgp_finalize_kernel failed: %s\n", hipGetErrorString(err));
+  }
+  return err;
 }
 
 hipError_t mgp_launch_fill(const uint32_t *words, const uint64_t *offs, uint32_t n_states,

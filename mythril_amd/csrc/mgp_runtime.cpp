@@ -222,6 +222,9 @@ int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words, const uint64_t *pro
   if (nb < 0) return fail(ctx, MGP_E_ARG, "bucket planning failed");
   MGP_HIP(ctx, ctx->order.ensure((size_t)n_states * 4u));
   MGP_HIP(ctx, hipMemcpyAsync(ctx->order.p, order.data(), (size_t)n_states * 4u, hipMemcpyHostToDevice, st));
+  // partial results start as an invalid value: a chunk that leaves none shows up as
+  // MGP_EVAL_FAULT instead of reusing a previous batch's result
+  MGP_HIP(ctx, hipMemsetAsync(ctx->partial.p, 0x7E, (size_t)n_states * n_chunks * 4u, st));
   MGP_HIP(ctx, mgp_launch_eval((const uint32_t *)ctx->words.p, (const uint64_t *)ctx->offs.p, n_states,
                                (const uint32_t *)ctx->cand_soa.p, n_cand, n_vars, (uint32_t)slots,
                                (int32_t *)ctx->first.p, (uint32_t *)ctx->wit.p, (int32_t *)ctx->partial.p,

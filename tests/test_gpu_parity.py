@@ -276,3 +276,22 @@ def test_division_all_variants_every_candidate(mgp_ctx, w):
         a, b, e = rows[s0][int(first[s0])]
         pytest.fail(f"{bad.size} states with a wrong quotient/remainder; first: op {ops[s0 // per_op]} "
                     f"a={a:#x} b={b:#x} expected {e:#x}")
+
+
+def test_back_to_back_batches_same_context(mgp_ctx):
+    """Consecutive batches of the same size on one context reuse the same device buffers
+    (and launch-descriptor addresses) with different programs: every batch must see its
+    own programs (the interpreter reads its launch descriptors past the scalar cache)."""
+    rng = np.random.default_rng(7)
+    batches = []
+    for seed in range(3):
+        b = N.synth_generate(1000 + seed, 0, 48, 40, 64)
+        words, po, status = _lower(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+        cands = random_cands(rng, 48, 64, b["n_vars"], interesting_frac=0.3)
+        want = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)
+        batches.append((words, po, status, cands, want))
+    for _ in range(3):
+        for words, po, status, cands, want in batches:
+            first, _ = mgp_ctx.eval_batch(words, po, cands)
+            ok = status == 0
+            assert np.array_equal(first[ok], want[ok])

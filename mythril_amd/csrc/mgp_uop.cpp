@@ -309,8 +309,9 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       flags |= MGP_UF_STORE;
       w2 |= dst * MGP_U_SLOT_BYTES;
     }
-    const uint32_t first = fetch_id(a.kind, b.kind, false);
     opid = epi_variant(opid, (flags & MGP_UF_STORE) != 0, (flags & MGP_UF_MASK) != 0);
+    // an operand in vA and no operand B: nothing to fetch, dispatch straight to the op
+    const uint32_t first = (a.kind == KACC && b.kind == KNONE) ? opid : fetch_id(a.kind, b.kind, false);
     emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
   }
 

@@ -104,12 +104,14 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         first = names[w0 & 0xFFFF]
         op = names[w0 >> 16]
         pa, pb = w1 & 0xFFFF, w1 >> 16
-        if first.startswith("F_"):
-            _, ka, kb, tgt = first.split("_")
+        if first not in U.BOOL_OPS:
+            # mask / sign constants named by the uop (the kernel's handlers load them)
             if w2 & U.F_MASK:
                 KM = pool((w2 >> 16) & 0x3F)
             if w2 & U.F_SEXT:
                 KH = pool(w3 & 0x3F)
+        if first.startswith("F_"):
+            _, ka, kb, tgt = first.split("_")
             if kb != "none":
                 vB = vA if kb == "acc" else load(kb, pb)
             if ka != "acc":

@@ -253,6 +253,47 @@ def amount_from_vB():
       f"v_and_b32 v4, 0xff, {v(VB)}")
 
 
+def top_limb(base, out):
+    """out = index of the top non-zero limb of the 256-bit value at base (0 when zero)."""
+    A(f"v_mov_b32 {v(out)}, 0")
+    for i in range(1, 8):
+        A(f"v_cmp_ne_u32 vcc, 0, {v(base + i)}", f"v_cndmask_b32_e64 {v(out)}, {v(out)}, {i}, vcc")
+
+
+def limb_masks(vk):
+    """Per-lane limb count vk (0..7) -> stage masks s[48:49] (4), s[50:51] (2), s[52:53] (1)."""
+    A(f"v_and_b32 v7, 4, {v(vk)}", "v_cmp_ne_u32_e64 s[48:49], 0, v7",
+      f"v_and_b32 v7, 2, {v(vk)}", "v_cmp_ne_u32_e64 s[50:51], 0, v7",
+      f"v_and_b32 v7, 1, {v(vk)}", "v_cmp_ne_u32_e64 s[52:53], 0, v7")
+
+
+def shl_limbs(regs, nz):
+    """In-place per-lane left shift by whole limbs after limb_masks; nz = number of low
+    limbs that may be non-zero on entry."""
+    n = len(regs)
+    for L, m in ((4, "s[48:49]"), (2, "s[50:51]"), (1, "s[52:53]")):
+        new_nz = min(n, nz + L)
+        for i in range(new_nz - 1, -1, -1):
+            src = i - L
+            if i >= nz:
+                if src >= 0:
+                    A(f"v_cndmask_b32_e64 {v(regs[i])}, 0, {v(regs[src])}, {m}")
+            elif src < 0:
+                A(f"v_cndmask_b32_e64 {v(regs[i])}, {v(regs[i])}, 0, {m}")
+            else:
+                A(f"v_cndmask_b32_e64 {v(regs[i])}, {v(regs[i])}, {v(regs[src])}, {m}")
+        nz = new_nz
+
+
+def shr_limbs(regs):
+    """In-place per-lane right shift by whole limbs after limb_masks (zero fill)."""
+    n = len(regs)
+    for L, m in ((4, "s[48:49]"), (2, "s[50:51]"), (1, "s[52:53]")):
+        for i in range(n):
+            val = v(regs[i + L]) if i + L < n else "0"
+            A(f"v_cndmask_b32_e64 {v(regs[i])}, {v(regs[i])}, {val}, {m}")
+
+
 # ---------------------------------------------------------------- handlers
 
 HBODY = {}
@@ -818,31 +859,16 @@ def vn(i):
     return v(VN + i)
 
 
-def bitlen_chain(base, out):
-    """out = bit length of the 256-bit value at base (garbage when zero); v60/v61/v62 scratch.
-    Returns with s[48:49] = (value != 0)."""
-    A("v_mov_b32 v60, 0", f"v_mov_b32 v61, {v(base)}")
-    for i in range(1, 8):
-        A(f"v_cmp_ne_u32 vcc, 0, {v(base + i)}",
-          f"v_cndmask_b32_e64 v60, v60, {i}, vcc",
-          f"v_cndmask_b32 v61, v61, {v(base + i)}, vcc")
-    A("v_mov_b32 v59, v60",
-      "v_ffbh_u32 v62, v61",
-      "v_lshlrev_b32 v60, 5, v60",
-      "v_add_u32 v60, 32, v60",
-      f"v_sub_u32 {v(out)}, v60, v62",
-      "v_cmp_ne_u32_e64 s[48:49], 0, v61")
-
-
 def knuth_digit(J):
     """One quotient digit of Knuth's algorithm D at window u[J..J+8] (vn normalised).
 
-    qhat = floor(U3/V2 + 2^-12) in double precision, U3 = u[J+8..J+6] (96 bits),
-    V2 = vn7:vn6 (64 bits, top bit set).  |U3/V2 - U/V| <= 2^-31 and the double
-    evaluation is within 2^-18 of U3/V2 (1/V2 from v_rcp_f64 + two Newton steps), so
-    with the 2^-12 bias qhat is the true digit q or q+1 — never below it.  q+1 makes the
-    multiply-subtract go negative: one add-back, taken by a wave only when one of its
-    lanes sits within 2^-12 of the next integer.
+    qhat = floor(2^32 U3/V3 + 2^-12) in double precision, U3 = u[J+8..J+6] (96 bits),
+    V3 = vn7:vn6:vn5 (96 bits, vn7 != 0 after the limb normalisation, so V3 >= 2^64).
+    Truncating U and V to those limbs moves U/V by at most 2^32/V3 <= 2^-32, and the
+    double evaluation is within 2^-18 of 2^32 U3/V3 (2^32/V3 from v_rcp_f64 + two Newton
+    steps), so with the 2^-12 bias qhat is the true digit q or q+1 — never below it.  q+1
+    makes the multiply-subtract go negative: one add-back, taken by a wave only when one
+    of its lanes sits within 2^-12 of the next integer.
     """
     A(f"v_cvt_f64_u32 v[30:31], {u(J + 8)}",
       f"v_cvt_f64_u32 v[4:5], {u(J + 7)}",
@@ -909,40 +935,40 @@ def h_div():
     A.label(lus)
     A("v_mov_b32 v24, 0", "v_mov_b32 v25, 0")
     A.label(lsd)
-    # lb = bitlen(b) -> v60 path into v26 temporarily; bnz -> s[26:27]
-    bitlen_chain(VB, 26)                               # v26 = lb, v59 = top limb index of b
-    A("s_mov_b64 s[26:27], s[48:49]")
-    # top non-zero limb index of a -> v27
-    A("v_mov_b32 v27, 0")
-    for i in range(1, 8):
-        A(f"v_cmp_ne_u32 vcc, 0, {v(VA + i)}", f"v_cndmask_b32_e64 v27, v27, {i}, vcc")
-    # a < b ?
+    # divides = b != 0 && a >= b, first: a wave where no lane divides skips everything else
+    or_reduce(61, range(VB, VB + 8))
+    A("v_cmp_ne_u32_e64 s[26:27], 0, v61")             # bnz
     ult_chain(VA, VB, tmp=62)
-    A("s_andn2_b64 s[24:25], s[26:27], vcc")          # divides = b != 0 && a >= b
-    # d = top limb(a) - top limb(b): quotient digits J > d are zero (u unchanged) -> skipped
-    A("v_sub_u32 v27, v27, v59",
-      "v_cndmask_b32_e64 v27, -1, v27, s[24:25]",
-      "v_sub_u32 v26, 0x100, v26",                     # s = 256 - lb
-      "v_cndmask_b32_e64 v26, 0, v26, s[24:25]")
+    A("s_andn2_b64 s[24:25], s[26:27], vcc")
     lpost = A.fresh("divpost")
-    # u = a (512 bits) before the all-lanes-trivial skip: a lane that does not divide keeps
-    # s = 0, and its digits are zero (qhat <= 1 with an exact add-back), so u[0..7] = a is
-    # its remainder and vA is free as scratch for the digit products
+    # u[0..7] = a: the remainder of a lane that does not divide (its shift is 0 and every
+    # digit of it is forced to 0, so u[0..7] stays a); vA is then free as product scratch
     copy8(UQ, VA)
+    A("s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {lpost}")
     for i in range(8, 16):
         A(f"v_mov_b32 {u(i)}, 0")
-    A("s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {lpost}")
-    # normalise: vn = b << s, u = a << s
+    # d = top limb(a) - top limb(b) (-1 when not dividing): digits J > d are zero
+    top_limb(VB, 59)
+    top_limb(VA, 27)
+    A("v_sub_u32 v27, v27, v59",
+      "v_cndmask_b32_e64 v27, -1, v27, s[24:25]",
+      "v_sub_u32 v26, 7, v59",                         # k = 7 - top limb(b) limbs
+      "v_cndmask_b32_e64 v26, 0, v26, s[24:25]")
+    # limb normalisation: vn = b << 32k, u = a << 32k (vn7 != 0 on dividing lanes; no bit
+    # shift is needed because qhat is estimated from the top three limbs of vn)
     copy8(VN, VB)
-    shift_setup(26, left=True)
-    shl_var(list(range(VN, VN + 8)), 8)
-    shl_var(list(range(UQ, UQ + 16)), 8)
-    # 1 / vn7 in double precision (rcp + one Newton step)
+    limb_masks(26)
+    shl_limbs(list(range(VN, VN + 8)), 8)
+    shl_limbs(list(range(UQ, UQ + 16)), 8)
+    # 2^32 / V3, V3 = vn7*2^64 + vn6*2^32 + vn5, in double precision (rcp + two Newton steps)
     A("s_mov_b32 s62, 0", "s_mov_b32 s63, 0x41f00000",      # 2^32
       "s_mov_b32 s28, 0", "s_mov_b32 s29, 0x3f300000",      # 2^-12 (qhat bias)
       f"v_cvt_f64_u32 v[30:31], {vn(7)}",
       f"v_cvt_f64_u32 v[4:5], {vn(6)}",
-      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",   # V2 = vn7*2^32 + vn6
+      f"v_cvt_f64_u32 v[6:7], {vn(5)}",
+      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",
+      "v_mov_b32 v4, 0", "v_mov_b32 v5, 0x3df00000",         # 2^-32
+      "v_fma_f64 v[30:31], v[6:7], v[4:5], v[30:31]",      # V3 / 2^32
       "v_rcp_f64 v[28:29], v[30:31]",
       "s_nop 1",
       "v_fma_f64 v[4:5], -v[30:31], v[28:29], 1.0",
@@ -955,12 +981,12 @@ def h_div():
           "s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lskip}")
         knuth_digit(J)
         A.label(lskip)
-    # remainder = u[0..7] >> s  (only UREM/SREM/SMOD need it)
+    # remainder = u[0..7] >> 32k  (only UREM/SREM/SMOD need it)
     lnorem = A.fresh("norem")
     A("s_cmp_eq_u32 s61, 0", f"s_cbranch_scc1 {lnorem}",
       "s_cmp_eq_u32 s61, 2", f"s_cbranch_scc1 {lnorem}")
-    shift_setup(26, left=False)
-    shr_var(list(range(UQ, UQ + 8)), "0")
+    limb_masks(26)
+    shr_limbs(list(range(UQ, UQ + 8)))
     A.label(lnorem)
     A.label(lpost)
     # per lane: dividing -> (q = u[8..15], r = u[0..7]); else q = (b == 0 ? ~0 : 0), r = u[0..7] = a

@@ -311,7 +311,7 @@ def wait_operands():
 
 
 # uop flag bits (w2 = s18, w3 = s19; see uop_spec)
-B_STORE, B_MASK, B_SEXT, B_INVERT = 22, 23, 24, 25
+B_STORE, B_MASK, B_SEXT, B_INVERT, B_REGST = 22, 23, 24, 25, 29
 
 
 def load_km():
@@ -335,6 +335,16 @@ def store_slot():
       f"ds_write_b128 v4, {vr(VA + 4, 4)} offset:1024")
 
 
+def store_reg():
+    """vA -> register-bank position p (w2[15:0] = 8p): GPR-index mode offsets the
+    destination of the moves into v[64:111]."""
+    A("s_and_b32 s48, s18, 0xffff",
+      "s_set_gpr_idx_on s48, gpr_idx(DST)")
+    for i in range(8):
+        A(f"v_mov_b32 {v(RV + i)}, {v(VA + i)}")
+    A("s_set_gpr_idx_off")
+
+
 EPI_MODE = [None]   # None: test the STORE/MASK flags at run time; else the variant's fixed epilogue
 
 
@@ -348,6 +358,8 @@ def bv_epilogue():
                 A(f"v_and_b32 {v(VA + i)}, {s(S_KM + i)}, {v(VA + i)}")
         if "S" in mode:
             store_slot()
+        if "R" in mode:
+            store_reg()
         tail()
         return
     lm, ls = A.fresh("mask"), A.fresh("store")
@@ -363,8 +375,15 @@ def bv_epilogue():
         tail()
 
     def stored():
+        lr = A.fresh("regst")
+        A(f"s_bitcmp1_b32 s18, {B_REGST}", f"s_cbranch_scc1 {lr}")
         store_slot()
         tail()
+
+        def reg():
+            store_reg()
+            tail()
+        A.out_of_line(lr, reg)
     A.out_of_line(lm, masked)
     A.out_of_line(ls, stored)
 

@@ -659,7 +659,10 @@ __global__ void mgp_desc_kernel(const uint32_t *__restrict__ words, const uint64
     page = reinterpret_cast<uint64_t>(u + 4);
     pool_rel = uh.z - 16u;
   }
-  desc[2 * (size_t)p] = make_uint4(state, undec, h.z, n_uops);
+  // slots: the LDS slots the interpreter allocates for the state (uop header word 3
+  // bits 16..23: the v1 slot count minus the register slots)
+  const uint32_t lds_slots = undec ? h.z : (npm >> 16) & 0xFFu;
+  desc[2 * (size_t)p] = make_uint4(state, undec, lds_slots, n_uops);
   desc[2 * (size_t)p + 1] = make_uint4((uint32_t)page, (uint32_t)(page >> 32), pool_rel, npm);
 }
 

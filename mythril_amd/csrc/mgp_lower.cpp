@@ -618,8 +618,18 @@ extern "C" int mgp_plan_buckets(const uint32_t *prog_words, const uint64_t *prog
   if (!prog_words || !prog_offsets || !order_out || !bounds_out || !slots_out || max_buckets == 0) return MGP_E_ARG;
   std::vector<uint32_t> cnt(257, 0);
   std::vector<uint16_t> sl(n_states);
+  // the gfx950 interpreter keeps some BV slots in registers: it allocates the LDS slot
+  // count of the uop header (word 3 bits 16..23) instead of the v1 count
+  const bool asm_engine = mgp_set_eval_engine(0) == MGP_ENGINE_ASM;
   for (uint32_t s = 0; s < n_states; ++s) {
-    const uint32_t v = std::min<uint32_t>(prog_words[prog_offsets[s] + 2], 256u);
+    const uint32_t *w = prog_words + prog_offsets[s];
+    uint32_t v = w[2];
+    if (asm_engine && (w[3] & 0xFFu) == MGP_ST_OK) {
+      const uint32_t v1 = 4u + 4u * w[0] + 8u * w[1];
+      const uint32_t *u = w + ((v1 + 3u) & ~3u) + 4u;
+      if (u[1] == 0u) v = (u[3] >> 16) & 0xFFu;
+    }
+    v = std::min<uint32_t>(v, 256u);
     sl[s] = (uint16_t)v;
     cnt[v]++;
   }

@@ -56,6 +56,9 @@ struct Translator {
   uint32_t n_ins, n_c;
   std::vector<uint32_t> pool;        // 8 words per constant
   uint32_t var_mask = 0;             // register variables the program reads (preloaded)
+  // register slots: BV slots idx >= n_lds live in register-bank position reg_pos[idx - n_lds]
+  uint32_t n_lds = 0xFFFFFFFFu;
+  uint8_t reg_pos[MGP_U_REG_VARS] = {0};
   std::map<uint32_t, uint32_t> mask_c, sign_c;  // width -> pool index
   bool bad = false;
 
@@ -95,6 +98,7 @@ struct Translator {
     switch (kind) {
       case MGP_K_ACC: return {KACC, 0};
       case MGP_K_SLOT:
+        if (idx >= n_lds) return {KRVAR, reg_pos[idx - n_lds]};
         if (idx >= MGP_U_MAX_LDS_SLOTS) bad = true;
         return {KSLOT, idx * MGP_U_SLOT_BYTES};
       case MGP_K_CONST: return {KCONST, pool_byte(idx)};
@@ -126,16 +130,19 @@ struct Translator {
 
 // w0 = entry offsets of the first handler and of the op handler (fetch handlers jump to it)
 // cheap BV ops have handler variants with a fixed epilogue (no flag tests at run time)
-inline uint32_t epi_variant(uint32_t op, bool store, bool mask) {
+inline uint32_t epi_variant(uint32_t op, bool store, bool mask, bool reg) {
   if (!store && !mask) return op;
-  static const uint32_t T[][4] = {
-      {MGP_U_ADD, MGP_U_ADD_S, MGP_U_ADD_M, MGP_U_ADD_MS}, {MGP_U_SUB, MGP_U_SUB_S, MGP_U_SUB_M, MGP_U_SUB_MS},
-      {MGP_U_AND, MGP_U_AND_S, MGP_U_AND_M, MGP_U_AND_MS}, {MGP_U_OR, MGP_U_OR_S, MGP_U_OR_M, MGP_U_OR_MS},
-      {MGP_U_XOR, MGP_U_XOR_S, MGP_U_XOR_M, MGP_U_XOR_MS}, {MGP_U_NOT, MGP_U_NOT_S, MGP_U_NOT_M, MGP_U_NOT_MS},
-      {MGP_U_NEG, MGP_U_NEG_S, MGP_U_NEG_M, MGP_U_NEG_MS}, {MGP_U_MOV, MGP_U_MOV_S, MGP_U_MOV_M, MGP_U_MOV_MS},
-      {MGP_U_ITE, MGP_U_ITE_S, MGP_U_ITE_M, MGP_U_ITE_MS}};
+#define MGP_EPI_ROW(o) {MGP_U_##o, MGP_U_##o##_S, MGP_U_##o##_M, MGP_U_##o##_MS, MGP_U_##o##_R, MGP_U_##o##_MR}
+  static const uint32_t T[][6] = {MGP_EPI_ROW(ADD), MGP_EPI_ROW(SUB), MGP_EPI_ROW(AND), MGP_EPI_ROW(OR),
+                                  MGP_EPI_ROW(XOR), MGP_EPI_ROW(NOT), MGP_EPI_ROW(NEG), MGP_EPI_ROW(MOV),
+                                  MGP_EPI_ROW(ITE)};
+#undef MGP_EPI_ROW
   for (const auto &e : T)
-    if (e[0] == op) return mask ? (store ? e[3] : e[2]) : e[1];
+    if (e[0] == op) {
+      if (!store) return e[2];
+      if (reg) return mask ? e[5] : e[4];
+      return mask ? e[3] : e[1];
+    }
   return op;
 }
 
@@ -162,159 +169,181 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     uops.push_back(w0); uops.push_back(w1); uops.push_back(w2); uops.push_back(w3);
   };
 
-  for (uint32_t pc = 0; v1_ok && pc < T.n_ins && !T.bad; ++pc) {
-    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
-    const uint32_t op = I[0] & 0xFFu, width = ((I[0] >> 8) & 0xFFu) + 1u, dst = (I[0] >> 16) & 0xFFu;
-    const bool store = ((I[0] >> 24) & MGP_INS_STORE) != 0;
-    const uint32_t oa = I[1] & 0xFFFFu, ob = I[1] >> 16, oc = I[2] & 0xFFFFu, imm = I[2] >> 16;
-    const bool narrow = width < 256u;
+  auto translate = [&]() {
+    for (uint32_t pc = 0; v1_ok && pc < T.n_ins && !T.bad; ++pc) {
+      const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
+      const uint32_t op = I[0] & 0xFFu, width = ((I[0] >> 8) & 0xFFu) + 1u, dst = (I[0] >> 16) & 0xFFu;
+      const bool store = ((I[0] >> 24) & MGP_INS_STORE) != 0;
+      const uint32_t oa = I[1] & 0xFFFFu, ob = I[1] >> 16, oc = I[2] & 0xFFFFu, imm = I[2] >> 16;
+      const bool narrow = width < 256u;
 
-    if (op == MGP_OP_RET) {
-      emit(w0_of(MGP_U_RET, MGP_U_RET), T.boolslot(oa), 0, 0);
-      break;
-    }
-    if (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) {
-      static const uint32_t ids[] = {MGP_U_BAND, MGP_U_BOR, MGP_U_BXOR, MGP_U_BNOT, MGP_U_BITE, MGP_U_BEQ};
-      const uint32_t id = ids[op - MGP_OP_BAND];
-      emit(w0_of(id, id), T.boolslot(oa) | (T.boolslot(ob) << 16), T.boolslot(oc), T.boolslot(dst) << 16);
-      continue;
-    }
-    if (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) {
-      Opnd a = T.bv(oa), b = T.bv(ob);
-      // base compare, invert, commutes-with-swap partner
-      uint32_t base;
-      bool inv = false;
+      if (op == MGP_OP_RET) {
+        emit(w0_of(MGP_U_RET, MGP_U_RET), T.boolslot(oa), 0, 0);
+        break;
+      }
+      if (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) {
+        static const uint32_t ids[] = {MGP_U_BAND, MGP_U_BOR, MGP_U_BXOR, MGP_U_BNOT, MGP_U_BITE, MGP_U_BEQ};
+        const uint32_t id = ids[op - MGP_OP_BAND];
+        emit(w0_of(id, id), T.boolslot(oa) | (T.boolslot(ob) << 16), T.boolslot(oc), T.boolslot(dst) << 16);
+        continue;
+      }
+      if (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) {
+        Opnd a = T.bv(oa), b = T.bv(ob);
+        // base compare, invert, commutes-with-swap partner
+        uint32_t base;
+        bool inv = false;
+        switch (op) {
+          case MGP_OP_EQ: base = MGP_U_EQ_RA; break;
+          case MGP_OP_ULT: base = MGP_U_ULT_RA; break;
+          case MGP_OP_UGE: base = MGP_U_ULT_RA; inv = true; break;
+          case MGP_OP_UGT: base = MGP_U_UGT_RA; break;
+          case MGP_OP_ULE: base = MGP_U_UGT_RA; inv = true; break;
+          case MGP_OP_SLT: base = MGP_U_SLT_RA; break;
+          case MGP_OP_SGE: base = MGP_U_SLT_RA; inv = true; break;
+          case MGP_OP_SGT: base = MGP_U_SGT_RA; break;
+          case MGP_OP_SLE: base = MGP_U_SGT_RA; inv = true; break;
+          case MGP_OP_UADD_NOOVF: base = narrow ? MGP_U_UADDNOW_RA : MGP_U_UADDNO256_RA; inv = true; break;
+          case MGP_OP_UMUL_NOOVF: base = narrow ? MGP_U_UMULNOW_RA : MGP_U_UMULNO256_RA; inv = true; break;
+          default: base = MGP_U_ULT_RA; inv = true; break;  // USUB_NOUDF(a,b) = !(a < b)
+        }
+        if (b.kind == KACC && a.kind != KACC) {
+          std::swap(a, b);
+          if (base == MGP_U_ULT_RA) base = MGP_U_UGT_RA;
+          else if (base == MGP_U_UGT_RA) base = MGP_U_ULT_RA;
+          else if (base == MGP_U_SLT_RA) base = MGP_U_SGT_RA;
+          else if (base == MGP_U_SGT_RA) base = MGP_U_SLT_RA;
+        }
+        uint32_t flags = inv ? MGP_UF_INVERT : 0u, w2 = 0, w3 = T.boolslot(dst) << 16;
+        if (narrow && (base == MGP_U_SLT_RA || base == MGP_U_SGT_RA)) {
+          flags |= MGP_UF_SEXT;
+          w3 |= T.sign_off(width);
+        }
+        if (base == MGP_U_UADDNOW_RA || base == MGP_U_UMULNOW_RA) {
+          flags |= MGP_UF_MASK;
+          w2 |= T.mask_off(width) << 16;
+        }
+        const bool ra = a.kind == KACC;
+        const uint32_t opid = ra ? base : base + 1u;  // _RC follows _RA
+        const uint32_t first = fetch_id(a.kind, b.kind, !ra);
+        emit(w0_of(first, opid), (ra ? 0u : a.param) | (b.param << 16), w2 | flags, w3);
+        continue;
+      }
+      // ---- BV-producing
+      uint32_t flags = 0, w2 = 0, w3 = 0, opid = 0;
+      Opnd a = {KNONE, 0}, b = {KNONE, 0};
+      bool need_mask = false;
       switch (op) {
-        case MGP_OP_EQ: base = MGP_U_EQ_RA; break;
-        case MGP_OP_ULT: base = MGP_U_ULT_RA; break;
-        case MGP_OP_UGE: base = MGP_U_ULT_RA; inv = true; break;
-        case MGP_OP_UGT: base = MGP_U_UGT_RA; break;
-        case MGP_OP_ULE: base = MGP_U_UGT_RA; inv = true; break;
-        case MGP_OP_SLT: base = MGP_U_SLT_RA; break;
-        case MGP_OP_SGE: base = MGP_U_SLT_RA; inv = true; break;
-        case MGP_OP_SGT: base = MGP_U_SGT_RA; break;
-        case MGP_OP_SLE: base = MGP_U_SGT_RA; inv = true; break;
-        case MGP_OP_UADD_NOOVF: base = narrow ? MGP_U_UADDNOW_RA : MGP_U_UADDNO256_RA; inv = true; break;
-        case MGP_OP_UMUL_NOOVF: base = narrow ? MGP_U_UMULNOW_RA : MGP_U_UMULNO256_RA; inv = true; break;
-        default: base = MGP_U_ULT_RA; inv = true; break;  // USUB_NOUDF(a,b) = !(a < b)
+        case MGP_OP_ADD: case MGP_OP_MUL: case MGP_OP_AND: case MGP_OP_OR: case MGP_OP_XOR: {
+          a = T.bv(oa); b = T.bv(ob);
+          if (b.kind == KACC && a.kind != KACC) std::swap(a, b);
+          opid = op == MGP_OP_ADD ? MGP_U_ADD : op == MGP_OP_MUL ? MGP_U_MUL : op == MGP_OP_AND ? MGP_U_AND
+               : op == MGP_OP_OR ? MGP_U_OR : MGP_U_XOR;
+          need_mask = narrow && (op == MGP_OP_ADD || op == MGP_OP_MUL);
+          break;
+        }
+        case MGP_OP_SUB:
+          a = T.bv(oa); b = T.bv(ob); opid = MGP_U_SUB; need_mask = narrow;
+          break;
+        case MGP_OP_SHL: case MGP_OP_LSHR: case MGP_OP_ASHR: {
+          a = T.bv(oa);
+          if ((ob >> 14) == MGP_K_CONST) {
+            uint32_t lo;
+            bool big;
+            T.const_value(ob, &lo, &big);
+            const uint32_t k = big ? 8u : lo >> 5, sb = big ? 0u : lo & 31u;
+            opid = (op == MGP_OP_SHL ? MGP_U_SHLI0 : op == MGP_OP_LSHR ? MGP_U_LSHRI0 : MGP_U_ASHRI0) + k;
+            w3 |= sb << MGP_U_SHIFT_B_POS;
+          } else {
+            b = T.bv(ob);
+            opid = op == MGP_OP_SHL ? MGP_U_SHL : op == MGP_OP_LSHR ? MGP_U_LSHR : MGP_U_ASHR;
+          }
+          if (op == MGP_OP_ASHR && narrow) {
+            flags |= MGP_UF_SEXT;
+            w3 |= T.sign_off(width);
+          }
+          need_mask = narrow && op != MGP_OP_LSHR;
+          break;
+        }
+        case MGP_OP_UDIV: case MGP_OP_UREM: case MGP_OP_SDIV: case MGP_OP_SREM: case MGP_OP_SMOD: {
+          a = T.bv(oa); b = T.bv(ob); opid = MGP_U_DIV;
+          static const uint32_t dv[] = {MGP_DIV_UDIV, MGP_DIV_UREM, MGP_DIV_SDIV, MGP_DIV_SREM, MGP_DIV_SMOD};
+          flags |= dv[op - MGP_OP_UDIV] << MGP_U_DIVOP_POS;
+          if (narrow && op >= MGP_OP_SDIV) {
+            flags |= MGP_UF_SEXT;
+            w3 |= T.sign_off(width);
+          }
+          need_mask = narrow && op != MGP_OP_UREM;
+          break;
+        }
+        case MGP_OP_NOT: case MGP_OP_NEG:
+          a = T.bv(oa); opid = op == MGP_OP_NOT ? MGP_U_NOT : MGP_U_NEG; need_mask = narrow;
+          break;
+        case MGP_OP_MOV: case MGP_OP_ZEXT:
+          a = T.bv(oa); opid = MGP_U_MOV; need_mask = narrow;
+          break;
+        case MGP_OP_EXTRACT:
+          a = T.bv(oa);
+          if (imm == 0) {
+            opid = MGP_U_MOV;
+          } else {
+            opid = MGP_U_LSHRI0 + (imm >> 5);
+            w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
+          }
+          need_mask = narrow;
+          break;
+        case MGP_OP_SEXT:
+          a = T.bv(oa); opid = MGP_U_SEXT; w3 |= T.sign_off(imm); need_mask = narrow;
+          break;
+        case MGP_OP_CONCAT:
+          a = T.bv(oa); b = T.bv(ob);
+          if (imm == 0 || imm >= 256u) { T.bad = true; break; }
+          opid = MGP_U_CONCAT0 + (imm >> 5);
+          w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
+          break;
+        case MGP_OP_ITE:
+          a = T.bv(ob); b = T.bv(oc); opid = MGP_U_ITE;
+          w3 |= T.boolslot(oa) << 16;
+          break;
+        default:
+          T.bad = true;
       }
-      if (b.kind == KACC && a.kind != KACC) {
-        std::swap(a, b);
-        if (base == MGP_U_ULT_RA) base = MGP_U_UGT_RA;
-        else if (base == MGP_U_UGT_RA) base = MGP_U_ULT_RA;
-        else if (base == MGP_U_SLT_RA) base = MGP_U_SGT_RA;
-        else if (base == MGP_U_SGT_RA) base = MGP_U_SLT_RA;
-      }
-      uint32_t flags = inv ? MGP_UF_INVERT : 0u, w2 = 0, w3 = T.boolslot(dst) << 16;
-      if (narrow && (base == MGP_U_SLT_RA || base == MGP_U_SGT_RA)) {
-        flags |= MGP_UF_SEXT;
-        w3 |= T.sign_off(width);
-      }
-      if (base == MGP_U_UADDNOW_RA || base == MGP_U_UMULNOW_RA) {
+      if (T.bad) break;
+      if (need_mask) {
         flags |= MGP_UF_MASK;
         w2 |= T.mask_off(width) << 16;
       }
-      const bool ra = a.kind == KACC;
-      const uint32_t opid = ra ? base : base + 1u;  // _RC follows _RA
-      const uint32_t first = fetch_id(a.kind, b.kind, !ra);
-      emit(w0_of(first, opid), (ra ? 0u : a.param) | (b.param << 16), w2 | flags, w3);
-      continue;
-    }
-    // ---- BV-producing
-    uint32_t flags = 0, w2 = 0, w3 = 0, opid = 0;
-    Opnd a = {KNONE, 0}, b = {KNONE, 0};
-    bool need_mask = false;
-    switch (op) {
-      case MGP_OP_ADD: case MGP_OP_MUL: case MGP_OP_AND: case MGP_OP_OR: case MGP_OP_XOR: {
-        a = T.bv(oa); b = T.bv(ob);
-        if (b.kind == KACC && a.kind != KACC) std::swap(a, b);
-        opid = op == MGP_OP_ADD ? MGP_U_ADD : op == MGP_OP_MUL ? MGP_U_MUL : op == MGP_OP_AND ? MGP_U_AND
-             : op == MGP_OP_OR ? MGP_U_OR : MGP_U_XOR;
-        need_mask = narrow && (op == MGP_OP_ADD || op == MGP_OP_MUL);
-        break;
+      if (store && dst >= T.n_lds) {
+        flags |= MGP_UF_STORE | MGP_UF_REGST;
+        w2 |= (uint32_t)T.reg_pos[dst - T.n_lds] * 8u;
+      } else if (store) {
+        if (dst >= MGP_U_MAX_LDS_SLOTS) { T.bad = true; break; }
+        flags |= MGP_UF_STORE;
+        w2 |= dst * MGP_U_SLOT_BYTES;
       }
-      case MGP_OP_SUB:
-        a = T.bv(oa); b = T.bv(ob); opid = MGP_U_SUB; need_mask = narrow;
-        break;
-      case MGP_OP_SHL: case MGP_OP_LSHR: case MGP_OP_ASHR: {
-        a = T.bv(oa);
-        if ((ob >> 14) == MGP_K_CONST) {
-          uint32_t lo;
-          bool big;
-          T.const_value(ob, &lo, &big);
-          const uint32_t k = big ? 8u : lo >> 5, sb = big ? 0u : lo & 31u;
-          opid = (op == MGP_OP_SHL ? MGP_U_SHLI0 : op == MGP_OP_LSHR ? MGP_U_LSHRI0 : MGP_U_ASHRI0) + k;
-          w3 |= sb << MGP_U_SHIFT_B_POS;
-        } else {
-          b = T.bv(ob);
-          opid = op == MGP_OP_SHL ? MGP_U_SHL : op == MGP_OP_LSHR ? MGP_U_LSHR : MGP_U_ASHR;
-        }
-        if (op == MGP_OP_ASHR && narrow) {
-          flags |= MGP_UF_SEXT;
-          w3 |= T.sign_off(width);
-        }
-        need_mask = narrow && op != MGP_OP_LSHR;
-        break;
-      }
-      case MGP_OP_UDIV: case MGP_OP_UREM: case MGP_OP_SDIV: case MGP_OP_SREM: case MGP_OP_SMOD: {
-        a = T.bv(oa); b = T.bv(ob); opid = MGP_U_DIV;
-        static const uint32_t dv[] = {MGP_DIV_UDIV, MGP_DIV_UREM, MGP_DIV_SDIV, MGP_DIV_SREM, MGP_DIV_SMOD};
-        flags |= dv[op - MGP_OP_UDIV] << MGP_U_DIVOP_POS;
-        if (narrow && op >= MGP_OP_SDIV) {
-          flags |= MGP_UF_SEXT;
-          w3 |= T.sign_off(width);
-        }
-        need_mask = narrow && op != MGP_OP_UREM;
-        break;
-      }
-      case MGP_OP_NOT: case MGP_OP_NEG:
-        a = T.bv(oa); opid = op == MGP_OP_NOT ? MGP_U_NOT : MGP_U_NEG; need_mask = narrow;
-        break;
-      case MGP_OP_MOV: case MGP_OP_ZEXT:
-        a = T.bv(oa); opid = MGP_U_MOV; need_mask = narrow;
-        break;
-      case MGP_OP_EXTRACT:
-        a = T.bv(oa);
-        if (imm == 0) {
-          opid = MGP_U_MOV;
-        } else {
-          opid = MGP_U_LSHRI0 + (imm >> 5);
-          w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
-        }
-        need_mask = narrow;
-        break;
-      case MGP_OP_SEXT:
-        a = T.bv(oa); opid = MGP_U_SEXT; w3 |= T.sign_off(imm); need_mask = narrow;
-        break;
-      case MGP_OP_CONCAT:
-        a = T.bv(oa); b = T.bv(ob);
-        if (imm == 0 || imm >= 256u) { T.bad = true; break; }
-        opid = MGP_U_CONCAT0 + (imm >> 5);
-        w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
-        break;
-      case MGP_OP_ITE:
-        a = T.bv(ob); b = T.bv(oc); opid = MGP_U_ITE;
-        w3 |= T.boolslot(oa) << 16;
-        break;
-      default:
-        T.bad = true;
+      opid = epi_variant(opid, (flags & MGP_UF_STORE) != 0, (flags & MGP_UF_MASK) != 0,
+                         (flags & MGP_UF_REGST) != 0);
+      // an operand in vA and no operand B: nothing to fetch, dispatch straight to the op
+      const uint32_t first = (a.kind == KACC && b.kind == KNONE) ? opid : fetch_id(a.kind, b.kind, false);
+      emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
     }
-    if (T.bad) break;
-    if (need_mask) {
-      flags |= MGP_UF_MASK;
-      w2 |= T.mask_off(width) << 16;
-    }
-    if (store) {
-      if (dst >= MGP_U_MAX_LDS_SLOTS) { T.bad = true; break; }
-      flags |= MGP_UF_STORE;
-      w2 |= dst * MGP_U_SLOT_BYTES;
-    }
-    opid = epi_variant(opid, (flags & MGP_UF_STORE) != 0, (flags & MGP_UF_MASK) != 0);
-    // an operand in vA and no operand B: nothing to fetch, dispatch straight to the op
-    const uint32_t first = (a.kind == KACC && b.kind == KNONE) ? opid : fetch_id(a.kind, b.kind, false);
-    emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
+  };
+  // pass 1 finds the register variables the program reads; pass 2 maps the state's
+  // highest BV slots onto the register-bank positions no variable uses (register slots:
+  // fewer LDS slots per wave -> more resident waves)
+  translate();
+  const uint32_t n_slots = v1_ok ? v1[2] : 0u;
+  uint32_t n_lds = n_slots;
+  if (v1_ok && !T.bad) {
+    uint32_t free_pos[MGP_U_REG_VARS], n_free = 0;
+    for (uint32_t p = 0; p < MGP_U_REG_VARS; ++p)
+      if (!(T.var_mask & (1u << p))) free_pos[n_free++] = (uint32_t)p;
+    const uint32_t k = n_free < n_slots ? n_free : n_slots;
+    n_lds = n_slots - k;
+    for (uint32_t j = 0; j < k; ++j) T.reg_pos[j] = (uint8_t)free_pos[j];
+    T.n_lds = n_lds;
+    uops.clear();
+    translate();
   }
-
   if (!v1_ok || T.bad || uops.empty()) {
     out[base + 0] = 0;
     out[base + 1] = 1;  // not runnable: the kernel reports MGP_UNDECIDED
@@ -345,7 +374,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   out[base + 0] = n_uops;
   out[base + 1] = 0;
   out[base + 2] = (uint32_t)((MGP_U_HDR_WORDS + (n_uops + 1) * MGP_U_UOP_WORDS) * 4u);
-  out[base + 3] = (uint32_t)(T.pool.size() / 8) | (T.var_mask << 8);
+  out[base + 3] = (uint32_t)(T.pool.size() / 8) | (T.var_mask << 8) | (n_lds << 16);
   out.insert(out.end(), T.pool.begin(), T.pool.end());
   return 0;
 }

@@ -10,6 +10,7 @@ at word offset align4(4 + 4*n_ins + 8*n_consts) + 4 from the program start):
   header   4 words: n_uops, status (0 = runnable), pool byte offset (from the
            uop header), n_pool | register-variable mask << 8 (bit v: the program
            reads variable v < REG_VARS, which the kernel preloads into VGPRs)
+           | LDS slots << 16 (BV slots left in LDS after register slots)
   uops     n_uops x 4 words in pages of 64: uop 63 of every full page is PAGE
            (the kernel holds one page in 4 VGPRs, uop k in lane k, and reads
            the current uop with v_readlane; PAGE loads the next page), then one
@@ -24,15 +25,20 @@ uop words:
      [31:16] entry offset / 4 of the op handler (fetch handlers jump to it)
              (offsets come from the assembled kernel's symbol table, gen_offsets.py)
   w1 [15:0] operand A parameter, [31:16] operand B parameter
-            SLOT: LDS byte offset (slot*2048), VAR / RVAR: variable index,
+            SLOT: LDS byte offset (slot*2048), VAR: variable index, RVAR:
+            register-bank position (a preloaded variable, or a register slot),
             CONST: pool index; Bool operands: bool slot * 2
-  w2 [15:0] store slot byte offset / third Bool operand * 2
+  w2 [15:0] store slot byte offset, or 8 x bank position with REGST /
+            third Bool operand * 2
      [21:16] mask pool index
      [22] STORE   result -> LDS slot
      [23] MASK    result &= pool[mask] (2^w - 1); compares: M for the overflow tests
      [24] SEXT    operands sign-extended from width w with H = pool[w3[5:0]]
      [25] INVERT  compare result negated
      [28:26]      division variant (DIV_*)
+     [29] REGST   the STORE goes to register-bank position w2[15:0]/8 (v[64+8p]),
+                  not to LDS: the translator maps a state's highest BV slots onto
+                  bank positions no variable of that state uses
   w3 [5:0]  sign-constant pool index, [12:8] uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT),
      [31:16] Bool destination * 2 (compares, Bool ops) or ITE condition * 2
 
@@ -63,7 +69,7 @@ CMP_VARIANTS = [f"{c}_{r}" for c in CMPS for r in ("RA", "RC")]
 # epilogue-specialised variants of the cheap BV ops: _S store, _M mask, _MS both (the
 # translator picks one from the STORE/MASK flags, so these handlers test no flags)
 EPI_OPS = ["ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "MOV", "ITE"]
-EPI_VARIANTS = [f"{o}_{v}" for o in EPI_OPS for v in ("S", "M", "MS")]
+EPI_VARIANTS = [f"{o}_{v}" for o in EPI_OPS for v in ("S", "M", "MS", "R", "MR")]
 
 OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
@@ -75,6 +81,7 @@ assert len(HANDLERS) < 256
 DIV_VARIANTS = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
 
 F_STORE, F_MASK, F_SEXT, F_INVERT = 1 << 22, 1 << 23, 1 << 24, 1 << 25   # in w2
+F_REGST = 1 << 29                                                         # in w2
 SHIFT_B_POS = 8     # in w3
 DIVOP_POS = 26      # in w2
 
@@ -97,6 +104,7 @@ def c_header() -> str:
     lines += [
         f"#define MGP_UF_STORE {F_STORE}u", f"#define MGP_UF_MASK {F_MASK}u",
         f"#define MGP_UF_SEXT {F_SEXT}u", f"#define MGP_UF_INVERT {F_INVERT}u",
+        f"#define MGP_UF_REGST {F_REGST}u",
         f"#define MGP_U_SHIFT_B_POS {SHIFT_B_POS}", f"#define MGP_U_DIVOP_POS {DIVOP_POS}",
         f"#define MGP_U_BOOL_SLOTS {BOOL_SLOTS}", f"#define MGP_U_MAX_LDS_SLOTS {MAX_LDS_SLOTS}",
         f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",

@@ -90,10 +90,17 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
     bools = [False] * U.BOOL_SLOTS
     bools[1] = True
 
+    # register bank v[64:111]: position p holds variable p when the program reads it
+    # (preloaded), else it is a register slot written by REGST stores
+    var_mask = (int(words[u0 + 3]) >> 8) & 0xFF
+    bank = {p: int(xs[p]) & M256 for p in range(U.REG_VARS) if var_mask >> p & 1}
+
     def load(kind: str, p: int) -> int:
         if kind == "slot":
             return lds[p]
-        if kind in ("var", "rvar"):
+        if kind == "rvar":
+            return bank[p]
+        if kind == "var":
             return int(xs[p]) & M256
         return pool(p)
 
@@ -212,7 +219,12 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         if w2 & U.F_MASK:
             vA &= KM
         if w2 & U.F_STORE:
-            lds[w2 & 0xFFFF] = vA
+            if w2 & U.F_REGST:
+                pos = (w2 & 0xFFFF) // 8
+                assert not var_mask >> pos & 1, "register slot over a preloaded variable"
+                bank[pos] = vA
+            else:
+                lds[w2 & 0xFFFF] = vA
     raise ValueError("uop program fell off the end without RET")
 
 

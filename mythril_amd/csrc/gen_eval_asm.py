@@ -429,8 +429,7 @@ def fetch_one(kind, dst, which):
     if kind == "rvar":
         # v[dst+i] = v[64 + 8*var + i]: GPR-index mode (gfx950 has no v_movrels) offsets
         # SRC0 of the moves by 8*var into the preloaded variable bank
-        A(f"s_lshl_b32 {sp}, {sp}, 3",
-          f"s_set_gpr_idx_on {sp}, gpr_idx(SRC0)")
+        A(f"s_set_gpr_idx_on {sp}, gpr_idx(SRC0)")
         for i in range(8):
             A(f"v_mov_b32 {v(dst + i)}, {v(RV + i)}")
         A("s_set_gpr_idx_off")
@@ -570,11 +569,42 @@ def bin_limbs(name, first, rest):
         bv_epilogue()
 
 
-bin_limbs("ADD", "v_add_co_u32 {d}, vcc, {a}, {b}", "v_addc_co_u32 {d}, vcc, {a}, {b}, vcc")
-bin_limbs("SUB", "v_sub_co_u32 {d}, vcc, {a}, {b}", "v_subb_co_u32 {d}, vcc, {a}, {b}, vcc")
-bin_limbs("AND", "v_and_b32 {d}, {a}, {b}", "v_and_b32 {d}, {a}, {b}")
-bin_limbs("OR", "v_or_b32 {d}, {a}, {b}", "v_or_b32 {d}, {a}, {b}")
-bin_limbs("XOR", "v_xor_b32 {d}, {a}, {b}", "v_xor_b32 {d}, {a}, {b}")
+BIN_LIMBS = {
+    "ADD": ("v_add_co_u32 {d}, vcc, {a}, {b}", "v_addc_co_u32 {d}, vcc, {a}, {b}, vcc"),
+    "SUB": ("v_sub_co_u32 {d}, vcc, {a}, {b}", "v_subb_co_u32 {d}, vcc, {a}, {b}, vcc"),
+    "AND": ("v_and_b32 {d}, {a}, {b}", "v_and_b32 {d}, {a}, {b}"),
+    "OR": ("v_or_b32 {d}, {a}, {b}", "v_or_b32 {d}, {a}, {b}"),
+    "XOR": ("v_xor_b32 {d}, {a}, {b}", "v_xor_b32 {d}, {a}, {b}"),
+}
+for _n, (_f, _r) in BIN_LIMBS.items():
+    bin_limbs(_n, _f, _r)
+
+
+def make_xr(name):
+    """XR_<op>[_<epilogue>]: vA = vA op bank[B].  Operand B (w1[31:16] = 8p) is read as
+    the indexed SRC1 of the limb ops themselves (GPR-index mode), so the uop needs no
+    fetch handler, no moves and no operand wait (vA and the bank are both resident)."""
+    base = name[3:]
+    op, mode = (base.split("_", 1) + [""])[:2]
+    first, rest = BIN_LIMBS[op]
+
+    def body():
+        A("s_lshr_b32 s50, s17, 16",
+          "s_set_gpr_idx_on s50, gpr_idx(SRC1)",
+          first.format(d=v(VA), a=v(VA), b=v(RV)))
+        for i in range(1, 8):
+            A(rest.format(d=v(VA + i), a=v(VA + i), b=v(RV + i)))
+        A("s_set_gpr_idx_off")
+        EPI_MODE[0] = mode
+        try:
+            bv_epilogue()
+        finally:
+            EPI_MODE[0] = None
+    return body
+
+
+for _x in U.XR_OPS:
+    HBODY[_x] = make_xr(_x)
 
 
 def mul_low(xa, yb, out):

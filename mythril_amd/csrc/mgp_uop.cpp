@@ -98,14 +98,14 @@ struct Translator {
     switch (kind) {
       case MGP_K_ACC: return {KACC, 0};
       case MGP_K_SLOT:
-        if (idx >= n_lds) return {KRVAR, reg_pos[idx - n_lds]};
+        if (idx >= n_lds) return {KRVAR, (uint32_t)reg_pos[idx - n_lds] * 8u};
         if (idx >= MGP_U_MAX_LDS_SLOTS) bad = true;
         return {KSLOT, idx * MGP_U_SLOT_BYTES};
       case MGP_K_CONST: return {KCONST, pool_byte(idx)};
       default:
         if (idx < MGP_U_REG_VARS) {
           var_mask |= 1u << idx;
-          return {KRVAR, idx};
+          return {KRVAR, idx * 8u};  // RVAR parameter: VGPR offset 8p into the bank
         }
         return {KVAR, idx};
     }
@@ -144,6 +144,13 @@ inline uint32_t epi_variant(uint32_t op, bool store, bool mask, bool reg) {
       return mask ? e[3] : e[1];
     }
   return op;
+}
+
+// fused "vA op= bank[B]" handler of an op (uop_spec.XR_OPS), or -1
+inline int xr_handler(uint32_t op) {
+  for (uint32_t i = 0; i < sizeof(kXrBase) / sizeof(kXrBase[0]); ++i)
+    if (kXrBase[i] == op) return (int)(MGP_U_XR_FIRST + i);
+  return -1;
 }
 
 inline uint32_t w0_of(uint32_t first, uint32_t op) {
@@ -323,7 +330,12 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       opid = epi_variant(opid, (flags & MGP_UF_STORE) != 0, (flags & MGP_UF_MASK) != 0,
                          (flags & MGP_UF_REGST) != 0);
       // an operand in vA and no operand B: nothing to fetch, dispatch straight to the op
-      const uint32_t first = (a.kind == KACC && b.kind == KNONE) ? opid : fetch_id(a.kind, b.kind, false);
+      uint32_t first = (a.kind == KACC && b.kind == KNONE) ? opid : fetch_id(a.kind, b.kind, false);
+      // vA op bank-register: one fused handler reads B straight from the bank
+      if (a.kind == KACC && b.kind == KRVAR) {
+        const int xr = xr_handler(opid);
+        if (xr >= 0) opid = first = (uint32_t)xr;
+      }
       emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
     }
   };

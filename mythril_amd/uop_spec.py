@@ -26,7 +26,8 @@ uop words:
              (offsets come from the assembled kernel's symbol table, gen_offsets.py)
   w1 [15:0] operand A parameter, [31:16] operand B parameter
             SLOT: LDS byte offset (slot*2048), VAR: variable index, RVAR:
-            register-bank position (a preloaded variable, or a register slot),
+            8 x register-bank position p (v[64+8p]: a preloaded variable, or a
+            register slot),
             CONST: pool index; Bool operands: bool slot * 2
   w2 [15:0] store slot byte offset, or 8 x bank position with REGST /
             third Bool operand * 2
@@ -71,7 +72,13 @@ CMP_VARIANTS = [f"{c}_{r}" for c in CMPS for r in ("RA", "RC")]
 EPI_OPS = ["ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "MOV", "ITE"]
 EPI_VARIANTS = [f"{o}_{v}" for o in EPI_OPS for v in ("S", "M", "MS", "R", "MR")]
 
-OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS
+# fused handlers "vA = vA op bank[B]" (F_acc_rvar_A + op in one handler: B is read in
+# GPR-index mode straight from the register bank, no moves, no second dispatch)
+XR_BASE = ["ADD", "SUB", "AND", "OR", "XOR"] + \
+          [f"{o}_{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR") for v in ("S", "M", "MS", "R", "MR")]
+XR_OPS = [f"XR_{o}" for o in XR_BASE]
+
+OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
 # id past the table ends the program instead of running off into memory
 HANDLERS = ["INVALID"] + FETCH + OPS
@@ -110,6 +117,8 @@ def c_header() -> str:
         f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",
         f"#define MGP_U_UOP_WORDS {UOP_WORDS}", f"#define MGP_U_REG_VARS {REG_VARS}",
         f"#define MGP_U_N_KINDS {len(KINDS)}", f"#define MGP_U_PAGE_UOPS {PAGE_UOPS}",
-        f"#define MGP_U_MAX_POOL {MAX_POOL}",
+        f"#define MGP_U_MAX_POOL {MAX_POOL}", f"#define MGP_U_XR_FIRST {ID[XR_OPS[0]]}",
     ]
+    lines.append("static const unsigned short kXrBase[%d] = {%s};" % (len(XR_BASE), ", ".join(
+        f"MGP_U_{o}" for o in XR_BASE)))
     return "\n".join(lines) + "\n"

@@ -99,7 +99,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         if kind == "slot":
             return lds[p]
         if kind == "rvar":
-            return bank[p]
+            return bank[p // 8]
         if kind == "var":
             return int(xs[p]) & M256
         return pool(p)
@@ -117,6 +117,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
                 KM = pool((w2 >> 16) & 0x3F)
             if w2 & U.F_SEXT:
                 KH = pool(w3 & 0x3F)
+        if first.startswith("XR_"):
+            vB = bank[pb // 8]          # fused: vA op bank[B]
+            first = op = first[3:]
         if first.startswith("F_"):
             _, ka, kb, tgt = first.split("_")
             if kb != "none":

@@ -607,6 +607,14 @@ for _x in U.XR_OPS:
     HBODY[_x] = make_xr(_x)
 
 
+def make_xs(name):
+    """XS_<op>: the B slot read of F_acc_slot_A at the top of the op handler itself."""
+    def body():
+        fetch_one("slot", VB, "B")
+        HBODY[name[3:]]()
+    return body
+
+
 def mul_low(xa, yb, out):
     """out[0..7] = low 256 bits of X*Y (Comba columns, v[4:5] + v6 accumulator)."""
     A("v_mov_b32 v6, 0")
@@ -1110,6 +1118,8 @@ for _name in U.EPI_VARIANTS:
 # the translator only names the base handler of these ops when neither flag is set
 for _op in U.EPI_OPS:
     HBODY[_op] = make_epi_variant(_EPI_BASE[_op], "")
+for _x in U.XS_OPS:
+    HBODY[_x] = make_xs(_x)
 
 
 # ---------------------------------------------------------------- kernel

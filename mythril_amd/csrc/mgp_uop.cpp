@@ -153,6 +153,13 @@ inline int xr_handler(uint32_t op) {
   return -1;
 }
 
+// fused "vA op= lds[B]" handler of an op (uop_spec.XS_OPS), or -1
+inline int xs_handler(uint32_t op) {
+  for (uint32_t i = 0; i < sizeof(kXsBase) / sizeof(kXsBase[0]); ++i)
+    if (kXsBase[i] == op) return (int)(MGP_U_XS_FIRST + i);
+  return -1;
+}
+
 inline uint32_t w0_of(uint32_t first, uint32_t op) {
   return (uint32_t)kUopHandlerOffset[first] | ((uint32_t)kUopHandlerOffset[op] << 16);
 }
@@ -230,8 +237,12 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           w2 |= T.mask_off(width) << 16;
         }
         const bool ra = a.kind == KACC;
-        const uint32_t opid = ra ? base : base + 1u;  // _RC follows _RA
-        const uint32_t first = fetch_id(a.kind, b.kind, !ra);
+        uint32_t opid = ra ? base : base + 1u;  // _RC follows _RA
+        uint32_t first = fetch_id(a.kind, b.kind, !ra);
+      if (ra && b.kind == KSLOT) {
+        const int xs = xs_handler(opid);
+        if (xs >= 0) opid = first = (uint32_t)xs;
+      }
         emit(w0_of(first, opid), (ra ? 0u : a.param) | (b.param << 16), w2 | flags, w3);
         continue;
       }
@@ -335,6 +346,9 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       if (a.kind == KACC && b.kind == KRVAR) {
         const int xr = xr_handler(opid);
         if (xr >= 0) opid = first = (uint32_t)xr;
+      } else if (a.kind == KACC && b.kind == KSLOT) {
+        const int xs = xs_handler(opid);
+        if (xs >= 0) opid = first = (uint32_t)xs;
       }
       emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
     }

@@ -74,11 +74,17 @@ EPI_VARIANTS = [f"{o}_{v}" for o in EPI_OPS for v in ("S", "M", "MS", "R", "MR")
 
 # fused handlers "vA = vA op bank[B]" (F_acc_rvar_A + op in one handler: B is read in
 # GPR-index mode straight from the register bank, no moves, no second dispatch)
-XR_BASE = ["ADD", "SUB", "AND", "OR", "XOR"] + \
-          [f"{o}_{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR") for v in ("S", "M", "MS", "R", "MR")]
+XR_BASE = [f"{o}{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR") for v in ("", "_S", "_R")]
 XR_OPS = [f"XR_{o}" for o in XR_BASE]
 
-OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS
+# fused handlers "vA = vA op lds[B]" (F_acc_slot_A + op in one handler: the B slot read
+# is issued at the top of the op, one dispatch instead of two)
+# (the masked variants and DIV stay two-dispatch: rare, or a long body not worth a copy)
+XS_BASE = [f"{c}_RA" for c in ("EQ", "ULT", "UGT", "SLT", "SGT")] + ["MUL"] + \
+          [f"{o}{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR", "ITE") for v in ("", "_S", "_R")]
+XS_OPS = [f"XS_{o}" for o in XS_BASE]
+
+OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + XS_OPS
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
 # id past the table ends the program instead of running off into memory
 HANDLERS = ["INVALID"] + FETCH + OPS
@@ -121,4 +127,7 @@ def c_header() -> str:
     ]
     lines.append("static const unsigned short kXrBase[%d] = {%s};" % (len(XR_BASE), ", ".join(
         f"MGP_U_{o}" for o in XR_BASE)))
+    lines.append(f"#define MGP_U_XS_FIRST {ID[XS_OPS[0]]}")
+    lines.append("static const unsigned short kXsBase[%d] = {%s};" % (len(XS_BASE), ", ".join(
+        f"MGP_U_{o}" for o in XS_BASE)))
     return "\n".join(lines) + "\n"

@@ -120,6 +120,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         if first.startswith("XR_"):
             vB = bank[pb // 8]          # fused: vA op bank[B]
             first = op = first[3:]
+        elif first.startswith("XS_"):
+            vB = lds[pb]                # fused: vA op lds[B]
+            first = op = first[3:]
         if first.startswith("F_"):
             _, ka, kb, tgt = first.split("_")
             if kb != "none":

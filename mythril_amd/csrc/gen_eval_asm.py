@@ -489,20 +489,22 @@ def h_page():
 
 # ---- Bool ops
 def diag_stamp():
-    """Diagnostic build-in (kernarg diag != 0): diag[item] = {first dispatch - entry,
-    RET - first dispatch, entry time lo, entry time hi} in shader clocks."""
+    """Diagnostic build-in (kernarg diag != 0): diag[item] = {descriptor landed - entry,
+    page/pool/variables landed - descriptor, first dispatch - loads, RET - first
+    dispatch} in shader clocks (32-bit differences)."""
     ln = A.fresh("nodiag")
     A("v_readlane_b32 s24, v126, 0", "v_readlane_b32 s25, v126, 1",
       "s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {ln}",
       "s_memtime s[54:55]",
-      "v_readlane_b32 s26, v126, 2", "v_readlane_b32 s27, v126, 3",
-      "v_readlane_b32 s28, v126, 4", "v_readlane_b32 s29, v126, 6",
-      "s_lshl_b32 s29, s29, 4", "s_add_u32 s24, s24, s29", "s_addc_u32 s25, s25, 0",
-      "s_sub_u32 s30, s28, s26",
+      "v_readlane_b32 s26, v126, 2", "v_readlane_b32 s27, v126, 7",
+      "v_readlane_b32 s28, v126, 8", "v_readlane_b32 s29, v126, 4",
+      "v_readlane_b32 s30, v126, 6",
+      "s_lshl_b32 s30, s30, 4", "s_add_u32 s24, s24, s30", "s_addc_u32 s25, s25, 0",
+      "s_sub_u32 s26, s27, s26", "s_sub_u32 s27, s28, s27", "s_sub_u32 s28, s29, s28",
       "s_waitcnt lgkmcnt(0)",
-      "s_sub_u32 s31, s54, s28",
+      "s_sub_u32 s29, s54, s29",
       "s_mov_b64 exec, 1",
-      "v_mov_b32 v4, s30", "v_mov_b32 v5, s31", "v_mov_b32 v6, s26", "v_mov_b32 v7, s27",
+      "v_mov_b32 v4, s26", "v_mov_b32 v5, s27", "v_mov_b32 v6, s28", "v_mov_b32 v7, s29",
       "v_mov_b32 v8, 0",
       "global_store_dwordx4 v8, v[4:7], s[24:25]")
     A.label(ln)
@@ -1164,6 +1166,12 @@ PROLOGUE = """\
   s_addc_u32 s83, s65, s83
   s_load_dwordx8 s[84:91], s[82:83], 0x0 glc
   s_waitcnt lgkmcnt(0)
+  s_cmp_eq_u64 s[70:71], 0
+  s_cbranch_scc1 .Lnostampd
+  s_memtime s[96:97]
+  s_waitcnt lgkmcnt(0)
+  v_writelane_b32 v126, s96, 7
+.Lnostampd:
   // s84 state  s85 undecided  s86 slots  s87 n_uops  s[88:89] page 0  s90 pool offset from
   // page 0  s91 n_pool | register-variable mask << 8
   // partial entry: partial + (state * n_chunks + chunk) * 4
@@ -1226,13 +1234,18 @@ PROLOGUE = """\
   s_cbranch_scc1 .Lundec
   s_mov_b32 s1, s11
   s_mov_b32 s13, s11
-{VAR_PRELOAD}{PAGE_DECODE}  s_cmp_eq_u64 s[70:71], 0
-  s_cbranch_scc1 .Lnostamp
+{VAR_PRELOAD}  s_cmp_eq_u64 s[70:71], 0
+  s_cbranch_scc1 .Lnostampl
+  s_memtime s[96:97]
+  s_waitcnt lgkmcnt(0)
+  v_writelane_b32 v126, s96, 8
+.Lnostampl:
+{PAGE_DECODE}  s_cmp_eq_u64 s[70:71], 0
+  s_cbranch_scc1 .Lnostampx
   s_memtime s[96:97]
   s_waitcnt lgkmcnt(0)
   v_writelane_b32 v126, s96, 4
-  v_writelane_b32 v126, s97, 5
-.Lnostamp:
+.Lnostampx:
   s_mov_b64 s[64:65], 0
   s_mov_b64 s[66:67], -1
   s_mov_b32 s62, 0

@@ -3,8 +3,8 @@
 
 Runs bench.py's synthetic batch once with mgp_set_eval_diag and reports, per wave,
 the prologue (entry -> first uop dispatch) and the program run (first dispatch -> RET)
-in shader clocks, overall and per LDS-slot bucket, plus the average number of waves
-resident per SIMD implied by the wave lifetimes.
+in shader clocks, split into descriptor / page+pool+variable loads / decode, overall
+and per v1 slot count.
     python profiles/stamps.py [--states 262144]
 """
 import argparse
@@ -60,18 +60,15 @@ def main():
     step()
     torch.cuda.synchronize(dev)
     N.lib().mgp_set_eval_diag(None)
-    d = d_diag.cpu().numpy().view(np.uint32).reshape(n_states, n_chunks, 4)
-    pro = d[:, :, 0].astype(np.float64)
-    run = d[:, :, 1].astype(np.float64)
-    t0 = (d[:, :, 3].astype(np.uint64) << np.uint64(32)) | d[:, :, 2].astype(np.uint64)
-    ok = (pro > 0) & (run > 0)
-    life = pro + run
-    span = float(t0[ok].max() - t0[ok].min()) + float(np.median(life[ok]))
-    res = {"waves": int(ok.sum()), "prologue_med": float(np.median(pro[ok])), "prologue_mean": float(pro[ok].mean()),
+    d = d_diag.cpu().numpy().view(np.uint32).reshape(n_states, n_chunks, 4).astype(np.float64)
+    desc, loads, disp, run = d[:, :, 0], d[:, :, 1], d[:, :, 2], d[:, :, 3]
+    ok = run > 0
+    pro = desc + loads + disp
+    res = {"waves": int(ok.sum()),
+           "desc_med": float(np.median(desc[ok])), "loads_med": float(np.median(loads[ok])),
+           "dispatch_med": float(np.median(disp[ok])), "prologue_med": float(np.median(pro[ok])),
            "run_med": float(np.median(run[ok])), "run_mean": float(run[ok].mean()),
-           "prologue_share": float(pro[ok].sum() / life[ok].sum()),
-           "span_clocks": span,
-           "resident_waves_per_simd": float(life[ok].sum() / span / 1024)}
+           "prologue_share": float(pro[ok].sum() / (pro[ok].sum() + run[ok].sum()))}
     print(json.dumps(res))
     slots = hdr[:, 2]
     uops = None
@@ -79,8 +76,8 @@ def main():
         m = (slots == sl)[:, None] & ok
         if m.sum() < 100:
             continue
-        print(f"slots {int(sl):2d}: waves {int(m.sum()):7d}  prologue med {np.median(pro[m]):8.0f}  "
-              f"run med {np.median(run[m]):8.0f}  run mean {run[m].mean():8.0f}")
+        print(f"v1 slots {int(sl):2d}: waves {int(m.sum()):7d}  desc {np.median(desc[m]):6.0f}  loads "
+              f"{np.median(loads[m]):6.0f}  dispatch {np.median(disp[m]):5.0f}  run med {np.median(run[m]):7.0f}")
     del uops
 
 

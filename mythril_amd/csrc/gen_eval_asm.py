@@ -610,9 +610,11 @@ for _x in U.XR_OPS:
 
 
 def make_xs(name):
-    """XS_<op>: the B slot read of F_acc_slot_A at the top of the op handler itself."""
+    """XS_<op>: the B slot read of F_acc_slot_A at the top of the op handler itself,
+    issued before the next uop's readlanes so that they overlap its latency."""
     def body():
         fetch_one("slot", VB, "B")
+        prefetch_next()
         HBODY[name[3:]]()
     return body
 
@@ -820,8 +822,8 @@ for _k in range(8):
 
 @handler("ITE")
 def h_ite():
+    bool_read("s19", 16, 50)      # SALU only: overlaps the operand wait
     wait_operands()
-    bool_read("s19", 16, 50)
     for i in range(8):
         A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VB + i)}, {v(VA + i)}, s[50:51]")
     bv_epilogue()
@@ -1328,7 +1330,7 @@ def generate() -> str:
     globals()["A"] = global_A
     A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
                    .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n"))
-    no_prefetch = set(U.FETCH) | {"INVALID", "RET", "PAGE"}
+    no_prefetch = set(U.FETCH) | set(U.XS_OPS) | {"INVALID", "RET", "PAGE"}
     for name in U.HANDLERS:
         A.lines.append(f".p2align 2\nmgp_h_{name}:")
         if name not in no_prefetch:

@@ -450,34 +450,88 @@ __constant__ uint64_t kKeccakRC[24] = {
     0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
     0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int n) {
-  return n == 0 ? x : ((x << n) | (x >> (64 - n)));
+// Keccak-f[1600] on 32-bit halves.  A 64-bit lane is (lo, hi); the compiler sees only
+// 32-bit operations, so theta's five-way parities become v_xor3_b32 / v_bitop3_b32,
+// chi's a ^ (~b & c) one v_bitop3_b32 per word, and every rotation two v_alignbit_b32
+// (a 64-bit rotate through lshl_b64 + lshr + or costs four).
+template <int R>
+__device__ __forceinline__ void rotl64_32(uint32_t lo, uint32_t hi, uint32_t &olo, uint32_t &ohi) {
+  if constexpr (R == 0) {
+    olo = lo;
+    ohi = hi;
+  } else if constexpr (R == 32) {
+    olo = hi;
+    ohi = lo;
+  } else if constexpr (R < 32) {
+    ohi = __builtin_amdgcn_alignbit(hi, lo, 32 - R);
+    olo = __builtin_amdgcn_alignbit(lo, hi, 32 - R);
+  } else {
+    ohi = __builtin_amdgcn_alignbit(lo, hi, 64 - R);
+    olo = __builtin_amdgcn_alignbit(hi, lo, 64 - R);
+  }
 }
 
-// Keccak-f[1600]; lane (x,y) at st[x + 5y].  Rotation offsets (FIPS 202 rho).
-__device__ __forceinline__ void keccak_f1600(uint64_t st[25]) {
-  constexpr int kRho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
-                            25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
-#pragma unroll 1
+template <int I>
+struct KeccakRho;  // FIPS 202 rho offsets, lane (x,y) at index x + 5y
+#define MGP_RHO(i, r) \
+  template <>        \
+  struct KeccakRho<i> { static constexpr int v = r; };
+MGP_RHO(0, 0) MGP_RHO(1, 1) MGP_RHO(2, 62) MGP_RHO(3, 28) MGP_RHO(4, 27) MGP_RHO(5, 36) MGP_RHO(6, 44)
+MGP_RHO(7, 6) MGP_RHO(8, 55) MGP_RHO(9, 20) MGP_RHO(10, 3) MGP_RHO(11, 10) MGP_RHO(12, 43) MGP_RHO(13, 25)
+MGP_RHO(14, 39) MGP_RHO(15, 41) MGP_RHO(16, 45) MGP_RHO(17, 15) MGP_RHO(18, 21) MGP_RHO(19, 8)
+MGP_RHO(20, 18) MGP_RHO(21, 2) MGP_RHO(22, 61) MGP_RHO(23, 56) MGP_RHO(24, 14)
+#undef MGP_RHO
+
+__device__ __forceinline__ void keccak_f1600_32(uint32_t lo[25], uint32_t hi[25]) {
+  // fully unrolled: the pi permutation then costs no moves and the round constants
+  // become literals
+#pragma unroll
   for (int round = 0; round < 24; ++round) {
-    uint64_t C[5], D[5], B[25];
+    uint32_t cl[5], ch[5], dl[5], dh[5], bl[25], bh[25];
 #pragma unroll
-    for (int x = 0; x < 5; ++x) C[x] = st[x] ^ st[x + 5] ^ st[x + 10] ^ st[x + 15] ^ st[x + 20];
+    for (int x = 0; x < 5; ++x) {
+      // three-input XOR = v_bitop3_b32 with truth table 0x96
+      cl[x] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(lo[x], lo[x + 5], lo[x + 10], 0x96),
+                                          lo[x + 15], lo[x + 20], 0x96);
+      ch[x] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(hi[x], hi[x + 5], hi[x + 10], 0x96),
+                                          hi[x + 15], hi[x + 20], 0x96);
+    }
 #pragma unroll
-    for (int x = 0; x < 5; ++x) D[x] = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
-#pragma unroll
-    for (int i = 0; i < 25; ++i) st[i] ^= D[i % 5];
-#pragma unroll
-    for (int x = 0; x < 5; ++x)
-#pragma unroll
-      for (int y = 0; y < 5; ++y) B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(st[x + 5 * y], kRho[x + 5 * y]);
+    for (int x = 0; x < 5; ++x) {
+      uint32_t rl, rh;
+      rotl64_32<1>(cl[(x + 1) % 5], ch[(x + 1) % 5], rl, rh);
+      dl[x] = cl[(x + 4) % 5] ^ rl;
+      dh[x] = ch[(x + 4) % 5] ^ rh;
+    }
+    static_for<25>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int x = i % 5, y = i / 5;
+      constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+      rotl64_32<KeccakRho<i>::v>(lo[i] ^ dl[x], hi[i] ^ dh[x], bl[dst], bh[dst]);
+    });
 #pragma unroll
     for (int y = 0; y < 5; ++y)
 #pragma unroll
-      for (int x = 0; x < 5; ++x)
-        st[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
-    st[0] ^= kKeccakRC[round];
+      for (int x = 0; x < 5; ++x) {
+        lo[x + 5 * y] = bl[x + 5 * y] ^ (~bl[(x + 1) % 5 + 5 * y] & bl[(x + 2) % 5 + 5 * y]);
+        hi[x + 5 * y] = bh[x + 5 * y] ^ (~bh[(x + 1) % 5 + 5 * y] & bh[(x + 2) % 5 + 5 * y]);
+      }
+    const uint64_t rc = kKeccakRC[round];
+    lo[0] ^= (uint32_t)rc;
+    hi[0] ^= (uint32_t)(rc >> 32);
   }
+}
+
+__device__ __forceinline__ void keccak_f1600(uint64_t st[25]) {
+  uint32_t lo[25], hi[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) {
+    lo[i] = (uint32_t)st[i];
+    hi[i] = (uint32_t)(st[i] >> 32);
+  }
+  keccak_f1600_32(lo, hi);
+#pragma unroll
+  for (int i = 0; i < 25; ++i) st[i] = ((uint64_t)hi[i] << 32) | lo[i];
 }
 }  // namespace
 

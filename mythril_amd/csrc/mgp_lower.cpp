@@ -634,8 +634,23 @@ extern "C" int mgp_plan_buckets(const uint32_t *prog_words, const uint64_t *prog
     cnt[v]++;
   }
   std::vector<uint32_t> distinct;
-  for (uint32_t v = 0; v <= 256; ++v)
-    if (cnt[v]) distinct.push_back(v);
+  // a class with few states costs a whole launch (≈ one wave lifetime of ramp-down) for
+  // little work: it joins the next larger slot count (its states then run with more LDS
+  // than they need, which is harmless), scanning upward so a run of small top classes
+  // ends in one launch
+  const uint32_t min_states = std::max<uint32_t>(256u, n_states / 128u);
+  uint32_t carried = 0;
+  for (uint32_t v = 0; v <= 256; ++v) {
+    if (!cnt[v]) continue;
+    carried += cnt[v];
+    bool last = true;
+    for (uint32_t w = v + 1; w <= 256; ++w)
+      if (cnt[w]) { last = false; break; }
+    if (carried >= min_states || last) {
+      distinct.push_back(v);
+      carried = 0;
+    }
+  }
   // merge the smallest classes into their upper neighbour until the plan fits
   while (distinct.size() > max_buckets) distinct.erase(distinct.begin());
   std::vector<uint32_t> bucket_of(257, 0);

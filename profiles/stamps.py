@@ -26,6 +26,7 @@ SEED = 0x4D595448
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--states", type=int, default=1 << 18)
+    ap.add_argument("--dump", default="", help="write per-wave stamps to this .npz")
     args = ap.parse_args()
     import torch
 
@@ -70,6 +71,9 @@ def main():
            "run_med": float(np.median(run[ok])), "run_mean": float(run[ok].mean()),
            "prologue_share": float(pro[ok].sum() / (pro[ok].sum() + run[ok].sum()))}
     print(json.dumps(res))
+    if args.dump:
+        np.savez_compressed(args.dump, desc=d[:, :, 0], loads=d[:, :, 1], disp=d[:, :, 2], run=d[:, :, 3],
+                            slots=hdr[:, 2])
     slots = hdr[:, 2]
     uops = None
     for sl in np.unique(slots):

@@ -27,9 +27,11 @@ def main(d):
                        f"{float(r['AverageNs'])/1e3:.1f} | {float(r['Percentage']):.1f} |")
     # per-dispatch durations of the eval kernel grouped into steps
     tr = os.path.join(d, "trace", "run_kernel_trace.csv")
-    evals = []
+    evals, kcalls = [], []
     with open(tr) as f:
         for r in csv.DictReader(f):
+            if short(r["Kernel_Name"]) == "mgp_keccak64_kernel":
+                kcalls.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             if short(r["Kernel_Name"]) in ("mgp_eval_kernel", "mgp_eval_gfx950", "mgp_finalize_kernel"):
                 evals.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     evals.sort()
@@ -97,6 +99,16 @@ def main(d):
                 # issued VALU wave-instructions per step (x 64 lanes = lane-ops, overhead included)
                 traffic[k]["valu_wave_insts_per_step"] = c["SQ_INSTS_VALU"] / n_steps
                 traffic[k]["salu_insts_per_step"] = c.get("SQ_INSTS_SALU", 0) / n_steps
+        if k == "mgp_keccak64_kernel" and c.get("SQ_WAVES"):
+            # one preimage per lane: per-hash figures are per-wave counts / 64
+            ncalls = sum(1 for _ in kcalls)
+            traffic[k] = {"valu_lane_ops_per_hash": c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"],
+                          "hbm_bytes_per_hash": (2 * c.get("FETCH_SIZE", 0) + c.get("WRITE_SIZE", 0)) * 1024
+                          / (64 * c["SQ_WAVES"]) if "FETCH_SIZE" in c else None,
+                          "dispatches": ncalls}
+            der["VALU lane-ops / hash"] = traffic[k]["valu_lane_ops_per_hash"]
+            if traffic[k]["hbm_bytes_per_hash"] is not None:
+                der["HBM bytes / hash (2 x FETCH_SIZE + WRITE_SIZE)"] = traffic[k]["hbm_bytes_per_hash"]
         if der:
             out.append("\nderived:\n")
             for n, val in der.items():
@@ -106,6 +118,12 @@ def main(d):
     # machine-readable traffic figure for bench.py's roofline.traffic (same workload shape only)
     bj = os.path.join(d, "bench_trace.json")
     for k, t in traffic.items():
+        if k == "mgp_keccak64_kernel":
+            t.update({"kernel": k, "source": f"profiles/{os.path.basename(os.path.normpath(d)).replace('prof_', '')}"
+                      f"_summary.md (rocprofv3 run {d})"})
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "keccak_pmc.json"), "w") as f:
+                json.dump(t, f, indent=1)
+            continue
         try:
             cfg = json.load(open(bj))["config"]
             tag = os.path.basename(os.path.normpath(d)).replace("prof_", "")

@@ -147,6 +147,31 @@ int mgp_plant_candidates_dev(uint32_t *d_cands, uint32_t n_states,
                              const uint32_t *d_plant_words, uint32_t n_plant,
                              void *stream);
 
+/* ----------------------------------------------------- UNSAT pre-check
+ * Host-side, no device needed (OpenMP over states).  Replaces, for the states
+ * it decides, the z3 check that follows a GPU miss: Constraints.is_possible
+ * (mythril/laser/ethereum/state/constraints.py:34-51, unsat -> False) and
+ * get_model (mythril/analysis/solver.py:27-61, unsat -> UnsatError).
+ * Sound abstract interpretation (known bits x unsigned interval per BV node,
+ * truth set per Bool node) with backward narrowing from root = true, at most
+ * max_passes forward+backward passes (0 = 16).  Node lists / constant pools as
+ * for mgp_lower.
+ *   out[s] = 1   no assignment satisfies state s (proven UNSAT)
+ *            0   not refuted (SAT or undecided: the caller's solver decides)
+ *           -1   not analysed (width > 256, malformed node list)
+ * A 1 is a proof; it never depends on candidates or randomness. */
+int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets,
+               uint32_t n_states, const uint32_t *consts,
+               const uint64_t *const_offsets, uint32_t max_passes,
+               int8_t *out);
+/* Diagnostic (tests): the refined abstract value of every node of ONE state,
+ * 33 words per node: known-zero mask, known-one mask, lo, hi (8 u32 limbs
+ * each) and the Bool truth set (bit0 = may be false, bit1 = may be true).
+ * Returns 1 / 0 / -1 as mgp_refute. */
+int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes,
+                     const uint32_t *consts, uint64_t n_consts,
+                     uint32_t max_passes, uint32_t *out_av);
+
 /* ---------------------------------------------------------- Keccak-256
  * n preimages of len bytes each, preimage i at in + i*stride; 32-byte
  * big-endian digests to out32 + 32*i.  Keccak-256 = Keccak[r=1088,c=512]

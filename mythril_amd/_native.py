@@ -86,6 +86,8 @@ def _bind(lib):
         "mgp_probe_valu_dev": (ctypes.c_int, [_U32, _U32, _P, _P, _P]),
         "mgp_set_eval_engine": (ctypes.c_int, [ctypes.c_int]),
         "mgp_set_eval_diag": (ctypes.c_int, [_P]),
+        "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
+        "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -133,6 +135,8 @@ EXPORTED_SYMBOLS = (
     "mgp_probe_valu_dev",
     "mgp_set_eval_engine",
     "mgp_set_eval_diag",
+    "mgp_refute",
+    "mgp_refute_trace",
 )
 
 ENGINE_HIP, ENGINE_ASM = 1, 2
@@ -198,6 +202,33 @@ def lower(
         _check(rc)
         return words[: int(used.value)], prog_offsets, status[:n_states]
     raise MgpError(MGP_E_CAPACITY, "lowering capacity")
+
+
+def refute(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,
+           max_passes: int = 0) -> np.ndarray:
+    """Sound UNSAT pre-check per state -> int8 (1 proven UNSAT, 0 not refuted, -1 not analysed)."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    const_offsets = np.ascontiguousarray(const_offsets, dtype=np.uint64)
+    n_states = len(node_offsets) - 1
+    out = np.zeros(max(n_states, 1), dtype=np.int8)
+    _check(lib().mgp_refute(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
+                            max_passes, _ptr(out)))
+    return out[:n_states]
+
+
+def refute_trace(nodes: np.ndarray, consts: np.ndarray, max_passes: int = 0):
+    """One state's refined abstract values -> (verdict, (n_nodes, 33) u32 array)."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    out = np.zeros((max(len(nodes), 1), 33), dtype=np.uint32)
+    r = lib().mgp_refute_trace(_ptr(nodes), len(nodes), _ptr(consts), consts.size // 8, max_passes, _ptr(out))
+    return int(r), out[: len(nodes)]
 
 
 def program_headers(words: np.ndarray, prog_offsets: np.ndarray) -> np.ndarray:

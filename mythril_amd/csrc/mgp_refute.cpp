@@ -1,0 +1,899 @@
+// mgp_refute.cpp — sound UNSAT pre-check of constraint DAGs (host side, OpenMP).
+//
+// The GPU evaluator proves SAT (a witness); every state it cannot prove goes
+// to z3 in the reference (Constraints.is_possible, constraints.py:34-51;
+// get_model, analysis/solver.py:27-61).  Many of those are infeasible for a
+// shallow reason: a jump condition contradicting an earlier one
+// (instructions.py:1556-1562 adds `cond` to one successor and `Not(cond)` to
+// the other, so a later branch on a related value is often decided by ranges
+// and bits), a calldata size bound against a byte index
+// (calldata.py:219-232), an overflow predicate whose operands are pinned
+// (integer.py:141-160).  This pass proves those UNSAT without a solver call.
+//
+// Abstract domain per BV node of width w <= 256: known bits (z = known-zero
+// mask, o = known-one mask) x unsigned interval [lo, hi]; per Bool node the set
+// of possible truth values.  Each pass runs forward transfer functions over the
+// topological node list, then backward narrowing from "root = true" (a
+// conjunct that must hold narrows its operands: x <u c bounds x, x == c pins
+// its bits, ...), until nothing changes or the pass limit is hit.  An empty
+// abstract value proves that no assignment of the free variables satisfies the
+// root: the state is UNSAT.  Every transfer function over-approximates its
+// operator under the z3 / SMT-LIB semantics of include/mgp_ir.h, so the claim
+// is sound; uninterpreted-function applications are left unconstrained (a
+// relaxation of the UF formula, still sound for UNSAT).  tests/test_refute.py
+// checks soundness against the oracle: node by node (every concrete evaluation
+// lies inside its node's abstract value) and state by state (no refuted state
+// has a model, exhaustively at small widths).
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/mgp.h"
+#include "mgp_bv.h"
+
+namespace {
+
+using V = U256;
+
+inline V M(uint32_t w) { return bv_mask(bv_ones(), w); }
+inline bool Z(const V &a) { return bv_is_zero(a); }
+inline bool EQV(const V &a, const V &b) { return bv_eq(a, b); }
+inline bool LT(const V &a, const V &b) { return bv_ult(a, b); }
+inline V AND(const V &a, const V &b) { return bv_and(a, b); }
+inline V OR(const V &a, const V &b) { return bv_or(a, b); }
+inline V XOR(const V &a, const V &b) { return bv_xor(a, b); }
+inline V NOT(const V &a) { return bv_not(a); }
+inline V MIN(const V &a, const V &b) { return LT(a, b) ? a : b; }
+inline V MAX(const V &a, const V &b) { return LT(a, b) ? b : a; }
+inline V SHL(const V &a, uint32_t s) { return s >= 256u ? bv_zero() : bv_shl(a, s); }
+inline V SHR(const V &a, uint32_t s) { return s >= 256u ? bv_zero() : bv_lshr(a, s); }
+inline V BIT(uint32_t i) { return SHL(bv_small(1u), i); }
+inline V ADDV(const V &a, const V &b) { return bv_add(a, b, nullptr); }
+inline V SUBV(const V &a, const V &b) { return bv_sub(a, b, nullptr); }
+inline V ONE() { return bv_small(1u); }
+
+// number of trailing one bits (a known-zero mask's run of low zeros)
+inline uint32_t ctz_ones(const V &z) {
+  uint32_t n = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (z.w[i] == 0xFFFFFFFFu) { n += 32; continue; }
+    return n + (uint32_t)__builtin_ctz(~z.w[i]);
+  }
+  return n;
+}
+
+struct AV {
+  V z, o, lo, hi;
+};
+inline bool same(const AV &a, const AV &b) {
+  return EQV(a.z, b.z) && EQV(a.o, b.o) && EQV(a.lo, b.lo) && EQV(a.hi, b.hi);
+}
+
+AV top(uint32_t w) {
+  AV a;
+  a.z = NOT(M(w));
+  a.o = bv_zero();
+  a.lo = bv_zero();
+  a.hi = M(w);
+  return a;
+}
+AV exact(V v, uint32_t w) {
+  v = bv_mask(v, w);
+  AV a;
+  a.z = NOT(v);
+  a.o = v;
+  a.lo = v;
+  a.hi = v;
+  return a;
+}
+inline bool is_exact(const AV &a) { return EQV(a.lo, a.hi); }
+
+// Re-establish the invariants (bits above w known zero, interval within the
+// bits' range, common high prefix of lo/hi as known bits).  false = empty.
+bool normalize(AV &a, uint32_t w) {
+  const V m = M(w);
+  a.z = OR(a.z, NOT(m));
+  a.o = AND(a.o, m);  // values are taken mod 2^w
+  for (int it = 0; it < 3; ++it) {
+    if (!Z(AND(a.o, a.z))) return false;
+    const V maxb = AND(NOT(a.z), m);
+    if (LT(a.lo, a.o)) a.lo = a.o;
+    if (LT(maxb, a.hi)) a.hi = maxb;
+    if (LT(a.hi, a.lo)) return false;
+    const uint32_t k = bv_bitlen(XOR(a.lo, a.hi));
+    const V pm = AND(NOT(M(k)), m);
+    const V nz = OR(a.z, AND(NOT(a.lo), pm)), no = OR(a.o, AND(a.lo, pm));
+    if (EQV(nz, a.z) && EQV(no, a.o)) break;
+    a.z = nz;
+    a.o = no;
+  }
+  return Z(AND(a.o, a.z));
+}
+
+// ------------------------------------------------------ transfer functions
+// LLVM-style known bits of a + b + carry (carry-in 0 or 1, known)
+void kb_add(const AV &a, const AV &b, uint32_t cin, uint32_t w, V &rz, V &ro) {
+  const V m = M(w);
+  const V c = bv_small(cin);
+  const V psz = AND(ADDV(ADDV(AND(NOT(a.z), m), AND(NOT(b.z), m)), c), m);
+  const V pso = AND(ADDV(ADDV(a.o, b.o), c), m);
+  const V ckz = NOT(XOR(XOR(psz, a.z), b.z));
+  const V cko = XOR(XOR(pso, a.o), b.o);
+  const V known = AND(AND(AND(OR(a.z, a.o), OR(b.z, b.o)), OR(ckz, cko)), m);
+  rz = OR(AND(NOT(psz), known), NOT(m));
+  ro = AND(pso, known);
+}
+
+// (x + y) mod 2^w and whether x + y >= 2^w (x, y < 2^w)
+inline V add_w(const V &x, const V &y, uint32_t w, bool &ovf) {
+  uint32_t c = 0;
+  V s = bv_add(x, y, &c);
+  if (w == 256u) {
+    ovf = c != 0u;
+    return s;
+  }
+  ovf = !Z(AND(s, NOT(M(w))));
+  return bv_mask(s, w);
+}
+
+AV av_not(const AV &a, uint32_t w) {
+  const V m = M(w);
+  AV r;
+  r.z = OR(a.o, NOT(m));
+  r.o = AND(a.z, m);
+  r.lo = SUBV(m, a.hi);
+  r.hi = SUBV(m, a.lo);
+  return r;
+}
+
+AV av_add(const AV &a, const AV &b, uint32_t w) {
+  AV r;
+  kb_add(a, b, 0u, w, r.z, r.o);
+  bool o1, o2;
+  const V s1 = add_w(a.lo, b.lo, w, o1), s2 = add_w(a.hi, b.hi, w, o2);
+  if (o1 == o2) {
+    r.lo = s1;
+    r.hi = s2;
+  } else {
+    r.lo = bv_zero();
+    r.hi = M(w);
+  }
+  return r;
+}
+
+AV av_sub(const AV &a, const AV &b, uint32_t w) {
+  // a - b = a + ~b + 1
+  const AV nb = av_not(b, w);
+  AV r;
+  kb_add(a, nb, 1u, w, r.z, r.o);
+  const bool u1 = LT(a.lo, b.hi), u2 = LT(a.hi, b.lo);
+  if (u1 == u2) {
+    r.lo = bv_mask(SUBV(a.lo, b.hi), w);
+    r.hi = bv_mask(SUBV(a.hi, b.lo), w);
+  } else {
+    r.lo = bv_zero();
+    r.hi = M(w);
+  }
+  return r;
+}
+
+AV av_and(const AV &a, const AV &b, uint32_t w) {
+  AV r = top(w);
+  r.z = OR(a.z, b.z);
+  r.o = AND(a.o, b.o);
+  r.hi = MIN(a.hi, b.hi);
+  return r;
+}
+AV av_or(const AV &a, const AV &b, uint32_t w) {
+  AV r = top(w);
+  r.z = AND(a.z, b.z);
+  r.o = OR(a.o, b.o);
+  r.lo = MAX(a.lo, b.lo);
+  return r;
+}
+AV av_xor(const AV &a, const AV &b, uint32_t w) {
+  AV r = top(w);
+  r.z = OR(AND(a.z, b.z), AND(a.o, b.o));
+  r.o = OR(AND(a.z, b.o), AND(a.o, b.z));
+  (void)w;
+  return r;
+}
+
+AV av_mul(const AV &a, const AV &b, uint32_t w) {
+  AV r = top(w);
+  const uint32_t tz = ctz_ones(a.z) + ctz_ones(b.z);
+  r.z = OR(r.z, M(tz < w ? tz : w));
+  V lo;
+  const V hi = bv_mul_full(a.hi, b.hi, &lo);
+  if (Z(hi) && (w == 256u || Z(AND(lo, NOT(M(w)))))) {
+    r.hi = lo;
+    r.lo = bv_mul(a.lo, b.lo);
+  }
+  return r;
+}
+
+// concrete value of a BV op on exact operands (semantics: include/mgp_ir.h)
+V fold_bv(uint8_t op, uint32_t w, const V &x, const V &y, uint32_t wa) {
+  switch (op) {
+    case MGP_OP_MUL: return bv_mul(x, y);
+    case MGP_OP_UDIV: { V q, r; bv_udivrem(x, y, &q, &r); return Z(y) ? M(w) : q; }
+    case MGP_OP_UREM: { V q, r; bv_udivrem(x, y, &q, &r); return Z(y) ? x : r; }
+    case MGP_OP_SDIV: return bv_sdiv(bv_sext(x, w), bv_sext(y, w));
+    case MGP_OP_SREM: return bv_srem(bv_sext(x, w), bv_sext(y, w));
+    case MGP_OP_SMOD: return bv_smod(bv_sext(x, w), bv_sext(y, w));
+    case MGP_OP_SHL: { const uint32_t s = bv_shift_amount(y); return s >= w ? bv_zero() : SHL(x, s); }
+    case MGP_OP_LSHR: { const uint32_t s = bv_shift_amount(y); return s >= w ? bv_zero() : SHR(x, s); }
+    case MGP_OP_ASHR: {
+      const uint32_t s = bv_shift_amount(y);
+      return bv_ashr(bv_sext(x, w), s >= w ? w : s);
+    }
+    case MGP_OP_SEXT: return bv_sext(x, wa);
+    default: return bv_zero();
+  }
+}
+
+// truth sets: bit0 = may be false, bit1 = may be true
+enum : uint8_t { BF = 1, BT = 2, BB = 3 };
+
+uint8_t dec_ult(const AV &a, const AV &b) {  // a <u b
+  if (LT(a.hi, b.lo)) return BT;
+  if (!LT(a.lo, b.hi)) return BF;
+  return BB;
+}
+uint8_t dec_ule(const AV &a, const AV &b) {  // a <=u b
+  if (!LT(b.lo, a.hi)) return BT;
+  if (LT(b.hi, a.lo)) return BF;
+  return BB;
+}
+uint8_t dec_eq(const AV &a, const AV &b) {
+  if (!Z(OR(AND(a.o, b.z), AND(a.z, b.o))) || LT(a.hi, b.lo) || LT(b.hi, a.lo)) return BF;
+  if (is_exact(a) && is_exact(b)) return BT;  // (and equal, else the test above fired)
+  return BB;
+}
+
+// signed order = unsigned order after flipping the sign bit
+AV flip(const AV &a, uint32_t w) {
+  const V sb = BIT(w - 1u), m = M(w);
+  AV r;
+  r.z = OR(AND(a.z, NOT(sb)), AND(a.o, sb));
+  r.o = OR(AND(a.o, NOT(sb)), AND(a.z, sb));
+  r.z = OR(r.z, NOT(m));
+  r.o = AND(r.o, m);
+  if (EQV(AND(a.lo, sb), AND(a.hi, sb))) {
+    r.lo = XOR(a.lo, sb);
+    r.hi = XOR(a.hi, sb);
+  } else {
+    r.lo = bv_zero();
+    r.hi = m;
+  }
+  return r;
+}
+
+struct State {
+  const mgp_node *nd;
+  uint32_t n;
+  const uint32_t *consts;
+  uint64_t n_consts;
+  std::vector<AV> av;
+  std::vector<uint8_t> bs;     // truth set of Bool nodes
+  std::vector<uint8_t> isb;    // node is Bool-typed
+  std::vector<int32_t> vtie;   // VAR node -> var table entry
+  std::vector<AV> vars;
+  std::vector<uint32_t> vkey;  // (index << 9) | width
+  bool changed = false;
+
+  uint32_t W(int32_t i) const { return nd[i].width; }
+
+  bool meet(int32_t i, const AV &s) {
+    const uint32_t w = nd[i].width;
+    AV t = av[i];
+    t.z = OR(t.z, s.z);
+    t.o = OR(t.o, s.o);
+    t.lo = MAX(t.lo, s.lo);
+    t.hi = MIN(t.hi, s.hi);
+    if (!normalize(t, w)) return false;
+    if (!same(t, av[i])) {
+      av[i] = t;
+      changed = true;
+    }
+    return true;
+  }
+  bool meetb(int32_t i, uint8_t s) {
+    const uint8_t t = bs[i] & s;
+    if (!t) return false;
+    if (t != bs[i]) {
+      bs[i] = t;
+      changed = true;
+    }
+    return true;
+  }
+  // would meeting s into node i leave it non-empty?
+  bool compatible(int32_t i, const AV &s) const {
+    AV t = av[i];
+    t.z = OR(t.z, s.z);
+    t.o = OR(t.o, s.o);
+    t.lo = MAX(t.lo, s.lo);
+    t.hi = MIN(t.hi, s.hi);
+    return normalize(t, nd[i].width);
+  }
+
+  // ------------------------------------------------------------ validate
+  bool setup() {
+    av.assign(n, AV());
+    bs.assign(n, BB);
+    isb.assign(n, 0);
+    vtie.assign(n, -1);
+    for (uint32_t i = 0; i < n; ++i) {
+      const mgp_node &x = nd[i];
+      const uint8_t op = x.op;
+      auto opnd = [&](int32_t k) { return k >= 0 && (uint32_t)k < i; };
+      const bool boolres = (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) ||
+                           (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) || op == MGP_OP_TRUE || op == MGP_OP_FALSE;
+      uint32_t nop = 0;
+      switch (op) {
+        case MGP_OP_VAR: case MGP_OP_CONST: case MGP_OP_TRUE: case MGP_OP_FALSE: nop = 0; break;
+        case MGP_OP_NOT: case MGP_OP_NEG: case MGP_OP_EXTRACT: case MGP_OP_ZEXT: case MGP_OP_SEXT:
+        case MGP_OP_BNOT: case MGP_OP_UFAPP: case MGP_OP_UFINV: nop = 1; break;
+        case MGP_OP_ITE: case MGP_OP_BITE: nop = 3; break;
+        default:
+          if ((op >= MGP_OP_ADD && op <= MGP_OP_ASHR) || op == MGP_OP_CONCAT || boolres) nop = 2;
+          else return false;  // unknown op
+      }
+      if (nop >= 1 && !opnd(x.a)) return false;
+      if (nop >= 2 && !opnd(x.b)) return false;
+      if (nop >= 3 && !opnd(x.c)) return false;
+      if (op == MGP_OP_ITE) {
+        isb[i] = isb[x.b];
+        if (isb[x.b] != isb[x.c] || !isb[x.a]) return false;
+      } else {
+        isb[i] = boolres;
+      }
+      if (!isb[i]) {
+        const uint32_t w = x.width;
+        if (w == 0u || w > MGP_MAX_WIDTH) return false;
+        av[i] = top(w);
+        if (op == MGP_OP_EXTRACT && (x.p0 < x.p1 || x.p0 - x.p1 + 1u != w || x.p0 >= W(x.a))) return false;
+        if (op == MGP_OP_CONCAT && W(x.a) + W(x.b) != w) return false;
+        if ((op == MGP_OP_ZEXT || op == MGP_OP_SEXT) && W(x.a) > w) return false;
+        if (op == MGP_OP_CONST && x.p0 >= n_consts) return false;
+        if (((op >= MGP_OP_ADD && op <= MGP_OP_ASHR) && op != MGP_OP_NOT && op != MGP_OP_NEG) &&
+            (W(x.a) != w || W(x.b) != w || isb[x.a] || isb[x.b]))
+          return false;
+        if ((op == MGP_OP_NOT || op == MGP_OP_NEG) && (W(x.a) != w || isb[x.a])) return false;
+        if (op == MGP_OP_ITE && (W(x.b) != w || W(x.c) != w)) return false;
+        if (op == MGP_OP_VAR) {
+          const uint32_t key = (x.p0 << 9) | w;
+          int32_t t = -1;
+          for (size_t k = 0; k < vkey.size(); ++k)
+            if (vkey[k] == key) t = (int32_t)k;
+          if (t < 0) {
+            t = (int32_t)vkey.size();
+            vkey.push_back(key);
+            vars.push_back(top(w));
+          }
+          vtie[i] = t;
+        }
+      } else if (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) {
+        if (isb[x.a] != isb[x.b]) return false;
+        if (isb[x.a] && op != MGP_OP_EQ) return false;
+        if (!isb[x.a] && W(x.a) != W(x.b)) return false;
+      } else if (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) {
+        if (!isb[x.a] || (nop >= 2 && !isb[x.b]) || (nop >= 3 && !isb[x.c])) return false;
+      }
+    }
+    return n > 0 && isb[n - 1];
+  }
+
+  // --------------------------------------------------------------- forward
+  bool forward(uint32_t i) {
+    const mgp_node &x = nd[i];
+    const uint32_t w = x.width;
+    if (isb[i]) {
+      uint8_t r = BB;
+      switch (x.op) {
+        case MGP_OP_TRUE: r = BT; break;
+        case MGP_OP_FALSE: r = BF; break;
+        case MGP_OP_BNOT: r = (uint8_t)(((bs[x.a] & BF) ? BT : 0) | ((bs[x.a] & BT) ? BF : 0)); break;
+        case MGP_OP_BAND: {
+          const uint8_t a = bs[x.a], b = bs[x.b];
+          r = (uint8_t)((((a & BT) && (b & BT)) ? BT : 0) | (((a & BF) || (b & BF)) ? BF : 0));
+          break;
+        }
+        case MGP_OP_BOR: {
+          const uint8_t a = bs[x.a], b = bs[x.b];
+          r = (uint8_t)((((a & BT) || (b & BT)) ? BT : 0) | (((a & BF) && (b & BF)) ? BF : 0));
+          break;
+        }
+        case MGP_OP_BXOR: case MGP_OP_BEQ: case MGP_OP_EQ:
+          if (x.op == MGP_OP_EQ && !isb[x.a]) {
+            r = dec_eq(av[x.a], av[x.b]);
+          } else {
+            const uint8_t a = bs[x.a], b = bs[x.b];
+            const bool diff = ((a & BT) && (b & BF)) || ((a & BF) && (b & BT));
+            const bool eqp = ((a & BT) && (b & BT)) || ((a & BF) && (b & BF));
+            r = (uint8_t)(x.op == MGP_OP_BXOR ? ((diff ? BT : 0) | (eqp ? BF : 0))
+                                              : ((eqp ? BT : 0) | (diff ? BF : 0)));
+          }
+          break;
+        case MGP_OP_BITE: case MGP_OP_ITE: {
+          const uint8_t c = bs[x.a];
+          r = (uint8_t)(((c & BT) ? bs[x.b] : 0) | ((c & BF) ? bs[x.c] : 0));
+          break;
+        }
+        case MGP_OP_ULT: r = dec_ult(av[x.a], av[x.b]); break;
+        case MGP_OP_ULE: r = dec_ule(av[x.a], av[x.b]); break;
+        case MGP_OP_UGT: r = dec_ult(av[x.b], av[x.a]); break;
+        case MGP_OP_UGE: r = dec_ule(av[x.b], av[x.a]); break;
+        case MGP_OP_SLT: case MGP_OP_SLE: case MGP_OP_SGT: case MGP_OP_SGE: {
+          const uint32_t ow = W(x.a);
+          const AV fa = flip(av[x.a], ow), fb = flip(av[x.b], ow);
+          r = x.op == MGP_OP_SLT ? dec_ult(fa, fb) : x.op == MGP_OP_SLE ? dec_ule(fa, fb)
+            : x.op == MGP_OP_SGT ? dec_ult(fb, fa) : dec_ule(fb, fa);
+          break;
+        }
+        case MGP_OP_UADD_NOOVF: {
+          const uint32_t ow = W(x.a);
+          bool oh, ol;
+          add_w(av[x.a].hi, av[x.b].hi, ow, oh);
+          add_w(av[x.a].lo, av[x.b].lo, ow, ol);
+          r = !oh ? BT : ol ? BF : BB;
+          break;
+        }
+        case MGP_OP_UMUL_NOOVF: {
+          const uint32_t ow = W(x.a);
+          auto ovf = [&](const V &p, const V &q) {
+            V lo;
+            const V hi = bv_mul_full(p, q, &lo);
+            return !Z(hi) || (ow < 256u && !Z(AND(lo, NOT(M(ow)))));
+          };
+          r = !ovf(av[x.a].hi, av[x.b].hi) ? BT : ovf(av[x.a].lo, av[x.b].lo) ? BF : BB;
+          break;
+        }
+        case MGP_OP_USUB_NOUDF: r = dec_ule(av[x.b], av[x.a]); break;
+        default: r = BB;
+      }
+      return meetb((int32_t)i, r);
+    }
+    AV r = top(w);
+    const AV *A = x.a >= 0 ? &av[x.a] : nullptr;
+    const AV *B = x.b >= 0 ? &av[x.b] : nullptr;
+    switch (x.op) {
+      case MGP_OP_VAR: r = vars[vtie[i]]; break;
+      case MGP_OP_CONST: {
+        V c;
+        memcpy(c.w, consts + 8ull * x.p0, 32);
+        r = exact(c, w);
+        break;
+      }
+      case MGP_OP_ADD: r = av_add(*A, *B, w); break;
+      case MGP_OP_SUB: r = av_sub(*A, *B, w); break;
+      case MGP_OP_NEG: r = av_sub(exact(bv_zero(), w), *A, w); break;
+      case MGP_OP_MUL: r = av_mul(*A, *B, w); break;
+      case MGP_OP_AND: r = av_and(*A, *B, w); break;
+      case MGP_OP_OR: r = av_or(*A, *B, w); break;
+      case MGP_OP_XOR: r = av_xor(*A, *B, w); break;
+      case MGP_OP_NOT: r = av_not(*A, w); break;
+      case MGP_OP_UDIV:
+        if (!Z(B->lo)) {  // divisor never 0: quotient monotone in both operands
+          V q1, q2, rr;
+          bv_udivrem(A->lo, B->hi, &q1, &rr);
+          bv_udivrem(A->hi, B->lo, &q2, &rr);
+          r.lo = q1;
+          r.hi = q2;
+        }
+        break;
+      case MGP_OP_UREM:
+        r.hi = A->hi;  // x % y <= x, and x % 0 = x
+        if (!Z(B->lo)) r.hi = MIN(r.hi, SUBV(B->hi, ONE()));
+        if (LT(A->hi, B->lo)) r = *A;  // x < y: x % y = x
+        break;
+      case MGP_OP_SHL: case MGP_OP_LSHR: case MGP_OP_ASHR: {
+        if (is_exact(*B)) {
+          const uint32_t s = bv_shift_amount(B->lo);
+          if (x.op == MGP_OP_SHL) {
+            if (s >= w) { r = exact(bv_zero(), w); break; }
+            r.z = OR(SHL(A->z, s), M(s));
+            r.o = SHL(A->o, s);
+            bool ovf;
+            V t, lo2;
+            t = bv_mul_full(A->hi, BIT(s), &lo2);
+            ovf = !Z(t) || (w < 256u && !Z(AND(lo2, NOT(M(w)))));
+            if (!ovf) {
+              r.lo = SHL(A->lo, s);
+              r.hi = lo2;
+            }
+          } else if (x.op == MGP_OP_LSHR) {
+            if (s >= w) { r = exact(bv_zero(), w); break; }
+            r.z = OR(SHR(AND(A->z, M(w)), s), NOT(M(w - s)));
+            r.o = SHR(A->o, s);
+            r.lo = SHR(A->lo, s);
+            r.hi = SHR(A->hi, s);
+          } else {
+            const uint32_t ss = s >= w ? w - 1u : s;  // shifting by >= w-1 leaves only sign copies
+            const V sb = BIT(w - 1u), m = M(w);
+            const bool s0 = !Z(AND(A->z, sb)), s1 = !Z(AND(A->o, sb));
+            const V zs = OR(AND(A->z, m), s0 ? NOT(m) : bv_zero());
+            const V os = OR(AND(A->o, m), s1 ? NOT(m) : bv_zero());
+            r.z = OR(bv_shr_fill(zs, ss, s0 ? 0xFFFFFFFFu : 0u), NOT(m));
+            r.o = AND(bv_shr_fill(os, ss, s1 ? 0xFFFFFFFFu : 0u), m);
+          }
+        } else if (x.op != MGP_OP_ASHR) {
+          const uint32_t slo = bv_shift_amount(B->lo);
+          if (slo >= w) {
+            r = exact(bv_zero(), w);
+          } else if (x.op == MGP_OP_LSHR) {  // monotone: up in x, down in s
+            const uint32_t shi = bv_shift_amount(B->hi);
+            r.hi = SHR(A->hi, slo);
+            r.lo = shi >= w ? bv_zero() : SHR(A->lo, shi);
+          } else {  // shl: at least min(s) low zero bits
+            r.z = OR(r.z, M(slo));
+          }
+        }
+        break;
+      }
+      case MGP_OP_EXTRACT: {
+        const uint32_t lo = x.p1, hiw = lo + w;
+        r.z = OR(SHR(A->z, lo), NOT(M(w)));
+        r.o = AND(SHR(A->o, lo), M(w));
+        if (EQV(SHR(A->lo, hiw), SHR(A->hi, hiw))) {  // same prefix above the field: monotone
+          r.lo = AND(SHR(A->lo, lo), M(w));
+          r.hi = AND(SHR(A->hi, lo), M(w));
+        }
+        break;
+      }
+      case MGP_OP_CONCAT: {
+        const uint32_t wb = W(x.b);
+        r.z = OR(SHL(A->z, wb), AND(B->z, M(wb)));
+        r.o = OR(SHL(A->o, wb), B->o);
+        r.lo = OR(SHL(A->lo, wb), B->lo);
+        r.hi = OR(SHL(A->hi, wb), B->hi);
+        break;
+      }
+      case MGP_OP_ZEXT: r.z = OR(A->z, NOT(M(W(x.a)))); r.o = A->o; r.lo = A->lo; r.hi = A->hi; break;
+      case MGP_OP_SEXT: {
+        const uint32_t wa = W(x.a);
+        const V sb = BIT(wa - 1u), ext = AND(NOT(M(wa)), M(w));
+        const bool s0 = !Z(AND(A->z, sb)), s1 = !Z(AND(A->o, sb));
+        r.z = OR(AND(A->z, M(wa)), s0 ? NOT(M(wa)) : NOT(M(w)));
+        r.o = OR(A->o, s1 ? ext : bv_zero());
+        if (s0) { r.lo = A->lo; r.hi = A->hi; }
+        if (s1) { r.lo = OR(A->lo, ext); r.hi = OR(A->hi, ext); }
+        break;
+      }
+      case MGP_OP_ITE: {
+        const uint8_t c = bs[x.a];
+        const AV &b = av[x.b], &e = av[x.c];
+        if (c == BT) r = b;
+        else if (c == BF) r = e;
+        else {
+          r.z = AND(b.z, e.z);
+          r.o = AND(b.o, e.o);
+          r.lo = MIN(b.lo, e.lo);
+          r.hi = MAX(b.hi, e.hi);
+        }
+        break;
+      }
+      default: break;  // UFAPP / UFINV / SDIV / SREM / SMOD: unconstrained unless folded
+    }
+    // exact operands: fold the ops whose transfer above is coarse
+    const bool two = x.op >= MGP_OP_MUL && x.op <= MGP_OP_ASHR && x.op != MGP_OP_AND && x.op != MGP_OP_OR &&
+                     x.op != MGP_OP_XOR && x.op != MGP_OP_NOT && x.op != MGP_OP_NEG;
+    if (two && is_exact(*A) && is_exact(*B)) r = exact(fold_bv(x.op, w, A->lo, B->lo, 0), w);
+    if (x.op == MGP_OP_SEXT && is_exact(*A)) r = exact(fold_bv(x.op, w, A->lo, bv_zero(), W(x.a)), w);
+    return meet((int32_t)i, r);
+  }
+
+  // -------------------------------------------------------------- backward
+  bool narrow_ult(int32_t a, int32_t b, bool strict) {  // require a < b (strict) or a <= b
+    const AV A = av[a], B = av[b];
+    AV ta = top(W(a)), tb = top(W(b));
+    if (strict) {
+      if (Z(B.hi) || EQV(A.lo, M(W(a)))) return false;
+      ta.hi = SUBV(B.hi, ONE());
+      tb.lo = ADDV(A.lo, ONE());
+    } else {
+      ta.hi = B.hi;
+      tb.lo = A.lo;
+    }
+    return meet(a, ta) && meet(b, tb);
+  }
+  // signed: the same on flipped images, mapped back
+  bool narrow_slt(int32_t a, int32_t b, bool strict) {
+    const uint32_t w = W(a);
+    AV fa = flip(av[a], w), fb = flip(av[b], w);
+    if (strict) {
+      if (Z(fb.hi) || EQV(fa.lo, M(w))) return false;
+      fa.hi = MIN(fa.hi, SUBV(fb.hi, ONE()));
+      fb.lo = MAX(fb.lo, ADDV(fa.lo, ONE()));
+    } else {
+      fa.hi = MIN(fa.hi, fb.hi);
+      fb.lo = MAX(fb.lo, fa.lo);
+    }
+    if (!normalize(fa, w) || !normalize(fb, w)) return false;
+    return meet(a, flip(fa, w)) && meet(b, flip(fb, w));
+  }
+
+  bool backward(uint32_t i) {
+    const mgp_node &x = nd[i];
+    if (isb[i]) {
+      const uint8_t r = bs[i];
+      switch (x.op) {
+        case MGP_OP_BNOT: return meetb(x.a, (uint8_t)(((r & BF) ? BT : 0) | ((r & BT) ? BF : 0)));
+        case MGP_OP_BAND:
+          if (r == BT) return meetb(x.a, BT) && meetb(x.b, BT);
+          if (r == BF) {
+            if (bs[x.a] == BT && !meetb(x.b, BF)) return false;
+            if (bs[x.b] == BT && !meetb(x.a, BF)) return false;
+          }
+          return true;
+        case MGP_OP_BOR:
+          if (r == BF) return meetb(x.a, BF) && meetb(x.b, BF);
+          if (r == BT) {
+            if (bs[x.a] == BF && !meetb(x.b, BT)) return false;
+            if (bs[x.b] == BF && !meetb(x.a, BT)) return false;
+          }
+          return true;
+        case MGP_OP_BITE: case MGP_OP_ITE:
+          if (bs[x.a] == BT) return meetb(x.b, r);
+          if (bs[x.a] == BF) return meetb(x.c, r);
+          if (!(bs[x.b] & r) && !meetb(x.a, BF)) return false;
+          if (!(bs[x.c] & r) && !meetb(x.a, BT)) return false;
+          return true;
+        default: break;
+      }
+      if (r == BB) return true;
+      const bool T = r == BT;
+      if ((x.op == MGP_OP_EQ && isb[x.a]) || x.op == MGP_OP_BEQ || x.op == MGP_OP_BXOR) {
+        const bool same_req = (x.op == MGP_OP_BXOR) ? !T : T;
+        auto other = [&](uint8_t v) -> uint8_t {
+          return same_req ? v : (uint8_t)(((v & BF) ? BT : 0) | ((v & BT) ? BF : 0));
+        };
+        if ((bs[x.a] == BT || bs[x.a] == BF) && !meetb(x.b, other(bs[x.a]))) return false;
+        if ((bs[x.b] == BT || bs[x.b] == BF) && !meetb(x.a, other(bs[x.b]))) return false;
+        return true;
+      }
+      switch (x.op) {
+        case MGP_OP_EQ:
+          if (T) {
+            const AV A = av[x.a], B = av[x.b];
+            return meet(x.a, B) && meet(x.b, A);
+          } else {  // a != b: an exact side trims the other's interval ends
+            for (int k = 0; k < 2; ++k) {
+              const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
+              if (!is_exact(av[q])) continue;
+              AV t = av[p];
+              if (EQV(t.lo, av[q].lo)) {
+                if (is_exact(t)) return false;
+                t.lo = ADDV(t.lo, ONE());
+              }
+              if (EQV(t.hi, av[q].lo)) t.hi = SUBV(t.hi, ONE());
+              if (!meet(p, t)) return false;
+            }
+            return true;
+          }
+        case MGP_OP_ULT: return T ? narrow_ult(x.a, x.b, true) : narrow_ult(x.b, x.a, false);
+        case MGP_OP_ULE: return T ? narrow_ult(x.a, x.b, false) : narrow_ult(x.b, x.a, true);
+        case MGP_OP_UGT: return T ? narrow_ult(x.b, x.a, true) : narrow_ult(x.a, x.b, false);
+        case MGP_OP_UGE: return T ? narrow_ult(x.b, x.a, false) : narrow_ult(x.a, x.b, true);
+        case MGP_OP_SLT: return T ? narrow_slt(x.a, x.b, true) : narrow_slt(x.b, x.a, false);
+        case MGP_OP_SLE: return T ? narrow_slt(x.a, x.b, false) : narrow_slt(x.b, x.a, true);
+        case MGP_OP_SGT: return T ? narrow_slt(x.b, x.a, true) : narrow_slt(x.a, x.b, false);
+        case MGP_OP_SGE: return T ? narrow_slt(x.b, x.a, false) : narrow_slt(x.a, x.b, true);
+        case MGP_OP_USUB_NOUDF: return T ? narrow_ult(x.b, x.a, false) : narrow_ult(x.a, x.b, true);
+        case MGP_OP_UADD_NOOVF: {
+          const uint32_t ow = W(x.a);
+          const V m = M(ow);
+          const AV A = av[x.a], B = av[x.b];
+          AV ta = top(ow), tb = top(ow);
+          if (T) {  // a + b < 2^w
+            ta.hi = SUBV(m, B.lo);
+            tb.hi = SUBV(m, A.lo);
+          } else {  // a + b >= 2^w
+            if (Z(A.hi) || Z(B.hi)) return false;
+            ta.lo = bv_mask(ADDV(SUBV(m, B.hi), ONE()), ow);
+            tb.lo = bv_mask(ADDV(SUBV(m, A.hi), ONE()), ow);
+          }
+          return meet(x.a, ta) && meet(x.b, tb);
+        }
+        case MGP_OP_UMUL_NOOVF:
+          if (T) {
+            const uint32_t ow = W(x.a);
+            const AV A = av[x.a], B = av[x.b];
+            V q, rr;
+            if (!Z(B.lo)) {
+              AV ta = top(ow);
+              bv_udivrem(M(ow), B.lo, &q, &rr);
+              ta.hi = q;
+              if (!meet(x.a, ta)) return false;
+            }
+            if (!Z(A.lo)) {
+              AV tb = top(ow);
+              bv_udivrem(M(ow), A.lo, &q, &rr);
+              tb.hi = q;
+              if (!meet(x.b, tb)) return false;
+            }
+          }
+          return true;
+        default: return true;
+      }
+    }
+    // BV node: the result's narrowed value constrains its operands
+    const uint32_t w = x.width;
+    const AV R = av[i];
+    switch (x.op) {
+      case MGP_OP_VAR: {  // every VAR node of one (index, width) shares the variable's value
+        AV &v = vars[vtie[i]];
+        AV t = v;
+        t.z = OR(t.z, R.z); t.o = OR(t.o, R.o); t.lo = MAX(t.lo, R.lo); t.hi = MIN(t.hi, R.hi);
+        if (!normalize(t, w)) return false;
+        if (!same(t, v)) {
+          v = t;
+          changed = true;
+        }
+        return true;
+      }
+      case MGP_OP_ADD: {
+        const AV A = av[x.a], B = av[x.b];
+        return meet(x.a, av_sub(R, B, w)) && meet(x.b, av_sub(R, A, w));
+      }
+      case MGP_OP_SUB: {
+        const AV A = av[x.a], B = av[x.b];
+        return meet(x.a, av_add(R, B, w)) && meet(x.b, av_sub(A, R, w));
+      }
+      case MGP_OP_XOR: {
+        const AV A = av[x.a], B = av[x.b];
+        return meet(x.a, av_xor(R, B, w)) && meet(x.b, av_xor(R, A, w));
+      }
+      case MGP_OP_NOT: return meet(x.a, av_not(R, w));
+      case MGP_OP_NEG: return meet(x.a, av_sub(exact(bv_zero(), w), R, w));
+      case MGP_OP_AND: {
+        const AV A = av[x.a], B = av[x.b];
+        AV ta = top(w), tb = top(w);
+        ta.o = R.o; tb.o = R.o;
+        ta.z = OR(ta.z, AND(R.z, B.o));
+        tb.z = OR(tb.z, AND(R.z, A.o));
+        ta.lo = R.lo; tb.lo = R.lo;  // a & b <= a
+        return meet(x.a, ta) && meet(x.b, tb);
+      }
+      case MGP_OP_OR: {
+        const AV A = av[x.a], B = av[x.b];
+        AV ta = top(w), tb = top(w);
+        ta.z = OR(ta.z, R.z); tb.z = OR(tb.z, R.z);
+        ta.o = AND(R.o, AND(B.z, M(w)));
+        tb.o = AND(R.o, AND(A.z, M(w)));
+        ta.hi = R.hi; tb.hi = R.hi;  // a | b >= a
+        return meet(x.a, ta) && meet(x.b, tb);
+      }
+      case MGP_OP_ZEXT: {
+        const uint32_t wa = W(x.a);
+        AV t = top(wa);
+        t.z = OR(t.z, R.z);
+        t.o = AND(R.o, M(wa));
+        if (!Z(AND(R.lo, NOT(M(wa))))) return false;
+        t.lo = R.lo;
+        t.hi = MIN(R.hi, M(wa));
+        return meet(x.a, t);
+      }
+      case MGP_OP_SEXT: {
+        const uint32_t wa = W(x.a);
+        AV t = top(wa);
+        t.z = OR(t.z, AND(R.z, M(wa)));
+        t.o = AND(R.o, M(wa));
+        return meet(x.a, t);
+      }
+      case MGP_OP_EXTRACT: {
+        const uint32_t wa = W(x.a), lo = x.p1;
+        AV t = top(wa);
+        t.z = OR(t.z, SHL(AND(R.z, M(w)), lo));
+        t.o = SHL(R.o, lo);
+        return meet(x.a, t);
+      }
+      case MGP_OP_CONCAT: {
+        const uint32_t wa = W(x.a), wb = W(x.b);
+        AV ta = top(wa), tb = top(wb);
+        ta.z = OR(ta.z, SHR(AND(R.z, M(w)), wb));
+        ta.o = SHR(R.o, wb);
+        ta.lo = SHR(R.lo, wb);
+        ta.hi = SHR(R.hi, wb);
+        tb.z = OR(tb.z, AND(R.z, M(wb)));
+        tb.o = AND(R.o, M(wb));
+        if (EQV(SHR(R.lo, wb), SHR(R.hi, wb))) {
+          tb.lo = AND(R.lo, M(wb));
+          tb.hi = AND(R.hi, M(wb));
+        }
+        return meet(x.a, ta) && meet(x.b, tb);
+      }
+      case MGP_OP_SHL: case MGP_OP_LSHR: {
+        if (!is_exact(av[x.b])) return true;
+        const uint32_t s = bv_shift_amount(av[x.b].lo);
+        if (s >= w) return true;
+        AV t = top(w);
+        if (x.op == MGP_OP_SHL) {  // r[w-1..s] = a[w-1-s..0]
+          t.z = OR(t.z, AND(SHR(AND(R.z, M(w)), s), M(w - s)));
+          t.o = SHR(R.o, s);
+        } else {  // r[w-1-s..0] = a[w-1..s]
+          t.z = OR(t.z, SHL(AND(R.z, M(w - s)), s));
+          t.o = SHL(AND(R.o, M(w - s)), s);
+          t.lo = SHL(R.lo, s);
+          t.hi = AND(OR(SHL(R.hi, s), M(s)), M(w));
+        }
+        return meet(x.a, t);
+      }
+      case MGP_OP_ITE: {
+        const uint8_t c = bs[x.a];
+        if (c == BT) return meet(x.b, R);
+        if (c == BF) return meet(x.c, R);
+        if (!compatible(x.b, R) && !meetb(x.a, BF)) return false;
+        if (!compatible(x.c, R) && !meetb(x.a, BT)) return false;
+        return true;
+      }
+      default: return true;
+    }
+  }
+
+  // 1 = refuted (UNSAT), 0 = not refuted
+  int run(uint32_t max_passes) {
+    if (!meetb((int32_t)n - 1, BT)) return 1;
+    for (uint32_t pass = 0; pass < max_passes; ++pass) {
+      changed = false;
+      for (uint32_t i = 0; i < n; ++i)
+        if (!forward(i)) return 1;
+      if (!meetb((int32_t)n - 1, BT)) return 1;
+      for (uint32_t i = n; i-- > 0;)
+        if (!backward(i)) return 1;
+      if (!changed) break;
+    }
+    return 0;
+  }
+};
+
+int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t max_passes,
+               State *keep) {
+  if (n == 0 || n > (1u << 20)) return -1;
+  State st;
+  State &s = keep ? *keep : st;
+  s.nd = nd;
+  s.n = (uint32_t)n;
+  s.consts = consts;
+  s.n_consts = n_consts;
+  if (!s.setup()) return -1;
+  return s.run(max_passes ? max_passes : 16u);
+}
+
+}  // namespace
+
+extern "C" int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                          const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                          int8_t *out) {
+  if (!node_offsets || !out || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
+    const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
+    if (n1 < n0 || c1 < c0) {
+      out[s] = -1;
+      continue;
+    }
+    out[s] = (int8_t)refute_one(nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0,
+                                max_passes, nullptr);
+  }
+  return MGP_OK;
+}
+
+extern "C" int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *consts,
+                                uint64_t n_consts, uint32_t max_passes, uint32_t *out_av) {
+  if (!nodes || !out_av) return MGP_E_ARG;
+  State s;
+  const int r = refute_one(nodes, n_nodes, consts, n_consts, max_passes, &s);
+  if (r < 0) return r;
+  for (uint64_t i = 0; i < n_nodes; ++i) {
+    uint32_t *o = out_av + 33ull * i;
+    memcpy(o, s.av[i].z.w, 32);
+    memcpy(o + 8, s.av[i].o.w, 32);
+    memcpy(o + 16, s.av[i].lo.w, 32);
+    memcpy(o + 24, s.av[i].hi.w, 32);
+    o[32] = s.bs[i];
+  }
+  return r;
+}

@@ -15,9 +15,12 @@ Mirrors, with the same names, argument meaning and error behaviour:
 
 What changes is the order: a batch of states is first evaluated on the GPU
 (libmgp.so) against candidate assignments; a witness PROVES satisfiability
-(`sat`).  Everything else — no witness, unsupported DAG, every UNSAT, every
-minimize/maximize query (tx-sequence model values must stay bit-identical to
-z3's, solver.py:88-136) — goes to the fallback backend unchanged.  The
+(`sat`).  A state without a witness goes through the host UNSAT pre-check
+(mgp_refute: known bits x intervals with backward narrowing, sound), which
+PROVES `unsat` for the shallow contradictions.  Everything else — no witness
+and no refutation, unsupported DAG, and the model of every minimize/maximize
+query (tx-sequence model values must stay bit-identical to z3's,
+solver.py:88-136) — goes to the fallback backend unchanged.  The
 fallback is z3 (mythril_amd.z3_backend, where z3 is installed); without it the
 answer is `unknown`, which each caller maps exactly as the reference does.
 """
@@ -64,12 +67,14 @@ class SolverStatistics(metaclass=_Singleton):
         self.gpu_queries = 0      # states sent to the GPU
         self.gpu_sat = 0          # states proven SAT by a GPU witness
         self.gpu_undecided = 0
+        self.refuted = 0          # states proven UNSAT by the host pre-check (mgp_refute)
         self.gpu_time = 0.0
         self.gpu_batches = 0
 
     def __repr__(self):
         return (f"Query count: {self.query_count} \nSolver time: {self.solver_time}\n"
-                f"GPU queries: {self.gpu_queries} (sat {self.gpu_sat}, undecided {self.gpu_undecided}, "
+                f"GPU queries: {self.gpu_queries} (sat {self.gpu_sat}, refuted {self.refuted}, "
+                f"undecided {self.gpu_undecided}, "
                 f"{self.gpu_batches} batches, {self.gpu_time:.3f}s)")
 
 
@@ -157,10 +162,16 @@ class Prefilter:
         self.n_cand = n_cand
         self.seed = seed
         self._calls = 0
+        self.refute = True  # host UNSAT pre-check (mgp_refute) on every GPU miss
 
     def check_states(self, states: Sequence[Sequence[Term]],
                      parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> List[Tuple[str, Optional[Dict[str, int]]]]:
-        """-> per state ('sat', assignment) or ('undecided', None)."""
+        """-> per state ('sat', assignment), ('unsat', None) or ('undecided', None).
+
+        'sat' = a GPU witness (a model); 'unsat' = proven by the host pre-check
+        (mgp_refute: known bits x intervals, sound); everything else is
+        'undecided' and goes to the fallback solver.
+        """
         if not states:
             return []
         stats = SolverStatistics()
@@ -172,16 +183,22 @@ class Prefilter:
         self._calls += 1
         cands = D.make_candidates(dags, self.n_cand, n_vars, seed=self.seed + self._calls, parents=parents)
         first, wit = self.ctx.eval_batch(words, po, cands)
+        proven = self._N.refute(nodes, noff, consts, coff) if self.refute else np.zeros(len(dags), np.int8)
         out: List[Tuple[str, Optional[Dict[str, int]]]] = []
         for i, d in enumerate(dags):
             if first[i] >= 0:
+                if proven[i] == 1:  # a witness and an UNSAT proof cannot both hold
+                    raise RuntimeError(f"mgp_refute refuted state {i} that has a GPU witness (soundness bug)")
                 out.append((sat, D.witness_to_model(d, wit[i])))
+            elif proven[i] == 1:
+                out.append((unsat, None))
             else:
                 out.append(("undecided", None))
         stats.gpu_batches += 1
         stats.gpu_queries += len(states)
         stats.gpu_sat += sum(1 for r in out if r[0] == sat)
-        stats.gpu_undecided += sum(1 for r in out if r[0] != sat)
+        stats.refuted += sum(1 for r in out if r[0] == unsat)
+        stats.gpu_undecided += sum(1 for r in out if r[0] == "undecided")
         stats.gpu_time += time.time() - t0
         return out
 
@@ -249,6 +266,9 @@ class Solver(BaseSolver):
             if res == sat:
                 self._model = Model([assign])
                 return sat
+            if res == unsat:
+                self._model = None
+                return unsat
         return self._fallback()
 
     @stat_smt_query
@@ -262,7 +282,8 @@ class Solver(BaseSolver):
 
 
 class Optimize(BaseSolver):
-    """Optimize: always the fallback solver — minimised model values are reported verbatim."""
+    """Optimize: minimised model values come from the fallback solver (they are reported
+    verbatim); a state the pre-check refutes is unsat without it."""
 
     def __init__(self):
         super().__init__()
@@ -276,13 +297,15 @@ class Optimize(BaseSolver):
         self._max.append(e.raw if isinstance(e, Expression) else e)
 
     def check(self, *args) -> str:
-        if not self._min and not self._max:
-            pf = prefilter()
-            if pf is not None:
-                res, assign = pf.check_states([self.constraints])[0]
-                if res == sat:
-                    self._model = Model([assign])
-                    return sat
+        pf = prefilter()
+        if pf is not None:
+            res, assign = pf.check_states([self.constraints])[0]
+            if res == unsat:  # no model exists, whatever the objectives
+                self._model = None
+                return unsat
+            if res == sat and not self._min and not self._max:
+                self._model = Model([assign])
+                return sat
         return self._fallback()
 
     @stat_smt_query
@@ -393,9 +416,10 @@ class Constraints(list):
 def batch_is_possible(items: Sequence[Constraints]) -> List[bool]:
     """The prune filter of LaserEVM.exec (svm.py:251-255) over a whole worklist.
 
-    One GPU batch for every uncached entry; each entry the GPU cannot prove SAT
-    goes through the reference's single-query path (100 ms fallback check,
-    unknown -> possible, constraints.py:42-51).
+    One GPU batch for every uncached entry; an entry with a witness is possible,
+    an entry the host pre-check proves UNSAT is not, and every other entry goes
+    through the reference's single-query path (100 ms fallback check, unknown ->
+    possible, constraints.py:42-51).
     """
     todo = [c for c in items if c._is_possible is None]
     pf = prefilter()
@@ -406,6 +430,9 @@ def batch_is_possible(items: Sequence[Constraints]) -> List[bool]:
         if res == sat:
             c._is_possible = True
             c.witness = assign
+            continue
+        if res == unsat:
+            c._is_possible = False
             continue
         s = Solver()
         s.set_timeout(c._default_timeout)

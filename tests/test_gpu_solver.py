@@ -3,8 +3,9 @@
 Mirrors tests/laser/keccak_tests.py:7-138 (same cases, same sat/unsat
 expectations) on top of mythril_amd.smt + mythril_amd.keccak: the GPU must
 prove every SAT case with a witness the oracle confirms, and must never claim
-SAT on an UNSAT case (those are left to the fallback solver: without z3 the
-answer is `unknown`, exactly what reaches z3 in the integrated path).
+SAT on an UNSAT case (those are proven UNSAT by the host pre-check or left to
+the fallback solver: without z3 the answer is `unknown`, exactly what reaches
+z3 in the integrated path).
 """
 import numpy as np
 import pytest
@@ -86,7 +87,8 @@ def test_keccak_basic(backend, input1, input2, expected):
         assert _oracle_confirms([And(c1, c2), o1 == o2], s.model().assignments[0])
     else:
         assert r != SV.sat
-        assert backend.calls == 1  # left to the fallback solver unchanged
+        # proven UNSAT by the host pre-check (no fallback call), or left to the fallback unchanged
+        assert (r == SV.unsat and backend.calls == 0) or (r == SV.unknown and backend.calls == 1)
 
 
 def test_keccak_symbol_and_val(backend):
@@ -158,9 +160,12 @@ def test_get_model_contract(backend):
     assert m[x] == 5
     with pytest.raises(SV.UnsatError):
         SV.get_model((False,))
-    with pytest.raises(SV.UnsatError):  # undecided -> fallback -> unknown -> UnsatError (solver.py:56-61)
+    with pytest.raises(SV.UnsatError):  # refuted by the host pre-check: no fallback call
         SV.get_model((x == BVV(5, 256), x == BVV(6, 256)))
-    with pytest.raises(SV.UnsatError):  # minimize always goes to the fallback
+    assert backend.calls == 0 and SV.SolverStatistics().refuted == 1
+    with pytest.raises(SV.UnsatError):  # undecided -> fallback -> unknown -> UnsatError (solver.py:56-61)
+        SV.get_model((x * x == BVV(5, 256),))
+    with pytest.raises(SV.UnsatError):  # minimize: the model comes from the fallback
         SV.get_model((x == BVV(5, 256),), minimize=(x,))
     assert backend.calls == 2
 
@@ -169,12 +174,14 @@ def test_constraints_is_possible_batch(backend):
     x, y = BVS("x", 256), BVS("y", 256)
     items = [SV.Constraints([x == BVV(i, 256), Not(y == x)]) for i in range(50)]
     items.append(SV.Constraints([x == BVV(1, 256), x == BVV(2, 256)]))
+    items.append(SV.Constraints([x * x == BVV(5, 256)]))  # no witness, not refuted (5 is no square mod 2^256)
     res = SV.batch_is_possible(items)
     assert res[:50] == [True] * 50
-    assert res[50] is True  # unknown counts as possible (constraints.py:50)
+    assert res[50] is False  # proven UNSAT by the host pre-check, no fallback call
+    assert res[51] is True  # unknown counts as possible (constraints.py:50)
     assert backend.calls == 1
     st = SV.SolverStatistics()
-    assert st.gpu_queries == 51 and st.gpu_sat == 50 and st.query_count == 1
+    assert st.gpu_queries == 52 and st.gpu_sat == 50 and st.refuted == 1 and st.query_count == 1
     # children inherit the witness as their first candidate
     child = items[0].copy()
     child.append(UGE_(y, BVV(0, 256)))

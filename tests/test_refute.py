@@ -1,0 +1,260 @@
+"""UNSAT pre-check (mgp_refute, host C++) vs the oracle — CPU only.
+
+mgp_refute claims "no assignment satisfies the state" (it replaces the z3
+call behind Constraints.is_possible, constraints.py:34-51, for the states it
+decides).  A claim is only useful if it is never wrong, so the tests check
+soundness against oracle.bvsem / oracle.coracle:
+
+* node by node: for a satisfying assignment, every node's concrete value lies
+  inside the abstract value the refuter ends with (known bits and interval),
+  and the state is not refuted;
+* state by state: no refuted state has a model — exhaustively over all
+  assignments for random small-width DAGs over the whole operator set, and by
+  candidate search (planted witnesses included) on the synthetic batch;
+* hand-written contradictions of the kinds LASER produces are refuted.
+"""
+import numpy as np
+import pytest
+
+from mythril_amd import _native as N
+from oracle import bvsem as S
+from oracle import coracle
+
+from ._util import node_array, pack_states, random_cands, state_slice
+
+X0 = [S.VAR, 256, -1, -1, -1, 0, 0]
+X1 = [S.VAR, 256, -1, -1, -1, 1, 0]
+
+
+def _refute(states, max_passes=0):
+    nodes, noff, consts, coff = pack_states(states)
+    return N.refute(nodes, noff, consts, coff, max_passes=max_passes)
+
+
+def _contains(av_row, v, w, is_bool):
+    if is_bool:
+        return bool(av_row[32] & (2 if v else 1))
+    z = S.limbs_to_int(av_row[0:8])
+    o = S.limbs_to_int(av_row[8:16])
+    lo = S.limbs_to_int(av_row[16:24])
+    hi = S.limbs_to_int(av_row[24:32])
+    return (v & z) == 0 and (v & o) == o and lo <= v <= hi and v <= S.mask(w)
+
+
+def _check_contained(nodes, consts, xs):
+    """xs satisfies the root -> not refuted and every node value inside its abstract value."""
+    vals = S.eval_dag(nodes, consts, xs)
+    assert vals[-1], "test bug: assignment does not satisfy the root"
+    arr = nodes if isinstance(nodes, np.ndarray) else node_array(nodes)
+    climbs = np.array([S.int_to_limbs(c) for c in consts], dtype=np.uint32).reshape(-1, 8)
+    r, av = N.refute_trace(arr, climbs)
+    assert r == 0, "refuted a satisfiable state"
+    for i, v in enumerate(vals):
+        isb = isinstance(v, bool)
+        w = 1 if isb else int(arr[i]["width"])
+        assert _contains(av[i], v, w, isb), (i, int(arr[i]["op"]), v)
+
+
+# ------------------------------------------------------------ hand cases
+def _st(extra_nodes, consts):
+    return ([X0, X1] + extra_nodes, consts)
+
+
+UNSAT_CASES = {
+    # x == 5 and x == 6
+    "eq_eq": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+                  [S.EQ, 1, 0, 2, -1, 0, 0], [S.EQ, 1, 0, 3, -1, 0, 0], [S.BAND, 1, 4, 5, -1, 0, 0]], [5, 6]),
+    # x <u 3 and x >u 5
+    "ult_ugt": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+                    [S.ULT, 1, 0, 2, -1, 0, 0], [S.UGT, 1, 0, 3, -1, 0, 0], [S.BAND, 1, 4, 5, -1, 0, 0]], [3, 5]),
+    # (x & 1) == 1 and (x & 1) == 0
+    "and_bit": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.AND, 256, 0, 2, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+                    [S.EQ, 1, 3, 2, -1, 0, 0], [S.EQ, 1, 3, 4, -1, 0, 0], [S.BAND, 1, 5, 6, -1, 0, 0]], [1, 0]),
+    # x + 1 == 0 (x = 2^256 - 1) and x <u 10
+    "add_wrap": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.ADD, 256, 0, 2, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+                     [S.EQ, 1, 3, 4, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 2, 0], [S.ULT, 1, 0, 6, -1, 0, 0],
+                     [S.BAND, 1, 5, 7, -1, 0, 0]], [1, 0, 10]),
+    # Extract(7, 0, x) == 0x41 and x == 0x42
+    "extract": _st([[S.EXTRACT, 8, 0, -1, -1, 7, 0], [S.CONST, 8, -1, -1, -1, 0, 0], [S.EQ, 1, 2, 3, -1, 0, 0],
+                    [S.CONST, 256, -1, -1, -1, 1, 0], [S.EQ, 1, 0, 5, -1, 0, 0], [S.BAND, 1, 4, 6, -1, 0, 0]],
+                   [0x41, 0x42]),
+    # Not(BVAddNoOverflow(x, y, False)) with x <u 10 and y <u 10
+    "addnoovf": _st([[S.UADD_NOOVF, 1, 0, 1, -1, 0, 0], [S.BNOT, 1, 2, -1, -1, 0, 0],
+                     [S.CONST, 256, -1, -1, -1, 0, 0], [S.ULT, 1, 0, 4, -1, 0, 0], [S.ULT, 1, 1, 4, -1, 0, 0],
+                     [S.BAND, 1, 3, 5, -1, 0, 0], [S.BAND, 1, 7, 6, -1, 0, 0]], [10]),
+    # jumpi pair: cond and Not(cond) on one path (instructions.py:1556-1562)
+    "jumpi_pair": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.SUB, 256, 0, 1, -1, 0, 0], [S.EQ, 1, 3, 2, -1, 0, 0],
+                       [S.BNOT, 1, 4, -1, -1, 0, 0], [S.BAND, 1, 4, 5, -1, 0, 0]], [0]),
+    # calldatasize bound vs byte index: size <u 4 and 35 <u size
+    "calldata": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.ULT, 1, 0, 2, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+                     [S.ULT, 1, 4, 0, -1, 0, 0], [S.BAND, 1, 3, 5, -1, 0, 0]], [4, 35]),
+    # signed: x <s 0 and x >=u 0 and Extract(255,255,x) == 0
+    "signed": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.SLT, 1, 0, 2, -1, 0, 0], [S.EXTRACT, 1, 0, -1, -1, 255, 255],
+                   [S.CONST, 1, -1, -1, -1, 0, 0], [S.EQ, 1, 4, 5, -1, 0, 0], [S.BAND, 1, 3, 6, -1, 0, 0]], [0]),
+    # ITE: If(x == 1, 7, 9) == 8
+    "ite": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.EQ, 1, 0, 2, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+                [S.CONST, 256, -1, -1, -1, 2, 0], [S.ITE, 256, 3, 4, 5, 0, 0], [S.CONST, 256, -1, -1, -1, 3, 0],
+                [S.EQ, 1, 6, 7, -1, 0, 0]], [1, 7, 9, 8]),
+    # shift: LShR(x, 248) == 0x1ff (the result has at most 8 bits)
+    "lshr": _st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.LSHR, 256, 0, 2, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+                 [S.EQ, 1, 3, 4, -1, 0, 0]], [248, 0x1FF]),
+    # Concat(x8, y8) == 0x1234 and x8 == 0x13 (8-bit vars)
+    "concat": ([[S.VAR, 8, -1, -1, -1, 0, 0], [S.VAR, 8, -1, -1, -1, 1, 0], [S.CONCAT, 16, 0, 1, -1, 0, 0],
+                [S.CONST, 16, -1, -1, -1, 0, 0], [S.EQ, 1, 2, 3, -1, 0, 0], [S.CONST, 8, -1, -1, -1, 1, 0],
+                [S.EQ, 1, 0, 5, -1, 0, 0], [S.BAND, 1, 4, 6, -1, 0, 0]], [0x1234, 0x13]),
+    # literal false
+    "false": ([[S.FALSE, 1, -1, -1, -1, 0, 0]], []),
+}
+
+SAT_CASES = {
+    "eq_lt": (_st([[S.CONST, 256, -1, -1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0], [S.EQ, 1, 0, 2, -1, 0, 0],
+                   [S.ULT, 1, 0, 3, -1, 0, 0], [S.BAND, 1, 4, 5, -1, 0, 0]], [5, 6]), [5, 0]),
+    "concat": (([[S.VAR, 8, -1, -1, -1, 0, 0], [S.VAR, 8, -1, -1, -1, 1, 0], [S.CONCAT, 16, 0, 1, -1, 0, 0],
+                 [S.CONST, 16, -1, -1, -1, 0, 0], [S.EQ, 1, 2, 3, -1, 0, 0]], [0x1234]), [0x12, 0x34]),
+    "mul_noovf": (_st([[S.UMUL_NOOVF, 1, 0, 1, -1, 0, 0], [S.BNOT, 1, 2, -1, -1, 0, 0]], []), [1 << 200, 1 << 100]),
+    "sdiv": (_st([[S.SDIV, 256, 0, 1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 0, 0], [S.EQ, 1, 2, 3, -1, 0, 0]],
+                 [(1 << 256) - 1]), [5, 0]),
+}
+
+
+@pytest.mark.parametrize("name", sorted(UNSAT_CASES))
+def test_refutes_contradictions(name):
+    nl, cl = UNSAT_CASES[name]
+    assert _refute([(nl, cl)])[0] == 1
+
+
+@pytest.mark.parametrize("name", sorted(SAT_CASES))
+def test_keeps_satisfiable(name):
+    (nl, cl), xs = SAT_CASES[name]
+    assert S.eval_root(nl, cl, xs)
+    assert _refute([(nl, cl)])[0] == 0
+    _check_contained(nl, cl, xs)
+
+
+def test_unsupported_and_empty():
+    wide = ([[S.VAR, 512, -1, -1, -1, 0, 0], [S.EQ, 1, 0, 0, -1, 0, 0]], [])
+    bad = ([[S.ADD, 256, 3, 4, -1, 0, 0]], [])
+    out = _refute([wide, bad, UNSAT_CASES["eq_eq"]])
+    assert list(out) == [-1, -1, 1]
+    nodes, noff, consts, coff = pack_states([])
+    assert N.refute(nodes, noff, consts, coff).size == 0
+
+
+# ------------------------------------------- exhaustive small-width DAGs
+def _random_small_dag(rng, w=4, n_ops=10):
+    """Random DAG over two w-bit vars using the whole operator set; root = AND of 2-3 Bools."""
+    nodes, consts = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]], []
+    bv = {w: [0, 1]}
+    bools = []
+
+    def const(width):
+        consts.append(int(rng.integers(0, 1 << width)))
+        nodes.append([S.CONST, width, -1, -1, -1, len(consts) - 1, 0])
+        bv.setdefault(width, []).append(len(nodes) - 1)
+        return len(nodes) - 1
+
+    def pick(width):
+        pool = bv.get(width, [])
+        if not pool or rng.random() < 0.2:
+            return const(width)
+        return int(pool[int(rng.integers(len(pool)))])
+
+    binops = [S.ADD, S.SUB, S.MUL, S.UDIV, S.UREM, S.SDIV, S.SREM, S.SMOD, S.AND, S.OR, S.XOR, S.SHL, S.LSHR, S.ASHR]
+    cmps = [S.EQ, S.ULT, S.ULE, S.UGT, S.UGE, S.SLT, S.SLE, S.SGT, S.SGE, S.UADD_NOOVF, S.UMUL_NOOVF, S.USUB_NOUDF]
+    h = w // 2
+    for _ in range(n_ops):
+        k = rng.random()
+        if k < 0.40:
+            op = binops[int(rng.integers(len(binops)))]
+            a, b = pick(w), pick(w)
+            nodes.append([op, w, a, b, -1, 0, 0])
+            bv[w].append(len(nodes) - 1)
+        elif k < 0.48:
+            nodes.append([[S.NOT, S.NEG][int(rng.integers(2))], w, pick(w), -1, -1, 0, 0])
+            bv[w].append(len(nodes) - 1)
+        elif k < 0.56:
+            lo = int(rng.integers(0, w - h + 1))
+            nodes.append([S.EXTRACT, h, pick(w), -1, -1, lo + h - 1, lo])
+            bv.setdefault(h, []).append(len(nodes) - 1)
+        elif k < 0.64:
+            op = [S.ZEXT, S.SEXT, S.CONCAT][int(rng.integers(3))]
+            if op == S.CONCAT:
+                nodes.append([S.CONCAT, w, pick(w - h), pick(h), -1, 0, 0])
+            else:
+                nodes.append([op, w, pick(h), -1, -1, 0, 0])
+            bv[w].append(len(nodes) - 1)
+        elif k < 0.70 and bools:
+            c = bools[int(rng.integers(len(bools)))]
+            nodes.append([S.ITE, w, c, pick(w), pick(w), 0, 0])
+            bv[w].append(len(nodes) - 1)
+        elif k < 0.92:
+            op = cmps[int(rng.integers(len(cmps)))]
+            nodes.append([op, 1, pick(w), pick(w), -1, 0, 0])
+            bools.append(len(nodes) - 1)
+        elif bools:
+            op = [S.BAND, S.BOR, S.BXOR, S.BNOT, S.BEQ, S.BITE][int(rng.integers(6))]
+            a = bools[int(rng.integers(len(bools)))]
+            b = bools[int(rng.integers(len(bools)))]
+            c = bools[int(rng.integers(len(bools)))]
+            if op == S.BNOT:
+                nodes.append([op, 1, a, -1, -1, 0, 0])
+            elif op == S.BITE:
+                nodes.append([op, 1, a, b, c, 0, 0])
+            else:
+                nodes.append([op, 1, a, b, -1, 0, 0])
+            bools.append(len(nodes) - 1)
+    while len(bools) < 2:
+        nodes.append([cmps[int(rng.integers(len(cmps)))], 1, pick(w), pick(w), -1, 0, 0])
+        bools.append(len(nodes) - 1)
+    root = bools[-1]
+    for b in bools[-3:-1]:
+        nodes.append([S.BAND, 1, root, b, -1, 0, 0])
+        root = len(nodes) - 1
+    return nodes, consts
+
+
+@pytest.mark.parametrize("w", [4, 6])
+def test_exhaustive_small_width_soundness(w):
+    rng = np.random.default_rng(0xBADC0DE + w)
+    n = 500 if w == 4 else 160
+    states = [_random_small_dag(rng, w=w, n_ops=int(rng.integers(4, 14))) for _ in range(n)]
+    verdict = _refute(states)
+    refuted = 0
+    space = [(x, y) for x in range(1 << w) for y in range(1 << w)]
+    for (nl, cl), r in zip(states, verdict):
+        assert r in (0, 1)
+        models = [xs for xs in space if S.eval_root(nl, cl, xs)]
+        if r == 1:
+            refuted += 1
+            assert not models, "refuted a satisfiable state"
+        else:
+            for xs in models[:: max(1, len(models) // 3)]:
+                _check_contained(nl, cl, xs)
+    assert refuted > n // 20  # the pass decides a real share of these
+
+
+# ------------------------------------------------------- synthetic batch
+def test_synthetic_witnesses_inside_abstract_values():
+    b = N.synth_generate(0x4D595448, 7, 120, 64, 16)
+    checked = 0
+    for s in range(120):
+        if not b["planted"][s]:
+            continue
+        nodes, consts = state_slice(b, s)
+        _check_contained(nodes, consts, [S.limbs_to_int(x) for x in b["plant_words"][s]])
+        checked += 1
+    assert checked > 30
+
+
+def test_synthetic_batch_no_refuted_state_has_a_model():
+    n_states, n_cand = 4096, 64
+    b = N.synth_generate(0x4D595448, 1 << 20, n_states, 64, n_cand)
+    verdict = N.refute(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+    assert set(np.unique(verdict)) <= {0, 1}
+    assert not verdict[b["planted"].astype(bool)].any()
+    cands = random_cands(np.random.default_rng(3), n_states, n_cand, b["n_vars"])
+    for s in range(n_states):
+        if b["planted"][s]:
+            cands[s, b["plant_idx"][s]] = b["plant_words"][s]
+    first = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)
+    assert not ((verdict == 1) & (first >= 0)).any()

@@ -1,0 +1,97 @@
+"""Solver front end with the host UNSAT pre-check — CPU only.
+
+The GPU stage is replaced by a stub context that finds no witness, so every
+state reaches mgp_refute and then, if not refuted, the fallback backend.  The
+contracts checked are the reference's: Constraints.is_possible
+(constraints.py:34-51: unsat -> False, unknown -> True), get_model
+(analysis/solver.py:27-61: UnsatError on unsat/unknown) and
+SolverStatistics.query_count (one per fallback check, solver_statistics.py).
+"""
+import numpy as np
+import pytest
+
+from mythril_amd import _native as N
+from mythril_amd import solver as SV
+from mythril_amd.smt import And, Not, Or, ULT, UGT, symbol_factory
+
+BVV = symbol_factory.BitVecVal
+BVS = symbol_factory.BitVecSym
+
+
+class NoWitnessContext:
+    """Stands in for the GPU context: no candidate satisfies any state."""
+
+    def __init__(self, device=0):
+        self.batches = 0
+
+    def eval_batch(self, words, po, cands):
+        self.batches += 1
+        n = len(po) - 1
+        return np.full(n, -1, dtype=np.int32), np.zeros((n, cands.shape[2], 8), dtype=np.uint32)
+
+    def close(self):
+        pass
+
+
+class CountingBackend(SV.Backend):
+    def __init__(self):
+        self.calls = 0
+
+    def check(self, terms, timeout_ms, minimize=(), maximize=()):
+        self.calls += 1
+        return SV.unknown, None
+
+
+@pytest.fixture()
+def fe(monkeypatch):
+    monkeypatch.setattr(N, "Context", NoWitnessContext)
+    monkeypatch.setattr(SV, "_prefilter", None)
+    SV.enable_gpu(True)
+    b = CountingBackend()
+    old = SV.set_backend(b)
+    SV.SolverStatistics().reset()
+    SV.get_model.cache_clear()
+    yield b
+    SV.set_backend(old)
+    SV.get_model.cache_clear()
+
+
+def test_is_possible_refuted_without_fallback(fe):
+    x, size = BVS("x", 256), BVS("calldatasize", 256)
+    items = [
+        SV.Constraints([x == BVV(1, 256), x == BVV(2, 256)]),
+        SV.Constraints([ULT(size, BVV(4, 256)), UGT(size, BVV(35, 256))]),
+        SV.Constraints([x == BVV(3, 256), Not(x == BVV(3, 256))]),
+        SV.Constraints([x * x == BVV(5, 256)]),  # UNSAT, but not by bits and ranges
+        SV.Constraints([Or(x == BVV(1, 256), x == BVV(2, 256))]),  # SAT; the stub finds no witness
+    ]
+    assert SV.batch_is_possible(items) == [False, False, False, True, True]
+    st = SV.SolverStatistics()
+    assert st.refuted == 3 and st.query_count == 2 and fe.calls == 2
+    assert [c._is_possible for c in items] == [False, False, False, True, True]
+
+
+def test_get_model_and_optimize(fe):
+    x = BVS("x", 256)
+    with pytest.raises(SV.UnsatError):
+        SV.get_model((x == BVV(5, 256), ULT(x, BVV(5, 256))))
+    assert fe.calls == 0
+    with pytest.raises(SV.UnsatError):  # minimize: still no model exists, no fallback needed
+        SV.get_model((And(x == BVV(5, 256), x == BVV(7, 256)),), minimize=(x,))
+    assert fe.calls == 0
+    with pytest.raises(SV.UnsatError):  # satisfiable but minimised -> fallback (unknown here)
+        SV.get_model((ULT(x, BVV(5, 256)),), minimize=(x,))
+    assert fe.calls == 1
+    s = SV.Solver()
+    s.add(x == BVV(9, 256), UGT(x, BVV(9, 256)))
+    assert s.check() == SV.unsat and fe.calls == 1
+    assert SV.SolverStatistics().query_count == 1
+
+
+def test_refute_off_restores_reference_path(fe):
+    x = BVS("x", 256)
+    pf = SV.prefilter()
+    pf.refute = False
+    items = [SV.Constraints([x == BVV(1, 256), x == BVV(2, 256)])]
+    assert SV.batch_is_possible(items) == [True]  # unknown -> possible, via the fallback
+    assert fe.calls == 1 and SV.SolverStatistics().refuted == 0

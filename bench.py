@@ -62,6 +62,8 @@ def main():
     ap.add_argument("--keccak-chunk", type=int, default=1 << 26)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--refute-sample", type=int, default=1 << 18,
+                    help="states of the rank-0 batch run through the host UNSAT pre-check (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -254,6 +256,28 @@ def main():
         }
         del d_pre, d_dig
 
+    # ------------------------------------------- solver-call accounting (host pre-check)
+    # Of a sample of the batch: states with a GPU witness (SAT, no solver call), states the
+    # host pre-check proves UNSAT (mgp_refute, no solver call), and the rest, which the
+    # integrated path hands to z3 (SURVEY.md 8d "z3 calls").  Not part of the timed step.
+    prefilter = None
+    if rank == 0 and args.refute_sample > 0:
+        ns = min(n_states, args.refute_sample)
+        tr = time.perf_counter()
+        ver = N.refute(b["nodes"][: int(b["node_offsets"][ns])], b["node_offsets"][: ns + 1], b["consts"],
+                       b["const_offsets"][: ns + 1])
+        dtr = time.perf_counter() - tr
+        sat_s, ref_s = first[:ns] >= 0, ver == 1
+        if (sat_s & ref_s).any():
+            raise RuntimeError("mgp_refute refuted a state with a GPU witness (soundness bug)")
+        fallback = int(ns - sat_s.sum() - ref_s.sum())
+        prefilter = {"sample_states": ns, "gpu_sat": int(sat_s.sum()), "refuted": int(ref_s.sum()),
+                     "fallback": fallback, "solver_call_reduction": ns / max(1, fallback),
+                     "refute_states_per_s": ns / dtr, "refute_threads": _threads(),
+                     "note": "synthetic DAGs (random ops), not solidity_examples; reduction = states / states "
+                             "left for z3 after GPU witnesses and host refutations"}
+        log(f"prefilter: {prefilter}")
+
     # ---------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -295,6 +319,7 @@ def main():
             "cpu_baseline": cpu,
             "results": {"sat_states": sat, "planted_states": int(len(pl)), "planted_found": planted_ok},
             "keccak": keccak,
+            "prefilter": prefilter,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

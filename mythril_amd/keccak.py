@@ -14,6 +14,8 @@ method names, constants and constraint shapes):
 The concrete hashes go through the HIP Keccak kernel (libmgp.so,
 mgp_keccak256_batch) — one launch for a whole batch via
 `find_concrete_keccak_batch` — instead of pyethereum's utils.sha3.
+`get_code_hash` / `get_code_hashes` mirror support/support_utils.py:29-41
+(pysha3 keccak_256 of the bytecode) on the same kernel.
 """
 from __future__ import annotations
 
@@ -57,6 +59,30 @@ def keccak256_batch(preimages: Sequence[bytes]) -> List[bytes]:
 
 def keccak256(data: bytes) -> bytes:
     return keccak256_batch([data])[0]
+
+
+def _code_bytes(code: str) -> Optional[bytes]:
+    code = code[2:] if code[:2] == "0x" else code
+    try:
+        return bytes.fromhex(code)
+    except ValueError:
+        return None
+
+
+def get_code_hashes(codes: Sequence[str]) -> List[str]:
+    """get_code_hash over many bytecodes, one GPU launch per distinct length."""
+    raw = [_code_bytes(c) for c in codes]
+    ok = [i for i, r in enumerate(raw) if r is not None]
+    digs = keccak256_batch([raw[i] for i in ok]) if ok else []
+    out = [""] * len(codes)
+    for i, d in zip(ok, digs):
+        out[i] = "0x" + d.hex()
+    return out
+
+
+def get_code_hash(code: str) -> str:
+    """support/support_utils.py:29-41: "0x" + keccak-256 hex of the bytecode, "" if not hex."""
+    return get_code_hashes([code])[0]
 
 
 class KeccakFunctionManager:

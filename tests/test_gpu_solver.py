@@ -12,7 +12,7 @@ import pytest
 
 from mythril_amd import dag as D
 from mythril_amd import solver as SV
-from mythril_amd.keccak import KeccakFunctionManager, keccak256_batch
+from mythril_amd.keccak import KeccakFunctionManager, get_code_hash, get_code_hashes, keccak256_batch
 from mythril_amd.smt import And, Not, symbol_factory
 from oracle import bvsem as S
 from oracle.keccak_ref import keccak256 as keccak_py
@@ -201,3 +201,19 @@ def test_concrete_keccak_batch_matches_reference_impl(mgp_ctx):
     km = KeccakFunctionManager()
     assert km.find_concrete_keccak(BVV(0, 256)).value == int.from_bytes(keccak_py(b"\0" * 32), "big")
     assert km.get_empty_keccak_hash().value == int.from_bytes(keccak_py(b""), "big")
+
+
+def test_code_hash_matches_support_utils_contract(mgp_ctx):
+    # support_utils.py:29-41: optional 0x prefix, "0x" + hex digest, "" when the code is not hex
+    codes = ["0x6080604052", "6080604052", "", "0x", "0xzz", "60" * 300, "0x" + "ff" * 136]
+    want = []
+    for c in codes:
+        h = c[2:] if c[:2] == "0x" else c
+        try:
+            want.append("0x" + keccak_py(bytes.fromhex(h)).hex())
+        except ValueError:
+            want.append("")
+    assert get_code_hashes(codes) == want
+    assert get_code_hash(codes[0]) == want[0] == want[1]
+    # the empty-code hash LASER compares against (keccak_function_manager.py:71-78)
+    assert get_code_hash("") == "0xc5d2460186f7233c927e7db2dcc703c0e500b653ca82273b7bfad8045d85a470"

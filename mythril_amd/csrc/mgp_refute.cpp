@@ -281,6 +281,12 @@ struct State {
   std::vector<int32_t> vtie;   // VAR node -> var table entry
   std::vector<AV> vars;
   std::vector<uint32_t> vkey;  // (index << 9) | width
+  // Compare atoms: ULT(a,b) = NOT ULE(b,a), UGE(a,b) = ULE(b,a), BVSubNoUnderflow(a,b) =
+  // ULE(b,a), ... (signed alike, EQ symmetric).  Nodes with the same atom share one truth
+  // value (or its negation), so `amount <= bal` and `Not(BVSubNoUnderflow(bal, amount))`
+  // contradict each other although neither operand has a useful range.
+  std::vector<int32_t> tie_rep;  // Bool node -> first node of its atom, -1 = none
+  std::vector<uint8_t> tie_neg;  // node = NOT(representative)
   bool changed = false;
 
   uint32_t W(int32_t i) const { return nd[i].width; }
@@ -382,7 +388,61 @@ struct State {
         if (!isb[x.a] || (nop >= 2 && !isb[x.b]) || (nop >= 3 && !isb[x.c])) return false;
       }
     }
-    return n > 0 && isb[n - 1];
+    if (n == 0 || !isb[n - 1]) return false;
+    build_atoms();
+    return true;
+  }
+
+  void build_atoms() {
+    tie_rep.assign(n, -1);
+    tie_neg.assign(n, 0);
+    struct Key {
+      uint8_t k;
+      int32_t x, y;
+      bool operator==(const Key &o) const { return k == o.k && x == o.x && y == o.y; }
+    };
+    std::vector<std::pair<Key, std::pair<int32_t, uint8_t>>> seen;  // atom -> (first node, its polarity)
+    for (uint32_t i = 0; i < n; ++i) {
+      const mgp_node &x = nd[i];
+      if (!(x.op >= MGP_OP_EQ && x.op <= MGP_OP_USUB_NOUDF) || isb[x.a]) continue;
+      Key key{0, x.a, x.b};
+      uint8_t neg = 0;
+      switch (x.op) {
+        case MGP_OP_EQ: key = {MGP_OP_EQ, x.a < x.b ? x.a : x.b, x.a < x.b ? x.b : x.a}; break;
+        case MGP_OP_ULE: key = {MGP_OP_ULE, x.a, x.b}; break;
+        case MGP_OP_ULT: key = {MGP_OP_ULE, x.b, x.a}; neg = 1; break;
+        case MGP_OP_UGT: key = {MGP_OP_ULE, x.a, x.b}; neg = 1; break;
+        case MGP_OP_UGE: case MGP_OP_USUB_NOUDF: key = {MGP_OP_ULE, x.b, x.a}; break;
+        case MGP_OP_SLE: key = {MGP_OP_SLE, x.a, x.b}; break;
+        case MGP_OP_SLT: key = {MGP_OP_SLE, x.b, x.a}; neg = 1; break;
+        case MGP_OP_SGT: key = {MGP_OP_SLE, x.a, x.b}; neg = 1; break;
+        case MGP_OP_SGE: key = {MGP_OP_SLE, x.b, x.a}; break;
+        default: continue;  // overflow predicates: no atom
+      }
+      bool found = false;
+      for (const auto &e : seen)
+        if (e.first == key) {
+          tie_rep[i] = e.second.first;
+          tie_neg[i] = (uint8_t)(neg ^ e.second.second);
+          found = true;
+          break;
+        }
+      if (!found) seen.push_back({key, {(int32_t)i, neg}});
+    }
+  }
+
+  static uint8_t bneg(uint8_t v) { return (uint8_t)(((v & BF) ? BT : 0) | ((v & BT) ? BF : 0)); }
+  bool tie() {
+    for (int sweep = 0; sweep < 2; ++sweep)
+      for (uint32_t i = 0; i < n; ++i) {
+        const int32_t r = tie_rep[i];
+        if (r < 0) continue;
+        const uint8_t mi = tie_neg[i] ? bneg(bs[i]) : bs[i];
+        if (!meetb(r, mi)) return false;
+        const uint8_t mr = tie_neg[i] ? bneg(bs[r]) : bs[r];
+        if (!meetb((int32_t)i, mr)) return false;
+      }
+    return true;
   }
 
   // --------------------------------------------------------------- forward
@@ -839,9 +899,10 @@ struct State {
       changed = false;
       for (uint32_t i = 0; i < n; ++i)
         if (!forward(i)) return 1;
-      if (!meetb((int32_t)n - 1, BT)) return 1;
+      if (!meetb((int32_t)n - 1, BT) || !tie()) return 1;
       for (uint32_t i = n; i-- > 0;)
         if (!backward(i)) return 1;
+      if (!tie()) return 1;
       if (!changed) break;
     }
     return 0;

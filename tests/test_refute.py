@@ -104,6 +104,14 @@ UNSAT_CASES = {
                 [S.EQ, 1, 0, 5, -1, 0, 0], [S.BAND, 1, 4, 6, -1, 0, 0]], [0x1234, 0x13]),
     # literal false
     "false": ([[S.FALSE, 1, -1, -1, -1, 0, 0]], []),
+    # SafeMath.sub after its assert: amount <= bal and Not(BVSubNoUnderflow(bal, amount)), amount = x0 * x1
+    "sub_atoms": ([X0, X1, [S.VAR, 256, -1, -1, -1, 2, 0], [S.MUL, 256, 0, 1, -1, 0, 0], [S.ULE, 1, 3, 2, -1, 0, 0],
+                   [S.USUB_NOUDF, 1, 2, 3, -1, 0, 0], [S.BNOT, 1, 5, -1, -1, 0, 0], [S.BAND, 1, 4, 6, -1, 0, 0]], []),
+    # x0 <s x1 and x0 >=s x1 (no ranges involved)
+    "signed_atoms": _st([[S.SLT, 1, 0, 1, -1, 0, 0], [S.SGE, 1, 0, 1, -1, 0, 0], [S.BAND, 1, 2, 3, -1, 0, 0]], []),
+    # x0 == x1 and Not(x1 == x0)
+    "eq_atoms": _st([[S.EQ, 1, 0, 1, -1, 0, 0], [S.EQ, 1, 1, 0, -1, 0, 0], [S.BNOT, 1, 3, -1, -1, 0, 0],
+                     [S.BAND, 1, 2, 4, -1, 0, 0]], []),
 }
 
 SAT_CASES = {

@@ -281,12 +281,18 @@ struct State {
   std::vector<int32_t> vtie;   // VAR node -> var table entry
   std::vector<AV> vars;
   std::vector<uint32_t> vkey;  // (index << 9) | width
-  // Compare atoms: ULT(a,b) = NOT ULE(b,a), UGE(a,b) = ULE(b,a), BVSubNoUnderflow(a,b) =
-  // ULE(b,a), ... (signed alike, EQ symmetric).  Nodes with the same atom share one truth
-  // value (or its negation), so `amount <= bal` and `Not(BVSubNoUnderflow(bal, amount))`
-  // contradict each other although neither operand has a useful range.
-  std::vector<int32_t> tie_rep;  // Bool node -> first node of its atom, -1 = none
-  std::vector<uint8_t> tie_neg;  // node = NOT(representative)
+  // Orderings of operand pairs: every compare node on the same two operand nodes reads
+  // one set of possible unsigned orderings {<, =, >} and one of signed orderings (the "="
+  // bit is shared).  ULT(a,b), ULE(a,b), UGE(b,a), BVSubNoUnderflow(b,a), the Or(ULT, ==)
+  // expansions and EQ all constrain the same set, so `amount <= bal` and
+  // `Not(BVSubNoUnderflow(bal, amount))` contradict each other although neither operand
+  // has a useful range.
+  enum : uint8_t { OLT = 1, OEQ = 2, OGT = 4, OALL = 7 };
+  struct Pair { int32_t x, y; uint8_t u, s; };
+  std::vector<Pair> pairs;
+  std::vector<int32_t> cmp_pair;  // compare node -> pair index, -1 = none
+  std::vector<uint8_t> cmp_dom;   // 0 unsigned, 1 signed, 2 both (EQ)
+  std::vector<uint8_t> cmp_t;     // orderings (x vs y) under which the node is true
   bool changed = false;
 
   uint32_t W(int32_t i) const { return nd[i].width; }
@@ -394,56 +400,82 @@ struct State {
   }
 
   void build_atoms() {
-    tie_rep.assign(n, -1);
-    tie_neg.assign(n, 0);
-    struct Key {
-      uint8_t k;
-      int32_t x, y;
-      bool operator==(const Key &o) const { return k == o.k && x == o.x && y == o.y; }
-    };
-    std::vector<std::pair<Key, std::pair<int32_t, uint8_t>>> seen;  // atom -> (first node, its polarity)
+    cmp_pair.assign(n, -1);
+    cmp_dom.assign(n, 0);
+    cmp_t.assign(n, 0);
     for (uint32_t i = 0; i < n; ++i) {
       const mgp_node &x = nd[i];
-      if (!(x.op >= MGP_OP_EQ && x.op <= MGP_OP_USUB_NOUDF) || isb[x.a]) continue;
-      Key key{0, x.a, x.b};
-      uint8_t neg = 0;
+      if (!(x.op >= MGP_OP_EQ && x.op <= MGP_OP_USUB_NOUDF) || isb[x.a] || x.a == x.b) continue;
+      uint8_t t, dom = 0;  // truth set for "a op b"
       switch (x.op) {
-        case MGP_OP_EQ: key = {MGP_OP_EQ, x.a < x.b ? x.a : x.b, x.a < x.b ? x.b : x.a}; break;
-        case MGP_OP_ULE: key = {MGP_OP_ULE, x.a, x.b}; break;
-        case MGP_OP_ULT: key = {MGP_OP_ULE, x.b, x.a}; neg = 1; break;
-        case MGP_OP_UGT: key = {MGP_OP_ULE, x.a, x.b}; neg = 1; break;
-        case MGP_OP_UGE: case MGP_OP_USUB_NOUDF: key = {MGP_OP_ULE, x.b, x.a}; break;
-        case MGP_OP_SLE: key = {MGP_OP_SLE, x.a, x.b}; break;
-        case MGP_OP_SLT: key = {MGP_OP_SLE, x.b, x.a}; neg = 1; break;
-        case MGP_OP_SGT: key = {MGP_OP_SLE, x.a, x.b}; neg = 1; break;
-        case MGP_OP_SGE: key = {MGP_OP_SLE, x.b, x.a}; break;
-        default: continue;  // overflow predicates: no atom
+        case MGP_OP_EQ: t = OEQ; dom = 2; break;
+        case MGP_OP_ULT: t = OLT; break;
+        case MGP_OP_ULE: t = OLT | OEQ; break;
+        case MGP_OP_UGT: t = OGT; break;
+        case MGP_OP_UGE: case MGP_OP_USUB_NOUDF: t = OGT | OEQ; break;  // b <= a
+        case MGP_OP_SLT: t = OLT; dom = 1; break;
+        case MGP_OP_SLE: t = OLT | OEQ; dom = 1; break;
+        case MGP_OP_SGT: t = OGT; dom = 1; break;
+        case MGP_OP_SGE: t = OGT | OEQ; dom = 1; break;
+        default: continue;  // overflow predicates: not an ordering
       }
-      bool found = false;
-      for (const auto &e : seen)
-        if (e.first == key) {
-          tie_rep[i] = e.second.first;
-          tie_neg[i] = (uint8_t)(neg ^ e.second.second);
-          found = true;
-          break;
-        }
-      if (!found) seen.push_back({key, {(int32_t)i, neg}});
+      int32_t px = x.a, py = x.b;
+      if (px > py) {  // orient as (smaller node id, larger): mirror < and >
+        px = x.b;
+        py = x.a;
+        t = (uint8_t)((t & OEQ) | ((t & OLT) ? OGT : 0) | ((t & OGT) ? OLT : 0));
+      }
+      int32_t pi = -1;
+      for (size_t k = 0; k < pairs.size(); ++k)
+        if (pairs[k].x == px && pairs[k].y == py) pi = (int32_t)k;
+      if (pi < 0) {
+        pi = (int32_t)pairs.size();
+        pairs.push_back({px, py, OALL, OALL});
+      }
+      cmp_pair[i] = pi;
+      cmp_dom[i] = dom;
+      cmp_t[i] = t;
     }
   }
 
-  static uint8_t bneg(uint8_t v) { return (uint8_t)(((v & BF) ? BT : 0) | ((v & BT) ? BF : 0)); }
+  bool set_order(Pair &p, uint8_t dom, uint8_t m) {
+    uint8_t u = p.u, s = p.s;
+    if (dom != 1) u &= m;
+    if (dom != 0) s &= m;
+    const uint8_t eq = (uint8_t)(u & s & OEQ);  // a == b is one fact in both orders
+    u = (uint8_t)((u & ~OEQ) | eq);
+    s = (uint8_t)((s & ~OEQ) | eq);
+    if (u == OEQ) s = OEQ;
+    if (s == OEQ) u = OEQ;
+    if (!u || !s) return false;
+    if (u != p.u || s != p.s) {
+      p.u = u;
+      p.s = s;
+      changed = true;
+    }
+    return true;
+  }
   bool tie() {
+    if (pairs.empty()) return true;
     for (int sweep = 0; sweep < 2; ++sweep)
       for (uint32_t i = 0; i < n; ++i) {
-        const int32_t r = tie_rep[i];
-        if (r < 0) continue;
-        const uint8_t mi = tie_neg[i] ? bneg(bs[i]) : bs[i];
-        if (!meetb(r, mi)) return false;
-        const uint8_t mr = tie_neg[i] ? bneg(bs[r]) : bs[r];
-        if (!meetb((int32_t)i, mr)) return false;
+        const int32_t pi = cmp_pair[i];
+        if (pi < 0) continue;
+        Pair &p = pairs[pi];
+        const uint8_t t = cmp_t[i], f = (uint8_t)(OALL & ~t);
+        if (bs[i] == BT && !set_order(p, cmp_dom[i], t)) return false;
+        if (bs[i] == BF && !set_order(p, cmp_dom[i], f)) return false;
+        const uint8_t cur = cmp_dom[i] == 1 ? p.s : p.u;
+        if (!meetb((int32_t)i, (uint8_t)(((cur & t) ? BT : 0) | ((cur & f) ? BF : 0)))) return false;
+      }
+    for (const Pair &p : pairs)  // known equal: the operands share one value
+      if (p.u == OEQ) {
+        const AV ax = av[p.x], ay = av[p.y];
+        if (!meet(p.x, ay) || !meet(p.y, ax)) return false;
       }
     return true;
   }
+
 
   // --------------------------------------------------------------- forward
   bool forward(uint32_t i) {

@@ -107,6 +107,20 @@ UNSAT_CASES = {
     # SafeMath.sub after its assert: amount <= bal and Not(BVSubNoUnderflow(bal, amount)), amount = x0 * x1
     "sub_atoms": ([X0, X1, [S.VAR, 256, -1, -1, -1, 2, 0], [S.MUL, 256, 0, 1, -1, 0, 0], [S.ULE, 1, 3, 2, -1, 0, 0],
                    [S.USUB_NOUDF, 1, 2, 3, -1, 0, 0], [S.BNOT, 1, 5, -1, -1, 0, 0], [S.BAND, 1, 4, 6, -1, 0, 0]], []),
+    # the same query as the smt mirror builds it: UGE/ULE as Or(strict, ==) (bitvec_helper.py:53-80)
+    "sub_or_expansion": ([[S.VAR, 256, -1, -1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 0, 0], [S.UGT, 1, 0, 1, -1, 0, 0],
+                          [S.CONST, 256, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 3, -1, 0, 0], [S.EQ, 1, 0, 3, -1, 0, 0],
+                          [S.BOR, 1, 4, 5, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.UGT, 1, 7, 1, -1, 0, 0],
+                          [S.VAR, 256, -1, -1, -1, 2, 0], [S.MUL, 256, 0, 7, -1, 0, 0], [S.UGT, 1, 9, 10, -1, 0, 0],
+                          [S.EQ, 1, 9, 10, -1, 0, 0], [S.BOR, 1, 11, 12, -1, 0, 0], [S.ULT, 1, 10, 9, -1, 0, 0],
+                          [S.EQ, 1, 10, 9, -1, 0, 0], [S.BOR, 1, 14, 15, -1, 0, 0], [S.USUB_NOUDF, 1, 9, 10, -1, 0, 0],
+                          [S.BNOT, 1, 17, -1, -1, 0, 0], [S.BAND, 1, 2, 6, -1, 0, 0], [S.BAND, 1, 19, 8, -1, 0, 0],
+                          [S.BAND, 1, 20, 13, -1, 0, 0], [S.BAND, 1, 21, 16, -1, 0, 0], [S.BAND, 1, 22, 18, -1, 0, 0]],
+                         [0, 20]),
+    # x0 <=u x1 and x1 <=u x0 and x0 == 3 and x1 == 4 (equal by order, different by value)
+    "order_eq": _st([[S.ULE, 1, 0, 1, -1, 0, 0], [S.UGE, 1, 0, 1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 0, 0],
+                     [S.EQ, 1, 0, 4, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0], [S.EQ, 1, 1, 6, -1, 0, 0],
+                     [S.BAND, 1, 2, 3, -1, 0, 0], [S.BAND, 1, 8, 5, -1, 0, 0], [S.BAND, 1, 9, 7, -1, 0, 0]], [3, 4]),
     # x0 <s x1 and x0 >=s x1 (no ranges involved)
     "signed_atoms": _st([[S.SLT, 1, 0, 1, -1, 0, 0], [S.SGE, 1, 0, 1, -1, 0, 0], [S.BAND, 1, 2, 3, -1, 0, 0]], []),
     # x0 == x1 and Not(x1 == x0)

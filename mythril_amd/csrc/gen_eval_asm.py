@@ -540,6 +540,20 @@ bool_binop("BXOR", "s_xor_b64")
 bool_binop("BEQ", "s_xnor_b64")
 
 
+@handler("BAND4")
+def h_band4():
+    # dst = a & b & c & d: a, b in w1 (s17), c, d in w2 (s18); each M0 write's wait state is
+    # filled with the next field extract or AND
+    A("s_and_b32 s48, s17, 0xffff", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s17, 16",
+      "s_movrels_b64 s[50:51], s[64:65]", "s_mov_b32 m0, s49", "s_and_b32 s48, s18, 0xffff",
+      "s_movrels_b64 s[52:53], s[64:65]", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s18, 16",
+      "s_movrels_b64 s[54:55], s[64:65]", "s_mov_b32 m0, s49", "s_and_b64 s[50:51], s[50:51], s[52:53]",
+      "s_movrels_b64 s[52:53], s[64:65]", "s_lshr_b32 s48, s19, 16",
+      "s_and_b64 s[50:51], s[50:51], s[54:55]", "s_mov_b32 m0, s48",
+      "s_and_b64 s[50:51], s[50:51], s[52:53]", "s_movreld_b64 s[64:65], s[50:51]")
+    tail()
+
+
 @handler("BNOT")
 def h_bnot():
     A("s_and_b32 s48, s17, 0xffff", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s19, 16",

@@ -160,6 +160,80 @@ inline int xs_handler(uint32_t op) {
   return -1;
 }
 
+// ---- Bool peepholes on the v1 instruction list (asm engine only; the v1 program is untouched)
+//   * a compare immediately followed by a BNOT of its result: the compare is emitted with
+//     its INVERT flag toggled and the BNOT's destination (one dispatch instead of two);
+//   * chains of adjacent BANDs whose intermediate result has no other reader: one BAND4
+//     (AND of up to four Bool slots).
+inline uint32_t v1_op(const uint32_t *I) { return I[0] & 0xFFu; }
+inline bool v1_writes_bool(const uint32_t *I, uint32_t bit) {
+  const uint32_t op = v1_op(I);
+  const bool boolres = (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) || (op >= MGP_OP_BAND && op <= MGP_OP_BEQ);
+  return boolres && ((I[0] >> 16) & 0xFFu) == bit;
+}
+inline bool v1_reads_bool(const uint32_t *I, uint32_t bit) {
+  const uint32_t op = v1_op(I), oa = I[1] & 0xFFFFu, ob = I[1] >> 16, oc = I[2] & 0xFFFFu;
+  switch (op) {
+    case MGP_OP_BAND: case MGP_OP_BOR: case MGP_OP_BXOR: case MGP_OP_BEQ: return oa == bit || ob == bit;
+    case MGP_OP_BNOT: case MGP_OP_ITE: case MGP_OP_RET: return oa == bit;
+    case MGP_OP_BITE: return oa == bit || ob == bit || oc == bit;
+    default: return false;
+  }
+}
+// is Bool bit `bit` read at or after instruction `from` before being redefined?
+inline bool v1_live_after(const uint32_t *ins, uint32_t n, uint32_t from, uint32_t bit) {
+  if (bit == MGP_BOOL_TRUE || bit == MGP_BOOL_FALSE) return true;
+  for (uint32_t k = from; k < n; ++k) {
+    const uint32_t *I = ins + (size_t)k * MGP_INS_WORDS;
+    if (v1_reads_bool(I, bit)) return true;
+    if (v1_writes_bool(I, bit)) return false;
+  }
+  return false;
+}
+
+struct BoolPlan {
+  std::vector<uint8_t> dead;                  // instruction folded into a neighbour
+  std::vector<uint8_t> inv;                   // compare: toggle INVERT
+  std::vector<uint32_t> dst;                  // compare: destination bit override
+  std::vector<std::vector<uint32_t>> andops;  // BAND: operand bits (2..4)
+};
+
+void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
+  P.dead.assign(n, 0);
+  P.inv.assign(n, 0);
+  P.dst.assign(n, 0xFFFFFFFFu);
+  P.andops.assign(n, {});
+  for (uint32_t pc = 0; pc + 1 < n; ++pc) {
+    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS, *J = I + MGP_INS_WORDS;
+    const uint32_t op = v1_op(I), d = (I[0] >> 16) & 0xFFu;
+    if (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF && v1_op(J) == MGP_OP_BNOT && (J[1] & 0xFFFFu) == d) {
+      const uint32_t e = (J[0] >> 16) & 0xFFu;
+      if (e == d || !v1_live_after(ins, n, pc + 2, d)) {
+        P.inv[pc] = 1;
+        P.dst[pc] = e;
+        P.dead[pc + 1] = 1;
+        ++pc;
+      }
+    }
+  }
+  for (uint32_t pc = 0; pc < n; ++pc) {
+    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
+    if (!P.dead[pc] && v1_op(I) == MGP_OP_BAND) P.andops[pc] = {I[1] & 0xFFFFu, I[1] >> 16};
+  }
+  for (uint32_t pc = 0; pc + 1 < n; ++pc) {
+    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS, *J = I + MGP_INS_WORDS;
+    if (P.dead[pc] || P.dead[pc + 1] || v1_op(I) != MGP_OP_BAND || v1_op(J) != MGP_OP_BAND) continue;
+    const uint32_t t = (I[0] >> 16) & 0xFFu, ja = J[1] & 0xFFFFu, jb = J[1] >> 16;
+    if ((ja == t) == (jb == t)) continue;  // J must read t exactly once
+    const bool j_redefines_t = ((J[0] >> 16) & 0xFFu) == t;
+    if (P.andops[pc].size() + 1 > 4 || (!j_redefines_t && v1_live_after(ins, n, pc + 2, t))) continue;
+    std::vector<uint32_t> ops = P.andops[pc];
+    ops.push_back(ja == t ? jb : ja);
+    P.andops[pc + 1] = ops;
+    P.dead[pc] = 1;
+  }
+}
+
 inline uint32_t w0_of(uint32_t first, uint32_t op) {
   return (uint32_t)kUopHandlerOffset[first] | ((uint32_t)kUopHandlerOffset[op] << 16);
 }
@@ -183,10 +257,14 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     uops.push_back(w0); uops.push_back(w1); uops.push_back(w2); uops.push_back(w3);
   };
 
+  BoolPlan BP;
+  if (v1_ok) plan_bools(ins, T.n_ins, BP);
   auto translate = [&]() {
     for (uint32_t pc = 0; v1_ok && pc < T.n_ins && !T.bad; ++pc) {
+      if (BP.dead[pc]) continue;
       const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
-      const uint32_t op = I[0] & 0xFFu, width = ((I[0] >> 8) & 0xFFu) + 1u, dst = (I[0] >> 16) & 0xFFu;
+      const uint32_t op = I[0] & 0xFFu, width = ((I[0] >> 8) & 0xFFu) + 1u;
+      const uint32_t dst = BP.dst[pc] != 0xFFFFFFFFu ? BP.dst[pc] : (I[0] >> 16) & 0xFFu;
       const bool store = ((I[0] >> 24) & MGP_INS_STORE) != 0;
       const uint32_t oa = I[1] & 0xFFFFu, ob = I[1] >> 16, oc = I[2] & 0xFFFFu, imm = I[2] >> 16;
       const bool narrow = width < 256u;
@@ -194,6 +272,13 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       if (op == MGP_OP_RET) {
         emit(w0_of(MGP_U_RET, MGP_U_RET), T.boolslot(oa), 0, 0);
         break;
+      }
+      if (op == MGP_OP_BAND && BP.andops[pc].size() > 2) {
+        const std::vector<uint32_t> &q = BP.andops[pc];
+        const uint32_t c = T.boolslot(q[2]), d = q.size() > 3 ? T.boolslot(q[3]) : T.boolslot(MGP_BOOL_TRUE);
+        emit(w0_of(MGP_U_BAND4, MGP_U_BAND4), T.boolslot(q[0]) | (T.boolslot(q[1]) << 16), c | (d << 16),
+             T.boolslot(dst) << 16);
+        continue;
       }
       if (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) {
         static const uint32_t ids[] = {MGP_U_BAND, MGP_U_BOR, MGP_U_BXOR, MGP_U_BNOT, MGP_U_BITE, MGP_U_BEQ};
@@ -227,6 +312,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           else if (base == MGP_U_SLT_RA) base = MGP_U_SGT_RA;
           else if (base == MGP_U_SGT_RA) base = MGP_U_SLT_RA;
         }
+        if (BP.inv[pc]) inv = !inv;  // a folded BNOT of this compare's result
         uint32_t flags = inv ? MGP_UF_INVERT : 0u, w2 = 0, w3 = T.boolslot(dst) << 16;
         if (narrow && (base == MGP_U_SLT_RA || base == MGP_U_SGT_RA)) {
           flags |= MGP_UF_SEXT;

@@ -30,7 +30,7 @@ uop words:
             register slot),
             CONST: pool index; Bool operands: bool slot * 2
   w2 [15:0] store slot byte offset, or 8 x bank position with REGST /
-            third Bool operand * 2
+            third Bool operand * 2;  BAND4: [31:16] fourth Bool operand * 2
      [21:16] mask pool index
      [22] STORE   result -> LDS slot
      [23] MASK    result &= pool[mask] (2^w - 1); compares: M for the overflow tests
@@ -59,7 +59,7 @@ B_KINDS = ("none",) + KINDS
 FETCH = [f"F_{ka}_{kb}_A" for ka in KINDS for kb in B_KINDS] + \
         [f"F_{ka}_{kb}_C" for ka in KINDS[1:] for kb in B_KINDS]
 
-BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ"]
+BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ", "BAND4"]
 BV_BIN = ["ADD", "SUB", "MUL", "AND", "OR", "XOR", "SHL", "LSHR", "ASHR", "DIV"]
 BV_UN = ["NOT", "NEG", "MOV", "SEXT"]
 SHIFT_I = [f"SHLI{k}" for k in range(9)] + [f"LSHRI{k}" for k in range(9)] + [f"ASHRI{k}" for k in range(9)]

@@ -144,6 +144,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
             a, b, c = bools[pa >> 1], bools[pb >> 1], bools[(w2 & 0xFFFF) >> 1]
             if op == "RET":
                 return a
+            if op == "BAND4":  # AND of four Bool slots (w1 lo/hi, w2 lo/hi)
+                bools[w3 >> 17] = a and b and c and bools[(w2 >> 16) >> 1]
+                continue
             r = {"BAND": a and b, "BOR": a or b, "BXOR": a != b, "BNOT": not a,
                  "BITE": b if a else c, "BEQ": a == b}[op]
             bools[w3 >> 17] = r

@@ -68,6 +68,7 @@ class SolverStatistics(metaclass=_Singleton):
         self.gpu_sat = 0          # states proven SAT by a GPU witness
         self.gpu_undecided = 0
         self.refuted = 0          # states proven UNSAT by the host pre-check (mgp_refute)
+        self.core_hits = 0        # states UNSAT because they contain a known UNSAT core
         self.gpu_time = 0.0
         self.gpu_batches = 0
 
@@ -150,6 +151,66 @@ def get_backend() -> Backend:
     return _backend
 
 
+# ------------------------------------------------------------ UNSAT cores
+class UnsatCores:
+    """Constraint sets known to be UNSAT (refuted by mgp_refute, or unsat from the fallback).
+
+    A conjunction only gets stronger as constraints are added (a child's Constraints
+    extends its parent's, constraints.py:67-85), so a state whose constraint set contains
+    a stored set is UNSAT with no analysis at all ("prefix/core
+    cache").  Refuted sets are first shrunk to a core (`shrink`), which then also covers
+    other paths that repeat the same contradiction.  Terms are hash-consed, so set
+    membership is identity of the interned constraint terms.
+    """
+
+    def __init__(self, max_sets: int = 1 << 14):
+        self.max_sets = max_sets
+        self.reset()
+
+    def reset(self) -> None:
+        self.sets: List[frozenset] = []
+        self.index: Dict[Term, List[int]] = {}  # every stored set under ONE of its members
+
+    def covered(self, terms: Iterable[Term]) -> bool:
+        s = set(terms)
+        for t in s:
+            for k in self.index.get(t, ()):
+                if self.sets[k] <= s:
+                    return True
+        return False
+
+    def add(self, core: Iterable[Term]) -> None:
+        fs = frozenset(core)
+        if not fs or len(self.sets) >= self.max_sets or self.covered(fs):
+            return
+        self.sets.append(fs)
+        anchor = min(fs, key=lambda t: len(self.index.get(t, ())))
+        self.index.setdefault(anchor, []).append(len(self.sets) - 1)
+
+    @staticmethod
+    def shrink(N, terms: Sequence[Term], max_terms: int = 32) -> List[Term]:
+        """Deletion-based core of a refuted constraint list: one batched mgp_refute call
+        tries every single-constraint deletion; the constraints whose deletion breaks the
+        refutation form the core if the refuter still refutes them alone."""
+        terms = list(dict.fromkeys(terms))
+        if len(terms) < 2 or len(terms) > max_terms:
+            return terms
+        trials = [terms[:i] + terms[i + 1:] for i in range(len(terms))]
+        dags = [D.build_state(t) for t in trials]
+        v = N.refute(*D.pack_states(dags))
+        need = [terms[i] for i in range(len(terms)) if v[i] != 1]
+        if need and len(need) < len(terms) and N.refute(*D.pack_states([D.build_state(need)]))[0] == 1:
+            return need
+        return terms
+
+
+_cores = UnsatCores()
+
+
+def unsat_cores() -> UnsatCores:
+    return _cores
+
+
 # ------------------------------------------------------------- GPU stage
 class Prefilter:
     """Batched GPU witness search over states (one libmgp context)."""
@@ -176,6 +237,14 @@ class Prefilter:
             return []
         stats = SolverStatistics()
         t0 = time.time()
+        # states that contain a known UNSAT core need no analysis
+        hit = [self.refute and _cores.covered(s) for s in states]
+        if any(hit):
+            stats.core_hits += sum(hit)
+            rest = [s for s, h in zip(states, hit) if not h]
+            rest_par = None if parents is None else [p for p, h in zip(parents, hit) if not h]
+            sub = iter(self.check_states(rest, rest_par) if rest else [])
+            return [(unsat, None) if h else next(sub) for h in hit]
         dags = [D.build_state(s) for s in states]
         n_vars = max(1, max(d.n_vars for d in dags))
         nodes, noff, consts, coff = D.pack_states(dags)
@@ -192,6 +261,7 @@ class Prefilter:
                 out.append((sat, D.witness_to_model(d, wit[i])))
             elif proven[i] == 1:
                 out.append((unsat, None))
+                _cores.add(UnsatCores.shrink(self._N, states[i]))
             else:
                 out.append(("undecided", None))
         stats.gpu_batches += 1
@@ -275,6 +345,8 @@ class Solver(BaseSolver):
     def _fallback(self) -> str:
         r, m = get_backend().check(self.constraints, self.timeout)
         self._model = m
+        if r == unsat:
+            _cores.add(self.constraints)
         return r
 
     def reset(self) -> None:
@@ -312,6 +384,8 @@ class Optimize(BaseSolver):
     def _fallback(self) -> str:
         r, m = get_backend().check(self.constraints, self.timeout, tuple(self._min), tuple(self._max))
         self._model = m
+        if r == unsat:
+            _cores.add(self.constraints)
         return r
 
 

@@ -86,6 +86,20 @@ __global__ __launch_bounds__(256) void mix_kernel(uint32_t iters, uint32_t *sink
             "v_alignbit_b32 %4, %4, %8, 7\n\tv_bitop3_b32 %5, %5, %8, %9 bitop3:0x96\n\t"
             "v_alignbit_b32 %6, %6, %8, 7\n\tv_bitop3_b32 %7, %7, %8, %9 bitop3:0x96"
             : CHAINS : "v"(b), "v"(c));
+      if constexpr (MODE == 12)  // four alignbit, then four bitop3: fewer slow/fast transitions
+        asm volatile(
+            "v_alignbit_b32 %0, %0, %8, 7\n\tv_alignbit_b32 %2, %2, %8, 7\n\t"
+            "v_alignbit_b32 %4, %4, %8, 7\n\tv_alignbit_b32 %6, %6, %8, 7\n\t"
+            "v_bitop3_b32 %1, %1, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %3, %3, %8, %9 bitop3:0x96\n\t"
+            "v_bitop3_b32 %5, %5, %8, %9 bitop3:0x96\n\tv_bitop3_b32 %7, %7, %8, %9 bitop3:0x96"
+            : CHAINS : "v"(b), "v"(c));
+      if constexpr (MODE == 13)  // keccak-like ratio: 1 alignbit per 2 full-rate ops
+        asm volatile(
+            "v_alignbit_b32 %0, %0, %8, 7\n\tv_bitop3_b32 %1, %1, %8, %9 bitop3:0x96\n\t"
+            "v_xor_b32 %2, %2, %8\n\tv_alignbit_b32 %3, %3, %8, 7\n\t"
+            "v_bitop3_b32 %4, %4, %8, %9 bitop3:0x96\n\tv_xor_b32 %5, %5, %8\n\t"
+            "v_bitop3_b32 %6, %6, %8, %9 bitop3:0x96\n\tv_xor_b32 %7, %7, %8"
+            : CHAINS : "v"(b), "v"(c));
       if constexpr (MODE == 11)
         asm volatile(
             "v_lshl_add_u32 %0, %0, 7, %8\n\tv_lshl_add_u32 %1, %1, 7, %8\n\tv_lshl_add_u32 %2, %2, 7, %8\n\t"
@@ -150,6 +164,8 @@ int main() {
   run<9>("v_perm_b32", sink, clk);
   run<10>("alignbit/bitop3 alternating", sink, clk);
   run<11>("v_lshl_add_u32", sink, clk);
+  run<12>("4 alignbit then 4 bitop3", sink, clk);
+  run<13>("alignbit : full-rate = 1 : 3", sink, clk);
   hipFree(sink);
   hipFree(clk);
   return 0;

@@ -44,6 +44,7 @@ def backend(mgp_ctx):
     b = CountingBackend()
     old = SV.set_backend(b)
     SV.SolverStatistics().reset()
+    SV.unsat_cores().reset()
     SV.get_model.cache_clear()
     SV.enable_gpu(True)
     yield b

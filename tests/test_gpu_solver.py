@@ -39,6 +39,7 @@ def backend(mgp_ctx):
     b = CountingBackend()
     old = SV.set_backend(b)
     SV.SolverStatistics().reset()
+    SV.unsat_cores().reset()
     SV.enable_gpu(True)
     yield b
     SV.set_backend(old)

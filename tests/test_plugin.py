@@ -122,6 +122,7 @@ def brute(monkeypatch):
     b = BruteBackend()
     old = SV.set_backend(b)
     SV.SolverStatistics().reset()
+    SV.unsat_cores().reset()
     yield b
     SV.set_backend(old)
 
@@ -178,5 +179,5 @@ def test_plugin_prunes_like_reference_gpu(brute, mgp_ctx, window):
     # the host pre-check or reach the fallback
     n_infeasible = sum(2 - len(states) for op, states in ref_vm.cfg if op == "JUMPI")
     st = SV.SolverStatistics()
-    assert brute.calls + st.refuted == n_infeasible < ref_calls
+    assert brute.calls + st.refuted + st.core_hits == n_infeasible < ref_calls
     assert st.gpu_sat > 0

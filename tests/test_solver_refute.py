@@ -50,6 +50,7 @@ def fe(monkeypatch):
     b = CountingBackend()
     old = SV.set_backend(b)
     SV.SolverStatistics().reset()
+    SV.unsat_cores().reset()
     SV.get_model.cache_clear()
     yield b
     SV.set_backend(old)
@@ -95,3 +96,33 @@ def test_refute_off_restores_reference_path(fe):
     items = [SV.Constraints([x == BVV(1, 256), x == BVV(2, 256)])]
     assert SV.batch_is_possible(items) == [True]  # unknown -> possible, via the fallback
     assert fe.calls == 1 and SV.SolverStatistics().refuted == 0
+
+
+def test_unsat_core_cache(fe):
+    x, y, z, w = (BVS(n, 256) for n in ("cx", "cy", "cz", "cw"))
+    a = [x == BVV(1, 256), ULT(y, BVV(5, 256)), x == BVV(2, 256), UGT(z, BVV(3, 256))]
+    assert SV.batch_is_possible([SV.Constraints(a)]) == [False]
+    st = SV.SolverStatistics()
+    assert st.refuted == 1 and st.core_hits == 0
+    # the stored core is the contradiction alone, not the whole path
+    assert SV.unsat_cores().sets == [frozenset({a[0].raw, a[2].raw})]
+    # another path repeating the contradiction: UNSAT from the cache, no analysis, no fallback
+    b = [w == BVV(7, 256), x == BVV(2, 256), UGT(z, BVV(9, 256)), x == BVV(1, 256)]
+    assert SV.batch_is_possible([SV.Constraints(b), SV.Constraints(b[:3])]) == [False, True]
+    assert st.refuted == 1 and st.core_hits == 1 and fe.calls == 1
+
+
+def test_fallback_unsat_feeds_the_cache(fe):
+    class UnsatBackend(SV.Backend):
+        calls = 0
+
+        def check(self, terms, timeout_ms, minimize=(), maximize=()):
+            UnsatBackend.calls += 1
+            return SV.unsat, None
+
+    SV.set_backend(UnsatBackend())
+    x = BVS("fx", 256)
+    base = [x * x == BVV(5, 256)]  # UNSAT for the solver, not for the pre-check
+    assert SV.batch_is_possible([SV.Constraints(base)]) == [False]
+    assert SV.batch_is_possible([SV.Constraints(base + [ULT(x, BVV(100, 256))])]) == [False]
+    assert UnsatBackend.calls == 1 and SV.SolverStatistics().core_hits == 1

@@ -601,6 +601,8 @@ def make_xr(name):
     the indexed SRC1 of the limb ops themselves (GPR-index mode), so the uop needs no
     fetch handler, no moves and no operand wait (vA and the bank are both resident)."""
     base = name[3:]
+    if base in ("EQ_RA", "ULT_RA", "UGT_RA"):
+        return make_xr_cmp(base[:-3])
     op, mode = (base.split("_", 1) + [""])[:2]
     first, rest = BIN_LIMBS[op]
 
@@ -616,6 +618,30 @@ def make_xr(name):
             bv_epilogue()
         finally:
             EPI_MODE[0] = None
+    return body
+
+
+def make_xr_cmp(base):
+    """XR_<cmp>_RA: Bool = vA cmp bank[B], B read in GPR-index mode as SRC1 (EQ, ULT) or,
+    for UGT (computed as B < vA), as SRC0 of the borrow chain."""
+    def body():
+        A("s_lshr_b32 s50, s17, 16")
+        if base == "EQ":
+            A("s_set_gpr_idx_on s50, gpr_idx(SRC1)")
+            for i in range(8):
+                A(f"v_xor_b32 {v(VT + i)}, {v(VA + i)}, {v(RV + i)}")
+            A("s_set_gpr_idx_off")
+            or_reduce(VT, range(VT, VT + 8))
+            A(f"v_cmp_eq_u32 vcc, 0, {v(VT)}")
+        elif base == "ULT":
+            A("s_set_gpr_idx_on s50, gpr_idx(SRC1)")
+            ult_chain(VA, RV)
+            A("s_set_gpr_idx_off")
+        else:
+            A("s_set_gpr_idx_on s50, gpr_idx(SRC0)")
+            ult_chain(RV, VA)
+            A("s_set_gpr_idx_off")
+        cmp_epilogue()
     return body
 
 

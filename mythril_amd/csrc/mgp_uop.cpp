@@ -328,6 +328,9 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       if (ra && b.kind == KSLOT) {
         const int xs = xs_handler(opid);
         if (xs >= 0) opid = first = (uint32_t)xs;
+      } else if (ra && b.kind == KRVAR && !(flags & (MGP_UF_SEXT | MGP_UF_MASK))) {
+        const int xr = xr_handler(opid);  // EQ / ULT / UGT against a register-bank operand
+        if (xr >= 0) opid = first = (uint32_t)xr;
       }
         emit(w0_of(first, opid), (ra ? 0u : a.param) | (b.param << 16), w2 | flags, w3);
         continue;

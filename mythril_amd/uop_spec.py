@@ -74,7 +74,8 @@ EPI_VARIANTS = [f"{o}_{v}" for o in EPI_OPS for v in ("S", "M", "MS", "R", "MR")
 
 # fused handlers "vA = vA op bank[B]" (F_acc_rvar_A + op in one handler: B is read in
 # GPR-index mode straight from the register bank, no moves, no second dispatch)
-XR_BASE = [f"{o}{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR") for v in ("", "_S", "_R")]
+XR_BASE = [f"{o}{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR") for v in ("", "_S", "_R")] + \
+          ["EQ_RA", "ULT_RA", "UGT_RA"]   # compares "vA cmp bank[B]" (Bool result)
 XR_OPS = [f"XR_{o}" for o in XR_BASE]
 
 # fused handlers "vA = vA op lds[B]" (F_acc_slot_A + op in one handler: the B slot read

@@ -69,6 +69,7 @@ class SolverStatistics(metaclass=_Singleton):
         self.gpu_undecided = 0
         self.refuted = 0          # states proven UNSAT by the host pre-check (mgp_refute)
         self.core_hits = 0        # states UNSAT because they contain a known UNSAT core
+        self.gpu_retry = 0        # states given a second, larger candidate round
         self.gpu_time = 0.0
         self.gpu_batches = 0
 
@@ -224,6 +225,9 @@ class Prefilter:
         self.seed = seed
         self._calls = 0
         self.refute = True  # host UNSAT pre-check (mgp_refute) on every GPU miss
+        # second witness round for the states the first round and the pre-check left open:
+        # fresh candidates, up to retry_cand per state (host candidate memory capped at 1 GiB)
+        self.retry_cand = 1024
 
     def check_states(self, states: Sequence[Sequence[Term]],
                      parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> List[Tuple[str, Optional[Dict[str, int]]]]:
@@ -253,6 +257,19 @@ class Prefilter:
         cands = D.make_candidates(dags, self.n_cand, n_vars, seed=self.seed + self._calls, parents=parents)
         first, wit = self.ctx.eval_batch(words, po, cands)
         proven = self._N.refute(nodes, noff, consts, coff) if self.refute else np.zeros(len(dags), np.int8)
+        retry = [i for i in range(len(dags)) if first[i] == -1 and proven[i] != 1]
+        if retry and self.retry_cand > self.n_cand:
+            budget = (1 << 30) // (len(retry) * n_vars * 32)
+            n2 = min(self.retry_cand, budget) // 64 * 64
+            if n2 > self.n_cand:
+                sub = [dags[i] for i in retry]
+                sw, sp, _ = self._N.lower(*D.pack_states(sub))
+                c2 = D.make_candidates(sub, n2, n_vars, seed=self.seed + 0x9E3779B9 + self._calls)
+                f2, w2 = self.ctx.eval_batch(sw, sp, c2)
+                for k, i in enumerate(retry):
+                    if f2[k] >= 0:
+                        first[i], wit[i] = f2[k], w2[k]
+                stats.gpu_retry += len(retry)
         out: List[Tuple[str, Optional[Dict[str, int]]]] = []
         for i, d in enumerate(dags):
             if first[i] >= 0:

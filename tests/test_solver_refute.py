@@ -126,3 +126,24 @@ def test_fallback_unsat_feeds_the_cache(fe):
     assert SV.batch_is_possible([SV.Constraints(base)]) == [False]
     assert SV.batch_is_possible([SV.Constraints(base + [ULT(x, BVV(100, 256))])]) == [False]
     assert UnsatBackend.calls == 1 and SV.SolverStatistics().core_hits == 1
+
+
+class SecondRoundContext(NoWitnessContext):
+    """No witness among the first round's candidates; candidate 0 of a larger round 'satisfies'."""
+
+    def eval_batch(self, words, po, cands):
+        if cands.shape[1] <= 256:
+            return super().eval_batch(words, po, cands)
+        self.batches += 1
+        return np.zeros(len(po) - 1, dtype=np.int32), np.ascontiguousarray(cands[:, 0])
+
+
+def test_second_candidate_round(fe, monkeypatch):
+    monkeypatch.setattr(N, "Context", SecondRoundContext)
+    x, y = BVS("rx", 256), BVS("ry", 256)
+    items = [SV.Constraints([ULT(x, y)]), SV.Constraints([x == BVV(1, 256), x == BVV(2, 256)])]
+    assert SV.batch_is_possible(items) == [True, False]
+    st = SV.SolverStatistics()
+    assert st.gpu_retry == 1 and st.gpu_sat == 1 and st.refuted == 1 and fe.calls == 0
+    assert SV.prefilter().ctx.batches == 2
+    assert set(items[0].witness) == {"rx", "ry"}

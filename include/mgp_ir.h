@@ -23,6 +23,18 @@
 #include <stdint.h>
 
 #define MGP_MAX_WIDTH 256   /* widest bit-vector a kernel slot holds        */
+#define MGP_MAX_WIDE 2048   /* widest DAG value (split into <= 256-bit pieces) */
+
+/* Wide values (MGP_MAX_WIDTH < width <= MGP_MAX_WIDE): the reference builds
+ * 512-bit mapping preimages Concat(key, slot) for keccak256_512 and its
+ * inverse (keccak_function_manager.py:56-69,122-146), 257-bit overflow sums
+ * and 776-bit calldata hashes.  In a DAG they are held as ceil(width/256)
+ * consecutive entries, low 256 bits first:
+ *   VAR    variables p0, p0+1, ...        CONST  pool entries p0, p0+1, ...
+ *   UFAPP / UFINV with a wide result: fresh variables p1, p1+1, ...
+ * Only CONCAT, EXTRACT, ZEXT, ITE, EQ and UF arguments/results may touch a
+ * wide value; the lowering splits it into pieces and emits narrow code only
+ * (any other op on a wide value makes the state MGP_ST_UNSUPPORTED). */
 #define MGP_LIMBS 8         /* 8 x u32 little-endian limbs per 256-bit value */
 
 /* ---------------------------------------------------------------- opcodes */
@@ -140,7 +152,7 @@ typedef struct mgp_node {
 
 /* per-state status (header w3 and lowering status output) */
 #define MGP_ST_OK 0
-#define MGP_ST_UNSUPPORTED 1   /* width > 256, too many live values, unknown op */
+#define MGP_ST_UNSUPPORTED 1   /* arithmetic on a wide value, too many live values, unknown op */
 
 /* first-SAT sentinels */
 #define MGP_NO_SAT (-1)

@@ -1,8 +1,9 @@
 // mgp_lower.cpp — constraint DAG -> flat bytecode (host side).
 //
 // Per state:
-//   1. validate the topologically ordered node list (widths <= 256, operand
-//      indices point backwards, root is Bool);
+//   1. validate the topologically ordered node list (operand indices point
+//      backwards, root is Bool); values wider than 256 bits are split into
+//      <= 256-bit pieces that only structural ops touch (mgp_ir.h);
 //   2. expand uninterpreted-function applications (keccak256_<n> and its
 //      inverse, keccak_function_manager.py:56-69, and base-array Selects) into
 //      EQ/ITE chains: Ackermann expansion with a lazily built interpretation
@@ -107,8 +108,18 @@ struct LowerState {
   }
 };
 
+// A value wider than one 256-bit slot (512-bit mapping preimages
+// Concat(key, slot), keccak256_512 / its inverse, 257-bit overflow sums) is a
+// list of <= 256-bit pieces, low bits first.  Only the structural ops act on
+// such lists (mgp_ir.h, "wide values"); every piece is an ordinary narrow value.
+struct Piece {
+  Ref r;
+  uint32_t w;
+};
+typedef std::vector<Piece> Pieces;
+
 struct UFApp {
-  Ref arg, val;
+  Pieces arg, val;
 };
 
 Lowered unsupported() {
@@ -125,17 +136,167 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   std::vector<Ref> val(n_nodes);
   std::vector<uint16_t> wid(n_nodes);
   std::vector<uint8_t> isb(n_nodes);
+  std::vector<Pieces> wide(n_nodes);  // non-empty iff wid > MGP_MAX_WIDTH
   std::unordered_map<uint32_t, std::vector<UFApp>> fapps, iapps;
+
+  // ------------------------------------------------ wide-value helpers
+  auto pieces_of = [&](int32_t j) -> Pieces {
+    if (wid[j] > MGP_MAX_WIDTH) return wide[j];
+    return Pieces{Piece{val[j], wid[j]}};
+  };
+  // bits [lo, lo + n) of a piece list, as a piece list
+  auto slice = [&](const Pieces &p, uint32_t lo, uint32_t n) -> Pieces {
+    Pieces out;
+    uint32_t off = 0;
+    for (const Piece &q : p) {
+      const uint32_t a = std::max(lo, off), b = std::min(lo + n, off + q.w);
+      if (a < b) {
+        if (a == off && b - a == q.w) out.push_back(q);
+        else out.push_back(Piece{S.add(MGP_OP_EXTRACT, (uint16_t)(b - a), false, q.r, Ref(), Ref(), a - off), b - a});
+      }
+      off += q.w;
+    }
+    return out;
+  };
+  // cut two equal-width piece lists at the union of their boundaries
+  auto align = [&](const Pieces &p, const Pieces &q, Pieces &pa, Pieces &qa) {
+    std::vector<uint32_t> cuts;
+    uint32_t o = 0;
+    for (const Piece &x : p) cuts.push_back(o += x.w);
+    o = 0;
+    for (const Piece &x : q) cuts.push_back(o += x.w);
+    std::sort(cuts.begin(), cuts.end());
+    cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    uint32_t lo = 0;
+    for (uint32_t c : cuts) {
+      Pieces a = slice(p, lo, c - lo), b = slice(q, lo, c - lo);
+      pa.push_back(a[0]);
+      qa.push_back(b[0]);
+      lo = c;
+    }
+  };
+  auto eq_pieces = [&](const Pieces &p, const Pieces &q) -> Ref {
+    if (p.size() == 1 && q.size() == 1) return S.add(MGP_OP_EQ, (uint16_t)p[0].w, true, p[0].r, q[0].r);
+    Pieces pa, qa;
+    align(p, q, pa, qa);
+    Ref e;
+    for (size_t k = 0; k < pa.size(); ++k) {
+      Ref ek = S.add(MGP_OP_EQ, (uint16_t)pa[k].w, true, pa[k].r, qa[k].r);
+      e = (k == 0) ? ek : S.add(MGP_OP_BAND, 1, true, e, ek);
+    }
+    return e;
+  };
+  auto ite_pieces = [&](Ref c, const Pieces &p, const Pieces &q) -> Pieces {
+    if (p.size() == 1 && q.size() == 1) return Pieces{Piece{S.add(MGP_OP_ITE, (uint16_t)p[0].w, false, c, p[0].r, q[0].r), p[0].w}};
+    Pieces pa, qa, out;
+    align(p, q, pa, qa);
+    for (size_t k = 0; k < pa.size(); ++k)
+      out.push_back(Piece{S.add(MGP_OP_ITE, (uint16_t)pa[k].w, false, c, pa[k].r, qa[k].r), pa[k].w});
+    return out;
+  };
+  // concatenation of narrow pieces (total <= 256) into one value
+  auto join = [&](const Pieces &p) -> Ref {
+    Ref r = p[0].r;
+    uint32_t w = p[0].w;
+    for (size_t k = 1; k < p.size(); ++k) {
+      r = S.add(MGP_OP_CONCAT, (uint16_t)(w + p[k].w), false, p[k].r, r, Ref(), w);
+      w += p[k].w;
+    }
+    return r;
+  };
+  // a w-bit value held in consecutive variables first, first+1, ... (low first)
+  auto var_pieces = [&](uint32_t first, uint32_t w) -> Pieces {
+    Pieces out;
+    for (uint32_t off = 0, k = 0; off < w; off += MGP_MAX_WIDTH, ++k) {
+      const uint32_t pw = std::min<uint32_t>(MGP_MAX_WIDTH, w - off);
+      Ref v;
+      v.k = R_VAR;
+      v.idx = first + k;
+      out.push_back(Piece{pw < 256u ? S.add(MGP_OP_MOV, (uint16_t)pw, false, v) : v, pw});
+    }
+    S.max_var = std::max(S.max_var, first + (w + MGP_MAX_WIDTH - 1) / MGP_MAX_WIDTH);
+    return out;
+  };
+  auto wid_of = [](const Pieces &p) -> uint32_t {
+    uint32_t w = 0;
+    for (const Piece &q : p) w += q.w;
+    return w;
+  };
+  auto set_val = [&](uint64_t i, const Pieces &p) {
+    if (wid[i] > MGP_MAX_WIDTH) wide[i] = p;
+    else val[i] = p.size() == 1 ? p[0].r : join(p);
+  };
 
   for (uint64_t i = 0; i < n_nodes; ++i) {
     const mgp_node &nd = nodes[i];
     const uint8_t op = nd.op;
     const bool rb = op_is_bool_result(op);
     uint32_t w = rb ? 1u : nd.width;
-    if (!rb && (w == 0 || w > MGP_MAX_WIDTH)) return unsupported();
+    if (!rb && (w == 0 || w > MGP_MAX_WIDE)) return unsupported();
     auto opnd = [&](int32_t j) -> bool { return j >= 0 && (uint64_t)j < i; };
+    auto is_wide = [&](int32_t j) -> bool { return opnd(j) && wid[j] > MGP_MAX_WIDTH; };
     wid[i] = (uint16_t)w;
     isb[i] = rb;
+    if (!rb && w > MGP_MAX_WIDTH) {
+      // ---------------------------------------- wide results: structural ops only
+      const uint32_t k = (w + MGP_MAX_WIDTH - 1) / MGP_MAX_WIDTH;
+      switch (op) {
+        case MGP_OP_VAR:
+          if (nd.p0 + k > 0x3FFFu) return unsupported();
+          wide[i] = var_pieces(nd.p0, w);
+          break;
+        case MGP_OP_CONST: {
+          if ((uint64_t)nd.p0 + k > n_consts) return unsupported();
+          for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t pw = std::min<uint32_t>(MGP_MAX_WIDTH, w - j * MGP_MAX_WIDTH);
+            wide[i].push_back(Piece{S.constant(consts + (size_t)(nd.p0 + j) * 8u, pw), pw});
+          }
+          break;
+        }
+        case MGP_OP_CONCAT: {
+          if (!opnd(nd.a) || !opnd(nd.b) || isb[nd.a] || isb[nd.b]) return unsupported();
+          if ((uint32_t)wid[nd.a] + wid[nd.b] != w) return unsupported();
+          wide[i] = pieces_of(nd.b);
+          for (const Piece &q : pieces_of(nd.a)) wide[i].push_back(q);
+          break;
+        }
+        case MGP_OP_EXTRACT: {
+          if (!opnd(nd.a) || isb[nd.a] || nd.p0 < nd.p1 || nd.p0 >= wid[nd.a] || nd.p0 - nd.p1 + 1 != w)
+            return unsupported();
+          wide[i] = slice(pieces_of(nd.a), nd.p1, w);
+          break;
+        }
+        case MGP_OP_ZEXT: {
+          if (!opnd(nd.a) || isb[nd.a] || wid[nd.a] > w) return unsupported();
+          wide[i] = pieces_of(nd.a);
+          static const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          for (uint32_t off = wid[nd.a]; off < w;) {
+            const uint32_t pw = std::min<uint32_t>(MGP_MAX_WIDTH, w - off);
+            wide[i].push_back(Piece{S.constant(zero, pw), pw});
+            off += pw;
+          }
+          break;
+        }
+        case MGP_OP_ITE: {
+          if (!opnd(nd.a) || !opnd(nd.b) || !opnd(nd.c) || !isb[nd.a] || isb[nd.b] || isb[nd.c]) return unsupported();
+          if (wid[nd.b] != w || wid[nd.c] != w) return unsupported();
+          wide[i] = ite_pieces(val[nd.a], pieces_of(nd.b), pieces_of(nd.c));
+          break;
+        }
+        case MGP_OP_UFAPP:
+        case MGP_OP_UFINV:
+          break;  // below, shared with narrow results
+        default:
+          return unsupported();
+      }
+      if (op != MGP_OP_UFAPP && op != MGP_OP_UFINV) continue;
+    }
+    // narrow results: a wide operand is only legal where the case below says so
+    if (is_wide(nd.a) || is_wide(nd.b) || is_wide(nd.c)) {
+      const bool ok = op == MGP_OP_EXTRACT || op == MGP_OP_UFAPP || op == MGP_OP_UFINV ||
+                      (op == MGP_OP_EQ && !isb[nd.a] && !isb[nd.b]);
+      if (!ok) return unsupported();
+    }
     switch (op) {
       case MGP_OP_VAR: {
         if (nd.p0 >= 0x3FFFu) return unsupported();
@@ -176,6 +337,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         if (!opnd(nd.a) || isb[nd.a]) return unsupported();
         const uint32_t hi = nd.p0, lo = nd.p1;
         if (hi < lo || hi >= wid[nd.a] || hi - lo + 1 != w) return unsupported();
+        if (wid[nd.a] > MGP_MAX_WIDTH) { val[i] = join(slice(wide[nd.a], lo, w)); break; }
         if (lo == 0 && w == wid[nd.a]) { val[i] = val[nd.a]; break; }
         val[i] = S.add(MGP_OP_EXTRACT, (uint16_t)w, false, val[nd.a], Ref(), Ref(), lo);
         break;
@@ -218,6 +380,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           break;
         }
         if (isb[nd.a] || isb[nd.b] || wid[nd.a] != wid[nd.b]) return unsupported();
+        if (wid[nd.a] > MGP_MAX_WIDTH) { val[i] = eq_pieces(wide[nd.a], wide[nd.b]); break; }
         val[i] = S.add(op, wid[nd.a], true, val[nd.a], val[nd.b]);
         break;
       }
@@ -238,45 +401,39 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         break;
       }
       case MGP_OP_UFAPP: {
-        // f(arg): first earlier f-app with equal argument, else fresh var p1
-        if (!opnd(nd.a) || isb[nd.a] || nd.p1 >= 0x3FFFu) return unsupported();
-        const uint32_t aw = wid[nd.a];
-        S.max_var = std::max(S.max_var, nd.p1 + 1);
-        Ref fresh;
-        fresh.k = R_VAR;
-        fresh.idx = nd.p1;
-        Ref v = (w < 256u) ? S.add(MGP_OP_MOV, (uint16_t)w, false, fresh) : fresh;
+        // f(arg): first earlier f-app with equal argument, else fresh var(s) p1..
+        const uint32_t k = (w + MGP_MAX_WIDTH - 1) / MGP_MAX_WIDTH;
+        if (!opnd(nd.a) || isb[nd.a] || nd.p1 + k > 0x3FFFu) return unsupported();
+        const Pieces arg = pieces_of(nd.a);
+        Pieces v = var_pieces(nd.p1, w);
         std::vector<UFApp> &fl = fapps[nd.p0];
         for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
-          Ref e = S.add(MGP_OP_EQ, (uint16_t)aw, true, val[nd.a], it->arg);
-          v = S.add(MGP_OP_ITE, (uint16_t)w, false, e, it->val, v);
+          if (wid_of(it->arg) != wid[nd.a] || wid_of(it->val) != w) return unsupported();
+          v = ite_pieces(eq_pieces(arg, it->arg), it->val, v);
         }
-        fl.push_back(UFApp{val[nd.a], v});
-        val[i] = v;
+        fl.push_back(UFApp{arg, v});
+        set_val(i, v);
         break;
       }
       case MGP_OP_UFINV: {
         // f^-1(arg): first earlier inverse app with equal argument, else the
-        // argument of the first earlier f-app whose value equals arg, else p1
-        if (!opnd(nd.a) || isb[nd.a] || nd.p1 >= 0x3FFFu) return unsupported();
-        const uint32_t aw = wid[nd.a];
-        S.max_var = std::max(S.max_var, nd.p1 + 1);
-        Ref fresh;
-        fresh.k = R_VAR;
-        fresh.idx = nd.p1;
-        Ref v = (w < 256u) ? S.add(MGP_OP_MOV, (uint16_t)w, false, fresh) : fresh;
+        // argument of the first earlier f-app whose value equals arg, else p1..
+        const uint32_t k = (w + MGP_MAX_WIDTH - 1) / MGP_MAX_WIDTH;
+        if (!opnd(nd.a) || isb[nd.a] || nd.p1 + k > 0x3FFFu) return unsupported();
+        const Pieces arg = pieces_of(nd.a);
+        Pieces v = var_pieces(nd.p1, w);
         std::vector<UFApp> &fl = fapps[nd.p0];
         for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
-          Ref e = S.add(MGP_OP_EQ, (uint16_t)aw, true, val[nd.a], it->val);
-          v = S.add(MGP_OP_ITE, (uint16_t)w, false, e, it->arg, v);
+          if (wid_of(it->val) != wid[nd.a] || wid_of(it->arg) != w) return unsupported();
+          v = ite_pieces(eq_pieces(arg, it->val), it->arg, v);
         }
         std::vector<UFApp> &il = iapps[nd.p0];
         for (auto it = il.rbegin(); it != il.rend(); ++it) {
-          Ref e = S.add(MGP_OP_EQ, (uint16_t)aw, true, val[nd.a], it->arg);
-          v = S.add(MGP_OP_ITE, (uint16_t)w, false, e, it->val, v);
+          if (wid_of(it->arg) != wid[nd.a] || wid_of(it->val) != w) return unsupported();
+          v = ite_pieces(eq_pieces(arg, it->arg), it->val, v);
         }
-        il.push_back(UFApp{val[nd.a], v});
-        val[i] = v;
+        il.push_back(UFApp{arg, v});
+        set_val(i, v);
         break;
       }
       default:

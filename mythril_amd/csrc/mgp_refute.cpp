@@ -272,6 +272,7 @@ AV flip(const AV &a, uint32_t w) {
 
 struct State {
   const mgp_node *nd;
+  std::vector<mgp_node> relaxed;  // nd when the DAG holds wide values (relax_wide)
   uint32_t n;
   const uint32_t *consts;
   uint64_t n_consts;
@@ -941,11 +942,55 @@ struct State {
   }
 };
 
+// Values wider than 256 bits (mgp_ir.h "wide values": 512-bit mapping preimages and
+// keccak inverses) are outside the abstract domain.  They are relaxed: every node that
+// produces or reads a wide value becomes a fresh unconstrained variable of its own width
+// (a Bool reader: EQ of two fresh 8-bit variables).  Replacing subterms by fresh
+// variables only enlarges the solution set, so a refutation of the relaxed DAG refutes
+// the original; the narrow constraints around the mapping stay exact.
+inline bool op_bool_result(uint8_t op) {
+  return (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) || (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) ||
+         op == MGP_OP_TRUE || op == MGP_OP_FALSE;
+}
+
+bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out) {
+  auto wide = [&](int32_t j) { return j >= 0 && (uint64_t)j < n && nd[j].width > MGP_MAX_WIDTH &&
+                                      !op_bool_result(nd[j].op); };
+  bool any = false;
+  for (uint64_t i = 0; i < n && !any; ++i) any = wide((int32_t)i);
+  if (!any) return false;
+  out.assign(nd, nd + n);
+  uint32_t fresh = 1u << 22;  // beyond every variable index of a real DAG (< 0x3FFF)
+  auto fresh_var = [&](mgp_node &x, uint16_t w) {
+    x.op = MGP_OP_VAR;
+    x.width = w;
+    x.a = x.b = x.c = -1;
+    x.p0 = fresh++;
+    x.p1 = 0;
+  };
+  for (uint64_t i = 0; i < n; ++i) {
+    mgp_node &x = out[i];
+    if (wide((int32_t)i)) { fresh_var(x, 8); continue; }
+    if (!(wide(nd[i].a) || wide(nd[i].b) || wide(nd[i].c))) continue;
+    if (op_bool_result(nd[i].op)) {
+      // operands are relaxed placeholders (8-bit fresh variables, distinct unless a == b)
+      x.op = MGP_OP_EQ;
+      x.width = 1;
+      x.c = -1;
+      if (!wide(x.a) || !wide(x.b)) return false;  // malformed; let setup reject it
+    } else {
+      fresh_var(x, nd[i].width);
+    }
+  }
+  return true;
+}
+
 int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t max_passes,
                State *keep) {
   if (n == 0 || n > (1u << 20)) return -1;
   State st;
   State &s = keep ? *keep : st;
+  if (relax_wide(nd, n, s.relaxed)) nd = s.relaxed.data();
   s.nd = nd;
   s.n = (uint32_t)n;
   s.consts = consts;

@@ -38,6 +38,9 @@ class StateDag:
     var_terms: List[Optional[Term]] = field(default_factory=list)
     hints: Dict[int, List[int]] = field(default_factory=dict)  # var index -> harvested values
     aliases: List[Tuple[int, int]] = field(default_factory=list)  # (dst var, src var) from x == y
+    # wide values (> 256 bits, include/mgp_ir.h): first slot -> full width; the value
+    # occupies ceil(width/256) consecutive var slots / pool entries, low 256 bits first
+    wide: Dict[int, int] = field(default_factory=dict)
 
     @property
     def n_vars(self) -> int:
@@ -49,14 +52,17 @@ def build_state(constraints: Sequence[Term]) -> StateDag:
     d = StateDag()
     memo: Dict[int, int] = {}
     var_idx: Dict[Tuple[str, int], int] = {}
-    const_idx: Dict[int, int] = {}
+    const_idx: Dict[Tuple[int, int], int] = {}
 
     def new_var(name: str, width: int, term: Optional[Term]) -> int:
         key = (name, width)
         if key not in var_idx:
             var_idx[key] = len(d.vars)
-            d.vars.append(key)
-            d.var_terms.append(term)
+            if width > 256:
+                d.wide[len(d.vars)] = width
+            for j, off in enumerate(range(0, width, 256)):
+                d.vars.append((name if j == 0 else f"{name}#{j}", min(256, width - off)))
+                d.var_terms.append(term if j == 0 else None)
         return var_idx[key]
 
     def emit(t: Term) -> int:
@@ -69,10 +75,11 @@ def build_state(constraints: Sequence[Term]) -> StateDag:
             p0 = new_var(str(t.params[0]), w, t)
         elif op == ir.CONST:
             v = t.params[0]
-            if v not in const_idx:
-                const_idx[v] = len(d.consts)
-                d.consts.append(v)
-            p0 = const_idx[v]
+            k = (w + 255) // 256
+            if (v, k) not in const_idx:
+                const_idx[(v, k)] = len(d.consts)
+                d.consts.extend((v >> (256 * j)) & ((1 << 256) - 1) for j in range(k))
+            p0 = const_idx[(v, k)]
         elif op == ir.EXTRACT:
             p0, p1 = t.params
         elif op in (ir.UFAPP, ir.UFINV):
@@ -131,7 +138,7 @@ def _harvest_hints(d: StateDag) -> None:
             d.aliases.append((va, vb))
             d.aliases.append((vb, va))
         for vi, y in ((va, b), (vb, a)):
-            if vi < 0 or nodes[y][0] != ir.CONST:
+            if vi < 0 or nodes[y][0] != ir.CONST or nodes[a][1] > 256:
                 continue
             cv = d.consts[nodes[y][5]]
             m = (1 << nodes[a][1]) - 1
@@ -203,8 +210,10 @@ def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: 
         if parents is not None and parents[s]:
             for vi, (name, w) in enumerate(st.vars):
                 if name in parents[s]:
-                    vals[0, vi] = parents[s][name] & ((1 << w) - 1)
-                    have[0, vi] = True
+                    pv = parents[s][name]
+                    for j in range((st.wide.get(vi, w) + 255) // 256):  # wide: its later slots too
+                        vals[0, vi + j] = (pv >> (256 * j)) & ((1 << st.vars[vi + j][1]) - 1)
+                        have[0, vi + j] = True
             row = 1
         for structured in (False, True):
             if row >= n_cand:
@@ -251,12 +260,37 @@ def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: 
 def witness_to_model(st: StateDag, words: np.ndarray) -> Dict[str, int]:
     """Witness words [n_vars, 8] -> {var name: value masked to its width} (free vars only)."""
     model: Dict[str, int] = {}
+    vals = []
     for vi, (name, w) in enumerate(st.vars):
         v = 0
         for l in range(8):
             v |= int(words[vi, l]) << (32 * l)
-        model[name] = v & ((1 << w) - 1)
+        vals.append(v & ((1 << w) - 1))
+    skip = set()
+    for vi, w in st.wide.items():
+        k = (w + 255) // 256
+        skip.update(range(vi + 1, vi + k))
+        model[st.vars[vi][0]] = sum(vals[vi + j] << (256 * j) for j in range(k))
+    for vi, (name, w) in enumerate(st.vars):
+        if vi not in skip and vi not in st.wide:
+            model[name] = vals[vi]
     return model
+
+
+def model_to_slots(st: StateDag, model: Dict[str, int]) -> List[int]:
+    """{var name: value} -> one int per var slot (a wide var spread over its slots);
+    the inverse of witness_to_model, missing names read as 0."""
+    out = [0] * st.n_vars
+    rest = set()
+    for vi, w in st.wide.items():
+        v = model.get(st.vars[vi][0], 0)
+        for j in range((w + 255) // 256):
+            out[vi + j] = (v >> (256 * j)) & ((1 << st.vars[vi + j][1]) - 1)
+            rest.add(vi + j)
+    for vi, (name, w) in enumerate(st.vars):
+        if vi not in rest:
+            out[vi] = model.get(name, 0) & ((1 << w) - 1)
+    return out
 
 
 def nominal_ops(st: StateDag) -> int:

@@ -191,6 +191,15 @@ def int_to_limbs(v: int, n: int = 8) -> List[int]:
     return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(n)]
 
 
+def wide_read(table: Sequence[int], first: int, w: int) -> int:
+    """A w-bit value held in ceil(w/256) consecutive 256-bit entries, low first
+    (include/mgp_ir.h "wide values"; w <= 256 is the single entry `first`)."""
+    v = 0
+    for j in range((w + 255) // 256):
+        v |= (int(table[first + j]) & mask(256)) << (256 * j)
+    return v & mask(w)
+
+
 def eval_dag(nodes, consts: Sequence[int], xs: Sequence[int]) -> List:
     """Evaluate a topologically ordered node list.
 
@@ -208,9 +217,9 @@ def eval_dag(nodes, consts: Sequence[int], xs: Sequence[int]) -> List:
         if op in BOOL_RESULT:
             w = 1
         if op == VAR:
-            v = xs[p0] & mask(w)
+            v = wide_read(xs, p0, w)
         elif op == CONST:
-            v = consts[p0] & mask(w)
+            v = wide_read(consts, p0, w)
         elif op == TRUE:
             v = True
         elif op == FALSE:
@@ -253,7 +262,7 @@ def eval_dag(nodes, consts: Sequence[int], xs: Sequence[int]) -> List:
             v = bool(vals[a]) == bool(vals[b])
         elif op == UFAPP:
             arg = vals[a]
-            v = xs[p1] & mask(w)
+            v = wide_read(xs, p1, w)
             for (aj, vj) in fapps.get(p0, []):
                 if aj == arg:
                     v = vj
@@ -272,7 +281,7 @@ def eval_dag(nodes, consts: Sequence[int], xs: Sequence[int]) -> List:
                         v = aj
                         break
             if v is None:
-                v = xs[p1] & mask(w)
+                v = wide_read(xs, p1, w)
             iapps.setdefault(p0, []).append((arg, v))
         else:
             raise ValueError(f"unknown op {op}")

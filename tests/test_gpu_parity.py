@@ -135,9 +135,10 @@ def test_edge_values_all_ops(mgp_ctx):
 
 
 def test_unsupported_and_empty(mgp_ctx):
-    # width 512 (not supported this round) -> MGP_UNDECIDED, other states unaffected
+    # arithmetic on a 512-bit value (only structural ops are lowered) -> MGP_UNDECIDED,
+    # other states unaffected
     nl_bad = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.CONCAT, 512, 0, 1, -1, 0, 0],
-              [S.EQ, 1, 2, 2, -1, 0, 0]]
+              [S.ADD, 512, 2, 2, -1, 0, 0], [S.EQ, 1, 3, 3, -1, 0, 0]]
     nl_ok = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 1, -1, 0, 0]]
     nl_true = [[S.TRUE, 1, -1, -1, -1, 0, 0]]
     nl_false = [[S.FALSE, 1, -1, -1, -1, 0, 0]]
@@ -150,6 +151,32 @@ def test_unsupported_and_empty(mgp_ctx):
     # zero states is a no-op
     f0, _ = mgp_ctx.eval_batch(np.zeros(0, np.uint32), np.zeros(1, np.uint64), np.zeros((0, 1, 1, 8), np.uint32))
     assert f0.size == 0
+
+
+def test_wide_values_parity(mgp_ctx):
+    """512/516-bit values (include/mgp_ir.h "wide values") and keccak256_512 mapping
+    preimages with the inverse: first-SAT per candidate row vs the oracle."""
+    from .test_lowering import wide_mapping_case, wide_struct_case
+    nl_s, c_s, rows_s = wide_struct_case()
+    nl_m, nl_c, c_m, rows_m = wide_mapping_case()
+    states = [(nl_s, c_s), (nl_m, c_m), (nl_c, c_m)]
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    n_vars = max(len(r) for r in rows_s + rows_m)
+    want = []
+    for s, (nl, cl) in enumerate(states):
+        rows = rows_s if s == 0 else rows_m
+        # one candidate per launch row: evaluate each row alone (first_sat 0 or -1)
+        for r in rows:
+            want.append(0 if S.eval_root(nl, cl, r) else -1)
+    batch = [states[0]] * len(rows_s) + [states[1]] * len(rows_m) + [states[2]] * len(rows_m)
+    nodes, noff, consts, coff = pack_states(batch)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    cand_rows = [[list(r) + [0] * (n_vars - len(r))] for r in rows_s + rows_m + rows_m]
+    first, _ = mgp_ctx.eval_batch(words, po, cands_from_ints(cand_rows))
+    assert list(first) == want
+    assert 0 in want and -1 in want
 
 
 def test_uf_ackermann_semantics(mgp_ctx):

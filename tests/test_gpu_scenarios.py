@@ -10,6 +10,10 @@ reading") and check what the GPU-first front end answers and how many fallback
   `suicide.py:76-99`): the path requires addr == 0, so the first query (`to ==
   ACTORS.attacker`) is UNSAT — proven by the host pre-check, no z3 call; the path
   itself is feasible.
+* BECToken.sol `balances[msg.sender]` (`BECToken.sol:256-258`): a storage read at
+  keccak256_512(Concat(caller, 0)) — a 512-bit preimage, lowered as word pairs
+  (include/mgp_ir.h "wide values") — with the manager's interval/inverse condition
+  (`keccak_function_manager.py:122-146`): SAT by a GPU witness, no z3 call.
 * BECToken.sol `batchTransfer` (`BECToken.sol:254-258`, module `integer.py:141-160,
   288-297`): the multiplication-overflow query is SAT — a GPU witness the oracle
   confirms, no z3 call; SafeMath's `sub` after `require(balance >= amount)`
@@ -18,6 +22,7 @@ reading") and check what the GPU-first front end answers and how many fallback
 import pytest
 
 from mythril_amd import dag as D
+from mythril_amd.keccak import KeccakFunctionManager
 from mythril_amd import solver as SV
 from mythril_amd.smt import (And, Array, BVMulNoOverflow, BVSubNoUnderflow, Concat, Extract, If, Not, UGE, UGT,
                              ULE, ULT, symbol_factory)
@@ -67,7 +72,7 @@ def _selector(calldata, size, sig):
 
 def _confirmed(constraints, model):
     st = D.build_state([c.raw for c in constraints])
-    return S.eval_root(st.nodes, st.consts, [model.assignments[0].get(n, 0) for (n, _) in st.vars])
+    return S.eval_root(st.nodes, st.consts, D.model_to_slots(st, model.assignments[0]))
 
 
 def test_suicide_kill_attacker_query_refuted(backend):
@@ -107,3 +112,25 @@ def test_bectoken_safemath_sub_cannot_underflow(backend):
     with pytest.raises(SV.UnsatError):
         SV.get_model(tuple(path + [underflow]))
     assert backend.calls == 0 and SV.SolverStatistics().refuted == 1
+
+
+def test_bectoken_mapping_balance_witness(backend):
+    kfm = KeccakFunctionManager()
+    caller, value, cnt = BVS("caller", 256), BVS("value", 256), BVS("receivers_length", 256)
+    storage = Array("Storage", 256, 256)
+    slot, cond = kfm.create_keccak(Concat(caller, BVV(0, 256)))       # balances[msg.sender]
+    bal = storage[slot]
+    amount = cnt * value
+    path = [cond, caller == BVV(ATTACKER, 256), UGT(cnt, BVV(0, 256)), ULE(cnt, BVV(20, 256)),
+            UGT(value, BVV(0, 256)), UGE(bal, amount)]
+    overflow = Not(BVMulNoOverflow(cnt, value, False))
+    m = SV.get_model(tuple(path + [overflow]))
+    assert _confirmed(path + [overflow], m)
+    assert backend.calls == 0 and SV.SolverStatistics().gpu_sat >= 1
+    assert m.assignments[0]["caller"] == ATTACKER
+    # two mappings with the same slot: equal hashes force equal keys (Ackermann with the inverse)
+    other, cond2 = kfm.create_keccak(Concat(value, BVV(0, 256)))
+    SV.get_model.cache_clear()
+    m2 = SV.get_model(tuple([cond, cond2, slot == other]))
+    assert m2.assignments[0]["caller"] == m2.assignments[0]["value"]
+    assert _confirmed([cond, cond2, slot == other], m2)

@@ -145,12 +145,89 @@ def test_many_live_values_rejected_cleanly():
     assert UR.run_uops(words, int(po[0]), [3, 5]) is None
 
 
+def wide_struct_case():
+    # 516-bit and 512-bit values (include/mgp_ir.h "wide values"): VAR over three
+    # slots, wide CONST over two pool entries, CONCAT with boundaries that do not
+    # line up with 256, EXTRACT (narrow and wide, across pieces), ZEXT, ITE, EQ
+    c512 = (0x1234 << 400) | (7 << 255) | 0xABCDEF
+    nl = [[S.VAR, 160, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.VAR, 100, -1, -1, -1, 2, 0],
+          [S.CONCAT, 356, 2, 1, -1, 0, 0], [S.CONCAT, 516, 3, 0, -1, 0, 0],        # 4: x2 . x1 . x0
+          [S.VAR, 516, -1, -1, -1, 3, 0],                                            # 5: x3,x4,x5 (3 slots)
+          [S.EQ, 1, 4, 5, -1, 0, 0],                                                 # 6
+          [S.EXTRACT, 200, 4, -1, -1, 299, 100], [S.EXTRACT, 200, 5, -1, -1, 299, 100],
+          [S.EQ, 1, 7, 8, -1, 0, 0],                                                 # 9
+          [S.EXTRACT, 400, 5, -1, -1, 459, 60], [S.ZEXT, 512, 1, -1, -1, 0, 0],      # 10, 11
+          [S.CONST, 512, -1, -1, -1, 0, 0], [S.ULT, 1, 7, 8, -1, 0, 0],              # 12, 13
+          [S.ITE, 512, 13, 11, 12, 0, 0], [S.EXTRACT, 512, 5, -1, -1, 511, 0],       # 14, 15
+          [S.EQ, 1, 14, 15, -1, 0, 0], [S.EXTRACT, 256, 10, -1, -1, 399, 144],      # 16, 17
+          [S.EXTRACT, 256, 5, -1, -1, 459, 204], [S.EQ, 1, 17, 18, -1, 0, 0],        # 18, 19
+          [S.BOR, 1, 6, 16, -1, 0, 0], [S.BAND, 1, 20, 19, -1, 0, 0], [S.BOR, 1, 21, 9, -1, 0, 0]]
+    consts = [c512 & ((1 << 256) - 1), c512 >> 256]
+    rng = np.random.default_rng(7)
+    rows = []
+    for _ in range(24):
+        x = [int(rng.integers(0, 2 ** 62)) << int(rng.integers(0, 190)) for _ in range(6)]
+        rows.append(x)
+        big = x[0] & ((1 << 160) - 1) | (x[1] << 160) | ((x[2] & ((1 << 100) - 1)) << 416)
+        rows.append(x[:3] + [big & ((1 << 256) - 1), (big >> 256) & ((1 << 256) - 1), big >> 512])  # 6 true
+        rows.append(x[:3] + [c512 & ((1 << 256) - 1), c512 >> 256, x[5]])                           # 16 via const
+        rows.append([x[0], 1 << 255, x[2], x[1], x[1] << 1, x[5]])
+    return nl, consts, rows
+
+
+def test_wide_structural_ops():
+    nl, consts, rows = wide_struct_case()
+    _, _, status = _check_states([(nl, consts)], [rows])
+    assert status[0] == N.ST_OK
+    assert sum(S.eval_root(nl, consts, r) for r in rows) >= 24
+
+
+def wide_mapping_case():
+    # keccak256_512 over Concat(key, slot) and its inverse, as
+    # keccak_function_manager.create_keccak builds them (keccak_function_manager.py:122-146):
+    # inv(f(k0 . 0)) == k0 . 0, inv(f(k1 . 1)) == k1 . 1, and f(k0 . 0) == f(k1 . 1) must then
+    # be impossible (different slots), while f(k0 . 0) == f(k2 . 0) forces k0 == k2
+    F = 5
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.VAR, 256, -1, -1, -1, 2, 0],
+          [S.CONST, 256, -1, -1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+          [S.CONCAT, 512, 0, 3, -1, 0, 0], [S.CONCAT, 512, 1, 4, -1, 0, 0], [S.CONCAT, 512, 2, 3, -1, 0, 0],
+          [S.UFAPP, 256, 5, -1, -1, F, 3], [S.UFAPP, 256, 6, -1, -1, F, 4], [S.UFAPP, 256, 7, -1, -1, F, 5],
+          [S.UFINV, 512, 8, -1, -1, F, 6], [S.UFINV, 512, 9, -1, -1, F, 8], [S.UFINV, 512, 10, -1, -1, F, 10],
+          [S.EQ, 1, 11, 5, -1, 0, 0], [S.EQ, 1, 12, 6, -1, 0, 0], [S.EQ, 1, 13, 7, -1, 0, 0],
+          [S.BAND, 1, 14, 15, -1, 0, 0], [S.BAND, 1, 17, 16, -1, 0, 0],                 # 17, 18: consistency
+          [S.EQ, 1, 8, 9, -1, 0, 0], [S.EQ, 1, 8, 10, -1, 0, 0], [S.EQ, 1, 0, 2, -1, 0, 0],  # 19, 20, 21
+          [S.BAND, 1, 18, 19, -1, 0, 0], [S.BXOR, 1, 20, 21, -1, 0, 0],                # 22, 23
+          [S.BAND, 1, 18, 23, -1, 0, 0], [S.BOR, 1, 22, 24, -1, 0, 0]]                  # root: never true
+    consts = [0, 1]
+    rows = []
+    for k0 in (3, 1 << 200):
+        for k1 in (3, 4):
+            for k2 in (3, 1 << 200, 9):
+                for h in ((10, 10, 10), (10, 11, 12), (10, 11, 10), (7, 7, 8)):
+                    for fr in ((0, 0, 0, 0, 0, 0), (3, 0, 3, 1, 9, 0), (k0, 0, k1, 1, k2, 0)):
+                        rows.append([k0, k1, k2, *h, *fr])
+    nl_cons = nl[:21] + [[S.BAND, 1, 18, 20, -1, 0, 0]]  # consistent and f(k0.0) == f(k2.0): sat iff k0 == k2 allowed
+    return nl, nl_cons, consts, rows
+
+
+def test_wide_keccak_mapping_uf():
+    nl, nl_cons, consts, rows = wide_mapping_case()
+    nodes, noff, cpk, coff = pack_states([(nl, consts)])
+    words, po, status = N.lower(nodes, noff, cpk, coff)
+    assert status[0] == N.ST_OK
+    _check_states([(nl, consts), (nl_cons, consts)], [rows, rows])
+    assert not any(S.eval_root(nl, consts, r) for r in rows)
+    assert any(S.eval_root(nl_cons, consts, r) for r in rows)
+    assert all(r[0] == r[2] for r in rows if S.eval_root(nl_cons, consts, r))
+
+
 @pytest.mark.parametrize("bad", ["wide", "forward_ref", "bool_as_bv", "width_mismatch", "root_bv", "unknown_op"])
 def test_malformed_dags_are_unsupported(bad):
     v0 = [S.VAR, 256, -1, -1, -1, 0, 0]
     v1 = [S.VAR, 256, -1, -1, -1, 1, 0]
     nl = {
-        "wide": [v0, v1, [S.CONCAT, 512, 0, 1, -1, 0, 0], [S.EQ, 1, 2, 2, -1, 0, 0]],
+        "wide": [v0, v1, [S.CONCAT, 512, 0, 1, -1, 0, 0], [S.ADD, 512, 2, 2, -1, 0, 0],
+                 [S.EXTRACT, 1, 3, -1, -1, 0, 0], [S.EQ, 1, 4, 4, -1, 0, 0]],
         "forward_ref": [v0, [S.ULT, 1, 0, 2, -1, 0, 0], v1],
         "bool_as_bv": [v0, [S.ULT, 1, 0, 0, -1, 0, 0], [S.ADD, 256, 0, 1, -1, 0, 0], [S.EQ, 1, 2, 0, -1, 0, 0]],
         "width_mismatch": [v0, [S.VAR, 8, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 1, -1, 0, 0]],

@@ -104,3 +104,37 @@ def test_bool_symbols_and_constants():
     _check([Or(p, x == BVV(3, 256)), Not(p) == (x == BVV(3, 256))], None, n=20)
     st = D.build_state([symbol_factory.Bool(True).raw])
     assert st.nodes[-1][0] == ir.TRUE
+
+
+def test_wide_mapping_preimage_state_lowers_and_candidates_satisfy():
+    """keccak256_512(Concat(key, slot)) with the manager's condition (keccak_function_manager.py:122-146):
+    the 512-bit preimage and inverse lower to narrow pieces, and the candidate generator's
+    assignments include a model (checked with the CPU uop interpreter, no GPU)."""
+    from mythril_amd import _native as N
+    from mythril_amd.keccak import KeccakFunctionManager
+    from mythril_amd.smt import Concat, ULT, symbol_factory
+    from oracle import bvsem as S
+    from oracle import uop_ref as UR
+    from tests._util import pack_states
+
+    kfm = KeccakFunctionManager()
+    key = symbol_factory.BitVecSym("key", 256)
+    h, cond = kfm.create_keccak(Concat(key, symbol_factory.BitVecVal(3, 256)))
+    st = D.build_state([cond.raw, ULT(key, symbol_factory.BitVecVal(1000, 256)).raw])
+    assert st.wide, "inverse result is a wide (512-bit) fresh value"
+    (vi, w), = st.wide.items()
+    assert w == 512 and st.vars[vi + 1][0].endswith("#1")
+    nodes, noff, consts, coff = pack_states([(st.nodes, st.consts)])
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert status[0] == N.ST_OK
+    cands = D.make_candidates([st], 64, st.n_vars)
+    hits = 0
+    for c in range(64):
+        xs = [S.limbs_to_int(cands[0, c, v]) for v in range(st.n_vars)]
+        want = S.eval_root(st.nodes, st.consts, xs)
+        assert UR.run_uops(words, int(po[0]), xs) == want
+        hits += want
+    assert hits > 0
+    model = D.witness_to_model(st, cands[0, 0])
+    assert D.model_to_slots(st, model) == [S.limbs_to_int(cands[0, 0, v]) & ((1 << st.vars[v][1]) - 1)
+                                           for v in range(st.n_vars)]

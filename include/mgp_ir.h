@@ -32,9 +32,12 @@
  * consecutive entries, low 256 bits first:
  *   VAR    variables p0, p0+1, ...        CONST  pool entries p0, p0+1, ...
  *   UFAPP / UFINV with a wide result: fresh variables p1, p1+1, ...
- * Only CONCAT, EXTRACT, ZEXT, ITE, EQ and UF arguments/results may touch a
- * wide value; the lowering splits it into pieces and emits narrow code only
- * (any other op on a wide value makes the state MGP_ST_UNSUPPORTED). */
+ * CONCAT, EXTRACT, ZEXT, ITE, EQ, UF arguments/results, ADD / SUB (carry chain
+ * between pieces: the 257-bit BVAddNoOverflow expansions), AND / OR / XOR / NOT
+ * and the unsigned compares ULT / ULE / UGT / UGE may touch a wide value; the
+ * lowering splits it into pieces and emits narrow code only.  Any other op on a
+ * wide value (MUL, DIV, shifts, signed compares) makes the state
+ * MGP_ST_UNSUPPORTED. */
 #define MGP_LIMBS 8         /* 8 x u32 little-endian limbs per 256-bit value */
 
 /* ---------------------------------------------------------------- opcodes */

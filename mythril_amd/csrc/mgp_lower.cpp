@@ -194,6 +194,55 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
       out.push_back(Piece{S.add(MGP_OP_ITE, (uint16_t)pa[k].w, false, c, pa[k].r, qa[k].r), pa[k].w});
     return out;
   };
+  auto const_small = [&](uint32_t v, uint32_t w) -> Ref {
+    uint32_t l[8] = {v, 0, 0, 0, 0, 0, 0, 0};
+    return S.constant(l, w);
+  };
+  auto const_ones = [&](uint32_t w) -> Ref {
+    static const uint32_t ones[8] = {~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u, ~0u};
+    return S.constant(ones, w);
+  };
+  // piecewise bitwise ops; ADD / SUB with a carry (borrow) chain between pieces:
+  //   carry_out = NOT BVAddNoOverflow(a_k, b_k) OR (carry_in AND a_k + b_k == ~0)
+  //   borrow_out = a_k <u b_k OR (borrow_in AND a_k == b_k)
+  auto arith_pieces = [&](uint8_t op, const Pieces &p, const Pieces &q) -> Pieces {
+    Pieces pa, qa, out;
+    align(p, q, pa, qa);
+    Ref cy;
+    bool have_cy = false;
+    for (size_t k = 0; k < pa.size(); ++k) {
+      const uint16_t pw = (uint16_t)pa[k].w;
+      Ref r = S.add(op, pw, false, pa[k].r, qa[k].r);
+      Ref part = r;
+      if (have_cy) r = S.add(op, pw, false, r, S.add(MGP_OP_ITE, pw, false, cy, const_small(1, pw), const_small(0, pw)));
+      if ((op == MGP_OP_ADD || op == MGP_OP_SUB) && k + 1 < pa.size()) {
+        Ref c1 = (op == MGP_OP_ADD) ? S.add(MGP_OP_BNOT, 1, true, S.add(MGP_OP_UADD_NOOVF, pw, true, pa[k].r, qa[k].r))
+                                    : S.add(MGP_OP_ULT, pw, true, pa[k].r, qa[k].r);
+        if (have_cy) {
+          Ref c2 = (op == MGP_OP_ADD) ? S.add(MGP_OP_EQ, pw, true, part, const_ones(pw))
+                                      : S.add(MGP_OP_EQ, pw, true, pa[k].r, qa[k].r);
+          c1 = S.add(MGP_OP_BOR, 1, true, c1, S.add(MGP_OP_BAND, 1, true, cy, c2));
+        }
+        cy = c1;
+        have_cy = true;
+      }
+      out.push_back(Piece{r, pw});
+    }
+    return out;
+  };
+  // a <u b over pieces: lt_k = a_k <u b_k OR (a_k == b_k AND lt_{k-1})
+  auto ult_pieces = [&](const Pieces &p, const Pieces &q) -> Ref {
+    Pieces pa, qa;
+    align(p, q, pa, qa);
+    Ref lt;
+    for (size_t k = 0; k < pa.size(); ++k) {
+      const uint16_t pw = (uint16_t)pa[k].w;
+      Ref l = S.add(MGP_OP_ULT, pw, true, pa[k].r, qa[k].r);
+      if (k) l = S.add(MGP_OP_BOR, 1, true, l, S.add(MGP_OP_BAND, 1, true, S.add(MGP_OP_EQ, pw, true, pa[k].r, qa[k].r), lt));
+      lt = l;
+    }
+    return lt;
+  };
   // concatenation of narrow pieces (total <= 256) into one value
   auto join = [&](const Pieces &p) -> Ref {
     Ref r = p[0].r;
@@ -283,6 +332,17 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           wide[i] = ite_pieces(val[nd.a], pieces_of(nd.b), pieces_of(nd.c));
           break;
         }
+        case MGP_OP_ADD: case MGP_OP_SUB: case MGP_OP_AND: case MGP_OP_OR: case MGP_OP_XOR: {
+          if (!opnd(nd.a) || !opnd(nd.b) || isb[nd.a] || isb[nd.b] || wid[nd.a] != w || wid[nd.b] != w)
+            return unsupported();
+          wide[i] = arith_pieces(op, wide[nd.a], wide[nd.b]);
+          break;
+        }
+        case MGP_OP_NOT: {
+          if (!opnd(nd.a) || isb[nd.a] || wid[nd.a] != w) return unsupported();
+          for (const Piece &q : wide[nd.a]) wide[i].push_back(Piece{S.add(MGP_OP_NOT, (uint16_t)q.w, false, q.r), q.w});
+          break;
+        }
         case MGP_OP_UFAPP:
         case MGP_OP_UFINV:
           break;  // below, shared with narrow results
@@ -294,7 +354,8 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     // narrow results: a wide operand is only legal where the case below says so
     if (is_wide(nd.a) || is_wide(nd.b) || is_wide(nd.c)) {
       const bool ok = op == MGP_OP_EXTRACT || op == MGP_OP_UFAPP || op == MGP_OP_UFINV ||
-                      (op == MGP_OP_EQ && !isb[nd.a] && !isb[nd.b]);
+                      ((op == MGP_OP_EQ || op == MGP_OP_ULT || op == MGP_OP_ULE || op == MGP_OP_UGT ||
+                        op == MGP_OP_UGE) && !isb[nd.a] && !isb[nd.b]);
       if (!ok) return unsupported();
     }
     switch (op) {
@@ -380,7 +441,18 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           break;
         }
         if (isb[nd.a] || isb[nd.b] || wid[nd.a] != wid[nd.b]) return unsupported();
-        if (wid[nd.a] > MGP_MAX_WIDTH) { val[i] = eq_pieces(wide[nd.a], wide[nd.b]); break; }
+        if (wid[nd.a] > MGP_MAX_WIDTH) {
+          const Pieces &x = wide[nd.a], &y = wide[nd.b];
+          switch (op) {
+            case MGP_OP_EQ: val[i] = eq_pieces(x, y); break;
+            case MGP_OP_ULT: val[i] = ult_pieces(x, y); break;
+            case MGP_OP_UGT: val[i] = ult_pieces(y, x); break;
+            case MGP_OP_ULE: val[i] = S.add(MGP_OP_BNOT, 1, true, ult_pieces(y, x)); break;
+            case MGP_OP_UGE: val[i] = S.add(MGP_OP_BNOT, 1, true, ult_pieces(x, y)); break;
+            default: return unsupported();
+          }
+          break;
+        }
         val[i] = S.add(op, wid[nd.a], true, val[nd.a], val[nd.b]);
         break;
       }

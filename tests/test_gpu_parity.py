@@ -135,10 +135,10 @@ def test_edge_values_all_ops(mgp_ctx):
 
 
 def test_unsupported_and_empty(mgp_ctx):
-    # arithmetic on a 512-bit value (only structural ops are lowered) -> MGP_UNDECIDED,
+    # a 512-bit multiply (not lowered for wide values) -> MGP_UNDECIDED,
     # other states unaffected
     nl_bad = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.CONCAT, 512, 0, 1, -1, 0, 0],
-              [S.ADD, 512, 2, 2, -1, 0, 0], [S.EQ, 1, 3, 3, -1, 0, 0]]
+              [S.MUL, 512, 2, 2, -1, 0, 0], [S.EQ, 1, 3, 3, -1, 0, 0]]
     nl_ok = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 1, -1, 0, 0]]
     nl_true = [[S.TRUE, 1, -1, -1, -1, 0, 0]]
     nl_false = [[S.FALSE, 1, -1, -1, -1, 0, 0]]
@@ -177,6 +177,20 @@ def test_wide_values_parity(mgp_ctx):
     first, _ = mgp_ctx.eval_batch(words, po, cands_from_ints(cand_rows))
     assert list(first) == want
     assert 0 in want and -1 in want
+
+
+def test_wide_arith_parity(mgp_ctx):
+    """257..776-bit ADD / SUB carry chains, bitwise ops and unsigned compares: first-SAT
+    over each state's candidate rows vs the oracle."""
+    from .test_lowering import wide_arith_cases
+    states, rows = wide_arith_cases()
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    first, _ = mgp_ctx.eval_batch(words, po, cands_from_ints(rows))
+    want = [S.first_sat(nl, cl, r) for (nl, cl), r in zip(states, rows)]
+    assert list(first) == want
+    assert any(x >= 0 for x in want) and any(x < 0 for x in want)
 
 
 def test_uf_ackermann_semantics(mgp_ctx):

@@ -182,6 +182,62 @@ def test_wide_structural_ops():
     assert sum(S.eval_root(nl, consts, r) for r in rows) >= 24
 
 
+def wide_arith_cases():
+    """ADD / SUB (carry chains), bitwise ops and unsigned compares on 257..776-bit values
+    built from 256-bit vars: BVAddNoOverflow's 257-bit expansion
+    Extract(256, 256, ZeroExt(1, a) + ZeroExt(1, b)) == 0 among them."""
+    states, rows = [], []
+    rng = np.random.default_rng(11)
+    edge = [0, 1, (1 << 256) - 1, (1 << 256) - 2, 1 << 255, (1 << 255) - 1, 5]
+    for w in (257, 300, 512, 516, 776):
+        for op in (S.ADD, S.SUB, S.AND, S.OR, S.XOR, S.NOT):
+            for cmp in (S.EQ, S.ULT, S.ULE, S.UGT, S.UGE):
+                # a = ZeroExt / Concat of vars, b likewise, r = a op b, check cmp(r, c) and Extract(top bit)
+                k = w - 256
+                nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0],
+                      [S.VAR, min(k, 256), -1, -1, -1, 2, 0], [S.VAR, 256, -1, -1, -1, 3, 0],
+                      [S.CONCAT, w, 2, 0, -1, 0, 0] if k <= 256 else [S.ZEXT, w, 0, -1, -1, 0, 0],
+                      [S.ZEXT, w, 1, -1, -1, 0, 0],
+                      [op, w, 4, 5, -1, 0, 0] if op != S.NOT else [S.NOT, w, 4, -1, -1, 0, 0],
+                      [S.CONCAT, w, 2, 3, -1, 0, 0] if k <= 256 else [S.ZEXT, w, 3, -1, -1, 0, 0],
+                      [cmp, 1, 6, 7, -1, 0, 0], [S.EXTRACT, 1, 6, -1, -1, w - 1, w - 1],
+                      [S.EXTRACT, 1, 6, -1, -1, 255, 255], [S.EQ, 1, 9, 10, -1, 0, 0],
+                      [S.BOR, 1, 8, 11, -1, 0, 0] if cmp != S.EQ else [S.BAND, 1, 8, 8, -1, 0, 0]]
+                states.append((nl, []))
+                r = []
+                for _ in range(5):
+                    xs = [edge[int(rng.integers(0, len(edge)))] if rng.random() < 0.6 else
+                          int(rng.integers(0, 2 ** 62)) << int(rng.integers(0, 194)) for _ in range(4)]
+                    xs[2] &= (1 << min(k, 256)) - 1
+                    r.append(xs)
+                # r == c exactly for EQ rows: pick x3 so that Concat(x2, x3) equals the result
+                xs = list(r[0])
+                vals = S.eval_dag(nl, [], xs)
+                res = vals[6]
+                if k <= 256:
+                    xs[2], xs[3] = res >> 256, res & ((1 << 256) - 1)
+                r.append(xs)
+                rows.append(r)
+    return states, rows
+
+
+def test_wide_arith_and_compares():
+    states, rows = wide_arith_cases()
+    _, _, status = _check_states(states, rows)
+    assert (status == 0).all()
+
+
+def test_wide_ops_left_unsupported():
+    v0 = [S.VAR, 256, -1, -1, -1, 0, 0]
+    for op in (S.MUL, S.UDIV, S.SHL, S.SLT):
+        nl = [v0, [S.CONCAT, 512, 0, 0, -1, 0, 0],
+              [op, 1 if op == S.SLT else 512, 1, 1, -1, 0, 0]]
+        nl.append([S.BAND, 1, 2, 2, -1, 0, 0] if op == S.SLT else [S.EQ, 1, 2, 1, -1, 0, 0])
+        nodes, noff, consts, coff = pack_states([(nl, [])])
+        _, _, status = N.lower(nodes, noff, consts, coff)
+        assert status[0] == N.ST_UNSUPPORTED, op
+
+
 def wide_mapping_case():
     # keccak256_512 over Concat(key, slot) and its inverse, as
     # keccak_function_manager.create_keccak builds them (keccak_function_manager.py:122-146):
@@ -226,7 +282,7 @@ def test_malformed_dags_are_unsupported(bad):
     v0 = [S.VAR, 256, -1, -1, -1, 0, 0]
     v1 = [S.VAR, 256, -1, -1, -1, 1, 0]
     nl = {
-        "wide": [v0, v1, [S.CONCAT, 512, 0, 1, -1, 0, 0], [S.ADD, 512, 2, 2, -1, 0, 0],
+        "wide": [v0, v1, [S.CONCAT, 512, 0, 1, -1, 0, 0], [S.MUL, 512, 2, 2, -1, 0, 0],
                  [S.EXTRACT, 1, 3, -1, -1, 0, 0], [S.EQ, 1, 4, 4, -1, 0, 0]],
         "forward_ref": [v0, [S.ULT, 1, 0, 2, -1, 0, 0], v1],
         "bool_as_bv": [v0, [S.ULT, 1, 0, 0, -1, 0, 0], [S.ADD, 256, 0, 1, -1, 0, 0], [S.EQ, 1, 2, 0, -1, 0, 0]],

@@ -15,7 +15,9 @@ The concrete hashes go through the HIP Keccak kernel (libmgp.so,
 mgp_keccak256_batch) — one launch for a whole batch via
 `find_concrete_keccak_batch` — instead of pyethereum's utils.sha3.
 `get_code_hash` / `get_code_hashes` mirror support/support_utils.py:29-41
-(pysha3 keccak_256 of the bytecode) on the same kernel.
+(pysha3 keccak_256 of the bytecode) on the same kernel, and
+`replace_with_actual_sha` mirrors the report-time substitution of
+analysis/solver.py:159-192 with all of its hashes in one batch.
 """
 from __future__ import annotations
 
@@ -136,7 +138,7 @@ class KeccakFunctionManager:
         for size in self.hash_result_store:
             concrete_hashes[size] = []
             for val in self.hash_result_store[size]:
-                v = model.eval(val.raw)
+                v = _as_int(model.eval(val.raw))
                 if v is not None:
                     concrete_hashes[size].append(v)
         return concrete_hashes
@@ -174,3 +176,90 @@ class KeccakFunctionManager:
 
 
 keccak_function_manager = KeccakFunctionManager()
+
+
+def _as_int(v) -> Optional[int]:
+    """A model value as an int: z3 numerals (as_long), plain ints, else None."""
+    if v is None or isinstance(v, bool):
+        return None
+    if hasattr(v, "as_long"):
+        try:
+            return int(v.as_long())
+        except Exception:
+            return None
+    return int(v) if isinstance(v, (int, np.integer)) else None
+
+
+def _hash_substitutions(tx_input: str, s_index: int, concrete_hashes, manager, model):
+    """The (window start, preimage BitVec) pairs analysis/solver.py:170-183 finds in one input."""
+    out = []
+    for i in range(s_index, len(tx_input)):
+        data_slice = tx_input[i: i + 64]
+        if hash_matcher not in data_slice or len(data_slice) != 64:
+            continue
+        find_input = int(data_slice, 16)
+        input_ = None
+        for size in concrete_hashes:
+            _, inverse = manager.store_function[size]
+            if find_input not in concrete_hashes[size]:
+                continue
+            v = _as_int(model.eval(inverse(symbol_factory.BitVecVal(find_input, 256)).raw))
+            if v is None:  # the reference's as_long() would raise here; leave the window alone
+                continue
+            input_ = symbol_factory.BitVecVal(v, size)
+        if input_ is not None:
+            out.append((i, input_))
+    return out
+
+
+def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, code=None,
+                            manager: Optional[KeccakFunctionManager] = None, hasher=None) -> None:
+    """analysis/solver.py:159-192 (`_replace_with_actual_sha`): every 64-hex-digit window of a
+    transaction's input that contains `hash_matcher` and equals a hash value of the model is
+    replaced by the real Keccak-256 of the preimage the model gives its inverse.
+
+    Same scan and the same in-place replacement order as the reference (a window is read from
+    the input as already rewritten by earlier windows).  The hashing is batched: a first pass
+    over the unmodified inputs collects every preimage and hashes them in one launch
+    (`hasher`: list of BitVec -> list of BitVec, default the GPU kernel); the exact
+    sequential pass then reads that table and hashes the rare preimage it did not predict.
+    """
+    manager = manager or keccak_function_manager
+    hasher = hasher or KeccakFunctionManager.find_concrete_keccak_batch
+    concrete_hashes = manager.get_concrete_hash_data(model)
+
+    def start(tx) -> Optional[int]:
+        if hash_matcher not in tx["input"]:
+            return None
+        if code is not None and code.bytecode in tx["input"]:
+            return len(code.bytecode) + 2
+        return 10
+
+    table: Dict[Tuple[int, int], int] = {}
+
+    def fill(preimages):
+        todo = [p for p in preimages if (p.value, p.size()) not in table]
+        if todo:
+            for p, h in zip(todo, hasher(todo)):
+                table[(p.value, p.size())] = h.value
+
+    predicted = []
+    for tx in concrete_transactions:
+        s_index = start(tx)
+        if s_index is not None:
+            predicted.extend(p for _, p in _hash_substitutions(tx["input"], s_index, concrete_hashes, manager,
+                                                               model))
+    fill(predicted)
+
+    for tx in concrete_transactions:
+        s_index = start(tx)
+        if s_index is None:
+            continue
+        for i in range(s_index, len(tx["input"])):
+            subs = _hash_substitutions(tx["input"][: i + 64], i, concrete_hashes, manager, model)
+            if not subs:
+                continue
+            _, input_ = subs[0]
+            fill([input_])
+            hex_keccak = hex(table[(input_.value, input_.size())])[2:].rjust(64, "0")
+            tx["input"] = tx["input"][:s_index] + tx["input"][s_index:].replace(tx["input"][i: 64 + i], hex_keccak)

@@ -50,6 +50,18 @@ def vp(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _slice_states(b, idx):
+    """Node lists / constant pools of the states idx of a synthetic batch, repacked."""
+    no, co = b["node_offsets"].astype(np.int64), b["const_offsets"].astype(np.int64)
+    nl = [b["nodes"][no[i]: no[i + 1]] for i in idx]
+    cl = [b["consts"][co[i]: co[i + 1]] for i in idx]
+    so = np.zeros(len(idx) + 1, np.uint64)
+    so[1:] = np.cumsum([len(x) for x in nl])
+    sco = np.zeros(len(idx) + 1, np.uint64)
+    sco[1:] = np.cumsum([len(x) for x in cl])
+    return np.concatenate(nl), so, np.concatenate(cl).reshape(-1, 8), sco
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,8 +74,10 @@ def main():
     ap.add_argument("--keccak-chunk", type=int, default=1 << 26)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--refute-sample", type=int, default=1 << 18,
+    ap.add_argument("--refute-sample", type=int, default=1 << 17,
                     help="states of the rank-0 batch run through the host UNSAT pre-check (0 = skip)")
+    ap.add_argument("--guided-sample", type=int, default=1 << 16,
+                    help="open states of that sample given the domain-guided second witness round")
     args = ap.parse_args()
 
     import torch
@@ -271,11 +285,37 @@ def main():
         if (sat_s & ref_s).any():
             raise RuntimeError("mgp_refute refuted a state with a GPU witness (soundness bug)")
         fallback = int(ns - sat_s.sum() - ref_s.sum())
+        # second witness round on the states still open: candidates drawn from the pre-check's
+        # refined domains, 16 rows by decisions (mgp_guided_candidates), the rest uniform
+        open_idx = np.nonzero(~sat_s & ~ref_s)[0][: args.guided_sample]
+        guided = None
+        if len(open_idx):
+            tg = time.perf_counter()
+            sn, so, sc, sco = _slice_states(b, open_idx)
+            gw, gpo, _ = N.lower(sn, so, sc, sco)
+            g_cand = 128
+            gc = np.random.default_rng(SEED).integers(0, 2 ** 32, size=(len(open_idx), g_cand, n_vars, 8),
+                                                      dtype=np.uint32)
+            gst = N.guided_candidates(sn, so, sc, sco, gc, seed=SEED, every=2, n_decide=16)
+            dgen = time.perf_counter() - tg
+            gctx = N.Context(local)
+            gfirst, _ = gctx.eval_batch(gw, gpo, gc)
+            gctx.close()
+            if ((gfirst >= 0) & (gst == 1)).any():
+                raise RuntimeError("mgp_refute refuted a state with a GPU witness (soundness bug)")
+            found = int((gfirst >= 0).sum())
+            left = fallback - found if len(open_idx) == fallback else None
+            guided = {"open_states": len(open_idx), "candidates": g_cand, "decision_rows": 16,
+                      "gpu_sat": found, "fallback_after": left,
+                      "solver_call_reduction": (ns / max(1, left)) if left is not None else None,
+                      "host_states_per_s": len(open_idx) / dgen, "seconds": time.perf_counter() - tg}
         prefilter = {"sample_states": ns, "gpu_sat": int(sat_s.sum()), "refuted": int(ref_s.sum()),
                      "fallback": fallback, "solver_call_reduction": ns / max(1, fallback),
                      "refute_states_per_s": ns / dtr, "refute_threads": _threads(),
+                     "guided_round": guided,
                      "note": "synthetic DAGs (random ops), not solidity_examples; reduction = states / states "
-                             "left for z3 after GPU witnesses and host refutations"}
+                             "left for z3 after GPU witnesses and host refutations (guided_round: after the "
+                             "second, domain-guided witness round as well)"}
         log(f"prefilter: {prefilter}")
 
     # ---------------------------------------------------------- CPU baseline

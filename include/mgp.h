@@ -172,6 +172,27 @@ int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes,
                      const uint32_t *consts, uint64_t n_consts,
                      uint32_t max_passes, uint32_t *out_av);
 
+/* Guided candidates for the states the first witness round missed: runs the
+ * same analysis as mgp_refute and, for every state it does not refute, writes
+ * values drawn from each variable's refined abstract value (interval bounds,
+ * then draws inside the interval with the known bits forced) into candidate
+ * rows 0, every, 2*every, ... of `cands` (host layout of mgp_eval_batch:
+ * [state][cand][var][8 limbs]); other rows and variables the DAG does not
+ * read are left as given.  The first n_decide of those rows are built by
+ * decisions: each variable in turn is fixed to a draw from its current
+ * abstract value and the analysis re-run (at most 6 passes), so later
+ * variables see the narrowing the earlier choices cause.  UF applications get their fresh value slot (p1)
+ * from the application's abstract value (keccak intervals, alignment).
+ * Deterministic in seed.  out[s] as mgp_refute.  Replaces nothing in the
+ * reference: it feeds the GPU witness search that answers get_model /
+ * is_possible (analysis/solver.py:27-61, constraints.py:34-51) before z3. */
+int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets,
+                          uint32_t n_states, const uint32_t *consts,
+                          const uint64_t *const_offsets, uint32_t max_passes,
+                          uint32_t n_cand, uint32_t n_vars, uint64_t seed,
+                          uint32_t every, uint32_t n_decide, uint32_t *cands,
+                          int8_t *out);
+
 /* ---------------------------------------------------------- Keccak-256
  * n preimages of len bytes each, preimage i at in + i*stride; 32-byte
  * big-endian digests to out32 + 32*i.  Keccak-256 = Keccak[r=1088,c=512]

@@ -88,6 +88,7 @@ def _bind(lib):
         "mgp_set_eval_diag": (ctypes.c_int, [_P]),
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
+        "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -137,6 +138,7 @@ EXPORTED_SYMBOLS = (
     "mgp_set_eval_diag",
     "mgp_refute",
     "mgp_refute_trace",
+    "mgp_guided_candidates",
 )
 
 ENGINE_HIP, ENGINE_ASM = 1, 2
@@ -202,6 +204,29 @@ def lower(
         _check(rc)
         return words[: int(used.value)], prog_offsets, status[:n_states]
     raise MgpError(MGP_E_CAPACITY, "lowering capacity")
+
+
+def guided_candidates(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,
+                      cands: np.ndarray, seed: int = 0x4D595448, every: int = 2, n_decide: int = 16,
+                      max_passes: int = 0) -> np.ndarray:
+    """Overwrite rows 0, every, 2*every, ... of cands (uint32 [n_states, n_cand, n_vars, 8], in place)
+    with draws from each variable's refined abstract value, the first n_decide of them by
+    decisions (include/mgp.h); -> int8 status per state as refute()."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    const_offsets = np.ascontiguousarray(const_offsets, dtype=np.uint64)
+    n_states = len(node_offsets) - 1
+    if cands.dtype != np.uint32 or not cands.flags.c_contiguous or cands.ndim != 4 or cands.shape[0] != n_states \
+            or cands.shape[3] != 8:
+        raise ValueError("cands must be a C-contiguous uint32 [n_states, n_cand, n_vars, 8] array")
+    out = np.zeros(max(n_states, 1), dtype=np.int8)
+    _check(lib().mgp_guided_candidates(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
+                                       max_passes, cands.shape[1], cands.shape[2], seed & (2 ** 64 - 1), every,
+                                       n_decide, _ptr(cands), _ptr(out)))
+    return out[:n_states]
 
 
 def refute(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,

@@ -1035,3 +1035,111 @@ extern "C" int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes, const u
   }
   return r;
 }
+
+namespace {
+inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// One value of width w inside the abstract value a (known bits z/o, interval lo..hi),
+// drawn from r: interval bounds and their neighbours for the first rows, then a
+// draw inside the interval with the known bits forced when that stays inside.
+V sample_av(const AV &a, uint32_t w, uint32_t row, uint64_t r0) {
+  V v;
+  uint64_t r = r0;
+  for (int l = 0; l < 8; ++l) {
+    if ((l & 1) == 0) r = mix64(r);
+    v.w[l] = (uint32_t)(r >> (32 * (l & 1)));
+  }
+  v = bv_mask(v, w);
+  const V span = SUBV(a.hi, a.lo);
+  if (row == 0) return a.lo;
+  if (row == 1) return a.hi;
+  V x;
+  bool small = true;
+  for (int l = 2; l < 8; ++l) small = small && span.w[l] == 0u;
+  if (small) {
+    const uint64_t sp = ((uint64_t)span.w[1] << 32) | span.w[0];
+    const uint64_t k = (row == 2) ? 1u : (sp == ~0ull ? mix64(r0 ^ 0x5851F42D4C957F2Dull) : mix64(r0 ^ 0x5851F42D4C957F2Dull) % (sp + 1u));
+    V kk = bv_zero();
+    kk.w[0] = (uint32_t)k;
+    kk.w[1] = (uint32_t)(k >> 32);
+    x = ADDV(a.lo, kk);
+    if (LT(a.hi, x)) x = a.hi;
+  } else {
+    x = v;  // wide interval: a full-width draw
+  }
+  const V y = OR(AND(x, NOT(a.z)), a.o);
+  const V yw = bv_mask(y, w);
+  if (!LT(yw, a.lo) && !LT(a.hi, yw)) return yw;
+  return (small || (!LT(x, a.lo) && !LT(a.hi, x))) ? x : ((row & 1) ? a.hi : a.lo);
+}
+}  // namespace
+
+extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                     const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                     uint32_t n_cand, uint32_t n_vars, uint64_t seed, uint32_t every,
+                                     uint32_t n_decide, uint32_t *cands, int8_t *out) {
+  if (!node_offsets || !out || (n_states && (!nodes || !const_offsets || !cands)) || every == 0u)
+    return MGP_E_ARG;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t st = 0; st < (int64_t)n_states; ++st) {
+    const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
+    const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
+    State s;
+    const int r = refute_one(nodes + n0, n1 - n0, consts + 8ull * c0, c1 - c0, max_passes, &s);
+    out[st] = (int8_t)r;
+    if (r != 0) continue;
+    // (var slot, width, abstract value): VAR nodes and the fresh value of UF applications
+    std::vector<uint32_t> slot, width;
+    std::vector<int32_t> node;
+    for (uint32_t i = 0; i < s.n; ++i) {
+      const mgp_node &x = s.nd[i];
+      uint32_t v;
+      if (x.op == MGP_OP_VAR) v = x.p0;
+      else if (x.op == MGP_OP_UFAPP || x.op == MGP_OP_UFINV) v = x.p1;
+      else continue;
+      if (v >= n_vars || x.width == 0u || x.width > MGP_MAX_WIDTH) continue;
+      slot.push_back(v);
+      width.push_back(x.width);
+      node.push_back((int32_t)i);
+    }
+    // The first n_decide guided rows are built by decisions: each variable in turn is
+    // fixed to a draw from its current abstract value and the analysis re-run, so later
+    // variables are drawn from values narrowed by the earlier choices (x + y == c, a
+    // mapping key fixed by an equality, ...).  A draw that empties a domain is replaced
+    // (up to kTries draws); the remaining rows are plain draws from the refined domains.
+    constexpr uint32_t kTries = 4;
+    const uint32_t passes = std::min(max_passes ? max_passes : 16u, 6u);
+    for (uint32_t c = 0, row = 0; c < n_cand; c += every, ++row) {
+      uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
+      if (row < n_decide) {
+        State d = s;
+        for (size_t kk = 0; kk < slot.size(); ++kk) {
+          const size_t k = (row & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
+          const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
+          V v = bv_zero();
+          for (uint32_t t = 0; t < kTries; ++t) {
+            v = sample_av(d.av[node[k]], width[k], t ? 3u + row + t : (row < 4 ? row / 2 : 3u + row), mix64(key + t));
+            State e = d;
+            if (e.meet(node[k], exact(v, width[k])) && e.tie() && e.run(passes) == 0) {
+              d = std::move(e);
+              break;
+            }
+          }
+          memcpy(dst + slot[k] * 8ull, v.w, 32);
+        }
+        continue;
+      }
+      for (size_t k = 0; k < slot.size(); ++k) {
+        const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
+        const V v = sample_av(s.av[node[k]], width[k], row, key);
+        memcpy(dst + slot[k] * 8ull, v.w, 32);
+      }
+    }
+  }
+  return 0;
+}

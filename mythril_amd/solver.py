@@ -226,7 +226,8 @@ class Prefilter:
         self._calls = 0
         self.refute = True  # host UNSAT pre-check (mgp_refute) on every GPU miss
         # second witness round for the states the first round and the pre-check left open:
-        # fresh candidates, up to retry_cand per state (host candidate memory capped at 1 GiB)
+        # fresh candidates (half of them guided by the pre-check's domains), up to retry_cand
+        # per state (host candidate memory capped at 1 GiB)
         self.retry_cand = 1024
 
     def check_states(self, states: Sequence[Sequence[Term]],
@@ -263,8 +264,12 @@ class Prefilter:
             n2 = min(self.retry_cand, budget) // 64 * 64
             if n2 > self.n_cand:
                 sub = [dags[i] for i in retry]
-                sw, sp, _ = self._N.lower(*D.pack_states(sub))
+                packed = D.pack_states(sub)
+                sw, sp, _ = self._N.lower(*packed)
                 c2 = D.make_candidates(sub, n2, n_vars, seed=self.seed + 0x9E3779B9 + self._calls)
+                # every other row drawn from the pre-check's refined domains, the first 16 of
+                # those by decisions (mgp_guided_candidates); the rest keep hints / uniform draws
+                self._N.guided_candidates(*packed, c2, seed=self.seed + self._calls, every=2, n_decide=16)
                 f2, w2 = self.ctx.eval_batch(sw, sp, c2)
                 for k, i in enumerate(retry):
                     if f2[k] >= 0:

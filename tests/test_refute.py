@@ -303,3 +303,42 @@ def test_synthetic_batch_no_refuted_state_has_a_model():
             cands[s, b["plant_idx"][s]] = b["plant_words"][s]
     first = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)
     assert not ((verdict == 1) & (first >= 0)).any()
+
+
+# ------------------------------------------------- domain-guided candidates
+def test_guided_candidates_decisions_solve_linked_vars():
+    # x0 + x1 == 1000 and x0 <u 10: uniform draws never satisfy this; deciding x0 inside
+    # [0, 9] and re-running the analysis fixes x1 = 1000 - x0
+    nl = [X0, X1, [S.ADD, 256, 0, 1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 0, 0], [S.EQ, 1, 2, 3, -1, 0, 0],
+          [S.CONST, 256, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 5, -1, 0, 0], [S.BAND, 1, 4, 6, -1, 0, 0]]
+    cl = [1000, 10]
+    nodes, noff, consts, coff = pack_states([(nl, cl)])
+    rng = np.random.default_rng(3)
+    cands = random_cands(rng, 1, 32, 2)
+    before = cands.copy()
+    st = N.guided_candidates(nodes, noff, consts, coff, cands, seed=1, every=2, n_decide=4)
+    assert st[0] == 0
+    assert np.array_equal(cands[:, 1::2], before[:, 1::2]), "rows outside the guided set are left alone"
+    rows = [[S.limbs_to_int(cands[0, c, v]) for v in range(2)] for c in range(0, 32, 2)]
+    hits = [S.eval_root(nl, cl, r) for r in rows]
+    assert all(hits[:4]), rows[:4]        # every decision row is a model here
+    assert all(r[0] < 10 for r in rows)   # every guided row lies in the refined domain of x0
+    again = before.copy()
+    N.guided_candidates(nodes, noff, consts, coff, again, seed=1, every=2, n_decide=4)
+    assert np.array_equal(again, cands), "deterministic in the seed"
+
+
+def test_guided_candidates_status_and_yield_on_synthetic():
+    b = N.synth_generate(0x4D595448, 0, 768, 64, 256)
+    nodes, noff, consts, coff = b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"]
+    nv = b["n_vars"]
+    rng = np.random.default_rng(5)
+    uni = random_cands(rng, 768, 64, nv, 0.25)
+    gd = uni.copy()
+    st = N.guided_candidates(nodes, noff, consts, coff, gd, seed=7, every=1, n_decide=16)
+    assert np.array_equal(st, N.refute(nodes, noff, consts, coff))
+    f_uni = coracle.first_sat(nodes, noff, consts, coff, uni)
+    f_gd = coracle.first_sat(nodes, noff, consts, coff, gd)
+    assert not ((f_gd >= 0) & (st == 1)).any()
+    # the guided rows find witnesses the same number of uniform rows misses
+    assert ((f_gd >= 0) & (f_uni < 0)).sum() > 2 * max(1, ((f_uni >= 0) & (f_gd < 0)).sum())

@@ -286,7 +286,7 @@ def main():
             raise RuntimeError("mgp_refute refuted a state with a GPU witness (soundness bug)")
         fallback = int(ns - sat_s.sum() - ref_s.sum())
         # second witness round on the states still open: candidates drawn from the pre-check's
-        # refined domains, 16 rows by decisions (mgp_guided_candidates), the rest uniform
+        # refined domains, 32 rows by decisions (mgp_guided_candidates), the rest uniform
         open_idx = np.nonzero(~sat_s & ~ref_s)[0][: args.guided_sample]
         guided = None
         if len(open_idx):
@@ -296,7 +296,7 @@ def main():
             g_cand = 128
             gc = np.random.default_rng(SEED).integers(0, 2 ** 32, size=(len(open_idx), g_cand, n_vars, 8),
                                                       dtype=np.uint32)
-            gst = N.guided_candidates(sn, so, sc, sco, gc, seed=SEED, every=2, n_decide=16)
+            gst = N.guided_candidates(sn, so, sc, sco, gc, seed=SEED, every=2, n_decide=32)
             dgen = time.perf_counter() - tg
             gctx = N.Context(local)
             gfirst, _ = gctx.eval_batch(gw, gpo, gc)
@@ -305,7 +305,7 @@ def main():
                 raise RuntimeError("mgp_refute refuted a state with a GPU witness (soundness bug)")
             found = int((gfirst >= 0).sum())
             left = fallback - found if len(open_idx) == fallback else None
-            guided = {"open_states": len(open_idx), "candidates": g_cand, "decision_rows": 16,
+            guided = {"open_states": len(open_idx), "candidates": g_cand, "decision_rows": 32,
                       "gpu_sat": found, "fallback_after": left,
                       "solver_call_reduction": (ns / max(1, left)) if left is not None else None,
                       "host_states_per_s": len(open_idx) / dgen, "seconds": time.perf_counter() - tg}

@@ -1123,7 +1123,7 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
           const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
           V v = bv_zero();
           for (uint32_t t = 0; t < kTries; ++t) {
-            v = sample_av(d.av[node[k]], width[k], t ? 3u + row + t : (row < 4 ? row / 2 : 3u + row), mix64(key + t));
+            v = sample_av(d.av[node[k]], width[k], t ? 3u + row + t : (row < 4 ? row / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + row : 0u)), mix64(key + t));
             State e = d;
             if (e.meet(node[k], exact(v, width[k])) && e.tie() && e.run(passes) == 0) {
               d = std::move(e);

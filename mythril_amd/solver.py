@@ -267,9 +267,9 @@ class Prefilter:
                 packed = D.pack_states(sub)
                 sw, sp, _ = self._N.lower(*packed)
                 c2 = D.make_candidates(sub, n2, n_vars, seed=self.seed + 0x9E3779B9 + self._calls)
-                # every other row drawn from the pre-check's refined domains, the first 16 of
+                # every other row drawn from the pre-check's refined domains, the first 32 of
                 # those by decisions (mgp_guided_candidates); the rest keep hints / uniform draws
-                self._N.guided_candidates(*packed, c2, seed=self.seed + self._calls, every=2, n_decide=16)
+                self._N.guided_candidates(*packed, c2, seed=self.seed + self._calls, every=2, n_decide=32)
                 f2, w2 = self.ctx.eval_batch(sw, sp, c2)
                 for k, i in enumerate(retry):
                     if f2[k] >= 0:

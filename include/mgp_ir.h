@@ -33,10 +33,11 @@
  *   VAR    variables p0, p0+1, ...        CONST  pool entries p0, p0+1, ...
  *   UFAPP / UFINV with a wide result: fresh variables p1, p1+1, ...
  * CONCAT, EXTRACT, ZEXT, ITE, EQ, UF arguments/results, ADD / SUB (carry chain
- * between pieces: the 257-bit BVAddNoOverflow expansions), AND / OR / XOR / NOT
- * and the unsigned compares ULT / ULE / UGT / UGE may touch a wide value; the
+ * between pieces: the 257-bit BVAddNoOverflow expansions), MUL (128-bit limb
+ * schoolbook: the 512-bit BVMulNoOverflow expansion), AND / OR / XOR / NOT and
+ * the unsigned compares ULT / ULE / UGT / UGE may touch a wide value; the
  * lowering splits it into pieces and emits narrow code only.  Any other op on a
- * wide value (MUL, DIV, shifts, signed compares) makes the state
+ * wide value (division, shifts, signed compares) makes the state
  * MGP_ST_UNSUPPORTED. */
 #define MGP_LIMBS 8         /* 8 x u32 little-endian limbs per 256-bit value */
 

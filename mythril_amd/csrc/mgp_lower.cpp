@@ -253,6 +253,46 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     }
     return r;
   };
+  // a * b mod 2^w over 128-bit limbs: every limb product is exact in one 256-bit MUL
+  // (limbs are stored zero-extended); column k sums the low halves of the products
+  // a_i b_j with i + j = k, the high halves of those with i + j = k - 1 and the carry
+  // out of column k - 1 (each term < 2^128, so a column never wraps 256 bits)
+  auto mul_pieces = [&](const Pieces &p, const Pieces &q, uint32_t w) -> Pieces {
+    const uint32_t n = (w + 127) / 128;
+    std::vector<Ref> a(n), b(n), lo, hi;
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t lw = std::min<uint32_t>(128, w - 128 * j);
+      a[j] = join(slice(p, 128 * j, lw));
+      b[j] = join(slice(q, 128 * j, lw));
+    }
+    std::vector<std::vector<Ref>> col(n + 1);
+    for (uint32_t i = 0; i < n; ++i)
+      for (uint32_t j = 0; i + j < n; ++j) {
+        Ref pr = S.add(MGP_OP_MUL, 256, false, a[i], b[j]);
+        col[i + j].push_back(S.add(MGP_OP_EXTRACT, 128, false, pr, Ref(), Ref(), 0));
+        if (i + j + 1 < n) col[i + j + 1].push_back(S.add(MGP_OP_EXTRACT, 128, false, pr, Ref(), Ref(), 128));
+      }
+    Pieces limbs;
+    Ref carry;
+    bool have_carry = false;
+    for (uint32_t k = 0; k < n; ++k) {
+      Ref acc = col[k][0];
+      for (size_t t = 1; t < col[k].size(); ++t) acc = S.add(MGP_OP_ADD, 256, false, acc, col[k][t]);
+      if (have_carry) acc = S.add(MGP_OP_ADD, 256, false, acc, carry);
+      const uint32_t lw = std::min<uint32_t>(128, w - 128 * k);
+      limbs.push_back(Piece{S.add(MGP_OP_EXTRACT, (uint16_t)lw, false, acc, Ref(), Ref(), 0), lw});
+      if (k + 1 < n) {
+        carry = S.add(MGP_OP_EXTRACT, 128, false, acc, Ref(), Ref(), 128);
+        have_carry = true;
+      }
+    }
+    Pieces out;  // pairs of limbs -> 256-bit pieces
+    for (size_t k = 0; k < limbs.size(); k += 2) {
+      if (k + 1 < limbs.size()) out.push_back(Piece{join(Pieces{limbs[k], limbs[k + 1]}), limbs[k].w + limbs[k + 1].w});
+      else out.push_back(limbs[k]);
+    }
+    return out;
+  };
   // a w-bit value held in consecutive variables first, first+1, ... (low first)
   auto var_pieces = [&](uint32_t first, uint32_t w) -> Pieces {
     Pieces out;
@@ -336,6 +376,12 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           if (!opnd(nd.a) || !opnd(nd.b) || isb[nd.a] || isb[nd.b] || wid[nd.a] != w || wid[nd.b] != w)
             return unsupported();
           wide[i] = arith_pieces(op, wide[nd.a], wide[nd.b]);
+          break;
+        }
+        case MGP_OP_MUL: {
+          if (!opnd(nd.a) || !opnd(nd.b) || isb[nd.a] || isb[nd.b] || wid[nd.a] != w || wid[nd.b] != w)
+            return unsupported();
+          wide[i] = mul_pieces(wide[nd.a], wide[nd.b], w);
           break;
         }
         case MGP_OP_NOT: {

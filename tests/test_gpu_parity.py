@@ -135,10 +135,10 @@ def test_edge_values_all_ops(mgp_ctx):
 
 
 def test_unsupported_and_empty(mgp_ctx):
-    # a 512-bit multiply (not lowered for wide values) -> MGP_UNDECIDED,
+    # a 512-bit division (not lowered for wide values) -> MGP_UNDECIDED,
     # other states unaffected
     nl_bad = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.CONCAT, 512, 0, 1, -1, 0, 0],
-              [S.MUL, 512, 2, 2, -1, 0, 0], [S.EQ, 1, 3, 3, -1, 0, 0]]
+              [S.UDIV, 512, 2, 2, -1, 0, 0], [S.EQ, 1, 3, 3, -1, 0, 0]]
     nl_ok = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 1, -1, 0, 0]]
     nl_true = [[S.TRUE, 1, -1, -1, -1, 0, 0]]
     nl_false = [[S.FALSE, 1, -1, -1, -1, 0, 0]]

@@ -183,14 +183,15 @@ def test_wide_structural_ops():
 
 
 def wide_arith_cases():
-    """ADD / SUB (carry chains), bitwise ops and unsigned compares on 257..776-bit values
+    """ADD / SUB (carry chains), MUL (128-bit limb schoolbook), bitwise ops and unsigned
+    compares on 257..776-bit values
     built from 256-bit vars: BVAddNoOverflow's 257-bit expansion
     Extract(256, 256, ZeroExt(1, a) + ZeroExt(1, b)) == 0 among them."""
     states, rows = [], []
     rng = np.random.default_rng(11)
     edge = [0, 1, (1 << 256) - 1, (1 << 256) - 2, 1 << 255, (1 << 255) - 1, 5]
     for w in (257, 300, 512, 516, 776):
-        for op in (S.ADD, S.SUB, S.AND, S.OR, S.XOR, S.NOT):
+        for op in (S.ADD, S.SUB, S.MUL, S.AND, S.OR, S.XOR, S.NOT):
             for cmp in (S.EQ, S.ULT, S.ULE, S.UGT, S.UGE):
                 # a = ZeroExt / Concat of vars, b likewise, r = a op b, check cmp(r, c) and Extract(top bit)
                 k = w - 256
@@ -229,13 +230,31 @@ def test_wide_arith_and_compares():
 
 def test_wide_ops_left_unsupported():
     v0 = [S.VAR, 256, -1, -1, -1, 0, 0]
-    for op in (S.MUL, S.UDIV, S.SHL, S.SLT):
+    for op in (S.UDIV, S.UREM, S.SHL, S.LSHR, S.SLT):
         nl = [v0, [S.CONCAT, 512, 0, 0, -1, 0, 0],
               [op, 1 if op == S.SLT else 512, 1, 1, -1, 0, 0]]
         nl.append([S.BAND, 1, 2, 2, -1, 0, 0] if op == S.SLT else [S.EQ, 1, 2, 1, -1, 0, 0])
         nodes, noff, consts, coff = pack_states([(nl, [])])
         _, _, status = N.lower(nodes, noff, consts, coff)
         assert status[0] == N.ST_UNSUPPORTED, op
+
+
+def test_wide_mul_no_overflow_expansion():
+    # z3's expansion of BVMulNoOverflow(a, b, False) (bitvec_helper.py:188-199):
+    # Extract(511, 256, ZeroExt(256, a) * ZeroExt(256, b)) == 0, against UMUL_NOOVF itself
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0],
+          [S.ZEXT, 512, 0, -1, -1, 0, 0], [S.ZEXT, 512, 1, -1, -1, 0, 0], [S.MUL, 512, 2, 3, -1, 0, 0],
+          [S.EXTRACT, 256, 4, -1, -1, 511, 256], [S.CONST, 256, -1, -1, -1, 0, 0], [S.EQ, 1, 5, 6, -1, 0, 0],
+          [S.UMUL_NOOVF, 1, 0, 1, -1, 0, 0], [S.BEQ, 1, 7, 8, -1, 0, 0],
+          [S.EXTRACT, 256, 4, -1, -1, 255, 0], [S.MUL, 256, 0, 1, -1, 0, 0], [S.EQ, 1, 10, 11, -1, 0, 0],
+          [S.BAND, 1, 9, 12, -1, 0, 0]]
+    rng = np.random.default_rng(13)
+    rows = [[a, b] for a in INTERESTING for b in INTERESTING[::3]]
+    rows += [[int(rng.integers(0, 2 ** 63)) << int(rng.integers(0, 193)),
+              int(rng.integers(0, 2 ** 63)) << int(rng.integers(0, 193))] for _ in range(40)]
+    _, _, status = _check_states([(nl, [0])], [rows])
+    assert status[0] == N.ST_OK
+    assert all(S.eval_root(nl, [0], r) for r in rows)  # the expansion agrees with the predicate
 
 
 def wide_mapping_case():
@@ -282,7 +301,7 @@ def test_malformed_dags_are_unsupported(bad):
     v0 = [S.VAR, 256, -1, -1, -1, 0, 0]
     v1 = [S.VAR, 256, -1, -1, -1, 1, 0]
     nl = {
-        "wide": [v0, v1, [S.CONCAT, 512, 0, 1, -1, 0, 0], [S.MUL, 512, 2, 2, -1, 0, 0],
+        "wide": [v0, v1, [S.CONCAT, 512, 0, 1, -1, 0, 0], [S.UDIV, 512, 2, 2, -1, 0, 0],
                  [S.EXTRACT, 1, 3, -1, -1, 0, 0], [S.EQ, 1, 4, 4, -1, 0, 0]],
         "forward_ref": [v0, [S.ULT, 1, 0, 2, -1, 0, 0], v1],
         "bool_as_bv": [v0, [S.ULT, 1, 0, 0, -1, 0, 0], [S.ADD, 256, 0, 1, -1, 0, 0], [S.EQ, 1, 2, 0, -1, 0, 0]],

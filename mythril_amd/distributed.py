@@ -6,6 +6,13 @@ collective.  The single exchange step is gathering the per-state first-SAT
 words (and, on request, witnesses) to the host-owning rank — RCCL `gather`
 over xGMI with backend "nccl" (= RCCL on ROCm), `gloo` on CPU for tests.
 Keccak batches split into contiguous index ranges.
+
+Division-heavy DAGs cost ~10x a cheap one, so equal-count hash
+shards can leave one GPU with much more work.  `balanced_shards` is the
+rebalancing option of SURVEY.md §8e done without moving data after the fact:
+every rank holds the batch's per-state cost estimate (nominal ops,
+`_native.nominal_ops`) and computes the same cost-balanced assignment locally
+(sort by cost, snake order over ranks), so no collective is needed to agree.
 """
 from __future__ import annotations
 
@@ -37,6 +44,22 @@ def shard_of(state_ids: Sequence[int], world: int) -> np.ndarray:
 def local_indices(state_ids: Sequence[int], rank: int, world: int) -> np.ndarray:
     """Positions (into state_ids) of the states this rank evaluates."""
     return np.nonzero(shard_of(state_ids, world) == rank)[0]
+
+
+def balanced_shards(costs: Sequence[float], world: int) -> np.ndarray:
+    """Owning rank of each state so that per-rank cost sums are even.
+
+    States sorted by cost (descending, ties by index) are dealt to ranks in snake
+    order 0..W-1, W-1..0, ...; deterministic, so every rank computes the same map.
+    The heaviest rank exceeds the mean by at most the largest single cost.
+    """
+    c = np.asarray(costs, dtype=np.float64)
+    order = np.lexsort((np.arange(len(c)), -c))
+    pos = np.arange(len(c)) % (2 * world)
+    lane = np.where(pos < world, pos, 2 * world - 1 - pos)
+    owner = np.empty(len(c), dtype=np.int64)
+    owner[order] = lane
+    return owner
 
 
 def keccak_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
@@ -80,11 +103,16 @@ def gather_first_sat(local_idx: np.ndarray, local_first: np.ndarray, n_total: in
 
 
 def run_sharded(state_ids: Sequence[int], evaluate: Callable[[np.ndarray], np.ndarray], dst: int = 0,
-                device=None) -> Optional[np.ndarray]:
-    """Evaluate this rank's shard with `evaluate(positions) -> first_sat` and gather to `dst`."""
+                device=None, costs: Optional[Sequence[float]] = None) -> Optional[np.ndarray]:
+    """Evaluate this rank's shard with `evaluate(positions) -> first_sat` and gather to `dst`.
+
+    Shards are hash shards, or cost-balanced shards when per-state `costs` are given."""
     import torch.distributed as dist
 
     rank, world = dist.get_rank(), dist.get_world_size()
-    idx = local_indices(state_ids, rank, world)
+    if costs is not None:
+        idx = np.nonzero(balanced_shards(costs, world) == rank)[0]
+    else:
+        idx = local_indices(state_ids, rank, world)
     first = evaluate(idx) if len(idx) else np.zeros(0, dtype=np.int32)
     return gather_first_sat(idx, first, len(state_ids), dst=dst, device=device)

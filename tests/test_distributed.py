@@ -44,7 +44,7 @@ def _slice(b, cands, idx):
     return nodes, noff, consts, coff, np.ascontiguousarray(cands[idx])
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, balanced=False):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -55,7 +55,8 @@ def _worker(rank, world, port, out_path):
     def evaluate(idx):
         return coracle.first_sat(*_slice(b, cands, idx))
 
-    res = D.run_sharded(ids, evaluate, dst=0)
+    costs = N.nominal_ops(b["nodes"], b["node_offsets"]) if balanced else None
+    res = D.run_sharded(ids, evaluate, dst=0, costs=costs)
     if rank == 0:
         np.save(out_path, res)
     dist.barrier()
@@ -82,10 +83,24 @@ def test_keccak_ranges_cover_exactly():
             assert f0 + c0 == f1
 
 
+def test_cost_balanced_shards():
+    b = N.synth_generate(0x4D595448, 0, 4096, 64, 256)
+    costs = N.nominal_ops(b["nodes"], b["node_offsets"]).astype(np.float64)
+    for world in (1, 2, 4, 8):
+        owner = D.balanced_shards(costs, world)
+        assert owner.min() >= 0 and owner.max() < world
+        load = np.bincount(owner, weights=costs, minlength=world)
+        assert load.max() - load.mean() <= costs.max()
+        assert np.array_equal(owner, D.balanced_shards(costs, world)), "deterministic"
+        hash_load = np.bincount(D.shard_of(np.arange(4096), world), weights=costs, minlength=world)
+        assert load.max() <= hash_load.max()
+
+
 @pytest.mark.timeout(180)
-def test_two_rank_gather_matches_single_process(tmp_path):
+@pytest.mark.parametrize("balanced", [False, True])
+def test_two_rank_gather_matches_single_process(tmp_path, balanced):
     out = str(tmp_path / "gathered.npy")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), out, balanced), nprocs=2, join=True)
     got = np.load(out)
     b, cands = _batch()
     want = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)

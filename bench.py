@@ -62,6 +62,32 @@ def _slice_states(b, idx):
     return np.concatenate(nl), so, np.concatenate(cl).reshape(-1, 8), sco
 
 
+def _contract_states(n: int):
+    """n path-constraint lists shaped like BECToken's batchTransfer queries, built through the
+    laser.smt mirror: a calldata word (32 guarded byte selects, calldata.py:219-232), a
+    balances[msg.sender] read through keccak256_512 with the manager's condition
+    (keccak_function_manager.py:122-146) and the integer module's overflow query
+    (integer.py:141-160)."""
+    from mythril_amd.keccak import KeccakFunctionManager
+    from mythril_amd.smt import Array, BVMulNoOverflow, Concat, If, Not, UGE, UGT, ULE, ULT, symbol_factory
+
+    bvv, bvs = symbol_factory.BitVecVal, symbol_factory.BitVecSym
+    kfm = KeccakFunctionManager()
+    calldata, size = Array("calldata", 256, 8), bvs("calldatasize", 256)
+    storage = Array("Storage", 256, 256)
+    caller = bvs("caller", 256)
+    out = []
+    for k in range(n):
+        off = 4 + 32 * (k % 3)
+        word = Concat(*[If(ULT(bvv(off + i, 256), size), calldata[bvv(off + i, 256)], bvv(0, 8)) for i in range(32)])
+        value = bvs(f"value_{k % 11}", 256)
+        slot, cond = kfm.create_keccak(Concat(caller, bvv(k % 5, 256)))
+        path = [cond, UGT(word, bvv(0, 256)), ULE(word, bvv(20 + k % 7, 256)), UGE(storage[slot], word * value)]
+        query = Not(BVMulNoOverflow(word, value, False)) if k % 2 == 0 else ULT(storage[slot], bvv(k, 256))
+        out.append(tuple(c.raw for c in path + [query]))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -76,6 +102,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--refute-sample", type=int, default=1 << 17,
                     help="states of the rank-0 batch run through the host UNSAT pre-check (0 = skip)")
+    ap.add_argument("--frontend", type=int, default=1024,
+                    help="contract-shaped states through the full Prefilter front end (0 = skip)")
     ap.add_argument("--guided-sample", type=int, default=1 << 16,
                     help="open states of that sample given the domain-guided second witness round")
     args = ap.parse_args()
@@ -318,6 +346,27 @@ def main():
                              "second, domain-guided witness round as well)"}
         log(f"prefilter: {prefilter}")
 
+    # ------------------------------------------ front end (host + GPU) on contract-shaped states
+    # The product path of Constraints.is_possible / get_model for a batch: DAG build, lowering,
+    # candidates, GPU evaluation, pre-check, guided second round.  Not part of the timed step.
+    frontend = None
+    if rank == 0 and args.frontend > 0:
+        from mythril_amd import solver as SV
+
+        pf = SV.Prefilter(device=local)
+        cs = _contract_states(args.frontend)
+        pf.check_states(cs[:64])  # warm-up
+        tf = time.perf_counter()
+        res = pf.check_states(cs)
+        dtf = time.perf_counter() - tf
+        kinds = [r[0] for r in res]
+        frontend = {"states": len(cs), "seconds": dtf, "states_per_s": len(cs) / dtf,
+                    "sat": kinds.count(SV.sat), "unsat": kinds.count(SV.unsat),
+                    "undecided": kinds.count("undecided"), "candidates": pf.n_cand,
+                    "shape": "BECToken batchTransfer: calldata word, keccak256_512 mapping read, overflow query"}
+        pf.ctx.close()
+        log(f"frontend: {frontend}")
+
     # ---------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -360,6 +409,7 @@ def main():
             "results": {"sat_states": sat, "planted_states": int(len(pl)), "planted_found": planted_ok},
             "keccak": keccak,
             "prefilter": prefilter,
+            "frontend": frontend,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

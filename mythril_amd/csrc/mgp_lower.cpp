@@ -186,6 +186,21 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     }
     return e;
   };
+  // equality of two UF arguments known at lowering time: 1 equal, 0 different, -1 unknown.
+  // Constants are pooled by value, so two constant pieces are equal iff their pool
+  // indices are.  Concrete arguments (calldata / storage indices) are the common case,
+  // and folding them keeps the Ackermann chain from holding every earlier value live.
+  auto known_eq = [&](const Pieces &p, const Pieces &q) -> int {
+    if (p.size() != q.size()) return -1;
+    bool all = true;
+    for (size_t k = 0; k < p.size(); ++k) {
+      if (p[k].w != q[k].w) return -1;
+      if (p[k].r == q[k].r) continue;
+      if (p[k].r.k == R_CONST && q[k].r.k == R_CONST) return 0;
+      all = false;
+    }
+    return all ? 1 : -1;
+  };
   auto ite_pieces = [&](Ref c, const Pieces &p, const Pieces &q) -> Pieces {
     if (p.size() == 1 && q.size() == 1) return Pieces{Piece{S.add(MGP_OP_ITE, (uint16_t)p[0].w, false, c, p[0].r, q[0].r), p[0].w}};
     Pieces pa, qa, out;
@@ -527,7 +542,9 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         std::vector<UFApp> &fl = fapps[nd.p0];
         for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
           if (wid_of(it->arg) != wid[nd.a] || wid_of(it->val) != w) return unsupported();
-          v = ite_pieces(eq_pieces(arg, it->arg), it->val, v);
+          const int ke = known_eq(arg, it->arg);
+          if (ke == 0) continue;
+          v = (ke == 1) ? it->val : ite_pieces(eq_pieces(arg, it->arg), it->val, v);
         }
         fl.push_back(UFApp{arg, v});
         set_val(i, v);
@@ -543,12 +560,16 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         std::vector<UFApp> &fl = fapps[nd.p0];
         for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
           if (wid_of(it->val) != wid[nd.a] || wid_of(it->arg) != w) return unsupported();
-          v = ite_pieces(eq_pieces(arg, it->val), it->arg, v);
+          const int ke = known_eq(arg, it->val);
+          if (ke == 0) continue;
+          v = (ke == 1) ? it->arg : ite_pieces(eq_pieces(arg, it->val), it->arg, v);
         }
         std::vector<UFApp> &il = iapps[nd.p0];
         for (auto it = il.rbegin(); it != il.rend(); ++it) {
           if (wid_of(it->arg) != wid[nd.a] || wid_of(it->val) != w) return unsupported();
-          v = ite_pieces(eq_pieces(arg, it->arg), it->val, v);
+          const int ke = known_eq(arg, it->arg);
+          if (ke == 0) continue;
+          v = (ke == 1) ? it->val : ite_pieces(eq_pieces(arg, it->arg), it->val, v);
         }
         il.push_back(UFApp{arg, v});
         set_val(i, v);
@@ -849,18 +870,25 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
     // one needing the fewest LDS slots — occupancy is set by the slot count
     // (bench A/B: the DFS order alone saves stores but costs slots, 5 % slower).
     const uint32_t *cp = consts ? consts + c0 * 8u : nullptr;
+    // A schedule only counts if the gfx950 interpreter can also run it (its Bool
+    // budget is smaller than the bytecode's), so each candidate is translated too.
+    std::vector<uint32_t> uops;
     Lowered a = lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, sched_mode == 0 ? 0 : (sched_mode == 1 ? 0 : sched_mode - 1));
+    if (a.status == MGP_ST_OK && mgp_uop_translate(a.words.data(), uops) != 0) a = unsupported();
     if (sched_mode == 1) {
       for (int alt = 1; alt <= 2; ++alt) {
         Lowered b = lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, alt);
         const bool a_ok = a.status == MGP_ST_OK, b_ok = b.status == MGP_ST_OK;
-        if (b_ok && (!a_ok || b.words[2] < a.words[2])) a = std::move(b);
+        if (!b_ok || (a_ok && b.words[2] >= a.words[2])) continue;
+        std::vector<uint32_t> bu;
+        if (mgp_uop_translate(b.words.data(), bu) != 0) continue;
+        a = std::move(b);
+        uops.swap(bu);
       }
     }
     // append the uop program of the gfx950 interpreter; a state it cannot run
     // is made unsupported in both encodings so that both engines agree
-    std::vector<uint32_t> uops;
-    if (mgp_uop_translate(a.words.data(), uops) != 0) {
+    if (a.status != MGP_ST_OK) {
       a = unsupported();
       uops.clear();
       mgp_uop_translate(a.words.data(), uops);

@@ -175,6 +175,24 @@ def _to_limbs(v: int) -> List[int]:
     return [(v >> (32 * l)) & 0xFFFFFFFF for l in range(8)]
 
 
+_M256 = (1 << 256) - 1
+
+
+def _limbs_of(values: Sequence[int]) -> np.ndarray:
+    """ints -> uint32 [n, 8] little-endian limbs (low 256 bits)."""
+    if not values:
+        return np.zeros((0, 8), dtype=np.uint32)
+    b = b"".join((int(v) & _M256).to_bytes(32, "little") for v in values)
+    return np.frombuffer(b, dtype=np.uint32).reshape(-1, 8).copy()
+
+
+def _width_mask(w: int) -> np.ndarray:
+    return _limbs_of([(1 << min(w, 256)) - 1])[0]
+
+
+_FIXED_POOL = ACTORS + SPECIAL
+
+
 def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: int = 0x4D595448,
                     parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> np.ndarray:
     """uint32 [n_states, n_cand, n_vars, 8] candidate assignments (host layout of mgp_eval_batch).
@@ -182,78 +200,70 @@ def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: 
     c0 parent witness (if any), c1 first hint of every var, c2 = c1 with every
     x == y alias applied, then a seeded mixture per var: 35 % harvested hint,
     25 % pool (state constants +-1, actors, boundary values), 15 % alias of an
-    equal-width var, 25 % uniform.
+    equal-width var, 25 % uniform.  Vectorised over candidates (numpy), one pass
+    per variable.
     """
     rng = np.random.default_rng(seed)
-    out = rng.integers(0, 2 ** 32, size=(len(states), n_cand, n_vars, 8), dtype=np.uint64).astype(np.uint32)
+    out = rng.integers(0, 2 ** 32, size=(len(states), n_cand, n_vars, 8), dtype=np.uint32)
     for s, st in enumerate(states):
         V = st.n_vars
+        if V == 0:
+            continue
         widths = [w for (_, w) in st.vars]
-        pools: List[List[int]] = []
-        for vi, w in enumerate(widths):
-            m = (1 << w) - 1
-            pool = [v & m for v in st.consts] + [(v + 1) & m for v in st.consts] + [(v - 1) & m for v in st.consts]
-            pools.append(pool + [v & m for v in ACTORS + SPECIAL])
+        o = out[s]
+        pool_all = _limbs_of(list(st.consts) + [v + 1 for v in st.consts] + [v - 1 for v in st.consts]
+                             + list(_FIXED_POOL))
+        masks = {w: _width_mask(w) for w in set(widths)}
+        hint_limbs = {vi: _limbs_of(h) for vi, h in st.hints.items() if h}
         same_w: Dict[int, List[int]] = {}
         for vi, w in enumerate(widths):
             same_w.setdefault(w, []).append(vi)
-        # masks so that uniform values respect narrow widths
-        for vi, w in enumerate(widths):
-            if w < 256:
-                for l in range(8):
-                    lo = 32 * l
-                    mask = 0xFFFFFFFF if w >= lo + 32 else (0 if w <= lo else (1 << (w - lo)) - 1)
-                    out[s, :, vi, l] &= np.uint32(mask)
-        vals = np.zeros((n_cand, V), dtype=object)
-        have = np.zeros((n_cand, V), dtype=bool)
+        alias_src: Dict[int, List[int]] = {}
+        for (dst, src) in st.aliases:
+            alias_src.setdefault(dst, []).append(src)
         row = 0
         if parents is not None and parents[s]:
             for vi, (name, w) in enumerate(st.vars):
                 if name in parents[s]:
                     pv = parents[s][name]
                     for j in range((st.wide.get(vi, w) + 255) // 256):  # wide: its later slots too
-                        vals[0, vi + j] = (pv >> (256 * j)) & ((1 << st.vars[vi + j][1]) - 1)
-                        have[0, vi + j] = True
+                        o[0, vi + j] = _limbs_of([(pv >> (256 * j)) & ((1 << st.vars[vi + j][1]) - 1)])[0]
             row = 1
-        for structured in (False, True):
+        for structured in (False, True):  # first hints, then first hints with aliases applied
             if row >= n_cand:
                 break
-            for vi in range(V):
-                if st.hints.get(vi):
-                    vals[row, vi] = st.hints[vi][0]
-                    have[row, vi] = True
+            for vi, h in hint_limbs.items():
+                o[row, vi] = h[0]
             if structured:
                 for (dst, src) in st.aliases:
-                    if widths[dst] == widths[src] and have[row, src] and not have[row, dst]:
-                        vals[row, dst] = vals[row, src]
-                        have[row, dst] = True
+                    if widths[dst] == widths[src] and src in hint_limbs and dst not in hint_limbs:
+                        o[row, dst] = o[row, src]
             row += 1
-        for c in range(row, n_cand):
-            alias_todo = []
+        rest = n_cand - row
+        if rest > 0:
+            r = rng.random((rest, V))
+            alias_rows: Dict[int, np.ndarray] = {}
             for vi in range(V):
-                r = rng.random()
-                hv = st.hints.get(vi)
-                if r < 0.35 and hv:
-                    vals[c, vi] = hv[int(rng.integers(0, len(hv)))]
-                    have[c, vi] = True
-                elif r < 0.60 and pools[vi]:
-                    vals[c, vi] = pools[vi][int(rng.integers(0, len(pools[vi])))]
-                    have[c, vi] = True
-                elif r < 0.75:
-                    alias_todo.append(vi)
-            for vi in alias_todo:  # after the others, so an alias can copy any var
-                srcs = [u for (d_, u) in st.aliases if d_ == vi] or [u for u in same_w[widths[vi]] if u != vi]
+                h = hint_limbs.get(vi)
+                take_h = (r[:, vi] < 0.35) if h is not None else np.zeros(rest, dtype=bool)
+                take_p = ~take_h & (r[:, vi] < 0.60)
+                take_a = ~take_h & ~take_p & (r[:, vi] < 0.75)
+                k = int(take_h.sum())
+                if k:
+                    o[row:][take_h, vi] = h[rng.integers(0, len(h), size=k)]
+                k = int(take_p.sum())
+                if k and len(pool_all):
+                    o[row:][take_p, vi] = pool_all[rng.integers(0, len(pool_all), size=k)]
+                if take_a.any():
+                    alias_rows[vi] = np.nonzero(take_a)[0]
+            for vi, rows_a in alias_rows.items():  # after the others, so an alias can copy any var
+                srcs = alias_src.get(vi) or [u for u in same_w[widths[vi]] if u != vi]
                 if srcs:
-                    u = srcs[int(rng.integers(0, len(srcs)))]
-                    if have[c, u]:
-                        vals[c, vi] = vals[c, u]
-                    else:
-                        vals[c, vi] = int(sum(int(out[s, c, u, l]) << (32 * l) for l in range(8)))
-                    have[c, vi] = True
-        for c in range(n_cand):
-            for vi in range(V):
-                if have[c, vi]:
-                    out[s, c, vi] = _to_limbs(int(vals[c, vi]))
+                    pick = np.asarray(srcs)[rng.integers(0, len(srcs), size=len(rows_a))]
+                    o[row + rows_a, vi] = o[row + rows_a, pick]
+        for vi, w in enumerate(widths):
+            if w < 256:
+                o[:, vi] &= masks[w]
     return out
 
 

@@ -103,6 +103,42 @@ def test_uf_chains():
     _check_states([(nl, [])], [rows])
 
 
+def test_uf_constant_arguments_fold():
+    # a 32-byte calldata word: 32 selects at constant indices (calldata.py:219-232), one
+    # index repeated and one symbolic index read first; constant-vs-constant argument comparisons fold
+    # at lowering time, so the state fits the slot budget and agrees with the oracle
+    F = 3
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.UFAPP, 8, 0, -1, -1, F, 40]]   # x0, calldata[x0]
+    sym = 1
+    consts = list(range(4, 36)) + [7]
+    apps = []
+    for i, ci in enumerate(list(range(32)) + [32]):               # last app repeats index 7
+        nl.append([S.CONST, 256, -1, -1, -1, ci, 0])
+        nl.append([S.UFAPP, 8, len(nl) - 1, -1, -1, F, 1 + i])
+        apps.append(len(nl) - 1)
+    acc = apps[0]
+    for a in apps[1:32]:
+        nl.append([S.CONCAT, nl[acc][1] + 8, acc, a, -1, 0, 0])
+        acc = len(nl) - 1
+    nl.append([S.EQ, 1, apps[32], apps[3], -1, 0, 0])               # f(7) twice: always equal
+    e_rep = len(nl) - 1
+    nl.append([S.EQ, 1, sym, apps[5], -1, 0, 0])                     # f(x0) == f(9)
+    e_sym = len(nl) - 1
+    nl.append([S.EXTRACT, 8, acc, -1, -1, 7, 0])
+    nl.append([S.EQ, 1, len(nl) - 1, apps[31], -1, 0, 0])            # low byte is f(35)
+    nl.append([S.BAND, 1, e_rep, len(nl) - 1, -1, 0, 0])
+    nl.append([S.BAND, 1, len(nl) - 1, e_sym, -1, 0, 0])
+    rng = np.random.default_rng(17)
+    rows = []
+    for _ in range(40):
+        xs = [int(rng.integers(0, 40))] + [int(rng.integers(0, 4)) for _ in range(41)]
+        rows.append(xs)
+    rows.append([9] + [1] * 41)
+    _, _, status = _check_states([(nl, consts)], [rows])
+    assert status[0] == N.ST_OK
+    assert S.eval_root(nl, consts, [9] + [1] * 41)
+
+
 def _live_chain(n):
     # n values each used by two chains that consume them in opposite orders:
     # whatever the schedule, all n are live at once

@@ -469,11 +469,43 @@ struct State {
         const uint8_t cur = cmp_dom[i] == 1 ? p.s : p.u;
         if (!meetb((int32_t)i, (uint8_t)(((cur & t) ? BT : 0) | ((cur & f) ? BF : 0)))) return false;
       }
-    for (const Pair &p : pairs)  // known equal: the operands share one value
-      if (p.u == OEQ) {
+    // a true Or of two compares on one operand pair (the Or(ULT, ==) expansion of ULE /
+    // UGE, bitvec_helper.py:53-80) allows only the union of their orderings
+    for (uint32_t i = 0; i < n; ++i) {
+      if (nd[i].op != MGP_OP_BOR || bs[i] != BT) continue;
+      const int32_t a = nd[i].a, b = nd[i].b;
+      const int32_t pa = cmp_pair[a], pb = cmp_pair[b];
+      if (pa < 0 || pa != pb) continue;
+      const uint8_t da = cmp_dom[a], db = cmp_dom[b];
+      if (da != db && da != 2 && db != 2) continue;  // signed with unsigned: no common set
+      const uint8_t dom = da == 2 ? db : da;
+      if (!set_order(pairs[pa], dom, (uint8_t)(cmp_t[a] | cmp_t[b]))) return false;
+    }
+    for (const Pair &p : pairs) {
+      if (p.u == OEQ) {  // known equal: the operands share one value
         const AV ax = av[p.x], ay = av[p.y];
         if (!meet(p.x, ay) || !meet(p.y, ax)) return false;
+        continue;
       }
+      // known unsigned order: x <= y (or x < y) bounds x from above by y.hi and y from
+      // below by x.lo (ULE / UGE arrive as Or(ULT, ==), bitvec_helper.py:53-80, whose
+      // operands the per-node backward pass cannot narrow)
+      const bool le = !(p.u & OGT), ge = !(p.u & OLT);
+      if (le == ge) continue;
+      const int32_t lo_n = le ? p.x : p.y, hi_n = le ? p.y : p.x;  // lo_n <= hi_n
+      const bool strict = (p.u & OEQ) == 0;
+      const uint32_t w = nd[lo_n].width;
+      if (w == 0u || w != nd[hi_n].width) continue;
+      AV a = top(w), b = top(w);
+      a.hi = av[hi_n].hi;
+      b.lo = av[lo_n].lo;
+      if (strict) {
+        if (Z(a.hi) || EQV(b.lo, M(w))) return false;
+        a.hi = SUBV(a.hi, ONE());
+        b.lo = ADDV(b.lo, ONE());
+      }
+      if (!meet(lo_n, a) || !meet(hi_n, b)) return false;
+    }
     return true;
   }
 
@@ -840,6 +872,18 @@ struct State {
       }
       case MGP_OP_NOT: return meet(x.a, av_not(R, w));
       case MGP_OP_NEG: return meet(x.a, av_sub(exact(bv_zero(), w), R, w));
+      case MGP_OP_UREM: {
+        // x % 2^k (k < w) is x's low k bits: the result's known bits below 2^k are x's
+        // (URem(hash, 64) == 0, keccak_function_manager.py:139)
+        const AV B = av[x.b];
+        if (!is_exact(B) || Z(B.lo)) return true;
+        const V m1 = SUBV(B.lo, ONE());
+        if (!Z(AND(B.lo, m1))) return true;  // not a power of two
+        AV ta = top(w);
+        ta.z = OR(ta.z, AND(R.z, m1));
+        ta.o = AND(R.o, m1);
+        return meet(x.a, ta);
+      }
       case MGP_OP_AND: {
         const AV A = av[x.a], B = av[x.b];
         AV ta = top(w), tb = top(w);
@@ -972,7 +1016,15 @@ bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out) {
     mgp_node &x = out[i];
     if (wide((int32_t)i)) { fresh_var(x, 8); continue; }
     if (!(wide(nd[i].a) || wide(nd[i].b) || wide(nd[i].c))) continue;
-    if (op_bool_result(nd[i].op)) {
+    if ((nd[i].op == MGP_OP_UFAPP || nd[i].op == MGP_OP_UFINV) && nd[i].width <= MGP_MAX_WIDTH) {
+      // a narrow UF value read through a wide argument: relaxed to its own fresh-value
+      // variable p1 (used by no other node, so still unconstrained), which keeps the
+      // constraints on the value attached to the slot the kernel reads it from
+      x.op = MGP_OP_VAR;
+      x.a = x.b = x.c = -1;
+      x.p0 = nd[i].p1;
+      x.p1 = 0;
+    } else if (op_bool_result(nd[i].op)) {
       // operands are relaxed placeholders (8-bit fresh variables, distinct unless a == b)
       x.op = MGP_OP_EQ;
       x.width = 1;

@@ -242,25 +242,31 @@ def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: 
         rest = n_cand - row
         if rest > 0:
             r = rng.random((rest, V))
-            alias_rows: Dict[int, np.ndarray] = {}
-            for vi in range(V):
-                h = hint_limbs.get(vi)
-                take_h = (r[:, vi] < 0.35) if h is not None else np.zeros(rest, dtype=bool)
-                take_p = ~take_h & (r[:, vi] < 0.60)
-                take_a = ~take_h & ~take_p & (r[:, vi] < 0.75)
-                k = int(take_h.sum())
-                if k:
-                    o[row:][take_h, vi] = h[rng.integers(0, len(h), size=k)]
-                k = int(take_p.sum())
-                if k and len(pool_all):
-                    o[row:][take_p, vi] = pool_all[rng.integers(0, len(pool_all), size=k)]
-                if take_a.any():
-                    alias_rows[vi] = np.nonzero(take_a)[0]
-            for vi, rows_a in alias_rows.items():  # after the others, so an alias can copy any var
-                srcs = alias_src.get(vi) or [u for u in same_w[widths[vi]] if u != vi]
-                if srcs:
-                    pick = np.asarray(srcs)[rng.integers(0, len(srcs), size=len(rows_a))]
-                    o[row + rows_a, vi] = o[row + rows_a, pick]
+            u = rng.random((rest, V))
+            blk = o[row:]
+            # hints: one table for all vars, a per-(row, var) draw from that var's slice
+            h_len = np.array([len(hint_limbs[vi]) if vi in hint_limbs else 0 for vi in range(V)], dtype=np.int64)
+            take_h = (r < 0.35) & (h_len > 0)[None, :]
+            take_p = ~take_h & (r < 0.60)
+            take_a = ~take_h & ~take_p & (r < 0.75)
+            if take_h.any():
+                h_tab = np.concatenate([hint_limbs[vi] for vi in range(V) if vi in hint_limbs])
+                h_off = np.concatenate([[0], np.cumsum(h_len)[:-1]])
+                rows_h, vars_h = np.nonzero(take_h)
+                pick = h_off[vars_h] + (u[rows_h, vars_h] * h_len[vars_h]).astype(np.int64)
+                blk[rows_h, vars_h] = h_tab[pick]
+            if take_p.any() and len(pool_all):
+                rows_p, vars_p = np.nonzero(take_p)
+                blk[rows_p, vars_p] = pool_all[(u[rows_p, vars_p] * len(pool_all)).astype(np.int64)]
+            if take_a.any():  # after the others, so an alias copies a var's hint / pool / uniform value
+                srcs = [alias_src.get(vi) or [x for x in same_w[widths[vi]] if x != vi] for vi in range(V)]
+                n_src = np.array([len(x) for x in srcs], dtype=np.int64)
+                tab = np.zeros((V, max(1, int(n_src.max()))), dtype=np.int64)
+                for vi, x in enumerate(srcs):
+                    tab[vi, : len(x)] = x
+                rows_a, vars_a = np.nonzero(take_a & (n_src > 0)[None, :])
+                src = tab[vars_a, (u[rows_a, vars_a] * n_src[vars_a]).astype(np.int64)]
+                blk[rows_a, vars_a] = blk[rows_a, src].copy()
         for vi, w in enumerate(widths):
             if w < 256:
                 o[:, vi] &= masks[w]

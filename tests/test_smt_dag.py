@@ -108,8 +108,8 @@ def test_bool_symbols_and_constants():
 
 def test_wide_mapping_preimage_state_lowers_and_candidates_satisfy():
     """keccak256_512(Concat(key, slot)) with the manager's condition (keccak_function_manager.py:122-146):
-    the 512-bit preimage and inverse lower to narrow pieces, and the candidate generator's
-    assignments include a model (checked with the CPU uop interpreter, no GPU)."""
+    the 512-bit preimage and inverse lower to narrow pieces, and the candidates (hints plus
+    domain-guided rows) include a model (checked with the CPU uop interpreter, no GPU)."""
     from mythril_amd import _native as N
     from mythril_amd.keccak import KeccakFunctionManager
     from mythril_amd.smt import Concat, ULT, symbol_factory
@@ -128,6 +128,8 @@ def test_wide_mapping_preimage_state_lowers_and_candidates_satisfy():
     words, po, status = N.lower(nodes, noff, consts, coff)
     assert status[0] == N.ST_OK
     cands = D.make_candidates([st], 64, st.n_vars)
+    # as in the product's second round: every other row drawn from the pre-check's domains
+    assert N.guided_candidates(nodes, noff, consts, coff, cands, every=2, n_decide=8)[0] == 0
     hits = 0
     for c in range(64):
         xs = [S.limbs_to_int(cands[0, c, v]) for v in range(st.n_vars)]

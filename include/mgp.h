@@ -193,6 +193,24 @@ int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets,
                           uint32_t every, uint32_t n_decide, uint32_t *cands,
                           int8_t *out);
 
+/* Candidate assignments for the first witness round (host, OpenMP over states):
+ * per state, row 0 is left for the parent witness when has_parent[s], then the
+ * first hint of every variable, that row with the x == y aliases applied, then
+ * a seeded mixture per variable (35 % hint, 25 % pool = constants, +-1, the
+ * fixed pool; 15 % alias of an equal-width variable; 25 % uniform), masked to
+ * the slot width.  Variables of state s are var_off[s]..var_off[s+1]; hints of
+ * variable v are rows hint_off[v]..hint_off[v+1] of `hints` (8 limbs each);
+ * aliases are (dst, src) pairs of state-local indices; consts as for
+ * mgp_lower.  out: [n_states][n_cand][n_vars][8], the host layout of
+ * mgp_eval_batch.  Deterministic in seed, independent of the thread count. */
+int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
+                        const uint64_t *var_off, const uint32_t *var_width,
+                        const uint64_t *hint_off, const uint32_t *hints,
+                        const uint64_t *alias_off, const uint32_t *aliases,
+                        const uint64_t *const_off, const uint32_t *consts,
+                        const uint32_t *fixed_pool, uint32_t n_fixed,
+                        const uint8_t *has_parent, uint32_t *out);
+
 /* ---------------------------------------------------------- Keccak-256
  * n preimages of len bytes each, preimage i at in + i*stride; 32-byte
  * big-endian digests to out32 + 32*i.  Keccak-256 = Keccak[r=1088,c=512]

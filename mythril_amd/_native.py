@@ -89,6 +89,8 @@ def _bind(lib):
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
         "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
+        "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P,
+                                               _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -139,6 +141,7 @@ EXPORTED_SYMBOLS = (
     "mgp_refute",
     "mgp_refute_trace",
     "mgp_guided_candidates",
+    "mgp_make_candidates",
 )
 
 ENGINE_HIP, ENGINE_ASM = 1, 2
@@ -204,6 +207,24 @@ def lower(
         _check(rc)
         return words[: int(used.value)], prog_offsets, status[:n_states]
     raise MgpError(MGP_E_CAPACITY, "lowering capacity")
+
+
+def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hint_off, hints, alias_off, aliases,
+                    const_off, consts, fixed_pool, has_parent) -> np.ndarray:
+    """mgp_make_candidates over flattened per-state tables -> uint32 [n_states, n_cand, n_vars, 8]."""
+    def u(a, dt):
+        a = np.ascontiguousarray(a, dtype=dt)
+        return a if a.size else np.zeros(8, dtype=dt)
+    n_states = len(var_off) - 1
+    out = np.empty((n_states, n_cand, n_vars, 8), dtype=np.uint32)
+    fixed = u(fixed_pool, np.uint32)
+    _check(lib().mgp_make_candidates(n_states, n_cand, n_vars, seed & (2 ** 64 - 1), _ptr(u(var_off, np.uint64)),
+                                     _ptr(u(var_width, np.uint32)), _ptr(u(hint_off, np.uint64)),
+                                     _ptr(u(hints, np.uint32)), _ptr(u(alias_off, np.uint64)),
+                                     _ptr(u(aliases, np.uint32)), _ptr(u(const_off, np.uint64)),
+                                     _ptr(u(consts, np.uint32)), _ptr(fixed), len(fixed_pool),
+                                     _ptr(u(has_parent, np.uint8)), _ptr(out)))
+    return out
 
 
 def guided_candidates(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,

@@ -193,6 +193,9 @@ def _width_mask(w: int) -> np.ndarray:
 _FIXED_POOL = ACTORS + SPECIAL
 
 
+_FIXED_LIMBS = _limbs_of(list(_FIXED_POOL))
+
+
 def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: int = 0x4D595448,
                     parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> np.ndarray:
     """uint32 [n_states, n_cand, n_vars, 8] candidate assignments (host layout of mgp_eval_batch).
@@ -200,76 +203,46 @@ def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: 
     c0 parent witness (if any), c1 first hint of every var, c2 = c1 with every
     x == y alias applied, then a seeded mixture per var: 35 % harvested hint,
     25 % pool (state constants +-1, actors, boundary values), 15 % alias of an
-    equal-width var, 25 % uniform.  Vectorised over candidates (numpy), one pass
-    per variable.
+    equal-width var, 25 % uniform.  Generated natively (mgp_make_candidates,
+    OpenMP over states) from the flattened per-state tables built here.
     """
-    rng = np.random.default_rng(seed)
-    out = rng.integers(0, 2 ** 32, size=(len(states), n_cand, n_vars, 8), dtype=np.uint32)
+    from . import _native as N
+
+    n = len(states)
+    var_off = np.zeros(n + 1, np.uint64)
+    const_off = np.zeros(n + 1, np.uint64)
+    alias_off = np.zeros(n + 1, np.uint64)
+    widths: List[int] = []
+    hint_counts: List[int] = []
+    hint_vals: List[int] = []
+    alias_pairs: List[Tuple[int, int]] = []
+    const_vals: List[int] = []
     for s, st in enumerate(states):
-        V = st.n_vars
-        if V == 0:
-            continue
-        widths = [w for (_, w) in st.vars]
-        o = out[s]
-        pool_all = _limbs_of(list(st.consts) + [v + 1 for v in st.consts] + [v - 1 for v in st.consts]
-                             + list(_FIXED_POOL))
-        masks = {w: _width_mask(w) for w in set(widths)}
-        hint_limbs = {vi: _limbs_of(h) for vi, h in st.hints.items() if h}
-        same_w: Dict[int, List[int]] = {}
-        for vi, w in enumerate(widths):
-            same_w.setdefault(w, []).append(vi)
-        alias_src: Dict[int, List[int]] = {}
-        for (dst, src) in st.aliases:
-            alias_src.setdefault(dst, []).append(src)
-        row = 0
-        if parents is not None and parents[s]:
+        widths.extend(w for (_, w) in st.vars)
+        for vi in range(st.n_vars):
+            h = st.hints.get(vi) or ()
+            hint_counts.append(len(h))
+            hint_vals.extend(h)
+        alias_pairs.extend(st.aliases)
+        const_vals.extend(st.consts)
+        var_off[s + 1] = len(widths)
+        alias_off[s + 1] = len(alias_pairs)
+        const_off[s + 1] = len(const_vals)
+    hint_off = np.zeros(len(hint_counts) + 1, np.uint64)
+    hint_off[1:] = np.cumsum(hint_counts)
+    has_parent = np.array([bool(parents is not None and parents[s]) for s in range(n)], dtype=np.uint8)
+    out = N.make_candidates(n_cand, n_vars, seed, var_off, np.array(widths, np.uint32), hint_off,
+                            _limbs_of(hint_vals), alias_off, np.array(alias_pairs, np.uint32).reshape(-1, 2),
+                            const_off, _limbs_of(const_vals), _FIXED_LIMBS, has_parent)
+    if parents is not None:
+        for s, st in enumerate(states):
+            if not parents[s] or n_cand == 0:
+                continue
             for vi, (name, w) in enumerate(st.vars):
                 if name in parents[s]:
                     pv = parents[s][name]
                     for j in range((st.wide.get(vi, w) + 255) // 256):  # wide: its later slots too
-                        o[0, vi + j] = _limbs_of([(pv >> (256 * j)) & ((1 << st.vars[vi + j][1]) - 1)])[0]
-            row = 1
-        for structured in (False, True):  # first hints, then first hints with aliases applied
-            if row >= n_cand:
-                break
-            for vi, h in hint_limbs.items():
-                o[row, vi] = h[0]
-            if structured:
-                for (dst, src) in st.aliases:
-                    if widths[dst] == widths[src] and src in hint_limbs and dst not in hint_limbs:
-                        o[row, dst] = o[row, src]
-            row += 1
-        rest = n_cand - row
-        if rest > 0:
-            r = rng.random((rest, V))
-            u = rng.random((rest, V))
-            blk = o[row:]
-            # hints: one table for all vars, a per-(row, var) draw from that var's slice
-            h_len = np.array([len(hint_limbs[vi]) if vi in hint_limbs else 0 for vi in range(V)], dtype=np.int64)
-            take_h = (r < 0.35) & (h_len > 0)[None, :]
-            take_p = ~take_h & (r < 0.60)
-            take_a = ~take_h & ~take_p & (r < 0.75)
-            if take_h.any():
-                h_tab = np.concatenate([hint_limbs[vi] for vi in range(V) if vi in hint_limbs])
-                h_off = np.concatenate([[0], np.cumsum(h_len)[:-1]])
-                rows_h, vars_h = np.nonzero(take_h)
-                pick = h_off[vars_h] + (u[rows_h, vars_h] * h_len[vars_h]).astype(np.int64)
-                blk[rows_h, vars_h] = h_tab[pick]
-            if take_p.any() and len(pool_all):
-                rows_p, vars_p = np.nonzero(take_p)
-                blk[rows_p, vars_p] = pool_all[(u[rows_p, vars_p] * len(pool_all)).astype(np.int64)]
-            if take_a.any():  # after the others, so an alias copies a var's hint / pool / uniform value
-                srcs = [alias_src.get(vi) or [x for x in same_w[widths[vi]] if x != vi] for vi in range(V)]
-                n_src = np.array([len(x) for x in srcs], dtype=np.int64)
-                tab = np.zeros((V, max(1, int(n_src.max()))), dtype=np.int64)
-                for vi, x in enumerate(srcs):
-                    tab[vi, : len(x)] = x
-                rows_a, vars_a = np.nonzero(take_a & (n_src > 0)[None, :])
-                src = tab[vars_a, (u[rows_a, vars_a] * n_src[vars_a]).astype(np.int64)]
-                blk[rows_a, vars_a] = blk[rows_a, src].copy()
-        for vi, w in enumerate(widths):
-            if w < 256:
-                o[:, vi] &= masks[w]
+                        out[s, 0, vi + j] = _limbs_of([(pv >> (256 * j)) & ((1 << st.vars[vi + j][1]) - 1)])[0]
     return out
 
 

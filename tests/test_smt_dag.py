@@ -140,3 +140,25 @@ def test_wide_mapping_preimage_state_lowers_and_candidates_satisfy():
     model = D.witness_to_model(st, cands[0, 0])
     assert D.model_to_slots(st, model) == [S.limbs_to_int(cands[0, 0, v]) & ((1 << st.vars[v][1]) - 1)
                                            for v in range(st.n_vars)]
+
+
+def test_native_candidates_layout_and_rows():
+    """mgp_make_candidates (via dag.make_candidates): parent row, hint row, alias row,
+    width masks, determinism in the seed."""
+    from mythril_amd.smt import symbol_factory as sf
+    x8, y8, z = sf.BitVecSym("x8", 8), sf.BitVecSym("y8", 8), sf.BitVecSym("z", 256)
+    st = D.build_state([(x8 == sf.BitVecVal(0x41, 8)).raw, (x8 == y8).raw, ULT(z, sf.BitVecVal(1000, 256)).raw])
+    names = [n for (n, _) in st.vars]
+    ix, iy, iz = names.index("x8"), names.index("y8"), names.index("z")
+    a = D.make_candidates([st], 64, st.n_vars, seed=9)
+    b = D.make_candidates([st], 64, st.n_vars, seed=9)
+    assert np.array_equal(a, b)
+    assert not np.array_equal(a, D.make_candidates([st], 64, st.n_vars, seed=10))
+    assert (a[0, :, ix, 1:] == 0).all() and (a[0, :, ix, 0] <= 0xFF).all()  # 8-bit slots masked
+    assert a[0, 0, ix, 0] == 0x41                                           # first hint row
+    assert a[0, 1, iy, 0] == 0x41                                           # alias row: y8 := x8
+    assert S.limbs_to_int(a[0, 0, iz]) in st.hints[iz]
+    p = D.make_candidates([st], 64, st.n_vars, seed=9, parents=[{"z": 7, "x8": 0x41}])
+    assert S.limbs_to_int(p[0, 0, iz]) == 7 and p[0, 0, ix, 0] == 0x41 and p[0, 1, ix, 0] == 0x41
+    assert sum(S.eval_root(st.nodes, st.consts, [S.limbs_to_int(a[0, c, v]) for v in range(st.n_vars)])
+               for c in range(64)) > 0

@@ -67,9 +67,11 @@ def _contract_states(n: int):
     laser.smt mirror: a calldata word (32 guarded byte selects, calldata.py:219-232), a
     balances[msg.sender] read through keccak256_512 with the manager's condition
     (keccak_function_manager.py:122-146) and the integer module's overflow query
-    (integer.py:141-160)."""
+    (integer.py:141-160); every fourth state asks SafeMath.sub's underflow query, which
+    the balance check makes UNSAT (integer.py:155-160)."""
     from mythril_amd.keccak import KeccakFunctionManager
-    from mythril_amd.smt import Array, BVMulNoOverflow, Concat, If, Not, UGE, UGT, ULE, ULT, symbol_factory
+    from mythril_amd.smt import (Array, BVMulNoOverflow, BVSubNoUnderflow, Concat, If, Not, UGE, UGT, ULE, ULT,
+                                 symbol_factory)
 
     bvv, bvs = symbol_factory.BitVecVal, symbol_factory.BitVecSym
     kfm = KeccakFunctionManager()
@@ -83,7 +85,10 @@ def _contract_states(n: int):
         value = bvs(f"value_{k % 11}", 256)
         slot, cond = kfm.create_keccak(Concat(caller, bvv(k % 5, 256)))
         path = [cond, UGT(word, bvv(0, 256)), ULE(word, bvv(20 + k % 7, 256)), UGE(storage[slot], word * value)]
-        query = Not(BVMulNoOverflow(word, value, False)) if k % 2 == 0 else ULT(storage[slot], bvv(k, 256))
+        if k % 4 == 3:  # SafeMath.sub after require(balance >= amount): the underflow query is UNSAT
+            query = Not(BVSubNoUnderflow(storage[slot], word * value, False))
+        else:
+            query = Not(BVMulNoOverflow(word, value, False)) if k % 2 == 0 else ULT(storage[slot], bvv(k, 256))
         out.append(tuple(c.raw for c in path + [query]))
     return out
 
@@ -363,7 +368,7 @@ def main():
         frontend = {"states": len(cs), "seconds": dtf, "states_per_s": len(cs) / dtf,
                     "sat": kinds.count(SV.sat), "unsat": kinds.count(SV.unsat),
                     "undecided": kinds.count("undecided"), "candidates": pf.n_cand,
-                    "shape": "BECToken batchTransfer: calldata word, keccak256_512 mapping read, overflow query"}
+                    "shape": "BECToken batchTransfer: calldata word, keccak256_512 mapping read, overflow / underflow query"}
         pf.ctx.close()
         log(f"frontend: {frontend}")
 

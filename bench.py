@@ -6,15 +6,23 @@ synthetic batch resident in HBM: n_states x n_cand candidate-model evaluations
 (2^20 states x 64-op-node 256-bit DAGs x 256
 candidates per GPU), followed by the first-SAT reduction and — for N > 1 — the
 RCCL gather of the per-state first-SAT words to rank 0.  Weak scaling: every
-rank owns its own 2^20 hash-shard of states (state ids rank*2^20 + i).
+rank owns its own contiguous 2^20-state id range (state ids rank*2^20 + i).
 
 Printed (rank 0, one JSON line): whole-job candidate-model evals/s, the
 roofline object of the eval kernel (INT32 VALU bound: nominal ops from the
-committed per-op table / measured kernel time vs 39.3 Tops/s), its HBM
-fraction, the CPU baseline (oracle/c restatement, OpenMP over the host cores,
-timed on a bounded sample), and the batched Keccak-256 line (config 5).
+committed per-op table / measured kernel time, priced against the measured
+v_add_u32 probe and, as `frac_spec`, against the 78.6 Tops/s spec peak), its
+HBM fraction, the CPU baseline (oracle/c restatement, OpenMP over the host
+cores, timed on a bounded sample whose first-SAT words must equal the GPU's),
+and the batched Keccak-256 line (config 5; the first 65 536 digests and a
+1-in-2^20 sample of the rest are checked against the oracle).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--states S] [--cand C]
+
+With --gpus N > 1 and no torchrun environment, bench.py launches N ranks itself
+(torch.distributed.run on 127.0.0.1, before any GPU call) and exits with their
+status.  --dry-run replaces the GPU work by a CPU pass over the same shards on
+gloo (launcher / rank plumbing test).
 """
 from __future__ import annotations
 
@@ -22,6 +30,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -111,7 +121,15 @@ def main():
                     help="contract-shaped states through the full Prefilter front end (0 = skip)")
     ap.add_argument("--guided-sample", type=int, default=1 << 16,
                     help="open states of that sample given the domain-guided second witness round")
+    ap.add_argument("--keccak-sample-every", type=int, default=1 << 20,
+                    help="beyond the first 65 536, check one digest in this many against the oracle")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo ranks run the shard plumbing on CPU and rank 0 prints one line")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launched without torchrun: start the N ranks here, before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -121,10 +139,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()  # the world RCCL actually formed
     N.lib()  # loud failure if the HIP library is missing
 
     # ---------------------------------------------------------- workload
@@ -267,6 +290,14 @@ def main():
             kel = float(t.item())
         kms = float(np.mean([a.elapsed_time(bb) for a, bb in kevs]))
         k_rate = world * nk * ksteps / kel
+        k_verified = verify_keccak(d_pre, d_dig, kfirst, nk, args.keccak_sample_every)
+        if world > 1:
+            t = torch.tensor([k_verified["checked"], k_verified["mismatches"]], dtype=torch.int64, device=dev)
+            dist.all_reduce(t)
+            k_verified.update(checked=int(t[0]), mismatches=int(t[1]), ranks=world)
+        log(f"keccak verification: {k_verified}")
+        if k_verified["mismatches"]:
+            raise RuntimeError(f"keccak digests differ from the oracle: {k_verified}")
         k_tops = chunk * KECCAK_OPS_PER_HASH / (kms * 1e-3) / 1e12
         k_gbs = chunk * KECCAK_BYTES_PER_HASH / (kms * 1e-3) / 1e9
         # HBM bytes and issued VALU lane-ops per hash from the committed rocprofv3 PMC run
@@ -299,6 +330,7 @@ def main():
                                 "frac can pass 1 -- valu_issued is the instruction-level figure",
                          "kernel": "mgp_keccak64_kernel", "launch_ms": kms, "hashes_per_launch": chunk},
             "valu_issued": k_issued,
+            "verified": k_verified,
             "roofline_hbm": {"achieved": k_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k_gbs / HBM_PEAK_GBS},
         }
         del d_pre, d_dig
@@ -360,13 +392,17 @@ def main():
 
         pf = SV.Prefilter(device=local)
         cs = _contract_states(args.frontend)
-        pf.check_states(cs[:64])  # warm-up
+        pf.check_states(cs[:64])  # warm-up (kernels loaded, host pools touched)
+        SV.unsat_cores().reset()  # cold: no UNSAT core from the warm-up answers the timed run
+        SV.SolverStatistics().reset()
         tf = time.perf_counter()
         res = pf.check_states(cs)
         dtf = time.perf_counter() - tf
         kinds = [r[0] for r in res]
+        st = SV.SolverStatistics()
         frontend = {"states": len(cs), "seconds": dtf, "states_per_s": len(cs) / dtf,
                     "sat": kinds.count(SV.sat), "unsat": kinds.count(SV.unsat),
+                    "refuted": st.refuted, "core_hits": st.core_hits,
                     "undecided": kinds.count("undecided"), "candidates": pf.n_cand,
                     "shape": "BECToken batchTransfer: calldata word, keccak256_512 mapping read, overflow / underflow query"}
         pf.ctx.close()
@@ -375,7 +411,8 @@ def main():
     # ---------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and not args.no_cpu:
-        cpu = cpu_baseline(b, d_cands, n_states, n_cand, n_vars, args.cpu_seconds, evals_rank / (kern_ms * 1e-3))
+        cpu = cpu_baseline(b, d_cands, n_states, n_cand, n_vars, args.cpu_seconds, evals_rank / (kern_ms * 1e-3),
+                           first, status)
         if keccak is not None:
             keccak["cpu_baseline"] = cpu_keccak(args.cpu_seconds / 2)
 
@@ -397,11 +434,13 @@ def main():
                 "workload": "synthetic: 1M states x 64-node 256-bit constraint DAGs x 256 candidate assignments"
                 if n_states == 1 << 20 and n_cand == 256 else f"synthetic: {n_states} states x {n_nodes} nodes x {n_cand} cand",
                 "states_per_gpu": n_states, "candidates": n_cand, "op_nodes": n_nodes, "n_vars": n_vars,
-                "parallelism": f"dp{world} (state hash-shards, RCCL gather of first-SAT)",
+                "parallelism": f"dp{world} (contiguous state-id shards, {n_states} per rank; RCCL gather of "
+                               "first-SAT)",
                 "lds_slots": n_slots, "nominal_ops_per_eval": float(ops_state.mean()),
             },
             "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": valu_peak, "unit": "TOP/s",
                          "frac": achieved_tops / valu_peak, "traffic": traffic, "peak_derived": VALU_PEAK_TOPS,
+                         "frac_spec": achieved_tops / VALU_PEAK_TOPS,
                          "ops": "nominal INT32 ops of the live DAG nodes (SURVEY.md 8d table) x candidates",
                          "kernel": ENGINE_KERNEL[N.set_eval_engine()] + "(+finalize)", "launch_ms": kern_ms,
                          "evals_per_launch": evals_rank},
@@ -409,7 +448,8 @@ def main():
                              "frac": achieved_gbs / HBM_PEAK_GBS, "bytes_per_launch": bytes_launch},
             # VALU busy: every issued VALU instruction (dispatch/decode overhead included) x 64 lanes
             "valu_busy": None if valu_busy is None else dict(
-                valu_busy, frac=valu_busy["issued_int32_lane_ops_per_s"] / (valu_peak * 1e12)),
+                valu_busy, frac=valu_busy["issued_int32_lane_ops_per_s"] / (valu_peak * 1e12),
+                frac_spec=valu_busy["issued_int32_lane_ops_per_s"] / (VALU_PEAK_TOPS * 1e12)),
             "cpu_baseline": cpu,
             "results": {"sat_states": sat, "planted_states": int(len(pl)), "planted_found": planted_ok},
             "keccak": keccak,
@@ -446,8 +486,10 @@ def _threads() -> int:
         return os.cpu_count() or 1
 
 
-def cpu_baseline(b, d_cands, n_states, n_cand, n_vars, target_s, gpu_rate):
-    """Time the C oracle (OpenMP, all candidates evaluated) on a bounded sample of the same batch."""
+def cpu_baseline(b, d_cands, n_states, n_cand, n_vars, target_s, gpu_rate, gpu_first, status):
+    """Time the C oracle (OpenMP, all candidates evaluated) on a bounded sample of the same batch,
+    and check that its first-SAT words equal the GPU's for every sampled state (a free full-size
+    parity check: the sample is the head of the timed batch)."""
     from oracle import coracle
 
     def sample(k):
@@ -471,11 +513,83 @@ def cpu_baseline(b, d_cands, n_states, n_cand, n_vars, target_s, gpu_rate):
             break
         k = min(n_states, int(k * min(8.0, max(2.0, target_s / max(t_used, 1e-3)))))
     rate = k * n_cand / t_used
-    log(f"cpu baseline: {k} states x {n_cand} cand in {t_used:.1f}s = {rate:.3g} evals/s")
+    ok = status[:k] == 0
+    diff = int((np.asarray(ref)[ok] != gpu_first[:k][ok]).sum())
+    log(f"cpu baseline: {k} states x {n_cand} cand in {t_used:.1f}s = {rate:.3g} evals/s; "
+        f"first-SAT parity {int(ok.sum()) - diff}/{int(ok.sum())}")
+    if diff:
+        raise RuntimeError(f"{diff} of {int(ok.sum())} sampled states: GPU first-SAT differs from the oracle")
     return {"value": rate, "unit": "evals/s", "cores": _threads(), "kind": "port",
             "sample": f"first {k} states of the rank-0 batch x {n_cand} candidates (all evaluated), "
                       f"oracle/c/oracle.c DAG evaluator, OpenMP", "seconds": t_used,
-            "gpu_over_cpu": gpu_rate / rate}
+            "gpu_over_cpu": gpu_rate / rate, "parity_states": int(ok.sum()), "parity_mismatches": diff}
+
+
+def verify_keccak(d_pre, d_dig, kfirst, nk, every):
+    """The first 65 536 digests of this rank's range and one in `every` after that (at a
+    seeded offset inside each block), bit-exact against the C oracle on the same preimages
+    (SURVEY.md 8d config-5 verification protocol)."""
+    from oracle import coracle
+
+    head = min(nk, 1 << 16)
+    pre = coracle.mapping_preimages(kfirst, head, SEED)
+    got = d_dig[: head * 32].cpu().numpy().reshape(head, 32)
+    bad = int((got != coracle.keccak256(pre.reshape(-1), head, 64, 64)).any(axis=1).sum())
+    gpu_pre_bad = int((d_pre[: head * 64].cpu().numpy().reshape(head, 64) != pre).any(axis=1).sum())
+    idx = np.arange(head, nk, max(1, every), dtype=np.int64)
+    if len(idx):
+        idx = idx + np.random.default_rng(SEED + kfirst).integers(0, max(1, every), size=len(idx))
+        idx = idx[idx < nk]
+    sampled = 0
+    if len(idx):
+        import torch
+
+        d_idx = torch.from_numpy(idx).to(d_dig.device)
+        got_s = d_dig.view(nk, 32).index_select(0, d_idx).cpu().numpy()
+        pre_s = np.concatenate([coracle.mapping_preimages(kfirst + int(i), 1, SEED) for i in idx])
+        bad += int((got_s != coracle.keccak256(pre_s.reshape(-1), len(idx), 64, 64)).any(axis=1).sum())
+        sampled = len(idx)
+    return {"checked": head + sampled, "first": head, "sampled": sampled, "sample_every": every,
+            "mismatches": bad + gpu_pre_bad, "against": "oracle/c keccak256 + mapping_preimages"}
+
+
+def launch_ranks(n: int) -> int:
+    """torch.distributed.run with n ranks on this node (127.0.0.1), this script's own argv."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {n} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
+def dry_run(args, world: int, rank: int):
+    """CPU-only pass of the rank plumbing: every rank builds and lowers its own contiguous
+    shard of a small synthetic batch, rank 0 gathers the per-rank counts over gloo and prints
+    one line (n_gpus = the world size the process group formed)."""
+    import torch
+    import torch.distributed as dist
+
+    from mythril_amd import _native as N
+
+    dist.init_process_group("gloo")
+    world = dist.get_world_size()
+    n_states = min(args.states, 256)
+    base = rank * n_states
+    b = N.synth_generate(SEED, base, n_states, args.nodes, args.cand)
+    words, po, status = N.lower(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
+    mine = torch.tensor([rank, base, n_states, int((status == 0).sum()), int(words.size)], dtype=torch.int64)
+    out = [torch.zeros_like(mine) for _ in range(world)] if rank == 0 else None
+    dist.gather(mine, out, dst=0)
+    if rank == 0:
+        ranks = [t.tolist() for t in out]
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "evals/s", "n_gpus": world, "dry_run": True,
+                          "world_size_seen": world, "ranks": [{"rank": r[0], "first_state": r[1], "states": r[2],
+                                                               "lowered_ok": r[3], "words": r[4]} for r in ranks],
+                          "config": {"parallelism": f"dp{world} (contiguous state-id shards, gloo dry run)"}}),
+              flush=True)
+    dist.destroy_process_group()
 
 
 def cpu_keccak(target_s):

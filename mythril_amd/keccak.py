@@ -52,8 +52,9 @@ def keccak256_batch(preimages: Sequence[bytes]) -> List[bytes]:
         by_len.setdefault(len(p), []).append(i)
     ctx = _context()
     for ln, idx in by_len.items():
+        # empty preimages: stride 0 over a 1-byte dummy buffer (every lane hashes the empty string)
         buf = np.frombuffer(b"".join(preimages[i] for i in idx), dtype=np.uint8) if ln else np.zeros(1, np.uint8)
-        dig = ctx.keccak256_n(buf, len(idx), ln, max(ln, 1) if ln else 1)
+        dig = ctx.keccak256_n(buf, len(idx), ln, ln)
         for k, i in enumerate(idx):
             out[i] = dig[k].tobytes()
     return out  # type: ignore[return-value]

@@ -22,6 +22,7 @@ decided here: that is the GPU kernel's job (or z3's).
 """
 from __future__ import annotations
 
+import weakref
 from typing import Any, Dict, List, Optional, Sequence, Set, Tuple, Union
 
 from . import ir
@@ -55,7 +56,10 @@ class Term:
         return f"Term({ir.OP_NAMES.get(self.op, self.op)}, w={self.width}, params={self.params})"
 
 
-_INTERN: Dict[Tuple, Term] = {}
+# Weak values: a term lives as long as something (a constraint list, a parent term, an UNSAT
+# core) holds it, as z3 reference-counts its ASTs.  A live term keeps its arguments alive, so
+# the id()s in its key stay valid for exactly as long as the entry exists.
+_INTERN: "weakref.WeakValueDictionary[Tuple, Term]" = weakref.WeakValueDictionary()
 
 
 def mk(op: int, width: int, args: Sequence[Term] = (), params: Tuple = ()) -> Term:

@@ -229,6 +229,7 @@ class Prefilter:
         # fresh candidates (half of them guided by the pre-check's domains), up to retry_cand
         # per state (host candidate memory capped at 1 GiB)
         self.retry_cand = 1024
+        self.cand_bytes = 1 << 30  # host candidate memory of one witness round
 
     def check_states(self, states: Sequence[Sequence[Term]],
                      parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> List[Tuple[str, Optional[Dict[str, int]]]]:
@@ -251,7 +252,39 @@ class Prefilter:
             sub = iter(self.check_states(rest, rest_par) if rest else [])
             return [(unsat, None) if h else next(sub) for h in hit]
         dags = [D.build_state(s) for s in states]
+        out = self._check_built(states, dags, parents)
+        stats.gpu_batches += 1
+        stats.gpu_queries += len(states)
+        stats.gpu_sat += sum(1 for r in out if r[0] == sat)
+        stats.refuted += sum(1 for r in out if r[0] == unsat)
+        stats.gpu_undecided += sum(1 for r in out if r[0] == "undecided")
+        stats.gpu_time += time.time() - t0
+        return out
+
+    def _check_built(self, states, dags, parents):
+        """Candidate memory of one round is n_states x n_cand x n_vars x 32 B with n_vars the
+        batch maximum: a batch past `cand_bytes` is split into sub-batches of similar n_vars."""
         n_vars = max(1, max(d.n_vars for d in dags))
+        if len(dags) > 1 and len(dags) * self.n_cand * n_vars * 32 > self.cand_bytes:
+            order = sorted(range(len(dags)), key=lambda i: dags[i].n_vars)
+            res: List = [None] * len(dags)
+            grp: List[int] = []
+            for i in order + [None]:
+                if i is not None:
+                    nv = max(1, dags[i].n_vars)
+                    if not grp or (len(grp) + 1) * self.n_cand * nv * 32 <= self.cand_bytes:
+                        grp.append(i)
+                        continue
+                sub = self._check_built([states[k] for k in grp], [dags[k] for k in grp],
+                                        None if parents is None else [parents[k] for k in grp])
+                for k, r in zip(grp, sub):
+                    res[k] = r
+                grp = [i] if i is not None else []
+            return res
+        return self._check_round(states, dags, parents, n_vars)
+
+    def _check_round(self, states, dags, parents, n_vars):
+        stats = SolverStatistics()
         nodes, noff, consts, coff = D.pack_states(dags)
         words, po, status = self._N.lower(nodes, noff, consts, coff)
         self._calls += 1
@@ -260,7 +293,7 @@ class Prefilter:
         proven = self._N.refute(nodes, noff, consts, coff) if self.refute else np.zeros(len(dags), np.int8)
         retry = [i for i in range(len(dags)) if first[i] == -1 and proven[i] != 1]
         if retry and self.retry_cand > self.n_cand:
-            budget = (1 << 30) // (len(retry) * n_vars * 32)
+            budget = self.cand_bytes // (len(retry) * n_vars * 32)
             n2 = min(self.retry_cand, budget) // 64 * 64
             if n2 > self.n_cand:
                 sub = [dags[i] for i in retry]
@@ -286,12 +319,6 @@ class Prefilter:
                 _cores.add(UnsatCores.shrink(self._N, states[i]))
             else:
                 out.append(("undecided", None))
-        stats.gpu_batches += 1
-        stats.gpu_queries += len(states)
-        stats.gpu_sat += sum(1 for r in out if r[0] == sat)
-        stats.refuted += sum(1 for r in out if r[0] == unsat)
-        stats.gpu_undecided += sum(1 for r in out if r[0] == "undecided")
-        stats.gpu_time += time.time() - t0
         return out
 
 

@@ -188,7 +188,7 @@ def run_evm(code: bytes, d: Dag):
             stack.append(d.op({0x1B: S.SHL, 0x1C: S.LSHR, 0x1D: S.ASHR}[op], 256, val, sh))
         elif op == 0x20:  # SHA3 over concrete memory
             off, ln = cval(stack.pop()), cval(stack.pop())
-            if off + ln > 1 << 20:
+            if off + ln > 1 << 25:  # sha3_bigOffset2 hashes 2 bytes at offset 2^24
                 raise Unsupported("huge SHA3 range")
             mem_ensure(off + ln)
             data = bytes(mem[off:off + ln])
@@ -242,15 +242,23 @@ def post_storage(data):
 
 
 def make_keccak(ref: str):
+    """Every vmSha3Test case: a KAT when the fixture has a post-state, else a dropped entry
+    (preimage/digest null) that names why -- the *oog cases run out of gas on a huge memory
+    range, so the fixture holds no post-state and no expected digest."""
     kats = []
     for name, data in load_vmtests(ref, "vmSha3Test"):
         st = post_storage(data)
         if not st:
+            kats.append({"source": f"VMTests/vmSha3Test/{name}.json", "preimage": None, "digest": None,
+                         "reference_agrees": True,
+                         "dropped": "no post-state in the fixture (out of gas before SSTORE): no expected digest"})
             continue
         d = Dag()
         try:
             storage, sha3s = run_evm(bytes.fromhex(data["exec"]["code"][2:]), d)
-        except Unsupported:
+        except Unsupported as e:
+            kats.append({"source": f"VMTests/vmSha3Test/{name}.json", "preimage": None, "digest": None,
+                         "reference_agrees": True, "dropped": f"not replayable here: {e}"})
             continue
         for key, node in storage.items():
             for (pre, h) in sha3s:
@@ -356,7 +364,9 @@ def main(ref: str):
     arith, skipped = make_arith(ref)
     with open(os.path.join(HERE, "vm_arith.json"), "w") as f:
         json.dump(arith, f, separators=(",", ":"))
-    print(f"keccak KATs: {len(kats)} ({sum(k['reference_agrees'] for k in kats)} agree)")
+    live = [k for k in kats if k["digest"] is not None]
+    print(f"keccak KATs: {len(live)} ({sum(k['reference_agrees'] for k in live)} agree), "
+          f"{len(kats) - len(live)} vmSha3Test cases listed as dropped")
     print(f"shift vectors: {len(shifts)}")
     print(f"VMTests arithmetic DAGs: {len(arith)} ({sum(t['reference_agrees'] for t in arith)} agree), "
           f"skipped {skipped}")

@@ -105,3 +105,26 @@ def test_two_rank_gather_matches_single_process(tmp_path, balanced):
     b, cands = _batch()
     want = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)
     assert np.array_equal(got, want)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` without a torchrun environment starts 2 ranks itself (before any
+    GPU call); --dry-run keeps it on CPU/gloo.  Rank 0's line reports the world size the
+    process group formed and each rank's contiguous shard."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                        "--states", "64"], capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world_size_seen"] == 2 and line["dry_run"]
+    assert [x["first_state"] for x in line["ranks"]] == [0, 64]
+    assert all(x["states"] == 64 and x["lowered_ok"] == 64 for x in line["ranks"])

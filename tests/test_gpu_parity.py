@@ -214,6 +214,8 @@ def test_uf_ackermann_semantics(mgp_ctx):
 # ------------------------------------------------------------------ Keccak
 def test_keccak_kats_on_gpu(mgp_ctx):
     for k in load_golden("keccak_kat.json"):
+        if k["digest"] is None:  # vmSha3Test *oog: no expected digest (listed with the reason)
+            continue
         pre = bytes.fromhex(k["preimage"])
         out = mgp_ctx.keccak256_n(np.frombuffer(pre, dtype=np.uint8), 1, len(pre), max(len(pre), 1))
         assert out[0].tobytes().hex() == k["digest"], k["source"]
@@ -229,6 +231,37 @@ def test_keccak_lengths_vs_oracle(mgp_ctx, length):
     ref = coracle.keccak256(data, n, length, stride)
     assert (out == ref).all()
     assert out[5].tobytes() == keccak_py(data[5 * stride:5 * stride + length].tobytes())
+
+
+def test_keccak_mapping_slot_fast_path_vs_oracle(mgp_ctx):
+    """Config 5: the bench's own preimages -- pad32(addr_i) || pad32(i mod 8)
+    from mgp_fill_mapping_preimages_dev -- hashed on the 64-byte fast path (stride 64,
+    16-B aligned device buffers: mgp_keccak64_kernel), 65 536 digests bit-exact against the
+    C oracle, plus a far-away slice at index 2^30 - 4096 (the bench's last chunk)."""
+    import ctypes
+
+    import torch
+
+    seed = 0x4D595448
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    for first, n in ((0, 1 << 16), ((1 << 30) - 4096, 4096)):
+        d_pre = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+        d_dig = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        assert d_pre.data_ptr() % 16 == 0 and d_dig.data_ptr() % 16 == 0
+        N.fill_mapping_preimages_dev(ctypes.c_void_p(d_pre.data_ptr()), first, n, seed, sh)
+        N.keccak256_dev(ctypes.c_void_p(d_pre.data_ptr()), n, 64, 64, ctypes.c_void_p(d_dig.data_ptr()), sh)
+        torch.cuda.synchronize(dev)
+        pre = coracle.mapping_preimages(first, n, seed)
+        assert np.array_equal(d_pre.cpu().numpy().reshape(n, 64), pre.reshape(n, 64)), "preimage fill differs"
+        ref = coracle.keccak256(pre.reshape(-1), n, 64, 64)
+        got = d_dig.cpu().numpy().reshape(n, 32)
+        bad = np.nonzero((got != ref).any(axis=1))[0]
+        assert bad.size == 0, f"{bad.size} of {n} digests differ from the oracle (first index {first + bad[0]})"
+    # the host entry point on the same preimages takes the same fast path
+    out = mgp_ctx.keccak256_n(pre.reshape(-1), n, 64, 64)
+    assert np.array_equal(out, ref)
 
 
 def _long_program(rng, n_ops, n_vars, n_consts):

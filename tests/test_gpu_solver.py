@@ -204,6 +204,34 @@ def test_concrete_keccak_batch_matches_reference_impl(mgp_ctx):
     assert km.get_empty_keccak_hash().value == int.from_bytes(keccak_py(b""), "big")
 
 
+def test_many_empty_preimages_in_one_batch(mgp_ctx):
+    """Three or more empty inputs in one batch: every one gets the empty hash."""
+    pre = [b"", b"", b"\x01", b"", b""]
+    assert keccak256_batch(pre) == [keccak_py(p) for p in pre]
+    assert get_code_hashes(["", "0x", "", "0x"]) == ["0x" + keccak_py(b"").hex()] * 4
+
+
+def test_first_round_candidate_memory_is_capped(backend):
+    """A batch whose candidate block would pass Prefilter.cand_bytes is split into
+    sub-batches grouped by variable count; answers are the same as unsplit."""
+    pf = SV.prefilter()
+    xs = [BVS(f"x{i}", 256) for i in range(12)]
+    states = []
+    for i in range(40):
+        k = 1 + i % 12  # 1..12 variables
+        states.append([c.raw for c in [xs[j] == BVV(i + j, 256) for j in range(k)]])
+    want = pf.check_states(states)
+    old = pf.cand_bytes
+    try:
+        pf.cand_bytes = 6 * pf.n_cand * 4 * 32  # about six 4-variable states per round
+        got = pf.check_states(states)
+    finally:
+        pf.cand_bytes = old
+    assert [r[0] for r in got] == [r[0] for r in want] == [SV.sat] * 40
+    for r, st in zip(got, states):
+        assert _oracle_confirms([SV.Bool(t) for t in st], r[1])
+
+
 def test_code_hash_matches_support_utils_contract(mgp_ctx):
     # support_utils.py:29-41: optional 0x prefix, "0x" + hex digest, "" when the code is not hex
     codes = ["0x6080604052", "6080604052", "", "0x", "0xzz", "60" * 300, "0x" + "ff" * 136]

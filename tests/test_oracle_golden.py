@@ -20,8 +20,12 @@ from ._util import load_golden, pack_states, random_cands, state_slice
 
 
 def test_keccak_kats_python_and_c():
-    kats = load_golden("keccak_kat.json")
-    assert len(kats) >= 10
+    allk = load_golden("keccak_kat.json")
+    # all 18 vmSha3Test cases are listed; the ones without an expected digest name why
+    assert sum(k["source"].startswith("VMTests/vmSha3Test/") for k in allk) == 18
+    assert all(k.get("dropped") for k in allk if k["digest"] is None)
+    kats = [k for k in allk if k["digest"] is not None]
+    assert len(kats) >= 13
     for k in kats:
         pre = bytes.fromhex(k["preimage"])
         assert keccak256(pre).hex() == k["digest"], k["source"]

@@ -404,6 +404,7 @@ def main():
                     "sat": kinds.count(SV.sat), "unsat": kinds.count(SV.unsat),
                     "refuted": st.refuted, "core_hits": st.core_hits,
                     "undecided": kinds.count("undecided"), "candidates": pf.n_cand,
+                    "stages_ms": pf.last_profile, "latency": frontend_latency(pf, SV, cs),
                     "shape": "BECToken batchTransfer: calldata word, keccak256_512 mapping read, overflow / underflow query"}
         pf.ctx.close()
         log(f"frontend: {frontend}")
@@ -523,6 +524,30 @@ def cpu_baseline(b, d_cands, n_states, n_cand, n_vars, target_s, gpu_rate, gpu_f
             "sample": f"first {k} states of the rank-0 batch x {n_cand} candidates (all evaluated), "
                       f"oracle/c/oracle.c DAG evaluator, OpenMP", "seconds": t_used,
             "gpu_over_cpu": gpu_rate / rate, "parity_states": int(ok.sum()), "parity_mismatches": diff}
+
+
+def frontend_latency(pf, SV, cs, sizes=(1, 2, 16, 128, 1024)):
+    """Wall time of one Prefilter.check_states call at LASER-like batch sizes (a JUMPI
+    fork hands the prune filter <= 2 successors, svm.py:251-255) up to a full worklist,
+    cold (no UNSAT core cached), median of repeated calls, with the stage split."""
+    out = []
+    for n in sizes:
+        if n > len(cs):
+            break
+        reps = max(3, min(30, 2048 // n))
+        walls, profs = [], []
+        for r in range(reps):
+            SV.unsat_cores().reset()
+            sub = cs[(r * n) % max(1, len(cs) - n + 1):][:n]
+            t = time.perf_counter()
+            pf.check_states(sub)
+            walls.append(1e3 * (time.perf_counter() - t))
+            profs.append(pf.last_profile or {})
+        med = int(np.argsort(walls)[len(walls) // 2])
+        row = {"states": n, "ms_per_call": walls[med], "states_per_s": 1e3 * n / walls[med], "reps": reps}
+        row.update({k: round(v, 3) for k, v in profs[med].items() if k.endswith("_ms")})
+        out.append(row)
+    return out
 
 
 def verify_keccak(d_pre, d_dig, kfirst, nk, every):

@@ -211,6 +211,76 @@ int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uin
                         const uint32_t *fixed_pool, uint32_t n_fixed,
                         const uint8_t *has_parent, uint32_t *out);
 
+/* ------------------------------------------------------ native front end
+ * Flattens a batch of states' path constraints (the roots) into node lists, constant
+ * pools, variable tables and candidate hints, OpenMP over states — what the reference
+ * re-adds to a fresh z3 solver per state (constraints.py:34-51, analysis/solver.py:
+ * 37-50).  Input: the term arena (mythril_amd/smt.py _Arena): per term op, width
+ * (Bool = 0), 3 argument term ids (-1 = none, always < the term's own id), 2 params
+ * (VAR: name id; CONST: limb offset, limb count; EXTRACT: hi, lo; UFAPP/UFINV:
+ * function id, function-name id) and the little-endian u32 limbs of the constants.
+ * roots[root_off[s] .. root_off[s+1]) are the term ids of state s's constraints.
+ * The batch is read back with mgp_fe_get (arrays owned by the batch, valid until
+ * mgp_fe_free; *count = number of ELEMENTS of the field's type listed below, e.g. 8
+ * uint32_t per constant).  Per variable slot: width (<= 256), full width (first slot of a
+ * value, else 0), name id, aux (slot index within a wide value; for a fresh
+ * uninterpreted-function value the node index of its application), kind (0 named
+ * variable, 1 fresh UF value).  hint_off is per variable slot (8 limbs per hint);
+ * aliases are (dst, src) slot pairs local to the state.  GPU_NODES equals NODES
+ * except for padded key equalities (mgp_front.cpp), replaced by the constant that
+ * strengthens the formula; FLAGS per state: */
+#define MGP_FE_SAT_UNSAFE 0x1u   /* a padded key equality under both polarities: no GPU SAT answer */
+#define MGP_FE_STRENGTHENED 0x2u /* GPU_NODES differs from NODES for this state */
+typedef struct mgp_fe_batch mgp_fe_batch;
+enum mgp_fe_field {
+  MGP_FE_NODES = 0,     /* mgp_node                     */
+  MGP_FE_GPU_NODES,     /* mgp_node                     */
+  MGP_FE_NODE_OFF,      /* uint64_t, n_states + 1       */
+  MGP_FE_CONSTS,        /* uint32_t, 8 per entry        */
+  MGP_FE_CONST_OFF,     /* uint64_t, n_states + 1       */
+  MGP_FE_VAR_OFF,       /* uint64_t, n_states + 1       */
+  MGP_FE_VAR_WIDTH,     /* uint32_t per slot            */
+  MGP_FE_VAR_FULL,      /* uint32_t per slot            */
+  MGP_FE_VAR_NAME,      /* uint32_t per slot            */
+  MGP_FE_VAR_AUX,       /* uint32_t per slot            */
+  MGP_FE_VAR_KIND,      /* uint8_t per slot             */
+  MGP_FE_HINT_OFF,      /* uint64_t, n_slots + 1        */
+  MGP_FE_HINTS,         /* uint32_t, 8 per hint         */
+  MGP_FE_ALIAS_OFF,     /* uint64_t, n_states + 1       */
+  MGP_FE_ALIASES,       /* uint32_t, 2 per pair         */
+  MGP_FE_FLAGS,         /* uint8_t per state            */
+  MGP_FE_VAR_KEY        /* uint64_t per slot: name id, kind, UF node, piece (parent matching) */
+};
+int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t *t_args, const uint32_t *t_p,
+                     uint64_t n_terms, const uint32_t *limbs, uint64_t n_limbs, const int32_t *roots,
+                     const uint64_t *root_off, uint32_t n_states, mgp_fe_batch **out);
+int mgp_fe_get(const mgp_fe_batch *batch, int field, const void **ptr, uint64_t *count);
+void mgp_fe_free(mgp_fe_batch *batch);
+
+/* One batch through the whole pre-filter (mgp_pipeline.cpp): lower the GPU programs,
+ * generate n_cand candidates per state ON THE GPU (the mgp_make_candidates mixture,
+ * bit-identical, from the batch's hints/aliases/constants + fixed_pool), evaluate, and
+ * run mgp_refute on the host while the GPU works.  Parent witnesses (optional):
+ * parent_keys/parent_vals[parent_off[s] .. parent_off[s+1]) are (slot key, 8 limbs)
+ * pairs of state s's parent witness; slot_keys = the batch's MGP_FE_VAR_KEY; a state
+ * with a parent gets those values in candidate row 0.  Outputs: out_first[s] as
+ * mgp_eval_batch, out_witness (may be NULL) n_states x n_vars x 8 u32 with n_vars =
+ * *out_n_vars = the batch's widest state (SAT rows only), out_refuted[s] as
+ * mgp_refute.  out_times (may be NULL) receives 5 stage times in ms: lower,
+ * upload+launch, refute, GPU wait, copy-back.  Replaces, for one batch, the z3
+ * checks of Constraints.is_possible (constraints.py:34-51) and the SAT-only get_model
+ * calls (analysis/solver.py:27-61) it can decide. */
+#define MGP_CHECK_NO_REFUTE 0x1u
+int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint64_t seed,
+                    const uint32_t *fixed_pool, uint32_t n_fixed, const uint64_t *parent_keys,
+                    const uint32_t *parent_vals, const uint64_t *parent_off, const uint64_t *slot_keys,
+                    uint32_t flags, int32_t *out_first, uint32_t *out_witness, int8_t *out_refuted,
+                    uint32_t *out_n_vars, double *out_times);
+/* Test hook: the candidates mgp_check_batch would evaluate (no parents), device layout
+ * [state][var][half][cand] of 16-byte groups, n_vars >= the batch's widest state. */
+int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
+                      const uint32_t *fixed_pool, uint32_t n_fixed, uint32_t *out);
+
 /* ---------------------------------------------------------- Keccak-256
  * n preimages of len bytes each, preimage i at in + i*stride; 32-byte
  * big-endian digests to out32 + 32*i.  Keccak-256 = Keccak[r=1088,c=512]

@@ -91,6 +91,11 @@ def _bind(lib):
         "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
         "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P,
                                                _P]),
+        "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, ctypes.POINTER(_P)]),
+        "mgp_fe_get": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
+        "mgp_fe_free": (None, [_P]),
+        "mgp_check_batch": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _P]),
+        "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -142,6 +147,11 @@ EXPORTED_SYMBOLS = (
     "mgp_refute_trace",
     "mgp_guided_candidates",
     "mgp_make_candidates",
+    "mgp_build_states",
+    "mgp_fe_get",
+    "mgp_fe_free",
+    "mgp_check_batch",
+    "mgp_fe_candidates",
 )
 
 ENGINE_HIP, ENGINE_ASM = 1, 2
@@ -318,6 +328,10 @@ class Context:
         )
         _check(rc, self._h)
         return first, wit
+
+    def check_batch(self, batch, n_cand: int, seed: int, parents=None, refute: bool = True):
+        """A front-end batch (mythril_amd.front.Batch) through mgp_check_batch."""
+        return batch._check_native(self, n_cand, seed, parents, refute)
 
     def keccak256(self, data: np.ndarray, length: int, stride: int) -> np.ndarray:
         data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)

@@ -1,0 +1,565 @@
+// mgp_front.cpp — native front end of the pre-filter: term arena -> per-state
+// constraint DAGs (include/mgp_ir.h node lists), variable tables, candidate hints.
+//
+// The reference checks one state at a time: Constraints.is_possible re-adds every
+// constraint of the state to a fresh z3 Solver (mythril/laser/ethereum/state/
+// constraints.py:34-51), and analysis.solver.get_model does the same with Optimize
+// (mythril/analysis/solver.py:27-61).  Here a whole batch of states is flattened at
+// once from the term arena (mythril_amd/smt.py: _Arena, one row per hash-consed term;
+// the z3 walker mythril_amd/z3_lower.py fills the same arena from z3 ASTs), OpenMP
+// over states.  The result is exactly what mythril_amd/dag.py build_state +
+// pack_states + make_candidates' table flattening produce in Python (the tests pin
+// the two against each other node for node), so every downstream stage — lowering
+// (mgp_lower.cpp), UNSAT pre-check (mgp_refute.cpp), candidate generation, the HIP
+// evaluation — consumes it unchanged.
+//
+// Per state:
+//   * nodes in DFS post-order over the roots (children a, b, c first), memoised per
+//     term; the roots are AND-chained into a final Bool node (TRUE if none);
+//   * constants pooled per (value, 256-bit pieces); variables per (name, width), a
+//     value wider than 256 bits spread over ceil(w/256) slots (low piece first);
+//     each uninterpreted-function application gets a fresh variable (Ackermann);
+//   * candidate hints x == c -> c, x <op> c -> c, c +- 1, 64-aligned neighbours, and
+//     x == y alias pairs;
+//   * padded key equalities: `key == x` with a constant key narrower than x reaches
+//     z3 as x == Concat(0, key) (bitvec.py:16-22; keccak_function_manager.py:141-145
+//     builds one per concrete hash seen for every symbolic hash input).  Whether z3
+//     sees such a disjunct at all depends on the manager's dict of concrete hashes,
+//     keyed by z3 AST hashes (tests/laser/keccak_tests.py expects `unsat` for
+//     keccak(100_8) == keccak(N1_256), which the formula as written satisfies).  The
+//     GPU program therefore replaces every such equality by the constant that makes
+//     the formula STRONGER — false where it occurs positively, true where it occurs
+//     negatively — so a GPU witness never rests on one: it is a model of the
+//     formula with or without those disjuncts.  A state where one occurs with both
+//     polarities gets no GPU SAT answer (flag FE_SAT_UNSAFE).  The UNSAT pre-check
+//     reads the original nodes (refuting the weaker formula is the sound direction).
+#include <omp.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mgp.h"
+
+namespace {
+
+struct StateOut {
+  std::vector<mgp_node> nodes;
+  std::vector<uint32_t> gpu_ops;           // (node index, op) pairs: padded equalities replaced
+  std::vector<uint32_t> consts;            // 8 limbs per pool entry
+  std::vector<uint32_t> var_width, var_full, var_name, var_aux;  // per slot
+  std::vector<uint8_t> var_kind;
+  std::vector<uint64_t> var_key;
+  std::vector<std::vector<uint32_t>> hints;  // per slot: 8 limbs per hint
+  std::vector<uint32_t> aliases;           // (dst, src) pairs
+  uint8_t flags = 0;
+  bool bad = false;
+};
+
+struct Arena {
+  const uint8_t *op;
+  const uint32_t *width;
+  const int32_t *args;
+  const uint32_t *p;
+  const uint32_t *limbs;
+  uint64_t n_terms, n_limbs;
+};
+
+inline uint64_t hash_limbs(const uint32_t *l, uint32_t n, uint32_t k) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ k;
+  for (uint32_t i = 0; i < n; ++i) {
+    h ^= l[i];
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+  }
+  return h;
+}
+
+inline void mask_limbs(uint32_t *v, uint32_t w) {
+  for (int l = 0; l < 8; ++l) {
+    const int lo = 32 * l;
+    v[l] &= (int)w >= lo + 32 ? 0xFFFFFFFFu : ((int)w <= lo ? 0u : ((1u << (w - lo)) - 1u));
+  }
+}
+
+inline void add_u64(const uint32_t *a, uint64_t d, bool sub, uint32_t *r) {  // r = a +- d mod 2^256
+  uint64_t carry = 0;
+  for (int l = 0; l < 8; ++l) {
+    const uint64_t dl = l == 0 ? (uint32_t)d : (l == 1 ? (uint32_t)(d >> 32) : 0u);
+    if (!sub) {
+      const uint64_t s = (uint64_t)a[l] + dl + carry;
+      r[l] = (uint32_t)s;
+      carry = s >> 32;
+    } else {
+      const uint64_t s = (uint64_t)a[l] - dl - carry;
+      r[l] = (uint32_t)s;
+      carry = (s >> 63) & 1u;
+    }
+  }
+}
+
+// Open-addressing map uint64 -> uint32 (linear probing), reused across the states one
+// thread builds: clear() resets only the slots that were used (no per-node allocation).
+struct FlatMap {
+  std::vector<uint64_t> keys;
+  std::vector<uint32_t> vals;
+  std::vector<uint32_t> used;
+  uint64_t mask = 0;
+  static constexpr uint64_t kEmpty = ~0ull;
+  void reset(uint64_t expect) {
+    uint64_t cap = 64;
+    while (cap < 2 * expect) cap <<= 1;
+    if (cap > keys.size()) {
+      keys.assign(cap, kEmpty);
+      vals.assign(cap, 0);
+      used.clear();
+      mask = cap - 1;
+      return;
+    }
+    for (uint32_t u : used) keys[u] = kEmpty;
+    used.clear();
+  }
+  uint64_t slot(uint64_t k) const {
+    uint64_t h = k * 0x9E3779B97F4A7C15ull;
+    return (h ^ (h >> 32)) & mask;
+  }
+  // value of k or nullptr
+  uint32_t *find(uint64_t k) {
+    for (uint64_t i = slot(k);; i = (i + 1) & mask) {
+      if (keys[i] == k) return &vals[i];
+      if (keys[i] == kEmpty) return nullptr;
+    }
+  }
+  void put(uint64_t k, uint32_t v) {
+    if (2 * (used.size() + 1) > keys.size()) grow();
+    uint64_t i = slot(k);
+    while (keys[i] != kEmpty && keys[i] != k) i = (i + 1) & mask;
+    if (keys[i] == kEmpty) used.push_back((uint32_t)i);
+    keys[i] = k;
+    vals[i] = v;
+  }
+  void grow() {
+    std::vector<uint64_t> ok;
+    std::vector<uint32_t> ov;
+    for (uint32_t u : used) {
+      ok.push_back(keys[u]);
+      ov.push_back(vals[u]);
+    }
+    keys.assign(keys.size() * 2, kEmpty);
+    vals.assign(keys.size(), 0);
+    mask = keys.size() - 1;
+    used.clear();
+    for (size_t i = 0; i < ok.size(); ++i) put(ok[i], ov[i]);
+  }
+};
+
+struct Scratch {
+  FlatMap memo, var_idx, const_idx;
+  struct CEnt {
+    uint32_t pool, term, k;
+  };
+  std::vector<CEnt> cents;
+  std::vector<std::pair<int32_t, bool>> stack;
+};
+
+// slot key: which variable (name, kind, UF node) and which 256-bit piece -- a parent
+// witness is matched to a child's slots by it (mgp_check_batch)
+inline uint64_t slot_key(uint32_t name, uint8_t kind, uint32_t aux, uint32_t j) {
+  return kind ? (1ull << 63) | ((uint64_t)(name & 0x7FFFFFFFu) << 32) | ((uint64_t)(aux & 0xFFFFFFu) << 8) | (j & 0xFFu)
+              : ((uint64_t)(name & 0x7FFFFFFFu) << 32) | (j & 0xFFFFFFFFu);
+}
+
+void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut &S, Scratch &X) {
+  FlatMap &memo = X.memo, &var_idx = X.var_idx, &const_idx = X.const_idx;
+  memo.reset(512);
+  var_idx.reset(64);
+  const_idx.reset(64);
+  X.cents.clear();
+  using CEnt = Scratch::CEnt;
+  auto new_slots = [&](uint32_t name, uint32_t width, uint8_t kind, uint32_t aux) -> uint32_t {
+    const uint32_t first = (uint32_t)S.var_width.size();
+    for (uint32_t off = 0, j = 0; off < width; off += 256, ++j) {
+      S.var_width.push_back(std::min<uint32_t>(256, width - off));
+      S.var_full.push_back(j == 0 ? width : 0u);
+      S.var_name.push_back(name);
+      S.var_aux.push_back(kind == 0 ? j : aux);
+      S.var_kind.push_back(kind);
+      S.var_key.push_back(slot_key(name, kind, aux, j));
+    }
+    return first;
+  };
+  auto emit = [&](int32_t t) -> int32_t {
+    mgp_node nd;
+    memset(&nd, 0, sizeof nd);
+    const uint8_t op = A.op[t];
+    const uint32_t w = A.width[t] == 0 ? 1u : A.width[t];
+    int32_t ch[3] = {-1, -1, -1};
+    for (int i = 0; i < 3; ++i) {
+      const int32_t a = A.args[3 * (uint64_t)t + i];
+      if (a >= 0) ch[i] = (int32_t)*memo.find((uint64_t)a);
+    }
+    nd.op = op;
+    nd.width = (uint16_t)w;
+    nd.a = ch[0];
+    nd.b = ch[1];
+    nd.c = ch[2];
+    const uint32_t p0 = A.p[2 * (uint64_t)t], p1 = A.p[2 * (uint64_t)t + 1];
+    if (w > 0xFFFFu) S.bad = true;
+    if (op == MGP_OP_VAR) {
+      const uint64_t key = ((uint64_t)p0 << 32) | w;
+      const uint32_t *it = var_idx.find(key);
+      if (it) {
+        nd.p0 = *it;
+      } else {
+        nd.p0 = new_slots(p0, w, 0, 0);
+        var_idx.put(key, nd.p0);
+      }
+    } else if (op == MGP_OP_CONST) {
+      const uint32_t k = (w + 255) / 256;
+      const uint32_t *l = A.limbs + p0;
+      uint32_t n = p1;
+      if ((uint64_t)p0 + p1 > A.n_limbs) {
+        S.bad = true;
+        n = 0;
+      }
+      while (n && l[n - 1] == 0) --n;  // the value, not its storage width, is the key
+      // hash -> entry; a genuine collision probes the next hash value
+      uint64_t h = hash_limbs(l, n, k) & ~(1ull << 63);
+      int64_t found = -1;
+      for (;; h = (h + 1) & ~(1ull << 63)) {
+        const uint32_t *ei = const_idx.find(h);
+        if (!ei) break;
+        const CEnt &e = X.cents[*ei];
+        const uint32_t *ul = A.limbs + A.p[2 * (uint64_t)e.term];
+        uint32_t un = A.p[2 * (uint64_t)e.term + 1];
+        while (un && ul[un - 1] == 0) --un;
+        if (e.k == k && un == n && (n == 0 || memcmp(ul, l, 4u * n) == 0)) {
+          found = e.pool;
+          break;
+        }
+      }
+      if (found < 0) {
+        found = (int64_t)(S.consts.size() / 8);
+        const_idx.put(h, (uint32_t)X.cents.size());
+        X.cents.push_back(CEnt{(uint32_t)found, (uint32_t)t, k});
+        for (uint32_t j = 0; j < k; ++j)
+          for (uint32_t q = 0; q < 8; ++q) {
+            const uint32_t li = 8 * j + q;
+            S.consts.push_back(li < n ? l[li] : 0u);
+          }
+      }
+      nd.p0 = (uint32_t)found;
+    } else if (op == MGP_OP_EXTRACT) {
+      nd.p0 = p0;
+      nd.p1 = p1;
+    } else if (op == MGP_OP_UFAPP || op == MGP_OP_UFINV) {
+      nd.p0 = p0;
+      nd.p1 = new_slots(p1, w, 1, (uint32_t)S.nodes.size());
+    }
+    S.nodes.push_back(nd);
+    return (int32_t)S.nodes.size() - 1;
+  };
+
+  std::vector<int32_t> root_nodes;
+  auto &stack = X.stack;
+  for (uint64_t r = 0; r < n_roots; ++r) {
+    const int32_t root = roots[r];
+    if (root < 0 || (uint64_t)root >= A.n_terms) {
+      S.bad = true;
+      return;
+    }
+    stack.clear();
+    stack.emplace_back(root, false);
+    while (!stack.empty()) {
+      const auto [t, done] = stack.back();
+      stack.pop_back();
+      if (memo.find((uint64_t)t)) continue;
+      if (done) {
+        const int32_t idx = emit(t);
+        memo.put((uint64_t)t, (uint32_t)idx);
+        continue;
+      }
+      stack.emplace_back(t, true);
+      for (int i = 2; i >= 0; --i) {
+        const int32_t a = A.args[3 * (uint64_t)t + i];
+        if (a < 0) continue;
+        if ((uint64_t)a >= A.n_terms || a >= t) {  // arguments are built before their users
+          S.bad = true;
+          return;
+        }
+        if (!memo.find((uint64_t)a)) stack.emplace_back(a, false);
+      }
+    }
+    root_nodes.push_back((int32_t)*memo.find((uint64_t)root));
+  }
+  auto push_bool = [&](uint8_t op, int32_t a, int32_t b) {
+    mgp_node nd;
+    memset(&nd, 0, sizeof nd);
+    nd.op = op;
+    nd.width = 1;
+    nd.a = a;
+    nd.b = b;
+    nd.c = -1;
+    S.nodes.push_back(nd);
+  };
+  if (root_nodes.empty()) {
+    push_bool(MGP_OP_TRUE, -1, -1);
+  } else {
+    int32_t r = root_nodes[0];
+    for (size_t i = 1; i < root_nodes.size(); ++i) {
+      push_bool(MGP_OP_BAND, r, root_nodes[i]);
+      r = (int32_t)S.nodes.size() - 1;
+    }
+    if (r != (int32_t)S.nodes.size() - 1) push_bool(MGP_OP_BAND, r, r);
+  }
+
+  // ---- hints and aliases (dag.py _harvest_hints)
+  const uint32_t n_slots = (uint32_t)S.var_width.size();
+  S.hints.assign(n_slots, {});
+  auto var_of = [&](int32_t x) -> int64_t {
+    const mgp_node &n = S.nodes[x];
+    if (n.op == MGP_OP_VAR) return n.p0;
+    if (n.op == MGP_OP_UFAPP || n.op == MGP_OP_UFINV) return n.p1;
+    return -1;
+  };
+  for (const mgp_node &n : S.nodes) {
+    if (n.op < MGP_OP_EQ || n.op > MGP_OP_USUB_NOUDF || n.a < 0 || n.b < 0) continue;
+    const int64_t va = var_of(n.a), vb = var_of(n.b);
+    if (n.op == MGP_OP_EQ && va >= 0 && vb >= 0 && va != vb) {
+      S.aliases.push_back((uint32_t)va);
+      S.aliases.push_back((uint32_t)vb);
+      S.aliases.push_back((uint32_t)vb);
+      S.aliases.push_back((uint32_t)va);
+    }
+    const uint32_t wa = S.nodes[n.a].width;
+    const std::pair<int64_t, int32_t> pairs[2] = {{va, n.b}, {vb, n.a}};
+    for (const auto &pr : pairs) {
+      if (pr.first < 0 || S.nodes[pr.second].op != MGP_OP_CONST || wa > 256) continue;
+      const uint32_t *cv = &S.consts[8u * S.nodes[pr.second].p0];
+      auto &H = S.hints[pr.first];
+      if (n.op == MGP_OP_EQ) {
+        uint32_t v[8];
+        memcpy(v, cv, 32);
+        mask_limbs(v, wa);  // the pool entry is the value's low 256 bits; w <= 256 here
+        H.insert(H.end(), v, v + 8);
+      } else {
+        uint32_t up[8], up64[8], c0[8], cm[8], cp[8];
+        add_u64(cv, 63, false, up);
+        up[0] &= ~63u;
+        mask_limbs(up, wa);
+        add_u64(up, 64, false, up64);
+        mask_limbs(up64, wa);
+        memcpy(c0, cv, 32);
+        mask_limbs(c0, wa);
+        add_u64(cv, 1, true, cm);
+        mask_limbs(cm, wa);
+        add_u64(cv, 1, false, cp);
+        mask_limbs(cp, wa);
+        for (const uint32_t *v : {up, up64, c0, cm, cp}) H.insert(H.end(), v, v + 8);
+      }
+    }
+  }
+
+  // ---- padded key equalities: polarity from the root, strengthened for the GPU
+  const int32_t N = (int32_t)S.nodes.size();
+  auto is_padded_eq = [&](const mgp_node &n) {
+    if (n.op != MGP_OP_EQ || n.a < 0 || n.b < 0) return false;
+    auto zc = [&](int32_t x) {
+      const mgp_node &z = S.nodes[x];
+      return z.op == MGP_OP_ZEXT && z.a >= 0 && S.nodes[z.a].op == MGP_OP_CONST;
+    };
+    const bool za = zc(n.a), zb = zc(n.b);
+    return (za && S.nodes[n.b].op != MGP_OP_CONST) || (zb && S.nodes[n.a].op != MGP_OP_CONST);
+  };
+  bool any = false;
+  for (const mgp_node &n : S.nodes) any |= is_padded_eq(n);
+  if (!any) return;
+  std::vector<uint8_t> pol(N, 0);
+  pol[N - 1] = 1;
+  for (int32_t i = N - 1; i >= 0; --i) {
+    const uint8_t p = pol[i];
+    if (!p) continue;
+    const mgp_node &n = S.nodes[i];
+    const uint8_t flip = (uint8_t)(((p & 1) << 1) | ((p >> 1) & 1));
+    switch (n.op) {
+      case MGP_OP_BAND: case MGP_OP_BOR:
+        if (n.a >= 0) pol[n.a] |= p;
+        if (n.b >= 0) pol[n.b] |= p;
+        break;
+      case MGP_OP_BNOT:
+        if (n.a >= 0) pol[n.a] |= flip;
+        break;
+      case MGP_OP_BXOR: case MGP_OP_BEQ:
+        if (n.a >= 0) pol[n.a] |= 3;
+        if (n.b >= 0) pol[n.b] |= 3;
+        break;
+      case MGP_OP_BITE:
+        if (n.a >= 0) pol[n.a] |= 3;
+        if (n.b >= 0) pol[n.b] |= p;
+        if (n.c >= 0) pol[n.c] |= p;
+        break;
+      case MGP_OP_ITE:
+        if (n.a >= 0) pol[n.a] |= 3;
+        break;
+      default:
+        break;
+    }
+  }
+  for (int32_t i = 0; i < N; ++i) {
+    if (!pol[i] || !is_padded_eq(S.nodes[i])) continue;
+    if (pol[i] == 3) {
+      S.flags |= MGP_FE_SAT_UNSAFE;
+      continue;
+    }
+    S.gpu_ops.push_back((uint32_t)i);
+    S.gpu_ops.push_back(pol[i] == 1 ? (uint32_t)MGP_OP_FALSE : (uint32_t)MGP_OP_TRUE);
+    S.flags |= MGP_FE_STRENGTHENED;
+  }
+}
+
+}  // namespace
+
+struct mgp_fe_batch {
+  uint32_t n_states = 0;
+  std::vector<mgp_node> nodes, gpu_nodes;
+  std::vector<uint64_t> node_off, const_off, var_off, hint_off, alias_off;
+  std::vector<uint32_t> consts, var_width, var_full, var_name, var_aux, hints, aliases;
+  std::vector<uint8_t> var_kind, flags;
+  std::vector<uint64_t> var_key;
+};
+
+extern "C" {
+
+int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t *t_args, const uint32_t *t_p,
+                     uint64_t n_terms, const uint32_t *limbs, uint64_t n_limbs, const int32_t *roots,
+                     const uint64_t *root_off, uint32_t n_states, mgp_fe_batch **out) {
+  if (!out || !root_off || (n_terms && (!t_op || !t_width || !t_args || !t_p)) || (n_states && !roots && root_off[n_states]))
+    return MGP_E_ARG;
+  *out = nullptr;
+  const Arena A{t_op, t_width, t_args, t_p, limbs, n_terms, n_limbs};
+  const double t_start = omp_get_wtime();
+  std::vector<StateOut> res(n_states);
+  int bad = 0;
+#pragma omp parallel
+  {
+    Scratch X;
+#pragma omp for schedule(dynamic, 4)
+    for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+      const uint64_t r0 = root_off[s], r1 = root_off[s + 1];
+      if (r1 < r0) {
+#pragma omp atomic write
+        bad = 1;
+        continue;
+      }
+      build_one(A, roots + r0, r1 - r0, res[s], X);
+      if (res[s].bad) {
+#pragma omp atomic write
+        bad = 1;
+      }
+    }
+  }
+  if (getenv("MGP_FE_TIMING")) fprintf(stderr, "[fe] build %.3f ms\n", 1e3 * omp_get_wtime() - 1e3 * t_start);
+  if (bad) return MGP_E_ARG;
+  mgp_fe_batch *B = new (std::nothrow) mgp_fe_batch();
+  if (!B) return MGP_E_NOMEM;
+  B->n_states = n_states;
+  B->node_off.assign(n_states + 1, 0);
+  B->const_off.assign(n_states + 1, 0);
+  B->var_off.assign(n_states + 1, 0);
+  B->alias_off.assign(n_states + 1, 0);
+  B->flags.assign(n_states, 0);
+  for (uint32_t s = 0; s < n_states; ++s) {
+    B->node_off[s + 1] = B->node_off[s] + res[s].nodes.size();
+    B->const_off[s + 1] = B->const_off[s] + res[s].consts.size() / 8;
+    B->var_off[s + 1] = B->var_off[s] + res[s].var_width.size();
+    B->alias_off[s + 1] = B->alias_off[s] + res[s].aliases.size() / 2;
+    B->flags[s] = res[s].flags;
+  }
+  const uint64_t nn = B->node_off[n_states], nv = B->var_off[n_states];
+  B->nodes.resize(nn);
+  B->consts.resize(B->const_off[n_states] * 8);
+  B->var_width.resize(nv);
+  B->var_full.resize(nv);
+  B->var_name.resize(nv);
+  B->var_aux.resize(nv);
+  B->var_kind.resize(nv);
+  B->var_key.resize(nv);
+  B->aliases.resize(B->alias_off[n_states] * 2);
+  B->hint_off.assign(nv + 1, 0);
+  bool strengthened = false;
+  for (uint32_t s = 0; s < n_states; ++s) {
+    const uint64_t v0 = B->var_off[s];
+    for (size_t v = 0; v < res[s].hints.size(); ++v) B->hint_off[v0 + v + 1] = res[s].hints[v].size() / 8;
+    strengthened |= !res[s].gpu_ops.empty();
+  }
+  for (uint64_t v = 0; v < nv; ++v) B->hint_off[v + 1] += B->hint_off[v];
+  B->hints.resize(B->hint_off[nv] * 8);
+#pragma omp parallel for schedule(static)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    const StateOut &S = res[s];
+    std::copy(S.nodes.begin(), S.nodes.end(), B->nodes.begin() + B->node_off[s]);
+    std::copy(S.consts.begin(), S.consts.end(), B->consts.begin() + B->const_off[s] * 8);
+    const uint64_t v0 = B->var_off[s];
+    std::copy(S.var_width.begin(), S.var_width.end(), B->var_width.begin() + v0);
+    std::copy(S.var_full.begin(), S.var_full.end(), B->var_full.begin() + v0);
+    std::copy(S.var_name.begin(), S.var_name.end(), B->var_name.begin() + v0);
+    std::copy(S.var_aux.begin(), S.var_aux.end(), B->var_aux.begin() + v0);
+    std::copy(S.var_kind.begin(), S.var_kind.end(), B->var_kind.begin() + v0);
+    std::copy(S.var_key.begin(), S.var_key.end(), B->var_key.begin() + v0);
+    std::copy(S.aliases.begin(), S.aliases.end(), B->aliases.begin() + B->alias_off[s] * 2);
+    for (size_t v = 0; v < S.hints.size(); ++v)
+      std::copy(S.hints[v].begin(), S.hints[v].end(), B->hints.begin() + B->hint_off[v0 + v] * 8);
+  }
+  if (strengthened) {
+    B->gpu_nodes = B->nodes;
+    for (uint32_t s = 0; s < n_states; ++s)
+      for (size_t k = 0; k < res[s].gpu_ops.size(); k += 2) {
+        mgp_node &nd = B->gpu_nodes[B->node_off[s] + res[s].gpu_ops[k]];
+        nd.op = (uint8_t)res[s].gpu_ops[k + 1];
+        nd.width = 1;
+        nd.a = nd.b = nd.c = -1;
+        nd.p0 = nd.p1 = 0;
+      }
+  }
+  if (getenv("MGP_FE_TIMING")) fprintf(stderr, "[fe] total %.3f ms\n", 1e3 * omp_get_wtime() - 1e3 * t_start);
+  *out = B;
+  return MGP_OK;
+}
+
+int mgp_fe_get(const mgp_fe_batch *B, int field, const void **ptr, uint64_t *count) {
+  if (!B || !ptr || !count) return MGP_E_ARG;
+  auto set = [&](const auto &v) {
+    *ptr = v.empty() ? nullptr : (const void *)v.data();
+    *count = v.size();
+    return MGP_OK;
+  };
+  switch (field) {
+    case MGP_FE_NODES: return set(B->nodes);
+    case MGP_FE_GPU_NODES: return set(B->gpu_nodes.empty() ? B->nodes : B->gpu_nodes);
+    case MGP_FE_NODE_OFF: return set(B->node_off);
+    case MGP_FE_CONSTS: return set(B->consts);
+    case MGP_FE_CONST_OFF: return set(B->const_off);
+    case MGP_FE_VAR_OFF: return set(B->var_off);
+    case MGP_FE_VAR_WIDTH: return set(B->var_width);
+    case MGP_FE_VAR_FULL: return set(B->var_full);
+    case MGP_FE_VAR_NAME: return set(B->var_name);
+    case MGP_FE_VAR_AUX: return set(B->var_aux);
+    case MGP_FE_VAR_KIND: return set(B->var_kind);
+    case MGP_FE_HINT_OFF: return set(B->hint_off);
+    case MGP_FE_HINTS: return set(B->hints);
+    case MGP_FE_ALIAS_OFF: return set(B->alias_off);
+    case MGP_FE_ALIASES: return set(B->aliases);
+    case MGP_FE_FLAGS: return set(B->flags);
+    case MGP_FE_VAR_KEY: return set(B->var_key);
+    default: return MGP_E_ARG;
+  }
+}
+
+void mgp_fe_free(mgp_fe_batch *B) { delete B; }
+
+}  // extern "C"

@@ -626,6 +626,166 @@ __global__ void mgp_preimage_kernel(uint8_t *__restrict__ out, uint64_t first, u
 }
 
 
+// ------------------------------------------------- front-end candidates
+// Device twin of mgp_make_candidates (mgp_cands.cpp): the same splitmix64 stream keyed by
+// (seed, state, row, variable), the same row structure (parent witness row, first-hint
+// row, hint row with x == y aliases applied, then the 35/25/15/25 mixture) and the same
+// final masking, bit for bit (tests/test_gpu_front.py), written straight into the
+// device layout [state][var][half][cand] the interpreter reads.  One thread per
+// (state, candidate row); the row is built in place (an alias copies the source cell as
+// written so far, as on the host) and masked to the slot widths at the end.
+namespace {
+__device__ __forceinline__ uint64_t fe_mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+struct FeRow {
+  uint4 *out;
+  uint32_t n_cand, n_vars, c;
+  uint64_t s;
+  __device__ uint4 *at(uint32_t v, uint32_t h) const {
+    return out + (((s * n_vars + v) * 2u + h) * (uint64_t)n_cand + c);
+  }
+  __device__ void put(uint32_t v, const uint32_t *x) const {
+    *at(v, 0) = make_uint4(x[0], x[1], x[2], x[3]);
+    *at(v, 1) = make_uint4(x[4], x[5], x[6], x[7]);
+  }
+  __device__ void copy(uint32_t dst, uint32_t src) const {
+    const uint4 a = *at(src, 0), b = *at(src, 1);
+    *at(dst, 0) = a;
+    *at(dst, 1) = b;
+  }
+};
+}  // namespace
+
+__global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
+    uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed, const uint64_t *__restrict__ var_off,
+    const uint32_t *__restrict__ var_width, const uint64_t *__restrict__ hint_off, const uint32_t *__restrict__ hints,
+    const uint64_t *__restrict__ alias_off, const uint32_t *__restrict__ aliases,
+    const uint64_t *__restrict__ const_off, const uint32_t *__restrict__ consts, const uint32_t *__restrict__ fixed,
+    uint32_t n_fixed, const int32_t *__restrict__ parent_idx, const uint32_t *__restrict__ pvals,
+    const uint8_t *__restrict__ pmask, uint4 *__restrict__ out) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (uint64_t)n_states * n_cand) return;
+  const uint64_t s = g / n_cand;
+  const uint32_t c = (uint32_t)(g % n_cand);
+  const FeRow R{out, n_cand, n_vars, c, s};
+  uint32_t x[8];
+  for (uint32_t v = 0; v < n_vars; ++v) {  // uniform everywhere first (also padding variables)
+    uint64_t k = fe_mix(seed ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
+    for (int l = 0; l < 8; l += 2) {
+      k = fe_mix(k);
+      x[l] = (uint32_t)k;
+      x[l + 1] = (uint32_t)(k >> 32);
+    }
+    R.put(v, x);
+  }
+  const uint64_t v0 = var_off[s], V = var_off[s + 1] - v0;
+  if (V == 0 || V > n_vars) return;
+  const uint64_t c0 = const_off[s], nc = const_off[s + 1] - c0;
+  const uint64_t n_pool = 3 * nc + n_fixed;
+  const uint64_t a0 = alias_off[s], na = alias_off[s + 1] - a0;
+  auto n_hint = [&](uint64_t v) { return hint_off[v0 + v + 1] - hint_off[v0 + v]; };
+  auto hint = [&](uint64_t v, uint64_t j) { return hints + (hint_off[v0 + v] + j) * 8u; };
+  auto pool = [&](uint64_t i, uint32_t *r) {
+    if (i >= 3 * nc) {
+      for (int l = 0; l < 8; ++l) r[l] = fixed[(i - 3 * nc) * 8u + l];
+      return;
+    }
+    const uint32_t *a = consts + (c0 + i % nc) * 8u;
+    const int d = i < nc ? 0 : (i < 2 * nc ? 1 : -1);
+    uint64_t carry = d > 0 ? 1u : 0u;
+    const uint32_t ext = d < 0 ? 0xFFFFFFFFu : 0u;
+    for (int l = 0; l < 8; ++l) {
+      if (d == 0) {
+        r[l] = a[l];
+        continue;
+      }
+      const uint64_t t = (uint64_t)a[l] + ext + carry;
+      r[l] = (uint32_t)t;
+      carry = t >> 32;
+    }
+  };
+  const int32_t pidx = parent_idx ? parent_idx[s] : -1;
+  const uint32_t first_row = pidx >= 0 ? 1u : 0u;
+  if (pidx >= 0 && c == 0) {  // parent witness row (values of the same variables, by name)
+    for (uint64_t v = 0; v < V; ++v)
+      if (pmask[(uint64_t)pidx * n_vars + v]) R.put((uint32_t)v, pvals + ((uint64_t)pidx * n_vars + v) * 8u);
+  } else if (c == first_row || c == first_row + 1) {
+    for (uint64_t v = 0; v < V; ++v)
+      if (n_hint(v)) R.put((uint32_t)v, hint(v, 0));
+    if (c == first_row + 1)
+      for (uint64_t a = 0; a < na; ++a) {
+        const uint32_t dst = aliases[2 * (a0 + a)], src = aliases[2 * (a0 + a) + 1];
+        if (dst < V && src < V && var_width[v0 + dst] == var_width[v0 + src] && n_hint(src) && !n_hint(dst))
+          R.copy(dst, src);
+      }
+  } else if (c > first_row + 1) {
+    auto draw = [&](uint64_t v, double *r, uint64_t *pick) {
+      const uint64_t k = fe_mix(seed ^ 0xA5A5A5A5ull ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
+      *r = (double)(k >> 11) * (1.0 / 9007199254740992.0);
+      *pick = fe_mix(k);
+    };
+    for (uint64_t v = 0; v < V; ++v) {
+      double r;
+      uint64_t pick;
+      draw(v, &r, &pick);
+      if (r < 0.35 && n_hint(v)) {
+        R.put((uint32_t)v, hint(v, pick % n_hint(v)));
+      } else if (r < 0.60 && n_pool) {
+        pool(pick % n_pool, x);
+        R.put((uint32_t)v, x);
+      }
+    }
+    for (uint64_t v = 0; v < V; ++v) {  // after the others, so an alias can copy any variable
+      double r;
+      uint64_t pick;
+      draw(v, &r, &pick);
+      const bool pend = !(r < 0.35 && n_hint(v)) && !(r < 0.60 && n_pool) && r < 0.75;
+      if (!pend) continue;
+      uint64_t n_src = 0;
+      for (uint64_t a = 0; a < na; ++a)
+        if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V) ++n_src;
+      const bool by_alias = n_src > 0;
+      if (!by_alias)
+        for (uint64_t u = 0; u < V; ++u)
+          if (u != v && var_width[v0 + u] == var_width[v0 + v]) ++n_src;
+      if (!n_src) continue;
+      const uint64_t k = fe_mix(seed ^ 0x5A5A5A5Aull ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
+      uint64_t want = k % n_src, src = 0;
+      if (by_alias) {
+        for (uint64_t a = 0; a < na; ++a)
+          if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V && want-- == 0) {
+            src = aliases[2 * (a0 + a) + 1];
+            break;
+          }
+      } else {
+        for (uint64_t u = 0; u < V; ++u)
+          if (u != v && var_width[v0 + u] == var_width[v0 + v] && want-- == 0) {
+            src = u;
+            break;
+          }
+      }
+      R.copy((uint32_t)v, (uint32_t)src);
+    }
+  }
+  for (uint64_t v = 0; v < V; ++v) {  // mask to the slot width
+    const uint32_t w = var_width[v0 + v];
+    if (w >= 256) continue;
+    for (uint32_t h = 0; h < 2; ++h) {
+      uint4 q = *R.at((uint32_t)v, h);
+      uint32_t *e = reinterpret_cast<uint32_t *>(&q);
+      for (int l = 0; l < 4; ++l) {
+        const int lo = 32 * (4 * (int)h + l);
+        e[l] &= (int)w >= lo + 32 ? 0xFFFFFFFFu : ((int)w <= lo ? 0u : ((1u << (w - lo)) - 1u));
+      }
+      *R.at((uint32_t)v, h) = q;
+    }
+  }
+}
+
 // ------------------------------------------------------ VALU peak probe
 // 8 independent v_add_u32 chains, 64 adds per chain per iteration, written as
 // inline asm so nothing is folded: measures the INT32 VALU issue rate the
@@ -878,6 +1038,22 @@ hipError_t mgp_launch_preimages(uint8_t *out, uint64_t first, uint64_t n, uint64
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(mgp_preimage_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, out, first, n,
                      seed);
+  return hipGetLastError();
+}
+
+hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
+                               const uint64_t *var_off, const uint32_t *var_width, const uint64_t *hint_off,
+                               const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
+                               const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
+                               uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
+                               const uint8_t *pmask, uint32_t *out, hipStream_t st) {
+  const uint64_t total = (uint64_t)n_states * n_cand;
+  if (total == 0) return hipSuccess;
+  const uint64_t blocks = (total + 255) / 256;
+  if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mgp_fe_cands_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, n_states, n_cand, n_vars, seed,
+                     var_off, var_width, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed,
+                     parent_idx, pvals, pmask, reinterpret_cast<uint4 *>(out));
   return hipGetLastError();
 }
 

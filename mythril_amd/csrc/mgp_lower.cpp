@@ -844,12 +844,11 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
 
 }  // namespace
 
-extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
-                         const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_slots,
-                         uint32_t *out_words, uint64_t out_cap, uint64_t *out_prog_offsets,
-                         uint8_t *out_status, uint64_t *out_words_used) {
-  if (!node_offsets || !out_prog_offsets || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
-  std::vector<Lowered> res(n_states);
+// Lower every state into res[s] (OpenMP over states); MGP_OK or MGP_E_ARG.
+static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                     const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_slots,
+                     std::vector<Lowered> &res) {
+  res.assign(n_states, Lowered());
   int bad = 0;
   // MGP_LOWER_SCHED (A/B studies): 0 input order, 2 DFS only, 3 greedy only;
   // default 1 = the fewest-slot schedule of the three
@@ -857,7 +856,7 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
     const char *e = getenv("MGP_LOWER_SCHED");
     return (e && e[0] >= '0' && e[0] <= '3' && e[1] == 0) ? e[0] - '0' : 1;
   }();
-#pragma omp parallel for schedule(dynamic, 256)
+#pragma omp parallel for schedule(dynamic, 8)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
     const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
@@ -896,7 +895,35 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
     a.words.insert(a.words.end(), uops.begin(), uops.end());
     res[s] = std::move(a);
   }
-  if (bad) return MGP_E_ARG;
+  return bad ? MGP_E_ARG : MGP_OK;
+}
+
+// In-library entry point (mgp_pipeline.cpp): the lowered programs as one vector.
+int mgp_lower_vec(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states, const uint32_t *consts,
+                  const uint64_t *const_offsets, uint32_t max_slots, std::vector<uint32_t> &words,
+                  std::vector<uint64_t> &offs, std::vector<uint8_t> &status) {
+  std::vector<Lowered> res;
+  const int rc = lower_all(nodes, node_offsets, n_states, consts, const_offsets, max_slots, res);
+  if (rc != MGP_OK) return rc;
+  offs.assign((size_t)n_states + 1, 0);
+  for (uint32_t s = 0; s < n_states; ++s) offs[s + 1] = offs[s] + res[s].words.size();
+  words.resize(offs[n_states]);
+  status.resize(n_states);
+#pragma omp parallel for schedule(static)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    memcpy(words.data() + offs[s], res[s].words.data(), res[s].words.size() * 4u);
+    status[s] = res[s].status;
+  }
+  return MGP_OK;
+}
+
+extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                         const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_slots,
+                         uint32_t *out_words, uint64_t out_cap, uint64_t *out_prog_offsets,
+                         uint8_t *out_status, uint64_t *out_words_used) {
+  if (!node_offsets || !out_prog_offsets || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
+  std::vector<Lowered> res;
+  if (lower_all(nodes, node_offsets, n_states, consts, const_offsets, max_slots, res) != MGP_OK) return MGP_E_ARG;
   uint64_t total = 0;
   for (uint32_t s = 0; s < n_states; ++s) {
     out_prog_offsets[s] = total;

@@ -1,0 +1,304 @@
+// mgp_pipeline.cpp — one call per batch of states: lower, generate candidates on the
+// GPU, evaluate, and run the host UNSAT pre-check while the GPU works.
+//
+// This is the native body of Prefilter.check_states (mythril_amd/solver.py), i.e. of
+// the batched prune filter at LaserEVM.exec (mythril/laser/ethereum/svm.py:251-255)
+// and of the SAT-only get_model calls (mythril/analysis/solver.py:27-61).  Input is a
+// front-end batch (mgp_front.cpp).  Stages, in order, on the context's stream:
+//   1. lower the GPU program of every state (mgp_lower.cpp, OpenMP);
+//   2. upload programs and the candidate tables (variable widths, hints, aliases,
+//      constants, parent-witness rows) — a few hundred bytes per state, instead of
+//      n_cand x n_vars x 32 B of host-built candidates;
+//   3. mgp_fe_cands_kernel writes the candidates straight into the interpreter's
+//      [state][var][half][cand] layout; launch descriptors, the gfx950 interpreter
+//      and the first-SAT reduction follow (mgp_launch_eval);
+//   4. while those run, mgp_refute proves UNSAT on the host for the states it can
+//      (original nodes: the sound direction, see mgp_front.cpp);
+//   5. first-SAT words and witnesses come back.
+// Stage times (ms) go to out_times[0..4] when given: lower, upload+launch, refute,
+// GPU wait, copy-back.
+#include <hip/hip_runtime.h>
+#include <omp.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mgp.h"
+
+extern "C" {
+hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t n_states, const uint32_t *cands,
+                           uint32_t n_cand, uint32_t n_vars, uint32_t n_slots, int32_t *first_sat,
+                           uint32_t *witness, int32_t *partial, const uint32_t *order,
+                           const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
+                           hipStream_t st);
+hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
+                               const uint64_t *var_off, const uint32_t *var_width, const uint64_t *hint_off,
+                               const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
+                               const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
+                               uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
+                               const uint8_t *pmask, uint32_t *out, hipStream_t st);
+int mgp_fe_get(const mgp_fe_batch *batch, int field, const void **ptr, uint64_t *count);
+int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device);
+int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg);
+}
+int mgp_lower_vec(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states, const uint32_t *consts,
+                  const uint64_t *const_offsets, uint32_t max_slots, std::vector<uint32_t> &words,
+                  std::vector<uint64_t> &offs, std::vector<uint8_t> &status);
+
+namespace {
+
+struct Arr {
+  const void *p = nullptr;
+  uint64_t n = 0;
+};
+
+Arr get(const mgp_fe_batch *B, int f) {
+  Arr a;
+  mgp_fe_get(B, f, &a.p, &a.n);
+  return a;
+}
+
+// device buffers of the pipeline, one set per (context); grown on demand
+struct PipeBufs {
+  void *p[16] = {};
+  size_t cap[16] = {};
+  hipError_t ensure(int i, size_t bytes) {
+    if (bytes <= cap[i]) return hipSuccess;
+    if (p[i]) (void)hipFree(p[i]);
+    p[i] = nullptr;
+    cap[i] = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1u << 16);
+    hipError_t e = hipMalloc(&p[i], want);
+    if (e == hipSuccess) cap[i] = want;
+    return e;
+  }
+};
+
+std::unordered_map<mgp_ctx *, PipeBufs> &bufs_of() {
+  static std::unordered_map<mgp_ctx *, PipeBufs> m;
+  return m;
+}
+
+enum { B_WORDS, B_OFFS, B_ORDER, B_CANDS, B_FIRST, B_WIT, B_PART, B_TABLES, B_NUM };
+
+}  // namespace
+
+extern "C" {
+
+void mgp_pipeline_release(mgp_ctx *ctx) {
+  auto &m = bufs_of();
+  auto it = m.find(ctx);
+  if (it == m.end()) return;
+  for (int i = 0; i < 16; ++i)
+    if (it->second.p[i]) (void)hipFree(it->second.p[i]);
+  m.erase(it);
+}
+
+int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64_t seed, const uint32_t *fixed_pool,
+                    uint32_t n_fixed, const uint64_t *parent_keys, const uint32_t *parent_vals,
+                    const uint64_t *parent_off, const uint64_t *slot_keys, uint32_t flags, int32_t *out_first,
+                    uint32_t *out_witness, int8_t *out_refuted, uint32_t *out_n_vars, double *out_times) {
+  if (!ctx || !B || !out_first || !out_refuted || n_cand == 0 || (n_fixed && !fixed_pool))
+    return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument to mgp_check_batch");
+  double t = omp_get_wtime();
+  auto lap = [&](int k) {
+    const double now = omp_get_wtime();
+    if (out_times) out_times[k] = 1e3 * (now - t);
+    t = now;
+  };
+  const Arr nodes = get(B, MGP_FE_NODES), gnodes = get(B, MGP_FE_GPU_NODES), noff = get(B, MGP_FE_NODE_OFF),
+            consts = get(B, MGP_FE_CONSTS), coff = get(B, MGP_FE_CONST_OFF), voff = get(B, MGP_FE_VAR_OFF),
+            vwidth = get(B, MGP_FE_VAR_WIDTH), hoff = get(B, MGP_FE_HINT_OFF), hints = get(B, MGP_FE_HINTS),
+            aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES);
+  const uint32_t n_states = (uint32_t)(noff.n ? noff.n - 1 : 0);
+  if (n_states == 0) return MGP_OK;
+  const uint64_t *vo = (const uint64_t *)voff.p;
+  uint32_t n_vars = 1;
+  for (uint32_t s = 0; s < n_states; ++s) n_vars = std::max<uint32_t>(n_vars, (uint32_t)(vo[s + 1] - vo[s]));
+  if (out_n_vars) *out_n_vars = n_vars;
+  static const uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t *cp = consts.n ? (const uint32_t *)consts.p : zero8;
+
+  // 1. lower the GPU programs
+  std::vector<uint32_t> words;
+  std::vector<uint64_t> offs;
+  std::vector<uint8_t> status;
+  int rc = mgp_lower_vec((const mgp_node *)gnodes.p, (const uint64_t *)noff.p, n_states, cp,
+                         (const uint64_t *)coff.p, 0, words, offs, status);
+  if (rc != MGP_OK) return mgp_ctx_fail(ctx, rc, "lowering failed");
+  std::vector<uint32_t> order(n_states), bounds(257), bslots(256);
+  const int nb = mgp_plan_buckets(words.data(), offs.data(), n_states, order.data(), bounds.data(), bslots.data(),
+                                  256);
+  if (nb < 0) return mgp_ctx_fail(ctx, MGP_E_ARG, "bucket planning failed");
+  uint32_t max_slots = 0;
+  for (int b = 0; b < nb; ++b) max_slots = std::max(max_slots, bslots[b]);
+  // parent-witness rows: for every state whose parent witness is given, the parent's
+  // value of each of its variable slots (matched by slot key = name, kind, aux)
+  std::vector<int32_t> pidx(n_states, -1);
+  std::vector<uint32_t> pvals;
+  std::vector<uint8_t> pmask;
+  if (parent_off && parent_keys && parent_vals && slot_keys) {
+    uint32_t np = 0;
+    for (uint32_t s = 0; s < n_states; ++s)
+      if (parent_off[s + 1] > parent_off[s]) pidx[s] = (int32_t)np++;
+    pvals.assign((size_t)np * n_vars * 8u, 0u);
+    pmask.assign((size_t)np * n_vars, 0u);
+    const uint32_t *vw = (const uint32_t *)vwidth.p;
+#pragma omp parallel for schedule(dynamic, 8)
+    for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+      if (pidx[s] < 0) continue;
+      std::unordered_map<uint64_t, uint64_t> at;
+      for (uint64_t k = parent_off[s]; k < parent_off[s + 1]; ++k) at.emplace(parent_keys[k], k);
+      for (uint64_t v = vo[s]; v < vo[s + 1]; ++v) {
+        auto it = at.find(slot_keys[v]);
+        if (it == at.end()) continue;
+        uint32_t *d = &pvals[((size_t)pidx[s] * n_vars + (v - vo[s])) * 8u];
+        memcpy(d, parent_vals + it->second * 8u, 32);
+        const uint32_t w = vw[v];
+        for (int l = 0; l < 8; ++l) {
+          const int lo = 32 * l;
+          d[l] &= (int)w >= lo + 32 ? 0xFFFFFFFFu : ((int)w <= lo ? 0u : ((1u << (w - lo)) - 1u));
+        }
+        pmask[(size_t)pidx[s] * n_vars + (v - vo[s])] = 1;
+      }
+    }
+  }
+  lap(0);
+
+  // 2. upload
+  void *stp = nullptr;
+  int dev = 0;
+  mgp_ctx_stream(ctx, &stp, &dev);
+  hipStream_t st = (hipStream_t)stp;
+  hipError_t e = hipSetDevice(dev);
+  PipeBufs &D = bufs_of()[ctx];
+  const size_t cand_bytes = (size_t)n_states * n_cand * n_vars * 32u;
+  const uint32_t n_chunks = (n_cand + 63u) / 64u;
+  // one table buffer: var_off | var_width | hint_off | hints | alias_off | aliases | const_off | consts |
+  // fixed | parent_idx | pvals | pmask, each 256-B aligned
+  // (mgp_fe_get counts elements of each array: u32 limbs for consts / hints / aliases)
+  const size_t sizes[12] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+                            coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32,
+                            (size_t)n_states * 4, pvals.size() * 4, pmask.size()};
+  const void *srcs[12] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
+                          pidx.data(), pvals.data(), pmask.data()};
+  size_t at[13];
+  at[0] = 0;
+  for (int i = 0; i < 12; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[12]);
+  for (int i = 0; i < 12; ++i)
+    if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
+  if (e == hipSuccess) e = D.ensure(B_WORDS, words.size() * 4u);
+  if (e == hipSuccess) e = D.ensure(B_OFFS, offs.size() * 8u);
+  if (e == hipSuccess) e = D.ensure(B_ORDER, (size_t)n_states * 4u);
+  if (e == hipSuccess) e = D.ensure(B_CANDS, cand_bytes);
+  if (e == hipSuccess) e = D.ensure(B_FIRST, (size_t)n_states * 4u);
+  if (e == hipSuccess) e = D.ensure(B_WIT, (size_t)n_states * n_vars * 32u);
+  if (e == hipSuccess) e = D.ensure(B_PART, (size_t)n_states * n_chunks * 4u);
+  if (e == hipSuccess) e = D.ensure(B_TABLES, at[12]);
+  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_WORDS], words.data(), words.size() * 4u, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_OFFS], offs.data(), offs.size() * 8u, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(D.p[B_ORDER], order.data(), (size_t)n_states * 4u, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], stage.data(), at[12], hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+  const uint8_t *tb = (const uint8_t *)D.p[B_TABLES];
+  e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
+                          (const uint32_t *)(tb + at[1]), (const uint64_t *)(tb + at[2]),
+                          (const uint32_t *)(tb + at[3]), (const uint64_t *)(tb + at[4]),
+                          (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
+                          (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed,
+                          (const int32_t *)(tb + at[9]), (const uint32_t *)(tb + at[10]),
+                          (const uint8_t *)(tb + at[11]), (uint32_t *)D.p[B_CANDS], st);
+  if (e == hipSuccess) e = hipMemsetAsync(D.p[B_PART], 0x7E, (size_t)n_states * n_chunks * 4u, st);
+  if (e == hipSuccess)
+    e = mgp_launch_eval((const uint32_t *)D.p[B_WORDS], (const uint64_t *)D.p[B_OFFS], n_states,
+                        (const uint32_t *)D.p[B_CANDS], n_cand, n_vars, max_slots, (int32_t *)D.p[B_FIRST],
+                        (uint32_t *)D.p[B_WIT], (int32_t *)D.p[B_PART], (const uint32_t *)D.p[B_ORDER],
+                        bounds.data(), bslots.data(), (uint32_t)nb, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(out_first, D.p[B_FIRST], (size_t)n_states * 4u, hipMemcpyDeviceToHost, st);
+  if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+  lap(1);
+
+  // 4. host UNSAT pre-check on the original nodes while the GPU runs
+  if (flags & MGP_CHECK_NO_REFUTE) {
+    memset(out_refuted, 0, n_states);
+  } else {
+    rc = mgp_refute((const mgp_node *)nodes.p, (const uint64_t *)noff.p, n_states, cp, (const uint64_t *)coff.p, 0,
+                    out_refuted);
+    if (rc != MGP_OK) {
+      (void)hipStreamSynchronize(st);
+      return mgp_ctx_fail(ctx, rc, "mgp_refute failed");
+    }
+  }
+  lap(2);
+  e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+  lap(3);
+  // 5. witnesses of the SAT states
+  if (out_witness) {
+    std::vector<uint32_t> w((size_t)n_states * n_vars * 8u);
+    e = hipMemcpy(w.data(), D.p[B_WIT], w.size() * 4u, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+    for (uint32_t s = 0; s < n_states; ++s)
+      if (out_first[s] >= 0) memcpy(out_witness + (size_t)s * n_vars * 8u, w.data() + (size_t)s * n_vars * 8u,
+                                    (size_t)n_vars * 32u);
+  }
+  for (uint32_t s = 0; s < n_states; ++s)
+    if (status[s] != MGP_ST_OK && out_first[s] >= 0) out_first[s] = MGP_UNDECIDED;  // never expected
+  lap(4);
+  return MGP_OK;
+}
+
+// Test hook: the candidates mgp_check_batch evaluates, copied back in the device layout
+// [state][var][half][cand] of 16-byte groups (tests compare them with mgp_make_candidates).
+int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
+                      const uint32_t *fixed_pool, uint32_t n_fixed, uint32_t *out) {
+  if (!ctx || !B || !out || n_cand == 0 || n_vars == 0) return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument");
+  const Arr noff = get(B, MGP_FE_NODE_OFF), consts = get(B, MGP_FE_CONSTS), coff = get(B, MGP_FE_CONST_OFF),
+            voff = get(B, MGP_FE_VAR_OFF), vwidth = get(B, MGP_FE_VAR_WIDTH), hoff = get(B, MGP_FE_HINT_OFF),
+            hints = get(B, MGP_FE_HINTS), aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES);
+  const uint32_t n_states = (uint32_t)(noff.n ? noff.n - 1 : 0);
+  if (n_states == 0) return MGP_OK;
+  void *stp = nullptr;
+  int dev = 0;
+  mgp_ctx_stream(ctx, &stp, &dev);
+  hipStream_t st = (hipStream_t)stp;
+  static const uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const size_t sizes[9] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+                           coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32};
+  const void *srcs[9] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
+                         consts.n ? consts.p : zero8, fixed_pool};
+  size_t at[10];
+  at[0] = 0;
+  for (int i = 0; i < 9; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[9]);
+  for (int i = 0; i < 9; ++i)
+    if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
+  const size_t cb = (size_t)n_states * n_cand * n_vars * 32u;
+  void *dt = nullptr, *dc = nullptr;
+  hipError_t e = hipSetDevice(dev);
+  if (e == hipSuccess) e = hipMalloc(&dt, at[9]);
+  if (e == hipSuccess) e = hipMalloc(&dc, cb);
+  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[9], hipMemcpyHostToDevice, st);
+  const uint8_t *tb = (const uint8_t *)dt;
+  if (e == hipSuccess)
+    e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
+                            (const uint32_t *)(tb + at[1]), (const uint64_t *)(tb + at[2]),
+                            (const uint32_t *)(tb + at[3]), (const uint64_t *)(tb + at[4]),
+                            (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
+                            (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed, nullptr,
+                            nullptr, nullptr, (uint32_t *)dc, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dc, cb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (dt) (void)hipFree(dt);
+  if (dc) (void)hipFree(dc);
+  return e == hipSuccess ? MGP_OK : mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -1057,7 +1057,7 @@ extern "C" int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets, u
                           const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
                           int8_t *out) {
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
-#pragma omp parallel for schedule(dynamic, 64)
+#pragma omp parallel for schedule(dynamic, 8)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
     const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
@@ -1137,7 +1137,7 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
                                      uint32_t n_decide, uint32_t *cands, int8_t *out) {
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets || !cands)) || every == 0u)
     return MGP_E_ARG;
-#pragma omp parallel for schedule(dynamic, 64)
+#pragma omp parallel for schedule(dynamic, 8)
   for (int64_t st = 0; st < (int64_t)n_states; ++st) {
     const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
     const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];

@@ -176,10 +176,22 @@ int mgp_create(int device, mgp_ctx **out) {
   return MGP_OK;
 }
 
+void mgp_pipeline_release(mgp_ctx *ctx);  // mgp_pipeline.cpp
+
+int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device) {
+  if (!ctx) return MGP_E_ARG;
+  *stream = ctx->stream;
+  *device = ctx->device;
+  return MGP_OK;
+}
+
+int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg) { return fail(ctx, code, msg ? msg : ""); }
+
 void mgp_destroy(mgp_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  mgp_pipeline_release(ctx);
   for (DevBuf *b : {&ctx->words, &ctx->offs, &ctx->cand_aos, &ctx->cand_soa, &ctx->first, &ctx->wit,
                     &ctx->partial, &ctx->kin, &ctx->kout, &ctx->order})
     b->release();

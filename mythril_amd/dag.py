@@ -41,6 +41,10 @@ class StateDag:
     # wide values (> 256 bits, include/mgp_ir.h): first slot -> full width; the value
     # occupies ceil(width/256) consecutive var slots / pool entries, low 256 bits first
     wide: Dict[int, int] = field(default_factory=dict)
+    # padded key equalities (csrc/mgp_front.cpp): node index -> TRUE/FALSE op in the GPU
+    # program; flags bit 0 = such an equality under both polarities (no GPU SAT answer)
+    gpu_ops: Dict[int, int] = field(default_factory=dict)
+    flags: int = 0
 
     @property
     def n_vars(self) -> int:
@@ -114,7 +118,59 @@ def build_state(constraints: Sequence[Term]) -> StateDag:
         if r != len(d.nodes) - 1:  # root must be the last node
             d.nodes.append((ir.BAND, 1, r, r, -1, 0, 0))
     _harvest_hints(d)
+    _strengthen_padded(d)
     return d
+
+
+def _is_padded_eq(nodes, n) -> bool:
+    """EQ(ZEXT(CONST), x) with x not constant: a narrower constant key compared with a
+    wider value (bitvec.py:16-22, keccak_function_manager.py:141-145)."""
+    op, w, a, b = n[0], n[1], n[2], n[3]
+    if op != ir.EQ or a < 0 or b < 0:
+        return False
+
+    def zc(x):
+        return nodes[x][0] == ir.ZEXT and nodes[x][2] >= 0 and nodes[nodes[x][2]][0] == ir.CONST
+
+    return (zc(a) and nodes[b][0] != ir.CONST) or (zc(b) and nodes[a][0] != ir.CONST)
+
+
+def _strengthen_padded(d: StateDag) -> None:
+    """Polarity of every padded key equality from the root; positive -> FALSE, negative ->
+    TRUE in the GPU program (a stronger formula: its witnesses are models with or without
+    those disjuncts), both -> flags |= 1 (csrc/mgp_front.cpp explains why)."""
+    nodes = d.nodes
+    if not any(_is_padded_eq(nodes, n) for n in nodes):
+        return
+    pol = [0] * len(nodes)
+    pol[-1] = 1
+    for i in range(len(nodes) - 1, -1, -1):
+        p = pol[i]
+        if not p:
+            continue
+        op, _, a, b, c = nodes[i][:5]
+        if op in (ir.BAND, ir.BOR):
+            for x in (a, b):
+                if x >= 0:
+                    pol[x] |= p
+        elif op == ir.BNOT:
+            pol[a] |= ((p & 1) << 1) | (p >> 1)
+        elif op in (ir.BXOR, ir.BEQ):
+            pol[a] |= 3
+            pol[b] |= 3
+        elif op == ir.BITE:
+            pol[a] |= 3
+            pol[b] |= p
+            pol[c] |= p
+        elif op == ir.ITE:
+            pol[a] |= 3
+    for i, n in enumerate(nodes):
+        if pol[i] and _is_padded_eq(nodes, n):
+            if pol[i] == 3:
+                d.flags |= 1
+            else:
+                d.gpu_ops[i] = ir.FALSE if pol[i] == 1 else ir.TRUE
+                d.flags |= 2
 
 
 def _var_of(nodes, x) -> int:
@@ -150,8 +206,9 @@ def _harvest_hints(d: StateDag) -> None:
             d.hints.setdefault(vi, []).extend(vals)
 
 
-def pack_states(states: Sequence[StateDag]):
-    """-> (nodes NODE_DTYPE, node_offsets u64, consts u32[n,8], const_offsets u64)."""
+def pack_states(states: Sequence[StateDag], gpu: bool = False):
+    """-> (nodes NODE_DTYPE, node_offsets u64, consts u32[n,8], const_offsets u64);
+    gpu=True: the GPU program (padded key equalities replaced, see _strengthen_padded)."""
     n_nodes = sum(len(s.nodes) for s in states)
     nodes = np.zeros(n_nodes, dtype=NODE_DTYPE)
     noff = np.zeros(len(states) + 1, dtype=np.uint64)
@@ -160,8 +217,11 @@ def pack_states(states: Sequence[StateDag]):
     coff = np.zeros(len(states) + 1, dtype=np.uint64)
     i = j = 0
     for k, s in enumerate(states):
-        for (op, w, a, b, c, p0, p1) in s.nodes:
-            nodes[i] = (op, 0, w, a, b, c, p0, p1)
+        for k_, (op, w, a, b, c, p0, p1) in enumerate(s.nodes):
+            if gpu and k_ in s.gpu_ops:
+                nodes[i] = (s.gpu_ops[k_], 0, 1, -1, -1, -1, 0, 0)
+            else:
+                nodes[i] = (op, 0, w, a, b, c, p0, p1)
             i += 1
         for v in s.consts:
             consts[j] = [(v >> (32 * l)) & 0xFFFFFFFF for l in range(8)] if v < (1 << 256) else 0

@@ -1,0 +1,278 @@
+"""Native front end: a batch of states' constraint terms -> packed DAGs, variable tables, hints.
+
+`Batch(term_lists)` hands the term arena (smt.ARENA) and the root term ids of every
+state to `mgp_build_states` (csrc/mgp_front.cpp, OpenMP over states) and exposes
+the result as numpy views: exactly the arrays mythril_amd/dag.py build_state +
+pack_states (+ make_candidates' flattened tables) produce in Python, which stay as
+the reference implementation the tests pin this one against.  Replaces, per batch,
+the per-state re-adding of every constraint to a fresh z3 solver that
+Constraints.is_possible (constraints.py:34-51) and get_model (analysis/solver.py:
+37-50) do.
+"""
+from __future__ import annotations
+
+import ctypes
+from collections.abc import Mapping
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .smt import ARENA, Term
+
+FE_SAT_UNSAFE = 0x1
+FE_STRENGTHENED = 0x2
+
+# include/mgp.h enum mgp_fe_field -> (index, dtype, items per entry)
+_FIELDS = {
+    "nodes": (0, N.NODE_DTYPE, 1), "gpu_nodes": (1, N.NODE_DTYPE, 1), "node_off": (2, np.uint64, 1),
+    "consts": (3, np.uint32, 8), "const_off": (4, np.uint64, 1), "var_off": (5, np.uint64, 1),
+    "var_width": (6, np.uint32, 1), "var_full": (7, np.uint32, 1), "var_name": (8, np.uint32, 1),
+    "var_aux": (9, np.uint32, 1), "var_kind": (10, np.uint8, 1), "hint_off": (11, np.uint64, 1),
+    "hints": (12, np.uint32, 8), "alias_off": (13, np.uint64, 1), "aliases": (14, np.uint32, 2),
+    "flags": (15, np.uint8, 1), "var_key": (16, np.uint64, 1),
+}
+_VAR_TABLES = ("var_off", "var_width", "var_full", "var_name", "var_aux", "var_kind", "var_key")
+FIXED_POOL_LIMBS = None  # dag._FIXED_LIMBS (set lazily: dag imports the native module too)
+
+
+def _arena_ptr(a) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.buffer_info()[0])
+
+
+class Batch:
+    """Flattened constraint DAGs of n states (owned by the native batch object)."""
+
+    def __init__(self, term_lists: Sequence[Sequence[Term]]):
+        L = N.lib()
+        roots = np.fromiter((t.tid for lst in term_lists for t in lst), dtype=np.int32)
+        off = np.zeros(len(term_lists) + 1, np.uint64)
+        if len(term_lists):
+            off[1:] = np.cumsum([len(lst) for lst in term_lists])
+        if roots.size == 0:
+            roots = np.zeros(1, np.int32)
+        self.n_states = len(term_lists)
+        self._vt = None
+        self._h = ctypes.c_void_p()
+        A = ARENA
+        rc = L.mgp_build_states(_arena_ptr(A.op), _arena_ptr(A.width), _arena_ptr(A.args), _arena_ptr(A.p),
+                                len(A.op), _arena_ptr(A.limbs), len(A.limbs), N._ptr(roots), N._ptr(off),
+                                self.n_states, ctypes.byref(self._h))
+        N._check(rc)
+        for name, (idx, dt, per) in _FIELDS.items():
+            p, n = ctypes.c_void_p(), ctypes.c_uint64()
+            N._check(L.mgp_fe_get(self._h, idx, ctypes.byref(p), ctypes.byref(n)))
+            cnt = int(n.value)
+            if cnt == 0 or not p.value:
+                arr = np.zeros((0, per) if per > 1 else 0, dtype=dt)
+            else:
+                buf = (ctypes.c_char * (cnt * np.dtype(dt).itemsize)).from_address(p.value)
+                arr = np.frombuffer(buf, dtype=dt)
+                if per > 1:
+                    arr = arr.reshape(-1, per)
+            setattr(self, name, arr)
+
+    def var_tables(self) -> "VarTables":
+        """Owned copies of the variable tables (witnesses outlive the native batch)."""
+        if self._vt is None:
+            self._vt = VarTables(*(np.array(getattr(self, k)) for k in _VAR_TABLES))
+        return self._vt
+
+    def check(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True):
+        """-> (first_sat i32[n], witness u32[n, n_vars, 8], refuted i8[n], stage ms[5]) through the
+        context's check_batch (mgp_check_batch on a libmgp context)."""
+        return ctx.check_batch(self, n_cand, seed, parents, refute)
+
+    def _check_native(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True):
+        """mgp_check_batch on libmgp context `ctx`."""
+        global FIXED_POOL_LIMBS
+        if FIXED_POOL_LIMBS is None:
+            from .dag import _FIXED_LIMBS
+
+            FIXED_POOL_LIMBS = np.ascontiguousarray(_FIXED_LIMBS, dtype=np.uint32)
+        n = self.n_states
+        n_vars = max(1, self.n_vars())
+        first = np.full(n, N.MGP_NO_SAT, np.int32)
+        wit = np.zeros((n, n_vars, 8), np.uint32)
+        ref = np.zeros(max(n, 1), np.int8)
+        times = np.zeros(5, np.float64)
+        nv = ctypes.c_uint32(0)
+        pk = pv = po = None
+        if parents is not None and any(p is not None for p in parents):
+            ks, vs, cnt = [], [], []
+            for p in parents:
+                k, v = parent_arrays(p)
+                ks.append(k)
+                vs.append(v)
+                cnt.append(len(k))
+            pk = np.ascontiguousarray(np.concatenate(ks), dtype=np.uint64)
+            pv = np.ascontiguousarray(np.concatenate(vs).reshape(-1, 8), dtype=np.uint32)
+            po = np.zeros(n + 1, np.uint64)
+            po[1:] = np.cumsum(cnt)
+            if pk.size == 0:
+                pk, pv = np.zeros(1, np.uint64), np.zeros((1, 8), np.uint32)
+        rc = N.lib().mgp_check_batch(ctx._h, self._h, n_cand, seed & (2 ** 64 - 1), N._ptr(FIXED_POOL_LIMBS),
+                                     len(FIXED_POOL_LIMBS), N._ptr(pk), N._ptr(pv), N._ptr(po),
+                                     N._ptr(self.var_key) if pk is not None else None,
+                                     0 if refute else 1, N._ptr(first), N._ptr(wit), N._ptr(ref),
+                                     ctypes.byref(nv), N._ptr(times))
+        N._check(rc, ctx._h)
+        return first, wit, ref[:n], times
+
+    def device_candidates(self, ctx, n_cand: int, n_vars: int, seed: int) -> np.ndarray:
+        """Test hook (mgp_fe_candidates): the GPU-generated first-round candidates, returned in
+        the host layout [state][cand][var][8] of mgp_make_candidates."""
+        global FIXED_POOL_LIMBS
+        if FIXED_POOL_LIMBS is None:
+            from .dag import _FIXED_LIMBS
+
+            FIXED_POOL_LIMBS = np.ascontiguousarray(_FIXED_LIMBS, dtype=np.uint32)
+        n = self.n_states
+        dev = np.zeros((n, n_vars, 2, n_cand, 4), np.uint32)
+        N._check(N.lib().mgp_fe_candidates(ctx._h, self._h, n_cand, n_vars, seed & (2 ** 64 - 1),
+                                           N._ptr(FIXED_POOL_LIMBS), len(FIXED_POOL_LIMBS), N._ptr(dev)), ctx._h)
+        return np.ascontiguousarray(dev.transpose(0, 3, 1, 2, 4).reshape(n, n_cand, n_vars, 8))
+
+    def witness(self, s: int, words: np.ndarray) -> "SlotWitness":
+        """State s's witness (words [n_vars, 8]) as a lazily decoded {name: value} mapping."""
+        vt = self.var_tables()
+        v0, v1 = int(vt.var_off[s]), int(vt.var_off[s + 1])
+        return SlotWitness(vt, v0, v1, words[: v1 - v0])
+
+    def close(self) -> None:
+        if self._h:
+            N.lib().mgp_fe_free(self._h)
+            self._h = ctypes.c_void_p()
+            for name in _FIELDS:
+                setattr(self, name, None)
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ views
+    def packed(self, gpu: bool = False):
+        """(nodes, node_offsets, consts [n, 8], const_offsets) as dag.pack_states; gpu=True
+        gives the program the GPU evaluates (padded key equalities strengthened)."""
+        return (self.gpu_nodes if gpu else self.nodes), self.node_off, self.consts, self.const_off
+
+    def n_vars(self, s: Optional[int] = None) -> int:
+        if s is None:
+            return int(np.diff(self.var_off).max()) if self.n_states else 0
+        return int(self.var_off[s + 1] - self.var_off[s])
+
+    def var_names(self, s: int) -> List[str]:
+        """dag.StateDag.vars names of state s (`name`, `name#j`, `fn@node`)."""
+        out = []
+        j = 0
+        for v in range(int(self.var_off[s]), int(self.var_off[s + 1])):
+            j = 0 if self.var_full[v] else j + 1  # slot index within a wide value
+            nm = ARENA.names[int(self.var_name[v])]
+            if self.var_kind[v]:
+                nm = f"{nm}@{int(self.var_aux[v])}"
+            out.append(nm if j == 0 else f"{nm}#{j}")
+        return out
+
+    def witness_to_model(self, s: int, words: np.ndarray) -> Dict[str, int]:
+        """Witness words [n_vars, 8] of state s -> {name: value} (dag.witness_to_model)."""
+        v0, v1 = int(self.var_off[s]), int(self.var_off[s + 1])
+        w = np.ascontiguousarray(words[: v1 - v0], dtype=np.uint32)
+        vals = [int.from_bytes(w[i].tobytes(), "little") & ((1 << int(self.var_width[v0 + i])) - 1)
+                for i in range(v1 - v0)]
+        model: Dict[str, int] = {}
+        i = 0
+        while i < v1 - v0:
+            full = int(self.var_full[v0 + i])
+            k = max(1, (full + 255) // 256)
+            nm = ARENA.names[int(self.var_name[v0 + i])]
+            if self.var_kind[v0 + i]:
+                nm = f"{nm}@{int(self.var_aux[v0 + i])}"
+            model[nm] = sum(vals[i + j] << (256 * j) for j in range(k)) if k > 1 else vals[i]
+            i += k
+        return model
+
+
+class VarTables:
+    """Owned copies of a batch's per-slot variable tables."""
+
+    def __init__(self, var_off, var_width, var_full, var_name, var_aux, var_kind, var_key):
+        self.var_off, self.var_width, self.var_full = var_off, var_width, var_full
+        self.var_name, self.var_aux, self.var_kind, self.var_key = var_name, var_aux, var_kind, var_key
+
+
+class SlotWitness(Mapping):
+    """A GPU witness: slot keys + 8-limb values, decoded to {name: int} on first access
+    (dag.witness_to_model semantics).  Children reuse `keys`/`vals` directly as their
+    parent-witness row (mgp_check_batch)."""
+
+    __slots__ = ("_vt", "_v0", "_v1", "vals", "_d")
+
+    def __init__(self, vt: VarTables, v0: int, v1: int, vals: np.ndarray):
+        self._vt, self._v0, self._v1, self.vals, self._d = vt, v0, v1, vals, None
+
+    @property
+    def keys_array(self) -> np.ndarray:
+        return self._vt.var_key[self._v0: self._v1]
+
+    def _dict(self) -> Dict[str, int]:
+        if self._d is None:
+            vt, v0, v1 = self._vt, self._v0, self._v1
+            vals = [int.from_bytes(np.ascontiguousarray(self.vals[i]).tobytes(), "little")
+                    & ((1 << int(vt.var_width[v0 + i])) - 1) for i in range(v1 - v0)]
+            d: Dict[str, int] = {}
+            i = 0
+            while i < v1 - v0:
+                full = int(vt.var_full[v0 + i])
+                k = max(1, (full + 255) // 256)
+                nm = ARENA.names[int(vt.var_name[v0 + i])]
+                if vt.var_kind[v0 + i]:
+                    nm = f"{nm}@{int(vt.var_aux[v0 + i])}"
+                d[nm] = sum(vals[i + j] << (256 * j) for j in range(k)) if k > 1 else vals[i]
+                i += k
+            self._d = d
+        return self._d
+
+    def __getitem__(self, k):
+        return self._dict()[k]
+
+    def __iter__(self):
+        return iter(self._dict())
+
+    def __len__(self):
+        return len(self._dict())
+
+    def __repr__(self):
+        return f"SlotWitness({self._dict()!r})"
+
+
+_KIND_UF = 1 << 63
+
+
+def parent_arrays(p) -> "tuple[np.ndarray, np.ndarray]":
+    """(slot keys u64[k], values u32[k, 8]) of a parent witness: a SlotWitness as is; a
+    {name: value} dict (e.g. a fallback solver's model) by name -- `name`, `fn@node`,
+    a value wider than 256 bits spread over its pieces."""
+    if p is None:
+        return np.zeros(0, np.uint64), np.zeros((0, 8), np.uint32)
+    if isinstance(p, SlotWitness):
+        return p.keys_array, np.ascontiguousarray(p.vals, dtype=np.uint32).reshape(-1, 8)
+    keys: List[int] = []
+    vals: List[bytes] = []
+    for name, value in p.items():
+        if not isinstance(value, int):
+            continue
+        uf = "@" in name and name.rsplit("@", 1)[1].isdigit()
+        base, node = (name.rsplit("@", 1)[0], int(name.rsplit("@", 1)[1])) if uf else (name, 0)
+        nid = ARENA.name_id.get(base)
+        if nid is None:
+            continue
+        value &= (1 << 2048) - 1
+        for j in range(max(1, (value.bit_length() + 255) // 256)):
+            piece = (value >> (256 * j)) & ((1 << 256) - 1)
+            keys.append((_KIND_UF | (nid << 32) | ((node & 0xFFFFFF) << 8) | j) if uf else ((nid << 32) | j))
+            vals.append(piece.to_bytes(32, "little"))
+    if not keys:
+        return np.zeros(0, np.uint64), np.zeros((0, 8), np.uint32)
+    return np.array(keys, np.uint64), np.frombuffer(b"".join(vals), np.uint32).reshape(-1, 8)

@@ -23,6 +23,7 @@ decided here: that is the GPU kernel's job (or z3's).
 from __future__ import annotations
 
 import weakref
+from array import array
 from typing import Any, Dict, List, Optional, Sequence, Set, Tuple, Union
 
 from . import ir
@@ -30,10 +31,62 @@ from . import ir
 Annotations = Set[Any]
 
 
-class Term:
-    """Hash-consed term node.  op/width/args/params as in include/mgp_ir.h."""
+class _Arena:
+    """Flat, append-only table of every term ever built: the native DAG builder
+    (mgp_build_states, csrc/mgp_front.cpp) walks it instead of the Python objects.
 
-    __slots__ = ("op", "width", "args", "params", "_h", "__weakref__")
+    Per term t: op[t], width[t] (Bool = 0), args[3t..3t+2] (term ids, -1 = none) and
+    p[2t], p[2t+1]: VAR (name id, 0), CONST (offset into `limbs`, number of u32 limbs,
+    little-endian), EXTRACT (hi, lo), UFAPP / UFINV (function id, function-name id).
+    Names are interned in `names`.  Entries of dead terms stay (about 30 B each).
+    """
+
+    def __init__(self):
+        self.op = array("B")
+        self.width = array("I")
+        self.args = array("i")
+        self.p = array("I")
+        self.limbs = array("I")
+        self.names: List[str] = []
+        self.name_id: Dict[str, int] = {}
+
+    def intern_name(self, name: str) -> int:
+        k = self.name_id.get(name)
+        if k is None:
+            k = self.name_id[name] = len(self.names)
+            self.names.append(name)
+        return k
+
+    def add(self, op: int, width: int, args: Tuple["Term", ...], params: Tuple) -> int:
+        tid = len(self.op)
+        self.op.append(op)
+        self.width.append(width)
+        ids = [a.tid for a in args] + [-1, -1, -1]
+        self.args.extend(ids[:3])
+        p0 = p1 = 0
+        if op == ir.VAR:
+            p0 = self.intern_name(str(params[0]))
+        elif op == ir.CONST:
+            n = max(1, (width + 31) // 32)
+            p0, p1 = len(self.limbs), n
+            self.limbs.frombytes(int(params[0]).to_bytes(4 * n, "little"))
+        elif op == ir.EXTRACT:
+            p0, p1 = params
+        elif op in (ir.UFAPP, ir.UFINV):
+            p0, p1 = params[0], self.intern_name(str(params[1]))
+        self.p.append(p0)
+        self.p.append(p1)
+        return tid
+
+
+ARENA = _Arena()
+
+
+class Term:
+    """Hash-consed term node.  op/width/args/params as in include/mgp_ir.h; `tid` is
+    its row in the term arena (ARENA) the native DAG builder reads."""
+
+    __slots__ = ("op", "width", "args", "params", "_h", "tid", "__weakref__")
 
     def __init__(self, op: int, width: int, args: Tuple["Term", ...], params: Tuple):
         self.op = op
@@ -41,6 +94,7 @@ class Term:
         self.args = args
         self.params = params
         self._h = hash((op, width, tuple(id(a) for a in args), params))
+        self.tid = ARENA.add(op, width, args, params)
 
     def __hash__(self):
         return self._h
@@ -329,11 +383,13 @@ def _coerce(x: Union["BitVec", int], w: int) -> "BitVec":
 
 
 def _padded(a: Term, b: Term) -> Tuple[Term, Term]:
-    """bitvec.py:16-22: zero-extend the narrower operand."""
+    """bitvec.py:16-22: zero-extend the narrower operand.  A narrower constant stays a
+    ZEXT node (not folded): z3 sees Concat(BitVecVal(0, k), c) there, and the builder
+    treats such a cross-width key equality specially (dag.py, padded equalities)."""
     if a.width < b.width:
-        a = zext(a, b.width)
+        a = mk(ir.ZEXT, b.width, (a,)) if a.op == ir.CONST and b.op != ir.CONST else zext(a, b.width)
     elif b.width < a.width:
-        b = zext(b, a.width)
+        b = mk(ir.ZEXT, a.width, (b,)) if b.op == ir.CONST and a.op != ir.CONST else zext(b, a.width)
     return a, b
 
 

@@ -190,19 +190,44 @@ class UnsatCores:
 
     @staticmethod
     def shrink(N, terms: Sequence[Term], max_terms: int = 32) -> List[Term]:
-        """Deletion-based core of a refuted constraint list: one batched mgp_refute call
-        tries every single-constraint deletion; the constraints whose deletion breaks the
-        refutation form the core if the refuter still refutes them alone."""
-        terms = list(dict.fromkeys(terms))
-        if len(terms) < 2 or len(terms) > max_terms:
-            return terms
-        trials = [terms[:i] + terms[i + 1:] for i in range(len(terms))]
-        dags = [D.build_state(t) for t in trials]
-        v = N.refute(*D.pack_states(dags))
-        need = [terms[i] for i in range(len(terms)) if v[i] != 1]
-        if need and len(need) < len(terms) and N.refute(*D.pack_states([D.build_state(need)]))[0] == 1:
-            return need
-        return terms
+        """Deletion-based core of one refuted constraint list (see shrink_many)."""
+        return UnsatCores.shrink_many(N, [terms], max_terms)[0]
+
+    @staticmethod
+    def shrink_many(N, lists: Sequence[Sequence[Term]], max_terms: int = 32) -> List[List[Term]]:
+        """Deletion-based cores of many refuted constraint lists in two native calls: one
+        batch holds every single-constraint deletion of every list (mgp_build_states +
+        mgp_refute); the constraints whose deletion breaks a refutation form that list's
+        core if a second batched refute confirms it alone."""
+        from .front import Batch
+
+        lists = [list(dict.fromkeys(t)) for t in lists]
+        trials, owner = [], []
+        for k, t in enumerate(lists):
+            if 2 <= len(t) <= max_terms:
+                trials.extend(t[:i] + t[i + 1:] for i in range(len(t)))
+                owner.extend([k] * len(t))
+        if not trials:
+            return lists
+        B = Batch(trials)
+        v = N.refute(*B.packed())
+        B.close()
+        need: Dict[int, List[Term]] = {}
+        pos = 0
+        for k, t in enumerate(lists):
+            if 2 <= len(t) <= max_terms:
+                need[k] = [t[i] for i in range(len(t)) if v[pos + i] != 1]
+                pos += len(t)
+        cand = [k for k, nd in need.items() if nd and len(nd) < len(lists[k])]
+        out = list(lists)
+        if cand:
+            B = Batch([need[k] for k in cand])
+            ok = N.refute(*B.packed())
+            B.close()
+            for k, r in zip(cand, ok):
+                if r == 1:
+                    out[k] = need[k]
+        return out
 
 
 _cores = UnsatCores()
@@ -229,7 +254,9 @@ class Prefilter:
         # fresh candidates (half of them guided by the pre-check's domains), up to retry_cand
         # per state (host candidate memory capped at 1 GiB)
         self.retry_cand = 1024
-        self.cand_bytes = 1 << 30  # host candidate memory of one witness round
+        self.cand_bytes = 1 << 30  # candidate memory of one witness round
+        self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
+        self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
     def check_states(self, states: Sequence[Sequence[Term]],
                      parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> List[Tuple[str, Optional[Dict[str, int]]]]:
@@ -251,8 +278,7 @@ class Prefilter:
             rest_par = None if parents is None else [p for p, h in zip(parents, hit) if not h]
             sub = iter(self.check_states(rest, rest_par) if rest else [])
             return [(unsat, None) if h else next(sub) for h in hit]
-        dags = [D.build_state(s) for s in states]
-        out = self._check_built(states, dags, parents)
+        out = self._check_native(states, parents)
         stats.gpu_batches += 1
         stats.gpu_queries += len(states)
         stats.gpu_sat += sum(1 for r in out if r[0] == sat)
@@ -261,65 +287,101 @@ class Prefilter:
         stats.gpu_time += time.time() - t0
         return out
 
-    def _check_built(self, states, dags, parents):
-        """Candidate memory of one round is n_states x n_cand x n_vars x 32 B with n_vars the
-        batch maximum: a batch past `cand_bytes` is split into sub-batches of similar n_vars."""
-        n_vars = max(1, max(d.n_vars for d in dags))
-        if len(dags) > 1 and len(dags) * self.n_cand * n_vars * 32 > self.cand_bytes:
-            order = sorted(range(len(dags)), key=lambda i: dags[i].n_vars)
-            res: List = [None] * len(dags)
+    def _check_native(self, states, parents):
+        """One native front-end batch (mgp_build_states) through mgp_check_batch: GPU
+        witnesses, host refutations overlapped with the GPU; a second, domain-guided
+        witness round for what is left; cores of the refuted states, batched.  A batch
+        whose candidate block would pass `cand_bytes` is split into sub-batches of
+        similar variable counts."""
+        from .front import FE_SAT_UNSAFE, Batch
+
+        tb = time.perf_counter()
+        B = Batch(states)
+        nv = np.diff(B.var_off).astype(np.int64)
+        n_vars = max(1, int(nv.max()) if len(nv) else 1)
+        if len(states) > 1 and len(states) * self.n_cand * n_vars * 32 > self.cand_bytes:
+            B.close()
+            order = sorted(range(len(states)), key=lambda i: int(nv[i]))
+            res: List = [None] * len(states)
             grp: List[int] = []
             for i in order + [None]:
                 if i is not None:
-                    nv = max(1, dags[i].n_vars)
-                    if not grp or (len(grp) + 1) * self.n_cand * nv * 32 <= self.cand_bytes:
+                    w = max(1, int(nv[i]))
+                    if not grp or (len(grp) + 1) * self.n_cand * w * 32 <= self.cand_bytes:
                         grp.append(i)
                         continue
-                sub = self._check_built([states[k] for k in grp], [dags[k] for k in grp],
-                                        None if parents is None else [parents[k] for k in grp])
+                sub = self._check_native([states[k] for k in grp], None if parents is None else
+                                         [parents[k] for k in grp])
                 for k, r in zip(grp, sub):
                     res[k] = r
                 grp = [i] if i is not None else []
             return res
-        return self._check_round(states, dags, parents, n_vars)
-
-    def _check_round(self, states, dags, parents, n_vars):
-        stats = SolverStatistics()
-        nodes, noff, consts, coff = D.pack_states(dags)
-        words, po, status = self._N.lower(nodes, noff, consts, coff)
         self._calls += 1
-        cands = D.make_candidates(dags, self.n_cand, n_vars, seed=self.seed + self._calls, parents=parents)
-        first, wit = self.ctx.eval_batch(words, po, cands)
-        proven = self._N.refute(nodes, noff, consts, coff) if self.refute else np.zeros(len(dags), np.int8)
-        retry = [i for i in range(len(dags)) if first[i] == -1 and proven[i] != 1]
+        prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
+        first, wit, proven, times = B.check(self.ctx, self.n_cand, self.seed + self._calls, parents,
+                                            refute=self.refute)
+        self.last_times = times
+        for k, name in enumerate(("lower_ms", "upload_launch_ms", "refute_ms", "gpu_wait_ms", "copy_back_ms")):
+            prof[name] = float(times[k])
+        tr = time.perf_counter()
+        unsafe = (B.flags & FE_SAT_UNSAFE) != 0
+        first[unsafe & (first >= 0)] = -1  # no GPU SAT answer for those (mgp_front.cpp)
+        witnesses: Dict[int, object] = {}
+        retry = [i for i in range(len(states)) if first[i] == -1 and proven[i] != 1]
         if retry and self.retry_cand > self.n_cand:
-            budget = self.cand_bytes // (len(retry) * n_vars * 32)
-            n2 = min(self.retry_cand, budget) // 64 * 64
-            if n2 > self.n_cand:
-                sub = [dags[i] for i in retry]
-                packed = D.pack_states(sub)
-                sw, sp, _ = self._N.lower(*packed)
-                c2 = D.make_candidates(sub, n2, n_vars, seed=self.seed + 0x9E3779B9 + self._calls)
-                # every other row drawn from the pre-check's refined domains, the first 32 of
-                # those by decisions (mgp_guided_candidates); the rest keep hints / uniform draws
-                self._N.guided_candidates(*packed, c2, seed=self.seed + self._calls, every=2, n_decide=32)
-                f2, w2 = self.ctx.eval_batch(sw, sp, c2)
-                for k, i in enumerate(retry):
-                    if f2[k] >= 0:
-                        first[i], wit[i] = f2[k], w2[k]
-                stats.gpu_retry += len(retry)
-        out: List[Tuple[str, Optional[Dict[str, int]]]] = []
-        for i, d in enumerate(dags):
+            self._retry_round(states, retry, n_vars, first, witnesses)
+        prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
+        prof["retry_states"] = len(retry)
+        tr = time.perf_counter()
+        out: List[Tuple[str, Optional[object]]] = []
+        refuted = []
+        for i in range(len(states)):
             if first[i] >= 0:
                 if proven[i] == 1:  # a witness and an UNSAT proof cannot both hold
                     raise RuntimeError(f"mgp_refute refuted state {i} that has a GPU witness (soundness bug)")
-                out.append((sat, D.witness_to_model(d, wit[i])))
+                out.append((sat, witnesses[i] if i in witnesses else B.witness(i, wit[i])))
             elif proven[i] == 1:
                 out.append((unsat, None))
-                _cores.add(UnsatCores.shrink(self._N, states[i]))
+                refuted.append(i)
             else:
                 out.append(("undecided", None))
+        B.close()
+        prof["results_ms"] = 1e3 * (time.perf_counter() - tr)
+        tr = time.perf_counter()
+        if refuted:
+            for core in UnsatCores.shrink_many(self._N, [states[i] for i in refuted]):
+                _cores.add(core)
+        prof["cores_ms"] = 1e3 * (time.perf_counter() - tr)
+        self.last_profile = prof
         return out
+
+    def _retry_round(self, states, retry, n_vars, first, witnesses) -> None:
+        """Fresh candidates for the states the first round and the pre-check left open: up to
+        retry_cand per state (host candidate memory capped at cand_bytes), every other row
+        drawn from the pre-check's refined domains, the first 32 of those by decisions
+        (mgp_guided_candidates); the rest the usual hint / pool / uniform mixture."""
+        from . import dag as D
+        from .front import FE_SAT_UNSAFE, Batch
+
+        budget = self.cand_bytes // (len(retry) * n_vars * 32)
+        n2 = min(self.retry_cand, budget) // 64 * 64
+        if n2 <= self.n_cand:
+            return
+        SB = Batch([states[i] for i in retry])
+        sv = max(1, SB.n_vars())
+        sw, sp, _ = self._N.lower(*SB.packed(gpu=True))
+        c2 = self._N.make_candidates(n2, sv, self.seed + 0x9E3779B9 + self._calls, SB.var_off, SB.var_width,
+                                     SB.hint_off, SB.hints, SB.alias_off, SB.aliases, SB.const_off, SB.consts,
+                                     D._FIXED_LIMBS, np.zeros(len(retry), np.uint8))
+        self._N.guided_candidates(*SB.packed(), c2, seed=self.seed + self._calls, every=2, n_decide=32)
+        f2, w2 = self.ctx.eval_batch(sw, sp, c2)
+        unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
+        for k, i in enumerate(retry):
+            if f2[k] >= 0 and not unsafe[k]:
+                first[i] = f2[k]
+                witnesses[i] = SB.witness(k, w2[k])
+        SB.close()
+        SolverStatistics().gpu_retry += len(retry)
 
 
 _prefilter: Optional[Prefilter] = None

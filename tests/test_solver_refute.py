@@ -29,6 +29,14 @@ class NoWitnessContext:
         n = len(po) - 1
         return np.full(n, -1, dtype=np.int32), np.zeros((n, cands.shape[2], 8), dtype=np.uint32)
 
+    def check_batch(self, batch, n_cand, seed, parents=None, refute=True):
+        """mgp_check_batch without a GPU: no witness; the host pre-check as in the pipeline."""
+        self.batches += 1
+        n = batch.n_states
+        ref = N.refute(*batch.packed()) if refute else np.zeros(n, np.int8)
+        return (np.full(n, -1, dtype=np.int32), np.zeros((n, max(1, batch.n_vars()), 8), dtype=np.uint32), ref,
+                np.zeros(5))
+
     def close(self):
         pass
 

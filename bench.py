@@ -73,34 +73,12 @@ def _slice_states(b, idx):
 
 
 def _contract_states(n: int):
-    """n path-constraint lists shaped like BECToken's batchTransfer queries, built through the
-    laser.smt mirror: a calldata word (32 guarded byte selects, calldata.py:219-232), a
-    balances[msg.sender] read through keccak256_512 with the manager's condition
-    (keccak_function_manager.py:122-146) and the integer module's overflow query
-    (integer.py:141-160); every fourth state asks SafeMath.sub's underflow query, which
-    the balance check makes UNSAT (integer.py:155-160)."""
-    from mythril_amd.keccak import KeccakFunctionManager
-    from mythril_amd.smt import (Array, BVMulNoOverflow, BVSubNoUnderflow, Concat, If, Not, UGE, UGT, ULE, ULT,
-                                 symbol_factory)
+    """n path-constraint lists of the mixed contract corpus (corpus.py): suicide.sol kill,
+    BECToken.sol batchTransfer (overflow / underflow queries) and WalletLibrary.sol
+    initWallet -> kill (prune queries along tx 2 and the suicide module's query)."""
+    import corpus
 
-    bvv, bvs = symbol_factory.BitVecVal, symbol_factory.BitVecSym
-    kfm = KeccakFunctionManager()
-    calldata, size = Array("calldata", 256, 8), bvs("calldatasize", 256)
-    storage = Array("Storage", 256, 256)
-    caller = bvs("caller", 256)
-    out = []
-    for k in range(n):
-        off = 4 + 32 * (k % 3)
-        word = Concat(*[If(ULT(bvv(off + i, 256), size), calldata[bvv(off + i, 256)], bvv(0, 8)) for i in range(32)])
-        value = bvs(f"value_{k % 11}", 256)
-        slot, cond = kfm.create_keccak(Concat(caller, bvv(k % 5, 256)))
-        path = [cond, UGT(word, bvv(0, 256)), ULE(word, bvv(20 + k % 7, 256)), UGE(storage[slot], word * value)]
-        if k % 4 == 3:  # SafeMath.sub after require(balance >= amount): the underflow query is UNSAT
-            query = Not(BVSubNoUnderflow(storage[slot], word * value, False))
-        else:
-            query = Not(BVMulNoOverflow(word, value, False)) if k % 2 == 0 else ULT(storage[slot], bvv(k, 256))
-        out.append(tuple(c.raw for c in path + [query]))
-    return out
+    return [c[1] for c in corpus.corpus(n)]
 
 
 def main():
@@ -400,12 +378,22 @@ def main():
         dtf = time.perf_counter() - tf
         kinds = [r[0] for r in res]
         st = SV.SolverStatistics()
+        import collections
+
+        import corpus
+
+        labels = [c[0] for c in corpus.corpus(len(cs))]
+        by_shape = collections.defaultdict(collections.Counter)
+        for lab, k in zip(labels, kinds):
+            by_shape[lab.split(":")[0]][k] += 1
         frontend = {"states": len(cs), "seconds": dtf, "states_per_s": len(cs) / dtf,
                     "sat": kinds.count(SV.sat), "unsat": kinds.count(SV.unsat),
                     "refuted": st.refuted, "core_hits": st.core_hits,
                     "undecided": kinds.count("undecided"), "candidates": pf.n_cand,
+                    "by_contract": {k: dict(v) for k, v in by_shape.items()},
                     "stages_ms": pf.last_profile, "latency": frontend_latency(pf, SV, cs),
-                    "shape": "BECToken batchTransfer: calldata word, keccak256_512 mapping read, overflow / underflow query"}
+                    "shape": "mixed corpus (corpus.py): suicide.sol kill, BECToken.sol batchTransfer, "
+                             "WalletLibrary.sol initWallet -> kill"}
         pf.ctx.close()
         log(f"frontend: {frontend}")
 

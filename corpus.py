@@ -1,0 +1,229 @@
+"""Contract-shaped constraint corpus (test and benchmark infrastructure, not product).
+
+No solc / z3 / mythril exists here or on the GPU box, so `myth analyze` cannot run
+("not measurable").  This module restates, through the
+laser.smt mirror (mythril_amd.smt + the keccak manager mirror), the path constraints
+LASER builds on the configs' hot spots and the solver queries asked there, so the
+pre-filter can be measured on a MIXED corpus instead of one repeated shape:
+
+* suicide.sol ``kill(address)`` (solidity_examples/suicide.sol:3-6; suicide.py:76-99):
+  the dispatcher, the JUMPI on ``addr == 0`` and the module's attacker query, UNSAT
+  because the path forces addr == 0;
+* BECToken.sol ``batchTransfer`` (BECToken.sol:254-258; integer.py:141-160): calldata
+  words, ``balances[msg.sender]`` through keccak256_512 with the manager's condition,
+  the multiplication-overflow query (SAT) and SafeMath.sub's underflow query after the
+  balance check (UNSAT);
+* WalletLibrary.sol ``initWallet`` then ``kill`` (WalletLibrary.sol:91-104,219-226,
+  288-320): tx 1 writes m_dailyLimit, m_lastDay, m_numOwners, m_owners[1],
+  m_ownerIndex[msg.sender] (a Store at keccak256_512(Concat(sender, 263))), the bounded
+  owners loop (-b 3) and m_required; tx 2 reads them through the Store chain
+  (read-over-write), hashes msg.data with a symbolic length (a fresh KECCAC_mem[...]
+  symbol, instructions.py:1003-1015), 2**ownerIndex as a fresh symbol
+  (instructions.py:582-600), and the suicide module asks for to == ATTACKER.  The
+  prune filter's queries along tx 2 (both branches of every JUMPI) come with it.
+
+Every transaction adds LASER's setup constraints: the sender is one of the ACTORS
+(transaction/symbolic.py:165-167) and can pay the call value
+(transaction_models.py:129-133); non-payable functions add call_value == 0; the
+dispatcher compares calldata[0:4] as solc 0.5 does (DIV by 2^224, AND 0xffffffff).
+
+`corpus(n)` returns n (label, constraint-term tuple, expected) entries cycling over
+the shapes with varied transaction ids, slots and loop counts; `expected` is "sat" or
+"unsat" where the shape decides it by construction, else None.  The expectations are
+by reading, not pinned by any reference fixture (issue-level parity stays unpinned).
+"""
+from __future__ import annotations
+
+import copy
+from typing import List, Optional, Tuple
+
+from mythril_amd.keccak import KeccakFunctionManager
+from mythril_amd.smt import (And, Array, BVMulNoOverflow, BVSubNoUnderflow, Concat, Extract, If, Not, Or, UDiv, UGE,
+                             UGT, ULE, ULT, symbol_factory)
+
+BVV, BVS = symbol_factory.BitVecVal, symbol_factory.BitVecSym
+CREATOR = 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE
+ATTACKER = 0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF
+SOMEGUY = 0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA
+ACTORS = (CREATOR, ATTACKER, SOMEGUY)
+
+# WalletLibrary.sol storage slots (solc 0.5 layout of the FIELDS section, lines 374-399)
+S_REQUIRED, S_NUM_OWNERS, S_DAILY_LIMIT, S_SPENT_TODAY, S_LAST_DAY = 1, 2, 3, 4, 5
+S_OWNERS, S_OWNER_INDEX, S_PENDING = 6, 263, 264
+
+
+class Tx:
+    """One symbolic message call: calldata, sender, value and LASER's setup constraints."""
+
+    def __init__(self, tid: int, balance: Array):
+        self.tid = tid
+        self.calldata = Array(f"{tid}_calldata", 256, 8)
+        self.size = BVS(f"{tid}_calldatasize", 256)
+        self.sender = BVS(f"sender_{tid}", 256)
+        self.value = BVS(f"call_value{tid}", 256)
+        self.timestamp = BVS(f"{tid}_timestamp", 256)
+        self.setup = [Or(*[self.sender == BVV(a, 256) for a in ACTORS]), UGE(balance[self.sender], self.value)]
+
+    def byte(self, idx) -> "object":
+        """calldata.py:219-232: If(idx < calldatasize, calldata[idx], 0) -- BitVec `<`, i.e.
+        a SIGNED compare (bitvec.py:138-147)."""
+        i = idx if not isinstance(idx, int) else BVV(idx, 256)
+        return If(i < self.size, self.calldata[i], BVV(0, 8))
+
+    def word(self, off) -> "object":
+        base = off if not isinstance(off, int) else BVV(off, 256)
+        return Concat(*[self.byte(base + i) for i in range(32)])
+
+    def dispatch(self, sig: int, payable: bool = False) -> list:
+        """solc 0.5 dispatcher: calldatasize >= 4, (word0 / 2^224) & 0xffffffff == sig, and
+        CALLVALUE == 0 for a non-payable function."""
+        sel = UDiv(self.word(0), BVV(1 << 224, 256)) & BVV(0xFFFFFFFF, 256)
+        out = [Not(ULT(self.size, BVV(4, 256))), sel == BVV(sig, 256)]
+        if not payable:
+            out.append(self.value == BVV(0, 256))
+        return out
+
+
+def _attacker_query(txs: List[Tx], to) -> list:
+    """suicide.py:76-99: every transaction sent by the attacker (caller == origin), and
+    the beneficiary is the attacker."""
+    return [And(t.sender == BVV(ATTACKER, 256), t.sender == t.sender) for t in txs] + [to == BVV(ATTACKER, 256)]
+
+
+# ----------------------------------------------------------------- suicide.sol
+def suicide_states(tid: int = 1) -> List[Tuple[str, tuple, Optional[str]]]:
+    balance = Array("balance", 256, 256)
+    tx = Tx(tid, balance)
+    addr = Concat(BVV(0, 96), Extract(159, 0, tx.word(4)))
+    path = tx.setup + tx.dispatch(0xCBF0B0C0)
+    out = [("suicide:dispatch", path, "sat"),
+           ("suicide:addr!=0 (revert branch)", path + [Not(addr == BVV(0, 256))], "sat"),
+           ("suicide:addr==0", path + [addr == BVV(0, 256)], "sat"),
+           ("suicide:attacker query", path + [addr == BVV(0, 256)] + _attacker_query([tx], addr), "unsat")]
+    return [(l, tuple(c.raw for c in cs), e) for l, cs, e in out]
+
+
+# ---------------------------------------------------------------- BECToken.sol
+def bectoken_states(k: int, kfm: KeccakFunctionManager) -> Tuple[str, tuple, Optional[str]]:
+    """batchTransfer (BECToken.sol:254-258): cnt = receivers.length <= 20, value > 0,
+    balances[msg.sender] >= cnt * value; the integer module's queries."""
+    balance = Array("balance", 256, 256)
+    tx = Tx(2 + k % 3, balance)
+    storage = Array("Storage", 256, 256)
+    cnt = tx.word(4 + 64 * (k % 2))   # receivers.length (its offset word varies), never the value word
+    value = tx.word(36)
+    slot, cond = kfm.create_keccak(Concat(tx.sender, BVV(k % 5, 256)))
+    bal = storage[slot]
+    path = tx.setup + tx.dispatch(0x83F12FEC) + [cond, UGT(cnt, BVV(0, 256)), ULE(cnt, BVV(20, 256)),
+                                                 UGT(value, BVV(0, 256)), UGE(bal, cnt * value)]
+    if k % 4 == 3:  # SafeMath.sub after require(balance >= amount): cannot underflow
+        return ("bectoken:safemath sub underflow", tuple(c.raw for c in path + [
+            Not(BVSubNoUnderflow(bal, cnt * value, False))]), "unsat")
+    if k % 2 == 0:
+        return ("bectoken:mul overflow", tuple(c.raw for c in path + [Not(BVMulNoOverflow(cnt, value, False))]),
+                "sat")
+    return ("bectoken:balance below k", tuple(c.raw for c in path + [ULT(bal, BVV(k, 256))]), None)
+
+
+# ------------------------------------------------------------ WalletLibrary.sol
+class _Storage:
+    """The contract's storage across transactions: one Array with its Store chain."""
+
+    def __init__(self):
+        self.arr = Array("Storage", 256, 256)
+
+    def fork(self) -> "_Storage":
+        s = _Storage.__new__(_Storage)
+        s.arr = copy.copy(self.arr)
+        return s
+
+    def __getitem__(self, k):
+        return self.arr[k if not isinstance(k, int) else BVV(k, 256)]
+
+    def __setitem__(self, k, v):
+        self.arr[k if not isinstance(k, int) else BVV(k, 256)] = v
+
+
+def _mapping_slot(kfm, key, slot: int):
+    """m[key] for a mapping at `slot`: keccak256(Concat(key, slot)) + the manager's condition."""
+    h, cond = kfm.create_keccak(Concat(key, BVV(slot, 256)))
+    return h, cond
+
+
+def wallet_states(variant: int, kfm: KeccakFunctionManager) -> List[Tuple[str, tuple, Optional[str]]]:
+    """initWallet (tx 1) then kill (tx 2), `variant` picks the owners-loop count (0..2) and
+    the transaction ids; returns the prune queries along tx 2 and the module's query."""
+    n_loop = variant % 3
+    t1, t2 = 1 + 2 * (variant // 3), 2 + 2 * (variant // 3)
+    balance = Array("balance", 256, 256)
+    st = _Storage()
+    a, b = Tx(t1, balance), Tx(t2, balance)
+    path: list = a.setup + a.dispatch(0xE46DCFEB)            # initWallet(address[],uint256,uint256)
+    off = a.word(4)                                          # _owners: head word = offset
+    length = a.word(BVV(4, 256) + off)                       # _owners.length at 4 + offset
+    required, daylimit = a.word(36), a.word(68)
+    path.append(st[S_NUM_OWNERS] == BVV(0, 256))             # only_uninitialized
+    st[S_DAILY_LIMIT] = daylimit                             # initDaylimit
+    st[S_LAST_DAY] = UDiv(a.timestamp, BVV(86400, 256))      # today()
+    st[S_NUM_OWNERS] = length + BVV(1, 256)                  # initMultiowned
+    st[S_OWNERS + 1] = a.sender
+    k1, c1 = _mapping_slot(kfm, a.sender, S_OWNER_INDEX)
+    path.append(c1)
+    st[k1] = BVV(1, 256)
+    for i in range(n_loop):                                  # bounded loop (-b 3)
+        path.append(ULT(BVV(i, 256), length))
+        owner = a.word(BVV(4 + 32 * (i + 1), 256) + off)
+        st[S_OWNERS + 2 + i] = owner
+        ki, ci = _mapping_slot(kfm, owner, S_OWNER_INDEX)
+        path.append(ci)
+        st[ki] = BVV(2 + i, 256)
+    path.append(Not(ULT(BVV(n_loop, 256), length)))         # loop exit
+    st[S_REQUIRED] = required
+
+    # tx 2: kill(address _to) onlymanyowners(keccak256(msg.data))
+    path += b.setup + b.dispatch(0xCBF0B0C0)
+    to = Concat(BVV(0, 96), Extract(159, 0, b.word(4)))
+    op = BVS(f"KECCAC_mem[{0x5EED + variant}]", 256)          # SHA3 over a symbolic length
+    k2, c2 = _mapping_slot(kfm, b.sender, S_OWNER_INDEX)
+    path.append(c2)
+    owner_index = st[k2]
+    kp, cp = _mapping_slot(kfm, op, S_PENDING)
+    path.append(cp)
+    yet_needed = st[kp]
+    owners_done = st[kp + BVV(1, 256)]
+    bit = BVS(f"invhash({variant})**invhash(owner_index_{t2})", 256)
+    out: List[Tuple[str, list, Optional[str]]] = []
+    out.append(("wallet:ownerIndex==0 (not an owner)", path + [owner_index == BVV(0, 256)], None))
+    path.append(Not(owner_index == BVV(0, 256)))
+    out.append(("wallet:owner", list(path), "sat"))
+    fresh = path + [yet_needed == BVV(0, 256)]
+    needed = st[S_REQUIRED]                                  # pending.yetNeeded = m_required
+    out.append(("wallet:new operation", list(fresh), "sat"))
+    confirm = fresh + [(owners_done & bit) == BVV(0, 256)]
+    out.append(("wallet:not yet confirmed", list(confirm), "sat"))
+    out.append(("wallet:more confirmations needed", confirm + [UGT(needed, BVV(1, 256))], "sat"))
+    killed = confirm + [Not(UGT(needed, BVV(1, 256)))]
+    out.append(("wallet:kill runs", list(killed), "sat"))
+    # SELFDESTRUCT(_to): the suicide module's query over both transactions
+    out.append(("wallet:attacker query", killed + _attacker_query([a, b], to), "sat"))
+    # the sender that initialised the wallet is an owner: ownerIndex == 0 is UNSAT for it
+    out.append(("wallet:initializer not owner", path[:-1] + [b.sender == a.sender, owner_index == BVV(0, 256)],
+                "unsat"))
+    return [(l, tuple(c.raw for c in cs), e) for l, cs, e in out]
+
+
+def corpus(n: int) -> List[Tuple[str, tuple, Optional[str]]]:
+    """n entries cycling over the suicide, BECToken and WalletLibrary shapes."""
+    kfm = KeccakFunctionManager()
+    out: List[Tuple[str, tuple, Optional[str]]] = []
+    k = 0
+    while len(out) < n:
+        r = k % 4
+        if r == 0:
+            out.extend(suicide_states(1 + (k // 4) % 5))
+        elif r == 1:
+            out.extend(wallet_states(k // 4, kfm))
+        else:
+            out.extend(bectoken_states(6 * k + j, kfm) for j in range(6))
+        k += 1
+    return out[:n]

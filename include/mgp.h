@@ -198,13 +198,14 @@ int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets,
  * first hint of every variable, that row with the x == y aliases applied, then
  * a seeded mixture per variable (35 % hint, 25 % pool = constants, +-1, the
  * fixed pool; 15 % alias of an equal-width variable; 25 % uniform), masked to
- * the slot width.  Variables of state s are var_off[s]..var_off[s+1]; hints of
+ * the slot width.  var_kind (may be NULL): slots of kind 2 (pinned constants,
+ * MGP_FE_VAR_KIND) hold their first hint in every row.  Variables of state s are var_off[s]..var_off[s+1]; hints of
  * variable v are rows hint_off[v]..hint_off[v+1] of `hints` (8 limbs each);
  * aliases are (dst, src) pairs of state-local indices; consts as for
  * mgp_lower.  out: [n_states][n_cand][n_vars][8], the host layout of
  * mgp_eval_batch.  Deterministic in seed, independent of the thread count. */
 int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                        const uint64_t *var_off, const uint32_t *var_width,
+                        const uint64_t *var_off, const uint32_t *var_width, const uint8_t *var_kind,
                         const uint64_t *hint_off, const uint32_t *hints,
                         const uint64_t *alias_off, const uint32_t *aliases,
                         const uint64_t *const_off, const uint32_t *consts,
@@ -224,13 +225,18 @@ int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uin
  * mgp_fe_free; *count = number of ELEMENTS of the field's type listed below, e.g. 8
  * uint32_t per constant).  Per variable slot: width (<= 256), full width (first slot of a
  * value, else 0), name id, aux (slot index within a wide value; for a fresh
- * uninterpreted-function value the node index of its application), kind (0 named
- * variable, 1 fresh UF value).  hint_off is per variable slot (8 limbs per hint);
- * aliases are (dst, src) slot pairs local to the state.  GPU_NODES equals NODES
- * except for padded key equalities (mgp_front.cpp), replaced by the constant that
- * strengthens the formula; FLAGS per state: */
+ * uninterpreted-function value the node index of its application; for a pinned
+ * constant its pool index), kind (0 named variable, 1 fresh UF value, 2 pinned
+ * constant: every candidate row holds hint 0 of the slot).  hint_off is per variable slot (8 limbs per hint);
+ * aliases are (dst, src) slot pairs local to the state.  GPU_NODES (offsets
+ * GPU_NODE_OFF) is the program the GPU evaluates: NODES except that padded key
+ * equalities are replaced by the constant that strengthens the formula, and that
+ * operand uses of pinned constants read VAR nodes placed in front of the state's
+ * program (mgp_front.cpp); FLAGS per state: */
 #define MGP_FE_SAT_UNSAFE 0x1u   /* a padded key equality under both polarities: no GPU SAT answer */
-#define MGP_FE_STRENGTHENED 0x2u /* GPU_NODES differs from NODES for this state */
+#define MGP_FE_STRENGTHENED 0x2u /* padded key equalities replaced in GPU_NODES */
+#define MGP_FE_PINNED 0x4u       /* constants past the pool budget are pinned variable slots in GPU_NODES */
+#define MGP_FE_POOL_KEEP 48u     /* constant-pool entries a GPU program keeps (the rest are pinned) */
 typedef struct mgp_fe_batch mgp_fe_batch;
 enum mgp_fe_field {
   MGP_FE_NODES = 0,     /* mgp_node                     */
@@ -249,7 +255,8 @@ enum mgp_fe_field {
   MGP_FE_ALIAS_OFF,     /* uint64_t, n_states + 1       */
   MGP_FE_ALIASES,       /* uint32_t, 2 per pair         */
   MGP_FE_FLAGS,         /* uint8_t per state            */
-  MGP_FE_VAR_KEY        /* uint64_t per slot: name id, kind, UF node, piece (parent matching) */
+  MGP_FE_VAR_KEY,       /* uint64_t per slot: name id, kind, UF node, piece (parent matching) */
+  MGP_FE_GPU_NODE_OFF   /* uint64_t, n_states + 1: offsets into GPU_NODES */
 };
 int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t *t_args, const uint32_t *t_p,
                      uint64_t n_terms, const uint32_t *limbs, uint64_t n_limbs, const int32_t *roots,

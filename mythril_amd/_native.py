@@ -89,8 +89,8 @@ def _bind(lib):
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
         "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
-        "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32, _P,
-                                               _P]),
+        "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32,
+                                               _P, _P]),
         "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, ctypes.POINTER(_P)]),
         "mgp_fe_get": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
         "mgp_fe_free": (None, [_P]),
@@ -220,7 +220,7 @@ def lower(
 
 
 def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hint_off, hints, alias_off, aliases,
-                    const_off, consts, fixed_pool, has_parent) -> np.ndarray:
+                    const_off, consts, fixed_pool, has_parent, var_kind=None) -> np.ndarray:
     """mgp_make_candidates over flattened per-state tables -> uint32 [n_states, n_cand, n_vars, 8]."""
     def u(a, dt):
         a = np.ascontiguousarray(a, dtype=dt)
@@ -229,7 +229,9 @@ def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hin
     out = np.empty((n_states, n_cand, n_vars, 8), dtype=np.uint32)
     fixed = u(fixed_pool, np.uint32)
     _check(lib().mgp_make_candidates(n_states, n_cand, n_vars, seed & (2 ** 64 - 1), _ptr(u(var_off, np.uint64)),
-                                     _ptr(u(var_width, np.uint32)), _ptr(u(hint_off, np.uint64)),
+                                     _ptr(u(var_width, np.uint32)),
+                                     None if var_kind is None else _ptr(u(var_kind, np.uint8)),
+                                     _ptr(u(hint_off, np.uint64)),
                                      _ptr(u(hints, np.uint32)), _ptr(u(alias_off, np.uint64)),
                                      _ptr(u(aliases, np.uint32)), _ptr(u(const_off, np.uint64)),
                                      _ptr(u(consts, np.uint32)), _ptr(fixed), len(fixed_pool),

@@ -7,6 +7,7 @@
 // mixture per variable: 35 % harvested hint, 25 % pool (state constants and their
 // neighbours +-1, LASER's actor addresses and boundary values), 15 % alias of an
 // equal-width variable, 25 % uniform.  Every value is masked to its slot width.
+// A pinned-constant slot (var_kind 2, mgp_front.cpp) holds its hint 0 in every row.
 // States are independent (OpenMP); the stream is splitmix64 keyed by (seed, state,
 // row, variable), so the result does not depend on the thread count.
 #include <stdint.h>
@@ -44,7 +45,7 @@ void mask_to(uint32_t *v, uint32_t w) {
 }  // namespace
 
 extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                                   const uint64_t *var_off, const uint32_t *var_width,
+                                   const uint64_t *var_off, const uint32_t *var_width, const uint8_t *var_kind,
                                    const uint64_t *hint_off, const uint32_t *hints,
                                    const uint64_t *alias_off, const uint32_t *aliases,
                                    const uint64_t *const_off, const uint32_t *consts,
@@ -118,7 +119,10 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
       }
     }
     for (uint32_t c = 0; c < n_cand; ++c)
-      for (uint64_t v = 0; v < V; ++v) mask_to(cell(c, v), var_width[v0 + v]);
+      for (uint64_t v = 0; v < V; ++v) {
+        if (var_kind && var_kind[v0 + v] == 2 && n_hint(v)) memcpy(cell(c, v), hint(v, 0), 32);  // pinned constant
+        mask_to(cell(c, v), var_width[v0 + v]);
+      }
   }
   return 0;
 }

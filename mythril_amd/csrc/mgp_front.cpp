@@ -51,6 +51,7 @@ namespace {
 struct StateOut {
   std::vector<mgp_node> nodes;
   std::vector<uint32_t> gpu_ops;           // (node index, op) pairs: padded equalities replaced
+  std::vector<mgp_node> gpu_nodes;         // the GPU program when it differs from `nodes` (else empty)
   std::vector<uint32_t> consts;            // 8 limbs per pool entry
   std::vector<uint32_t> var_width, var_full, var_name, var_aux;  // per slot
   std::vector<uint8_t> var_kind;
@@ -170,9 +171,14 @@ struct Scratch {
 // slot key: which variable (name, kind, UF node) and which 256-bit piece -- a parent
 // witness is matched to a child's slots by it (mgp_check_batch)
 inline uint64_t slot_key(uint32_t name, uint8_t kind, uint32_t aux, uint32_t j) {
+  if (kind == 2) return ~0ull;  // pinned constant: never matched to a parent
   return kind ? (1ull << 63) | ((uint64_t)(name & 0x7FFFFFFFu) << 32) | ((uint64_t)(aux & 0xFFFFFFu) << 8) | (j & 0xFFu)
               : ((uint64_t)(name & 0x7FFFFFFFu) << 32) | (j & 0xFFFFFFFFu);
 }
+
+template <typename IsPadded>
+void strengthen_padded(StateOut &S, IsPadded is_padded_eq);
+void pin_constants(StateOut &S);
 
 void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut &S, Scratch &X) {
   FlatMap &memo = X.memo, &var_idx = X.var_idx, &const_idx = X.const_idx;
@@ -366,7 +372,6 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
   }
 
   // ---- padded key equalities: polarity from the root, strengthened for the GPU
-  const int32_t N = (int32_t)S.nodes.size();
   auto is_padded_eq = [&](const mgp_node &n) {
     if (n.op != MGP_OP_EQ || n.a < 0 || n.b < 0) return false;
     auto zc = [&](int32_t x) {
@@ -378,7 +383,23 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
   };
   bool any = false;
   for (const mgp_node &n : S.nodes) any |= is_padded_eq(n);
-  if (!any) return;
+  if (any) strengthen_padded(S, is_padded_eq);
+  pin_constants(S);
+  if (!S.gpu_ops.empty() && S.gpu_nodes.empty()) S.gpu_nodes = S.nodes;
+  const uint32_t shift = S.gpu_nodes.size() - S.nodes.size();  // front VAR nodes of pinned constants
+  for (size_t k = 0; k < S.gpu_ops.size(); k += 2) {
+    mgp_node &nd = S.gpu_nodes[shift + S.gpu_ops[k]];
+    nd.op = (uint8_t)S.gpu_ops[k + 1];
+    nd.width = 1;
+    nd.a = nd.b = nd.c = -1;
+    nd.p0 = nd.p1 = 0;
+  }
+}
+
+// Polarity of every padded key equality from the root (bit 0 positive, bit 1 negative).
+template <typename IsPadded>
+void strengthen_padded(StateOut &S, IsPadded is_padded_eq) {
+  const int32_t N = (int32_t)S.nodes.size();
   std::vector<uint8_t> pol(N, 0);
   pol[N - 1] = 1;
   for (int32_t i = N - 1; i >= 0; --i) {
@@ -422,12 +443,91 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
   }
 }
 
+// Constant-pool budget of the GPU program.  The gfx950 interpreter holds a state's
+// constants in VGPR lanes (<= 64 entries, width masks and sign constants included,
+// mgp_uop.cpp); LASER's calldata words alone bring 32 byte indices each
+// (calldata.py:219-232), so two or three words overflow it.  A CONST node whose pool
+// entry lies at or past MGP_FE_POOL_KEEP is PINNED in the GPU program: its operand uses
+// read a new VAR node (placed in front of the program, so every index shifts by the
+// number of such nodes) of a pinned variable slot (kind 2), which every candidate row
+// fills with the constant (hint 0 of the slot, written last by the generators).  Uses
+// as an uninterpreted-function argument keep the CONST node: the lowering compares
+// known arguments at lowering time and needs no pool entry for them (a calldata byte
+// index is both a select argument and a bound in If(i < calldatasize, ...)).  The
+// UNSAT pre-check and the hints keep the original nodes.
+void pin_constants(StateOut &S) {
+  const uint32_t n_pool = (uint32_t)(S.consts.size() / 8);
+  if (n_pool <= MGP_FE_POOL_KEEP) return;
+  const uint32_t N = (uint32_t)S.nodes.size();
+  std::vector<uint8_t> pinned(N, 0), other_use(N, 0);
+  bool any = false;
+  for (uint32_t i = 0; i < N; ++i) {
+    const mgp_node &n = S.nodes[i];
+    if (n.op == MGP_OP_CONST && n.p0 + (n.width + 255u) / 256u > MGP_FE_POOL_KEEP) pinned[i] = 1, any = true;
+  }
+  if (!any) return;
+  for (uint32_t i = 0; i < N; ++i) {
+    const mgp_node &n = S.nodes[i];
+    const int32_t ops[3] = {n.a, n.b, n.c};
+    for (int k = 0; k < 3; ++k) {
+      const int32_t x = ops[k];
+      if (x < 0 || !pinned[x]) continue;
+      if (k == 0 && (n.op == MGP_OP_UFAPP || n.op == MGP_OP_UFINV)) continue;  // UF argument
+      other_use[x] = 1;
+    }
+  }
+  std::vector<int64_t> slot_of(n_pool, -1);
+  std::vector<int32_t> front(N, -1);
+  std::vector<mgp_node> pre;
+  for (uint32_t i = 0; i < N; ++i) {
+    if (!other_use[i]) continue;
+    const mgp_node &n = S.nodes[i];
+    const uint32_t k = (n.width + 255u) / 256u;
+    if (slot_of[n.p0] < 0) {
+      slot_of[n.p0] = (int64_t)S.var_width.size();
+      for (uint32_t j = 0; j < k; ++j) {
+        S.var_width.push_back(std::min<uint32_t>(256, n.width - 256 * j));
+        S.var_full.push_back(j == 0 ? n.width : 0u);
+        S.var_name.push_back(0u);
+        S.var_aux.push_back(n.p0);
+        S.var_kind.push_back(2u);
+        S.var_key.push_back(slot_key(0, 2, n.p0, j));
+        S.hints.emplace_back(S.consts.begin() + 8ull * (n.p0 + j), S.consts.begin() + 8ull * (n.p0 + j) + 8);
+      }
+    }
+    mgp_node v;
+    memset(&v, 0, sizeof v);
+    v.op = MGP_OP_VAR;
+    v.width = n.width;
+    v.a = v.b = v.c = -1;
+    v.p0 = (uint32_t)slot_of[n.p0];
+    front[i] = (int32_t)pre.size();
+    pre.push_back(v);
+  }
+  if (pre.empty()) return;
+  const int32_t P = (int32_t)pre.size();
+  S.gpu_nodes = pre;
+  S.gpu_nodes.reserve(P + N);
+  for (uint32_t i = 0; i < N; ++i) {
+    mgp_node n = S.nodes[i];
+    int32_t *ops[3] = {&n.a, &n.b, &n.c};
+    for (int k = 0; k < 3; ++k) {
+      const int32_t x = *ops[k];
+      if (x < 0) continue;
+      const bool uf_arg = k == 0 && (n.op == MGP_OP_UFAPP || n.op == MGP_OP_UFINV);
+      *ops[k] = (front[x] >= 0 && !uf_arg) ? front[x] : x + P;
+    }
+    S.gpu_nodes.push_back(n);
+  }
+  S.flags |= MGP_FE_PINNED;
+}
+
 }  // namespace
 
 struct mgp_fe_batch {
   uint32_t n_states = 0;
   std::vector<mgp_node> nodes, gpu_nodes;
-  std::vector<uint64_t> node_off, const_off, var_off, hint_off, alias_off;
+  std::vector<uint64_t> node_off, gpu_node_off, const_off, var_off, hint_off, alias_off;
   std::vector<uint32_t> consts, var_width, var_full, var_name, var_aux, hints, aliases;
   std::vector<uint8_t> var_kind, flags;
   std::vector<uint64_t> var_key;
@@ -495,7 +595,7 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
   for (uint32_t s = 0; s < n_states; ++s) {
     const uint64_t v0 = B->var_off[s];
     for (size_t v = 0; v < res[s].hints.size(); ++v) B->hint_off[v0 + v + 1] = res[s].hints[v].size() / 8;
-    strengthened |= !res[s].gpu_ops.empty();
+    strengthened |= !res[s].gpu_nodes.empty();
   }
   for (uint64_t v = 0; v < nv; ++v) B->hint_off[v + 1] += B->hint_off[v];
   B->hints.resize(B->hint_off[nv] * 8);
@@ -515,16 +615,17 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
     for (size_t v = 0; v < S.hints.size(); ++v)
       std::copy(S.hints[v].begin(), S.hints[v].end(), B->hints.begin() + B->hint_off[v0 + v] * 8);
   }
-  if (strengthened) {
-    B->gpu_nodes = B->nodes;
+  if (strengthened) {  // some state's GPU program differs: a separate node list and offsets
+    B->gpu_node_off.assign(n_states + 1, 0);
     for (uint32_t s = 0; s < n_states; ++s)
-      for (size_t k = 0; k < res[s].gpu_ops.size(); k += 2) {
-        mgp_node &nd = B->gpu_nodes[B->node_off[s] + res[s].gpu_ops[k]];
-        nd.op = (uint8_t)res[s].gpu_ops[k + 1];
-        nd.width = 1;
-        nd.a = nd.b = nd.c = -1;
-        nd.p0 = nd.p1 = 0;
-      }
+      B->gpu_node_off[s + 1] = B->gpu_node_off[s] +
+                               (res[s].gpu_nodes.empty() ? res[s].nodes.size() : res[s].gpu_nodes.size());
+    B->gpu_nodes.resize(B->gpu_node_off[n_states]);
+#pragma omp parallel for schedule(static)
+    for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+      const auto &g = res[s].gpu_nodes.empty() ? res[s].nodes : res[s].gpu_nodes;
+      std::copy(g.begin(), g.end(), B->gpu_nodes.begin() + B->gpu_node_off[s]);
+    }
   }
   if (getenv("MGP_FE_TIMING")) fprintf(stderr, "[fe] total %.3f ms\n", 1e3 * omp_get_wtime() - 1e3 * t_start);
   *out = B;
@@ -556,6 +657,7 @@ int mgp_fe_get(const mgp_fe_batch *B, int field, const void **ptr, uint64_t *cou
     case MGP_FE_ALIASES: return set(B->aliases);
     case MGP_FE_FLAGS: return set(B->flags);
     case MGP_FE_VAR_KEY: return set(B->var_key);
+    case MGP_FE_GPU_NODE_OFF: return set(B->gpu_nodes.empty() ? B->node_off : B->gpu_node_off);
     default: return MGP_E_ARG;
   }
 }

@@ -662,7 +662,8 @@ struct FeRow {
 
 __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
     uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed, const uint64_t *__restrict__ var_off,
-    const uint32_t *__restrict__ var_width, const uint64_t *__restrict__ hint_off, const uint32_t *__restrict__ hints,
+    const uint32_t *__restrict__ var_width, const uint8_t *__restrict__ var_kind,
+    const uint64_t *__restrict__ hint_off, const uint32_t *__restrict__ hints,
     const uint64_t *__restrict__ alias_off, const uint32_t *__restrict__ aliases,
     const uint64_t *__restrict__ const_off, const uint32_t *__restrict__ consts, const uint32_t *__restrict__ fixed,
     uint32_t n_fixed, const int32_t *__restrict__ parent_idx, const uint32_t *__restrict__ pvals,
@@ -771,7 +772,8 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       R.copy((uint32_t)v, (uint32_t)src);
     }
   }
-  for (uint64_t v = 0; v < V; ++v) {  // mask to the slot width
+  for (uint64_t v = 0; v < V; ++v) {  // pinned constants, then the mask to the slot width
+    if (var_kind && var_kind[v0 + v] == 2 && n_hint(v)) R.put((uint32_t)v, hint(v, 0));
     const uint32_t w = var_width[v0 + v];
     if (w >= 256) continue;
     for (uint32_t h = 0; h < 2; ++h) {
@@ -1042,7 +1044,8 @@ hipError_t mgp_launch_preimages(uint8_t *out, uint64_t first, uint64_t n, uint64
 }
 
 hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                               const uint64_t *var_off, const uint32_t *var_width, const uint64_t *hint_off,
+                               const uint64_t *var_off, const uint32_t *var_width, const uint8_t *var_kind,
+                               const uint64_t *hint_off,
                                const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
@@ -1052,7 +1055,7 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
   const uint64_t blocks = (total + 255) / 256;
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mgp_fe_cands_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, n_states, n_cand, n_vars, seed,
-                     var_off, var_width, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed,
+                     var_off, var_width, var_kind, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed,
                      parent_idx, pvals, pmask, reinterpret_cast<uint4 *>(out));
   return hipGetLastError();
 }

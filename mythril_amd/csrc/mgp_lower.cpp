@@ -18,6 +18,7 @@
 //      (mgp_uop.cpp; layout in mythril_amd/uop_spec.py).
 // States are independent; the batch is lowered in parallel with OpenMP.
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -119,15 +120,20 @@ struct Piece {
 typedef std::vector<Piece> Pieces;
 
 struct UFApp {
-  Pieces arg, val;
+  Pieces arg, val, fresh;  // argument, value, the application's own fresh variable(s)
 };
 
-Lowered unsupported() {
+// MGP_LOWER_WHY=1: name the source line of every "unsupported" verdict (diagnostics)
+Lowered unsupported_at(int line) {
+  static const bool why = getenv("MGP_LOWER_WHY") != nullptr;
+  if (why) fprintf(stderr, "[mgp_lower] unsupported at mgp_lower.cpp:%d\n", line);
   Lowered L;
   L.status = MGP_ST_UNSUPPORTED;
   L.words = {0u, 0u, 0u, (uint32_t)MGP_ST_UNSUPPORTED, 0u, 0u, 0u, 0u};
   return L;
 }
+
+#define unsupported() unsupported_at(__LINE__)
 
 Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *consts, uint64_t n_consts,
                   uint32_t max_slots, int sched) {
@@ -537,16 +543,21 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         // f(arg): first earlier f-app with equal argument, else fresh var(s) p1..
         const uint32_t k = (w + MGP_MAX_WIDTH - 1) / MGP_MAX_WIDTH;
         if (!opnd(nd.a) || isb[nd.a] || nd.p1 + k > 0x3FFFu) return unsupported();
+        // The chain selects the OLDEST earlier application with an equal argument; that
+        // one has no older equal application, so its value is its own fresh variable:
+        // chaining on fresh variables (free reads) instead of earlier chain results keeps
+        // no earlier value live (calldata words are 32 selects of one array each).
         const Pieces arg = pieces_of(nd.a);
-        Pieces v = var_pieces(nd.p1, w);
+        const Pieces fresh = var_pieces(nd.p1, w);
+        Pieces v = fresh;
         std::vector<UFApp> &fl = fapps[nd.p0];
         for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
           if (wid_of(it->arg) != wid[nd.a] || wid_of(it->val) != w) return unsupported();
           const int ke = known_eq(arg, it->arg);
           if (ke == 0) continue;
-          v = (ke == 1) ? it->val : ite_pieces(eq_pieces(arg, it->arg), it->val, v);
+          v = (ke == 1) ? it->fresh : ite_pieces(eq_pieces(arg, it->arg), it->fresh, v);
         }
-        fl.push_back(UFApp{arg, v});
+        fl.push_back(UFApp{arg, v, fresh});
         set_val(i, v);
         break;
       }
@@ -571,7 +582,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           if (ke == 0) continue;
           v = (ke == 1) ? it->val : ite_pieces(eq_pieces(arg, it->arg), it->val, v);
         }
-        il.push_back(UFApp{arg, v});
+        il.push_back(UFApp{arg, v, var_pieces(nd.p1, w)});
         set_val(i, v);
         break;
       }
@@ -606,6 +617,23 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     }
     S.ins.swap(kept);
     if (root.k == R_INS) root.idx = remap[root.idx];
+  }
+  // pool compaction: constants only read at lowering time (uninterpreted-function
+  // arguments compared here, dead code) take no pool entry in the program
+  {
+    std::vector<int64_t> cmap(S.pool.size(), -1);
+    std::vector<ConstKey> used;
+    for (VIns &I : S.ins)
+      for (Ref *r : {&I.a, &I.b, &I.c})
+        if (r->k == R_CONST) {
+          if (cmap[r->idx] < 0) {
+            cmap[r->idx] = (int64_t)used.size();
+            used.push_back(S.pool[r->idx]);
+          }
+          r->idx = (uint32_t)cmap[r->idx];
+        }
+    S.pool.swap(used);
+    S.pool_map.clear();
   }
 
   // ------------------------------------------- register-pressure scheduling

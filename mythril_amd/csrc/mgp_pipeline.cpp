@@ -36,7 +36,8 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
                            const uint32_t *bucket_bounds, const uint32_t *bucket_slots, uint32_t n_buckets,
                            hipStream_t st);
 hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                               const uint64_t *var_off, const uint32_t *var_width, const uint64_t *hint_off,
+                               const uint64_t *var_off, const uint32_t *var_width, const uint8_t *var_kind,
+                               const uint64_t *hint_off,
                                const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
@@ -111,9 +112,10 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
     t = now;
   };
   const Arr nodes = get(B, MGP_FE_NODES), gnodes = get(B, MGP_FE_GPU_NODES), noff = get(B, MGP_FE_NODE_OFF),
+            gnoff = get(B, MGP_FE_GPU_NODE_OFF),
             consts = get(B, MGP_FE_CONSTS), coff = get(B, MGP_FE_CONST_OFF), voff = get(B, MGP_FE_VAR_OFF),
             vwidth = get(B, MGP_FE_VAR_WIDTH), hoff = get(B, MGP_FE_HINT_OFF), hints = get(B, MGP_FE_HINTS),
-            aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES);
+            aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES), vkind = get(B, MGP_FE_VAR_KIND);
   const uint32_t n_states = (uint32_t)(noff.n ? noff.n - 1 : 0);
   if (n_states == 0) return MGP_OK;
   const uint64_t *vo = (const uint64_t *)voff.p;
@@ -127,7 +129,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   std::vector<uint32_t> words;
   std::vector<uint64_t> offs;
   std::vector<uint8_t> status;
-  int rc = mgp_lower_vec((const mgp_node *)gnodes.p, (const uint64_t *)noff.p, n_states, cp,
+  int rc = mgp_lower_vec((const mgp_node *)gnodes.p, (const uint64_t *)gnoff.p, n_states, cp,
                          (const uint64_t *)coff.p, 0, words, offs, status);
   if (rc != MGP_OK) return mgp_ctx_fail(ctx, rc, "lowering failed");
   std::vector<uint32_t> order(n_states), bounds(257), bslots(256);
@@ -179,18 +181,18 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   const size_t cand_bytes = (size_t)n_states * n_cand * n_vars * 32u;
   const uint32_t n_chunks = (n_cand + 63u) / 64u;
   // one table buffer: var_off | var_width | hint_off | hints | alias_off | aliases | const_off | consts |
-  // fixed | parent_idx | pvals | pmask, each 256-B aligned
+  // fixed | parent_idx | pvals | pmask | var_kind, each 256-B aligned
   // (mgp_fe_get counts elements of each array: u32 limbs for consts / hints / aliases)
-  const size_t sizes[12] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+  const size_t sizes[13] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
                             coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32,
-                            (size_t)n_states * 4, pvals.size() * 4, pmask.size()};
-  const void *srcs[12] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
-                          pidx.data(), pvals.data(), pmask.data()};
-  size_t at[13];
+                            (size_t)n_states * 4, pvals.size() * 4, pmask.size(), vkind.n};
+  const void *srcs[13] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
+                          pidx.data(), pvals.data(), pmask.data(), vkind.p};
+  size_t at[14];
   at[0] = 0;
-  for (int i = 0; i < 12; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
-  std::vector<uint8_t> stage(at[12]);
-  for (int i = 0; i < 12; ++i)
+  for (int i = 0; i < 13; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[13]);
+  for (int i = 0; i < 13; ++i)
     if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
   if (e == hipSuccess) e = D.ensure(B_WORDS, words.size() * 4u);
   if (e == hipSuccess) e = D.ensure(B_OFFS, offs.size() * 8u);
@@ -199,16 +201,17 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   if (e == hipSuccess) e = D.ensure(B_FIRST, (size_t)n_states * 4u);
   if (e == hipSuccess) e = D.ensure(B_WIT, (size_t)n_states * n_vars * 32u);
   if (e == hipSuccess) e = D.ensure(B_PART, (size_t)n_states * n_chunks * 4u);
-  if (e == hipSuccess) e = D.ensure(B_TABLES, at[12]);
+  if (e == hipSuccess) e = D.ensure(B_TABLES, at[13]);
   if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_WORDS], words.data(), words.size() * 4u, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_OFFS], offs.data(), offs.size() * 8u, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(D.p[B_ORDER], order.data(), (size_t)n_states * 4u, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], stage.data(), at[12], hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], stage.data(), at[13], hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
   const uint8_t *tb = (const uint8_t *)D.p[B_TABLES];
   e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
-                          (const uint32_t *)(tb + at[1]), (const uint64_t *)(tb + at[2]),
+                          (const uint32_t *)(tb + at[1]), vkind.n ? (const uint8_t *)(tb + at[12]) : nullptr,
+                          (const uint64_t *)(tb + at[2]),
                           (const uint32_t *)(tb + at[3]), (const uint64_t *)(tb + at[4]),
                           (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
                           (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed,
@@ -262,7 +265,8 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
   if (!ctx || !B || !out || n_cand == 0 || n_vars == 0) return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument");
   const Arr noff = get(B, MGP_FE_NODE_OFF), consts = get(B, MGP_FE_CONSTS), coff = get(B, MGP_FE_CONST_OFF),
             voff = get(B, MGP_FE_VAR_OFF), vwidth = get(B, MGP_FE_VAR_WIDTH), hoff = get(B, MGP_FE_HINT_OFF),
-            hints = get(B, MGP_FE_HINTS), aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES);
+            hints = get(B, MGP_FE_HINTS), aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES),
+            vkind = get(B, MGP_FE_VAR_KIND);
   const uint32_t n_states = (uint32_t)(noff.n ? noff.n - 1 : 0);
   if (n_states == 0) return MGP_OK;
   void *stp = nullptr;
@@ -270,26 +274,27 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
   mgp_ctx_stream(ctx, &stp, &dev);
   hipStream_t st = (hipStream_t)stp;
   static const uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const size_t sizes[9] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
-                           coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32};
-  const void *srcs[9] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
-                         consts.n ? consts.p : zero8, fixed_pool};
-  size_t at[10];
+  const size_t sizes[10] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+                            coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32, vkind.n};
+  const void *srcs[10] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
+                          consts.n ? consts.p : zero8, fixed_pool, vkind.p};
+  size_t at[11];
   at[0] = 0;
-  for (int i = 0; i < 9; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
-  std::vector<uint8_t> stage(at[9]);
-  for (int i = 0; i < 9; ++i)
+  for (int i = 0; i < 10; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[10]);
+  for (int i = 0; i < 10; ++i)
     if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
   const size_t cb = (size_t)n_states * n_cand * n_vars * 32u;
   void *dt = nullptr, *dc = nullptr;
   hipError_t e = hipSetDevice(dev);
-  if (e == hipSuccess) e = hipMalloc(&dt, at[9]);
+  if (e == hipSuccess) e = hipMalloc(&dt, at[10]);
   if (e == hipSuccess) e = hipMalloc(&dc, cb);
-  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[9], hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[10], hipMemcpyHostToDevice, st);
   const uint8_t *tb = (const uint8_t *)dt;
   if (e == hipSuccess)
     e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
-                            (const uint32_t *)(tb + at[1]), (const uint64_t *)(tb + at[2]),
+                            (const uint32_t *)(tb + at[1]), vkind.n ? (const uint8_t *)(tb + at[9]) : nullptr,
+                            (const uint64_t *)(tb + at[2]),
                             (const uint32_t *)(tb + at[3]), (const uint64_t *)(tb + at[4]),
                             (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
                             (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed, nullptr,

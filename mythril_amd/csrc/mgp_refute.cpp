@@ -1159,6 +1159,25 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
       width.push_back(x.width);
       node.push_back((int32_t)i);
     }
+    // Values each variable is compared equal to (x == c anywhere in the DAG, e.g. the
+    // sender against every ACTORS address, transaction/symbolic.py:165-167): an interval
+    // cannot hold such a value set, so decisions try them first and plain domain rows
+    // draw one half of the time when it lies inside the refined domain.
+    std::vector<std::vector<V>> eqh(slot.size());
+    for (size_t k = 0; k < slot.size(); ++k)
+      for (uint32_t i = 0; i < s.n; ++i) {
+        const mgp_node &x = s.nd[i];
+        if (x.op != MGP_OP_EQ || x.a < 0 || x.b < 0) continue;
+        const int32_t other = x.a == node[k] ? x.b : (x.b == node[k] ? x.a : -1);
+        if (other < 0 || s.nd[other].op != MGP_OP_CONST || s.nd[other].width > MGP_MAX_WIDTH) continue;
+        if (s.nd[other].p0 >= s.n_consts || eqh[k].size() >= 16) continue;
+        V c;
+        memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
+        eqh[k].push_back(bv_mask(c, width[k]));
+      }
+    auto inside = [&](const AV &a, const V &v) {
+      return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
+    };
     // The first n_decide guided rows are built by decisions: each variable in turn is
     // fixed to a draw from its current abstract value and the analysis re-run, so later
     // variables are drawn from values narrowed by the earlier choices (x + y == c, a
@@ -1173,9 +1192,16 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
         for (size_t kk = 0; kk < slot.size(); ++kk) {
           const size_t k = (row & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
           const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
+          if (EQV(d.av[node[k]].lo, d.av[node[k]].hi)) {  // already one value: nothing to decide
+            memcpy(dst + slot[k] * 8ull, d.av[node[k]].lo.w, 32);
+            continue;
+          }
           V v = bv_zero();
-          for (uint32_t t = 0; t < kTries; ++t) {
-            v = sample_av(d.av[node[k]], width[k], t ? 3u + row + t : (row < 4 ? row / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + row : 0u)), mix64(key + t));
+          const uint32_t nh = (uint32_t)eqh[k].size();
+          for (uint32_t t = 0; t < kTries + nh; ++t) {
+            v = t < nh ? eqh[k][(t + row) % nh]
+                       : sample_av(d.av[node[k]], width[k], t > nh ? 3u + row + t : (row < 4 ? row / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + row : 0u)), mix64(key + t));
+            if (t < nh && !inside(d.av[node[k]], v)) continue;
             State e = d;
             if (e.meet(node[k], exact(v, width[k])) && e.tie() && e.run(passes) == 0) {
               d = std::move(e);
@@ -1188,7 +1214,11 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
       }
       for (size_t k = 0; k < slot.size(); ++k) {
         const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
-        const V v = sample_av(s.av[node[k]], width[k], row, key);
+        V v = sample_av(s.av[node[k]], width[k], row, key);
+        if (!eqh[k].empty() && (mix64(key ^ 0x9E37ull) & 1u)) {
+          const V h = eqh[k][mix64(key ^ 0x7F4Aull) % eqh[k].size()];
+          if (inside(s.av[node[k]], h)) v = h;
+        }
         memcpy(dst + slot[k] * 8ull, v.w, 32);
       }
     }

@@ -18,6 +18,8 @@
 //   * LDS slot / pool / Bool operands are pre-scaled byte offsets.
 // Encoding: mythril_amd/uop_spec.py (mgp_uop.h is generated from it).
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <map>
@@ -459,6 +461,10 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     uops.clear();
     translate();
   }
+  static const bool why = getenv("MGP_LOWER_WHY") != nullptr;
+  if (why && (!v1_ok || T.bad || uops.empty() || T.pool.size() / 8 > MGP_U_MAX_POOL))
+    fprintf(stderr, "[mgp_uop] not runnable: v1_ok %d bad %d uops %zu pool %zu\n", (int)v1_ok, (int)T.bad,
+            uops.size(), T.pool.size() / 8);
   if (!v1_ok || T.bad || uops.empty()) {
     out[base + 0] = 0;
     out[base + 1] = 1;  // not runnable: the kernel reports MGP_UNDECIDED

@@ -43,8 +43,12 @@ class StateDag:
     wide: Dict[int, int] = field(default_factory=dict)
     # padded key equalities (csrc/mgp_front.cpp): node index -> TRUE/FALSE op in the GPU
     # program; flags bit 0 = such an equality under both polarities (no GPU SAT answer)
-    gpu_ops: Dict[int, int] = field(default_factory=dict)
+    gpu_ops: Dict[int, int] = field(default_factory=dict)  # node -> TRUE / FALSE
     flags: int = 0
+    # pinned constants (csrc/mgp_front.cpp pin_constants): var slots of the GPU program
+    # holding a pool constant in every candidate row
+    pinned: Dict[int, int] = field(default_factory=dict)  # slot -> value
+    gpu_nodes: Optional[List[Tuple[int, int, int, int, int, int, int]]] = None  # when it differs from nodes
 
     @property
     def n_vars(self) -> int:
@@ -119,7 +123,69 @@ def build_state(constraints: Sequence[Term]) -> StateDag:
             d.nodes.append((ir.BAND, 1, r, r, -1, 0, 0))
     _harvest_hints(d)
     _strengthen_padded(d)
+    _pin_constants(d)
+    if d.gpu_ops and d.gpu_nodes is None:
+        d.gpu_nodes = list(d.nodes)
+    if d.gpu_ops:
+        shift = len(d.gpu_nodes) - len(d.nodes)
+        for i, op in d.gpu_ops.items():
+            d.gpu_nodes[shift + i] = (op, 1, -1, -1, -1, 0, 0)
     return d
+
+
+POOL_KEEP = 48  # include/mgp.h MGP_FE_POOL_KEEP
+
+
+def _pin_constants(d: StateDag) -> None:
+    """Pool entries from POOL_KEEP on are pinned in the GPU program (csrc/mgp_front.cpp
+    pin_constants; the gfx950 interpreter holds <= 64 constants): operand uses other than
+    a UF argument read a VAR node placed in front of the program, of a pinned slot."""
+    if len(d.consts) <= POOL_KEEP:
+        return
+    nodes = d.nodes
+    pinned = [n[0] == ir.CONST and n[5] + (n[1] + 255) // 256 > POOL_KEEP for n in nodes]
+    if not any(pinned):
+        return
+    other = [False] * len(nodes)
+    for (op, w, a, b, c, p0, p1) in nodes:
+        for k, x in enumerate((a, b, c)):
+            if x < 0 or not pinned[x] or (k == 0 and op in (ir.UFAPP, ir.UFINV)):
+                continue
+            other[x] = True
+    slot_of: Dict[int, int] = {}
+    front: Dict[int, int] = {}
+    pre = []
+    for i, (op, w, a, b, c, p0, p1) in enumerate(nodes):
+        if not other[i]:
+            continue
+        k = (w + 255) // 256
+        if p0 not in slot_of:
+            slot_of[p0] = len(d.vars)
+            if k > 1:
+                d.wide[len(d.vars)] = w
+            for j in range(k):
+                d.pinned[len(d.vars)] = d.consts[p0 + j]
+                d.hints[len(d.vars)] = [d.consts[p0 + j]]
+                d.vars.append((f"#pool{p0}" if j == 0 else f"#pool{p0}#{j}", min(256, w - 256 * j)))
+                d.var_terms.append(None)
+        front[i] = len(pre)
+        pre.append((ir.VAR, w, -1, -1, -1, slot_of[p0], 0))
+    if not pre:
+        return
+    P = len(pre)
+    out = list(pre)
+    for (op, w, a, b, c, p0, p1) in nodes:
+        ops = []
+        for k, x in enumerate((a, b, c)):
+            if x < 0:
+                ops.append(x)
+            elif x in front and not (k == 0 and op in (ir.UFAPP, ir.UFINV)):
+                ops.append(front[x])
+            else:
+                ops.append(x + P)
+        out.append((op, w, ops[0], ops[1], ops[2], p0, p1))
+    d.gpu_nodes = out
+    d.flags |= 4
 
 
 def _is_padded_eq(nodes, n) -> bool:
@@ -209,7 +275,8 @@ def _harvest_hints(d: StateDag) -> None:
 def pack_states(states: Sequence[StateDag], gpu: bool = False):
     """-> (nodes NODE_DTYPE, node_offsets u64, consts u32[n,8], const_offsets u64);
     gpu=True: the GPU program (padded key equalities replaced, see _strengthen_padded)."""
-    n_nodes = sum(len(s.nodes) for s in states)
+    lists = [(s.gpu_nodes if gpu and s.gpu_nodes is not None else s.nodes) for s in states]
+    n_nodes = sum(len(x) for x in lists)
     nodes = np.zeros(n_nodes, dtype=NODE_DTYPE)
     noff = np.zeros(len(states) + 1, dtype=np.uint64)
     n_c = sum(len(s.consts) for s in states)
@@ -217,11 +284,8 @@ def pack_states(states: Sequence[StateDag], gpu: bool = False):
     coff = np.zeros(len(states) + 1, dtype=np.uint64)
     i = j = 0
     for k, s in enumerate(states):
-        for k_, (op, w, a, b, c, p0, p1) in enumerate(s.nodes):
-            if gpu and k_ in s.gpu_ops:
-                nodes[i] = (s.gpu_ops[k_], 0, 1, -1, -1, -1, 0, 0)
-            else:
-                nodes[i] = (op, 0, w, a, b, c, p0, p1)
+        for (op, w, a, b, c, p0, p1) in lists[k]:
+            nodes[i] = (op, 0, w, a, b, c, p0, p1)
             i += 1
         for v in s.consts:
             consts[j] = [(v >> (32 * l)) & 0xFFFFFFFF for l in range(8)] if v < (1 << 256) else 0
@@ -291,9 +355,10 @@ def make_candidates(states: Sequence[StateDag], n_cand: int, n_vars: int, seed: 
     hint_off = np.zeros(len(hint_counts) + 1, np.uint64)
     hint_off[1:] = np.cumsum(hint_counts)
     has_parent = np.array([bool(parents is not None and parents[s]) for s in range(n)], dtype=np.uint8)
+    kinds = np.array([2 if vi in st.pinned else 0 for st in states for vi in range(st.n_vars)], np.uint8)
     out = N.make_candidates(n_cand, n_vars, seed, var_off, np.array(widths, np.uint32), hint_off,
                             _limbs_of(hint_vals), alias_off, np.array(alias_pairs, np.uint32).reshape(-1, 2),
-                            const_off, _limbs_of(const_vals), _FIXED_LIMBS, has_parent)
+                            const_off, _limbs_of(const_vals), _FIXED_LIMBS, has_parent, var_kind=kinds)
     if parents is not None:
         for s, st in enumerate(states):
             if not parents[s] or n_cand == 0:
@@ -319,9 +384,10 @@ def witness_to_model(st: StateDag, words: np.ndarray) -> Dict[str, int]:
     for vi, w in st.wide.items():
         k = (w + 255) // 256
         skip.update(range(vi + 1, vi + k))
-        model[st.vars[vi][0]] = sum(vals[vi + j] << (256 * j) for j in range(k))
+        if vi not in st.pinned:
+            model[st.vars[vi][0]] = sum(vals[vi + j] << (256 * j) for j in range(k))
     for vi, (name, w) in enumerate(st.vars):
-        if vi not in skip and vi not in st.wide:
+        if vi not in skip and vi not in st.wide and vi not in st.pinned:
             model[name] = vals[vi]
     return model
 

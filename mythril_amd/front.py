@@ -30,7 +30,7 @@ _FIELDS = {
     "var_width": (6, np.uint32, 1), "var_full": (7, np.uint32, 1), "var_name": (8, np.uint32, 1),
     "var_aux": (9, np.uint32, 1), "var_kind": (10, np.uint8, 1), "hint_off": (11, np.uint64, 1),
     "hints": (12, np.uint32, 8), "alias_off": (13, np.uint64, 1), "aliases": (14, np.uint32, 2),
-    "flags": (15, np.uint8, 1), "var_key": (16, np.uint64, 1),
+    "flags": (15, np.uint8, 1), "var_key": (16, np.uint64, 1), "gpu_node_off": (17, np.uint64, 1),
 }
 _VAR_TABLES = ("var_off", "var_width", "var_full", "var_name", "var_aux", "var_kind", "var_key")
 FIXED_POOL_LIMBS = None  # dag._FIXED_LIMBS (set lazily: dag imports the native module too)
@@ -156,7 +156,9 @@ class Batch:
     def packed(self, gpu: bool = False):
         """(nodes, node_offsets, consts [n, 8], const_offsets) as dag.pack_states; gpu=True
         gives the program the GPU evaluates (padded key equalities strengthened)."""
-        return (self.gpu_nodes if gpu else self.nodes), self.node_off, self.consts, self.const_off
+        if gpu:
+            return self.gpu_nodes, self.gpu_node_off, self.consts, self.const_off
+        return self.nodes, self.node_off, self.consts, self.const_off
 
     def n_vars(self, s: Optional[int] = None) -> int:
         if s is None:
@@ -169,9 +171,13 @@ class Batch:
         j = 0
         for v in range(int(self.var_off[s]), int(self.var_off[s + 1])):
             j = 0 if self.var_full[v] else j + 1  # slot index within a wide value
-            nm = ARENA.names[int(self.var_name[v])]
-            if self.var_kind[v]:
-                nm = f"{nm}@{int(self.var_aux[v])}"
+            kind = int(self.var_kind[v])
+            if kind == 2:
+                nm = f"#pool{int(self.var_aux[v])}"
+            else:
+                nm = ARENA.names[int(self.var_name[v])]
+                if kind:
+                    nm = f"{nm}@{int(self.var_aux[v])}"
             out.append(nm if j == 0 else f"{nm}#{j}")
         return out
 
@@ -179,19 +185,8 @@ class Batch:
         """Witness words [n_vars, 8] of state s -> {name: value} (dag.witness_to_model)."""
         v0, v1 = int(self.var_off[s]), int(self.var_off[s + 1])
         w = np.ascontiguousarray(words[: v1 - v0], dtype=np.uint32)
-        vals = [int.from_bytes(w[i].tobytes(), "little") & ((1 << int(self.var_width[v0 + i])) - 1)
-                for i in range(v1 - v0)]
-        model: Dict[str, int] = {}
-        i = 0
-        while i < v1 - v0:
-            full = int(self.var_full[v0 + i])
-            k = max(1, (full + 255) // 256)
-            nm = ARENA.names[int(self.var_name[v0 + i])]
-            if self.var_kind[v0 + i]:
-                nm = f"{nm}@{int(self.var_aux[v0 + i])}"
-            model[nm] = sum(vals[i + j] << (256 * j) for j in range(k)) if k > 1 else vals[i]
-            i += k
-        return model
+        vals = [int.from_bytes(w[i].tobytes(), "little") for i in range(v1 - v0)]
+        return _decode(self.var_width, self.var_full, self.var_name, self.var_aux, self.var_kind, v0, v1, vals)
 
 
 class VarTables:
@@ -219,19 +214,8 @@ class SlotWitness(Mapping):
     def _dict(self) -> Dict[str, int]:
         if self._d is None:
             vt, v0, v1 = self._vt, self._v0, self._v1
-            vals = [int.from_bytes(np.ascontiguousarray(self.vals[i]).tobytes(), "little")
-                    & ((1 << int(vt.var_width[v0 + i])) - 1) for i in range(v1 - v0)]
-            d: Dict[str, int] = {}
-            i = 0
-            while i < v1 - v0:
-                full = int(vt.var_full[v0 + i])
-                k = max(1, (full + 255) // 256)
-                nm = ARENA.names[int(vt.var_name[v0 + i])]
-                if vt.var_kind[v0 + i]:
-                    nm = f"{nm}@{int(vt.var_aux[v0 + i])}"
-                d[nm] = sum(vals[i + j] << (256 * j) for j in range(k)) if k > 1 else vals[i]
-                i += k
-            self._d = d
+            vals = [int.from_bytes(np.ascontiguousarray(self.vals[i]).tobytes(), "little") for i in range(v1 - v0)]
+            self._d = _decode(vt.var_width, vt.var_full, vt.var_name, vt.var_aux, vt.var_kind, v0, v1, vals)
         return self._d
 
     def __getitem__(self, k):
@@ -248,6 +232,25 @@ class SlotWitness(Mapping):
 
 
 _KIND_UF = 1 << 63
+
+
+def _decode(var_width, var_full, var_name, var_aux, var_kind, v0: int, v1: int, vals) -> Dict[str, int]:
+    """Slot values of one state -> {name: value} (dag.witness_to_model): a wide value joined
+    from its pieces, fresh UF values as `fn@node`, pinned constants left out."""
+    d: Dict[str, int] = {}
+    i = 0
+    while i < v1 - v0:
+        full = int(var_full[v0 + i])
+        k = max(1, (full + 255) // 256)
+        kind = int(var_kind[v0 + i])
+        if kind != 2:
+            nm = ARENA.names[int(var_name[v0 + i])]
+            if kind:
+                nm = f"{nm}@{int(var_aux[v0 + i])}"
+            pieces = [vals[i + j] & ((1 << int(var_width[v0 + i + j])) - 1) for j in range(k)]
+            d[nm] = sum(p << (256 * j) for j, p in enumerate(pieces))
+        i += k
+    return d
 
 
 def parent_arrays(p) -> "tuple[np.ndarray, np.ndarray]":

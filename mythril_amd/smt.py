@@ -219,6 +219,10 @@ def bv_op(op: int, a: Term, b: Term) -> Term:
         raise ValueError(f"width mismatch {a.width} vs {b.width}")
     if a.op == ir.CONST and b.op == ir.CONST:
         return const(_fold_bin(op, a.params[0], b.params[0], w), w)
+    if op == ir.UDIV and b.op == ir.CONST and b.params[0] and b.params[0] & (b.params[0] - 1) == 0:
+        # x / 2^k is a logical shift: z3's simplify() rewrites bvudiv by a power of two so
+        # (solc <= 0.5.4 dispatchers: CALLDATALOAD(0) / 2^224, instructions.py:463-477)
+        return mk(ir.LSHR, w, (a, const(b.params[0].bit_length() - 1, w)))
     return mk(op, w, (a, b))
 
 

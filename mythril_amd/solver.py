@@ -355,32 +355,47 @@ class Prefilter:
         self.last_profile = prof
         return out
 
+    # escalating witness rounds for the states left open: (candidates per state, decision
+    # rows); each round takes only what the previous one left.  Decisions re-run the domain
+    # analysis per variable, so they are kept few until a state proves hard.
+    RETRY_SCHEDULE = ((64, 2), (256, 8), (1024, 32))
+
     def _retry_round(self, states, retry, n_vars, first, witnesses) -> None:
-        """Fresh candidates for the states the first round and the pre-check left open: up to
-        retry_cand per state (host candidate memory capped at cand_bytes), every other row
-        drawn from the pre-check's refined domains, the first 32 of those by decisions
-        (mgp_guided_candidates); the rest the usual hint / pool / uniform mixture."""
+        """Fresh candidates for the states the first round and the pre-check left open, in
+        escalating rounds (RETRY_SCHEDULE, capped by retry_cand and by cand_bytes of host
+        candidate memory): every other row drawn from the pre-check's refined domains, the
+        first of those by decisions (mgp_guided_candidates); the rest the usual hint /
+        pool / uniform mixture."""
         from . import dag as D
         from .front import FE_SAT_UNSAFE, Batch
 
-        budget = self.cand_bytes // (len(retry) * n_vars * 32)
-        n2 = min(self.retry_cand, budget) // 64 * 64
-        if n2 <= self.n_cand:
-            return
-        SB = Batch([states[i] for i in retry])
-        sv = max(1, SB.n_vars())
-        sw, sp, _ = self._N.lower(*SB.packed(gpu=True))
-        c2 = self._N.make_candidates(n2, sv, self.seed + 0x9E3779B9 + self._calls, SB.var_off, SB.var_width,
-                                     SB.hint_off, SB.hints, SB.alias_off, SB.aliases, SB.const_off, SB.consts,
-                                     D._FIXED_LIMBS, np.zeros(len(retry), np.uint8))
-        self._N.guided_candidates(*SB.packed(), c2, seed=self.seed + self._calls, every=2, n_decide=32)
-        f2, w2 = self.ctx.eval_batch(sw, sp, c2)
-        unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
-        for k, i in enumerate(retry):
-            if f2[k] >= 0 and not unsafe[k]:
-                first[i] = f2[k]
-                witnesses[i] = SB.witness(k, w2[k])
-        SB.close()
+        open_ = list(retry)
+        for rnd, (n_cand, n_decide) in enumerate(self.RETRY_SCHEDULE):
+            if not open_:
+                break
+            budget = self.cand_bytes // (len(open_) * n_vars * 32)
+            n2 = min(n_cand, self.retry_cand, budget) // 64 * 64
+            if n2 < 64:
+                break
+            SB = Batch([states[i] for i in open_])
+            sv = max(1, SB.n_vars())
+            sw, sp, _ = self._N.lower(*SB.packed(gpu=True))
+            seed = self.seed + 0x9E3779B9 * (rnd + 1) + self._calls
+            c2 = self._N.make_candidates(n2, sv, seed, SB.var_off, SB.var_width, SB.hint_off, SB.hints,
+                                         SB.alias_off, SB.aliases, SB.const_off, SB.consts, D._FIXED_LIMBS,
+                                         np.zeros(len(open_), np.uint8), var_kind=SB.var_kind)
+            self._N.guided_candidates(*SB.packed(), c2, seed=seed, every=2, n_decide=n_decide)
+            f2, w2 = self.ctx.eval_batch(sw, sp, c2)
+            unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
+            left = []
+            for k, i in enumerate(open_):
+                if f2[k] >= 0 and not unsafe[k]:
+                    first[i] = f2[k]
+                    witnesses[i] = SB.witness(k, w2[k])
+                else:
+                    left.append(i)
+            SB.close()
+            open_ = left
         SolverStatistics().gpu_retry += len(retry)
 
 

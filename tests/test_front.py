@@ -22,6 +22,7 @@ def _assert_same(states):
     g = D.pack_states(dags, gpu=True)
     assert np.array_equal(B.nodes, p[0])
     assert np.array_equal(B.gpu_nodes, g[0])
+    assert np.array_equal(B.gpu_node_off, g[1])
     assert np.array_equal(B.node_off, p[1])
     assert np.array_equal(B.consts, p[2].reshape(-1, 8))
     assert np.array_equal(B.const_off, p[3])
@@ -30,6 +31,7 @@ def _assert_same(states):
         v0, v1 = int(B.var_off[s]), int(B.var_off[s + 1])
         assert B.var_names(s) == [n for n, _ in d.vars]
         assert list(B.var_width[v0:v1]) == [w for _, w in d.vars]
+        assert [vi for vi in range(d.n_vars) if B.var_kind[v0 + vi] == 2] == sorted(d.pinned)
         for vi in range(d.n_vars):
             h = B.hints[int(B.hint_off[v0 + vi]): int(B.hint_off[v0 + vi + 1])]
             assert [int.from_bytes(x.tobytes(), "little") for x in h] == d.hints.get(vi, []), (s, vi)
@@ -42,9 +44,9 @@ def _assert_same(states):
 
 
 def test_contract_shaped_states():
-    import bench
+    import corpus
 
-    _assert_same([[type("T", (), {"raw": t})() for t in st] for st in bench._contract_states(96)])
+    _assert_same([[type("T", (), {"raw": t})() for t in c[1]] for c in corpus.corpus(96)])
 
 
 def test_operator_zoo_wide_values_arrays_ufs():
@@ -97,3 +99,16 @@ def test_empty_batch_and_state():
     assert B.n_states == 0 and len(B.node_off) == 1
     B.close()
     _assert_same([[]])
+
+
+def test_mixed_corpus_with_pinned_constants():
+    """suicide / BECToken / WalletLibrary shapes (corpus.py): several calldata words push the
+    constant pool past MGP_FE_POOL_KEEP, so the GPU program pins the rest."""
+    import corpus
+
+    dags = _assert_same([[type("T", (), {"raw": t})() for t in c[1]] for c in corpus.corpus(40)])
+    assert any(d.flags & 4 for d in dags) and any(d.pinned for d in dags)
+    for d in dags:  # the GPU program's front VAR nodes read exactly the pinned slots
+        if d.gpu_nodes is not None and d.flags & 4:
+            front = [n for n in d.gpu_nodes[: len(d.gpu_nodes) - len(d.nodes)]]
+            assert all(n[0] == 1 for n in front) and {n[5] for n in front} <= set(d.pinned)

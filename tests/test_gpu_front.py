@@ -22,9 +22,9 @@ BVV, BVS = symbol_factory.BitVecVal, symbol_factory.BitVecSym
 
 
 def _contract_batch(n):
-    import bench
+    import corpus
 
-    return bench._contract_states(n)
+    return [c[1] for c in corpus.corpus(n)]  # suicide, BECToken, WalletLibrary shapes (pinned constants too)
 
 
 def test_device_candidates_equal_host_generator(mgp_ctx):
@@ -34,7 +34,8 @@ def test_device_candidates_equal_host_generator(mgp_ctx):
     for n_cand, seed in ((64, 5), (256, 0x4D595448), (37, 11)):
         dev = B.device_candidates(mgp_ctx, n_cand, n_vars, seed)
         host = N.make_candidates(n_cand, n_vars, seed, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off,
-                                 B.aliases, B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8))
+                                 B.aliases, B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8),
+                                 var_kind=B.var_kind)
         bad = np.nonzero((dev != host).any(axis=(1, 2, 3)))[0]
         assert bad.size == 0, f"n_cand={n_cand}: {bad.size} states differ, first {bad[:5]}"
     B.close()
@@ -51,7 +52,10 @@ def test_check_batch_matches_oracle_and_refute(mgp_ctx):
     n_vars = max(1, B.n_vars())
     cands = B.device_candidates(mgp_ctx, n_cand, n_vars, seed)
     want = coracle.first_sat(*B.packed(gpu=True), cands)
-    assert np.array_equal(first, want)
+    _, _, status = N.lower(*B.packed(gpu=True))
+    ok = status == 0  # the rest (WalletLibrary shapes past the lowering's budgets) is undecided
+    assert np.array_equal(first[ok], want[ok]) and (first[~ok] == N.MGP_UNDECIDED).all()
+    assert ok.sum() >= len(states) // 2
     assert np.array_equal(ref, N.refute(*B.packed()))
     assert ref[200] == 1 and first[200] == -1
     assert first[202] >= 0

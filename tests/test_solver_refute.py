@@ -153,5 +153,8 @@ def test_second_candidate_round(fe, monkeypatch):
     assert SV.batch_is_possible(items) == [True, False]
     st = SV.SolverStatistics()
     assert st.gpu_retry == 1 and st.gpu_sat == 1 and st.refuted == 1 and fe.calls == 0
-    assert SV.prefilter().ctx.batches == 2
+    # the first round, then the escalating retry rounds (64, 256, 1024 candidates): the
+    # stub only "satisfies" in the 1024-candidate one
+    assert [n for n, _ in SV.Prefilter.RETRY_SCHEDULE] == [64, 256, 1024]
+    assert SV.prefilter().ctx.batches == 4
     assert set(items[0].witness) == {"rx", "ry"}

@@ -210,7 +210,15 @@ int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uin
                         const uint64_t *alias_off, const uint32_t *aliases,
                         const uint64_t *const_off, const uint32_t *consts,
                         const uint32_t *fixed_pool, uint32_t n_fixed,
-                        const uint8_t *has_parent, uint32_t *out);
+                        const uint8_t *has_parent, const uint32_t *dom, uint32_t *out);
+/* mgp_refute plus the refined abstract value of every variable slot of the states it
+ * does not refute: out_dom has 33 u32 per slot of var_off (known-zero, known-one, lo,
+ * hi as 8 limbs each, then 1 if the slot has a domain, else 0).  `dom` of
+ * mgp_make_candidates / the device generator: every other mixture row draws those
+ * slots from their domains (mgp_fe_sample.h), an inside hint half of the time. */
+int mgp_refute_domains(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                       const uint32_t *consts, const uint64_t *const_offsets, const uint64_t *var_off,
+                       uint32_t max_passes, int8_t *out, uint32_t *out_dom);
 
 /* ------------------------------------------------------ native front end
  * Flattens a batch of states' path constraints (the roots) into node lists, constant
@@ -256,7 +264,8 @@ enum mgp_fe_field {
   MGP_FE_ALIASES,       /* uint32_t, 2 per pair         */
   MGP_FE_FLAGS,         /* uint8_t per state            */
   MGP_FE_VAR_KEY,       /* uint64_t per slot: name id, kind, UF node, piece (parent matching) */
-  MGP_FE_GPU_NODE_OFF   /* uint64_t, n_states + 1: offsets into GPU_NODES */
+  MGP_FE_GPU_NODE_OFF,  /* uint64_t, n_states + 1: offsets into GPU_NODES */
+  MGP_FE_VAR_TID        /* int32_t per slot: arena id of the VAR / UF term it stands for (-1 pinned) */
 };
 int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t *t_args, const uint32_t *t_p,
                      uint64_t n_terms, const uint32_t *limbs, uint64_t n_limbs, const int32_t *roots,
@@ -274,10 +283,11 @@ void mgp_fe_free(mgp_fe_batch *batch);
  * mgp_eval_batch, out_witness (may be NULL) n_states x n_vars x 8 u32 with n_vars =
  * *out_n_vars = the batch's widest state (SAT rows only), out_refuted[s] as
  * mgp_refute.  out_times (may be NULL) receives 5 stage times in ms: lower,
- * upload+launch, refute, GPU wait, copy-back.  Replaces, for one batch, the z3
+ * refute, upload+launch, GPU wait, copy-back.  Replaces, for one batch, the z3
  * checks of Constraints.is_possible (constraints.py:34-51) and the SAT-only get_model
  * calls (analysis/solver.py:27-61) it can decide. */
-#define MGP_CHECK_NO_REFUTE 0x1u
+#define MGP_CHECK_NO_REFUTE 0x1u   /* skip the host pre-check (and the domain rows) */
+#define MGP_CHECK_NO_DOMAINS 0x2u  /* plain mixture rows only (A/B)                    */
 int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint64_t seed,
                     const uint32_t *fixed_pool, uint32_t n_fixed, const uint64_t *parent_keys,
                     const uint32_t *parent_vals, const uint64_t *parent_off, const uint64_t *slot_keys,
@@ -286,7 +296,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, ui
 /* Test hook: the candidates mgp_check_batch would evaluate (no parents), device layout
  * [state][var][half][cand] of 16-byte groups, n_vars >= the batch's widest state. */
 int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                      const uint32_t *fixed_pool, uint32_t n_fixed, uint32_t *out);
+                      const uint32_t *fixed_pool, uint32_t n_fixed, const uint32_t *dom, uint32_t *out);
 
 /* ---------------------------------------------------------- Keccak-256
  * n preimages of len bytes each, preimage i at in + i*stride; 32-byte

@@ -90,12 +90,13 @@ def _bind(lib):
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
         "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
         "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32,
-                                               _P, _P]),
+                                               _P, _P, _P]),
+        "mgp_refute_domains": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
         "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, ctypes.POINTER(_P)]),
         "mgp_fe_get": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
         "mgp_fe_free": (None, [_P]),
         "mgp_check_batch": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _P]),
-        "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P]),
+        "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -147,6 +148,7 @@ EXPORTED_SYMBOLS = (
     "mgp_refute_trace",
     "mgp_guided_candidates",
     "mgp_make_candidates",
+    "mgp_refute_domains",
     "mgp_build_states",
     "mgp_fe_get",
     "mgp_fe_free",
@@ -220,7 +222,7 @@ def lower(
 
 
 def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hint_off, hints, alias_off, aliases,
-                    const_off, consts, fixed_pool, has_parent, var_kind=None) -> np.ndarray:
+                    const_off, consts, fixed_pool, has_parent, var_kind=None, dom=None) -> np.ndarray:
     """mgp_make_candidates over flattened per-state tables -> uint32 [n_states, n_cand, n_vars, 8]."""
     def u(a, dt):
         a = np.ascontiguousarray(a, dtype=dt)
@@ -235,8 +237,27 @@ def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hin
                                      _ptr(u(hints, np.uint32)), _ptr(u(alias_off, np.uint64)),
                                      _ptr(u(aliases, np.uint32)), _ptr(u(const_off, np.uint64)),
                                      _ptr(u(consts, np.uint32)), _ptr(fixed), len(fixed_pool),
-                                     _ptr(u(has_parent, np.uint8)), _ptr(out)))
+                                     _ptr(u(has_parent, np.uint8)),
+                                     None if dom is None else _ptr(np.ascontiguousarray(dom, dtype=np.uint32)),
+                                     _ptr(out)))
     return out
+
+
+def refute_domains(nodes, node_offsets, consts, const_offsets, var_off, max_passes: int = 0):
+    """mgp_refute + per-slot refined abstract values -> (status int8[n], dom uint32[n_slots, 33])."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    const_offsets = np.ascontiguousarray(const_offsets, dtype=np.uint64)
+    var_off = np.ascontiguousarray(var_off, dtype=np.uint64)
+    n_states = len(node_offsets) - 1
+    out = np.zeros(max(n_states, 1), dtype=np.int8)
+    dom = np.zeros((max(int(var_off[-1]), 1), 33), dtype=np.uint32)
+    _check(lib().mgp_refute_domains(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
+                                    _ptr(var_off), max_passes, _ptr(out), _ptr(dom)))
+    return out[:n_states], dom[: int(var_off[-1])]
 
 
 def guided_candidates(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,

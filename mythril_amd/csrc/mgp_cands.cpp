@@ -8,6 +8,8 @@
 // neighbours +-1, LASER's actor addresses and boundary values), 15 % alias of an
 // equal-width variable, 25 % uniform.  Every value is masked to its slot width.
 // A pinned-constant slot (var_kind 2, mgp_front.cpp) holds its hint 0 in every row.
+// With domains (mgp_refute_domains), every other mixture row draws the variables that
+// have a refined abstract value from it (mgp_fe_sample.h).
 // States are independent (OpenMP); the stream is splitmix64 keyed by (seed, state,
 // row, variable), so the result does not depend on the thread count.
 #include <stdint.h>
@@ -16,6 +18,7 @@
 #include <vector>
 
 #include "../../include/mgp.h"
+#include "mgp_fe_sample.h"
 
 namespace {
 inline uint64_t mix(uint64_t z) {
@@ -50,7 +53,7 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
                                    const uint64_t *alias_off, const uint32_t *aliases,
                                    const uint64_t *const_off, const uint32_t *consts,
                                    const uint32_t *fixed_pool, uint32_t n_fixed,
-                                   const uint8_t *has_parent, uint32_t *out) {
+                                   const uint8_t *has_parent, const uint32_t *dom, uint32_t *out) {
   if (!var_off || !hint_off || !alias_off || !const_off || !out || (n_states && !has_parent)) return MGP_E_ARG;
 #pragma omp parallel for schedule(dynamic, 4)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
@@ -95,6 +98,7 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
     }
     std::vector<uint32_t> srcs;
     std::vector<uint8_t> pend(V);
+    const uint32_t mix0 = row;  // first mixture row
     for (uint32_t c = row; c < n_cand; ++c) {
       for (uint64_t v = 0; v < V; ++v) {
         const uint64_t k = mix(seed ^ 0xA5A5A5A5ull ^ mix(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
@@ -117,6 +121,28 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
         const uint64_t k = mix(seed ^ 0x5A5A5A5Aull ^ mix(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
         memcpy(cell(c, v), cell(c, srcs[k % srcs.size()]), 32);
       }
+      // domain rows (every other mixture row): variables with a refined abstract value
+      // (mgp_refute_domains) are drawn from it, an inside hint half of the time
+      const uint32_t kk = c - mix0;
+      if (dom && (kk & 1u) == 0u)
+        for (uint64_t v = 0; v < V; ++v) {
+          const uint32_t *d = dom + (v0 + v) * 33u;
+          if (!d[32]) continue;
+          U256 z, o, lo, hi;
+          memcpy(z.w, d, 32);
+          memcpy(o.w, d + 8, 32);
+          memcpy(lo.w, d + 16, 32);
+          memcpy(hi.w, d + 24, 32);
+          const uint64_t key = fe_mix64(seed ^ 0xD0D0D0D0ull ^ fe_mix64(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
+          U256 x = fe_sample_domain(z, o, lo, hi, var_width[v0 + v], kk / 2u, key);
+          if (n_hint(v) && (fe_mix64(key ^ 0x9E37ull) & 1u)) {
+            U256 h;
+            memcpy(h.w, hint(v, fe_mix64(key ^ 0x7F4Aull) % n_hint(v)), 32);
+            h = bv_mask(h, var_width[v0 + v]);
+            if (fe_inside(z, o, lo, hi, h)) x = h;
+          }
+          memcpy(cell(c, v), x.w, 32);
+        }
     }
     for (uint32_t c = 0; c < n_cand; ++c)
       for (uint64_t v = 0; v < V; ++v) {

@@ -56,6 +56,7 @@ struct StateOut {
   std::vector<uint32_t> var_width, var_full, var_name, var_aux;  // per slot
   std::vector<uint8_t> var_kind;
   std::vector<uint64_t> var_key;
+  std::vector<int32_t> var_tid;            // per slot: the VAR / UF term it stands for (-1 pinned)
   std::vector<std::vector<uint32_t>> hints;  // per slot: 8 limbs per hint
   std::vector<uint32_t> aliases;           // (dst, src) pairs
   uint8_t flags = 0;
@@ -187,9 +188,10 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
   const_idx.reset(64);
   X.cents.clear();
   using CEnt = Scratch::CEnt;
-  auto new_slots = [&](uint32_t name, uint32_t width, uint8_t kind, uint32_t aux) -> uint32_t {
+  auto new_slots = [&](uint32_t name, uint32_t width, uint8_t kind, uint32_t aux, int32_t tid) -> uint32_t {
     const uint32_t first = (uint32_t)S.var_width.size();
     for (uint32_t off = 0, j = 0; off < width; off += 256, ++j) {
+      S.var_tid.push_back(tid);
       S.var_width.push_back(std::min<uint32_t>(256, width - off));
       S.var_full.push_back(j == 0 ? width : 0u);
       S.var_name.push_back(name);
@@ -222,7 +224,7 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
       if (it) {
         nd.p0 = *it;
       } else {
-        nd.p0 = new_slots(p0, w, 0, 0);
+        nd.p0 = new_slots(p0, w, 0, 0, t);
         var_idx.put(key, nd.p0);
       }
     } else if (op == MGP_OP_CONST) {
@@ -265,7 +267,7 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
       nd.p1 = p1;
     } else if (op == MGP_OP_UFAPP || op == MGP_OP_UFINV) {
       nd.p0 = p0;
-      nd.p1 = new_slots(p1, w, 1, (uint32_t)S.nodes.size());
+      nd.p1 = new_slots(p1, w, 1, (uint32_t)S.nodes.size(), t);
     }
     S.nodes.push_back(nd);
     return (int32_t)S.nodes.size() - 1;
@@ -492,6 +494,7 @@ void pin_constants(StateOut &S) {
         S.var_aux.push_back(n.p0);
         S.var_kind.push_back(2u);
         S.var_key.push_back(slot_key(0, 2, n.p0, j));
+        S.var_tid.push_back(-1);
         S.hints.emplace_back(S.consts.begin() + 8ull * (n.p0 + j), S.consts.begin() + 8ull * (n.p0 + j) + 8);
       }
     }
@@ -531,6 +534,7 @@ struct mgp_fe_batch {
   std::vector<uint32_t> consts, var_width, var_full, var_name, var_aux, hints, aliases;
   std::vector<uint8_t> var_kind, flags;
   std::vector<uint64_t> var_key;
+  std::vector<int32_t> var_tid;
 };
 
 extern "C" {
@@ -589,6 +593,7 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
   B->var_aux.resize(nv);
   B->var_kind.resize(nv);
   B->var_key.resize(nv);
+  B->var_tid.resize(nv);
   B->aliases.resize(B->alias_off[n_states] * 2);
   B->hint_off.assign(nv + 1, 0);
   bool strengthened = false;
@@ -611,6 +616,7 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
     std::copy(S.var_aux.begin(), S.var_aux.end(), B->var_aux.begin() + v0);
     std::copy(S.var_kind.begin(), S.var_kind.end(), B->var_kind.begin() + v0);
     std::copy(S.var_key.begin(), S.var_key.end(), B->var_key.begin() + v0);
+    std::copy(S.var_tid.begin(), S.var_tid.end(), B->var_tid.begin() + v0);
     std::copy(S.aliases.begin(), S.aliases.end(), B->aliases.begin() + B->alias_off[s] * 2);
     for (size_t v = 0; v < S.hints.size(); ++v)
       std::copy(S.hints[v].begin(), S.hints[v].end(), B->hints.begin() + B->hint_off[v0 + v] * 8);
@@ -657,6 +663,7 @@ int mgp_fe_get(const mgp_fe_batch *B, int field, const void **ptr, uint64_t *cou
     case MGP_FE_ALIASES: return set(B->aliases);
     case MGP_FE_FLAGS: return set(B->flags);
     case MGP_FE_VAR_KEY: return set(B->var_key);
+    case MGP_FE_VAR_TID: return set(B->var_tid);
     case MGP_FE_GPU_NODE_OFF: return set(B->gpu_nodes.empty() ? B->node_off : B->gpu_node_off);
     default: return MGP_E_ARG;
   }

@@ -29,6 +29,7 @@
 
 #include "../../include/mgp.h"
 #include "mgp_bv.h"
+#include "mgp_fe_sample.h"
 
 #define MGP_WAVE 64
 #define MGP_PARTIAL_NONE 0x7FFFFFFF
@@ -667,7 +668,7 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
     const uint64_t *__restrict__ alias_off, const uint32_t *__restrict__ aliases,
     const uint64_t *__restrict__ const_off, const uint32_t *__restrict__ consts, const uint32_t *__restrict__ fixed,
     uint32_t n_fixed, const int32_t *__restrict__ parent_idx, const uint32_t *__restrict__ pvals,
-    const uint8_t *__restrict__ pmask, uint4 *__restrict__ out) {
+    const uint8_t *__restrict__ pmask, const uint32_t *__restrict__ dom, uint4 *__restrict__ out) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (uint64_t)n_states * n_cand) return;
   const uint64_t s = g / n_cand;
@@ -771,6 +772,29 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       }
       R.copy((uint32_t)v, (uint32_t)src);
     }
+    const uint32_t kk = c - (first_row + 2u);  // domain rows: as mgp_make_candidates
+    if (dom && (kk & 1u) == 0u)
+      for (uint64_t v = 0; v < V; ++v) {
+        const uint32_t *d = dom + (v0 + v) * 33u;
+        if (!d[32]) continue;
+        U256 z, o, lo, hi;
+        for (int l = 0; l < 8; ++l) {
+          z.w[l] = d[l];
+          o.w[l] = d[8 + l];
+          lo.w[l] = d[16 + l];
+          hi.w[l] = d[24 + l];
+        }
+        const uint64_t key = fe_mix64(seed ^ 0xD0D0D0D0ull ^ fe_mix64((s << 40) ^ ((uint64_t)c << 16) ^ v));
+        U256 xv = fe_sample_domain(z, o, lo, hi, var_width[v0 + v], kk / 2u, key);
+        if (n_hint(v) && (fe_mix64(key ^ 0x9E37ull) & 1u)) {
+          const uint32_t *hp = hint(v, fe_mix64(key ^ 0x7F4Aull) % n_hint(v));
+          U256 h;
+          for (int l = 0; l < 8; ++l) h.w[l] = hp[l];
+          h = bv_mask(h, var_width[v0 + v]);
+          if (fe_inside(z, o, lo, hi, h)) xv = h;
+        }
+        R.put((uint32_t)v, xv.w);
+      }
   }
   for (uint64_t v = 0; v < V; ++v) {  // pinned constants, then the mask to the slot width
     if (var_kind && var_kind[v0 + v] == 2 && n_hint(v)) R.put((uint32_t)v, hint(v, 0));
@@ -1049,14 +1073,14 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
                                const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
-                               const uint8_t *pmask, uint32_t *out, hipStream_t st) {
+                               const uint8_t *pmask, const uint32_t *dom, uint32_t *out, hipStream_t st) {
   const uint64_t total = (uint64_t)n_states * n_cand;
   if (total == 0) return hipSuccess;
   const uint64_t blocks = (total + 255) / 256;
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mgp_fe_cands_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, n_states, n_cand, n_vars, seed,
                      var_off, var_width, var_kind, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed,
-                     parent_idx, pvals, pmask, reinterpret_cast<uint4 *>(out));
+                     parent_idx, pvals, pmask, dom, reinterpret_cast<uint4 *>(out));
   return hipGetLastError();
 }
 

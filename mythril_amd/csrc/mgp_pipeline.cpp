@@ -6,16 +6,18 @@
 // and of the SAT-only get_model calls (mythril/analysis/solver.py:27-61).  Input is a
 // front-end batch (mgp_front.cpp).  Stages, in order, on the context's stream:
 //   1. lower the GPU program of every state (mgp_lower.cpp, OpenMP);
-//   2. upload programs and the candidate tables (variable widths, hints, aliases,
-//      constants, parent-witness rows) — a few hundred bytes per state, instead of
-//      n_cand x n_vars x 32 B of host-built candidates;
-//   3. mgp_fe_cands_kernel writes the candidates straight into the interpreter's
-//      [state][var][half][cand] layout; launch descriptors, the gfx950 interpreter
-//      and the first-SAT reduction follow (mgp_launch_eval);
-//   4. while those run, mgp_refute proves UNSAT on the host for the states it can
-//      (original nodes: the sound direction, see mgp_front.cpp);
+//   2. the host UNSAT pre-check (mgp_refute_domains, original nodes: the sound
+//      direction, see mgp_front.cpp), which also yields every variable's refined
+//      abstract value;
+//   3. upload programs and the candidate tables (variable widths, hints, aliases,
+//      constants, parent-witness rows, domains) — a few hundred bytes per variable,
+//      instead of n_cand x n_vars x 32 B of host-built candidates;
+//   4. mgp_fe_cands_kernel writes the candidates straight into the interpreter's
+//      [state][var][half][cand] layout (every other mixture row drawn from the
+//      domains); launch descriptors, the gfx950 interpreter and the first-SAT
+//      reduction follow (mgp_launch_eval);
 //   5. first-SAT words and witnesses come back.
-// Stage times (ms) go to out_times[0..4] when given: lower, upload+launch, refute,
+// Stage times (ms) go to out_times[0..4] when given: lower, refute, upload+launch,
 // GPU wait, copy-back.
 #include <hip/hip_runtime.h>
 #include <omp.h>
@@ -41,7 +43,7 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
                                const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
-                               const uint8_t *pmask, uint32_t *out, hipStream_t st);
+                               const uint8_t *pmask, const uint32_t *dom, uint32_t *out, hipStream_t st);
 int mgp_fe_get(const mgp_fe_batch *batch, int field, const void **ptr, uint64_t *count);
 int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device);
 int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg);
@@ -171,7 +173,22 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   }
   lap(0);
 
-  // 2. upload
+  // 2. host UNSAT pre-check + variable domains
+  std::vector<uint32_t> dom;
+  if (flags & MGP_CHECK_NO_REFUTE) {
+    memset(out_refuted, 0, n_states);
+  } else {
+    const bool want_dom = !(flags & MGP_CHECK_NO_DOMAINS);
+    if (want_dom) dom.assign((size_t)vo[n_states] * 33u, 0u);
+    rc = want_dom ? mgp_refute_domains((const mgp_node *)nodes.p, (const uint64_t *)noff.p, n_states, cp,
+                                       (const uint64_t *)coff.p, vo, 0, out_refuted, dom.data())
+                  : mgp_refute((const mgp_node *)nodes.p, (const uint64_t *)noff.p, n_states, cp,
+                               (const uint64_t *)coff.p, 0, out_refuted);
+    if (rc != MGP_OK) return mgp_ctx_fail(ctx, rc, "mgp_refute failed");
+  }
+  lap(1);
+
+  // 3. upload
   void *stp = nullptr;
   int dev = 0;
   mgp_ctx_stream(ctx, &stp, &dev);
@@ -181,18 +198,18 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   const size_t cand_bytes = (size_t)n_states * n_cand * n_vars * 32u;
   const uint32_t n_chunks = (n_cand + 63u) / 64u;
   // one table buffer: var_off | var_width | hint_off | hints | alias_off | aliases | const_off | consts |
-  // fixed | parent_idx | pvals | pmask | var_kind, each 256-B aligned
+  // fixed | parent_idx | pvals | pmask | var_kind | dom, each 256-B aligned
   // (mgp_fe_get counts elements of each array: u32 limbs for consts / hints / aliases)
-  const size_t sizes[13] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+  const size_t sizes[14] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
                             coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32,
-                            (size_t)n_states * 4, pvals.size() * 4, pmask.size(), vkind.n};
-  const void *srcs[13] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
-                          pidx.data(), pvals.data(), pmask.data(), vkind.p};
-  size_t at[14];
+                            (size_t)n_states * 4, pvals.size() * 4, pmask.size(), vkind.n, dom.size() * 4};
+  const void *srcs[14] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
+                          pidx.data(), pvals.data(), pmask.data(), vkind.p, dom.data()};
+  size_t at[15];
   at[0] = 0;
-  for (int i = 0; i < 13; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
-  std::vector<uint8_t> stage(at[13]);
-  for (int i = 0; i < 13; ++i)
+  for (int i = 0; i < 14; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[14]);
+  for (int i = 0; i < 14; ++i)
     if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
   if (e == hipSuccess) e = D.ensure(B_WORDS, words.size() * 4u);
   if (e == hipSuccess) e = D.ensure(B_OFFS, offs.size() * 8u);
@@ -201,12 +218,12 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   if (e == hipSuccess) e = D.ensure(B_FIRST, (size_t)n_states * 4u);
   if (e == hipSuccess) e = D.ensure(B_WIT, (size_t)n_states * n_vars * 32u);
   if (e == hipSuccess) e = D.ensure(B_PART, (size_t)n_states * n_chunks * 4u);
-  if (e == hipSuccess) e = D.ensure(B_TABLES, at[13]);
+  if (e == hipSuccess) e = D.ensure(B_TABLES, at[14]);
   if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_WORDS], words.data(), words.size() * 4u, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_OFFS], offs.data(), offs.size() * 8u, hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(D.p[B_ORDER], order.data(), (size_t)n_states * 4u, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], stage.data(), at[13], hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], stage.data(), at[14], hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
   const uint8_t *tb = (const uint8_t *)D.p[B_TABLES];
   e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
@@ -216,7 +233,8 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
                           (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
                           (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed,
                           (const int32_t *)(tb + at[9]), (const uint32_t *)(tb + at[10]),
-                          (const uint8_t *)(tb + at[11]), (uint32_t *)D.p[B_CANDS], st);
+                          (const uint8_t *)(tb + at[11]), dom.empty() ? nullptr : (const uint32_t *)(tb + at[13]),
+                          (uint32_t *)D.p[B_CANDS], st);
   if (e == hipSuccess) e = hipMemsetAsync(D.p[B_PART], 0x7E, (size_t)n_states * n_chunks * 4u, st);
   if (e == hipSuccess)
     e = mgp_launch_eval((const uint32_t *)D.p[B_WORDS], (const uint64_t *)D.p[B_OFFS], n_states,
@@ -226,19 +244,6 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   if (e == hipSuccess)
     e = hipMemcpyAsync(out_first, D.p[B_FIRST], (size_t)n_states * 4u, hipMemcpyDeviceToHost, st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
-  lap(1);
-
-  // 4. host UNSAT pre-check on the original nodes while the GPU runs
-  if (flags & MGP_CHECK_NO_REFUTE) {
-    memset(out_refuted, 0, n_states);
-  } else {
-    rc = mgp_refute((const mgp_node *)nodes.p, (const uint64_t *)noff.p, n_states, cp, (const uint64_t *)coff.p, 0,
-                    out_refuted);
-    if (rc != MGP_OK) {
-      (void)hipStreamSynchronize(st);
-      return mgp_ctx_fail(ctx, rc, "mgp_refute failed");
-    }
-  }
   lap(2);
   e = hipStreamSynchronize(st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
@@ -261,7 +266,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
 // Test hook: the candidates mgp_check_batch evaluates, copied back in the device layout
 // [state][var][half][cand] of 16-byte groups (tests compare them with mgp_make_candidates).
 int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                      const uint32_t *fixed_pool, uint32_t n_fixed, uint32_t *out) {
+                      const uint32_t *fixed_pool, uint32_t n_fixed, const uint32_t *dom, uint32_t *out) {
   if (!ctx || !B || !out || n_cand == 0 || n_vars == 0) return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument");
   const Arr noff = get(B, MGP_FE_NODE_OFF), consts = get(B, MGP_FE_CONSTS), coff = get(B, MGP_FE_CONST_OFF),
             voff = get(B, MGP_FE_VAR_OFF), vwidth = get(B, MGP_FE_VAR_WIDTH), hoff = get(B, MGP_FE_HINT_OFF),
@@ -274,22 +279,23 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
   mgp_ctx_stream(ctx, &stp, &dev);
   hipStream_t st = (hipStream_t)stp;
   static const uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const size_t sizes[10] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
-                            coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32, vkind.n};
-  const void *srcs[10] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
-                          consts.n ? consts.p : zero8, fixed_pool, vkind.p};
-  size_t at[11];
+  const size_t sizes[11] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+                            coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32, vkind.n,
+                            dom ? (size_t)((const uint64_t *)voff.p)[n_states] * 33u * 4u : 0};
+  const void *srcs[11] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
+                          consts.n ? consts.p : zero8, fixed_pool, vkind.p, dom};
+  size_t at[12];
   at[0] = 0;
-  for (int i = 0; i < 10; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
-  std::vector<uint8_t> stage(at[10]);
-  for (int i = 0; i < 10; ++i)
+  for (int i = 0; i < 11; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[11]);
+  for (int i = 0; i < 11; ++i)
     if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
   const size_t cb = (size_t)n_states * n_cand * n_vars * 32u;
   void *dt = nullptr, *dc = nullptr;
   hipError_t e = hipSetDevice(dev);
-  if (e == hipSuccess) e = hipMalloc(&dt, at[10]);
+  if (e == hipSuccess) e = hipMalloc(&dt, at[11]);
   if (e == hipSuccess) e = hipMalloc(&dc, cb);
-  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[10], hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[11], hipMemcpyHostToDevice, st);
   const uint8_t *tb = (const uint8_t *)dt;
   if (e == hipSuccess)
     e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
@@ -298,7 +304,7 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
                             (const uint32_t *)(tb + at[3]), (const uint64_t *)(tb + at[4]),
                             (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
                             (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed, nullptr,
-                            nullptr, nullptr, (uint32_t *)dc, st);
+                            nullptr, nullptr, dom ? (const uint32_t *)(tb + at[10]) : nullptr, (uint32_t *)dc, st);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dc, cb, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (dt) (void)hipFree(dt);

@@ -31,6 +31,7 @@
 
 #include "../../include/mgp.h"
 #include "mgp_bv.h"
+#include "mgp_fe_sample.h"
 
 namespace {
 
@@ -1071,6 +1072,47 @@ extern "C" int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets, u
   return MGP_OK;
 }
 
+// mgp_refute plus, for every variable slot of a state it does not refute, the slot's
+// refined abstract value: 33 u32 per slot of var_off (z, o, lo, hi as 8 limbs each,
+// then 1 if the slot has a domain).  The device candidate generator draws every other
+// first-round row from these domains (mgp_check_batch).
+extern "C" int mgp_refute_domains(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                  const uint32_t *consts, const uint64_t *const_offsets, const uint64_t *var_off,
+                                  uint32_t max_passes, int8_t *out, uint32_t *out_dom) {
+  if (!node_offsets || !out || !var_off || !out_dom || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
+  memset(out_dom, 0, (size_t)var_off[n_states] * 33u * 4u);
+#pragma omp parallel for schedule(dynamic, 8)
+  for (int64_t st = 0; st < (int64_t)n_states; ++st) {
+    const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
+    const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
+    if (n1 < n0 || c1 < c0) {
+      out[st] = -1;
+      continue;
+    }
+    State s;
+    const int r = refute_one(nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, &s);
+    out[st] = (int8_t)r;
+    if (r != 0) continue;
+    const uint64_t nv = var_off[st + 1] - var_off[st];
+    for (uint32_t i = 0; i < s.n; ++i) {
+      const mgp_node &x = s.nd[i];
+      uint32_t v;
+      if (x.op == MGP_OP_VAR) v = x.p0;
+      else if (x.op == MGP_OP_UFAPP || x.op == MGP_OP_UFINV) v = x.p1;
+      else continue;
+      if (v >= nv || x.width == 0u || x.width > MGP_MAX_WIDTH) continue;
+      uint32_t *d = out_dom + (var_off[st] + v) * 33u;
+      const AV &a = s.av[i];
+      memcpy(d, a.z.w, 32);
+      memcpy(d + 8, a.o.w, 32);
+      memcpy(d + 16, a.lo.w, 32);
+      memcpy(d + 24, a.hi.w, 32);
+      d[32] = 1u;
+    }
+  }
+  return MGP_OK;
+}
+
 extern "C" int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *consts,
                                 uint64_t n_consts, uint32_t max_passes, uint32_t *out_av) {
   if (!nodes || !out_av) return MGP_E_ARG;
@@ -1089,45 +1131,12 @@ extern "C" int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes, const u
 }
 
 namespace {
-inline uint64_t mix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
+inline uint64_t mix64(uint64_t z) { return fe_mix64(z); }
 
-// One value of width w inside the abstract value a (known bits z/o, interval lo..hi),
-// drawn from r: interval bounds and their neighbours for the first rows, then a
-// draw inside the interval with the known bits forced when that stays inside.
+// One value of width w inside the abstract value a (mgp_fe_sample.h, shared with the
+// candidate generators).
 V sample_av(const AV &a, uint32_t w, uint32_t row, uint64_t r0) {
-  V v;
-  uint64_t r = r0;
-  for (int l = 0; l < 8; ++l) {
-    if ((l & 1) == 0) r = mix64(r);
-    v.w[l] = (uint32_t)(r >> (32 * (l & 1)));
-  }
-  v = bv_mask(v, w);
-  const V span = SUBV(a.hi, a.lo);
-  if (row == 0) return a.lo;
-  if (row == 1) return a.hi;
-  V x;
-  bool small = true;
-  for (int l = 2; l < 8; ++l) small = small && span.w[l] == 0u;
-  if (small) {
-    const uint64_t sp = ((uint64_t)span.w[1] << 32) | span.w[0];
-    const uint64_t k = (row == 2) ? 1u : (sp == ~0ull ? mix64(r0 ^ 0x5851F42D4C957F2Dull) : mix64(r0 ^ 0x5851F42D4C957F2Dull) % (sp + 1u));
-    V kk = bv_zero();
-    kk.w[0] = (uint32_t)k;
-    kk.w[1] = (uint32_t)(k >> 32);
-    x = ADDV(a.lo, kk);
-    if (LT(a.hi, x)) x = a.hi;
-  } else {
-    x = v;  // wide interval: a full-width draw
-  }
-  const V y = OR(AND(x, NOT(a.z)), a.o);
-  const V yw = bv_mask(y, w);
-  if (!LT(yw, a.lo) && !LT(a.hi, yw)) return yw;
-  return (small || (!LT(x, a.lo) && !LT(a.hi, x))) ? x : ((row & 1) ? a.hi : a.lo);
+  return fe_sample_domain(a.z, a.o, a.lo, a.hi, w, row, r0);
 }
 }  // namespace
 

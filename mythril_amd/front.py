@@ -31,8 +31,9 @@ _FIELDS = {
     "var_aux": (9, np.uint32, 1), "var_kind": (10, np.uint8, 1), "hint_off": (11, np.uint64, 1),
     "hints": (12, np.uint32, 8), "alias_off": (13, np.uint64, 1), "aliases": (14, np.uint32, 2),
     "flags": (15, np.uint8, 1), "var_key": (16, np.uint64, 1), "gpu_node_off": (17, np.uint64, 1),
+    "var_tid": (18, np.int32, 1),
 }
-_VAR_TABLES = ("var_off", "var_width", "var_full", "var_name", "var_aux", "var_kind", "var_key")
+_VAR_TABLES = ("var_off", "var_width", "var_full", "var_name", "var_aux", "var_kind", "var_key", "var_tid")
 FIXED_POOL_LIMBS = None  # dag._FIXED_LIMBS (set lazily: dag imports the native module too)
 
 
@@ -119,7 +120,7 @@ class Batch:
         N._check(rc, ctx._h)
         return first, wit, ref[:n], times
 
-    def device_candidates(self, ctx, n_cand: int, n_vars: int, seed: int) -> np.ndarray:
+    def device_candidates(self, ctx, n_cand: int, n_vars: int, seed: int, dom=None) -> np.ndarray:
         """Test hook (mgp_fe_candidates): the GPU-generated first-round candidates, returned in
         the host layout [state][cand][var][8] of mgp_make_candidates."""
         global FIXED_POOL_LIMBS
@@ -130,7 +131,9 @@ class Batch:
         n = self.n_states
         dev = np.zeros((n, n_vars, 2, n_cand, 4), np.uint32)
         N._check(N.lib().mgp_fe_candidates(ctx._h, self._h, n_cand, n_vars, seed & (2 ** 64 - 1),
-                                           N._ptr(FIXED_POOL_LIMBS), len(FIXED_POOL_LIMBS), N._ptr(dev)), ctx._h)
+                                           N._ptr(FIXED_POOL_LIMBS), len(FIXED_POOL_LIMBS),
+                                           None if dom is None else N._ptr(np.ascontiguousarray(dom, np.uint32)),
+                                           N._ptr(dev)), ctx._h)
         return np.ascontiguousarray(dev.transpose(0, 3, 1, 2, 4).reshape(n, n_cand, n_vars, 8))
 
     def witness(self, s: int, words: np.ndarray) -> "SlotWitness":
@@ -192,9 +195,10 @@ class Batch:
 class VarTables:
     """Owned copies of a batch's per-slot variable tables."""
 
-    def __init__(self, var_off, var_width, var_full, var_name, var_aux, var_kind, var_key):
+    def __init__(self, var_off, var_width, var_full, var_name, var_aux, var_kind, var_key, var_tid):
         self.var_off, self.var_width, self.var_full = var_off, var_width, var_full
         self.var_name, self.var_aux, self.var_kind, self.var_key = var_name, var_aux, var_kind, var_key
+        self.var_tid = var_tid
 
 
 class SlotWitness(Mapping):

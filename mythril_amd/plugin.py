@@ -103,11 +103,14 @@ class GpuPrefilterPlugin:
                     break
             if not window:
                 break
-            if self._timed_out(vm, create):
-                rest = window if track_gas else None
-                return (final_states + rest) if rest is not None else None
             executed = []
+            stopped = None
             for gs in window:
+                # svm.py:229-244: the timeout is checked before every state; the first state
+                # not executed is returned behind the final states
+                if self._timed_out(vm, create):
+                    stopped = gs
+                    break
                 try:
                     new_states, op_code = vm.execute_state(gs)
                 except NotImplementedError:
@@ -123,6 +126,9 @@ class GpuPrefilterPlugin:
                 elif track_gas:
                     final_states.append(gs)
                 vm.total_states += len(new_states)
+            if stopped is not None:
+                log.debug("Hit timeout, returning.")
+                return final_states + [stopped] if track_gas else None
         return final_states if track_gas else None
 
     @staticmethod

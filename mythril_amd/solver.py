@@ -72,6 +72,9 @@ class SolverStatistics(metaclass=_Singleton):
         self.gpu_retry = 0        # states given a second, larger candidate round
         self.gpu_time = 0.0
         self.gpu_batches = 0
+        self.rechecks = 0         # GPU witnesses re-checked by the fallback's evaluator (z3)
+        self.recheck_rejects = 0  # ... and rejected (the query then went to the fallback)
+        self.not_lowerable = 0    # queries with a construct outside the node set
 
     def __repr__(self):
         return (f"Query count: {self.query_count} \nSolver time: {self.solver_time}\n"
@@ -119,6 +122,8 @@ class Model:
         return None
 
     def eval(self, expression, model_completion: bool = False):
+        if self.raw is not None and hasattr(self.raw, "eval"):  # a z3 model from the fallback
+            return self.raw.eval(getattr(expression, "raw", expression), model_completion=model_completion)
         t = expression.raw if isinstance(expression, Expression) else expression
         if isinstance(t, Term):
             if t.op == 2:  # CONST
@@ -131,11 +136,30 @@ class Model:
 
 # --------------------------------------------------------------- backends
 class Backend:
-    """Fallback solver interface: check(terms, timeout_ms, minimize, maximize) -> (result, Model|None)."""
+    """Fallback solver interface: check(terms, timeout_ms, minimize, maximize) -> (result, Model|None).
+
+    The base class is the null backend of an installation without z3: every query it gets
+    is `unknown`, which each caller maps exactly as the reference maps a z3 timeout
+    (is_possible -> True, get_model -> UnsatError).  It says so once, loudly; install
+    z3 and ``set_backend(mythril_amd.z3_backend.Z3Backend())`` for the real fallback."""
 
     name = "none"
+    _warned = False
 
     def check(self, terms: Sequence[Term], timeout_ms: int, minimize=(), maximize=()) -> Tuple[str, Optional[Model]]:
+        if type(self) is Backend and not Backend._warned:
+            Backend._warned = True
+            import warnings
+
+            warnings.warn("mythril_amd: no fallback solver set; queries the GPU and the host pre-check "
+                          "leave open answer 'unknown' (set_backend(z3_backend.Z3Backend()) where z3 exists)",
+                          RuntimeWarning, stacklevel=3)
+        return unknown, None
+
+    def check_raw(self, raw_constraints: Sequence, lowered: Sequence[Term], timeout_ms: int, minimize=(),
+                  maximize=()) -> Tuple[str, Optional[Model]]:
+        """A query with constraints the pre-filter could not lower (given as the caller's
+        own objects) -- only a backend that understands them (z3) can answer."""
         return unknown, None
 
 
@@ -321,7 +345,7 @@ class Prefilter:
         first, wit, proven, times = B.check(self.ctx, self.n_cand, self.seed + self._calls, parents,
                                             refute=self.refute)
         self.last_times = times
-        for k, name in enumerate(("lower_ms", "upload_launch_ms", "refute_ms", "gpu_wait_ms", "copy_back_ms")):
+        for k, name in enumerate(("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")):
             prof[name] = float(times[k])
         tr = time.perf_counter()
         unsafe = (B.flags & FE_SAT_UNSAFE) != 0
@@ -418,22 +442,57 @@ def enable_gpu(flag: bool = True) -> None:
     _enabled = flag
 
 
+class NotLowerable(Exception):
+    """A constraint outside the pre-filter's node set (z3_lower.Unsupported): the query
+    goes to the fallback solver unchanged."""
+
+
 def _terms(constraints: Iterable) -> List[Term]:
+    """Constraints as pre-filter terms: laser.smt mirror expressions (.raw Term), the
+    reference's own laser.smt wrappers or bare z3 expressions (lowered by
+    mythril_amd.z3_lower), Python bools."""
+    from . import z3_lower
+
     out = []
     for c in constraints:
         if isinstance(c, bool):
             out.append(bconst(c))
         elif isinstance(c, Expression):
             out.append(c.raw)
-        else:
+        elif isinstance(c, Term):
             out.append(c)
+        else:
+            raw = getattr(c, "raw", c)
+            if not z3_lower.is_z3_expr(raw):
+                raise NotLowerable(f"unknown constraint type {type(c)!r}")
+            t = z3_lower.to_terms([raw])
+            if t is None:
+                raise NotLowerable("z3 construct outside the node set")
+            out.extend(t)
     return out
+
+
+def _recheck(terms: Sequence[Term], witness) -> bool:
+    """A GPU witness is trusted unless the fallback backend can re-check it and rejects it
+    (Z3Backend.recheck: z3's evaluator on the original constraints)."""
+    rc = getattr(get_backend(), "recheck", None)
+    if rc is None:
+        return True
+    ok = rc(terms, witness)
+    stats = SolverStatistics()
+    stats.rechecks += ok is not None
+    if ok is False:
+        stats.recheck_rejects += 1
+        return False
+    return True
 
 
 # ------------------------------------------------------------ Solver API
 class BaseSolver:
     def __init__(self):
         self.constraints: List[Term] = []
+        self.raw_constraints: List = []  # constraints the pre-filter cannot lower
+        self.lowerable = True
         self.timeout = 10000
         self._model: Optional[Model] = None
 
@@ -444,7 +503,12 @@ class BaseSolver:
         flat = []
         for c in constraints:
             flat.extend(c if isinstance(c, (list, tuple)) else [c])
-        self.constraints.extend(_terms(flat))
+        try:
+            self.constraints.extend(_terms(flat))
+        except NotLowerable:
+            self.lowerable = False
+            SolverStatistics().not_lowerable += 1
+            self.raw_constraints.extend(flat)
 
     append = add
 
@@ -456,10 +520,10 @@ class Solver(BaseSolver):
     """GPU witness first, then the fallback solver (counted in SolverStatistics.query_count)."""
 
     def check(self, *args) -> str:
-        pf = prefilter()
+        pf = prefilter() if self.lowerable else None
         if pf is not None:
             res, assign = pf.check_states([self.constraints])[0]
-            if res == sat:
+            if res == sat and _recheck(self.constraints, assign):
                 self._model = Model([assign])
                 return sat
             if res == unsat:
@@ -469,6 +533,10 @@ class Solver(BaseSolver):
 
     @stat_smt_query
     def _fallback(self) -> str:
+        if not self.lowerable:
+            r, m = get_backend().check_raw(self.raw_constraints, self.constraints, self.timeout)
+            self._model = m
+            return r
         r, m = get_backend().check(self.constraints, self.timeout)
         self._model = m
         if r == unsat:
@@ -495,19 +563,24 @@ class Optimize(BaseSolver):
         self._max.append(e.raw if isinstance(e, Expression) else e)
 
     def check(self, *args) -> str:
-        pf = prefilter()
+        pf = prefilter() if self.lowerable else None
         if pf is not None:
             res, assign = pf.check_states([self.constraints])[0]
             if res == unsat:  # no model exists, whatever the objectives
                 self._model = None
                 return unsat
-            if res == sat and not self._min and not self._max:
+            if res == sat and not self._min and not self._max and _recheck(self.constraints, assign):
                 self._model = Model([assign])
                 return sat
         return self._fallback()
 
     @stat_smt_query
     def _fallback(self) -> str:
+        if not self.lowerable:
+            r, m = get_backend().check_raw(self.raw_constraints, self.constraints, self.timeout, tuple(self._min),
+                                           tuple(self._max))
+            self._model = m
+            return r
         r, m = get_backend().check(self.constraints, self.timeout, tuple(self._min), tuple(self._max))
         self._model = m
         if r == unsat:
@@ -621,13 +694,23 @@ def batch_is_possible(items: Sequence[Constraints]) -> List[bool]:
     through the reference's single-query path (100 ms fallback check, unknown ->
     possible, constraints.py:42-51).
     """
-    todo = [c for c in items if c._is_possible is None]
+    todo = [c for c in items if getattr(c, "_is_possible", None) is None]
     pf = prefilter()
     results: List[Tuple[str, Optional[Dict[str, int]]]] = [("undecided", None)] * len(todo)
-    if pf is not None and todo:
-        results = pf.check_states([_terms(c) for c in todo], parents=[c.witness for c in todo])
-    for c, (res, assign) in zip(todo, results):
-        if res == sat:
+    lowered: List[Optional[List[Term]]] = []
+    for c in todo:
+        try:
+            lowered.append(_terms(c))
+        except NotLowerable:
+            SolverStatistics().not_lowerable += 1
+            lowered.append(None)
+    idx = [k for k, t in enumerate(lowered) if t is not None]
+    if pf is not None and idx:
+        sub = pf.check_states([lowered[k] for k in idx], parents=[getattr(todo[k], "witness", None) for k in idx])
+        for k, r in zip(idx, sub):
+            results[k] = r
+    for c, t, (res, assign) in zip(todo, lowered, results):
+        if res == sat and _recheck(t, assign):
             c._is_possible = True
             c.witness = assign
             continue

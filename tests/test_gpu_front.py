@@ -31,11 +31,12 @@ def test_device_candidates_equal_host_generator(mgp_ctx):
     states = _contract_batch(96)
     B = F.Batch(states)
     n_vars = B.n_vars() + 2  # padding variables are filled too
-    for n_cand, seed in ((64, 5), (256, 0x4D595448), (37, 11)):
-        dev = B.device_candidates(mgp_ctx, n_cand, n_vars, seed)
+    _, dom = N.refute_domains(*B.packed(), B.var_off)
+    for n_cand, seed, d in ((64, 5, None), (256, 0x4D595448, dom), (37, 11, dom)):
+        dev = B.device_candidates(mgp_ctx, n_cand, n_vars, seed, dom=d)
         host = N.make_candidates(n_cand, n_vars, seed, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off,
                                  B.aliases, B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8),
-                                 var_kind=B.var_kind)
+                                 var_kind=B.var_kind, dom=d)
         bad = np.nonzero((dev != host).any(axis=(1, 2, 3)))[0]
         assert bad.size == 0, f"n_cand={n_cand}: {bad.size} states differ, first {bad[:5]}"
     B.close()
@@ -50,7 +51,8 @@ def test_check_batch_matches_oracle_and_refute(mgp_ctx):
     seed, n_cand = 1234, 256
     first, wit, ref, times = B.check(mgp_ctx, n_cand, seed)
     n_vars = max(1, B.n_vars())
-    cands = B.device_candidates(mgp_ctx, n_cand, n_vars, seed)
+    _, dom = N.refute_domains(*B.packed(), B.var_off)  # the pipeline draws domain rows from these
+    cands = B.device_candidates(mgp_ctx, n_cand, n_vars, seed, dom=dom)
     want = coracle.first_sat(*B.packed(gpu=True), cands)
     _, _, status = N.lower(*B.packed(gpu=True))
     ok = status == 0  # the rest (WalletLibrary shapes past the lowering's budgets) is undecided

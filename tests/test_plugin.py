@@ -81,6 +81,7 @@ class FakeLaser:
         self.cfg = []
         self.create_timeout = None
         self.execution_timeout = None
+        self.timeout_after = None  # stand-in clock: "timed out" once this many states ran
 
     def execute_state(self, gs):
         self.executed.append(gs.tag)
@@ -96,6 +97,9 @@ class FakeLaser:
             a.append(X[0] == BVV(7, 256))
         return [GS(gs.depth + 1, a, gs.tag + "a"), GS(gs.depth + 1, b, gs.tag + "b")], "JUMPI"
 
+    def timed_out(self):
+        return self.timeout_after is not None and len(self.executed) >= self.timeout_after
+
     def manage_cfg(self, op, states):
         self.cfg.append((op, [s.tag for s in states]))
 
@@ -103,6 +107,8 @@ class FakeLaser:
     def exec(self, create=False, track_gas=False):
         final_states = []
         for global_state in self.strategy:
+            if self.timed_out():  # svm.py:229-244
+                return final_states + [global_state] if track_gas else None
             try:
                 new_states, op_code = self.execute_state(global_state)
             except NotImplementedError:
@@ -181,3 +187,21 @@ def test_plugin_prunes_like_reference_gpu(brute, mgp_ctx, window):
     st = SV.SolverStatistics()
     assert brute.calls + st.refuted + st.core_hits == n_infeasible < ref_calls
     assert st.gpu_sat > 0
+
+
+@pytest.mark.parametrize("window", [3, 16])
+@pytest.mark.parametrize("after", [1, 4, 7])
+def test_windowed_exec_timeout_returns_like_reference(brute, monkeypatch, window, after):
+    """svm.py:229-244: on a timeout the loop returns final_states + [the first state not
+    executed]; the windowed loop checks before every state and returns the same list."""
+    monkeypatch.setattr(SV, "prefilter", lambda: None)
+    monkeypatch.setattr(P.GpuPrefilterPlugin, "_timed_out", staticmethod(lambda vm, create: vm.timed_out()))
+    ref = FakeLaser()
+    ref.timeout_after = after
+    ref_final = ref.exec(track_gas=True)
+    vm = FakeLaser()
+    vm.timeout_after = after
+    P.LaserPluginLoader(vm).load(P.GpuPrefilterPlugin(window=window))
+    got = vm.exec(track_gas=True)
+    assert [g.tag for g in got] == [g.tag for g in ref_final]
+    assert vm.executed == ref.executed

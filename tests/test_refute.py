@@ -342,3 +342,33 @@ def test_guided_candidates_status_and_yield_on_synthetic():
     assert not ((f_gd >= 0) & (st == 1)).any()
     # the guided rows find witnesses the same number of uniform rows misses
     assert ((f_gd >= 0) & (f_uni < 0)).sum() > 2 * max(1, ((f_uni >= 0) & (f_gd < 0)).sum())
+
+
+def test_refute_domains_agree_with_refute_and_contain_witnesses():
+    """mgp_refute_domains: the same verdicts as mgp_refute, and every planted witness value
+    of a non-refuted synthetic state lies inside its variable's exported domain (the
+    domains are sound over-approximations, so domain rows never exclude a model)."""
+    from mythril_amd import _native as N
+
+    b = N.synth_generate(0x4D595448, 777, 512, 64, 256)
+    n = 512
+    var_off = np.arange(n + 1, dtype=np.uint64) * b["n_vars"]
+    st, dom = N.refute_domains(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], var_off)
+    assert np.array_equal(st, N.refute(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"]))
+    checked = 0
+    for s in np.nonzero(b["planted"])[0]:
+        assert st[s] != 1
+        for v in range(b["n_vars"]):
+            d = dom[s * b["n_vars"] + v]
+            if not d[32]:
+                continue
+            limb = lambda a: int.from_bytes(np.ascontiguousarray(a).tobytes(), "little")
+            z, o, lo, hi = limb(d[0:8]), limb(d[8:16]), limb(d[16:24]), limb(d[24:32])
+            x = limb(b["plant_words"][s, v])
+            # UF slots hold fresh values that the planted row may not use: check VAR slots only
+            if v >= 4:
+                continue
+            x &= (1 << 256) - 1
+            assert lo <= x <= hi and x & z == 0 and x & o == o, (s, v)
+            checked += 1
+    assert checked > 100

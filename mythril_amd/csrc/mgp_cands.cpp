@@ -5,8 +5,8 @@
 // adds constraints to its parent, svm.py:251-255), then the first harvested hint of
 // every variable, the same row with the x == y aliases applied, then a seeded
 // mixture per variable: 35 % harvested hint, 25 % pool (state constants and their
-// neighbours +-1, LASER's actor addresses and boundary values), 15 % alias of an
-// equal-width variable, 25 % uniform.  Every value is masked to its slot width.
+// neighbours +-1, LASER's actor addresses and boundary values), 15 % alias (an x == y
+// partner, else the next equal-width variable from a random start), 25 % uniform.  Every value is masked to its slot width.
 // A pinned-constant slot (var_kind 2, mgp_front.cpp) holds its hint 0 in every row.
 // With domains (mgp_refute_domains), every other mixture row draws the variables that
 // have a refined abstract value from it (mgp_fe_sample.h).
@@ -114,12 +114,20 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
         srcs.clear();
         for (uint64_t a = 0; a < na; ++a)
           if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V) srcs.push_back(aliases[2 * (a0 + a) + 1]);
-        if (srcs.empty())
-          for (uint64_t u = 0; u < V; ++u)
-            if (u != v && var_width[v0 + u] == var_width[v0 + v]) srcs.push_back((uint32_t)u);
-        if (srcs.empty()) continue;
         const uint64_t k = mix(seed ^ 0x5A5A5A5Aull ^ mix(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
-        memcpy(cell(c, v), cell(c, srcs[k % srcs.size()]), 32);
+        if (!srcs.empty()) {
+          memcpy(cell(c, v), cell(c, srcs[k % srcs.size()]), 32);
+          continue;
+        }
+        // no x == y alias: the next equal-width variable from a random start (O(1) when
+        // widths repeat, instead of collecting all of them: states hold hundreds of slots)
+        for (uint64_t t = 0, st0 = k % V; t < V; ++t) {
+          const uint64_t u = (st0 + t) % V;
+          if (u != v && var_width[v0 + u] == var_width[v0 + v]) {
+            memcpy(cell(c, v), cell(c, u), 32);
+            break;
+          }
+        }
       }
       // domain rows (every other mixture row): variables with a refined abstract value
       // (mgp_refute_domains) are drawn from it, an inside hint half of the time

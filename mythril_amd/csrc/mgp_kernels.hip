@@ -750,27 +750,24 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       uint64_t n_src = 0;
       for (uint64_t a = 0; a < na; ++a)
         if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V) ++n_src;
-      const bool by_alias = n_src > 0;
-      if (!by_alias)
-        for (uint64_t u = 0; u < V; ++u)
-          if (u != v && var_width[v0 + u] == var_width[v0 + v]) ++n_src;
-      if (!n_src) continue;
       const uint64_t k = fe_mix(seed ^ 0x5A5A5A5Aull ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
-      uint64_t want = k % n_src, src = 0;
-      if (by_alias) {
+      if (n_src) {
+        uint64_t want = k % n_src;
         for (uint64_t a = 0; a < na; ++a)
           if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V && want-- == 0) {
-            src = aliases[2 * (a0 + a) + 1];
+            R.copy((uint32_t)v, aliases[2 * (a0 + a) + 1]);
             break;
           }
-      } else {
-        for (uint64_t u = 0; u < V; ++u)
-          if (u != v && var_width[v0 + u] == var_width[v0 + v] && want-- == 0) {
-            src = u;
-            break;
-          }
+        continue;
       }
-      R.copy((uint32_t)v, (uint32_t)src);
+      // the next equal-width variable from a random start (mgp_make_candidates)
+      for (uint64_t t = 0, st0 = k % V; t < V; ++t) {
+        const uint64_t u = (st0 + t) % V;
+        if (u != v && var_width[v0 + u] == var_width[v0 + v]) {
+          R.copy((uint32_t)v, (uint32_t)u);
+          break;
+        }
+      }
     }
     const uint32_t kk = c - (first_row + 2u);  // domain rows: as mgp_make_candidates
     if (dom && (kk & 1u) == 0u)
@@ -917,7 +914,24 @@ extern "C" hipError_t mgp_launch_eval_asm(const void *desc, uint32_t n_states, c
 // for the stream first (the old buffer may still be read by enqueued kernels).  Not
 // stream-ordered allocation (hipMallocAsync / hipFreeAsync): a descriptor buffer must stay
 // mapped until the interpreter launches that read it have finished.
+//
+// MGP_DESC_MODE (fault triage of DESIGN.md §4 "Launch descriptors"; never set in
+// measurements): "exact" = a buffer of exactly n_states x 32 B per launch, freed after a
+// stream synchronise (no floor, no slack: an out-of-bounds descriptor read faults);
+// "async" = hipMallocAsync / hipFreeAsync of exactly that size on the launch stream
+// (the round-1 variant whose lifetime was suspected).  Unset: the grow-only buffer.
+static int desc_mode() {
+  static const int v = [] {
+    const char *e = getenv("MGP_DESC_MODE");
+    if (!e) return 0;
+    return e[0] == 'e' ? 1 : (e[0] == 'a' ? 2 : 0);
+  }();
+  return v;
+}
+
 static hipError_t desc_buffer(hipStream_t st, size_t bytes, void **out) {
+  if (desc_mode() == 1) return hipMalloc(out, bytes);
+  if (desc_mode() == 2) return hipMallocAsync(out, bytes, st);
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> bufs;
   int dev = 0;
@@ -952,6 +966,8 @@ static bool sync_debug() {
 // (mgp_eval_gfx950, default), MGP_ENGINE_HIP = the HIP C++ interpreter above
 // (kept as an independent second implementation; A/B and cross-checks).
 // MGP_ENGINE=hip|asm in the environment sets the initial choice.
+static thread_local void *g_last_desc = nullptr;  // the triage modes' per-launch buffer
+
 static int g_engine = [] {
   const char *e = getenv("MGP_ENGINE");
   return (e && e[0] == 'h') ? MGP_ENGINE_HIP : MGP_ENGINE_ASM;
@@ -978,6 +994,7 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
     void *desc = nullptr;
     err = desc_buffer(st, (size_t)n_states * 32u, &desc);
     if (err != hipSuccess) return err;
+    g_last_desc = desc;
     hipLaunchKernelGGL(mgp_desc_kernel, dim3((n_states + 255) / 256), dim3(256), 0, st, words, offs, n_states,
                        bucketed ? order : nullptr, n_vars, reinterpret_cast<uint4 *>(desc));
     err = hipGetLastError();
@@ -1003,6 +1020,12 @@ hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t
                      n_states, n_chunks, reinterpret_cast<const uint4 *>(cands), n_cand, n_vars,
                      first_sat, reinterpret_cast<uint4 *>(witness));
   err = hipGetLastError();
+  if (g_engine == MGP_ENGINE_ASM && desc_mode() && g_last_desc) {  // triage modes: release the exact buffer
+    const hipError_t fe = desc_mode() == 1 ? hipStreamSynchronize(st) : hipSuccess;
+    if (fe == hipSuccess) (void)(desc_mode() == 1 ? hipFree(g_last_desc) : hipFreeAsync(g_last_desc, st));
+    g_last_desc = nullptr;
+    if (err == hipSuccess) err = fe;
+  }
   if (err == hipSuccess && sync_debug()) {
     err = hipStreamSynchronize(st);
     if (err != hipSuccess) fprintf(stderr, "[mgp] mgp_finalize_kernel failed: %s\n", hipGetErrorString(err));

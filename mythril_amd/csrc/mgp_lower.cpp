@@ -686,6 +686,9 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           if (state[ch[i]] == 0) stack.push_back(ch[i]);
       }
     } else {
+      // the greedy list scheduler rescans the ready list per step (quadratic): not worth it
+      // for very long programs, whose other schedules are kept instead
+      if (n0 > 1536) return unsupported();
       std::vector<uint32_t> uses(n0, 0), pending(n0, 0);
       std::vector<std::vector<uint32_t>> users(n0);
       for (uint32_t t = 0; t < n0; ++t) {

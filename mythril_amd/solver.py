@@ -379,23 +379,36 @@ class Prefilter:
         self.last_profile = prof
         return out
 
-    # escalating witness rounds for the states left open: (candidates per state, decision
-    # rows); each round takes only what the previous one left.  Decisions re-run the domain
-    # analysis per variable, so they are kept few until a state proves hard.
-    RETRY_SCHEDULE = ((64, 2), (256, 8), (1024, 32))
+    # witness rounds for the states the first round and the pre-check leave open: a larger
+    # GPU round (candidates generated on the device, domain rows with a new seed), then --
+    # for at most DECIDE_MAX states -- host decisions, which re-run the domain analysis per
+    # variable and are kept for the few states that need them.
+    RETRY_GPU_CAND = 1024
+    RETRY_SCHEDULE = ((256, 8),)  # (candidates per state, decision rows) of the host rounds
+    DECIDE_MAX = 64
 
     def _retry_round(self, states, retry, n_vars, first, witnesses) -> None:
-        """Fresh candidates for the states the first round and the pre-check left open, in
-        escalating rounds (RETRY_SCHEDULE, capped by retry_cand and by cand_bytes of host
-        candidate memory): every other row drawn from the pre-check's refined domains, the
-        first of those by decisions (mgp_guided_candidates); the rest the usual hint /
-        pool / uniform mixture."""
         from . import dag as D
         from .front import FE_SAT_UNSAFE, Batch
 
         open_ = list(retry)
+        budget = self.cand_bytes // (len(open_) * n_vars * 32)
+        n2 = min(self.RETRY_GPU_CAND, self.retry_cand, budget) // 64 * 64
+        if n2 > self.n_cand:
+            SB = Batch([states[i] for i in open_])
+            f2, w2, _, _ = SB.check(self.ctx, n2, self.seed + 0x9E3779B9 + self._calls)
+            unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
+            left = []
+            for k, i in enumerate(open_):
+                if f2[k] >= 0 and not unsafe[k]:
+                    first[i] = f2[k]
+                    witnesses[i] = SB.witness(k, w2[k])
+                else:
+                    left.append(i)
+            SB.close()
+            open_ = left
         for rnd, (n_cand, n_decide) in enumerate(self.RETRY_SCHEDULE):
-            if not open_:
+            if not open_ or len(open_) > self.DECIDE_MAX:
                 break
             budget = self.cand_bytes // (len(open_) * n_vars * 32)
             n2 = min(n_cand, self.retry_cand, budget) // 64 * 64
@@ -404,7 +417,7 @@ class Prefilter:
             SB = Batch([states[i] for i in open_])
             sv = max(1, SB.n_vars())
             sw, sp, _ = self._N.lower(*SB.packed(gpu=True))
-            seed = self.seed + 0x9E3779B9 * (rnd + 1) + self._calls
+            seed = self.seed + 0x7F4A7C15 * (rnd + 1) + self._calls
             c2 = self._N.make_candidates(n2, sv, seed, SB.var_off, SB.var_width, SB.hint_off, SB.hints,
                                          SB.alias_off, SB.aliases, SB.const_off, SB.consts, D._FIXED_LIMBS,
                                          np.zeros(len(open_), np.uint8), var_kind=SB.var_kind)
@@ -701,8 +714,7 @@ def batch_is_possible(items: Sequence[Constraints]) -> List[bool]:
     for c in todo:
         try:
             lowered.append(_terms(c))
-        except NotLowerable:
-            SolverStatistics().not_lowerable += 1
+        except NotLowerable:  # counted by the fallback Solver.add below
             lowered.append(None)
     idx = [k for k, t in enumerate(lowered) if t is not None]
     if pf is not None and idx:

@@ -507,7 +507,10 @@ class Solver:
                 return unsat
             funcs[name][arg] = val
         self._env, self._funcs = env, funcs
-        ok = all(evaluate(e, env, funcs) for kind, e, _ in rest if kind == "c")
+        try:
+            ok = all(evaluate(e, env, funcs) for kind, e, _ in rest if kind == "c")
+        except NotImplementedError:  # an operator the stand-in does not model
+            return unknown
         return sat if ok else unsat
 
     def model(self):

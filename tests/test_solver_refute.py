@@ -137,11 +137,10 @@ def test_fallback_unsat_feeds_the_cache(fe):
 
 
 class SecondRoundContext(NoWitnessContext):
-    """No witness among the first round's candidates; candidate 0 of a larger round 'satisfies'."""
+    """No witness among the first round's candidates; candidate 0 of the host decision round
+    (host-built candidates) 'satisfies'."""
 
     def eval_batch(self, words, po, cands):
-        if cands.shape[1] <= 256:
-            return super().eval_batch(words, po, cands)
         self.batches += 1
         return np.zeros(len(po) - 1, dtype=np.int32), np.ascontiguousarray(cands[:, 0])
 
@@ -153,8 +152,8 @@ def test_second_candidate_round(fe, monkeypatch):
     assert SV.batch_is_possible(items) == [True, False]
     st = SV.SolverStatistics()
     assert st.gpu_retry == 1 and st.gpu_sat == 1 and st.refuted == 1 and fe.calls == 0
-    # the first round, then the escalating retry rounds (64, 256, 1024 candidates): the
-    # stub only "satisfies" in the 1024-candidate one
-    assert [n for n, _ in SV.Prefilter.RETRY_SCHEDULE] == [64, 256, 1024]
-    assert SV.prefilter().ctx.batches == 4
+    # the first round and the larger device round (check_batch: no witness from the stub),
+    # then the host decision round (eval_batch), which the stub satisfies
+    assert SV.Prefilter.RETRY_GPU_CAND == 1024 and [n for n, _ in SV.Prefilter.RETRY_SCHEDULE] == [256]
+    assert SV.prefilter().ctx.batches == 3
     assert set(items[0].witness) == {"rx", "ry"}

@@ -14,10 +14,10 @@ from mythril_amd import solver as SV  # noqa: E402
 
 
 def main():
-    items = [c[1] for c in corpus.corpus(64) if not c[0].startswith("wallet")]
+    items = [c[1] for c in corpus.corpus(512) if not c[0].startswith("wallet")]
     pf = SV.Prefilter(device=0)
     pf.check_states(items[:4])
-    for n in (1, 2, 16):
+    for n in [int(x) for x in os.environ.get("FE_SIZES", "1,2,16").split(",")]:
         rows = []
         for r in range(20):
             SV.unsat_cores().reset()

@@ -29,6 +29,7 @@ here is a contraction.  No scalar memory writes anywhere (vector stores only).
 from __future__ import annotations
 
 import os
+import re
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
@@ -39,7 +40,13 @@ VA, VB, VC, VT = 8, 16, 24, 32
 RV = 64          # v[64:111]: candidate variables 0..5 of this lane, preloaded at wave start
 PG = 112         # v[112:116]: the current 64-uop page, uop k in lane k (read with v_readlane):
                  #   v112 first-handler address (low 32 bits), v113 op-handler address, v114-116 w1-w3
-PQ = 118         # v[118:125]: the constant pool, constant c in lane c, limb l in v[118+l]
+PQ = 118         # v[118:125]: the constant pool, constant c in lane c (CONST_SMEM = False)
+# A v_readlane costs a wave64 ~8.7 SIMD-cycles of VALU issue at 4 waves/SIMD
+# (profiles/contention_probe.hip, contention_r2.json), so a handler reads only the uop
+# fields it uses, and pool constants come through the scalar cache (one s_load_dwordx8
+# instead of 8 readlanes).  The uop stream itself stays in VGPR lanes: read through the
+# scalar cache, every 4th uop missed it (SQC_DCACHE_MISSES) and the step got slower.
+CONST_SMEM = True
 S_KB, S_KH, S_KM = 24, 32, 40
 
 
@@ -96,16 +103,18 @@ A = Asm()
 
 
 def prefetch_next():
-    """At handler entry: read the next uop (lane s3 of the page): its first-handler address
-    straight into s0 (s1 = high half of the code address, constant), op-handler address and
-    w1-w3 into N = s[20:23].  The addresses were computed lane-parallel when the page was
-    loaded, so dispatch costs one SALU op (the lane counter) besides the moves."""
-    A("v_readlane_b32 s0, v112, s3",
-      "v_readlane_b32 s20, v113, s3",
-      "v_readlane_b32 s21, v114, s3",
-      "v_readlane_b32 s22, v115, s3",
-      "v_readlane_b32 s23, v116, s3",
-      "s_add_u32 s3, s3, 1")
+    """At handler entry: the first-handler address of the next uop (lane s21 + 1 of the
+    page, computed lane-parallel when the page was loaded) straight into s0; s1 is the
+    constant high half of the code address.  s21 = lane of the current uop."""
+    A("s_add_u32 s3, s21, 1",
+      "v_readlane_b32 s0, v112, s3")
+
+
+def read_fields(used):
+    """The uop fields a handler uses (w1-w3 -> s17-s19), read from lane s21 of the page."""
+    for f in (17, 18, 19):
+        if f in used:
+            A(f"v_readlane_b32 s{f}, v{PG + f - 15}, s21")
 
 
 def page_decode():
@@ -121,16 +130,23 @@ def page_decode():
       "s_nop 1")   # VALU write -> v_readlane of the same VGPR
 
 
+def tail_wait():
+    pass
+
+
+def tail_jump():
+    tail()
+
+
 def tail():
-    """Make the prefetched uop current and jump to its first handler."""
-    A("s_mov_b64 s[16:17], s[20:21]",
-      "s_mov_b64 s[18:19], s[22:23]",
+    """Make the prefetched uop current (s21 = its lane) and jump to its first handler."""
+    A("s_mov_b32 s21, s3",
       "s_setpc_b64 s[0:1]")
 
 
 def op_target():
-    """s[12:13] <- address of the op handler (s16 = its low 32 bits, s13 = code high half)."""
-    A("s_mov_b32 s12, s16")
+    """s[12:13] <- address of the op handler of the current uop (s13 = code high half)."""
+    A("v_readlane_b32 s12, v113, s21")
 
 
 def op_dispatch():
@@ -314,18 +330,27 @@ def wait_operands():
 B_STORE, B_MASK, B_SEXT, B_INVERT, B_REGST = 22, 23, 24, 25, 29
 
 
+def load_pool(dst, idx_sreg):
+    """s[dst:dst+7] <- pool entry idx (32 B per entry at s[14:15], or lane idx of PQ)."""
+    if CONST_SMEM:
+        A(f"s_lshl_b32 {idx_sreg}, {idx_sreg}, 5",
+          f"s_load_dwordx8 {sr(dst, 8)}, s[14:15], {idx_sreg}",
+          "s_waitcnt lgkmcnt(0)")
+    else:
+        for i in range(8):
+            A(f"v_readlane_b32 {s(dst + i)}, {v(PQ + i)}, {idx_sreg}")
+
+
 def load_km():
     """s[40:47] <- pool[mask index w2[21:16]] (2^w - 1)."""
     A(f"s_bfe_u32 s48, s18, {(6 << 16) | 16:#x}")
-    for i in range(8):
-        A(f"v_readlane_b32 {s(S_KM + i)}, {v(PQ + i)}, s48")
+    load_pool(S_KM, "s48")
 
 
 def load_kh():
     """s[32:39] <- pool[sign index w3[5:0]] (2^(w-1))."""
     A("s_and_b32 s49, s19, 0x3f")
-    for i in range(8):
-        A(f"v_readlane_b32 {s(S_KH + i)}, {v(PQ + i)}, s49")
+    load_pool(S_KH, "s49")
 
 
 def store_slot():
@@ -357,7 +382,10 @@ def bv_epilogue():
             for i in range(8):
                 A(f"v_and_b32 {v(VA + i)}, {s(S_KM + i)}, {v(VA + i)}")
         if "S" in mode:
+            tail_wait()
             store_slot()
+            tail_jump()
+            return
         if "R" in mode:
             store_reg()
         tail()
@@ -377,8 +405,9 @@ def bv_epilogue():
     def stored():
         lr = A.fresh("regst")
         A(f"s_bitcmp1_b32 s18, {B_REGST}", f"s_cbranch_scc1 {lr}")
+        tail_wait()
         store_slot()
-        tail()
+        tail_jump()
 
         def reg():
             store_reg()
@@ -446,21 +475,50 @@ def fetch_one(kind, dst, which):
           f"s_addc_u32 s{lo + 1}, s7, 0",
           f"global_load_dwordx4 {vr(dst, 4)}, v2, {pr}",
           f"global_load_dwordx4 {vr(dst + 4, 4)}, v3, {pr}")
-    else:  # const: broadcast lane `idx` of the pool registers
+    else:  # const: pool entry `idx` through the scalar cache (make_fetch issues it first)
+        const_issue(which)
+        const_finish(dst, which)
+
+
+def const_issue(which):
+    """Issue the scalar load of a pool-constant operand (A: w1[15:0] -> s[32:39], B:
+    w1[31:16] -> s[24:31]; 32 B per pool entry at s[14:15]); VGPR pool: the readlanes."""
+    sp = "s51" if which == "A" else "s50"
+    ks = S_KB if which == "B" else S_KH
+    A(f"s_and_b32 {sp}, s17, 0xffff" if which == "A" else f"s_lshr_b32 {sp}, s17, 16")
+    if CONST_SMEM:
+        A(f"s_lshl_b32 {sp}, {sp}, 5",
+          f"s_load_dwordx8 {sr(ks, 8)}, s[14:15], {sp}")
+    else:
         for i in range(8):
-            A(f"v_readlane_b32 {s(S_KB + i)}, {v(PQ + i)}, {sp}")
-        for i in range(8):
-            A(f"v_mov_b32 {v(dst + i)}, {s(S_KB + i)}")
+            A(f"v_readlane_b32 {s(ks + i)}, {v(PQ + i)}, {sp}")
+
+
+def const_finish(dst, which):
+    ks = S_KB if which == "B" else S_KH
+    if CONST_SMEM:
+        A("s_waitcnt lgkmcnt(0)")
+    for i in range(8):
+        A(f"v_mov_b32 {v(dst + i)}, {s(ks + i)}")
 
 
 def make_fetch(name):
     _, ka, kb, tgt = name.split("_")
 
     def body():
+        # pool constants first: their scalar loads overlap the other operand's fetch
+        for kind, which in ((kb, "B"), (ka, "A")):
+            if kind == "const":
+                const_issue(which)
         op_target()
-        if kb != "none":
+        if kb not in ("none", "const"):
             fetch_one(kb, VB, "B")
-        fetch_one(ka, VA if tgt == "A" else VC, "A")
+        if ka != "const":
+            fetch_one(ka, VA if tgt == "A" else VC, "A")
+        if kb == "const":
+            const_finish(VB, "B")
+        if ka == "const":
+            const_finish(VA if tgt == "A" else VC, "A")
         op_dispatch()
     return body
 
@@ -483,7 +541,7 @@ def h_page():
       "s_waitcnt vmcnt(0)",
       "s_mov_b32 s3, 0")
     page_decode()
-    prefetch_next()
+    A("v_readlane_b32 s0, v112, s3")
     tail()
 
 
@@ -493,8 +551,8 @@ def diag_stamp():
     page/pool/variables landed - descriptor, first dispatch - loads, RET - first
     dispatch} in shader clocks (32-bit differences)."""
     ln = A.fresh("nodiag")
-    A("v_readlane_b32 s24, v126, 0", "v_readlane_b32 s25, v126, 1",
-      "s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {ln}",
+    A("s_cmp_eq_u32 s20, 0", f"s_cbranch_scc1 {ln}",
+      "v_readlane_b32 s24, v126, 0", "v_readlane_b32 s25, v126, 1",
       "s_memtime s[54:55]",
       "v_readlane_b32 s26, v126, 2", "v_readlane_b32 s27, v126, 7",
       "v_readlane_b32 s28, v126, 8", "v_readlane_b32 s29, v126, 4",
@@ -520,7 +578,59 @@ def h_ret():
       "s_cmp_lt_i32 s52, 0",
       "s_cselect_b32 s53, 0x7fffffff, s53")
     diag_stamp()
-    write_partial_and_end("s53")
+    A("s_mov_b64 exec, 1",
+      "v_mov_b32 v4, s53",
+      "v_mov_b32 v5, 0",
+      "global_store_dword v5, v4, s[58:59]",
+      "s_mov_b64 exec, -1",
+      "s_add_u32 s22, s22, 1",
+      "s_cmp_lt_u32 s22, s23",
+      "s_cbranch_scc1 .Lnext_chunk",
+      "s_endpgm")
+    next_chunk()
+
+
+def next_chunk():
+    """RET of a wave with chunks left: the same program on the next 64 candidates of
+    the state.  Partial entry, first candidate, valid lanes and candidate offsets
+    advance; page 0 is reloaded when the program had more than one page; the
+    variables are preloaded again; Bool slots 0/1 and the f64 constant are restored."""
+    A.label(".Lnext_chunk")
+    A("s_add_u32 s58, s58, 4",
+      "s_addc_u32 s59, s59, 0",
+      "s_add_u32 s60, s60, 64",
+      "v_readlane_b32 s49, v126, 15",
+      "v_readlane_b32 s2, v126, 13",
+      "v_readlane_b32 s4, v126, 11",
+      "v_readlane_b32 s5, v126, 12",
+      "v_readlane_b32 s91, v126, 14",
+      "s_sub_u32 s50, s49, 1",
+      "s_lshl_b32 s51, s49, 4",
+      # VALU-written SGPRs feed VALU operands and a VMEM base below
+      "s_nop 4",
+      "v_add_u32 v5, s60, v0",
+      "v_cmp_gt_u32_e64 s[56:57], s49, v5",
+      "v_min_u32 v5, s50, v5",
+      "v_lshlrev_b32 v2, 4, v5",
+      "v_add_u32 v3, s51, v2",
+      "s_cmp_lt_u32 s2, 64",
+      "s_cbranch_scc1 .Lpage0_kept",
+      "v_min_u32 v4, s2, v0",
+      "v_lshlrev_b32 v4, 4, v4",
+      "global_load_dwordx4 v[112:115], v4, s[4:5]")
+    A.lines.append(var_preload("r").rstrip("\n"))
+    page_decode()
+    A("s_branch .Lrestart")
+    A.label(".Lpage0_kept")
+    A.lines.append(var_preload("k").rstrip("\n"))
+    A.label(".Lrestart")
+    A("s_mov_b64 s[64:65], 0",
+      "s_mov_b64 s[66:67], -1",
+      "s_mov_b32 s62, 0",
+      "s_mov_b32 s63, 0x41f00000",
+      "s_mov_b32 s3, 0",
+      "v_readlane_b32 s0, v112, s3")
+    tail()
 
 
 def bool_binop(name, instr):
@@ -983,24 +1093,19 @@ def knuth_digit(J):
       # top limb(b) <= 7 - J, so its normalised divisor has vn[i] = 0 for i < J: the
       # products and the subtraction only involve vn[J..7] and u[2J..J+8]
       "v_cndmask_b32 v60, 0, v60, vcc")
-    # u[2J..J+8] -= qhat * vn[J..7]: the products are independent (no carry between the
-    # mads); their sum  lo_J | lo_J+1 + hi_J | ... | hi_7  is formed by an add chain
-    # (carry in s[48:49]) interleaved with the borrow chain of the subtraction (VCC)
-    pairs = [(8, 9), (10, 11), (12, 13), (14, 15), (56, 57), (58, 59), (62, 63), (4, 5)]
-    for i in range(J, 8):
-        lo, hi = pairs[i]
-        A(f"v_mad_u64_u32 v[{lo}:{hi}], s[50:51], v60, {vn(i)}, 0")
-    A(f"v_sub_co_u32 {u(2 * J)}, vcc, {u(2 * J)}, v{pairs[J][0]}")
+    # u[2J..J+8] -= qhat * vn[J..7]: one multiply-accumulate chain, the high half of each
+    # product (+ carry) entering the next as its 64-bit addend (qhat * vn[i] + c < 2^64),
+    # interleaved with the borrow chain of the subtraction (VCC).  Per limb: mad + mov +
+    # subb, against mad + add + subb with independent products (carry ops issue at half
+    # the rate of a mov)
+    A("v_mov_b32 v63, 0",
+      f"v_mad_u64_u32 v[4:5], s[50:51], v60, {vn(J)}, 0",
+      f"v_sub_co_u32 {u(2 * J)}, vcc, {u(2 * J)}, v4")
     for i in range(J + 1, 8):
-        lo, hi_prev = pairs[i][0], pairs[i - 1][1]
-        if i == J + 1:
-            A(f"v_add_co_u32 v{lo}, s[48:49], v{lo}, v{hi_prev}")
-        else:
-            A(f"v_addc_co_u32 v{lo}, s[48:49], v{lo}, v{hi_prev}, s[48:49]")
-        A(f"v_subb_co_u32 {u(J + i)}, vcc, {u(J + i)}, v{lo}, vcc")
-    if J < 7:
-        A(f"v_addc_co_u32 v{pairs[7][1]}, s[48:49], 0, v{pairs[7][1]}, s[48:49]")
-    A(f"v_subb_co_u32 {u(J + 8)}, vcc, {u(J + 8)}, v{pairs[7][1]}, vcc")
+        A("v_mov_b32 v62, v5",
+          f"v_mad_u64_u32 v[4:5], s[50:51], v60, {vn(i)}, v[62:63]",
+          f"v_subb_co_u32 {u(J + i)}, vcc, {u(J + i)}, v4, vcc")
+    A(f"v_subb_co_u32 {u(J + 8)}, vcc, {u(J + 8)}, v5, vcc")
     lno = A.fresh("noaddback")
     A("s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lno}",
       "s_mov_b64 s[50:51], vcc",
@@ -1168,6 +1273,19 @@ for _x in U.XS_OPS:
 
 # ---------------------------------------------------------------- kernel
 
+POOL_LOAD = """\
+  // VGPR pool (CONST_SMEM = False): v[118:125], lane c = constant min(c, n_pool-1)
+  s_and_b32 s93, s91, 0xff
+  s_cmp_eq_u32 s93, 0
+  s_cbranch_scc1 .Lno_pool
+  s_sub_u32 s92, s93, 1
+  v_min_u32 v4, s92, v0
+  v_lshlrev_b32 v4, 5, v4
+  global_load_dwordx4 v[118:121], v4, s[14:15]
+  global_load_dwordx4 v[122:125], v4, s[14:15] offset:16
+.Lno_pool:
+"""
+
 PROLOGUE = """\
   s_memtime s[96:97]
   s_load_dwordx8 s[64:71], s[0:1], 0x0
@@ -1175,6 +1293,12 @@ PROLOGUE = """\
   s_waitcnt lgkmcnt(0)
   // s[64:65] desc  s[66:67] cands  s[68:69] partial  s[70:71] diag
   // s72 n_states  s73 n_cand  s74 n_vars  s75 n_chunks  s76 n_slots  s77 position base  s78 grid x
+  // s79 chunks per wave: this wave runs chunks [s3, s80) of its state one after the other
+  // (RET restarts the program on the next chunk), s3 = workgroup y * chunks per wave
+  s_max_u32 s79, s79, 1
+  s_mul_i32 s3, s3, s79
+  s_add_u32 s80, s3, s79
+  s_min_u32 s80, s80, s75
   // diagnostic stamps (diag != 0): v126 lanes 0-1 diag, 2-3 entry time, 4-5 first
   // dispatch time, 6 item index; written at RET as 16 B per (state, chunk) item
   v_writelane_b32 v126, s70, 0
@@ -1224,6 +1348,17 @@ PROLOGUE = """\
   s_lshl_b32 s82, s82, 2
   s_add_u32 s58, s68, s82
   s_addc_u32 s59, s69, s83
+  // loop state for RET: s22 chunk, s23 end chunk, s20 diag != 0; the SGPRs above s63
+  // become Bool slots, so v126 keeps lanes 11-12 page 0, 13 n_uops, 14 n_pool |
+  // variable mask << 8, 15 n_cand
+  s_mov_b32 s22, s3
+  s_mov_b32 s23, s80
+  s_or_b32 s20, s70, s71
+  v_writelane_b32 v126, s88, 11
+  v_writelane_b32 v126, s89, 12
+  v_writelane_b32 v126, s87, 13
+  v_writelane_b32 v126, s91, 14
+  v_writelane_b32 v126, s73, 15
   s_cmp_lg_u32 s85, 0
   s_cbranch_scc1 .Lundec
   s_cmp_gt_u32 s86, s76
@@ -1250,21 +1385,11 @@ PROLOGUE = """\
   s_lshl_b32 s92, s73, 4
   v_add_u32 v3, s92, v2
   v_lshlrev_b32 v1, 4, v0
-  // uop page 0 -> v[112:115] (lane k = uop min(k, n_uops): lanes past the end hold the INVALID pad); pool -> v[116:123] (lane c = constant
-  // min(c, n_pool-1)); both issued before the variable loads so that vmcnt(12) covers them
+  // uop page 0 -> v[112:115] (lane k = uop min(k, n_uops): lanes past the end hold the INVALID pad)
   v_min_u32 v4, s2, v0
   v_lshlrev_b32 v4, 4, v4
   global_load_dwordx4 v[112:115], v4, s[4:5]
-  s_and_b32 s93, s91, 0xff
-  s_cmp_eq_u32 s93, 0
-  s_cbranch_scc1 .Lno_pool
-  s_sub_u32 s92, s93, 1
-  v_min_u32 v4, s92, v0
-  v_lshlrev_b32 v4, 5, v4
-  global_load_dwordx4 v[118:121], v4, s[14:15]
-  global_load_dwordx4 v[122:125], v4, s[14:15] offset:16
-.Lno_pool:
-  // preload variables 0..min(n_vars, 6)-1 of this lane's candidate into v[64:111]
+{POOL_LOAD}  // preload variables 0..min(n_vars, 6)-1 of this lane's candidate into v[64:111]
   // s[10:11] = kernel entry address: uops hold handler offsets / 4 from it.  Handler
   // addresses are formed as 32-bit sums: a code object crossing a 4 GiB boundary (never
   // seen; would need the loader to place it there) makes every wave report undecided.
@@ -1295,9 +1420,12 @@ PROLOGUE = """\
   s_mov_b32 s3, 0
 {FIRST_DISPATCH}
 .Lundec:
-  s_mov_b64 exec, 1
+  // -2 into the partial entries of chunks [s3, s80): lane i writes chunk s3 + i
+  s_sub_u32 s48, s80, s3
+  v_cmp_gt_u32_e64 vcc, s48, v0
+  s_mov_b64 exec, vcc
   v_mov_b32 v4, -2
-  v_mov_b32 v5, 0
+  v_lshlrev_b32 v5, 2, v0
   global_store_dword v5, v4, s[58:59]
 .Lexit:
   s_endpgm
@@ -1306,7 +1434,7 @@ PROLOGUE = """\
 KARGS = [("desc", 8, "global_buffer"), ("cands", 8, "global_buffer"), ("partial", 8, "global_buffer"),
          ("diag", 8, "global_buffer"), ("n_states", 4, "by_value"), ("n_cand", 4, "by_value"),
          ("n_vars", 4, "by_value"), ("n_chunks", 4, "by_value"), ("n_slots", 4, "by_value"),
-         ("pos_base", 4, "by_value"), ("grid_x", 4, "by_value"), ("pad", 4, "by_value")]
+         ("pos_base", 4, "by_value"), ("grid_x", 4, "by_value"), ("chunks_per_wave", 4, "by_value")]
 
 
 def metadata():
@@ -1336,18 +1464,18 @@ def metadata():
     return "\n".join(out), ksize
 
 
-def var_preload() -> str:
+def var_preload(tag: str = "") -> str:
     """Variables v < REG_VARS the program reads (mask bit 8+v of s91) -> v[64+8v : 72+8v]
     (index clamped to n_vars-1); the others are never read and not loaded."""
     out = []
     for i in range(U.REG_VARS):
         r = RV + 8 * i
-        out += [f"  s_bitcmp1_b32 s91, {8 + i}", f"  s_cbranch_scc0 .Lnovar{i}",
+        out += [f"  s_bitcmp1_b32 s91, {8 + i}", f"  s_cbranch_scc0 .Lnovar{tag}{i}",
                 f"  s_min_u32 s94, s9, {i}", "  s_mul_i32 s94, s94, s8",
                 "  s_add_u32 s92, s6, s94", "  s_addc_u32 s93, s7, 0",
                 f"  global_load_dwordx4 v[{r}:{r + 3}], v2, s[92:93]",
                 f"  global_load_dwordx4 v[{r + 4}:{r + 7}], v3, s[92:93]",
-                f".Lnovar{i}:"]
+                f".Lnovar{tag}{i}:"]
     # page, pool and variables all present before the first uop (the variable loads were
     # issued right behind the page and pool, so this adds little over waiting for those)
     out.append("  s_waitcnt vmcnt(0)")
@@ -1361,22 +1489,42 @@ def generate() -> str:
     first = Asm()
     global_A = A
     globals()["A"] = first
-    prefetch_next()
+    A("v_readlane_b32 s0, v112, s3")
     tail()
     globals()["A"] = global_A
     dec = Asm()
     globals()["A"] = dec
     page_decode()
     globals()["A"] = global_A
+    pool = "" if CONST_SMEM else POOL_LOAD
     A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
-                   .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n"))
+                   .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n").replace("{POOL_LOAD}", pool))
     no_prefetch = set(U.FETCH) | set(U.XS_OPS) | {"INVALID", "RET", "PAGE"}
+    wait = "  s_waitcnt vmcnt(0) lgkmcnt(0)"
     for name in U.HANDLERS:
+        # two entries per handler: mgp_h_<name> (reached from a fetch handler, whose
+        # operand loads are still in flight) and mgp_hd_<name> (dispatched directly: its
+        # operands are resident, so the leading operand wait is skipped).  An op handler
+        # that waits for operands is laid out [wait][prefetch][body]: the direct entry
+        # sits right behind the wait, 4 bytes in.
+        body = Asm()
+        body.n = A.n
+        globals()["A"] = body
+        HBODY[name]()
+        body.flush_ool()
+        globals()["A"] = global_A
+        A.n = body.n
+        lines = body.lines
+        used = {f for f in (17, 18, 19) if any(re.search(rf"\bs{f}\b|\bs\[{f}:|\bs\[\d+:{f}\]", l) for l in lines)}
         A.lines.append(f".p2align 2\nmgp_h_{name}:")
+        if name not in no_prefetch and lines and lines[0] == wait:
+            A.lines.append(wait)
+            lines = lines[1:]
+        A.lines.append(f"mgp_hd_{name}:")
+        read_fields(used)
         if name not in no_prefetch:
             prefetch_next()
-        HBODY[name]()
-        A.flush_ool()
+        A.lines.extend(lines)
     md, ksize = metadata()
     head = [
         '.amdgcn_target "amdgcn-amd-amdhsa--gfx950"',

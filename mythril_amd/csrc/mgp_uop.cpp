@@ -36,6 +36,12 @@ extern "C" const uint16_t *mgp_uop_handler_offsets(uint32_t *n) {
   return kUopHandlerOffset;
 }
 
+// the direct-dispatch entries (a uop whose first handler is its op handler)
+extern "C" const uint16_t *mgp_uop_direct_offsets(uint32_t *n) {
+  if (n) *n = MGP_U_N_HANDLERS;
+  return kUopDirectOffset;
+}
+
 namespace {
 
 struct Opnd {
@@ -236,8 +242,12 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
   }
 }
 
+// w0 = first-handler offset | op-handler offset << 16.  A uop dispatched straight to its
+// op handler enters past the handler's operand wait (its operands are resident); the op
+// field keeps the fetch-path entry that a fetch handler jumps to.
 inline uint32_t w0_of(uint32_t first, uint32_t op) {
-  return (uint32_t)kUopHandlerOffset[first] | ((uint32_t)kUopHandlerOffset[op] << 16);
+  const uint32_t f = first == op ? kUopDirectOffset[first] : kUopHandlerOffset[first];
+  return f | ((uint32_t)kUopHandlerOffset[op] << 16);
 }
 
 }  // namespace

@@ -27,13 +27,17 @@ def _names():
 
         from mythril_amd import _native as N
 
-        fn = N.lib().mgp_uop_handler_offsets
-        fn.restype = ctypes.POINTER(ctypes.c_uint16)
-        fn.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
-        n = ctypes.c_uint32()
-        p = fn(ctypes.byref(n))
-        assert n.value == len(U.HANDLERS)
-        _NAME_BY_OFF = {p[i]: U.HANDLERS[i] for i in range(n.value)}
+        _NAME_BY_OFF = {}
+        # the direct-dispatch entries first: where a handler has one entry, both tables
+        # hold the same offset
+        for sym in ("mgp_uop_direct_offsets", "mgp_uop_handler_offsets"):
+            fn = getattr(N.lib(), sym)
+            fn.restype = ctypes.POINTER(ctypes.c_uint16)
+            fn.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+            n = ctypes.c_uint32()
+            p = fn(ctypes.byref(n))
+            assert n.value == len(U.HANDLERS)
+            _NAME_BY_OFF.update({p[i]: U.HANDLERS[i] for i in range(n.value)})
     return _NAME_BY_OFF
 
 

@@ -38,6 +38,23 @@ def classify(op):
     return None
 
 
+# SIMD-cycles of VALU issue per wave64 instruction at 4 waves/SIMD (profiles/valu_mix_r1.json,
+# profiles/contention_r2.json); f64 ops and cndmask are assumed, not measured
+_QUARTER = ("v_alignbit", "v_alignbyte", "v_perm", "v_lshl_or", "v_lshl_add", "v_mad_u64", "v_fma_f64",
+            "v_cvt_f64", "v_cvt_u32_f64", "v_rcp_f64")
+_CARRY = ("v_add_co", "v_addc_co", "v_sub_co", "v_subb_co", "v_subrev_co", "v_subbrev_co")
+
+
+def valu_cost(op):
+    if op.startswith(("v_readlane", "v_writelane", "v_readfirstlane")):
+        return 8.7
+    if op.startswith(_CARRY):
+        return 4.5
+    if op.startswith(_QUARTER):
+        return 4.0
+    return 2.0 if op.startswith("v_") else 0.0
+
+
 def handler_paths(lines):
     """handler name -> Counter of instruction classes along the fall-through path."""
     out = {}
@@ -58,6 +75,7 @@ def handler_paths(lines):
         c = classify(op)
         if c:
             out[cur][c] += 1
+        out[cur]["COST"] += valu_cost(op)
         if op.startswith("s_setpc") or op == "s_endpgm":
             done = True
     return out
@@ -90,6 +108,11 @@ def main():
     print("per wave (fall-through paths; DIV digits not counted):")
     for k in ("VALU", "SALU", "BR", "WAIT", "LDS", "VMEM", "SMEM"):
         print(f"  {k:5s} {tot[k] / n:8.1f}")
+    print(f"  VALU SIMD-cycle estimate {tot['COST'] / n:8.1f}")
+    print("\ntop handlers by estimated VALU SIMD-cycles per wave:")
+    cc = {h: per[h] * paths[h]["COST"] / n for h in per}
+    for h, c in sorted(cc.items(), key=lambda x: -x[1])[:30]:
+        print(f"  {h:18s} x{per[h] / n:5.2f}  cost {paths[h]['COST']:6.1f} -> {c:6.1f}")
     print("\ntop handlers by SALU+VALU contribution per wave:")
     contrib = {h: per[h] * (paths[h]["SALU"] + paths[h]["VALU"] + paths[h]["BR"]) / n for h in per}
     for h, c in sorted(contrib.items(), key=lambda x: -x[1])[:25]:

@@ -105,8 +105,8 @@ def test_assembles_for_gfx950(asm, tmp_path):
 
 
 def test_address_registers_initialised_before_first_load(asm):
-    # v1 (LDS lane base), v2/v3 (candidate offsets) and the table base s[10:11] must be
-    # written in the prologue before the first instruction that uses them
+    # v1 (LDS lane base), v2/v3 (candidate offsets), the code base s[10:11], the uop page
+    # and the pool base must be written in the prologue before the first instruction using them
     _, lines = asm
     body = [l.strip() for l in lines]
 
@@ -122,6 +122,9 @@ def test_address_registers_initialised_before_first_load(asm):
     assert first(lambda l: l.startswith("s_getpc_b64 s[10:11]")) < first(lambda l: l.startswith("s_setpc_b64"))
     assert first(lambda l: l.startswith("global_load_dwordx4 v[112:115]")) < \
         first(lambda l: l.startswith("v_readlane_b32 s0, v112"))
+    # pool constants are read with scalar loads from s[14:15]
+    assert first(lambda l: l.startswith("s_add_u32 s14,")) < \
+        first(lambda l: l.startswith("s_load") and "s[14:15]" in l)
 
 
 @pytest.mark.skipif(not os.path.exists(f"{LLVM}/ld.lld"), reason="ROCm LLVM linker not installed")

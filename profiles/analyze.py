@@ -99,6 +99,18 @@ def main(d):
                 # issued VALU wave-instructions per step (x 64 lanes = lane-ops, overhead included)
                 traffic[k]["valu_wave_insts_per_step"] = c["SQ_INSTS_VALU"] / n_steps
                 traffic[k]["salu_insts_per_step"] = c.get("SQ_INSTS_SALU", 0) / n_steps
+                # against the INT32 VALU spec peak (256 CU x 4 SIMD-32 x 2.4 GHz = 78.6 Tops/s),
+                # over the traced run's average eval launch time
+                try:
+                    bl = json.load(open(os.path.join(d, "bench_trace.json")))
+                    launch_s = bl["roofline"]["launch_ms"] * 1e-3
+                    issued = c["SQ_INSTS_VALU"] / n_steps * 64 / launch_s / 1e12
+                    der["issued VALU lane-ops/s (Tops/s, over the launch time)"] = issued
+                    der["issued VALU / 78.64 Tops/s spec peak"] = issued / 78.6432
+                    der["nominal ops/s (Tops/s, bench roofline.achieved)"] = bl["roofline"]["achieved"]
+                    der["nominal / 78.64 Tops/s spec peak"] = bl["roofline"]["achieved"] / 78.6432
+                except (OSError, ValueError, KeyError):
+                    pass
         if k == "mgp_keccak64_kernel" and c.get("SQ_WAVES"):
             # one preimage per lane: per-hash figures are per-wave counts / 64
             ncalls = sum(1 for _ in kcalls)

@@ -121,8 +121,8 @@ typedef struct mgp_node {
 
 /* --------------------------------------------------------------- bytecode
  * Per state, 16-byte aligned (offsets in u32 words, multiple of 4):
- *   header  : w0 = n_ins, w1 = n_consts, w2 = n_slots (BV slots used),
- *             w3 = status (MGP_ST_*)
+ *   header  : w0 = n_ins, w1 = n_consts, w2 = n_slots (BV slots used, spill
+ *             slots included), w3 = status (MGP_ST_*) | max_var << 8
  *   n_ins   x 4 words  instructions
  *   n_consts x 8 words constants (little-endian u32 limbs)
  *
@@ -140,6 +140,27 @@ typedef struct mgp_node {
 #define MGP_HDR_WORDS 4
 #define MGP_INS_WORDS 4
 #define MGP_INS_STORE 0x1u
+
+/* BV slots 0..MGP_LDS_SLOTS-1 live in per-lane LDS.  A slot s >= MGP_LDS_SLOTS is a
+ * SPILL slot: it lives in the evaluating lane's own candidate row, at variable index
+ * MGP_SPILL_BASE(max_var) + (s - MGP_LDS_SLOTS), where max_var = header w3 >> 8 (one
+ * past the highest variable the program reads), so a spill never overlaps a variable
+ * the program reads.  Every spill slot is written before it is read.  A program with
+ * spill slots therefore needs a candidate block of at least MGP_PROG_VARS(header)
+ * variables per state; the rows past the state's own variables are scratch (the
+ * gfx950 interpreter keeps up to 31 slots in LDS and may use one more spill row, which
+ * MGP_PROG_VARS includes).  Slot numbers of a spilling program are ordered by access
+ * count, so the most used values stay in LDS. */
+#define MGP_LDS_SLOTS 32u
+#define MGP_MAX_SLOTS 255u
+#define MGP_SPILL_BASE(max_var) ((max_var) > 8u ? (max_var) : 8u)
+#define MGP_PROG_VARS(h)                                                                        \
+  ((h)[2] >= MGP_LDS_SLOTS ? MGP_SPILL_BASE((h)[3] >> 8) + (h)[2] - MGP_LDS_SLOTS + 1u : ((h)[3] >> 8))
+/* live Bool values a program keeps in bits; past it the lowering demotes the Bool
+ * with the farthest next use to a 1-bit BV value (ITE(b, 1, 0), re-tested by EQ at
+ * each reader), which can spill like any BV value (= the gfx950 interpreter's 17
+ * allocatable Bool registers) */
+#define MGP_BOOL_LIVE 17u
 
 /* BV operand (16 bits): kind in bits 15:14, index in 13:0 */
 #define MGP_K_SLOT 0u

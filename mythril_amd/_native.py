@@ -221,6 +221,20 @@ def lower(
     raise MgpError(MGP_E_CAPACITY, "lowering capacity")
 
 
+LDS_SLOTS = 32  # include/mgp_ir.h MGP_LDS_SLOTS
+
+
+def prog_rows(words: np.ndarray, prog_offsets: np.ndarray) -> np.ndarray:
+    """Candidate rows each lowered program needs (include/mgp_ir.h MGP_PROG_VARS): the
+    variables it reads, plus the spill rows of a program with more live values than
+    LDS slots.  A device candidate block for mgp_eval_batch_dev needs the maximum."""
+    h = np.asarray(words, dtype=np.uint64)[np.asarray(prog_offsets[:-1], dtype=np.int64)[:, None] + np.arange(4)]
+    max_var = h[:, 3] >> np.uint64(8)
+    spill = np.maximum(max_var, 8) + h[:, 2] - LDS_SLOTS + 1
+    ok = (h[:, 3] & np.uint64(0xFF)) == 0
+    return np.where(ok & (h[:, 2] >= LDS_SLOTS), spill, np.where(ok, max_var, 0)).astype(np.int64)
+
+
 def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hint_off, hints, alias_off, aliases,
                     const_off, consts, fixed_pool, has_parent, var_kind=None, dom=None) -> np.ndarray:
     """mgp_make_candidates over flattened per-state tables -> uint32 [n_states, n_cand, n_vars, 8]."""

@@ -545,6 +545,21 @@ def h_page():
     tail()
 
 
+# ---- spill rows
+@handler("VST")
+def h_vst():
+    """vA -> this lane's candidate row w2[15:0]: a BV slot past the LDS slots (spill,
+    include/mgp_ir.h).  Later uops read the row back as a VAR operand; a wave's vector
+    memory accesses to one address stay in order, so the load sees this store."""
+    A("s_and_b32 s48, s18, 0xffff",
+      "s_mul_i32 s48, s48, s8",
+      "s_add_u32 s52, s6, s48",
+      "s_addc_u32 s53, s7, 0",
+      f"global_store_dwordx4 v2, {vr(VA, 4)}, s[52:53]",
+      f"global_store_dwordx4 v3, {vr(VA + 4, 4)}, s[52:53]")
+    tail()
+
+
 # ---- Bool ops
 def diag_stamp():
     """Diagnostic build-in (kernarg diag != 0): diag[item] = {descriptor landed - entry,

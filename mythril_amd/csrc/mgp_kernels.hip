@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <type_traits>
@@ -63,9 +64,10 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nblk) {
 struct EvalCtx {
   const uint4 *lds;
   const uint32_t *cpool;
-  const uint4 *cbase;  // this state's candidates, device layout
+  uint4 *cbase;  // this state's candidates, device layout (spill rows are written)
   uint32_t n_cand;
   uint32_t lane;
+  uint32_t spill0;  // candidate row of spill slot MGP_LDS_SLOTS (include/mgp_ir.h)
 };
 
 __device__ __forceinline__ U256 u256_from(uint4 lo, uint4 hi) {
@@ -80,6 +82,10 @@ template <int CPL>
 __device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx &e, int c, uint32_t cand) {
   uint32_t kind = o >> 14, idx = o & 0x3FFFu;
   if (kind == MGP_K_ACC) return acc;
+  if (kind == MGP_K_SLOT && idx >= MGP_LDS_SLOTS) {  // spill slot: this lane's candidate row
+    const uint4 *p = e.cbase + (size_t)(e.spill0 + idx - MGP_LDS_SLOTS) * 2u * e.n_cand + cand;
+    return u256_from(p[0], p[e.n_cand]);
+  }
   if (kind == MGP_K_SLOT) {
     const uint4 *p = e.lds + ((size_t)idx * CPL + c) * 2u * MGP_WAVE + e.lane;
     return u256_from(p[0], p[MGP_WAVE]);
@@ -96,7 +102,14 @@ __device__ __forceinline__ U256 fetch(uint32_t o, const U256 &acc, const EvalCtx
 }
 
 template <int CPL>
-__device__ __forceinline__ void store_slot(uint4 *lds, uint32_t slot, int c, uint32_t lane, const U256 &v) {
+__device__ __forceinline__ void store_slot(uint4 *lds, uint32_t slot, int c, uint32_t lane, const U256 &v,
+                                           const EvalCtx &e, uint32_t cand) {
+  if (slot >= MGP_LDS_SLOTS) {  // spill slot: a later fetch by this lane reads the same address
+    uint4 *p = e.cbase + (size_t)(e.spill0 + slot - MGP_LDS_SLOTS) * 2u * e.n_cand + cand;
+    p[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+    p[e.n_cand] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+    return;
+  }
   uint4 *p = lds + ((size_t)slot * CPL + c) * 2u * MGP_WAVE + lane;
   p[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
   p[MGP_WAVE] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
@@ -196,7 +209,7 @@ __device__ __forceinline__ U256 eval_unary(uint32_t op, const U256 &a, uint32_t 
 template <int CPL>
 __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
     const uint32_t *__restrict__ words, const uint64_t *__restrict__ offs,
-    uint32_t n_states, const uint4 *__restrict__ cands, uint32_t n_cand,
+    uint32_t n_states, uint4 *__restrict__ cands, uint32_t n_cand,
     uint32_t n_vars, uint32_t n_chunks, uint32_t n_slots,
     int32_t *__restrict__ partial, const uint32_t *__restrict__ order, uint32_t order_base) {
   extern __shared__ uint4 mgp_lds[];
@@ -211,7 +224,10 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
   const uint32_t n_ins = uni(prog[0]);
   const uint32_t h_slots = uni(prog[2]);
   const uint32_t h_stat = uni(prog[3]);
-  if ((h_stat & 0xFFu) != MGP_ST_OK || h_slots > n_slots || (h_stat >> 8) > n_vars) {
+  // spill slots live in candidate rows, not LDS: a spilling program needs MGP_LDS_SLOTS
+  // slots of LDS and MGP_PROG_VARS rows per candidate
+  const uint32_t hw[4] = {n_ins, uni(prog[1]), h_slots, h_stat};
+  if ((h_stat & 0xFFu) != MGP_ST_OK || min(h_slots, MGP_LDS_SLOTS) > n_slots || MGP_PROG_VARS(hw) > n_vars) {
     if (lane == 0) partial[(size_t)state * n_chunks + chunk] = MGP_PARTIAL_UNDEC;
     return;
   }
@@ -222,6 +238,7 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
   e.cbase = cands + (size_t)state * n_vars * 2u * n_cand;
   e.n_cand = n_cand;
   e.lane = lane;
+  e.spill0 = MGP_SPILL_BASE(h_stat >> 8);
 
   uint32_t cand[CPL];
   bool valid[CPL];
@@ -304,7 +321,7 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
       }
       if (width < 256u) r = bv_mask(r, width);
       acc[c] = r;
-      if (flags & MGP_INS_STORE) store_slot<CPL>(mgp_lds, dst, c, lane, r);
+      if (flags & MGP_INS_STORE) store_slot<CPL>(mgp_lds, dst, c, lane, r, e, cand[c]);
     });
   }
 
@@ -847,12 +864,14 @@ static hipError_t launch_eval_cpl(const uint32_t *words, const uint64_t *offs, u
   for (uint32_t bkt = 0; bkt < nb; ++bkt) {
     const uint32_t lo = bucketed ? bucket_bounds[bkt] : 0u;
     const uint32_t hi = bucketed ? bucket_bounds[bkt + 1] : n_states;
-    const uint32_t sl = bucketed ? bucket_slots[bkt] : n_slots;
+    // spill slots (>= MGP_LDS_SLOTS) take no LDS
+    const uint32_t sl = std::min<uint32_t>(bucketed ? bucket_slots[bkt] : n_slots, MGP_LDS_SLOTS);
     if (hi <= lo) continue;
     const uint64_t nblk = (uint64_t)(hi - lo) * n_chunks;
     const size_t lds = (size_t)(sl ? sl : 1u) * CPL * 2u * MGP_WAVE * sizeof(uint4);
     hipLaunchKernelGGL(mgp_eval_kernel<CPL>, dim3((uint32_t)nblk), dim3(MGP_WAVE), lds, st, words, offs, n_states,
-                       reinterpret_cast<const uint4 *>(cands), n_cand, n_vars, n_chunks, sl, partial,
+                       reinterpret_cast<uint4 *>(const_cast<uint32_t *>(cands)), n_cand, n_vars, n_chunks, sl,
+                       partial,
                        bucketed ? order : nullptr, lo);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
@@ -886,13 +905,13 @@ __global__ void mgp_desc_kernel(const uint32_t *__restrict__ words, const uint64
   const uint4 h = make_uint4(w[0], w[1], w[2], w[3]);
   uint32_t undec = 1u, n_uops = 0u, pool_rel = 0u, npm = 0u;
   uint64_t page = 0u;
-  if ((h.w & 0xFFu) == MGP_ST_OK && (h.w >> 8) <= n_vars) {
+  if ((h.w & 0xFFu) == MGP_ST_OK && MGP_PROG_VARS(w) <= n_vars) {
     const uint32_t v1 = 4u + 4u * h.x + 8u * h.y;
     const uint32_t *u = w + ((v1 + 3u) & ~3u) + 4u;
     const uint4 uh = make_uint4(u[0], u[1], u[2], u[3]);
     n_uops = uh.x;
     npm = uh.w;
-    undec = (uh.y == 0u && (npm & 0xFFu) <= 64u && n_uops > 0u) ? 0u : 1u;
+    undec = (uh.y == 0u && n_uops > 0u) ? 0u : 1u;
     page = reinterpret_cast<uint64_t>(u + 4);
     pool_rel = uh.z - 16u;
   }

@@ -747,6 +747,128 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     }
   }
 
+  // ------------------------------------------------ Bool pressure: demotion
+  // At most MGP_BOOL_LIVE Bool values are live at once (the gfx950 interpreter's Bool
+  // registers).  While the schedule needs more, the live Bool whose next read is
+  // farthest becomes a 1-bit BV value: D = ITE(b, 1, 0) right after its definition and
+  // EQ(D, 1) right before each reader.  BV values can spill, Bools cannot.
+  {
+    auto const_ref = [&](uint32_t v) {
+      ConstKey k;
+      memset(k.w, 0, sizeof(k.w));
+      k.w[0] = v;
+      Ref r;
+      r.k = R_CONST;
+      for (uint32_t i = 0; i < S.pool.size(); ++i)
+        if (S.pool[i] == k) {
+          r.idx = i;
+          return r;
+        }
+      r.idx = (uint32_t)S.pool.size();
+      S.pool.push_back(k);
+      return r;
+    };
+    // the Bool operand positions of an instruction (ITE: the condition only)
+    auto bool_refs = [](VIns &I, Ref *out[3]) -> int {
+      if (op_takes_bools(I.op)) {
+        out[0] = &I.a, out[1] = &I.b, out[2] = &I.c;
+        return 3;
+      }
+      if (I.op == MGP_OP_ITE) {
+        out[0] = &I.a;
+        return 1;
+      }
+      return 0;
+    };
+    for (int round = 0;; ++round) {
+      const uint32_t n0 = (uint32_t)S.ins.size();
+      std::vector<int64_t> lu(n0, -1);
+      std::vector<std::vector<uint32_t>> readers(n0);
+      for (uint32_t t = 0; t < n0; ++t) {
+        Ref *br[3];
+        const int k = bool_refs(S.ins[t], br);
+        for (int i = 0; i < k; ++i)
+          if (br[i]->k == R_INS) {
+            lu[br[i]->idx] = std::max<int64_t>(lu[br[i]->idx], t);
+            if (readers[br[i]->idx].empty() || readers[br[i]->idx].back() != t) readers[br[i]->idx].push_back(t);
+          }
+      }
+      if (root.k == R_INS) lu[root.idx] = std::max<int64_t>(lu[root.idx], n0);
+      // dry run of the Bool bit allocation below
+      std::vector<std::vector<uint32_t>> expire_at(n0 + 1);
+      for (uint32_t t = 0; t < n0; ++t)
+        if (S.ins[t].is_bool && lu[t] > (int64_t)t && lu[t] <= (int64_t)n0) expire_at[lu[t]].push_back(t);
+      std::vector<uint32_t> cur;
+      int64_t fail_at = -1;
+      for (uint32_t t = 0; t < n0 && fail_at < 0; ++t) {
+        for (uint32_t v : expire_at[t]) cur.erase(std::find(cur.begin(), cur.end(), v));
+        if (S.ins[t].is_bool && lu[t] > (int64_t)t) {
+          if (cur.size() >= MGP_BOOL_LIVE) fail_at = t;
+          else cur.push_back(t);
+        }
+      }
+      if (fail_at < 0) break;
+      if (round >= 1024) return unsupported();
+      // victim: the live Bool read farthest in the future (the root counts as n0)
+      uint32_t victim = cur[0];
+      int64_t best = -1;
+      for (uint32_t v : cur) {
+        int64_t nx = (int64_t)n0;
+        for (uint32_t r : readers[v])
+          if ((int64_t)r >= fail_at) {
+            nx = r;
+            break;
+          }
+        if (nx > best) best = nx, victim = v;
+      }
+      const Ref one = const_ref(1u), zero = const_ref(0u);
+      std::vector<VIns> re;
+      re.reserve(n0 + 2 + readers[victim].size());
+      std::vector<uint32_t> remap(n0, 0);
+      Ref dref;
+      for (uint32_t t = 0; t < n0; ++t) {
+        VIns I = S.ins[t];
+        for (Ref *r : {&I.a, &I.b, &I.c})
+          if (r->k == R_INS) r->idx = remap[r->idx];
+        if (t > victim) {
+          Ref *br[3];
+          const int k = bool_refs(S.ins[t], br);
+          bool reads = false;
+          for (int i = 0; i < k; ++i) reads |= br[i]->k == R_INS && br[i]->idx == victim;
+          if (reads) {
+            re.push_back(VIns{MGP_OP_EQ, 1, true, dref, one, Ref(), 0});
+            Ref e;
+            e.k = R_INS;
+            e.idx = (uint32_t)re.size() - 1;
+            Ref *nr[3];
+            const int kk = bool_refs(I, nr);
+            for (int i = 0; i < kk; ++i)
+              if (nr[i]->k == R_INS && nr[i]->idx == remap[victim]) *nr[i] = e;
+          }
+        }
+        remap[t] = (uint32_t)re.size();
+        re.push_back(I);
+        if (t == victim) {
+          Ref b;
+          b.k = R_INS;
+          b.idx = remap[t];
+          re.push_back(VIns{MGP_OP_ITE, 1, false, b, one, zero, 0});
+          dref.k = R_INS;
+          dref.idx = (uint32_t)re.size() - 1;
+        }
+      }
+      if (root.k == R_INS) {
+        if (root.idx == victim) {
+          re.push_back(VIns{MGP_OP_EQ, 1, true, dref, one, Ref(), 0});
+          root.idx = (uint32_t)re.size() - 1;
+        } else {
+          root.idx = remap[root.idx];
+        }
+      }
+      S.ins.swap(re);
+    }
+  }
+
   // ---------------------------------------------------------- liveness
   const uint32_t n = (uint32_t)S.ins.size();
   std::vector<int64_t> last_use(n, -1);       // last instruction reading the value
@@ -778,11 +900,17 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   if (root.k == R_INS) last_use[root.idx] = std::max<int64_t>(last_use[root.idx], n);
 
   // ---------------------------------------------------------- allocation
-  const uint32_t slot_cap = std::min<uint32_t>(max_slots ? max_slots : 32u, 255u);
+  // LDS slots first (max_slots < MGP_LDS_SLOTS is a test knob that spills earlier), then
+  // spill slots MGP_LDS_SLOTS.. (include/mgp_ir.h), up to MGP_MAX_SLOTS in all
+  const uint32_t slot_cap = std::min<uint32_t>(max_slots ? max_slots : MGP_LDS_SLOTS, MGP_LDS_SLOTS);
   std::vector<int32_t> loc(n, -1);
-  std::vector<uint32_t> free_slots, free_bools;
+  std::vector<uint32_t> free_slots, free_bools, free_spill;
+  uint32_t next_spill = MGP_LDS_SLOTS;
   for (int32_t s = (int32_t)slot_cap - 1; s >= 0; --s) free_slots.push_back((uint32_t)s);
-  for (int32_t b = MGP_BOOL_ALLOC - 1; b >= 0; --b) free_bools.push_back((uint32_t)b);
+  for (int32_t b = MGP_BOOL_LIVE - 1; b >= 0; --b) free_bools.push_back((uint32_t)b);
+  // fields naming a BV slot, for the access-count renumbering of spilling programs:
+  // (word index, bit shift) of an operand (14-bit index) or of a STORE destination
+  std::vector<std::pair<uint32_t, uint32_t>> slot_fields;
   std::vector<std::vector<uint32_t>> expire(n + 1);
   for (uint32_t t = 0; t < n; ++t)
     if (last_use[t] >= 0 && last_use[t] <= (int64_t)n) expire[last_use[t]].push_back(t);
@@ -808,23 +936,31 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     return MGP_BOOL_FALSE;
   };
 
+  auto in_slot = [&](const Ref &r, uint32_t t) { return r.k == R_INS && prev_bv[t] != (int64_t)r.idx; };
   uint32_t n_emit = 0;
   for (uint32_t t = 0; t < n; ++t) {
     const VIns &I = S.ins[t];
     uint32_t oa, ob = 0, oc = 0;
+    const uint32_t base = (uint32_t)out.size();
     if (op_takes_bools(I.op)) {
       oa = bool_opnd(I.a); ob = bool_opnd(I.b); oc = bool_opnd(I.c);
     } else if (I.op == MGP_OP_ITE) {
       oa = bool_opnd(I.a); ob = bv_opnd(I.b, t); oc = bv_opnd(I.c, t);
+      if (in_slot(I.b, t)) slot_fields.push_back({base + 1, 16});
+      if (in_slot(I.c, t)) slot_fields.push_back({base + 2, 0});
     } else {
       oa = bv_opnd(I.a, t);
       ob = I.b.k != R_NONE ? bv_opnd(I.b, t) : 0u;
       oc = I.c.k != R_NONE ? bv_opnd(I.c, t) : 0u;
+      if (in_slot(I.a, t)) slot_fields.push_back({base + 1, 0});
+      if (I.b.k != R_NONE && in_slot(I.b, t)) slot_fields.push_back({base + 1, 16});
+      if (I.c.k != R_NONE && in_slot(I.c, t)) slot_fields.push_back({base + 2, 0});
     }
     // operands read first: free values whose last use is this instruction
     for (uint32_t v : expire[t]) {
       if (loc[v] < 0) continue;
       if (S.ins[v].is_bool) free_bools.push_back((uint32_t)loc[v]);
+      else if ((uint32_t)loc[v] >= MGP_LDS_SLOTS) free_spill.push_back((uint32_t)loc[v]);
       else free_slots.push_back((uint32_t)loc[v]);
     }
     uint32_t dst = 0, flags = 0;
@@ -839,12 +975,20 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         return unsupported();  // unreachable after DCE
       }
     } else if (live && needs_slot[t]) {
-      if (free_slots.empty()) return unsupported();
-      dst = free_slots.back();
-      free_slots.pop_back();
+      if (!free_slots.empty()) {
+        dst = free_slots.back();
+        free_slots.pop_back();
+      } else if (!free_spill.empty()) {
+        dst = free_spill.back();
+        free_spill.pop_back();
+      } else {
+        if (next_spill >= MGP_MAX_SLOTS) return unsupported();
+        dst = next_spill++;
+      }
       loc[t] = (int32_t)dst;
       slots_used = std::max(slots_used, dst + 1);
       flags = MGP_INS_STORE;
+      slot_fields.push_back({base, 16});
     }
     const uint32_t width_field = (uint32_t)(I.width ? I.width - 1 : 0) & 0xFFu;
     out.push_back((uint32_t)I.op | (width_field << 8) | (dst << 16) | (flags << 24));
@@ -859,6 +1003,24 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   out.push_back(0u);
   out.push_back(0u);
   ++n_emit;
+
+  // a spilling program: slot numbers by access count (reads + stores), most used first,
+  // so that the LDS slots (and the gfx950 interpreter's register slots) hold the hot values
+  if (slots_used > MGP_LDS_SLOTS && slot_cap == MGP_LDS_SLOTS) {
+    auto field = [&](const std::pair<uint32_t, uint32_t> &f) -> uint32_t {
+      return f.first % 4u == 0u ? (out[f.first] >> 16) & 0xFFu : (out[f.first] >> f.second) & 0x3FFFu;
+    };
+    std::vector<uint32_t> cnt(slots_used, 0), by(slots_used), rank(slots_used);
+    for (const auto &f : slot_fields) cnt[field(f)]++;
+    for (uint32_t s = 0; s < slots_used; ++s) by[s] = s;
+    std::stable_sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return cnt[x] > cnt[y]; });
+    for (uint32_t r = 0; r < slots_used; ++r) rank[by[r]] = r;
+    for (const auto &f : slot_fields) {
+      const uint32_t nw = rank[field(f)];
+      if (f.first % 4u == 0u) out[f.first] = (out[f.first] & ~(0xFFu << 16)) | (nw << 16);
+      else out[f.first] = (out[f.first] & ~(0x3FFFu << f.second)) | (nw << f.second);
+    }
+  }
 
   out[0] = n_emit;
   out[1] = (uint32_t)S.pool.size();
@@ -984,7 +1146,7 @@ extern "C" int mgp_plan_buckets(const uint32_t *prog_words, const uint64_t *prog
   const bool asm_engine = mgp_set_eval_engine(0) == MGP_ENGINE_ASM;
   for (uint32_t s = 0; s < n_states; ++s) {
     const uint32_t *w = prog_words + prog_offsets[s];
-    uint32_t v = w[2];
+    uint32_t v = std::min<uint32_t>(w[2], MGP_LDS_SLOTS);  // spill slots take no LDS
     if (asm_engine && (w[3] & 0xFFu) == MGP_ST_OK) {
       const uint32_t v1 = 4u + 4u * w[0] + 8u * w[1];
       const uint32_t *u = w + ((v1 + 3u) & ~3u) + 4u;

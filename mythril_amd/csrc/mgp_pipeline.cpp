@@ -140,6 +140,11 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   if (nb < 0) return mgp_ctx_fail(ctx, MGP_E_ARG, "bucket planning failed");
   uint32_t max_slots = 0;
   for (int b = 0; b < nb; ++b) max_slots = std::max(max_slots, bslots[b]);
+  // candidate rows per state: the variables, plus the spill rows of programs with more
+  // live values than LDS slots (include/mgp_ir.h); only the variables come back
+  const uint32_t user_vars = n_vars;
+  for (uint32_t s = 0; s < n_states; ++s)
+    if (status[s] == MGP_ST_OK) n_vars = std::max<uint32_t>(n_vars, MGP_PROG_VARS(words.data() + offs[s]));
   // parent-witness rows: for every state whose parent witness is given, the parent's
   // value of each of its variable slots (matched by slot key = name, kind, aux)
   std::vector<int32_t> pidx(n_states, -1);
@@ -254,8 +259,8 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
     e = hipMemcpy(w.data(), D.p[B_WIT], w.size() * 4u, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
     for (uint32_t s = 0; s < n_states; ++s)
-      if (out_first[s] >= 0) memcpy(out_witness + (size_t)s * n_vars * 8u, w.data() + (size_t)s * n_vars * 8u,
-                                    (size_t)n_vars * 32u);
+      if (out_first[s] >= 0) memcpy(out_witness + (size_t)s * user_vars * 8u, w.data() + (size_t)s * n_vars * 8u,
+                                    (size_t)user_vars * 32u);
   }
   for (uint32_t s = 0; s < n_states; ++s)
     if (status[s] != MGP_ST_OK && out_first[s] >= 0) out_first[s] = MGP_UNDECIDED;  // never expected

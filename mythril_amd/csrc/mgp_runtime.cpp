@@ -86,8 +86,9 @@ int hip_fail(mgp_ctx *ctx, hipError_t e, const char *where) {
 // never make the kernel read outside its LDS slots, constant pool or
 // candidate rows.  Returns the max slot count over the batch or -1.
 int64_t validate_programs(const uint32_t *w, const uint64_t *offs, uint32_t n_states, uint32_t n_vars,
-                          std::string *why) {
+                          std::string *why, uint32_t *rows_needed) {
   uint32_t max_slots = 0;
+  *rows_needed = n_vars;
   const uint64_t total = offs[n_states];
   for (uint32_t s = 0; s < n_states; ++s) {
     const uint64_t o = offs[s], e = offs[s + 1];
@@ -136,6 +137,7 @@ int64_t validate_programs(const uint32_t *w, const uint64_t *offs, uint32_t n_st
       return -1;
     }
     max_slots = std::max(max_slots, n_sl);
+    *rows_needed = std::max<uint32_t>(*rows_needed, MGP_PROG_VARS(w + o));  // spill rows past the variables
   }
   return (int64_t)max_slots;
 }
@@ -209,9 +211,22 @@ int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words, const uint64_t *pro
   if (!prog_words || !prog_offsets || !cand_words || !out_first_sat || n_cand == 0 || n_vars == 0)
     return fail(ctx, MGP_E_ARG, "NULL buffer or zero n_cand/n_vars");
   std::string why;
-  const int64_t slots = validate_programs(prog_words, prog_offsets, n_states, n_vars, &why);
+  uint32_t rows = n_vars;
+  const int64_t slots = validate_programs(prog_words, prog_offsets, n_states, n_vars, &why, &rows);
   if (slots < 0) return fail(ctx, MGP_E_ARG, why);
   MGP_HIP(ctx, hipSetDevice(ctx->device));
+  // programs with spill slots (include/mgp_ir.h) use candidate rows past the caller's
+  // n_vars as scratch: the device block gets `rows` rows per candidate, the extra ones
+  // left for the program to write
+  std::vector<uint32_t> padded;
+  const uint32_t user_vars = n_vars;
+  if (rows > n_vars) {
+    padded.assign((size_t)n_states * n_cand * rows * 8u, 0u);
+    for (size_t sc = 0; sc < (size_t)n_states * n_cand; ++sc)
+      memcpy(padded.data() + sc * rows * 8u, cand_words + sc * n_vars * 8u, (size_t)n_vars * 32u);
+    cand_words = padded.data();
+    n_vars = rows;
+  }
   const uint64_t total_words = prog_offsets[n_states];
   const size_t cand_bytes = (size_t)n_states * n_cand * n_vars * 32u;
   const uint32_t n_chunks = (n_cand + 63u) / 64u;
@@ -250,7 +265,7 @@ int mgp_eval_batch(mgp_ctx *ctx, const uint32_t *prog_words, const uint64_t *pro
     MGP_HIP(ctx, hipStreamSynchronize(st));
     for (uint32_t s = 0; s < n_states; ++s)
       if (out_first_sat[s] >= 0)
-        memcpy(out_witness + (size_t)s * n_vars * 8u, w.data() + (size_t)s * n_vars * 8u, n_vars * 32u);
+        memcpy(out_witness + (size_t)s * user_vars * 8u, w.data() + (size_t)s * n_vars * 8u, user_vars * 32u);
   }
   return MGP_OK;
 }

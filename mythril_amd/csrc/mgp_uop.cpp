@@ -22,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <vector>
 
@@ -62,17 +63,20 @@ inline uint32_t fetch_id(int ka, int kb, bool to_c) {
 struct Translator {
   const uint32_t *v1;
   uint32_t n_ins, n_c;
-  std::vector<uint32_t> pool;        // 8 words per constant
+  std::vector<uint32_t> v1pool;      // the v1 constants, 8 words each (by v1 index)
+  std::vector<uint32_t> ms;          // mask / sign constants: pool entries 0.. (6-bit index fields)
+  uint32_t ms_base = 0;              // pool index of v1 constant 0 (pass 2: the mask/sign count)
   uint32_t var_mask = 0;             // register variables the program reads (preloaded)
-  // register slots: BV slots idx >= n_lds live in register-bank position reg_pos[idx - n_lds]
-  uint32_t n_lds = 0xFFFFFFFFu;
-  uint8_t reg_pos[MGP_U_REG_VARS] = {0};
+  // BV slot map (pass 2): v1 slot -> LDS slot, register-bank position or spill row (KVAR)
+  std::vector<Opnd> slot_map;
+  uint32_t n_lds = 0;                // LDS slots the program uses
   std::map<uint32_t, uint32_t> mask_c, sign_c;  // width -> pool index
   bool bad = false;
 
-  uint32_t add_const(const uint32_t w[8]) {
-    const uint32_t idx = (uint32_t)(pool.size() / 8);
-    pool.insert(pool.end(), w, w + 8);
+  uint32_t add_ms(const uint32_t w[8]) {
+    const uint32_t idx = (uint32_t)(ms.size() / 8);
+    if (idx >= MGP_U_MAX_MS) bad = true;
+    ms.insert(ms.end(), w, w + 8);
     return idx;
   }
   uint32_t mask_off(uint32_t width) {
@@ -83,33 +87,32 @@ struct Translator {
         const int lo = 32 * l;
         w[l] = (int)width >= lo + 32 ? 0xFFFFFFFFu : ((int)width <= lo ? 0u : ((1u << (width - lo)) - 1u));
       }
-      it = mask_c.emplace(width, add_const(w)).first;
+      it = mask_c.emplace(width, add_ms(w)).first;
     }
-    return pool_byte(it->second);
+    return it->second;
   }
   uint32_t sign_off(uint32_t width) {
     auto it = sign_c.find(width);
     if (it == sign_c.end()) {
       uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       w[(width - 1) >> 5] = 1u << ((width - 1) & 31);
-      it = sign_c.emplace(width, add_const(w)).first;
+      it = sign_c.emplace(width, add_ms(w)).first;
     }
-    return pool_byte(it->second);
+    return it->second;
   }
-  // constants are addressed by pool index (the kernel keeps constant c in lane c)
-  uint32_t pool_byte(uint32_t idx) {
-    if (idx >= MGP_U_MAX_POOL) bad = true;
-    return idx;
+  // pool index of v1 constant idx (the kernel reads entry idx with one scalar load)
+  uint32_t pool_idx(uint32_t idx) {
+    if (idx + ms_base >= MGP_U_MAX_POOL) bad = true;
+    return idx + ms_base;
   }
   Opnd bv(uint32_t o) {
     const uint32_t kind = o >> 14, idx = o & 0x3FFFu;
     switch (kind) {
       case MGP_K_ACC: return {KACC, 0};
       case MGP_K_SLOT:
-        if (idx >= n_lds) return {KRVAR, (uint32_t)reg_pos[idx - n_lds] * 8u};
-        if (idx >= MGP_U_MAX_LDS_SLOTS) bad = true;
-        return {KSLOT, idx * MGP_U_SLOT_BYTES};
-      case MGP_K_CONST: return {KCONST, pool_byte(idx)};
+        if (idx < slot_map.size()) return slot_map[idx];
+        return {KSLOT, 0};  // pass 1: only the variable mask and the mask/sign set matter
+      case MGP_K_CONST: return {KCONST, pool_idx(idx)};
       default:
         if (idx < MGP_U_REG_VARS) {
           var_mask |= 1u << idx;
@@ -125,14 +128,44 @@ struct Translator {
     if (s >= MGP_U_BOOL_SLOTS) bad = true;
     return s * 2;
   }
-  // value of a v1 constant operand (pool index), low limb + "any high bits"
+  // value of a v1 constant operand (v1 pool index), low limb + "any high bits"
   void const_value(uint32_t o, uint32_t *lo, bool *big) {
     const uint32_t idx = o & 0x3FFFu;
-    const uint32_t *c = &pool[(size_t)idx * 8];
+    const uint32_t *c = &v1pool[(size_t)idx * 8];
     *lo = c[0];
     bool hi = false;
     for (int l = 1; l < 8; ++l) hi |= c[l] != 0;
     *big = hi || c[0] >= 256u;
+  }
+  // pass 2: where each v1 BV slot lives.  A program within MGP_LDS_SLOTS keeps its highest
+  // slots in the register-bank positions no variable uses (register slots) and the rest in
+  // LDS; a spilling program (slots numbered by access count, mgp_lower) gives the register
+  // positions to its lowest slots, then LDS, then spill rows MGP_SPILL_BASE(max_var) + j.
+  void map_slots(uint32_t n_slots, uint32_t max_var) {
+    uint32_t free_pos[MGP_U_REG_VARS], n_free = 0;
+    for (uint32_t p = 0; p < MGP_U_REG_VARS; ++p)
+      if (!(var_mask & (1u << p))) free_pos[n_free++] = p;
+    const uint32_t k = n_free < n_slots ? n_free : n_slots;
+    const uint32_t spill0 = MGP_SPILL_BASE(max_var);
+    slot_map.assign(n_slots, Opnd{KSLOT, 0});
+    uint32_t n_spill = 0;
+    n_lds = 0;
+    auto lds_or_spill = [&](uint32_t s, uint32_t l) {
+      if (l < MGP_U_MAX_LDS_SLOTS) {
+        slot_map[s] = {KSLOT, l * MGP_U_SLOT_BYTES};
+        n_lds = std::max(n_lds, l + 1);
+      } else {
+        slot_map[s] = {KVAR, spill0 + n_spill++};
+      }
+    };
+    if (n_slots <= MGP_LDS_SLOTS) {
+      const uint32_t nl = n_slots - k;
+      for (uint32_t s = 0; s < nl; ++s) lds_or_spill(s, s);
+      for (uint32_t s = nl; s < n_slots; ++s) slot_map[s] = {KRVAR, free_pos[s - nl] * 8u};
+    } else {
+      for (uint32_t s = 0; s < k; ++s) slot_map[s] = {KRVAR, free_pos[s] * 8u};
+      for (uint32_t s = k; s < n_slots; ++s) lds_or_spill(s, s - k);
+    }
   }
 };
 
@@ -263,7 +296,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   T.n_c = v1[1];
   const bool v1_ok = (v1[3] & 0xFFu) == MGP_ST_OK;
   const uint32_t *ins = v1 + MGP_HDR_WORDS;
-  if (v1_ok) T.pool.assign(ins + (size_t)T.n_ins * MGP_INS_WORDS, ins + (size_t)T.n_ins * MGP_INS_WORDS + (size_t)T.n_c * 8);
+  if (v1_ok) T.v1pool.assign(ins + (size_t)T.n_ins * MGP_INS_WORDS, ins + (size_t)T.n_ins * MGP_INS_WORDS + (size_t)T.n_c * 8);
   std::vector<uint32_t> uops;
   auto emit = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
     uops.push_back(w0); uops.push_back(w1); uops.push_back(w2); uops.push_back(w3);
@@ -431,13 +464,20 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         flags |= MGP_UF_MASK;
         w2 |= T.mask_off(width) << 16;
       }
-      if (store && dst >= T.n_lds) {
-        flags |= MGP_UF_STORE | MGP_UF_REGST;
-        w2 |= (uint32_t)T.reg_pos[dst - T.n_lds] * 8u;
-      } else if (store) {
-        if (dst >= MGP_U_MAX_LDS_SLOTS) { T.bad = true; break; }
-        flags |= MGP_UF_STORE;
-        w2 |= dst * MGP_U_SLOT_BYTES;
+      // the slot the result is stored to: a register slot, an LDS slot, or a spill row
+      // (the op keeps its result in vA; a VST uop behind it writes the row)
+      int32_t vst_row = -1;
+      if (store) {
+        const Opnd d = T.bv(MGP_OPND(MGP_K_SLOT, dst));
+        if (d.kind == KRVAR) {
+          flags |= MGP_UF_STORE | MGP_UF_REGST;
+          w2 |= d.param;
+        } else if (d.kind == KVAR) {
+          vst_row = (int32_t)d.param;
+        } else {
+          flags |= MGP_UF_STORE;
+          w2 |= d.param;
+        }
       }
       opid = epi_variant(opid, (flags & MGP_UF_STORE) != 0, (flags & MGP_UF_MASK) != 0,
                          (flags & MGP_UF_REGST) != 0);
@@ -452,41 +492,33 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         if (xs >= 0) opid = first = (uint32_t)xs;
       }
       emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
+      if (vst_row >= 0) emit(w0_of(MGP_U_VST, MGP_U_VST), 0u, (uint32_t)vst_row, 0u);
     }
   };
-  // pass 1 finds the register variables the program reads; pass 2 maps the state's
-  // highest BV slots onto the register-bank positions no variable uses (register slots:
-  // fewer LDS slots per wave -> more resident waves)
+  // pass 1 finds the register variables the program reads and the mask / sign constants;
+  // pass 2 places the BV slots (map_slots) and puts the v1 pool behind the mask / sign
+  // entries (their index fields are 6 bits, the operand fields 16)
   translate();
   const uint32_t n_slots = v1_ok ? v1[2] : 0u;
-  uint32_t n_lds = n_slots;
   if (v1_ok && !T.bad) {
-    uint32_t free_pos[MGP_U_REG_VARS], n_free = 0;
-    for (uint32_t p = 0; p < MGP_U_REG_VARS; ++p)
-      if (!(T.var_mask & (1u << p))) free_pos[n_free++] = (uint32_t)p;
-    const uint32_t k = n_free < n_slots ? n_free : n_slots;
-    n_lds = n_slots - k;
-    for (uint32_t j = 0; j < k; ++j) T.reg_pos[j] = (uint8_t)free_pos[j];
-    T.n_lds = n_lds;
+    T.map_slots(n_slots, v1[3] >> 8);
+    T.ms_base = (uint32_t)(T.ms.size() / 8);
+    const size_t n_ms = T.ms.size();
     uops.clear();
     translate();
+    if (T.ms.size() != n_ms) T.bad = true;  // pass 2 found a constant pass 1 did not
   }
+  const size_t n_pool = (T.ms.size() + T.v1pool.size()) / 8;
   static const bool why = getenv("MGP_LOWER_WHY") != nullptr;
-  if (why && (!v1_ok || T.bad || uops.empty() || T.pool.size() / 8 > MGP_U_MAX_POOL))
+  if (why && (!v1_ok || T.bad || uops.empty() || n_pool > MGP_U_MAX_POOL))
     fprintf(stderr, "[mgp_uop] not runnable: v1_ok %d bad %d uops %zu pool %zu\n", (int)v1_ok, (int)T.bad,
-            uops.size(), T.pool.size() / 8);
-  if (!v1_ok || T.bad || uops.empty()) {
+            uops.size(), n_pool);
+  if (!v1_ok || T.bad || uops.empty() || n_pool > MGP_U_MAX_POOL) {
     out[base + 0] = 0;
     out[base + 1] = 1;  // not runnable: the kernel reports MGP_UNDECIDED
     out[base + 2] = MGP_U_HDR_WORDS * 4u;
     for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);
     return v1_ok ? 1 : 0;
-  }
-  if (T.pool.size() / 8 > MGP_U_MAX_POOL) {
-    out[base + 1] = 1;
-    out[base + 2] = MGP_U_HDR_WORDS * 4u;
-    for (int k = 0; k < MGP_U_UOP_WORDS; ++k) out.push_back(0u);
-    return 1;
   }
   // pages of 64 uops: the last uop of every full page is PAGE (load the next page)
   const uint32_t n_real = (uint32_t)(uops.size() / MGP_U_UOP_WORDS);
@@ -505,7 +537,8 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   out[base + 0] = n_uops;
   out[base + 1] = 0;
   out[base + 2] = (uint32_t)((MGP_U_HDR_WORDS + (n_uops + 1) * MGP_U_UOP_WORDS) * 4u);
-  out[base + 3] = (uint32_t)(T.pool.size() / 8) | (T.var_mask << 8) | (n_lds << 16);
-  out.insert(out.end(), T.pool.begin(), T.pool.end());
+  out[base + 3] = (uint32_t)n_pool | (T.var_mask << 8) | (T.n_lds << 16);
+  out.insert(out.end(), T.ms.begin(), T.ms.end());
+  out.insert(out.end(), T.v1pool.begin(), T.v1pool.end());
   return 0;
 }

@@ -15,9 +15,9 @@ at word offset align4(4 + 4*n_ins + 8*n_consts) + 4 from the program start):
            (the kernel holds one page in 4 VGPRs, uop k in lane k, and reads
            the current uop with v_readlane; PAGE loads the next page), then one
            all-zero uop
-  pool     n_pool <= 64 constants, 8 little-endian u32 limbs each (the v1 pool
-           followed by the width masks 2^w-1 and sign constants 2^(w-1) the uops
-           use); constant c lives in lane c of 8 VGPRs (limb l in the l-th)
+  pool     n_pool <= 255 constants, 8 little-endian u32 limbs each: the width masks
+           2^w-1 and sign constants 2^(w-1) the uops use first (their index fields
+           are 6 bits), then the v1 pool; handlers read an entry with one scalar load
 
 uop words:
   w0 [15:0]  entry offset / 4 (from the kernel entry) of the FIRST handler: a fetch
@@ -25,7 +25,8 @@ uop words:
      [31:16] entry offset / 4 of the op handler (fetch handlers jump to it)
              (offsets come from the assembled kernel's symbol table, gen_offsets.py)
   w1 [15:0] operand A parameter, [31:16] operand B parameter
-            SLOT: LDS byte offset (slot*2048), VAR: variable index, RVAR:
+            SLOT: LDS byte offset (slot*2048), VAR: variable index (a spilled
+            BV slot is the VAR row the state's VST uops write, mgp_ir.h), RVAR:
             8 x register-bank position p (v[64+8p]: a preloaded variable, or a
             register slot),
             CONST: pool index; Bool operands: bool slot * 2
@@ -40,6 +41,7 @@ uop words:
      [29] REGST   the STORE goes to register-bank position w2[15:0]/8 (v[64+8p]),
                   not to LDS: the translator maps a state's highest BV slots onto
                   bank positions no variable of that state uses
+  VST: w2 [15:0] candidate variable row the lane's vA is stored to (a spill slot)
   w3 [5:0]  sign-constant pool index, [12:8] uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT),
      [31:16] Bool destination * 2 (compares, Bool ops) or ITE condition * 2
 
@@ -60,6 +62,8 @@ FETCH = [f"F_{ka}_{kb}_A" for ka in KINDS for kb in B_KINDS] + \
         [f"F_{ka}_{kb}_C" for ka in KINDS[1:] for kb in B_KINDS]
 
 BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ", "BAND4"]
+# vA -> the lane's candidate row w2[15:0] (a spilled BV slot; read back as a VAR operand)
+MEM_OPS = ["VST"]
 BV_BIN = ["ADD", "SUB", "MUL", "AND", "OR", "XOR", "SHL", "LSHR", "ASHR", "DIV"]
 BV_UN = ["NOT", "NEG", "MOV", "SEXT"]
 SHIFT_I = [f"SHLI{k}" for k in range(9)] + [f"LSHRI{k}" for k in range(9)] + [f"ASHRI{k}" for k in range(9)]
@@ -85,7 +89,7 @@ XS_BASE = [f"{c}_RA" for c in ("EQ", "ULT", "UGT", "SLT", "SGT")] + ["MUL"] + \
           [f"{o}{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR", "ITE") for v in ("", "_S", "_R")]
 XS_OPS = [f"XS_{o}" for o in XS_BASE]
 
-OPS = BOOL_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + XS_OPS
+OPS = BOOL_OPS + MEM_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + XS_OPS
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
 # id past the table ends the program instead of running off into memory
 HANDLERS = ["INVALID"] + FETCH + OPS
@@ -100,12 +104,13 @@ SHIFT_B_POS = 8     # in w3
 DIVOP_POS = 26      # in w2
 
 BOOL_SLOTS = 19          # 0 false, 1 true, 2..18 allocatable
-MAX_LDS_SLOTS = 31       # slot byte offsets must fit 16 bits with the +1024 half
+MAX_LDS_SLOTS = 31       # LDS slots per wave (62 KiB); more BV slots spill to candidate rows
 SLOT_BYTES = 2048        # 64 lanes x 32 B
 HDR_WORDS = 4
 UOP_WORDS = 4
 PAGE_UOPS = 64           # uops per VGPR page (one per lane); the last one is PAGE
-MAX_POOL = 64            # constants per state (one per lane)
+MAX_POOL = 255           # constants per state (header byte; scalar loads, no lane limit)
+MAX_MS = 64              # mask / sign constants (6-bit index fields)
 
 
 def c_header() -> str:
@@ -124,7 +129,7 @@ def c_header() -> str:
         f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",
         f"#define MGP_U_UOP_WORDS {UOP_WORDS}", f"#define MGP_U_REG_VARS {REG_VARS}",
         f"#define MGP_U_N_KINDS {len(KINDS)}", f"#define MGP_U_PAGE_UOPS {PAGE_UOPS}",
-        f"#define MGP_U_MAX_POOL {MAX_POOL}", f"#define MGP_U_XR_FIRST {ID[XR_OPS[0]]}",
+        f"#define MGP_U_MAX_POOL {MAX_POOL}", f"#define MGP_U_MAX_MS {MAX_MS}", f"#define MGP_U_XR_FIRST {ID[XR_OPS[0]]}",
     ]
     lines.append("static const unsigned short kXrBase[%d] = {%s};" % (len(XR_BASE), ", ".join(
         f"MGP_U_{o}" for o in XR_BASE)))

@@ -14,6 +14,7 @@ from . import bvsem as S
 K_SLOT, K_CONST, K_ACC, K_VAR = 0, 1, 2, 3
 OP_MOV, OP_RET = 80, 90
 BOOL_FALSE, BOOL_TRUE = 62, 63
+LDS_SLOTS = 32   # MGP_LDS_SLOTS
 
 
 def _limbs(words, off) -> int:
@@ -31,6 +32,11 @@ def run_program(words: Sequence[int], off: int, xs: Sequence[int]):
     ins0 = off + 4
     pool = [_limbs(words, ins0 + 4 * n_ins + 8 * k) for k in range(n_c)]
     slots = {}
+    # spill slots (>= LDS_SLOTS) live in the lane's candidate row past its variables
+    # (include/mgp_ir.h): a row there must never be a variable the program reads
+    max_var = status >> 8
+    spill0 = max(max_var, 8)
+    rows = {}
     acc = 0
     bools = 1 << BOOL_TRUE
 
@@ -39,9 +45,12 @@ def run_program(words: Sequence[int], off: int, xs: Sequence[int]):
         if kind == K_ACC:
             return acc
         if kind == K_SLOT:
+            if idx >= LDS_SLOTS:
+                return rows[spill0 + idx - LDS_SLOTS]
             return slots[idx]
         if kind == K_CONST:
             return pool[idx]
+        assert idx < max_var and idx not in rows
         return xs[idx] & S.mask(256)
 
     def bl(o: int) -> bool:
@@ -86,7 +95,10 @@ def run_program(words: Sequence[int], off: int, xs: Sequence[int]):
         r &= m
         acc = r
         if store:
-            slots[dst] = r
+            if dst >= LDS_SLOTS:
+                rows[spill0 + dst - LDS_SLOTS] = r
+            else:
+                slots[dst] = r
     raise ValueError("program fell off the end without RET")
 
 

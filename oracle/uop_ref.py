@@ -97,7 +97,11 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
     # register bank v[64:111]: position p holds variable p when the program reads it
     # (preloaded), else it is a register slot written by REGST stores
     var_mask = (int(words[u0 + 3]) >> 8) & 0xFF
+    var_rows = int(words[off + 3]) >> 8   # v1 header: one past the highest variable read
     bank = {p: int(xs[p]) & M256 for p in range(U.REG_VARS) if var_mask >> p & 1}
+
+    # the lane's candidate row: variables, then the spill rows VST writes (mgp_ir.h)
+    mem = {}
 
     def load(kind: str, p: int) -> int:
         if kind == "slot":
@@ -105,6 +109,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         if kind == "rvar":
             return bank[p // 8]
         if kind == "var":
+            if p in mem:
+                return mem[p]
+            assert p < len(xs), "read of a spill row before its VST"
             return int(xs[p]) & M256
         return pool(p)
 
@@ -143,6 +150,10 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         sb = (w3 >> U.SHIFT_B_POS) & 31
         if op == "PAGE":
             assert pc % U.PAGE_UOPS == U.PAGE_UOPS - 1, "PAGE must end a 64-uop page"
+            continue
+        if op == "VST":
+            assert (w2 & 0xFFFF) >= max(var_rows, 8), "spill row over a variable the program reads"
+            mem[w2 & 0xFFFF] = vA
             continue
         if op in U.BOOL_OPS:
             a, b, c = bools[pa >> 1], bools[pb >> 1], bools[(w2 & 0xFFFF) >> 1]

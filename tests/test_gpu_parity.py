@@ -11,7 +11,7 @@ from oracle import bvsem as S
 from oracle import coracle
 from oracle.keccak_ref import keccak256 as keccak_py
 
-from ._util import cands_from_ints, load_golden, pack_states, random_cands
+from ._util import cands_from_ints, load_golden, pack_states, random_cands, state_slice
 
 pytestmark = pytest.mark.gpu
 
@@ -369,3 +369,44 @@ def test_back_to_back_batches_same_context(mgp_ctx):
             first, _ = mgp_ctx.eval_batch(words, po, cands)
             ok = status == 0
             assert np.array_equal(first[ok], want[ok])
+
+
+def test_spilled_values_and_demoted_bools(mgp_ctx):
+    """Programs past the LDS slots (BV values spilled to candidate rows past the state's
+    variables), past the 17 Bool registers (demoted Bools) and past 64 constants, in one
+    batch with ordinary states: the C ABI pads the candidate rows, both engines agree
+    with the oracle, and the witness rows of the variables come back unchanged."""
+    from .test_lowering import _bool_fan, _live_chain
+
+    rng = np.random.default_rng(77)
+    states = [(_live_chain(n), []) for n in (36, 90, 200)] + [_bool_fan(n) for n in (24, 60)]
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]
+    pool = [(k * 0x9E3779B97F4A7C15 + 1) % 2 ** 256 for k in range(150)]
+    acc = 0
+    for k in range(150):
+        nl.append([S.CONST, 256, -1, -1, -1, k, 0])
+        nl.append([S.XOR if k % 3 else S.ADD, 256, acc, len(nl) - 1, -1, 0, 0])
+        acc = len(nl) - 1
+    nl.append([S.ULT, 1, acc, 1, -1, 0, 0])
+    states.append((nl, pool))
+    b = N.synth_generate(0x4D595448, 4242, 40, 64, 100)
+    for s in range(40):
+        ns, cs = state_slice(b, s)
+        states.append(([[int(r[f]) for f in ("op", "width", "a", "b", "c", "p0", "p1")] for r in ns], cs))
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    rows = N.prog_rows(words, po)
+    n_vars = 6
+    assert rows.max() > n_vars  # some program needs spill rows
+    cands = random_cands(rng, len(states), 100, n_vars, interesting_frac=0.2)
+    for s in range(len(states) - 40, len(states)):  # planted witnesses of the synthetic states
+        if b["planted"][s - (len(states) - 40)]:
+            cands[s, 7] = b["plant_words"][s - (len(states) - 40)]
+    first, wit = mgp_ctx.eval_batch(words, po, cands)
+    want = coracle.first_sat(nodes, noff, consts, coff, cands)
+    mism = np.nonzero(first != want)[0]
+    assert mism.size == 0, f"states {mism[:8]} gpu={first[mism[:8]]} oracle={want[mism[:8]]}"
+    assert (first >= 0).sum() > 10
+    for s in np.nonzero(first >= 0)[0]:
+        assert (wit[s] == cands[s, first[s]]).all()

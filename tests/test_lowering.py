@@ -159,26 +159,81 @@ def _live_chain(n):
     return nl
 
 
-def test_many_live_values_rejected_cleanly():
-    # 28 live values: a 4-slot cap is unsupported (never wrong), the default cap lowers
-    nl = _live_chain(28)
+def _bool_fan(n):
+    # n compares that are all live at once (read again in reverse order by a BAND chain
+    # after a BOR chain over them): more than the 17 Bool registers of the interpreter
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]
+    cmps = []
+    for i in range(n):
+        nl.append([S.CONST, 256, -1, -1, -1, i, 0])
+        nl.append([S.ULT if i % 2 else S.EQ, 1, len(nl) - 1, i % 2, -1, 0, 0])
+        cmps.append(len(nl) - 1)
+    acc = cmps[0]
+    for c in cmps[1:]:
+        nl.append([S.BOR, 1, acc, c, -1, 0, 0])
+        acc = len(nl) - 1
+    acc2 = cmps[-1]
+    for c in reversed(cmps[:-1]):
+        nl.append([S.BXOR, 1, acc2, c, -1, 0, 0])
+        acc2 = len(nl) - 1
+    nl.append([S.BAND, 1, acc, acc2, -1, 0, 0])
+    return nl, list(range(3, 3 + 7 * n, 7))
+
+
+def _header(words, po, s):
+    return [int(words[int(po[s]) + k]) for k in range(4)]
+
+
+def test_many_live_values_spill_to_candidate_rows():
+    """Past the LDS slots, BV values spill to the lane's candidate rows past its variables
+    (include/mgp_ir.h): a 4-slot cap, 40 and 200 live values all lower and agree with the
+    DAG in both encodings (the reference interpreters assert that no spill row is a
+    variable the program reads, and that every row is written before it is read);
+    past MGP_MAX_SLOTS the state is unsupported, never wrong."""
+    rows = [[3, 5], [INTERESTING[3], INTERESTING[4]], [0, 2 ** 256 - 1]]
+    for n, cap in ((28, 4), (40, 0), (200, 0)):
+        nl = _live_chain(n)
+        words, po, status = _check_states([(nl, [])], [rows], max_slots=cap)
+        assert status[0] == N.ST_OK, (n, cap)
+        h = _header(words, po, 0)
+        assert h[2] >= 32 if (n > 32 or cap) else True
+        assert N.prog_rows(words, po)[0] == (max(h[3] >> 8, 8) + h[2] - 31 if h[2] >= 32 else h[3] >> 8)
+    nl = _live_chain(300)
     nodes, noff, consts, coff = pack_states([(nl, [])])
-    _, _, status = N.lower(nodes, noff, consts, coff, max_slots=4)
-    assert status[0] == N.ST_UNSUPPORTED
-    words, po, status = N.lower(nodes, noff, consts, coff, max_slots=64)
-    assert status[0] == N.ST_OK
-    for xs in ([3, 5], [INTERESTING[3], INTERESTING[4]]):
-        want = S.eval_root(nl, [], xs)
-        assert BR.run_program(words, int(po[0]), xs) == want
-        assert UR.run_uops(words, int(po[0]), xs) == want
-    # 40 live values exceed the interpreter's 31 LDS slots (62 KiB per wave):
-    # unsupported in both encodings, so both engines answer "undecided"
-    nl = _live_chain(40)
-    nodes, noff, consts, coff = pack_states([(nl, [])])
-    words, po, status = N.lower(nodes, noff, consts, coff, max_slots=64)
+    words, po, status = N.lower(nodes, noff, consts, coff)
     assert status[0] == N.ST_UNSUPPORTED
     assert BR.run_program(words, int(po[0]), [3, 5]) is None
     assert UR.run_uops(words, int(po[0]), [3, 5]) is None
+
+
+def test_bool_pressure_demotes_to_bv():
+    """More live Bools than the interpreter's 17 registers: the lowering demotes the
+    farthest-read ones to 1-bit values (ITE / EQ) and the program still agrees."""
+    for n in (16, 24, 60):
+        nl, consts = _bool_fan(n)
+        rows = [[consts[k], consts[k] + 1] for k in (0, 1, n // 2, n - 1)] + [[0, 0], [5, 2 ** 255]]
+        _, _, status = _check_states([(nl, consts)], [rows])
+        assert status[0] == N.ST_OK, n
+
+
+def test_constant_pool_past_64_entries():
+    """More than 64 constants: the interpreter's pool has the mask / sign constants first
+    (6-bit index fields), then up to 255 entries in all."""
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 64, -1, -1, -1, 1, 0]]
+    consts = [(k * 0x9E3779B97F4A7C15 + 1) % 2 ** 256 for k in range(150)]
+    acc = 0
+    for k in range(150):
+        nl.append([S.CONST, 256, -1, -1, -1, k, 0])
+        nl.append([S.XOR if k % 3 else S.ADD, 256, acc, len(nl) - 1, -1, 0, 0])
+        acc = len(nl) - 1
+    nl.append([S.EXTRACT, 64, acc, -1, -1, 63, 0])
+    nl.append([S.ADD, 64, len(nl) - 1, 1, -1, 0, 0])                   # masked: a width-64 mask constant
+    nl.append([S.SLT, 1, len(nl) - 1, 1, -1, 0, 0])                    # signed: a sign constant
+    rows = [[7, 9], [INTERESTING[5], 2 ** 63], [0, 2 ** 64 - 1]]
+    words, po, status = _check_states([(nl, consts)], [rows])
+    assert status[0] == N.ST_OK
+    u0 = UR.uop_offset(words, int(po[0]))
+    assert int(words[u0 + 3]) & 0xFF > 64
 
 
 def wide_struct_case():

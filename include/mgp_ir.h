@@ -160,7 +160,9 @@ typedef struct mgp_node {
  * with the farthest next use to a 1-bit BV value (ITE(b, 1, 0), re-tested by EQ at
  * each reader), which can spill like any BV value (= the gfx950 interpreter's 17
  * allocatable Bool registers) */
+#ifndef MGP_BOOL_LIVE
 #define MGP_BOOL_LIVE 17u
+#endif
 
 /* BV operand (16 bits): kind in bits 15:14, index in 13:0 */
 #define MGP_K_SLOT 0u

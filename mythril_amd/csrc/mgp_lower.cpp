@@ -1006,7 +1006,8 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
 
   // a spilling program: slot numbers by access count (reads + stores), most used first,
   // so that the LDS slots (and the gfx950 interpreter's register slots) hold the hot values
-  if (slots_used > MGP_LDS_SLOTS && slot_cap == MGP_LDS_SLOTS) {
+  static const bool norenum_dbg = getenv("MGP_LOWER_NORENUM") != nullptr;
+  if (slots_used > MGP_LDS_SLOTS && slot_cap == MGP_LDS_SLOTS && !norenum_dbg) {
     auto field = [&](const std::pair<uint32_t, uint32_t> &f) -> uint32_t {
       return f.first % 4u == 0u ? (out[f.first] >> 16) & 0xFFu : (out[f.first] >> f.second) & 0x3FFFu;
     };

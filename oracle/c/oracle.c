@@ -183,11 +183,11 @@ static w256 from_u32(const uint32_t *p) {
   return r;
 }
 
-/* evaluate one state's DAG for one candidate; returns root (0/1) or -2 */
-static int eval_state(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t nc,
-                      const uint32_t *xs /* n_vars*8 */, uint32_t n_vars, w256 *v, unsigned char *b,
-                      uint16_t *wd) {
-  for (uint64_t i = 0; i < n; ++i) {
+/* evaluate node i of a DAG (operands already evaluated); 0, or -2 when not evaluable */
+static int eval_node(const mgp_node *nd, uint64_t i, const uint32_t *consts, uint64_t nc,
+                     const uint32_t *xs /* n_vars*8 */, uint32_t n_vars, w256 *v, unsigned char *b,
+                     uint16_t *wd) {
+  {
     const mgp_node *x = &nd[i];
     unsigned w = x->width;
     w256 r = z256();
@@ -282,7 +282,203 @@ static int eval_state(const mgp_node *nd, uint64_t n, const uint32_t *consts, ui
     if (isbool) { b[i] = (unsigned char)(bv ? 1 : 0); wd[i] = 1; v[i] = z256(); }
     else { b[i] = 2; wd[i] = (uint16_t)w; v[i] = r; }
   }
+  return 0;
+}
+
+/* evaluate one state's DAG (values <= 256 bits) for one candidate; root (0/1) or -2 */
+static int eval_state(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t nc,
+                      const uint32_t *xs /* n_vars*8 */, uint32_t n_vars, w256 *v, unsigned char *b,
+                      uint16_t *wd) {
+  for (uint64_t i = 0; i < n; ++i)
+    if (eval_node(nd, i, consts, nc, xs, n_vars, v, b, wd) != 0) return -2;
   return n ? (b[n - 1] == 1) : -2;
+}
+
+static int eval_one(const mgp_node *nd, uint64_t i, w256 *v, unsigned char *b, uint16_t *wd) {
+  return eval_node(nd, i, NULL, 0, NULL, 0, v, b, wd);
+}
+
+/* ---------------------------------------------------------- wide values
+ * A state with a value wider than 256 bits (512-bit mapping preimages Concat(key, slot),
+ * keccak256_512 and its inverse, 257-bit overflow sums; include/mgp_ir.h "wide values")
+ * is evaluated with MGP_MAX_WIDE-bit values: a w-bit VAR / CONST / fresh UF value is
+ * ceil(w/256) consecutive 256-bit entries, low bits first.  Ops on values <= 256 bits
+ * reuse the w256 helpers above; the ops the node format allows on wide values
+ * (structural ops, EQ / unsigned compares, ADD / SUB / MUL, bitwise ops, UF arguments
+ * and results) act on all limbs. */
+#define WL (MGP_MAX_WIDE / 64)
+typedef struct { uint64_t l[WL]; } wbig;
+
+static wbig bz(void) { wbig r; memset(&r, 0, sizeof(r)); return r; }
+static wbig b_trunc(wbig a, unsigned w) {
+  for (unsigned i = 0; i < WL; ++i) {
+    const unsigned lo = 64u * i;
+    if (w <= lo) a.l[i] = 0;
+    else if (w < lo + 64) a.l[i] &= (1ull << (w - lo)) - 1ull;
+  }
+  return a;
+}
+static wbig b_from256(w256 a) { wbig r = bz(); memcpy(r.l, a.l, sizeof(a.l)); return r; }
+static w256 b_to256(wbig a) { w256 r; memcpy(r.l, a.l, sizeof(r.l)); return r; }
+static wbig b_shl(wbig a, unsigned s) {
+  wbig r = bz();
+  if (s >= MGP_MAX_WIDE) return r;
+  const unsigned q = s >> 6, b = s & 63;
+  for (int i = WL - 1; i >= (int)q; --i) {
+    uint64_t v = a.l[i - q] << b;
+    if (b && i - (int)q - 1 >= 0) v |= a.l[i - q - 1] >> (64 - b);
+    r.l[i] = v;
+  }
+  return r;
+}
+static wbig b_lshr(wbig a, unsigned s) {
+  wbig r = bz();
+  if (s >= MGP_MAX_WIDE) return r;
+  const unsigned q = s >> 6, b = s & 63;
+  for (unsigned i = 0; i + q < WL; ++i) {
+    uint64_t v = a.l[i + q] >> b;
+    if (b && i + q + 1 < WL) v |= a.l[i + q + 1] << (64 - b);
+    r.l[i] = v;
+  }
+  return r;
+}
+static int b_cmp(wbig a, wbig b) {
+  for (int i = WL - 1; i >= 0; --i) {
+    if (a.l[i] < b.l[i]) return -1;
+    if (a.l[i] > b.l[i]) return 1;
+  }
+  return 0;
+}
+static wbig b_add(wbig a, wbig b) {
+  u128 c = 0;
+  for (unsigned i = 0; i < WL; ++i) {
+    c += (u128)a.l[i] + b.l[i];
+    a.l[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  return a;
+}
+static wbig b_not(wbig a) { for (unsigned i = 0; i < WL; ++i) a.l[i] = ~a.l[i]; return a; }
+static wbig b_sub(wbig a, wbig b) { wbig one = bz(); one.l[0] = 1; return b_add(a, b_add(b_not(b), one)); }
+static wbig b_mul(wbig a, wbig b) {
+  wbig r = bz();
+  for (unsigned i = 0; i < WL; ++i) {
+    if (!a.l[i]) continue;
+    u128 c = 0;
+    for (unsigned j = 0; i + j < WL; ++j) {
+      c += (u128)a.l[i] * b.l[j] + r.l[i + j];
+      r.l[i + j] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  return r;
+}
+/* ceil(w/256) consecutive 256-bit entries starting at base[idx], low first */
+static int b_entries(const uint32_t *base, uint64_t n_entries, uint64_t idx, unsigned w, wbig *out) {
+  const unsigned k = (w + 255u) / 256u;
+  if (idx + k > n_entries) return 0;
+  wbig r = bz();
+  for (unsigned j = 0; j < k; ++j) {
+    w256 e = from_u32(base + 8u * (idx + j));
+    for (int i = 0; i < 4 && 4 * j + i < WL; ++i) r.l[4 * j + i] = e.l[i];
+  }
+  *out = b_trunc(r, w);
+  return 1;
+}
+
+static int eval_state_wide(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t nc,
+                           const uint32_t *xs, uint32_t n_vars, wbig *v, unsigned char *b, uint16_t *wd) {
+  for (uint64_t i = 0; i < n; ++i) {
+    const mgp_node *x = &nd[i];
+    unsigned w = x->width;
+    wbig r = bz();
+    int isbool = 0, bv = 0;
+    const int wide_in = (x->a >= 0 && wd[x->a] > 256) || (x->b >= 0 && wd[x->b] > 256);
+    switch (x->op) {
+      case MGP_OP_VAR:
+        if (!b_entries(xs, n_vars, x->p0, w, &r)) return -2;
+        break;
+      case MGP_OP_CONST:
+        if (!b_entries(consts, nc, x->p0, w, &r)) return -2;
+        break;
+      case MGP_OP_TRUE: isbool = 1; bv = 1; break;
+      case MGP_OP_FALSE: isbool = 1; bv = 0; break;
+      case MGP_OP_ADD: r = b_trunc(b_add(v[x->a], v[x->b]), w); break;
+      case MGP_OP_SUB: r = b_trunc(b_sub(v[x->a], v[x->b]), w); break;
+      case MGP_OP_MUL: r = b_trunc(b_mul(v[x->a], v[x->b]), w); break;
+      case MGP_OP_AND: for (unsigned k = 0; k < WL; ++k) r.l[k] = v[x->a].l[k] & v[x->b].l[k]; break;
+      case MGP_OP_OR: for (unsigned k = 0; k < WL; ++k) r.l[k] = v[x->a].l[k] | v[x->b].l[k]; break;
+      case MGP_OP_XOR: for (unsigned k = 0; k < WL; ++k) r.l[k] = v[x->a].l[k] ^ v[x->b].l[k]; break;
+      case MGP_OP_NOT: r = b_trunc(b_not(v[x->a]), w); break;
+      case MGP_OP_EXTRACT: w = x->p0 - x->p1 + 1; r = b_trunc(b_lshr(v[x->a], x->p1), w); break;
+      case MGP_OP_CONCAT: r = b_trunc(b_add(b_shl(v[x->a], wd[x->b]), v[x->b]), w); break;
+      case MGP_OP_ZEXT: r = v[x->a]; break;
+      case MGP_OP_ITE:
+        if (b[x->b] != 2) { isbool = 1; bv = b[x->a] ? b[x->b] : b[x->c]; }
+        else r = b[x->a] ? v[x->b] : v[x->c];
+        break;
+      case MGP_OP_EQ:
+        isbool = 1;
+        if (b[x->a] != 2) bv = b[x->a] == b[x->b];
+        else bv = b_cmp(v[x->a], v[x->b]) == 0;
+        break;
+      case MGP_OP_ULT: isbool = 1; bv = b_cmp(v[x->a], v[x->b]) < 0; break;
+      case MGP_OP_ULE: isbool = 1; bv = b_cmp(v[x->a], v[x->b]) <= 0; break;
+      case MGP_OP_UGT: isbool = 1; bv = b_cmp(v[x->a], v[x->b]) > 0; break;
+      case MGP_OP_UGE: isbool = 1; bv = b_cmp(v[x->a], v[x->b]) >= 0; break;
+      case MGP_OP_BAND: isbool = 1; bv = b[x->a] && b[x->b]; break;
+      case MGP_OP_BOR: isbool = 1; bv = b[x->a] || b[x->b]; break;
+      case MGP_OP_BXOR: isbool = 1; bv = b[x->a] != b[x->b]; break;
+      case MGP_OP_BNOT: isbool = 1; bv = !b[x->a]; break;
+      case MGP_OP_BITE: isbool = 1; bv = b[x->a] ? b[x->b] : b[x->c]; break;
+      case MGP_OP_BEQ: isbool = 1; bv = b[x->a] == b[x->b]; break;
+      case MGP_OP_UFAPP: {
+        if (!b_entries(xs, n_vars, x->p1, w, &r)) return -2;
+        for (uint64_t j = 0; j < i; ++j)
+          if (nd[j].op == MGP_OP_UFAPP && nd[j].p0 == x->p0 && b_cmp(v[nd[j].a], v[x->a]) == 0) { r = v[j]; break; }
+        break;
+      }
+      case MGP_OP_UFINV: {
+        int found = 0;
+        for (uint64_t j = 0; j < i && !found; ++j)
+          if (nd[j].op == MGP_OP_UFINV && nd[j].p0 == x->p0 && b_cmp(v[nd[j].a], v[x->a]) == 0) { r = v[j]; found = 1; }
+        for (uint64_t j = 0; j < i && !found; ++j)
+          if (nd[j].op == MGP_OP_UFAPP && nd[j].p0 == x->p0 && b_cmp(v[j], v[x->a]) == 0) { r = v[nd[j].a]; found = 1; }
+        if (!found && !b_entries(xs, n_vars, x->p1, w, &r)) return -2;
+        break;
+      }
+      default: {
+        /* every other op acts on values <= 256 bits: the w256 evaluator's rules */
+        if (wide_in || w > 256) return -2;
+        const mgp_node y = {x->op, 0, (uint16_t)w, x->a >= 0 ? 0 : -1, x->b >= 0 ? 1 : -1, x->c >= 0 ? 2 : -1,
+                            x->p0, x->p1};
+        mgp_node tmp[4];
+        w256 tv[4];
+        unsigned char tb[4];
+        uint16_t tw[4];
+        const int32_t ops[3] = {x->a, x->b, x->c};
+        for (int k = 0; k < 3; ++k) {
+          tmp[k].op = MGP_OP_FALSE;  /* placeholders; their values are set directly */
+          if (ops[k] >= 0) { tv[k] = b_to256(v[ops[k]]); tb[k] = b[ops[k]]; tw[k] = wd[ops[k]]; }
+          else { tv[k] = z256(); tb[k] = 0; tw[k] = 1; }
+        }
+        tmp[3] = y;
+        if (eval_one(tmp, 3, tv, tb, tw) != 0) return -2;
+        if (tb[3] != 2) { isbool = 1; bv = tb[3]; }
+        else { r = b_from256(tv[3]); w = tw[3]; }
+        break;
+      }
+    }
+    if (isbool) { b[i] = (unsigned char)(bv ? 1 : 0); wd[i] = 1; v[i] = bz(); }
+    else { b[i] = 2; wd[i] = (uint16_t)w; v[i] = r; }
+  }
+  return n ? (b[n - 1] == 1) : -2;
+}
+
+static int state_is_wide(const mgp_node *nd, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i)
+    if (nd[i].width > 256) return 1;
+  return 0;
 }
 
 /* first satisfying candidate per state; cands AoS [state][cand][var][8] */
@@ -292,8 +488,9 @@ int oracle_first_sat(const mgp_node *nodes, const uint64_t *node_offsets, uint32
   int rc = 0;
 #pragma omp parallel
   {
-    uint64_t cap = 0;
+    uint64_t cap = 0, wcap = 0;
     w256 *v = NULL;
+    wbig *vw = NULL;
     unsigned char *b = NULL;
     uint16_t *wd = NULL;
 #pragma omp for schedule(dynamic, 16)
@@ -306,17 +503,25 @@ int oracle_first_sat(const mgp_node *nodes, const uint64_t *node_offsets, uint32
         b = (unsigned char *)malloc(cap);
         wd = (uint16_t *)malloc(cap * sizeof(uint16_t));
       }
+      const int wide = state_is_wide(nodes + n0, n);
+      if (wide && n > wcap) {
+        free(vw);
+        wcap = n;
+        vw = (wbig *)malloc(wcap * sizeof(wbig));
+      }
       int32_t res = -1;
       for (uint32_t c = 0; c < n_cand; ++c) {
         const uint32_t *xs = cands + ((uint64_t)s * n_cand + c) * n_vars * 8u;
-        int r = eval_state(nodes + n0, n, consts + const_offsets[s] * 8u, const_offsets[s + 1] - const_offsets[s],
-                           xs, n_vars, v, b, wd);
+        const uint32_t *cs = consts + const_offsets[s] * 8u;
+        const uint64_t nc = const_offsets[s + 1] - const_offsets[s];
+        int r = wide ? eval_state_wide(nodes + n0, n, cs, nc, xs, n_vars, vw, b, wd)
+                     : eval_state(nodes + n0, n, cs, nc, xs, n_vars, v, b, wd);
         if (r == -2) { res = -2; break; }
         if (r == 1 && res < 0) { res = (int32_t)c; if (!full) break; }
       }
       out[s] = res;
     }
-    free(v); free(b); free(wd);
+    free(v); free(vw); free(b); free(wd);
   }
   return rc;
 }

@@ -14,7 +14,7 @@ from oracle import bvsem as S
 from oracle import bytecode_ref as BR
 from oracle import uop_ref as UR
 
-from ._util import INTERESTING, load_golden, pack_states, state_slice
+from ._util import INTERESTING, cands_from_ints, load_golden, pack_states, state_slice
 
 
 def _check_states(states, cand_rows, max_slots=0):
@@ -444,3 +444,50 @@ def test_synthetic_generator_is_deterministic_and_sliceable():
     assert np.array_equal(a["plant_words"][32:], b["plant_words"])
     ops = N.nominal_ops(a["nodes"], a["node_offsets"])
     assert 1000 < ops.mean() < 6000
+
+
+def test_c_oracle_wide_values_match_python_oracle():
+    """The C oracle (the GPU tests' checker and the CPU baseline) evaluates states with
+    values wider than 256 bits on MGP_MAX_WIDE-bit values: it must agree with
+    oracle.bvsem on the wide structural, arithmetic and keccak256_512 mapping cases and
+    on contract-shaped states with 512-bit mapping preimages (WalletLibrary)."""
+    from oracle import coracle
+
+    nl_s, c_s, rows_s = wide_struct_case()
+    nl_m, nl_c, c_m, rows_m = wide_mapping_case()
+    a_states, a_rows = wide_arith_cases()
+    cases = [((nl_s, c_s), rows_s), ((nl_m, c_m), rows_m), ((nl_c, c_m), rows_m)]
+    cases += [(st, r) for st, r in zip(a_states, a_rows)]
+    for (nl, cl), rows in cases:
+        n_vars = max(len(r) for r in rows)
+        full = [list(r) + [0] * (n_vars - len(r)) for r in rows]
+        nodes, noff, consts, coff = pack_states([(nl, cl)])
+        got = coracle.first_sat(nodes, noff, consts, coff, cands_from_ints([full]))
+        assert got[0] == S.first_sat(nl, cl, full)
+
+
+def test_c_oracle_contract_states_match_python_oracle():
+    import corpus
+    from mythril_amd import dag as D
+    from mythril_amd import front as F
+    from mythril_amd.keccak import KeccakFunctionManager
+    from oracle import coracle
+
+    kfm = KeccakFunctionManager()
+    items = corpus.wallet_states(0, kfm)[:3] + [corpus.bectoken_states(k, kfm) for k in range(2)]
+    B = F.Batch([list(c[1]) for c in items])
+    nv = B.n_vars()
+    _, dom = N.refute_domains(*B.packed(), B.var_off)
+    cands = N.make_candidates(12, nv, 99, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off, B.aliases,
+                              B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8),
+                              var_kind=B.var_kind, dom=dom)
+    N.guided_candidates(*B.packed(), cands, seed=5, every=2, n_decide=2)
+    nodes, noff, consts, coff = B.packed(gpu=True)
+    got = coracle.first_sat(nodes, noff, consts, coff, cands)
+    for s in range(B.n_states):
+        n0, n1 = int(noff[s]), int(noff[s + 1])
+        nl = [[int(r[f]) for f in ("op", "width", "a", "b", "c", "p0", "p1")] for r in nodes[n0:n1]]
+        cl = [S.limbs_to_int(c) for c in consts[int(coff[s]):int(coff[s + 1])]]
+        rows = [[S.limbs_to_int(cands[s, k, v]) for v in range(nv)] for k in range(12)]
+        assert got[s] == S.first_sat(nl, cl, rows), s
+    B.close()

@@ -780,86 +780,115 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
       }
       return 0;
     };
-    for (int round = 0;; ++round) {
-      const uint32_t n0 = (uint32_t)S.ins.size();
-      std::vector<int64_t> lu(n0, -1);
-      std::vector<std::vector<uint32_t>> readers(n0);
-      for (uint32_t t = 0; t < n0; ++t) {
-        Ref *br[3];
-        const int k = bool_refs(S.ins[t], br);
-        for (int i = 0; i < k; ++i)
-          if (br[i]->k == R_INS) {
-            lu[br[i]->idx] = std::max<int64_t>(lu[br[i]->idx], t);
-            if (readers[br[i]->idx].empty() || readers[br[i]->idx].back() != t) readers[br[i]->idx].push_back(t);
-          }
-      }
-      if (root.k == R_INS) lu[root.idx] = std::max<int64_t>(lu[root.idx], n0);
-      // dry run of the Bool bit allocation below
-      std::vector<std::vector<uint32_t>> expire_at(n0 + 1);
-      for (uint32_t t = 0; t < n0; ++t)
-        if (S.ins[t].is_bool && lu[t] > (int64_t)t && lu[t] <= (int64_t)n0) expire_at[lu[t]].push_back(t);
-      std::vector<uint32_t> cur;
-      int64_t fail_at = -1;
-      for (uint32_t t = 0; t < n0 && fail_at < 0; ++t) {
-        for (uint32_t v : expire_at[t]) cur.erase(std::find(cur.begin(), cur.end(), v));
-        if (S.ins[t].is_bool && lu[t] > (int64_t)t) {
-          if (cur.size() >= MGP_BOOL_LIVE) fail_at = t;
-          else cur.push_back(t);
+    // one pass over the schedule plans every demotion (victim: the live Bool read farthest
+    // in the future; a demoted Bool's readers need one short-lived EQ bit each, right
+    // before them), then one rewrite applies them
+    const uint32_t n0 = (uint32_t)S.ins.size();
+    std::vector<int64_t> lu(n0, -1);
+    std::vector<std::vector<uint32_t>> readers(n0);
+    for (uint32_t t = 0; t < n0; ++t) {
+      Ref *br[3];
+      const int k = bool_refs(S.ins[t], br);
+      for (int i = 0; i < k; ++i)
+        if (br[i]->k == R_INS) {
+          lu[br[i]->idx] = std::max<int64_t>(lu[br[i]->idx], t);
+          if (readers[br[i]->idx].empty() || readers[br[i]->idx].back() != t) readers[br[i]->idx].push_back(t);
         }
-      }
-      if (fail_at < 0) break;
-      if (round >= 1024) return unsupported();
-      // victim: the live Bool read farthest in the future (the root counts as n0)
-      uint32_t victim = cur[0];
+    }
+    if (root.k == R_INS) lu[root.idx] = std::max<int64_t>(lu[root.idx], n0);
+    std::vector<std::vector<uint32_t>> expire_at(n0 + 1);
+    for (uint32_t t = 0; t < n0; ++t)
+      if (S.ins[t].is_bool && lu[t] > (int64_t)t && lu[t] <= (int64_t)n0) expire_at[lu[t]].push_back(t);
+    std::vector<uint8_t> demoted(n0, 0);
+    bool any = false;
+    std::vector<uint32_t> cur;  // live Bools holding a bit
+    auto next_read = [&](uint32_t v, uint32_t t) -> int64_t {
+      auto it = std::lower_bound(readers[v].begin(), readers[v].end(), t);
+      return it == readers[v].end() ? (int64_t)n0 : (int64_t)*it;
+    };
+    // demote the member of cur read farthest after t (not one t itself reads)
+    auto demote_one = [&](uint32_t t, const uint32_t *keep, int n_keep) -> bool {
       int64_t best = -1;
-      for (uint32_t v : cur) {
-        int64_t nx = (int64_t)n0;
-        for (uint32_t r : readers[v])
-          if ((int64_t)r >= fail_at) {
-            nx = r;
-            break;
-          }
-        if (nx > best) best = nx, victim = v;
+      size_t at = 0;
+      for (size_t j = 0; j < cur.size(); ++j) {
+        bool kept = false;
+        for (int q = 0; q < n_keep; ++q) kept |= keep[q] == cur[j];
+        if (kept) continue;
+        const int64_t nx = next_read(cur[j], t);
+        if (nx > best) best = nx, at = j;
       }
+      if (best < 0) return false;
+      demoted[cur[at]] = 1;
+      any = true;
+      cur.erase(cur.begin() + (ptrdiff_t)at);
+      return true;
+    };
+    for (uint32_t t = 0; t < n0; ++t) {
+      Ref *br[3];
+      const int k = bool_refs(S.ins[t], br);
+      uint32_t rd[3];
+      int n_rd = 0, transients = 0;
+      for (int i = 0; i < k; ++i)
+        if (br[i]->k == R_INS) {
+          bool dup = false;
+          for (int q = 0; q < n_rd; ++q) dup |= rd[q] == br[i]->idx;
+          if (dup) continue;
+          rd[n_rd++] = br[i]->idx;
+          transients += demoted[br[i]->idx];
+        }
+      while (cur.size() + (size_t)transients > MGP_BOOL_LIVE)
+        if (!demote_one(t, rd, n_rd)) return unsupported();
+      for (uint32_t v : expire_at[t]) {
+        auto it = std::find(cur.begin(), cur.end(), v);
+        if (it != cur.end()) cur.erase(it);
+      }
+      if (S.ins[t].is_bool && lu[t] > (int64_t)t) {
+        if (cur.size() >= MGP_BOOL_LIVE && !demote_one(t, nullptr, 0)) return unsupported();
+        cur.push_back(t);
+      }
+    }
+    if (any) {
       const Ref one = const_ref(1u), zero = const_ref(0u);
       std::vector<VIns> re;
-      re.reserve(n0 + 2 + readers[victim].size());
+      re.reserve(n0 + n0 / 4 + 8);
       std::vector<uint32_t> remap(n0, 0);
-      Ref dref;
+      std::vector<Ref> dref(n0);  // the 1-bit value of a demoted Bool
       for (uint32_t t = 0; t < n0; ++t) {
         VIns I = S.ins[t];
         for (Ref *r : {&I.a, &I.b, &I.c})
           if (r->k == R_INS) r->idx = remap[r->idx];
-        if (t > victim) {
-          Ref *br[3];
-          const int k = bool_refs(S.ins[t], br);
-          bool reads = false;
-          for (int i = 0; i < k; ++i) reads |= br[i]->k == R_INS && br[i]->idx == victim;
-          if (reads) {
-            re.push_back(VIns{MGP_OP_EQ, 1, true, dref, one, Ref(), 0});
-            Ref e;
-            e.k = R_INS;
+        Ref *br[3], *nr[3];
+        const int k = bool_refs(S.ins[t], br);
+        bool_refs(I, nr);
+        for (int i = 0; i < k; ++i) {
+          if (br[i]->k != R_INS || !demoted[br[i]->idx]) continue;
+          const uint32_t v = br[i]->idx;
+          // one EQ per distinct demoted operand (BITE / BAND may read one Bool twice)
+          Ref e;
+          e.k = R_INS;
+          e.idx = 0xFFFFFFFFu;
+          for (int j = 0; j < i; ++j)
+            if (br[j]->k == R_INS && br[j]->idx == v) e = *nr[j];
+          if (e.idx == 0xFFFFFFFFu) {
+            re.push_back(VIns{MGP_OP_EQ, 1, true, dref[v], one, Ref(), 0});
             e.idx = (uint32_t)re.size() - 1;
-            Ref *nr[3];
-            const int kk = bool_refs(I, nr);
-            for (int i = 0; i < kk; ++i)
-              if (nr[i]->k == R_INS && nr[i]->idx == remap[victim]) *nr[i] = e;
           }
+          *nr[i] = e;
         }
         remap[t] = (uint32_t)re.size();
         re.push_back(I);
-        if (t == victim) {
+        if (demoted[t]) {
           Ref b;
           b.k = R_INS;
           b.idx = remap[t];
           re.push_back(VIns{MGP_OP_ITE, 1, false, b, one, zero, 0});
-          dref.k = R_INS;
-          dref.idx = (uint32_t)re.size() - 1;
+          dref[t].k = R_INS;
+          dref[t].idx = (uint32_t)re.size() - 1;
         }
       }
       if (root.k == R_INS) {
-        if (root.idx == victim) {
-          re.push_back(VIns{MGP_OP_EQ, 1, true, dref, one, Ref(), 0});
+        if (demoted[root.idx]) {
+          re.push_back(VIns{MGP_OP_EQ, 1, true, dref[root.idx], one, Ref(), 0});
           root.idx = (uint32_t)re.size() - 1;
         } else {
           root.idx = remap[root.idx];
@@ -1072,7 +1101,13 @@ static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32
       for (int alt = 1; alt <= 2; ++alt) {
         Lowered b = lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, alt);
         const bool a_ok = a.status == MGP_ST_OK, b_ok = b.status == MGP_ST_OK;
-        if (!b_ok || (a_ok && b.words[2] >= a.words[2])) continue;
+        // fewer slots wins (occupancy); between spilling programs, fewer instructions
+        // (a spill is a memory access either way, an instruction is issue time)
+        if (!b_ok) continue;
+        if (a_ok) {
+          const bool spill = a.words[2] > MGP_LDS_SLOTS || b.words[2] > MGP_LDS_SLOTS;
+          if (spill ? b.words[0] >= a.words[0] : b.words[2] >= a.words[2]) continue;
+        }
         std::vector<uint32_t> bu;
         if (mgp_uop_translate(b.words.data(), bu) != 0) continue;
         a = std::move(b);

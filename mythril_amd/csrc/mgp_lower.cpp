@@ -196,6 +196,34 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   // Constants are pooled by value, so two constant pieces are equal iff their pool
   // indices are.  Concrete arguments (calldata / storage indices) are the common case,
   // and folding them keeps the Ackermann chain from holding every earlier value live.
+  // A piece that is a sum of one symbolic term and constants (calldata indices
+  // 4 + offset + i, calldata.py:219-232 with a symbolic ABI offset) is compared by its
+  // base term and its constant offset (mod 2^w): two such indices of one base are equal
+  // iff their offsets are, so the selects of one symbolic word never test each other.
+  auto sum_form = [&](Ref r, uint32_t w, Ref *base, uint32_t off[8]) {
+    memset(off, 0, 8 * sizeof(uint32_t));
+    auto addc = [&](const ConstKey &c) {
+      uint64_t cy = 0;
+      for (int l = 0; l < 8; ++l) {
+        cy += (uint64_t)off[l] + c.w[l];
+        off[l] = (uint32_t)cy;
+        cy >>= 32;
+      }
+    };
+    for (int depth = 0; depth < 64 && r.k == R_INS; ++depth) {
+      const VIns &I = S.ins[r.idx];
+      if (I.op != MGP_OP_ADD || I.width != w) break;
+      if (I.b.k == R_CONST) addc(S.pool[I.b.idx]), r = I.a;
+      else if (I.a.k == R_CONST) addc(S.pool[I.a.idx]), r = I.b;
+      else break;
+    }
+    if (r.k == R_CONST) {  // a constant: base none, offset = its value
+      addc(S.pool[r.idx]);
+      r = Ref();
+    }
+    for (int l = 0; l < 8; ++l) off[l] &= limb_mask(w, l);
+    *base = r;
+  };
   auto known_eq = [&](const Pieces &p, const Pieces &q) -> int {
     if (p.size() != q.size()) return -1;
     bool all = true;
@@ -203,6 +231,14 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
       if (p[k].w != q[k].w) return -1;
       if (p[k].r == q[k].r) continue;
       if (p[k].r.k == R_CONST && q[k].r.k == R_CONST) return 0;
+      Ref bp, bq;
+      uint32_t op_[8], oq[8];
+      sum_form(p[k].r, p[k].w, &bp, op_);
+      sum_form(q[k].r, q[k].w, &bq, oq);
+      if (bp == bq) {
+        if (memcmp(op_, oq, sizeof(op_)) != 0) return 0;
+        continue;
+      }
       all = false;
     }
     return all ? 1 : -1;

@@ -491,3 +491,47 @@ def test_c_oracle_contract_states_match_python_oracle():
         rows = [[S.limbs_to_int(cands[s, k, v]) for v in range(nv)] for k in range(12)]
         assert got[s] == S.first_sat(nl, cl, rows), s
     B.close()
+
+
+def test_uf_symbolic_base_offsets_fold():
+    """Selects at base + constant (a calldata word at a symbolic ABI offset): two indices
+    of one base compare by their constant offsets at lowering time (mod 2^256, nested
+    sums flattened), so only selects of different bases are tested at run time."""
+    F = 4
+    nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]     # B, y
+    consts = [4, 36, 2 ** 256 - 1, 0]
+    nl += [[S.CONST, 256, -1, -1, -1, k, 0] for k in range(4)]               # 2..5
+    nl.append([S.ADD, 256, 2, 0, -1, 0, 0])                                   # 6: 4 + B
+    nl.append([S.ADD, 256, 3, 0, -1, 0, 0])                                   # 7: 36 + B
+    apps, fresh = [], 10
+    for base in (6, 7):
+        for i in range(0, 40, 3):
+            nl.append([S.CONST, 256, -1, -1, -1, len(consts), 0])
+            consts.append(i)
+            nl.append([S.ADD, 256, base, len(nl) - 1, -1, 0, 0])             # (c + B) + i
+            nl.append([S.UFAPP, 8, len(nl) - 1, -1, -1, F, fresh])
+            fresh += 1
+            apps.append(len(nl) - 1)
+    nl.append([S.ADD, 256, 0, 4, -1, 0, 0])                                   # B + (2^256 - 1) = B - 1
+    nl.append([S.UFAPP, 8, len(nl) - 1, -1, -1, F, fresh])
+    apps.append(len(nl) - 1)
+    nl.append([S.UFAPP, 8, 1, -1, -1, F, fresh + 1])                          # f(y): unknown vs all
+    apps.append(len(nl) - 1)
+    acc = apps[0]
+    for a in apps[1:]:
+        nl.append([S.XOR, 8, acc, a, -1, 0, 0])
+        acc = len(nl) - 1
+    nl.append([S.CONST, 8, -1, -1, -1, len(consts), 0])
+    consts.append(0x5A)
+    nl.append([S.EQ, 1, acc, len(nl) - 1, -1, 0, 0])
+    rng = np.random.default_rng(3)
+    rows = []
+    for _ in range(30):
+        b = int(rng.integers(0, 2 ** 62))
+        y = b + int(rng.choice([4, 36, 40, 3, 0, 7, 100])) if rng.random() < 0.7 else int(rng.integers(0, 2 ** 62))
+        rows.append([b, y] + [0] * 8 + [int(rng.integers(0, 256)) for _ in range(fresh + 2 - 10)])
+    words, po, status = _check_states([(nl, consts)], [rows])
+    assert status[0] == N.ST_OK
+    # every select has base B except f(y): only f(y) is tested against the others at run time
+    n_eq = sum(1 for k in range(int(words[0])) if int(words[4 + 4 * k]) & 0xFF == S.EQ)
+    assert n_eq <= 2 * len(apps) + 2, n_eq

@@ -1146,13 +1146,22 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
                                      uint32_t n_decide, uint32_t *cands, int8_t *out) {
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets || !cands)) || every == 0u)
     return MGP_E_ARG;
-#pragma omp parallel for schedule(dynamic, 8)
-  for (int64_t st = 0; st < (int64_t)n_states; ++st) {
+  // one task per (state, decision row) and one per state for its plain rows, so that a
+  // small batch (LASER forks two states per JUMPI, svm.py:251-255) spreads its decision
+  // rows over the host threads; each task re-runs the state's base analysis, which is
+  // one analysis against the n_vars analyses of a decision row
+  uint32_t n_dec_rows = 0;
+  for (uint32_t c = 0, row = 0; c < n_cand && row < n_decide; c += every, ++row) ++n_dec_rows;
+  const int64_t per_state = (int64_t)n_dec_rows + 1;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t task = 0; task < (int64_t)n_states * per_state; ++task) {
+    const int64_t st = task / per_state;
+    const uint32_t task_row = (uint32_t)(task % per_state);  // < n_dec_rows: that decision row
     const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
     const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
     State s;
     const int r = refute_one(nodes + n0, n1 - n0, consts + 8ull * c0, c1 - c0, max_passes, &s);
-    out[st] = (int8_t)r;
+    if (task_row == n_dec_rows) out[st] = (int8_t)r;
     if (r != 0) continue;
     // (var slot, width, abstract value): VAR nodes and the fresh value of UF applications
     std::vector<uint32_t> slot, width;
@@ -1196,6 +1205,7 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
     const uint32_t passes = std::min(max_passes ? max_passes : 16u, 6u);
     for (uint32_t c = 0, row = 0; c < n_cand; c += every, ++row) {
       uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
+      if (task_row < n_dec_rows ? row != task_row : row < n_dec_rows) continue;
       if (row < n_decide) {
         State d = s;
         for (size_t kk = 0; kk < slot.size(); ++kk) {

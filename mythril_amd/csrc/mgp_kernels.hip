@@ -685,7 +685,9 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
     const uint64_t *__restrict__ alias_off, const uint32_t *__restrict__ aliases,
     const uint64_t *__restrict__ const_off, const uint32_t *__restrict__ consts, const uint32_t *__restrict__ fixed,
     uint32_t n_fixed, const int32_t *__restrict__ parent_idx, const uint32_t *__restrict__ pvals,
-    const uint8_t *__restrict__ pmask, const uint32_t *__restrict__ dom, uint4 *__restrict__ out) {
+    const uint8_t *__restrict__ pmask, const uint32_t *__restrict__ dom, const uint32_t *__restrict__ asrc_off,
+    const uint32_t *__restrict__ asrc, const uint32_t *__restrict__ wcls, const uint32_t *__restrict__ wlist,
+    uint4 *__restrict__ out) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (uint64_t)n_states * n_cand) return;
   const uint64_t s = g / n_cand;
@@ -764,24 +766,31 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       draw(v, &r, &pick);
       const bool pend = !(r < 0.35 && n_hint(v)) && !(r < 0.60 && n_pool) && r < 0.75;
       if (!pend) continue;
-      uint64_t n_src = 0;
-      for (uint64_t a = 0; a < na; ++a)
-        if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V) ++n_src;
+      // x == y alias sources of v in alias order, and the equal-width variables in index
+      // order, from the host's per-variable tables (mgp_fe_alias_tables): O(log V) per
+      // variable instead of the host generator's scans, same choice
+      const uint32_t *srcs = asrc + asrc_off[v0 + v];
+      const uint32_t n_src = asrc_off[v0 + v + 1] - asrc_off[v0 + v];
       const uint64_t k = fe_mix(seed ^ 0x5A5A5A5Aull ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
       if (n_src) {
-        uint64_t want = k % n_src;
-        for (uint64_t a = 0; a < na; ++a)
-          if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V && want-- == 0) {
-            R.copy((uint32_t)v, aliases[2 * (a0 + a) + 1]);
-            break;
-          }
+        R.copy((uint32_t)v, srcs[k % n_src]);
         continue;
       }
-      // the next equal-width variable from a random start (mgp_make_candidates)
-      for (uint64_t t = 0, st0 = k % V; t < V; ++t) {
-        const uint64_t u = (st0 + t) % V;
-        if (u != v && var_width[v0 + u] == var_width[v0 + v]) {
-          R.copy((uint32_t)v, (uint32_t)u);
+      // the next equal-width variable from a random start: the first u != v at or after
+      // st0 (circularly) in the sorted list of v's width class
+      const uint32_t *L = wlist + wcls[2 * (v0 + v)];
+      const uint32_t len = wcls[2 * (v0 + v) + 1];
+      const uint32_t st0 = (uint32_t)(k % V);
+      uint32_t lo = 0, hi = len;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (L[mid] < st0) lo = mid + 1;
+        else hi = mid;
+      }
+      for (uint32_t t = 0; t < 2 && t < len; ++t) {
+        const uint32_t u = L[(lo + t) % len];
+        if (u != v) {
+          R.copy((uint32_t)v, u);
           break;
         }
       }
@@ -1115,14 +1124,16 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
                                const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
-                               const uint8_t *pmask, const uint32_t *dom, uint32_t *out, hipStream_t st) {
+                               const uint8_t *pmask, const uint32_t *dom, const uint32_t *asrc_off,
+                               const uint32_t *asrc, const uint32_t *wcls, const uint32_t *wlist, uint32_t *out,
+                               hipStream_t st) {
   const uint64_t total = (uint64_t)n_states * n_cand;
   if (total == 0) return hipSuccess;
   const uint64_t blocks = (total + 255) / 256;
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mgp_fe_cands_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, n_states, n_cand, n_vars, seed,
                      var_off, var_width, var_kind, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed,
-                     parent_idx, pvals, pmask, dom, reinterpret_cast<uint4 *>(out));
+                     parent_idx, pvals, pmask, dom, asrc_off, asrc, wcls, wlist, reinterpret_cast<uint4 *>(out));
   return hipGetLastError();
 }
 

@@ -43,7 +43,9 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
                                const uint32_t *hints, const uint64_t *alias_off, const uint32_t *aliases,
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
-                               const uint8_t *pmask, const uint32_t *dom, uint32_t *out, hipStream_t st);
+                               const uint8_t *pmask, const uint32_t *dom, const uint32_t *asrc_off,
+                               const uint32_t *asrc, const uint32_t *wcls, const uint32_t *wlist, uint32_t *out,
+                               hipStream_t st);
 int mgp_fe_get(const mgp_fe_batch *batch, int field, const void **ptr, uint64_t *count);
 int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device);
 int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg);
@@ -69,6 +71,18 @@ Arr get(const mgp_fe_batch *B, int f) {
 struct PipeBufs {
   void *p[16] = {};
   size_t cap[16] = {};
+  void *host = nullptr;  // pinned staging: one upload and one download per call (pageable
+  size_t hcap = 0;       // hipMemcpyAsync is a blocking staged copy, ~0.4 ms each)
+  hipError_t ensure_host(size_t bytes) {
+    if (bytes <= hcap) return hipSuccess;
+    if (host) (void)hipHostFree(host);
+    host = nullptr;
+    hcap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1u << 20);
+    hipError_t e = hipHostMalloc(&host, want, hipHostMallocDefault);
+    if (e == hipSuccess) hcap = want;
+    return e;
+  }
   hipError_t ensure(int i, size_t bytes) {
     if (bytes <= cap[i]) return hipSuccess;
     if (p[i]) (void)hipFree(p[i]);
@@ -88,6 +102,52 @@ std::unordered_map<mgp_ctx *, PipeBufs> &bufs_of() {
 
 enum { B_WORDS, B_OFFS, B_ORDER, B_CANDS, B_FIRST, B_WIT, B_PART, B_TABLES, B_NUM };
 
+// Per-variable tables of the device candidate generator (mgp_fe_cands_kernel), so that
+// its alias step is a lookup instead of the host generator's scans: asrc_off / asrc =
+// the x == y alias sources of each variable (global variable index, CSR, alias order,
+// sources inside the state), wcls[2g] / wcls[2g+1] = offset / length in wlist of the
+// sorted local indices of the variables with g's width in its state
+struct AliasTables {
+  std::vector<uint32_t> asrc_off, asrc, wcls, wlist;
+};
+void alias_tables(uint32_t n_states, const uint64_t *vo, const uint32_t *vw, const uint64_t *ao,
+                  const uint32_t *al, AliasTables &T) {
+  const uint64_t nv = n_states ? vo[n_states] : 0;
+  T.asrc_off.assign(nv + 1, 0u);
+  T.wcls.assign(2 * nv + 2, 0u);
+  T.asrc.clear();
+  T.wlist.clear();
+  for (uint32_t s = 0; s < n_states; ++s) {
+    const uint64_t v0 = vo[s], V = vo[s + 1] - v0;
+    for (uint64_t a = ao[s]; a < ao[s + 1]; ++a)
+      if (al[2 * a] < V && al[2 * a + 1] < V) T.asrc_off[v0 + al[2 * a] + 1]++;
+  }
+  for (uint64_t g = 0; g < nv; ++g) T.asrc_off[g + 1] += T.asrc_off[g];
+  T.asrc.assign(T.asrc_off[nv] ? T.asrc_off[nv] : 1u, 0u);
+  std::vector<uint32_t> fill(T.asrc_off.begin(), T.asrc_off.end() - 1);
+  std::vector<std::pair<uint32_t, uint32_t>> byw;
+  for (uint32_t s = 0; s < n_states; ++s) {
+    const uint64_t v0 = vo[s], V = vo[s + 1] - v0;
+    for (uint64_t a = ao[s]; a < ao[s + 1]; ++a)
+      if (al[2 * a] < V && al[2 * a + 1] < V) T.asrc[fill[v0 + al[2 * a]]++] = al[2 * a + 1];
+    byw.clear();
+    for (uint64_t v = 0; v < V; ++v) byw.push_back({vw[v0 + v], (uint32_t)v});
+    std::sort(byw.begin(), byw.end());
+    for (size_t i = 0; i < byw.size();) {
+      size_t j = i;
+      while (j < byw.size() && byw[j].first == byw[i].first) ++j;
+      const uint32_t off = (uint32_t)T.wlist.size();
+      for (size_t k = i; k < j; ++k) T.wlist.push_back(byw[k].second);
+      for (size_t k = i; k < j; ++k) {
+        T.wcls[2 * (v0 + byw[k].second)] = off;
+        T.wcls[2 * (v0 + byw[k].second) + 1] = (uint32_t)(j - i);
+      }
+      i = j;
+    }
+  }
+  if (T.wlist.empty()) T.wlist.push_back(0u);
+}
+
 }  // namespace
 
 extern "C" {
@@ -98,6 +158,7 @@ void mgp_pipeline_release(mgp_ctx *ctx) {
   if (it == m.end()) return;
   for (int i = 0; i < 16; ++i)
     if (it->second.p[i]) (void)hipFree(it->second.p[i]);
+  if (it->second.host) (void)hipHostFree(it->second.host);
   m.erase(it);
 }
 
@@ -205,61 +266,69 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   // one table buffer: var_off | var_width | hint_off | hints | alias_off | aliases | const_off | consts |
   // fixed | parent_idx | pvals | pmask | var_kind | dom, each 256-B aligned
   // (mgp_fe_get counts elements of each array: u32 limbs for consts / hints / aliases)
-  const size_t sizes[14] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+  AliasTables AT;
+  alias_tables(n_states, vo, (const uint32_t *)vwidth.p, (const uint64_t *)aoff.p, (const uint32_t *)aliases.p, AT);
+  const size_t sizes[18] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
                             coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32,
-                            (size_t)n_states * 4, pvals.size() * 4, pmask.size(), vkind.n, dom.size() * 4};
-  const void *srcs[14] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
-                          pidx.data(), pvals.data(), pmask.data(), vkind.p, dom.data()};
-  size_t at[15];
+                            (size_t)n_states * 4, pvals.size() * 4, pmask.size(), vkind.n, dom.size() * 4,
+                            AT.asrc_off.size() * 4, AT.asrc.size() * 4, AT.wcls.size() * 4, AT.wlist.size() * 4};
+  const void *srcs[18] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
+                          pidx.data(), pvals.data(), pmask.data(), vkind.p, dom.data(),
+                          AT.asrc_off.data(), AT.asrc.data(), AT.wcls.data(), AT.wlist.data()};
+  // one upload: programs | program offsets | launch order | the 18 tables, 256-B aligned
+  const size_t pre[3] = {words.size() * 4u, offs.size() * 8u, (size_t)n_states * 4u};
+  size_t at[22];
   at[0] = 0;
-  for (int i = 0; i < 14; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
-  std::vector<uint8_t> stage(at[14]);
-  for (int i = 0; i < 14; ++i)
-    if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
-  if (e == hipSuccess) e = D.ensure(B_WORDS, words.size() * 4u);
-  if (e == hipSuccess) e = D.ensure(B_OFFS, offs.size() * 8u);
-  if (e == hipSuccess) e = D.ensure(B_ORDER, (size_t)n_states * 4u);
+  for (int i = 0; i < 3; ++i) at[i + 1] = (at[i] + pre[i] + 255) & ~(size_t)255;
+  for (int i = 0; i < 18; ++i) at[i + 4] = (at[i + 3] + sizes[i] + 255) & ~(size_t)255;
+  const size_t up = at[21];
+  const size_t wit_bytes = (size_t)n_states * n_vars * 32u, first_bytes = ((size_t)n_states * 4u + 255) & ~(size_t)255;
+  if (e == hipSuccess) e = D.ensure_host(std::max(up, first_bytes + (out_witness ? wit_bytes : 0)));
+  if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+  uint8_t *H = (uint8_t *)D.host;
+  memcpy(H + at[0], words.data(), pre[0]);
+  memcpy(H + at[1], offs.data(), pre[1]);
+  memcpy(H + at[2], order.data(), pre[2]);
+  for (int i = 0; i < 18; ++i)
+    if (sizes[i] && srcs[i]) memcpy(H + at[i + 3], srcs[i], sizes[i]);
   if (e == hipSuccess) e = D.ensure(B_CANDS, cand_bytes);
   if (e == hipSuccess) e = D.ensure(B_FIRST, (size_t)n_states * 4u);
-  if (e == hipSuccess) e = D.ensure(B_WIT, (size_t)n_states * n_vars * 32u);
+  if (e == hipSuccess) e = D.ensure(B_WIT, wit_bytes);
   if (e == hipSuccess) e = D.ensure(B_PART, (size_t)n_states * n_chunks * 4u);
-  if (e == hipSuccess) e = D.ensure(B_TABLES, at[14]);
-  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_WORDS], words.data(), words.size() * 4u, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_OFFS], offs.data(), offs.size() * 8u, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(D.p[B_ORDER], order.data(), (size_t)n_states * 4u, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], stage.data(), at[14], hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = D.ensure(B_TABLES, up);
+  if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], H, up, hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
-  const uint8_t *tb = (const uint8_t *)D.p[B_TABLES];
-  e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
-                          (const uint32_t *)(tb + at[1]), vkind.n ? (const uint8_t *)(tb + at[12]) : nullptr,
-                          (const uint64_t *)(tb + at[2]),
-                          (const uint32_t *)(tb + at[3]), (const uint64_t *)(tb + at[4]),
-                          (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
-                          (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed,
-                          (const int32_t *)(tb + at[9]), (const uint32_t *)(tb + at[10]),
-                          (const uint8_t *)(tb + at[11]), dom.empty() ? nullptr : (const uint32_t *)(tb + at[13]),
+  const uint8_t *base = (const uint8_t *)D.p[B_TABLES], *tb = base + at[3];
+  auto T = [&](int i) { return tb + (at[i + 3] - at[3]); };
+  e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)T(0), (const uint32_t *)T(1),
+                          vkind.n ? (const uint8_t *)T(12) : nullptr, (const uint64_t *)T(2), (const uint32_t *)T(3),
+                          (const uint64_t *)T(4), (const uint32_t *)T(5), (const uint64_t *)T(6),
+                          (const uint32_t *)T(7), (const uint32_t *)T(8), n_fixed, (const int32_t *)T(9),
+                          (const uint32_t *)T(10), (const uint8_t *)T(11),
+                          dom.empty() ? nullptr : (const uint32_t *)T(13), (const uint32_t *)T(14),
+                          (const uint32_t *)T(15), (const uint32_t *)T(16), (const uint32_t *)T(17),
                           (uint32_t *)D.p[B_CANDS], st);
   if (e == hipSuccess) e = hipMemsetAsync(D.p[B_PART], 0x7E, (size_t)n_states * n_chunks * 4u, st);
   if (e == hipSuccess)
-    e = mgp_launch_eval((const uint32_t *)D.p[B_WORDS], (const uint64_t *)D.p[B_OFFS], n_states,
+    e = mgp_launch_eval((const uint32_t *)(base + at[0]), (const uint64_t *)(base + at[1]), n_states,
                         (const uint32_t *)D.p[B_CANDS], n_cand, n_vars, max_slots, (int32_t *)D.p[B_FIRST],
-                        (uint32_t *)D.p[B_WIT], (int32_t *)D.p[B_PART], (const uint32_t *)D.p[B_ORDER],
+                        (uint32_t *)D.p[B_WIT], (int32_t *)D.p[B_PART], (const uint32_t *)(base + at[2]),
                         bounds.data(), bslots.data(), (uint32_t)nb, st);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(out_first, D.p[B_FIRST], (size_t)n_states * 4u, hipMemcpyDeviceToHost, st);
+  // one download into the pinned buffer (the upload has been consumed by then: same stream)
+  if (e == hipSuccess) e = hipMemcpyAsync(H, D.p[B_FIRST], (size_t)n_states * 4u, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && out_witness)
+    e = hipMemcpyAsync(H + first_bytes, D.p[B_WIT], wit_bytes, hipMemcpyDeviceToHost, st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
   lap(2);
   e = hipStreamSynchronize(st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
   lap(3);
-  // 5. witnesses of the SAT states
+  // 5. first-SAT words and the witnesses of the SAT states
+  memcpy(out_first, H, (size_t)n_states * 4u);
   if (out_witness) {
-    std::vector<uint32_t> w((size_t)n_states * n_vars * 8u);
-    e = hipMemcpy(w.data(), D.p[B_WIT], w.size() * 4u, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+    const uint32_t *w = (const uint32_t *)(H + first_bytes);
     for (uint32_t s = 0; s < n_states; ++s)
-      if (out_first[s] >= 0) memcpy(out_witness + (size_t)s * user_vars * 8u, w.data() + (size_t)s * n_vars * 8u,
+      if (out_first[s] >= 0) memcpy(out_witness + (size_t)s * user_vars * 8u, w + (size_t)s * n_vars * 8u,
                                     (size_t)user_vars * 32u);
   }
   for (uint32_t s = 0; s < n_states; ++s)
@@ -284,23 +353,28 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
   mgp_ctx_stream(ctx, &stp, &dev);
   hipStream_t st = (hipStream_t)stp;
   static const uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const size_t sizes[11] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+  AliasTables AT;
+  alias_tables(n_states, (const uint64_t *)voff.p, (const uint32_t *)vwidth.p, (const uint64_t *)aoff.p,
+               (const uint32_t *)aliases.p, AT);
+  const size_t sizes[15] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
                             coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32, vkind.n,
-                            dom ? (size_t)((const uint64_t *)voff.p)[n_states] * 33u * 4u : 0};
-  const void *srcs[11] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
-                          consts.n ? consts.p : zero8, fixed_pool, vkind.p, dom};
-  size_t at[12];
+                            dom ? (size_t)((const uint64_t *)voff.p)[n_states] * 33u * 4u : 0,
+                            AT.asrc_off.size() * 4, AT.asrc.size() * 4, AT.wcls.size() * 4, AT.wlist.size() * 4};
+  const void *srcs[15] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
+                          consts.n ? consts.p : zero8, fixed_pool, vkind.p, dom,
+                          AT.asrc_off.data(), AT.asrc.data(), AT.wcls.data(), AT.wlist.data()};
+  size_t at[16];
   at[0] = 0;
-  for (int i = 0; i < 11; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
-  std::vector<uint8_t> stage(at[11]);
-  for (int i = 0; i < 11; ++i)
+  for (int i = 0; i < 15; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[15]);
+  for (int i = 0; i < 15; ++i)
     if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
   const size_t cb = (size_t)n_states * n_cand * n_vars * 32u;
   void *dt = nullptr, *dc = nullptr;
   hipError_t e = hipSetDevice(dev);
-  if (e == hipSuccess) e = hipMalloc(&dt, at[11]);
+  if (e == hipSuccess) e = hipMalloc(&dt, at[15]);
   if (e == hipSuccess) e = hipMalloc(&dc, cb);
-  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[11], hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[15], hipMemcpyHostToDevice, st);
   const uint8_t *tb = (const uint8_t *)dt;
   if (e == hipSuccess)
     e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
@@ -309,7 +383,9 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
                             (const uint32_t *)(tb + at[3]), (const uint64_t *)(tb + at[4]),
                             (const uint32_t *)(tb + at[5]), (const uint64_t *)(tb + at[6]),
                             (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed, nullptr,
-                            nullptr, nullptr, dom ? (const uint32_t *)(tb + at[10]) : nullptr, (uint32_t *)dc, st);
+                            nullptr, nullptr, dom ? (const uint32_t *)(tb + at[10]) : nullptr,
+                            (const uint32_t *)(tb + at[11]), (const uint32_t *)(tb + at[12]),
+                            (const uint32_t *)(tb + at[13]), (const uint32_t *)(tb + at[14]), (uint32_t *)dc, st);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dc, cb, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (dt) (void)hipFree(dt);

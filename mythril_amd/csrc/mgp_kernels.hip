@@ -819,18 +819,35 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
         R.put((uint32_t)v, xv.w);
       }
   }
-  for (uint64_t v = 0; v < V; ++v) {  // pinned constants, then the mask to the slot width
+  for (uint64_t v = 0; v < V; ++v)  // pinned constants
     if (var_kind && var_kind[v0 + v] == 2 && n_hint(v)) R.put((uint32_t)v, hint(v, 0));
-    const uint32_t w = var_width[v0 + v];
-    if (w >= 256) continue;
-    for (uint32_t h = 0; h < 2; ++h) {
-      uint4 q = *R.at((uint32_t)v, h);
-      uint32_t *e = reinterpret_cast<uint32_t *>(&q);
-      for (int l = 0; l < 4; ++l) {
-        const int lo = 32 * (4 * (int)h + l);
-        e[l] &= (int)w >= lo + 32 ? 0xFFFFFFFFu : ((int)w <= lo ? 0u : ((1u << (w - lo)) - 1u));
+  // the mask to the slot width, 8 variables per round trip: their 16 loads are
+  // independent, so a small batch (a few waves on the chip) pays one load latency per
+  // 8 variables instead of one per 16 bytes
+  constexpr uint32_t kB = 8;
+  for (uint64_t vb = 0; vb < V; vb += kB) {
+    uint4 q[kB][2];
+    uint32_t w[kB];
+    const uint32_t nb = (uint32_t)((V - vb) < kB ? (V - vb) : kB);
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j) {
+      w[j] = j < nb ? var_width[v0 + vb + j] : 256u;
+      if (w[j] < 256u) {
+        q[j][0] = *R.at((uint32_t)(vb + j), 0);
+        q[j][1] = *R.at((uint32_t)(vb + j), 1);
       }
-      *R.at((uint32_t)v, h) = q;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kB; ++j) {
+      if (w[j] >= 256u) continue;
+      for (uint32_t h = 0; h < 2; ++h) {
+        uint32_t *e = reinterpret_cast<uint32_t *>(&q[j][h]);
+        for (int l = 0; l < 4; ++l) {
+          const int lo = 32 * (4 * (int)h + l);
+          e[l] &= (int)w[j] >= lo + 32 ? 0xFFFFFFFFu : ((int)w[j] <= lo ? 0u : ((1u << (w[j] - lo)) - 1u));
+        }
+        *R.at((uint32_t)(vb + j), h) = q[j][h];
+      }
     }
   }
 }

@@ -135,8 +135,465 @@ Lowered unsupported_at(int line) {
 
 #define unsupported() unsupported_at(__LINE__)
 
+// Lists of u32 per key (CSR) from (key, value) pairs in emission order: one allocation
+// instead of one vector per instruction (20 000-instruction programs)
+struct Lists {
+  std::vector<uint32_t> off, val;
+  const uint32_t *begin(uint32_t k) const { return val.data() + off[k]; }
+  const uint32_t *end(uint32_t k) const { return val.data() + off[k + 1]; }
+};
+Lists make_lists(uint32_t n_keys, const std::vector<std::pair<uint32_t, uint32_t>> &kv) {
+  Lists L;
+  L.off.assign((size_t)n_keys + 1, 0u);
+  for (const auto &p : kv) L.off[p.first + 1]++;
+  for (uint32_t k = 0; k < n_keys; ++k) L.off[k + 1] += L.off[k];
+  L.val.resize(kv.size());
+  std::vector<uint32_t> pos(L.off.begin(), L.off.end() - 1);
+  for (const auto &p : kv) L.val[pos[p.first]++] = p.second;
+  return L;
+}
+
+// Scheduling, Bool demotion, liveness, slot allocation and emission of one prepared
+// state (lower_one runs it once per schedule it tries on a copy of the prepared state).
+Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
+  // ------------------------------------------- register-pressure scheduling
+  // sched 1: depth-first post-order from the root, operand with the larger
+  //          Sethi-Ullman need first (trees need O(log n) live values and a
+  //          parent usually follows its last operand: accumulator forwarding);
+  // sched 2: greedy list scheduling — among ready instructions take the one
+  //          that frees the most BV values (last use) minus the one it creates,
+  //          ties to the one reading the most recent result.
+  // The caller keeps whichever schedule needs the fewest LDS slots.
+  if (sched != 0) {
+    const uint32_t n0 = (uint32_t)S.ins.size();
+    auto kids = [&](uint32_t t, uint32_t out[3]) -> int {
+      int k = 0;
+      const VIns &I = S.ins[t];
+      for (const Ref *r : {&I.a, &I.b, &I.c})
+        if (r->k == R_INS) {
+          bool dup = false;
+          for (int j = 0; j < k; ++j) dup |= out[j] == r->idx;
+          if (!dup) out[k++] = r->idx;
+        }
+      return k;
+    };
+    std::vector<uint32_t> order;
+    order.reserve(n0);
+    if (sched == 1) {
+      std::vector<uint32_t> need(n0, 1);
+      for (uint32_t t = 0; t < n0; ++t) {
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        uint32_t nd[3] = {0, 0, 0};
+        for (int i = 0; i < k; ++i) nd[i] = need[ch[i]];
+        std::sort(nd, nd + k, [](uint32_t x, uint32_t y) { return x > y; });
+        uint32_t m = 1;
+        for (int i = 0; i < k; ++i) m = std::max(m, nd[i] + (uint32_t)i);
+        need[t] = m;
+      }
+      std::vector<uint8_t> state(n0, 0);  // 0 new, 1 expanded, 2 emitted
+      std::vector<uint32_t> stack;
+      if (root.k == R_INS) stack.push_back(root.idx);
+      while (!stack.empty()) {
+        const uint32_t t = stack.back();
+        if (state[t] == 2) { stack.pop_back(); continue; }
+        if (state[t] == 1) { state[t] = 2; order.push_back(t); stack.pop_back(); continue; }
+        state[t] = 1;
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        std::sort(ch, ch + k, [&](uint32_t x, uint32_t y) { return need[x] < need[y]; });
+        for (int i = 0; i < k; ++i)
+          if (state[ch[i]] == 0) stack.push_back(ch[i]);
+      }
+    } else {
+      // the greedy list scheduler rescans the ready list per step (quadratic): not worth it
+      // for very long programs, whose other schedules are kept instead
+      if (n0 > 1536) return unsupported();
+      std::vector<uint32_t> uses(n0, 0), pending(n0, 0);
+      std::vector<std::vector<uint32_t>> users(n0);
+      for (uint32_t t = 0; t < n0; ++t) {
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        pending[t] = (uint32_t)k;
+        for (int i = 0; i < k; ++i) {
+          uses[ch[i]]++;
+          users[ch[i]].push_back(t);
+        }
+      }
+      std::vector<uint32_t> ready;
+      for (uint32_t t = 0; t < n0; ++t)
+        if (pending[t] == 0) ready.push_back(t);
+      int64_t last = -1;
+      while (!ready.empty()) {
+        size_t best = 0;
+        int best_score = -1000, best_recent = -1;
+        for (size_t r = 0; r < ready.size(); ++r) {
+          const uint32_t t = ready[r];
+          uint32_t ch[3];
+          const int k = kids(t, ch);
+          int score = 0, recent = 0;
+          for (int i = 0; i < k; ++i) {
+            if (!S.ins[ch[i]].is_bool && uses[ch[i]] == 1) score += 1;
+            if ((int64_t)ch[i] == last) recent = 1;
+          }
+          if (!S.ins[t].is_bool && !users[t].empty()) score -= 1;
+          if (score > best_score || (score == best_score && recent > best_recent)) {
+            best = r, best_score = score, best_recent = recent;
+          }
+        }
+        const uint32_t t = ready[best];
+        ready.erase(ready.begin() + (ptrdiff_t)best);
+        order.push_back(t);
+        last = t;
+        uint32_t ch[3];
+        const int k = kids(t, ch);
+        for (int i = 0; i < k; ++i) uses[ch[i]]--;
+        for (uint32_t u : users[t])
+          if (--pending[u] == 0) ready.push_back(u);
+      }
+    }
+    if (order.size() == n0) {
+      std::vector<uint32_t> remap(n0);
+      for (uint32_t i = 0; i < n0; ++i) remap[order[i]] = i;
+      std::vector<VIns> re(n0);
+      for (uint32_t i = 0; i < n0; ++i) {
+        VIns I = S.ins[order[i]];
+        for (Ref *r : {&I.a, &I.b, &I.c})
+          if (r->k == R_INS) r->idx = remap[r->idx];
+        re[i] = I;
+      }
+      S.ins.swap(re);
+      if (root.k == R_INS) root.idx = remap[root.idx];
+    }
+  }
+
+  // ------------------------------------------------ Bool pressure: demotion
+  // At most MGP_BOOL_LIVE Bool values are live at once (the gfx950 interpreter's Bool
+  // registers).  While the schedule needs more, the live Bool whose next read is
+  // farthest becomes a 1-bit BV value: D = ITE(b, 1, 0) right after its definition and
+  // EQ(D, 1) right before each reader.  BV values can spill, Bools cannot.
+  {
+    auto const_ref = [&](uint32_t v) {
+      ConstKey k;
+      memset(k.w, 0, sizeof(k.w));
+      k.w[0] = v;
+      Ref r;
+      r.k = R_CONST;
+      for (uint32_t i = 0; i < S.pool.size(); ++i)
+        if (S.pool[i] == k) {
+          r.idx = i;
+          return r;
+        }
+      r.idx = (uint32_t)S.pool.size();
+      S.pool.push_back(k);
+      return r;
+    };
+    // the Bool operand positions of an instruction (ITE: the condition only)
+    auto bool_refs = [](VIns &I, Ref *out[3]) -> int {
+      if (op_takes_bools(I.op)) {
+        out[0] = &I.a, out[1] = &I.b, out[2] = &I.c;
+        return 3;
+      }
+      if (I.op == MGP_OP_ITE) {
+        out[0] = &I.a;
+        return 1;
+      }
+      return 0;
+    };
+    // one pass over the schedule plans every demotion (victim: the live Bool read farthest
+    // in the future; a demoted Bool's readers need one short-lived EQ bit each, right
+    // before them), then one rewrite applies them
+    const uint32_t n0 = (uint32_t)S.ins.size();
+    std::vector<int64_t> lu(n0, -1);
+    std::vector<std::pair<uint32_t, uint32_t>> kv;
+    std::vector<int64_t> last_t(n0, -1);
+    for (uint32_t t = 0; t < n0; ++t) {
+      Ref *br[3];
+      const int k = bool_refs(S.ins[t], br);
+      for (int i = 0; i < k; ++i)
+        if (br[i]->k == R_INS) {
+          lu[br[i]->idx] = std::max<int64_t>(lu[br[i]->idx], t);
+          if (last_t[br[i]->idx] != (int64_t)t) kv.push_back({br[i]->idx, t}), last_t[br[i]->idx] = t;
+        }
+    }
+    const Lists readers = make_lists(n0, kv);  // readers of each Bool, ascending
+    if (root.k == R_INS) lu[root.idx] = std::max<int64_t>(lu[root.idx], n0);
+    kv.clear();
+    for (uint32_t t = 0; t < n0; ++t)
+      if (S.ins[t].is_bool && lu[t] > (int64_t)t && lu[t] <= (int64_t)n0) kv.push_back({(uint32_t)lu[t], t});
+    const Lists expire_at = make_lists(n0 + 1, kv);
+    std::vector<uint8_t> demoted(n0, 0);
+    bool any = false;
+    std::vector<uint32_t> cur;  // live Bools holding a bit
+    auto next_read = [&](uint32_t v, uint32_t t) -> int64_t {
+      const uint32_t *it = std::lower_bound(readers.begin(v), readers.end(v), t);
+      return it == readers.end(v) ? (int64_t)n0 : (int64_t)*it;
+    };
+    // demote the member of cur read farthest after t (not one t itself reads)
+    auto demote_one = [&](uint32_t t, const uint32_t *keep, int n_keep) -> bool {
+      int64_t best = -1;
+      size_t at = 0;
+      for (size_t j = 0; j < cur.size(); ++j) {
+        bool kept = false;
+        for (int q = 0; q < n_keep; ++q) kept |= keep[q] == cur[j];
+        if (kept) continue;
+        const int64_t nx = next_read(cur[j], t);
+        if (nx > best) best = nx, at = j;
+      }
+      if (best < 0) return false;
+      demoted[cur[at]] = 1;
+      any = true;
+      cur.erase(cur.begin() + (ptrdiff_t)at);
+      return true;
+    };
+    for (uint32_t t = 0; t < n0; ++t) {
+      Ref *br[3];
+      const int k = bool_refs(S.ins[t], br);
+      uint32_t rd[3];
+      int n_rd = 0, transients = 0;
+      for (int i = 0; i < k; ++i)
+        if (br[i]->k == R_INS) {
+          bool dup = false;
+          for (int q = 0; q < n_rd; ++q) dup |= rd[q] == br[i]->idx;
+          if (dup) continue;
+          rd[n_rd++] = br[i]->idx;
+          transients += demoted[br[i]->idx];
+        }
+      while (cur.size() + (size_t)transients > MGP_BOOL_LIVE)
+        if (!demote_one(t, rd, n_rd)) return unsupported();
+      for (const uint32_t *pv = expire_at.begin(t); pv != expire_at.end(t); ++pv) {
+        const uint32_t v = *pv;
+        auto it = std::find(cur.begin(), cur.end(), v);
+        if (it != cur.end()) cur.erase(it);
+      }
+      if (S.ins[t].is_bool && lu[t] > (int64_t)t) {
+        if (cur.size() >= MGP_BOOL_LIVE && !demote_one(t, nullptr, 0)) return unsupported();
+        cur.push_back(t);
+      }
+    }
+    if (any) {
+      const Ref one = const_ref(1u), zero = const_ref(0u);
+      std::vector<VIns> re;
+      re.reserve(n0 + n0 / 4 + 8);
+      std::vector<uint32_t> remap(n0, 0);
+      std::vector<Ref> dref(n0);  // the 1-bit value of a demoted Bool
+      for (uint32_t t = 0; t < n0; ++t) {
+        VIns I = S.ins[t];
+        for (Ref *r : {&I.a, &I.b, &I.c})
+          if (r->k == R_INS) r->idx = remap[r->idx];
+        Ref *br[3], *nr[3];
+        const int k = bool_refs(S.ins[t], br);
+        bool_refs(I, nr);
+        for (int i = 0; i < k; ++i) {
+          if (br[i]->k != R_INS || !demoted[br[i]->idx]) continue;
+          const uint32_t v = br[i]->idx;
+          // one EQ per distinct demoted operand (BITE / BAND may read one Bool twice)
+          Ref e;
+          e.k = R_INS;
+          e.idx = 0xFFFFFFFFu;
+          for (int j = 0; j < i; ++j)
+            if (br[j]->k == R_INS && br[j]->idx == v) e = *nr[j];
+          if (e.idx == 0xFFFFFFFFu) {
+            re.push_back(VIns{MGP_OP_EQ, 1, true, dref[v], one, Ref(), 0});
+            e.idx = (uint32_t)re.size() - 1;
+          }
+          *nr[i] = e;
+        }
+        remap[t] = (uint32_t)re.size();
+        re.push_back(I);
+        if (demoted[t]) {
+          Ref b;
+          b.k = R_INS;
+          b.idx = remap[t];
+          re.push_back(VIns{MGP_OP_ITE, 1, false, b, one, zero, 0});
+          dref[t].k = R_INS;
+          dref[t].idx = (uint32_t)re.size() - 1;
+        }
+      }
+      if (root.k == R_INS) {
+        if (demoted[root.idx]) {
+          re.push_back(VIns{MGP_OP_EQ, 1, true, dref[root.idx], one, Ref(), 0});
+          root.idx = (uint32_t)re.size() - 1;
+        } else {
+          root.idx = remap[root.idx];
+        }
+      }
+      S.ins.swap(re);
+    }
+  }
+
+  // ---------------------------------------------------------- liveness
+  const uint32_t n = (uint32_t)S.ins.size();
+  std::vector<int64_t> last_use(n, -1);       // last instruction reading the value
+  std::vector<uint8_t> needs_slot(n, 0);      // some use cannot be served from ACC
+  std::vector<int64_t> prev_bv(n + 1, -1);    // last BV-producing instruction before t
+  {
+    int64_t last = -1;
+    for (uint32_t t = 0; t < n; ++t) {
+      prev_bv[t] = last;
+      if (!S.ins[t].is_bool) last = t;
+    }
+    prev_bv[n] = last;
+  }
+  auto use = [&](const Ref &r, uint32_t t, bool bool_opnd) {
+    if (r.k != R_INS) return;
+    last_use[r.idx] = std::max<int64_t>(last_use[r.idx], t);
+    if (!bool_opnd && prev_bv[t] != (int64_t)r.idx) needs_slot[r.idx] = 1;
+  };
+  for (uint32_t t = 0; t < n; ++t) {
+    const VIns &I = S.ins[t];
+    if (op_takes_bools(I.op)) {
+      use(I.a, t, true); use(I.b, t, true); use(I.c, t, true);
+    } else if (I.op == MGP_OP_ITE) {
+      use(I.a, t, true); use(I.b, t, false); use(I.c, t, false);
+    } else {
+      use(I.a, t, false); use(I.b, t, false); use(I.c, t, false);
+    }
+  }
+  if (root.k == R_INS) last_use[root.idx] = std::max<int64_t>(last_use[root.idx], n);
+
+  // ---------------------------------------------------------- allocation
+  // LDS slots first (max_slots < MGP_LDS_SLOTS is a test knob that spills earlier), then
+  // spill slots MGP_LDS_SLOTS.. (include/mgp_ir.h), up to MGP_MAX_SLOTS in all
+  const uint32_t slot_cap = std::min<uint32_t>(max_slots ? max_slots : MGP_LDS_SLOTS, MGP_LDS_SLOTS);
+  std::vector<int32_t> loc(n, -1);
+  std::vector<uint32_t> free_slots, free_bools, free_spill;
+  uint32_t next_spill = MGP_LDS_SLOTS;
+  for (int32_t s = (int32_t)slot_cap - 1; s >= 0; --s) free_slots.push_back((uint32_t)s);
+  for (int32_t b = MGP_BOOL_LIVE - 1; b >= 0; --b) free_bools.push_back((uint32_t)b);
+  // fields naming a BV slot, for the access-count renumbering of spilling programs:
+  // (word index, bit shift) of an operand (14-bit index) or of a STORE destination
+  std::vector<std::pair<uint32_t, uint32_t>> slot_fields;
+  std::vector<std::pair<uint32_t, uint32_t>> ekv;
+  for (uint32_t t = 0; t < n; ++t)
+    if (last_use[t] >= 0 && last_use[t] <= (int64_t)n) ekv.push_back({(uint32_t)last_use[t], t});
+  const Lists expire = make_lists(n + 1, ekv);
+  uint32_t slots_used = 0;
+
+  std::vector<uint32_t> out;
+  out.reserve(4 + 4 * n + 8 * S.pool.size() + 4);
+  out.resize(4, 0u);
+
+  auto bv_opnd = [&](const Ref &r, uint32_t t) -> uint32_t {
+    switch (r.k) {
+      case R_VAR: return MGP_OPND(MGP_K_VAR, r.idx);
+      case R_CONST: return MGP_OPND(MGP_K_CONST, r.idx);
+      case R_INS:
+        if (prev_bv[t] == (int64_t)r.idx) return MGP_OPND(MGP_K_ACC, 0);
+        return MGP_OPND(MGP_K_SLOT, (uint32_t)loc[r.idx]);
+      default: return 0;
+    }
+  };
+  auto bool_opnd = [&](const Ref &r) -> uint32_t {
+    if (r.k == R_BOOLC) return r.idx ? MGP_BOOL_TRUE : MGP_BOOL_FALSE;
+    if (r.k == R_INS) return (uint32_t)loc[r.idx];
+    return MGP_BOOL_FALSE;
+  };
+
+  auto in_slot = [&](const Ref &r, uint32_t t) { return r.k == R_INS && prev_bv[t] != (int64_t)r.idx; };
+  uint32_t n_emit = 0;
+  for (uint32_t t = 0; t < n; ++t) {
+    const VIns &I = S.ins[t];
+    uint32_t oa, ob = 0, oc = 0;
+    const uint32_t base = (uint32_t)out.size();
+    if (op_takes_bools(I.op)) {
+      oa = bool_opnd(I.a); ob = bool_opnd(I.b); oc = bool_opnd(I.c);
+    } else if (I.op == MGP_OP_ITE) {
+      oa = bool_opnd(I.a); ob = bv_opnd(I.b, t); oc = bv_opnd(I.c, t);
+      if (in_slot(I.b, t)) slot_fields.push_back({base + 1, 16});
+      if (in_slot(I.c, t)) slot_fields.push_back({base + 2, 0});
+    } else {
+      oa = bv_opnd(I.a, t);
+      ob = I.b.k != R_NONE ? bv_opnd(I.b, t) : 0u;
+      oc = I.c.k != R_NONE ? bv_opnd(I.c, t) : 0u;
+      if (in_slot(I.a, t)) slot_fields.push_back({base + 1, 0});
+      if (I.b.k != R_NONE && in_slot(I.b, t)) slot_fields.push_back({base + 1, 16});
+      if (I.c.k != R_NONE && in_slot(I.c, t)) slot_fields.push_back({base + 2, 0});
+    }
+    // operands read first: free values whose last use is this instruction
+    for (const uint32_t *pv = expire.begin(t); pv != expire.end(t); ++pv) {
+      const uint32_t v = *pv;
+      if (loc[v] < 0) continue;
+      if (S.ins[v].is_bool) free_bools.push_back((uint32_t)loc[v]);
+      else if ((uint32_t)loc[v] >= MGP_LDS_SLOTS) free_spill.push_back((uint32_t)loc[v]);
+      else free_slots.push_back((uint32_t)loc[v]);
+    }
+    uint32_t dst = 0, flags = 0;
+    const bool live = last_use[t] > (int64_t)t;
+    if (I.is_bool) {
+      if (live) {
+        if (free_bools.empty()) return unsupported();
+        dst = free_bools.back();
+        free_bools.pop_back();
+        loc[t] = (int32_t)dst;
+      } else {
+        return unsupported();  // unreachable after DCE
+      }
+    } else if (live && needs_slot[t]) {
+      if (!free_slots.empty()) {
+        dst = free_slots.back();
+        free_slots.pop_back();
+      } else if (!free_spill.empty()) {
+        dst = free_spill.back();
+        free_spill.pop_back();
+      } else {
+        if (next_spill >= MGP_MAX_SLOTS) return unsupported();
+        dst = next_spill++;
+      }
+      loc[t] = (int32_t)dst;
+      slots_used = std::max(slots_used, dst + 1);
+      flags = MGP_INS_STORE;
+      slot_fields.push_back({base, 16});
+    }
+    const uint32_t width_field = (uint32_t)(I.width ? I.width - 1 : 0) & 0xFFu;
+    out.push_back((uint32_t)I.op | (width_field << 8) | (dst << 16) | (flags << 24));
+    out.push_back((oa & 0xFFFFu) | (ob << 16));
+    out.push_back((oc & 0xFFFFu) | ((I.imm & 0xFFFFu) << 16));
+    out.push_back(0u);
+    ++n_emit;
+  }
+  // RET
+  out.push_back((uint32_t)MGP_OP_RET);
+  out.push_back(bool_opnd(root));
+  out.push_back(0u);
+  out.push_back(0u);
+  ++n_emit;
+
+  // a spilling program: slot numbers by access count (reads + stores), most used first,
+  // so that the LDS slots (and the gfx950 interpreter's register slots) hold the hot values
+  static const bool norenum_dbg = getenv("MGP_LOWER_NORENUM") != nullptr;
+  if (slots_used > MGP_LDS_SLOTS && slot_cap == MGP_LDS_SLOTS && !norenum_dbg) {
+    auto field = [&](const std::pair<uint32_t, uint32_t> &f) -> uint32_t {
+      return f.first % 4u == 0u ? (out[f.first] >> 16) & 0xFFu : (out[f.first] >> f.second) & 0x3FFFu;
+    };
+    std::vector<uint32_t> cnt(slots_used, 0), by(slots_used), rank(slots_used);
+    for (const auto &f : slot_fields) cnt[field(f)]++;
+    for (uint32_t s = 0; s < slots_used; ++s) by[s] = s;
+    std::stable_sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return cnt[x] > cnt[y]; });
+    for (uint32_t r = 0; r < slots_used; ++r) rank[by[r]] = r;
+    for (const auto &f : slot_fields) {
+      const uint32_t nw = rank[field(f)];
+      if (f.first % 4u == 0u) out[f.first] = (out[f.first] & ~(0xFFu << 16)) | (nw << 16);
+      else out[f.first] = (out[f.first] & ~(0x3FFFu << f.second)) | (nw << f.second);
+    }
+  }
+
+  out[0] = n_emit;
+  out[1] = (uint32_t)S.pool.size();
+  out[2] = slots_used;
+  out[3] = (uint32_t)MGP_ST_OK | (S.max_var << 8);
+  for (const ConstKey &k : S.pool)
+    for (int l = 0; l < 8; ++l) out.push_back(k.w[l]);
+  while (out.size() % 4) out.push_back(0u);
+  for (int k = 0; k < 4; ++k) out.push_back(0u);  // the kernel prefetches one instruction past RET
+  Lowered L;
+  L.words.swap(out);
+  return L;
+}
+
+
 Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *consts, uint64_t n_consts,
-                  uint32_t max_slots, int sched) {
+                  uint32_t max_slots, const int *scheds, int n_scheds, std::vector<uint32_t> *uops) {
   if (n_nodes == 0) return unsupported();
   LowerState S;
   std::vector<Ref> val(n_nodes);
@@ -672,433 +1129,28 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     S.pool_map.clear();
   }
 
-  // ------------------------------------------- register-pressure scheduling
-  // sched 1: depth-first post-order from the root, operand with the larger
-  //          Sethi-Ullman need first (trees need O(log n) live values and a
-  //          parent usually follows its last operand: accumulator forwarding);
-  // sched 2: greedy list scheduling — among ready instructions take the one
-  //          that frees the most BV values (last use) minus the one it creates,
-  //          ties to the one reading the most recent result.
-  // The caller keeps whichever schedule needs the fewest LDS slots.
-  if (sched != 0) {
-    const uint32_t n0 = (uint32_t)S.ins.size();
-    auto kids = [&](uint32_t t, uint32_t out[3]) -> int {
-      int k = 0;
-      const VIns &I = S.ins[t];
-      for (const Ref *r : {&I.a, &I.b, &I.c})
-        if (r->k == R_INS) {
-          bool dup = false;
-          for (int j = 0; j < k; ++j) dup |= out[j] == r->idx;
-          if (!dup) out[k++] = r->idx;
-        }
-      return k;
-    };
-    std::vector<uint32_t> order;
-    order.reserve(n0);
-    if (sched == 1) {
-      std::vector<uint32_t> need(n0, 1);
-      for (uint32_t t = 0; t < n0; ++t) {
-        uint32_t ch[3];
-        const int k = kids(t, ch);
-        uint32_t nd[3] = {0, 0, 0};
-        for (int i = 0; i < k; ++i) nd[i] = need[ch[i]];
-        std::sort(nd, nd + k, [](uint32_t x, uint32_t y) { return x > y; });
-        uint32_t m = 1;
-        for (int i = 0; i < k; ++i) m = std::max(m, nd[i] + (uint32_t)i);
-        need[t] = m;
-      }
-      std::vector<uint8_t> state(n0, 0);  // 0 new, 1 expanded, 2 emitted
-      std::vector<uint32_t> stack;
-      if (root.k == R_INS) stack.push_back(root.idx);
-      while (!stack.empty()) {
-        const uint32_t t = stack.back();
-        if (state[t] == 2) { stack.pop_back(); continue; }
-        if (state[t] == 1) { state[t] = 2; order.push_back(t); stack.pop_back(); continue; }
-        state[t] = 1;
-        uint32_t ch[3];
-        const int k = kids(t, ch);
-        std::sort(ch, ch + k, [&](uint32_t x, uint32_t y) { return need[x] < need[y]; });
-        for (int i = 0; i < k; ++i)
-          if (state[ch[i]] == 0) stack.push_back(ch[i]);
-      }
-    } else {
-      // the greedy list scheduler rescans the ready list per step (quadratic): not worth it
-      // for very long programs, whose other schedules are kept instead
-      if (n0 > 1536) return unsupported();
-      std::vector<uint32_t> uses(n0, 0), pending(n0, 0);
-      std::vector<std::vector<uint32_t>> users(n0);
-      for (uint32_t t = 0; t < n0; ++t) {
-        uint32_t ch[3];
-        const int k = kids(t, ch);
-        pending[t] = (uint32_t)k;
-        for (int i = 0; i < k; ++i) {
-          uses[ch[i]]++;
-          users[ch[i]].push_back(t);
-        }
-      }
-      std::vector<uint32_t> ready;
-      for (uint32_t t = 0; t < n0; ++t)
-        if (pending[t] == 0) ready.push_back(t);
-      int64_t last = -1;
-      while (!ready.empty()) {
-        size_t best = 0;
-        int best_score = -1000, best_recent = -1;
-        for (size_t r = 0; r < ready.size(); ++r) {
-          const uint32_t t = ready[r];
-          uint32_t ch[3];
-          const int k = kids(t, ch);
-          int score = 0, recent = 0;
-          for (int i = 0; i < k; ++i) {
-            if (!S.ins[ch[i]].is_bool && uses[ch[i]] == 1) score += 1;
-            if ((int64_t)ch[i] == last) recent = 1;
-          }
-          if (!S.ins[t].is_bool && !users[t].empty()) score -= 1;
-          if (score > best_score || (score == best_score && recent > best_recent)) {
-            best = r, best_score = score, best_recent = recent;
-          }
-        }
-        const uint32_t t = ready[best];
-        ready.erase(ready.begin() + (ptrdiff_t)best);
-        order.push_back(t);
-        last = t;
-        uint32_t ch[3];
-        const int k = kids(t, ch);
-        for (int i = 0; i < k; ++i) uses[ch[i]]--;
-        for (uint32_t u : users[t])
-          if (--pending[u] == 0) ready.push_back(u);
-      }
+  // ---------------------------------------------- schedules
+  // The prepared state (expansion, DCE, pool) is shared by every schedule tried; a
+  // schedule only counts if the gfx950 interpreter can run it (uop translation).
+  // Fewer slots wins (occupancy); between spilling programs, fewer instructions (a
+  // spill is a memory access either way, an instruction is issue time).
+  Lowered best;
+  bool have = false;
+  for (int k = 0; k < n_scheds; ++k) {
+    Lowered b = finish_one(S, root, max_slots, scheds[k]);
+    if (b.status != MGP_ST_OK) continue;
+    if (have) {
+      const bool spill = best.words[2] > MGP_LDS_SLOTS || b.words[2] > MGP_LDS_SLOTS;
+      if (spill ? b.words[0] >= best.words[0] : b.words[2] >= best.words[2]) continue;
     }
-    if (order.size() == n0) {
-      std::vector<uint32_t> remap(n0);
-      for (uint32_t i = 0; i < n0; ++i) remap[order[i]] = i;
-      std::vector<VIns> re(n0);
-      for (uint32_t i = 0; i < n0; ++i) {
-        VIns I = S.ins[order[i]];
-        for (Ref *r : {&I.a, &I.b, &I.c})
-          if (r->k == R_INS) r->idx = remap[r->idx];
-        re[i] = I;
-      }
-      S.ins.swap(re);
-      if (root.k == R_INS) root.idx = remap[root.idx];
-    }
+    std::vector<uint32_t> bu;
+    if (mgp_uop_translate(b.words.data(), bu) != 0) continue;
+    best = std::move(b);
+    uops->swap(bu);
+    have = true;
   }
-
-  // ------------------------------------------------ Bool pressure: demotion
-  // At most MGP_BOOL_LIVE Bool values are live at once (the gfx950 interpreter's Bool
-  // registers).  While the schedule needs more, the live Bool whose next read is
-  // farthest becomes a 1-bit BV value: D = ITE(b, 1, 0) right after its definition and
-  // EQ(D, 1) right before each reader.  BV values can spill, Bools cannot.
-  {
-    auto const_ref = [&](uint32_t v) {
-      ConstKey k;
-      memset(k.w, 0, sizeof(k.w));
-      k.w[0] = v;
-      Ref r;
-      r.k = R_CONST;
-      for (uint32_t i = 0; i < S.pool.size(); ++i)
-        if (S.pool[i] == k) {
-          r.idx = i;
-          return r;
-        }
-      r.idx = (uint32_t)S.pool.size();
-      S.pool.push_back(k);
-      return r;
-    };
-    // the Bool operand positions of an instruction (ITE: the condition only)
-    auto bool_refs = [](VIns &I, Ref *out[3]) -> int {
-      if (op_takes_bools(I.op)) {
-        out[0] = &I.a, out[1] = &I.b, out[2] = &I.c;
-        return 3;
-      }
-      if (I.op == MGP_OP_ITE) {
-        out[0] = &I.a;
-        return 1;
-      }
-      return 0;
-    };
-    // one pass over the schedule plans every demotion (victim: the live Bool read farthest
-    // in the future; a demoted Bool's readers need one short-lived EQ bit each, right
-    // before them), then one rewrite applies them
-    const uint32_t n0 = (uint32_t)S.ins.size();
-    std::vector<int64_t> lu(n0, -1);
-    std::vector<std::vector<uint32_t>> readers(n0);
-    for (uint32_t t = 0; t < n0; ++t) {
-      Ref *br[3];
-      const int k = bool_refs(S.ins[t], br);
-      for (int i = 0; i < k; ++i)
-        if (br[i]->k == R_INS) {
-          lu[br[i]->idx] = std::max<int64_t>(lu[br[i]->idx], t);
-          if (readers[br[i]->idx].empty() || readers[br[i]->idx].back() != t) readers[br[i]->idx].push_back(t);
-        }
-    }
-    if (root.k == R_INS) lu[root.idx] = std::max<int64_t>(lu[root.idx], n0);
-    std::vector<std::vector<uint32_t>> expire_at(n0 + 1);
-    for (uint32_t t = 0; t < n0; ++t)
-      if (S.ins[t].is_bool && lu[t] > (int64_t)t && lu[t] <= (int64_t)n0) expire_at[lu[t]].push_back(t);
-    std::vector<uint8_t> demoted(n0, 0);
-    bool any = false;
-    std::vector<uint32_t> cur;  // live Bools holding a bit
-    auto next_read = [&](uint32_t v, uint32_t t) -> int64_t {
-      auto it = std::lower_bound(readers[v].begin(), readers[v].end(), t);
-      return it == readers[v].end() ? (int64_t)n0 : (int64_t)*it;
-    };
-    // demote the member of cur read farthest after t (not one t itself reads)
-    auto demote_one = [&](uint32_t t, const uint32_t *keep, int n_keep) -> bool {
-      int64_t best = -1;
-      size_t at = 0;
-      for (size_t j = 0; j < cur.size(); ++j) {
-        bool kept = false;
-        for (int q = 0; q < n_keep; ++q) kept |= keep[q] == cur[j];
-        if (kept) continue;
-        const int64_t nx = next_read(cur[j], t);
-        if (nx > best) best = nx, at = j;
-      }
-      if (best < 0) return false;
-      demoted[cur[at]] = 1;
-      any = true;
-      cur.erase(cur.begin() + (ptrdiff_t)at);
-      return true;
-    };
-    for (uint32_t t = 0; t < n0; ++t) {
-      Ref *br[3];
-      const int k = bool_refs(S.ins[t], br);
-      uint32_t rd[3];
-      int n_rd = 0, transients = 0;
-      for (int i = 0; i < k; ++i)
-        if (br[i]->k == R_INS) {
-          bool dup = false;
-          for (int q = 0; q < n_rd; ++q) dup |= rd[q] == br[i]->idx;
-          if (dup) continue;
-          rd[n_rd++] = br[i]->idx;
-          transients += demoted[br[i]->idx];
-        }
-      while (cur.size() + (size_t)transients > MGP_BOOL_LIVE)
-        if (!demote_one(t, rd, n_rd)) return unsupported();
-      for (uint32_t v : expire_at[t]) {
-        auto it = std::find(cur.begin(), cur.end(), v);
-        if (it != cur.end()) cur.erase(it);
-      }
-      if (S.ins[t].is_bool && lu[t] > (int64_t)t) {
-        if (cur.size() >= MGP_BOOL_LIVE && !demote_one(t, nullptr, 0)) return unsupported();
-        cur.push_back(t);
-      }
-    }
-    if (any) {
-      const Ref one = const_ref(1u), zero = const_ref(0u);
-      std::vector<VIns> re;
-      re.reserve(n0 + n0 / 4 + 8);
-      std::vector<uint32_t> remap(n0, 0);
-      std::vector<Ref> dref(n0);  // the 1-bit value of a demoted Bool
-      for (uint32_t t = 0; t < n0; ++t) {
-        VIns I = S.ins[t];
-        for (Ref *r : {&I.a, &I.b, &I.c})
-          if (r->k == R_INS) r->idx = remap[r->idx];
-        Ref *br[3], *nr[3];
-        const int k = bool_refs(S.ins[t], br);
-        bool_refs(I, nr);
-        for (int i = 0; i < k; ++i) {
-          if (br[i]->k != R_INS || !demoted[br[i]->idx]) continue;
-          const uint32_t v = br[i]->idx;
-          // one EQ per distinct demoted operand (BITE / BAND may read one Bool twice)
-          Ref e;
-          e.k = R_INS;
-          e.idx = 0xFFFFFFFFu;
-          for (int j = 0; j < i; ++j)
-            if (br[j]->k == R_INS && br[j]->idx == v) e = *nr[j];
-          if (e.idx == 0xFFFFFFFFu) {
-            re.push_back(VIns{MGP_OP_EQ, 1, true, dref[v], one, Ref(), 0});
-            e.idx = (uint32_t)re.size() - 1;
-          }
-          *nr[i] = e;
-        }
-        remap[t] = (uint32_t)re.size();
-        re.push_back(I);
-        if (demoted[t]) {
-          Ref b;
-          b.k = R_INS;
-          b.idx = remap[t];
-          re.push_back(VIns{MGP_OP_ITE, 1, false, b, one, zero, 0});
-          dref[t].k = R_INS;
-          dref[t].idx = (uint32_t)re.size() - 1;
-        }
-      }
-      if (root.k == R_INS) {
-        if (demoted[root.idx]) {
-          re.push_back(VIns{MGP_OP_EQ, 1, true, dref[root.idx], one, Ref(), 0});
-          root.idx = (uint32_t)re.size() - 1;
-        } else {
-          root.idx = remap[root.idx];
-        }
-      }
-      S.ins.swap(re);
-    }
-  }
-
-  // ---------------------------------------------------------- liveness
-  const uint32_t n = (uint32_t)S.ins.size();
-  std::vector<int64_t> last_use(n, -1);       // last instruction reading the value
-  std::vector<uint8_t> needs_slot(n, 0);      // some use cannot be served from ACC
-  std::vector<int64_t> prev_bv(n + 1, -1);    // last BV-producing instruction before t
-  {
-    int64_t last = -1;
-    for (uint32_t t = 0; t < n; ++t) {
-      prev_bv[t] = last;
-      if (!S.ins[t].is_bool) last = t;
-    }
-    prev_bv[n] = last;
-  }
-  auto use = [&](const Ref &r, uint32_t t, bool bool_opnd) {
-    if (r.k != R_INS) return;
-    last_use[r.idx] = std::max<int64_t>(last_use[r.idx], t);
-    if (!bool_opnd && prev_bv[t] != (int64_t)r.idx) needs_slot[r.idx] = 1;
-  };
-  for (uint32_t t = 0; t < n; ++t) {
-    const VIns &I = S.ins[t];
-    if (op_takes_bools(I.op)) {
-      use(I.a, t, true); use(I.b, t, true); use(I.c, t, true);
-    } else if (I.op == MGP_OP_ITE) {
-      use(I.a, t, true); use(I.b, t, false); use(I.c, t, false);
-    } else {
-      use(I.a, t, false); use(I.b, t, false); use(I.c, t, false);
-    }
-  }
-  if (root.k == R_INS) last_use[root.idx] = std::max<int64_t>(last_use[root.idx], n);
-
-  // ---------------------------------------------------------- allocation
-  // LDS slots first (max_slots < MGP_LDS_SLOTS is a test knob that spills earlier), then
-  // spill slots MGP_LDS_SLOTS.. (include/mgp_ir.h), up to MGP_MAX_SLOTS in all
-  const uint32_t slot_cap = std::min<uint32_t>(max_slots ? max_slots : MGP_LDS_SLOTS, MGP_LDS_SLOTS);
-  std::vector<int32_t> loc(n, -1);
-  std::vector<uint32_t> free_slots, free_bools, free_spill;
-  uint32_t next_spill = MGP_LDS_SLOTS;
-  for (int32_t s = (int32_t)slot_cap - 1; s >= 0; --s) free_slots.push_back((uint32_t)s);
-  for (int32_t b = MGP_BOOL_LIVE - 1; b >= 0; --b) free_bools.push_back((uint32_t)b);
-  // fields naming a BV slot, for the access-count renumbering of spilling programs:
-  // (word index, bit shift) of an operand (14-bit index) or of a STORE destination
-  std::vector<std::pair<uint32_t, uint32_t>> slot_fields;
-  std::vector<std::vector<uint32_t>> expire(n + 1);
-  for (uint32_t t = 0; t < n; ++t)
-    if (last_use[t] >= 0 && last_use[t] <= (int64_t)n) expire[last_use[t]].push_back(t);
-  uint32_t slots_used = 0;
-
-  std::vector<uint32_t> out;
-  out.reserve(4 + 4 * n + 8 * S.pool.size() + 4);
-  out.resize(4, 0u);
-
-  auto bv_opnd = [&](const Ref &r, uint32_t t) -> uint32_t {
-    switch (r.k) {
-      case R_VAR: return MGP_OPND(MGP_K_VAR, r.idx);
-      case R_CONST: return MGP_OPND(MGP_K_CONST, r.idx);
-      case R_INS:
-        if (prev_bv[t] == (int64_t)r.idx) return MGP_OPND(MGP_K_ACC, 0);
-        return MGP_OPND(MGP_K_SLOT, (uint32_t)loc[r.idx]);
-      default: return 0;
-    }
-  };
-  auto bool_opnd = [&](const Ref &r) -> uint32_t {
-    if (r.k == R_BOOLC) return r.idx ? MGP_BOOL_TRUE : MGP_BOOL_FALSE;
-    if (r.k == R_INS) return (uint32_t)loc[r.idx];
-    return MGP_BOOL_FALSE;
-  };
-
-  auto in_slot = [&](const Ref &r, uint32_t t) { return r.k == R_INS && prev_bv[t] != (int64_t)r.idx; };
-  uint32_t n_emit = 0;
-  for (uint32_t t = 0; t < n; ++t) {
-    const VIns &I = S.ins[t];
-    uint32_t oa, ob = 0, oc = 0;
-    const uint32_t base = (uint32_t)out.size();
-    if (op_takes_bools(I.op)) {
-      oa = bool_opnd(I.a); ob = bool_opnd(I.b); oc = bool_opnd(I.c);
-    } else if (I.op == MGP_OP_ITE) {
-      oa = bool_opnd(I.a); ob = bv_opnd(I.b, t); oc = bv_opnd(I.c, t);
-      if (in_slot(I.b, t)) slot_fields.push_back({base + 1, 16});
-      if (in_slot(I.c, t)) slot_fields.push_back({base + 2, 0});
-    } else {
-      oa = bv_opnd(I.a, t);
-      ob = I.b.k != R_NONE ? bv_opnd(I.b, t) : 0u;
-      oc = I.c.k != R_NONE ? bv_opnd(I.c, t) : 0u;
-      if (in_slot(I.a, t)) slot_fields.push_back({base + 1, 0});
-      if (I.b.k != R_NONE && in_slot(I.b, t)) slot_fields.push_back({base + 1, 16});
-      if (I.c.k != R_NONE && in_slot(I.c, t)) slot_fields.push_back({base + 2, 0});
-    }
-    // operands read first: free values whose last use is this instruction
-    for (uint32_t v : expire[t]) {
-      if (loc[v] < 0) continue;
-      if (S.ins[v].is_bool) free_bools.push_back((uint32_t)loc[v]);
-      else if ((uint32_t)loc[v] >= MGP_LDS_SLOTS) free_spill.push_back((uint32_t)loc[v]);
-      else free_slots.push_back((uint32_t)loc[v]);
-    }
-    uint32_t dst = 0, flags = 0;
-    const bool live = last_use[t] > (int64_t)t;
-    if (I.is_bool) {
-      if (live) {
-        if (free_bools.empty()) return unsupported();
-        dst = free_bools.back();
-        free_bools.pop_back();
-        loc[t] = (int32_t)dst;
-      } else {
-        return unsupported();  // unreachable after DCE
-      }
-    } else if (live && needs_slot[t]) {
-      if (!free_slots.empty()) {
-        dst = free_slots.back();
-        free_slots.pop_back();
-      } else if (!free_spill.empty()) {
-        dst = free_spill.back();
-        free_spill.pop_back();
-      } else {
-        if (next_spill >= MGP_MAX_SLOTS) return unsupported();
-        dst = next_spill++;
-      }
-      loc[t] = (int32_t)dst;
-      slots_used = std::max(slots_used, dst + 1);
-      flags = MGP_INS_STORE;
-      slot_fields.push_back({base, 16});
-    }
-    const uint32_t width_field = (uint32_t)(I.width ? I.width - 1 : 0) & 0xFFu;
-    out.push_back((uint32_t)I.op | (width_field << 8) | (dst << 16) | (flags << 24));
-    out.push_back((oa & 0xFFFFu) | (ob << 16));
-    out.push_back((oc & 0xFFFFu) | ((I.imm & 0xFFFFu) << 16));
-    out.push_back(0u);
-    ++n_emit;
-  }
-  // RET
-  out.push_back((uint32_t)MGP_OP_RET);
-  out.push_back(bool_opnd(root));
-  out.push_back(0u);
-  out.push_back(0u);
-  ++n_emit;
-
-  // a spilling program: slot numbers by access count (reads + stores), most used first,
-  // so that the LDS slots (and the gfx950 interpreter's register slots) hold the hot values
-  static const bool norenum_dbg = getenv("MGP_LOWER_NORENUM") != nullptr;
-  if (slots_used > MGP_LDS_SLOTS && slot_cap == MGP_LDS_SLOTS && !norenum_dbg) {
-    auto field = [&](const std::pair<uint32_t, uint32_t> &f) -> uint32_t {
-      return f.first % 4u == 0u ? (out[f.first] >> 16) & 0xFFu : (out[f.first] >> f.second) & 0x3FFFu;
-    };
-    std::vector<uint32_t> cnt(slots_used, 0), by(slots_used), rank(slots_used);
-    for (const auto &f : slot_fields) cnt[field(f)]++;
-    for (uint32_t s = 0; s < slots_used; ++s) by[s] = s;
-    std::stable_sort(by.begin(), by.end(), [&](uint32_t x, uint32_t y) { return cnt[x] > cnt[y]; });
-    for (uint32_t r = 0; r < slots_used; ++r) rank[by[r]] = r;
-    for (const auto &f : slot_fields) {
-      const uint32_t nw = rank[field(f)];
-      if (f.first % 4u == 0u) out[f.first] = (out[f.first] & ~(0xFFu << 16)) | (nw << 16);
-      else out[f.first] = (out[f.first] & ~(0x3FFFu << f.second)) | (nw << f.second);
-    }
-  }
-
-  out[0] = n_emit;
-  out[1] = (uint32_t)S.pool.size();
-  out[2] = slots_used;
-  out[3] = (uint32_t)MGP_ST_OK | (S.max_var << 8);
-  for (const ConstKey &k : S.pool)
-    for (int l = 0; l < 8; ++l) out.push_back(k.w[l]);
-  while (out.size() % 4) out.push_back(0u);
-  for (int k = 0; k < 4; ++k) out.push_back(0u);  // the kernel prefetches one instruction past RET
-  Lowered L;
-  L.words.swap(out);
-  return L;
+  if (!have) uops->clear();
+  return have ? best : unsupported();
 }
 
 }  // namespace
@@ -1124,32 +1176,14 @@ static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32
       bad = 1;
       continue;
     }
-    // Three schedules (input order, Sethi-Ullman DFS, greedy list); keep the
-    // one needing the fewest LDS slots — occupancy is set by the slot count
-    // (bench A/B: the DFS order alone saves stores but costs slots, 5 % slower).
+    // Three schedules (input order, Sethi-Ullman DFS, greedy list) over one prepared
+    // state; lower_one keeps the best one the gfx950 interpreter can run.
     const uint32_t *cp = consts ? consts + c0 * 8u : nullptr;
-    // A schedule only counts if the gfx950 interpreter can also run it (its Bool
-    // budget is smaller than the bytecode's), so each candidate is translated too.
+    static const int all3[3] = {0, 1, 2};
+    const int one = sched_mode == 0 ? 0 : sched_mode - 1;
     std::vector<uint32_t> uops;
-    Lowered a = lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, sched_mode == 0 ? 0 : (sched_mode == 1 ? 0 : sched_mode - 1));
-    if (a.status == MGP_ST_OK && mgp_uop_translate(a.words.data(), uops) != 0) a = unsupported();
-    if (sched_mode == 1) {
-      for (int alt = 1; alt <= 2; ++alt) {
-        Lowered b = lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, alt);
-        const bool a_ok = a.status == MGP_ST_OK, b_ok = b.status == MGP_ST_OK;
-        // fewer slots wins (occupancy); between spilling programs, fewer instructions
-        // (a spill is a memory access either way, an instruction is issue time)
-        if (!b_ok) continue;
-        if (a_ok) {
-          const bool spill = a.words[2] > MGP_LDS_SLOTS || b.words[2] > MGP_LDS_SLOTS;
-          if (spill ? b.words[0] >= a.words[0] : b.words[2] >= a.words[2]) continue;
-        }
-        std::vector<uint32_t> bu;
-        if (mgp_uop_translate(b.words.data(), bu) != 0) continue;
-        a = std::move(b);
-        uops.swap(bu);
-      }
-    }
+    Lowered a = sched_mode == 1 ? lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, all3, 3, &uops)
+                                : lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, &one, 1, &uops);
     // append the uop program of the gfx950 interpreter; a state it cannot run
     // is made unsupported in both encodings so that both engines agree
     if (a.status != MGP_ST_OK) {

@@ -279,6 +279,11 @@ class Prefilter:
         # per state (host candidate memory capped at 1 GiB)
         self.retry_cand = 1024
         self.cand_bytes = 1 << 30  # candidate memory of one witness round
+        # host decision rows (mgp_guided_candidates) cost one domain analysis per variable
+        # and row: states are taken cheapest first while the estimated wall time of the
+        # round stays within this budget (a WalletLibrary state costs ~70 ms of one core
+        # per row, a BECToken state ~10 ms)
+        self.decide_budget_ms = 100.0
         self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
@@ -410,6 +415,9 @@ class Prefilter:
         for rnd, (n_cand, n_decide) in enumerate(self.RETRY_SCHEDULE):
             if not open_ or len(open_) > self.DECIDE_MAX:
                 break
+            open_ = self._within_decide_budget(states, open_, n_decide)
+            if not open_:
+                break
             budget = self.cand_bytes // (len(open_) * n_vars * 32)
             n2 = min(n_cand, self.retry_cand, budget) // 64 * 64
             if n2 < 64:
@@ -434,6 +442,29 @@ class Prefilter:
             SB.close()
             open_ = left
         SolverStatistics().gpu_retry += len(retry)
+
+    DECIDE_US_PER_UNIT = 0.2  # host cost of one decision row, per (variable x DAG node)
+
+    def _within_decide_budget(self, states, open_, n_decide):
+        """The open states whose host decision rows fit decide_budget_ms of wall time (one
+        task per state and row over the host threads), cheapest first."""
+        import os
+
+        from .front import Batch
+
+        B = Batch([states[i] for i in open_])
+        units = np.diff(B.var_off).astype(np.float64) * np.diff(B.node_off).astype(np.float64)
+        B.close()
+        threads = max(1, min(16, os.cpu_count() or 1))
+        keep, cpu_ms = [], 0.0
+        for k in np.argsort(units, kind="stable"):
+            c = units[k] * n_decide * self.DECIDE_US_PER_UNIT * 1e-3
+            tasks = (len(keep) + 1) * n_decide
+            if (cpu_ms + c) / min(threads, tasks) > self.decide_budget_ms:
+                break
+            keep.append(open_[int(k)])
+            cpu_ms += c
+        return sorted(keep)
 
 
 _prefilter: Optional[Prefilter] = None

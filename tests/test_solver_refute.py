@@ -157,3 +157,24 @@ def test_second_candidate_round(fe, monkeypatch):
     assert SV.Prefilter.RETRY_GPU_CAND == 1024 and [n for n, _ in SV.Prefilter.RETRY_SCHEDULE] == [256]
     assert SV.prefilter().ctx.batches == 3
     assert set(items[0].witness) == {"rx", "ry"}
+
+
+def test_host_decisions_keep_to_their_time_budget():
+    """The retry round's host decision rows take the open states cheapest first while the
+    estimated wall time fits Prefilter.decide_budget_ms (one task per state and row)."""
+    import types
+
+    import corpus
+    from mythril_amd.keccak import KeccakFunctionManager
+
+    kfm = KeccakFunctionManager()
+    states = [list(t) for _, t, _ in corpus.wallet_states(0, kfm)[:4]]
+    states += [list(corpus.bectoken_states(k, kfm)[1]) for k in range(4)]
+    fake = types.SimpleNamespace(decide_budget_ms=100.0, DECIDE_US_PER_UNIT=SV.Prefilter.DECIDE_US_PER_UNIT)
+    pick = SV.Prefilter._within_decide_budget(fake, states, list(range(8)), 8)
+    assert set(range(4, 8)) <= set(pick)          # the small BECToken states first
+    assert len(pick) < 8
+    fake.decide_budget_ms = 1e9
+    assert SV.Prefilter._within_decide_budget(fake, states, list(range(8)), 8) == list(range(8))
+    fake.decide_budget_ms = 0.0
+    assert SV.Prefilter._within_decide_budget(fake, states, list(range(8)), 8) == []

@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -148,6 +149,129 @@ void alias_tables(uint32_t n_states, const uint64_t *vo, const uint32_t *vw, con
   if (T.wlist.empty()) T.wlist.push_back(0u);
 }
 
+// Lowered programs of recent states, keyed by the exact content of the state's GPU node
+// list and constants (compared in full on a hit, so a hash collision can only cost a
+// lowering).  The retry round of a batch re-checks its open states (solver.py
+// _retry_round) and detection modules re-ask queries of states already pruned, so the
+// same programs come back; a WalletLibrary program costs milliseconds to lower.
+struct ProgCache {
+  struct Entry {
+    std::vector<uint8_t> key;
+    std::vector<uint32_t> words;
+    uint8_t status;
+  };
+  std::mutex mu;
+  std::unordered_map<uint64_t, Entry> map;
+  std::vector<uint64_t> fifo;
+  size_t head = 0, bytes = 0;
+  static constexpr size_t kMaxBytes = 256u << 20;
+};
+ProgCache &prog_cache() {
+  static ProgCache c;
+  return c;
+}
+uint64_t fnv(const uint8_t *p, size_t n, uint64_t h = 1469598103934665603ull) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {  // 8 bytes per step (keys are tens of KiB)
+    uint64_t w;
+    memcpy(&w, p + i, 8);
+    h = (h ^ w) * 0x100000001B3ull;
+    h ^= h >> 29;
+  }
+  for (; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+  return h;
+}
+
+int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states, const uint32_t *consts,
+                 const uint64_t *coff, std::vector<uint32_t> &words, std::vector<uint64_t> &offs,
+                 std::vector<uint8_t> &status) {
+  ProgCache &C = prog_cache();
+  std::vector<std::vector<uint8_t>> keys(n_states);
+  std::vector<uint64_t> hs(n_states);
+  std::vector<const ProgCache::Entry *> hit(n_states, nullptr);
+  std::vector<uint32_t> miss;
+  {
+    std::lock_guard<std::mutex> lk(C.mu);
+    for (uint32_t s = 0; s < n_states; ++s) {
+      const size_t nb = (noff[s + 1] - noff[s]) * sizeof(mgp_node), cb = (coff[s + 1] - coff[s]) * 32u;
+      keys[s].resize(16 + nb + cb);
+      const uint64_t hdr[2] = {noff[s + 1] - noff[s], coff[s + 1] - coff[s]};
+      memcpy(keys[s].data(), hdr, 16);
+      memcpy(keys[s].data() + 16, nodes + noff[s], nb);
+      if (cb) memcpy(keys[s].data() + 16 + nb, consts + coff[s] * 8u, cb);
+      hs[s] = fnv(keys[s].data(), keys[s].size());
+      auto it = C.map.find(hs[s]);
+      if (it != C.map.end() && it->second.key == keys[s]) hit[s] = &it->second;
+      else miss.push_back(s);
+    }
+    // the hits are copied below while holding the lock (an insert may evict them)
+    std::vector<mgp_node> mn;
+    std::vector<uint32_t> mc;
+    std::vector<uint64_t> mno(1, 0), mco(1, 0);
+    for (uint32_t s : miss) {
+      mn.insert(mn.end(), nodes + noff[s], nodes + noff[s + 1]);
+      mc.insert(mc.end(), consts + coff[s] * 8u, consts + coff[s + 1] * 8u);
+      mno.push_back(mn.size());
+      mco.push_back(mc.size() / 8u);
+    }
+    std::vector<uint32_t> mw;
+    std::vector<uint64_t> mo;
+    std::vector<uint8_t> mst;
+    if (!miss.empty()) {
+      if (mc.empty()) mc.assign(8, 0u);
+      const int rc = mgp_lower_vec(mn.data(), mno.data(), (uint32_t)miss.size(), mc.data(), mco.data(), 0, mw, mo,
+                                   mst);
+      if (rc != MGP_OK) return rc;
+    }
+    offs.assign((size_t)n_states + 1, 0u);
+    status.assign(n_states, 0u);
+    std::vector<int64_t> mi(n_states, -1);
+    for (size_t k = 0; k < miss.size(); ++k) mi[miss[k]] = (int64_t)k;
+    for (uint32_t s = 0; s < n_states; ++s)
+      offs[s + 1] = offs[s] + (mi[s] >= 0 ? mo[mi[s] + 1] - mo[mi[s]] : hit[s]->words.size());
+    words.resize(offs[n_states]);
+    for (uint32_t s = 0; s < n_states; ++s) {
+      if (mi[s] >= 0) {
+        memcpy(words.data() + offs[s], mw.data() + mo[mi[s]], (mo[mi[s] + 1] - mo[mi[s]]) * 4u);
+        status[s] = mst[mi[s]];
+      } else {
+        memcpy(words.data() + offs[s], hit[s]->words.data(), hit[s]->words.size() * 4u);
+        status[s] = hit[s]->status;
+      }
+    }
+    // insert the new programs, evicting the oldest past the byte budget
+    for (size_t k = 0; k < miss.size(); ++k) {
+      const uint32_t s = miss[k];
+      ProgCache::Entry e;
+      e.key = std::move(keys[s]);
+      e.words.assign(mw.begin() + mo[k], mw.begin() + mo[k + 1]);
+      e.status = mst[k];
+      const size_t sz = e.key.size() + e.words.size() * 4u;
+      if (sz > ProgCache::kMaxBytes / 8) continue;
+      auto it = C.map.find(hs[s]);
+      if (it != C.map.end()) {
+        C.bytes -= it->second.key.size() + it->second.words.size() * 4u;
+        it->second = std::move(e);
+      } else {
+        C.map.emplace(hs[s], std::move(e));
+        C.fifo.push_back(hs[s]);
+      }
+      C.bytes += sz;
+      while (C.bytes > ProgCache::kMaxBytes && C.head < C.fifo.size()) {
+        auto old = C.map.find(C.fifo[C.head++]);
+        if (old == C.map.end()) continue;
+        C.bytes -= old->second.key.size() + old->second.words.size() * 4u;
+        C.map.erase(old);
+      }
+      if (C.head > 4096 && C.head * 2 > C.fifo.size()) {
+        C.fifo.erase(C.fifo.begin(), C.fifo.begin() + (ptrdiff_t)C.head);
+        C.head = 0;
+      }
+    }
+  }
+  return MGP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -188,12 +312,12 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   static const uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t *cp = consts.n ? (const uint32_t *)consts.p : zero8;
 
-  // 1. lower the GPU programs
+  // 1. lower the GPU programs (programs lowered by an earlier call come from the cache)
   std::vector<uint32_t> words;
   std::vector<uint64_t> offs;
   std::vector<uint8_t> status;
-  int rc = mgp_lower_vec((const mgp_node *)gnodes.p, (const uint64_t *)gnoff.p, n_states, cp,
-                         (const uint64_t *)coff.p, 0, words, offs, status);
+  int rc = lower_cached((const mgp_node *)gnodes.p, (const uint64_t *)gnoff.p, n_states, cp,
+                        (const uint64_t *)coff.p, words, offs, status);
   if (rc != MGP_OK) return mgp_ctx_fail(ctx, rc, "lowering failed");
   std::vector<uint32_t> order(n_states), bounds(257), bslots(256);
   const int nb = mgp_plan_buckets(words.data(), offs.data(), n_states, order.data(), bounds.data(), bslots.data(),

@@ -85,3 +85,27 @@ def test_parent_witness_is_row_zero(mgp_ctx):
     w = C.witness(0, cw[0])
     assert w["x"] == 17 and w["y"] == 23
     C.close()
+
+
+def test_check_batch_program_cache(mgp_ctx):
+    """mgp_check_batch keeps the programs it lowered (keyed by the exact node list and
+    constants): a second call on the same states, and a call on a subset in another
+    order (the retry round's shape), give the results of a fresh lowering."""
+    states = _contract_batch(120)
+    B = F.Batch(states)
+    f1, w1, r1, _ = B.check(mgp_ctx, 256, 77)
+    f2, w2, r2, _ = B.check(mgp_ctx, 256, 77)
+    assert np.array_equal(f1, f2) and np.array_equal(w1, w2) and np.array_equal(r1, r2)
+    sub = list(range(len(states) - 1, -1, -3))
+    S = F.Batch([states[i] for i in sub])
+    fs, _, rs, _ = S.check(mgp_ctx, 256, 5)
+    n_vars = max(1, S.n_vars())
+    _, dom = N.refute_domains(*S.packed(), S.var_off)
+    cands = S.device_candidates(mgp_ctx, 256, n_vars, 5, dom=dom)
+    want = coracle.first_sat(*S.packed(gpu=True), cands)
+    _, _, status = N.lower(*S.packed(gpu=True))
+    ok = status == 0
+    assert np.array_equal(fs[ok], want[ok]) and (fs[~ok] == N.MGP_UNDECIDED).all()
+    assert np.array_equal(rs, r1[sub])
+    B.close()
+    S.close()

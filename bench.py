@@ -526,6 +526,7 @@ def frontend_latency(pf, SV, cs, sizes=(1, 2, 16, 128, 1024)):
         walls, profs = [], []
         for r in range(reps):
             SV.unsat_cores().reset()
+            pf._N.program_cache_clear()  # cold: no lowered program reused across calls
             sub = cs[(r * n) % max(1, len(cs) - n + 1):][:n]
             t = time.perf_counter()
             pf.check_states(sub)

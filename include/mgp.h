@@ -293,6 +293,11 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, ui
                     const uint32_t *parent_vals, const uint64_t *parent_off, const uint64_t *slot_keys,
                     uint32_t flags, int32_t *out_first, uint32_t *out_witness, int8_t *out_refuted,
                     uint32_t *out_n_vars, double *out_times);
+/* mgp_check_batch keeps the programs it lowers in a process-wide cache keyed by the
+ * exact node list and constants of each state (compared in full on a hit; 256 MiB,
+ * oldest first out): a retry round or a repeated query skips the lowering.  This
+ * empties it (cold measurements, tests); returns the number of programs dropped. */
+uint64_t mgp_program_cache_clear(void);
 /* Test hook: the candidates mgp_check_batch would evaluate (no parents), device layout
  * [state][var][half][cand] of 16-byte groups, n_vars >= the batch's widest state. */
 int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint32_t n_vars, uint64_t seed,

@@ -97,6 +97,7 @@ def _bind(lib):
         "mgp_fe_free": (None, [_P]),
         "mgp_check_batch": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _P]),
         "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P, _P]),
+        "mgp_program_cache_clear": (_U64, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -154,7 +155,14 @@ EXPORTED_SYMBOLS = (
     "mgp_fe_free",
     "mgp_check_batch",
     "mgp_fe_candidates",
+    "mgp_program_cache_clear",
 )
+
+
+def program_cache_clear() -> int:
+    """Empty mgp_check_batch's cache of lowered programs (cold measurements, tests)."""
+    return int(lib().mgp_program_cache_clear())
+
 
 ENGINE_HIP, ENGINE_ASM = 1, 2
 ENGINES = {"hip": ENGINE_HIP, "asm": ENGINE_ASM}

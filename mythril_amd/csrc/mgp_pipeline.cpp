@@ -276,6 +276,17 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
 
 extern "C" {
 
+uint64_t mgp_program_cache_clear(void) {
+  ProgCache &C = prog_cache();
+  std::lock_guard<std::mutex> lk(C.mu);
+  const uint64_t n = C.map.size();
+  C.map.clear();
+  C.fifo.clear();
+  C.head = 0;
+  C.bytes = 0;
+  return n;
+}
+
 void mgp_pipeline_release(mgp_ctx *ctx) {
   auto &m = bufs_of();
   auto it = m.find(ctx);

@@ -1202,7 +1202,15 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
     // mapping key fixed by an equality, ...).  A draw that empties a domain is replaced
     // (up to kTries draws); the remaining rows are plain draws from the refined domains.
     constexpr uint32_t kTries = 4;
-    const uint32_t passes = std::min(max_passes ? max_passes : 16u, 6u);
+    // two forward + backward passes per decision carry a fixed value to its relations
+    // (x + y == c, a mapping key), which is what the later draws need: the same witnesses
+    // as six passes on the contract corpus and on synthetic states, 1.3-1.7x faster (one
+    // pass loses 4 % on synthetic states).  MGP_DECIDE_PASSES overrides (A/B).
+    static const uint32_t decide_passes = [] {
+      const char *e = getenv("MGP_DECIDE_PASSES");
+      return e ? (uint32_t)atoi(e) : 2u;
+    }();
+    const uint32_t passes = std::min(max_passes ? max_passes : 16u, decide_passes ? decide_passes : 1u);
     for (uint32_t c = 0, row = 0; c < n_cand; c += every, ++row) {
       uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
       if (task_row < n_dec_rows ? row != task_row : row < n_dec_rows) continue;

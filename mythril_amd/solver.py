@@ -279,11 +279,13 @@ class Prefilter:
         # per state (host candidate memory capped at 1 GiB)
         self.retry_cand = 1024
         self.cand_bytes = 1 << 30  # candidate memory of one witness round
-        # host decision rows (mgp_guided_candidates) cost one domain analysis per variable
-        # and row: states are taken cheapest first while the estimated wall time of the
-        # round stays within this budget (a WalletLibrary state costs ~70 ms of one core
-        # per row, a BECToken state ~10 ms)
+        # host decision rows (mgp_guided_candidates) cost two domain-analysis passes per
+        # variable and row: states are taken cheapest first while the estimated wall time of
+        # the round stays within max(decide_budget_ms, decide_ms_per_state x batch size) (a
+        # WalletLibrary state costs ~40 ms of one core per row, a BECToken state ~6 ms;
+        # each witness found saves a fallback call)
         self.decide_budget_ms = 100.0
+        self.decide_ms_per_state = 1.0
         self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
@@ -385,12 +387,12 @@ class Prefilter:
         return out
 
     # witness rounds for the states the first round and the pre-check leave open: a larger
-    # GPU round (candidates generated on the device, domain rows with a new seed), then --
-    # for at most DECIDE_MAX states -- host decisions, which re-run the domain analysis per
-    # variable and are kept for the few states that need them.
+    # GPU round (candidates generated on the device, domain rows with a new seed), then
+    # host decision rows, which re-run the domain analysis per variable: for the open
+    # states that fit the round's time budget (_within_decide_budget), cheapest first.
     RETRY_GPU_CAND = 1024
     RETRY_SCHEDULE = ((256, 8),)  # (candidates per state, decision rows) of the host rounds
-    DECIDE_MAX = 64
+    DECIDE_MAX = 4096
 
     def _retry_round(self, states, retry, n_vars, first, witnesses) -> None:
         from . import dag as D
@@ -415,7 +417,8 @@ class Prefilter:
         for rnd, (n_cand, n_decide) in enumerate(self.RETRY_SCHEDULE):
             if not open_ or len(open_) > self.DECIDE_MAX:
                 break
-            open_ = self._within_decide_budget(states, open_, n_decide)
+            open_ = self._within_decide_budget(states, open_, n_decide,
+                                               max(self.decide_budget_ms, self.decide_ms_per_state * len(states)))
             if not open_:
                 break
             budget = self.cand_bytes // (len(open_) * n_vars * 32)
@@ -443,11 +446,12 @@ class Prefilter:
             open_ = left
         SolverStatistics().gpu_retry += len(retry)
 
-    DECIDE_US_PER_UNIT = 0.2  # host cost of one decision row, per (variable x DAG node)
+    DECIDE_US_PER_UNIT = 0.12  # host cost of one decision row, per (variable x DAG node)
 
-    def _within_decide_budget(self, states, open_, n_decide):
-        """The open states whose host decision rows fit decide_budget_ms of wall time (one
-        task per state and row over the host threads), cheapest first."""
+    def _within_decide_budget(self, states, open_, n_decide, budget_ms=None):
+        """The open states whose host decision rows fit budget_ms (default decide_budget_ms)
+        of wall time (one task per state and row over the host threads), cheapest first."""
+        budget_ms = self.decide_budget_ms if budget_ms is None else budget_ms
         import os
 
         from .front import Batch
@@ -460,7 +464,7 @@ class Prefilter:
         for k in np.argsort(units, kind="stable"):
             c = units[k] * n_decide * self.DECIDE_US_PER_UNIT * 1e-3
             tasks = (len(keep) + 1) * n_decide
-            if (cpu_ms + c) / min(threads, tasks) > self.decide_budget_ms:
+            if (cpu_ms + c) / min(threads, tasks) > budget_ms:
                 break
             keep.append(open_[int(k)])
             cpu_ms += c

@@ -500,6 +500,52 @@ MGP_RHO(14, 39) MGP_RHO(15, 41) MGP_RHO(16, 45) MGP_RHO(17, 15) MGP_RHO(18, 21) 
 MGP_RHO(20, 18) MGP_RHO(21, 2) MGP_RHO(22, 61) MGP_RHO(23, 56) MGP_RHO(24, 14)
 #undef MGP_RHO
 
+// one round on K independent states (K = 2: two hashes per lane, interleaved by the
+// scheduler; A/B knob MGP_KECCAK_X2)
+template <int K>
+__device__ __forceinline__ void keccak_round_k(uint32_t (*lo)[25], uint32_t (*hi)[25], int round) {
+#pragma unroll
+  for (int q = 0; q < K; ++q) {
+    uint32_t cl[5], ch[5], dl[5], dh[5], bl[25], bh[25];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      cl[x] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(lo[q][x], lo[q][x + 5], lo[q][x + 10], 0x96),
+                                          lo[q][x + 15], lo[q][x + 20], 0x96);
+      ch[x] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(hi[q][x], hi[q][x + 5], hi[q][x + 10], 0x96),
+                                          hi[q][x + 15], hi[q][x + 20], 0x96);
+    }
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+      uint32_t rl, rh;
+      rotl64_32<1>(cl[(x + 1) % 5], ch[(x + 1) % 5], rl, rh);
+      dl[x] = cl[(x + 4) % 5] ^ rl;
+      dh[x] = ch[(x + 4) % 5] ^ rh;
+    }
+    static_for<25>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int x = i % 5, y = i / 5;
+      constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+      rotl64_32<KeccakRho<i>::v>(lo[q][i] ^ dl[x], hi[q][i] ^ dh[x], bl[dst], bh[dst]);
+    });
+#pragma unroll
+    for (int y = 0; y < 5; ++y)
+#pragma unroll
+      for (int x = 0; x < 5; ++x) {
+        lo[q][x + 5 * y] = bl[x + 5 * y] ^ (~bl[(x + 1) % 5 + 5 * y] & bl[(x + 2) % 5 + 5 * y]);
+        hi[q][x + 5 * y] = bh[x + 5 * y] ^ (~bh[(x + 1) % 5 + 5 * y] & bh[(x + 2) % 5 + 5 * y]);
+      }
+    const uint64_t rc = kKeccakRC[round];
+    lo[q][0] ^= (uint32_t)rc;
+    hi[q][0] ^= (uint32_t)(rc >> 32);
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void keccak_f1600_32k(uint32_t (*lo)[25], uint32_t (*hi)[25]) {
+#pragma unroll
+  for (int round = 0; round < 24; ++round) keccak_round_k<K>(lo, hi, round);
+}
+
 __device__ __forceinline__ void keccak_f1600_32(uint32_t lo[25], uint32_t hi[25]) {
   // fully unrolled: the pi permutation then costs no moves and the round constants
   // become literals
@@ -588,8 +634,61 @@ __global__ void mgp_keccak_kernel(const uint8_t *__restrict__ in, uint64_t n, ui
     for (int b = 0; b < 8; ++b) o[8 * k + b] = (uint8_t)(st[k] >> (8 * b));
 }
 
+// fast path, two hashes per lane (i and i + half): A/B variant (MGP_KECCAK_X2=1)
+__global__ __launch_bounds__(256) void mgp_keccak64x2_kernel(const uint4 *__restrict__ in, uint64_t n,
+                                                             uint32_t stride16, uint4 *__restrict__ out) {
+  const uint64_t half = (n + 1) / 2;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= half) return;
+  const uint64_t j = i + half < n ? i + half : i;  // odd n: the last lane hashes i twice
+  uint32_t lo[2][25], hi[2][25];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const uint4 *p = in + (q ? j : i) * stride16;
+#pragma unroll
+    for (int k = 0; k < 25; ++k) lo[q][k] = hi[q][k] = 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint4 v = p[c];
+      lo[q][2 * c] = v.x; hi[q][2 * c] = v.y; lo[q][2 * c + 1] = v.z; hi[q][2 * c + 1] = v.w;
+    }
+    lo[q][8] = 0x01u;
+    hi[q][16] = 0x80000000u;
+  }
+  keccak_f1600_32k<2>(lo, hi);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    uint4 *o = out + (q ? j : i) * 2u;
+    o[0] = make_uint4(lo[q][0], hi[q][0], lo[q][1], hi[q][1]);
+    o[1] = make_uint4(lo[q][2], hi[q][2], lo[q][3], hi[q][3]);
+  }
+}
+
 // fast path: 64-byte preimages, 16-byte aligned stride (mapping slots)
 __global__ __launch_bounds__(256) void mgp_keccak64_kernel(const uint4 *__restrict__ in, uint64_t n,
+                                                           uint32_t stride16, uint4 *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4 *p = in + i * stride16;
+  uint64_t st[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) st[k] = 0ull;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint4 v = p[q];
+    st[2 * q] = ((uint64_t)v.y << 32) | v.x;
+    st[2 * q + 1] = ((uint64_t)v.w << 32) | v.z;
+  }
+  st[8] = 0x01ull;
+  st[16] = 0x8000000000000000ull;
+  keccak_f1600(st);
+  uint4 *o = out + i * 2u;
+  o[0] = make_uint4((uint32_t)st[0], (uint32_t)(st[0] >> 32), (uint32_t)st[1], (uint32_t)(st[1] >> 32));
+  o[1] = make_uint4((uint32_t)st[2], (uint32_t)(st[2] >> 32), (uint32_t)st[3], (uint32_t)(st[3] >> 32));
+}
+
+// fast path at 8 waves/SIMD (<= 64 VGPRs, the compiler spills a few words): A/B variant (MGP_KECCAK_W8=1)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void mgp_keccak64w8_kernel(const uint4 *__restrict__ in, uint64_t n,
                                                            uint32_t stride16, uint4 *__restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1119,7 +1218,21 @@ hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32
                     ((uintptr_t)out % 16u) == 0u;
   const uint64_t blocks = (n + 255) / 256;
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  if (fast) {
+  static const bool x2 = [] {
+    const char *e = getenv("MGP_KECCAK_X2");
+    return e && e[0] == '1';
+  }();
+  static const bool w8 = [] {
+    const char *e = getenv("MGP_KECCAK_W8");
+    return e && e[0] == '1';
+  }();
+  if (fast && w8) {
+    hipLaunchKernelGGL(mgp_keccak64w8_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
+                       reinterpret_cast<const uint4 *>(in), n, stride / 16u, reinterpret_cast<uint4 *>(out));
+  } else if (fast && x2) {
+    hipLaunchKernelGGL(mgp_keccak64x2_kernel, dim3((uint32_t)((n + 1) / 2 + 255) / 256), dim3(256), 0, st,
+                       reinterpret_cast<const uint4 *>(in), n, stride / 16u, reinterpret_cast<uint4 *>(out));
+  } else if (fast) {
     hipLaunchKernelGGL(mgp_keccak64_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
                        reinterpret_cast<const uint4 *>(in), n, stride / 16u, reinterpret_cast<uint4 *>(out));
   } else {

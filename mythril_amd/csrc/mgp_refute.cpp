@@ -296,6 +296,20 @@ struct State {
   std::vector<uint8_t> cmp_dom;   // 0 unsigned, 1 signed, 2 both (EQ)
   std::vector<uint8_t> cmp_t;     // orderings (x vs y) under which the node is true
   bool changed = false;
+  // decision rows (mgp_guided_candidates): every change can go to an undo log (a failed
+  // draw rolls back instead of copying the state) and the changed nodes to a work list
+  // (a decision propagates from the decided node, run_from); var-table entries are
+  // listed as kVarBit | entry
+  struct UndoRec {
+    uint8_t kind;  // 0 av, 1 bs, 2 pair, 3 var entry
+    uint32_t idx;
+    AV av;
+    uint8_t b, pu, ps;
+  };
+  static constexpr uint32_t kVarBit = 0x80000000u;
+  std::vector<UndoRec> *undo = nullptr;
+  std::vector<uint32_t> *touched = nullptr;
+  std::vector<uint32_t> uoff, ulist, voff, vlist;  // users of each node; VAR nodes of each entry
 
   uint32_t W(int32_t i) const { return nd[i].width; }
 
@@ -308,6 +322,8 @@ struct State {
     t.hi = MIN(t.hi, s.hi);
     if (!normalize(t, w)) return false;
     if (!same(t, av[i])) {
+      if (undo) undo->push_back(UndoRec{0, (uint32_t)i, av[i], 0, 0, 0});
+      if (touched) touched->push_back((uint32_t)i);
       av[i] = t;
       changed = true;
     }
@@ -317,6 +333,8 @@ struct State {
     const uint8_t t = bs[i] & s;
     if (!t) return false;
     if (t != bs[i]) {
+      if (undo) undo->push_back(UndoRec{1, (uint32_t)i, AV(), bs[i], 0, 0});
+      if (touched) touched->push_back((uint32_t)i);
       bs[i] = t;
       changed = true;
     }
@@ -451,6 +469,7 @@ struct State {
     if (s == OEQ) u = OEQ;
     if (!u || !s) return false;
     if (u != p.u || s != p.s) {
+      if (undo) undo->push_back(UndoRec{2, (uint32_t)(&p - pairs.data()), AV(), 0, p.u, p.s});
       p.u = u;
       p.s = s;
       changed = true;
@@ -854,6 +873,8 @@ struct State {
         t.z = OR(t.z, R.z); t.o = OR(t.o, R.o); t.lo = MAX(t.lo, R.lo); t.hi = MIN(t.hi, R.hi);
         if (!normalize(t, w)) return false;
         if (!same(t, v)) {
+          if (undo) undo->push_back(UndoRec{3, (uint32_t)vtie[i], v, 0, 0, 0});
+          if (touched) touched->push_back(kVarBit | (uint32_t)vtie[i]);
           v = t;
           changed = true;
         }
@@ -968,6 +989,68 @@ struct State {
       }
       default: return true;
     }
+  }
+
+  // ---------------------------------------------------- decision support
+  void build_graph() {
+    uoff.assign(n + 1, 0u);
+    for (uint32_t i = 0; i < n; ++i)
+      for (int32_t o : {nd[i].a, nd[i].b, nd[i].c})
+        if (o >= 0 && (uint32_t)o < i) uoff[o + 1]++;
+    for (uint32_t i = 0; i < n; ++i) uoff[i + 1] += uoff[i];
+    ulist.assign(uoff[n], 0u);
+    std::vector<uint32_t> pos(uoff.begin(), uoff.end() - 1);
+    for (uint32_t i = 0; i < n; ++i)
+      for (int32_t o : {nd[i].a, nd[i].b, nd[i].c})
+        if (o >= 0 && (uint32_t)o < i) ulist[pos[o]++] = i;
+    voff.assign(vars.size() + 1, 0u);
+    for (uint32_t i = 0; i < n; ++i)
+      if (nd[i].op == MGP_OP_VAR && vtie[i] >= 0) voff[vtie[i] + 1]++;
+    for (size_t j = 0; j < vars.size(); ++j) voff[j + 1] += voff[j];
+    vlist.assign(voff[vars.size()], 0u);
+    std::vector<uint32_t> vp(voff.begin(), voff.end() - 1);
+    for (uint32_t i = 0; i < n; ++i)
+      if (nd[i].op == MGP_OP_VAR && vtie[i] >= 0) vlist[vp[vtie[i]]++] = i;
+  }
+  void rollback(size_t mark) {
+    while (undo->size() > mark) {
+      const UndoRec &u = undo->back();
+      if (u.kind == 0) av[u.idx] = u.av;
+      else if (u.kind == 1) bs[u.idx] = u.b;
+      else if (u.kind == 2) pairs[u.idx].u = u.pu, pairs[u.idx].s = u.ps;
+      else vars[u.idx] = u.av;
+      undo->pop_back();
+    }
+  }
+  // Propagation from one changed node (a decision): backward into its operands, forward
+  // and backward through its users, transitively over the nodes that change, then the
+  // pair orderings; at most `budget` node visits.  1 = the decision empties a domain.
+  // Only decision rows use it (candidates, checked on the GPU); refutations run().
+  int run_from(uint32_t seed, uint32_t budget) {
+    std::vector<uint32_t> &T = *touched;
+    T.clear();
+    T.push_back(seed);
+    size_t head = 0;
+    uint32_t visits = 0;
+    for (int round = 0; round < 3; ++round) {
+      while (head < T.size()) {
+        const uint32_t t = T[head++];
+        if (++visits > budget) return 0;
+        if (t & kVarBit) {  // a variable's shared value changed: every VAR node of it
+          const uint32_t j = t & ~kVarBit;
+          for (uint32_t k = voff[j]; k < voff[j + 1]; ++k)
+            if (!forward(vlist[k])) return 1;
+          continue;
+        }
+        if (!backward(t)) return 1;
+        for (uint32_t k = uoff[t]; k < uoff[t + 1]; ++k)
+          if (!forward(ulist[k]) || !backward(ulist[k])) return 1;
+      }
+      const size_t before = T.size();
+      if (!meetb((int32_t)n - 1, BT) || !tie()) return 1;
+      if (T.size() == before) break;
+    }
+    return 0;
   }
 
   // 1 = refuted (UNSAT), 0 = not refuted
@@ -1146,107 +1229,142 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
                                      uint32_t n_decide, uint32_t *cands, int8_t *out) {
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets || !cands)) || every == 0u)
     return MGP_E_ARG;
-  // one task per (state, decision row) and one per state for its plain rows, so that a
-  // small batch (LASER forks two states per JUMPI, svm.py:251-255) spreads its decision
-  // rows over the host threads; each task re-runs the state's base analysis, which is
-  // one analysis against the n_vars analyses of a decision row
+  // Per chunk of states: the base analysis, the variable slots and their compared
+  // constants once per state (in parallel), then one task per (state, decision row) and
+  // one per state for its plain rows, so that a small batch (LASER forks two states per
+  // JUMPI, svm.py:251-255) spreads its decision rows over the host threads.
   uint32_t n_dec_rows = 0;
   for (uint32_t c = 0, row = 0; c < n_cand && row < n_decide; c += every, ++row) ++n_dec_rows;
   const int64_t per_state = (int64_t)n_dec_rows + 1;
-#pragma omp parallel for schedule(dynamic, 1)
-  for (int64_t task = 0; task < (int64_t)n_states * per_state; ++task) {
-    const int64_t st = task / per_state;
-    const uint32_t task_row = (uint32_t)(task % per_state);  // < n_dec_rows: that decision row
-    const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
-    const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
+  struct Prep {
     State s;
-    const int r = refute_one(nodes + n0, n1 - n0, consts + 8ull * c0, c1 - c0, max_passes, &s);
-    if (task_row == n_dec_rows) out[st] = (int8_t)r;
-    if (r != 0) continue;
-    // (var slot, width, abstract value): VAR nodes and the fresh value of UF applications
+    int r = -1;
     std::vector<uint32_t> slot, width;
     std::vector<int32_t> node;
-    for (uint32_t i = 0; i < s.n; ++i) {
-      const mgp_node &x = s.nd[i];
-      uint32_t v;
-      if (x.op == MGP_OP_VAR) v = x.p0;
-      else if (x.op == MGP_OP_UFAPP || x.op == MGP_OP_UFINV) v = x.p1;
-      else continue;
-      if (v >= n_vars || x.width == 0u || x.width > MGP_MAX_WIDTH) continue;
-      slot.push_back(v);
-      width.push_back(x.width);
-      node.push_back((int32_t)i);
-    }
-    // Values each variable is compared equal to (x == c anywhere in the DAG, e.g. the
-    // sender against every ACTORS address, transaction/symbolic.py:165-167): an interval
-    // cannot hold such a value set, so decisions try them first and plain domain rows
-    // draw one half of the time when it lies inside the refined domain.
-    std::vector<std::vector<V>> eqh(slot.size());
-    for (size_t k = 0; k < slot.size(); ++k)
+    std::vector<std::vector<V>> eqh;
+  };
+  constexpr uint32_t kChunk = 256;
+  for (uint32_t cs = 0; cs < n_states; cs += kChunk) {
+    const uint32_t ce = std::min<uint32_t>(n_states, cs + kChunk);
+    std::vector<Prep> prep(ce - cs);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t st = cs; st < (int64_t)ce; ++st) {
+      Prep &P = prep[st - cs];
+      const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
+      const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
+      P.r = refute_one(nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, &P.s);
+      out[st] = (int8_t)P.r;
+      if (P.r != 0) continue;
+      const State &s = P.s;
+      // (var slot, width, abstract value): VAR nodes and the fresh value of UF applications
+      std::vector<int32_t> kof(s.n, -1);
+      for (uint32_t i = 0; i < s.n; ++i) {
+        const mgp_node &x = s.nd[i];
+        uint32_t v;
+        if (x.op == MGP_OP_VAR) v = x.p0;
+        else if (x.op == MGP_OP_UFAPP || x.op == MGP_OP_UFINV) v = x.p1;
+        else continue;
+        if (v >= n_vars || x.width == 0u || x.width > MGP_MAX_WIDTH) continue;
+        kof[i] = (int32_t)P.slot.size();
+        P.slot.push_back(v);
+        P.width.push_back(x.width);
+        P.node.push_back((int32_t)i);
+      }
+      // Values each variable is compared equal to (x == c anywhere in the DAG, e.g. the
+      // sender against every ACTORS address, transaction/symbolic.py:165-167): an interval
+      // cannot hold such a value set, so decisions try them first and plain domain rows
+      // draw one half of the time when it lies inside the refined domain.  In node order
+      // per variable, at most 16.
+      P.eqh.assign(P.slot.size(), {});
       for (uint32_t i = 0; i < s.n; ++i) {
         const mgp_node &x = s.nd[i];
         if (x.op != MGP_OP_EQ || x.a < 0 || x.b < 0) continue;
-        const int32_t other = x.a == node[k] ? x.b : (x.b == node[k] ? x.a : -1);
-        if (other < 0 || s.nd[other].op != MGP_OP_CONST || s.nd[other].width > MGP_MAX_WIDTH) continue;
-        if (s.nd[other].p0 >= s.n_consts || eqh[k].size() >= 16) continue;
-        V c;
-        memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
-        eqh[k].push_back(bv_mask(c, width[k]));
+        for (int side = 0; side < 2; ++side) {
+          const int32_t me = side ? x.b : x.a, other = side ? x.a : x.b;
+          const int32_t k = kof[me];
+          if (k < 0 || (side && x.a == x.b)) continue;
+          if (s.nd[other].op != MGP_OP_CONST || s.nd[other].width > MGP_MAX_WIDTH) continue;
+          if (s.nd[other].p0 >= s.n_consts || P.eqh[k].size() >= 16) continue;
+          V c;
+          memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
+          P.eqh[k].push_back(bv_mask(c, P.width[k]));
+        }
       }
-    auto inside = [&](const AV &a, const V &v) {
-      return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
-    };
-    // The first n_decide guided rows are built by decisions: each variable in turn is
-    // fixed to a draw from its current abstract value and the analysis re-run, so later
-    // variables are drawn from values narrowed by the earlier choices (x + y == c, a
-    // mapping key fixed by an equality, ...).  A draw that empties a domain is replaced
-    // (up to kTries draws); the remaining rows are plain draws from the refined domains.
-    constexpr uint32_t kTries = 4;
-    // two forward + backward passes per decision carry a fixed value to its relations
-    // (x + y == c, a mapping key), which is what the later draws need: the same witnesses
-    // as six passes on the contract corpus and on synthetic states, 1.3-1.7x faster (one
-    // pass loses 4 % on synthetic states).  MGP_DECIDE_PASSES overrides (A/B).
-    static const uint32_t decide_passes = [] {
-      const char *e = getenv("MGP_DECIDE_PASSES");
-      return e ? (uint32_t)atoi(e) : 2u;
-    }();
-    const uint32_t passes = std::min(max_passes ? max_passes : 16u, decide_passes ? decide_passes : 1u);
-    for (uint32_t c = 0, row = 0; c < n_cand; c += every, ++row) {
-      uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
-      if (task_row < n_dec_rows ? row != task_row : row < n_dec_rows) continue;
-      if (row < n_decide) {
-        State d = s;
-        for (size_t kk = 0; kk < slot.size(); ++kk) {
-          const size_t k = (row & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
-          const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
-          if (EQV(d.av[node[k]].lo, d.av[node[k]].hi)) {  // already one value: nothing to decide
-            memcpy(dst + slot[k] * 8ull, d.av[node[k]].lo.w, 32);
-            continue;
-          }
-          V v = bv_zero();
-          const uint32_t nh = (uint32_t)eqh[k].size();
-          for (uint32_t t = 0; t < kTries + nh; ++t) {
-            v = t < nh ? eqh[k][(t + row) % nh]
-                       : sample_av(d.av[node[k]], width[k], t > nh ? 3u + row + t : (row < 4 ? row / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + row : 0u)), mix64(key + t));
-            if (t < nh && !inside(d.av[node[k]], v)) continue;
-            State e = d;
-            if (e.meet(node[k], exact(v, width[k])) && e.tie() && e.run(passes) == 0) {
-              d = std::move(e);
-              break;
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t task = (int64_t)cs * per_state; task < (int64_t)ce * per_state; ++task) {
+      const int64_t st = task / per_state;
+      const uint32_t task_row = (uint32_t)(task % per_state);  // < n_dec_rows: that decision row
+      const Prep &P = prep[st - cs];
+      if (P.r != 0) continue;
+      const State &s = P.s;
+      const std::vector<uint32_t> &slot = P.slot, &width = P.width;
+      const std::vector<int32_t> &node = P.node;
+      const std::vector<std::vector<V>> &eqh = P.eqh;
+      auto inside = [&](const AV &a, const V &v) {
+        return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
+      };
+      // The first n_decide guided rows are built by decisions: each variable in turn is
+      // fixed to a draw from its current abstract value and the analysis re-run, so later
+      // variables are drawn from values narrowed by the earlier choices (x + y == c, a
+      // mapping key fixed by an equality, ...).  A draw that empties a domain is replaced
+      // (up to kTries draws); the remaining rows are plain draws from the refined domains.
+      constexpr uint32_t kTries = 4;
+      // a decision propagates from the decided node only (State::run_from: backward into
+      // its operands, through its users, transitively, then the pair orderings), with an
+      // undo log for a draw that empties a domain; MGP_DECIDE_PASSES=k re-runs k full
+      // passes instead (A/B: the same witnesses)
+      static const uint32_t decide_passes = [] {
+        const char *e = getenv("MGP_DECIDE_PASSES");
+        return e ? (uint32_t)atoi(e) : 0u;
+      }();
+      const uint32_t passes = std::min(max_passes ? max_passes : 16u, decide_passes ? decide_passes : 1u);
+      for (uint32_t c = 0, row = 0; c < n_cand; c += every, ++row) {
+        uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
+        if (task_row < n_dec_rows ? row != task_row : row < n_dec_rows) continue;
+        if (row < n_decide) {
+          State d = s;
+          std::vector<State::UndoRec> undo_log;
+          std::vector<uint32_t> work;
+          d.build_graph();
+          d.undo = &undo_log;
+          d.touched = &work;
+          const uint32_t budget = 2u * d.n + 64u;
+          for (size_t kk = 0; kk < slot.size(); ++kk) {
+            const size_t k = (row & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
+            const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
+            if (EQV(d.av[node[k]].lo, d.av[node[k]].hi)) {  // already one value: nothing to decide
+              memcpy(dst + slot[k] * 8ull, d.av[node[k]].lo.w, 32);
+              continue;
             }
+            V v = bv_zero();
+            const uint32_t nh = (uint32_t)eqh[k].size();
+            for (uint32_t t = 0; t < kTries + nh; ++t) {
+              v = t < nh ? eqh[k][(t + row) % nh]
+                         : sample_av(d.av[node[k]], width[k], t > nh ? 3u + row + t : (row < 4 ? row / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + row : 0u)), mix64(key + t));
+              if (t < nh && !inside(d.av[node[k]], v)) continue;
+              const size_t mark = undo_log.size();
+              work.clear();
+              if (d.meet(node[k], exact(v, width[k])) &&
+                  (decide_passes ? d.tie() && d.run(passes) == 0 : d.run_from((uint32_t)node[k], budget) == 0)) {
+                undo_log.clear();
+                break;
+              }
+              d.rollback(mark);
+            }
+            memcpy(dst + slot[k] * 8ull, v.w, 32);
+          }
+          continue;
+        }
+        for (size_t k = 0; k < slot.size(); ++k) {
+          const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
+          V v = sample_av(s.av[node[k]], width[k], row, key);
+          if (!eqh[k].empty() && (mix64(key ^ 0x9E37ull) & 1u)) {
+            const V h = eqh[k][mix64(key ^ 0x7F4Aull) % eqh[k].size()];
+            if (inside(s.av[node[k]], h)) v = h;
           }
           memcpy(dst + slot[k] * 8ull, v.w, 32);
         }
-        continue;
-      }
-      for (size_t k = 0; k < slot.size(); ++k) {
-        const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
-        V v = sample_av(s.av[node[k]], width[k], row, key);
-        if (!eqh[k].empty() && (mix64(key ^ 0x9E37ull) & 1u)) {
-          const V h = eqh[k][mix64(key ^ 0x7F4Aull) % eqh[k].size()];
-          if (inside(s.av[node[k]], h)) v = h;
-        }
-        memcpy(dst + slot[k] * 8ull, v.w, 32);
       }
     }
   }

@@ -352,6 +352,71 @@ def test_division_all_variants_every_candidate(mgp_ctx, w):
                     f"a={a:#x} b={b:#x} expected {e:#x}")
 
 
+def _single_digit_pairs(rng, n, w, signed):
+    """(a, b) with top limb(a) = top limb(b) on every dividing lane (quotient < 2^32: the
+    interpreter's single-digit path), the top limb varying per lane, quotients at the
+    extremes (0, 1, 2^32 - 1, exact multiples and one below), a few b = 0 / a < b lanes."""
+    limbs = w // 32 - (1 if signed else 0)
+    m = (1 << w) - 1
+    out = []
+    for j in range(n):
+        t = int(rng.integers(0, max(1, limbs)))
+        kind = j % 8
+        if kind == 7:
+            out.append((int(rng.integers(0, 2 ** 31)) << (32 * t), 0))
+            continue
+        q = [0, 1, 2 ** 32 - 1, int(rng.integers(0, 2 ** 32)), int(rng.integers(0, 2 ** 16)),
+             2 ** 32 - 2, int(rng.integers(2 ** 31, 2 ** 32))][kind]
+        top = int(rng.integers(1, max(2, (2 ** 32 - 1) // (q + 1) + 1)))
+        low = int.from_bytes(rng.integers(0, 256, size=32, dtype=np.uint8).tobytes(), "little")
+        big = int.from_bytes(rng.integers(0, 256, size=40, dtype=np.uint8).tobytes(), "little")
+        a = b = 0
+        for lowmask in ((1 << (32 * t)) - 1, 0):     # lower limbs of b random, else zero
+            b = (top << (32 * t)) | (low & lowmask)
+            r = [0, b - 1, big % b, 0][j % 4]
+            a = q * b + r
+            if not (a >> (32 * (t + 1)) or (signed and a >> (w - 1))):
+                break
+        else:
+            a = b
+        if signed:
+            if rng.integers(0, 2):
+                a = (-a) & m
+            if rng.integers(0, 2):
+                b = (-b) & m
+        out.append((a, b))
+    return out
+
+
+@pytest.mark.parametrize("w", [256, 64])
+def test_division_single_digit_waves(mgp_ctx, w):
+    """Waves whose dividing lanes all have one quotient digit take the interpreter's
+    double-precision single-digit path (gen_eval_asm.single_digit): every variant, every
+    candidate, root = (op(x0, x1) != x2) as in the test above."""
+    rng = np.random.default_rng(31 + w)
+    ops = [S.UDIV, S.UREM, S.SDIV, S.SREM, S.SMOD]
+    n_cand, per_op = 256, 3
+    states, rows = [], []
+    for op in ops:
+        for _ in range(per_op):
+            pairs = _single_digit_pairs(rng, n_cand, w, op in (S.SDIV, S.SREM, S.SMOD))
+            exp = [S.binop(op, x, y, w) for x, y in pairs]
+            nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0], [S.VAR, w, -1, -1, -1, 2, 0],
+                  [op, w, 0, 1, -1, 0, 0], [S.EQ, 1, 3, 2, -1, 0, 0], [S.BNOT, 1, 4, -1, -1, 0, 0]]
+            states.append((nl, []))
+            rows.append([[x, y, e] for (x, y), e in zip(pairs, exp)])
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    first, _ = mgp_ctx.eval_batch(words, po, cands_from_ints(rows))
+    bad = np.nonzero(first != N.MGP_NO_SAT)[0]
+    if bad.size:
+        s0 = int(bad[0])
+        a, b, e = rows[s0][int(first[s0])]
+        pytest.fail(f"{bad.size} states with a wrong quotient/remainder; first: op {ops[s0 // per_op]} "
+                    f"a={a:#x} b={b:#x} expected {e:#x}")
+
+
 def test_back_to_back_batches_same_context(mgp_ctx):
     """Consecutive batches of the same size on one context reuse the same device buffers
     (and launch-descriptor addresses) with different programs: every batch must see its

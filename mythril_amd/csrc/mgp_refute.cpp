@@ -26,6 +26,7 @@
 // has a model, exhaustively at small widths).
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 
 #include <vector>
 
@@ -255,18 +256,30 @@ uint8_t dec_eq(const AV &a, const AV &b) {
 
 // signed order = unsigned order after flipping the sign bit
 AV flip(const AV &a, uint32_t w) {
-  const V sb = BIT(w - 1u), m = M(w);
+  // the sign bit sits in one limb: swap it between the known-zero and known-one masks and
+  // toggle it in the bounds there (limb-wise; the decision rows call this per signed
+  // compare, e.g. every calldata byte guard)
+  const uint32_t li = (w - 1u) >> 5, sb = 1u << ((w - 1u) & 31u);
   AV r;
-  r.z = OR(AND(a.z, NOT(sb)), AND(a.o, sb));
-  r.o = OR(AND(a.o, NOT(sb)), AND(a.z, sb));
-  r.z = OR(r.z, NOT(m));
-  r.o = AND(r.o, m);
-  if (EQV(AND(a.lo, sb), AND(a.hi, sb))) {
-    r.lo = XOR(a.lo, sb);
-    r.hi = XOR(a.hi, sb);
+  for (uint32_t i = 0; i < 8; ++i) {
+    const uint32_t m = bv_limb_mask(w, (int)i);
+    uint32_t z = a.z.w[i], o = a.o.w[i];
+    if (i == li) {
+      const uint32_t zb = z & sb, ob = o & sb;
+      z = (z & ~sb) | ob;
+      o = (o & ~sb) | zb;
+    }
+    r.z.w[i] = z | ~m;
+    r.o.w[i] = o & m;
+  }
+  if ((a.lo.w[li] & sb) == (a.hi.w[li] & sb)) {
+    r.lo = a.lo;
+    r.hi = a.hi;
+    r.lo.w[li] ^= sb;
+    r.hi.w[li] ^= sb;
   } else {
     r.lo = bv_zero();
-    r.hi = m;
+    r.hi = M(w);
   }
   return r;
 }
@@ -310,6 +323,7 @@ struct State {
   std::vector<UndoRec> *undo = nullptr;
   std::vector<uint32_t> *touched = nullptr;
   std::vector<uint32_t> uoff, ulist, voff, vlist;  // users of each node; VAR nodes of each entry
+  std::vector<uint8_t> tie_rel;  // nodes tie() reads: compares with a pair, BOR, pair operands
 
   uint32_t W(int32_t i) const { return nd[i].width; }
 
@@ -320,6 +334,7 @@ struct State {
     t.o = OR(t.o, s.o);
     t.lo = MAX(t.lo, s.lo);
     t.hi = MIN(t.hi, s.hi);
+    if (same(t, av[i])) return true;  // s adds nothing (stored values are normalised)
     if (!normalize(t, w)) return false;
     if (!same(t, av[i])) {
       if (undo) undo->push_back(UndoRec{0, (uint32_t)i, av[i], 0, 0, 0});
@@ -347,7 +362,7 @@ struct State {
     t.o = OR(t.o, s.o);
     t.lo = MAX(t.lo, s.lo);
     t.hi = MIN(t.hi, s.hi);
-    return normalize(t, nd[i].width);
+    return same(t, av[i]) || normalize(t, nd[i].width);
   }
 
   // ------------------------------------------------------------ validate
@@ -1011,6 +1026,10 @@ struct State {
     std::vector<uint32_t> vp(voff.begin(), voff.end() - 1);
     for (uint32_t i = 0; i < n; ++i)
       if (nd[i].op == MGP_OP_VAR && vtie[i] >= 0) vlist[vp[vtie[i]]++] = i;
+    tie_rel.assign(n, 0);
+    for (uint32_t i = 0; i < n; ++i)
+      if (cmp_pair[i] >= 0 || nd[i].op == MGP_OP_BOR) tie_rel[i] = 1;
+    for (const Pair &p : pairs) tie_rel[p.x] = tie_rel[p.y] = 1;
   }
   void rollback(size_t mark) {
     while (undo->size() > mark) {
@@ -1024,30 +1043,39 @@ struct State {
   }
   // Propagation from one changed node (a decision): backward into its operands, forward
   // and backward through its users, transitively over the nodes that change, then the
-  // pair orderings; at most `budget` node visits.  1 = the decision empties a domain.
-  // Only decision rows use it (candidates, checked on the GPU); refutations run().
+  // pair orderings when a node they read changed; at most `budget` transfer-function
+  // evaluations (a node with many users, e.g. calldatasize under every byte guard, counts
+  // each of them).  1 = the decision empties a domain.  Only decision rows use it
+  // (candidates, checked on the GPU); refutations run().
   int run_from(uint32_t seed, uint32_t budget) {
     std::vector<uint32_t> &T = *touched;
     T.clear();
     T.push_back(seed);
     size_t head = 0;
-    uint32_t visits = 0;
+    uint32_t work = 0;
+    bool need_tie = false;
     for (int round = 0; round < 3; ++round) {
       while (head < T.size()) {
         const uint32_t t = T[head++];
-        if (++visits > budget) return 0;
         if (t & kVarBit) {  // a variable's shared value changed: every VAR node of it
           const uint32_t j = t & ~kVarBit;
+          if ((work += voff[j + 1] - voff[j] + 1) > budget) return 0;
           for (uint32_t k = voff[j]; k < voff[j + 1]; ++k)
             if (!forward(vlist[k])) return 1;
           continue;
         }
+        need_tie |= tie_rel[t] != 0;
+        if ((work += 2u * (uoff[t + 1] - uoff[t]) + 1u) > budget) return 0;
         if (!backward(t)) return 1;
         for (uint32_t k = uoff[t]; k < uoff[t + 1]; ++k)
           if (!forward(ulist[k]) || !backward(ulist[k])) return 1;
       }
       const size_t before = T.size();
-      if (!meetb((int32_t)n - 1, BT) || !tie()) return 1;
+      if (!meetb((int32_t)n - 1, BT)) return 1;
+      if (need_tie) {  // tie() is at its fixpoint unless a node it reads changed
+        need_tie = false;
+        if (!tie()) return 1;
+      }
       if (T.size() == before) break;
     }
     return 0;
@@ -1329,9 +1357,16 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
           d.build_graph();
           d.undo = &undo_log;
           d.touched = &work;
-          const uint32_t budget = 2u * d.n + 64u;
+          const uint32_t budget = 4u * d.n + 64u;
+          // the draw schedule of decision row `row`: the first eight rows decide in node
+          // order (schedules 0, 2, .., 14), later ones add the reverse-order schedules
+          // (odd) and then the rest, so any n_decide = 16 + k covers schedules 0..15+k.
+          // Node order is what contract states need (WalletLibrary's loop and mapping
+          // queries: 60 against 57 states of the mixed corpus at eight rows, at a third
+          // of the host time)
+          const uint32_t drow = row < 8u ? 2u * row : row < 16u ? 2u * (row - 8u) + 1u : row;
           for (size_t kk = 0; kk < slot.size(); ++kk) {
-            const size_t k = (row & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
+            const size_t k = (drow & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
             const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
             if (EQV(d.av[node[k]].lo, d.av[node[k]].hi)) {  // already one value: nothing to decide
               memcpy(dst + slot[k] * 8ull, d.av[node[k]].lo.w, 32);
@@ -1340,8 +1375,8 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
             V v = bv_zero();
             const uint32_t nh = (uint32_t)eqh[k].size();
             for (uint32_t t = 0; t < kTries + nh; ++t) {
-              v = t < nh ? eqh[k][(t + row) % nh]
-                         : sample_av(d.av[node[k]], width[k], t > nh ? 3u + row + t : (row < 4 ? row / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + row : 0u)), mix64(key + t));
+              v = t < nh ? eqh[k][(t + drow) % nh]
+                         : sample_av(d.av[node[k]], width[k], t > nh ? 3u + drow + t : (drow < 4 ? drow / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + drow : 0u)), mix64(key + t));
               if (t < nh && !inside(d.av[node[k]], v)) continue;
               const size_t mark = undo_log.size();
               work.clear();

@@ -446,7 +446,7 @@ class Prefilter:
             open_ = left
         SolverStatistics().gpu_retry += len(retry)
 
-    DECIDE_US_PER_UNIT = 0.12  # host cost of one decision row, per (variable x DAG node)
+    DECIDE_US_PER_UNIT = 0.06  # host CPU cost of one decision row, per (variable x DAG node)
 
     def _within_decide_budget(self, states, open_, n_decide, budget_ms=None):
         """The open states whose host decision rows fit budget_ms (default decide_budget_ms)

@@ -170,7 +170,7 @@ def test_host_decisions_keep_to_their_time_budget():
     kfm = KeccakFunctionManager()
     states = [list(t) for _, t, _ in corpus.wallet_states(0, kfm)[:4]]
     states += [list(corpus.bectoken_states(k, kfm)[1]) for k in range(4)]
-    fake = types.SimpleNamespace(decide_budget_ms=100.0, DECIDE_US_PER_UNIT=SV.Prefilter.DECIDE_US_PER_UNIT)
+    fake = types.SimpleNamespace(decide_budget_ms=20.0, DECIDE_US_PER_UNIT=SV.Prefilter.DECIDE_US_PER_UNIT)
     pick = SV.Prefilter._within_decide_budget(fake, states, list(range(8)), 8)
     assert set(range(4, 8)) <= set(pick)          # the small BECToken states first
     assert len(pick) < 8

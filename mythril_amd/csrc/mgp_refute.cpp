@@ -1375,7 +1375,7 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
             V v = bv_zero();
             const uint32_t nh = (uint32_t)eqh[k].size();
             for (uint32_t t = 0; t < kTries + nh; ++t) {
-              v = t < nh ? eqh[k][(t + drow) % nh]
+              v = t < nh ? eqh[k][(t + drow + (drow < 8u ? 0u : (uint32_t)(key >> 40))) % nh]
                          : sample_av(d.av[node[k]], width[k], t > nh ? 3u + drow + t : (drow < 4 ? drow / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + drow : 0u)), mix64(key + t));
               if (t < nh && !inside(d.av[node[k]], v)) continue;
               const size_t mark = undo_log.size();

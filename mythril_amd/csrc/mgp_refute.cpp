@@ -28,6 +28,8 @@
 #include <string.h>
 #include <stdlib.h>
 
+#include <algorithm>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/mgp.h"
@@ -287,6 +289,7 @@ AV flip(const AV &a, uint32_t w) {
 struct State {
   const mgp_node *nd;
   std::vector<mgp_node> relaxed;  // nd when the DAG holds wide values (relax_wide)
+  const mgp_node *orig = nullptr;  // the DAG before relax_wide (UF arguments, congruence)
   uint32_t n;
   const uint32_t *consts;
   uint64_t n_consts;
@@ -324,6 +327,16 @@ struct State {
   std::vector<uint32_t> *touched = nullptr;
   std::vector<uint32_t> uoff, ulist, voff, vlist;  // users of each node; VAR nodes of each entry
   std::vector<uint8_t> tie_rel;  // nodes tie() reads: compares with a pair, BOR, pair operands
+  // UF congruence (f(a) = f(b) when a = b is known, the Ackermann axiom the lowering's
+  // ITE chains implement, include/mgp_ir.h): the applications of each function with at
+  // most kUfGroup of them, sorted by (op, function); arguments compared on the original
+  // DAG, so a keccak256_512 application whose 512-bit argument was relaxed still meets
+  // the value of an application of the same key (WalletLibrary's m_ownerIndex[sender]
+  // read in tx 2 against the write in tx 1 when both senders are equal)
+  struct UfApp { int32_t node, arg; uint32_t fn; uint8_t op; };
+  static constexpr uint32_t kUfGroup = 48;
+  std::vector<UfApp> ufs;
+  std::unordered_map<uint64_t, int32_t> pair_of;  // (x << 32 | y), x < y -> pairs index
 
   uint32_t W(int32_t i) const { return nd[i].width; }
 
@@ -460,17 +473,60 @@ struct State {
         py = x.a;
         t = (uint8_t)((t & OEQ) | ((t & OLT) ? OGT : 0) | ((t & OGT) ? OLT : 0));
       }
-      int32_t pi = -1;
-      for (size_t k = 0; k < pairs.size(); ++k)
-        if (pairs[k].x == px && pairs[k].y == py) pi = (int32_t)k;
+      const uint64_t pk = ((uint64_t)(uint32_t)px << 32) | (uint32_t)py;
+      auto pit = pair_of.find(pk);
+      int32_t pi = pit == pair_of.end() ? -1 : pit->second;
       if (pi < 0) {
         pi = (int32_t)pairs.size();
         pairs.push_back({px, py, OALL, OALL});
+        pair_of.emplace(pk, pi);
       }
       cmp_pair[i] = pi;
       cmp_dom[i] = dom;
       cmp_t[i] = t;
     }
+    ufs.clear();
+    const mgp_node *o = orig ? orig : nd;
+    for (uint32_t i = 0; i < n; ++i)
+      if ((o[i].op == MGP_OP_UFAPP || o[i].op == MGP_OP_UFINV) && !isb[i] && o[i].width == nd[i].width)
+        ufs.push_back({(int32_t)i, o[i].a, o[i].p0, o[i].op});
+    std::stable_sort(ufs.begin(), ufs.end(), [](const UfApp &x, const UfApp &y) {
+      return x.op != y.op ? x.op < y.op : x.fn < y.fn;
+    });
+    std::vector<UfApp> keep;
+    for (size_t i = 0; i < ufs.size();) {
+      size_t j = i;
+      while (j < ufs.size() && ufs[j].op == ufs[i].op && ufs[j].fn == ufs[i].fn) ++j;
+      if (j - i >= 2 && j - i <= kUfGroup) keep.insert(keep.end(), ufs.begin() + i, ufs.begin() + j);
+      i = j;
+    }
+    ufs.swap(keep);
+  }
+
+  // x and y (nodes of the original DAG) are known to have equal values: the same node,
+  // equal exact values, a pair known equal, or the same operator over operands known
+  // equal (depth-limited)
+  bool arg_equal(int32_t x, int32_t y, int depth) const {
+    if (x == y) return true;
+    if (x < 0 || y < 0) return false;
+    const mgp_node *o = orig ? orig : nd;
+    const mgp_node &a = o[x], &b = o[y];
+    if (a.width != b.width) return false;
+    if (a.width <= MGP_MAX_WIDTH && !isb[x] && !isb[y]) {
+      if (is_exact(av[x]) && is_exact(av[y]) && EQV(av[x].lo, av[y].lo)) return true;
+      const uint64_t pk = x < y ? ((uint64_t)(uint32_t)x << 32) | (uint32_t)y : ((uint64_t)(uint32_t)y << 32) | (uint32_t)x;
+      auto it = pair_of.find(pk);
+      if (it != pair_of.end() && pairs[it->second].u == OEQ) return true;
+    }
+    if (depth == 0 || a.op != b.op || a.p0 != b.p0 || a.p1 != b.p1) return false;
+    switch (a.op) {
+      case MGP_OP_VAR: return true;  // same variable, same width
+      case MGP_OP_CONST: return false;  // different pool entries (narrow ones compared above)
+      case MGP_OP_TRUE: case MGP_OP_FALSE: return true;
+      default: break;
+    }
+    return (a.a < 0 || arg_equal(a.a, b.a, depth - 1)) && (a.b < 0 || arg_equal(a.b, b.b, depth - 1)) &&
+           (a.c < 0 || arg_equal(a.c, b.c, depth - 1));
   }
 
   bool set_order(Pair &p, uint8_t dom, uint8_t m) {
@@ -492,7 +548,7 @@ struct State {
     return true;
   }
   bool tie() {
-    if (pairs.empty()) return true;
+    if (pairs.empty() && ufs.empty()) return true;
     for (int sweep = 0; sweep < 2; ++sweep)
       for (uint32_t i = 0; i < n; ++i) {
         const int32_t pi = cmp_pair[i];
@@ -541,6 +597,15 @@ struct State {
       }
       if (!meet(lo_n, a) || !meet(hi_n, b)) return false;
     }
+    for (size_t i = 0; i < ufs.size(); ++i)
+      for (size_t j = i + 1; j < ufs.size() && ufs[j].fn == ufs[i].fn && ufs[j].op == ufs[i].op; ++j) {
+        if (!arg_equal(ufs[i].arg, ufs[j].arg, 3)) continue;
+        const int32_t x = ufs[i].node, y = ufs[j].node;
+        const AV ax = av[x], ay = av[y];
+        if (!meet(x, ay) || !meet(y, ax)) return false;
+        auto it = pair_of.find(((uint64_t)(uint32_t)std::min(x, y) << 32) | (uint32_t)std::max(x, y));
+        if (it != pair_of.end() && !set_order(pairs[it->second], 2, OEQ)) return false;
+      }
     return true;
   }
 
@@ -1030,6 +1095,7 @@ struct State {
     for (uint32_t i = 0; i < n; ++i)
       if (cmp_pair[i] >= 0 || nd[i].op == MGP_OP_BOR) tie_rel[i] = 1;
     for (const Pair &p : pairs) tie_rel[p.x] = tie_rel[p.y] = 1;
+    for (const UfApp &u : ufs) tie_rel[u.node] = 1;
   }
   void rollback(size_t mark) {
     while (undo->size() > mark) {
@@ -1154,6 +1220,7 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
   if (n == 0 || n > (1u << 20)) return -1;
   State st;
   State &s = keep ? *keep : st;
+  s.orig = nd;
   if (relax_wide(nd, n, s.relaxed)) nd = s.relaxed.data();
   s.nd = nd;
   s.n = (uint32_t)n;

@@ -372,3 +372,100 @@ def test_refute_domains_agree_with_refute_and_contain_witnesses():
             assert lo <= x <= hi and x & z == 0 and x & o == o, (s, v)
             checked += 1
     assert checked > 100
+
+
+# ------------------------------------------------- UF congruence (pair ties)
+def test_uf_congruence_refutes_equal_keys_with_different_values():
+    """f(Concat(a, c)) and f(Concat(b, c)) with a == b asserted have equal values (the
+    Ackermann axiom of include/mgp_ir.h UFAPP): asserting the values differ is refuted
+    (WalletLibrary: the tx-2 sender equal to the initializer reads m_ownerIndex[sender] != 0,
+    corpus.py "wallet:initializer not owner"); without a == b it stays open; with the
+    arguments structurally different (c vs c') nothing is concluded."""
+    A_, B_ = X0, X1
+    C0 = [S.CONST, 256, -1, -1, -1, 0, 0]
+    C1 = [S.CONST, 256, -1, -1, -1, 1, 0]
+    base = [A_, B_, C0, C1,
+            [S.CONCAT, 512, 0, 2, -1, 0, 0], [S.CONCAT, 512, 1, 2, -1, 0, 0],      # 4, 5
+            [S.UFAPP, 256, 4, -1, -1, 9, 2], [S.UFAPP, 256, 5, -1, -1, 9, 3],      # 6, 7
+            [S.EQ, 1, 6, 7, -1, 0, 0], [S.BNOT, 1, 8, -1, -1, 0, 0]]               # 8, 9
+    eq_ab = base + [[S.EQ, 1, 0, 1, -1, 0, 0], [S.BAND, 1, 9, 10, -1, 0, 0]]
+    free = base + [[S.ULT, 1, 0, 3, -1, 0, 0], [S.BAND, 1, 9, 10, -1, 0, 0]]
+    # the keys differ in their constant part: f-values may differ even when a == b
+    other = [A_, B_, C0, C1, [S.CONCAT, 512, 0, 2, -1, 0, 0], [S.CONCAT, 512, 1, 3, -1, 0, 0],
+             [S.UFAPP, 256, 4, -1, -1, 9, 2], [S.UFAPP, 256, 5, -1, -1, 9, 3],
+             [S.EQ, 1, 6, 7, -1, 0, 0], [S.BNOT, 1, 8, -1, -1, 0, 0],
+             [S.EQ, 1, 0, 1, -1, 0, 0], [S.BAND, 1, 9, 10, -1, 0, 0]]
+    # the value equality reached through a read-over-write ITE (value must be 0, the
+    # stored value at the equal key is 1)
+    row = base[:8] + [[S.EQ, 1, 6, 7, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 2, 0],
+                      [S.ITE, 256, 8, 9, 1, 0, 0], [S.EQ, 1, 10, 2, -1, 0, 0],     # ITE(k2==k1, 1, b) == 0
+                      [S.EQ, 1, 0, 1, -1, 0, 0], [S.BAND, 1, 11, 12, -1, 0, 0]]
+    out = _refute([(eq_ab, [0, 7]), (free, [0, 7]), (other, [0, 7]), (row, [0, 7, 1])])
+    assert list(out) == [1, 0, 0, 1]
+    # free: a != b and different fresh values is a model
+    assert S.eval_root(free, [0, 7], [1, 2, 5, 6])
+
+
+def test_uf_congruence_exhaustive_soundness():
+    """Random small DAGs over two 3-bit variables and applications of one UF (direct and
+    through Concat arguments) with compares, ITEs and Bool structure: no refuted state
+    has a model among every assignment of the variables and the fresh UF values
+    (C oracle over all 8^k combinations)."""
+    rng = np.random.default_rng(0xC0C0)
+    w = 3
+    states = []
+    for _ in range(160):
+        nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
+        cl = [int(rng.integers(0, 8)) for _ in range(2)]
+        nl += [[S.CONST, w, -1, -1, -1, 0, 0], [S.CONST, w, -1, -1, -1, 1, 0]]
+        vals, bools = [0, 1, 2, 3], []
+        n_uf = 0
+        for _ in range(int(rng.integers(6, 14))):
+            k = rng.random()
+            if k < 0.35 and n_uf < 3:
+                a = int(rng.choice(vals))
+                if rng.random() < 0.5:     # f(Concat(x, c)) at twice the width, value w bits
+                    nl.append([S.CONCAT, 2 * w, a, int(rng.choice([2, 3])), -1, 0, 0])
+                    nl.append([S.UFAPP, w, len(nl) - 1, -1, -1, 5, 2 + n_uf])
+                    # (2w-bit argument: the function is keyed by its argument width too)
+                    nl[-1][5] = 6
+                else:
+                    nl.append([S.UFAPP, w, a, -1, -1, 5, 2 + n_uf])
+                n_uf += 1
+                vals.append(len(nl) - 1)
+            elif k < 0.55:
+                op = [S.ADD, S.XOR, S.SUB][int(rng.integers(3))]
+                nl.append([op, w, int(rng.choice(vals)), int(rng.choice(vals)), -1, 0, 0])
+                vals.append(len(nl) - 1)
+            elif k < 0.65 and bools:
+                nl.append([S.ITE, w, int(rng.choice(bools)), int(rng.choice(vals)), int(rng.choice(vals)), 0, 0])
+                vals.append(len(nl) - 1)
+            elif k < 0.9:
+                op = [S.EQ, S.ULT, S.EQ][int(rng.integers(3))]
+                nl.append([op, 1, int(rng.choice(vals)), int(rng.choice(vals)), -1, 0, 0])
+                bools.append(len(nl) - 1)
+            elif bools:
+                nl.append([S.BNOT, 1, int(rng.choice(bools)), -1, -1, 0, 0])
+                bools.append(len(nl) - 1)
+        while len(bools) < 2:
+            nl.append([S.EQ, 1, int(rng.choice(vals)), int(rng.choice(vals)), -1, 0, 0])
+            bools.append(len(nl) - 1)
+        root = bools[-1]
+        for b in bools[-4:-1]:
+            nl.append([S.BAND, 1, root, b, -1, 0, 0])
+            root = len(nl) - 1
+        states.append((nl, cl))
+    verdict = _refute(states)
+    n_vars = 5
+    grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T  # 32768 x 5
+    cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    refuted = 0
+    for (nl, cl), r in zip(states, verdict):
+        assert r in (0, 1)
+        if r != 1:
+            continue
+        refuted += 1
+        nodes, noff, consts, coff = pack_states([(nl, cl)])
+        assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
+    assert refuted > 10

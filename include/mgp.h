@@ -180,8 +180,11 @@ int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes,
  * [state][cand][var][8 limbs]); other rows and variables the DAG does not
  * read are left as given.  The first n_decide of those rows are built by
  * decisions: each variable in turn is fixed to a draw from its current
- * abstract value and the analysis re-run (at most 6 passes), so later
- * variables see the narrowing the earlier choices cause.  UF applications get their fresh value slot (p1)
+ * abstract value and the analysis re-propagated from the decided node (a
+ * bounded worklist; MGP_DECIDE_PASSES=k re-runs k full passes instead), so
+ * later variables see the narrowing the earlier choices cause.  Decision rows
+ * 0-7 decide in variable order, rows 8-15 in reverse order, later rows in
+ * either.  UF applications get their fresh value slot (p1)
  * from the application's abstract value (keccak intervals, alignment).
  * Deterministic in seed.  out[s] as mgp_refute.  Replaces nothing in the
  * reference: it feeds the GPU witness search that answers get_model /

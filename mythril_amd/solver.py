@@ -195,6 +195,15 @@ class UnsatCores:
     def reset(self) -> None:
         self.sets: List[frozenset] = []
         self.index: Dict[Term, List[int]] = {}  # every stored set under ONE of its members
+        self.pending: List[list] = []  # refuted lists not yet shrunk (Prefilter.core_batch)
+
+    def flush(self, N) -> None:
+        """Shrink the pending refuted constraint lists to cores (one batched shrink_many)
+        and store them."""
+        if self.pending:
+            pending, self.pending = self.pending, []
+            for core in UnsatCores.shrink_many(N, pending):
+                self.add(core)
 
     def covered(self, terms: Iterable[Term]) -> bool:
         s = set(terms)
@@ -286,6 +295,13 @@ class Prefilter:
         # each witness found saves a fallback call)
         self.decide_budget_ms = 100.0
         self.decide_ms_per_state = 1.0
+        # host CPU microseconds per decision row and (variable x DAG node), re-measured on
+        # every decision round (moving average), so the budget admits what this host runs
+        self.decide_us_per_unit = self.DECIDE_US_PER_UNIT
+        # refuted constraint lists wait in the core cache and are shrunk to cores together
+        # once core_batch of them are pending (flush_cores): one batched shrink instead of
+        # one per call keeps the deletion trials off the latency of small calls
+        self.core_batch = 32
         self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
@@ -380,11 +396,16 @@ class Prefilter:
         prof["results_ms"] = 1e3 * (time.perf_counter() - tr)
         tr = time.perf_counter()
         if refuted:
-            for core in UnsatCores.shrink_many(self._N, [states[i] for i in refuted]):
-                _cores.add(core)
+            _cores.pending.extend(list(states[i]) for i in refuted)
+            if len(_cores.pending) >= self.core_batch:
+                self.flush_cores()
         prof["cores_ms"] = 1e3 * (time.perf_counter() - tr)
         self.last_profile = prof
         return out
+
+    def flush_cores(self) -> None:
+        """Shrink the pending refuted constraint lists to cores and store them."""
+        _cores.flush(self._N)
 
     # witness rounds for the states the first round and the pre-check leave open: a larger
     # GPU round (candidates generated on the device, domain rows with a new seed), then
@@ -432,7 +453,12 @@ class Prefilter:
             c2 = self._N.make_candidates(n2, sv, seed, SB.var_off, SB.var_width, SB.hint_off, SB.hints,
                                          SB.alias_off, SB.aliases, SB.const_off, SB.consts, D._FIXED_LIMBS,
                                          np.zeros(len(open_), np.uint8), var_kind=SB.var_kind)
+            tg = time.perf_counter()
             self._N.guided_candidates(*SB.packed(), c2, seed=seed, every=2, n_decide=n_decide)
+            units = float((np.diff(SB.var_off).astype(np.float64) * np.diff(SB.node_off)).sum())
+            if units > 0:
+                meas = (time.perf_counter() - tg) * 1e6 * self._decide_threads() / (units * n_decide)
+                self.decide_us_per_unit = min(1.0, max(0.005, 0.5 * self.decide_us_per_unit + 0.5 * meas))
             f2, w2 = self.ctx.eval_batch(sw, sp, c2)
             unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
             left = []
@@ -448,21 +474,26 @@ class Prefilter:
 
     DECIDE_US_PER_UNIT = 0.06  # host CPU cost of one decision row, per (variable x DAG node)
 
+    @staticmethod
+    def _decide_threads() -> int:
+        import os
+
+        return max(1, min(16, os.cpu_count() or 1))
+
     def _within_decide_budget(self, states, open_, n_decide, budget_ms=None):
         """The open states whose host decision rows fit budget_ms (default decide_budget_ms)
         of wall time (one task per state and row over the host threads), cheapest first."""
         budget_ms = self.decide_budget_ms if budget_ms is None else budget_ms
-        import os
-
         from .front import Batch
 
         B = Batch([states[i] for i in open_])
         units = np.diff(B.var_off).astype(np.float64) * np.diff(B.node_off).astype(np.float64)
         B.close()
-        threads = max(1, min(16, os.cpu_count() or 1))
+        threads = Prefilter._decide_threads()
+        us_per_unit = getattr(self, "decide_us_per_unit", self.DECIDE_US_PER_UNIT)
         keep, cpu_ms = [], 0.0
         for k in np.argsort(units, kind="stable"):
-            c = units[k] * n_decide * self.DECIDE_US_PER_UNIT * 1e-3
+            c = units[k] * n_decide * us_per_unit * 1e-3
             tasks = (len(keep) + 1) * n_decide
             if (cpu_ms + c) / min(threads, tasks) > budget_ms:
                 break

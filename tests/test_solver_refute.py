@@ -112,6 +112,9 @@ def test_unsat_core_cache(fe):
     assert SV.batch_is_possible([SV.Constraints(a)]) == [False]
     st = SV.SolverStatistics()
     assert st.refuted == 1 and st.core_hits == 0
+    # refuted lists are shrunk in batches (Prefilter.core_batch); flush the pending one
+    assert SV.unsat_cores().sets == [] and len(SV.unsat_cores().pending) == 1
+    SV.prefilter().flush_cores()
     # the stored core is the contradiction alone, not the whole path
     assert SV.unsat_cores().sets == [frozenset({a[0].raw, a[2].raw})]
     # another path repeating the contradiction: UNSAT from the cache, no analysis, no fallback

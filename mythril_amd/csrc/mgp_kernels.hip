@@ -1073,11 +1073,24 @@ static int desc_mode() {
   return v;
 }
 
+static std::mutex g_desc_mu;
+static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> g_desc_bufs;
+
+// A context's stream is about to be destroyed (mgp_destroy): free its descriptor buffer
+// (the stream has been synchronised, so no launch still reads it).
+extern "C" void mgp_desc_release(int dev, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_desc_mu);
+  auto it = g_desc_bufs.find({dev, st});
+  if (it == g_desc_bufs.end()) return;
+  if (it->second.first) (void)hipFree(it->second.first);
+  g_desc_bufs.erase(it);
+}
+
 static hipError_t desc_buffer(hipStream_t st, size_t bytes, void **out) {
   if (desc_mode() == 1) return hipMalloc(out, bytes);
   if (desc_mode() == 2) return hipMallocAsync(out, bytes, st);
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> bufs;
+  std::mutex &mu = g_desc_mu;
+  auto &bufs = g_desc_bufs;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;

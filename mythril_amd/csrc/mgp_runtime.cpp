@@ -27,6 +27,7 @@ hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32
                              hipStream_t st);
 hipError_t mgp_launch_preimages(uint8_t *out, uint64_t first, uint64_t n, uint64_t seed, hipStream_t st);
 hipError_t mgp_launch_valu_probe(uint32_t iters, uint32_t blocks, uint32_t *sink, hipStream_t st);
+void mgp_desc_release(int dev, hipStream_t st);
 }
 
 namespace {
@@ -197,7 +198,10 @@ void mgp_destroy(mgp_ctx *ctx) {
   for (DevBuf *b : {&ctx->words, &ctx->offs, &ctx->cand_aos, &ctx->cand_soa, &ctx->first, &ctx->wit,
                     &ctx->partial, &ctx->kin, &ctx->kout, &ctx->order})
     b->release();
-  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream) {
+    mgp_desc_release(ctx->device, ctx->stream);  // the stream's launch-descriptor buffer
+    (void)hipStreamDestroy(ctx->stream);
+  }
   delete ctx;
 }
 

@@ -184,7 +184,8 @@ int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes,
  * bounded worklist; MGP_DECIDE_PASSES=k re-runs k full passes instead), so
  * later variables see the narrowing the earlier choices cause.  Decision rows
  * 0-7 decide in variable order, rows 8-15 in reverse order, later rows in
- * either.  UF applications get their fresh value slot (p1)
+ * either; the first eight take draw schedules 0, 4, 6, 8, 2, 10, 12, 14 (the
+ * lo/hi schedule and three random-draw schedules first).  UF applications get their fresh value slot (p1)
  * from the application's abstract value (keccak intervals, alignment).
  * Deterministic in seed.  out[s] as mgp_refute.  Replaces nothing in the
  * reference: it feeds the GPU witness search that answers get_model /
@@ -195,6 +196,19 @@ int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets,
                           uint32_t n_cand, uint32_t n_vars, uint64_t seed,
                           uint32_t every, uint32_t n_decide, uint32_t *cands,
                           int8_t *out);
+
+/* mgp_guided_candidates with a decision-row count per state: state s gets
+ * min(rows_per_state[s], n_decide) decision rows, the rest of its guided rows
+ * are plain domain draws (the front end gives expensive states fewer rows so
+ * that more of them fit its time budget).  rows_per_state = NULL is
+ * mgp_guided_candidates. */
+int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t *node_offsets,
+                               uint32_t n_states, const uint32_t *consts,
+                               const uint64_t *const_offsets, uint32_t max_passes,
+                               uint32_t n_cand, uint32_t n_vars, uint64_t seed,
+                               uint32_t every, uint32_t n_decide,
+                               const uint8_t *rows_per_state, uint32_t *cands,
+                               int8_t *out);
 
 /* Candidate assignments for the first witness round (host, OpenMP over states):
  * per state, row 0 is left for the parent witness when has_parent[s], then the

@@ -89,6 +89,8 @@ def _bind(lib):
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
         "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
+        "mgp_guided_candidates_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P,
+                                                      _P]),
         "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32,
                                                _P, _P, _P]),
         "mgp_refute_domains": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
@@ -148,6 +150,7 @@ EXPORTED_SYMBOLS = (
     "mgp_refute",
     "mgp_refute_trace",
     "mgp_guided_candidates",
+    "mgp_guided_candidates_rows",
     "mgp_make_candidates",
     "mgp_refute_domains",
     "mgp_build_states",
@@ -284,7 +287,7 @@ def refute_domains(nodes, node_offsets, consts, const_offsets, var_off, max_pass
 
 def guided_candidates(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,
                       cands: np.ndarray, seed: int = 0x4D595448, every: int = 2, n_decide: int = 16,
-                      max_passes: int = 0) -> np.ndarray:
+                      max_passes: int = 0, rows_per_state: Optional[np.ndarray] = None) -> np.ndarray:
     """Overwrite rows 0, every, 2*every, ... of cands (uint32 [n_states, n_cand, n_vars, 8], in place)
     with draws from each variable's refined abstract value, the first n_decide of them by
     decisions (include/mgp.h); -> int8 status per state as refute()."""
@@ -299,9 +302,18 @@ def guided_candidates(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.nd
             or cands.shape[3] != 8:
         raise ValueError("cands must be a C-contiguous uint32 [n_states, n_cand, n_vars, 8] array")
     out = np.zeros(max(n_states, 1), dtype=np.int8)
-    _check(lib().mgp_guided_candidates(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
-                                       max_passes, cands.shape[1], cands.shape[2], seed & (2 ** 64 - 1), every,
-                                       n_decide, _ptr(cands), _ptr(out)))
+    if rows_per_state is None:
+        _check(lib().mgp_guided_candidates(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts),
+                                           _ptr(const_offsets), max_passes, cands.shape[1], cands.shape[2],
+                                           seed & (2 ** 64 - 1), every, n_decide, _ptr(cands), _ptr(out)))
+    else:
+        rows = np.ascontiguousarray(np.minimum(rows_per_state, 255), dtype=np.uint8)
+        if rows.shape != (n_states,):
+            raise ValueError("rows_per_state must hold one entry per state")
+        _check(lib().mgp_guided_candidates_rows(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts),
+                                                _ptr(const_offsets), max_passes, cands.shape[1], cands.shape[2],
+                                                seed & (2 ** 64 - 1), every, n_decide, _ptr(rows), _ptr(cands),
+                                                _ptr(out)))
     return out[:n_states]
 
 

@@ -1318,10 +1318,11 @@ V sample_av(const AV &a, uint32_t w, uint32_t row, uint64_t r0) {
 }
 }  // namespace
 
-extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
-                                     const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
-                                     uint32_t n_cand, uint32_t n_vars, uint64_t seed, uint32_t every,
-                                     uint32_t n_decide, uint32_t *cands, int8_t *out) {
+extern "C" int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                          const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                          uint32_t n_cand, uint32_t n_vars, uint64_t seed, uint32_t every,
+                                          uint32_t n_decide, const uint8_t *rows_per_state, uint32_t *cands,
+                                          int8_t *out) {
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets || !cands)) || every == 0u)
     return MGP_E_ARG;
   // Per chunk of states: the base analysis, the variable slots and their compared
@@ -1392,6 +1393,9 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
       const uint32_t task_row = (uint32_t)(task % per_state);  // < n_dec_rows: that decision row
       const Prep &P = prep[st - cs];
       if (P.r != 0) continue;
+      // decision rows of this state (the rest of its guided rows are plain domain draws)
+      const uint32_t rs = rows_per_state ? std::min<uint32_t>(rows_per_state[st], n_dec_rows) : n_dec_rows;
+      if (task_row < n_dec_rows && task_row >= rs) continue;
       const State &s = P.s;
       const std::vector<uint32_t> &slot = P.slot, &width = P.width;
       const std::vector<int32_t> &node = P.node;
@@ -1416,8 +1420,8 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
       const uint32_t passes = std::min(max_passes ? max_passes : 16u, decide_passes ? decide_passes : 1u);
       for (uint32_t c = 0, row = 0; c < n_cand; c += every, ++row) {
         uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
-        if (task_row < n_dec_rows ? row != task_row : row < n_dec_rows) continue;
-        if (row < n_decide) {
+        if (task_row < n_dec_rows ? row != task_row : row < rs) continue;
+        if (row < rs) {
           State d = s;
           std::vector<State::UndoRec> undo_log;
           std::vector<uint32_t> work;
@@ -1426,12 +1430,15 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
           d.touched = &work;
           const uint32_t budget = 4u * d.n + 64u;
           // the draw schedule of decision row `row`: the first eight rows decide in node
-          // order (schedules 0, 2, .., 14), later ones add the reverse-order schedules
+          // order (schedules 0, 4, 6, 8, 2, 10, 12, 14: the lo/hi schedule 0 that BECToken's
+          // mapping witness needs and three random-draw schedules first, so a state given
+          // four rows keeps most of its yield), later ones add the reverse-order schedules
           // (odd) and then the rest, so any n_decide = 16 + k covers schedules 0..15+k.
           // Node order is what contract states need (WalletLibrary's loop and mapping
           // queries: 60 against 57 states of the mixed corpus at eight rows, at a third
           // of the host time)
-          const uint32_t drow = row < 8u ? 2u * row : row < 16u ? 2u * (row - 8u) + 1u : row;
+          static const uint8_t kFirst8[8] = {0, 4, 6, 8, 2, 10, 12, 14};
+          const uint32_t drow = row < 8u ? kFirst8[row] : row < 16u ? 2u * (row - 8u) + 1u : row;
           for (size_t kk = 0; kk < slot.size(); ++kk) {
             const size_t k = (drow & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
             const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
@@ -1471,4 +1478,12 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
     }
   }
   return 0;
+}
+
+extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                     const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                     uint32_t n_cand, uint32_t n_vars, uint64_t seed, uint32_t every,
+                                     uint32_t n_decide, uint32_t *cands, int8_t *out) {
+  return mgp_guided_candidates_rows(nodes, node_offsets, n_states, consts, const_offsets, max_passes, n_cand, n_vars,
+                                    seed, every, n_decide, nullptr, cands, out);
 }

@@ -412,7 +412,11 @@ class Prefilter:
     # host decision rows, which re-run the domain analysis per variable: for the open
     # states that fit the round's time budget (_within_decide_budget), cheapest first.
     RETRY_GPU_CAND = 1024
-    RETRY_SCHEDULE = ((256, 8),)  # (candidates per state, decision rows) of the host rounds
+    # (candidates per state, decision rows) of the host rounds: four rows (draw schedules
+    # 0, 4, 6, 8) find the same witnesses as eight on the mixed corpus at half the cost;
+    # states the budget cannot give four get two (DECIDE_MIN_ROWS)
+    RETRY_SCHEDULE = ((256, 4),)
+    DECIDE_MIN_ROWS = 2
     DECIDE_MAX = 4096
 
     def _retry_round(self, states, retry, n_vars, first, witnesses) -> None:
@@ -438,8 +442,8 @@ class Prefilter:
         for rnd, (n_cand, n_decide) in enumerate(self.RETRY_SCHEDULE):
             if not open_ or len(open_) > self.DECIDE_MAX:
                 break
-            open_ = self._within_decide_budget(states, open_, n_decide,
-                                               max(self.decide_budget_ms, self.decide_ms_per_state * len(states)))
+            open_, rows = self._decide_plan(states, open_, n_decide,
+                                            max(self.decide_budget_ms, self.decide_ms_per_state * len(states)))
             if not open_:
                 break
             budget = self.cand_bytes // (len(open_) * n_vars * 32)
@@ -454,10 +458,10 @@ class Prefilter:
                                          SB.alias_off, SB.aliases, SB.const_off, SB.consts, D._FIXED_LIMBS,
                                          np.zeros(len(open_), np.uint8), var_kind=SB.var_kind)
             tg = time.perf_counter()
-            self._N.guided_candidates(*SB.packed(), c2, seed=seed, every=2, n_decide=n_decide)
-            units = float((np.diff(SB.var_off).astype(np.float64) * np.diff(SB.node_off)).sum())
+            self._N.guided_candidates(*SB.packed(), c2, seed=seed, every=2, n_decide=n_decide, rows_per_state=rows)
+            units = float((np.diff(SB.var_off).astype(np.float64) * np.diff(SB.node_off) * rows).sum())
             if units > 0:
-                meas = (time.perf_counter() - tg) * 1e6 * self._decide_threads() / (units * n_decide)
+                meas = (time.perf_counter() - tg) * 1e6 * self._decide_threads() / units
                 self.decide_us_per_unit = min(1.0, max(0.005, 0.5 * self.decide_us_per_unit + 0.5 * meas))
             f2, w2 = self.ctx.eval_batch(sw, sp, c2)
             unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
@@ -480,9 +484,11 @@ class Prefilter:
 
         return max(1, min(16, os.cpu_count() or 1))
 
-    def _within_decide_budget(self, states, open_, n_decide, budget_ms=None):
-        """The open states whose host decision rows fit budget_ms (default decide_budget_ms)
-        of wall time (one task per state and row over the host threads), cheapest first."""
+    def _decide_plan(self, states, open_, n_decide, budget_ms=None):
+        """-> (open states whose host decision rows fit budget_ms of wall time, sorted; their
+        decision-row counts).  Cheapest first (variables x DAG nodes, one task per state and
+        row over the host threads); a state that does not fit with n_decide rows may still
+        fit with DECIDE_MIN_ROWS."""
         budget_ms = self.decide_budget_ms if budget_ms is None else budget_ms
         from .front import Batch
 
@@ -491,15 +497,24 @@ class Prefilter:
         B.close()
         threads = Prefilter._decide_threads()
         us_per_unit = getattr(self, "decide_us_per_unit", self.DECIDE_US_PER_UNIT)
-        keep, cpu_ms = [], 0.0
+        lo = min(n_decide, getattr(self, "DECIDE_MIN_ROWS", n_decide))
+        keep: Dict[int, int] = {}
+        cpu_ms, tasks = 0.0, 0
         for k in np.argsort(units, kind="stable"):
-            c = units[k] * n_decide * us_per_unit * 1e-3
-            tasks = (len(keep) + 1) * n_decide
-            if (cpu_ms + c) / min(threads, tasks) > budget_ms:
-                break
-            keep.append(open_[int(k)])
-            cpu_ms += c
-        return sorted(keep)
+            for r in (n_decide, lo) if lo < n_decide else (n_decide,):
+                c = units[k] * r * us_per_unit * 1e-3
+                if (cpu_ms + c) / min(threads, tasks + r) <= budget_ms:
+                    keep[open_[int(k)]] = r
+                    cpu_ms += c
+                    tasks += r
+                    break
+        order = sorted(keep)
+        return order, np.array([keep[i] for i in order], dtype=np.uint8)
+
+    def _within_decide_budget(self, states, open_, n_decide, budget_ms=None):
+        """The open states that get all n_decide host decision rows within budget_ms."""
+        keep, rows = self._decide_plan(states, open_, n_decide, budget_ms)
+        return [i for i, r in zip(keep, rows) if r == n_decide]
 
 
 _prefilter: Optional[Prefilter] = None

@@ -164,7 +164,8 @@ def test_second_candidate_round(fe, monkeypatch):
 
 def test_host_decisions_keep_to_their_time_budget():
     """The retry round's host decision rows take the open states cheapest first while the
-    estimated wall time fits Prefilter.decide_budget_ms (one task per state and row)."""
+    estimated wall time fits Prefilter.decide_budget_ms (one task per state and row); a
+    state that does not fit with all rows may still get DECIDE_MIN_ROWS."""
     import types
 
     import corpus
@@ -173,11 +174,18 @@ def test_host_decisions_keep_to_their_time_budget():
     kfm = KeccakFunctionManager()
     states = [list(t) for _, t, _ in corpus.wallet_states(0, kfm)[:4]]
     states += [list(corpus.bectoken_states(k, kfm)[1]) for k in range(4)]
-    fake = types.SimpleNamespace(decide_budget_ms=20.0, DECIDE_US_PER_UNIT=SV.Prefilter.DECIDE_US_PER_UNIT)
-    pick = SV.Prefilter._within_decide_budget(fake, states, list(range(8)), 8)
-    assert set(range(4, 8)) <= set(pick)          # the small BECToken states first
-    assert len(pick) < 8
+    fake = types.SimpleNamespace(decide_budget_ms=20.0, DECIDE_US_PER_UNIT=SV.Prefilter.DECIDE_US_PER_UNIT,
+                                 decide_us_per_unit=SV.Prefilter.DECIDE_US_PER_UNIT, DECIDE_MIN_ROWS=2)
+    keep, rows = SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)
+    full = [i for i, r in zip(keep, rows) if r == 8]
+    assert set(range(4, 8)) <= set(full)          # the small BECToken states first, all rows
+    assert len(full) < 8 and all(r in (2, 8) for r in rows)
     fake.decide_budget_ms = 1e9
-    assert SV.Prefilter._within_decide_budget(fake, states, list(range(8)), 8) == list(range(8))
+    keep, rows = SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)
+    assert keep == list(range(8)) and (rows == 8).all()
     fake.decide_budget_ms = 0.0
-    assert SV.Prefilter._within_decide_budget(fake, states, list(range(8)), 8) == []
+    assert SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)[0] == []
+    # at 20 ms a WalletLibrary state that does not fit with eight rows still gets two
+    fake.decide_budget_ms = 20.0
+    keep, rows = SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)
+    assert any(i < 4 and r == 2 for i, r in zip(keep, rows))

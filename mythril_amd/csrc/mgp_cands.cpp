@@ -55,7 +55,7 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
                                    const uint32_t *fixed_pool, uint32_t n_fixed,
                                    const uint8_t *has_parent, const uint32_t *dom, uint32_t *out) {
   if (!var_off || !hint_off || !alias_off || !const_off || !out || (n_states && !has_parent)) return MGP_E_ARG;
-#pragma omp parallel for schedule(dynamic, 4)
+#pragma omp parallel for schedule(dynamic, 1)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t v0 = var_off[s], V = var_off[s + 1] - v0;
     uint32_t *o = out + (uint64_t)s * n_cand * n_vars * 8u;

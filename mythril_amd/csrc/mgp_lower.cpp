@@ -22,6 +22,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <omp.h>
+
 #include <algorithm>
 #include <unordered_map>
 #include <vector>
@@ -593,7 +595,8 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
 
 
 Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *consts, uint64_t n_consts,
-                  uint32_t max_slots, const int *scheds, int n_scheds, std::vector<uint32_t> *uops) {
+                  uint32_t max_slots, const int *scheds, int n_scheds, std::vector<uint32_t> *uops,
+                  bool par_scheds = false) {
   if (n_nodes == 0) return unsupported();
   LowerState S;
   std::vector<Ref> val(n_nodes);
@@ -1134,10 +1137,14 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   // schedule only counts if the gfx950 interpreter can run it (uop translation).
   // Fewer slots wins (occupancy); between spilling programs, fewer instructions (a
   // spill is a memory access either way, an instruction is issue time).
+  // the schedules are independent: in parallel when the caller runs few states
+  std::vector<Lowered> tried(n_scheds);
+#pragma omp parallel for schedule(dynamic, 1) if (par_scheds && n_scheds > 1)
+  for (int k = 0; k < n_scheds; ++k) tried[k] = finish_one(S, root, max_slots, scheds[k]);
   Lowered best;
   bool have = false;
   for (int k = 0; k < n_scheds; ++k) {
-    Lowered b = finish_one(S, root, max_slots, scheds[k]);
+    Lowered &b = tried[k];
     if (b.status != MGP_ST_OK) continue;
     if (have) {
       const bool spill = best.words[2] > MGP_LDS_SLOTS || b.words[2] > MGP_LDS_SLOTS;
@@ -1167,7 +1174,9 @@ static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32
     const char *e = getenv("MGP_LOWER_SCHED");
     return (e && e[0] >= '0' && e[0] <= '3' && e[1] == 0) ? e[0] - '0' : 1;
   }();
-#pragma omp parallel for schedule(dynamic, 8)
+  // few states (LASER's JUMPI forks): states in turn, each state's schedules in parallel
+  const bool few = (int64_t)n_states * 2 < (int64_t)omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) if (!few)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
     const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
@@ -1182,8 +1191,8 @@ static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32
     static const int all3[3] = {0, 1, 2};
     const int one = sched_mode == 0 ? 0 : sched_mode - 1;
     std::vector<uint32_t> uops;
-    Lowered a = sched_mode == 1 ? lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, all3, 3, &uops)
-                                : lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, &one, 1, &uops);
+    Lowered a = sched_mode == 1 ? lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, all3, 3, &uops, few)
+                                : lower_one(nodes + n0, n1 - n0, cp, c1 - c0, max_slots, &one, 1, &uops, few);
     // append the uop program of the gfx950 interpreter; a state it cannot run
     // is made unsupported in both encodings so that both engines agree
     if (a.status != MGP_ST_OK) {

@@ -353,7 +353,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
     pvals.assign((size_t)np * n_vars * 8u, 0u);
     pmask.assign((size_t)np * n_vars, 0u);
     const uint32_t *vw = (const uint32_t *)vwidth.p;
-#pragma omp parallel for schedule(dynamic, 8)
+#pragma omp parallel for schedule(dynamic, 1)
     for (int64_t s = 0; s < (int64_t)n_states; ++s) {
       if (pidx[s] < 0) continue;
       std::unordered_map<uint64_t, uint64_t> at;

@@ -1236,7 +1236,7 @@ extern "C" int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets, u
                           const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
                           int8_t *out) {
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
-#pragma omp parallel for schedule(dynamic, 8)
+#pragma omp parallel for schedule(dynamic, 1)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
     const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
@@ -1259,7 +1259,7 @@ extern "C" int mgp_refute_domains(const mgp_node *nodes, const uint64_t *node_of
                                   uint32_t max_passes, int8_t *out, uint32_t *out_dom) {
   if (!node_offsets || !out || !var_off || !out_dom || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
   memset(out_dom, 0, (size_t)var_off[n_states] * 33u * 4u);
-#pragma omp parallel for schedule(dynamic, 8)
+#pragma omp parallel for schedule(dynamic, 1)
   for (int64_t st = 0; st < (int64_t)n_states; ++st) {
     const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
     const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];

@@ -328,6 +328,28 @@ def test_guided_candidates_decisions_solve_linked_vars():
     assert np.array_equal(again, cands), "deterministic in the seed"
 
 
+def test_guided_candidates_rows_per_state():
+    """mgp_guided_candidates_rows: a state given r decision rows gets exactly the rows a
+    call with n_decide = r writes (decision rows first, plain domain draws after), and
+    every state's rows are independent of the other states' counts."""
+    b = N.synth_generate(0x5EED, 0, 24, 48, 32)
+    nodes, noff, consts, coff = b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"]
+    base = random_cands(np.random.default_rng(9), 24, 32, b["n_vars"])
+    full, four, mixed = base.copy(), base.copy(), base.copy()
+    st8 = N.guided_candidates(nodes, noff, consts, coff, full, seed=3, every=2, n_decide=8)
+    st4 = N.guided_candidates(nodes, noff, consts, coff, four, seed=3, every=2, n_decide=4)
+    rows = np.array([8 if s % 2 else 4 for s in range(24)], np.uint8)
+    stm = N.guided_candidates(nodes, noff, consts, coff, mixed, seed=3, every=2, n_decide=8, rows_per_state=rows)
+    assert np.array_equal(st8, st4) and np.array_equal(st8, stm)
+    for s in range(24):
+        want = full[s] if rows[s] == 8 else four[s]
+        assert np.array_equal(mixed[s], want), s
+    same = base.copy()
+    N.guided_candidates(nodes, noff, consts, coff, same, seed=3, every=2, n_decide=8,
+                        rows_per_state=np.full(24, 8, np.uint8))
+    assert np.array_equal(same, full)
+
+
 def test_guided_candidates_status_and_yield_on_synthetic():
     b = N.synth_generate(0x4D595448, 0, 768, 64, 256)
     nodes, noff, consts, coff = b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"]

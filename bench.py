@@ -372,6 +372,7 @@ def main():
         cs = _contract_states(args.frontend)
         pf.check_states(cs[:64])  # warm-up (kernels loaded, host pools touched)
         SV.unsat_cores().reset()  # cold: no UNSAT core from the warm-up answers the timed run
+        pf._N.program_cache_clear()  # and no lowered program from it either
         SV.SolverStatistics().reset()
         tf = time.perf_counter()
         res = pf.check_states(cs)
@@ -382,14 +383,31 @@ def main():
 
         import corpus
 
-        labels = [c[0] for c in corpus.corpus(len(cs))]
+        items = corpus.corpus(len(cs))
+        labels = [c[0] for c in items]
         by_shape = collections.defaultdict(collections.Counter)
         for lab, k in zip(labels, kinds):
             by_shape[lab.split(":")[0]][k] += 1
+        # answers against the corpus' by-construction expectations (corpus.py): a "sat" on an
+        # expected-unsat state would be a wrong answer, an "unsat" on an expected-sat one too
+        expect = {"expected_unsat": 0, "expected_unsat_refuted": 0, "expected_sat": 0, "expected_sat_witness": 0,
+                  "contradicted": 0}
+        for (_, _, e), k in zip(items, kinds):
+            if e == "unsat":
+                expect["expected_unsat"] += 1
+                expect["expected_unsat_refuted"] += k == SV.unsat
+                expect["contradicted"] += k == SV.sat
+            elif e == "sat":
+                expect["expected_sat"] += 1
+                expect["expected_sat_witness"] += k == SV.sat
+                expect["contradicted"] += k == SV.unsat
+        if expect["contradicted"]:
+            raise RuntimeError(f"front end contradicts the corpus expectations: {expect}")
         frontend = {"states": len(cs), "seconds": dtf, "states_per_s": len(cs) / dtf,
                     "sat": kinds.count(SV.sat), "unsat": kinds.count(SV.unsat),
                     "refuted": st.refuted, "core_hits": st.core_hits,
                     "undecided": kinds.count("undecided"), "candidates": pf.n_cand,
+                    "solver_call_reduction": len(cs) / max(1, kinds.count("undecided")), "expectations": expect,
                     "by_contract": {k: dict(v) for k, v in by_shape.items()},
                     "stages_ms": pf.last_profile, "latency": frontend_latency(pf, SV, cs),
                     "shape": "mixed corpus (corpus.py): suicide.sol kill, BECToken.sol batchTransfer, "

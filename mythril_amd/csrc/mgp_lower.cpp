@@ -1137,6 +1137,18 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   // schedule only counts if the gfx950 interpreter can run it (uop translation).
   // Fewer slots wins (occupancy); between spilling programs, fewer instructions (a
   // spill is a memory access either way, an instruction is issue time).
+  // very long programs (WalletLibrary's 8-30 k instructions) keep input order alone: the
+  // greedy scheduler is quadratic there, and Sethi-Ullman DFS fails on a third of them (Bool
+  // budget) and saves < 0.2 % of the instructions on the rest, for twice the lowering time
+  static const int kInputOrder[1] = {0};
+  if (n_scheds > 1 && S.ins.size() > 1536) {
+    bool has0 = false;
+    for (int k = 0; k < n_scheds; ++k) has0 |= scheds[k] == 0;
+    if (has0) {
+      scheds = kInputOrder;
+      n_scheds = 1;
+    }
+  }
   // the schedules are independent: in parallel when the caller runs few states
   std::vector<Lowered> tried(n_scheds);
 #pragma omp parallel for schedule(dynamic, 1) if (par_scheds && n_scheds > 1)

@@ -328,6 +328,7 @@ def wait_operands():
 
 # uop flag bits (w2 = s18, w3 = s19; see uop_spec)
 B_STORE, B_MASK, B_SEXT, B_INVERT, B_REGST = 22, 23, 24, 25, 29
+B_BCOMB, B_BCOMB_OR = U.F_BCOMB.bit_length() - 1, U.F_BCOMB_OR.bit_length() - 1
 
 
 def load_pool(dst, idx_sreg):
@@ -418,16 +419,30 @@ def bv_epilogue():
 
 
 def cmp_epilogue():
+    """vcc -> Bool slot w3[31:16].  Out of line: INVERT negates it; BCOMB combines it with
+    the Bool slot w3[15:8] (AND, or OR with BCOMB_OR) first: a compare whose result only
+    feeds the next BAND / BOR, folded by the translator (one dispatch instead of two)."""
     li = A.fresh("inv")
-    A(f"s_bitcmp1_b32 s18, {B_INVERT}", f"s_cbranch_scc1 {li}")
+    A(f"s_and_b32 s48, s18, {(1 << B_INVERT) | (1 << B_BCOMB):#x}", f"s_cbranch_scc1 {li}")
     bool_write("vcc")
     tail()
 
-    def inverted():
-        A("s_not_b64 vcc, vcc")
+    def special():
+        lni, lw, lor = A.fresh("noinv"), A.fresh("cwrite"), A.fresh("cor")
+        A(f"s_bitcmp1_b32 s18, {B_INVERT}", f"s_cbranch_scc0 {lni}",
+          "s_not_b64 vcc, vcc")
+        A.label(lni)
+        A(f"s_bitcmp1_b32 s18, {B_BCOMB}", f"s_cbranch_scc0 {lw}",
+          f"s_bfe_u32 s48, s19, {(8 << 16) | U.BCOMB_POS:#x}",
+          "s_mov_b32 m0, s48", "s_nop 0", "s_movrels_b64 s[50:51], s[64:65]",
+          f"s_bitcmp1_b32 s18, {B_BCOMB_OR}", f"s_cbranch_scc1 {lor}",
+          "s_and_b64 vcc, vcc, s[50:51]", f"s_branch {lw}")
+        A.label(lor)
+        A("s_or_b64 vcc, vcc, s[50:51]")
+        A.label(lw)
         bool_write("vcc")
         tail()
-    A.out_of_line(li, inverted)
+    A.out_of_line(li, special)
 
 
 def write_partial_and_end(value_sreg):
@@ -676,6 +691,16 @@ def h_band4():
       "s_movrels_b64 s[52:53], s[64:65]", "s_lshr_b32 s48, s19, 16",
       "s_and_b64 s[50:51], s[50:51], s[54:55]", "s_mov_b32 m0, s48",
       "s_and_b64 s[50:51], s[50:51], s[52:53]", "s_movreld_b64 s[64:65], s[50:51]")
+    tail()
+
+
+@handler("BANDN")
+def h_bandn():
+    # dst = a & ~b (a BNOT whose result only feeds the next BAND, folded by the translator)
+    A("s_and_b32 s48, s17, 0xffff", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s17, 16",
+      "s_movrels_b64 s[50:51], s[64:65]", "s_mov_b32 m0, s49", "s_lshr_b32 s48, s19, 16",
+      "s_movrels_b64 s[52:53], s[64:65]", "s_mov_b32 m0, s48",
+      "s_andn2_b64 s[50:51], s[50:51], s[52:53]", "s_movreld_b64 s[64:65], s[50:51]")
     tail()
 
 

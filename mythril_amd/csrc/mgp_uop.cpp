@@ -235,8 +235,10 @@ inline bool v1_live_after(const uint32_t *ins, uint32_t n, uint32_t from, uint32
 struct BoolPlan {
   std::vector<uint8_t> dead;                  // instruction folded into a neighbour
   std::vector<uint8_t> inv;                   // compare: toggle INVERT
-  std::vector<uint32_t> dst;                  // compare: destination bit override
+  std::vector<uint32_t> dst;                  // compare / BAND: destination bit override
   std::vector<std::vector<uint32_t>> andops;  // BAND: operand bits (2..4)
+  std::vector<uint32_t> comb;                 // compare: 1 + other bit | OR << 16 (folded BAND / BOR)
+  std::vector<uint32_t> andn;                 // BAND: 1 + negated bit (folded BNOT), andops[0] the other
 };
 
 void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
@@ -244,6 +246,8 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
   P.inv.assign(n, 0);
   P.dst.assign(n, 0xFFFFFFFFu);
   P.andops.assign(n, {});
+  P.comb.assign(n, 0);
+  P.andn.assign(n, 0);
   for (uint32_t pc = 0; pc + 1 < n; ++pc) {
     const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS, *J = I + MGP_INS_WORDS;
     const uint32_t op = v1_op(I), d = (I[0] >> 16) & 0xFFu;
@@ -271,6 +275,53 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
     std::vector<uint32_t> ops = P.andops[pc];
     ops.push_back(ja == t ? jb : ja);
     P.andops[pc + 1] = ops;
+    P.dead[pc] = 1;
+  }
+  // the next instruction left after pc
+  auto next_live = [&](uint32_t pc) {
+    uint32_t q = pc + 1;
+    while (q < n && P.dead[q]) ++q;
+    return q;
+  };
+  // a plain two-operand BAND / BOR at q that reads bit t exactly once and is t's last
+  // reader (or redefines it): the other operand, else 0xFFFFFFFF
+  auto sole_reader = [&](uint32_t q, uint32_t t, bool allow_or) -> uint32_t {
+    if (q >= n || P.dead[q]) return 0xFFFFFFFFu;
+    const uint32_t *J = ins + (size_t)q * MGP_INS_WORDS;
+    const uint32_t jop = v1_op(J);
+    if (!(jop == MGP_OP_BAND && P.andops[q].size() == 2) && !(allow_or && jop == MGP_OP_BOR)) return 0xFFFFFFFFu;
+    const uint32_t ja = J[1] & 0xFFFFu, jb = J[1] >> 16;
+    if ((ja == t) == (jb == t)) return 0xFFFFFFFFu;
+    if (t == MGP_BOOL_TRUE || t == MGP_BOOL_FALSE) return 0xFFFFFFFFu;
+    const bool redefines = ((J[0] >> 16) & 0xFFu) == t;
+    if (!redefines && v1_live_after(ins, n, q + 1, t)) return 0xFFFFFFFFu;
+    return ja == t ? jb : ja;
+  };
+  // a compare whose result only feeds the next BAND / BOR: the compare combines it (BCOMB)
+  for (uint32_t pc = 0; pc < n; ++pc) {
+    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
+    const uint32_t op = v1_op(I);
+    if (P.dead[pc] || !(op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF)) continue;
+    const uint32_t t = P.dst[pc] != 0xFFFFFFFFu ? P.dst[pc] : (I[0] >> 16) & 0xFFu;
+    const uint32_t q = next_live(pc);
+    const uint32_t x = sole_reader(q, t, true);
+    if (x == 0xFFFFFFFFu) continue;
+    const uint32_t *J = ins + (size_t)q * MGP_INS_WORDS;
+    P.comb[pc] = (1u + x) | (v1_op(J) == MGP_OP_BOR ? 1u << 16 : 0u);
+    P.dst[pc] = (J[0] >> 16) & 0xFFu;
+    P.dead[q] = 1;
+  }
+  // a BNOT whose result only feeds the next BAND: BANDN
+  for (uint32_t pc = 0; pc < n; ++pc) {
+    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
+    if (P.dead[pc] || v1_op(I) != MGP_OP_BNOT) continue;
+    const uint32_t t = (I[0] >> 16) & 0xFFu, x = I[1] & 0xFFFFu;
+    if (x == t) continue;
+    const uint32_t q = next_live(pc);
+    const uint32_t y = sole_reader(q, t, false);
+    if (y == 0xFFFFFFFFu) continue;
+    P.andn[q] = 1u + x;
+    P.andops[q] = {y, x};
     P.dead[pc] = 1;
   }
 }
@@ -318,6 +369,11 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         emit(w0_of(MGP_U_RET, MGP_U_RET), T.boolslot(oa), 0, 0);
         break;
       }
+      if (op == MGP_OP_BAND && BP.andn[pc]) {  // a & ~b
+        emit(w0_of(MGP_U_BANDN, MGP_U_BANDN), T.boolslot(BP.andops[pc][0]) | (T.boolslot(BP.andops[pc][1]) << 16),
+             0u, T.boolslot(dst) << 16);
+        continue;
+      }
       if (op == MGP_OP_BAND && BP.andops[pc].size() > 2) {
         const std::vector<uint32_t> &q = BP.andops[pc];
         const uint32_t c = T.boolslot(q[2]), d = q.size() > 3 ? T.boolslot(q[3]) : T.boolslot(MGP_BOOL_TRUE);
@@ -359,6 +415,10 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         }
         if (BP.inv[pc]) inv = !inv;  // a folded BNOT of this compare's result
         uint32_t flags = inv ? MGP_UF_INVERT : 0u, w2 = 0, w3 = T.boolslot(dst) << 16;
+        if (BP.comb[pc]) {  // a folded BAND / BOR of this compare's result
+          flags |= MGP_UF_BCOMB | ((BP.comb[pc] >> 16) ? MGP_UF_BCOMB_OR : 0u);
+          w3 |= T.boolslot((BP.comb[pc] & 0xFFFFu) - 1u) << MGP_U_BCOMB_POS;
+        }
         if (narrow && (base == MGP_U_SLT_RA || base == MGP_U_SGT_RA)) {
           flags |= MGP_UF_SEXT;
           w3 |= T.sign_off(width);

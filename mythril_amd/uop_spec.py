@@ -41,8 +41,12 @@ uop words:
      [29] REGST   the STORE goes to register-bank position w2[15:0]/8 (v[64+8p]),
                   not to LDS: the translator maps a state's highest BV slots onto
                   bank positions no variable of that state uses
+     [30] BCOMB   compares: the (possibly inverted) result is combined with Bool slot
+                  w3[15:8]/2 before it is written: AND, or OR with [31] BCOMB_OR
+  BANDN: dst = a & ~b (a = w1[15:0], b = w1[31:16])
   VST: w2 [15:0] candidate variable row the lane's vA is stored to (a spill slot)
   w3 [5:0]  sign-constant pool index, [12:8] uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT),
+     [15:8] compares with BCOMB: the other Bool operand * 2,
      [31:16] Bool destination * 2 (compares, Bool ops) or ITE condition * 2
 
 Registers of the interpreter: vA (accumulator / operand A), vB (operand B),
@@ -61,7 +65,7 @@ B_KINDS = ("none",) + KINDS
 FETCH = [f"F_{ka}_{kb}_A" for ka in KINDS for kb in B_KINDS] + \
         [f"F_{ka}_{kb}_C" for ka in KINDS[1:] for kb in B_KINDS]
 
-BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ", "BAND4"]
+BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ", "BAND4", "BANDN"]
 # vA -> the lane's candidate row w2[15:0] (a spilled BV slot; read back as a VAR operand)
 MEM_OPS = ["VST"]
 BV_BIN = ["ADD", "SUB", "MUL", "AND", "OR", "XOR", "SHL", "LSHR", "ASHR", "DIV"]
@@ -100,6 +104,8 @@ DIV_VARIANTS = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
 
 F_STORE, F_MASK, F_SEXT, F_INVERT = 1 << 22, 1 << 23, 1 << 24, 1 << 25   # in w2
 F_REGST = 1 << 29                                                         # in w2
+F_BCOMB, F_BCOMB_OR = 1 << 30, 1 << 31                                    # in w2
+BCOMB_POS = 8       # in w3
 SHIFT_B_POS = 8     # in w3
 DIVOP_POS = 26      # in w2
 
@@ -123,7 +129,8 @@ def c_header() -> str:
     lines += [
         f"#define MGP_UF_STORE {F_STORE}u", f"#define MGP_UF_MASK {F_MASK}u",
         f"#define MGP_UF_SEXT {F_SEXT}u", f"#define MGP_UF_INVERT {F_INVERT}u",
-        f"#define MGP_UF_REGST {F_REGST}u",
+        f"#define MGP_UF_REGST {F_REGST}u", f"#define MGP_UF_BCOMB {F_BCOMB}u",
+        f"#define MGP_UF_BCOMB_OR {F_BCOMB_OR}u", f"#define MGP_U_BCOMB_POS {BCOMB_POS}",
         f"#define MGP_U_SHIFT_B_POS {SHIFT_B_POS}", f"#define MGP_U_DIVOP_POS {DIVOP_POS}",
         f"#define MGP_U_BOOL_SLOTS {BOOL_SLOTS}", f"#define MGP_U_MAX_LDS_SLOTS {MAX_LDS_SLOTS}",
         f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",

@@ -163,7 +163,7 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
                 bools[w3 >> 17] = a and b and c and bools[(w2 >> 16) >> 1]
                 continue
             r = {"BAND": a and b, "BOR": a or b, "BXOR": a != b, "BNOT": not a,
-                 "BITE": b if a else c, "BEQ": a == b}[op]
+                 "BITE": b if a else c, "BEQ": a == b, "BANDN": a and not b}[op]
             bools[w3 >> 17] = r
             continue
         if op.endswith("_RA") or op.endswith("_RC"):
@@ -193,7 +193,11 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
                 raw = (p >> 256) != 0 or (p & M256) > KM
             else:
                 raise ValueError(op)
-            bools[w3 >> 17] = bool(raw) != bool(w2 & U.F_INVERT)
+            r = bool(raw) != bool(w2 & U.F_INVERT)
+            if w2 & U.F_BCOMB:  # a folded BAND / BOR with Bool slot w3[15:8]/2
+                o = bools[((w3 >> U.BCOMB_POS) & 0xFF) >> 1]
+                r = (r or o) if w2 & U.F_BCOMB_OR else (r and o)
+            bools[w3 >> 17] = r
             continue
         # BV-producing
         if op == "ITE":

@@ -412,6 +412,20 @@ def main():
                     "stages_ms": pf.last_profile, "latency": frontend_latency(pf, SV, cs),
                     "shape": "mixed corpus (corpus.py): suicide.sol kill, BECToken.sol batchTransfer, "
                              "WalletLibrary.sol initWallet -> kill"}
+        # the same batch, cold, with the first GPU round and the host pre-check only (no
+        # retry round, no host decision rows): the throughput end of the policy
+        SV.unsat_cores().reset()
+        pf._N.program_cache_clear()
+        keep_retry, pf.retry_cand = pf.retry_cand, pf.n_cand
+        tf = time.perf_counter()
+        res1 = pf.check_states(cs)
+        dt1 = time.perf_counter() - tf
+        pf.retry_cand = keep_retry
+        k1 = [r[0] for r in res1]
+        frontend["first_round_only"] = {"seconds": dt1, "states_per_s": len(cs) / dt1, "sat": k1.count(SV.sat),
+                                        "unsat": k1.count(SV.unsat), "undecided": k1.count("undecided"),
+                                        "solver_call_reduction": len(cs) / max(1, k1.count("undecided")),
+                                        "stages_ms": pf.last_profile}
         pf.ctx.close()
         log(f"frontend: {frontend}")
 

@@ -417,6 +417,57 @@ def test_division_single_digit_waves(mgp_ctx, w):
                     f"a={a:#x} b={b:#x} expected {e:#x}")
 
 
+def _bool_fold_states(rng, n):
+    """DAGs whose compares feed the next BAND / BOR and whose BNOTs feed the next BAND
+    (the translator's BCOMB / BANDN folds), inverted compares (UGE / ULE / SGE) among
+    them, over three 8-bit variables so random candidates hit both outcomes."""
+    w = 8
+    cmps = [S.EQ, S.ULT, S.UGE, S.ULE, S.SLT, S.SGE, S.UGT]
+    out = []
+    for _ in range(n):
+        nl = [[S.VAR, w, -1, -1, -1, k, 0] for k in range(3)]
+        cl = [int(x) for x in rng.integers(0, 256, size=4)]
+        nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(4)]
+        bools = []
+        for _ in range(int(rng.integers(3, 9))):
+            a, b = int(rng.integers(0, 7)), int(rng.integers(0, 7))
+            nl.append([cmps[int(rng.integers(len(cmps)))], 1, a, b, -1, 0, 0])
+            c = len(nl) - 1
+            if bools and rng.random() < 0.7:
+                if rng.random() < 0.3:
+                    nl.append([S.BNOT, 1, bools[-1], -1, -1, 0, 0])
+                    nl.append([S.BAND, 1, c, len(nl) - 1, -1, 0, 0])
+                else:
+                    nl.append([S.BAND if rng.random() < 0.6 else S.BOR, 1, c, bools[-1], -1, 0, 0])
+                bools.append(len(nl) - 1)
+            else:
+                bools.append(c)
+        root = bools[-1]
+        for b in bools[:-1][-2:]:
+            nl.append([S.BOR, 1, root, b, -1, 0, 0])
+            root = len(nl) - 1
+        out.append((nl, cl))
+    return out
+
+
+def test_bool_folds_vs_oracle(mgp_ctx):
+    """Compare -> BAND/BOR (BCOMB) and BNOT -> BAND (BANDN) folds of the gfx950 uop
+    translation against the C oracle on every candidate (both engines)."""
+    rng = np.random.default_rng(77)
+    states = _bool_fold_states(rng, 600)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = random_cands(rng, len(states), 128, 3, interesting_frac=0.0)
+    cands[:, :, :, 1:] = 0
+    cands[:, :, :, 0] &= 0xFF
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    mism = np.nonzero(first != ref)[0]
+    assert mism.size == 0, f"{mism.size} states differ, e.g. {mism[:5]} gpu={first[mism[:5]]} ref={ref[mism[:5]]}"
+    assert 0 < (first >= 0).sum() < len(states)
+
+
 def test_back_to_back_batches_same_context(mgp_ctx):
     """Consecutive batches of the same size on one context reuse the same device buffers
     (and launch-descriptor addresses) with different programs: every batch must see its

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from mythril_amd import _native as N
+from mythril_amd import uop_spec as U
 from oracle import bvsem as S
 from oracle import bytecode_ref as BR
 from oracle import uop_ref as UR
@@ -535,3 +536,30 @@ def test_uf_symbolic_base_offsets_fold():
     # every select has base B except f(y): only f(y) is tested against the others at run time
     n_eq = sum(1 for k in range(int(words[0])) if int(words[4 + 4 * k]) & 0xFF == S.EQ)
     assert n_eq <= 2 * len(apps) + 2, n_eq
+
+
+def test_bool_folds_uop_reference_matches_oracle():
+    """The translator's compare -> BAND/BOR (BCOMB) and BNOT -> BAND (BANDN) folds, run
+    through the uop reference interpreter, agree with the C oracle (CPU side of
+    tests/test_gpu_parity.py::test_bool_folds_vs_oracle)."""
+    from oracle import coracle
+
+    from .test_gpu_parity import _bool_fold_states
+
+    rng = np.random.default_rng(78)
+    states = _bool_fold_states(rng, 200)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    n_cand = 12
+    vals = rng.integers(0, 256, size=(len(states), n_cand, 3))
+    cands = np.zeros((len(states), n_cand, 3, 8), np.uint32)
+    cands[..., 0] = vals
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    folded = 0
+    for s in range(len(states)):
+        rows = [[int(x) for x in vals[s, k]] for k in range(n_cand)]
+        assert UR.first_sat_uops(words, int(po[s]), rows) == ref[s], s
+        u0 = UR.uop_offset(words, int(po[s]))
+        folded += sum(bool(int(words[u0 + 6 + 4 * k]) & U.F_BCOMB) for k in range(int(words[u0])))
+    assert folded > 100

@@ -376,7 +376,7 @@ class Prefilter:
         witnesses: Dict[int, object] = {}
         retry = [i for i in range(len(states)) if first[i] == -1 and proven[i] != 1]
         if retry and self.retry_cand > self.n_cand:
-            self._retry_round(states, retry, n_vars, first, witnesses)
+            self._retry_round(states, retry, n_vars, first, witnesses, prof)
         prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["retry_states"] = len(retry)
         tr = time.perf_counter()
@@ -419,10 +419,12 @@ class Prefilter:
     DECIDE_MIN_ROWS = 2
     DECIDE_MAX = 4096
 
-    def _retry_round(self, states, retry, n_vars, first, witnesses) -> None:
+    def _retry_round(self, states, retry, n_vars, first, witnesses, prof=None) -> None:
         from . import dag as D
         from .front import FE_SAT_UNSAFE, Batch
 
+        prof = {} if prof is None else prof
+        t_gpu = time.perf_counter()
         open_ = list(retry)
         budget = self.cand_bytes // (len(open_) * n_vars * 32)
         n2 = min(self.RETRY_GPU_CAND, self.retry_cand, budget) // 64 * 64
@@ -439,6 +441,10 @@ class Prefilter:
                     left.append(i)
             SB.close()
             open_ = left
+        prof["retry_gpu_ms"] = 1e3 * (time.perf_counter() - t_gpu)   # device retry round
+        prof["retry_gpu_sat"] = len(retry) - len(open_)
+        prof["decide_states"] = 0
+        t_dec = time.perf_counter()
         for rnd, (n_cand, n_decide) in enumerate(self.RETRY_SCHEDULE):
             if not open_ or len(open_) > self.DECIDE_MAX:
                 break
@@ -458,6 +464,7 @@ class Prefilter:
                                          SB.alias_off, SB.aliases, SB.const_off, SB.consts, D._FIXED_LIMBS,
                                          np.zeros(len(open_), np.uint8), var_kind=SB.var_kind)
             tg = time.perf_counter()
+            prof["decide_states"] += len(open_)
             self._N.guided_candidates(*SB.packed(), c2, seed=seed, every=2, n_decide=n_decide, rows_per_state=rows)
             units = float((np.diff(SB.var_off).astype(np.float64) * np.diff(SB.node_off) * rows).sum())
             if units > 0:
@@ -474,6 +481,7 @@ class Prefilter:
                     left.append(i)
             SB.close()
             open_ = left
+        prof["decide_ms"] = 1e3 * (time.perf_counter() - t_dec)      # host decision rows + their GPU round
         SolverStatistics().gpu_retry += len(retry)
 
     DECIDE_US_PER_UNIT = 0.06  # host CPU cost of one decision row, per (variable x DAG node)

@@ -27,6 +27,7 @@ answer is `unknown`, which each caller maps exactly as the reference does.
 from __future__ import annotations
 
 import threading
+import os
 import time
 from functools import lru_cache
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple, Union
@@ -302,6 +303,9 @@ class Prefilter:
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
         # one per call keeps the deletion trials off the latency of small calls
         self.core_batch = 32
+        # candidates per state of the device retry round before host decisions (0 = none;
+        # MGP_RETRY_GPU_CAND overrides, for A/B runs)
+        self.retry_gpu_cand = int(os.environ.get("MGP_RETRY_GPU_CAND", self.RETRY_GPU_CAND))
         self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
@@ -427,7 +431,7 @@ class Prefilter:
         t_gpu = time.perf_counter()
         open_ = list(retry)
         budget = self.cand_bytes // (len(open_) * n_vars * 32)
-        n2 = min(self.RETRY_GPU_CAND, self.retry_cand, budget) // 64 * 64
+        n2 = min(self.retry_gpu_cand, self.retry_cand, budget) // 64 * 64
         if n2 > self.n_cand:
             SB = Batch([states[i] for i in open_])
             f2, w2, _, _ = SB.check(self.ctx, n2, self.seed + 0x9E3779B9 + self._calls)

@@ -304,8 +304,12 @@ class Prefilter:
         # one per call keeps the deletion trials off the latency of small calls
         self.core_batch = 32
         # candidates per state of the device retry round before host decisions (0 = none;
-        # MGP_RETRY_GPU_CAND overrides, for A/B runs)
+        # MGP_RETRY_GPU_CAND overrides, for A/B runs), run only for at least
+        # retry_gpu_min_states open states: on the mixed corpus it finds 7 witnesses among
+        # 263 open states for 80 ms, and a small call's decisions fit their budget anyway
+        # (2-state call 5.8 -> 4.1 ms without it, bench_r2k3)
         self.retry_gpu_cand = int(os.environ.get("MGP_RETRY_GPU_CAND", self.RETRY_GPU_CAND))
+        self.retry_gpu_min_states = 32
         self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
@@ -432,7 +436,7 @@ class Prefilter:
         open_ = list(retry)
         budget = self.cand_bytes // (len(open_) * n_vars * 32)
         n2 = min(self.retry_gpu_cand, self.retry_cand, budget) // 64 * 64
-        if n2 > self.n_cand:
+        if n2 > self.n_cand and len(open_) >= self.retry_gpu_min_states:
             SB = Batch([states[i] for i in open_])
             f2, w2, _, _ = SB.check(self.ctx, n2, self.seed + 0x9E3779B9 + self._calls)
             unsafe = (SB.flags & FE_SAT_UNSAFE) != 0

@@ -155,10 +155,11 @@ def test_second_candidate_round(fe, monkeypatch):
     assert SV.batch_is_possible(items) == [True, False]
     st = SV.SolverStatistics()
     assert st.gpu_retry == 1 and st.gpu_sat == 1 and st.refuted == 1 and fe.calls == 0
-    # the first round and the larger device round (check_batch: no witness from the stub),
-    # then the host decision round (eval_batch), which the stub satisfies
+    # the first round (check_batch: no witness from the stub), no device retry round for
+    # one open state (Prefilter.retry_gpu_min_states), then the host decision round
+    # (eval_batch), which the stub satisfies
     assert SV.Prefilter.RETRY_GPU_CAND == 1024 and [n for n, _ in SV.Prefilter.RETRY_SCHEDULE] == [256]
-    assert SV.prefilter().ctx.batches == 3
+    assert SV.prefilter().retry_gpu_min_states > 1 and SV.prefilter().ctx.batches == 2
     assert set(items[0].witness) == {"rx", "ry"}
 
 

@@ -809,6 +809,17 @@ def make_xs(name):
     return body
 
 
+def make_xc(name):
+    """XC_<op>: the pool-constant fetch of F_acc_const_A at the top of the op handler itself
+    (scalar load issued before the next uop's readlane, so that the readlane overlaps it)."""
+    def body():
+        const_issue("B")
+        prefetch_next()
+        const_finish(VB, "B")
+        HBODY[name[3:]]()
+    return body
+
+
 def mul_low(xa, yb, out):
     """out[0..7] = low 256 bits of X*Y (Comba columns, v[4:5] + v6 accumulator)."""
     A("v_mov_b32 v6, 0")
@@ -1352,6 +1363,8 @@ for _op in U.EPI_OPS:
     HBODY[_op] = make_epi_variant(_EPI_BASE[_op], "")
 for _x in U.XS_OPS:
     HBODY[_x] = make_xs(_x)
+for _x in U.XC_OPS:
+    HBODY[_x] = make_xc(_x)
 
 
 # ---------------------------------------------------------------- kernel
@@ -1582,7 +1595,7 @@ def generate() -> str:
     pool = "" if CONST_SMEM else POOL_LOAD
     A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
                    .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n").replace("{POOL_LOAD}", pool))
-    no_prefetch = set(U.FETCH) | set(U.XS_OPS) | {"INVALID", "RET", "PAGE"}
+    no_prefetch = set(U.FETCH) | set(U.XS_OPS) | set(U.XC_OPS) | {"INVALID", "RET", "PAGE"}
     wait = "  s_waitcnt vmcnt(0) lgkmcnt(0)"
     for name in U.HANDLERS:
         # two entries per handler: mgp_h_<name> (reached from a fetch handler, whose

@@ -201,6 +201,13 @@ inline int xs_handler(uint32_t op) {
   return -1;
 }
 
+// fused "vA op= pool[B]" handler of an op (uop_spec.XC_OPS), or -1
+inline int xc_handler(uint32_t op) {
+  for (uint32_t i = 0; i < sizeof(kXcBase) / sizeof(kXcBase[0]); ++i)
+    if (kXcBase[i] == op) return (int)(MGP_U_XC_FIRST + i);
+  return -1;
+}
+
 // ---- Bool peepholes on the v1 instruction list (asm engine only; the v1 program is untouched)
 //   * a compare immediately followed by a BNOT of its result: the compare is emitted with
 //     its INVERT flag toggled and the BNOT's destination (one dispatch instead of two);
@@ -433,6 +440,9 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       if (ra && b.kind == KSLOT) {
         const int xs = xs_handler(opid);
         if (xs >= 0) opid = first = (uint32_t)xs;
+      } else if (ra && b.kind == KCONST) {
+        const int xc = xc_handler(opid);
+        if (xc >= 0) opid = first = (uint32_t)xc;
       } else if (ra && b.kind == KRVAR && !(flags & (MGP_UF_SEXT | MGP_UF_MASK))) {
         const int xr = xr_handler(opid);  // EQ / ULT / UGT against a register-bank operand
         if (xr >= 0) opid = first = (uint32_t)xr;
@@ -550,6 +560,9 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       } else if (a.kind == KACC && b.kind == KSLOT) {
         const int xs = xs_handler(opid);
         if (xs >= 0) opid = first = (uint32_t)xs;
+      } else if (a.kind == KACC && b.kind == KCONST) {
+        const int xc = xc_handler(opid);
+        if (xc >= 0) opid = first = (uint32_t)xc;
       }
       emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
       if (vst_row >= 0) emit(w0_of(MGP_U_VST, MGP_U_VST), 0u, (uint32_t)vst_row, 0u);

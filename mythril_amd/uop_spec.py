@@ -93,7 +93,13 @@ XS_BASE = [f"{c}_RA" for c in ("EQ", "ULT", "UGT", "SLT", "SGT")] + ["MUL"] + \
           [f"{o}{v}" for o in ("ADD", "SUB", "AND", "OR", "XOR", "ITE") for v in ("", "_S", "_R")]
 XS_OPS = [f"XS_{o}" for o in XS_BASE]
 
-OPS = BOOL_OPS + MEM_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + XS_OPS
+# fused handlers "vA = vA op pool[B]" (F_acc_const_A + op in one handler: the scalar load
+# of the constant is issued at the top, the next uop's readlane overlaps it)
+XC_BASE = list(XS_BASE)
+XC_OPS = [f"XC_{o}" for o in XC_BASE]
+
+OPS = BOOL_OPS + MEM_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + \
+    XS_OPS + XC_OPS
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
 # id past the table ends the program instead of running off into memory
 HANDLERS = ["INVALID"] + FETCH + OPS
@@ -143,4 +149,7 @@ def c_header() -> str:
     lines.append(f"#define MGP_U_XS_FIRST {ID[XS_OPS[0]]}")
     lines.append("static const unsigned short kXsBase[%d] = {%s};" % (len(XS_BASE), ", ".join(
         f"MGP_U_{o}" for o in XS_BASE)))
+    lines.append(f"#define MGP_U_XC_FIRST {ID[XC_OPS[0]]}")
+    lines.append("static const unsigned short kXcBase[%d] = {%s};" % (len(XC_BASE), ", ".join(
+        f"MGP_U_{o}" for o in XC_BASE)))
     return "\n".join(lines) + "\n"

@@ -134,6 +134,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         elif first.startswith("XS_"):
             vB = lds[pb]                # fused: vA op lds[B]
             first = op = first[3:]
+        elif first.startswith("XC_"):
+            vB = load("const", pb)      # fused: vA op pool[B]
+            first = op = first[3:]
         if first.startswith("F_"):
             _, ka, kb, tgt = first.split("_")
             if kb != "none":

@@ -40,7 +40,17 @@ namespace {
 
 using V = U256;
 
-inline V M(uint32_t w) { return bv_mask(bv_ones(), w); }
+// 2^w - 1 for w = 0..256, from a table (the transfer functions build masks constantly)
+struct MaskTable {
+  V m[257];
+  MaskTable() {
+    for (uint32_t w = 0; w <= 256; ++w) m[w] = bv_mask(bv_ones(), w);
+  }
+};
+inline const V &M(uint32_t w) {
+  static const MaskTable t;
+  return t.m[w < 256u ? w : 256u];
+}
 inline bool Z(const V &a) { return bv_is_zero(a); }
 inline bool EQV(const V &a, const V &b) { return bv_eq(a, b); }
 inline bool LT(const V &a, const V &b) { return bv_ult(a, b); }

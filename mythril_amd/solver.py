@@ -197,14 +197,41 @@ class UnsatCores:
         self.sets: List[frozenset] = []
         self.index: Dict[Term, List[int]] = {}  # every stored set under ONE of its members
         self.pending: List[list] = []  # refuted lists not yet shrunk (Prefilter.core_batch)
+        self.gen = getattr(self, "gen", 0) + 1  # a background shrink of an older generation is dropped
+        self._worker = getattr(self, "_worker", None)
 
-    def flush(self, N) -> None:
+    def flush(self, N, background: bool = False) -> None:
         """Shrink the pending refuted constraint lists to cores (one batched shrink_many)
-        and store them."""
-        if self.pending:
-            pending, self.pending = self.pending, []
-            for core in UnsatCores.shrink_many(N, pending):
-                self.add(core)
+        and store them; background=True runs it on a worker thread (the native calls
+        release the GIL) unless one is still running, which then keeps them pending."""
+        if not self.pending:
+            return
+        if background:
+            if self._worker is not None and self._worker.is_alive():
+                return
+            import threading
+
+            pending, self.pending, gen = self.pending, [], self.gen
+
+            def work():
+                cores = UnsatCores.shrink_many(N, pending)
+                if self.gen == gen:
+                    for core in cores:
+                        self.add(core)
+
+            self._worker = threading.Thread(target=work, name="mgp-unsat-cores", daemon=True)
+            self._worker.start()
+            return
+        self.join()
+        pending, self.pending = self.pending, []
+        for core in UnsatCores.shrink_many(N, pending):
+            self.add(core)
+
+    def join(self) -> None:
+        """Wait for a background shrink."""
+        if self._worker is not None:
+            self._worker.join()
+            self._worker = None
 
     def covered(self, terms: Iterable[Term]) -> bool:
         s = set(terms)
@@ -303,6 +330,7 @@ class Prefilter:
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
         # one per call keeps the deletion trials off the latency of small calls
         self.core_batch = 32
+        self.core_async = True  # shrink on a worker thread, off the caller's latency
         # candidates per state of the device retry round before host decisions (0 = none;
         # MGP_RETRY_GPU_CAND overrides, for A/B runs), run only for at least
         # retry_gpu_min_states open states: on the mixed corpus it finds 7 witnesses among
@@ -406,13 +434,14 @@ class Prefilter:
         if refuted:
             _cores.pending.extend(list(states[i]) for i in refuted)
             if len(_cores.pending) >= self.core_batch:
-                self.flush_cores()
+                _cores.flush(self._N, background=self.core_async)
         prof["cores_ms"] = 1e3 * (time.perf_counter() - tr)
         self.last_profile = prof
         return out
 
     def flush_cores(self) -> None:
-        """Shrink the pending refuted constraint lists to cores and store them."""
+        """Shrink the pending refuted constraint lists to cores and store them (waits for
+        a background shrink first)."""
         _cores.flush(self._N)
 
     # witness rounds for the states the first round and the pre-check leave open: a larger

@@ -330,7 +330,10 @@ class Prefilter:
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
         # one per call keeps the deletion trials off the latency of small calls
         self.core_batch = 32
-        self.core_async = True  # shrink on a worker thread, off the caller's latency
+        # shrink on a worker thread (off the caller's latency) only when the caller leaves
+        # the host idle between calls: back to back, its OpenMP team competes with the next
+        # call's (the bench's first-round pass fell from 3 850 to 2 680 states/s with it on)
+        self.core_async = False
         # candidates per state of the device retry round before host decisions (0 = none;
         # MGP_RETRY_GPU_CAND overrides, for A/B runs), run only for at least
         # retry_gpu_min_states open states: on the mixed corpus it finds 7 witnesses among

@@ -599,6 +599,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
                   bool par_scheds = false) {
   if (n_nodes == 0) return unsupported();
   LowerState S;
+  S.ins.reserve((size_t)n_nodes * 4u + 64u);  // UF chains and wide pieces expand nodes; fewer regrowths
   std::vector<Ref> val(n_nodes);
   std::vector<uint16_t> wid(n_nodes);
   std::vector<uint8_t> isb(n_nodes);

@@ -982,6 +982,27 @@ struct State {
         const AV A = av[x.a], B = av[x.b];
         return meet(x.a, av_xor(R, B, w)) && meet(x.b, av_xor(R, A, w));
       }
+      case MGP_OP_MUL: {
+        // a * b = R (mod 2^w) with b exact and odd: b is invertible mod 2^k, so the k known
+        // low bits of R fix the k low bits of a = R * b^-1 (x * 5 == 1 pins x)
+        for (int k = 0; k < 2; ++k) {
+          const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
+          const AV B = av[q];
+          if (!is_exact(B) || !(B.lo.w[0] & 1u)) continue;
+          uint32_t kn = ctz_ones(OR(R.z, R.o));
+          if (kn > w) kn = w;
+          if (kn == 0) continue;
+          V inv = B.lo;  // Newton: b * b = 1 (mod 8), each step doubles the correct bits
+          for (int it = 0; it < 7; ++it) inv = bv_mul(inv, SUBV(bv_small(2u), bv_mul(B.lo, inv)));
+          const V lowm = M(kn);
+          const V al = AND(bv_mul(AND(R.o, lowm), inv), lowm);
+          AV t = top(w);
+          t.z = OR(t.z, AND(NOT(al), lowm));
+          t.o = al;
+          if (!meet(p, t)) return false;
+        }
+        return true;
+      }
       case MGP_OP_NOT: return meet(x.a, av_not(R, w));
       case MGP_OP_NEG: return meet(x.a, av_sub(exact(bv_zero(), w), R, w));
       case MGP_OP_UREM: {

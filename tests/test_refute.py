@@ -491,3 +491,17 @@ def test_uf_congruence_exhaustive_soundness():
         nodes, noff, consts, coff = pack_states([(nl, cl)])
         assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
     assert refuted > 10
+
+
+def test_mul_by_odd_constant_narrows_backward():
+    """x * c == k with c odd pins x = k * c^-1 (mod 2^w) on the known low bits of k: with
+    x <u 100 that is refuted when c^-1 * k is huge and kept when it is small."""
+    C5 = [S.CONST, 256, -1, -1, -1, 0, 0]
+    base = [X0, C5, [S.MUL, 256, 0, 1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0], [S.EQ, 1, 2, 3, -1, 0, 0],
+            [S.CONST, 256, -1, -1, -1, 2, 0], [S.ULT, 1, 0, 5, -1, 0, 0], [S.BAND, 1, 4, 6, -1, 0, 0]]
+    out = _refute([(base, [5, 1, 100]), (base, [5, 10, 100]), (base, [6, 1, 100])])
+    # 5x = 1: x = 5^-1 mod 2^256 (huge); 5x = 10: x = 2; 6x = 1: even c, 6x is even (no rule
+    # needed: the known low bit already contradicts, or the state stays open) -- never
+    # refuted when a model exists
+    assert out[0] == 1 and out[1] == 0
+    assert S.eval_root(base, [5, 10, 100], [2])

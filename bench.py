@@ -416,7 +416,7 @@ def main():
         # retry round, no host decision rows): the throughput end of the policy
         SV.unsat_cores().reset()
         pf._N.program_cache_clear()
-        keep_retry, pf.retry_cand = pf.retry_cand, pf.n_cand
+        keep_retry, pf.retry_cand = pf.retry_cand, 0
         tf = time.perf_counter()
         res1 = pf.check_states(cs)
         dt1 = time.perf_counter() - tf

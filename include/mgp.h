@@ -210,6 +210,20 @@ int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t *node_offse
                                const uint8_t *rows_per_state, uint32_t *cands,
                                int8_t *out);
 
+/* Decision rows only (host, OpenMP over (state, row) tasks): the rows the first n_decide
+ * rows of mgp_guided_candidates_rows would write, as explicit rows for mgp_check_batch:
+ * out_rows [n_states][n_decide][n_vars][8], out_mask [n_states][n_decide][n_vars] (1 =
+ * the row sets that slot; a row of a refuted or unanalysed state sets none).  State s
+ * gets min(rows_per_state[s], n_decide) rows (NULL = n_decide).  Draws are keyed by
+ * (seed, state_keys[s] or s, row, slot); each decision propagates within
+ * 4 x nodes + 64 transfer-function evaluations, so the rows depend on the state's
+ * content and the seed only -- not on the thread count, the batch or the host's speed.
+ * out[s] as mgp_refute. */
+int mgp_decision_rows(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                      const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                      uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
+                      const uint8_t *rows_per_state, uint32_t *out_rows, uint8_t *out_mask, int8_t *out);
+
 /* Candidate assignments for the first witness round (host, OpenMP over states):
  * per state, row 0 is left for the parent witness when has_parent[s], then the
  * first hint of every variable, that row with the x == y aliases applied, then
@@ -220,14 +234,17 @@ int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t *node_offse
  * variable v are rows hint_off[v]..hint_off[v+1] of `hints` (8 limbs each);
  * aliases are (dst, src) pairs of state-local indices; consts as for
  * mgp_lower.  out: [n_states][n_cand][n_vars][8], the host layout of
- * mgp_eval_batch.  Deterministic in seed, independent of the thread count. */
+ * mgp_eval_batch.  Deterministic in seed, independent of the thread count.
+ * state_keys (may be NULL): per-state stream tags (MGP_FE_STATE_KEY), so that a
+ * state's rows depend on its content, not on its index in the batch. */
 int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
                         const uint64_t *var_off, const uint32_t *var_width, const uint8_t *var_kind,
                         const uint64_t *hint_off, const uint32_t *hints,
                         const uint64_t *alias_off, const uint32_t *aliases,
                         const uint64_t *const_off, const uint32_t *consts,
                         const uint32_t *fixed_pool, uint32_t n_fixed,
-                        const uint8_t *has_parent, const uint32_t *dom, uint32_t *out);
+                        const uint8_t *has_parent, const uint32_t *dom, const uint64_t *state_keys,
+                        uint32_t *out);
 /* mgp_refute plus the refined abstract value of every variable slot of the states it
  * does not refute: out_dom has 33 u32 per slot of var_off (known-zero, known-one, lo,
  * hi as 8 limbs each, then 1 if the slot has a domain, else 0).  `dom` of
@@ -253,7 +270,10 @@ int mgp_refute_domains(const mgp_node *nodes, const uint64_t *node_offsets, uint
  * uninterpreted-function value the node index of its application; for a pinned
  * constant its pool index), kind (0 named variable, 1 fresh UF value, 2 pinned
  * constant: every candidate row holds hint 0 of the slot).  hint_off is per variable slot (8 limbs per hint);
- * aliases are (dst, src) slot pairs local to the state.  GPU_NODES (offsets
+ * aliases are (dst, src) slot pairs local to the state.  name_hash[id] (may be NULL, n_names
+ * entries) is a stable hash of the text of arena name `id`; STATE_KEY folds it in place of the
+ * id, so a state's key (and its candidates) do not depend on the order names were interned.
+ * GPU_NODES (offsets
  * GPU_NODE_OFF) is the program the GPU evaluates: NODES except that padded key
  * equalities are replaced by the constant that strengthens the formula, and that
  * operand uses of pinned constants read VAR nodes placed in front of the state's
@@ -282,11 +302,14 @@ enum mgp_fe_field {
   MGP_FE_FLAGS,         /* uint8_t per state            */
   MGP_FE_VAR_KEY,       /* uint64_t per slot: name id, kind, UF node, piece (parent matching) */
   MGP_FE_GPU_NODE_OFF,  /* uint64_t, n_states + 1: offsets into GPU_NODES */
-  MGP_FE_VAR_TID        /* int32_t per slot: arena id of the VAR / UF term it stands for (-1 pinned) */
+  MGP_FE_VAR_TID,       /* int32_t per slot: arena id of the VAR / UF term it stands for (-1 pinned) */
+  MGP_FE_STATE_KEY      /* uint64_t per state: content key (nodes, constants, variable names by
+                           name_hash, not arena ids); candidate streams are keyed by it */
 };
 int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t *t_args, const uint32_t *t_p,
                      uint64_t n_terms, const uint32_t *limbs, uint64_t n_limbs, const int32_t *roots,
-                     const uint64_t *root_off, uint32_t n_states, mgp_fe_batch **out);
+                     const uint64_t *root_off, uint32_t n_states, const uint64_t *name_hash,
+                     uint64_t n_names, mgp_fe_batch **out);
 int mgp_fe_get(const mgp_fe_batch *batch, int field, const void **ptr, uint64_t *count);
 void mgp_fe_free(mgp_fe_batch *batch);
 
@@ -300,7 +323,12 @@ void mgp_fe_free(mgp_fe_batch *batch);
  * mgp_eval_batch, out_witness (may be NULL) n_states x n_vars x 8 u32 with n_vars =
  * *out_n_vars = the batch's widest state (SAT rows only), out_refuted[s] as
  * mgp_refute.  out_times (may be NULL) receives 5 stage times in ms: lower,
- * refute, upload+launch, GPU wait, copy-back.  Replaces, for one batch, the z3
+ * refute, upload+launch, GPU wait, copy-back.  Candidate streams are keyed by the
+ * batch's MGP_FE_STATE_KEY, so a state's answer does not depend on the batch it is in.
+ * Explicit rows (optional, n_xrows > 0): xrows [n_states][n_xrows][n_xvars][8] and
+ * xmask [n_states][n_xrows][n_xvars] -- the first n_xrows mixture rows of state s take
+ * the values of the slots the mask marks (decision rows, mgp_decision_rows).
+ * Replaces, for one batch, the z3
  * checks of Constraints.is_possible (constraints.py:34-51) and the SAT-only get_model
  * calls (analysis/solver.py:27-61) it can decide. */
 #define MGP_CHECK_NO_REFUTE 0x1u   /* skip the host pre-check (and the domain rows) */
@@ -308,6 +336,7 @@ void mgp_fe_free(mgp_fe_batch *batch);
 int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint64_t seed,
                     const uint32_t *fixed_pool, uint32_t n_fixed, const uint64_t *parent_keys,
                     const uint32_t *parent_vals, const uint64_t *parent_off, const uint64_t *slot_keys,
+                    const uint32_t *xrows, const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars,
                     uint32_t flags, int32_t *out_first, uint32_t *out_witness, int8_t *out_refuted,
                     uint32_t *out_n_vars, double *out_times);
 /* mgp_check_batch keeps the programs it lowers in a process-wide cache keyed by the
@@ -318,7 +347,8 @@ uint64_t mgp_program_cache_clear(void);
 /* Test hook: the candidates mgp_check_batch would evaluate (no parents), device layout
  * [state][var][half][cand] of 16-byte groups, n_vars >= the batch's widest state. */
 int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                      const uint32_t *fixed_pool, uint32_t n_fixed, const uint32_t *dom, uint32_t *out);
+                      const uint32_t *fixed_pool, uint32_t n_fixed, const uint32_t *dom, const uint32_t *xrows,
+                      const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars, uint32_t *out);
 
 /* ---------------------------------------------------------- Keccak-256
  * n preimages of len bytes each, preimage i at in + i*stride; 32-byte

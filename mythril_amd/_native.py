@@ -92,13 +92,16 @@ def _bind(lib):
         "mgp_guided_candidates_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P,
                                                       _P]),
         "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32,
-                                               _P, _P, _P]),
+                                               _P, _P, _P, _P]),
+        "mgp_decision_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _P]),
         "mgp_refute_domains": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
-        "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, ctypes.POINTER(_P)]),
+        "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, _P, _U64,
+                                            ctypes.POINTER(_P)]),
         "mgp_fe_get": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
         "mgp_fe_free": (None, [_P]),
-        "mgp_check_batch": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _U32, _P, _P, _P, _P, _P]),
-        "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P, _P]),
+        "mgp_check_batch": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _U32, _U32,
+                                           _P, _P, _P, _P, _P]),
+        "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _U32, _U32, _P]),
         "mgp_program_cache_clear": (_U64, []),
     }
     for name, (res, args) in sig.items():
@@ -152,6 +155,7 @@ EXPORTED_SYMBOLS = (
     "mgp_guided_candidates",
     "mgp_guided_candidates_rows",
     "mgp_make_candidates",
+    "mgp_decision_rows",
     "mgp_refute_domains",
     "mgp_build_states",
     "mgp_fe_get",
@@ -247,8 +251,9 @@ def prog_rows(words: np.ndarray, prog_offsets: np.ndarray) -> np.ndarray:
 
 
 def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hint_off, hints, alias_off, aliases,
-                    const_off, consts, fixed_pool, has_parent, var_kind=None, dom=None) -> np.ndarray:
-    """mgp_make_candidates over flattened per-state tables -> uint32 [n_states, n_cand, n_vars, 8]."""
+                    const_off, consts, fixed_pool, has_parent, var_kind=None, dom=None, state_keys=None) -> np.ndarray:
+    """mgp_make_candidates over flattened per-state tables -> uint32 [n_states, n_cand, n_vars, 8]
+    (state_keys: per-state stream tags, front.Batch.state_key; None = the state index)."""
     def u(a, dt):
         a = np.ascontiguousarray(a, dtype=dt)
         return a if a.size else np.zeros(8, dtype=dt)
@@ -264,8 +269,37 @@ def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hin
                                      _ptr(u(consts, np.uint32)), _ptr(fixed), len(fixed_pool),
                                      _ptr(u(has_parent, np.uint8)),
                                      None if dom is None else _ptr(np.ascontiguousarray(dom, dtype=np.uint32)),
+                                     None if state_keys is None else _ptr(np.ascontiguousarray(state_keys, np.uint64)),
                                      _ptr(out)))
     return out
+
+
+def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed: int, n_decide: int,
+                  rows_per_state: Optional[np.ndarray] = None, state_keys: Optional[np.ndarray] = None,
+                  max_passes: int = 0):
+    """mgp_decision_rows -> (rows u32 [n, n_decide, n_vars, 8], mask u8 [n, n_decide, n_vars], status i8[n])."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    const_offsets = np.ascontiguousarray(const_offsets, dtype=np.uint64)
+    n_states = len(node_offsets) - 1
+    rows = np.zeros((n_states, n_decide, n_vars, 8), np.uint32)
+    mask = np.zeros((n_states, n_decide, n_vars), np.uint8)
+    out = np.zeros(max(n_states, 1), np.int8)
+    rps = None
+    if rows_per_state is not None:
+        rps = np.ascontiguousarray(np.minimum(rows_per_state, 255), dtype=np.uint8)
+        if rps.shape != (n_states,):
+            raise ValueError("rows_per_state must hold one entry per state")
+    keys = None if state_keys is None else np.ascontiguousarray(state_keys, dtype=np.uint64)
+    if keys is not None and keys.shape != (n_states,):
+        raise ValueError("state_keys must hold one entry per state")
+    _check(lib().mgp_decision_rows(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
+                                   max_passes, n_vars, seed & (2 ** 64 - 1), _ptr(keys), n_decide, _ptr(rps),
+                                   _ptr(rows) if rows.size else None, _ptr(mask) if mask.size else None, _ptr(out)))
+    return rows, mask, out[:n_states]
 
 
 def refute_domains(nodes, node_offsets, consts, const_offsets, var_off, max_passes: int = 0):
@@ -386,9 +420,9 @@ class Context:
         _check(rc, self._h)
         return first, wit
 
-    def check_batch(self, batch, n_cand: int, seed: int, parents=None, refute: bool = True):
+    def check_batch(self, batch, n_cand: int, seed: int, parents=None, refute: bool = True, xrows=None):
         """A front-end batch (mythril_amd.front.Batch) through mgp_check_batch."""
-        return batch._check_native(self, n_cand, seed, parents, refute)
+        return batch._check_native(self, n_cand, seed, parents, refute, xrows)
 
     def keccak256(self, data: np.ndarray, length: int, stride: int) -> np.ndarray:
         data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)

@@ -10,8 +10,9 @@
 // A pinned-constant slot (var_kind 2, mgp_front.cpp) holds its hint 0 in every row.
 // With domains (mgp_refute_domains), every other mixture row draws the variables that
 // have a refined abstract value from it (mgp_fe_sample.h).
-// States are independent (OpenMP); the stream is splitmix64 keyed by (seed, state,
-// row, variable), so the result does not depend on the thread count.
+// States are independent (OpenMP); the stream is splitmix64 keyed by (seed, state tag,
+// row, variable), so the result does not depend on the thread count; with state_keys the
+// tag is the state's content key, so it does not depend on the batch either.
 #include <stdint.h>
 #include <string.h>
 
@@ -53,17 +54,21 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
                                    const uint64_t *alias_off, const uint32_t *aliases,
                                    const uint64_t *const_off, const uint32_t *consts,
                                    const uint32_t *fixed_pool, uint32_t n_fixed,
-                                   const uint8_t *has_parent, const uint32_t *dom, uint32_t *out) {
+                                   const uint8_t *has_parent, const uint32_t *dom, const uint64_t *state_keys,
+                                   uint32_t *out) {
   if (!var_off || !hint_off || !alias_off || !const_off || !out || (n_states && !has_parent)) return MGP_E_ARG;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t v0 = var_off[s], V = var_off[s + 1] - v0;
+    // the state's stream tag: its content key (MGP_FE_STATE_KEY) when given, so the rows do
+    // not depend on the state's position in the batch; else its index
+    const uint64_t tag = state_keys ? state_keys[s] : (uint64_t)s << 40;
     uint32_t *o = out + (uint64_t)s * n_cand * n_vars * 8u;
     // uniform everywhere first (also the padding variables of narrower states)
     for (uint32_t c = 0; c < n_cand; ++c)
       for (uint32_t v = 0; v < n_vars; ++v) {
         uint32_t *d = o + ((uint64_t)c * n_vars + v) * 8u;
-        uint64_t k = mix(seed ^ mix(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
+        uint64_t k = mix(seed ^ mix(tag ^ ((uint64_t)c << 16) ^ v));
         for (int l = 0; l < 8; l += 2) {
           k = mix(k);
           d[l] = (uint32_t)k;
@@ -101,7 +106,7 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
     const uint32_t mix0 = row;  // first mixture row
     for (uint32_t c = row; c < n_cand; ++c) {
       for (uint64_t v = 0; v < V; ++v) {
-        const uint64_t k = mix(seed ^ 0xA5A5A5A5ull ^ mix(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
+        const uint64_t k = mix(seed ^ 0xA5A5A5A5ull ^ mix(tag ^ ((uint64_t)c << 16) ^ v));
         const double r = (double)(k >> 11) * (1.0 / 9007199254740992.0);
         const uint64_t pick = mix(k);
         pend[v] = 0;
@@ -114,7 +119,7 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
         srcs.clear();
         for (uint64_t a = 0; a < na; ++a)
           if (aliases[2 * (a0 + a)] == v && aliases[2 * (a0 + a) + 1] < V) srcs.push_back(aliases[2 * (a0 + a) + 1]);
-        const uint64_t k = mix(seed ^ 0x5A5A5A5Aull ^ mix(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
+        const uint64_t k = mix(seed ^ 0x5A5A5A5Aull ^ mix(tag ^ ((uint64_t)c << 16) ^ v));
         if (!srcs.empty()) {
           memcpy(cell(c, v), cell(c, srcs[k % srcs.size()]), 32);
           continue;
@@ -141,7 +146,7 @@ extern "C" int mgp_make_candidates(uint32_t n_states, uint32_t n_cand, uint32_t 
           memcpy(o.w, d + 8, 32);
           memcpy(lo.w, d + 16, 32);
           memcpy(hi.w, d + 24, 32);
-          const uint64_t key = fe_mix64(seed ^ 0xD0D0D0D0ull ^ fe_mix64(((uint64_t)s << 40) ^ ((uint64_t)c << 16) ^ v));
+          const uint64_t key = fe_mix64(seed ^ 0xD0D0D0D0ull ^ fe_mix64(tag ^ ((uint64_t)c << 16) ^ v));
           U256 x = fe_sample_domain(z, o, lo, hi, var_width[v0 + v], kk / 2u, key);
           if (n_hint(v) && (fe_mix64(key ^ 0x9E37ull) & 1u)) {
             U256 h;

@@ -535,13 +535,50 @@ struct mgp_fe_batch {
   std::vector<uint8_t> var_kind, flags;
   std::vector<uint64_t> var_key;
   std::vector<int32_t> var_tid;
+  std::vector<uint64_t> state_key;
 };
+
+namespace {
+inline uint64_t key_mix(uint64_t h, uint64_t x) {
+  h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  h *= 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 31);
+}
+// Content key of one built state: its node list with every name replaced by a stable hash
+// of the name's text (the arena's name ids depend on the order names were first seen),
+// its GPU program, constants and variable table.  Candidate generators key their streams
+// by it instead of the state's position in the batch, so a state gets the same candidates
+// -- and the same answer -- whatever batch it arrives in and in whatever order.
+uint64_t state_key_of(const StateOut &S, const uint64_t *name_hash, uint64_t n_names) {
+  auto nh = [&](uint32_t id) -> uint64_t { return (name_hash && id < n_names) ? name_hash[id] : 0xA11CEull ^ id; };
+  uint64_t h = 0x4D595448ull;
+  auto node = [&](const mgp_node &n) {
+    h = key_mix(h, (uint64_t)n.op | ((uint64_t)n.flags << 8) | ((uint64_t)n.width << 16));
+    h = key_mix(h, ((uint64_t)(uint32_t)n.a << 32) | (uint32_t)n.b);
+    const bool uf = n.op == MGP_OP_UFAPP || n.op == MGP_OP_UFINV;
+    const uint64_t p0 = uf && n.p1 < S.var_name.size() ? nh(S.var_name[n.p1]) : n.p0;
+    h = key_mix(h, ((uint64_t)(uint32_t)n.c << 32) ^ p0);
+    h = key_mix(h, n.p1);
+  };
+  for (const mgp_node &n : S.nodes) node(n);
+  h = key_mix(h, S.gpu_nodes.size());
+  for (const mgp_node &n : S.gpu_nodes) node(n);
+  for (uint32_t c : S.consts) h = key_mix(h, c);
+  for (size_t v = 0; v < S.var_width.size(); ++v) {
+    h = key_mix(h, nh(S.var_name[v]));
+    h = key_mix(h, ((uint64_t)S.var_width[v] << 40) ^ ((uint64_t)S.var_kind[v] << 32) ^ S.var_aux[v]);
+    h = key_mix(h, S.var_full[v]);
+  }
+  return key_mix(h, S.flags);
+}
+}  // namespace
 
 extern "C" {
 
 int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t *t_args, const uint32_t *t_p,
                      uint64_t n_terms, const uint32_t *limbs, uint64_t n_limbs, const int32_t *roots,
-                     const uint64_t *root_off, uint32_t n_states, mgp_fe_batch **out) {
+                     const uint64_t *root_off, uint32_t n_states, const uint64_t *name_hash, uint64_t n_names,
+                     mgp_fe_batch **out) {
   if (!out || !root_off || (n_terms && (!t_op || !t_width || !t_args || !t_p)) || (n_states && !roots && root_off[n_states]))
     return MGP_E_ARG;
   *out = nullptr;
@@ -595,6 +632,7 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
   B->var_key.resize(nv);
   B->var_tid.resize(nv);
   B->aliases.resize(B->alias_off[n_states] * 2);
+  B->state_key.resize(n_states);
   B->hint_off.assign(nv + 1, 0);
   bool strengthened = false;
   for (uint32_t s = 0; s < n_states; ++s) {
@@ -620,6 +658,7 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
     std::copy(S.aliases.begin(), S.aliases.end(), B->aliases.begin() + B->alias_off[s] * 2);
     for (size_t v = 0; v < S.hints.size(); ++v)
       std::copy(S.hints[v].begin(), S.hints[v].end(), B->hints.begin() + B->hint_off[v0 + v] * 8);
+    B->state_key[s] = state_key_of(S, name_hash, n_names);
   }
   if (strengthened) {  // some state's GPU program differs: a separate node list and offsets
     B->gpu_node_off.assign(n_states + 1, 0);
@@ -664,6 +703,7 @@ int mgp_fe_get(const mgp_fe_batch *B, int field, const void **ptr, uint64_t *cou
     case MGP_FE_FLAGS: return set(B->flags);
     case MGP_FE_VAR_KEY: return set(B->var_key);
     case MGP_FE_VAR_TID: return set(B->var_tid);
+    case MGP_FE_STATE_KEY: return set(B->state_key);
     case MGP_FE_GPU_NODE_OFF: return set(B->gpu_nodes.empty() ? B->node_off : B->gpu_node_off);
     default: return MGP_E_ARG;
   }

@@ -786,15 +786,17 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
     uint32_t n_fixed, const int32_t *__restrict__ parent_idx, const uint32_t *__restrict__ pvals,
     const uint8_t *__restrict__ pmask, const uint32_t *__restrict__ dom, const uint32_t *__restrict__ asrc_off,
     const uint32_t *__restrict__ asrc, const uint32_t *__restrict__ wcls, const uint32_t *__restrict__ wlist,
-    uint4 *__restrict__ out) {
+    const uint64_t *__restrict__ state_keys, const uint32_t *__restrict__ xrows, const uint8_t *__restrict__ xmask,
+    uint32_t n_xrows, uint32_t n_xvars, uint4 *__restrict__ out) {
   const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (uint64_t)n_states * n_cand) return;
   const uint64_t s = g / n_cand;
+  const uint64_t tag = state_keys ? state_keys[s] : s << 40;  // as mgp_make_candidates
   const uint32_t c = (uint32_t)(g % n_cand);
   const FeRow R{out, n_cand, n_vars, c, s};
   uint32_t x[8];
   for (uint32_t v = 0; v < n_vars; ++v) {  // uniform everywhere first (also padding variables)
-    uint64_t k = fe_mix(seed ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
+    uint64_t k = fe_mix(seed ^ fe_mix(tag ^ ((uint64_t)c << 16) ^ v));
     for (int l = 0; l < 8; l += 2) {
       k = fe_mix(k);
       x[l] = (uint32_t)k;
@@ -844,7 +846,7 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       }
   } else if (c > first_row + 1) {
     auto draw = [&](uint64_t v, double *r, uint64_t *pick) {
-      const uint64_t k = fe_mix(seed ^ 0xA5A5A5A5ull ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
+      const uint64_t k = fe_mix(seed ^ 0xA5A5A5A5ull ^ fe_mix(tag ^ ((uint64_t)c << 16) ^ v));
       *r = (double)(k >> 11) * (1.0 / 9007199254740992.0);
       *pick = fe_mix(k);
     };
@@ -870,7 +872,7 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       // variable instead of the host generator's scans, same choice
       const uint32_t *srcs = asrc + asrc_off[v0 + v];
       const uint32_t n_src = asrc_off[v0 + v + 1] - asrc_off[v0 + v];
-      const uint64_t k = fe_mix(seed ^ 0x5A5A5A5Aull ^ fe_mix((s << 40) ^ ((uint64_t)c << 16) ^ v));
+      const uint64_t k = fe_mix(seed ^ 0x5A5A5A5Aull ^ fe_mix(tag ^ ((uint64_t)c << 16) ^ v));
       if (n_src) {
         R.copy((uint32_t)v, srcs[k % n_src]);
         continue;
@@ -906,7 +908,7 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
           lo.w[l] = d[16 + l];
           hi.w[l] = d[24 + l];
         }
-        const uint64_t key = fe_mix64(seed ^ 0xD0D0D0D0ull ^ fe_mix64((s << 40) ^ ((uint64_t)c << 16) ^ v));
+        const uint64_t key = fe_mix64(seed ^ 0xD0D0D0D0ull ^ fe_mix64(tag ^ ((uint64_t)c << 16) ^ v));
         U256 xv = fe_sample_domain(z, o, lo, hi, var_width[v0 + v], kk / 2u, key);
         if (n_hint(v) && (fe_mix64(key ^ 0x9E37ull) & 1u)) {
           const uint32_t *hp = hint(v, fe_mix64(key ^ 0x7F4Aull) % n_hint(v));
@@ -917,6 +919,13 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
         }
         R.put((uint32_t)v, xv.w);
       }
+    // explicit rows (host or device decision rows, mgp_decision_rows): the first n_xrows
+    // mixture rows take the given values of the slots their mask marks
+    if (xrows && kk < n_xrows) {
+      const uint64_t r0 = (s * n_xrows + kk) * (uint64_t)n_xvars;
+      for (uint64_t v = 0; v < V && v < n_xvars; ++v)
+        if (xmask[r0 + v]) R.put((uint32_t)v, xrows + (r0 + v) * 8u);
+    }
   }
   for (uint64_t v = 0; v < V; ++v)  // pinned constants
     if (var_kind && var_kind[v0 + v] == 2 && n_hint(v)) R.put((uint32_t)v, hint(v, 0));
@@ -1268,15 +1277,17 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
                                const uint8_t *pmask, const uint32_t *dom, const uint32_t *asrc_off,
-                               const uint32_t *asrc, const uint32_t *wcls, const uint32_t *wlist, uint32_t *out,
-                               hipStream_t st) {
+                               const uint32_t *asrc, const uint32_t *wcls, const uint32_t *wlist,
+                               const uint64_t *state_keys, const uint32_t *xrows, const uint8_t *xmask,
+                               uint32_t n_xrows, uint32_t n_xvars, uint32_t *out, hipStream_t st) {
   const uint64_t total = (uint64_t)n_states * n_cand;
   if (total == 0) return hipSuccess;
   const uint64_t blocks = (total + 255) / 256;
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mgp_fe_cands_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, n_states, n_cand, n_vars, seed,
                      var_off, var_width, var_kind, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed,
-                     parent_idx, pvals, pmask, dom, asrc_off, asrc, wcls, wlist, reinterpret_cast<uint4 *>(out));
+                     parent_idx, pvals, pmask, dom, asrc_off, asrc, wcls, wlist, state_keys, xrows, xmask, n_xrows,
+                     n_xvars, reinterpret_cast<uint4 *>(out));
   return hipGetLastError();
 }
 

@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -45,8 +46,9 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
                                const uint64_t *const_off, const uint32_t *consts, const uint32_t *fixed,
                                uint32_t n_fixed, const int32_t *parent_idx, const uint32_t *pvals,
                                const uint8_t *pmask, const uint32_t *dom, const uint32_t *asrc_off,
-                               const uint32_t *asrc, const uint32_t *wcls, const uint32_t *wlist, uint32_t *out,
-                               hipStream_t st);
+                               const uint32_t *asrc, const uint32_t *wcls, const uint32_t *wlist,
+                               const uint64_t *state_keys, const uint32_t *xrows, const uint8_t *xmask,
+                               uint32_t n_xrows, uint32_t n_xvars, uint32_t *out, hipStream_t st);
 int mgp_fe_get(const mgp_fe_batch *batch, int field, const void **ptr, uint64_t *count);
 int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device);
 int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg);
@@ -96,9 +98,22 @@ struct PipeBufs {
   }
 };
 
-std::unordered_map<mgp_ctx *, PipeBufs> &bufs_of() {
-  static std::unordered_map<mgp_ctx *, PipeBufs> m;
+// one buffer set per context; contexts may be driven from several host threads at once
+// (Prefilter(devices=[...]), ctypes releases the GIL), so the map is guarded and holds
+// the sets by pointer: a reference handed out stays valid while other contexts insert
+std::mutex &bufs_mu() {
+  static std::mutex m;
   return m;
+}
+std::unordered_map<mgp_ctx *, std::unique_ptr<PipeBufs>> &bufs_map() {
+  static std::unordered_map<mgp_ctx *, std::unique_ptr<PipeBufs>> m;
+  return m;
+}
+PipeBufs &bufs_of(mgp_ctx *ctx) {
+  std::lock_guard<std::mutex> lk(bufs_mu());
+  auto &p = bufs_map()[ctx];
+  if (!p) p.reset(new PipeBufs());
+  return *p;
 }
 
 enum { B_WORDS, B_OFFS, B_ORDER, B_CANDS, B_FIRST, B_WIT, B_PART, B_TABLES, B_NUM };
@@ -288,18 +303,25 @@ uint64_t mgp_program_cache_clear(void) {
 }
 
 void mgp_pipeline_release(mgp_ctx *ctx) {
-  auto &m = bufs_of();
-  auto it = m.find(ctx);
-  if (it == m.end()) return;
+  std::unique_ptr<PipeBufs> b;
+  {
+    std::lock_guard<std::mutex> lk(bufs_mu());
+    auto &m = bufs_map();
+    auto it = m.find(ctx);
+    if (it == m.end()) return;
+    b = std::move(it->second);
+    m.erase(it);
+  }
+  if (!b) return;
   for (int i = 0; i < 16; ++i)
-    if (it->second.p[i]) (void)hipFree(it->second.p[i]);
-  if (it->second.host) (void)hipHostFree(it->second.host);
-  m.erase(it);
+    if (b->p[i]) (void)hipFree(b->p[i]);
+  if (b->host) (void)hipHostFree(b->host);
 }
 
 int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64_t seed, const uint32_t *fixed_pool,
                     uint32_t n_fixed, const uint64_t *parent_keys, const uint32_t *parent_vals,
-                    const uint64_t *parent_off, const uint64_t *slot_keys, uint32_t flags, int32_t *out_first,
+                    const uint64_t *parent_off, const uint64_t *slot_keys, const uint32_t *xrows,
+                    const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars, uint32_t flags, int32_t *out_first,
                     uint32_t *out_witness, int8_t *out_refuted, uint32_t *out_n_vars, double *out_times) {
   if (!ctx || !B || !out_first || !out_refuted || n_cand == 0 || (n_fixed && !fixed_pool))
     return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument to mgp_check_batch");
@@ -313,9 +335,12 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
             gnoff = get(B, MGP_FE_GPU_NODE_OFF),
             consts = get(B, MGP_FE_CONSTS), coff = get(B, MGP_FE_CONST_OFF), voff = get(B, MGP_FE_VAR_OFF),
             vwidth = get(B, MGP_FE_VAR_WIDTH), hoff = get(B, MGP_FE_HINT_OFF), hints = get(B, MGP_FE_HINTS),
-            aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES), vkind = get(B, MGP_FE_VAR_KIND);
+            aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES), vkind = get(B, MGP_FE_VAR_KIND),
+            skey = get(B, MGP_FE_STATE_KEY);
   const uint32_t n_states = (uint32_t)(noff.n ? noff.n - 1 : 0);
   if (n_states == 0) return MGP_OK;
+  if (n_xrows && (!xrows || !xmask || n_xvars == 0))
+    return mgp_ctx_fail(ctx, MGP_E_ARG, "explicit rows need xrows, xmask and n_xvars");
   const uint64_t *vo = (const uint64_t *)voff.p;
   uint32_t n_vars = 1;
   for (uint32_t s = 0; s < n_states; ++s) n_vars = std::max<uint32_t>(n_vars, (uint32_t)(vo[s + 1] - vo[s]));
@@ -395,7 +420,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   mgp_ctx_stream(ctx, &stp, &dev);
   hipStream_t st = (hipStream_t)stp;
   hipError_t e = hipSetDevice(dev);
-  PipeBufs &D = bufs_of()[ctx];
+  PipeBufs &D = bufs_of(ctx);
   const size_t cand_bytes = (size_t)n_states * n_cand * n_vars * 32u;
   const uint32_t n_chunks = (n_cand + 63u) / 64u;
   // one table buffer: var_off | var_width | hint_off | hints | alias_off | aliases | const_off | consts |
@@ -403,20 +428,23 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   // (mgp_fe_get counts elements of each array: u32 limbs for consts / hints / aliases)
   AliasTables AT;
   alias_tables(n_states, vo, (const uint32_t *)vwidth.p, (const uint64_t *)aoff.p, (const uint32_t *)aliases.p, AT);
-  const size_t sizes[18] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+  const size_t xr_words = (size_t)n_states * n_xrows * n_xvars;
+  const size_t sizes[21] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
                             coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32,
                             (size_t)n_states * 4, pvals.size() * 4, pmask.size(), vkind.n, dom.size() * 4,
-                            AT.asrc_off.size() * 4, AT.asrc.size() * 4, AT.wcls.size() * 4, AT.wlist.size() * 4};
-  const void *srcs[18] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
+                            AT.asrc_off.size() * 4, AT.asrc.size() * 4, AT.wcls.size() * 4, AT.wlist.size() * 4,
+                            skey.n * 8, xr_words * 32, xr_words};
+  const void *srcs[21] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p, cp, fixed_pool,
                           pidx.data(), pvals.data(), pmask.data(), vkind.p, dom.data(),
-                          AT.asrc_off.data(), AT.asrc.data(), AT.wcls.data(), AT.wlist.data()};
-  // one upload: programs | program offsets | launch order | the 18 tables, 256-B aligned
+                          AT.asrc_off.data(), AT.asrc.data(), AT.wcls.data(), AT.wlist.data(),
+                          skey.p, xrows, xmask};
+  // one upload: programs | program offsets | launch order | the 21 tables, 256-B aligned
   const size_t pre[3] = {words.size() * 4u, offs.size() * 8u, (size_t)n_states * 4u};
-  size_t at[22];
+  size_t at[25];
   at[0] = 0;
   for (int i = 0; i < 3; ++i) at[i + 1] = (at[i] + pre[i] + 255) & ~(size_t)255;
-  for (int i = 0; i < 18; ++i) at[i + 4] = (at[i + 3] + sizes[i] + 255) & ~(size_t)255;
-  const size_t up = at[21];
+  for (int i = 0; i < 21; ++i) at[i + 4] = (at[i + 3] + sizes[i] + 255) & ~(size_t)255;
+  const size_t up = at[24];
   const size_t wit_bytes = (size_t)n_states * n_vars * 32u, first_bytes = ((size_t)n_states * 4u + 255) & ~(size_t)255;
   if (e == hipSuccess) e = D.ensure_host(std::max(up, first_bytes + (out_witness ? wit_bytes : 0)));
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
@@ -424,7 +452,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   memcpy(H + at[0], words.data(), pre[0]);
   memcpy(H + at[1], offs.data(), pre[1]);
   memcpy(H + at[2], order.data(), pre[2]);
-  for (int i = 0; i < 18; ++i)
+  for (int i = 0; i < 21; ++i)
     if (sizes[i] && srcs[i]) memcpy(H + at[i + 3], srcs[i], sizes[i]);
   if (e == hipSuccess) e = D.ensure(B_CANDS, cand_bytes);
   if (e == hipSuccess) e = D.ensure(B_FIRST, (size_t)n_states * 4u);
@@ -442,7 +470,8 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
                           (const uint32_t *)T(10), (const uint8_t *)T(11),
                           dom.empty() ? nullptr : (const uint32_t *)T(13), (const uint32_t *)T(14),
                           (const uint32_t *)T(15), (const uint32_t *)T(16), (const uint32_t *)T(17),
-                          (uint32_t *)D.p[B_CANDS], st);
+                          skey.n ? (const uint64_t *)T(18) : nullptr, n_xrows ? (const uint32_t *)T(19) : nullptr,
+                          n_xrows ? (const uint8_t *)T(20) : nullptr, n_xrows, n_xvars, (uint32_t *)D.p[B_CANDS], st);
   if (e == hipSuccess) e = hipMemsetAsync(D.p[B_PART], 0x7E, (size_t)n_states * n_chunks * 4u, st);
   if (e == hipSuccess)
     e = mgp_launch_eval((const uint32_t *)(base + at[0]), (const uint64_t *)(base + at[1]), n_states,
@@ -475,14 +504,16 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
 // Test hook: the candidates mgp_check_batch evaluates, copied back in the device layout
 // [state][var][half][cand] of 16-byte groups (tests compare them with mgp_make_candidates).
 int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint32_t n_vars, uint64_t seed,
-                      const uint32_t *fixed_pool, uint32_t n_fixed, const uint32_t *dom, uint32_t *out) {
+                      const uint32_t *fixed_pool, uint32_t n_fixed, const uint32_t *dom, const uint32_t *xrows,
+                      const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars, uint32_t *out) {
   if (!ctx || !B || !out || n_cand == 0 || n_vars == 0) return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument");
   const Arr noff = get(B, MGP_FE_NODE_OFF), consts = get(B, MGP_FE_CONSTS), coff = get(B, MGP_FE_CONST_OFF),
             voff = get(B, MGP_FE_VAR_OFF), vwidth = get(B, MGP_FE_VAR_WIDTH), hoff = get(B, MGP_FE_HINT_OFF),
             hints = get(B, MGP_FE_HINTS), aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES),
-            vkind = get(B, MGP_FE_VAR_KIND);
+            vkind = get(B, MGP_FE_VAR_KIND), skey = get(B, MGP_FE_STATE_KEY);
   const uint32_t n_states = (uint32_t)(noff.n ? noff.n - 1 : 0);
   if (n_states == 0) return MGP_OK;
+  if (n_xrows && (!xrows || !xmask || n_xvars == 0)) return mgp_ctx_fail(ctx, MGP_E_ARG, "bad explicit rows");
   void *stp = nullptr;
   int dev = 0;
   mgp_ctx_stream(ctx, &stp, &dev);
@@ -491,25 +522,27 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
   AliasTables AT;
   alias_tables(n_states, (const uint64_t *)voff.p, (const uint32_t *)vwidth.p, (const uint64_t *)aoff.p,
                (const uint32_t *)aliases.p, AT);
-  const size_t sizes[15] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
+  const size_t xr_words = (size_t)n_states * n_xrows * n_xvars;
+  const size_t sizes[18] = {voff.n * 8, vwidth.n * 4, hoff.n * 8, hints.n * 4, aoff.n * 8, aliases.n * 4,
                             coff.n * 8, consts.n ? consts.n * 4 : 32, (size_t)n_fixed * 32, vkind.n,
                             dom ? (size_t)((const uint64_t *)voff.p)[n_states] * 33u * 4u : 0,
-                            AT.asrc_off.size() * 4, AT.asrc.size() * 4, AT.wcls.size() * 4, AT.wlist.size() * 4};
-  const void *srcs[15] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
+                            AT.asrc_off.size() * 4, AT.asrc.size() * 4, AT.wcls.size() * 4, AT.wlist.size() * 4,
+                            skey.n * 8, xr_words * 32, xr_words};
+  const void *srcs[18] = {voff.p, vwidth.p, hoff.p, hints.p, aoff.p, aliases.p, coff.p,
                           consts.n ? consts.p : zero8, fixed_pool, vkind.p, dom,
-                          AT.asrc_off.data(), AT.asrc.data(), AT.wcls.data(), AT.wlist.data()};
-  size_t at[16];
+                          AT.asrc_off.data(), AT.asrc.data(), AT.wcls.data(), AT.wlist.data(), skey.p, xrows, xmask};
+  size_t at[19];
   at[0] = 0;
-  for (int i = 0; i < 15; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
-  std::vector<uint8_t> stage(at[15]);
-  for (int i = 0; i < 15; ++i)
+  for (int i = 0; i < 18; ++i) at[i + 1] = (at[i] + sizes[i] + 255) & ~(size_t)255;
+  std::vector<uint8_t> stage(at[18]);
+  for (int i = 0; i < 18; ++i)
     if (sizes[i] && srcs[i]) memcpy(stage.data() + at[i], srcs[i], sizes[i]);
   const size_t cb = (size_t)n_states * n_cand * n_vars * 32u;
   void *dt = nullptr, *dc = nullptr;
   hipError_t e = hipSetDevice(dev);
-  if (e == hipSuccess) e = hipMalloc(&dt, at[15]);
+  if (e == hipSuccess) e = hipMalloc(&dt, at[18]);
   if (e == hipSuccess) e = hipMalloc(&dc, cb);
-  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[15], hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dt, stage.data(), at[18], hipMemcpyHostToDevice, st);
   const uint8_t *tb = (const uint8_t *)dt;
   if (e == hipSuccess)
     e = mgp_launch_fe_cands(n_states, n_cand, n_vars, seed, (const uint64_t *)(tb + at[0]),
@@ -520,7 +553,10 @@ int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint
                             (const uint32_t *)(tb + at[7]), (const uint32_t *)(tb + at[8]), n_fixed, nullptr,
                             nullptr, nullptr, dom ? (const uint32_t *)(tb + at[10]) : nullptr,
                             (const uint32_t *)(tb + at[11]), (const uint32_t *)(tb + at[12]),
-                            (const uint32_t *)(tb + at[13]), (const uint32_t *)(tb + at[14]), (uint32_t *)dc, st);
+                            (const uint32_t *)(tb + at[13]), (const uint32_t *)(tb + at[14]),
+                            skey.n ? (const uint64_t *)(tb + at[15]) : nullptr,
+                            n_xrows ? (const uint32_t *)(tb + at[16]) : nullptr,
+                            n_xrows ? (const uint8_t *)(tb + at[17]) : nullptr, n_xrows, n_xvars, (uint32_t *)dc, st);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dc, cb, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (dt) (void)hipFree(dt);

@@ -322,6 +322,11 @@ struct State {
   std::vector<uint8_t> cmp_dom;   // 0 unsigned, 1 signed, 2 both (EQ)
   std::vector<uint8_t> cmp_t;     // orderings (x vs y) under which the node is true
   bool changed = false;
+  // decision mode (decision rows only, never a refutation): backward rules may also
+  // narrow to the PREFERRED part of a solution set -- e.g. the non-wrapping preimages of
+  // a product -- because a decision row is only a candidate that the GPU evaluation
+  // checks.  Such narrowing is unsound for a proof, so run()/refute_one never enable it.
+  bool heur = false;
   // decision rows (mgp_guided_candidates): every change can go to an undo log (a failed
   // draw rolls back instead of copying the state) and the changed nodes to a work list
   // (a decision propagates from the decided node, run_from); var-table entries are
@@ -932,6 +937,21 @@ struct State {
           return meet(x.a, ta) && meet(x.b, tb);
         }
         case MGP_OP_UMUL_NOOVF:
+          if (!T) {  // a * b >= 2^w: a >= ceil(2^w / b.hi) and b >= ceil(2^w / a.hi)
+            const uint32_t ow = W(x.a);
+            const V m = M(ow);
+            const AV A = av[x.a], B = av[x.b];
+            if (Z(A.hi) || Z(B.hi)) return false;
+            V q, rr;
+            for (int k = 0; k < 2; ++k) {
+              bv_udivrem(m, k ? A.hi : B.hi, &q, &rr);  // floor((2^w - 1) / h) + 1 = ceil(2^w / h)
+              if (EQV(q, m)) return false;            // h = 1: the other operand would need 2^w
+              AV t = top(ow);
+              t.lo = ADDV(q, ONE());
+              if (!meet(k ? x.b : x.a, t)) return false;
+            }
+            return true;
+          }
           if (T) {
             const uint32_t ow = W(x.a);
             const AV A = av[x.a], B = av[x.b];
@@ -1000,6 +1020,22 @@ struct State {
           t.z = OR(t.z, AND(NOT(al), lowm));
           t.o = al;
           if (!meet(p, t)) return false;
+        }
+        if (heur) {  // decision mode: a * c in [R.lo, R.hi] without wrapping, when that is possible
+          for (int k = 0; k < 2; ++k) {
+            const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
+            const AV B = av[q];
+            if (!is_exact(B) || Z(B.lo) || is_exact(av[p])) continue;
+            V lo, hi, rl, rh;
+            bv_udivrem(av[i].lo, B.lo, &lo, &rl);
+            if (!Z(rl)) lo = ADDV(lo, ONE());
+            bv_udivrem(av[i].hi, B.lo, &hi, &rh);
+            if (LT(hi, lo)) continue;
+            AV t = top(w);
+            t.lo = lo;
+            t.hi = hi;
+            if (compatible(p, t) && !meet(p, t)) return false;
+          }
         }
         return true;
       }
@@ -1349,6 +1385,130 @@ V sample_av(const AV &a, uint32_t w, uint32_t row, uint64_t r0) {
 }
 }  // namespace
 
+namespace {
+// One state prepared for decision rows: its base analysis (refute_one), the variable
+// slots the decisions fix (VAR nodes and the fresh value of UF applications) and, per
+// slot, the constants it is compared equal to.
+struct Prep {
+  State s;
+  int r = -1;
+  std::vector<uint32_t> slot, width;
+  std::vector<int32_t> node;
+  std::vector<std::vector<V>> eqh;
+};
+
+void prep_state(Prep &P, const mgp_node *nodes, uint64_t n, const uint32_t *consts, uint64_t n_consts,
+                uint32_t max_passes, uint32_t n_vars) {
+  P.r = refute_one(nodes, n, consts, n_consts, max_passes, &P.s);
+  if (P.r != 0) return;
+  const State &s = P.s;
+  // (var slot, width, abstract value): VAR nodes and the fresh value of UF applications
+  std::vector<int32_t> kof(s.n, -1);
+  for (uint32_t i = 0; i < s.n; ++i) {
+    const mgp_node &x = s.nd[i];
+    uint32_t v;
+    if (x.op == MGP_OP_VAR) v = x.p0;
+    else if (x.op == MGP_OP_UFAPP || x.op == MGP_OP_UFINV) v = x.p1;
+    else continue;
+    if (v >= n_vars || x.width == 0u || x.width > MGP_MAX_WIDTH) continue;
+    kof[i] = (int32_t)P.slot.size();
+    P.slot.push_back(v);
+    P.width.push_back(x.width);
+    P.node.push_back((int32_t)i);
+  }
+  // Values each variable is compared equal to (x == c anywhere in the DAG, e.g. the
+  // sender against every ACTORS address, transaction/symbolic.py:165-167): an interval
+  // cannot hold such a value set, so decisions try them first and plain domain rows
+  // draw one half of the time when it lies inside the refined domain.  In node order
+  // per variable, at most 16.
+  P.eqh.assign(P.slot.size(), {});
+  for (uint32_t i = 0; i < s.n; ++i) {
+    const mgp_node &x = s.nd[i];
+    if (x.op != MGP_OP_EQ || x.a < 0 || x.b < 0) continue;
+    for (int side = 0; side < 2; ++side) {
+      const int32_t me = side ? x.b : x.a, other = side ? x.a : x.b;
+      const int32_t k = kof[me];
+      if (k < 0 || (side && x.a == x.b)) continue;
+      if (s.nd[other].op != MGP_OP_CONST || s.nd[other].width > MGP_MAX_WIDTH) continue;
+      if (s.nd[other].p0 >= s.n_consts || P.eqh[k].size() >= 16) continue;
+      V c;
+      memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
+      P.eqh[k].push_back(bv_mask(c, P.width[k]));
+    }
+  }
+}
+
+inline bool inside_av(const AV &a, const V &v) {
+  return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
+}
+
+// Decision row `row` of a prepared state: each variable slot in turn is fixed to a draw
+// from its current abstract value and the analysis re-propagated from the decided node
+// (State::run_from: backward into its operands, through its users, transitively, then
+// the pair orderings), so later variables are drawn from values narrowed by the earlier
+// choices (x + y == c, a mapping key fixed by an equality, ...).  A draw that empties a
+// domain is rolled back through the undo log and replaced (up to kTries draws).  Writes
+// the value of slot k to put(slot[k], value).  Stream key per slot: (seed, tag, c, slot).
+template <typename Put>
+void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, uint32_t max_passes,
+                  Put put) {
+  const State &s = P.s;
+  const std::vector<uint32_t> &slot = P.slot, &width = P.width;
+  const std::vector<int32_t> &node = P.node;
+  const std::vector<std::vector<V>> &eqh = P.eqh;
+  constexpr uint32_t kTries = 4;
+  // MGP_DECIDE_PASSES=k re-runs k full passes per decision instead of run_from (A/B: the
+  // same witnesses)
+  static const uint32_t decide_passes = [] {
+    const char *e = getenv("MGP_DECIDE_PASSES");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  const uint32_t passes = std::min(max_passes ? max_passes : 16u, decide_passes ? decide_passes : 1u);
+  State d = s;
+  std::vector<State::UndoRec> undo_log;
+  std::vector<uint32_t> work;
+  d.build_graph();
+  d.undo = &undo_log;
+  d.touched = &work;
+  d.heur = true;
+  const uint32_t budget = 4u * d.n + 64u;
+  // the draw schedule of decision row `row`: the first eight rows decide in node
+  // order (schedules 0, 4, 6, 8, 2, 10, 12, 14: the lo/hi schedule 0 that BECToken's
+  // mapping witness needs and three random-draw schedules first, so a state given
+  // four rows keeps most of its yield), later ones add the reverse-order schedules
+  // (odd) and then the rest, so any n_decide = 16 + k covers schedules 0..15+k.
+  // Node order is what contract states need (WalletLibrary's loop and mapping
+  // queries: 60 against 57 states of the mixed corpus at eight rows, at a third
+  // of the host time)
+  static const uint8_t kFirst8[8] = {0, 4, 6, 8, 2, 10, 12, 14};
+  const uint32_t drow = row < 8u ? kFirst8[row] : row < 16u ? 2u * (row - 8u) + 1u : row;
+  for (size_t kk = 0; kk < slot.size(); ++kk) {
+    const size_t k = (drow & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
+    const uint64_t key = mix64(seed ^ mix64(tag ^ ((uint64_t)c << 12) ^ slot[k]));
+    if (EQV(d.av[node[k]].lo, d.av[node[k]].hi)) {  // already one value: nothing to decide
+      put(slot[k], d.av[node[k]].lo);
+      continue;
+    }
+    V v = bv_zero();
+    const uint32_t nh = (uint32_t)eqh[k].size();
+    for (uint32_t t = 0; t < kTries + nh; ++t) {
+      v = t < nh ? eqh[k][(t + drow + (drow < 8u ? 0u : (uint32_t)(key >> 40))) % nh]
+                 : sample_av(d.av[node[k]], width[k], t > nh ? 3u + drow + t : (drow < 4 ? drow / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + drow : 0u)), mix64(key + t));
+      if (t < nh && !inside_av(d.av[node[k]], v)) continue;
+      const size_t mark = undo_log.size();
+      work.clear();
+      if (d.meet(node[k], exact(v, width[k])) &&
+          (decide_passes ? d.tie() && d.run(passes) == 0 : d.run_from((uint32_t)node[k], budget) == 0)) {
+        undo_log.clear();
+        break;
+      }
+      d.rollback(mark);
+    }
+    put(slot[k], v);
+  }
+}
+}  // namespace
+
 extern "C" int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
                                           const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
                                           uint32_t n_cand, uint32_t n_vars, uint64_t seed, uint32_t every,
@@ -1363,13 +1523,6 @@ extern "C" int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t 
   uint32_t n_dec_rows = 0;
   for (uint32_t c = 0, row = 0; c < n_cand && row < n_decide; c += every, ++row) ++n_dec_rows;
   const int64_t per_state = (int64_t)n_dec_rows + 1;
-  struct Prep {
-    State s;
-    int r = -1;
-    std::vector<uint32_t> slot, width;
-    std::vector<int32_t> node;
-    std::vector<std::vector<V>> eqh;
-  };
   constexpr uint32_t kChunk = 256;
   for (uint32_t cs = 0; cs < n_states; cs += kChunk) {
     const uint32_t ce = std::min<uint32_t>(n_states, cs + kChunk);
@@ -1379,44 +1532,8 @@ extern "C" int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t 
       Prep &P = prep[st - cs];
       const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
       const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
-      P.r = refute_one(nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, &P.s);
+      prep_state(P, nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, n_vars);
       out[st] = (int8_t)P.r;
-      if (P.r != 0) continue;
-      const State &s = P.s;
-      // (var slot, width, abstract value): VAR nodes and the fresh value of UF applications
-      std::vector<int32_t> kof(s.n, -1);
-      for (uint32_t i = 0; i < s.n; ++i) {
-        const mgp_node &x = s.nd[i];
-        uint32_t v;
-        if (x.op == MGP_OP_VAR) v = x.p0;
-        else if (x.op == MGP_OP_UFAPP || x.op == MGP_OP_UFINV) v = x.p1;
-        else continue;
-        if (v >= n_vars || x.width == 0u || x.width > MGP_MAX_WIDTH) continue;
-        kof[i] = (int32_t)P.slot.size();
-        P.slot.push_back(v);
-        P.width.push_back(x.width);
-        P.node.push_back((int32_t)i);
-      }
-      // Values each variable is compared equal to (x == c anywhere in the DAG, e.g. the
-      // sender against every ACTORS address, transaction/symbolic.py:165-167): an interval
-      // cannot hold such a value set, so decisions try them first and plain domain rows
-      // draw one half of the time when it lies inside the refined domain.  In node order
-      // per variable, at most 16.
-      P.eqh.assign(P.slot.size(), {});
-      for (uint32_t i = 0; i < s.n; ++i) {
-        const mgp_node &x = s.nd[i];
-        if (x.op != MGP_OP_EQ || x.a < 0 || x.b < 0) continue;
-        for (int side = 0; side < 2; ++side) {
-          const int32_t me = side ? x.b : x.a, other = side ? x.a : x.b;
-          const int32_t k = kof[me];
-          if (k < 0 || (side && x.a == x.b)) continue;
-          if (s.nd[other].op != MGP_OP_CONST || s.nd[other].width > MGP_MAX_WIDTH) continue;
-          if (s.nd[other].p0 >= s.n_consts || P.eqh[k].size() >= 16) continue;
-          V c;
-          memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
-          P.eqh[k].push_back(bv_mask(c, P.width[k]));
-        }
-      }
     }
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t task = (int64_t)cs * per_state; task < (int64_t)ce * per_state; ++task) {
@@ -1428,87 +1545,67 @@ extern "C" int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t 
       const uint32_t rs = rows_per_state ? std::min<uint32_t>(rows_per_state[st], n_dec_rows) : n_dec_rows;
       if (task_row < n_dec_rows && task_row >= rs) continue;
       const State &s = P.s;
-      const std::vector<uint32_t> &slot = P.slot, &width = P.width;
-      const std::vector<int32_t> &node = P.node;
-      const std::vector<std::vector<V>> &eqh = P.eqh;
-      auto inside = [&](const AV &a, const V &v) {
-        return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
-      };
-      // The first n_decide guided rows are built by decisions: each variable in turn is
-      // fixed to a draw from its current abstract value and the analysis re-run, so later
-      // variables are drawn from values narrowed by the earlier choices (x + y == c, a
-      // mapping key fixed by an equality, ...).  A draw that empties a domain is replaced
-      // (up to kTries draws); the remaining rows are plain draws from the refined domains.
-      constexpr uint32_t kTries = 4;
-      // a decision propagates from the decided node only (State::run_from: backward into
-      // its operands, through its users, transitively, then the pair orderings), with an
-      // undo log for a draw that empties a domain; MGP_DECIDE_PASSES=k re-runs k full
-      // passes instead (A/B: the same witnesses)
-      static const uint32_t decide_passes = [] {
-        const char *e = getenv("MGP_DECIDE_PASSES");
-        return e ? (uint32_t)atoi(e) : 0u;
-      }();
-      const uint32_t passes = std::min(max_passes ? max_passes : 16u, decide_passes ? decide_passes : 1u);
       for (uint32_t c = 0, row = 0; c < n_cand; c += every, ++row) {
         uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
         if (task_row < n_dec_rows ? row != task_row : row < rs) continue;
         if (row < rs) {
-          State d = s;
-          std::vector<State::UndoRec> undo_log;
-          std::vector<uint32_t> work;
-          d.build_graph();
-          d.undo = &undo_log;
-          d.touched = &work;
-          const uint32_t budget = 4u * d.n + 64u;
-          // the draw schedule of decision row `row`: the first eight rows decide in node
-          // order (schedules 0, 4, 6, 8, 2, 10, 12, 14: the lo/hi schedule 0 that BECToken's
-          // mapping witness needs and three random-draw schedules first, so a state given
-          // four rows keeps most of its yield), later ones add the reverse-order schedules
-          // (odd) and then the rest, so any n_decide = 16 + k covers schedules 0..15+k.
-          // Node order is what contract states need (WalletLibrary's loop and mapping
-          // queries: 60 against 57 states of the mixed corpus at eight rows, at a third
-          // of the host time)
-          static const uint8_t kFirst8[8] = {0, 4, 6, 8, 2, 10, 12, 14};
-          const uint32_t drow = row < 8u ? kFirst8[row] : row < 16u ? 2u * (row - 8u) + 1u : row;
-          for (size_t kk = 0; kk < slot.size(); ++kk) {
-            const size_t k = (drow & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
-            const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
-            if (EQV(d.av[node[k]].lo, d.av[node[k]].hi)) {  // already one value: nothing to decide
-              memcpy(dst + slot[k] * 8ull, d.av[node[k]].lo.w, 32);
-              continue;
-            }
-            V v = bv_zero();
-            const uint32_t nh = (uint32_t)eqh[k].size();
-            for (uint32_t t = 0; t < kTries + nh; ++t) {
-              v = t < nh ? eqh[k][(t + drow + (drow < 8u ? 0u : (uint32_t)(key >> 40))) % nh]
-                         : sample_av(d.av[node[k]], width[k], t > nh ? 3u + drow + t : (drow < 4 ? drow / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + drow : 0u)), mix64(key + t));
-              if (t < nh && !inside(d.av[node[k]], v)) continue;
-              const size_t mark = undo_log.size();
-              work.clear();
-              if (d.meet(node[k], exact(v, width[k])) &&
-                  (decide_passes ? d.tie() && d.run(passes) == 0 : d.run_from((uint32_t)node[k], budget) == 0)) {
-                undo_log.clear();
-                break;
-              }
-              d.rollback(mark);
-            }
-            memcpy(dst + slot[k] * 8ull, v.w, 32);
-          }
+          decision_row(P, row, c, seed, (uint64_t)st << 32, max_passes,
+                       [&](uint32_t sl, const V &v) { memcpy(dst + sl * 8ull, v.w, 32); });
           continue;
         }
-        for (size_t k = 0; k < slot.size(); ++k) {
-          const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ slot[k]));
-          V v = sample_av(s.av[node[k]], width[k], row, key);
-          if (!eqh[k].empty() && (mix64(key ^ 0x9E37ull) & 1u)) {
-            const V h = eqh[k][mix64(key ^ 0x7F4Aull) % eqh[k].size()];
-            if (inside(s.av[node[k]], h)) v = h;
+        for (size_t k = 0; k < P.slot.size(); ++k) {
+          const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ P.slot[k]));
+          V v = sample_av(s.av[P.node[k]], P.width[k], row, key);
+          if (!P.eqh[k].empty() && (mix64(key ^ 0x9E37ull) & 1u)) {
+            const V h = P.eqh[k][mix64(key ^ 0x7F4Aull) % P.eqh[k].size()];
+            if (inside_av(s.av[P.node[k]], h)) v = h;
           }
-          memcpy(dst + slot[k] * 8ull, v.w, 32);
+          memcpy(dst + P.slot[k] * 8ull, v.w, 32);
         }
       }
     }
   }
   return 0;
+}
+
+extern "C" int mgp_decision_rows(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                 const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                 uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
+                                 const uint8_t *rows_per_state, uint32_t *out_rows, uint8_t *out_mask,
+                                 int8_t *out) {
+  if (!node_offsets || !out || (n_states && (!nodes || !const_offsets)) ||
+      (n_states && n_decide && (!out_rows || !out_mask)))
+    return MGP_E_ARG;
+  if (n_states && n_decide) memset(out_mask, 0, (size_t)n_states * n_decide * n_vars);
+  constexpr uint32_t kChunk = 256;
+  for (uint32_t cs = 0; cs < n_states; cs += kChunk) {
+    const uint32_t ce = std::min<uint32_t>(n_states, cs + kChunk);
+    std::vector<Prep> prep(ce - cs);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t st = cs; st < (int64_t)ce; ++st) {
+      const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
+      const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
+      prep_state(prep[st - cs], nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes,
+                 n_vars);
+      out[st] = (int8_t)prep[st - cs].r;
+    }
+    // one task per (state, row): a small batch spreads its rows over the host threads
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t task = (int64_t)cs * n_decide; task < (int64_t)ce * n_decide; ++task) {
+      const int64_t st = task / n_decide;
+      const uint32_t row = (uint32_t)(task % n_decide);
+      const Prep &P = prep[st - cs];
+      const uint32_t rs = rows_per_state ? std::min<uint32_t>(rows_per_state[st], n_decide) : n_decide;
+      if (P.r != 0 || row >= rs) continue;
+      const uint64_t tag = state_keys ? state_keys[st] : (uint64_t)st << 32;
+      const uint64_t r0 = ((uint64_t)st * n_decide + row) * n_vars;
+      decision_row(P, row, 2u * row, seed, tag, max_passes, [&](uint32_t sl, const V &v) {
+        memcpy(out_rows + (r0 + sl) * 8ull, v.w, 32);
+        out_mask[r0 + sl] = 1;
+      });
+    }
+  }
+  return MGP_OK;
 }
 
 extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,

@@ -31,7 +31,7 @@ _FIELDS = {
     "var_aux": (9, np.uint32, 1), "var_kind": (10, np.uint8, 1), "hint_off": (11, np.uint64, 1),
     "hints": (12, np.uint32, 8), "alias_off": (13, np.uint64, 1), "aliases": (14, np.uint32, 2),
     "flags": (15, np.uint8, 1), "var_key": (16, np.uint64, 1), "gpu_node_off": (17, np.uint64, 1),
-    "var_tid": (18, np.int32, 1),
+    "var_tid": (18, np.int32, 1), "state_key": (19, np.uint64, 1),
 }
 _VAR_TABLES = ("var_off", "var_width", "var_full", "var_name", "var_aux", "var_kind", "var_key", "var_tid")
 FIXED_POOL_LIMBS = None  # dag._FIXED_LIMBS (set lazily: dag imports the native module too)
@@ -44,7 +44,9 @@ def _arena_ptr(a) -> ctypes.c_void_p:
 class Batch:
     """Flattened constraint DAGs of n states (owned by the native batch object)."""
 
-    def __init__(self, term_lists: Sequence[Sequence[Term]]):
+    def __init__(self, term_lists: Sequence[Sequence[Term]], arena=None):
+        """arena: the term arena to read (smt.ARENA, or a snapshot of it with the same
+        arrays for a builder running off the thread that creates terms)."""
         L = N.lib()
         roots = np.fromiter((t.tid for lst in term_lists for t in lst), dtype=np.int32)
         off = np.zeros(len(term_lists) + 1, np.uint64)
@@ -55,10 +57,11 @@ class Batch:
         self.n_states = len(term_lists)
         self._vt = None
         self._h = ctypes.c_void_p()
-        A = ARENA
+        A = ARENA if arena is None else arena
         rc = L.mgp_build_states(_arena_ptr(A.op), _arena_ptr(A.width), _arena_ptr(A.args), _arena_ptr(A.p),
                                 len(A.op), _arena_ptr(A.limbs), len(A.limbs), N._ptr(roots), N._ptr(off),
-                                self.n_states, ctypes.byref(self._h))
+                                self.n_states, _arena_ptr(A.name_hash) if len(A.name_hash) else None,
+                                len(A.name_hash), ctypes.byref(self._h))
         N._check(rc)
         for name, (idx, dt, per) in _FIELDS.items():
             p, n = ctypes.c_void_p(), ctypes.c_uint64()
@@ -79,12 +82,15 @@ class Batch:
             self._vt = VarTables(*(np.array(getattr(self, k)) for k in _VAR_TABLES))
         return self._vt
 
-    def check(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True):
+    def check(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True,
+              xrows=None):
         """-> (first_sat i32[n], witness u32[n, n_vars, 8], refuted i8[n], stage ms[5]) through the
-        context's check_batch (mgp_check_batch on a libmgp context)."""
-        return ctx.check_batch(self, n_cand, seed, parents, refute)
+        context's check_batch (mgp_check_batch on a libmgp context).  xrows = (rows u32 [n, k,
+        nv, 8], mask u8 [n, k, nv]): explicit rows placed in the first k mixture rows."""
+        return ctx.check_batch(self, n_cand, seed, parents, refute, xrows)
 
-    def _check_native(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True):
+    def _check_native(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True,
+                      xrows=None):
         """mgp_check_batch on libmgp context `ctx`."""
         global FIXED_POOL_LIMBS
         if FIXED_POOL_LIMBS is None:
@@ -112,15 +118,29 @@ class Batch:
             po[1:] = np.cumsum(cnt)
             if pk.size == 0:
                 pk, pv = np.zeros(1, np.uint64), np.zeros((1, 8), np.uint32)
+        xr, xm, nx, nxv = self._xrows(xrows)
         rc = N.lib().mgp_check_batch(ctx._h, self._h, n_cand, seed & (2 ** 64 - 1), N._ptr(FIXED_POOL_LIMBS),
                                      len(FIXED_POOL_LIMBS), N._ptr(pk), N._ptr(pv), N._ptr(po),
                                      N._ptr(self.var_key) if pk is not None else None,
+                                     N._ptr(xr), N._ptr(xm), nx, nxv,
                                      0 if refute else 1, N._ptr(first), N._ptr(wit), N._ptr(ref),
                                      ctypes.byref(nv), N._ptr(times))
         N._check(rc, ctx._h)
         return first, wit, ref[:n], times
 
-    def device_candidates(self, ctx, n_cand: int, n_vars: int, seed: int, dom=None) -> np.ndarray:
+    def _xrows(self, xrows):
+        if xrows is None:
+            return None, None, 0, 0
+        rows, mask = xrows
+        rows = np.ascontiguousarray(rows, dtype=np.uint32)
+        mask = np.ascontiguousarray(mask, dtype=np.uint8)
+        if rows.ndim != 4 or rows.shape[0] != self.n_states or rows.shape[3] != 8 or mask.shape != rows.shape[:3]:
+            raise ValueError("xrows must be (rows u32 [n_states, k, n_vars, 8], mask u8 [n_states, k, n_vars])")
+        if rows.shape[1] == 0 or rows.shape[2] == 0:
+            return None, None, 0, 0
+        return rows, mask, rows.shape[1], rows.shape[2]
+
+    def device_candidates(self, ctx, n_cand: int, n_vars: int, seed: int, dom=None, xrows=None) -> np.ndarray:
         """Test hook (mgp_fe_candidates): the GPU-generated first-round candidates, returned in
         the host layout [state][cand][var][8] of mgp_make_candidates."""
         global FIXED_POOL_LIMBS
@@ -130,10 +150,11 @@ class Batch:
             FIXED_POOL_LIMBS = np.ascontiguousarray(_FIXED_LIMBS, dtype=np.uint32)
         n = self.n_states
         dev = np.zeros((n, n_vars, 2, n_cand, 4), np.uint32)
+        xr, xm, nx, nxv = self._xrows(xrows)
         N._check(N.lib().mgp_fe_candidates(ctx._h, self._h, n_cand, n_vars, seed & (2 ** 64 - 1),
                                            N._ptr(FIXED_POOL_LIMBS), len(FIXED_POOL_LIMBS),
                                            None if dom is None else N._ptr(np.ascontiguousarray(dom, np.uint32)),
-                                           N._ptr(dev)), ctx._h)
+                                           N._ptr(xr), N._ptr(xm), nx, nxv, N._ptr(dev)), ctx._h)
         return np.ascontiguousarray(dev.transpose(0, 3, 1, 2, 4).reshape(n, n_cand, n_vars, 8))
 
     def witness(self, s: int, words: np.ndarray) -> "SlotWitness":

@@ -22,6 +22,7 @@ decided here: that is the GPU kernel's job (or z3's).
 """
 from __future__ import annotations
 
+import hashlib
 import weakref
 from array import array
 from typing import Any, Dict, List, Optional, Sequence, Set, Tuple, Union
@@ -49,12 +50,17 @@ class _Arena:
         self.limbs = array("I")
         self.names: List[str] = []
         self.name_id: Dict[str, int] = {}
+        # a stable 64-bit hash of each name's text (blake2b; Python's str hash is salted
+        # per process): the native front end keys a state's candidates by its content with
+        # names folded in by these, not by the interning order of the ids
+        self.name_hash = array("Q")
 
     def intern_name(self, name: str) -> int:
         k = self.name_id.get(name)
         if k is None:
             k = self.name_id[name] = len(self.names)
             self.names.append(name)
+            self.name_hash.append(int.from_bytes(hashlib.blake2b(name.encode(), digest_size=8).digest(), "little"))
         return k
 
     def add(self, op: int, width: int, args: Tuple["Term", ...], params: Tuple) -> int:

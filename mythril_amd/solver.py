@@ -187,18 +187,29 @@ class UnsatCores:
     cache").  Refuted sets are first shrunk to a core (`shrink`), which then also covers
     other paths that repeat the same contradiction.  Terms are hash-consed, so set
     membership is identity of the interned constraint terms.
+
+    Thread safety: a background shrink (flush(background=True)) works on a snapshot of the
+    term arena taken on the caller's thread (the arena's arrays may be reallocated while
+    the worker's native calls run without the GIL), and its cores are stored under the
+    cache lock only if no reset() happened since the snapshot.
     """
 
     def __init__(self, max_sets: int = 1 << 14):
         self.max_sets = max_sets
+        self._lock = threading.RLock()
         self.reset()
 
     def reset(self) -> None:
-        self.sets: List[frozenset] = []
-        self.index: Dict[Term, List[int]] = {}  # every stored set under ONE of its members
-        self.pending: List[list] = []  # refuted lists not yet shrunk (Prefilter.core_batch)
-        self.gen = getattr(self, "gen", 0) + 1  # a background shrink of an older generation is dropped
-        self._worker = getattr(self, "_worker", None)
+        with self._lock:
+            self.sets: List[frozenset] = []
+            self.index: Dict[Term, List[int]] = {}  # every stored set under ONE of its members
+            self.pending: List[list] = []  # refuted lists not yet shrunk (Prefilter.core_batch)
+            self.gen = getattr(self, "gen", 0) + 1  # a background shrink of an older generation is dropped
+            self._worker = getattr(self, "_worker", None)
+
+    def add_pending(self, lists: Sequence[list]) -> None:
+        with self._lock:
+            self.pending.extend(lists)
 
     def flush(self, N, background: bool = False) -> None:
         """Shrink the pending refuted constraint lists to cores (one batched shrink_many)
@@ -209,21 +220,25 @@ class UnsatCores:
         if background:
             if self._worker is not None and self._worker.is_alive():
                 return
-            import threading
+            from .smt import ARENA
 
-            pending, self.pending, gen = self.pending, [], self.gen
+            with self._lock:
+                pending, self.pending, gen = self.pending, [], self.gen
+            snap = _ArenaSnapshot(ARENA)  # on this thread: the worker never reads the live arena
 
             def work():
-                cores = UnsatCores.shrink_many(N, pending)
-                if self.gen == gen:
-                    for core in cores:
-                        self.add(core)
+                cores = UnsatCores.shrink_many(N, pending, arena=snap)
+                with self._lock:
+                    if self.gen == gen:
+                        for core in cores:
+                            self.add(core)
 
             self._worker = threading.Thread(target=work, name="mgp-unsat-cores", daemon=True)
             self._worker.start()
             return
         self.join()
-        pending, self.pending = self.pending, []
+        with self._lock:
+            pending, self.pending = self.pending, []
         for core in UnsatCores.shrink_many(N, pending):
             self.add(core)
 
@@ -235,19 +250,21 @@ class UnsatCores:
 
     def covered(self, terms: Iterable[Term]) -> bool:
         s = set(terms)
-        for t in s:
-            for k in self.index.get(t, ()):
-                if self.sets[k] <= s:
-                    return True
+        with self._lock:
+            for t in s:
+                for k in self.index.get(t, ()):
+                    if self.sets[k] <= s:
+                        return True
         return False
 
     def add(self, core: Iterable[Term]) -> None:
         fs = frozenset(core)
-        if not fs or len(self.sets) >= self.max_sets or self.covered(fs):
-            return
-        self.sets.append(fs)
-        anchor = min(fs, key=lambda t: len(self.index.get(t, ())))
-        self.index.setdefault(anchor, []).append(len(self.sets) - 1)
+        with self._lock:
+            if not fs or len(self.sets) >= self.max_sets or self.covered(fs):
+                return
+            self.sets.append(fs)
+            anchor = min(fs, key=lambda t: len(self.index.get(t, ())))
+            self.index.setdefault(anchor, []).append(len(self.sets) - 1)
 
     @staticmethod
     def shrink(N, terms: Sequence[Term], max_terms: int = 32) -> List[Term]:
@@ -255,12 +272,17 @@ class UnsatCores:
         return UnsatCores.shrink_many(N, [terms], max_terms)[0]
 
     @staticmethod
-    def shrink_many(N, lists: Sequence[Sequence[Term]], max_terms: int = 32) -> List[List[Term]]:
+    def shrink_many(N, lists: Sequence[Sequence[Term]], max_terms: int = 32, arena=None) -> List[List[Term]]:
         """Deletion-based cores of many refuted constraint lists in two native calls: one
         batch holds every single-constraint deletion of every list (mgp_build_states +
         mgp_refute); the constraints whose deletion breaks a refutation form that list's
-        core if a second batched refute confirms it alone."""
+        core if a second batched refute confirms it alone.  `arena`: the term arena to read
+        (a snapshot for a background shrink; default the live one)."""
+        from functools import partial
+
         from .front import Batch
+
+        Batch = partial(Batch, arena=arena) if arena is not None else Batch
 
         lists = [list(dict.fromkeys(t)) for t in lists]
         trials, owner = [], []
@@ -291,6 +313,16 @@ class UnsatCores:
         return out
 
 
+class _ArenaSnapshot:
+    """A copy of the term arena's arrays (front.Batch reads these through raw pointers)."""
+
+    def __init__(self, A):
+        from array import array
+
+        self.op, self.width, self.args = array("B", A.op), array("I", A.width), array("i", A.args)
+        self.p, self.limbs, self.name_hash = array("I", A.p), array("I", A.limbs), array("Q", A.name_hash)
+
+
 _cores = UnsatCores()
 
 
@@ -300,32 +332,45 @@ def unsat_cores() -> UnsatCores:
 
 # ------------------------------------------------------------- GPU stage
 class Prefilter:
-    """Batched GPU witness search over states (one libmgp context)."""
+    """Batched GPU witness search over states: one libmgp context per device.
 
-    def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448):
+    Answers are a function of each state's content only.  Candidate streams are keyed
+    by the state's content key (mgp_build_states MGP_FE_STATE_KEY) and a fixed seed,
+    every open state gets the same second round (decision rows within a per-state work
+    cap, not a wall-clock budget), so a state is SAT / refuted / undecided the same way
+    in any batch, in any order, on any number of host threads or devices.
+
+    devices=[d0, d1, ...]: one context and one host thread per device; a batch is
+    hash-sharded over them by state content key (distributed.shard_of) and the results
+    are merged in input order (BASELINE config 4)."""
+
+    # second witness round for the states the first round and the pre-check leave open:
+    # RETRY_CAND device-generated candidates (a new seed, domain rows) whose first
+    # DECIDE_ROWS mixture rows are host decision rows (mgp_decision_rows)
+    RETRY_CAND = 256
+    DECIDE_ROWS = 4
+    DECIDE_MIN_ROWS = 2
+    # per-state work cap of the decision rows: variables x DAG nodes x rows (a deterministic
+    # count; the largest WalletLibrary state of the corpus needs 1.8 M at four rows)
+    DECIDE_MAX_UNITS = 1 << 25
+
+    def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,
+                 devices: Optional[Sequence[int]] = None):
         from . import _native as N
 
         self._N = N
-        self.ctx = N.Context(device)
+        self.devices = list(devices) if devices is not None else [device]
+        if not self.devices:
+            raise ValueError("Prefilter needs at least one device")
+        self.ctxs = [N.Context(d) for d in self.devices]
+        self.ctx = self.ctxs[0]
         self.n_cand = n_cand
         self.seed = seed
-        self._calls = 0
         self.refute = True  # host UNSAT pre-check (mgp_refute) on every GPU miss
-        # second witness round for the states the first round and the pre-check left open:
-        # fresh candidates (half of them guided by the pre-check's domains), up to retry_cand
-        # per state (host candidate memory capped at 1 GiB)
-        self.retry_cand = 1024
-        self.cand_bytes = 1 << 30  # candidate memory of one witness round
-        # host decision rows (mgp_guided_candidates) cost two domain-analysis passes per
-        # variable and row: states are taken cheapest first while the estimated wall time of
-        # the round stays within max(decide_budget_ms, decide_ms_per_state x batch size) (a
-        # WalletLibrary state costs ~40 ms of one core per row, a BECToken state ~6 ms;
-        # each witness found saves a fallback call)
-        self.decide_budget_ms = 100.0
-        self.decide_ms_per_state = 1.0
-        # host CPU microseconds per decision row and (variable x DAG node), re-measured on
-        # every decision round (moving average), so the budget admits what this host runs
-        self.decide_us_per_unit = self.DECIDE_US_PER_UNIT
+        self.retry_cand = self.RETRY_CAND  # 0 (or <= n_cand) = no second round
+        self.decide_rows = self.DECIDE_ROWS
+        self.decide_max_units = self.DECIDE_MAX_UNITS
+        self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # refuted constraint lists wait in the core cache and are shrunk to cores together
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
         # one per call keeps the deletion trials off the latency of small calls
@@ -334,15 +379,12 @@ class Prefilter:
         # the host idle between calls: back to back, its OpenMP team competes with the next
         # call's (the bench's first-round pass fell from 3 850 to 2 680 states/s with it on)
         self.core_async = False
-        # candidates per state of the device retry round before host decisions (0 = none;
-        # MGP_RETRY_GPU_CAND overrides, for A/B runs), run only for at least
-        # retry_gpu_min_states open states: on the mixed corpus it finds 7 witnesses among
-        # 263 open states for 80 ms, and a small call's decisions fit their budget anyway
-        # (2-state call 5.8 -> 4.1 ms without it, bench_r2k3)
-        self.retry_gpu_cand = int(os.environ.get("MGP_RETRY_GPU_CAND", self.RETRY_GPU_CAND))
-        self.retry_gpu_min_states = 32
         self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
+
+    def close(self) -> None:
+        for c in self.ctxs:
+            c.close()
 
     def check_states(self, states: Sequence[Sequence[Term]],
                      parents: Optional[Sequence[Optional[Dict[str, int]]]] = None) -> List[Tuple[str, Optional[Dict[str, int]]]]:
@@ -364,7 +406,17 @@ class Prefilter:
             rest_par = None if parents is None else [p for p, h in zip(parents, hit) if not h]
             sub = iter(self.check_states(rest, rest_par) if rest else [])
             return [(unsat, None) if h else next(sub) for h in hit]
-        out = self._check_native(states, parents)
+        if len(self.ctxs) > 1 and len(states) > 1:
+            out, refuted = self._check_sharded(states, parents)
+        else:
+            out, refuted = self._check_native(self.ctx, states, parents)
+        if refuted:
+            _cores.add_pending([list(states[i]) for i in refuted])
+            if len(_cores.pending) >= self.core_batch:
+                tr = time.perf_counter()
+                _cores.flush(self._N, background=self.core_async)
+                if self.last_profile is not None:
+                    self.last_profile["cores_ms"] = 1e3 * (time.perf_counter() - tr)
         stats.gpu_batches += 1
         stats.gpu_queries += len(states)
         stats.gpu_sat += sum(1 for r in out if r[0] == sat)
@@ -373,12 +425,57 @@ class Prefilter:
         stats.gpu_time += time.time() - t0
         return out
 
-    def _check_native(self, states, parents):
-        """One native front-end batch (mgp_build_states) through mgp_check_batch: GPU
-        witnesses, host refutations overlapped with the GPU; a second, domain-guided
-        witness round for what is left; cores of the refuted states, batched.  A batch
-        whose candidate block would pass `cand_bytes` is split into sub-batches of
-        similar variable counts."""
+    def shard(self, states: Sequence[Sequence[Term]]) -> np.ndarray:
+        """Device index (into self.devices) of every state: hash of its content key."""
+        from .distributed import shard_of
+        from .front import Batch
+
+        B = Batch(states)
+        keys = np.array(B.state_key, dtype=np.uint64)
+        B.close()
+        return shard_of(keys, len(self.ctxs))
+
+    def _check_sharded(self, states, parents):
+        """One host thread per device, each running the whole pipeline on its hash shard
+        (the native calls release the GIL); results merged in input order."""
+        owner = self.shard(states)
+        parts = [np.nonzero(owner == g)[0] for g in range(len(self.ctxs))]
+        results: List = [None] * len(self.ctxs)
+        errors: List = []
+
+        def work(g):
+            idx = parts[g]
+            try:
+                results[g] = self._check_native(self.ctxs[g], [states[i] for i in idx],
+                                                None if parents is None else [parents[i] for i in idx])
+            except BaseException as e:  # re-raised on the caller's thread
+                errors.append(e)
+
+        threads = [threading.Thread(target=work, args=(g,), name=f"mgp-dev{self.devices[g]}")
+                   for g in range(len(self.ctxs)) if len(parts[g])]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]
+        out: List = [None] * len(states)
+        refuted: List[int] = []
+        for g, idx in enumerate(parts):
+            if not len(idx):
+                continue
+            sub, sub_ref = results[g]
+            for k, i in enumerate(idx):
+                out[int(i)] = sub[k]
+            refuted.extend(int(idx[k]) for k in sub_ref)
+        return out, sorted(refuted)
+
+    def _check_native(self, ctx, states, parents):
+        """One native front-end batch (mgp_build_states) through mgp_check_batch on `ctx`:
+        GPU witnesses, host refutations overlapped with the GPU; the second witness round
+        for what is left.  -> (results, indices of the refuted states).  A batch whose
+        candidate block would pass `cand_bytes` is split into sub-batches of similar
+        variable counts (the answers do not change: candidates are keyed by content)."""
         from .front import FE_SAT_UNSAFE, Batch
 
         tb = time.perf_counter()
@@ -387,25 +484,17 @@ class Prefilter:
         n_vars = max(1, int(nv.max()) if len(nv) else 1)
         if len(states) > 1 and len(states) * self.n_cand * n_vars * 32 > self.cand_bytes:
             B.close()
-            order = sorted(range(len(states)), key=lambda i: int(nv[i]))
             res: List = [None] * len(states)
-            grp: List[int] = []
-            for i in order + [None]:
-                if i is not None:
-                    w = max(1, int(nv[i]))
-                    if not grp or (len(grp) + 1) * self.n_cand * w * 32 <= self.cand_bytes:
-                        grp.append(i)
-                        continue
-                sub = self._check_native([states[k] for k in grp], None if parents is None else
-                                         [parents[k] for k in grp])
+            refuted: List[int] = []
+            for grp in self._groups(nv, self.n_cand):
+                sub, sub_ref = self._check_native(ctx, [states[k] for k in grp],
+                                                  None if parents is None else [parents[k] for k in grp])
                 for k, r in zip(grp, sub):
                     res[k] = r
-                grp = [i] if i is not None else []
-            return res
-        self._calls += 1
+                refuted.extend(grp[k] for k in sub_ref)
+            return res, sorted(refuted)
         prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
-        first, wit, proven, times = B.check(self.ctx, self.n_cand, self.seed + self._calls, parents,
-                                            refute=self.refute)
+        first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute)
         self.last_times = times
         for k, name in enumerate(("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")):
             prof[name] = float(times[k])
@@ -414,8 +503,8 @@ class Prefilter:
         first[unsafe & (first >= 0)] = -1  # no GPU SAT answer for those (mgp_front.cpp)
         witnesses: Dict[int, object] = {}
         retry = [i for i in range(len(states)) if first[i] == -1 and proven[i] != 1]
-        if retry and self.retry_cand > self.n_cand:
-            self._retry_round(states, retry, n_vars, first, witnesses, prof)
+        if retry and self.retry_cand > 0:
+            self._retry_round(ctx, states, retry, first, witnesses, prof)
         prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["retry_states"] = len(retry)
         tr = time.perf_counter()
@@ -433,136 +522,78 @@ class Prefilter:
                 out.append(("undecided", None))
         B.close()
         prof["results_ms"] = 1e3 * (time.perf_counter() - tr)
-        tr = time.perf_counter()
-        if refuted:
-            _cores.pending.extend(list(states[i]) for i in refuted)
-            if len(_cores.pending) >= self.core_batch:
-                _cores.flush(self._N, background=self.core_async)
-        prof["cores_ms"] = 1e3 * (time.perf_counter() - tr)
+        prof["cores_ms"] = 0.0
         self.last_profile = prof
-        return out
+        return out, refuted
 
     def flush_cores(self) -> None:
         """Shrink the pending refuted constraint lists to cores and store them (waits for
         a background shrink first)."""
         _cores.flush(self._N)
 
-    # witness rounds for the states the first round and the pre-check leave open: a larger
-    # GPU round (candidates generated on the device, domain rows with a new seed), then
-    # host decision rows, which re-run the domain analysis per variable: for the open
-    # states that fit the round's time budget (_within_decide_budget), cheapest first.
-    RETRY_GPU_CAND = 1024
-    # (candidates per state, decision rows) of the host rounds: four rows (draw schedules
-    # 0, 4, 6, 8) find the same witnesses as eight on the mixed corpus at half the cost;
-    # states the budget cannot give four get two (DECIDE_MIN_ROWS)
-    RETRY_SCHEDULE = ((256, 4),)
-    DECIDE_MIN_ROWS = 2
-    DECIDE_MAX = 4096
+    def _groups(self, nv: np.ndarray, n_cand: int) -> List[List[int]]:
+        """Indices grouped by variable count so that each group's candidate block fits cand_bytes."""
+        order = sorted(range(len(nv)), key=lambda i: (int(nv[i]), i))
+        groups: List[List[int]] = []
+        grp: List[int] = []
+        for i in order:
+            w = max(1, int(nv[i]))
+            if grp and (len(grp) + 1) * n_cand * w * 32 > self.cand_bytes:
+                groups.append(grp)
+                grp = []
+            grp.append(i)
+        if grp:
+            groups.append(grp)
+        return groups
 
-    def _retry_round(self, states, retry, n_vars, first, witnesses, prof=None) -> None:
-        from . import dag as D
+    def rows_per_state(self, B) -> np.ndarray:
+        """Decision rows each state of batch B gets: DECIDE_ROWS while variables x nodes x rows
+        stays within decide_max_units, else DECIDE_MIN_ROWS if that fits, else none -- a rule
+        on the state alone, so its answer does not depend on the rest of the batch."""
+        units = np.diff(B.var_off).astype(np.float64) * np.diff(B.node_off).astype(np.float64)
+        rows = np.where(units * self.decide_rows <= self.decide_max_units, self.decide_rows,
+                        np.where(units * self.DECIDE_MIN_ROWS <= self.decide_max_units, self.DECIDE_MIN_ROWS, 0))
+        return rows.astype(np.uint8)
+
+    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None) -> None:
+        """The second witness round for the open states: host decision rows
+        (mgp_decision_rows, each variable fixed in turn and the analysis re-propagated)
+        placed in the first mixture rows of a device-generated round with a new seed."""
         from .front import FE_SAT_UNSAFE, Batch
 
         prof = {} if prof is None else prof
-        t_gpu = time.perf_counter()
-        open_ = list(retry)
-        budget = self.cand_bytes // (len(open_) * n_vars * 32)
-        n2 = min(self.retry_gpu_cand, self.retry_cand, budget) // 64 * 64
-        if n2 > self.n_cand and len(open_) >= self.retry_gpu_min_states:
-            SB = Batch([states[i] for i in open_])
-            f2, w2, _, _ = SB.check(self.ctx, n2, self.seed + 0x9E3779B9 + self._calls)
-            unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
-            left = []
-            for k, i in enumerate(open_):
-                if f2[k] >= 0 and not unsafe[k]:
-                    first[i] = f2[k]
-                    witnesses[i] = SB.witness(k, w2[k])
-                else:
-                    left.append(i)
-            SB.close()
-            open_ = left
-        prof["retry_gpu_ms"] = 1e3 * (time.perf_counter() - t_gpu)   # device retry round
-        prof["retry_gpu_sat"] = len(retry) - len(open_)
-        prof["decide_states"] = 0
+        n2 = max(64, self.retry_cand // 64 * 64)
+        seed2 = (self.seed + 0x7F4A7C15) & (2 ** 64 - 1)
+        SB = Batch([states[i] for i in retry])
+        nv = np.diff(SB.var_off).astype(np.int64)
+        groups = self._groups(nv, n2) if len(retry) * n2 * max(1, int(nv.max())) * 32 > self.cand_bytes \
+            else [list(range(len(retry)))]
+        SB.close()
         t_dec = time.perf_counter()
-        for rnd, (n_cand, n_decide) in enumerate(self.RETRY_SCHEDULE):
-            if not open_ or len(open_) > self.DECIDE_MAX:
-                break
-            open_, rows = self._decide_plan(states, open_, n_decide,
-                                            max(self.decide_budget_ms, self.decide_ms_per_state * len(states)))
-            if not open_:
-                break
-            budget = self.cand_bytes // (len(open_) * n_vars * 32)
-            n2 = min(n_cand, self.retry_cand, budget) // 64 * 64
-            if n2 < 64:
-                break
-            SB = Batch([states[i] for i in open_])
-            sv = max(1, SB.n_vars())
-            sw, sp, _ = self._N.lower(*SB.packed(gpu=True))
-            seed = self.seed + 0x7F4A7C15 * (rnd + 1) + self._calls
-            c2 = self._N.make_candidates(n2, sv, seed, SB.var_off, SB.var_width, SB.hint_off, SB.hints,
-                                         SB.alias_off, SB.aliases, SB.const_off, SB.consts, D._FIXED_LIMBS,
-                                         np.zeros(len(open_), np.uint8), var_kind=SB.var_kind)
-            tg = time.perf_counter()
-            prof["decide_states"] += len(open_)
-            self._N.guided_candidates(*SB.packed(), c2, seed=seed, every=2, n_decide=n_decide, rows_per_state=rows)
-            units = float((np.diff(SB.var_off).astype(np.float64) * np.diff(SB.node_off) * rows).sum())
-            if units > 0:
-                meas = (time.perf_counter() - tg) * 1e6 * self._decide_threads() / units
-                self.decide_us_per_unit = min(1.0, max(0.005, 0.5 * self.decide_us_per_unit + 0.5 * meas))
-            f2, w2 = self.ctx.eval_batch(sw, sp, c2)
-            unsafe = (SB.flags & FE_SAT_UNSAFE) != 0
-            left = []
-            for k, i in enumerate(open_):
+        dec_ms = 0.0
+        found = 0
+        for grp in groups:
+            GB = Batch([states[retry[k]] for k in grp])
+            gv = max(1, GB.n_vars())
+            rps = self.rows_per_state(GB)
+            td = time.perf_counter()
+            rows, mask, _ = self._N.decision_rows(*GB.packed(), gv, seed2, self.decide_rows, rps,
+                                                  state_keys=GB.state_key)
+            dec_ms += 1e3 * (time.perf_counter() - td)
+            f2, w2, _, _ = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
+            unsafe = (GB.flags & FE_SAT_UNSAFE) != 0
+            for k, j in enumerate(grp):
+                i = retry[j]
                 if f2[k] >= 0 and not unsafe[k]:
                     first[i] = f2[k]
-                    witnesses[i] = SB.witness(k, w2[k])
-                else:
-                    left.append(i)
-            SB.close()
-            open_ = left
-        prof["decide_ms"] = 1e3 * (time.perf_counter() - t_dec)      # host decision rows + their GPU round
+                    witnesses[i] = GB.witness(k, w2[k])
+                    found += 1
+            GB.close()
+        prof["decide_host_ms"] = dec_ms
+        prof["decide_ms"] = 1e3 * (time.perf_counter() - t_dec)  # host decision rows + their GPU round
+        prof["decide_states"] = len(retry)
+        prof["retry_sat"] = found
         SolverStatistics().gpu_retry += len(retry)
-
-    DECIDE_US_PER_UNIT = 0.06  # host CPU cost of one decision row, per (variable x DAG node)
-
-    @staticmethod
-    def _decide_threads() -> int:
-        import os
-
-        return max(1, min(16, os.cpu_count() or 1))
-
-    def _decide_plan(self, states, open_, n_decide, budget_ms=None):
-        """-> (open states whose host decision rows fit budget_ms of wall time, sorted; their
-        decision-row counts).  Cheapest first (variables x DAG nodes, one task per state and
-        row over the host threads); a state that does not fit with n_decide rows may still
-        fit with DECIDE_MIN_ROWS."""
-        budget_ms = self.decide_budget_ms if budget_ms is None else budget_ms
-        from .front import Batch
-
-        B = Batch([states[i] for i in open_])
-        units = np.diff(B.var_off).astype(np.float64) * np.diff(B.node_off).astype(np.float64)
-        B.close()
-        threads = Prefilter._decide_threads()
-        us_per_unit = getattr(self, "decide_us_per_unit", self.DECIDE_US_PER_UNIT)
-        lo = min(n_decide, getattr(self, "DECIDE_MIN_ROWS", n_decide))
-        keep: Dict[int, int] = {}
-        cpu_ms, tasks = 0.0, 0
-        for k in np.argsort(units, kind="stable"):
-            for r in (n_decide, lo) if lo < n_decide else (n_decide,):
-                c = units[k] * r * us_per_unit * 1e-3
-                if (cpu_ms + c) / min(threads, tasks + r) <= budget_ms:
-                    keep[open_[int(k)]] = r
-                    cpu_ms += c
-                    tasks += r
-                    break
-        order = sorted(keep)
-        return order, np.array([keep[i] for i in order], dtype=np.uint8)
-
-    def _within_decide_budget(self, states, open_, n_decide, budget_ms=None):
-        """The open states that get all n_decide host decision rows within budget_ms."""
-        keep, rows = self._decide_plan(states, open_, n_decide, budget_ms)
-        return [i for i, r in zip(keep, rows) if r == n_decide]
 
 
 _prefilter: Optional[Prefilter] = None

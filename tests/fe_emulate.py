@@ -1,0 +1,92 @@
+"""CPU emulation of the pre-filter's witness rounds (test infrastructure; uses the C oracle).
+
+The GPU evaluates candidates; here the C oracle does, over exactly the candidates the
+device generator would produce (mgp_make_candidates is bit-identical to it,
+tests/test_gpu_front.py).  Used to study which corpus states stay undecided without a
+GPU:  python -m tests.fe_emulate [n_states]
+"""
+from __future__ import annotations
+
+import collections
+import sys
+import time
+
+import numpy as np
+
+from mythril_amd import _native as N
+from mythril_amd import dag as D
+from mythril_amd import front as F
+from oracle import coracle
+
+
+def host_round(B, n_cand, seed, dom=None, xrows=None):
+    """The candidates mgp_check_batch evaluates (content-keyed device mixture, domain rows,
+    explicit rows in the first mixture rows), evaluated by the C oracle."""
+    nv = max(1, B.n_vars())
+    c = N.make_candidates(n_cand, nv, seed, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off, B.aliases,
+                          B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8),
+                          var_kind=B.var_kind, dom=dom, state_keys=B.state_key)
+    if xrows is not None:
+        apply_xrows(B, c, *xrows)
+    _, _, status = N.lower(*B.packed(gpu=True))
+    f = coracle.first_sat(*B.packed(gpu=True), c)
+    f[status != 0] = -2
+    f[(B.flags & F.FE_SAT_UNSAFE) != 0] = -1
+    return f
+
+
+def apply_xrows(B, cands, rows, mask, first_row=2):
+    """Host restatement of mgp_fe_cands_kernel's explicit rows: mixture row k (candidate
+    first_row + k) takes the masked slots of row k; pinned constants stay."""
+    for s in range(B.n_states):
+        V = B.n_vars(s)
+        kind = B.var_kind[int(B.var_off[s]): int(B.var_off[s + 1])]
+        for k in range(rows.shape[1]):
+            c = first_row + k
+            if c >= cands.shape[1]:
+                break
+            m = mask[s, k, :V].astype(bool) & (kind != 2)
+            cands[s, c, :V][m] = rows[s, k, :V][m]
+            # the slot-width mask of the kernel (decision values are inside their width already)
+    return cands
+
+
+def run(n: int = 1024, seed: int = 0x4D595448, decide_rows: int = 4, n2: int = 256):
+    import corpus
+
+    from mythril_amd import solver as SV
+
+    C = corpus.corpus(n)
+    states = [c[1] for c in C]
+    t = time.time()
+    B = F.Batch(states)
+    ref, dom = N.refute_domains(*B.packed(), B.var_off)
+    f1 = host_round(B, 256, seed, dom=dom)
+    B.close()
+    open_ = [i for i in range(n) if f1[i] < 0 and ref[i] != 1]
+    print(f"first round: sat {int((f1 >= 0).sum())} refuted {int((ref == 1).sum())} open {len(open_)} "
+          f"({time.time() - t:.1f}s)")
+    t = time.time()
+    SB = F.Batch([states[i] for i in open_])
+    seed2 = seed + 0x7F4A7C15
+    fake = type("P", (), {"decide_rows": decide_rows, "decide_max_units": SV.Prefilter.DECIDE_MAX_UNITS,
+                          "DECIDE_MIN_ROWS": SV.Prefilter.DECIDE_MIN_ROWS})()
+    rps = SV.Prefilter.rows_per_state(fake, SB)
+    td = time.time()
+    rows, mask, _ = N.decision_rows(*SB.packed(), max(1, SB.n_vars()), seed2, decide_rows, rps,
+                                    state_keys=SB.state_key)
+    td = time.time() - td
+    _, dom2 = N.refute_domains(*SB.packed(), SB.var_off)
+    f2 = host_round(SB, n2, seed2, dom=dom2, xrows=(rows, mask))
+    SB.close()
+    open2 = [i for k, i in enumerate(open_) if f2[k] < 0]
+    print(f"second round: +{len(open_) - len(open2)} open {len(open2)} (decisions {td:.2f}s, "
+          f"{time.time() - t:.1f}s)")
+    cnt = collections.Counter(C[i][0] for i in open2)
+    for k, v in sorted(cnt.items()):
+        print(f"  {v:4d}  {k}  (expected {next(c[2] for c in C if c[0] == k)})")
+    return open2, C
+
+
+if __name__ == "__main__":
+    run(int(sys.argv[1]) if len(sys.argv) > 1 else 1024)

@@ -1,0 +1,123 @@
+"""Deterministic answers and the second witness round on the GPU.
+
+* explicit (decision) rows land in the device candidates exactly where the host
+  restatement (tests/fe_emulate.apply_xrows) puts them;
+* a state's answer does not depend on its batch: the mixed corpus in two orders, a
+  subset alone, and Prefilter(devices=[0, 0]) (two contexts, two host threads, hash
+  shards by content key) give the same sat / unsat / undecided vector and witnesses;
+* the whole two-round policy on the 1024-state corpus leaves for z3 exactly the states
+  the CPU restatement of the same rounds (C oracle over the same candidates) leaves,
+  at most 20 (>= 50x fewer solver calls), and contradicts no expectation.
+"""
+import collections
+
+import numpy as np
+import pytest
+
+from mythril_amd import _native as N
+from mythril_amd import dag as D
+from mythril_amd import front as F
+from mythril_amd import solver as SV
+
+pytestmark = pytest.mark.gpu
+
+
+def _corpus(n):
+    import corpus
+
+    return corpus.corpus(n)
+
+
+@pytest.fixture()
+def clean():
+    SV.SolverStatistics().reset()
+    SV.unsat_cores().reset()
+    yield
+    SV.unsat_cores().reset()
+
+
+def test_explicit_rows_in_device_candidates(mgp_ctx):
+    from tests.fe_emulate import apply_xrows
+
+    states = [c[1] for c in _corpus(64)]
+    B = F.Batch(states)
+    nv = B.n_vars() + 1
+    rows, mask, _ = N.decision_rows(*B.packed(), nv, 77, 4, None, state_keys=B.state_key)
+    _, dom = N.refute_domains(*B.packed(), B.var_off)
+    for n_cand in (64, 256):
+        dev = B.device_candidates(mgp_ctx, n_cand, nv, 77, dom=dom, xrows=(rows, mask))
+        host = N.make_candidates(n_cand, nv, 77, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off, B.aliases,
+                                 B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8),
+                                 var_kind=B.var_kind, dom=dom, state_keys=B.state_key)
+        apply_xrows(B, host, rows, mask)
+        bad = np.nonzero((dev != host).any(axis=(1, 2, 3)))[0]
+        assert bad.size == 0, f"n_cand={n_cand}: {bad.size} states differ, first {bad[:5]}"
+    B.close()
+
+
+def _kinds(res):
+    return [r[0] for r in res]
+
+
+def _same_answers(a, b):
+    assert _kinds(a) == _kinds(b)
+    for (ka, wa), (kb, wb) in zip(a, b):
+        if ka == SV.sat:
+            assert dict(wa) == dict(wb)
+
+
+def test_answers_do_not_depend_on_the_batch(clean):
+    pf = SV.Prefilter(0)
+    try:
+        cs = [c[1] for c in _corpus(240)]
+        base = pf.check_states(cs)
+        SV.unsat_cores().reset()
+        perm = np.random.default_rng(7).permutation(len(cs))
+        got = pf.check_states([cs[i] for i in perm])
+        _same_answers([base[i] for i in perm], got)
+        SV.unsat_cores().reset()
+        sub = list(range(3, len(cs), 11))
+        _same_answers([base[i] for i in sub], pf.check_states([cs[i] for i in sub]))
+        SV.unsat_cores().reset()
+        _same_answers([base[17]], pf.check_states([cs[17]]))
+    finally:
+        pf.close()
+
+
+def test_two_contexts_answer_like_one(clean):
+    """Prefilter(devices=[0, 0]): two contexts on one GPU, one host thread each, states
+    hash-sharded by content key -- the same answers as Prefilter(0)."""
+    one, two = SV.Prefilter(0), SV.Prefilter(devices=[0, 0])
+    try:
+        cs = [c[1] for c in _corpus(300)]
+        owner = two.shard(cs)
+        assert set(owner.tolist()) == {0, 1}
+        a = one.check_states(cs)
+        SV.unsat_cores().reset()
+        b = two.check_states(cs)
+        _same_answers(a, b)
+    finally:
+        one.close()
+        two.close()
+
+
+def test_corpus_undecided_equals_cpu_restatement(clean):
+    """The 1024-state mixed corpus through the product Prefilter (two rounds, decision rows)
+    leaves exactly the states the CPU restatement of the same rounds leaves."""
+    from tests import fe_emulate
+
+    C = _corpus(1024)
+    pf = SV.Prefilter(0)
+    try:
+        res = pf.check_states([c[1] for c in C])
+    finally:
+        pf.close()
+    kinds = _kinds(res)
+    undecided = [i for i, k in enumerate(kinds) if k == "undecided"]
+    want, _ = fe_emulate.run(1024)
+    assert undecided == sorted(want), (collections.Counter(C[i][0] for i in undecided), len(want))
+    assert len(undecided) <= 20
+    for (lab, _, exp), k in zip(C, kinds):
+        assert not (exp == "unsat" and k == SV.sat) and not (exp == "sat" and k == SV.unsat), lab
+    assert sum(1 for (_, _, e), k in zip(C, kinds) if e == "unsat" and k == SV.unsat) == \
+        sum(1 for _, _, e in C if e == "unsat")

@@ -29,7 +29,7 @@ class NoWitnessContext:
         n = len(po) - 1
         return np.full(n, -1, dtype=np.int32), np.zeros((n, cands.shape[2], 8), dtype=np.uint32)
 
-    def check_batch(self, batch, n_cand, seed, parents=None, refute=True):
+    def check_batch(self, batch, n_cand, seed, parents=None, refute=True, xrows=None):
         """mgp_check_batch without a GPU: no witness; the host pre-check as in the pipeline."""
         self.batches += 1
         n = batch.n_states
@@ -140,12 +140,17 @@ def test_fallback_unsat_feeds_the_cache(fe):
 
 
 class SecondRoundContext(NoWitnessContext):
-    """No witness among the first round's candidates; candidate 0 of the host decision round
-    (host-built candidates) 'satisfies'."""
+    """No witness among the first round's candidates; in the second round (the one that
+    carries host decision rows) the first decision row 'satisfies'."""
 
-    def eval_batch(self, words, po, cands):
-        self.batches += 1
-        return np.zeros(len(po) - 1, dtype=np.int32), np.ascontiguousarray(cands[:, 0])
+    def check_batch(self, batch, n_cand, seed, parents=None, refute=True, xrows=None):
+        f, w, ref, t = super().check_batch(batch, n_cand, seed, parents, refute, xrows)
+        if xrows is None:
+            return f, w, ref, t
+        rows, mask = xrows
+        nv = w.shape[1]
+        w[:, : rows.shape[2]] = rows[:, 0, :nv]
+        return np.where(mask[:, 0].any(axis=1), 0, -1).astype(np.int32), w, ref, t
 
 
 def test_second_candidate_round(fe, monkeypatch):
@@ -155,38 +160,34 @@ def test_second_candidate_round(fe, monkeypatch):
     assert SV.batch_is_possible(items) == [True, False]
     st = SV.SolverStatistics()
     assert st.gpu_retry == 1 and st.gpu_sat == 1 and st.refuted == 1 and fe.calls == 0
-    # the first round (check_batch: no witness from the stub), no device retry round for
-    # one open state (Prefilter.retry_gpu_min_states), then the host decision round
-    # (eval_batch), which the stub satisfies
-    assert SV.Prefilter.RETRY_GPU_CAND == 1024 and [n for n, _ in SV.Prefilter.RETRY_SCHEDULE] == [256]
-    assert SV.prefilter().retry_gpu_min_states > 1 and SV.prefilter().ctx.batches == 2
-    assert set(items[0].witness) == {"rx", "ry"}
+    # the first round (no witness from the stub), then ONE second round for the open state
+    # whose decision rows the stub satisfies
+    assert SV.prefilter().ctx.batches == 2
+    w = items[0].witness
+    assert set(w) == {"rx", "ry"} and w["rx"] < w["ry"]  # decision row 0 is a model of rx < ry
 
 
-def test_host_decisions_keep_to_their_time_budget():
-    """The retry round's host decision rows take the open states cheapest first while the
-    estimated wall time fits Prefilter.decide_budget_ms (one task per state and row); a
-    state that does not fit with all rows may still get DECIDE_MIN_ROWS."""
+def test_decision_rows_per_state_rule():
+    """Decision rows per state depend on the state alone (variables x nodes x rows against
+    Prefilter.decide_max_units), not on a wall-clock budget or on the rest of the batch."""
     import types
 
     import corpus
+    from mythril_amd.front import Batch
     from mythril_amd.keccak import KeccakFunctionManager
 
     kfm = KeccakFunctionManager()
     states = [list(t) for _, t, _ in corpus.wallet_states(0, kfm)[:4]]
     states += [list(corpus.bectoken_states(k, kfm)[1]) for k in range(4)]
-    fake = types.SimpleNamespace(decide_budget_ms=20.0, DECIDE_US_PER_UNIT=SV.Prefilter.DECIDE_US_PER_UNIT,
-                                 decide_us_per_unit=SV.Prefilter.DECIDE_US_PER_UNIT, DECIDE_MIN_ROWS=2)
-    keep, rows = SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)
-    full = [i for i, r in zip(keep, rows) if r == 8]
-    assert set(range(4, 8)) <= set(full)          # the small BECToken states first, all rows
-    assert len(full) < 8 and all(r in (2, 8) for r in rows)
-    fake.decide_budget_ms = 1e9
-    keep, rows = SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)
-    assert keep == list(range(8)) and (rows == 8).all()
-    fake.decide_budget_ms = 0.0
-    assert SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)[0] == []
-    # at 20 ms a WalletLibrary state that does not fit with eight rows still gets two
-    fake.decide_budget_ms = 20.0
-    keep, rows = SV.Prefilter._decide_plan(fake, states, list(range(8)), 8)
-    assert any(i < 4 and r == 2 for i, r in zip(keep, rows))
+    B = Batch(states)
+    units = np.diff(B.var_off).astype(float) * np.diff(B.node_off)
+    fake = types.SimpleNamespace(decide_rows=4, decide_max_units=SV.Prefilter.DECIDE_MAX_UNITS,
+                                 DECIDE_MIN_ROWS=SV.Prefilter.DECIDE_MIN_ROWS)
+    assert (SV.Prefilter.rows_per_state(fake, B) == 4).all()  # the corpus fits the default cap
+    fake.decide_max_units = float(units[4:].max()) * 4      # BECToken fits four, WalletLibrary not
+    r = SV.Prefilter.rows_per_state(fake, B)
+    assert (r[4:] == 4).all() and all(r[i] in (0, 2) for i in range(4))
+    B2 = Batch(states[::-1])  # the same states in another batch order: the same rule per state
+    assert np.array_equal(SV.Prefilter.rows_per_state(fake, B2), r[::-1])
+    B.close()
+    B2.close()

@@ -303,8 +303,11 @@ enum mgp_fe_field {
   MGP_FE_VAR_KEY,       /* uint64_t per slot: name id, kind, UF node, piece (parent matching) */
   MGP_FE_GPU_NODE_OFF,  /* uint64_t, n_states + 1: offsets into GPU_NODES */
   MGP_FE_VAR_TID,       /* int32_t per slot: arena id of the VAR / UF term it stands for (-1 pinned) */
-  MGP_FE_STATE_KEY      /* uint64_t per state: content key (nodes, constants, variable names by
+  MGP_FE_STATE_KEY,     /* uint64_t per state: content key (nodes, constants, variable names by
                            name_hash, not arena ids); candidate streams are keyed by it */
+  MGP_FE_DEC_NODES      /* mgp_node, offsets NODE_OFF: NODES with the GPU program's padded-key
+                           strengthening applied and no pinning -- the formula witness searches
+                           (decision rows, domain rows) aim at; never used for a refutation */
 };
 int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t *t_args, const uint32_t *t_p,
                      uint64_t n_terms, const uint32_t *limbs, uint64_t n_limbs, const int32_t *roots,

@@ -283,24 +283,40 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
     }
     stack.clear();
     stack.emplace_back(root, false);
+    // Rows of dead terms are reused (smt._Arena.release), so an argument's row may come
+    // after its user's; a term being expanded is marked kOpen, and meeting an open term
+    // again below itself is a cycle (malformed input), never a DAG.
+    constexpr uint32_t kOpen = 0xFFFFFFFFu;
     while (!stack.empty()) {
       const auto [t, done] = stack.back();
       stack.pop_back();
-      if (memo.find((uint64_t)t)) continue;
       if (done) {
         const int32_t idx = emit(t);
         memo.put((uint64_t)t, (uint32_t)idx);
         continue;
       }
+      if (const uint32_t *m = memo.find((uint64_t)t)) {
+        if (*m == kOpen) {
+          S.bad = true;
+          return;
+        }
+        continue;
+      }
+      memo.put((uint64_t)t, kOpen);
       stack.emplace_back(t, true);
       for (int i = 2; i >= 0; --i) {
         const int32_t a = A.args[3 * (uint64_t)t + i];
         if (a < 0) continue;
-        if ((uint64_t)a >= A.n_terms || a >= t) {  // arguments are built before their users
+        if ((uint64_t)a >= A.n_terms || a == t) {
           S.bad = true;
           return;
         }
-        if (!memo.find((uint64_t)a)) stack.emplace_back(a, false);
+        const uint32_t *m = memo.find((uint64_t)a);
+        if (m && *m == kOpen) {
+          S.bad = true;
+          return;
+        }
+        if (!m) stack.emplace_back(a, false);
       }
     }
     root_nodes.push_back((int32_t)*memo.find((uint64_t)root));
@@ -529,7 +545,7 @@ void pin_constants(StateOut &S) {
 
 struct mgp_fe_batch {
   uint32_t n_states = 0;
-  std::vector<mgp_node> nodes, gpu_nodes;
+  std::vector<mgp_node> nodes, gpu_nodes, dec_nodes;
   std::vector<uint64_t> node_off, gpu_node_off, const_off, var_off, hint_off, alias_off;
   std::vector<uint32_t> consts, var_width, var_full, var_name, var_aux, hints, aliases;
   std::vector<uint8_t> var_kind, flags;
@@ -660,6 +676,22 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
       std::copy(S.hints[v].begin(), S.hints[v].end(), B->hints.begin() + B->hint_off[v0 + v] * 8);
     B->state_key[s] = state_key_of(S, name_hash, n_names);
   }
+  bool any_ops = false;
+  for (uint32_t s = 0; s < n_states; ++s) any_ops |= !res[s].gpu_ops.empty();
+  if (any_ops) {  // the strengthened formula on the original node indices (decision rows)
+    B->dec_nodes = B->nodes;
+#pragma omp parallel for schedule(static)
+    for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+      const auto &ops = res[s].gpu_ops;
+      for (size_t k = 0; k < ops.size(); k += 2) {
+        mgp_node &nd = B->dec_nodes[B->node_off[s] + ops[k]];
+        nd.op = (uint8_t)ops[k + 1];
+        nd.width = 1;
+        nd.a = nd.b = nd.c = -1;
+        nd.p0 = nd.p1 = 0;
+      }
+    }
+  }
   if (strengthened) {  // some state's GPU program differs: a separate node list and offsets
     B->gpu_node_off.assign(n_states + 1, 0);
     for (uint32_t s = 0; s < n_states; ++s)
@@ -705,6 +737,7 @@ int mgp_fe_get(const mgp_fe_batch *B, int field, const void **ptr, uint64_t *cou
     case MGP_FE_VAR_TID: return set(B->var_tid);
     case MGP_FE_STATE_KEY: return set(B->state_key);
     case MGP_FE_GPU_NODE_OFF: return set(B->gpu_nodes.empty() ? B->node_off : B->gpu_node_off);
+    case MGP_FE_DEC_NODES: return set(B->dec_nodes.empty() ? B->nodes : B->dec_nodes);
     default: return MGP_E_ARG;
   }
 }

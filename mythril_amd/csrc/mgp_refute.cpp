@@ -1482,6 +1482,32 @@ void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64
   // of the host time)
   static const uint8_t kFirst8[8] = {0, 4, 6, 8, 2, 10, 12, 14};
   const uint32_t drow = row < 8u ? kFirst8[row] : row < 16u ? 2u * (row - 8u) + 1u : row;
+  // rows whose decisions start with the Or case split: 1 and 3 (MGP_DECIDE_OR=mask for
+  // A/B; rows 0 and 2 keep the plain schedules, the corpus yield is the same either way)
+  static const uint32_t or_rows = [] {
+    const char *e = getenv("MGP_DECIDE_OR");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : 0xAu;
+  }();
+  if (row < 32u && ((or_rows >> row) & 1u)) {
+    // case split on the disjunctions the root requires: from the root down, a required Or
+    // with both operands open takes its first operand (else its second) before any
+    // variable is drawn, so its domain narrows as if that disjunct were a plain conjunct
+    // (keccak_function_manager.py:158-168: Or(interval condition, concrete-hash matches))
+    for (uint32_t i = d.n; i-- > 0;) {
+      if (d.nd[i].op != MGP_OP_BOR || d.bs[i] != BT) continue;
+      const int32_t a = d.nd[i].a, b = d.nd[i].b;
+      if (a < 0 || b < 0 || d.bs[a] != BB || d.bs[b] != BB) continue;
+      for (int32_t pick : {a, b}) {
+        const size_t mark = undo_log.size();
+        work.clear();
+        if (d.meetb(pick, BT) && d.run_from((uint32_t)pick, budget) == 0) {
+          undo_log.clear();
+          break;
+        }
+        d.rollback(mark);
+      }
+    }
+  }
   for (size_t kk = 0; kk < slot.size(); ++kk) {
     const size_t k = (drow & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
     const uint64_t key = mix64(seed ^ mix64(tag ^ ((uint64_t)c << 12) ^ slot[k]));

@@ -31,7 +31,7 @@ _FIELDS = {
     "var_aux": (9, np.uint32, 1), "var_kind": (10, np.uint8, 1), "hint_off": (11, np.uint64, 1),
     "hints": (12, np.uint32, 8), "alias_off": (13, np.uint64, 1), "aliases": (14, np.uint32, 2),
     "flags": (15, np.uint8, 1), "var_key": (16, np.uint64, 1), "gpu_node_off": (17, np.uint64, 1),
-    "var_tid": (18, np.int32, 1), "state_key": (19, np.uint64, 1),
+    "var_tid": (18, np.int32, 1), "state_key": (19, np.uint64, 1), "dec_nodes": (20, N.NODE_DTYPE, 1),
 }
 _VAR_TABLES = ("var_off", "var_width", "var_full", "var_name", "var_aux", "var_kind", "var_key", "var_tid")
 FIXED_POOL_LIMBS = None  # dag._FIXED_LIMBS (set lazily: dag imports the native module too)
@@ -177,11 +177,16 @@ class Batch:
             pass
 
     # ------------------------------------------------------------ views
-    def packed(self, gpu: bool = False):
+    def packed(self, gpu: bool = False, decide: bool = False):
         """(nodes, node_offsets, consts [n, 8], const_offsets) as dag.pack_states; gpu=True
-        gives the program the GPU evaluates (padded key equalities strengthened)."""
+        gives the program the GPU evaluates (padded key equalities strengthened, excess
+        constants pinned); decide=True the strengthened formula on the original node
+        indices, which witness searches aim at (never refutations: it implies the
+        original formula, not the other way round)."""
         if gpu:
             return self.gpu_nodes, self.gpu_node_off, self.consts, self.const_off
+        if decide:
+            return self.dec_nodes, self.node_off, self.consts, self.const_off
         return self.nodes, self.node_off, self.consts, self.const_off
 
     def n_vars(self, s: Optional[int] = None) -> int:

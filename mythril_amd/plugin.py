@@ -22,7 +22,13 @@ hook:
   to ``window`` states from the strategy, executes them, and prunes all their
   successors in one batch.  For the breadth-first strategy the work-list order
   is exactly the sequential one (successors are appended behind every state
-  already queued); depth-first strategies keep ``window = 1``.
+  already queued, strategy/basic.py:50-61), so BFS -- the CLI's default strategy
+  (interfaces/cli.py:405-410) -- gets ``window = BFS_WINDOW`` unless the caller
+  picks one.  Every other strategy (DFS pops the newest state, basic.py:36-47; the
+  random ones draw from the whole list, basic.py:64-92) would see a different work
+  list with a window, so ``initialize`` forces ``window = 1`` for them.  Strategy
+  extensions (BoundedLoopsStrategy, CoverageStrategy) are looked through via their
+  ``super_strategy``.
 
 Everything the GPU cannot prove satisfiable reaches the fallback solver with
 the reference's own arguments, so the pruning decision is the reference's
@@ -43,14 +49,31 @@ def _constraints_of(global_state):
     return global_state.world_state.constraints
 
 
-class GpuPrefilterPlugin:
-    """The toggle: loading it routes LASER's prune point through the GPU."""
+def is_breadth_first(strategy) -> bool:
+    """Is the strategy (under any extensions wrapping it) BreadthFirstSearchStrategy?"""
+    seen = 0
+    while strategy is not None and seen < 16:
+        if type(strategy).__name__ == "BreadthFirstSearchStrategy":
+            return True
+        strategy = getattr(strategy, "super_strategy", None)
+        seen += 1
+    return False
 
-    def __init__(self, window: int = 1, batch: Callable[[Sequence], List[bool]] = SV.batch_is_possible,
+
+class GpuPrefilterPlugin:
+    """The toggle: loading it routes LASER's prune point through the GPU.
+
+    window=None: BFS_WINDOW states per batch under breadth-first search, 1 otherwise;
+    an explicit window > 1 is honoured only under breadth-first search."""
+
+    BFS_WINDOW = 16
+
+    def __init__(self, window: Optional[int] = None, batch: Callable[[Sequence], List[bool]] = SV.batch_is_possible,
                  constraints_of: Callable = _constraints_of):
-        if window < 1:
+        if window is not None and window < 1:
             raise ValueError("window must be >= 1")
-        self.window = window
+        self.requested_window = window
+        self.window = window or 1
         self._batch = batch
         self._constraints_of = constraints_of
         self.batches = 0
@@ -62,6 +85,13 @@ class GpuPrefilterPlugin:
     # plugins/plugin.py:18-23
     def initialize(self, symbolic_vm) -> None:
         SV.enable_gpu(True)
+        if is_breadth_first(getattr(symbolic_vm, "strategy", None)):
+            self.window = self.requested_window or self.BFS_WINDOW
+        else:
+            if (self.requested_window or 1) > 1:
+                log.warning("GPU pre-filter: window=%d needs breadth-first search; using window=1",
+                            self.requested_window)
+            self.window = 1
         orig_execute = symbolic_vm.execute_state
 
         def execute_state(global_state):
@@ -146,7 +176,7 @@ class PluginFactory:
     """plugin_factory.py:4-41 — one more builder next to the reference's."""
 
     @staticmethod
-    def build_gpu_prefilter_plugin(window: int = 1) -> GpuPrefilterPlugin:
+    def build_gpu_prefilter_plugin(window: Optional[int] = None) -> GpuPrefilterPlugin:
         return GpuPrefilterPlugin(window=window)
 
 

@@ -33,13 +33,16 @@ Annotations = Set[Any]
 
 
 class _Arena:
-    """Flat, append-only table of every term ever built: the native DAG builder
-    (mgp_build_states, csrc/mgp_front.cpp) walks it instead of the Python objects.
+    """Flat table of the live terms: the native DAG builder (mgp_build_states,
+    csrc/mgp_front.cpp) walks it instead of the Python objects.
 
     Per term t: op[t], width[t] (Bool = 0), args[3t..3t+2] (term ids, -1 = none) and
     p[2t], p[2t+1]: VAR (name id, 0), CONST (offset into `limbs`, number of u32 limbs,
     little-endian), EXTRACT (hi, lo), UFAPP / UFINV (function id, function-name id).
-    Names are interned in `names`.  Entries of dead terms stay (about 30 B each).
+    Names are interned in `names`.  The row of a dead term (and a dead constant's limbs)
+    goes to a free list and is reused by the next term (`release`), so the table's size
+    follows the live terms, not every term ever built.  A live term keeps its arguments
+    alive, so no live row ever points at a reused one.
     """
 
     def __init__(self):
@@ -54,6 +57,8 @@ class _Arena:
         # per process): the native front end keys a state's candidates by its content with
         # names folded in by these, not by the interning order of the ids
         self.name_hash = array("Q")
+        self.free: List[int] = []                 # rows of dead terms
+        self.free_limbs: Dict[int, List[int]] = {}  # limb count -> offsets of dead constants' limbs
 
     def intern_name(self, name: str) -> int:
         k = self.name_id.get(name)
@@ -64,25 +69,49 @@ class _Arena:
         return k
 
     def add(self, op: int, width: int, args: Tuple["Term", ...], params: Tuple) -> int:
-        tid = len(self.op)
-        self.op.append(op)
-        self.width.append(width)
         ids = [a.tid for a in args] + [-1, -1, -1]
-        self.args.extend(ids[:3])
         p0 = p1 = 0
         if op == ir.VAR:
             p0 = self.intern_name(str(params[0]))
         elif op == ir.CONST:
             n = max(1, (width + 31) // 32)
-            p0, p1 = len(self.limbs), n
-            self.limbs.frombytes(int(params[0]).to_bytes(4 * n, "little"))
+            limbs = array("I", int(params[0]).to_bytes(4 * n, "little"))
+            spare = self.free_limbs.get(n)
+            if spare:
+                p0 = spare.pop()
+                self.limbs[p0:p0 + n] = limbs
+            else:
+                p0 = len(self.limbs)
+                self.limbs.extend(limbs)
+            p1 = n
         elif op == ir.EXTRACT:
             p0, p1 = params
         elif op in (ir.UFAPP, ir.UFINV):
             p0, p1 = params[0], self.intern_name(str(params[1]))
+        if self.free:
+            tid = self.free.pop()
+            self.op[tid] = op
+            self.width[tid] = width
+            self.args[3 * tid:3 * tid + 3] = array("i", ids[:3])
+            self.p[2 * tid] = p0
+            self.p[2 * tid + 1] = p1
+            return tid
+        tid = len(self.op)
+        self.op.append(op)
+        self.width.append(width)
+        self.args.extend(ids[:3])
         self.p.append(p0)
         self.p.append(p1)
         return tid
+
+    def release(self, tid: int) -> None:
+        """The term of row `tid` is gone: its row (and a constant's limbs) can be reused."""
+        if self.op[tid] == ir.CONST:
+            self.free_limbs.setdefault(self.p[2 * tid + 1], []).append(self.p[2 * tid])
+        self.free.append(tid)
+
+    def live(self) -> int:
+        return len(self.op) - len(self.free)
 
 
 ARENA = _Arena()
@@ -101,6 +130,12 @@ class Term:
         self.params = params
         self._h = hash((op, width, tuple(id(a) for a in args), params))
         self.tid = ARENA.add(op, width, args, params)
+
+    def __del__(self):
+        try:
+            ARENA.release(self.tid)
+        except Exception:  # interpreter shutdown, or a term whose constructor failed
+            pass
 
     def __hash__(self):
         return self._h

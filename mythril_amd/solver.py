@@ -76,6 +76,8 @@ class SolverStatistics(metaclass=_Singleton):
         self.rechecks = 0         # GPU witnesses re-checked by the fallback's evaluator (z3)
         self.recheck_rejects = 0  # ... and rejected (the query then went to the fallback)
         self.not_lowerable = 0    # queries with a construct outside the node set
+        self.refute_rechecks = 0       # host refutations the fallback re-asked (Z3Backend.recheck_refutations)
+        self.refute_disagreements = 0  # ... that it answered sat: a pre-check soundness bug, z3 wins
 
     def __repr__(self):
         return (f"Query count: {self.query_count} \nSolver time: {self.solver_time}\n"
@@ -577,7 +579,7 @@ class Prefilter:
             gv = max(1, GB.n_vars())
             rps = self.rows_per_state(GB)
             td = time.perf_counter()
-            rows, mask, _ = self._N.decision_rows(*GB.packed(), gv, seed2, self.decide_rows, rps,
+            rows, mask, _ = self._N.decision_rows(*GB.packed(decide=True), gv, seed2, self.decide_rows, rps,
                                                   state_keys=GB.state_key)
             dec_ms += 1e3 * (time.perf_counter() - td)
             f2, w2, _, _ = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
@@ -660,6 +662,29 @@ def _recheck(terms: Sequence[Term], witness) -> bool:
     return True
 
 
+def _confirm_refutation(terms: Sequence[Term]) -> Tuple[bool, Optional[Model]]:
+    """-> (refutation stands, model).  A backend that audits refutations
+    (Z3Backend(recheck_refutations=f)) answers for a sampled fraction of them; a `sat`
+    from it overrides the pre-check and is counted as a disagreement."""
+    rc = getattr(get_backend(), "recheck_refutation", None)
+    if rc is None:
+        return True, None
+    r = rc(terms)
+    if r is None:
+        return True, None
+    stats = SolverStatistics()
+    stats.refute_rechecks += 1
+    if r[0] == sat:
+        stats.refute_disagreements += 1
+        _cores.reset()  # cores shrunk by the same pre-check are suspect too
+        import warnings
+
+        warnings.warn("mythril_amd: the fallback solver found a model for a state the host pre-check "
+                      "refuted (mgp_refute soundness bug); using the fallback's answer", RuntimeWarning, stacklevel=3)
+        return False, r[1]
+    return True, None
+
+
 # ------------------------------------------------------------ Solver API
 class BaseSolver:
     def __init__(self):
@@ -700,8 +725,9 @@ class Solver(BaseSolver):
                 self._model = Model([assign])
                 return sat
             if res == unsat:
-                self._model = None
-                return unsat
+                stands, model = _confirm_refutation(self.constraints)
+                self._model = model
+                return unsat if stands else sat
         return self._fallback()
 
     @stat_smt_query
@@ -740,8 +766,11 @@ class Optimize(BaseSolver):
         if pf is not None:
             res, assign = pf.check_states([self.constraints])[0]
             if res == unsat:  # no model exists, whatever the objectives
-                self._model = None
-                return unsat
+                stands, _ = _confirm_refutation(self.constraints)
+                if stands:
+                    self._model = None
+                    return unsat
+                return self._fallback()
             if res == sat and not self._min and not self._max and _recheck(self.constraints, assign):
                 self._model = Model([assign])
                 return sat
@@ -887,7 +916,8 @@ def batch_is_possible(items: Sequence[Constraints]) -> List[bool]:
             c.witness = assign
             continue
         if res == unsat:
-            c._is_possible = False
+            stands, model = _confirm_refutation(t)
+            c._is_possible = not stands
             continue
         s = Solver()
         s.set_timeout(c._default_timeout)

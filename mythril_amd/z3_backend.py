@@ -13,6 +13,14 @@ read the witness assigns is pinned to its value, and z3 must answer sat for the
 original constraints under those pins — an evaluation, not a search.  A witness z3
 rejects is dropped and the query goes to the fallback unchanged.  Terms built by the
 laser.smt mirror (no z3 origin) cannot be re-checked and are reported as such.
+
+``recheck_refutation(terms)`` is the same audit for the UNSAT side: a refutation by
+the host pre-check (mgp_refute) answers unsat with no z3 call, which is a deliberate
+divergence from the reference for states z3 would time out on.  With
+``recheck_refutations=f`` > 0 a deterministic fraction f of the refuted states (every
+state when f = 1) is also put to z3 with the reference's timeout; a z3 `sat` there is a
+pre-check soundness bug, counted in SolverStatistics.refute_disagreements, and z3's
+answer wins.
 """
 from __future__ import annotations
 
@@ -25,13 +33,19 @@ from . import z3_lower
 class Z3Backend(SV.Backend):
     name = "z3"
 
-    def __init__(self, z3=None, recheck_timeout_ms: int = 1000):
+    def __init__(self, z3=None, recheck_timeout_ms: int = 1000, recheck_refutations: float = 0.0,
+                 refutation_timeout_ms: int = 10000):
         if z3 is None:
             import z3  # noqa: F811  (the reference's dependency, requirements.txt:30)
+        if not 0.0 <= recheck_refutations <= 1.0:
+            raise ValueError("recheck_refutations is a fraction in [0, 1]")
         self.z3 = z3
         self.recheck_timeout_ms = recheck_timeout_ms
         self.rechecks = 0
         self.recheck_failures = 0
+        self.recheck_refutations = recheck_refutations
+        self.refutation_timeout_ms = refutation_timeout_ms
+        self._refutations_seen = 0
 
     # ------------------------------------------------------------ helpers
     def _lowering(self) -> Optional[z3_lower.Z3Lowering]:
@@ -139,3 +153,17 @@ class Z3Backend(SV.Backend):
         if not ok:
             self.recheck_failures += 1
         return ok
+
+    def recheck_refutation(self, terms: Sequence) -> Optional[Tuple[str, Optional[SV.Model]]]:
+        """z3's answer for a state the pre-check refuted, for the sampled fraction
+        `recheck_refutations` of them (the k-th refutation is sampled when floor(k f)
+        steps); None when not sampled or not checkable (terms without a z3 origin)."""
+        f = self.recheck_refutations
+        if f <= 0.0:
+            return None
+        k = self._refutations_seen = self._refutations_seen + 1
+        if int(k * f) == int((k - 1) * f):
+            return None
+        if self._exprs(terms) is None:
+            return None
+        return self.check(terms, self.refutation_timeout_ms)

@@ -24,6 +24,7 @@ walker also remembers where every variable and uninterpreted application came fr
 from __future__ import annotations
 
 import sys
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import ir
@@ -52,8 +53,54 @@ class _Array:
         self.parent, self.key, self.val = parent, key, val
 
 
+class TermMap:
+    """term id -> value, for as long as the term lives.
+
+    An entry holds its term weakly: once the term is gone (its arena row may then be
+    reused by a new term, smt._Arena.release) the entry reads as absent and is swept.
+    Sweeps run when the map has doubled since the last one, so a long analysis keeps
+    only the entries of terms that something still holds (amortised O(1) per insert)."""
+
+    def __init__(self):
+        self._d: Dict[int, Tuple["weakref.ref[Term]", object]] = {}
+        self._sweep_at = 4096
+
+    def setdefault(self, term: Term, value) -> None:
+        cur = self._d.get(term.tid)
+        if cur is not None and cur[0]() is term:
+            return
+        self._d[term.tid] = (weakref.ref(term), value)
+        if len(self._d) >= self._sweep_at:
+            self.sweep()
+
+    def sweep(self) -> None:
+        self._d = {k: v for k, v in self._d.items() if v[0]() is not None}
+        self._sweep_at = max(4096, 2 * len(self._d))
+
+    def get(self, tid: int, default=None):
+        cur = self._d.get(tid)
+        if cur is None or cur[0]() is None:
+            return default
+        return cur[1]
+
+    def __getitem__(self, tid: int):
+        cur = self._d.get(tid)
+        if cur is None or cur[0]() is None:
+            raise KeyError(tid)
+        return cur[1]
+
+    def __len__(self) -> int:
+        return len(self._d)
+
+
 class Z3Lowering:
-    """z3 expressions of one z3 module -> mythril_amd.smt terms (memoised by AST id)."""
+    """z3 expressions of one z3 module -> mythril_amd.smt terms (memoised by AST id).
+
+    Memory stays bounded over a long analysis: the AST memo is dropped whenever it
+    passes `max_memo` entries (re-walking an AST gives the same hash-consed terms while
+    they live), and `origin` / `roots` forget a term when it dies (TermMap)."""
+
+    max_memo = 1 << 16
 
     def __init__(self, z3):
         self.z3 = z3
@@ -62,12 +109,16 @@ class Z3Lowering:
         self.funcs: Dict[str, Function] = {}
         # term id -> the z3 expression a variable / uninterpreted application term stands for
         # (a base-array read is (array expr, index expr)), and root term id -> z3 constraint
-        self.origin: Dict[int, object] = {}
-        self.roots: Dict[int, object] = {}
+        self.origin = TermMap()
+        self.roots = TermMap()
 
     # ------------------------------------------------------------------ API
     def lower(self, e) -> Term:
         """One z3 Bool or BitVec expression -> Term (raises Unsupported)."""
+        if len(self.memo) > self.max_memo:
+            self.memo.clear()  # the terms only the memo held die here ...
+            self.origin.sweep()  # ... and so do their map entries (and the z3 ASTs they hold)
+            self.roots.sweep()
         r = self._walk(e)
         if isinstance(r, _Array):
             raise Unsupported("array-valued expression")
@@ -77,7 +128,7 @@ class Z3Lowering:
         out = []
         for e in exprs:
             t = self.lower(e)
-            self.roots.setdefault(t.tid, e)
+            self.roots.setdefault(t, e)
             out.append(t)
         return out
 
@@ -133,7 +184,7 @@ class Z3Lowering:
         else:
             f = a.fn
             r = T.mk(ir.UFAPP, f.range, (idx,), (f.fid, f.name))
-            self.origin.setdefault(r.tid, (a.expr, idx_expr))
+            self.origin.setdefault(r, (a.expr, idx_expr))
         for st in reversed(chain):  # oldest store innermost
             r = T.ite(T.cmp_op(ir.EQ, idx, st.key), st.val, r)
         return r
@@ -156,12 +207,12 @@ class Z3Lowering:
             if not ch:
                 if sk == z3.Z3_BOOL_SORT:
                     v = T.mk(ir.VAR, 1, (), (name,))
-                    self.origin.setdefault(v.tid, e)
+                    self.origin.setdefault(v, e)
                     return T.mk(ir.EQ, T.BOOL, (v, T.const(1, 1)))
                 if sk != z3.Z3_BV_SORT:
                     raise Unsupported(f"constant of sort kind {sk}")
                 v = T.mk(ir.VAR, self._width(e), (), (name,))
-                self.origin.setdefault(v.tid, e)
+                self.origin.setdefault(v, e)
                 return v
             if len(ch) != 1 or isinstance(ch[0], _Array) or ch[0].is_bool or sk != z3.Z3_BV_SORT:
                 raise Unsupported(f"function {name}/{len(ch)}")
@@ -170,7 +221,7 @@ class Z3Lowering:
                 raise Unsupported(f"function {name} used at two signatures")
             op = ir.UFINV if f.inverse_of is not None else ir.UFAPP
             r = T.mk(op, f.range, (ch[0],), (f.fid, f.name))
-            self.origin.setdefault(r.tid, e)
+            self.origin.setdefault(r, e)
             return r
         if kind == "SELECT":
             if not isinstance(ch[0], _Array):

@@ -73,7 +73,7 @@ def run(n: int = 1024, seed: int = 0x4D595448, decide_rows: int = 4, n2: int = 2
                           "DECIDE_MIN_ROWS": SV.Prefilter.DECIDE_MIN_ROWS})()
     rps = SV.Prefilter.rows_per_state(fake, SB)
     td = time.time()
-    rows, mask, _ = N.decision_rows(*SB.packed(), max(1, SB.n_vars()), seed2, decide_rows, rps,
+    rows, mask, _ = N.decision_rows(*SB.packed(decide=True), max(1, SB.n_vars()), seed2, decide_rows, rps,
                                     state_keys=SB.state_key)
     td = time.time() - td
     _, dom2 = N.refute_domains(*SB.packed(), SB.var_off)

@@ -34,7 +34,7 @@ class RefConstraints(list):
 
 
 def test_reference_constraints_through_gpu_with_z3_recheck(mgp_ctx):
-    be = Z3Backend(z3)
+    be = Z3Backend(z3, recheck_refutations=1.0)  # every host refutation is audited by z3
     old = SV.set_backend(be)
     SV.SolverStatistics().reset()
     SV.unsat_cores().reset()
@@ -56,6 +56,7 @@ def test_reference_constraints_through_gpu_with_z3_recheck(mgp_ctx):
         assert res == [True, False, True]
         assert st.gpu_sat == 2 and st.refuted == 1 and st.query_count == 0
         assert st.rechecks == 2 and st.recheck_rejects == 0 and be.rechecks == 2
+        assert st.refute_rechecks == 1 and st.refute_disagreements == 0
         w = items[2].witness
         assert w["sender_9"] in (0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF, 0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE)
         # an unlowerable constraint keeps the whole query on z3 with the original objects

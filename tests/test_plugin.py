@@ -52,8 +52,8 @@ class GS:
         self.tag = tag
 
 
-class BFS:
-    """strategy/basic.py BreadthFirstSearchStrategy: pop(0); empty -> StopIteration."""
+class BreadthFirstSearchStrategy:
+    """strategy/basic.py:50-61: pop(0); empty -> StopIteration."""
 
     def __init__(self, work_list):
         self.work_list = work_list
@@ -61,20 +61,41 @@ class BFS:
     def __iter__(self):
         return self
 
+    def pick(self):
+        return self.work_list.pop(0)
+
     def __next__(self):
         try:
-            return self.work_list.pop(0)
+            return self.pick()
         except IndexError:
             raise StopIteration
+
+
+class DepthFirstSearchStrategy(BreadthFirstSearchStrategy):
+    """strategy/basic.py:36-47: pop()."""
+
+    def pick(self):
+        return self.work_list.pop()
+
+
+class BoundedLoopsStrategy(BreadthFirstSearchStrategy):
+    """strategy/extensions/bounded_loops.py:27-46: wraps a strategy (no loops here)."""
+
+    def __init__(self, super_strategy):
+        self.super_strategy = super_strategy
+        super().__init__(super_strategy.work_list)
+
+    def pick(self):
+        return self.super_strategy.pick()
 
 
 X = [BVS(f"x{i}", 256) for i in range(4)]
 
 
 class FakeLaser:
-    def __init__(self, max_depth=4):
+    def __init__(self, max_depth=4, strategy=BreadthFirstSearchStrategy):
         self.work_list = [GS(0, SV.Constraints([ULT(X[0], BVV(3, 256))]), "r")]
-        self.strategy = BFS(self.work_list)
+        self.strategy = strategy(self.work_list)
         self.total_states = 0
         self.max_depth = max_depth
         self.executed = []
@@ -133,8 +154,8 @@ def brute(monkeypatch):
     SV.set_backend(old)
 
 
-def _run(plugin=None, track_gas=True):
-    vm = FakeLaser()
+def _run(plugin=None, track_gas=True, strategy=BreadthFirstSearchStrategy):
+    vm = FakeLaser(strategy=strategy)
     if plugin is not None:
         P.LaserPluginLoader(vm).load(plugin)
     finals = vm.exec(track_gas=track_gas)
@@ -156,6 +177,32 @@ def test_plugin_prunes_like_reference_cpu(brute, monkeypatch, window):
     assert brute.calls == ref_calls  # same queries, batched
     assert plugin.states_checked == ref_calls
     assert any(not states for _, states in ref_vm.cfg) or ref_vm.total_states < 2 ** 5
+
+
+@pytest.mark.parametrize("window", [None, 1, 16])
+def test_strategy_decides_the_window(brute, monkeypatch, window):
+    """BFS (the CLI default, interfaces/cli.py:405-410) batches BFS_WINDOW states unless told
+    otherwise and keeps the sequential work-list order; DFS (and any strategy that is not
+    breadth-first, under any extension) is forced to window = 1 and runs exactly as the
+    reference's loop."""
+    monkeypatch.setattr(SV, "prefilter", lambda: None)
+    for strategy, want in ((BreadthFirstSearchStrategy, window or P.GpuPrefilterPlugin.BFS_WINDOW),
+                           (DepthFirstSearchStrategy, 1),
+                           (lambda wl: BoundedLoopsStrategy(BreadthFirstSearchStrategy(wl)),
+                            window or P.GpuPrefilterPlugin.BFS_WINDOW),
+                           (lambda wl: BoundedLoopsStrategy(DepthFirstSearchStrategy(wl)), 1)):
+        brute.calls = 0
+        ref_vm, ref_final = _run(strategy=strategy)
+        ref_calls = brute.calls
+        brute.calls = 0
+        plugin = P.PluginFactory.build_gpu_prefilter_plugin(window=window)
+        vm, final = _run(plugin, strategy=strategy)
+        assert plugin.window == want
+        assert vm.executed == ref_vm.executed and vm.cfg == ref_vm.cfg and final == ref_final
+        assert brute.calls == ref_calls
+        if want > 1:
+            assert plugin.batches < plugin.states_checked  # several states' successors per batch
+    assert DepthFirstSearchStrategy([1, 2]).pick() == 2
 
 
 def test_plugin_loader_contract():

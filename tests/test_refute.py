@@ -505,3 +505,74 @@ def test_mul_by_odd_constant_narrows_backward():
     # refuted when a model exists
     assert out[0] == 1 and out[1] == 0
     assert S.eval_root(base, [5, 10, 100], [2])
+
+
+# ------------------------------- soak biased to the round-2/3 multiplication rules
+def _random_mul_dag(rng, w):
+    """Two w-bit variables; products by odd (and some even) constants under EQ and
+    compares, BVMulNoOverflow and its negation, sums of products, plus a little Bool
+    structure: the shapes backward narrowing through multiplication acts on."""
+    nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
+    cl = []
+    m = (1 << w) - 1
+
+    def const(v):
+        cl.append(int(v) & m)
+        nl.append([S.CONST, w, -1, -1, -1, len(cl) - 1, 0])
+        return len(nl) - 1
+
+    vals, bools = [0, 1], []
+    for _ in range(int(rng.integers(3, 9))):
+        k = rng.random()
+        if k < 0.35:  # x * c, c odd 3/4 of the time
+            c = int(rng.integers(0, 1 << w)) | (1 if rng.random() < 0.75 else 0)
+            a = int(rng.choice(vals))
+            nl.append([S.MUL, w, a, const(c), -1, 0, 0] if rng.random() < 0.5 else [S.MUL, w, const(c), a, -1, 0, 0])
+            vals.append(len(nl) - 1)
+        elif k < 0.45:
+            nl.append([[S.ADD, S.SUB, S.XOR][int(rng.integers(3))], w, int(rng.choice(vals)), int(rng.choice(vals)), -1, 0, 0])
+            vals.append(len(nl) - 1)
+        elif k < 0.55:
+            nl.append([S.UMUL_NOOVF, 1, int(rng.choice(vals)), int(rng.choice(vals)), -1, 0, 0])
+            bools.append(len(nl) - 1)
+            if rng.random() < 0.6:
+                nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+                bools.append(len(nl) - 1)
+        else:  # EQ mostly: product == k
+            op = [S.EQ, S.EQ, S.EQ, S.ULT, S.UGT, S.ULE, S.SLT][int(rng.integers(7))]
+            a = int(rng.choice(vals[2:] or vals))
+            b = const(rng.integers(0, 1 << w)) if rng.random() < 0.7 else int(rng.choice(vals))
+            nl.append([op, 1, a, b, -1, 0, 0])
+            bools.append(len(nl) - 1)
+    while len(bools) < 2:
+        nl.append([S.EQ, 1, int(rng.choice(vals)), const(rng.integers(0, 1 << w)), -1, 0, 0])
+        bools.append(len(nl) - 1)
+    root = bools[-1]
+    for b in bools[-4:-1]:
+        nl.append([S.BAND, 1, root, b, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl
+
+
+@pytest.mark.parametrize("w", [4, 6, 8])
+def test_exhaustive_soundness_multiplication_shapes(w):
+    """Every refuted state has no model over ALL 2^(2w) assignments (C oracle), and the
+    product rules really fire: states with `x * odd == k` are refuted in numbers."""
+    rng = np.random.default_rng(0x30DD + w)
+    n = {4: 600, 6: 400, 8: 200}[w]
+    states = [_random_mul_dag(rng, w) for _ in range(n)]
+    verdict = _refute(states)
+    grid = np.array(np.meshgrid(np.arange(1 << w), np.arange(1 << w), indexing="ij")).reshape(2, -1).T
+    cands = np.zeros((1, grid.shape[0], 2, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    refuted = unsat = odd_eq_refuted = 0
+    for (nl, cl), r in zip(states, verdict):
+        assert r in (0, 1)
+        nodes, noff, consts, coff = pack_states([(nl, cl)])
+        has_model = coracle.first_sat(nodes, noff, consts, coff, cands)[0] >= 0
+        unsat += not has_model
+        if r == 1:
+            refuted += 1
+            assert not has_model, "refuted a satisfiable state"
+            odd_eq_refuted += any(x[0] == S.EQ and nl[x[2]][0] == S.MUL for x in nl)
+    assert refuted > n // 3 and odd_eq_refuted > n // 6, (refuted, odd_eq_refuted, unsat)

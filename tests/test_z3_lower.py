@@ -163,3 +163,52 @@ def test_z3_backend_check_and_recheck():
     r, _ = be.check(SV._terms([x == 3, y == 2, z3.ULT(x, y)]), 100)
     assert r == SV.unsat
     B.close()
+
+
+class _AllUnsat:
+    """A pre-filter stand-in that refutes everything (a deliberately unsound pre-check)."""
+
+    def check_states(self, states, parents=None):
+        return [(SV.unsat, None)] * len(states)
+
+
+def test_refutation_audit_counts_disagreements(monkeypatch):
+    """Z3Backend(recheck_refutations=f) puts a deterministic fraction f of the host's
+    refutations to z3; a z3 `sat` is counted as a disagreement and z3's answer wins
+    (VERDICT r2 item 4)."""
+    from mythril_amd.z3_backend import Z3Backend
+
+    x, y = z3.BitVec("ax", 256), z3.BitVec("ay", 256)
+
+    class RC(list):
+        def __init__(self, items):
+            super().__init__(items)
+            self._is_possible, self._default_timeout, self.witness = None, 100, None
+
+    be = Z3Backend(z3, recheck_refutations=1.0)
+    old = SV.set_backend(be)
+    monkeypatch.setattr(SV, "prefilter", lambda: _AllUnsat())
+    try:
+        st = SV.SolverStatistics()
+        st.reset()
+        SV.unsat_cores().reset()
+        items = [RC([x == 3, y == 2, z3.ULT(x, y)]), RC([x == 3, y == 9, z3.ULT(x, y)])]
+        with pytest.warns(RuntimeWarning, match="soundness"):
+            assert SV.batch_is_possible(items) == [False, True]
+        assert st.refute_rechecks == 2 and st.refute_disagreements == 1
+        s = SV.Solver()
+        s.add(x == 1, y == 2)
+        with pytest.warns(RuntimeWarning):
+            assert s.check() == SV.sat  # the refutation is overridden with z3's model
+        assert s.model().raw is not None and st.refute_disagreements == 2
+        # a fraction: every other refutation is audited
+        be.recheck_refutations, be._refutations_seen = 0.5, 0
+        st.reset()
+        SV.batch_is_possible([RC([x == k, y == k + 1, z3.ULT(y, x)]) for k in range(6)])
+        assert st.refute_rechecks == 3 and st.refute_disagreements == 0
+        # off by default
+        assert Z3Backend(z3).recheck_refutation([]) is None
+        with pytest.raises(ValueError):
+            Z3Backend(z3, recheck_refutations=2.0)
+    finally:
+        SV.set_backend(old)

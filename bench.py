@@ -276,6 +276,20 @@ def main():
         log(f"keccak verification: {k_verified}")
         if k_verified["mismatches"]:
             raise RuntimeError(f"keccak digests differ from the oracle: {k_verified}")
+        # A/B: the same passes on the other 64-byte kernel (compiler-allocated HIP vs the
+        # hand-allocated gfx950 one), timed the same way; digests were verified above
+        k_engine = N.set_keccak_engine()
+        other = "hip" if k_engine == "asm" else "asm"
+        N.set_keccak_engine(other)
+        kpass()
+        torch.cuda.synchronize(dev)
+        kevs_o = []
+        for _ in range(ksteps):
+            kpass(kevs_o)
+        torch.cuda.synchronize(dev)
+        N.set_keccak_engine(k_engine)
+        kms_o = float(np.mean([a.elapsed_time(bb) for a, bb in kevs_o]))
+        k_ab = {"engine": other, "launch_ms": kms_o, "hashes_per_s_per_gpu": chunk / (kms_o * 1e-3)}
         k_tops = chunk * KECCAK_OPS_PER_HASH / (kms * 1e-3) / 1e12
         k_gbs = chunk * KECCAK_BYTES_PER_HASH / (kms * 1e-3) / 1e9
         # HBM bytes and issued VALU lane-ops per hash from the committed rocprofv3 PMC run
@@ -286,27 +300,51 @@ def main():
             try:
                 with open(kp) as f:
                     km = json.load(f)
-                if km.get("hbm_bytes_per_hash"):
+                k_kernel = "mgp_keccak64_gfx950" if k_engine == "asm" else "mgp_keccak64_kernel"
+                if km.get("kernel") != k_kernel:  # a profile of the other kernel says nothing here
+                    km = {}
+                if km.get("hbm_bytes_per_hash") and k_traffic is None:
                     k_traffic = km["hbm_bytes_per_hash"] * chunk
                 if km.get("valu_lane_ops_per_hash"):
                     iss = km["valu_lane_ops_per_hash"] * chunk / (kms * 1e-3) / 1e12
                     k_issued = {"lane_ops_per_hash": km["valu_lane_ops_per_hash"], "achieved": iss,
-                                "peak": valu_peak, "unit": "TOP/s", "frac": iss / valu_peak,
+                                "peak": VALU_PEAK_TOPS, "unit": "TOP/s", "frac": iss / VALU_PEAK_TOPS,
+                                "peak_measured": valu_peak, "frac_measured": iss / valu_peak,
                                 "source": km.get("source")}
             except (OSError, ValueError):
                 pass
+        if k_issued is None and k_engine == "asm":
+            # the hand-allocated kernel is straight-line code: every VALU instruction of its
+            # source issues exactly once per wave (one hash per lane)
+            sys.path.insert(0, os.path.join(ROOT, "mythril_amd", "csrc"))
+            import gen_keccak_asm
+
+            n_valu = sum(1 for ln in gen_keccak_asm.kernel_source()[0].split("\n") if ln.strip().startswith("v_"))
+            iss = n_valu * chunk / (kms * 1e-3) / 1e12
+            k_issued = {"lane_ops_per_hash": n_valu, "achieved": iss, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                        "frac": iss / VALU_PEAK_TOPS, "peak_measured": valu_peak, "frac_measured": iss / valu_peak,
+                        "source": "static count of mgp_keccak64_gfx950 (straight-line: each VALU instruction "
+                                  "issues once per wave)"}
         keccak = {
             "metric": "keccak256 hashes/s (64-byte mapping-slot preimages)",
             "value": k_rate,
             "unit": "hashes/s",
             "hashes_per_gpu": nk,
             "ms_per_pass": 1e3 * kel / ksteps,
-            "roofline": {"bound": "valu", "achieved": k_tops, "peak": valu_peak, "unit": "TOP/s",
-                         "frac": k_tops / valu_peak, "traffic": k_traffic,
-                         "ops": f"nominal {KECCAK_OPS_PER_HASH} INT32 ops/hash (SURVEY.md 8d); gfx950 "
-                                "v_bitop3/v_alignbit fold several nominal ops into one instruction, so "
-                                "frac can pass 1 -- valu_issued is the instruction-level figure",
-                         "kernel": "mgp_keccak64_kernel", "launch_ms": kms, "hashes_per_launch": chunk},
+            "engine": k_engine,
+            "kernel": "mgp_keccak64_gfx950" if k_engine == "asm" else "mgp_keccak64_kernel",
+            "ab_other_engine": k_ab,
+            # frac = ISSUED VALU lane-ops (PMC, profiles/keccak_pmc.json) over the spec peak: a
+            # true fraction (<= 1).  The nominal-op rate (7 458 ops/hash) counts
+            # ops that v_bitop3 / v_alignbit fold into one instruction, so it can pass the peak;
+            # it is kept as nominal_achieved / nominal_frac.
+            "roofline": {"bound": "valu", "achieved": k_issued["achieved"] if k_issued else None,
+                         "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                         "frac": k_issued["frac"] if k_issued else None, "traffic": k_traffic,
+                         "ops": "issued VALU lane-ops per hash (PMC SQ_INSTS_VALU x 64) x hashes",
+                         "nominal_achieved": k_tops, "nominal_frac": k_tops / VALU_PEAK_TOPS,
+                         "kernel": "mgp_keccak64_gfx950" if k_engine == "asm" else "mgp_keccak64_kernel",
+                         "launch_ms": kms, "hashes_per_launch": chunk},
             "valu_issued": k_issued,
             "verified": k_verified,
             "roofline_hbm": {"achieved": k_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k_gbs / HBM_PEAK_GBS},
@@ -459,9 +497,11 @@ def main():
                                "first-SAT)",
                 "lds_slots": n_slots, "nominal_ops_per_eval": float(ops_state.mean()),
             },
-            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": valu_peak, "unit": "TOP/s",
-                         "frac": achieved_tops / valu_peak, "traffic": traffic, "peak_derived": VALU_PEAK_TOPS,
-                         "frac_spec": achieved_tops / VALU_PEAK_TOPS,
+            # peak = the spec INT32 VALU peak (MI355X_MICROARCH.md); the box's v_add_u32 probe is
+            # reported beside it (peak_measured / frac_measured)
+            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                         "frac": achieved_tops / VALU_PEAK_TOPS, "traffic": traffic, "peak_measured": valu_peak,
+                         "frac_measured": achieved_tops / valu_peak, "frac_spec": achieved_tops / VALU_PEAK_TOPS,
                          "ops": "nominal INT32 ops of the live DAG nodes (SURVEY.md 8d table) x candidates",
                          "kernel": ENGINE_KERNEL[N.set_eval_engine()] + "(+finalize)", "launch_ms": kern_ms,
                          "evals_per_launch": evals_rank},

@@ -85,6 +85,7 @@ def _bind(lib):
         "mgp_nominal_ops": (ctypes.c_int, [_P, _P, _U32, _P]),
         "mgp_probe_valu_dev": (ctypes.c_int, [_U32, _U32, _P, _P, _P]),
         "mgp_set_eval_engine": (ctypes.c_int, [ctypes.c_int]),
+        "mgp_set_keccak_engine": (ctypes.c_int, [ctypes.c_int]),
         "mgp_set_eval_diag": (ctypes.c_int, [_P]),
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
@@ -149,6 +150,7 @@ EXPORTED_SYMBOLS = (
     "mgp_nominal_ops",
     "mgp_probe_valu_dev",
     "mgp_set_eval_engine",
+    "mgp_set_keccak_engine",
     "mgp_set_eval_diag",
     "mgp_refute",
     "mgp_refute_trace",
@@ -179,6 +181,13 @@ def set_eval_engine(name: Optional[str] = None) -> str:
     """Select the evaluation kernel ('asm' = hand-written gfx950 interpreter, default;
     'hip' = HIP C++ interpreter); returns the engine in use."""
     cur = lib().mgp_set_eval_engine(ENGINES[name] if name else 0)
+    return {v: k for k, v in ENGINES.items()}[cur]
+
+
+def set_keccak_engine(name: Optional[str] = None) -> str:
+    """Select the 64-byte Keccak kernel ('asm' = hand-allocated mgp_keccak64_gfx950,
+    default; 'hip' = compiler-allocated mgp_keccak64_kernel); returns the one in use."""
+    cur = lib().mgp_set_keccak_engine(ENGINES[name] if name else 0)
     return {v: k for k, v in ENGINES.items()}[cur]
 
 

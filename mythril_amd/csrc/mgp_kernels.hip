@@ -1233,6 +1233,19 @@ hipError_t mgp_launch_transpose(const uint32_t *aos, uint32_t *soa, uint32_t n_s
   return hipGetLastError();
 }
 
+static int g_keccak_engine = [] {
+  const char *e = getenv("MGP_KECCAK_ENGINE");
+  return (e && e[0] == 'h') ? MGP_ENGINE_HIP : MGP_ENGINE_ASM;
+}();
+
+extern "C" int mgp_set_keccak_engine(int engine) {
+  if (engine == MGP_ENGINE_HIP || engine == MGP_ENGINE_ASM) g_keccak_engine = engine;
+  return g_keccak_engine;
+}
+
+extern "C" hipError_t mgp_launch_keccak64_asm(const void *in, uint64_t n, uint32_t stride16, void *out,
+                                              hipStream_t st);
+
 hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32_t stride, uint8_t *out,
                              hipStream_t st) {
   if (n == 0) return hipSuccess;
@@ -1248,6 +1261,10 @@ hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32
     const char *e = getenv("MGP_KECCAK_W8");
     return e && e[0] == '1';
   }();
+  // the hand-allocated kernel (gen_keccak_asm.py) unless the compiler-allocated one is
+  // selected (mgp_set_keccak_engine / MGP_KECCAK_ENGINE=hip, A/B)
+  if (fast && g_keccak_engine == MGP_ENGINE_ASM && !w8 && !x2 && n < (1ull << 32))
+    return mgp_launch_keccak64_asm(in, n, stride / 16u, out, st);
   if (fast && w8) {
     hipLaunchKernelGGL(mgp_keccak64w8_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
                        reinterpret_cast<const uint4 *>(in), n, stride / 16u, reinterpret_cast<uint4 *>(out));

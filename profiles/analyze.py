@@ -10,6 +10,9 @@ import sys
 from collections import defaultdict
 
 
+KECCAK64 = ("mgp_keccak64_gfx950", "mgp_keccak64_kernel")  # hand-allocated asm / compiler-allocated HIP
+
+
 def short(name):
     return name.split("(")[0].replace("void ", "").split("<")[0]
 
@@ -30,7 +33,7 @@ def main(d):
     evals, kcalls = [], []
     with open(tr) as f:
         for r in csv.DictReader(f):
-            if short(r["Kernel_Name"]) == "mgp_keccak64_kernel":
+            if short(r["Kernel_Name"]) in KECCAK64:
                 kcalls.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             if short(r["Kernel_Name"]) in ("mgp_eval_kernel", "mgp_eval_gfx950", "mgp_finalize_kernel"):
                 evals.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
@@ -62,12 +65,16 @@ def main(d):
     out.append("\n## PMC counters (summed over dispatches; separate passes)\n")
     traffic = {}
     n_steps = max(1, sum(1 for e in evals if e[2] == "mgp_finalize_kernel"))
-    for k in ("mgp_eval_gfx950", "mgp_eval_kernel", "mgp_keccak64_kernel", "mgp_valu_probe_kernel"):
+    for k in ("mgp_eval_gfx950", "mgp_eval_kernel") + KECCAK64 + ("mgp_valu_probe_kernel",):
         if k not in agg:
             continue
         c = agg[k]
         v, sg, lds, scr = meta[k]
-        out.append(f"### {k}  (VGPR {v}, SGPR {sg}, LDS {lds} B, scratch {scr})\n")
+        # rocprofv3's VGPR_Count decodes the descriptor's granulated count with a granule of 4;
+        # gfx950 allocates arch VGPRs in granules of 8, so the field reads half the allocation
+        # (mgp_eval_gfx950 declares .amdhsa_next_free_vgpr 128 and reads as 64)
+        out.append(f"### {k}  (VGPR {2 * int(float(v))} allocated = rocprof VGPR_Count {v} x 2, SGPR {sg}, "
+                   f"LDS {lds} B, scratch {scr})\n")
         out.append("| counter | value |")
         out.append("|---|---|")
         for n in sorted(c):
@@ -111,7 +118,7 @@ def main(d):
                     der["nominal / 78.64 Tops/s spec peak"] = bl["roofline"]["achieved"] / 78.6432
                 except (OSError, ValueError, KeyError):
                     pass
-        if k == "mgp_keccak64_kernel" and c.get("SQ_WAVES"):
+        if k in KECCAK64 and c.get("SQ_WAVES"):
             # one preimage per lane: per-hash figures are per-wave counts / 64
             ncalls = sum(1 for _ in kcalls)
             traffic[k] = {"valu_lane_ops_per_hash": c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"],
@@ -130,7 +137,7 @@ def main(d):
     # machine-readable traffic figure for bench.py's roofline.traffic (same workload shape only)
     bj = os.path.join(d, "bench_trace.json")
     for k, t in traffic.items():
-        if k == "mgp_keccak64_kernel":
+        if k in KECCAK64:
             t.update({"kernel": k, "source": f"profiles/{os.path.basename(os.path.normpath(d)).replace('prof_', '')}"
                       f"_summary.md (rocprofv3 run {d})"})
             with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "keccak_pmc.json"), "w") as f:

@@ -233,7 +233,28 @@ def test_keccak_lengths_vs_oracle(mgp_ctx, length):
     assert out[5].tobytes() == keccak_py(data[5 * stride:5 * stride + length].tobytes())
 
 
-def test_keccak_mapping_slot_fast_path_vs_oracle(mgp_ctx):
+@pytest.fixture(params=["asm", "hip"])
+def keccak_engine(request):
+    old = N.set_keccak_engine()
+    N.set_keccak_engine(request.param)
+    yield request.param
+    N.set_keccak_engine(old)
+
+
+@pytest.mark.parametrize("n", [1, 63, 255, 257, 1000, 4099])
+def test_keccak64_engines_ragged_counts(mgp_ctx, keccak_engine, n):
+    """The 64-byte fast path on both kernels (hand-allocated mgp_keccak64_gfx950 and the
+    compiler-allocated mgp_keccak64_kernel): counts that leave a partial workgroup, and a
+    stride past the preimage (80 B: 16-B aligned, 16 B of padding per record)."""
+    rng = np.random.default_rng(n)
+    for stride in (64, 80):
+        data = rng.integers(0, 256, size=n * stride, dtype=np.uint8)
+        out = mgp_ctx.keccak256_n(data, n, 64, stride)
+        ref = coracle.keccak256(data, n, 64, stride)
+        assert (out == ref).all(), (keccak_engine, n, stride)
+
+
+def test_keccak_mapping_slot_fast_path_vs_oracle(mgp_ctx, keccak_engine):
     """Config 5: the bench's own preimages -- pad32(addr_i) || pad32(i mod 8)
     from mgp_fill_mapping_preimages_dev -- hashed on the 64-byte fast path (stride 64,
     16-B aligned device buffers: mgp_keccak64_kernel), 65 536 digests bit-exact against the

@@ -46,6 +46,7 @@ SEED = 0x4D595448
 # a wave64 VALU op issues over 2 cycles).  SURVEY.md's 39.3 counts 64 lanes/CU/clk, half the SIMD width;
 # bench.py prices against the v_add_u32 probe (mgp_probe_valu_dev) it measures on the box.
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
+KECCAK_KERNEL = {"asm": "mgp_keccak64_gfx950", "asm_dx": "mgp_keccak64_gfx950_dx", "hip": "mgp_keccak64_kernel"}
 HBM_PEAK_GBS = 8000.0
 KECCAK_OPS_PER_HASH = 7458  # SURVEY.md §8d (310/round x 24 + absorb)
 KECCAK_BYTES_PER_HASH = 96
@@ -279,17 +280,20 @@ def main():
         # A/B: the same passes on the other 64-byte kernel (compiler-allocated HIP vs the
         # hand-allocated gfx950 one), timed the same way; digests were verified above
         k_engine = N.set_keccak_engine()
-        other = "hip" if k_engine == "asm" else "asm"
-        N.set_keccak_engine(other)
-        kpass()
-        torch.cuda.synchronize(dev)
-        kevs_o = []
-        for _ in range(ksteps):
-            kpass(kevs_o)
-        torch.cuda.synchronize(dev)
+        k_ab = {}
+        for other in ("asm", "asm_dx", "hip"):
+            if other == k_engine:
+                continue
+            N.set_keccak_engine(other)
+            kpass()
+            torch.cuda.synchronize(dev)
+            kevs_o = []
+            for _ in range(ksteps):
+                kpass(kevs_o)
+            torch.cuda.synchronize(dev)
+            kms_o = float(np.mean([a.elapsed_time(bb) for a, bb in kevs_o]))
+            k_ab[other] = {"launch_ms": kms_o, "hashes_per_s_per_gpu": chunk / (kms_o * 1e-3)}
         N.set_keccak_engine(k_engine)
-        kms_o = float(np.mean([a.elapsed_time(bb) for a, bb in kevs_o]))
-        k_ab = {"engine": other, "launch_ms": kms_o, "hashes_per_s_per_gpu": chunk / (kms_o * 1e-3)}
         k_tops = chunk * KECCAK_OPS_PER_HASH / (kms * 1e-3) / 1e12
         k_gbs = chunk * KECCAK_BYTES_PER_HASH / (kms * 1e-3) / 1e9
         # HBM bytes and issued VALU lane-ops per hash from the committed rocprofv3 PMC run
@@ -300,8 +304,7 @@ def main():
             try:
                 with open(kp) as f:
                     km = json.load(f)
-                k_kernel = "mgp_keccak64_gfx950" if k_engine == "asm" else "mgp_keccak64_kernel"
-                if km.get("kernel") != k_kernel:  # a profile of the other kernel says nothing here
+                if km.get("kernel") != KECCAK_KERNEL[k_engine]:  # a profile of the other kernel says nothing here
                     km = {}
                 if km.get("hbm_bytes_per_hash") and k_traffic is None:
                     k_traffic = km["hbm_bytes_per_hash"] * chunk
@@ -313,13 +316,15 @@ def main():
                                 "source": km.get("source")}
             except (OSError, ValueError):
                 pass
-        if k_issued is None and k_engine == "asm":
+        if k_issued is None and k_engine != "hip":
             # the hand-allocated kernel is straight-line code: every VALU instruction of its
             # source issues exactly once per wave (one hash per lane)
             sys.path.insert(0, os.path.join(ROOT, "mythril_amd", "csrc"))
             import gen_keccak_asm
 
-            n_valu = sum(1 for ln in gen_keccak_asm.kernel_source()[0].split("\n") if ln.strip().startswith("v_"))
+            theta = dict(gen_keccak_asm.VARIANTS)[KECCAK_KERNEL[k_engine]]
+            n_valu = sum(1 for ln in gen_keccak_asm.generate(theta=theta)[0].split("\n") if ln.strip().startswith("v_"))
+            n_valu += 8  # prologue: index, bound compare, address arithmetic (the digest gather is in the body)
             iss = n_valu * chunk / (kms * 1e-3) / 1e12
             k_issued = {"lane_ops_per_hash": n_valu, "achieved": iss, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                         "frac": iss / VALU_PEAK_TOPS, "peak_measured": valu_peak, "frac_measured": iss / valu_peak,
@@ -332,8 +337,8 @@ def main():
             "hashes_per_gpu": nk,
             "ms_per_pass": 1e3 * kel / ksteps,
             "engine": k_engine,
-            "kernel": "mgp_keccak64_gfx950" if k_engine == "asm" else "mgp_keccak64_kernel",
-            "ab_other_engine": k_ab,
+            "kernel": KECCAK_KERNEL[k_engine],
+            "ab_other_engines": k_ab,
             # frac = ISSUED VALU lane-ops (PMC, profiles/keccak_pmc.json) over the spec peak: a
             # true fraction (<= 1).  The nominal-op rate (7 458 ops/hash) counts
             # ops that v_bitop3 / v_alignbit fold into one instruction, so it can pass the peak;
@@ -343,8 +348,7 @@ def main():
                          "frac": k_issued["frac"] if k_issued else None, "traffic": k_traffic,
                          "ops": "issued VALU lane-ops per hash (PMC SQ_INSTS_VALU x 64) x hashes",
                          "nominal_achieved": k_tops, "nominal_frac": k_tops / VALU_PEAK_TOPS,
-                         "kernel": "mgp_keccak64_gfx950" if k_engine == "asm" else "mgp_keccak64_kernel",
-                         "launch_ms": kms, "hashes_per_launch": chunk},
+                         "kernel": KECCAK_KERNEL[k_engine], "launch_ms": kms, "hashes_per_launch": chunk},
             "valu_issued": k_issued,
             "verified": k_verified,
             "roofline_hbm": {"achieved": k_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": k_gbs / HBM_PEAK_GBS},

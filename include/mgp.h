@@ -119,9 +119,11 @@ int mgp_set_eval_engine(int engine);
 
 /* Keccak kernel of the 64-byte fast path (mgp_keccak256_batch / _dev with len = 64 and a
  * 16-B aligned stride): MGP_ENGINE_ASM = mgp_keccak64_gfx950 (gen_keccak_asm.py, VGPRs
- * placed by bank), default; MGP_ENGINE_HIP = mgp_keccak64_kernel (compiler-allocated).
- * Same digests.  Sets it when `engine` is one of them; returns the current one.
- * MGP_KECCAK_ENGINE=hip|asm sets the initial value. */
+ * placed by bank), default; MGP_ENGINE_ASM_DX = its variant with theta through D[x]
+ * (two-source XORs); MGP_ENGINE_HIP = mgp_keccak64_kernel (compiler-allocated).  Same
+ * digests.  Sets it when `engine` is one of them; returns the current one.
+ * MGP_KECCAK_ENGINE=hip|asm|asm_dx sets the initial value. */
+#define MGP_ENGINE_ASM_DX 3
 int mgp_set_keccak_engine(int engine);
 
 /* Diagnostic only: when d_diag (device memory, 16 B per state x chunk) is non-null the

@@ -184,11 +184,15 @@ def set_eval_engine(name: Optional[str] = None) -> str:
     return {v: k for k, v in ENGINES.items()}[cur]
 
 
+KECCAK_ENGINES = {"hip": 1, "asm": 2, "asm_dx": 3}
+
+
 def set_keccak_engine(name: Optional[str] = None) -> str:
     """Select the 64-byte Keccak kernel ('asm' = hand-allocated mgp_keccak64_gfx950,
-    default; 'hip' = compiler-allocated mgp_keccak64_kernel); returns the one in use."""
-    cur = lib().mgp_set_keccak_engine(ENGINES[name] if name else 0)
-    return {v: k for k, v in ENGINES.items()}[cur]
+    default; 'asm_dx' = its theta-through-D variant; 'hip' = compiler-allocated
+    mgp_keccak64_kernel); returns the one in use."""
+    cur = lib().mgp_set_keccak_engine(KECCAK_ENGINES[name] if name else 0)
+    return {v: k for k, v in KECCAK_ENGINES.items()}[cur]
 
 
 def _ptr(a: Optional[np.ndarray]):

@@ -59,8 +59,12 @@ class Prog:
         return d
 
 
-def build(p: Prog, state: List[List[int]]) -> List[List[int]]:
-    """24 rounds on state[lane][half] (virtual registers); returns the final state."""
+def build(p: Prog, state: List[List[int]], theta: str = "bitop3") -> List[List[int]]:
+    """24 rounds on state[lane][half] (virtual registers); returns the final state.
+    theta="bitop3": E = bitop3(A, C[x-1], R[x]) (one instruction per half-lane, but its
+    three sources cannot always sit in distinct banks); theta="xor": D[x] = C[x-1] ^ R[x]
+    once per column, E = A ^ D (two-source v_xor, bank-insensitive; 10 more instructions
+    per round)."""
     A = state
     for rnd in range(24):
         C = [[0, 0] for _ in range(5)]
@@ -74,9 +78,14 @@ def build(p: Prog, state: List[List[int]]) -> List[List[int]]:
             rl = p.emit("alignbit", (c1[0], c1[1]), 31)   # rotl64 by 1: lo' = lo<<1 | hi>>31
             rh = p.emit("alignbit", (c1[1], c1[0]), 31)   #               hi' = hi<<1 | lo>>31
             R = (rl, rh)
+            if theta == "xor":
+                D = [p.emit("xor", (C[(x + 4) % 5][h], R[h])) for h in range(2)]
             for y in range(5):
                 i = x + 5 * y
-                e = [p.emit("bitop3", (A[i][h], C[(x + 4) % 5][h], R[h]), XOR3) for h in range(2)]
+                if theta == "xor":
+                    e = [p.emit("xor", (A[i][h], D[h])) for h in range(2)]
+                else:
+                    e = [p.emit("bitop3", (A[i][h], C[(x + 4) % 5][h], R[h]), XOR3) for h in range(2)]
                 r = RHO[i]
                 if r == 0:
                     b = e
@@ -150,7 +159,7 @@ def conflicts(p: Prog, phys: Dict[int, int]) -> Tuple[int, int, int]:
     return tot, pair, three
 
 
-def generate(n_phys: int = 100) -> Tuple[str, dict]:
+def generate(n_phys: int = 100, theta: str = "bitop3") -> Tuple[str, dict]:
     p = Prog()
     # inputs: lanes 0..7 from the four loads (v[4:19]), lane 8 lo = 0x01, lane 16 hi =
     # 0x80000000 (pad), every other half 0; constants materialised by v_mov
@@ -167,7 +176,7 @@ def generate(n_phys: int = 100) -> Tuple[str, dict]:
             k = 0x01 if (lane, h) == (8, 0) else 0x80000000 if (lane, h) == (16, 1) else 0
             state[lane][h] = p.emit("mov", (), k)
             movs.append(state[lane][h])
-    out = build(p, state)
+    out = build(p, state, theta)
     phys = allocate(p, pinned, n_phys)
     used = max(phys.values()) + 1
     lines: List[str] = []
@@ -177,6 +186,8 @@ def generate(n_phys: int = 100) -> Tuple[str, dict]:
             lines.append(f"  v_bitop3_b32 v{phys[d]}, {r[0]}, {r[1]}, {r[2]} bitop3:{imm:#x}")
         elif kind == "alignbit":
             lines.append(f"  v_alignbit_b32 v{phys[d]}, {r[0]}, {r[1]}, {imm}")
+        elif kind == "xor":
+            lines.append(f"  v_xor_b32 v{phys[d]}, {r[0]}, {r[1]}")
         elif kind == "xorlit":
             lines.append(f"  v_xor_b32 v{phys[d]}, {imm:#x}, {r[0]}")
         elif kind == "mov":
@@ -186,7 +197,7 @@ def generate(n_phys: int = 100) -> Tuple[str, dict]:
     # digest = lanes 0..3: gathered into v[4:11] (free again: the loads' registers were
     # renamed away in round 0) unless already in place
     dig = [phys[out[l][h]] for l in range(4) for h in range(2)]
-    tmp_base = used  # scratch beyond the program's registers: no overlap with live values
+    tmp_base = (used + 3) // 4 * 4  # beyond the program's registers (no live value), tuple-aligned
     for j, r in enumerate(dig):
         lines.append(f"  v_mov_b32 v{tmp_base + j}, v{r}")
     stats = dict(zip(("bitop3", "shared_pair", "one_bank"), conflicts(p, phys)), vgprs=tmp_base + 8,
@@ -221,15 +232,18 @@ PROLOGUE = """\
 """
 
 
-def kernel_source() -> Tuple[str, dict]:
-    body, st = generate()
+VARIANTS = ((KNAME, "bitop3"), (KNAME + "_dx", "xor"))  # default first; _dx: theta through D (A/B)
+
+
+def _kernel(name: str, theta: str) -> Tuple[str, str, dict]:
+    body, st = generate(theta=theta)
     ob = st["out_base"]
     nv = (st["vgprs"] + 7) // 8 * 8
     epi = (f"  global_store_dwordx4 v[2:3], v[{ob}:{ob + 3}], off\n"
            f"  global_store_dwordx4 v[2:3], v[{ob + 4}:{ob + 7}], off offset:16\n"
-           ".Lkend:\n  s_endpgm\n")
+           f".Lkend_{name}:\n  s_endpgm\n")
     md = "\n".join([
-        "amdhsa.kernels:", "  - .args:",
+        "  - .args:",
         "      - .name: preimages", "        .address_space: global", "        .offset: 0", "        .size: 8",
         "        .value_kind: global_buffer",
         "      - .name: count", "        .offset: 8", "        .size: 8", "        .value_kind: by_value",
@@ -237,20 +251,38 @@ def kernel_source() -> Tuple[str, dict]:
         "      - .name: digests", "        .address_space: global", "        .offset: 24", "        .size: 8",
         "        .value_kind: global_buffer",
         "    .group_segment_fixed_size: 0", "    .kernarg_segment_align: 8", "    .kernarg_segment_size: 32",
-        "    .max_flat_workgroup_size: 256", f"    .name: {KNAME}", "    .private_segment_fixed_size: 0",
-        "    .sgpr_count: 24", f"    .symbol: {KNAME}.kd", f"    .vgpr_count: {nv}", "    .wavefront_size: 64",
-        "amdhsa.target: amdgcn-amd-amdhsa--gfx950", "amdhsa.version:", "  - 1", "  - 2"])
-    src = "\n".join([
-        '.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".text", f".globl {KNAME}", ".p2align 8",
-        f".type {KNAME},@function", f"{KNAME}:", PROLOGUE + body, epi + ".Lkfunc_end:",
-        f".size {KNAME}, .Lkfunc_end-{KNAME}", "", ".rodata", ".p2align 6", f".amdhsa_kernel {KNAME}",
+        "    .max_flat_workgroup_size: 256", f"    .name: {name}", "    .private_segment_fixed_size: 0",
+        "    .sgpr_count: 24", f"    .symbol: {name}.kd", f"    .vgpr_count: {nv}", "    .wavefront_size: 64"])
+    text = "\n".join([
+        f".globl {name}", ".p2align 8", f".type {name},@function", f"{name}:",
+        PROLOGUE.replace(".Lkend", f".Lkend_{name}") + body, epi + f".Lkfunc_end_{name}:",
+        f".size {name}, .Lkfunc_end_{name}-{name}"])
+    desc = "\n".join([
+        ".p2align 6", f".amdhsa_kernel {name}",
         "  .amdhsa_group_segment_fixed_size 0", "  .amdhsa_private_segment_fixed_size 0",
         "  .amdhsa_kernarg_size 32", "  .amdhsa_user_sgpr_count 2", "  .amdhsa_user_sgpr_kernarg_segment_ptr 1",
         "  .amdhsa_system_sgpr_workgroup_id_x 1", "  .amdhsa_system_vgpr_workitem_id 0",
         f"  .amdhsa_next_free_vgpr {nv}", "  .amdhsa_next_free_sgpr 16", f"  .amdhsa_accum_offset {nv}",
-        "  .amdhsa_reserve_vcc 1", ".end_amdhsa_kernel", "", ".amdgpu_metadata", "---", md, "...",
-        ".end_amdgpu_metadata"])
-    return src + "\n", st
+        "  .amdhsa_reserve_vcc 1", ".end_amdhsa_kernel"])
+    return text, desc + "\n" + "", dict(st, metadata=md)
+
+
+def kernel_source() -> Tuple[str, dict]:
+    """Every variant in one code object (one metadata note listing them all); stats of the
+    default variant."""
+    texts, descs, mds, stats = [], [], [], None
+    for name, theta in VARIANTS:
+        t, d, st = _kernel(name, theta)
+        texts.append(t)
+        descs.append(d)
+        mds.append(st.pop("metadata"))
+        stats = stats or st
+    src = "\n".join(['.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', ".text"] + texts +
+                    ["", ".rodata"] + descs +
+                    ["", ".amdgpu_metadata", "---", "amdhsa.kernels:"] + mds +
+                    ["amdhsa.target: amdgcn-amd-amdhsa--gfx950", "amdhsa.version:", "  - 1", "  - 2", "...",
+                     ".end_amdgpu_metadata"])
+    return src + "\n", stats
 
 
 def main():

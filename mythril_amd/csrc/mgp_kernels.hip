@@ -21,6 +21,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 #include <map>
@@ -1235,16 +1236,17 @@ hipError_t mgp_launch_transpose(const uint32_t *aos, uint32_t *soa, uint32_t n_s
 
 static int g_keccak_engine = [] {
   const char *e = getenv("MGP_KECCAK_ENGINE");
-  return (e && e[0] == 'h') ? MGP_ENGINE_HIP : MGP_ENGINE_ASM;
+  return !e ? MGP_ENGINE_ASM : e[0] == 'h' ? MGP_ENGINE_HIP : strcmp(e, "asm_dx") == 0 ? MGP_ENGINE_ASM_DX
+                                                                                        : MGP_ENGINE_ASM;
 }();
 
 extern "C" int mgp_set_keccak_engine(int engine) {
-  if (engine == MGP_ENGINE_HIP || engine == MGP_ENGINE_ASM) g_keccak_engine = engine;
+  if (engine == MGP_ENGINE_HIP || engine == MGP_ENGINE_ASM || engine == MGP_ENGINE_ASM_DX) g_keccak_engine = engine;
   return g_keccak_engine;
 }
 
 extern "C" hipError_t mgp_launch_keccak64_asm(const void *in, uint64_t n, uint32_t stride16, void *out,
-                                              hipStream_t st);
+                                              int variant, hipStream_t st);
 
 hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32_t stride, uint8_t *out,
                              hipStream_t st) {
@@ -1263,8 +1265,8 @@ hipError_t mgp_launch_keccak(const uint8_t *in, uint64_t n, uint32_t len, uint32
   }();
   // the hand-allocated kernel (gen_keccak_asm.py) unless the compiler-allocated one is
   // selected (mgp_set_keccak_engine / MGP_KECCAK_ENGINE=hip, A/B)
-  if (fast && g_keccak_engine == MGP_ENGINE_ASM && !w8 && !x2 && n < (1ull << 32))
-    return mgp_launch_keccak64_asm(in, n, stride / 16u, out, st);
+  if (fast && g_keccak_engine != MGP_ENGINE_HIP && !w8 && !x2 && n < (1ull << 32))
+    return mgp_launch_keccak64_asm(in, n, stride / 16u, out, g_keccak_engine == MGP_ENGINE_ASM_DX ? 1 : 0, st);
   if (fast && w8) {
     hipLaunchKernelGGL(mgp_keccak64w8_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
                        reinterpret_cast<const uint4 *>(in), n, stride / 16u, reinterpret_cast<uint4 *>(out));

@@ -233,7 +233,7 @@ def test_keccak_lengths_vs_oracle(mgp_ctx, length):
     assert out[5].tobytes() == keccak_py(data[5 * stride:5 * stride + length].tobytes())
 
 
-@pytest.fixture(params=["asm", "hip"])
+@pytest.fixture(params=["asm", "asm_dx", "hip"])
 def keccak_engine(request):
     old = N.set_keccak_engine()
     N.set_keccak_engine(request.param)

@@ -95,6 +95,8 @@ def _bind(lib):
         "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32,
                                                _P, _P, _P, _P]),
         "mgp_decision_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _P]),
+        "mgp_decision_rows_dev": (ctypes.c_int, [_P, _P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P,
+                                                 _P]),
         "mgp_refute_domains": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
         "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, _P, _U64,
                                             ctypes.POINTER(_P)]),
@@ -158,6 +160,7 @@ EXPORTED_SYMBOLS = (
     "mgp_guided_candidates_rows",
     "mgp_make_candidates",
     "mgp_decision_rows",
+    "mgp_decision_rows_dev",
     "mgp_refute_domains",
     "mgp_build_states",
     "mgp_fe_get",
@@ -289,8 +292,9 @@ def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hin
 
 def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed: int, n_decide: int,
                   rows_per_state: Optional[np.ndarray] = None, state_keys: Optional[np.ndarray] = None,
-                  max_passes: int = 0):
-    """mgp_decision_rows -> (rows u32 [n, n_decide, n_vars, 8], mask u8 [n, n_decide, n_vars], status i8[n])."""
+                  max_passes: int = 0, ctx: Optional["Context"] = None):
+    """mgp_decision_rows -> (rows u32 [n, n_decide, n_vars, 8], mask u8 [n, n_decide, n_vars], status i8[n]);
+    with `ctx`, mgp_decision_rows_dev: the same rows computed on ctx's GPU."""
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
     node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
     consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
@@ -309,9 +313,16 @@ def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed:
     keys = None if state_keys is None else np.ascontiguousarray(state_keys, dtype=np.uint64)
     if keys is not None and keys.shape != (n_states,):
         raise ValueError("state_keys must hold one entry per state")
-    _check(lib().mgp_decision_rows(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
-                                   max_passes, n_vars, seed & (2 ** 64 - 1), _ptr(keys), n_decide, _ptr(rps),
-                                   _ptr(rows) if rows.size else None, _ptr(mask) if mask.size else None, _ptr(out)))
+    args = (_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets), max_passes, n_vars,
+            seed & (2 ** 64 - 1), _ptr(keys), n_decide, _ptr(rps), _ptr(rows) if rows.size else None,
+            _ptr(mask) if mask.size else None, _ptr(out))
+    if ctx is not None:
+        rc = lib().mgp_decision_rows_dev(ctx._h, *args)
+        if rc != 0:
+            msg = lib().mgp_last_error(ctx._h)
+            raise MgpError(rc, msg.decode() if msg else "")
+    else:
+        _check(lib().mgp_decision_rows(*args))
     return rows, mask, out[:n_states]
 
 

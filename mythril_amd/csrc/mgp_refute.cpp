@@ -34,268 +34,16 @@
 
 #include "../../include/mgp.h"
 #include "mgp_bv.h"
+#include "mgp_domain.h"
 #include "mgp_fe_sample.h"
+
 
 namespace {
 
-using V = U256;
+using namespace mgpd;
 
-// 2^w - 1 for w = 0..256, from a table (the transfer functions build masks constantly)
-struct MaskTable {
-  V m[257];
-  MaskTable() {
-    for (uint32_t w = 0; w <= 256; ++w) m[w] = bv_mask(bv_ones(), w);
-  }
-};
-inline const V &M(uint32_t w) {
-  static const MaskTable t;
-  return t.m[w < 256u ? w : 256u];
-}
-inline bool Z(const V &a) { return bv_is_zero(a); }
-inline bool EQV(const V &a, const V &b) { return bv_eq(a, b); }
-inline bool LT(const V &a, const V &b) { return bv_ult(a, b); }
-inline V AND(const V &a, const V &b) { return bv_and(a, b); }
-inline V OR(const V &a, const V &b) { return bv_or(a, b); }
-inline V XOR(const V &a, const V &b) { return bv_xor(a, b); }
-inline V NOT(const V &a) { return bv_not(a); }
-inline V MIN(const V &a, const V &b) { return LT(a, b) ? a : b; }
-inline V MAX(const V &a, const V &b) { return LT(a, b) ? b : a; }
-inline V SHL(const V &a, uint32_t s) { return s >= 256u ? bv_zero() : bv_shl(a, s); }
-inline V SHR(const V &a, uint32_t s) { return s >= 256u ? bv_zero() : bv_lshr(a, s); }
-inline V BIT(uint32_t i) { return SHL(bv_small(1u), i); }
-inline V ADDV(const V &a, const V &b) { return bv_add(a, b, nullptr); }
-inline V SUBV(const V &a, const V &b) { return bv_sub(a, b, nullptr); }
-inline V ONE() { return bv_small(1u); }
-
-// number of trailing one bits (a known-zero mask's run of low zeros)
-inline uint32_t ctz_ones(const V &z) {
-  uint32_t n = 0;
-  for (int i = 0; i < 8; ++i) {
-    if (z.w[i] == 0xFFFFFFFFu) { n += 32; continue; }
-    return n + (uint32_t)__builtin_ctz(~z.w[i]);
-  }
-  return n;
-}
-
-struct AV {
-  V z, o, lo, hi;
-};
-inline bool same(const AV &a, const AV &b) {
-  return EQV(a.z, b.z) && EQV(a.o, b.o) && EQV(a.lo, b.lo) && EQV(a.hi, b.hi);
-}
-
-AV top(uint32_t w) {
-  AV a;
-  a.z = NOT(M(w));
-  a.o = bv_zero();
-  a.lo = bv_zero();
-  a.hi = M(w);
-  return a;
-}
-AV exact(V v, uint32_t w) {
-  v = bv_mask(v, w);
-  AV a;
-  a.z = NOT(v);
-  a.o = v;
-  a.lo = v;
-  a.hi = v;
-  return a;
-}
-inline bool is_exact(const AV &a) { return EQV(a.lo, a.hi); }
-
-// Re-establish the invariants (bits above w known zero, interval within the
-// bits' range, common high prefix of lo/hi as known bits).  false = empty.
-bool normalize(AV &a, uint32_t w) {
-  const V m = M(w);
-  a.z = OR(a.z, NOT(m));
-  a.o = AND(a.o, m);  // values are taken mod 2^w
-  for (int it = 0; it < 3; ++it) {
-    if (!Z(AND(a.o, a.z))) return false;
-    const V maxb = AND(NOT(a.z), m);
-    if (LT(a.lo, a.o)) a.lo = a.o;
-    if (LT(maxb, a.hi)) a.hi = maxb;
-    if (LT(a.hi, a.lo)) return false;
-    const uint32_t k = bv_bitlen(XOR(a.lo, a.hi));
-    const V pm = AND(NOT(M(k)), m);
-    const V nz = OR(a.z, AND(NOT(a.lo), pm)), no = OR(a.o, AND(a.lo, pm));
-    if (EQV(nz, a.z) && EQV(no, a.o)) break;
-    a.z = nz;
-    a.o = no;
-  }
-  return Z(AND(a.o, a.z));
-}
-
-// ------------------------------------------------------ transfer functions
-// LLVM-style known bits of a + b + carry (carry-in 0 or 1, known)
-void kb_add(const AV &a, const AV &b, uint32_t cin, uint32_t w, V &rz, V &ro) {
-  const V m = M(w);
-  const V c = bv_small(cin);
-  const V psz = AND(ADDV(ADDV(AND(NOT(a.z), m), AND(NOT(b.z), m)), c), m);
-  const V pso = AND(ADDV(ADDV(a.o, b.o), c), m);
-  const V ckz = NOT(XOR(XOR(psz, a.z), b.z));
-  const V cko = XOR(XOR(pso, a.o), b.o);
-  const V known = AND(AND(AND(OR(a.z, a.o), OR(b.z, b.o)), OR(ckz, cko)), m);
-  rz = OR(AND(NOT(psz), known), NOT(m));
-  ro = AND(pso, known);
-}
-
-// (x + y) mod 2^w and whether x + y >= 2^w (x, y < 2^w)
-inline V add_w(const V &x, const V &y, uint32_t w, bool &ovf) {
-  uint32_t c = 0;
-  V s = bv_add(x, y, &c);
-  if (w == 256u) {
-    ovf = c != 0u;
-    return s;
-  }
-  ovf = !Z(AND(s, NOT(M(w))));
-  return bv_mask(s, w);
-}
-
-AV av_not(const AV &a, uint32_t w) {
-  const V m = M(w);
-  AV r;
-  r.z = OR(a.o, NOT(m));
-  r.o = AND(a.z, m);
-  r.lo = SUBV(m, a.hi);
-  r.hi = SUBV(m, a.lo);
-  return r;
-}
-
-AV av_add(const AV &a, const AV &b, uint32_t w) {
-  AV r;
-  kb_add(a, b, 0u, w, r.z, r.o);
-  bool o1, o2;
-  const V s1 = add_w(a.lo, b.lo, w, o1), s2 = add_w(a.hi, b.hi, w, o2);
-  if (o1 == o2) {
-    r.lo = s1;
-    r.hi = s2;
-  } else {
-    r.lo = bv_zero();
-    r.hi = M(w);
-  }
-  return r;
-}
-
-AV av_sub(const AV &a, const AV &b, uint32_t w) {
-  // a - b = a + ~b + 1
-  const AV nb = av_not(b, w);
-  AV r;
-  kb_add(a, nb, 1u, w, r.z, r.o);
-  const bool u1 = LT(a.lo, b.hi), u2 = LT(a.hi, b.lo);
-  if (u1 == u2) {
-    r.lo = bv_mask(SUBV(a.lo, b.hi), w);
-    r.hi = bv_mask(SUBV(a.hi, b.lo), w);
-  } else {
-    r.lo = bv_zero();
-    r.hi = M(w);
-  }
-  return r;
-}
-
-AV av_and(const AV &a, const AV &b, uint32_t w) {
-  AV r = top(w);
-  r.z = OR(a.z, b.z);
-  r.o = AND(a.o, b.o);
-  r.hi = MIN(a.hi, b.hi);
-  return r;
-}
-AV av_or(const AV &a, const AV &b, uint32_t w) {
-  AV r = top(w);
-  r.z = AND(a.z, b.z);
-  r.o = OR(a.o, b.o);
-  r.lo = MAX(a.lo, b.lo);
-  return r;
-}
-AV av_xor(const AV &a, const AV &b, uint32_t w) {
-  AV r = top(w);
-  r.z = OR(AND(a.z, b.z), AND(a.o, b.o));
-  r.o = OR(AND(a.z, b.o), AND(a.o, b.z));
-  (void)w;
-  return r;
-}
-
-AV av_mul(const AV &a, const AV &b, uint32_t w) {
-  AV r = top(w);
-  const uint32_t tz = ctz_ones(a.z) + ctz_ones(b.z);
-  r.z = OR(r.z, M(tz < w ? tz : w));
-  V lo;
-  const V hi = bv_mul_full(a.hi, b.hi, &lo);
-  if (Z(hi) && (w == 256u || Z(AND(lo, NOT(M(w)))))) {
-    r.hi = lo;
-    r.lo = bv_mul(a.lo, b.lo);
-  }
-  return r;
-}
-
-// concrete value of a BV op on exact operands (semantics: include/mgp_ir.h)
-V fold_bv(uint8_t op, uint32_t w, const V &x, const V &y, uint32_t wa) {
-  switch (op) {
-    case MGP_OP_MUL: return bv_mul(x, y);
-    case MGP_OP_UDIV: { V q, r; bv_udivrem(x, y, &q, &r); return Z(y) ? M(w) : q; }
-    case MGP_OP_UREM: { V q, r; bv_udivrem(x, y, &q, &r); return Z(y) ? x : r; }
-    case MGP_OP_SDIV: return bv_sdiv(bv_sext(x, w), bv_sext(y, w));
-    case MGP_OP_SREM: return bv_srem(bv_sext(x, w), bv_sext(y, w));
-    case MGP_OP_SMOD: return bv_smod(bv_sext(x, w), bv_sext(y, w));
-    case MGP_OP_SHL: { const uint32_t s = bv_shift_amount(y); return s >= w ? bv_zero() : SHL(x, s); }
-    case MGP_OP_LSHR: { const uint32_t s = bv_shift_amount(y); return s >= w ? bv_zero() : SHR(x, s); }
-    case MGP_OP_ASHR: {
-      const uint32_t s = bv_shift_amount(y);
-      return bv_ashr(bv_sext(x, w), s >= w ? w : s);
-    }
-    case MGP_OP_SEXT: return bv_sext(x, wa);
-    default: return bv_zero();
-  }
-}
-
-// truth sets: bit0 = may be false, bit1 = may be true
-enum : uint8_t { BF = 1, BT = 2, BB = 3 };
-
-uint8_t dec_ult(const AV &a, const AV &b) {  // a <u b
-  if (LT(a.hi, b.lo)) return BT;
-  if (!LT(a.lo, b.hi)) return BF;
-  return BB;
-}
-uint8_t dec_ule(const AV &a, const AV &b) {  // a <=u b
-  if (!LT(b.lo, a.hi)) return BT;
-  if (LT(b.hi, a.lo)) return BF;
-  return BB;
-}
-uint8_t dec_eq(const AV &a, const AV &b) {
-  if (!Z(OR(AND(a.o, b.z), AND(a.z, b.o))) || LT(a.hi, b.lo) || LT(b.hi, a.lo)) return BF;
-  if (is_exact(a) && is_exact(b)) return BT;  // (and equal, else the test above fired)
-  return BB;
-}
-
-// signed order = unsigned order after flipping the sign bit
-AV flip(const AV &a, uint32_t w) {
-  // the sign bit sits in one limb: swap it between the known-zero and known-one masks and
-  // toggle it in the bounds there (limb-wise; the decision rows call this per signed
-  // compare, e.g. every calldata byte guard)
-  const uint32_t li = (w - 1u) >> 5, sb = 1u << ((w - 1u) & 31u);
-  AV r;
-  for (uint32_t i = 0; i < 8; ++i) {
-    const uint32_t m = bv_limb_mask(w, (int)i);
-    uint32_t z = a.z.w[i], o = a.o.w[i];
-    if (i == li) {
-      const uint32_t zb = z & sb, ob = o & sb;
-      z = (z & ~sb) | ob;
-      o = (o & ~sb) | zb;
-    }
-    r.z.w[i] = z | ~m;
-    r.o.w[i] = o & m;
-  }
-  if ((a.lo.w[li] & sb) == (a.hi.w[li] & sb)) {
-    r.lo = a.lo;
-    r.hi = a.hi;
-    r.lo.w[li] ^= sb;
-    r.hi.w[li] ^= sb;
-  } else {
-    r.lo = bv_zero();
-    r.hi = M(w);
-  }
-  return r;
-}
-
+// A state's DAG with std::vector storage: validated and set up here (host only), then
+// analysed through a view (mgpd::Dom) whose mutable arrays are this state's own.
 struct State {
   const mgp_node *nd;
   std::vector<mgp_node> relaxed;  // nd when the DAG holds wide values (relax_wide)
@@ -309,88 +57,46 @@ struct State {
   std::vector<int32_t> vtie;   // VAR node -> var table entry
   std::vector<AV> vars;
   std::vector<uint32_t> vkey;  // (index << 9) | width
-  // Orderings of operand pairs: every compare node on the same two operand nodes reads
-  // one set of possible unsigned orderings {<, =, >} and one of signed orderings (the "="
-  // bit is shared).  ULT(a,b), ULE(a,b), UGE(b,a), BVSubNoUnderflow(b,a), the Or(ULT, ==)
-  // expansions and EQ all constrain the same set, so `amount <= bal` and
-  // `Not(BVSubNoUnderflow(bal, amount))` contradict each other although neither operand
-  // has a useful range.
-  enum : uint8_t { OLT = 1, OEQ = 2, OGT = 4, OALL = 7 };
-  struct Pair { int32_t x, y; uint8_t u, s; };
   std::vector<Pair> pairs;
   std::vector<int32_t> cmp_pair;  // compare node -> pair index, -1 = none
   std::vector<uint8_t> cmp_dom;   // 0 unsigned, 1 signed, 2 both (EQ)
   std::vector<uint8_t> cmp_t;     // orderings (x vs y) under which the node is true
-  bool changed = false;
-  // decision mode (decision rows only, never a refutation): backward rules may also
-  // narrow to the PREFERRED part of a solution set -- e.g. the non-wrapping preimages of
-  // a product -- because a decision row is only a candidate that the GPU evaluation
-  // checks.  Such narrowing is unsound for a proof, so run()/refute_one never enable it.
-  bool heur = false;
-  // decision rows (mgp_guided_candidates): every change can go to an undo log (a failed
-  // draw rolls back instead of copying the state) and the changed nodes to a work list
-  // (a decision propagates from the decided node, run_from); var-table entries are
-  // listed as kVarBit | entry
-  struct UndoRec {
-    uint8_t kind;  // 0 av, 1 bs, 2 pair, 3 var entry
-    uint32_t idx;
-    AV av;
-    uint8_t b, pu, ps;
-  };
-  static constexpr uint32_t kVarBit = 0x80000000u;
-  std::vector<UndoRec> *undo = nullptr;
-  std::vector<uint32_t> *touched = nullptr;
-  std::vector<uint32_t> uoff, ulist, voff, vlist;  // users of each node; VAR nodes of each entry
-  std::vector<uint8_t> tie_rel;  // nodes tie() reads: compares with a pair, BOR, pair operands
-  // UF congruence (f(a) = f(b) when a = b is known, the Ackermann axiom the lowering's
-  // ITE chains implement, include/mgp_ir.h): the applications of each function with at
-  // most kUfGroup of them, sorted by (op, function); arguments compared on the original
-  // DAG, so a keccak256_512 application whose 512-bit argument was relaxed still meets
-  // the value of an application of the same key (WalletLibrary's m_ownerIndex[sender]
-  // read in tx 2 against the write in tx 1 when both senders are equal)
-  struct UfApp { int32_t node, arg; uint32_t fn; uint8_t op; };
-  static constexpr uint32_t kUfGroup = 48;
   std::vector<UfApp> ufs;
   std::unordered_map<uint64_t, int32_t> pair_of;  // (x << 32 | y), x < y -> pairs index
+  std::vector<uint64_t> pair_keys;                // the same map, sorted (Dom::pair_find)
+  std::vector<int32_t> pair_idx;
+  std::vector<uint32_t> uoff, ulist, voff, vlist;  // users of each node; VAR nodes of each entry
+  std::vector<uint8_t> tie_rel;  // nodes tie() reads: compares with a pair, BOR, pair operands
 
   uint32_t W(int32_t i) const { return nd[i].width; }
 
-  bool meet(int32_t i, const AV &s) {
-    const uint32_t w = nd[i].width;
-    AV t = av[i];
-    t.z = OR(t.z, s.z);
-    t.o = OR(t.o, s.o);
-    t.lo = MAX(t.lo, s.lo);
-    t.hi = MIN(t.hi, s.hi);
-    if (same(t, av[i])) return true;  // s adds nothing (stored values are normalised)
-    if (!normalize(t, w)) return false;
-    if (!same(t, av[i])) {
-      if (undo) undo->push_back(UndoRec{0, (uint32_t)i, av[i], 0, 0, 0});
-      if (touched) touched->push_back((uint32_t)i);
-      av[i] = t;
-      changed = true;
-    }
-    return true;
-  }
-  bool meetb(int32_t i, uint8_t s) {
-    const uint8_t t = bs[i] & s;
-    if (!t) return false;
-    if (t != bs[i]) {
-      if (undo) undo->push_back(UndoRec{1, (uint32_t)i, AV(), bs[i], 0, 0});
-      if (touched) touched->push_back((uint32_t)i);
-      bs[i] = t;
-      changed = true;
-    }
-    return true;
-  }
-  // would meeting s into node i leave it non-empty?
-  bool compatible(int32_t i, const AV &s) const {
-    AV t = av[i];
-    t.z = OR(t.z, s.z);
-    t.o = OR(t.o, s.o);
-    t.lo = MAX(t.lo, s.lo);
-    t.hi = MIN(t.hi, s.hi);
-    return same(t, av[i]) || normalize(t, nd[i].width);
+  Dom view() {
+    Dom d;
+    d.nd = nd;
+    d.orig = orig;
+    d.n = n;
+    d.consts = consts;
+    d.n_consts = n_consts;
+    d.av = av.data();
+    d.bs = bs.data();
+    d.isb = isb.data();
+    d.vtie = vtie.data();
+    d.vars = vars.data();
+    d.pairs = pairs.data();
+    d.n_pairs = (uint32_t)pairs.size();
+    d.cmp_pair = cmp_pair.data();
+    d.cmp_dom = cmp_dom.data();
+    d.cmp_t = cmp_t.data();
+    d.pair_keys = pair_keys.data();
+    d.pair_idx = pair_idx.data();
+    d.ufs = ufs.data();
+    d.n_ufs = (uint32_t)ufs.size();
+    d.uoff = uoff.data();
+    d.ulist = ulist.data();
+    d.voff = voff.data();
+    d.vlist = vlist.data();
+    d.tie_rel = tie_rel.data();
+    return d;
   }
 
   // ------------------------------------------------------------ validate
@@ -516,625 +222,14 @@ struct State {
       i = j;
     }
     ufs.swap(keep);
-  }
-
-  // x and y (nodes of the original DAG) are known to have equal values: the same node,
-  // equal exact values, a pair known equal, or the same operator over operands known
-  // equal (depth-limited)
-  bool arg_equal(int32_t x, int32_t y, int depth) const {
-    if (x == y) return true;
-    if (x < 0 || y < 0) return false;
-    const mgp_node *o = orig ? orig : nd;
-    const mgp_node &a = o[x], &b = o[y];
-    if (a.width != b.width) return false;
-    if (a.width <= MGP_MAX_WIDTH && !isb[x] && !isb[y]) {
-      if (is_exact(av[x]) && is_exact(av[y]) && EQV(av[x].lo, av[y].lo)) return true;
-      const uint64_t pk = x < y ? ((uint64_t)(uint32_t)x << 32) | (uint32_t)y : ((uint64_t)(uint32_t)y << 32) | (uint32_t)x;
-      auto it = pair_of.find(pk);
-      if (it != pair_of.end() && pairs[it->second].u == OEQ) return true;
-    }
-    if (depth == 0 || a.op != b.op || a.p0 != b.p0 || a.p1 != b.p1) return false;
-    switch (a.op) {
-      case MGP_OP_VAR: return true;  // same variable, same width
-      case MGP_OP_CONST: return false;  // different pool entries (narrow ones compared above)
-      case MGP_OP_TRUE: case MGP_OP_FALSE: return true;
-      default: break;
-    }
-    return (a.a < 0 || arg_equal(a.a, b.a, depth - 1)) && (a.b < 0 || arg_equal(a.b, b.b, depth - 1)) &&
-           (a.c < 0 || arg_equal(a.c, b.c, depth - 1));
-  }
-
-  bool set_order(Pair &p, uint8_t dom, uint8_t m) {
-    uint8_t u = p.u, s = p.s;
-    if (dom != 1) u &= m;
-    if (dom != 0) s &= m;
-    const uint8_t eq = (uint8_t)(u & s & OEQ);  // a == b is one fact in both orders
-    u = (uint8_t)((u & ~OEQ) | eq);
-    s = (uint8_t)((s & ~OEQ) | eq);
-    if (u == OEQ) s = OEQ;
-    if (s == OEQ) u = OEQ;
-    if (!u || !s) return false;
-    if (u != p.u || s != p.s) {
-      if (undo) undo->push_back(UndoRec{2, (uint32_t)(&p - pairs.data()), AV(), 0, p.u, p.s});
-      p.u = u;
-      p.s = s;
-      changed = true;
-    }
-    return true;
-  }
-  bool tie() {
-    if (pairs.empty() && ufs.empty()) return true;
-    for (int sweep = 0; sweep < 2; ++sweep)
-      for (uint32_t i = 0; i < n; ++i) {
-        const int32_t pi = cmp_pair[i];
-        if (pi < 0) continue;
-        Pair &p = pairs[pi];
-        const uint8_t t = cmp_t[i], f = (uint8_t)(OALL & ~t);
-        if (bs[i] == BT && !set_order(p, cmp_dom[i], t)) return false;
-        if (bs[i] == BF && !set_order(p, cmp_dom[i], f)) return false;
-        const uint8_t cur = cmp_dom[i] == 1 ? p.s : p.u;
-        if (!meetb((int32_t)i, (uint8_t)(((cur & t) ? BT : 0) | ((cur & f) ? BF : 0)))) return false;
-      }
-    // a true Or of two compares on one operand pair (the Or(ULT, ==) expansion of ULE /
-    // UGE, bitvec_helper.py:53-80) allows only the union of their orderings
-    for (uint32_t i = 0; i < n; ++i) {
-      if (nd[i].op != MGP_OP_BOR || bs[i] != BT) continue;
-      const int32_t a = nd[i].a, b = nd[i].b;
-      const int32_t pa = cmp_pair[a], pb = cmp_pair[b];
-      if (pa < 0 || pa != pb) continue;
-      const uint8_t da = cmp_dom[a], db = cmp_dom[b];
-      if (da != db && da != 2 && db != 2) continue;  // signed with unsigned: no common set
-      const uint8_t dom = da == 2 ? db : da;
-      if (!set_order(pairs[pa], dom, (uint8_t)(cmp_t[a] | cmp_t[b]))) return false;
-    }
-    for (const Pair &p : pairs) {
-      if (p.u == OEQ) {  // known equal: the operands share one value
-        const AV ax = av[p.x], ay = av[p.y];
-        if (!meet(p.x, ay) || !meet(p.y, ax)) return false;
-        continue;
-      }
-      // known unsigned order: x <= y (or x < y) bounds x from above by y.hi and y from
-      // below by x.lo (ULE / UGE arrive as Or(ULT, ==), bitvec_helper.py:53-80, whose
-      // operands the per-node backward pass cannot narrow)
-      const bool le = !(p.u & OGT), ge = !(p.u & OLT);
-      if (le == ge) continue;
-      const int32_t lo_n = le ? p.x : p.y, hi_n = le ? p.y : p.x;  // lo_n <= hi_n
-      const bool strict = (p.u & OEQ) == 0;
-      const uint32_t w = nd[lo_n].width;
-      if (w == 0u || w != nd[hi_n].width) continue;
-      AV a = top(w), b = top(w);
-      a.hi = av[hi_n].hi;
-      b.lo = av[lo_n].lo;
-      if (strict) {
-        if (Z(a.hi) || EQV(b.lo, M(w))) return false;
-        a.hi = SUBV(a.hi, ONE());
-        b.lo = ADDV(b.lo, ONE());
-      }
-      if (!meet(lo_n, a) || !meet(hi_n, b)) return false;
-    }
-    for (size_t i = 0; i < ufs.size(); ++i)
-      for (size_t j = i + 1; j < ufs.size() && ufs[j].fn == ufs[i].fn && ufs[j].op == ufs[i].op; ++j) {
-        if (!arg_equal(ufs[i].arg, ufs[j].arg, 3)) continue;
-        const int32_t x = ufs[i].node, y = ufs[j].node;
-        const AV ax = av[x], ay = av[y];
-        if (!meet(x, ay) || !meet(y, ax)) return false;
-        auto it = pair_of.find(((uint64_t)(uint32_t)std::min(x, y) << 32) | (uint32_t)std::max(x, y));
-        if (it != pair_of.end() && !set_order(pairs[it->second], 2, OEQ)) return false;
-      }
-    return true;
-  }
-
-
-  // --------------------------------------------------------------- forward
-  bool forward(uint32_t i) {
-    const mgp_node &x = nd[i];
-    const uint32_t w = x.width;
-    if (isb[i]) {
-      uint8_t r = BB;
-      switch (x.op) {
-        case MGP_OP_TRUE: r = BT; break;
-        case MGP_OP_FALSE: r = BF; break;
-        case MGP_OP_BNOT: r = (uint8_t)(((bs[x.a] & BF) ? BT : 0) | ((bs[x.a] & BT) ? BF : 0)); break;
-        case MGP_OP_BAND: {
-          const uint8_t a = bs[x.a], b = bs[x.b];
-          r = (uint8_t)((((a & BT) && (b & BT)) ? BT : 0) | (((a & BF) || (b & BF)) ? BF : 0));
-          break;
-        }
-        case MGP_OP_BOR: {
-          const uint8_t a = bs[x.a], b = bs[x.b];
-          r = (uint8_t)((((a & BT) || (b & BT)) ? BT : 0) | (((a & BF) && (b & BF)) ? BF : 0));
-          break;
-        }
-        case MGP_OP_BXOR: case MGP_OP_BEQ: case MGP_OP_EQ:
-          if (x.op == MGP_OP_EQ && !isb[x.a]) {
-            r = dec_eq(av[x.a], av[x.b]);
-          } else {
-            const uint8_t a = bs[x.a], b = bs[x.b];
-            const bool diff = ((a & BT) && (b & BF)) || ((a & BF) && (b & BT));
-            const bool eqp = ((a & BT) && (b & BT)) || ((a & BF) && (b & BF));
-            r = (uint8_t)(x.op == MGP_OP_BXOR ? ((diff ? BT : 0) | (eqp ? BF : 0))
-                                              : ((eqp ? BT : 0) | (diff ? BF : 0)));
-          }
-          break;
-        case MGP_OP_BITE: case MGP_OP_ITE: {
-          const uint8_t c = bs[x.a];
-          r = (uint8_t)(((c & BT) ? bs[x.b] : 0) | ((c & BF) ? bs[x.c] : 0));
-          break;
-        }
-        case MGP_OP_ULT: r = dec_ult(av[x.a], av[x.b]); break;
-        case MGP_OP_ULE: r = dec_ule(av[x.a], av[x.b]); break;
-        case MGP_OP_UGT: r = dec_ult(av[x.b], av[x.a]); break;
-        case MGP_OP_UGE: r = dec_ule(av[x.b], av[x.a]); break;
-        case MGP_OP_SLT: case MGP_OP_SLE: case MGP_OP_SGT: case MGP_OP_SGE: {
-          const uint32_t ow = W(x.a);
-          const AV fa = flip(av[x.a], ow), fb = flip(av[x.b], ow);
-          r = x.op == MGP_OP_SLT ? dec_ult(fa, fb) : x.op == MGP_OP_SLE ? dec_ule(fa, fb)
-            : x.op == MGP_OP_SGT ? dec_ult(fb, fa) : dec_ule(fb, fa);
-          break;
-        }
-        case MGP_OP_UADD_NOOVF: {
-          const uint32_t ow = W(x.a);
-          bool oh, ol;
-          add_w(av[x.a].hi, av[x.b].hi, ow, oh);
-          add_w(av[x.a].lo, av[x.b].lo, ow, ol);
-          r = !oh ? BT : ol ? BF : BB;
-          break;
-        }
-        case MGP_OP_UMUL_NOOVF: {
-          const uint32_t ow = W(x.a);
-          auto ovf = [&](const V &p, const V &q) {
-            V lo;
-            const V hi = bv_mul_full(p, q, &lo);
-            return !Z(hi) || (ow < 256u && !Z(AND(lo, NOT(M(ow)))));
-          };
-          r = !ovf(av[x.a].hi, av[x.b].hi) ? BT : ovf(av[x.a].lo, av[x.b].lo) ? BF : BB;
-          break;
-        }
-        case MGP_OP_USUB_NOUDF: r = dec_ule(av[x.b], av[x.a]); break;
-        default: r = BB;
-      }
-      return meetb((int32_t)i, r);
-    }
-    AV r = top(w);
-    const AV *A = x.a >= 0 ? &av[x.a] : nullptr;
-    const AV *B = x.b >= 0 ? &av[x.b] : nullptr;
-    switch (x.op) {
-      case MGP_OP_VAR: r = vars[vtie[i]]; break;
-      case MGP_OP_CONST: {
-        V c;
-        memcpy(c.w, consts + 8ull * x.p0, 32);
-        r = exact(c, w);
-        break;
-      }
-      case MGP_OP_ADD: r = av_add(*A, *B, w); break;
-      case MGP_OP_SUB: r = av_sub(*A, *B, w); break;
-      case MGP_OP_NEG: r = av_sub(exact(bv_zero(), w), *A, w); break;
-      case MGP_OP_MUL: r = av_mul(*A, *B, w); break;
-      case MGP_OP_AND: r = av_and(*A, *B, w); break;
-      case MGP_OP_OR: r = av_or(*A, *B, w); break;
-      case MGP_OP_XOR: r = av_xor(*A, *B, w); break;
-      case MGP_OP_NOT: r = av_not(*A, w); break;
-      case MGP_OP_UDIV:
-        if (!Z(B->lo)) {  // divisor never 0: quotient monotone in both operands
-          V q1, q2, rr;
-          bv_udivrem(A->lo, B->hi, &q1, &rr);
-          bv_udivrem(A->hi, B->lo, &q2, &rr);
-          r.lo = q1;
-          r.hi = q2;
-        }
-        break;
-      case MGP_OP_UREM:
-        r.hi = A->hi;  // x % y <= x, and x % 0 = x
-        if (!Z(B->lo)) r.hi = MIN(r.hi, SUBV(B->hi, ONE()));
-        if (LT(A->hi, B->lo)) r = *A;  // x < y: x % y = x
-        break;
-      case MGP_OP_SHL: case MGP_OP_LSHR: case MGP_OP_ASHR: {
-        if (is_exact(*B)) {
-          const uint32_t s = bv_shift_amount(B->lo);
-          if (x.op == MGP_OP_SHL) {
-            if (s >= w) { r = exact(bv_zero(), w); break; }
-            r.z = OR(SHL(A->z, s), M(s));
-            r.o = SHL(A->o, s);
-            bool ovf;
-            V t, lo2;
-            t = bv_mul_full(A->hi, BIT(s), &lo2);
-            ovf = !Z(t) || (w < 256u && !Z(AND(lo2, NOT(M(w)))));
-            if (!ovf) {
-              r.lo = SHL(A->lo, s);
-              r.hi = lo2;
-            }
-          } else if (x.op == MGP_OP_LSHR) {
-            if (s >= w) { r = exact(bv_zero(), w); break; }
-            r.z = OR(SHR(AND(A->z, M(w)), s), NOT(M(w - s)));
-            r.o = SHR(A->o, s);
-            r.lo = SHR(A->lo, s);
-            r.hi = SHR(A->hi, s);
-          } else {
-            const uint32_t ss = s >= w ? w - 1u : s;  // shifting by >= w-1 leaves only sign copies
-            const V sb = BIT(w - 1u), m = M(w);
-            const bool s0 = !Z(AND(A->z, sb)), s1 = !Z(AND(A->o, sb));
-            const V zs = OR(AND(A->z, m), s0 ? NOT(m) : bv_zero());
-            const V os = OR(AND(A->o, m), s1 ? NOT(m) : bv_zero());
-            r.z = OR(bv_shr_fill(zs, ss, s0 ? 0xFFFFFFFFu : 0u), NOT(m));
-            r.o = AND(bv_shr_fill(os, ss, s1 ? 0xFFFFFFFFu : 0u), m);
-          }
-        } else if (x.op != MGP_OP_ASHR) {
-          const uint32_t slo = bv_shift_amount(B->lo);
-          if (slo >= w) {
-            r = exact(bv_zero(), w);
-          } else if (x.op == MGP_OP_LSHR) {  // monotone: up in x, down in s
-            const uint32_t shi = bv_shift_amount(B->hi);
-            r.hi = SHR(A->hi, slo);
-            r.lo = shi >= w ? bv_zero() : SHR(A->lo, shi);
-          } else {  // shl: at least min(s) low zero bits
-            r.z = OR(r.z, M(slo));
-          }
-        }
-        break;
-      }
-      case MGP_OP_EXTRACT: {
-        const uint32_t lo = x.p1, hiw = lo + w;
-        r.z = OR(SHR(A->z, lo), NOT(M(w)));
-        r.o = AND(SHR(A->o, lo), M(w));
-        if (EQV(SHR(A->lo, hiw), SHR(A->hi, hiw))) {  // same prefix above the field: monotone
-          r.lo = AND(SHR(A->lo, lo), M(w));
-          r.hi = AND(SHR(A->hi, lo), M(w));
-        }
-        break;
-      }
-      case MGP_OP_CONCAT: {
-        const uint32_t wb = W(x.b);
-        r.z = OR(SHL(A->z, wb), AND(B->z, M(wb)));
-        r.o = OR(SHL(A->o, wb), B->o);
-        r.lo = OR(SHL(A->lo, wb), B->lo);
-        r.hi = OR(SHL(A->hi, wb), B->hi);
-        break;
-      }
-      case MGP_OP_ZEXT: r.z = OR(A->z, NOT(M(W(x.a)))); r.o = A->o; r.lo = A->lo; r.hi = A->hi; break;
-      case MGP_OP_SEXT: {
-        const uint32_t wa = W(x.a);
-        const V sb = BIT(wa - 1u), ext = AND(NOT(M(wa)), M(w));
-        const bool s0 = !Z(AND(A->z, sb)), s1 = !Z(AND(A->o, sb));
-        r.z = OR(AND(A->z, M(wa)), s0 ? NOT(M(wa)) : NOT(M(w)));
-        r.o = OR(A->o, s1 ? ext : bv_zero());
-        if (s0) { r.lo = A->lo; r.hi = A->hi; }
-        if (s1) { r.lo = OR(A->lo, ext); r.hi = OR(A->hi, ext); }
-        break;
-      }
-      case MGP_OP_ITE: {
-        const uint8_t c = bs[x.a];
-        const AV &b = av[x.b], &e = av[x.c];
-        if (c == BT) r = b;
-        else if (c == BF) r = e;
-        else {
-          r.z = AND(b.z, e.z);
-          r.o = AND(b.o, e.o);
-          r.lo = MIN(b.lo, e.lo);
-          r.hi = MAX(b.hi, e.hi);
-        }
-        break;
-      }
-      default: break;  // UFAPP / UFINV / SDIV / SREM / SMOD: unconstrained unless folded
-    }
-    // exact operands: fold the ops whose transfer above is coarse
-    const bool two = x.op >= MGP_OP_MUL && x.op <= MGP_OP_ASHR && x.op != MGP_OP_AND && x.op != MGP_OP_OR &&
-                     x.op != MGP_OP_XOR && x.op != MGP_OP_NOT && x.op != MGP_OP_NEG;
-    if (two && is_exact(*A) && is_exact(*B)) r = exact(fold_bv(x.op, w, A->lo, B->lo, 0), w);
-    if (x.op == MGP_OP_SEXT && is_exact(*A)) r = exact(fold_bv(x.op, w, A->lo, bv_zero(), W(x.a)), w);
-    return meet((int32_t)i, r);
-  }
-
-  // -------------------------------------------------------------- backward
-  bool narrow_ult(int32_t a, int32_t b, bool strict) {  // require a < b (strict) or a <= b
-    const AV A = av[a], B = av[b];
-    AV ta = top(W(a)), tb = top(W(b));
-    if (strict) {
-      if (Z(B.hi) || EQV(A.lo, M(W(a)))) return false;
-      ta.hi = SUBV(B.hi, ONE());
-      tb.lo = ADDV(A.lo, ONE());
-    } else {
-      ta.hi = B.hi;
-      tb.lo = A.lo;
-    }
-    return meet(a, ta) && meet(b, tb);
-  }
-  // signed: the same on flipped images, mapped back
-  bool narrow_slt(int32_t a, int32_t b, bool strict) {
-    const uint32_t w = W(a);
-    AV fa = flip(av[a], w), fb = flip(av[b], w);
-    if (strict) {
-      if (Z(fb.hi) || EQV(fa.lo, M(w))) return false;
-      fa.hi = MIN(fa.hi, SUBV(fb.hi, ONE()));
-      fb.lo = MAX(fb.lo, ADDV(fa.lo, ONE()));
-    } else {
-      fa.hi = MIN(fa.hi, fb.hi);
-      fb.lo = MAX(fb.lo, fa.lo);
-    }
-    if (!normalize(fa, w) || !normalize(fb, w)) return false;
-    return meet(a, flip(fa, w)) && meet(b, flip(fb, w));
-  }
-
-  bool backward(uint32_t i) {
-    const mgp_node &x = nd[i];
-    if (isb[i]) {
-      const uint8_t r = bs[i];
-      switch (x.op) {
-        case MGP_OP_BNOT: return meetb(x.a, (uint8_t)(((r & BF) ? BT : 0) | ((r & BT) ? BF : 0)));
-        case MGP_OP_BAND:
-          if (r == BT) return meetb(x.a, BT) && meetb(x.b, BT);
-          if (r == BF) {
-            if (bs[x.a] == BT && !meetb(x.b, BF)) return false;
-            if (bs[x.b] == BT && !meetb(x.a, BF)) return false;
-          }
-          return true;
-        case MGP_OP_BOR:
-          if (r == BF) return meetb(x.a, BF) && meetb(x.b, BF);
-          if (r == BT) {
-            if (bs[x.a] == BF && !meetb(x.b, BT)) return false;
-            if (bs[x.b] == BF && !meetb(x.a, BT)) return false;
-          }
-          return true;
-        case MGP_OP_BITE: case MGP_OP_ITE:
-          if (bs[x.a] == BT) return meetb(x.b, r);
-          if (bs[x.a] == BF) return meetb(x.c, r);
-          if (!(bs[x.b] & r) && !meetb(x.a, BF)) return false;
-          if (!(bs[x.c] & r) && !meetb(x.a, BT)) return false;
-          return true;
-        default: break;
-      }
-      if (r == BB) return true;
-      const bool T = r == BT;
-      if ((x.op == MGP_OP_EQ && isb[x.a]) || x.op == MGP_OP_BEQ || x.op == MGP_OP_BXOR) {
-        const bool same_req = (x.op == MGP_OP_BXOR) ? !T : T;
-        auto other = [&](uint8_t v) -> uint8_t {
-          return same_req ? v : (uint8_t)(((v & BF) ? BT : 0) | ((v & BT) ? BF : 0));
-        };
-        if ((bs[x.a] == BT || bs[x.a] == BF) && !meetb(x.b, other(bs[x.a]))) return false;
-        if ((bs[x.b] == BT || bs[x.b] == BF) && !meetb(x.a, other(bs[x.b]))) return false;
-        return true;
-      }
-      switch (x.op) {
-        case MGP_OP_EQ:
-          if (T) {
-            const AV A = av[x.a], B = av[x.b];
-            return meet(x.a, B) && meet(x.b, A);
-          } else {  // a != b: an exact side trims the other's interval ends
-            for (int k = 0; k < 2; ++k) {
-              const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
-              if (!is_exact(av[q])) continue;
-              AV t = av[p];
-              if (EQV(t.lo, av[q].lo)) {
-                if (is_exact(t)) return false;
-                t.lo = ADDV(t.lo, ONE());
-              }
-              if (EQV(t.hi, av[q].lo)) t.hi = SUBV(t.hi, ONE());
-              if (!meet(p, t)) return false;
-            }
-            return true;
-          }
-        case MGP_OP_ULT: return T ? narrow_ult(x.a, x.b, true) : narrow_ult(x.b, x.a, false);
-        case MGP_OP_ULE: return T ? narrow_ult(x.a, x.b, false) : narrow_ult(x.b, x.a, true);
-        case MGP_OP_UGT: return T ? narrow_ult(x.b, x.a, true) : narrow_ult(x.a, x.b, false);
-        case MGP_OP_UGE: return T ? narrow_ult(x.b, x.a, false) : narrow_ult(x.a, x.b, true);
-        case MGP_OP_SLT: return T ? narrow_slt(x.a, x.b, true) : narrow_slt(x.b, x.a, false);
-        case MGP_OP_SLE: return T ? narrow_slt(x.a, x.b, false) : narrow_slt(x.b, x.a, true);
-        case MGP_OP_SGT: return T ? narrow_slt(x.b, x.a, true) : narrow_slt(x.a, x.b, false);
-        case MGP_OP_SGE: return T ? narrow_slt(x.b, x.a, false) : narrow_slt(x.a, x.b, true);
-        case MGP_OP_USUB_NOUDF: return T ? narrow_ult(x.b, x.a, false) : narrow_ult(x.a, x.b, true);
-        case MGP_OP_UADD_NOOVF: {
-          const uint32_t ow = W(x.a);
-          const V m = M(ow);
-          const AV A = av[x.a], B = av[x.b];
-          AV ta = top(ow), tb = top(ow);
-          if (T) {  // a + b < 2^w
-            ta.hi = SUBV(m, B.lo);
-            tb.hi = SUBV(m, A.lo);
-          } else {  // a + b >= 2^w
-            if (Z(A.hi) || Z(B.hi)) return false;
-            ta.lo = bv_mask(ADDV(SUBV(m, B.hi), ONE()), ow);
-            tb.lo = bv_mask(ADDV(SUBV(m, A.hi), ONE()), ow);
-          }
-          return meet(x.a, ta) && meet(x.b, tb);
-        }
-        case MGP_OP_UMUL_NOOVF:
-          if (!T) {  // a * b >= 2^w: a >= ceil(2^w / b.hi) and b >= ceil(2^w / a.hi)
-            const uint32_t ow = W(x.a);
-            const V m = M(ow);
-            const AV A = av[x.a], B = av[x.b];
-            if (Z(A.hi) || Z(B.hi)) return false;
-            V q, rr;
-            for (int k = 0; k < 2; ++k) {
-              bv_udivrem(m, k ? A.hi : B.hi, &q, &rr);  // floor((2^w - 1) / h) + 1 = ceil(2^w / h)
-              if (EQV(q, m)) return false;            // h = 1: the other operand would need 2^w
-              AV t = top(ow);
-              t.lo = ADDV(q, ONE());
-              if (!meet(k ? x.b : x.a, t)) return false;
-            }
-            return true;
-          }
-          if (T) {
-            const uint32_t ow = W(x.a);
-            const AV A = av[x.a], B = av[x.b];
-            V q, rr;
-            if (!Z(B.lo)) {
-              AV ta = top(ow);
-              bv_udivrem(M(ow), B.lo, &q, &rr);
-              ta.hi = q;
-              if (!meet(x.a, ta)) return false;
-            }
-            if (!Z(A.lo)) {
-              AV tb = top(ow);
-              bv_udivrem(M(ow), A.lo, &q, &rr);
-              tb.hi = q;
-              if (!meet(x.b, tb)) return false;
-            }
-          }
-          return true;
-        default: return true;
-      }
-    }
-    // BV node: the result's narrowed value constrains its operands
-    const uint32_t w = x.width;
-    const AV R = av[i];
-    switch (x.op) {
-      case MGP_OP_VAR: {  // every VAR node of one (index, width) shares the variable's value
-        AV &v = vars[vtie[i]];
-        AV t = v;
-        t.z = OR(t.z, R.z); t.o = OR(t.o, R.o); t.lo = MAX(t.lo, R.lo); t.hi = MIN(t.hi, R.hi);
-        if (!normalize(t, w)) return false;
-        if (!same(t, v)) {
-          if (undo) undo->push_back(UndoRec{3, (uint32_t)vtie[i], v, 0, 0, 0});
-          if (touched) touched->push_back(kVarBit | (uint32_t)vtie[i]);
-          v = t;
-          changed = true;
-        }
-        return true;
-      }
-      case MGP_OP_ADD: {
-        const AV A = av[x.a], B = av[x.b];
-        return meet(x.a, av_sub(R, B, w)) && meet(x.b, av_sub(R, A, w));
-      }
-      case MGP_OP_SUB: {
-        const AV A = av[x.a], B = av[x.b];
-        return meet(x.a, av_add(R, B, w)) && meet(x.b, av_sub(A, R, w));
-      }
-      case MGP_OP_XOR: {
-        const AV A = av[x.a], B = av[x.b];
-        return meet(x.a, av_xor(R, B, w)) && meet(x.b, av_xor(R, A, w));
-      }
-      case MGP_OP_MUL: {
-        // a * b = R (mod 2^w) with b exact and odd: b is invertible mod 2^k, so the k known
-        // low bits of R fix the k low bits of a = R * b^-1 (x * 5 == 1 pins x)
-        for (int k = 0; k < 2; ++k) {
-          const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
-          const AV B = av[q];
-          if (!is_exact(B) || !(B.lo.w[0] & 1u)) continue;
-          uint32_t kn = ctz_ones(OR(R.z, R.o));
-          if (kn > w) kn = w;
-          if (kn == 0) continue;
-          V inv = B.lo;  // Newton: b * b = 1 (mod 8), each step doubles the correct bits
-          for (int it = 0; it < 7; ++it) inv = bv_mul(inv, SUBV(bv_small(2u), bv_mul(B.lo, inv)));
-          const V lowm = M(kn);
-          const V al = AND(bv_mul(AND(R.o, lowm), inv), lowm);
-          AV t = top(w);
-          t.z = OR(t.z, AND(NOT(al), lowm));
-          t.o = al;
-          if (!meet(p, t)) return false;
-        }
-        if (heur) {  // decision mode: a * c in [R.lo, R.hi] without wrapping, when that is possible
-          for (int k = 0; k < 2; ++k) {
-            const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
-            const AV B = av[q];
-            if (!is_exact(B) || Z(B.lo) || is_exact(av[p])) continue;
-            V lo, hi, rl, rh;
-            bv_udivrem(av[i].lo, B.lo, &lo, &rl);
-            if (!Z(rl)) lo = ADDV(lo, ONE());
-            bv_udivrem(av[i].hi, B.lo, &hi, &rh);
-            if (LT(hi, lo)) continue;
-            AV t = top(w);
-            t.lo = lo;
-            t.hi = hi;
-            if (compatible(p, t) && !meet(p, t)) return false;
-          }
-        }
-        return true;
-      }
-      case MGP_OP_NOT: return meet(x.a, av_not(R, w));
-      case MGP_OP_NEG: return meet(x.a, av_sub(exact(bv_zero(), w), R, w));
-      case MGP_OP_UREM: {
-        // x % 2^k (k < w) is x's low k bits: the result's known bits below 2^k are x's
-        // (URem(hash, 64) == 0, keccak_function_manager.py:139)
-        const AV B = av[x.b];
-        if (!is_exact(B) || Z(B.lo)) return true;
-        const V m1 = SUBV(B.lo, ONE());
-        if (!Z(AND(B.lo, m1))) return true;  // not a power of two
-        AV ta = top(w);
-        ta.z = OR(ta.z, AND(R.z, m1));
-        ta.o = AND(R.o, m1);
-        return meet(x.a, ta);
-      }
-      case MGP_OP_AND: {
-        const AV A = av[x.a], B = av[x.b];
-        AV ta = top(w), tb = top(w);
-        ta.o = R.o; tb.o = R.o;
-        ta.z = OR(ta.z, AND(R.z, B.o));
-        tb.z = OR(tb.z, AND(R.z, A.o));
-        ta.lo = R.lo; tb.lo = R.lo;  // a & b <= a
-        return meet(x.a, ta) && meet(x.b, tb);
-      }
-      case MGP_OP_OR: {
-        const AV A = av[x.a], B = av[x.b];
-        AV ta = top(w), tb = top(w);
-        ta.z = OR(ta.z, R.z); tb.z = OR(tb.z, R.z);
-        ta.o = AND(R.o, AND(B.z, M(w)));
-        tb.o = AND(R.o, AND(A.z, M(w)));
-        ta.hi = R.hi; tb.hi = R.hi;  // a | b >= a
-        return meet(x.a, ta) && meet(x.b, tb);
-      }
-      case MGP_OP_ZEXT: {
-        const uint32_t wa = W(x.a);
-        AV t = top(wa);
-        t.z = OR(t.z, R.z);
-        t.o = AND(R.o, M(wa));
-        if (!Z(AND(R.lo, NOT(M(wa))))) return false;
-        t.lo = R.lo;
-        t.hi = MIN(R.hi, M(wa));
-        return meet(x.a, t);
-      }
-      case MGP_OP_SEXT: {
-        const uint32_t wa = W(x.a);
-        AV t = top(wa);
-        t.z = OR(t.z, AND(R.z, M(wa)));
-        t.o = AND(R.o, M(wa));
-        return meet(x.a, t);
-      }
-      case MGP_OP_EXTRACT: {
-        const uint32_t wa = W(x.a), lo = x.p1;
-        AV t = top(wa);
-        t.z = OR(t.z, SHL(AND(R.z, M(w)), lo));
-        t.o = SHL(R.o, lo);
-        return meet(x.a, t);
-      }
-      case MGP_OP_CONCAT: {
-        const uint32_t wa = W(x.a), wb = W(x.b);
-        AV ta = top(wa), tb = top(wb);
-        ta.z = OR(ta.z, SHR(AND(R.z, M(w)), wb));
-        ta.o = SHR(R.o, wb);
-        ta.lo = SHR(R.lo, wb);
-        ta.hi = SHR(R.hi, wb);
-        tb.z = OR(tb.z, AND(R.z, M(wb)));
-        tb.o = AND(R.o, M(wb));
-        if (EQV(SHR(R.lo, wb), SHR(R.hi, wb))) {
-          tb.lo = AND(R.lo, M(wb));
-          tb.hi = AND(R.hi, M(wb));
-        }
-        return meet(x.a, ta) && meet(x.b, tb);
-      }
-      case MGP_OP_SHL: case MGP_OP_LSHR: {
-        if (!is_exact(av[x.b])) return true;
-        const uint32_t s = bv_shift_amount(av[x.b].lo);
-        if (s >= w) return true;
-        AV t = top(w);
-        if (x.op == MGP_OP_SHL) {  // r[w-1..s] = a[w-1-s..0]
-          t.z = OR(t.z, AND(SHR(AND(R.z, M(w)), s), M(w - s)));
-          t.o = SHR(R.o, s);
-        } else {  // r[w-1-s..0] = a[w-1..s]
-          t.z = OR(t.z, SHL(AND(R.z, M(w - s)), s));
-          t.o = SHL(AND(R.o, M(w - s)), s);
-          t.lo = SHL(R.lo, s);
-          t.hi = AND(OR(SHL(R.hi, s), M(s)), M(w));
-        }
-        return meet(x.a, t);
-      }
-      case MGP_OP_ITE: {
-        const uint8_t c = bs[x.a];
-        if (c == BT) return meet(x.b, R);
-        if (c == BF) return meet(x.c, R);
-        if (!compatible(x.b, R) && !meetb(x.a, BF)) return false;
-        if (!compatible(x.c, R) && !meetb(x.a, BT)) return false;
-        return true;
-      }
-      default: return true;
+    // the pair lookup as a sorted array (the view's binary search, host and device)
+    pair_keys.clear();
+    pair_idx.clear();
+    std::vector<std::pair<uint64_t, int32_t>> kv(pair_of.begin(), pair_of.end());
+    std::sort(kv.begin(), kv.end());
+    for (const auto &e : kv) {
+      pair_keys.push_back(e.first);
+      pair_idx.push_back(e.second);
     }
   }
 
@@ -1163,71 +258,6 @@ struct State {
       if (cmp_pair[i] >= 0 || nd[i].op == MGP_OP_BOR) tie_rel[i] = 1;
     for (const Pair &p : pairs) tie_rel[p.x] = tie_rel[p.y] = 1;
     for (const UfApp &u : ufs) tie_rel[u.node] = 1;
-  }
-  void rollback(size_t mark) {
-    while (undo->size() > mark) {
-      const UndoRec &u = undo->back();
-      if (u.kind == 0) av[u.idx] = u.av;
-      else if (u.kind == 1) bs[u.idx] = u.b;
-      else if (u.kind == 2) pairs[u.idx].u = u.pu, pairs[u.idx].s = u.ps;
-      else vars[u.idx] = u.av;
-      undo->pop_back();
-    }
-  }
-  // Propagation from one changed node (a decision): backward into its operands, forward
-  // and backward through its users, transitively over the nodes that change, then the
-  // pair orderings when a node they read changed; at most `budget` transfer-function
-  // evaluations (a node with many users, e.g. calldatasize under every byte guard, counts
-  // each of them).  1 = the decision empties a domain.  Only decision rows use it
-  // (candidates, checked on the GPU); refutations run().
-  int run_from(uint32_t seed, uint32_t budget) {
-    std::vector<uint32_t> &T = *touched;
-    T.clear();
-    T.push_back(seed);
-    size_t head = 0;
-    uint32_t work = 0;
-    bool need_tie = false;
-    for (int round = 0; round < 3; ++round) {
-      while (head < T.size()) {
-        const uint32_t t = T[head++];
-        if (t & kVarBit) {  // a variable's shared value changed: every VAR node of it
-          const uint32_t j = t & ~kVarBit;
-          if ((work += voff[j + 1] - voff[j] + 1) > budget) return 0;
-          for (uint32_t k = voff[j]; k < voff[j + 1]; ++k)
-            if (!forward(vlist[k])) return 1;
-          continue;
-        }
-        need_tie |= tie_rel[t] != 0;
-        if ((work += 2u * (uoff[t + 1] - uoff[t]) + 1u) > budget) return 0;
-        if (!backward(t)) return 1;
-        for (uint32_t k = uoff[t]; k < uoff[t + 1]; ++k)
-          if (!forward(ulist[k]) || !backward(ulist[k])) return 1;
-      }
-      const size_t before = T.size();
-      if (!meetb((int32_t)n - 1, BT)) return 1;
-      if (need_tie) {  // tie() is at its fixpoint unless a node it reads changed
-        need_tie = false;
-        if (!tie()) return 1;
-      }
-      if (T.size() == before) break;
-    }
-    return 0;
-  }
-
-  // 1 = refuted (UNSAT), 0 = not refuted
-  int run(uint32_t max_passes) {
-    if (!meetb((int32_t)n - 1, BT)) return 1;
-    for (uint32_t pass = 0; pass < max_passes; ++pass) {
-      changed = false;
-      for (uint32_t i = 0; i < n; ++i)
-        if (!forward(i)) return 1;
-      if (!meetb((int32_t)n - 1, BT) || !tie()) return 1;
-      for (uint32_t i = n; i-- > 0;)
-        if (!backward(i)) return 1;
-      if (!tie()) return 1;
-      if (!changed) break;
-    }
-    return 0;
   }
 };
 
@@ -1294,7 +324,8 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
   s.consts = consts;
   s.n_consts = n_consts;
   if (!s.setup()) return -1;
-  return s.run(max_passes ? max_passes : 16u);
+  Dom d = s.view();
+  return d.run(max_passes ? max_passes : 16u);
 }
 
 }  // namespace
@@ -1376,32 +407,40 @@ extern "C" int mgp_refute_trace(const mgp_node *nodes, uint64_t n_nodes, const u
 }
 
 namespace {
-inline uint64_t mix64(uint64_t z) { return fe_mix64(z); }
-
 // One value of width w inside the abstract value a (mgp_fe_sample.h, shared with the
 // candidate generators).
 V sample_av(const AV &a, uint32_t w, uint32_t row, uint64_t r0) {
   return fe_sample_domain(a.z, a.o, a.lo, a.hi, w, row, r0);
 }
-}  // namespace
 
-namespace {
-// One state prepared for decision rows: its base analysis (refute_one), the variable
-// slots the decisions fix (VAR nodes and the fresh value of UF applications) and, per
-// slot, the constants it is compared equal to.
+// One state prepared for decision rows: its base analysis (refute_one) with the
+// propagation graph built, the variable slots the decisions fix (VAR nodes and the fresh
+// value of UF applications) and, per slot, the constants it is compared equal to.
 struct Prep {
   State s;
   int r = -1;
   std::vector<uint32_t> slot, width;
   std::vector<int32_t> node;
-  std::vector<std::vector<V>> eqh;
+  std::vector<uint32_t> eqh_off;  // per slot, into eqh
+  std::vector<V> eqh;
+  PrepView view() const {
+    PrepView p;
+    p.n_slot = (uint32_t)slot.size();
+    p.slot = slot.data();
+    p.width = width.data();
+    p.node = node.data();
+    p.eqh_off = eqh_off.data();
+    p.eqh = eqh.data();
+    return p;
+  }
 };
 
 void prep_state(Prep &P, const mgp_node *nodes, uint64_t n, const uint32_t *consts, uint64_t n_consts,
                 uint32_t max_passes, uint32_t n_vars) {
   P.r = refute_one(nodes, n, consts, n_consts, max_passes, &P.s);
   if (P.r != 0) return;
-  const State &s = P.s;
+  State &s = P.s;
+  s.build_graph();
   // (var slot, width, abstract value): VAR nodes and the fresh value of UF applications
   std::vector<int32_t> kof(s.n, -1);
   for (uint32_t i = 0; i < s.n; ++i) {
@@ -1421,7 +460,7 @@ void prep_state(Prep &P, const mgp_node *nodes, uint64_t n, const uint32_t *cons
   // cannot hold such a value set, so decisions try them first and plain domain rows
   // draw one half of the time when it lies inside the refined domain.  In node order
   // per variable, at most 16.
-  P.eqh.assign(P.slot.size(), {});
+  std::vector<std::vector<V>> eqh(P.slot.size());
   for (uint32_t i = 0; i < s.n; ++i) {
     const mgp_node &x = s.nd[i];
     if (x.op != MGP_OP_EQ || x.a < 0 || x.b < 0) continue;
@@ -1430,108 +469,59 @@ void prep_state(Prep &P, const mgp_node *nodes, uint64_t n, const uint32_t *cons
       const int32_t k = kof[me];
       if (k < 0 || (side && x.a == x.b)) continue;
       if (s.nd[other].op != MGP_OP_CONST || s.nd[other].width > MGP_MAX_WIDTH) continue;
-      if (s.nd[other].p0 >= s.n_consts || P.eqh[k].size() >= 16) continue;
+      if (s.nd[other].p0 >= s.n_consts || eqh[k].size() >= 16) continue;
       V c;
       memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
-      P.eqh[k].push_back(bv_mask(c, P.width[k]));
+      eqh[k].push_back(bv_mask(c, P.width[k]));
     }
+  }
+  P.eqh_off.assign(1, 0u);
+  for (const auto &e : eqh) {
+    P.eqh.insert(P.eqh.end(), e.begin(), e.end());
+    P.eqh_off.push_back((uint32_t)P.eqh.size());
   }
 }
 
-inline bool inside_av(const AV &a, const V &v) {
-  return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
+// MGP_DECIDE_OR=mask: the rows that start with the Or case split (A/B)
+uint32_t or_rows_mask() {
+  static const uint32_t m = [] {
+    const char *e = getenv("MGP_DECIDE_OR");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : kOrRowsDefault;
+  }();
+  return m;
 }
 
-// Decision row `row` of a prepared state: each variable slot in turn is fixed to a draw
-// from its current abstract value and the analysis re-propagated from the decided node
-// (State::run_from: backward into its operands, through its users, transitively, then
-// the pair orderings), so later variables are drawn from values narrowed by the earlier
-// choices (x + y == c, a mapping key fixed by an equality, ...).  A draw that empties a
-// domain is rolled back through the undo log and replaced (up to kTries draws).  Writes
-// the value of slot k to put(slot[k], value).  Stream key per slot: (seed, tag, c, slot).
+// Host run of mgpd::decision_row on a private copy of P's base analysis.
 template <typename Put>
-void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, uint32_t max_passes,
-                  Put put) {
+void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, Put &put) {
   const State &s = P.s;
-  const std::vector<uint32_t> &slot = P.slot, &width = P.width;
-  const std::vector<int32_t> &node = P.node;
-  const std::vector<std::vector<V>> &eqh = P.eqh;
-  constexpr uint32_t kTries = 4;
-  // MGP_DECIDE_PASSES=k re-runs k full passes per decision instead of run_from (A/B: the
-  // same witnesses)
-  static const uint32_t decide_passes = [] {
-    const char *e = getenv("MGP_DECIDE_PASSES");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  const uint32_t passes = std::min(max_passes ? max_passes : 16u, decide_passes ? decide_passes : 1u);
-  State d = s;
-  std::vector<State::UndoRec> undo_log;
-  std::vector<uint32_t> work;
-  d.build_graph();
-  d.undo = &undo_log;
+  std::vector<AV> av(s.av), vars(s.vars);
+  std::vector<uint8_t> bs(s.bs);
+  std::vector<Pair> pairs(s.pairs);
+  // the undo log and work list live in per-thread buffers reused across rows (only the
+  // first `cap` entries of each are addressable, as on the device)
+  static thread_local std::vector<UndoRec> undo_buf;
+  static thread_local std::vector<uint32_t> work_buf;
+  const uint32_t ucap = undo_cap(s.n, (uint32_t)s.pairs.size(), (uint32_t)s.ufs.size());
+  const uint32_t wcap = work_cap(s.n, (uint32_t)s.pairs.size(), (uint32_t)s.ufs.size());
+  if (undo_buf.size() < ucap) undo_buf.resize(ucap);
+  if (work_buf.size() < wcap) work_buf.resize(wcap);
+  Stack<UndoRec> undo;
+  undo.p = undo_buf.data();
+  undo.cap = ucap;
+  Stack<uint32_t> work;
+  work.p = work_buf.data();
+  work.cap = wcap;
+  Dom d = const_cast<State &>(s).view();
+  d.av = av.data();
+  d.bs = bs.data();
+  d.vars = vars.data();
+  d.pairs = pairs.data();
+  d.undo = &undo;
   d.touched = &work;
   d.heur = true;
-  const uint32_t budget = 4u * d.n + 64u;
-  // the draw schedule of decision row `row`: the first eight rows decide in node
-  // order (schedules 0, 4, 6, 8, 2, 10, 12, 14: the lo/hi schedule 0 that BECToken's
-  // mapping witness needs and three random-draw schedules first, so a state given
-  // four rows keeps most of its yield), later ones add the reverse-order schedules
-  // (odd) and then the rest, so any n_decide = 16 + k covers schedules 0..15+k.
-  // Node order is what contract states need (WalletLibrary's loop and mapping
-  // queries: 60 against 57 states of the mixed corpus at eight rows, at a third
-  // of the host time)
-  static const uint8_t kFirst8[8] = {0, 4, 6, 8, 2, 10, 12, 14};
-  const uint32_t drow = row < 8u ? kFirst8[row] : row < 16u ? 2u * (row - 8u) + 1u : row;
-  // rows whose decisions start with the Or case split: 1 and 3 (MGP_DECIDE_OR=mask for
-  // A/B; rows 0 and 2 keep the plain schedules, the corpus yield is the same either way)
-  static const uint32_t or_rows = [] {
-    const char *e = getenv("MGP_DECIDE_OR");
-    return e ? (uint32_t)strtoul(e, nullptr, 0) : 0xAu;
-  }();
-  if (row < 32u && ((or_rows >> row) & 1u)) {
-    // case split on the disjunctions the root requires: from the root down, a required Or
-    // with both operands open takes its first operand (else its second) before any
-    // variable is drawn, so its domain narrows as if that disjunct were a plain conjunct
-    // (keccak_function_manager.py:158-168: Or(interval condition, concrete-hash matches))
-    for (uint32_t i = d.n; i-- > 0;) {
-      if (d.nd[i].op != MGP_OP_BOR || d.bs[i] != BT) continue;
-      const int32_t a = d.nd[i].a, b = d.nd[i].b;
-      if (a < 0 || b < 0 || d.bs[a] != BB || d.bs[b] != BB) continue;
-      for (int32_t pick : {a, b}) {
-        const size_t mark = undo_log.size();
-        work.clear();
-        if (d.meetb(pick, BT) && d.run_from((uint32_t)pick, budget) == 0) {
-          undo_log.clear();
-          break;
-        }
-        d.rollback(mark);
-      }
-    }
-  }
-  for (size_t kk = 0; kk < slot.size(); ++kk) {
-    const size_t k = (drow & 1) ? slot.size() - 1 - kk : kk;  // odd rows decide in reverse order
-    const uint64_t key = mix64(seed ^ mix64(tag ^ ((uint64_t)c << 12) ^ slot[k]));
-    if (EQV(d.av[node[k]].lo, d.av[node[k]].hi)) {  // already one value: nothing to decide
-      put(slot[k], d.av[node[k]].lo);
-      continue;
-    }
-    V v = bv_zero();
-    const uint32_t nh = (uint32_t)eqh[k].size();
-    for (uint32_t t = 0; t < kTries + nh; ++t) {
-      v = t < nh ? eqh[k][(t + drow + (drow < 8u ? 0u : (uint32_t)(key >> 40))) % nh]
-                 : sample_av(d.av[node[k]], width[k], t > nh ? 3u + drow + t : (drow < 4 ? drow / 2 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + drow : 0u)), mix64(key + t));
-      if (t < nh && !inside_av(d.av[node[k]], v)) continue;
-      const size_t mark = undo_log.size();
-      work.clear();
-      if (d.meet(node[k], exact(v, width[k])) &&
-          (decide_passes ? d.tie() && d.run(passes) == 0 : d.run_from((uint32_t)node[k], budget) == 0)) {
-        undo_log.clear();
-        break;
-      }
-      d.rollback(mark);
-    }
-    put(slot[k], v);
-  }
+  const PrepView pv = P.view();
+  mgpd::decision_row(pv, d, row, c, seed, tag, or_rows_mask(), put);
 }
 }  // namespace
 
@@ -1575,15 +565,16 @@ extern "C" int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t 
         uint32_t *dst = cands + ((uint64_t)st * n_cand + c) * n_vars * 8ull;
         if (task_row < n_dec_rows ? row != task_row : row < rs) continue;
         if (row < rs) {
-          decision_row(P, row, c, seed, (uint64_t)st << 32, max_passes,
-                       [&](uint32_t sl, const V &v) { memcpy(dst + sl * 8ull, v.w, 32); });
+          auto put = [&](uint32_t sl, const V &v) { memcpy(dst + sl * 8ull, v.w, 32); };
+          decision_row(P, row, c, seed, (uint64_t)st << 32, put);
           continue;
         }
         for (size_t k = 0; k < P.slot.size(); ++k) {
-          const uint64_t key = mix64(seed ^ mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ P.slot[k]));
+          const uint64_t key = fe_mix64(seed ^ fe_mix64(((uint64_t)st << 32) ^ ((uint64_t)c << 12) ^ P.slot[k]));
           V v = sample_av(s.av[P.node[k]], P.width[k], row, key);
-          if (!P.eqh[k].empty() && (mix64(key ^ 0x9E37ull) & 1u)) {
-            const V h = P.eqh[k][mix64(key ^ 0x7F4Aull) % P.eqh[k].size()];
+          const uint32_t h0 = P.eqh_off[k], nh = P.eqh_off[k + 1] - h0;
+          if (nh && (fe_mix64(key ^ 0x9E37ull) & 1u)) {
+            const V h = P.eqh[h0 + fe_mix64(key ^ 0x7F4Aull) % nh];
             if (inside_av(s.av[P.node[k]], h)) v = h;
           }
           memcpy(dst + P.slot[k] * 8ull, v.w, 32);
@@ -1625,10 +616,11 @@ extern "C" int mgp_decision_rows(const mgp_node *nodes, const uint64_t *node_off
       if (P.r != 0 || row >= rs) continue;
       const uint64_t tag = state_keys ? state_keys[st] : (uint64_t)st << 32;
       const uint64_t r0 = ((uint64_t)st * n_decide + row) * n_vars;
-      decision_row(P, row, 2u * row, seed, tag, max_passes, [&](uint32_t sl, const V &v) {
+      auto put = [&](uint32_t sl, const V &v) {
         memcpy(out_rows + (r0 + sl) * 8ull, v.w, 32);
         out_mask[r0 + sl] = 1;
-      });
+      };
+      decision_row(P, row, 2u * row, seed, tag, put);
     }
   }
   return MGP_OK;
@@ -1640,4 +632,198 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
                                      uint32_t n_decide, uint32_t *cands, int8_t *out) {
   return mgp_guided_candidates_rows(nodes, node_offsets, n_states, consts, const_offsets, max_passes, n_cand, n_vars,
                                     seed, every, n_decide, nullptr, cands, out);
+}
+
+// ------------------------------------------------- decision rows on the device
+// mgp_decision_rows with the rows computed by mgp_decide.hip: the states are prepared
+// here (base analysis, propagation graph, decision slots: the same prep_state), packed
+// into one read-only blob, and every (state, row) task runs mgpd::decision_row on the
+// GPU in a workspace of its own.  Same outputs as mgp_decision_rows, bit for bit.
+#include <map>
+#include <mutex>
+
+#include "mgp_decide.h"
+
+extern "C" int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device);
+extern "C" int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg);
+
+namespace {
+
+struct ByteBlob {
+  std::vector<uint8_t> b;
+  uint64_t put(const void *p, size_t bytes) {
+    const uint64_t off = (b.size() + 15u) / 16u * 16u;
+    b.resize(off + ((bytes + 15u) / 16u) * 16u + 16u, 0);  // padded: 16-B copies never read past
+    if (bytes) memcpy(b.data() + off, p, bytes);
+    return off;
+  }
+  template <typename T>
+  uint64_t put(const std::vector<T> &v) { return put(v.data(), v.size() * sizeof(T)); }
+};
+
+struct DevGrow {
+  void *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4u, 1u << 20);
+    const hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+};
+struct DecBufs {
+  DevGrow blob, states, tasks, ws, rows, mask;
+};
+std::mutex g_dec_mu;
+std::map<std::pair<int, void *>, DecBufs> g_dec;  // per (device, stream)
+
+inline uint64_t up16(uint64_t x) { return (x + 15u) / 16u * 16u; }
+
+// workspace bytes a task may take before the tasks are split over several launches
+constexpr uint64_t kWsLaunchBytes = 4ull << 30;
+
+}  // namespace
+
+extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
+                                     uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
+                                     uint32_t max_passes, uint32_t n_vars, uint64_t seed, const uint64_t *state_keys,
+                                     uint32_t n_decide, const uint8_t *rows_per_state, uint32_t *out_rows,
+                                     uint8_t *out_mask, int8_t *out) {
+  if (!ctx || !node_offsets || !out || (n_states && (!nodes || !const_offsets)) ||
+      (n_states && n_decide && (!out_rows || !out_mask)))
+    return MGP_E_ARG;
+  void *stp = nullptr;
+  int dev = 0;
+  int rc = mgp_ctx_stream(ctx, &stp, &dev);
+  if (rc != MGP_OK) return rc;
+  hipStream_t st = (hipStream_t)stp;
+  const size_t rows_bytes = (size_t)n_states * n_decide * n_vars * 32u, mask_bytes = (size_t)n_states * n_decide * n_vars;
+  if (n_states && n_decide) {
+    memset(out_mask, 0, mask_bytes);
+    memset(out_rows, 0, rows_bytes);
+  }
+  std::vector<Prep> prep(n_states);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
+    const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
+    prep_state(prep[s], nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, n_vars);
+    out[s] = (int8_t)prep[s].r;
+  }
+  if (!n_decide || !n_states) return MGP_OK;
+  // pack the prepared states and list the tasks
+  ByteBlob B;
+  std::vector<mgp_dec_state> hdr;
+  std::vector<mgp_dec_task> tasks;
+  std::vector<uint64_t> task_ws;  // workspace bytes of each task
+  for (uint32_t s = 0; s < n_states; ++s) {
+    const Prep &P = prep[s];
+    const uint32_t rs = rows_per_state ? std::min<uint32_t>(rows_per_state[s], n_decide) : n_decide;
+    if (P.r != 0 || rs == 0) continue;
+    const State &S = P.s;
+    mgp_dec_state h;
+    memset(&h, 0, sizeof h);
+    h.nd = B.put(S.nd, (size_t)S.n * sizeof(mgp_node));
+    h.orig = (S.orig && S.orig != S.nd) ? B.put(S.orig, (size_t)S.n * sizeof(mgp_node)) : h.nd;
+    h.consts = B.put(S.consts, (size_t)S.n_consts * 32u);
+    h.n_consts = S.n_consts;
+    h.av = B.put(S.av);
+    h.bs = B.put(S.bs);
+    h.isb = B.put(S.isb);
+    h.vtie = B.put(S.vtie);
+    h.vars = B.put(S.vars);
+    h.pairs = B.put(S.pairs);
+    h.cmp_pair = B.put(S.cmp_pair);
+    h.cmp_dom = B.put(S.cmp_dom);
+    h.cmp_t = B.put(S.cmp_t);
+    h.pair_keys = B.put(S.pair_keys);
+    h.pair_idx = B.put(S.pair_idx);
+    h.ufs = B.put(S.ufs);
+    h.uoff = B.put(S.uoff);
+    h.ulist = B.put(S.ulist);
+    h.voff = B.put(S.voff);
+    h.vlist = B.put(S.vlist);
+    h.tie_rel = B.put(S.tie_rel);
+    h.slot = B.put(P.slot);
+    h.width = B.put(P.width);
+    h.node = B.put(P.node);
+    h.eqh_off = B.put(P.eqh_off);
+    h.eqh = B.put(P.eqh);
+    h.n = S.n;
+    h.n_vt = (uint32_t)S.vars.size();
+    h.n_pairs = (uint32_t)S.pairs.size();
+    h.n_ufs = (uint32_t)S.ufs.size();
+    h.n_slot = (uint32_t)P.slot.size();
+    h.ucap = undo_cap(h.n, h.n_pairs, h.n_ufs);
+    h.wcap = work_cap(h.n, h.n_pairs, h.n_ufs);
+    uint64_t o = 0;
+    h.ws_av = o;
+    o = up16(o + (uint64_t)h.n * sizeof(AV));
+    h.ws_vars = o;
+    o = up16(o + (uint64_t)h.n_vt * sizeof(AV));
+    h.ws_pairs = o;
+    o = up16(o + (uint64_t)h.n_pairs * sizeof(Pair));
+    h.ws_bs = o;
+    o = up16(o + h.n);
+    h.ws_undo = o;
+    o = up16(o + (uint64_t)h.ucap * sizeof(UndoRec));
+    h.ws_work = o;
+    o = up16(o + (uint64_t)h.wcap * 4u);
+    h.ws_bytes = o;
+    const uint32_t si = (uint32_t)hdr.size();
+    hdr.push_back(h);
+    const uint64_t tag = state_keys ? state_keys[s] : (uint64_t)s << 32;
+    for (uint32_t row = 0; row < rs; ++row) {
+      tasks.push_back(mgp_dec_task{si, row, 0, tag, ((uint64_t)s * n_decide + row) * n_vars});
+      task_ws.push_back(h.ws_bytes);
+    }
+  }
+  if (tasks.empty()) return MGP_OK;
+  std::lock_guard<std::mutex> lk(g_dec_mu);
+  DecBufs &D = g_dec[{dev, stp}];
+  hipError_t e = hipSetDevice(dev);
+  // launches of at most kWsLaunchBytes of workspace each
+  std::vector<std::pair<size_t, size_t>> launches;
+  uint64_t ws_max = 0;
+  for (size_t a = 0; a < tasks.size();) {
+    uint64_t o = 0;
+    size_t b = a;
+    while (b < tasks.size() && (b == a || o + task_ws[b] <= kWsLaunchBytes)) {
+      tasks[b].ws = o;
+      o += task_ws[b];
+      ++b;
+    }
+    ws_max = std::max(ws_max, o);
+    launches.emplace_back(a, b);
+    a = b;
+  }
+  if (e == hipSuccess) e = D.blob.ensure(B.b.size());
+  if (e == hipSuccess) e = D.states.ensure(hdr.size() * sizeof(mgp_dec_state));
+  if (e == hipSuccess) e = D.tasks.ensure(tasks.size() * sizeof(mgp_dec_task));
+  if (e == hipSuccess) e = D.ws.ensure(ws_max);
+  if (e == hipSuccess) e = D.rows.ensure(rows_bytes);
+  if (e == hipSuccess) e = D.mask.ensure(mask_bytes);
+  if (e == hipSuccess) e = hipMemcpyAsync(D.blob.p, B.b.data(), B.b.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(D.states.p, hdr.data(), hdr.size() * sizeof(mgp_dec_state), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(D.tasks.p, tasks.data(), tasks.size() * sizeof(mgp_dec_task), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemsetAsync(D.rows.p, 0, rows_bytes, st);
+  if (e == hipSuccess) e = hipMemsetAsync(D.mask.p, 0, mask_bytes, st);
+  static const uint32_t or_rows = or_rows_mask();
+  for (const auto &L : launches) {
+    if (e != hipSuccess) break;
+    e = mgp_launch_decide((const uint8_t *)D.blob.p, (const mgp_dec_state *)D.states.p,
+                          (const mgp_dec_task *)D.tasks.p + L.first, (uint32_t)(L.second - L.first),
+                          (uint8_t *)D.ws.p, seed, or_rows, (uint32_t *)D.rows.p, (uint8_t *)D.mask.p, st);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out_rows, D.rows.p, rows_bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_mask, D.mask.p, mask_bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+  return MGP_OK;
 }

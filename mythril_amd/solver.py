@@ -355,6 +355,10 @@ class Prefilter:
     # per-state work cap of the decision rows: variables x DAG nodes x rows (a deterministic
     # count; the largest WalletLibrary state of the corpus needs 1.8 M at four rows)
     DECIDE_MAX_UNITS = 1 << 25
+    # decision rows run on the GPU (mgp_decision_rows_dev, bit-identical to the host's)
+    # for a retry round of at least this many open states; smaller rounds stay on the
+    # host threads, where a single row is faster than on one GPU lane
+    DECIDE_GPU_MIN = 64
 
     def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,
                  devices: Optional[Sequence[int]] = None):
@@ -372,6 +376,7 @@ class Prefilter:
         self.retry_cand = self.RETRY_CAND  # 0 (or <= n_cand) = no second round
         self.decide_rows = self.DECIDE_ROWS
         self.decide_max_units = self.DECIDE_MAX_UNITS
+        self.decide_on_gpu = "auto"  # "auto" (>= DECIDE_GPU_MIN open states), "always" or "never"
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # refuted constraint lists wait in the core cache and are shrunk to cores together
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
@@ -579,9 +584,12 @@ class Prefilter:
             gv = max(1, GB.n_vars())
             rps = self.rows_per_state(GB)
             td = time.perf_counter()
+            on_gpu = self.decide_on_gpu == "always" or (self.decide_on_gpu == "auto" and
+                                                        len(grp) >= self.DECIDE_GPU_MIN)
             rows, mask, _ = self._N.decision_rows(*GB.packed(decide=True), gv, seed2, self.decide_rows, rps,
-                                                  state_keys=GB.state_key)
+                                                  state_keys=GB.state_key, ctx=ctx if on_gpu else None)
             dec_ms += 1e3 * (time.perf_counter() - td)
+            prof["decide_on_gpu"] = bool(on_gpu)
             f2, w2, _, _ = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
             unsafe = (GB.flags & FE_SAT_UNSAFE) != 0
             for k, j in enumerate(grp):

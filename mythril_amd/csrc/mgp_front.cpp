@@ -442,10 +442,14 @@ void strengthen_padded(StateOut &S, IsPadded is_padded_eq) {
         if (n.b >= 0) pol[n.b] |= p;
         if (n.c >= 0) pol[n.c] |= p;
         break;
-      case MGP_OP_ITE:
-        if (n.a >= 0) pol[n.a] |= 3;
-        break;
       default:
+        // a node the pass does not model (a compare, a BV ITE, a BV operator, a UF
+        // application): its operands -- a padded equality under If(eq, 1, 0) == 1, the
+        // shape LASER's EQ / ISZERO build -- are reached with both polarities, which flags
+        // the state SAT-unsafe instead of leaving the equality unstrengthened
+        if (n.a >= 0) pol[n.a] |= 3;
+        if (n.b >= 0) pol[n.b] |= 3;
+        if (n.c >= 0) pol[n.c] |= 3;
         break;
     }
   }

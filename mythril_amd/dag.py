@@ -228,8 +228,13 @@ def _strengthen_padded(d: StateDag) -> None:
             pol[a] |= 3
             pol[b] |= p
             pol[c] |= p
-        elif op == ir.ITE:
-            pol[a] |= 3
+        else:
+            # a node the pass does not model (a compare, a BV ITE, a BV operator, a UF
+            # application): its operands -- a padded equality under If(eq, 1, 0) == 1,
+            # the shape LASER's EQ / ISZERO build -- are reached with both polarities
+            for x in (a, b, c):
+                if x >= 0:
+                    pol[x] |= 3
     for i, n in enumerate(nodes):
         if pol[i] and _is_padded_eq(nodes, n):
             if pol[i] == 3:

@@ -125,16 +125,35 @@ class Model:
         return None
 
     def eval(self, expression, model_completion: bool = False):
-        if self.raw is not None and hasattr(self.raw, "eval"):  # a z3 model from the fallback
-            return self.raw.eval(getattr(expression, "raw", expression), model_completion=model_completion)
+        """model.py:45-59.  Either kind of model answers with a value that has z3's
+        `.as_long()` (a z3 numeral from a fallback model, a ModelValue from a GPU witness),
+        so reference callers work with both; None = not determined by this model."""
         t = expression.raw if isinstance(expression, Expression) else expression
+        if self.raw is not None and hasattr(self.raw, "eval"):  # a z3 model from the fallback
+            if isinstance(t, Term):  # a mirror term: the z3 expression it was lowered from
+                from . import z3_lower
+
+                z = z3_lower.z3_expr_of(t)
+                if z is None:
+                    return None
+                t = z
+            return self.raw.eval(t, model_completion=model_completion)
         if isinstance(t, Term):
             if t.op == 2:  # CONST
-                return t.params[0]
+                return ModelValue(t.params[0])
             if t.op == 1:  # VAR
                 v = self[str(t.params[0])]
-                return 0 if v is None and model_completion else v
+                if v is None:
+                    return ModelValue(0) if model_completion else None
+                return ModelValue(v)
         return None
+
+
+class ModelValue(int):
+    """An integer model value with z3's numeral accessor (BitVecNumRef.as_long)."""
+
+    def as_long(self) -> int:
+        return int(self)
 
 
 # --------------------------------------------------------------- backends

@@ -357,6 +357,16 @@ def lowering_of_module(z3) -> Optional[Z3Lowering]:
     return None
 
 
+def z3_expr_of(t: Term):
+    """The z3 expression a term was lowered from (a root constraint, a variable or an
+    uninterpreted application; a base-array read becomes Select(array, index)), or None."""
+    for w in _lowerings.values():
+        e = w.roots.get(t.tid) or w.origin.get(t.tid)
+        if e is not None:
+            return w.z3.Select(e[0], e[1]) if isinstance(e, tuple) else e
+    return None
+
+
 def is_z3_expr(x) -> bool:
     return hasattr(x, "decl") and hasattr(x, "children") and hasattr(x, "get_id")
 

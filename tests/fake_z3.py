@@ -514,7 +514,19 @@ class Solver:
         return sat if ok else unsat
 
     def model(self):
-        return ("model", dict(self._env), dict(self._funcs))
+        return ModelRef(dict(self._env), dict(self._funcs))
+
+
+class ModelRef:
+    """z3py's ModelRef.eval over the stand-in's decided environment."""
+
+    def __init__(self, env, funcs):
+        self.env, self.funcs = env, funcs
+
+    def eval(self, e, model_completion=False):
+        if e.sort().kind() == Z3_BOOL_SORT:
+            return BoolVal(bool(evaluate(e, self.env, self.funcs)))
+        return BitVecVal(evaluate(e, self.env, self.funcs), e.size())
 
 
 class Optimize(Solver):

@@ -87,11 +87,16 @@ def test_padded_key_equalities_strengthened_by_polarity(monkeypatch):
     neg = [c2, Not(BVV(5, 8) == BVS("q", 256))]            # padded equality under a negation
     mixed = [Xor(BVV(5, 8) == BVS("q", 256), BVS("r", 256) == 1)]  # both polarities
     none = [BVS("a", 256) == BVV(5, 256)]
-    dags = _assert_same([pos, neg, mixed, none])
+    # the padded equality reached only through a BV context: If(eq, 1, 0) == 1, the shape
+    # LASER's EQ / ISZERO instructions build: flagged, not left unstrengthened
+    from mythril_amd.smt import If
+    bvctx = [If(BVV(5, 8) == BVS("q", 256), BVV(1, 256), BVV(0, 256)) == BVV(1, 256)]
+    dags = _assert_same([pos, neg, mixed, none, bvctx])
     assert dags[0].flags == 2 and set(dags[0].gpu_ops.values()) == {4}   # FALSE
     assert dags[1].flags == 2 and 3 in dags[1].gpu_ops.values()          # TRUE
     assert dags[2].flags & 1
     assert dags[3].flags == 0 and not dags[3].gpu_ops
+    assert dags[4].flags & 1 and not dags[4].gpu_ops
 
 
 def test_empty_batch_and_state():

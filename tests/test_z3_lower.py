@@ -160,6 +160,12 @@ def test_z3_backend_check_and_recheck():
     # the fallback on the original constraints: pinned -> decided by the stand-in
     r, m = be.check(SV._terms([x == 3, y == 9, z3.ULT(x, y)]), 100)
     assert r == SV.sat and m.raw is not None
+    # Model.eval on a mirror term of a z3 model: mapped back to the z3 expression
+    # (ADVICE r2); both kinds of model answer with a value that has .as_long()
+    tx = ZL.lowering_for(x).lower(x)
+    assert m.eval(tx).as_long() == 3
+    gm = SV.Model([{"rx": 7}])
+    assert gm.eval(tx).as_long() == 7 and gm.eval(ZL.lowering_for(y).lower(y)) is None
     r, _ = be.check(SV._terms([x == 3, y == 2, z3.ULT(x, y)]), 100)
     assert r == SV.unsat
     B.close()

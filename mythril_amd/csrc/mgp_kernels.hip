@@ -778,7 +778,13 @@ struct FeRow {
 };
 }  // namespace
 
-__global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
+// One candidate row (s, c), built by `nl` cooperating lanes (lane = 0..nl-1; nl = 1 is
+// one thread per row): every pass that writes only its own variable's cell is strided
+// over the lanes, the two alias passes (an alias copies a cell as written so far, in
+// variable order) run on lane 0, and SYNC separates the passes when nl > 1.  Same
+// values either way.
+template <bool BLOCK>
+__device__ __forceinline__ void fe_cands_row(
     uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed, const uint64_t *__restrict__ var_off,
     const uint32_t *__restrict__ var_width, const uint8_t *__restrict__ var_kind,
     const uint64_t *__restrict__ hint_off, const uint32_t *__restrict__ hints,
@@ -788,15 +794,15 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
     const uint8_t *__restrict__ pmask, const uint32_t *__restrict__ dom, const uint32_t *__restrict__ asrc_off,
     const uint32_t *__restrict__ asrc, const uint32_t *__restrict__ wcls, const uint32_t *__restrict__ wlist,
     const uint64_t *__restrict__ state_keys, const uint32_t *__restrict__ xrows, const uint8_t *__restrict__ xmask,
-    uint32_t n_xrows, uint32_t n_xvars, uint4 *__restrict__ out) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= (uint64_t)n_states * n_cand) return;
-  const uint64_t s = g / n_cand;
+    uint32_t n_xrows, uint32_t n_xvars, uint4 *__restrict__ out, uint64_t s, uint32_t c, uint32_t lane, uint32_t nl) {
+#define SYNC()                      \
+  do {                              \
+    if constexpr (BLOCK) __syncthreads(); \
+  } while (0)
   const uint64_t tag = state_keys ? state_keys[s] : s << 40;  // as mgp_make_candidates
-  const uint32_t c = (uint32_t)(g % n_cand);
   const FeRow R{out, n_cand, n_vars, c, s};
   uint32_t x[8];
-  for (uint32_t v = 0; v < n_vars; ++v) {  // uniform everywhere first (also padding variables)
+  for (uint32_t v = lane; v < n_vars; v += nl) {  // uniform everywhere first (also padding variables)
     uint64_t k = fe_mix(seed ^ fe_mix(tag ^ ((uint64_t)c << 16) ^ v));
     for (int l = 0; l < 8; l += 2) {
       k = fe_mix(k);
@@ -833,13 +839,15 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
   };
   const int32_t pidx = parent_idx ? parent_idx[s] : -1;
   const uint32_t first_row = pidx >= 0 ? 1u : 0u;
+  SYNC();
   if (pidx >= 0 && c == 0) {  // parent witness row (values of the same variables, by name)
-    for (uint64_t v = 0; v < V; ++v)
+    for (uint64_t v = lane; v < V; v += nl)
       if (pmask[(uint64_t)pidx * n_vars + v]) R.put((uint32_t)v, pvals + ((uint64_t)pidx * n_vars + v) * 8u);
   } else if (c == first_row || c == first_row + 1) {
-    for (uint64_t v = 0; v < V; ++v)
+    for (uint64_t v = lane; v < V; v += nl)
       if (n_hint(v)) R.put((uint32_t)v, hint(v, 0));
-    if (c == first_row + 1)
+    SYNC();
+    if (c == first_row + 1 && lane == 0)
       for (uint64_t a = 0; a < na; ++a) {
         const uint32_t dst = aliases[2 * (a0 + a)], src = aliases[2 * (a0 + a) + 1];
         if (dst < V && src < V && var_width[v0 + dst] == var_width[v0 + src] && n_hint(src) && !n_hint(dst))
@@ -851,7 +859,7 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       *r = (double)(k >> 11) * (1.0 / 9007199254740992.0);
       *pick = fe_mix(k);
     };
-    for (uint64_t v = 0; v < V; ++v) {
+    for (uint64_t v = lane; v < V; v += nl) {
       double r;
       uint64_t pick;
       draw(v, &r, &pick);
@@ -862,7 +870,8 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
         R.put((uint32_t)v, x);
       }
     }
-    for (uint64_t v = 0; v < V; ++v) {  // after the others, so an alias can copy any variable
+    SYNC();
+    for (uint64_t v = 0; v < V && lane == 0; ++v) {  // after the others, so an alias can copy any variable
       double r;
       uint64_t pick;
       draw(v, &r, &pick);
@@ -897,9 +906,10 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
         }
       }
     }
+    SYNC();
     const uint32_t kk = c - (first_row + 2u);  // domain rows: as mgp_make_candidates
     if (dom && (kk & 1u) == 0u)
-      for (uint64_t v = 0; v < V; ++v) {
+      for (uint64_t v = lane; v < V; v += nl) {
         const uint32_t *d = dom + (v0 + v) * 33u;
         if (!d[32]) continue;
         U256 z, o, lo, hi;
@@ -924,17 +934,19 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
     // mixture rows take the given values of the slots their mask marks
     if (xrows && kk < n_xrows) {
       const uint64_t r0 = (s * n_xrows + kk) * (uint64_t)n_xvars;
-      for (uint64_t v = 0; v < V && v < n_xvars; ++v)
+      for (uint64_t v = lane; v < V && v < n_xvars; v += nl)
         if (xmask[r0 + v]) R.put((uint32_t)v, xrows + (r0 + v) * 8u);
     }
   }
-  for (uint64_t v = 0; v < V; ++v)  // pinned constants
+  SYNC();
+  for (uint64_t v = lane; v < V; v += nl)  // pinned constants
     if (var_kind && var_kind[v0 + v] == 2 && n_hint(v)) R.put((uint32_t)v, hint(v, 0));
+  SYNC();
   // the mask to the slot width, 8 variables per round trip: their 16 loads are
   // independent, so a small batch (a few waves on the chip) pays one load latency per
   // 8 variables instead of one per 16 bytes
   constexpr uint32_t kB = 8;
-  for (uint64_t vb = 0; vb < V; vb += kB) {
+  for (uint64_t vb = (uint64_t)lane * kB; vb < V; vb += (uint64_t)nl * kB) {
     uint4 q[kB][2];
     uint32_t w[kB];
     const uint32_t nb = (uint32_t)((V - vb) < kB ? (V - vb) : kB);
@@ -959,6 +971,43 @@ __global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
       }
     }
   }
+}
+
+#undef SYNC
+
+__global__ __launch_bounds__(256) void mgp_fe_cands_kernel(
+    uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed, const uint64_t *__restrict__ var_off,
+    const uint32_t *__restrict__ var_width, const uint8_t *__restrict__ var_kind,
+    const uint64_t *__restrict__ hint_off, const uint32_t *__restrict__ hints,
+    const uint64_t *__restrict__ alias_off, const uint32_t *__restrict__ aliases,
+    const uint64_t *__restrict__ const_off, const uint32_t *__restrict__ consts, const uint32_t *__restrict__ fixed,
+    uint32_t n_fixed, const int32_t *__restrict__ parent_idx, const uint32_t *__restrict__ pvals,
+    const uint8_t *__restrict__ pmask, const uint32_t *__restrict__ dom, const uint32_t *__restrict__ asrc_off,
+    const uint32_t *__restrict__ asrc, const uint32_t *__restrict__ wcls, const uint32_t *__restrict__ wlist,
+    const uint64_t *__restrict__ state_keys, const uint32_t *__restrict__ xrows, const uint8_t *__restrict__ xmask,
+    uint32_t n_xrows, uint32_t n_xvars, uint4 *__restrict__ out) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (uint64_t)n_states * n_cand) return;
+  fe_cands_row<false>(n_states, n_cand, n_vars, seed, var_off, var_width, var_kind, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed, parent_idx, pvals, pmask, dom, asrc_off, asrc, wcls, wlist, state_keys, xrows, xmask, n_xrows, n_xvars, out, g / n_cand, (uint32_t)(g % n_cand), 0u, 1u);
+}
+
+// one 64-lane workgroup per row: a small batch of contract states (hundreds of variables
+// per row, a few waves on the whole chip) builds a row in a few variable-steps per lane
+// instead of one long sequential pass per thread
+__global__ __launch_bounds__(64) void mgp_fe_cands_rowblock_kernel(
+    uint32_t n_states, uint32_t n_cand, uint32_t n_vars, uint64_t seed, const uint64_t *__restrict__ var_off,
+    const uint32_t *__restrict__ var_width, const uint8_t *__restrict__ var_kind,
+    const uint64_t *__restrict__ hint_off, const uint32_t *__restrict__ hints,
+    const uint64_t *__restrict__ alias_off, const uint32_t *__restrict__ aliases,
+    const uint64_t *__restrict__ const_off, const uint32_t *__restrict__ consts, const uint32_t *__restrict__ fixed,
+    uint32_t n_fixed, const int32_t *__restrict__ parent_idx, const uint32_t *__restrict__ pvals,
+    const uint8_t *__restrict__ pmask, const uint32_t *__restrict__ dom, const uint32_t *__restrict__ asrc_off,
+    const uint32_t *__restrict__ asrc, const uint32_t *__restrict__ wcls, const uint32_t *__restrict__ wlist,
+    const uint64_t *__restrict__ state_keys, const uint32_t *__restrict__ xrows, const uint8_t *__restrict__ xmask,
+    uint32_t n_xrows, uint32_t n_xvars, uint4 *__restrict__ out) {
+  const uint64_t g = blockIdx.x;
+  if (g >= (uint64_t)n_states * n_cand) return;
+  fe_cands_row<true>(n_states, n_cand, n_vars, seed, var_off, var_width, var_kind, hint_off, hints, alias_off, aliases, const_off, consts, fixed, n_fixed, parent_idx, pvals, pmask, dom, asrc_off, asrc, wcls, wlist, state_keys, xrows, xmask, n_xrows, n_xvars, out, g / n_cand, (uint32_t)(g % n_cand), threadIdx.x, blockDim.x);
 }
 
 // ------------------------------------------------------ VALU peak probe
@@ -1301,6 +1350,20 @@ hipError_t mgp_launch_fe_cands(uint32_t n_states, uint32_t n_cand, uint32_t n_va
                                uint32_t n_xrows, uint32_t n_xvars, uint32_t *out, hipStream_t st) {
   const uint64_t total = (uint64_t)n_states * n_cand;
   if (total == 0) return hipSuccess;
+  // few rows of many variables (LASER's 2-successor forks of contract states): a
+  // workgroup per row; otherwise a thread per row (MGP_FE_ROWBLOCK=0/1 forces one, A/B)
+  static const int rb_env = [] {
+    const char *e = getenv("MGP_FE_ROWBLOCK");
+    return e ? atoi(e) : -1;
+  }();
+  const bool rowblock = rb_env >= 0 ? rb_env != 0 : (total <= 16384u && n_vars >= 32u);
+  if (rowblock) {
+    hipLaunchKernelGGL(mgp_fe_cands_rowblock_kernel, dim3((uint32_t)total), dim3(64), 0, st, n_states, n_cand,
+                       n_vars, seed, var_off, var_width, var_kind, hint_off, hints, alias_off, aliases, const_off,
+                       consts, fixed, n_fixed, parent_idx, pvals, pmask, dom, asrc_off, asrc, wcls, wlist,
+                       state_keys, xrows, xmask, n_xrows, n_xvars, reinterpret_cast<uint4 *>(out));
+    return hipGetLastError();
+  }
   const uint64_t blocks = (total + 255) / 256;
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mgp_fe_cands_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, n_states, n_cand, n_vars, seed,

@@ -36,10 +36,13 @@ def clean():
     SV.unsat_cores().reset()
 
 
-def test_explicit_rows_in_device_candidates(mgp_ctx):
+@pytest.mark.parametrize("n_states", [64, 200])
+def test_explicit_rows_in_device_candidates(mgp_ctx, n_states):
+    """64 states (<= 16 384 rows of hundreds of variables): a workgroup per row
+    (mgp_fe_cands_rowblock_kernel); 200 states x 256: a thread per row."""
     from tests.fe_emulate import apply_xrows
 
-    states = [c[1] for c in _corpus(64)]
+    states = [c[1] for c in _corpus(n_states)]
     B = F.Batch(states)
     nv = B.n_vars() + 1
     rows, mask, _ = N.decision_rows(*B.packed(), nv, 77, 4, None, state_keys=B.state_key)

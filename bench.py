@@ -452,6 +452,9 @@ def main():
                     "solver_call_reduction": len(cs) / max(1, kinds.count("undecided")), "expectations": expect,
                     "by_contract": {k: dict(v) for k, v in by_shape.items()},
                     "stages_ms": pf.last_profile, "latency": frontend_latency(pf, SV, cs),
+                    "latency_2_by_contract": {
+                        k: frontend_latency(pf, SV, [c for c, lab in zip(cs, labels) if lab.startswith(k)], sizes=(2,))
+                        for k in ("suicide", "bectoken", "wallet")},
                     "shape": "mixed corpus (corpus.py): suicide.sol kill, BECToken.sol batchTransfer, "
                              "WalletLibrary.sol initWallet -> kill"}
         # the same batch, cold, with the first GPU round and the host pre-check only (no

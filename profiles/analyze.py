@@ -136,8 +136,13 @@ def main(d):
     print("\n".join(out))
     # machine-readable traffic figure for bench.py's roofline.traffic (same workload shape only)
     bj = os.path.join(d, "bench_trace.json")
+    keccak_done = False
     for k, t in traffic.items():
         if k in KECCAK64:
+            # the bench's default engine (the hand-allocated kernel) when the run had both
+            if keccak_done or (k != KECCAK64[0] and KECCAK64[0] in traffic):
+                continue
+            keccak_done = True
             t.update({"kernel": k, "source": f"profiles/{os.path.basename(os.path.normpath(d)).replace('prof_', '')}"
                       f"_summary.md (rocprofv3 run {d})"})
             with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "keccak_pmc.json"), "w") as f:

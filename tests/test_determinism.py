@@ -34,7 +34,7 @@ def _digest(states):
     cands = N.make_candidates(64, nv, 11, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off, B.aliases,
                               B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8),
                               var_kind=B.var_kind, state_keys=B.state_key)
-    rows, mask, st = N.decision_rows(*B.packed(), nv, 5, 4, None, state_keys=B.state_key)
+    rows, mask, st = N.decision_rows(*B.packed(decide=True), nv, 5, 4, None, state_keys=B.state_key)
     keys = np.array(B.state_key)
     nvs = np.diff(B.var_off).astype(int)
     B.close()

@@ -576,3 +576,72 @@ def test_exhaustive_soundness_multiplication_shapes(w):
             assert not has_model, "refuted a satisfiable state"
             odd_eq_refuted += any(x[0] == S.EQ and nl[x[2]][0] == S.MUL for x in nl)
     assert refuted > n // 3 and odd_eq_refuted > n // 6, (refuted, odd_eq_refuted, unsat)
+
+
+def _random_store_chain_dag(rng, w=3):
+    """Storage-shaped reads (array.py:16-63 as LASER builds them): Select(Store(Store(a,
+    k1, v1), k2, v2), i) = If(i == k2, v2, If(i == k1, v1, a[i])) with a[i] a UF
+    application of the base array, several reads of one chain at related indices, and
+    constraints on the read values (== / != constants, orderings between reads)."""
+    nl = [[S.VAR, w, -1, -1, -1, v, 0] for v in range(4)]        # k1, k2, i, j
+    cl = [int(rng.integers(0, 1 << w)) for _ in range(3)]
+    nl += [[S.CONST, w, -1, -1, -1, c, 0] for c in range(3)]     # 4, 5, 6
+    vals = [0, 1, 2, 3, 4, 5, 6]
+    n_uf = 0
+
+    def read(idx):
+        nonlocal n_uf
+        nl.append([S.UFAPP, w, idx, -1, -1, 9, 4 + n_uf])       # base read a[idx]: fresh value slot 4+
+        n_uf += 1
+        r = len(nl) - 1
+        for k, v in ((0, 4), (1, 5)):                            # oldest store innermost
+            nl.append([S.EQ, 1, idx, k, -1, 0, 0])
+            nl.append([S.ITE, w, len(nl) - 1, v, r, 0, 0])
+            r = len(nl) - 1
+        return r
+
+    reads = [read(int(rng.choice([2, 3, 0]))) for _ in range(int(rng.integers(2, 4)))]
+    bools = []
+    for _ in range(int(rng.integers(2, 5))):
+        a = int(rng.choice(reads))
+        k = rng.random()
+        if k < 0.4:
+            nl.append([S.EQ, 1, a, int(rng.choice(vals[4:])), -1, 0, 0])
+        elif k < 0.6:
+            nl.append([S.EQ, 1, a, int(rng.choice(reads)), -1, 0, 0])
+        elif k < 0.8:
+            nl.append([S.ULT, 1, a, int(rng.choice(reads + [6])), -1, 0, 0])
+        else:
+            nl.append([S.EQ, 1, int(rng.choice([0, 1, 2, 3])), int(rng.choice([0, 1, 2, 3])), -1, 0, 0])
+        bools.append(len(nl) - 1)
+        if rng.random() < 0.4:
+            nl.append([S.BNOT, 1, bools[-1], -1, -1, 0, 0])
+            bools[-1] = len(nl) - 1
+    root = bools[0]
+    for b in bools[1:]:
+        nl.append([S.BAND, 1, root, b, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl, 4 + n_uf
+
+
+def test_exhaustive_soundness_store_chains():
+    """Read-over-write chains: no refuted state has a model over all
+    assignments of the four index variables and every fresh base-read value (2-bit, C
+    oracle), and the pre-check does refute a share of them (equal indices force equal
+    reads through the ITE chains and UF congruence)."""
+    rng = np.random.default_rng(0x570E)
+    w = 2
+    states = [_random_store_chain_dag(rng, w) for _ in range(240)]
+    verdict = _refute([(nl, cl) for nl, cl, _ in states])
+    refuted = 0
+    for (nl, cl, n_vars), r in zip(states, verdict):
+        assert r in (0, 1)
+        if r != 1:
+            continue
+        refuted += 1
+        grid = np.array(np.meshgrid(*[np.arange(1 << w)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
+        cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+        cands[0, :, :, 0] = grid
+        nodes, noff, consts, coff = pack_states([(nl, cl)])
+        assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
+    assert refuted > 40, refuted

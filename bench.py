@@ -471,6 +471,18 @@ def main():
                                         "unsat": k1.count(SV.unsat), "undecided": k1.count("undecided"),
                                         "solver_call_reduction": len(cs) / max(1, k1.count("undecided")),
                                         "stages_ms": pf.last_profile}
+        # A/B: the same cold batch with the UNSAT-core shrink on a worker thread (a quarter of
+        # the OpenMP threads), then the default policy's result vector is compared
+        SV.unsat_cores().reset()
+        pf._N.program_cache_clear()
+        pf.core_async = True
+        tf = time.perf_counter()
+        res_a = pf.check_states(cs)
+        dta = time.perf_counter() - tf
+        SV.unsat_cores().join()
+        pf.core_async = False
+        frontend["core_async"] = {"seconds": dta, "states_per_s": len(cs) / dta,
+                                  "same_answers": [r[0] for r in res_a] == kinds}
         pf.ctx.close()
         log(f"frontend: {frontend}")
 

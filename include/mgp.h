@@ -56,6 +56,11 @@ void mgp_destroy(mgp_ctx *ctx);
 const char *mgp_last_error(mgp_ctx *ctx); /* ctx may be NULL: global error */
 int mgp_device_count(int *out);
 const char *mgp_version(void);
+/* Host threads of the OpenMP stages started FROM THE CALLING THREAD (lowering, pre-check,
+ * decision rows, ...): n > 0 sets it for this thread only; returns the previous value.
+ * The background UNSAT-core shrink (mythril_amd.solver.UnsatCores) uses it so that it
+ * does not oversubscribe the cores the foreground calls use. */
+int mgp_set_thread_omp(int n);
 
 /* -------------------------------------------------------------- lowering
  * Host-side, no device needed.  Lowers n_states node lists to bytecode.

@@ -86,6 +86,7 @@ def _bind(lib):
         "mgp_probe_valu_dev": (ctypes.c_int, [_U32, _U32, _P, _P, _P]),
         "mgp_set_eval_engine": (ctypes.c_int, [ctypes.c_int]),
         "mgp_set_keccak_engine": (ctypes.c_int, [ctypes.c_int]),
+        "mgp_set_thread_omp": (ctypes.c_int, [ctypes.c_int]),
         "mgp_set_eval_diag": (ctypes.c_int, [_P]),
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
@@ -153,6 +154,7 @@ EXPORTED_SYMBOLS = (
     "mgp_probe_valu_dev",
     "mgp_set_eval_engine",
     "mgp_set_keccak_engine",
+    "mgp_set_thread_omp",
     "mgp_set_eval_diag",
     "mgp_refute",
     "mgp_refute_trace",

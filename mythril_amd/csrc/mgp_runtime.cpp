@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <omp.h>
+
 #include <algorithm>
 #include <string>
 #include <vector>
@@ -148,6 +150,12 @@ int64_t validate_programs(const uint32_t *w, const uint64_t *offs, uint32_t n_st
 extern "C" {
 
 const char *mgp_version(void) { return "mgp 0.1 (gfx950)"; }
+
+int mgp_set_thread_omp(int n) {
+  const int old = omp_get_max_threads();
+  if (n > 0) omp_set_num_threads(n);
+  return old;
+}
 
 int mgp_device_count(int *out) {
   if (!out) return MGP_E_ARG;

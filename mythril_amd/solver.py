@@ -248,6 +248,8 @@ class UnsatCores:
             snap = _ArenaSnapshot(ARENA)  # on this thread: the worker never reads the live arena
 
             def work():
+                # a small OpenMP team: the foreground calls keep the rest of the cores
+                N.lib().mgp_set_thread_omp(max(1, N.lib().mgp_set_thread_omp(0) // 4))
                 cores = UnsatCores.shrink_many(N, pending, arena=snap)
                 with self._lock:
                     if self.gen == gen:

@@ -16,7 +16,8 @@ from typing import Optional, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmgp.so")
+# MGP_LIB_PATH: an alternative build of the same library (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("MGP_LIB_PATH") or os.path.join(_HERE, "libmgp.so")
 
 # include/mgp_ir.h : mgp_node (24 bytes)
 NODE_DTYPE = np.dtype(

@@ -11,7 +11,8 @@ Handlers are straight-line gfx950 code on fixed registers:
 
   VGPR  v0 lane, v1 lane*16 (LDS lane base), v2/v3 candidate byte offsets of
         the two 16-B halves, v4-v7 scratch, vA=v[8:15], vB=v[16:23],
-        vC=v[24:31], T=v[32:63] (product / division temporaries)
+        vC=v[24:31], T=v[32:41] (product / division temporaries), v[42:89]
+        register bank, v[90:94] uop page, v95 loop state; 96 in all
   SGPR  s[4:5] uop pointer, s[6:7] candidate base of the state, s8 bytes per
         variable, s9 n_vars-1, s[10:11] jump table, s[14:15] constant pool,
         s[16:19] current uop C, s[20:23] prefetched uop N, s[24:31] constant
@@ -36,17 +37,33 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from mythril_amd import uop_spec as U  # noqa: E402
 
 KNAME = "mgp_eval_gfx950"
+# The same code under two kernel descriptors that differ only in the VGPR count they
+# reserve: KNAME reserves 128 (4 waves/SIMD), KNAME_W5 96 (5 waves/SIMD; the host picks it
+# per bucket only under MGP_W5_MAX_SLOTS: on the synthetic batch 5 waves/SIMD measured
+# slower).
+KNAME_W5 = "mgp_eval_gfx950_w5"
+# 96 VGPRs (5 waves/SIMD; 128 gave 4): the division keeps its 16-limb dividend in vA:vC and
+# normalises the divisor in vB, so the temporaries shrink to the 10 registers of T
 VA, VB, VC, VT = 8, 16, 24, 32
-RV = 64          # v[64:111]: candidate variables 0..5 of this lane, preloaded at wave start
-PG = 112         # v[112:116]: the current 64-uop page, uop k in lane k (read with v_readlane):
-                 #   v112 first-handler address (low 32 bits), v113 op-handler address, v114-116 w1-w3
-PQ = 118         # v[118:125]: the constant pool, constant c in lane c (CONST_SMEM = False)
+NT = 10          # T = v[32:41]: products / compare scratch; in DIV the f64 and digit registers
+RV = int(os.environ.get("MGP_RV", "42"))  # v[RV:RV+47]: candidate variables 0..5 of this lane, preloaded at wave start
+PG = 90          # v[90:94]: the current 64-uop page, uop k in lane k (read with v_readlane):
+                 #   v90 first-handler address (low 32 bits), v91 op-handler address, v92-94 w1-w3
+VD = 95          # descriptor / loop state / diagnostic lanes (s_ registers above s63 are Bools)
+NVGPR = 96        # registers the code names (KNAME_W5 reserves exactly these)
+DECL_VGPR = 128   # KNAME's reservation
+HALIGN = int(os.environ.get("MGP_HALIGN", "2"))   # log2 byte alignment of handler entries
+# division registers inside T
+D_FA, D_FB = 32, 34          # f64 pairs: dividend / reciprocal, divisor / estimate
+D_M = 36                     # v36 carry into the next product, v37 = 0 (64-bit mad addend)
+D_Q, D_T = 38, 39            # qhat, scratch
+D_K, D_D = (40, 41) if RV == 42 else (88, 89)   # per-lane limb shift k, top-limb difference d
+D_SA, D_SB = "s[32:33]", "s[34:35]"   # operand sign lane masks (SDIV/SREM/SMOD)
 # A v_readlane costs a wave64 ~8.7 SIMD-cycles of VALU issue at 4 waves/SIMD
 # (profiles/contention_probe.hip, contention_r2.json), so a handler reads only the uop
 # fields it uses, and pool constants come through the scalar cache (one s_load_dwordx8
 # instead of 8 readlanes).  The uop stream itself stays in VGPR lanes: read through the
 # scalar cache, every 4th uop missed it (SQC_DCACHE_MISSES) and the step got slower.
-CONST_SMEM = True
 S_KB, S_KH, S_KM = 24, 32, 40
 
 
@@ -107,7 +124,7 @@ def prefetch_next():
     page, computed lane-parallel when the page was loaded) straight into s0; s1 is the
     constant high half of the code address.  s21 = lane of the current uop."""
     A("s_add_u32 s3, s21, 1",
-      "v_readlane_b32 s0, v112, s3")
+      f"v_readlane_b32 s0, {v(PG)}, s3")
 
 
 def read_fields(used):
@@ -118,15 +135,15 @@ def read_fields(used):
 
 
 def page_decode():
-    """v[112:115] raw uop words w0-w3 -> v112/v113 absolute handler addresses (low 32 bits;
-    the prologue checked that the kernel code does not cross a 4 GiB boundary), v114-116 w1-w3."""
-    A("v_mov_b32 v116, v115",
-      "v_mov_b32 v115, v114",
-      "v_mov_b32 v114, v113",
-      "v_lshrrev_b32 v113, 16, v112",
-      "v_lshl_add_u32 v113, v113, 2, s10",
-      "v_and_b32 v112, 0xffff, v112",
-      "v_lshl_add_u32 v112, v112, 2, s10",
+    """v[PG:PG+3] raw uop words w0-w3 -> PG / PG+1 absolute handler addresses (low 32 bits;
+    the prologue checked that the kernel code does not cross a 4 GiB boundary), PG+2..4 w1-w3."""
+    A(f"v_mov_b32 {v(PG + 4)}, {v(PG + 3)}",
+      f"v_mov_b32 {v(PG + 3)}, {v(PG + 2)}",
+      f"v_mov_b32 {v(PG + 2)}, {v(PG + 1)}",
+      f"v_lshrrev_b32 {v(PG + 1)}, 16, {v(PG)}",
+      f"v_lshl_add_u32 {v(PG + 1)}, {v(PG + 1)}, 2, s10",
+      f"v_and_b32 {v(PG)}, 0xffff, {v(PG)}",
+      f"v_lshl_add_u32 {v(PG)}, {v(PG)}, 2, s10",
       "s_nop 1")   # VALU write -> v_readlane of the same VGPR
 
 
@@ -146,7 +163,7 @@ def tail():
 
 def op_target():
     """s[12:13] <- address of the op handler of the current uop (s13 = code high half)."""
-    A("v_readlane_b32 s12, v113, s21")
+    A(f"v_readlane_b32 s12, {v(PG + 1)}, s21")
 
 
 def op_dispatch():
@@ -173,26 +190,27 @@ def copy8(dst, src):
 
 def sext_inplace(base):
     """x = (x ^ H) - H, H = 2^(w-1) in s[32:39] (load_kh first): sign-extends a zero-extended w-bit value.
-    (gfx950 VOP2 carry ops read VCC over the constant bus, so H is copied to v[56:63] first.)"""
+    (gfx950 VOP2 carry ops read VCC over the constant bus, so H is copied to T first.)"""
     sext_to(base, base)
 
 
 def sext_to(dst, src):
     for i in range(8):
-        A(f"v_mov_b32 {v(56 + i)}, {s(S_KH + i)}")
+        A(f"v_mov_b32 {v(VT + i)}, {s(S_KH + i)}")
     for i in range(8):
-        A(f"v_xor_b32 {v(dst + i)}, {v(56 + i)}, {v(src + i)}")
-    A(f"v_sub_co_u32 {v(dst)}, vcc, {v(dst)}, v56")
+        A(f"v_xor_b32 {v(dst + i)}, {v(VT + i)}, {v(src + i)}")
+    A(f"v_sub_co_u32 {v(dst)}, vcc, {v(dst)}, {v(VT)}")
     for i in range(1, 8):
-        A(f"v_subb_co_u32 {v(dst + i)}, vcc, {v(dst + i)}, {v(56 + i)}, vcc")
+        A(f"v_subb_co_u32 {v(dst + i)}, vcc, {v(dst + i)}, {v(VT + i)}, vcc")
 
 
-def cneg(base, mvgpr, tmp):
-    """x = m ? -x : x with m a per-lane all-ones/zero mask in a VGPR."""
+def cneg(base, smask):
+    """x = m ? -x : x with m a lane mask in an SGPR pair (v4, v5 scratch)."""
+    A(f"v_cndmask_b32_e64 v4, 0, -1, {smask}")
     for i in range(8):
-        A(f"v_xor_b32 {v(base + i)}, {v(base + i)}, {v(mvgpr)}")
-    A(f"v_lshrrev_b32 {v(tmp)}, 31, {v(mvgpr)}",
-      f"v_add_co_u32 {v(base)}, vcc, {v(tmp)}, {v(base)}")
+        A(f"v_xor_b32 {v(base + i)}, {v(base + i)}, v4")
+    A("v_lshrrev_b32 v5, 31, v4",
+      f"v_add_co_u32 {v(base)}, vcc, v5, {v(base)}")
     for i in range(1, 8):
         A(f"v_addc_co_u32 {v(base + i)}, vcc, 0, {v(base + i)}, vcc")
 
@@ -332,14 +350,10 @@ B_BCOMB, B_BCOMB_OR = U.F_BCOMB.bit_length() - 1, U.F_BCOMB_OR.bit_length() - 1
 
 
 def load_pool(dst, idx_sreg):
-    """s[dst:dst+7] <- pool entry idx (32 B per entry at s[14:15], or lane idx of PQ)."""
-    if CONST_SMEM:
-        A(f"s_lshl_b32 {idx_sreg}, {idx_sreg}, 5",
-          f"s_load_dwordx8 {sr(dst, 8)}, s[14:15], {idx_sreg}",
-          "s_waitcnt lgkmcnt(0)")
-    else:
-        for i in range(8):
-            A(f"v_readlane_b32 {s(dst + i)}, {v(PQ + i)}, {idx_sreg}")
+    """s[dst:dst+7] <- pool entry idx (32 B per entry at s[14:15])."""
+    A(f"s_lshl_b32 {idx_sreg}, {idx_sreg}, 5",
+      f"s_load_dwordx8 {sr(dst, 8)}, s[14:15], {idx_sreg}",
+      "s_waitcnt lgkmcnt(0)")
 
 
 def load_km():
@@ -501,18 +515,13 @@ def const_issue(which):
     sp = "s51" if which == "A" else "s50"
     ks = S_KB if which == "B" else S_KH
     A(f"s_and_b32 {sp}, s17, 0xffff" if which == "A" else f"s_lshr_b32 {sp}, s17, 16")
-    if CONST_SMEM:
-        A(f"s_lshl_b32 {sp}, {sp}, 5",
-          f"s_load_dwordx8 {sr(ks, 8)}, s[14:15], {sp}")
-    else:
-        for i in range(8):
-            A(f"v_readlane_b32 {s(ks + i)}, {v(PQ + i)}, {sp}")
+    A(f"s_lshl_b32 {sp}, {sp}, 5",
+      f"s_load_dwordx8 {sr(ks, 8)}, s[14:15], {sp}")
 
 
 def const_finish(dst, which):
     ks = S_KB if which == "B" else S_KH
-    if CONST_SMEM:
-        A("s_waitcnt lgkmcnt(0)")
+    A("s_waitcnt lgkmcnt(0)")
     for i in range(8):
         A(f"v_mov_b32 {v(dst + i)}, {s(ks + i)}")
 
@@ -545,18 +554,18 @@ for _f in U.FETCH:
 # ---- program paging
 @handler("PAGE")
 def h_page():
-    # next 64 uops: lane k loads uop min(k, remaining) of the next page into v[112:115]
+    # next 64 uops: lane k loads uop min(k, remaining) of the next page into v[PG:PG+3]
     # (s2 = uops left from the page start; index `remaining` is the INVALID pad)
     A("s_add_u32 s4, s4, 0x400", "s_addc_u32 s5, s5, 0",
       "s_sub_u32 s2, s2, 64",
       "v_min_u32 v4, s2, v0",
       "v_lshlrev_b32 v4, 4, v4",
       "s_waitcnt vmcnt(0)",
-      "global_load_dwordx4 v[112:115], v4, s[4:5]",
+      f"global_load_dwordx4 {vr(PG, 4)}, v4, s[4:5]",
       "s_waitcnt vmcnt(0)",
       "s_mov_b32 s3, 0")
     page_decode()
-    A("v_readlane_b32 s0, v112, s3")
+    A(f"v_readlane_b32 s0, {v(PG)}, s3")
     tail()
 
 
@@ -582,11 +591,11 @@ def diag_stamp():
     dispatch} in shader clocks (32-bit differences)."""
     ln = A.fresh("nodiag")
     A("s_cmp_eq_u32 s20, 0", f"s_cbranch_scc1 {ln}",
-      "v_readlane_b32 s24, v126, 0", "v_readlane_b32 s25, v126, 1",
+      f"v_readlane_b32 s24, {v(VD)}, 0", f"v_readlane_b32 s25, {v(VD)}, 1",
       "s_memtime s[54:55]",
-      "v_readlane_b32 s26, v126, 2", "v_readlane_b32 s27, v126, 7",
-      "v_readlane_b32 s28, v126, 8", "v_readlane_b32 s29, v126, 4",
-      "v_readlane_b32 s30, v126, 6",
+      f"v_readlane_b32 s26, {v(VD)}, 2", f"v_readlane_b32 s27, {v(VD)}, 7",
+      f"v_readlane_b32 s28, {v(VD)}, 8", f"v_readlane_b32 s29, {v(VD)}, 4",
+      f"v_readlane_b32 s30, {v(VD)}, 6",
       "s_lshl_b32 s30, s30, 4", "s_add_u32 s24, s24, s30", "s_addc_u32 s25, s25, 0",
       "s_sub_u32 s26, s27, s26", "s_sub_u32 s27, s28, s27", "s_sub_u32 s28, s29, s28",
       "s_waitcnt lgkmcnt(0)",
@@ -629,11 +638,11 @@ def next_chunk():
     A("s_add_u32 s58, s58, 4",
       "s_addc_u32 s59, s59, 0",
       "s_add_u32 s60, s60, 64",
-      "v_readlane_b32 s49, v126, 15",
-      "v_readlane_b32 s2, v126, 13",
-      "v_readlane_b32 s4, v126, 11",
-      "v_readlane_b32 s5, v126, 12",
-      "v_readlane_b32 s91, v126, 14",
+      f"v_readlane_b32 s49, {v(VD)}, 15",
+      f"v_readlane_b32 s2, {v(VD)}, 13",
+      f"v_readlane_b32 s4, {v(VD)}, 11",
+      f"v_readlane_b32 s5, {v(VD)}, 12",
+      f"v_readlane_b32 s91, {v(VD)}, 14",
       "s_sub_u32 s50, s49, 1",
       "s_lshl_b32 s51, s49, 4",
       # VALU-written SGPRs feed VALU operands and a VMEM base below
@@ -647,7 +656,7 @@ def next_chunk():
       "s_cbranch_scc1 .Lpage0_kept",
       "v_min_u32 v4, s2, v0",
       "v_lshlrev_b32 v4, 4, v4",
-      "global_load_dwordx4 v[112:115], v4, s[4:5]")
+      f"global_load_dwordx4 {vr(PG, 4)}, v4, s[4:5]")
     A.lines.append(var_preload("r").rstrip("\n"))
     page_decode()
     A("s_branch .Lrestart")
@@ -659,7 +668,7 @@ def next_chunk():
       "s_mov_b32 s62, 0",
       "s_mov_b32 s63, 0x41f00000",
       "s_mov_b32 s3, 0",
-      "v_readlane_b32 s0, v112, s3")
+      f"v_readlane_b32 s0, {v(PG)}, s3")
     tail()
 
 
@@ -835,16 +844,23 @@ def mul_low(xa, yb, out):
             A("v_mov_b32 v4, v5", "v_mov_b32 v5, v6", "v_mov_b32 v6, 0")
 
 
-def mul_full(xa, yb, out):
-    """out[0..15] = X*Y (512 bits)."""
+def mul_full(xa, yb, out, hi_or):
+    """out[0..7] = low 256 bits of X*Y, hi_or = OR of the high 256 bits' limbs (!= 0 iff
+    the 512-bit product overflows 256 bits)."""
     A("v_mov_b32 v4, 0", "v_mov_b32 v5, 0", "v_mov_b32 v6, 0")
     for k in range(15):
         for i in range(max(0, k - 7), min(k, 7) + 1):
             j = k - i
             A(f"v_mad_u64_u32 v[4:5], s[48:49], {v(xa + i)}, {v(yb + j)}, v[4:5]",
               "v_addc_co_u32 v6, s[50:51], v6, 0, s[48:49]")
-        A(f"v_mov_b32 {v(out + k)}, v4", "v_mov_b32 v4, v5", "v_mov_b32 v5, v6", "v_mov_b32 v6, 0")
-    A(f"v_mov_b32 {v(out + 15)}, v4")
+        if k < 8:
+            A(f"v_mov_b32 {v(out + k)}, v4")
+        elif k == 8:
+            A(f"v_mov_b32 {v(hi_or)}, v4")
+        else:
+            A(f"v_or_b32 {v(hi_or)}, {v(hi_or)}, v4")
+        A("v_mov_b32 v4, v5", "v_mov_b32 v5, v6", "v_mov_b32 v6, 0")
+    A(f"v_or_b32 {v(hi_or)}, {v(hi_or)}, v4")
 
 
 @handler("MUL")
@@ -1064,10 +1080,11 @@ def make_cmp(base, xreg):
             slt_chain(x, y)
             A(f"s_branch {ldone}")
             A.label(lsx)
+            # X (vA or vC) sign-extended into vC (vA stays the accumulator), Y in place
             load_kh()
-            sext_to(40, X)
-            sext_to(48, Y)
-            x, y = (40, 48) if base == "SLT" else (48, 40)
+            sext_to(VC, X)
+            sext_to(VB, Y)
+            x, y = (VC, VB) if base == "SLT" else (VB, VC)
             slt_chain(x, y)
             A.label(ldone)
         elif base == "UADDNO256":
@@ -1079,25 +1096,24 @@ def make_cmp(base, xreg):
             A(f"v_add_co_u32 {v(VT)}, vcc, {v(X)}, {v(Y)}")
             for i in range(1, 8):
                 A(f"v_addc_co_u32 {v(VT + i)}, vcc, {v(X + i)}, {v(Y + i)}, vcc")
-            # raw = M < sum
+            # raw = M < sum (M copied into vB: operand B is dead once the sum is formed)
             for i in range(8):
-                A(f"v_mov_b32 {v(40 + i)}, {s(S_KM + i)}")
-            A(f"v_sub_co_u32 v4, vcc, v40, {v(VT)}")
+                A(f"v_mov_b32 {v(VB + i)}, {s(S_KM + i)}")
+            A(f"v_sub_co_u32 v4, vcc, {v(VB)}, {v(VT)}")
             for i in range(1, 8):
-                A(f"v_subb_co_u32 v4, vcc, {v(40 + i)}, {v(VT + i)}, vcc")
+                A(f"v_subb_co_u32 v4, vcc, {v(VB + i)}, {v(VT + i)}, vcc")
         elif base in ("UMULNO256", "UMULNOW"):
             if base == "UMULNOW":
                 load_km()
-            mul_full(X, Y, VT)
-            or_reduce(VT + 8, range(VT + 8, VT + 16))
-            A(f"v_cmp_ne_u32 vcc, 0, {v(VT + 8)}")
+            mul_full(X, Y, VT, 7)
+            A("v_cmp_ne_u32 vcc, 0, v7")
             if base == "UMULNOW":
                 A("s_mov_b64 s[52:53], vcc")
                 for i in range(8):
-                    A(f"v_mov_b32 {v(48 + i)}, {s(S_KM + i)}")
-                A(f"v_sub_co_u32 v4, vcc, v48, {v(VT)}")
+                    A(f"v_mov_b32 {v(VB + i)}, {s(S_KM + i)}")
+                A(f"v_sub_co_u32 v4, vcc, {v(VB)}, {v(VT)}")
                 for i in range(1, 8):
-                    A(f"v_subb_co_u32 v4, vcc, {v(48 + i)}, {v(VT + i)}, vcc")
+                    A(f"v_subb_co_u32 v4, vcc, {v(VB + i)}, {v(VT + i)}, vcc")
                 A("s_or_b64 vcc, vcc, s[52:53]")
         cmp_epilogue()
     return _
@@ -1109,16 +1125,17 @@ for _c in U.CMPS:
 
 
 # ---- division (Knuth D, 32-bit digits)
-UQ = 32          # u[0..15] = v[32:47]; q digit J is stored into u[J+8]
-VN = 48          # normalised divisor v[48:55]
+# The 16-limb working dividend u is vA (u[0..7]) : vC (u[8..15]); quotient digit J is stored
+# into u[J+8].  The normalised divisor is formed in place in vB (the single-digit path keeps
+# vB as it is).  f64, qhat and the digit bookkeeping live in T (D_* registers).
 
 
 def u(i):
-    return v(UQ + i)
+    return v(VA + i) if i < 8 else v(VC + i - 8)
 
 
 def vn(i):
-    return v(VN + i)
+    return v(VB + i)
 
 
 def knuth_digit(J):
@@ -1132,50 +1149,52 @@ def knuth_digit(J):
     makes the multiply-subtract go negative: one add-back, taken by a wave only when one
     of its lanes sits within 2^-12 of the next integer.
     """
-    A(f"v_cvt_f64_u32 v[30:31], {u(J + 8)}",
+    E, R = vr(D_FB, 2), vr(D_FA, 2)
+    A(f"v_cvt_f64_u32 {E}, {u(J + 8)}",
       f"v_cvt_f64_u32 v[4:5], {u(J + 7)}",
       f"v_cvt_f64_u32 v[6:7], {u(J + 6)}",
-      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",
-      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[6:7]",
-      "v_fma_f64 v[30:31], v[30:31], v[28:29], s[28:29]",
-      "v_cvt_u32_f64 v60, v[30:31]",
+      f"v_fma_f64 {E}, {E}, s[62:63], v[4:5]",
+      f"v_fma_f64 {E}, {E}, s[62:63], v[6:7]",
+      f"v_fma_f64 {E}, {E}, {R}, s[28:29]",
+      f"v_cvt_u32_f64 {v(D_Q)}, {E}",
       # lanes whose digit J is zero (J > d = top limb(a) - top limb(b), or not dividing;
       # vcc from the caller's skip test) take qhat = 0.  Every lane left has
       # top limb(b) <= 7 - J, so its normalised divisor has vn[i] = 0 for i < J: the
       # products and the subtraction only involve vn[J..7] and u[2J..J+8]
-      "v_cndmask_b32 v60, 0, v60, vcc")
-    msub_digit(J, VN)
+      f"v_cndmask_b32 {v(D_Q)}, 0, {v(D_Q)}, vcc")
+    msub_digit(J, VB)
 
 
 def msub_digit(J, dv):
-    """u[2J..J+8] -= qhat (v60) * d[J..7] (d = v[dv:dv+8]); one add-back when it goes
+    """u[2J..J+8] -= qhat (D_Q) * d[J..7] (d = v[dv:dv+8]); one add-back when it goes
     negative (qhat = q + 1), then u[J+8] <- the digit."""
     # u[2J..J+8] -= qhat * vn[J..7]: one multiply-accumulate chain, the high half of each
     # product (+ carry) entering the next as its 64-bit addend (qhat * vn[i] + c < 2^64),
     # interleaved with the borrow chain of the subtraction (VCC).  Per limb: mad + mov +
     # subb, against mad + add + subb with independent products (carry ops issue at half
     # the rate of a mov)
-    A("v_mov_b32 v63, 0",
-      f"v_mad_u64_u32 v[4:5], s[50:51], v60, {v(dv + J)}, 0",
+    q, t, m = v(D_Q), v(D_T), vr(D_M, 2)
+    A(f"v_mov_b32 {v(D_M + 1)}, 0",
+      f"v_mad_u64_u32 v[4:5], s[50:51], {q}, {v(dv + J)}, 0",
       f"v_sub_co_u32 {u(2 * J)}, vcc, {u(2 * J)}, v4")
     for i in range(J + 1, 8):
-        A("v_mov_b32 v62, v5",
-          f"v_mad_u64_u32 v[4:5], s[50:51], v60, {v(dv + i)}, v[62:63]",
+        A(f"v_mov_b32 {v(D_M)}, v5",
+          f"v_mad_u64_u32 v[4:5], s[50:51], {q}, {v(dv + i)}, {m}",
           f"v_subb_co_u32 {u(J + i)}, vcc, {u(J + i)}, v4, vcc")
     A(f"v_subb_co_u32 {u(J + 8)}, vcc, {u(J + 8)}, v5, vcc")
     lno = A.fresh("noaddback")
     A("s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lno}",
       "s_mov_b64 s[50:51], vcc",
-      "v_subb_co_u32 v60, s[48:49], v60, 0, s[50:51]")
+      f"v_subb_co_u32 {q}, s[48:49], {q}, 0, s[50:51]")
     for i in range(J, 8):
-        A(f"v_cndmask_b32_e64 v61, 0, {v(dv + i)}, s[50:51]")
+        A(f"v_cndmask_b32_e64 {t}, 0, {v(dv + i)}, s[50:51]")
         if i == J:
-            A(f"v_add_co_u32 {u(J + i)}, vcc, v61, {u(J + i)}")
+            A(f"v_add_co_u32 {u(J + i)}, vcc, {t}, {u(J + i)}")
         else:
-            A(f"v_addc_co_u32 {u(J + i)}, vcc, v61, {u(J + i)}, vcc")
+            A(f"v_addc_co_u32 {u(J + i)}, vcc, {t}, {u(J + i)}, vcc")
     A(f"v_addc_co_u32 {u(J + 8)}, vcc, 0, {u(J + 8)}, vcc")
     A.label(lno)
-    A(f"v_mov_b32 {u(J + 8)}, v60")
+    A(f"v_mov_b32 {u(J + 8)}, {q}")
 
 
 def single_digit():
@@ -1188,24 +1207,25 @@ def single_digit():
     rounding.  So a_f / b_f is within 2^-48 relative, 2^-16 absolute (q < 2^32), of a / b,
     and with the 2^-12 bias qhat is q or q + 1 (v_cvt_u32_f64 clamps 2^32 to q): at most
     one add-back in msub_digit.  Non-dividing lanes take qhat = 0 (u[0..8] stays a, 0)."""
+    FA, FB = vr(D_FA, 2), vr(D_FB, 2)
     A("s_mov_b32 s62, 0", "s_mov_b32 s63, 0x41f00000",      # 2^32
       "s_mov_b32 s28, 0", "s_mov_b32 s29, 0x3f300000",      # 2^-12 (qhat bias)
-      f"v_cvt_f64_u32 v[28:29], {u(7)}",
-      f"v_cvt_f64_u32 v[30:31], {v(VB + 7)}")
+      f"v_cvt_f64_u32 {FA}, {u(7)}",
+      f"v_cvt_f64_u32 {FB}, {v(VB + 7)}")
     for i in range(6, -1, -1):
         A(f"v_cvt_f64_u32 v[4:5], {u(i)}",
           f"v_cvt_f64_u32 v[6:7], {v(VB + i)}",
-          "v_fma_f64 v[28:29], v[28:29], s[62:63], v[4:5]",
-          "v_fma_f64 v[30:31], v[30:31], s[62:63], v[6:7]")
-    A("v_rcp_f64 v[6:7], v[30:31]",
+          f"v_fma_f64 {FA}, {FA}, s[62:63], v[4:5]",
+          f"v_fma_f64 {FB}, {FB}, s[62:63], v[6:7]")
+    A(f"v_rcp_f64 v[6:7], {FB}",
       "s_nop 1",
-      "v_fma_f64 v[4:5], -v[30:31], v[6:7], 1.0",
+      f"v_fma_f64 v[4:5], -{FB}, v[6:7], 1.0",
       "v_fma_f64 v[6:7], v[6:7], v[4:5], v[6:7]",
-      "v_fma_f64 v[4:5], -v[30:31], v[6:7], 1.0",
+      f"v_fma_f64 v[4:5], -{FB}, v[6:7], 1.0",
       "v_fma_f64 v[6:7], v[6:7], v[4:5], v[6:7]",
-      "v_fma_f64 v[4:5], v[28:29], v[6:7], s[28:29]",
-      "v_cvt_u32_f64 v60, v[4:5]",
-      "v_cndmask_b32_e64 v60, 0, v60, s[24:25]")
+      f"v_fma_f64 v[4:5], {FA}, v[6:7], s[28:29]",
+      f"v_cvt_u32_f64 {v(D_Q)}, v[4:5]",
+      f"v_cndmask_b32_e64 {v(D_Q)}, 0, {v(D_Q)}, s[24:25]")
     msub_digit(0, VB)
 
 
@@ -1219,127 +1239,124 @@ def h_div():
     sext_inplace(VB)
     A.label(maybe_sext_op)
     lus, lsd = A.fresh("udiv"), A.fresh("sdone")
+    # operand signs as lane masks D_SA / D_SB (s[32:35]: the sign constant is no longer needed)
     A(f"s_bfe_u32 s61, s18, {(3 << 16) | U.DIVOP_POS:#x}",
       "s_cmp_lt_u32 s61, 2", f"s_cbranch_scc1 {lus}",
-      f"v_ashrrev_i32 v24, 31, {v(VA + 7)}",
-      f"v_ashrrev_i32 v25, 31, {v(VB + 7)}")
-    cneg(VA, 24, 61)
-    cneg(VB, 25, 61)
+      f"v_cmp_gt_i32_e64 {D_SA}, 0, {v(VA + 7)}",
+      f"v_cmp_gt_i32_e64 {D_SB}, 0, {v(VB + 7)}")
+    cneg(VA, D_SA)
+    cneg(VB, D_SB)
     A(f"s_branch {lsd}")
     A.label(lus)
-    A("v_mov_b32 v24, 0", "v_mov_b32 v25, 0")
+    A(f"s_mov_b64 {D_SA}, 0", f"s_mov_b64 {D_SB}, 0")
     A.label(lsd)
     # divides = b != 0 && a >= b, first: a wave where no lane divides skips everything else
-    or_reduce(61, range(VB, VB + 8))
-    A("v_cmp_ne_u32_e64 s[26:27], 0, v61")             # bnz
-    ult_chain(VA, VB, tmp=62)
+    or_reduce(D_T, range(VB, VB + 8))
+    A(f"v_cmp_ne_u32_e64 s[26:27], 0, {v(D_T)}")       # bnz
+    ult_chain(VA, VB, tmp=D_T)
     A("s_andn2_b64 s[24:25], s[26:27], vcc")
     lpost = A.fresh("divpost")
-    # u[0..7] = a: the remainder of a lane that does not divide (its shift is 0 and every
-    # digit of it is forced to 0, so u[0..7] stays a); vA is then free as product scratch
-    copy8(UQ, VA)
+    # u[0..7] = vA = a: the remainder of a lane that does not divide (its shift is 0 and
+    # every digit of it is forced to 0, so u[0..7] stays a)
     A("s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {lpost}")
     for i in range(8, 16):
         A(f"v_mov_b32 {u(i)}, 0")
     # d = top limb(a) - top limb(b) (-1 when not dividing): digits J > d are zero
-    top_limb(VB, 59)
-    top_limb(VA, 27)
-    A("v_sub_u32 v27, v27, v59",
-      "v_cndmask_b32_e64 v27, -1, v27, s[24:25]",
-      "v_sub_u32 v26, 7, v59",                         # k = 7 - top limb(b) limbs
-      "v_cndmask_b32_e64 v26, 0, v26, s[24:25]")
+    K, D = v(D_K), v(D_D)
+    top_limb(VB, D_K)
+    top_limb(VA, D_D)
+    A(f"v_sub_u32 {D}, {D}, {K}",
+      f"v_cndmask_b32_e64 {D}, -1, {D}, s[24:25]",
+      f"v_sub_u32 {K}, 7, {K}",                        # k = 7 - top limb(b) limbs
+      f"v_cndmask_b32_e64 {K}, 0, {K}, s[24:25]")
     # single-digit waves (d <= 0 on every lane: 47 % of the executed DIVs on the synthetic
     # batch) skip the normalisation and the remainder shift
     lmulti, lnorem = A.fresh("multidig"), A.fresh("norem")
-    A("v_cmp_lt_i32 vcc, 0, v27", "s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc0 {lmulti}")
+    A(f"v_cmp_lt_i32 vcc, 0, {D}", "s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc0 {lmulti}")
     single_digit()
     A(f"s_branch {lnorem}")
     A.label(lmulti)
-    # limb normalisation: vn = b << 32k, u = a << 32k (vn7 != 0 on dividing lanes; no bit
-    # shift is needed because qhat is estimated from the top three limbs of vn)
-    copy8(VN, VB)
-    limb_masks(26)
-    shl_limbs(list(range(VN, VN + 8)), 8)
-    shl_limbs(list(range(UQ, UQ + 16)), 8)
+    # limb normalisation in place: vn = b << 32k, u = a << 32k (vn7 != 0 on dividing lanes;
+    # no bit shift is needed because qhat is estimated from the top three limbs of vn)
+    limb_masks(D_K)
+    shl_limbs(list(range(VB, VB + 8)), 8)
+    shl_limbs([VA + i for i in range(8)] + [VC + i for i in range(8)], 8)
     # 2^32 / V3, V3 = vn7*2^64 + vn6*2^32 + vn5, in double precision (rcp + two Newton steps)
+    E, R = vr(D_FB, 2), vr(D_FA, 2)
     A("s_mov_b32 s62, 0", "s_mov_b32 s63, 0x41f00000",      # 2^32
       "s_mov_b32 s28, 0", "s_mov_b32 s29, 0x3f300000",      # 2^-12 (qhat bias)
-      f"v_cvt_f64_u32 v[30:31], {vn(7)}",
+      f"v_cvt_f64_u32 {E}, {vn(7)}",
       f"v_cvt_f64_u32 v[4:5], {vn(6)}",
       f"v_cvt_f64_u32 v[6:7], {vn(5)}",
-      "v_fma_f64 v[30:31], v[30:31], s[62:63], v[4:5]",
+      f"v_fma_f64 {E}, {E}, s[62:63], v[4:5]",
       "v_mov_b32 v4, 0", "v_mov_b32 v5, 0x3df00000",         # 2^-32
-      "v_fma_f64 v[30:31], v[6:7], v[4:5], v[30:31]",      # V3 / 2^32
-      "v_rcp_f64 v[28:29], v[30:31]",
+      f"v_fma_f64 {E}, v[6:7], v[4:5], {E}",               # V3 / 2^32
+      f"v_rcp_f64 {R}, {E}",
       "s_nop 1",
-      "v_fma_f64 v[4:5], -v[30:31], v[28:29], 1.0",
-      "v_fma_f64 v[28:29], v[28:29], v[4:5], v[28:29]",
-      "v_fma_f64 v[4:5], -v[30:31], v[28:29], 1.0",
-      "v_fma_f64 v[28:29], v[28:29], v[4:5], v[28:29]")
+      f"v_fma_f64 v[4:5], -{E}, {R}, 1.0",
+      f"v_fma_f64 {R}, {R}, v[4:5], {R}",
+      f"v_fma_f64 v[4:5], -{E}, {R}, 1.0",
+      f"v_fma_f64 {R}, {R}, v[4:5], {R}")
     for J in range(7, -1, -1):
         lskip = A.fresh(f"skipdig{J}")
-        A(f"v_cmp_le_i32 vcc, {J}, v27",
+        A(f"v_cmp_le_i32 vcc, {J}, {D}",
           "s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc1 {lskip}")
         knuth_digit(J)
         A.label(lskip)
-    # remainder = u[0..7] >> 32k  (only UREM/SREM/SMOD need it)
+    # remainder = u[0..7] >> 32k (only UREM/SREM/SMOD need it); SMOD also needs |b| back
+    # from the normalised divisor
+    lnob = A.fresh("nob")
     A("s_cmp_eq_u32 s61, 0", f"s_cbranch_scc1 {lnorem}",
       "s_cmp_eq_u32 s61, 2", f"s_cbranch_scc1 {lnorem}")
-    limb_masks(26)
-    shr_limbs(list(range(UQ, UQ + 8)))
+    limb_masks(D_K)
+    shr_limbs(list(range(VA, VA + 8)))
+    A("s_cmp_lg_u32 s61, 4", f"s_cbranch_scc1 {lnob}")
+    shr_limbs(list(range(VB, VB + 8)))
+    A.label(lnob)
     A.label(lnorem)
     A.label(lpost)
     # per lane: dividing -> (q = u[8..15], r = u[0..7]); else q = (b == 0 ? ~0 : 0), r = u[0..7] = a
-    A("v_cndmask_b32_e64 v61, -1, 0, s[26:27]")
+    A(f"v_cndmask_b32_e64 {v(D_T)}, -1, 0, s[26:27]")
     for i in range(8):
-        A(f"v_cndmask_b32_e64 {u(8 + i)}, v61, {u(8 + i)}, s[24:25]")
-    # result by variant: 0 UDIV, 1 UREM, 2 SDIV, 3 SREM, 4 SMOD
-    l_r, l_sd, l_sr, l_end = A.fresh("rem"), A.fresh("sdiv"), A.fresh("srem"), A.fresh("divend")
-    A("s_cmp_eq_u32 s61, 1", f"s_cbranch_scc1 {l_r}",
+        A(f"v_cndmask_b32_e64 {u(8 + i)}, {v(D_T)}, {u(8 + i)}, s[24:25]")
+    # result by variant: 0 UDIV, 1 UREM, 2 SDIV, 3 SREM, 4 SMOD (the remainder is vA already)
+    l_sd, l_sr, l_end = A.fresh("sdiv"), A.fresh("srem"), A.fresh("divend")
+    A("s_cmp_eq_u32 s61, 1", f"s_cbranch_scc1 {l_end}",
       "s_cmp_eq_u32 s61, 2", f"s_cbranch_scc1 {l_sd}",
       "s_cmp_eq_u32 s61, 3", f"s_cbranch_scc1 {l_sr}",
       "s_cmp_eq_u32 s61, 4", f"s_cbranch_scc1 {l_end}_smod")
-    copy8(VA, UQ + 8)                                 # UDIV
-    A(f"s_branch {l_end}")
-    A.label(l_r)
-    copy8(VA, UQ)
+    copy8(VA, VC)                                     # UDIV
     A(f"s_branch {l_end}")
     A.label(l_sd)
-    copy8(VA, UQ + 8)
-    A("v_xor_b32 v24, v24, v25")
-    cneg(VA, 24, 61)
+    copy8(VA, VC)
+    A(f"s_xor_b64 {D_SA}, {D_SA}, {D_SB}")
+    cneg(VA, D_SA)
     A(f"s_branch {l_end}")
     A.label(l_sr)
-    copy8(VA, UQ)
-    cneg(VA, 24, 61)
+    cneg(VA, D_SA)
     A(f"s_branch {l_end}")
     A.label(f"{l_end}_smod")
-    # r = |a| mod |b| in u[0..7], |b| in vB; sign follows the divisor
-    copy8(VA, UQ)
-    or_reduce(61, range(UQ, UQ + 8))
-    A("v_cmp_ne_u32_e64 s[48:49], 0, v61",             # r != 0
-      "v_cmp_ne_u32_e64 s[50:51], 0, v24",             # sa
-      "v_cmp_ne_u32_e64 s[52:53], 0, v25",             # sb
-      "s_and_b64 s[50:51], s[50:51], s[48:49]",
-      "s_and_b64 s[52:53], s[52:53], s[48:49]",
+    # r = |a| mod |b| in vA, |b| in vB; the sign follows the divisor (candidates in vC)
+    or_reduce(D_T, range(VA, VA + 8))
+    A(f"v_cmp_ne_u32_e64 s[48:49], 0, {v(D_T)}",       # r != 0
+      f"s_and_b64 s[50:51], {D_SA}, s[48:49]",         # sa
+      f"s_and_b64 s[52:53], {D_SB}, s[48:49]",         # sb
       "s_andn2_b64 s[54:55], s[50:51], s[52:53]",       # sa & !sb & r != 0 -> |b| - r
       "s_andn2_b64 s[48:49], s[52:53], s[50:51]",       # !sa & sb & r != 0 -> r - |b|
       "s_and_b64 s[50:51], s[50:51], s[52:53]")         # sa & sb & r != 0 -> -r
-    A(f"v_sub_co_u32 {vn(0)}, vcc, {v(VB)}, {u(0)}")
+    A(f"v_sub_co_u32 {v(VC)}, vcc, {v(VB)}, {v(VA)}")
     for i in range(1, 8):
-        A(f"v_subb_co_u32 {vn(i)}, vcc, {v(VB + i)}, {u(i)}, vcc")
-    for i in range(8):
-        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {vn(i)}, s[54:55]")
-    A(f"v_sub_co_u32 {vn(0)}, vcc, {u(0)}, {v(VB)}")
+        A(f"v_subb_co_u32 {v(VC + i)}, vcc, {v(VB + i)}, {v(VA + i)}, vcc")
+    A(f"v_sub_co_u32 {v(VT)}, vcc, {v(VA)}, {v(VB)}")
     for i in range(1, 8):
-        A(f"v_subb_co_u32 {vn(i)}, vcc, {u(i)}, {v(VB + i)}, vcc")
-    for i in range(8):
-        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {vn(i)}, s[48:49]")
-    A(f"v_sub_co_u32 {vn(0)}, vcc, 0, {u(0)}")
+        A(f"v_subb_co_u32 {v(VT + i)}, vcc, {v(VA + i)}, {v(VB + i)}, vcc")
+    A(f"v_sub_co_u32 {v(VB)}, vcc, 0, {v(VA)}")       # -r (|b| is no longer needed)
     for i in range(1, 8):
-        A(f"v_subb_co_u32 {vn(i)}, vcc, 0, {u(i)}, vcc")
+        A(f"v_subb_co_u32 {v(VB + i)}, vcc, 0, {v(VA + i)}, vcc")
     for i in range(8):
-        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {vn(i)}, s[50:51]")
+        A(f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {v(VC + i)}, s[54:55]",
+          f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {v(VT + i)}, s[48:49]",
+          f"v_cndmask_b32_e64 {v(VA + i)}, {v(VA + i)}, {v(VB + i)}, s[50:51]")
     A.label(l_end)
     bv_epilogue()
 
@@ -1368,19 +1385,6 @@ for _x in U.XC_OPS:
 
 
 # ---------------------------------------------------------------- kernel
-
-POOL_LOAD = """\
-  // VGPR pool (CONST_SMEM = False): v[118:125], lane c = constant min(c, n_pool-1)
-  s_and_b32 s93, s91, 0xff
-  s_cmp_eq_u32 s93, 0
-  s_cbranch_scc1 .Lno_pool
-  s_sub_u32 s92, s93, 1
-  v_min_u32 v4, s92, v0
-  v_lshlrev_b32 v4, 5, v4
-  global_load_dwordx4 v[118:121], v4, s[14:15]
-  global_load_dwordx4 v[122:125], v4, s[14:15] offset:16
-.Lno_pool:
-"""
 
 PROLOGUE = """\
   s_memtime s[96:97]
@@ -1485,7 +1489,7 @@ PROLOGUE = """\
   v_min_u32 v4, s2, v0
   v_lshlrev_b32 v4, 4, v4
   global_load_dwordx4 v[112:115], v4, s[4:5]
-{POOL_LOAD}  // preload variables 0..min(n_vars, 6)-1 of this lane's candidate into v[64:111]
+  // preload variables 0..min(n_vars, 6)-1 of this lane's candidate into the register bank
   // s[10:11] = kernel entry address: uops hold handler offsets / 4 from it.  Handler
   // addresses are formed as 32-bit sums: a code object crossing a 4 GiB boundary (never
   // seen; would need the loader to place it there) makes every wave report undecided.
@@ -1534,29 +1538,30 @@ KARGS = [("desc", 8, "global_buffer"), ("cands", 8, "global_buffer"), ("partial"
 
 
 def metadata():
-    out = ["amdhsa.kernels:", "  - .args:"]
-    off = 0
-    for name, size, kind in KARGS:
-        out.append(f"      - .name: {name}")
-        if kind == "global_buffer":
-            out.append("        .address_space: global")
-        out += [f"        .offset: {off}", f"        .size: {size}", f"        .value_kind: {kind}"]
-        off += size
-    ksize = (off + 7) // 8 * 8
-    out += [
-        "    .group_segment_fixed_size: 0",
-        "    .kernarg_segment_align: 8",
-        f"    .kernarg_segment_size: {ksize}",
-        "    .max_flat_workgroup_size: 64",
-        f"    .name: {KNAME}",
-        "    .private_segment_fixed_size: 0",
-        "    .sgpr_count: 104",
-        f"    .symbol: {KNAME}.kd",
-        "    .vgpr_count: 128",
-        "    .wavefront_size: 64",
-        "amdhsa.target: amdgcn-amd-amdhsa--gfx950",
-        "amdhsa.version:", "  - 1", "  - 2",
-    ]
+    out = ["amdhsa.kernels:"]
+    for kname, nv in ((KNAME, DECL_VGPR), (KNAME_W5, NVGPR)):
+        out.append("  - .args:")
+        off = 0
+        for name, size, kind in KARGS:
+            out.append(f"      - .name: {name}")
+            if kind == "global_buffer":
+                out.append("        .address_space: global")
+            out += [f"        .offset: {off}", f"        .size: {size}", f"        .value_kind: {kind}"]
+            off += size
+        ksize = (off + 7) // 8 * 8
+        out += [
+            "    .group_segment_fixed_size: 0",
+            "    .kernarg_segment_align: 8",
+            f"    .kernarg_segment_size: {ksize}",
+            "    .max_flat_workgroup_size: 64",
+            f"    .name: {kname}",
+            "    .private_segment_fixed_size: 0",
+            "    .sgpr_count: 104",
+            f"    .symbol: {kname}.kd",
+            f"    .vgpr_count: {nv}",
+            "    .wavefront_size: 64",
+        ]
+    out += ["amdhsa.target: amdgcn-amd-amdhsa--gfx950", "amdhsa.version:", "  - 1", "  - 2"]
     return "\n".join(out), ksize
 
 
@@ -1585,16 +1590,17 @@ def generate() -> str:
     first = Asm()
     global_A = A
     globals()["A"] = first
-    A("v_readlane_b32 s0, v112, s3")
+    A(f"v_readlane_b32 s0, {v(PG)}, s3")
     tail()
     globals()["A"] = global_A
     dec = Asm()
     globals()["A"] = dec
     page_decode()
     globals()["A"] = global_A
-    pool = "" if CONST_SMEM else POOL_LOAD
-    A.lines.append(PROLOGUE.replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
-                   .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n").replace("{POOL_LOAD}", pool))
+    pro = (PROLOGUE.replace("v126", v(VD)).replace("v[112:115]", vr(PG, 4))
+           .replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
+           .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n"))
+    A.lines.append(pro)
     no_prefetch = set(U.FETCH) | set(U.XS_OPS) | set(U.XC_OPS) | {"INVALID", "RET", "PAGE"}
     wait = "  s_waitcnt vmcnt(0) lgkmcnt(0)"
     for name in U.HANDLERS:
@@ -1612,7 +1618,7 @@ def generate() -> str:
         A.n = body.n
         lines = body.lines
         used = {f for f in (17, 18, 19) if any(re.search(rf"\bs{f}\b|\bs\[{f}:|\bs\[\d+:{f}\]", l) for l in lines)}
-        A.lines.append(f".p2align 2\nmgp_h_{name}:")
+        A.lines.append(f".p2align {HALIGN}\nmgp_h_{name}:")
         if name not in no_prefetch and lines and lines[0] == wait:
             A.lines.append(wait)
             lines = lines[1:]
@@ -1626,33 +1632,41 @@ def generate() -> str:
         '.amdgcn_target "amdgcn-amd-amdhsa--gfx950"',
         ".text",
         f".globl {KNAME}",
+        f".globl {KNAME_W5}",
         ".p2align 8",
         f".type {KNAME},@function",
+        f".type {KNAME_W5},@function",
         f"{KNAME}:",
+        f"{KNAME_W5}:",
     ]
+    def kd(kname, nv):
+        return [
+            ".rodata",
+            ".p2align 6",
+            f".amdhsa_kernel {kname}",
+            "  .amdhsa_group_segment_fixed_size 0",
+            "  .amdhsa_private_segment_fixed_size 0",
+            f"  .amdhsa_kernarg_size {ksize}",
+            "  .amdhsa_user_sgpr_count 2",
+            "  .amdhsa_user_sgpr_kernarg_segment_ptr 1",
+            "  .amdhsa_system_sgpr_workgroup_id_x 1",
+            "  .amdhsa_system_sgpr_workgroup_id_y 1",
+            "  .amdhsa_system_vgpr_workitem_id 0",
+            f"  .amdhsa_next_free_vgpr {nv}",
+            "  .amdhsa_next_free_sgpr 102",
+            f"  .amdhsa_accum_offset {nv}",
+            "  .amdhsa_reserve_vcc 1",
+            "  .amdhsa_float_denorm_mode_32 3",
+            "  .amdhsa_float_denorm_mode_16_64 3",
+            ".end_amdhsa_kernel",
+            "",
+        ]
     tail_ = [
         ".Lfunc_end:",
         f".size {KNAME}, .Lfunc_end-{KNAME}",
+        f".size {KNAME_W5}, .Lfunc_end-{KNAME_W5}",
         "",
-        ".rodata",
-        ".p2align 6",
-        f".amdhsa_kernel {KNAME}",
-        "  .amdhsa_group_segment_fixed_size 0",
-        "  .amdhsa_private_segment_fixed_size 0",
-        f"  .amdhsa_kernarg_size {ksize}",
-        "  .amdhsa_user_sgpr_count 2",
-        "  .amdhsa_user_sgpr_kernarg_segment_ptr 1",
-        "  .amdhsa_system_sgpr_workgroup_id_x 1",
-        "  .amdhsa_system_sgpr_workgroup_id_y 1",
-        "  .amdhsa_system_vgpr_workitem_id 0",
-        "  .amdhsa_next_free_vgpr 128",
-        "  .amdhsa_next_free_sgpr 102",
-        "  .amdhsa_accum_offset 128",
-        "  .amdhsa_reserve_vcc 1",
-        "  .amdhsa_float_denorm_mode_32 3",
-        "  .amdhsa_float_denorm_mode_16_64 3",
-        ".end_amdhsa_kernel",
-        "",
+    ] + kd(KNAME, DECL_VGPR) + kd(KNAME_W5, NVGPR) + [
         ".amdgpu_metadata",
         "---",
         md,

@@ -56,7 +56,7 @@ vC (operand A of a compare that is not the accumulator); Bool slots are
 
 # operand kinds: acc = the accumulator vA, slot = per-lane LDS slot, var = candidate
 # variable loaded from HBM, const = constant pool (scalar load), rvar = candidate
-# variable 0..REG_VARS-1 preloaded into v[64:111] at wave start (GPR-index moves)
+# variable 0..REG_VARS-1 preloaded into the register bank v[42:89] at wave start (GPR-index moves)
 KINDS = ("acc", "slot", "var", "const", "rvar")
 REG_VARS = 6
 B_KINDS = ("none",) + KINDS

@@ -10,6 +10,8 @@ properties the GPU run depends on hold by construction:
     offsets the library's translator uses;
   * no scalar-memory writes anywhere (results go out through vector stores);
   * 64-bit VGPR operands are even-aligned (gfx950 register-tuple rule);
+  * no instruction names a VGPR at or past the kernel's declared VGPR count (the bank's
+    GPR-index offsets included);
   * the file assembles for gfx950 with the ROCm LLVM assembler.
 """
 import os
@@ -95,6 +97,35 @@ def test_vgpr_pairs_even_aligned(asm):
                 assert int(a) % 2 == 0, l
 
 
+def _gen_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_eval_asm", GEN)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+G = _gen_module()
+
+
+def test_vgprs_within_the_declared_count(asm):
+    from mythril_amd import uop_spec as U
+
+    _, lines = asm
+    top = 0
+    for l in lines:
+        code = l.split("//")[0]
+        for a in re.findall(r"\bv(\d+)\b", code):
+            top = max(top, int(a))
+        for a, b in re.findall(r"v\[(\d+):(\d+)\]", code):
+            top = max(top, int(b))
+    assert top < G.NVGPR
+    assert any(f".amdhsa_next_free_vgpr {G.NVGPR}" in l for l in lines)
+    # GPR-index mode reads / writes bank position p at RV + 8p + limb: the last position
+    # the translator can name must end inside the allocation
+    assert G.RV + 8 * U.REG_VARS <= G.PG < G.NVGPR
+
+
 @pytest.mark.skipif(not os.path.exists(f"{LLVM}/clang"), reason="ROCm LLVM assembler not installed")
 def test_assembles_for_gfx950(asm, tmp_path):
     s, _ = asm
@@ -120,8 +151,9 @@ def test_address_registers_initialised_before_first_load(asm):
     assert w2 < first(lambda l: l.startswith("global_load") and ", v2," in l)
     assert w1 < first(lambda l: l.startswith("ds_") and ", v" in l)
     assert first(lambda l: l.startswith("s_getpc_b64 s[10:11]")) < first(lambda l: l.startswith("s_setpc_b64"))
-    assert first(lambda l: l.startswith("global_load_dwordx4 v[112:115]")) < \
-        first(lambda l: l.startswith("v_readlane_b32 s0, v112"))
+    pg = f"v[{G.PG}:{G.PG + 3}]"
+    assert first(lambda l: l.startswith(f"global_load_dwordx4 {pg}")) < \
+        first(lambda l: l.startswith(f"v_readlane_b32 s0, v{G.PG}"))
     # pool constants are read with scalar loads from s[14:15]
     assert first(lambda l: l.startswith("s_add_u32 s14,")) < \
         first(lambda l: l.startswith("s_load") and "s[14:15]" in l)

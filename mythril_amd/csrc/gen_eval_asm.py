@@ -11,8 +11,8 @@ Handlers are straight-line gfx950 code on fixed registers:
 
   VGPR  v0 lane, v1 lane*16 (LDS lane base), v2/v3 candidate byte offsets of
         the two 16-B halves, v4-v7 scratch, vA=v[8:15], vB=v[16:23],
-        vC=v[24:31], T=v[32:41] (product / division temporaries), v[42:89]
-        register bank, v[90:94] uop page, v95 loop state; 96 in all
+        vC=v[24:31], T=v[32:41] (product / division temporaries), v[42:121]
+        register bank (10 positions), v[122:126] uop page, v127 loop state
   SGPR  s[4:5] uop pointer, s[6:7] candidate base of the state, s8 bytes per
         variable, s9 n_vars-1, s[10:11] jump table, s[14:15] constant pool,
         s[16:19] current uop C, s[20:23] prefetched uop N, s[24:31] constant
@@ -37,27 +37,22 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from mythril_amd import uop_spec as U  # noqa: E402
 
 KNAME = "mgp_eval_gfx950"
-# The same code under two kernel descriptors that differ only in the VGPR count they
-# reserve: KNAME reserves 128 (4 waves/SIMD), KNAME_W5 96 (5 waves/SIMD; the host picks it
-# per bucket only under MGP_W5_MAX_SLOTS: on the synthetic batch 5 waves/SIMD measured
-# slower).
-KNAME_W5 = "mgp_eval_gfx950_w5"
-# 96 VGPRs (5 waves/SIMD; 128 gave 4): the division keeps its 16-limb dividend in vA:vC and
-# normalises the divisor in vB, so the temporaries shrink to the 10 registers of T
+# The division keeps its 16-limb dividend in vA:vC and normalises the divisor in vB, so the
+# temporaries fit the 10 registers of T; that leaves 80 VGPRs for the register bank: 10
+# positions, 6 for preloaded variables and register slots, 4 for register slots only
 VA, VB, VC, VT = 8, 16, 24, 32
 NT = 10          # T = v[32:41]: products / compare scratch; in DIV the f64 and digit registers
-RV = int(os.environ.get("MGP_RV", "42"))  # v[RV:RV+47]: candidate variables 0..5 of this lane, preloaded at wave start
-PG = 90          # v[90:94]: the current 64-uop page, uop k in lane k (read with v_readlane):
-                 #   v90 first-handler address (low 32 bits), v91 op-handler address, v92-94 w1-w3
-VD = 95          # descriptor / loop state / diagnostic lanes (s_ registers above s63 are Bools)
-NVGPR = 96        # registers the code names (KNAME_W5 reserves exactly these)
-DECL_VGPR = 128   # KNAME's reservation
+RV = 42          # v[42:121]: register bank, U.REG_POS positions of 8 (variables 0..5 preloaded)
+PG = RV + 8 * U.REG_POS   # v[122:126]: the current 64-uop page, uop k in lane k (v_readlane):
+                 #   PG first-handler address (low 32 bits), PG+1 op-handler address, PG+2..4 w1-w3
+VD = PG + 5      # v127: descriptor / loop state / diagnostic lanes (SGPRs above s63 are Bools)
+NVGPR = 128
 HALIGN = int(os.environ.get("MGP_HALIGN", "2"))   # log2 byte alignment of handler entries
 # division registers inside T
 D_FA, D_FB = 32, 34          # f64 pairs: dividend / reciprocal, divisor / estimate
 D_M = 36                     # v36 carry into the next product, v37 = 0 (64-bit mad addend)
 D_Q, D_T = 38, 39            # qhat, scratch
-D_K, D_D = (40, 41) if RV == 42 else (88, 89)   # per-lane limb shift k, top-limb difference d
+D_K, D_D = 40, 41            # per-lane limb shift k, top-limb difference d
 D_SA, D_SB = "s[32:33]", "s[34:35]"   # operand sign lane masks (SDIV/SREM/SMOD)
 # A v_readlane costs a wave64 ~8.7 SIMD-cycles of VALU issue at 4 waves/SIMD
 # (profiles/contention_probe.hip, contention_r2.json), so a handler reads only the uop
@@ -377,7 +372,7 @@ def store_slot():
 
 def store_reg():
     """vA -> register-bank position p (w2[15:0] = 8p): GPR-index mode offsets the
-    destination of the moves into v[64:111]."""
+    destination of the moves into the bank."""
     A("s_and_b32 s48, s18, 0xffff",
       "s_set_gpr_idx_on s48, gpr_idx(DST)")
     for i in range(8):
@@ -485,7 +480,7 @@ def fetch_one(kind, dst, which):
         return
     A(get)
     if kind == "rvar":
-        # v[dst+i] = v[64 + 8*var + i]: GPR-index mode (gfx950 has no v_movrels) offsets
+        # v[dst+i] = v[RV + 8*p + i]: GPR-index mode (gfx950 has no v_movrels) offsets
         # SRC0 of the moves by 8*var into the preloaded variable bank
         A(f"s_set_gpr_idx_on {sp}, gpr_idx(SRC0)")
         for i in range(8):
@@ -1539,7 +1534,7 @@ KARGS = [("desc", 8, "global_buffer"), ("cands", 8, "global_buffer"), ("partial"
 
 def metadata():
     out = ["amdhsa.kernels:"]
-    for kname, nv in ((KNAME, DECL_VGPR), (KNAME_W5, NVGPR)):
+    for kname, nv in ((KNAME, NVGPR),):
         out.append("  - .args:")
         off = 0
         for name, size, kind in KARGS:
@@ -1632,12 +1627,9 @@ def generate() -> str:
         '.amdgcn_target "amdgcn-amd-amdhsa--gfx950"',
         ".text",
         f".globl {KNAME}",
-        f".globl {KNAME_W5}",
         ".p2align 8",
         f".type {KNAME},@function",
-        f".type {KNAME_W5},@function",
         f"{KNAME}:",
-        f"{KNAME_W5}:",
     ]
     def kd(kname, nv):
         return [
@@ -1664,9 +1656,8 @@ def generate() -> str:
     tail_ = [
         ".Lfunc_end:",
         f".size {KNAME}, .Lfunc_end-{KNAME}",
-        f".size {KNAME_W5}, .Lfunc_end-{KNAME_W5}",
         "",
-    ] + kd(KNAME, DECL_VGPR) + kd(KNAME_W5, NVGPR) + [
+    ] + kd(KNAME, NVGPR) + [
         ".amdgpu_metadata",
         "---",
         md,

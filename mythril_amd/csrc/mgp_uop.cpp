@@ -142,9 +142,9 @@ struct Translator {
   // LDS; a spilling program (slots numbered by access count, mgp_lower) gives the register
   // positions to its lowest slots, then LDS, then spill rows MGP_SPILL_BASE(max_var) + j.
   void map_slots(uint32_t n_slots, uint32_t max_var) {
-    uint32_t free_pos[MGP_U_REG_VARS], n_free = 0;
-    for (uint32_t p = 0; p < MGP_U_REG_VARS; ++p)
-      if (!(var_mask & (1u << p))) free_pos[n_free++] = p;
+    uint32_t free_pos[MGP_U_REG_POS], n_free = 0;
+    for (uint32_t p = 0; p < MGP_U_REG_POS; ++p)
+      if (p >= MGP_U_REG_VARS || !(var_mask & (1u << p))) free_pos[n_free++] = p;
     const uint32_t k = n_free < n_slots ? n_free : n_slots;
     const uint32_t spill0 = MGP_SPILL_BASE(max_var);
     slot_map.assign(n_slots, Opnd{KSLOT, 0});

@@ -27,7 +27,7 @@ uop words:
   w1 [15:0] operand A parameter, [31:16] operand B parameter
             SLOT: LDS byte offset (slot*2048), VAR: variable index (a spilled
             BV slot is the VAR row the state's VST uops write, mgp_ir.h), RVAR:
-            8 x register-bank position p (v[64+8p]: a preloaded variable, or a
+            8 x register-bank position p (v[42+8p]: a preloaded variable, or a
             register slot),
             CONST: pool index; Bool operands: bool slot * 2
   w2 [15:0] store slot byte offset, or 8 x bank position with REGST /
@@ -38,7 +38,7 @@ uop words:
      [24] SEXT    operands sign-extended from width w with H = pool[w3[5:0]]
      [25] INVERT  compare result negated
      [28:26]      division variant (DIV_*)
-     [29] REGST   the STORE goes to register-bank position w2[15:0]/8 (v[64+8p]),
+     [29] REGST   the STORE goes to register-bank position w2[15:0]/8 (v[42+8p]),
                   not to LDS: the translator maps a state's highest BV slots onto
                   bank positions no variable of that state uses
      [30] BCOMB   compares: the (possibly inverted) result is combined with Bool slot
@@ -56,9 +56,12 @@ vC (operand A of a compare that is not the accumulator); Bool slots are
 
 # operand kinds: acc = the accumulator vA, slot = per-lane LDS slot, var = candidate
 # variable loaded from HBM, const = constant pool (scalar load), rvar = candidate
-# variable 0..REG_VARS-1 preloaded into the register bank v[42:89] at wave start (GPR-index moves)
+# variable 0..REG_VARS-1 preloaded into the register bank at wave start (GPR-index moves);
+# the bank has REG_POS positions of 8 VGPRs (v[42+8p]): positions no preloaded variable uses
+# hold BV slots (register slots), so a program needs fewer LDS slots
 KINDS = ("acc", "slot", "var", "const", "rvar")
 REG_VARS = 6
+REG_POS = 10
 B_KINDS = ("none",) + KINDS
 
 # fetch handlers: F_<kindA>_<kindB>_<target of A>; A = acc with target C never occurs
@@ -140,7 +143,7 @@ def c_header() -> str:
         f"#define MGP_U_SHIFT_B_POS {SHIFT_B_POS}", f"#define MGP_U_DIVOP_POS {DIVOP_POS}",
         f"#define MGP_U_BOOL_SLOTS {BOOL_SLOTS}", f"#define MGP_U_MAX_LDS_SLOTS {MAX_LDS_SLOTS}",
         f"#define MGP_U_SLOT_BYTES {SLOT_BYTES}", f"#define MGP_U_HDR_WORDS {HDR_WORDS}",
-        f"#define MGP_U_UOP_WORDS {UOP_WORDS}", f"#define MGP_U_REG_VARS {REG_VARS}",
+        f"#define MGP_U_UOP_WORDS {UOP_WORDS}", f"#define MGP_U_REG_VARS {REG_VARS}", f"#define MGP_U_REG_POS {REG_POS}",
         f"#define MGP_U_N_KINDS {len(KINDS)}", f"#define MGP_U_PAGE_UOPS {PAGE_UOPS}",
         f"#define MGP_U_MAX_POOL {MAX_POOL}", f"#define MGP_U_MAX_MS {MAX_MS}", f"#define MGP_U_XR_FIRST {ID[XR_OPS[0]]}",
     ]

@@ -94,7 +94,8 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
     bools = [False] * U.BOOL_SLOTS
     bools[1] = True
 
-    # register bank v[64:111]: position p holds variable p when the program reads it
+    # register bank (uop_spec.REG_POS positions): position p < REG_VARS holds variable p when
+    # the program reads it; the other positions hold register slots
     # (preloaded), else it is a register slot written by REGST stores
     var_mask = (int(words[u0 + 3]) >> 8) & 0xFF
     var_rows = int(words[off + 3]) >> 8   # v1 header: one past the highest variable read

@@ -14,9 +14,7 @@ KECCAK64 = ("mgp_keccak64_gfx950", "mgp_keccak64_kernel")  # hand-allocated asm 
 
 
 def short(name):
-    n = name.split("(")[0].replace("void ", "").split("<")[0]
-    # the interpreter's two descriptors (128 / 96 VGPRs reserved) run the same code: one row
-    return "mgp_eval_gfx950" if n == "mgp_eval_gfx950_w5" else n
+    return name.split("(")[0].replace("void ", "").split("<")[0]
 
 
 def main(d):
@@ -74,8 +72,7 @@ def main(d):
         v, sg, lds, scr = meta[k]
         # rocprofv3's VGPR_Count decodes the descriptor's granulated count with a granule of 4;
         # gfx950 allocates arch VGPRs in granules of 8, so the field reads half the allocation
-        # (mgp_eval_gfx950 declares .amdhsa_next_free_vgpr 128 and reads as 64; its _w5
-        # descriptor over the same code reserves 96 and is summed into the same row)
+        # (mgp_eval_gfx950 declares .amdhsa_next_free_vgpr 128 and reads as 64)
         out.append(f"### {k}  (VGPR {2 * int(float(v))} allocated = rocprof VGPR_Count {v} x 2, SGPR {sg}, "
                    f"LDS {lds} B, scratch {scr})\n")
         out.append("| counter | value |")

@@ -123,7 +123,7 @@ def test_vgprs_within_the_declared_count(asm):
     assert any(f".amdhsa_next_free_vgpr {G.NVGPR}" in l for l in lines)
     # GPR-index mode reads / writes bank position p at RV + 8p + limb: the last position
     # the translator can name must end inside the allocation
-    assert G.RV + 8 * U.REG_VARS <= G.PG < G.NVGPR
+    assert U.REG_VARS <= U.REG_POS and G.RV + 8 * U.REG_POS <= G.PG < G.NVGPR
 
 
 @pytest.mark.skipif(not os.path.exists(f"{LLVM}/clang"), reason="ROCm LLVM assembler not installed")

@@ -824,6 +824,21 @@ def make_xc(name):
     return body
 
 
+def make_xv(name):
+    """XV_<ka>_<kb>_<tgt>_<op>: a register-only fetch (accumulator / bank moves, nothing to
+    wait for) followed by the op body in one handler."""
+    _, ka, kb, tgt, op = name.split("_", 4)
+
+    def body():
+        if kb != "none":
+            fetch_one(kb, VB, "B")
+        if ka != "acc":
+            fetch_one(ka, VA if tgt == "A" else VC, "A")
+        prefetch_next()
+        HBODY[op]()
+    return body
+
+
 def mul_low(xa, yb, out):
     """out[0..7] = low 256 bits of X*Y (Comba columns, v[4:5] + v6 accumulator)."""
     A("v_mov_b32 v6, 0")
@@ -1377,6 +1392,8 @@ for _x in U.XS_OPS:
     HBODY[_x] = make_xs(_x)
 for _x in U.XC_OPS:
     HBODY[_x] = make_xc(_x)
+for _x in U.XV_OPS:
+    HBODY[_x] = make_xv(_x)
 
 
 # ---------------------------------------------------------------- kernel
@@ -1596,7 +1613,7 @@ def generate() -> str:
            .replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
            .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n"))
     A.lines.append(pro)
-    no_prefetch = set(U.FETCH) | set(U.XS_OPS) | set(U.XC_OPS) | {"INVALID", "RET", "PAGE"}
+    no_prefetch = set(U.FETCH) | set(U.XS_OPS) | set(U.XC_OPS) | set(U.XV_OPS) | {"INVALID", "RET", "PAGE"}
     wait = "  s_waitcnt vmcnt(0) lgkmcnt(0)"
     for name in U.HANDLERS:
         # two entries per handler: mgp_h_<name> (reached from a fetch handler, whose

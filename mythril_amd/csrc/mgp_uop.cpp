@@ -208,6 +208,15 @@ inline int xc_handler(uint32_t op) {
   return -1;
 }
 
+// fused "register operands + op" handler (uop_spec.XV_LIST) of a fetch pattern and op, or -1
+inline int xv_handler(int ka, int kb, bool to_c, uint32_t op) {
+  for (uint32_t i = 0; i < sizeof(kXv) / sizeof(kXv[0]); ++i)
+    if (kXv[i][0] == ka && kXv[i][1] == kb && (kXv[i][2] != 0) == to_c && (uint32_t)kXv[i][3] == op)
+      return (int)(MGP_U_XV_FIRST + i);
+  return -1;
+}
+inline bool reg_kind(int k) { return k == KACC || k == KRVAR; }
+
 // ---- Bool peepholes on the v1 instruction list (asm engine only; the v1 program is untouched)
 //   * a compare immediately followed by a BNOT of its result: the compare is emitted with
 //     its INVERT flag toggled and the BNOT's destination (one dispatch instead of two);
@@ -443,9 +452,11 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       } else if (ra && b.kind == KCONST) {
         const int xc = xc_handler(opid);
         if (xc >= 0) opid = first = (uint32_t)xc;
-      } else if (ra && b.kind == KRVAR && !(flags & (MGP_UF_SEXT | MGP_UF_MASK))) {
-        const int xr = xr_handler(opid);  // EQ / ULT / UGT against a register-bank operand
-        if (xr >= 0) opid = first = (uint32_t)xr;
+      } else if (ra && b.kind == KRVAR && !(flags & (MGP_UF_SEXT | MGP_UF_MASK)) && xr_handler(opid) >= 0) {
+        opid = first = (uint32_t)xr_handler(opid);  // EQ / ULT / UGT against a register-bank operand
+      } else if (reg_kind(a.kind) && (reg_kind(b.kind) || b.kind == KNONE)) {
+        const int xv = xv_handler(a.kind, b.kind, !ra, opid);
+        if (xv >= 0) opid = first = (uint32_t)xv;
       }
         emit(w0_of(first, opid), (ra ? 0u : a.param) | (b.param << 16), w2 | flags, w3);
         continue;
@@ -563,6 +574,10 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       } else if (a.kind == KACC && b.kind == KCONST) {
         const int xc = xc_handler(opid);
         if (xc >= 0) opid = first = (uint32_t)xc;
+      }
+      if (first != opid && reg_kind(a.kind) && (reg_kind(b.kind) || b.kind == KNONE)) {
+        const int xv = xv_handler(a.kind, b.kind, false, opid);  // register operands + op
+        if (xv >= 0) opid = first = (uint32_t)xv;
       }
       emit(w0_of(first, opid), a.param | (b.param << 16), w2 | flags, w3);
       if (vst_row >= 0) emit(w0_of(MGP_U_VST, MGP_U_VST), 0u, (uint32_t)vst_row, 0u);

@@ -101,13 +101,26 @@ XS_OPS = [f"XS_{o}" for o in XS_BASE]
 XC_BASE = list(XS_BASE)
 XC_OPS = [f"XC_{o}" for o in XC_BASE]
 
+# fused handlers "register operands + op": a fetch whose operands are all registers (the
+# accumulator or register-bank positions) and its op in one handler (the bank moves, then
+# the op body: no second dispatch).  XV_<kindA>_<kindB>_<target>_<op>; the pairs most
+# frequent on the synthetic batch (profiles/uop_mix.py), DIV excluded (a long body)
+XV_LIST = [("acc", "rvar", "A", o) for o in ("MUL", "ITE", "ITE_R", "SLT_RA")] + \
+          [("rvar", "rvar", "C", o) for o in ("EQ_RC", "ULT_RC", "UGT_RC", "SLT_RC")] + \
+          [("rvar", "rvar", "A", o) for o in ("ITE", "ITE_R", "MUL", "ADD", "ADD_R", "SUB", "SUB_R", "AND", "AND_R",
+                                              "OR", "OR_R", "XOR", "XOR_R")] + \
+          [("acc", "acc", "A", o) for o in ("EQ_RA", "ULT_RA")] + \
+          [("rvar", "acc", "A", o) for o in ("SUB", "SUB_R", "ITE", "ITE_R")] + \
+          [("rvar", "none", "A", o) for o in ("NOT", "NOT_R") + tuple(f"LSHRI{k}" for k in range(8))]
+XV_OPS = [f"XV_{ka}_{kb}_{t}_{o}" for ka, kb, t, o in XV_LIST]
+
 OPS = BOOL_OPS + MEM_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + \
-    XS_OPS + XC_OPS
+    XS_OPS + XC_OPS + XV_OPS
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
 # id past the table ends the program instead of running off into memory
 HANDLERS = ["INVALID"] + FETCH + OPS
 ID = {name: i for i, name in enumerate(HANDLERS)}
-assert len(HANDLERS) < 256
+assert len(HANDLERS) < 1024   # ids are host-side table indices (uops carry offsets)
 
 DIV_VARIANTS = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
 
@@ -149,6 +162,9 @@ def c_header() -> str:
     ]
     lines.append("static const unsigned short kXrBase[%d] = {%s};" % (len(XR_BASE), ", ".join(
         f"MGP_U_{o}" for o in XR_BASE)))
+    lines.append(f"#define MGP_U_XV_FIRST {ID[XV_OPS[0]]}")
+    lines.append("static const short kXv[%d][4] = {%s};" % (len(XV_LIST), ", ".join(
+        "{%d, %d, %d, MGP_U_%s}" % (KINDS.index(ka), B_KINDS.index(kb) - 1, t == "C", o) for ka, kb, t, o in XV_LIST)))
     lines.append(f"#define MGP_U_XS_FIRST {ID[XS_OPS[0]]}")
     lines.append("static const unsigned short kXsBase[%d] = {%s};" % (len(XS_BASE), ", ".join(
         f"MGP_U_{o}" for o in XS_BASE)))

@@ -138,6 +138,9 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         elif first.startswith("XC_"):
             vB = load("const", pb)      # fused: vA op pool[B]
             first = op = first[3:]
+        elif first.startswith("XV_"):   # fused: register-only fetch + op
+            _, ka, kb, tgt, op = first.split("_", 4)
+            first = f"F_{ka}_{kb}_{tgt}"
         if first.startswith("F_"):
             _, ka, kb, tgt = first.split("_")
             if kb != "none":

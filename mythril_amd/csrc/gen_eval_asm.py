@@ -46,7 +46,7 @@ RV = 42          # v[42:121]: register bank, U.REG_POS positions of 8 (variables
 PG = RV + 8 * U.REG_POS   # v[122:126]: the current 64-uop page, uop k in lane k (v_readlane):
                  #   PG first-handler address (low 32 bits), PG+1 op-handler address, PG+2..4 w1-w3
 VD = PG + 5      # v127: descriptor / loop state / diagnostic lanes (SGPRs above s63 are Bools)
-NVGPR = 128
+NVGPR = (VD + 1 + 7) // 8 * 8   # 128 with the 10-position bank (4 waves/SIMD); 96 with 6 (5 waves)
 HALIGN = int(os.environ.get("MGP_HALIGN", "2"))   # log2 byte alignment of handler entries
 # division registers inside T
 D_FA, D_FB = 32, 34          # f64 pairs: dividend / reciprocal, divisor / estimate
@@ -775,25 +775,26 @@ def make_xr(name):
     return body
 
 
-def make_xr_cmp(base):
-    """XR_<cmp>_RA: Bool = vA cmp bank[B], B read in GPR-index mode as SRC1 (EQ, ULT) or,
-    for UGT (computed as B < vA), as SRC0 of the borrow chain."""
+def make_xr_cmp(base, X=VA):
+    """XR_<cmp>_RA: Bool = X cmp bank[B] (X = vA; vC for the XV C-target forms), B read in
+    GPR-index mode as SRC1 (EQ, ULT) or, for UGT (computed as B < X), as SRC0 of the borrow
+    chain."""
     def body():
         A("s_lshr_b32 s50, s17, 16")
         if base == "EQ":
             A("s_set_gpr_idx_on s50, gpr_idx(SRC1)")
             for i in range(8):
-                A(f"v_xor_b32 {v(VT + i)}, {v(VA + i)}, {v(RV + i)}")
+                A(f"v_xor_b32 {v(VT + i)}, {v(X + i)}, {v(RV + i)}")
             A("s_set_gpr_idx_off")
             or_reduce(VT, range(VT, VT + 8))
             A(f"v_cmp_eq_u32 vcc, 0, {v(VT)}")
         elif base == "ULT":
             A("s_set_gpr_idx_on s50, gpr_idx(SRC1)")
-            ult_chain(VA, RV)
+            ult_chain(X, RV)
             A("s_set_gpr_idx_off")
         else:
             A("s_set_gpr_idx_on s50, gpr_idx(SRC0)")
-            ult_chain(RV, VA)
+            ult_chain(RV, X)
             A("s_set_gpr_idx_off")
         cmp_epilogue()
     return body
@@ -824,18 +825,109 @@ def make_xc(name):
     return body
 
 
-def make_xv(name):
-    """XV_<ka>_<kb>_<tgt>_<op>: a register-only fetch (accumulator / bank moves, nothing to
-    wait for) followed by the op body in one handler."""
-    _, ka, kb, tgt, op = name.split("_", 4)
+def with_epi(mode):
+    """bv_epilogue() with a fixed epilogue variant ("" / "S" / "R" ...)."""
+    EPI_MODE[0] = mode
+    try:
+        bv_epilogue()
+    finally:
+        EPI_MODE[0] = None
 
-    def body():
+
+def idx_on(field, mode):
+    """GPR-index mode on the bank offset of operand A (field "A": w1[15:0]) or B (w1[31:16])."""
+    A("s_and_b32 s51, s17, 0xffff" if field == "A" else "s_lshr_b32 s51, s17, 16",
+      f"s_set_gpr_idx_on s51, gpr_idx({mode})")
+
+
+def xv_ite(field, then_bank):
+    """vA = c ? then : else with one of the two read straight from the bank (GPR-index mode
+    on the VOP2 cndmask: the else value is SRC0, the then value SRC1; c moved to vcc)."""
+    bool_read("s19", 16, 50)
+    A("s_mov_b64 vcc, s[50:51]")
+    idx_on(field, "SRC1" if then_bank else "SRC0")
+    for i in range(8):
+        if then_bank:
+            A(f"v_cndmask_b32 {v(VA + i)}, {v(VA + i)}, {v(RV + i)}, vcc")
+        else:
+            A(f"v_cndmask_b32 {v(VA + i)}, {v(RV + i)}, {v(VA + i)}, vcc")
+    A("s_set_gpr_idx_off")
+
+
+def make_xv(name):
+    """XV_<ka>_<kb>_<tgt>_<op>: a register-only fetch and its op in one handler.  Where the
+    op body reads a bank operand through one operand position, that position is read in
+    GPR-index mode (no moves); otherwise the operands are moved (accumulator / bank) and
+    the op body follows."""
+    _, ka, kb, tgt, op = name.split("_", 4)
+    base, mode = (op.split("_", 1) + [""])[:2]
+
+    def generic():
         if kb != "none":
             fetch_one(kb, VB, "B")
         if ka != "acc":
             fetch_one(ka, VA if tgt == "A" else VC, "A")
         prefetch_next()
         HBODY[op]()
+
+    def body():
+        if kb == "rvar" and ka in ("acc", "rvar") and tgt == "A" and op in U.XR_BASE:
+            # vA = A op bank[B]: A moved when it is a bank value, B indexed (the XR body)
+            if ka == "rvar":
+                fetch_one("rvar", VA, "A")
+            prefetch_next()
+            HBODY["XR_" + op]()
+        elif kb == "rvar" and ka == "rvar" and tgt == "C" and base in ("EQ", "ULT", "UGT") and mode == "RC":
+            fetch_one("rvar", VC, "A")
+            prefetch_next()
+            make_xr_cmp(base, VC)()
+        elif kb == "rvar" and tgt == "A" and base == "ITE" and mode in ("", "R"):
+            if ka == "rvar":
+                fetch_one("rvar", VA, "A")
+            prefetch_next()
+            xv_ite("B", then_bank=False)
+            with_epi(mode)
+        elif kb == "acc" and ka == "rvar" and base == "ITE" and mode in ("", "R"):
+            prefetch_next()
+            xv_ite("A", then_bank=True)
+            with_epi(mode)
+        elif kb == "acc" and ka == "rvar" and base == "SUB" and mode in ("", "R"):
+            # vA = bank[A] - vA: the minuend indexed as SRC0
+            prefetch_next()
+            idx_on("A", "SRC0")
+            A(f"v_sub_co_u32 {v(VA)}, vcc, {v(RV)}, {v(VA)}")
+            for i in range(1, 8):
+                A(f"v_subb_co_u32 {v(VA + i)}, vcc, {v(RV + i)}, {v(VA + i)}, vcc")
+            A("s_set_gpr_idx_off")
+            with_epi(mode)
+        elif kb == "none" and ka == "rvar" and base == "NOT" and mode in ("", "R"):
+            prefetch_next()
+            idx_on("A", "SRC0")
+            for i in range(8):
+                A(f"v_not_b32 {v(VA + i)}, {v(RV + i)}")
+            A("s_set_gpr_idx_off")
+            with_epi(mode)
+        elif kb == "none" and ka == "rvar" and re.fullmatch(r"LSHRI[0-7]", op):
+            # vA = bank[A] >> (32k + b): both funnel sources from the bank (SRC0 | SRC1)
+            k = int(op[-1])
+            prefetch_next()
+            uniform_b()
+            idx_on("A", "SRC0,SRC1")
+            shri_body(k, "0", src=RV)
+            A("s_set_gpr_idx_off")
+            bv_epilogue()          # MASK / STORE tested at run time, as in LSHRI<k>
+        elif kb == "rvar" and ka in ("acc", "rvar") and tgt == "A" and op == "MUL":
+            # the multiplier's limbs are SRC1 of every v_mad_u64_u32: indexed
+            if ka == "rvar":
+                fetch_one("rvar", VA, "A")
+            prefetch_next()
+            A("s_lshr_b32 s52, s17, 16", "s_set_gpr_idx_on s52, gpr_idx(SRC1)")
+            mul_low(VA, RV, VT)
+            A("s_set_gpr_idx_off")
+            copy8(VA, VT)
+            bv_epilogue()          # MASK / STORE tested at run time, as in MUL
+        else:
+            generic()
     return body
 
 
@@ -989,14 +1081,15 @@ def shli_body(k, regs_base=VA):
     A.label(ldone)
 
 
-def shri_body(k, fill):
+def shri_body(k, fill, src=VA):
+    """vA = src >> (32k + b), b in s48 (src = vA, or the bank in GPR-index mode)."""
     for i in range(8):
         lo, hi = i + k, i + k + 1
         if lo >= 8:
             A(f"v_mov_b32 {v(VA + i)}, {fill}")
         else:
-            hv = v(VA + hi) if hi < 8 else fill
-            A(f"v_alignbit_b32 {v(VA + i)}, {hv}, {v(VA + lo)}, s48")
+            hv = v(src + hi) if hi < 8 else fill
+            A(f"v_alignbit_b32 {v(VA + i)}, {hv}, {v(src + lo)}, s48")
 
 
 def make_shli(k):

@@ -1301,8 +1301,8 @@ def msub_digit(J, dv):
 
 
 def single_digit():
-    """Quotient of a wave whose dividing lanes all have top limb(a) = top limb(b) = t, so
-    q = floor(a / b) < 2^32: one digit against the unnormalised divisor.
+    """Quotient of a wave whose dividing lanes all have q = floor(a / b) < 2^32: one digit
+    against the unnormalised divisor.
 
     qhat = trunc(a_f * (1 / b_f) + 2^-12).  a_f, b_f are the 256-bit values in double
     precision by a Horner chain over the limbs (one rounding per step, each relative error
@@ -1364,6 +1364,19 @@ def h_div():
     A("s_cmp_eq_u64 s[24:25], 0", f"s_cbranch_scc1 {lpost}")
     for i in range(8, 16):
         A(f"v_mov_b32 {u(i)}, 0")
+    # single-digit waves: q < 2^32, i.e. (a >> 32) < b, on every dividing lane (one borrow
+    # chain; the top-limb bookkeeping of the general path is skipped).  Covers every wave
+    # whose dividing lanes have top limb(a) = top limb(b) (47 % of the executed DIVs on the
+    # synthetic batch) and more
+    lmulti, lnorem = A.fresh("multidig"), A.fresh("norem")
+    A(f"v_sub_co_u32 {v(D_T)}, vcc, {v(VA + 1)}, {v(VB)}")
+    for i in range(1, 7):
+        A(f"v_subb_co_u32 {v(D_T)}, vcc, {v(VA + i + 1)}, {v(VB + i)}, vcc")
+    A(f"v_subb_co_u32 {v(D_T)}, vcc, 0, {v(VB + 7)}, vcc",
+      "s_andn2_b64 s[48:49], s[24:25], vcc", "s_cmp_eq_u64 s[48:49], 0", f"s_cbranch_scc0 {lmulti}")
+    single_digit()
+    A(f"s_branch {lnorem}")
+    A.label(lmulti)
     # d = top limb(a) - top limb(b) (-1 when not dividing): digits J > d are zero
     K, D = v(D_K), v(D_D)
     top_limb(VB, D_K)
@@ -1372,13 +1385,6 @@ def h_div():
       f"v_cndmask_b32_e64 {D}, -1, {D}, s[24:25]",
       f"v_sub_u32 {K}, 7, {K}",                        # k = 7 - top limb(b) limbs
       f"v_cndmask_b32_e64 {K}, 0, {K}, s[24:25]")
-    # single-digit waves (d <= 0 on every lane: 47 % of the executed DIVs on the synthetic
-    # batch) skip the normalisation and the remainder shift
-    lmulti, lnorem = A.fresh("multidig"), A.fresh("norem")
-    A(f"v_cmp_lt_i32 vcc, 0, {D}", "s_cmp_eq_u64 vcc, 0", f"s_cbranch_scc0 {lmulti}")
-    single_digit()
-    A(f"s_branch {lnorem}")
-    A.label(lmulti)
     # limb normalisation in place: vn = b << 32k, u = a << 32k (vn7 != 0 on dividing lanes;
     # no bit shift is needed because qhat is estimated from the top three limbs of vn)
     limb_masks(D_K)

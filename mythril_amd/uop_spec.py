@@ -53,6 +53,8 @@ Registers of the interpreter: vA (accumulator / operand A), vB (operand B),
 vC (operand A of a compare that is not the accumulator); Bool slots are
 64-bit lane masks in SGPRs: slot 0 = false, slot 1 = true, 2.. allocatable.
 """
+import os
+
 
 # operand kinds: acc = the accumulator vA, slot = per-lane LDS slot, var = candidate
 # variable loaded from HBM, const = constant pool (scalar load), rvar = candidate
@@ -61,7 +63,7 @@ vC (operand A of a compare that is not the accumulator); Bool slots are
 # hold BV slots (register slots), so a program needs fewer LDS slots
 KINDS = ("acc", "slot", "var", "const", "rvar")
 REG_VARS = 6
-REG_POS = 10
+REG_POS = int(os.environ.get("MGP_REG_POS", "10"))   # build-time knob (A/B of bank size vs occupancy)
 B_KINDS = ("none",) + KINDS
 
 # fetch handlers: F_<kindA>_<kindB>_<target of A>; A = acc with target C never occurs

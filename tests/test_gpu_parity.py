@@ -438,6 +438,67 @@ def test_division_single_digit_waves(mgp_ctx, w):
                     f"a={a:#x} b={b:#x} expected {e:#x}")
 
 
+def _q32_pairs(rng, n, w, signed):
+    """(a, b) with q = a // b < 2^32 but top limb(a) = top limb(b) + 1 (the single-digit
+    path's (a >> 32) < b test admits them; the top-limb test did not), quotients at the
+    extremes, remainders 0 / b - 1 / random, a few b = 0 and a < b lanes."""
+    limbs = w // 32 - (1 if signed else 0)
+    m = (1 << w) - 1
+    out = []
+    for j in range(n):
+        kind = j % 8
+        t = int(rng.integers(0, max(1, limbs - 1)))      # top limb of b; a's is t + 1
+        if kind == 7:
+            out.append((int(rng.integers(0, 2 ** 31)) << (32 * t), 0 if j % 16 == 7 else m >> 1))
+            continue
+        top_b = int(rng.integers(1, 2 ** 32))
+        low = int.from_bytes(rng.integers(0, 256, size=32, dtype=np.uint8).tobytes(), "little")
+        b = (top_b << (32 * t)) | (low & ((1 << (32 * t)) - 1))
+        qmin = -(-(1 << (32 * (t + 1))) // b)          # smallest q with q * b >= 2^(32(t+1))
+        q = [qmin, 2 ** 32 - 1, int(rng.integers(qmin, 2 ** 32)), 2 ** 32 - 2, qmin + 1,
+             int(rng.integers(qmin, 2 ** 32)), int(rng.integers(2 ** 31, 2 ** 32))][kind]
+        q = min(max(q, qmin), 2 ** 32 - 1)
+        r = [0, b - 1, int(rng.integers(0, 2 ** 62)) % b, 0][j % 4]
+        a = q * b + r
+        if a >> (w - (1 if signed else 0)):
+            a, b = b, b                                 # out of range for this width: q = 1
+        if signed:
+            if rng.integers(0, 2):
+                a = (-a) & m
+            if rng.integers(0, 2):
+                b = (-b) & m
+        out.append((a, b))
+    return out
+
+
+@pytest.mark.parametrize("w", [256, 96])
+def test_division_q32_waves(mgp_ctx, w):
+    """Waves whose dividing lanes have one quotient digit but different top limbs take the
+    single-digit path too: every variant, every candidate, root = (op(x0, x1) != x2)."""
+    rng = np.random.default_rng(57 + w)
+    ops = [S.UDIV, S.UREM, S.SDIV, S.SREM, S.SMOD]
+    n_cand, per_op = 256, 3
+    states, rows = [], []
+    for op in ops:
+        for _ in range(per_op):
+            pairs = _q32_pairs(rng, n_cand, w, op in (S.SDIV, S.SREM, S.SMOD))
+            exp = [S.binop(op, x, y, w) for x, y in pairs]
+            nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0], [S.VAR, w, -1, -1, -1, 2, 0],
+                  [op, w, 0, 1, -1, 0, 0], [S.EQ, 1, 3, 2, -1, 0, 0], [S.BNOT, 1, 4, -1, -1, 0, 0]]
+            states.append((nl, []))
+            rows.append([[x, y, e] for (x, y), e in zip(pairs, exp)])
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    first, _ = mgp_ctx.eval_batch(words, po, cands_from_ints(rows))
+    bad = np.nonzero(first != N.MGP_NO_SAT)[0]
+    if bad.size:
+        s0 = int(bad[0])
+        a, b, e = rows[s0][int(first[s0])]
+        pytest.fail(f"{bad.size} states with a wrong quotient/remainder; first: op {ops[s0 // per_op]} "
+                    f"a={a:#x} b={b:#x} expected {e:#x}")
+
+
 def _bool_fold_states(rng, n):
     """DAGs whose compares feed the next BAND / BOR and whose BNOTs feed the next BAND
     (the translator's BCOMB / BANDN folds), inverted compares (UGE / ULE / SGE) among

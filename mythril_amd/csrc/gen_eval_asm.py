@@ -15,7 +15,7 @@ Handlers are straight-line gfx950 code on fixed registers:
         register bank (10 positions), v[122:126] uop page, v127 loop state
   SGPR  s[4:5] uop pointer, s[6:7] candidate base of the state, s8 bytes per
         variable, s9 n_vars-1, s[10:11] jump table, s[14:15] constant pool,
-        s[16:19] current uop C, s[20:23] prefetched uop N, s[24:31] constant
+        s16 w1 of the next uop, s[17:19] w1-w3 of the current uop, s[24:31] constant
         operand, s[32:39] sign constant H, s[40:47] mask constant M,
         s[48:55] temporaries, s[56:57] valid-lane mask, s[58:59] partial
         result address, s60 first candidate of the chunk, s[62:63] 2^32 (f64),
@@ -116,15 +116,19 @@ A = Asm()
 
 def prefetch_next():
     """At handler entry: the first-handler address of the next uop (lane s21 + 1 of the
-    page, computed lane-parallel when the page was loaded) straight into s0; s1 is the
-    constant high half of the code address.  s21 = lane of the current uop."""
+    page, computed lane-parallel when the page was loaded) straight into s0 (s1 is the
+    constant high half of the code address) and its w1 into s16, which the tail moves to
+    s17: a handler finds its w1 in place instead of waiting on a v_readlane at its top.
+    s21 = lane of the current uop."""
     A("s_add_u32 s3, s21, 1",
-      f"v_readlane_b32 s0, {v(PG)}, s3")
+      f"v_readlane_b32 s0, {v(PG)}, s3",
+      f"v_readlane_b32 s16, {v(PG + 2)}, s3")
 
 
 def read_fields(used):
-    """The uop fields a handler uses (w1-w3 -> s17-s19), read from lane s21 of the page."""
-    for f in (17, 18, 19):
+    """The uop fields a handler uses (w2, w3 -> s18, s19), read from lane s21 of the page
+    (w1 is in s17 already: the previous uop's prefetch_next and tail)."""
+    for f in (18, 19):
         if f in used:
             A(f"v_readlane_b32 s{f}, v{PG + f - 15}, s21")
 
@@ -150,9 +154,16 @@ def tail_jump():
     tail()
 
 
+def first_fields():
+    """s16 <- w1 of the uop at lane s3 (a new page, a chunk restart, the first dispatch)."""
+    A(f"v_readlane_b32 s16, {v(PG + 2)}, s3")
+
+
 def tail():
-    """Make the prefetched uop current (s21 = its lane) and jump to its first handler."""
+    """Make the prefetched uop current (s21 = its lane, s17 = its w1) and jump to its first
+    handler."""
     A("s_mov_b32 s21, s3",
+      "s_mov_b32 s17, s16",
       "s_setpc_b64 s[0:1]")
 
 
@@ -561,6 +572,7 @@ def h_page():
       "s_mov_b32 s3, 0")
     page_decode()
     A(f"v_readlane_b32 s0, {v(PG)}, s3")
+    first_fields()
     tail()
 
 
@@ -664,6 +676,7 @@ def next_chunk():
       "s_mov_b32 s63, 0x41f00000",
       "s_mov_b32 s3, 0",
       f"v_readlane_b32 s0, {v(PG)}, s3")
+    first_fields()
     tail()
 
 
@@ -696,6 +709,40 @@ def h_band4():
       "s_and_b64 s[50:51], s[50:51], s[54:55]", "s_mov_b32 m0, s48",
       "s_and_b64 s[50:51], s[50:51], s[52:53]", "s_movreld_b64 s[64:65], s[50:51]")
     tail()
+
+
+def make_band4n(m):
+    """BAND4N<m>: dst = a' & b' & c' & d' where x' = ~x for the operands in mask m (bit 0 =
+    a), same schedule as BAND4 (each M0 write's wait state filled)."""
+    def comb(r, x, neg):
+        A(f"s_andn2_b64 {r}, {r}, {x}" if neg else f"s_and_b64 {r}, {r}, {x}")
+
+    def first():   # s[50:51] = a' & b'
+        na, nb = m & 1, m >> 1 & 1
+        if na and nb:
+            A("s_nor_b64 s[50:51], s[50:51], s[52:53]")
+        elif na:
+            A("s_andn2_b64 s[50:51], s[52:53], s[50:51]")
+        else:
+            comb("s[50:51]", "s[52:53]", nb)
+
+    def _():
+        A("s_and_b32 s48, s17, 0xffff", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s17, 16",
+          "s_movrels_b64 s[50:51], s[64:65]", "s_mov_b32 m0, s49", "s_and_b32 s48, s18, 0xffff",
+          "s_movrels_b64 s[52:53], s[64:65]", "s_mov_b32 m0, s48", "s_lshr_b32 s49, s18, 16",
+          "s_movrels_b64 s[54:55], s[64:65]", "s_mov_b32 m0, s49")
+        first()
+        A("s_movrels_b64 s[52:53], s[64:65]", "s_lshr_b32 s48, s19, 16")
+        comb("s[50:51]", "s[54:55]", m >> 2 & 1)
+        A("s_mov_b32 m0, s48")
+        comb("s[50:51]", "s[52:53]", m >> 3 & 1)
+        A("s_movreld_b64 s[64:65], s[50:51]")
+        tail()
+    return _
+
+
+for _m in range(1, 16):
+    HBODY[f"BAND4N{_m}"] = make_band4n(_m)
 
 
 @handler("BANDN")
@@ -932,18 +979,20 @@ def make_xv(name):
 
 
 def mul_low(xa, yb, out):
-    """out[0..7] = low 256 bits of X*Y (Comba columns, v[4:5] + v6 accumulator)."""
-    A("v_mov_b32 v6, 0")
+    """out[0..7] = low 256 bits of X*Y (Comba columns, v[4:5] + v6 accumulator; the first
+    carry of a column sets v6 instead of adding to a zeroed one)."""
     for k in range(8):
         pairs = [(i, k - i) for i in range(k + 1)]
         for n, (i, j) in enumerate(pairs):
             src2 = "0" if (k == 0 and n == 0) else "v[4:5]"
             A(f"v_mad_u64_u32 v[4:5], s[48:49], {v(xa + i)}, {v(yb + j)}, {src2}")
             if k < 7 and not (k == 0 and n == 0):
-                A("v_addc_co_u32 v6, s[50:51], v6, 0, s[48:49]")
+                A("v_addc_co_u32 v6, s[50:51], 0, 0, s[48:49]" if n == 0 else
+                  "v_addc_co_u32 v6, s[50:51], v6, 0, s[48:49]")
         A(f"v_mov_b32 {v(out + k)}, v4")
         if k < 7:
-            A("v_mov_b32 v4, v5", "v_mov_b32 v5, v6", "v_mov_b32 v6, 0")
+            # column 0 has one product and no carry word
+            A("v_mov_b32 v4, v5", "v_mov_b32 v5, 0" if k == 0 else "v_mov_b32 v5, v6")
 
 
 def mul_full(xa, yb, out, hi_or):
@@ -1702,6 +1751,7 @@ def generate() -> str:
     global_A = A
     globals()["A"] = first
     A(f"v_readlane_b32 s0, {v(PG)}, s3")
+    first_fields()
     tail()
     globals()["A"] = global_A
     dec = Asm()
@@ -1728,7 +1778,7 @@ def generate() -> str:
         globals()["A"] = global_A
         A.n = body.n
         lines = body.lines
-        used = {f for f in (17, 18, 19) if any(re.search(rf"\bs{f}\b|\bs\[{f}:|\bs\[\d+:{f}\]", l) for l in lines)}
+        used = {f for f in (18, 19) if any(re.search(rf"\bs{f}\b|\bs\[{f}:|\bs\[\d+:{f}\]", l) for l in lines)}
         A.lines.append(f".p2align {HALIGN}\nmgp_h_{name}:")
         if name not in no_prefetch and lines and lines[0] == wait:
             A.lines.append(wait)

@@ -255,6 +255,8 @@ struct BoolPlan {
   std::vector<std::vector<uint32_t>> andops;  // BAND: operand bits (2..4)
   std::vector<uint32_t> comb;                 // compare: 1 + other bit | OR << 16 (folded BAND / BOR)
   std::vector<uint32_t> andn;                 // BAND: 1 + negated bit (folded BNOT), andops[0] the other
+  std::vector<uint8_t> merged;                // BAND merged into the next BAND of its AND chain
+  std::vector<uint8_t> neg;                   // BAND: andops negated (bit j = andops[j]; BAND4N)
 };
 
 void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
@@ -264,6 +266,8 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
   P.andops.assign(n, {});
   P.comb.assign(n, 0);
   P.andn.assign(n, 0);
+  P.merged.assign(n, 0);
+  P.neg.assign(n, 0);
   for (uint32_t pc = 0; pc + 1 < n; ++pc) {
     const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS, *J = I + MGP_INS_WORDS;
     const uint32_t op = v1_op(I), d = (I[0] >> 16) & 0xFFu;
@@ -292,6 +296,7 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
     ops.push_back(ja == t ? jb : ja);
     P.andops[pc + 1] = ops;
     P.dead[pc] = 1;
+    P.merged[pc] = 1;
   }
   // the next instruction left after pc
   auto next_live = [&](uint32_t pc) {
@@ -339,6 +344,46 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
     P.andn[q] = 1u + x;
     P.andops[q] = {y, x};
     P.dead[pc] = 1;
+  }
+  // a BNOT whose result only one AND chain reads, anywhere before it: the chain's last BAND
+  // reads the BNOT's source with a negate flag (BAND4N) and the BNOT goes.  Checked on the v1
+  // stream with folded instructions included, so every reader counts: x (the BNOT's result)
+  // is read exactly once before q, inside the chain, and is not live after q; s (its
+  // source) is not written between the BNOT and q.
+  auto writes = [&](uint32_t r, uint32_t bit) {
+    return v1_writes_bool(ins + (size_t)r * MGP_INS_WORDS, bit) || (!P.dead[r] && P.dst[r] == bit);
+  };
+  for (uint32_t q = 0; q < n; ++q) {
+    if (P.dead[q] || v1_op(ins + (size_t)q * MGP_INS_WORDS) != MGP_OP_BAND || P.andn[q]) continue;
+    uint32_t lo = q;  // the AND chain ending at q
+    while (lo > 0 && P.merged[lo - 1]) --lo;
+    std::vector<uint32_t> &ops = P.andops[q];
+    for (size_t j = 0; j < ops.size(); ++j) {
+      const uint32_t x = ops[j];
+      if (x == MGP_BOOL_TRUE || x == MGP_BOOL_FALSE || std::count(ops.begin(), ops.end(), x) != 1) continue;
+      int64_t p = -1;
+      for (int64_t r = (int64_t)q - 1; r >= 0; --r)
+        if (writes((uint32_t)r, x)) { p = r; break; }
+      if (p < 0 || (uint32_t)p >= lo || P.dead[p]) continue;
+      const uint32_t *B = ins + (size_t)p * MGP_INS_WORDS;
+      const uint32_t sx = B[1] & 0xFFFFu;
+      if (v1_op(B) != MGP_OP_BNOT || P.dst[p] != 0xFFFFFFFFu) continue;  // in place (sx == x) too
+      uint32_t reads = 0, reads_in_chain = 0;
+      bool s_written = false;
+      for (uint32_t r = (uint32_t)p + 1; r <= q; ++r) {
+        if (v1_reads_bool(ins + (size_t)r * MGP_INS_WORDS, x)) {
+          ++reads;
+          reads_in_chain += r >= lo;
+        }
+        s_written |= writes(r, sx) && r < q;
+      }
+      const bool q_redefines = v1_writes_bool(ins + (size_t)q * MGP_INS_WORDS, x);
+      if (reads != 1 || reads_in_chain != 1 || s_written || (!q_redefines && v1_live_after(ins, n, q + 1, x)))
+        continue;
+      ops[j] = sx;
+      P.neg[q] |= (uint8_t)(1u << j);
+      P.dead[p] = 1;
+    }
   }
 }
 
@@ -388,6 +433,14 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       if (op == MGP_OP_BAND && BP.andn[pc]) {  // a & ~b
         emit(w0_of(MGP_U_BANDN, MGP_U_BANDN), T.boolslot(BP.andops[pc][0]) | (T.boolslot(BP.andops[pc][1]) << 16),
              0u, T.boolslot(dst) << 16);
+        continue;
+      }
+      if (op == MGP_OP_BAND && BP.neg[pc]) {  // AND chain with negated operands
+        const std::vector<uint32_t> &q = BP.andops[pc];
+        const uint32_t c = q.size() > 2 ? T.boolslot(q[2]) : T.boolslot(MGP_BOOL_TRUE);
+        const uint32_t d = q.size() > 3 ? T.boolslot(q[3]) : T.boolslot(MGP_BOOL_TRUE);
+        const uint32_t id = MGP_U_BAND4N_FIRST + BP.neg[pc] - 1u;
+        emit(w0_of(id, id), T.boolslot(q[0]) | (T.boolslot(q[1]) << 16), c | (d << 16), T.boolslot(dst) << 16);
         continue;
       }
       if (op == MGP_OP_BAND && BP.andops[pc].size() > 2) {

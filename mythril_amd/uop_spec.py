@@ -70,7 +70,10 @@ B_KINDS = ("none",) + KINDS
 FETCH = [f"F_{ka}_{kb}_A" for ka in KINDS for kb in B_KINDS] + \
         [f"F_{ka}_{kb}_C" for ka in KINDS[1:] for kb in B_KINDS]
 
-BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ", "BAND4", "BANDN"]
+# BAND4N<m>: BAND4 with the operands of mask m (bit 0 = first .. bit 3 = fourth) negated (a
+# BNOT whose result only one AND chain reads, folded by the translator)
+BAND4N = [f"BAND4N{m}" for m in range(1, 16)]
+BOOL_OPS = ["PAGE", "RET", "BAND", "BOR", "BXOR", "BNOT", "BITE", "BEQ", "BAND4", "BANDN"] + BAND4N
 # vA -> the lane's candidate row w2[15:0] (a spilled BV slot; read back as a VAR operand)
 MEM_OPS = ["VST"]
 BV_BIN = ["ADD", "SUB", "MUL", "AND", "OR", "XOR", "SHL", "LSHR", "ASHR", "DIV"]
@@ -164,6 +167,7 @@ def c_header() -> str:
     ]
     lines.append("static const unsigned short kXrBase[%d] = {%s};" % (len(XR_BASE), ", ".join(
         f"MGP_U_{o}" for o in XR_BASE)))
+    lines.append(f"#define MGP_U_BAND4N_FIRST {ID[BAND4N[0]]}")
     lines.append(f"#define MGP_U_XV_FIRST {ID[XV_OPS[0]]}")
     lines.append("static const short kXv[%d][4] = {%s};" % (len(XV_LIST), ", ".join(
         "{%d, %d, %d, MGP_U_%s}" % (KINDS.index(ka), B_KINDS.index(kb) - 1, t == "C", o) for ka, kb, t, o in XV_LIST)))

@@ -169,6 +169,11 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
             if op == "BAND4":  # AND of four Bool slots (w1 lo/hi, w2 lo/hi)
                 bools[w3 >> 17] = a and b and c and bools[(w2 >> 16) >> 1]
                 continue
+            if op.startswith("BAND4N"):  # the same with the operands of mask m negated
+                m = int(op[6:])
+                xs = [a, b, c, bools[(w2 >> 16) >> 1]]
+                bools[w3 >> 17] = all(x != bool(m >> i & 1) for i, x in enumerate(xs))
+                continue
             r = {"BAND": a and b, "BOR": a or b, "BXOR": a != b, "BNOT": not a,
                  "BITE": b if a else c, "BEQ": a == b, "BANDN": a and not b}[op]
             bools[w3 >> 17] = r

@@ -47,6 +47,10 @@ PG = RV + 8 * U.REG_POS   # v[122:126]: the current 64-uop page, uop k in lane k
                  #   PG first-handler address (low 32 bits), PG+1 op-handler address, PG+2..4 w1-w3
 VD = PG + 5      # v127: descriptor / loop state / diagnostic lanes (SGPRs above s63 are Bools)
 NVGPR = (VD + 1 + 7) // 8 * 8   # 128 with the 10-position bank (4 waves/SIMD); 96 with 6 (5 waves)
+# 64-B pool lines of the state's constants pulled into the scalar cache by each wave, hidden
+# behind the variable loads (4 measured 0.8 % faster than none and than 8; MGP_POOL_PF A/B)
+POOL_PREFETCH_LINES = int(os.environ.get("MGP_POOL_PF", "4"))
+POOL_PREFETCH_CHUNK = bool(int(os.environ.get("MGP_POOL_PF_CHUNK", "0")))   # again at each chunk
 HALIGN = int(os.environ.get("MGP_HALIGN", "2"))   # log2 byte alignment of handler entries
 # division registers inside T
 D_FA, D_FB = 32, 34          # f64 pairs: dividend / reciprocal, divisor / estimate
@@ -664,10 +668,14 @@ def next_chunk():
       "v_min_u32 v4, s2, v0",
       "v_lshlrev_b32 v4, 4, v4",
       f"global_load_dwordx4 {vr(PG, 4)}, v4, s[4:5]")
+    if POOL_PREFETCH_CHUNK:
+        A.lines.extend(pool_prefetch("r"))
     A.lines.append(var_preload("r").rstrip("\n"))
     page_decode()
     A("s_branch .Lrestart")
     A.label(".Lpage0_kept")
+    if POOL_PREFETCH_CHUNK:
+        A.lines.extend(pool_prefetch("k"))
     A.lines.append(var_preload("k").rstrip("\n"))
     A.label(".Lrestart")
     A("s_mov_b64 s[64:65], 0",
@@ -1627,7 +1635,7 @@ PROLOGUE = """\
   s_add_u32 s14, s88, s90
   s_addc_u32 s15, s89, 0
   s_mov_b32 s2, s87
-  // candidates of this state: cands + state * n_vars * n_cand * 32, layout [var][half][cand] x 16 B
+{POOL_PREFETCH}  // candidates of this state: cands + state * n_vars * n_cand * 32, layout [var][half][cand] x 16 B
   s_lshl_b32 s8, s73, 5
   s_mul_i32 s92, s74, s8
   s_mul_i32 s6, s84, s92
@@ -1725,6 +1733,20 @@ def metadata():
     return "\n".join(out), ksize
 
 
+def pool_prefetch(tag: str) -> list:
+    """The first POOL_PREFETCH_LINES 64-B lines of the pool (within n_pool = s91 & 0xff) into
+    the scalar cache: s_load_dwordx16 into s[24:39], results discarded (those SGPRs are free
+    until the first uop); var_preload's wait includes them."""
+    if not POOL_PREFETCH_LINES:
+        return []
+    pf = ["  s_and_b32 s93, s91, 0xff"]
+    for i in range(POOL_PREFETCH_LINES):
+        pf += [f"  s_cmp_le_u32 s93, {2 * i}", f"  s_cbranch_scc1 .Lpoolpf_end{tag}",
+               f"  s_load_dwordx16 s[24:39], s[14:15], {64 * i:#x}"]
+    pf.append(f".Lpoolpf_end{tag}:")
+    return pf
+
+
 def var_preload(tag: str = "") -> str:
     """Variables v < REG_VARS the program reads (mask bit 8+v of s91) -> v[64+8v : 72+8v]
     (index clamped to n_vars-1); the others are never read and not loaded."""
@@ -1738,8 +1760,10 @@ def var_preload(tag: str = "") -> str:
                 f"  global_load_dwordx4 v[{r + 4}:{r + 7}], v3, s[92:93]",
                 f".Lnovar{tag}{i}:"]
     # page, pool and variables all present before the first uop (the variable loads were
-    # issued right behind the page and pool, so this adds little over waiting for those)
-    out.append("  s_waitcnt vmcnt(0)")
+    # issued right behind the page and pool, so this adds little over waiting for those);
+    # in the prologue also the pool prefetch (scalar loads)
+    pf = POOL_PREFETCH_LINES and (tag == "" or POOL_PREFETCH_CHUNK)
+    out.append("  s_waitcnt vmcnt(0)" + (" lgkmcnt(0)" if pf else ""))
     return "\n".join(out) + "\n"
 
 
@@ -1758,7 +1782,8 @@ def generate() -> str:
     globals()["A"] = dec
     page_decode()
     globals()["A"] = global_A
-    pro = (PROLOGUE.replace("v126", v(VD)).replace("v[112:115]", vr(PG, 4))
+    pf = pool_prefetch("")
+    pro = (PROLOGUE.replace("{POOL_PREFETCH}", "\n".join(pf) + ("\n" if pf else "")).replace("v126", v(VD)).replace("v[112:115]", vr(PG, 4))
            .replace("{VAR_PRELOAD}", var_preload()).replace("{FIRST_DISPATCH}", "\n".join(first.lines))
            .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n"))
     A.lines.append(pro)

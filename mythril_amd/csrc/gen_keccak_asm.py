@@ -27,6 +27,7 @@ No scalar memory writes (vector stores only).
 """
 from __future__ import annotations
 
+import os
 import sys
 from typing import Dict, List, Optional, Tuple
 
@@ -159,7 +160,10 @@ def conflicts(p: Prog, phys: Dict[int, int]) -> Tuple[int, int, int]:
     return tot, pair, three
 
 
-def generate(n_phys: int = 100, theta: str = "bitop3") -> Tuple[str, dict]:
+N_PHYS = int(os.environ.get("MGP_KECCAK_VGPRS", "72"))   # register budget: 72 -> 7 waves/SIMD
+
+
+def generate(n_phys: int = N_PHYS, theta: str = "bitop3") -> Tuple[str, dict]:
     p = Prog()
     # inputs: lanes 0..7 from the four loads (v[4:19]), lane 8 lo = 0x01, lane 16 hi =
     # 0x80000000 (pad), every other half 0; constants materialised by v_mov
@@ -194,15 +198,34 @@ def generate(n_phys: int = 100, theta: str = "bitop3") -> Tuple[str, dict]:
             lines.append(f"  v_mov_b32 v{phys[d]}, {imm:#x}")
         else:
             raise ValueError(kind)
-    # digest = lanes 0..3: gathered into v[4:11] (free again: the loads' registers were
-    # renamed away in round 0) unless already in place
+    # digest = lanes 0..3 -> v[4:11] by a parallel copy: at the end only those 8 values are
+    # live, so any other register is a scratch for breaking a cycle (no registers past the
+    # program's own: the VGPR count, hence the waves per SIMD, is the allocation's)
     dig = [phys[out[l][h]] for l in range(4) for h in range(2)]
-    tmp_base = (used + 3) // 4 * 4  # beyond the program's registers (no live value), tuple-aligned
-    for j, r in enumerate(dig):
-        lines.append(f"  v_mov_b32 v{tmp_base + j}, v{r}")
-    stats = dict(zip(("bitop3", "shared_pair", "one_bank"), conflicts(p, phys)), vgprs=tmp_base + 8,
+    lines += parallel_copy({4 + j: r for j, r in enumerate(dig)}, scratch=next(
+        r for r in range(FIRST_FREE, used + 9) if r not in dig and not 4 <= r < 12))
+    stats = dict(zip(("bitop3", "shared_pair", "one_bank"), conflicts(p, phys)), vgprs=max(used, 12),
                  alignbit=sum(1 for o in p.ops if o[0] == "alignbit"), ops=len(p.ops))
-    return "\n".join(lines), dict(stats, out_base=tmp_base)
+    return "\n".join(lines), dict(stats, out_base=4)
+
+
+def parallel_copy(moves: Dict[int, int], scratch: int) -> List[str]:
+    """v_mov sequence for dst <- src (all at once): a move whose destination no pending move
+    still reads goes first; a cycle is broken through `scratch`."""
+    pend = {d: s_ for d, s_ in moves.items() if d != s_}
+    out = []
+    while pend:
+        ready = [d for d in pend if d not in pend.values()]
+        if ready:
+            d = ready[0]
+            out.append(f"  v_mov_b32 v{d}, v{pend.pop(d)}")
+            continue
+        d = next(iter(pend))          # every destination is still a source: a cycle
+        out.append(f"  v_mov_b32 v{scratch}, v{d}")
+        for k, v_ in pend.items():
+            if v_ == d:
+                pend[k] = scratch
+    return out
 
 
 PROLOGUE = """\

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Cache / stall counters of the interpreter with and without the 5-wave descriptor
 # (MGP_W5_MAX_SLOTS=4 vs -1), separate PMC passes:  bash profiles/run_pmc_w5.sh <tag>
+# (measured on commit a4ff032, which had the 96-VGPR descriptor and the knob; the 10-position
+# register bank that followed needs all 128 VGPRs, so later trees ignore MGP_W5_MAX_SLOTS)
 set -e
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp

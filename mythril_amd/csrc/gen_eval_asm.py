@@ -351,7 +351,10 @@ def handler(name):
 
 
 def wait_operands():
-    A("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    """Operands of the op: LDS slot and pool-constant reads (a fetch handler with an HBM
+    variable operand waits for its own vector loads before it dispatches, so outstanding
+    spill stores do not hold up the op handlers)."""
+    A("s_waitcnt lgkmcnt(0)")
 
 
 # uop flag bits (w2 = s18, w3 = s19; see uop_spec)
@@ -553,6 +556,8 @@ def make_fetch(name):
             const_finish(VB, "B")
         if ka == "const":
             const_finish(VA if tgt == "A" else VC, "A")
+        if "var" in (ka, kb):
+            A("s_waitcnt vmcnt(0)")
         op_dispatch()
     return body
 
@@ -1788,7 +1793,7 @@ def generate() -> str:
            .replace("{PAGE_DECODE}", "\n".join(dec.lines) + "\n"))
     A.lines.append(pro)
     no_prefetch = set(U.FETCH) | set(U.XS_OPS) | set(U.XC_OPS) | set(U.XV_OPS) | {"INVALID", "RET", "PAGE"}
-    wait = "  s_waitcnt vmcnt(0) lgkmcnt(0)"
+    wait = "  s_waitcnt lgkmcnt(0)"
     for name in U.HANDLERS:
         # two entries per handler: mgp_h_<name> (reached from a fetch handler, whose
         # operand loads are still in flight) and mgp_hd_<name> (dispatched directly: its

@@ -532,6 +532,67 @@ def _bool_fold_states(rng, n):
     return out
 
 
+def _band4n_states(rng, n):
+    """DAGs whose BNOTs (not next to their reader) feed AND chains of 2-4 operands (the
+    translator's BAND4N fold), some BNOT results read again later by a BOR or an ITE (no
+    fold allowed there), over three 8-bit variables."""
+    w = 8
+    cmps = [S.EQ, S.ULT, S.UGE, S.ULE, S.SLT, S.SGE, S.UGT]
+    out = []
+    for _ in range(n):
+        nl = [[S.VAR, w, -1, -1, -1, k, 0] for k in range(3)]
+        cl = [int(x) for x in rng.integers(0, 256, size=4)]
+        nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(4)]
+        pool = []
+        for _ in range(int(rng.integers(4, 9))):
+            a, b = int(rng.integers(0, 7)), int(rng.integers(0, 7))
+            nl.append([cmps[int(rng.integers(len(cmps)))], 1, a, b, -1, 0, 0])
+            pool.append(len(nl) - 1)
+            if rng.random() < 0.5:
+                nl.append([S.BNOT, 1, len(nl) - 1 if rng.random() < 0.3 else int(rng.choice(pool)), -1, -1, 0, 0])
+                pool.append(len(nl) - 1)
+        chains = []
+        for _ in range(int(rng.integers(1, 4))):
+            ops = [int(x) for x in rng.choice(pool, size=int(rng.integers(2, 5)))]
+            acc = ops[0]
+            for o in ops[1:]:
+                nl.append([S.BAND, 1, acc, o, -1, 0, 0])
+                acc = len(nl) - 1
+            chains.append(acc)
+        root = chains[0]
+        for c in chains[1:]:
+            nl.append([S.BOR, 1, root, c, -1, 0, 0])
+            root = len(nl) - 1
+        if rng.random() < 0.3:       # a BNOT result read again after its chain
+            nl.append([S.BOR, 1, root, int(rng.choice(pool)), -1, 0, 0])
+            root = len(nl) - 1
+        if rng.random() < 0.2:       # ... or as an ITE condition
+            nl.append([S.ITE, w, int(rng.choice(pool)), 0, 1, 0, 0])
+            nl.append([S.ULT, 1, len(nl) - 1, 2, -1, 0, 0])
+            nl.append([S.BOR, 1, root, len(nl) - 1, -1, 0, 0])
+            root = len(nl) - 1
+        out.append((nl, cl))
+    return out
+
+
+def test_band4n_folds_vs_oracle(mgp_ctx):
+    """BNOTs folded into AND chains (BAND4N) against the C oracle on every candidate (both
+    engines; the HIP engine runs the v1 program, which has no fold)."""
+    rng = np.random.default_rng(91)
+    states = _band4n_states(rng, 600)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    n_cand = 256
+    vals = rng.integers(0, 256, size=(len(states), n_cand, 3))
+    cands = np.zeros((len(states), n_cand, 3, 8), np.uint32)
+    cands[..., 0] = vals
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    bad = np.nonzero(first != ref)[0]
+    assert bad.size == 0, f"{bad.size} states differ, e.g. {bad[:5]}"
+
+
 def test_bool_folds_vs_oracle(mgp_ctx):
     """Compare -> BAND/BOR (BCOMB) and BNOT -> BAND (BANDN) folds of the gfx950 uop
     translation against the C oracle on every candidate (both engines)."""

@@ -563,3 +563,34 @@ def test_bool_folds_uop_reference_matches_oracle():
         u0 = UR.uop_offset(words, int(po[s]))
         folded += sum(bool(int(words[u0 + 6 + 4 * k]) & U.F_BCOMB) for k in range(int(words[u0])))
     assert folded > 100
+
+
+def test_band4n_folds_uop_reference_matches_oracle():
+    """BNOTs read by one AND chain fold into BAND4N<mask>; BNOTs read again elsewhere stay.
+    The uop reference interpreter agrees with the C oracle on every candidate, and the fold
+    fires (CPU side of tests/test_gpu_parity.py::test_band4n_folds_vs_oracle)."""
+    from oracle import coracle
+
+    from .test_gpu_parity import _band4n_states
+
+    rng = np.random.default_rng(92)
+    states = _band4n_states(rng, 300)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    n_cand = 12
+    vals = rng.integers(0, 256, size=(len(states), n_cand, 3))
+    cands = np.zeros((len(states), n_cand, 3, 8), np.uint32)
+    cands[..., 0] = vals
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    names = UR._names()
+    folded = kept = 0
+    for s in range(len(states)):
+        rows = [[int(x) for x in vals[s, k]] for k in range(n_cand)]
+        assert UR.first_sat_uops(words, int(po[s]), rows) == ref[s], s
+        u0 = UR.uop_offset(words, int(po[s]))
+        for k in range(int(words[u0])):
+            nm = names[int(words[u0 + 4 + 4 * k]) & 0xFFFF]
+            folded += nm.startswith("BAND4N")
+            kept += nm == "BNOT"
+    assert folded > 50 and kept > 0, (folded, kept)

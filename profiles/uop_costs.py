@@ -58,6 +58,14 @@ def chain(op, k, width=256, bkind="var", store_every=0):
         nl.append([S.EQ, 1, 0, 1, -1, 0, 0])
         nl.append([S.BOR, 1, b, len(nl) - 1, -1, 0, 0])
         return nl, consts
+    if op == "MIX4":  # four cheap ops in rotation (handler switching on every uop)
+        for i in range(k):
+            nl.append([(S.ADD, S.XOR, S.SUB, S.OR)[i % 4], 256, t, b, -1, 0, 0])
+            t = len(nl) - 1
+        nl.append([S.EQ, 1, t, 0, -1, 0, 0])
+        nl.append([S.EQ, 1, 1, t, -1, 0, 0])
+        nl.append([S.BOR, 1, len(nl) - 2, len(nl) - 1, -1, 0, 0])
+        return nl, consts
     for i in range(k):
         if op in (S.EQ, S.ULT, S.SLT):
             c = len(nl)
@@ -131,7 +139,7 @@ def main():
     waves = args.states * (n_cand // 64)
     base_t, _, _ = run(*chain(S.ADD, 0), args.states, n_cand, torch, dev, stream, sh)
     rows = []
-    cases = [("FIB slot+st", "FIB", "var"), ("BAND/BOR", "BAND", "var"), ("ADD var", S.ADD, "var"), ("ADD const", S.ADD, "const"), ("SUB var", S.SUB, "var"),
+    cases = [("MIX4 var", "MIX4", "var"), ("FIB slot+st", "FIB", "var"), ("BAND/BOR", "BAND", "var"), ("ADD var", S.ADD, "var"), ("ADD const", S.ADD, "const"), ("SUB var", S.SUB, "var"),
              ("XOR var", S.XOR, "var"), ("MUL var", S.MUL, "var"), ("UDIV var", S.UDIV, "var"),
              ("UREM var", S.UREM, "var"), ("SDIV var", S.SDIV, "var"),
              ("SHL var", S.SHL, "var"), ("LSHR const", S.LSHR, "const"),

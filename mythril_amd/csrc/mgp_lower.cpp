@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/mgp.h"
+#include "mgp_buf.h"
 
 int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out);  // mgp_uop.cpp
 
@@ -1221,7 +1222,7 @@ static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32
 
 // In-library entry point (mgp_pipeline.cpp): the lowered programs as one vector.
 int mgp_lower_vec(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states, const uint32_t *consts,
-                  const uint64_t *const_offsets, uint32_t max_slots, std::vector<uint32_t> &words,
+                  const uint64_t *const_offsets, uint32_t max_slots, U32Buf &words,
                   std::vector<uint64_t> &offs, std::vector<uint8_t> &status) {
   std::vector<Lowered> res;
   const int rc = lower_all(nodes, node_offsets, n_states, consts, const_offsets, max_slots, res);

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/mgp.h"
+#include "mgp_buf.h"
 
 extern "C" {
 hipError_t mgp_launch_eval(const uint32_t *words, const uint64_t *offs, uint32_t n_states, const uint32_t *cands,
@@ -54,7 +55,7 @@ int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device);
 int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg);
 }
 int mgp_lower_vec(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states, const uint32_t *consts,
-                  const uint64_t *const_offsets, uint32_t max_slots, std::vector<uint32_t> &words,
+                  const uint64_t *const_offsets, uint32_t max_slots, U32Buf &words,
                   std::vector<uint64_t> &offs, std::vector<uint8_t> &status);
 
 namespace {
@@ -172,7 +173,7 @@ void alias_tables(uint32_t n_states, const uint64_t *vo, const uint32_t *vw, con
 struct ProgCache {
   struct Entry {
     std::vector<uint8_t> key;
-    std::vector<uint32_t> words;
+    std::shared_ptr<const std::vector<uint32_t>> words;  // shared: a hit outlives its eviction
     uint8_t status;
   };
   std::mutex mu;
@@ -197,75 +198,92 @@ uint64_t fnv(const uint8_t *p, size_t n, uint64_t h = 1469598103934665603ull) {
   return h;
 }
 
+// Keys and hashes are built in parallel without the lock; the lock covers the lookups
+// and, later, the inserts.  A hit holds its program by shared_ptr, so the copy into the
+// batch's program vector runs in parallel outside the lock, and other threads (one host
+// thread per device) lower their misses concurrently.
 int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states, const uint32_t *consts,
-                 const uint64_t *coff, std::vector<uint32_t> &words, std::vector<uint64_t> &offs,
+                 const uint64_t *coff, U32Buf &words, std::vector<uint64_t> &offs,
                  std::vector<uint8_t> &status) {
   ProgCache &C = prog_cache();
   std::vector<std::vector<uint8_t>> keys(n_states);
   std::vector<uint64_t> hs(n_states);
-  std::vector<const ProgCache::Entry *> hit(n_states, nullptr);
+#pragma omp parallel for schedule(dynamic, 8)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    const size_t nb = (noff[s + 1] - noff[s]) * sizeof(mgp_node), cb = (coff[s + 1] - coff[s]) * 32u;
+    keys[s].resize(16 + nb + cb);
+    const uint64_t hdr[2] = {noff[s + 1] - noff[s], coff[s + 1] - coff[s]};
+    memcpy(keys[s].data(), hdr, 16);
+    memcpy(keys[s].data() + 16, nodes + noff[s], nb);
+    if (cb) memcpy(keys[s].data() + 16 + nb, consts + coff[s] * 8u, cb);
+    hs[s] = fnv(keys[s].data(), keys[s].size());
+  }
+  std::vector<std::shared_ptr<const std::vector<uint32_t>>> hit(n_states);
+  std::vector<uint8_t> hit_status(n_states, 0);
   std::vector<uint32_t> miss;
   {
     std::lock_guard<std::mutex> lk(C.mu);
     for (uint32_t s = 0; s < n_states; ++s) {
-      const size_t nb = (noff[s + 1] - noff[s]) * sizeof(mgp_node), cb = (coff[s + 1] - coff[s]) * 32u;
-      keys[s].resize(16 + nb + cb);
-      const uint64_t hdr[2] = {noff[s + 1] - noff[s], coff[s + 1] - coff[s]};
-      memcpy(keys[s].data(), hdr, 16);
-      memcpy(keys[s].data() + 16, nodes + noff[s], nb);
-      if (cb) memcpy(keys[s].data() + 16 + nb, consts + coff[s] * 8u, cb);
-      hs[s] = fnv(keys[s].data(), keys[s].size());
       auto it = C.map.find(hs[s]);
-      if (it != C.map.end() && it->second.key == keys[s]) hit[s] = &it->second;
-      else miss.push_back(s);
-    }
-    // the hits are copied below while holding the lock (an insert may evict them)
-    std::vector<mgp_node> mn;
-    std::vector<uint32_t> mc;
-    std::vector<uint64_t> mno(1, 0), mco(1, 0);
-    for (uint32_t s : miss) {
-      mn.insert(mn.end(), nodes + noff[s], nodes + noff[s + 1]);
-      mc.insert(mc.end(), consts + coff[s] * 8u, consts + coff[s + 1] * 8u);
-      mno.push_back(mn.size());
-      mco.push_back(mc.size() / 8u);
-    }
-    std::vector<uint32_t> mw;
-    std::vector<uint64_t> mo;
-    std::vector<uint8_t> mst;
-    if (!miss.empty()) {
-      if (mc.empty()) mc.assign(8, 0u);
-      const int rc = mgp_lower_vec(mn.data(), mno.data(), (uint32_t)miss.size(), mc.data(), mco.data(), 0, mw, mo,
-                                   mst);
-      if (rc != MGP_OK) return rc;
-    }
-    offs.assign((size_t)n_states + 1, 0u);
-    status.assign(n_states, 0u);
-    std::vector<int64_t> mi(n_states, -1);
-    for (size_t k = 0; k < miss.size(); ++k) mi[miss[k]] = (int64_t)k;
-    for (uint32_t s = 0; s < n_states; ++s)
-      offs[s + 1] = offs[s] + (mi[s] >= 0 ? mo[mi[s] + 1] - mo[mi[s]] : hit[s]->words.size());
-    words.resize(offs[n_states]);
-    for (uint32_t s = 0; s < n_states; ++s) {
-      if (mi[s] >= 0) {
-        memcpy(words.data() + offs[s], mw.data() + mo[mi[s]], (mo[mi[s] + 1] - mo[mi[s]]) * 4u);
-        status[s] = mst[mi[s]];
+      if (it != C.map.end() && it->second.key == keys[s]) {
+        hit[s] = it->second.words;
+        hit_status[s] = it->second.status;
       } else {
-        memcpy(words.data() + offs[s], hit[s]->words.data(), hit[s]->words.size() * 4u);
-        status[s] = hit[s]->status;
+        miss.push_back(s);
       }
     }
+  }
+  std::vector<mgp_node> mn;
+  std::vector<uint32_t> mc;
+  std::vector<uint64_t> mno(1, 0), mco(1, 0);
+  for (uint32_t s : miss) {
+    mn.insert(mn.end(), nodes + noff[s], nodes + noff[s + 1]);
+    mc.insert(mc.end(), consts + coff[s] * 8u, consts + coff[s + 1] * 8u);
+    mno.push_back(mn.size());
+    mco.push_back(mc.size() / 8u);
+  }
+  U32Buf mw;
+  std::vector<uint64_t> mo;
+  std::vector<uint8_t> mst;
+  if (!miss.empty()) {
+    if (mc.empty()) mc.assign(8, 0u);
+    const int rc = mgp_lower_vec(mn.data(), mno.data(), (uint32_t)miss.size(), mc.data(), mco.data(), 0, mw, mo, mst);
+    if (rc != MGP_OK) return rc;
+  }
+  offs.assign((size_t)n_states + 1, 0u);
+  status.assign(n_states, 0u);
+  std::vector<int64_t> mi(n_states, -1);
+  for (size_t k = 0; k < miss.size(); ++k) mi[miss[k]] = (int64_t)k;
+  for (uint32_t s = 0; s < n_states; ++s)
+    offs[s + 1] = offs[s] + (mi[s] >= 0 ? mo[mi[s] + 1] - mo[mi[s]] : hit[s]->size());
+  words.resize(offs[n_states]);
+  // the new programs as cache entries (built in parallel, inserted under the lock below)
+  std::vector<ProgCache::Entry> ents(miss.size());
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    if (mi[s] >= 0) {
+      const size_t k = (size_t)mi[s];
+      memcpy(words.data() + offs[s], mw.data() + mo[k], (mo[k + 1] - mo[k]) * 4u);
+      status[s] = mst[k];
+      ents[k].key = std::move(keys[s]);
+      ents[k].words = std::make_shared<const std::vector<uint32_t>>(mw.begin() + mo[k], mw.begin() + mo[k + 1]);
+      ents[k].status = mst[k];
+    } else {
+      memcpy(words.data() + offs[s], hit[s]->data(), hit[s]->size() * 4u);
+      status[s] = hit_status[s];
+    }
+  }
+  if (!miss.empty()) {
     // insert the new programs, evicting the oldest past the byte budget
+    std::lock_guard<std::mutex> lk(C.mu);
     for (size_t k = 0; k < miss.size(); ++k) {
       const uint32_t s = miss[k];
-      ProgCache::Entry e;
-      e.key = std::move(keys[s]);
-      e.words.assign(mw.begin() + mo[k], mw.begin() + mo[k + 1]);
-      e.status = mst[k];
-      const size_t sz = e.key.size() + e.words.size() * 4u;
+      ProgCache::Entry &e = ents[k];
+      const size_t sz = e.key.size() + e.words->size() * 4u;
       if (sz > ProgCache::kMaxBytes / 8) continue;
       auto it = C.map.find(hs[s]);
       if (it != C.map.end()) {
-        C.bytes -= it->second.key.size() + it->second.words.size() * 4u;
+        C.bytes -= it->second.key.size() + it->second.words->size() * 4u;
         it->second = std::move(e);
       } else {
         C.map.emplace(hs[s], std::move(e));
@@ -275,7 +293,7 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
       while (C.bytes > ProgCache::kMaxBytes && C.head < C.fifo.size()) {
         auto old = C.map.find(C.fifo[C.head++]);
         if (old == C.map.end()) continue;
-        C.bytes -= old->second.key.size() + old->second.words.size() * 4u;
+        C.bytes -= old->second.key.size() + old->second.words->size() * 4u;
         C.map.erase(old);
       }
       if (C.head > 4096 && C.head * 2 > C.fifo.size()) {
@@ -349,7 +367,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   const uint32_t *cp = consts.n ? (const uint32_t *)consts.p : zero8;
 
   // 1. lower the GPU programs (programs lowered by an earlier call come from the cache)
-  std::vector<uint32_t> words;
+  U32Buf words;
   std::vector<uint64_t> offs;
   std::vector<uint8_t> status;
   int rc = lower_cached((const mgp_node *)gnodes.p, (const uint64_t *)gnoff.p, n_states, cp,
@@ -449,7 +467,15 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   if (e == hipSuccess) e = D.ensure_host(std::max(up, first_bytes + (out_witness ? wit_bytes : 0)));
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
   uint8_t *H = (uint8_t *)D.host;
-  memcpy(H + at[0], words.data(), pre[0]);
+  {  // the programs (hundreds of MB for contract states): copied in 4-MiB pieces in parallel
+    const size_t piece = (size_t)4 << 20, n_pieces = (pre[0] + piece - 1) / piece;
+    const uint8_t *src = (const uint8_t *)words.data();
+#pragma omp parallel for schedule(dynamic, 1) if (n_pieces > 1)
+    for (int64_t k = 0; k < (int64_t)n_pieces; ++k) {
+      const size_t o = (size_t)k * piece;
+      memcpy(H + at[0] + o, src + o, std::min(piece, pre[0] - o));
+    }
+  }
   memcpy(H + at[1], offs.data(), pre[1]);
   memcpy(H + at[2], order.data(), pre[2]);
   for (int i = 0; i < 21; ++i)

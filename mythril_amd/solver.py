@@ -602,6 +602,7 @@ class Prefilter:
         t_dec = time.perf_counter()
         dec_ms = 0.0
         found = 0
+        round2_ms = [0.0] * 5  # the second round's check_batch stages (lower, refute, upload, GPU, copy)
         for grp in groups:
             GB = Batch([states[retry[k]] for k in grp])
             gv = max(1, GB.n_vars())
@@ -613,7 +614,8 @@ class Prefilter:
                                                   state_keys=GB.state_key, ctx=ctx if on_gpu else None)
             dec_ms += 1e3 * (time.perf_counter() - td)
             prof["decide_on_gpu"] = bool(on_gpu)
-            f2, w2, _, _ = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
+            f2, w2, _, st2 = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
+            round2_ms = [a + float(b) for a, b in zip(round2_ms, st2)]
             unsafe = (GB.flags & FE_SAT_UNSAFE) != 0
             for k, j in enumerate(grp):
                 i = retry[j]
@@ -623,6 +625,7 @@ class Prefilter:
                     found += 1
             GB.close()
         prof["decide_host_ms"] = dec_ms
+        prof["round2_stages"] = dict(zip(("lower", "refute", "upload_launch", "gpu_wait", "copy_back"), round2_ms))
         prof["decide_ms"] = 1e3 * (time.perf_counter() - t_dec)  # host decision rows + their GPU round
         prof["decide_states"] = len(retry)
         prof["retry_sat"] = found

@@ -215,6 +215,9 @@ class UnsatCores:
     cache lock only if no reset() happened since the snapshot.
     """
 
+    HALVINGS = 3  # halving rounds before the single deletions (shrink_many)
+    HALVE_MIN = 8  # shortest list a halving round tries
+
     def __init__(self, max_sets: int = 1 << 14):
         self.max_sets = max_sets
         self._lock = threading.RLock()
@@ -296,10 +299,12 @@ class UnsatCores:
 
     @staticmethod
     def shrink_many(N, lists: Sequence[Sequence[Term]], max_terms: int = 32, arena=None) -> List[List[Term]]:
-        """Deletion-based cores of many refuted constraint lists in two native calls: one
-        batch holds every single-constraint deletion of every list (mgp_build_states +
-        mgp_refute); the constraints whose deletion breaks a refutation form that list's
-        core if a second batched refute confirms it alone.  `arena`: the term arena to read
+        """Deletion-based cores of many refuted constraint lists in a few batched native
+        calls (mgp_build_states + mgp_refute): up to HALVINGS rounds that keep the first or
+        second half of a list when it alone is refuted, then one batch with every
+        single-constraint deletion of every list; the constraints whose deletion breaks a
+        refutation form that list's core if a last batched refute confirms it alone.  Every
+        set returned is one the refuter refuted.  `arena`: the term arena to read
         (a snapshot for a background shrink; default the live one)."""
         from functools import partial
 
@@ -308,6 +313,27 @@ class UnsatCores:
         Batch = partial(Batch, arena=arena) if arena is not None else Batch
 
         lists = [list(dict.fromkeys(t)) for t in lists]
+        # halving first: a list whose first or second half alone is refuted has a core in
+        # that half, which then needs half the single-deletion trials (and a list that
+        # reaches its contradiction twice, where no single deletion matters, still shrinks)
+        for _ in range(UnsatCores.HALVINGS):
+            idx = [k for k, t in enumerate(lists) if UnsatCores.HALVE_MIN <= len(t) <= max_terms]
+            if not idx:
+                break
+            halves = []
+            for k in idx:
+                m = len(lists[k]) // 2
+                halves += [lists[k][:m], lists[k][m:]]
+            B = Batch(halves)
+            v = N.refute(*B.packed())
+            B.close()
+            changed = False
+            for j, k in enumerate(idx):
+                if v[2 * j] == 1 or v[2 * j + 1] == 1:
+                    lists[k] = halves[2 * j] if v[2 * j] == 1 else halves[2 * j + 1]
+                    changed = True
+            if not changed:
+                break
         trials, owner = [], []
         for k, t in enumerate(lists):
             if 2 <= len(t) <= max_terms:

@@ -191,3 +191,30 @@ def test_decision_rows_per_state_rule():
     assert np.array_equal(SV.Prefilter.rows_per_state(fake, B2), r[::-1])
     B.close()
     B2.close()
+
+
+def test_core_shrink_halving_finds_a_core_of_a_redundant_list():
+    """A list reaching its contradiction twice (no single deletion matters) still shrinks:
+    a halving round keeps the half that is refuted alone (UnsatCores.shrink_many)."""
+    v = [BVS(f"h{i}", 256) for i in range(12)]
+    x, y = BVS("hx", 256), BVS("hy", 256)
+    # first half: one contradiction on x among fillers; second half: another on y
+    first = [ULT(v[0], BVV(9, 256)), x == BVV(1, 256), UGT(v[1], BVV(2, 256)), x == BVV(2, 256),
+             ULT(v[2], BVV(7, 256)), UGT(v[3], BVV(1, 256)), ULT(v[4], BVV(5, 256)), UGT(v[5], BVV(4, 256))]
+    second = [ULT(v[6], BVV(9, 256)), y == BVV(3, 256), UGT(v[7], BVV(2, 256)), ULT(v[8], BVV(7, 256)),
+              y == BVV(4, 256), UGT(v[9], BVV(1, 256)), ULT(v[10], BVV(5, 256)), UGT(v[11], BVV(4, 256))]
+    terms = [c.raw for c in first + second]
+    from mythril_amd.front import Batch
+
+    B = Batch([terms, terms[:8], terms[8:]])
+    assert list(N.refute(*B.packed())) == [1, 1, 1]  # the list, and each half alone
+    B.close()
+    old = SV.UnsatCores.HALVINGS
+    try:
+        SV.UnsatCores.HALVINGS = 0  # single deletions alone: nothing is necessary, the list stays
+        assert SV.UnsatCores.shrink(N, terms) == terms
+        SV.UnsatCores.HALVINGS = old
+        core = SV.UnsatCores.shrink(N, terms)
+    finally:
+        SV.UnsatCores.HALVINGS = old
+    assert set(core) == {first[1].raw, first[3].raw}

@@ -624,13 +624,15 @@ class Prefilter:
         nv = np.diff(SB.var_off).astype(np.int64)
         groups = self._groups(nv, n2) if len(retry) * n2 * max(1, int(nv.max())) * 32 > self.cand_bytes \
             else [list(range(len(retry)))]
-        SB.close()
+        if len(groups) > 1:
+            SB.close()
         t_dec = time.perf_counter()
         dec_ms = 0.0
         found = 0
         round2_ms = [0.0] * 5  # the second round's check_batch stages (lower, refute, upload, GPU, copy)
         for grp in groups:
-            GB = Batch([states[retry[k]] for k in grp])
+            # one group (the usual case): the batch built for the grouping is the round's batch
+            GB = SB if len(groups) == 1 else Batch([states[retry[k]] for k in grp])
             gv = max(1, GB.n_vars())
             rps = self.rows_per_state(GB)
             td = time.perf_counter()

@@ -218,3 +218,29 @@ def test_core_shrink_halving_finds_a_core_of_a_redundant_list():
     finally:
         SV.UnsatCores.HALVINGS = old
     assert set(core) == {first[1].raw, first[3].raw}
+
+
+def test_retry_round_groups(fe):
+    """The second round's open states in one group (its grouping batch reused as the round's
+    batch) or, past cand_bytes, in several (one batch per group): same answers, every open
+    state retried once."""
+    def items():
+        return [SV.Constraints([ULT(BVS(f"rg{i}_{j}", 256), BVV(7 + j, 256)) for j in range(1 + i % 5)])
+                for i in range(24)]
+
+    pf = SV.prefilter()
+    got = {}
+    old = pf.cand_bytes
+    try:
+        # the second cap holds the first round (24 states x n_cand x 5 variables) but not
+        # the second round's larger candidate block
+        pf.retry_cand = 2 * pf.n_cand
+        for cap in (old, 24 * pf.n_cand * 5 * 32):
+            pf.cand_bytes = cap
+            SV.SolverStatistics().reset()
+            got[cap] = SV.batch_is_possible(items())
+            assert SV.SolverStatistics().gpu_retry == 24
+    finally:
+        pf.cand_bytes = old
+        pf.retry_cand = pf.RETRY_CAND
+    assert list(got.values())[0] == list(got.values())[1] == [True] * 24

@@ -317,7 +317,9 @@ class UnsatCores:
         # that half, which then needs half the single-deletion trials (and a list that
         # reaches its contradiction twice, where no single deletion matters, still shrinks)
         for _ in range(UnsatCores.HALVINGS):
-            idx = [k for k, t in enumerate(lists) if UnsatCores.HALVE_MIN <= len(t) <= max_terms]
+            # any length: a path longer than max_terms, too long for single deletions,
+            # can halve into range
+            idx = [k for k, t in enumerate(lists) if len(t) >= UnsatCores.HALVE_MIN]
             if not idx:
                 break
             halves = []

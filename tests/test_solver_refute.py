@@ -244,3 +244,21 @@ def test_retry_round_groups(fe):
         pf.cand_bytes = old
         pf.retry_cand = pf.RETRY_CAND
     assert list(got.values())[0] == list(got.values())[1] == [True] * 24
+
+
+def test_core_shrink_halves_a_list_longer_than_max_terms():
+    """A 48-constraint refuted list (past max_terms = 32, no single-deletion pass) halves
+    into range and shrinks to its two-constraint core."""
+    fill = [ULT(BVS(f"lf{i}", 256), BVV(100 + i, 256)) for i in range(46)]
+    x = BVS("lx", 256)
+    terms = [c.raw for c in fill[:5] + [x == BVV(5, 256)] + fill[5:9] + [x == BVV(6, 256)] + fill[9:]]
+    assert len(terms) == 48
+    old = SV.UnsatCores.HALVINGS
+    try:
+        SV.UnsatCores.HALVINGS = 0
+        assert SV.UnsatCores.shrink(N, terms) == terms  # too long: stored whole
+        SV.UnsatCores.HALVINGS = old
+        core = SV.UnsatCores.shrink(N, terms)
+    finally:
+        SV.UnsatCores.HALVINGS = old
+    assert set(core) == {terms[5], terms[10]}

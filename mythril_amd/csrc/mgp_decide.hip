@@ -96,6 +96,8 @@ __global__ __launch_bounds__(64) void mgp_decide_kernel(const uint8_t *__restric
   d.pair_idx = at<int32_t>(blob, S.pair_idx);
   d.ufs = at<UfApp>(blob, S.ufs);
   d.n_ufs = S.n_ufs;
+  d.cong = at<int32_t>(blob, S.cong);
+  d.n_cong = S.n_cong;
   d.uoff = at<uint32_t>(blob, S.uoff);
   d.ulist = at<uint32_t>(blob, S.ulist);
   d.voff = at<uint32_t>(blob, S.voff);

@@ -293,6 +293,7 @@ MGP_RD AV flip(const AV &a, uint32_t w) {
 enum : uint8_t { OLT = 1, OEQ = 2, OGT = 4, OALL = 7 };
 constexpr uint32_t kVarBit = 0x80000000u;  // a work-list entry naming a variable-table entry
 constexpr uint32_t kUfGroup = 48;          // UF congruence: functions with at most this many applications
+constexpr int kCongDepth = 4;              // structural congruence: operator levels arg_equal looks through
 
 struct Pair { int32_t x, y; uint8_t u, s; };
 struct UfApp { int32_t node, arg; uint32_t fn; uint8_t op; };
@@ -360,6 +361,14 @@ struct Dom {
   // read in tx 2 against the write in tx 1 when both senders are equal)
   const UfApp *ufs = nullptr;
   uint32_t n_ufs = 0;
+  // Structural congruence (round 4): pairs whose two operand nodes apply the same
+  // operator with the same parameters (on the original DAG).  Once arg_equal proves their
+  // operands equal -- a pair known equal, equal exact values, recursively -- the pair is
+  // {=}: f(a, b) = f(a', b') for any operator f.  This is what makes
+  // `calldata[i] != calldata[j] ∧ i == j` UNSAT (tests/laser/state/calldata_test.py:79-91):
+  // both loads are If(i < size, Select(cd, i), 0) with i, j known equal.
+  const int32_t *cong = nullptr;
+  uint32_t n_cong = 0;
   // decision rows: users of each node, VAR nodes of each variable entry, nodes tie() reads
   const uint32_t *uoff = nullptr, *ulist = nullptr, *voff = nullptr, *vlist = nullptr;
   const uint8_t *tie_rel = nullptr;
@@ -429,7 +438,8 @@ struct Dom {
   // equal (depth-limited)
   MGP_RD bool arg_equal(int32_t x0, int32_t y0, int depth0) const {
     // the conjunction over operand pairs, on an explicit stack (no recursion: the device
-    // kernel then needs no dynamic stack); depth <= 3 keeps it within 3 x depth + 1 entries
+    // kernel then needs no dynamic stack); each level pops one entry and pushes at most
+    // three, so depth <= 4 stays within 2 x depth + 1 <= 9 live entries (bounded below anyway)
     struct Q { int32_t x, y, d; } q[16];
     int nq = 0;
     q[nq++] = Q{x0, y0, depth0};
@@ -441,13 +451,17 @@ struct Dom {
       const mgp_node *o = orig ? orig : nd;
       const mgp_node &a = o[x], &b = o[y];
       if (a.width != b.width) return false;
+      if (isb[x] && isb[y] && (bs[x] == BT || bs[x] == BF) && bs[x] == bs[y]) continue;  // one known truth value
       if (a.width <= MGP_MAX_WIDTH && !isb[x] && !isb[y]) {
         if (is_exact(av[x]) && is_exact(av[y]) && EQV(av[x].lo, av[y].lo)) continue;
         const uint64_t pk = x < y ? ((uint64_t)(uint32_t)x << 32) | (uint32_t)y : ((uint64_t)(uint32_t)y << 32) | (uint32_t)x;
         const int32_t pi = pair_find(pk);
         if (pi >= 0 && pairs[pi].u == OEQ) continue;
       }
-      if (e.d == 0 || a.op != b.op || a.p0 != b.p0 || a.p1 != b.p1) return false;
+      // (a UF application's p1 is its own fresh-value slot: applications of one function
+      // are congruent whatever their slots)
+      const bool uf = a.op == MGP_OP_UFAPP || a.op == MGP_OP_UFINV;
+      if (e.d == 0 || a.op != b.op || a.p0 != b.p0 || (a.p1 != b.p1 && !uf)) return false;
       if (a.op == MGP_OP_VAR || a.op == MGP_OP_TRUE || a.op == MGP_OP_FALSE) continue;  // same variable / constant
       if (a.op == MGP_OP_CONST) return false;  // different pool entries (narrow ones compared above)
       if (nq + 3 > 16) return false;
@@ -500,6 +514,10 @@ struct Dom {
       if (da != db && da != 2 && db != 2) continue;  // signed with unsigned: no common set
       const uint8_t dom = da == 2 ? db : da;
       if (!set_order(pairs[pa], dom, (uint8_t)(cmp_t[a] | cmp_t[b]))) return false;
+    }
+    for (uint32_t k = 0; k < n_cong; ++k) {
+      Pair &p = pairs[cong[k]];
+      if (p.u != OEQ && arg_equal(p.x, p.y, kCongDepth) && !set_order(p, 2, OEQ)) return false;
     }
     for (uint32_t pj = 0; pj < n_pairs; ++pj) {
       const Pair &p = pairs[pj];

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <memory>
 #include <unordered_map>
 #include <vector>
 
@@ -62,6 +63,7 @@ struct State {
   std::vector<uint8_t> cmp_dom;   // 0 unsigned, 1 signed, 2 both (EQ)
   std::vector<uint8_t> cmp_t;     // orderings (x vs y) under which the node is true
   std::vector<UfApp> ufs;
+  std::vector<int32_t> cong;  // pairs of structurally matching operand nodes (Dom::cong)
   std::unordered_map<uint64_t, int32_t> pair_of;  // (x << 32 | y), x < y -> pairs index
   std::vector<uint64_t> pair_keys;                // the same map, sorted (Dom::pair_find)
   std::vector<int32_t> pair_idx;
@@ -91,6 +93,8 @@ struct State {
     d.pair_idx = pair_idx.data();
     d.ufs = ufs.data();
     d.n_ufs = (uint32_t)ufs.size();
+    d.cong = cong.data();
+    d.n_cong = (uint32_t)cong.size();
     d.uoff = uoff.data();
     d.ulist = ulist.data();
     d.voff = voff.data();
@@ -222,6 +226,17 @@ struct State {
       i = j;
     }
     ufs.swap(keep);
+    // structural congruence candidates: both operands of the pair apply one operator with
+    // the same parameters and width (leaves excluded: one variable is one node's value
+    // already, two constants are compared exactly)
+    cong.clear();
+    for (size_t k = 0; k < pairs.size(); ++k) {
+      const mgp_node &a = o[pairs[k].x], &b = o[pairs[k].y];
+      const bool uf = a.op == MGP_OP_UFAPP || a.op == MGP_OP_UFINV;  // p1: the application's own slot
+      if (a.op != b.op || a.p0 != b.p0 || (a.p1 != b.p1 && !uf) || a.width != b.width) continue;
+      if (a.op == MGP_OP_VAR || a.op == MGP_OP_CONST || a.op == MGP_OP_TRUE || a.op == MGP_OP_FALSE) continue;
+      cong.push_back((int32_t)k);
+    }
     // the pair lookup as a sorted array (the view's binary search, host and device)
     pair_keys.clear();
     pair_idx.clear();
@@ -491,6 +506,28 @@ uint32_t or_rows_mask() {
   return m;
 }
 
+// A per-thread scratch array: grows on demand without value-initialising its entries,
+// and trim() frees it once it holds more than kKeepBytes.
+template <typename T>
+struct RowBuf {
+  static constexpr size_t kKeepBytes = 8u << 20;
+  std::unique_ptr<T[]> p;
+  size_t cap = 0;
+  T *ensure(size_t n) {
+    if (n > cap) {
+      p.reset(new T[n]);
+      cap = n;
+    }
+    return p.get();
+  }
+  void trim() {
+    if (cap * sizeof(T) > kKeepBytes) {
+      p.reset();
+      cap = 0;
+    }
+  }
+};
+
 // Host run of mgpd::decision_row on a private copy of P's base analysis.
 template <typename Put>
 void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, Put &put) {
@@ -499,18 +536,18 @@ void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64
   std::vector<uint8_t> bs(s.bs);
   std::vector<Pair> pairs(s.pairs);
   // the undo log and work list live in per-thread buffers reused across rows (only the
-  // first `cap` entries of each are addressable, as on the device)
-  static thread_local std::vector<UndoRec> undo_buf;
-  static thread_local std::vector<uint32_t> work_buf;
+  // first `cap` entries of each are addressable, as on the device); allocated without a
+  // zero fill, and released after a row of a large state so that one big state does not
+  // pin hundreds of MB per OpenMP thread for the rest of the process
+  static thread_local RowBuf<UndoRec> undo_buf;
+  static thread_local RowBuf<uint32_t> work_buf;
   const uint32_t ucap = undo_cap(s.n, (uint32_t)s.pairs.size(), (uint32_t)s.ufs.size());
   const uint32_t wcap = work_cap(s.n, (uint32_t)s.pairs.size(), (uint32_t)s.ufs.size());
-  if (undo_buf.size() < ucap) undo_buf.resize(ucap);
-  if (work_buf.size() < wcap) work_buf.resize(wcap);
   Stack<UndoRec> undo;
-  undo.p = undo_buf.data();
+  undo.p = undo_buf.ensure(ucap);
   undo.cap = ucap;
   Stack<uint32_t> work;
-  work.p = work_buf.data();
+  work.p = work_buf.ensure(wcap);
   work.cap = wcap;
   Dom d = const_cast<State &>(s).view();
   d.av = av.data();
@@ -522,6 +559,8 @@ void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64
   d.heur = true;
   const PrepView pv = P.view();
   mgpd::decision_row(pv, d, row, c, seed, tag, or_rows_mask(), put);
+  undo_buf.trim();
+  work_buf.trim();
 }
 }  // namespace
 
@@ -676,10 +715,11 @@ struct DevGrow {
   }
 };
 struct DecBufs {
+  std::mutex mu;  // held across one call's upload, launches and synchronize
   DevGrow blob, states, tasks, ws, rows, mask;
 };
-std::mutex g_dec_mu;
-std::map<std::pair<int, void *>, DecBufs> g_dec;  // per (device, stream)
+std::mutex g_dec_mu;                              // guards the map only
+std::map<std::pair<int, void *>, DecBufs> g_dec;  // per (device, stream); entries never move
 
 inline uint64_t up16(uint64_t x) { return (x + 15u) / 16u * 16u; }
 
@@ -748,6 +788,8 @@ extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const 
     h.voff = B.put(S.voff);
     h.vlist = B.put(S.vlist);
     h.tie_rel = B.put(S.tie_rel);
+    h.cong = B.put(S.cong);
+    h.n_cong = (uint32_t)S.cong.size();
     h.slot = B.put(P.slot);
     h.width = B.put(P.width);
     h.node = B.put(P.node);
@@ -783,8 +825,13 @@ extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const 
     }
   }
   if (tasks.empty()) return MGP_OK;
-  std::lock_guard<std::mutex> lk(g_dec_mu);
-  DecBufs &D = g_dec[{dev, stp}];
+  DecBufs *Dp;
+  {
+    std::lock_guard<std::mutex> lk(g_dec_mu);
+    Dp = &g_dec[{dev, stp}];
+  }
+  DecBufs &D = *Dp;
+  std::lock_guard<std::mutex> lk(D.mu);  // contexts on other devices / streams run concurrently
   hipError_t e = hipSetDevice(dev);
   // launches of at most kWsLaunchBytes of workspace each
   std::vector<std::pair<size_t, size_t>> launches;

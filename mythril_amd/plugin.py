@@ -26,9 +26,10 @@ hook:
   (interfaces/cli.py:405-410) -- gets ``window = BFS_WINDOW`` unless the caller
   picks one.  Every other strategy (DFS pops the newest state, basic.py:36-47; the
   random ones draw from the whole list, basic.py:64-92) would see a different work
-  list with a window, so ``initialize`` forces ``window = 1`` for them.  Strategy
-  extensions (BoundedLoopsStrategy, CoverageStrategy) are looked through via their
-  ``super_strategy``.
+  list with a window, so ``initialize`` forces ``window = 1`` for them.  Only
+  BoundedLoopsStrategy is looked through (via ``super_strategy``): its pick reads the
+  popped state alone.  CoverageStrategy's pick depends on coverage, which changes as
+  states run, so under it the window is 1.
 
 Everything the GPU cannot prove satisfiable reaches the fallback solver with
 the reference's own arguments, so the pruning decision is the reference's
@@ -49,12 +50,23 @@ def _constraints_of(global_state):
     return global_state.world_state.constraints
 
 
+# Wrappers whose pick depends only on the popped state itself, so picking a window of states
+# before any of them runs gives the sequential order.  BoundedLoopsStrategy reads the state's
+# own JumpdestCountAnnotation (strategy/extensions/bounded_loops.py:27-141).  CoverageStrategy
+# (plugins/implementations/coverage/coverage_strategy.py:8-37) is NOT one: it picks the first
+# state at an uncovered instruction, and coverage changes as states execute.
+_ORDER_PRESERVING_WRAPPERS = frozenset({"BoundedLoopsStrategy"})
+
+
 def is_breadth_first(strategy) -> bool:
-    """Is the strategy (under any extensions wrapping it) BreadthFirstSearchStrategy?"""
+    """Is the strategy BreadthFirstSearchStrategy, under wrappers that keep its order?"""
     seen = 0
     while strategy is not None and seen < 16:
-        if type(strategy).__name__ == "BreadthFirstSearchStrategy":
+        name = type(strategy).__name__
+        if name == "BreadthFirstSearchStrategy":
             return True
+        if name not in _ORDER_PRESERVING_WRAPPERS:
+            return False
         strategy = getattr(strategy, "super_strategy", None)
         seen += 1
     return False

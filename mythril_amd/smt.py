@@ -115,6 +115,16 @@ class _Arena:
 
 
 ARENA = _Arena()
+_ROW_REFS: Dict[int, "weakref.ref"] = {}   # arena row -> the weakref that frees it
+
+
+def _free_row(tid: int, ref) -> None:
+    try:
+        if _ROW_REFS.get(tid) is ref:
+            del _ROW_REFS[tid]
+            ARENA.release(tid)
+    except Exception:  # interpreter shutdown: the module's globals may be gone
+        pass
 
 
 class Term:
@@ -129,13 +139,12 @@ class Term:
         self.args = args
         self.params = params
         self._h = hash((op, width, tuple(id(a) for a in args), params))
-        self.tid = ARENA.add(op, width, args, params)
-
-    def __del__(self):
-        try:
-            ARENA.release(self.tid)
-        except Exception:  # interpreter shutdown, or a term whose constructor failed
-            pass
+        self.tid = tid = ARENA.add(op, width, args, params)
+        # The row is freed by a weakref callback, not by __del__: CPython runs __del__
+        # before it clears the term's weakrefs, so another thread could still fetch the
+        # dying term from _INTERN (resurrecting it on a freed row); callbacks run after
+        # every weakref to the term is cleared, when no lookup can return it any more.
+        _ROW_REFS[tid] = weakref.ref(self, lambda r, tid=tid: _free_row(tid, r))
 
     def __hash__(self):
         return self._h

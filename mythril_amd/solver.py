@@ -12,6 +12,9 @@ Mirrors, with the same names, argument meaning and error behaviour:
   Solver / Optimize / SolverStatistics
       mythril/laser/smt/solver/solver.py:15-105, solver_statistics.py:8-43 —
       query_count counts every check() that reaches the fallback solver.
+  IndependenceSolver / DependenceMap / DependenceBucket
+      mythril/laser/smt/solver/independence_solver.py:10-153 — buckets of
+      constraints that share no variable, checked separately (one GPU batch).
 
 What changes is the order: a batch of states is first evaluated on the GPU
 (libmgp.so) against candidate assignments; a witness PROVES satisfiability
@@ -30,11 +33,12 @@ import threading
 import os
 import time
 from functools import lru_cache
-from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple, Union
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple, Union
 
 import numpy as np
 
 from . import dag as D
+from . import ir
 from .smt import Bool, Expression, Term, bconst
 
 sat, unsat, unknown = "sat", "unsat", "unknown"
@@ -852,6 +856,138 @@ class Optimize(BaseSolver):
         if r == unsat:
             _cores.add(self.constraints)
         return r
+
+
+def _get_expr_variables(t: Term) -> List[str]:
+    """independence_solver.py:10-22 over terms: the leaves of the expression that are not
+    bit-vector numerals, by name.  z3's leaves are constants (BitVec / Bool symbols, the
+    array constant under a Select, and the Bool literals True / False); a UF application's
+    function symbol is no child, so it is no leaf.  Here an array select is a UFAPP of the
+    function ``array:<name>`` (smt.Array), whose leaf is the array itself."""
+    out: List[str] = []
+    seen: Set[int] = set()
+    stack = [t]
+    while stack:
+        u = stack.pop()
+        if id(u) in seen:
+            continue
+        seen.add(id(u))
+        if u.op == ir.VAR:
+            out.append(str(u.params[0]))
+        elif u.op in (ir.TRUE, ir.FALSE):
+            out.append("True" if u.op == ir.TRUE else "False")
+        elif u.op == ir.UFAPP and str(u.params[1]).startswith("array:"):
+            out.append(str(u.params[1])[len("array:"):])
+        stack.extend(u.args)
+    return out
+
+
+class DependenceBucket:
+    """independence_solver.py:25-35: conditions that share variables."""
+
+    def __init__(self, variables=None, conditions=None):
+        self.variables: List[str] = variables or []
+        self.conditions: List[Term] = conditions or []
+
+
+class DependenceMap:
+    """independence_solver.py:38-83: buckets of conditions, merged when they share a variable."""
+
+    def __init__(self):
+        self.buckets: List[DependenceBucket] = []
+        self.variable_map: Dict[str, DependenceBucket] = {}
+
+    def add_condition(self, condition: Term) -> None:
+        variables = list(dict.fromkeys(_get_expr_variables(condition)))
+        relevant = [b for b in self.buckets if any(self.variable_map.get(v) is b for v in variables)]
+        new_bucket = DependenceBucket(variables, [condition])
+        self.buckets.append(new_bucket)
+        if relevant:
+            relevant.append(new_bucket)
+            new_bucket = self._merge_buckets(relevant)
+        for v in new_bucket.variables:
+            self.variable_map[v] = new_bucket
+
+    def _merge_buckets(self, bucket_list: List[DependenceBucket]) -> DependenceBucket:
+        variables: List[str] = []
+        conditions: List[Term] = []
+        for b in bucket_list:
+            self.buckets.remove(b)
+            variables += b.variables
+            conditions += b.conditions
+        merged = DependenceBucket(variables, conditions)
+        self.buckets.append(merged)
+        return merged
+
+
+class IndependenceSolver(BaseSolver):
+    """independence_solver.py:86-153: the constraints split into buckets that share no
+    variable, each checked on its own, the first non-sat bucket's answer returned.  GPU
+    first: all buckets go to the pre-filter as ONE batch (a bucket is a state); a bucket
+    with a witness is sat, a refuted one unsat; the buckets left open go to the fallback
+    in bucket order, inside one counted check (the reference decorates check() itself
+    with stat_smt_query, so one IndependenceSolver.check is at most one query)."""
+
+    def __init__(self):
+        super().__init__()
+        self.models: List[Dict[str, int]] = []
+
+    def check(self, *args) -> str:
+        if not self.lowerable:
+            return self._fallback_raw()
+        dm = DependenceMap()
+        for c in self.constraints:
+            dm.add_condition(c)
+        buckets = dm.buckets
+        pf = prefilter()
+        answers = pf.check_states([b.conditions for b in buckets]) if pf is not None and buckets else \
+            [("undecided", None)] * len(buckets)
+        self.models = []
+        open_from = None
+        for k, (b, (res, assign)) in enumerate(zip(buckets, answers)):
+            if res == sat and _recheck(b.conditions, assign):
+                self.models.append(assign)
+                continue
+            if res == unsat and _confirm_refutation(b.conditions)[0]:
+                self._model = None
+                return unsat
+            open_from = k
+            break
+        if open_from is not None:
+            return self._fallback_buckets(buckets[open_from:], answers[open_from:])
+        self._model = Model(self.models)
+        return sat
+
+    @stat_smt_query
+    def _fallback_buckets(self, buckets, answers) -> str:
+        for b, (res, assign) in zip(buckets, answers):
+            if res == sat and _recheck(b.conditions, assign):
+                self.models.append(assign)
+                continue
+            if res == unsat and _confirm_refutation(b.conditions)[0]:
+                self._model = None
+                return unsat
+            r, m = get_backend().check(b.conditions, self.timeout)
+            if r != sat:
+                if r == unsat:
+                    _cores.add(b.conditions)
+                self._model = None
+                return r
+            self.models.extend(m.assignments if m is not None else [])
+        self._model = Model(self.models)
+        return sat
+
+    @stat_smt_query
+    def _fallback_raw(self) -> str:
+        r, m = get_backend().check_raw(self.raw_constraints, self.constraints, self.timeout)
+        self._model = m
+        return r
+
+    def reset(self) -> None:
+        self.constraints = []
+
+    def pop(self, num) -> None:
+        self.constraints.pop(num)
 
 
 class _Clock:

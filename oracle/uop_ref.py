@@ -171,8 +171,8 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
                 continue
             if op.startswith("BAND4N"):  # the same with the operands of mask m negated
                 m = int(op[6:])
-                xs = [a, b, c, bools[(w2 >> 16) >> 1]]
-                bools[w3 >> 17] = all(x != bool(m >> i & 1) for i, x in enumerate(xs))
+                ops4 = [a, b, c, bools[(w2 >> 16) >> 1]]   # not `xs`: load() reads the candidates through it
+                bools[w3 >> 17] = all(x != bool(m >> i & 1) for i, x in enumerate(ops4))
                 continue
             r = {"BAND": a and b, "BOR": a or b, "BXOR": a != b, "BNOT": not a,
                  "BITE": b if a else c, "BEQ": a == b, "BANDN": a and not b}[op]

@@ -532,10 +532,14 @@ def _bool_fold_states(rng, n):
     return out
 
 
-def _band4n_states(rng, n):
+def _band4n_states(rng, n, late_vars: int = 0):
     """DAGs whose BNOTs (not next to their reader) feed AND chains of 2-4 operands (the
     translator's BAND4N fold), some BNOT results read again later by a BOR or an ITE (no
-    fold allowed there), over three 8-bit variables."""
+    fold allowed there), over three 8-bit variables.  With `late_vars` > 0 the states get
+    that many more variables (indices 3.., past the register bank from index 6 on), and
+    compares that read them are ANDed onto the root after the chains, so HBM variable
+    loads follow a folded chain (the uop reference once lost its candidate row
+    there)."""
     w = 8
     cmps = [S.EQ, S.ULT, S.UGE, S.ULE, S.SLT, S.SGE, S.UGT]
     out = []
@@ -571,8 +575,30 @@ def _band4n_states(rng, n):
             nl.append([S.ULT, 1, len(nl) - 1, 2, -1, 0, 0])
             nl.append([S.BOR, 1, root, len(nl) - 1, -1, 0, 0])
             root = len(nl) - 1
+        for k in range(late_vars):   # compares on HBM variables, read after the chains
+            nl.append([S.VAR, w, -1, -1, -1, 3 + k, 0])
+            nl.append([cmps[int(rng.integers(len(cmps)))], 1, len(nl) - 1, 3 + int(rng.integers(4)), -1, 0, 0])
+            nl.append([S.BAND, 1, root, len(nl) - 1, -1, 0, 0])
+            root = len(nl) - 1
         out.append((nl, cl))
     return out
+
+
+def test_band4n_then_hbm_variables_vs_oracle(mgp_ctx):
+    """Compares on variables 6.. (HBM loads, not the register bank) after folded BAND4N
+    chains, against the C oracle on every candidate (both engines)."""
+    rng = np.random.default_rng(93)
+    states = _band4n_states(rng, 400, late_vars=6)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = np.zeros((len(states), 256, 9, 8), np.uint32)
+    cands[..., 0] = rng.integers(0, 256, size=(len(states), 256, 9))
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    bad = np.nonzero(first != ref)[0]
+    assert bad.size == 0, f"{bad.size} states differ, e.g. {bad[:5]}"
+    assert (ref >= 0).sum() > 20
 
 
 def test_band4n_folds_vs_oracle(mgp_ctx):

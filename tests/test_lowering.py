@@ -594,3 +594,35 @@ def test_band4n_folds_uop_reference_matches_oracle():
             folded += nm.startswith("BAND4N")
             kept += nm == "BNOT"
     assert folded > 50 and kept > 0, (folded, kept)
+
+
+def test_band4n_then_hbm_variable_loads_uop_reference():
+    """a compare that reads an HBM variable (index >= 6) after a folded BAND4N
+    chain.  The uop reference once rebound its candidate row inside the BAND4N branch, so
+    every later VAR load read the chain's four Bools; this case fails on that code."""
+    from oracle import coracle
+
+    from .test_gpu_parity import _band4n_states
+
+    rng = np.random.default_rng(94)
+    states = _band4n_states(rng, 200, late_vars=6)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    n_cand = 12
+    vals = rng.integers(0, 256, size=(len(states), n_cand, 9))
+    cands = np.zeros((len(states), n_cand, 9, 8), np.uint32)
+    cands[..., 0] = vals
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    names = UR._names()
+    hit = 0
+    for s in range(len(states)):
+        rows = [[int(x) for x in vals[s, k]] for k in range(n_cand)]
+        assert UR.first_sat_uops(words, int(po[s]), rows) == ref[s], s
+        u0 = UR.uop_offset(words, int(po[s]))
+        seen = False
+        for k in range(int(words[u0])):
+            nm = names[int(words[u0 + 4 + 4 * k]) & 0xFFFF]
+            seen |= nm.startswith("BAND4N")
+            hit += seen and "_var_" in nm
+    assert hit > 20, hit

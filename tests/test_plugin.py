@@ -252,3 +252,20 @@ def test_windowed_exec_timeout_returns_like_reference(brute, monkeypatch, window
     got = vm.exec(track_gas=True)
     assert [g.tag for g in got] == [g.tag for g in ref_final]
     assert vm.executed == ref.executed
+
+
+def test_coverage_strategy_is_not_looked_through():
+    """CoverageStrategy picks the first state at an uncovered instruction, and
+    coverage changes as states run, so a window would reorder the work list: under it the
+    window is 1 even over BFS; BoundedLoopsStrategy (the state's own trace) is looked through."""
+    class CoverageStrategy:
+        def __init__(self, inner):
+            self.super_strategy = inner
+            self.work_list = inner.work_list
+
+    bfs = BreadthFirstSearchStrategy([])
+    assert P.is_breadth_first(bfs)
+    assert P.is_breadth_first(BoundedLoopsStrategy(bfs))
+    assert not P.is_breadth_first(CoverageStrategy(bfs))
+    assert not P.is_breadth_first(BoundedLoopsStrategy(CoverageStrategy(bfs)))
+    assert not P.is_breadth_first(CoverageStrategy(BoundedLoopsStrategy(bfs)))

@@ -493,6 +493,130 @@ def test_uf_congruence_exhaustive_soundness():
     assert refuted > 10
 
 
+def _congruence_state(rng, w=3):
+    """One random term shape T (two operator levels; an ITE's compare adds one more, within
+    the congruence depth kCongDepth = 4) instantiated over x0 and over x1 (compares, ITEs,
+    adds, a UF application), with x0 = x1 asserted in one of three forms (EQ, ULE both ways, or not at
+    all) and T(x0) vs T(x1) constrained to differ (NE, ULT or UGT)."""
+    nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
+    cl = [int(x) for x in rng.integers(0, 1 << w, size=3)]
+    nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(3)]   # nodes 2, 3, 4
+    n_uf = [0]
+
+    def shape(depth):
+        k = rng.random()
+        if depth == 0 or k < 0.2:
+            return ("v",) if rng.random() < 0.7 else ("c", int(rng.integers(3)))
+        if k < 0.45:
+            return (["add", "xor", "sub"][int(rng.integers(3))], shape(depth - 1), shape(depth - 1))
+        if k < 0.7:
+            return ("ite", int(rng.integers(3)), shape(depth - 1), shape(depth - 1), shape(depth - 1))
+        if k < 0.85 and n_uf[0] < 1:
+            n_uf[0] += 1
+            return ("uf", shape(depth - 1))
+        return ("not", shape(depth - 1))
+
+    slots = [2]
+
+    def build(t, v):
+        if t[0] == "v":
+            return v
+        if t[0] == "c":
+            return 2 + t[1]
+        if t[0] in ("add", "xor", "sub"):
+            a, b = build(t[1], v), build(t[2], v)
+            nl.append([{"add": S.ADD, "xor": S.XOR, "sub": S.SUB}[t[0]], w, a, b, -1, 0, 0])
+        elif t[0] == "ite":   # ITE(ULT(T1, c), T2, T3)
+            a = build(t[2], v)
+            nl.append([S.ULT, 1, a, 2 + t[1], -1, 0, 0])
+            c = len(nl) - 1
+            b, d = build(t[3], v), build(t[4], v)
+            nl.append([S.ITE, w, c, b, d, 0, 0])
+        elif t[0] == "uf":
+            a = build(t[1], v)
+            nl.append([S.UFAPP, w, a, -1, -1, 5, slots[0]])
+            slots[0] += 1
+        else:
+            a = build(t[1], v)
+            nl.append([S.NOT, w, a, -1, -1, 0, 0])
+        return len(nl) - 1
+
+    t = shape(2)
+    t0, t1 = build(t, 0), build(t, 1)
+    conj = []
+    form = int(rng.integers(3))
+    if form == 0:
+        nl.append([S.EQ, 1, 0, 1, -1, 0, 0])
+        conj.append(len(nl) - 1)
+    elif form == 1:
+        nl.append([S.ULE, 1, 0, 1, -1, 0, 0])
+        conj.append(len(nl) - 1)
+        nl.append([S.ULE, 1, 1, 0, -1, 0, 0])
+        conj.append(len(nl) - 1)
+    rel = int(rng.integers(3))
+    nl.append([[S.EQ, S.ULT, S.UGT][rel], 1, t0, t1, -1, 0, 0])
+    if rel == 0:
+        nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+    conj.append(len(nl) - 1)
+    if rng.random() < 0.5:   # an unrelated side constraint
+        nl.append([S.ULT, 1, 0, 2 + int(rng.integers(3)), -1, 0, 0])
+        conj.append(len(nl) - 1)
+    root = conj[0]
+    for c in conj[1:]:
+        nl.append([S.BAND, 1, root, c, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl, form
+
+
+def test_structural_congruence_refutes_calldata_equal_indices():
+    """tests/laser/state/calldata_test.py:79-91 at the DAG level: two symbolic calldata loads
+    If(i < size, Select(cd, i), 0) at indices asserted equal cannot differ.  Refuted through
+    structural congruence (mgp_domain.h Dom::cong): the two ITEs apply one operator to
+    operands known equal (the SLT compares over equal indices, the UF applications of one
+    function at equal arguments, the same constant)."""
+    w = 256
+    nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0], [S.EQ, 1, 0, 1, -1, 0, 0],
+          [S.VAR, w, -1, -1, -1, 2, 0], [S.SLT, 1, 0, 3, -1, 0, 0], [S.UFAPP, 8, 0, -1, -1, 0, 3],
+          [S.CONST, 8, -1, -1, -1, 0, 0], [S.ITE, 8, 4, 5, 6, 0, 0], [S.SLT, 1, 1, 3, -1, 0, 0],
+          [S.UFAPP, 8, 1, -1, -1, 0, 4], [S.ITE, 8, 8, 9, 6, 0, 0], [S.EQ, 1, 7, 10, -1, 0, 0],
+          [S.BNOT, 1, 11, -1, -1, 0, 0], [S.BAND, 1, 2, 12, -1, 0, 0]]
+    # the same without i == j: satisfiable, kept
+    free = [r[:] for r in nl]
+    free[2] = [S.ULT, 1, 0, 1, -1, 0, 0]
+    # different functions (two calldata arrays): no congruence
+    other = [r[:] for r in nl]
+    other[9] = [S.UFAPP, 8, 1, -1, -1, 1, 4]
+    assert list(_refute([(nl, [0]), (free, [0]), (other, [0])])) == [1, 0, 0]
+
+
+def test_structural_congruence_exhaustive_soundness():
+    """Random shapes T instantiated over x0 and x1 (3-bit), T(x0) and T(x1) constrained to
+    differ, x0 = x1 asserted as EQ, as ULE both ways, or not at all: no refuted state has a
+    model among every assignment of the variables and the UF's fresh values (C oracle over
+    all 8^4 combinations), and the asserted-equal states are mostly refuted."""
+    rng = np.random.default_rng(0xC0C1)
+    states, forms = [], []
+    for _ in range(300):
+        nl, cl, form = _congruence_state(rng)
+        states.append((nl, cl))
+        forms.append(form)
+    verdict = _refute(states)
+    n_vars = 4
+    grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
+    cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    refuted = {0: 0, 1: 0, 2: 0}
+    for (nl, cl), r, form in zip(states, verdict, forms):
+        assert r in (0, 1)
+        if r != 1:
+            continue
+        refuted[form] += 1
+        nodes, noff, consts, coff = pack_states([(nl, cl)])
+        assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
+    n_form = {f: forms.count(f) for f in (0, 1)}
+    assert refuted[0] > 0.8 * n_form[0] and refuted[1] > 0.8 * n_form[1], (refuted, n_form)
+
+
 def test_mul_by_odd_constant_narrows_backward():
     """x * c == k with c odd pins x = k * c^-1 (mod 2^w) on the known low bits of k: with
     x <u 100 that is refuted when c^-1 * k is huge and kept when it is small."""

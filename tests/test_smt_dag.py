@@ -164,3 +164,35 @@ def test_native_candidates_layout_and_rows():
     assert S.limbs_to_int(p[0, 0, iz]) == 7 and p[0, 0, ix, 0] == 0x41 and p[0, 1, ix, 0] == 0x41
     assert sum(S.eval_root(st.nodes, st.consts, [S.limbs_to_int(a[0, c, v]) for v in range(st.n_vars)])
                for c in range(64)) > 0
+
+
+def test_arena_rows_never_shared_between_live_terms():
+    """arena rows are freed by a weakref callback, after every weakref to the
+    dying term is cleared, so no thread can fetch a dying term from the intern table and
+    keep it alive on a freed row.  Terms are built and dropped by four threads at once;
+    afterwards every live interned term owns a distinct row that is not on the free list."""
+    import gc
+    import threading
+
+    from mythril_amd import smt as M
+
+    def churn(seed):
+        x = BV(f"churn_{seed % 2}", 256)
+        for i in range(3000):
+            t = (x + BVV(i % 97, 256)) * BVV(seed + 1, 256)
+            u = ULT(t, BVV(i % 13, 256))
+            del t, u
+
+    th = [threading.Thread(target=churn, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    keep = [BV("kept", 256) + BVV(k, 256) for k in range(50)]
+    gc.collect()
+    live = list(M._INTERN.values())
+    tids = [t.tid for t in live]
+    assert len(set(tids)) == len(tids)
+    assert not set(tids) & set(M.ARENA.free)
+    assert all(M._ROW_REFS[t.tid]() is t for t in live)
+    assert len(keep) == 50

@@ -370,8 +370,11 @@ extern "C" int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets, u
 extern "C" int mgp_refute_domains(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
                                   const uint32_t *consts, const uint64_t *const_offsets, const uint64_t *var_off,
                                   uint32_t max_passes, int8_t *out, uint32_t *out_dom) {
-  if (!node_offsets || !out || !var_off || !out_dom || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
-  memset(out_dom, 0, (size_t)var_off[n_states] * 33u * 4u);
+  // out_dom may be null when the batch has no variable at all (e.g. a state that is one
+  // literal False, tests/laser/state/calldata_test.py:41-55 after folding)
+  if (!node_offsets || !out || !var_off || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
+  if (!out_dom && var_off[n_states] > 0) return MGP_E_ARG;
+  if (out_dom) memset(out_dom, 0, (size_t)var_off[n_states] * 33u * 4u);
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t st = 0; st < (int64_t)n_states; ++st) {
     const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];

@@ -188,13 +188,23 @@ def backend(mgp_ctx):
 @pytest.mark.parametrize("name", sorted(UNSAT))
 @pytest.mark.parametrize("solver", ["Solver", "IndependenceSolver"])
 def test_unsat_pins_refuted_no_fallback(backend, name, solver):
-    """unsat through Solver and IndependenceSolver: refuted, no GPU witness, no fallback."""
+    """unsat through Solver and IndependenceSolver: refuted, no fallback; no GPU witness
+    for the whole query (Solver) or for the contradictory bucket (IndependenceSolver
+    batches every bucket, and a satisfiable bucket like {a == b} gets its own witness)."""
+    cs = UNSAT[name]()
     s = getattr(SV, solver)()
-    s.add(*UNSAT[name]())
+    s.add(*cs)
     assert s.check() == SV.unsat
     st = SV.SolverStatistics()
     assert backend.calls == 0 and st.query_count == 0
-    assert st.gpu_sat == 0 and st.refuted >= 1
+    assert st.refuted >= 1
+    if solver == "Solver":
+        assert st.gpu_sat == 0
+    else:
+        dm = SV.DependenceMap()
+        for c in cs:
+            dm.add_condition(c.raw)
+        assert st.gpu_sat + st.refuted == len(dm.buckets)
 
 
 @pytest.mark.gpu
@@ -235,3 +245,17 @@ def test_prefilter_batch_of_pins(backend):
     assert backend.calls == 0
     assert _oracle_confirms(_independence_sat(), [res[-1][1]])
     assert np.all([r[1] is None for r in res[:-1]])
+
+
+def test_state_without_variables_through_refute_domains():
+    """A batch whose only state folds to a literal False has no variable slot: the domain
+    export (the pipeline's refute step) must accept an empty domain table (the GPU suite
+    once failed here with 'mgp_refute failed')."""
+    from mythril_amd.front import Batch
+
+    B = Batch([[_concrete_calldata_constrain_index()[0].raw]])
+    assert B.n_vars() == 0
+    p = B.packed()
+    ref, dom = N.refute_domains(*p[:4], B.var_off)
+    assert list(ref) == [1] and dom.shape == (0, 33)
+    B.close()

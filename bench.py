@@ -96,6 +96,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--refute-sample", type=int, default=1 << 17,
                     help="states of the rank-0 batch run through the host UNSAT pre-check (0 = skip)")
+    ap.add_argument("--suite", type=int, default=1, help="the 13-contract solidity_examples suite (0 = skip)")
     ap.add_argument("--frontend", type=int, default=1024,
                     help="contract-shaped states through the full Prefilter front end (0 = skip)")
     ap.add_argument("--guided-sample", type=int, default=1 << 16,
@@ -486,6 +487,39 @@ def main():
         pf.ctx.close()
         log(f"frontend: {frontend}")
 
+    # ------------------------------------ the 13 solidity_examples contracts (configs 1, 2, 4 + 10 more)
+    # Every query a `myth analyze <contract> -t N` run asks, restated by corpus.laser /
+    # corpus.contracts and tagged prune / SAT-only get_model / get_transaction_sequence, through
+    # the product Prefilter cold, one batch per contract.  z3 calls are counted the honest way
+    # (corpus.account): a tx-sequence query is a z3 Optimize call unless refuted.
+    suite = None
+    if rank == 0 and args.suite:
+        from mythril_amd import solver as SV
+
+        import corpus
+
+        tg = time.perf_counter()
+        qs = corpus.suite()
+        gen_s = time.perf_counter() - tg
+        pf = SV.Prefilter(device=local)
+        pf.check_states([list(q[3]) for q in qs[:64]])        # warm-up (kernels loaded, pools touched)
+        SV.unsat_cores().reset()
+        pf._N.program_cache_clear()
+        SV.SolverStatistics().reset()
+        t_all = time.perf_counter()
+        answers, _ = corpus.answer(pf, qs)   # level by level along parent links, parent witnesses passed
+        dt_all = time.perf_counter() - t_all
+        acc = corpus.account(qs, answers)
+        if acc["all"]["contradicted"]:
+            raise RuntimeError(f"suite answers contradict the expectations: {acc['all']}")
+        suite = dict(acc, queries=len(qs), seconds=dt_all, queries_per_s=len(qs) / dt_all, generate_s=gen_s,
+                     held_out_contracts=sorted(corpus.held_out()),
+                     note="queries restated by reading the reference (corpus/laser.py, corpus/contracts.py); "
+                          "ref_calls = the reference's z3 calls (get_model lru-deduplicated), z3_calls = "
+                          "undecided prune/model queries + every tx-sequence query not refuted")
+        pf.ctx.close()
+        log(f"suite: {json.dumps(suite['all'])} held_out {json.dumps(suite['held_out'])}")
+
     # ---------------------------------------------------------- CPU baseline
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -535,6 +569,7 @@ def main():
             "keccak": keccak,
             "prefilter": prefilter,
             "frontend": frontend,
+            "suite": suite,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

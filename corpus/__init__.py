@@ -227,3 +227,126 @@ def corpus(n: int) -> List[Tuple[str, tuple, Optional[str]]]:
             out.extend(bectoken_states(6 * k + j, kfm) for j in range(6))
         k += 1
     return out[:n]
+
+
+# ------------------------------------------------------------- the 13-contract suite
+def suite(hasher=None, max_open: int = 6, contracts=None):
+    """Every contract of solidity_examples/ through the LASER restatement (corpus.laser,
+    corpus.contracts): -> list of (contract, kind, label, terms, expected) queries in the
+    order a `myth analyze <contract> -t N` run asks them (kind: prune / model / txseq).
+    The last field is the index of the query's parent (the prune query that established the
+    asking state; -1 for none): the plugin hands a child its parent's witness.
+
+    `hasher(bytes) -> bytes` is the concrete Keccak-256 the keccak manager uses for concrete
+    preimages (default: the product's GPU batch, mythril_amd.keccak; CPU tests pass a CPU
+    one).  Each contract gets a fresh manager, as each `myth analyze` run does."""
+    from . import contracts as C
+    from .laser import analyze
+
+    out = []
+    for cls in C.ALL:
+        if contracts is not None and cls.name not in contracts:
+            continue
+        kfm = KeccakFunctionManager()
+        if hasher is not None:
+            def fck(data, _h=hasher):
+                d = _h(data.value.to_bytes(data.size() // 8, byteorder="big"))
+                return symbol_factory.BitVecVal(int.from_bytes(d, "big"), 256)
+            kfm.find_concrete_keccak = fck
+        run = analyze(cls(), kfm, max_open=max_open)
+        base = len(out)
+        out.extend((cls.name, kind, label, terms, exp, -1 if par < 0 else base + par)
+                   for kind, label, terms, exp, par in run.queries)
+    return out
+
+
+def held_out() -> set:
+    from .contracts import HELD_OUT
+    return set(HELD_OUT)
+
+
+def account(queries, answers, held=None) -> dict:
+    """Solver calls of the reference and of the pre-filter path for `suite()` queries.
+
+    answers[k] is the pre-filter's 'sat' (GPU witness) / 'unsat' (host refutation) /
+    'undecided' for queries[k].  The reference makes one z3 call per query, except that
+    get_model is lru_cached (analysis/solver.py:27): a repeated SAT-only or tx-sequence
+    query with identical constraints is one call.  The pre-filter path makes:
+      prune / model: one fallback call when undecided;
+      txseq: one z3 Optimize call unless refuted -- a GPU witness does not save it, the
+      minimised model values go into the report (analysis/solver.py:88-136).
+    A contradiction is a GPU witness on an expected-unsat query or a refutation of an
+    expected-sat one (expectations by reading, corpus.laser)."""
+    held = held_out() if held is None else held
+    import collections
+
+    per = collections.OrderedDict()
+    seen = set()
+    for (contract, kind, label, terms, exp, _parent), ans in zip(queries, answers):
+        c = per.setdefault(contract, {"queries": 0, "ref_calls": 0, "z3_calls": 0, "sat": 0, "unsat": 0,
+                                      "undecided": 0, "contradicted": 0, "expected_sat": 0, "expected_sat_witness": 0,
+                                      "expected_unsat": 0, "expected_unsat_refuted": 0,
+                                      "by_kind": {k: {"queries": 0, "ref_calls": 0, "z3_calls": 0}
+                                                  for k in ("prune", "model", "txseq")}})
+        c["queries"] += 1
+        c[ans] += 1
+        bk = c["by_kind"][kind]
+        bk["queries"] += 1
+        if kind != "prune":
+            key = (contract, kind, terms)
+            if key in seen:
+                continue
+            seen.add(key)
+        c["ref_calls"] += 1
+        bk["ref_calls"] += 1
+        z3 = (ans != "unsat") if kind == "txseq" else (ans == "undecided")
+        c["z3_calls"] += z3
+        bk["z3_calls"] += z3
+        if exp == "unsat":
+            c["expected_unsat"] += 1
+            c["expected_unsat_refuted"] += ans == "unsat"
+            c["contradicted"] += ans == "sat"
+        elif exp == "sat":
+            c["expected_sat"] += 1
+            c["expected_sat_witness"] += ans == "sat"
+            c["contradicted"] += ans == "unsat"
+    for c in per.values():
+        c["reduction"] = c["ref_calls"] / max(1, c["z3_calls"])
+        c["held_out"] = False
+    for name in per:
+        per[name]["held_out"] = name in held
+
+    def total(names):
+        r = sum(per[n]["ref_calls"] for n in names)
+        z = sum(per[n]["z3_calls"] for n in names)
+        return {"contracts": len(names), "queries": sum(per[n]["queries"] for n in names), "ref_calls": r,
+                "z3_calls": z, "reduction": r / max(1, z),
+                "contradicted": sum(per[n]["contradicted"] for n in names)}
+    names = list(per)
+    return {"by_contract": dict(per), "all": total(names),
+            "tuned": total([n for n in names if n not in held]),
+            "held_out": total([n for n in names if n in held])}
+
+
+def answer(pf, queries):
+    """Answer `suite()` queries with a Prefilter the way the plugin feeds it: level by level
+    along the parent links (a query is asked once the state it extends is answered), each
+    query given its parent's witness when the parent was SAT (mythril_amd.plugin: a child
+    inherits its parent's witness as its first candidate).  -> (answers, witnesses)."""
+    n = len(queries)
+    depth = [0] * n
+    for i, q in enumerate(queries):
+        depth[i] = depth[q[5]] + 1 if q[5] >= 0 else 0
+    answers = [None] * n
+    wits = [None] * n
+    levels = {}
+    for i, d in enumerate(depth):
+        levels.setdefault(d, []).append(i)
+    for d in sorted(levels):
+        idx = levels[d]
+        par = [wits[queries[i][5]] if queries[i][5] >= 0 else None for i in idx]
+        res = pf.check_states([list(queries[i][3]) for i in idx], parents=par)
+        for i, (a, w) in zip(idx, res):
+            answers[i] = a
+            wits[i] = w if a == "sat" else None
+    return answers, wits

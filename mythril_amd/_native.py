@@ -97,6 +97,10 @@ def _bind(lib):
         "mgp_make_candidates": (ctypes.c_int, [_U32, _U32, _U32, _U64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _U32,
                                                _P, _P, _P, _P]),
         "mgp_decision_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _P]),
+        "mgp_decision_rows_seeded": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P,
+                                                    _U32, _P, _P, _P]),
+        "mgp_decision_rows_seeded_dev": (ctypes.c_int, [_P, _P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P,
+                                                        _P, _P, _U32, _P, _P, _P]),
         "mgp_decision_rows_dev": (ctypes.c_int, [_P, _P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P,
                                                  _P]),
         "mgp_refute_domains": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
@@ -164,6 +168,8 @@ EXPORTED_SYMBOLS = (
     "mgp_make_candidates",
     "mgp_decision_rows",
     "mgp_decision_rows_dev",
+    "mgp_decision_rows_seeded",
+    "mgp_decision_rows_seeded_dev",
     "mgp_refute_domains",
     "mgp_build_states",
     "mgp_fe_get",
@@ -295,9 +301,11 @@ def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hin
 
 def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed: int, n_decide: int,
                   rows_per_state: Optional[np.ndarray] = None, state_keys: Optional[np.ndarray] = None,
-                  max_passes: int = 0, ctx: Optional["Context"] = None):
+                  max_passes: int = 0, ctx: Optional["Context"] = None, seeds=None, seed_rows: int = 0):
     """mgp_decision_rows -> (rows u32 [n, n_decide, n_vars, 8], mask u8 [n, n_decide, n_vars], status i8[n]);
-    with `ctx`, mgp_decision_rows_dev: the same rows computed on ctx's GPU."""
+    with `ctx`, mgp_decision_rows_dev: the same rows computed on ctx's GPU.  seeds = (vals u32
+    [n, n_vars, 8], mask u8 [n, n_vars]): parent values the rows in `seed_rows` (a bit mask)
+    fix first (mgp_decision_rows_seeded)."""
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
     node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
     consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
@@ -319,6 +327,20 @@ def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed:
     args = (_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets), max_passes, n_vars,
             seed & (2 ** 64 - 1), _ptr(keys), n_decide, _ptr(rps), _ptr(rows) if rows.size else None,
             _ptr(mask) if mask.size else None, _ptr(out))
+    if seeds is not None:
+        sv = np.ascontiguousarray(seeds[0], dtype=np.uint32)
+        sm = np.ascontiguousarray(seeds[1], dtype=np.uint8)
+        if sv.shape != (n_states, n_vars, 8) or sm.shape != (n_states, n_vars):
+            raise ValueError("seeds must be (vals u32 [n_states, n_vars, 8], mask u8 [n_states, n_vars])")
+        sargs = args[:11] + (_ptr(sv), _ptr(sm), seed_rows) + args[11:]
+        if ctx is not None:
+            rc = lib().mgp_decision_rows_seeded_dev(ctx._h, *sargs)
+            if rc != 0:
+                msg = lib().mgp_last_error(ctx._h)
+                raise MgpError(rc, msg.decode() if msg else "")
+        else:
+            _check(lib().mgp_decision_rows_seeded(*sargs))
+        return rows, mask, out[:n_states]
     if ctx is not None:
         rc = lib().mgp_decision_rows_dev(ctx._h, *args)
         if rc != 0:

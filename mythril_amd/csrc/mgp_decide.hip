@@ -53,6 +53,8 @@ __global__ __launch_bounds__(64) void mgp_decide_kernel(const uint8_t *__restric
                                                         const mgp_dec_state *__restrict__ states,
                                                         const mgp_dec_task *__restrict__ tasks, uint32_t n_tasks,
                                                         uint8_t *__restrict__ ws, uint64_t seed, uint32_t or_rows,
+                                                        const uint32_t *__restrict__ seed_vals,
+                                                        const uint8_t *__restrict__ seed_mask, uint32_t seed_rows,
                                                         uint32_t *__restrict__ out_rows,
                                                         uint8_t *__restrict__ out_mask) {
   const uint32_t t = blockIdx.x;
@@ -98,6 +100,13 @@ __global__ __launch_bounds__(64) void mgp_decide_kernel(const uint8_t *__restric
   d.n_ufs = S.n_ufs;
   d.cong = at<int32_t>(blob, S.cong);
   d.n_cong = S.n_cong;
+  d.arel = at<ArithRel>(blob, S.arel);
+  d.n_arel = S.n_arel;
+  d.og = at<OrGroup>(blob, S.og);
+  d.n_og = S.n_og;
+  d.odis = at<OrDis>(blob, S.odis);
+  d.oatom = at<int32_t>(blob, S.oatom);
+  d.otgt = at<int32_t>(blob, S.otgt);
   d.uoff = at<uint32_t>(blob, S.uoff);
   d.ulist = at<uint32_t>(blob, S.ulist);
   d.voff = at<uint32_t>(blob, S.voff);
@@ -114,16 +123,18 @@ __global__ __launch_bounds__(64) void mgp_decide_kernel(const uint8_t *__restric
   pv.eqh_off = at<uint32_t>(blob, S.eqh_off);
   pv.eqh = at<V>(blob, S.eqh);
   RowPut put{out_rows, out_mask, T.out_row};
-  decision_row(pv, d, T.row, 2u * T.row, seed, T.tag, or_rows, put);
+  decision_row(pv, d, T.row, 2u * T.row, seed, T.tag, or_rows, put, seed_vals ? seed_vals + T.seed_row * 8u : nullptr,
+               seed_mask ? seed_mask + T.seed_row : nullptr, seed_rows);
 }
 
 }  // namespace
 
 extern "C" hipError_t mgp_launch_decide(const uint8_t *blob, const mgp_dec_state *states, const mgp_dec_task *tasks,
                                         uint32_t n_tasks, uint8_t *ws, uint64_t seed, uint32_t or_rows,
+                                        const uint32_t *seed_vals, const uint8_t *seed_mask, uint32_t seed_rows,
                                         uint32_t *out_rows, uint8_t *out_mask, hipStream_t st) {
   if (n_tasks == 0) return hipSuccess;
   hipLaunchKernelGGL(mgp_decide_kernel, dim3(n_tasks), dim3(64), 0, st, blob, states, tasks, n_tasks, ws, seed,
-                     or_rows, out_rows, out_mask);
+                     or_rows, seed_vals, seed_mask, seed_rows, out_rows, out_mask);
   return hipGetLastError();
 }

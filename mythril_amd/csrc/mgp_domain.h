@@ -297,6 +297,14 @@ constexpr int kCongDepth = 4;              // structural congruence: operator le
 
 struct Pair { int32_t x, y; uint8_t u, s; };
 struct UfApp { int32_t node, arg; uint32_t fn; uint8_t op; };
+// r = a + b (op ADD; flag = a BVAddNoOverflow(a, b) node or -1) or r = a - b (op SUB)
+struct ArithRel { int32_t r, a, b, flag; uint8_t op; };
+// Disjunctive hull: a BOR tree (root) of disjuncts [d0, d1), each an AND tree of atoms
+// [a0, a1) (an atom: a compare of a node with a constant, or a BOR of two such compares on
+// one node, e.g. ULE's Or(ULT, ==) expansion); targets [t0, t1): the nodes every disjunct
+// bounds.  See Dom::or_hull.
+struct OrGroup { int32_t root; uint32_t d0, d1, t0, t1; };
+struct OrDis { int32_t node; uint32_t a0, a1; };
 struct UndoRec {
   uint8_t kind;  // 0 av, 1 bs, 2 pair, 3 var entry
   uint32_t idx;
@@ -369,6 +377,26 @@ struct Dom {
   // both loads are If(i < size, Select(cd, i), 0) with i, j known equal.
   const int32_t *cong = nullptr;
   uint32_t n_cong = 0;
+  // Wrap orderings (round 4): r = a + b does not wrap iff r >=u a (and then r >=u b); it
+  // wraps iff r <u a.  r = a - b does not underflow iff r <=u a; it underflows iff r >u a.
+  // A known wrap status (a BVAddNoOverflow node's truth, b <= a as a pair ordering, or the
+  // operands' intervals) orders (r, a) and (r, b) for the compares that read those pairs,
+  // and a known ordering of (r, a) decides the BVAddNoOverflow node.  So SafeMath.add's
+  // assert(c >= a) contradicts the integer module's Not(BVAddNoOverflow(a, b))
+  // (BECToken.sol:25-29, integer.py:141-147).
+  const ArithRel *arel = nullptr;
+  uint32_t n_arel = 0;
+  // Disjunctive hull (round 4): when a BOR tree is true, one of its disjuncts holds, so a
+  // node that every disjunct bounds by constants lies in the hull of those bounds.  The
+  // keccak manager's `Or(lo <= f(x) < hi ∧ f(x) % 64 == 0, f(x) == H_1 ∧ x == k_1, ...)`
+  // (keccak_function_manager.py:118-146) then keeps f(x) away from every small storage slot,
+  // so a read of mapping[x] over a Store chain that also wrote slots 0..n sees those keys as
+  // different.  A disjunct whose bounds are empty is false.
+  const OrGroup *og = nullptr;
+  uint32_t n_og = 0;
+  const OrDis *odis = nullptr;
+  const int32_t *oatom = nullptr;
+  const int32_t *otgt = nullptr;
   // decision rows: users of each node, VAR nodes of each variable entry, nodes tie() reads
   const uint32_t *uoff = nullptr, *ulist = nullptr, *voff = nullptr, *vlist = nullptr;
   const uint8_t *tie_rel = nullptr;
@@ -490,8 +518,137 @@ struct Dom {
     }
     return true;
   }
+  // the unsigned orderings of node i vs node j that a compare pair on them allows (OALL
+  // when no compare reads the pair)
+  MGP_RD uint8_t known_order(int32_t i, int32_t j) const {
+    if (i == j) return OEQ;
+    const bool sw = i > j;
+    const int32_t x = sw ? j : i, y = sw ? i : j;
+    const int32_t pi = pair_find(((uint64_t)(uint32_t)x << 32) | (uint32_t)y);
+    if (pi < 0) return OALL;
+    const uint8_t m = pairs[pi].u;
+    return sw ? (uint8_t)((m & OEQ) | ((m & OLT) ? OGT : 0) | ((m & OGT) ? OLT : 0)) : m;
+  }
+  // restrict the unsigned orderings of node i vs node j to m (no-op without a pair)
+  MGP_RD bool order(int32_t i, int32_t j, uint8_t m) {
+    if (i == j) return (m & OEQ) != 0;
+    const bool sw = i > j;
+    const int32_t x = sw ? j : i, y = sw ? i : j;
+    const int32_t pi = pair_find(((uint64_t)(uint32_t)x << 32) | (uint32_t)y);
+    if (pi < 0) return true;
+    if (sw) m = (uint8_t)((m & OEQ) | ((m & OLT) ? OGT : 0) | ((m & OGT) ? OLT : 0));
+    return set_order(pairs[pi], 0, m);
+  }
+  MGP_RD bool arith_rel(const ArithRel &e) {
+    const uint32_t w = nd[e.r].width;
+    if (e.op == MGP_OP_ADD) {
+      int wrap = -1;
+      if (e.flag >= 0) wrap = bs[e.flag] == BT ? 0 : (bs[e.flag] == BF ? 1 : -1);
+      if (wrap < 0) {
+        bool o1 = false, o2 = false;
+        add_w(av[e.a].hi, av[e.b].hi, w, o1);
+        if (!o1) {
+          wrap = 0;
+        } else {
+          add_w(av[e.a].lo, av[e.b].lo, w, o2);
+          if (o2) wrap = 1;
+        }
+      }
+      if (wrap < 0) {  // the ordering of (r, a) or (r, b) decides the wrap
+        const uint8_t ra = known_order(e.r, e.a), rb = known_order(e.r, e.b);
+        if (ra == OLT || rb == OLT) wrap = 1;
+        else if (!(ra & OLT) || !(rb & OLT)) wrap = 0;
+      }
+      if (wrap < 0) return true;
+      if (e.flag >= 0 && !meetb(e.flag, wrap ? BF : BT)) return false;
+      const uint8_t m = wrap ? (uint8_t)OLT : (uint8_t)(OGT | OEQ);
+      return order(e.r, e.a, m) && order(e.r, e.b, m);
+    }
+    int udf = -1;  // r = a - b underflows iff b >u a
+    const uint8_t ab = known_order(e.a, e.b);
+    if (!(ab & OLT)) udf = 0;
+    else if (ab == OLT) udf = 1;
+    if (udf < 0) {
+      if (!LT(av[e.a].lo, av[e.b].hi)) udf = 0;
+      else if (LT(av[e.a].hi, av[e.b].lo)) udf = 1;
+    }
+    if (udf < 0) {
+      const uint8_t ra = known_order(e.r, e.a);
+      if (ra == OGT) udf = 1;
+      else if (!(ra & OGT)) udf = 0;
+    }
+    if (udf < 0) return true;
+    if (!order(e.a, e.b, udf ? (uint8_t)OLT : (uint8_t)(OGT | OEQ))) return false;
+    return order(e.r, e.a, udf ? (uint8_t)OGT : (uint8_t)(OLT | OEQ));
+  }
+
+  // narrow [lo, hi] of node t by compare atom k (a compare of t with an exact node);
+  // false = the atom cannot hold within [lo, hi]
+  MGP_RD bool atom_bound(int32_t k, int32_t t, V &lo, V &hi) const {
+    const mgp_node &x = nd[k];
+    const bool left = x.a == t;
+    const int32_t c = left ? x.b : x.a;
+    if ((!left && x.b != t) || !is_exact(av[c])) return true;
+    const V v = av[c].lo, mw = M(nd[t].width);
+    uint8_t op = x.op;  // normalise to "t op v"
+    if (!left) op = op == MGP_OP_ULT ? MGP_OP_UGT : op == MGP_OP_UGT ? MGP_OP_ULT :
+                     op == MGP_OP_ULE ? MGP_OP_UGE : op == MGP_OP_UGE ? MGP_OP_ULE : op;
+    switch (op) {
+      case MGP_OP_EQ: lo = MAX(lo, v); hi = MIN(hi, v); break;
+      case MGP_OP_ULT: if (Z(v)) return false; hi = MIN(hi, SUBV(v, ONE())); break;
+      case MGP_OP_ULE: hi = MIN(hi, v); break;
+      case MGP_OP_UGT: if (EQV(v, mw)) return false; lo = MAX(lo, ADDV(v, ONE())); break;
+      case MGP_OP_UGE: lo = MAX(lo, v); break;
+      default: break;
+    }
+    return !LT(hi, lo);
+  }
+  MGP_RD bool or_hull(const OrGroup &g) {
+    if (bs[g.root] != BT) return true;
+    for (uint32_t ti = g.t0; ti < g.t1; ++ti) {
+      const int32_t t = otgt[ti];
+      V hlo = M(256), hhi = bv_zero();
+      bool any = false;
+      for (uint32_t di = g.d0; di < g.d1; ++di) {
+        const OrDis &d = odis[di];
+        if (bs[d.node] == BF) continue;
+        V lo = av[t].lo, hi = av[t].hi;
+        bool ok = true;
+        for (uint32_t ai = d.a0; ai < d.a1 && ok; ++ai) {
+          const int32_t k = oatom[ai];
+          if (nd[k].op != MGP_OP_BOR) {
+            ok = atom_bound(k, t, lo, hi);
+            continue;
+          }
+          // BOR of two atoms on t: the hull of both (an atom that cannot hold drops out)
+          V l1 = lo, h1 = hi, l2 = lo, h2 = hi;
+          const bool o1 = atom_bound(nd[k].a, t, l1, h1), o2 = atom_bound(nd[k].b, t, l2, h2);
+          if (o1 && o2) { lo = MIN(l1, l2); hi = MAX(h1, h2); }
+          else if (o1) { lo = l1; hi = h1; }
+          else if (o2) { lo = l2; hi = h2; }
+          else ok = false;
+        }
+        if (!ok) {  // this disjunct cannot hold
+          if (!meetb(d.node, BF)) return false;
+          continue;
+        }
+        hlo = MIN(hlo, lo);
+        hhi = MAX(hhi, hi);
+        any = true;
+      }
+      if (!any) return false;
+      AV a = top(nd[t].width);
+      a.lo = hlo;
+      a.hi = hhi;
+      if (!meet(t, a)) return false;
+    }
+    return true;
+  }
+
   MGP_RD bool tie() {
-    if (n_pairs == 0 && n_ufs == 0) return true;
+    for (uint32_t k = 0; k < n_og; ++k)
+      if (!or_hull(og[k])) return false;
+    if (n_pairs == 0 && n_ufs == 0 && n_arel == 0) return true;
     for (int sweep = 0; sweep < 2; ++sweep)
       for (uint32_t i = 0; i < n; ++i) {
         const int32_t pi = cmp_pair[i];
@@ -519,6 +676,8 @@ struct Dom {
       Pair &p = pairs[cong[k]];
       if (p.u != OEQ && arg_equal(p.x, p.y, kCongDepth) && !set_order(p, 2, OEQ)) return false;
     }
+    for (uint32_t k = 0; k < n_arel; ++k)
+      if (!arith_rel(arel[k])) return false;
     for (uint32_t pj = 0; pj < n_pairs; ++pj) {
       const Pair &p = pairs[pj];
       if (p.u == OEQ) {  // known equal: the operands share one value
@@ -1166,13 +1325,39 @@ constexpr uint32_t kOrRowsDefault = 0xAu;
 // kTries draws).  Writes the value of slot k through put(slot[k], value); stops early
 // (remaining slots unwritten) if the undo log overflows.  Stream key per slot:
 // (seed, tag, c, slot).
+//
+// Seeded rows (round 4): with `sv` / `sm` (a value and a flag per variable slot: the parent
+// state's witness, matched by slot key) and bit `row` of `seed_rows` set, every seeded slot
+// is first fixed to its parent value and propagated (a value the child's constraints reject
+// is rolled back and left to the draws), before the Or case split and the draws.  A child
+// state extends its parent by one constraint (svm.py:251-255), so the parent's values fix
+// most of the row and the draws only decide what the new constraint brought in (a new
+// keccak application, a new calldata word).
 template <typename Put>
 MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag,
-                         uint32_t or_rows, Put &put) {
+                         uint32_t or_rows, Put &put, const uint32_t *sv = nullptr, const uint8_t *sm = nullptr,
+                         uint32_t seed_rows = 0) {
   constexpr uint32_t kTries = 4;
   Stack<UndoRec> &undo_log = *d.undo;
   Stack<uint32_t> &work = *d.touched;
   const uint32_t budget = 4u * d.n + 64u;
+  if (sv && sm && row < 32u && ((seed_rows >> row) & 1u)) {
+    for (uint32_t k = 0; k < P.n_slot; ++k) {
+      if (!sm[P.slot[k]]) continue;
+      V v;
+      for (int l = 0; l < 8; ++l) v.w[l] = sv[P.slot[k] * 8u + l];
+      v = bv_mask(v, P.width[k]);
+      const int32_t nk = P.node[k];
+      const uint32_t mark = undo_log.size();
+      work.clear();
+      if (d.meet(nk, exact(v, P.width[k])) && d.run_from((uint32_t)nk, budget) == 0 && !undo_log.over) {
+        undo_log.clear();
+        continue;
+      }
+      if (undo_log.over) return;
+      d.rollback(mark);
+    }
+  }
   // the draw schedule of decision row `row`: the first eight rows decide in node
   // order (schedules 0, 4, 6, 8, 2, 10, 12, 14: the lo/hi schedule 0 that BECToken's
   // mapping witness needs and three random-draw schedules first, so a state given
@@ -1205,12 +1390,34 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
       }
     }
   }
+  // Fresh values of one function's applications are drawn pairwise distinct (round 4).
+  // keccak is injective on the formula's models (inv(f(x)) == x,
+  // keccak_function_manager.py:118-146), so two applications with different arguments need
+  // different values; the lo / hi schedules used to give every application of a keccak
+  // interval the same bound, and the inverse then read the first application's argument
+  // (WalletLibrary's m_ownerIndex[owner] next to m_ownerIndex[sender]).  Applications with
+  // equal arguments lose nothing: the evaluation gives a later one the earlier one's value.
+  constexpr uint32_t kSeenUf = 64;
+  uint32_t seen_fn[kSeenUf];
+  V seen_v[kSeenUf];
+  uint32_t n_seen = 0;
+  auto taken = [&](uint32_t fn, const V &v) {
+    for (uint32_t j = 0; j < n_seen; ++j)
+      if (seen_fn[j] == fn && EQV(seen_v[j], v)) return true;
+    return false;
+  };
   for (uint32_t kk = 0; kk < P.n_slot; ++kk) {
     const uint32_t k = (drow & 1) ? P.n_slot - 1 - kk : kk;  // odd rows decide in reverse order
     const uint64_t key = fe_mix64(seed ^ fe_mix64(tag ^ ((uint64_t)c << 12) ^ P.slot[k]));
     const int32_t nk = P.node[k];
+    const bool ufapp = d.nd[nk].op == MGP_OP_UFAPP;
+    const uint32_t fn = d.nd[nk].p0;
     if (EQV(d.av[nk].lo, d.av[nk].hi)) {  // already one value: nothing to decide
       put(P.slot[k], d.av[nk].lo);
+      if (ufapp && n_seen < kSeenUf) {
+        seen_fn[n_seen] = fn;
+        seen_v[n_seen++] = d.av[nk].lo;
+      }
       continue;
     }
     V v = bv_zero();
@@ -1227,10 +1434,25 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
                                                 : (uint32_t)(key % 3u) * 3u / 2u + (key % 3u == 2u ? 1u + drow : 0u)),
                              fe_mix64(key + t));
       }
+      if (ufapp && taken(fn, v)) {  // step past the taken values along the domain's alignment
+        const uint32_t al = ctz_ones(d.av[nk].z);
+        const V step = SHL(ONE(), al < P.width[k] ? al : 0u);
+        bool free = false;
+        for (uint32_t r = 0; r < 4u && !free; ++r) {
+          v = bv_mask(ADDV(v, step), P.width[k]);
+          if (!inside_av(d.av[nk], v)) break;
+          free = !taken(fn, v);
+        }
+        if (!free) continue;
+      }
       const uint32_t mark = undo_log.size();
       work.clear();
       if (d.meet(nk, exact(v, P.width[k])) && d.run_from((uint32_t)nk, budget) == 0 && !undo_log.over) {
         undo_log.clear();
+        if (ufapp && n_seen < kSeenUf) {
+          seen_fn[n_seen] = fn;
+          seen_v[n_seen++] = v;
+        }
         break;
       }
       if (undo_log.over) return;

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <iterator>
 #include <memory>
 #include <unordered_map>
 #include <vector>
@@ -64,6 +65,10 @@ struct State {
   std::vector<uint8_t> cmp_t;     // orderings (x vs y) under which the node is true
   std::vector<UfApp> ufs;
   std::vector<int32_t> cong;  // pairs of structurally matching operand nodes (Dom::cong)
+  std::vector<ArithRel> arel;  // ADD / SUB nodes whose wrap status orders a compare pair (Dom::arel)
+  std::vector<OrGroup> og;     // disjunctive hulls (Dom::or_hull)
+  std::vector<OrDis> odis;
+  std::vector<int32_t> oatom, otgt;
   std::unordered_map<uint64_t, int32_t> pair_of;  // (x << 32 | y), x < y -> pairs index
   std::vector<uint64_t> pair_keys;                // the same map, sorted (Dom::pair_find)
   std::vector<int32_t> pair_idx;
@@ -95,6 +100,13 @@ struct State {
     d.n_ufs = (uint32_t)ufs.size();
     d.cong = cong.data();
     d.n_cong = (uint32_t)cong.size();
+    d.arel = arel.data();
+    d.n_arel = (uint32_t)arel.size();
+    d.og = og.data();
+    d.n_og = (uint32_t)og.size();
+    d.odis = odis.data();
+    d.oatom = oatom.data();
+    d.otgt = otgt.data();
     d.uoff = uoff.data();
     d.ulist = ulist.data();
     d.voff = voff.data();
@@ -237,6 +249,33 @@ struct State {
       if (a.op == MGP_OP_VAR || a.op == MGP_OP_CONST || a.op == MGP_OP_TRUE || a.op == MGP_OP_FALSE) continue;
       cong.push_back((int32_t)k);
     }
+    // wrap orderings: ADD / SUB nodes on narrow values where a compare reads (r, a), (r, b)
+    // or (a, b), or a BVAddNoOverflow node reads the same operands
+    arel.clear();
+    {
+      std::unordered_map<uint64_t, int32_t> noovf;  // operand pair -> BVAddNoOverflow node
+      auto okey = [](int32_t x, int32_t y) {
+        return x < y ? ((uint64_t)(uint32_t)x << 32) | (uint32_t)y : ((uint64_t)(uint32_t)y << 32) | (uint32_t)x;
+      };
+      for (uint32_t i = 0; i < n; ++i)
+        if (nd[i].op == MGP_OP_UADD_NOOVF && !isb[nd[i].a]) noovf.emplace(okey(nd[i].a, nd[i].b), (int32_t)i);
+      auto has_pair = [&](int32_t x, int32_t y) { return x != y && pair_of.count(okey(x, y)) != 0; };
+      for (uint32_t i = 0; i < n; ++i) {
+        const mgp_node &x = nd[i];
+        if ((x.op != MGP_OP_ADD && x.op != MGP_OP_SUB) || isb[i] || x.width == 0u || x.width > MGP_MAX_WIDTH) continue;
+        int32_t flag = -1;
+        if (x.op == MGP_OP_ADD) {
+          auto it = noovf.find(okey(x.a, x.b));
+          if (it != noovf.end()) flag = it->second;
+        }
+        const int32_t r = (int32_t)i;
+        if (flag < 0 && !has_pair(r, x.a) && !(x.op == MGP_OP_ADD && has_pair(r, x.b)) &&
+            !(x.op == MGP_OP_SUB && has_pair(x.a, x.b)))
+          continue;
+        arel.push_back(ArithRel{r, x.a, x.b, flag, x.op});
+      }
+    }
+    build_or_groups();
     // the pair lookup as a sorted array (the view's binary search, host and device)
     pair_keys.clear();
     pair_idx.clear();
@@ -245,6 +284,95 @@ struct State {
     for (const auto &e : kv) {
       pair_keys.push_back(e.first);
       pair_idx.push_back(e.second);
+    }
+  }
+
+  // The BOR trees for Dom::or_hull: maximal BOR trees (a BOR that is no operand of another
+  // BOR), at most kMaxDis disjuncts of at most kMaxAtoms conjuncts each; a conjunct is a
+  // compare of a node with a constant, or a BOR of two of those on one node.
+  void build_or_groups() {
+    constexpr size_t kMaxDis = 16, kMaxAtoms = 24;
+    og.clear();
+    odis.clear();
+    oatom.clear();
+    otgt.clear();
+    std::vector<uint8_t> under_or(n, 0);
+    for (uint32_t i = 0; i < n; ++i)
+      if (nd[i].op == MGP_OP_BOR) under_or[nd[i].a] = under_or[nd[i].b] = 1;
+    auto cmp_const = [&](int32_t k, int32_t *target) {
+      const mgp_node &x = nd[k];
+      if (!(x.op == MGP_OP_EQ || (x.op >= MGP_OP_ULT && x.op <= MGP_OP_UGE)) || isb[x.a]) return false;
+      const bool ca = nd[x.a].op == MGP_OP_CONST, cb = nd[x.b].op == MGP_OP_CONST;
+      if (ca == cb) return false;
+      *target = ca ? x.b : x.a;
+      return true;
+    };
+    std::vector<int32_t> st, dis, conj;
+    for (uint32_t r = 0; r < n; ++r) {
+      if (nd[r].op != MGP_OP_BOR || under_or[r]) continue;
+      dis.clear();
+      st.assign(1, (int32_t)r);
+      while (!st.empty() && dis.size() <= kMaxDis) {
+        const int32_t k = st.back();
+        st.pop_back();
+        if (nd[k].op == MGP_OP_BOR) { st.push_back(nd[k].b); st.push_back(nd[k].a); }
+        else dis.push_back(k);
+      }
+      if (dis.size() < 2 || dis.size() > kMaxDis || !st.empty()) continue;
+      const uint32_t d0 = (uint32_t)odis.size();
+      std::vector<std::vector<int32_t>> tg;  // per disjunct: nodes it bounds
+      bool good = true;
+      for (int32_t d : dis) {
+        const uint32_t a0 = (uint32_t)oatom.size();
+        std::vector<int32_t> bound;
+        conj.clear();
+        st.assign(1, d);
+        while (!st.empty() && conj.size() <= kMaxAtoms) {
+          const int32_t k = st.back();
+          st.pop_back();
+          if (nd[k].op == MGP_OP_BAND) { st.push_back(nd[k].b); st.push_back(nd[k].a); }
+          else conj.push_back(k);
+        }
+        if (!st.empty()) { good = false; break; }
+        for (int32_t k : conj) {
+          int32_t t = -1, t2 = -1;
+          if (cmp_const(k, &t)) {
+            oatom.push_back(k);
+            bound.push_back(t);
+          } else if (nd[k].op == MGP_OP_BOR && cmp_const(nd[k].a, &t) && cmp_const(nd[k].b, &t2) && t == t2) {
+            oatom.push_back(k);
+            bound.push_back(t);
+          } else if (nd[k].op == MGP_OP_FALSE) {
+            oatom.push_back(k);  // never bounds anything; the disjunct is false anyway (forward)
+          }
+        }
+        odis.push_back(OrDis{d, a0, (uint32_t)oatom.size()});
+        std::sort(bound.begin(), bound.end());
+        bound.erase(std::unique(bound.begin(), bound.end()), bound.end());
+        tg.push_back(bound);
+      }
+      if (!good) {
+        odis.resize(d0);
+        continue;
+      }
+      // targets: bounded in every disjunct
+      std::vector<int32_t> common = tg[0];
+      for (size_t j = 1; j < tg.size(); ++j) {
+        std::vector<int32_t> keep;
+        std::set_intersection(common.begin(), common.end(), tg[j].begin(), tg[j].end(), std::back_inserter(keep));
+        common.swap(keep);
+      }
+      if (common.empty()) {
+        odis.resize(d0);
+        continue;
+      }
+      const uint32_t t0 = (uint32_t)otgt.size();
+      otgt.insert(otgt.end(), common.begin(), common.end());
+      og.push_back(OrGroup{(int32_t)r, d0, (uint32_t)odis.size(), t0, (uint32_t)otgt.size()});
+    }
+    if (og.empty()) {
+      odis.clear();
+      oatom.clear();
     }
   }
 
@@ -273,6 +401,15 @@ struct State {
       if (cmp_pair[i] >= 0 || nd[i].op == MGP_OP_BOR) tie_rel[i] = 1;
     for (const Pair &p : pairs) tie_rel[p.x] = tie_rel[p.y] = 1;
     for (const UfApp &u : ufs) tie_rel[u.node] = 1;
+    for (const ArithRel &e : arel) {
+      tie_rel[e.r] = tie_rel[e.a] = tie_rel[e.b] = 1;
+      if (e.flag >= 0) tie_rel[e.flag] = 1;
+    }
+    for (const OrGroup &g : og) {
+      tie_rel[g.root] = 1;
+      for (uint32_t k = g.d0; k < g.d1; ++k) tie_rel[odis[k].node] = 1;
+      for (uint32_t k = g.t0; k < g.t1; ++k) tie_rel[otgt[k]] = 1;
+    }
   }
 };
 
@@ -533,7 +670,8 @@ struct RowBuf {
 
 // Host run of mgpd::decision_row on a private copy of P's base analysis.
 template <typename Put>
-void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, Put &put) {
+void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, Put &put,
+                  const uint32_t *sv = nullptr, const uint8_t *sm = nullptr, uint32_t seed_rows = 0) {
   const State &s = P.s;
   std::vector<AV> av(s.av), vars(s.vars);
   std::vector<uint8_t> bs(s.bs);
@@ -561,7 +699,7 @@ void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64
   d.touched = &work;
   d.heur = true;
   const PrepView pv = P.view();
-  mgpd::decision_row(pv, d, row, c, seed, tag, or_rows_mask(), put);
+  mgpd::decision_row(pv, d, row, c, seed, tag, or_rows_mask(), put, sv, sm, seed_rows);
   undo_buf.trim();
   work_buf.trim();
 }
@@ -627,11 +765,29 @@ extern "C" int mgp_guided_candidates_rows(const mgp_node *nodes, const uint64_t 
   return 0;
 }
 
+extern "C" int mgp_decision_rows_seeded(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                        const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                        uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
+                                        const uint8_t *rows_per_state, const uint32_t *seed_vals,
+                                        const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
+                                        uint8_t *out_mask, int8_t *out);
+
 extern "C" int mgp_decision_rows(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
                                  const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
                                  uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
                                  const uint8_t *rows_per_state, uint32_t *out_rows, uint8_t *out_mask,
                                  int8_t *out) {
+  return mgp_decision_rows_seeded(nodes, node_offsets, n_states, consts, const_offsets, max_passes, n_vars, seed,
+                                  state_keys, n_decide, rows_per_state, nullptr, nullptr, 0u, out_rows, out_mask, out);
+}
+
+extern "C" int mgp_decision_rows_seeded(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                        const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                        uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
+                                        const uint8_t *rows_per_state, const uint32_t *seed_vals,
+                                        const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
+                                        uint8_t *out_mask, int8_t *out) {
+  if ((seed_vals == nullptr) != (seed_mask == nullptr)) return MGP_E_ARG;
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets)) ||
       (n_states && n_decide && (!out_rows || !out_mask)))
     return MGP_E_ARG;
@@ -662,7 +818,9 @@ extern "C" int mgp_decision_rows(const mgp_node *nodes, const uint64_t *node_off
         memcpy(out_rows + (r0 + sl) * 8ull, v.w, 32);
         out_mask[r0 + sl] = 1;
       };
-      decision_row(P, row, 2u * row, seed, tag, put);
+      const uint64_t sb = (uint64_t)st * n_vars;
+      decision_row(P, row, 2u * row, seed, tag, put, seed_vals ? seed_vals + sb * 8u : nullptr,
+                   seed_mask ? seed_mask + sb : nullptr, seed_rows);
     }
   }
   return MGP_OK;
@@ -719,7 +877,7 @@ struct DevGrow {
 };
 struct DecBufs {
   std::mutex mu;  // held across one call's upload, launches and synchronize
-  DevGrow blob, states, tasks, ws, rows, mask;
+  DevGrow blob, states, tasks, ws, rows, mask, svals, smask;
 };
 std::mutex g_dec_mu;                              // guards the map only
 std::map<std::pair<int, void *>, DecBufs> g_dec;  // per (device, stream); entries never move
@@ -731,13 +889,33 @@ constexpr uint64_t kWsLaunchBytes = 4ull << 30;
 
 }  // namespace
 
+extern "C" int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
+                                            uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
+                                            uint32_t max_passes, uint32_t n_vars, uint64_t seed,
+                                            const uint64_t *state_keys, uint32_t n_decide,
+                                            const uint8_t *rows_per_state, const uint32_t *seed_vals,
+                                            const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
+                                            uint8_t *out_mask, int8_t *out);
+
 extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
                                      uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
                                      uint32_t max_passes, uint32_t n_vars, uint64_t seed, const uint64_t *state_keys,
                                      uint32_t n_decide, const uint8_t *rows_per_state, uint32_t *out_rows,
                                      uint8_t *out_mask, int8_t *out) {
+  return mgp_decision_rows_seeded_dev(ctx, nodes, node_offsets, n_states, consts, const_offsets, max_passes, n_vars,
+                                      seed, state_keys, n_decide, rows_per_state, nullptr, nullptr, 0u, out_rows,
+                                      out_mask, out);
+}
+
+extern "C" int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
+                                            uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
+                                            uint32_t max_passes, uint32_t n_vars, uint64_t seed,
+                                            const uint64_t *state_keys, uint32_t n_decide,
+                                            const uint8_t *rows_per_state, const uint32_t *seed_vals,
+                                            const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
+                                            uint8_t *out_mask, int8_t *out) {
   if (!ctx || !node_offsets || !out || (n_states && (!nodes || !const_offsets)) ||
-      (n_states && n_decide && (!out_rows || !out_mask)))
+      (n_states && n_decide && (!out_rows || !out_mask)) || ((seed_vals == nullptr) != (seed_mask == nullptr)))
     return MGP_E_ARG;
   void *stp = nullptr;
   int dev = 0;
@@ -793,6 +971,13 @@ extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const 
     h.tie_rel = B.put(S.tie_rel);
     h.cong = B.put(S.cong);
     h.n_cong = (uint32_t)S.cong.size();
+    h.arel = B.put(S.arel);
+    h.n_arel = (uint32_t)S.arel.size();
+    h.og = B.put(S.og);
+    h.n_og = (uint32_t)S.og.size();
+    h.odis = B.put(S.odis);
+    h.oatom = B.put(S.oatom);
+    h.otgt = B.put(S.otgt);
     h.slot = B.put(P.slot);
     h.width = B.put(P.width);
     h.node = B.put(P.node);
@@ -823,7 +1008,7 @@ extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const 
     hdr.push_back(h);
     const uint64_t tag = state_keys ? state_keys[s] : (uint64_t)s << 32;
     for (uint32_t row = 0; row < rs; ++row) {
-      tasks.push_back(mgp_dec_task{si, row, 0, tag, ((uint64_t)s * n_decide + row) * n_vars});
+      tasks.push_back(mgp_dec_task{si, row, 0, tag, ((uint64_t)s * n_decide + row) * n_vars, (uint64_t)s * n_vars});
       task_ws.push_back(h.ws_bytes);
     }
   }
@@ -862,6 +1047,11 @@ extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const 
     e = hipMemcpyAsync(D.states.p, hdr.data(), hdr.size() * sizeof(mgp_dec_state), hipMemcpyHostToDevice, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(D.tasks.p, tasks.data(), tasks.size() * sizeof(mgp_dec_task), hipMemcpyHostToDevice, st);
+  const size_t sv_bytes = seed_vals ? (size_t)n_states * n_vars * 32u : 0u, sm_bytes = seed_vals ? (size_t)n_states * n_vars : 0u;
+  if (e == hipSuccess && sv_bytes) e = D.svals.ensure(sv_bytes);
+  if (e == hipSuccess && sv_bytes) e = D.smask.ensure(sm_bytes);
+  if (e == hipSuccess && sv_bytes) e = hipMemcpyAsync(D.svals.p, seed_vals, sv_bytes, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && sv_bytes) e = hipMemcpyAsync(D.smask.p, seed_mask, sm_bytes, hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipMemsetAsync(D.rows.p, 0, rows_bytes, st);
   if (e == hipSuccess) e = hipMemsetAsync(D.mask.p, 0, mask_bytes, st);
   static const uint32_t or_rows = or_rows_mask();
@@ -869,7 +1059,9 @@ extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const 
     if (e != hipSuccess) break;
     e = mgp_launch_decide((const uint8_t *)D.blob.p, (const mgp_dec_state *)D.states.p,
                           (const mgp_dec_task *)D.tasks.p + L.first, (uint32_t)(L.second - L.first),
-                          (uint8_t *)D.ws.p, seed, or_rows, (uint32_t *)D.rows.p, (uint8_t *)D.mask.p, st);
+                          (uint8_t *)D.ws.p, seed, or_rows, sv_bytes ? (const uint32_t *)D.svals.p : nullptr,
+                          sv_bytes ? (const uint8_t *)D.smask.p : nullptr, seed_rows, (uint32_t *)D.rows.p,
+                          (uint8_t *)D.mask.p, st);
   }
   if (e == hipSuccess) e = hipMemcpyAsync(out_rows, D.rows.p, rows_bytes, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipMemcpyAsync(out_mask, D.mask.p, mask_bytes, hipMemcpyDeviceToHost, st);

@@ -309,3 +309,30 @@ def parent_arrays(p) -> "tuple[np.ndarray, np.ndarray]":
     if not keys:
         return np.zeros(0, np.uint64), np.zeros((0, 8), np.uint32)
     return np.array(keys, np.uint64), np.frombuffer(b"".join(vals), np.uint32).reshape(-1, 8)
+
+
+def seed_arrays(B: "Batch", parents: Sequence) -> "tuple[np.ndarray, np.ndarray]":
+    """Per state of batch B, its parent witness's values on B's variable slots, matched by
+    slot key as mgp_check_batch matches the parent row: (vals u32 [n, n_vars, 8], mask u8
+    [n, n_vars]) for mgp_decision_rows_seeded."""
+    n, nv = B.n_states, max(1, B.n_vars())
+    vals = np.zeros((n, nv, 8), np.uint32)
+    mask = np.zeros((n, nv), np.uint8)
+    for s, p in enumerate(parents):
+        if p is None:
+            continue
+        pk, pv = parent_arrays(p)
+        if pk.size == 0:
+            continue
+        v0, v1 = int(B.var_off[s]), int(B.var_off[s + 1])
+        keys = np.asarray(B.var_key[v0:v1], dtype=np.uint64)
+        order = np.argsort(pk, kind="stable")
+        sk = pk[order]
+        pos = np.searchsorted(sk, keys)
+        pos = np.minimum(pos, len(sk) - 1)
+        hit = (sk[pos] == keys) & (keys != np.uint64(0xFFFFFFFFFFFFFFFF))
+        idx = np.nonzero(hit)[0]
+        vals[s, idx] = pv[order[pos[idx]]]
+        mask[s, idx] = 1
+    return vals, mask
+

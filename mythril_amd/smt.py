@@ -647,18 +647,25 @@ def simplify(e: Expression) -> Expression:
 
 # --------------------------------------------------------------- UF / arrays
 class Function:
-    """Uninterpreted function (function.py:7-25).  `inverse_of` marks a keccak inverse."""
+    """Uninterpreted function (function.py:7-25).  `inverse_of` marks a keccak inverse.
 
-    _next_id = 0
+    Functions are identified by name and signature, as z3 identifies its declarations: two
+    Function("f", 256, 256) objects are one function (one id), and two Array("balance", ...)
+    objects read one array -- LASER's world state copies `balances` into `starting_balances`
+    and every account's storage is an Array named "Storage" (account.py:28), all of which z3
+    sees as the same symbol (mythril_amd.z3_lower interns declarations the same way)."""
+
+    _ids: Dict[Tuple[str, int, int], int] = {}
 
     def __init__(self, name: str, domain: int, value_range: int, inverse_of: Optional["Function"] = None):
         self.name = name
         self.domain = domain
         self.range = value_range
         self.inverse_of = inverse_of
-        self.fid = Function._next_id if inverse_of is None else inverse_of.fid
-        if inverse_of is None:
-            Function._next_id += 1
+        if inverse_of is not None:
+            self.fid = inverse_of.fid
+        else:
+            self.fid = Function._ids.setdefault((name, domain, value_range), len(Function._ids))
 
     def __call__(self, item: BitVec) -> BitVec:
         if item.size() != self.domain:

@@ -414,6 +414,9 @@ class Prefilter:
     # row tasks take 166 ms on 16 host threads and 1 138 ms on the GPU (one sequential
     # propagation per lane, 128-B abstract values spilled to scratch)
     DECIDE_GPU_MIN = 64
+    # decision rows seeded with the parent witness (bit mask of rows; states without a parent
+    # witness decide every row unseeded)
+    SEED_ROWS = 0x3
 
     def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,
                  devices: Optional[Sequence[int]] = None):
@@ -432,6 +435,7 @@ class Prefilter:
         self.decide_rows = self.DECIDE_ROWS
         self.decide_max_units = self.DECIDE_MAX_UNITS
         self.decide_on_gpu = "never"  # "never" (host), "auto" (>= DECIDE_GPU_MIN open states) or "always"
+        self.seed_rows = self.SEED_ROWS
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # refuted constraint lists wait in the core cache and are shrunk to cores together
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
@@ -566,7 +570,8 @@ class Prefilter:
         witnesses: Dict[int, object] = {}
         retry = [i for i in range(len(states)) if first[i] == -1 and proven[i] != 1]
         if retry and self.retry_cand > 0:
-            self._retry_round(ctx, states, retry, first, witnesses, prof)
+            self._retry_round(ctx, states, retry, first, witnesses, prof,
+                              None if parents is None else [parents[i] for i in retry])
         prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["retry_states"] = len(retry)
         tr = time.perf_counter()
@@ -617,11 +622,14 @@ class Prefilter:
                         np.where(units * self.DECIDE_MIN_ROWS <= self.decide_max_units, self.DECIDE_MIN_ROWS, 0))
         return rows.astype(np.uint8)
 
-    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None) -> None:
+    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None, parents=None) -> None:
         """The second witness round for the open states: host decision rows
         (mgp_decision_rows, each variable fixed in turn and the analysis re-propagated)
-        placed in the first mixture rows of a device-generated round with a new seed."""
-        from .front import FE_SAT_UNSAFE, Batch
+        placed in the first mixture rows of a device-generated round with a new seed.  A
+        state with a parent witness gets SEED_ROWS of its rows seeded with the parent's
+        values (mgp_decision_rows_seeded): the draws then only decide what the child's new
+        constraint brought in."""
+        from .front import FE_SAT_UNSAFE, Batch, seed_arrays
 
         prof = {} if prof is None else prof
         n2 = max(64, self.retry_cand // 64 * 64)
@@ -644,8 +652,13 @@ class Prefilter:
             td = time.perf_counter()
             on_gpu = self.decide_on_gpu == "always" or (self.decide_on_gpu == "auto" and
                                                         len(grp) >= self.DECIDE_GPU_MIN)
+            par = None if parents is None else [parents[j] for j in grp]
+            seeds = seed_arrays(GB, par) if par is not None and any(p is not None for p in par) else None
+            if seeds is not None and seeds[0].shape[1] != gv:
+                seeds = None
             rows, mask, _ = self._N.decision_rows(*GB.packed(decide=True), gv, seed2, self.decide_rows, rps,
-                                                  state_keys=GB.state_key, ctx=ctx if on_gpu else None)
+                                                  state_keys=GB.state_key, ctx=ctx if on_gpu else None,
+                                                  seeds=seeds, seed_rows=self.seed_rows)
             dec_ms += 1e3 * (time.perf_counter() - td)
             prof["decide_on_gpu"] = bool(on_gpu)
             f2, w2, _, st2 = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))

@@ -617,6 +617,128 @@ def test_structural_congruence_exhaustive_soundness():
     assert refuted[0] > 0.8 * n_form[0] and refuted[1] > 0.8 * n_form[1], (refuted, n_form)
 
 
+def _wrap_or_state(rng, w=3):
+    """Random DAGs over three w-bit variables mixing ADD / SUB results compared with their
+    operands (the wrap-ordering rule), BVAddNoOverflow / BVSubNoUnderflow flags on the same
+    operands, and BOR trees of AND-ed compares with constants (the disjunctive hull), plus
+    EQ / ITE reads of the bounded nodes."""
+    nl = [[S.VAR, w, -1, -1, -1, k, 0] for k in range(3)]
+    n_c = 4
+    cl = [int(x) for x in rng.integers(0, 1 << w, size=n_c)]
+    nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(n_c)]   # nodes 3..6
+    vals = [0, 1, 2]
+    bools = []
+    cmps = [S.ULT, S.ULE, S.UGT, S.UGE, S.EQ]
+
+    def const():
+        return 3 + int(rng.integers(n_c))
+
+    for _ in range(int(rng.integers(6, 12))):
+        k = rng.random()
+        if k < 0.3:
+            a, b = int(rng.choice(vals)), int(rng.choice(vals))
+            op = S.ADD if rng.random() < 0.5 else S.SUB
+            nl.append([op, w, a, b, -1, 0, 0])
+            r = len(nl) - 1
+            vals.append(r)
+            # compare the result with an operand, and maybe the flag
+            nl.append([cmps[int(rng.integers(4))], 1, r, a if rng.random() < 0.7 else b, -1, 0, 0])
+            bools.append(len(nl) - 1)
+            if rng.random() < 0.6:
+                nl.append([S.UADD_NOOVF if op == S.ADD else S.USUB_NOUDF, 1, a, b, -1, 0, 0])
+                if rng.random() < 0.5:
+                    nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+                bools.append(len(nl) - 1)
+        elif k < 0.55:
+            # Or of 2-3 disjuncts, each an AND of 1-2 compares of one target with constants
+            t = int(rng.choice(vals))
+            dis = []
+            for _ in range(int(rng.integers(2, 4))):
+                nl.append([cmps[int(rng.integers(5))], 1, t, const(), -1, 0, 0])
+                c = len(nl) - 1
+                if rng.random() < 0.5:
+                    nl.append([cmps[int(rng.integers(5))], 1, const(), t, -1, 0, 0])
+                    nl.append([S.BAND, 1, c, len(nl) - 1, -1, 0, 0])
+                    c = len(nl) - 1
+                if rng.random() < 0.3:      # ULE's Or(ULT, ==) shape as a conjunct
+                    cc = const()
+                    nl.append([S.ULT, 1, t, cc, -1, 0, 0])
+                    nl.append([S.EQ, 1, t, cc, -1, 0, 0])
+                    nl.append([S.BOR, 1, len(nl) - 2, len(nl) - 1, -1, 0, 0])
+                    nl.append([S.BAND, 1, c, len(nl) - 1, -1, 0, 0])
+                    c = len(nl) - 1
+                dis.append(c)
+            root = dis[0]
+            for d in dis[1:]:
+                nl.append([S.BOR, 1, root, d, -1, 0, 0])
+                root = len(nl) - 1
+            bools.append(root)
+        elif k < 0.75:
+            nl.append([cmps[int(rng.integers(5))], 1, int(rng.choice(vals)), const() if rng.random() < 0.6
+                       else int(rng.choice(vals)), -1, 0, 0])
+            bools.append(len(nl) - 1)
+        elif bools:
+            nl.append([S.ITE, w, int(rng.choice(bools)), int(rng.choice(vals)), const(), 0, 0])
+            vals.append(len(nl) - 1)
+    while len(bools) < 2:
+        nl.append([S.EQ, 1, int(rng.choice(vals)), const(), -1, 0, 0])
+        bools.append(len(nl) - 1)
+    root = bools[-1]
+    for b in bools[-5:-1]:
+        nl.append([S.BAND, 1, root, b, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl
+
+
+def test_wrap_orderings_and_disjunctive_hull_exhaustive_soundness():
+    """The wrap-ordering rule (mgp_domain.h Dom::arith_rel) and the disjunctive hull
+    (Dom::or_hull): random 3-bit DAGs of their shapes, every refuted state checked over all
+    8^3 assignments with the C oracle; both rules must fire (refutations exist)."""
+    rng = np.random.default_rng(0xA11CE)
+    states = [_wrap_or_state(rng) for _ in range(1500)]
+    verdict = _refute(states)
+    grid = np.array(np.meshgrid(*[np.arange(8)] * 3, indexing="ij")).reshape(3, -1).T
+    cands = np.zeros((1, grid.shape[0], 3, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    refuted = 0
+    for st, r in zip(states, verdict):
+        assert r in (0, 1)
+        if r != 1:
+            continue
+        refuted += 1
+        nodes, noff, consts, coff = pack_states([st])
+        assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
+    assert refuted > 100, refuted
+
+
+def test_wrap_ordering_refutes_safemath_add_overflow():
+    """BECToken.sol:25-29 + integer.py:141-147: c = a + b, assert(c >= a) passed, and
+    Not(BVAddNoOverflow(a, b)) asserted: contradictory (a wrap makes c < a)."""
+    nl = [X0, X1, [S.ADD, 256, 0, 1, -1, 0, 0], [S.UGE, 1, 2, 0, -1, 0, 0],
+          [S.UADD_NOOVF, 1, 0, 1, -1, 0, 0], [S.BNOT, 1, 4, -1, -1, 0, 0], [S.BAND, 1, 3, 5, -1, 0, 0]]
+    ok = [r[:] for r in nl]
+    ok[5] = [S.UADD_NOOVF, 1, 0, 1, -1, 0, 0]      # no overflow: satisfiable
+    sub = [X0, X1, [S.SUB, 256, 0, 1, -1, 0, 0], [S.UGT, 1, 2, 0, -1, 0, 0],   # a - b > a ...
+           [S.UGE, 1, 0, 1, -1, 0, 0], [S.BAND, 1, 3, 4, -1, 0, 0]]          # ... with b <= a
+    assert list(_refute([(nl, []), (ok, []), (sub, [])])) == [1, 0, 1]
+
+
+def test_disjunctive_hull_separates_keccak_keys_from_small_slots():
+    """keccak_function_manager.py:118-146: f(x) in [lo, hi) or f(x) == H; then f(x) == 8 (a
+    small storage slot) is refuted, and a Store chain's value at f(x) skips slot 8."""
+    lo, hi, H = 1 << 250, (1 << 250) + (1 << 123), (1 << 255) + 12345
+    nl = [X0, [S.UFAPP, 256, 0, -1, -1, 0, 1],                              # 1: f(x)
+          [S.CONST, 256, -1, -1, -1, 0, 0], [S.CONST, 256, -1, -1, -1, 1, 0],
+          [S.CONST, 256, -1, -1, -1, 2, 0], [S.CONST, 256, -1, -1, -1, 3, 0],
+          [S.ULT, 1, 2, 1, -1, 0, 0], [S.EQ, 1, 2, 1, -1, 0, 0], [S.BOR, 1, 6, 7, -1, 0, 0],   # 8: lo <= f
+          [S.ULT, 1, 1, 3, -1, 0, 0], [S.BAND, 1, 8, 9, -1, 0, 0],               # 10: lo <= f < hi
+          [S.EQ, 1, 1, 4, -1, 0, 0], [S.BOR, 1, 10, 11, -1, 0, 0],               # 12: ... or f == H
+          [S.EQ, 1, 1, 5, -1, 0, 0], [S.BAND, 1, 12, 13, -1, 0, 0]]              # f == 8
+    free = [r[:] for r in nl]
+    free[13] = [S.UGT, 1, 1, 5, -1, 0, 0]                                      # f > 8: fine
+    assert list(_refute([(nl, [lo, hi, H, 8]), (free, [lo, hi, H, 8])])) == [1, 0]
+
+
 def test_mul_by_odd_constant_narrows_backward():
     """x * c == k with c odd pins x = k * c^-1 (mod 2^w) on the known low bits of k: with
     x <u 100 that is refuted when c^-1 * k is huge and kept when it is small."""

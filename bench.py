@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--refute-sample", type=int, default=1 << 17,
                     help="states of the rank-0 batch run through the host UNSAT pre-check (0 = skip)")
     ap.add_argument("--suite", type=int, default=1, help="the 13-contract solidity_examples suite (0 = skip)")
+    ap.add_argument("--div-split", type=int, default=1, help="time the division-free twin batch (0 = skip)")
     ap.add_argument("--frontend", type=int, default=1024,
                     help="contract-shaped states through the full Prefilter front end (0 = skip)")
     ap.add_argument("--guided-sample", type=int, default=1 << 16,
@@ -200,6 +201,23 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # the rest of the §8e exchange step, outside the timed steps (which gather first-SAT
+    # words only): the SAT states' witness words to rank 0 (distributed.gather_witnesses)
+    gather = None
+    if world > 1:
+        from mythril_amd import distributed as DIST
+
+        ids_t = torch.arange(base, base + n_states, dtype=torch.int64, device=dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        gres = DIST.gather_witnesses(ids_t, d_first, d_wit.view(n_states, n_vars * 8), dst=0)
+        torch.cuda.synchronize(dev)
+        gms = 1e3 * (time.perf_counter() - tg)
+        if rank == 0:
+            gather = {"witness_states": int(len(gres[0])), "gather_bytes": int(gres[3]), "gather_ms": gms,
+                      "first_sat_bytes_per_step": 4 * n_states * world,
+                      "note": "RCCL gather of (state id, first-SAT, witness words) of every SAT state to rank 0"}
     first = d_first.cpu().numpy()
     sat = int((first >= 0).sum())
     planted_ok = bool(np.all(first[pl] >= 0) and np.all(first[pl] <= b["plant_idx"][pl].astype(np.int64)))
@@ -212,6 +230,44 @@ def main():
     achieved_gbs = bytes_launch / (kern_ms * 1e-3) / 1e9
     log(f"rank {rank}: kernel {kern_ms:.2f} ms/launch, step {1e3 * elapsed / args.steps:.2f} ms, SAT {sat}/{n_states}, "
         f"planted found {planted_ok}")
+
+    # Division split: the same states with every division drawn as an ADD
+    # (mgp_synth_set_ablate; the random stream is unchanged otherwise), timed on the same
+    # candidates.  div_share = the part of a launch the divisions take; frac_nondiv = the
+    # nominal ops of the division-free DAGs per second of their launch, against the spec
+    # peak -- the roofline of everything but the 1024-op division pricing.
+    div_split = None
+    if args.div_split and rank == 0:
+        N.synth_set_ablate(1)
+        try:
+            b2 = N.synth_generate(SEED, base, n_states, n_nodes, n_cand)
+        finally:
+            N.synth_set_ablate(0)
+        w2, po2, _ = N.lower(b2["nodes"], b2["node_offsets"], b2["consts"], b2["const_offsets"])
+        ops2 = N.nominal_ops(b2["nodes"], b2["node_offsets"]).astype(np.float64)
+        slots2 = int(N.program_headers(w2, po2)[:, 2].max())
+        order2, bounds2, bslots2 = N.plan_buckets(w2, po2)
+        d_w2 = torch.from_numpy(w2.view(np.int32)).to(dev)
+        d_po2 = torch.from_numpy(po2.view(np.int64)).to(dev)
+        d_order2 = torch.from_numpy(order2.view(np.int32)).to(dev)
+        ev2 = []
+        for k in range(args.warmup + args.steps):
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            e[0].record(stream)
+            N.eval_batch_dev(vp(d_w2), vp(d_po2), n_states, vp(d_cands), n_cand, n_vars, slots2, vp(d_first),
+                             vp(d_wit), vp(d_scratch), sh, vp(d_order2), bounds2, bslots2)
+            e[1].record(stream)
+            if k >= args.warmup:
+                ev2.append(e)
+        torch.cuda.synchronize(dev)
+        t2 = float(np.mean([a.elapsed_time(bb) for a, bb in ev2]))
+        ops_nondiv = float(ops2.sum()) * n_cand
+        div_split = {"launch_ms_nodiv": t2, "div_share": 1.0 - t2 / kern_ms,
+                     "ops_per_eval_nodiv": float(ops2.mean()),
+                     "achieved_nondiv": ops_nondiv / (t2 * 1e-3) / 1e12,
+                     "frac_nondiv": ops_nondiv / (t2 * 1e-3) / 1e12 / VALU_PEAK_TOPS}
+        del d_w2, d_po2, d_order2
+        log(f"rank {rank}: division split {div_split}")
 
     # HBM bytes and issued VALU instructions per step from the committed rocprofv3 PMC
     # run of the same workload (profiles/collect.sh -> analyze.py -> profiles/eval_pmc.json)
@@ -557,7 +613,10 @@ def main():
                          "frac_measured": achieved_tops / valu_peak, "frac_spec": achieved_tops / VALU_PEAK_TOPS,
                          "ops": "nominal INT32 ops of the live DAG nodes (SURVEY.md 8d table) x candidates",
                          "kernel": ENGINE_KERNEL[N.set_eval_engine()] + "(+finalize)", "launch_ms": kern_ms,
-                         "evals_per_launch": evals_rank},
+                         "evals_per_launch": evals_rank,
+                         **({} if div_split is None else {
+                             "frac_nondiv": div_split["frac_nondiv"], "div_share": div_split["div_share"],
+                             "div_split": div_split})},
             "roofline_hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": achieved_gbs / HBM_PEAK_GBS, "bytes_per_launch": bytes_launch},
             # VALU busy: every issued VALU instruction (dispatch/decode overhead included) x 64 lanes
@@ -570,6 +629,7 @@ def main():
             "prefilter": prefilter,
             "frontend": frontend,
             "suite": suite,
+            "gather": gather,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

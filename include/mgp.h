@@ -425,6 +425,10 @@ int mgp_synth_generate(uint64_t seed, uint64_t state_base, uint32_t n_states,
                        uint32_t *consts_out, uint64_t *const_offsets,
                        uint8_t *planted, uint32_t *plant_idx,
                        uint32_t *plant_words);
+/* Ablation of the synthetic generator for the benchmark's division split: mode 1 draws
+ * every division (UDIV/UREM/SDIV/SREM/SMOD) as an ADD, 2 every MUL, 3 both, 0 none; the
+ * DAGs are otherwise the same.  Process-wide (default from MGP_SYNTH_ABLATE). */
+int mgp_synth_set_ablate(int mode);
 
 /* Nominal INT32 op counts summed over the op-nodes of
  * each state — the algorithmic work the roofline fraction is priced on. */

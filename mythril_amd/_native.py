@@ -83,6 +83,7 @@ def _bind(lib):
         "mgp_keccak256_dev": (ctypes.c_int, [_P, _U64, _U32, _U32, _P, _P]),
         "mgp_fill_mapping_preimages_dev": (ctypes.c_int, [_P, _U64, _U64, _U64, _P]),
         "mgp_synth_generate": (ctypes.c_int, [_U64, _U64, _U32, _U32, _U32, _P, _P, _P, _P, _P, _P, _P]),
+        "mgp_synth_set_ablate": (ctypes.c_int, [ctypes.c_int]),
         "mgp_nominal_ops": (ctypes.c_int, [_P, _P, _U32, _P]),
         "mgp_probe_valu_dev": (ctypes.c_int, [_U32, _U32, _P, _P, _P]),
         "mgp_set_eval_engine": (ctypes.c_int, [ctypes.c_int]),
@@ -155,6 +156,7 @@ EXPORTED_SYMBOLS = (
     "mgp_keccak256_dev",
     "mgp_fill_mapping_preimages_dev",
     "mgp_synth_generate",
+    "mgp_synth_set_ablate",
     "mgp_nominal_ops",
     "mgp_probe_valu_dev",
     "mgp_set_eval_engine",
@@ -493,6 +495,11 @@ class Context:
 
 # ------------------------------------------------------------- synthetic
 SYNTH_VARS = 6
+
+
+def synth_set_ablate(mode: int) -> None:
+    """mgp_synth_set_ablate: 0 none, 1 divisions drawn as ADD, 2 MUL, 3 both."""
+    _check(lib().mgp_synth_set_ablate(int(mode)))
 
 
 def synth_generate(seed: int, state_base: int, n_states: int, n_nodes: int = 64, n_cand: int = 256):

@@ -10,9 +10,9 @@ struct mgp_dec_state {
   // blob: DAG, pre-relaxation DAG (congruence arguments), constants, base analysis,
   // propagation graph and the decision slots
   uint64_t nd, orig, consts, av, bs, isb, vtie, vars, pairs, cmp_pair, cmp_dom, cmp_t, pair_keys, pair_idx, ufs;
-  uint64_t uoff, ulist, voff, vlist, tie_rel, slot, width, node, eqh_off, eqh, cong, arel, og, odis, oatom, otgt;
+  uint64_t uoff, ulist, voff, vlist, tie_rel, slot, width, node, eqh_off, eqh, cong, arel, og, odis, oatom, otgt, inj;
   uint64_t n_consts;
-  uint32_t n, n_vt, n_pairs, n_ufs, n_slot, ucap, wcap, n_cong, n_arel, n_og;
+  uint32_t n, n_vt, n_pairs, n_ufs, n_slot, ucap, wcap, n_cong, n_arel, n_og, n_inj, pad;
   // workspace of one task of this state: private node values, variable values, pair
   // orderings, truth sets, undo log, work list
   uint64_t ws_av, ws_vars, ws_pairs, ws_bs, ws_undo, ws_work, ws_bytes;

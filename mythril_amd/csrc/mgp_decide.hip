@@ -107,6 +107,8 @@ __global__ __launch_bounds__(64) void mgp_decide_kernel(const uint8_t *__restric
   d.odis = at<OrDis>(blob, S.odis);
   d.oatom = at<int32_t>(blob, S.oatom);
   d.otgt = at<int32_t>(blob, S.otgt);
+  d.inj = at<InjApp>(blob, S.inj);
+  d.n_inj = S.n_inj;
   d.uoff = at<uint32_t>(blob, S.uoff);
   d.ulist = at<uint32_t>(blob, S.ulist);
   d.voff = at<uint32_t>(blob, S.voff);

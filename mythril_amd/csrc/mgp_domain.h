@@ -304,6 +304,8 @@ struct ArithRel { int32_t r, a, b, flag; uint8_t op; };
 // one node, e.g. ULE's Or(ULT, ==) expansion); targets [t0, t1): the nodes every disjunct
 // bounds.  See Dom::or_hull.
 struct OrGroup { int32_t root; uint32_t d0, d1, t0, t1; };
+// an application u = f(arg) whose inverse is asserted: eq is the node inv(u) == arg
+struct InjApp { int32_t u, arg, eq; uint32_t fn; };
 struct OrDis { int32_t node; uint32_t a0, a1; };
 struct UndoRec {
   uint8_t kind;  // 0 av, 1 bs, 2 pair, 3 var entry
@@ -397,6 +399,14 @@ struct Dom {
   const OrDis *odis = nullptr;
   const int32_t *oatom = nullptr;
   const int32_t *otgt = nullptr;
+  // Injectivity (round 4): the keccak manager asserts inv(f(x)) == x for every
+  // application (keccak_function_manager.py:118-146), so two applications with equal
+  // values have equal arguments.  When both inverse equalities are required and the
+  // values are known equal, the arguments are equated -- a wide Concat(key, slot) argument
+  // piecewise, on the original DAG -- so a Store chain read m[owner] that must meet the
+  // write m[sender] forces owner == sender (WalletLibrary's ownerIndex reads).
+  const InjApp *inj = nullptr;
+  uint32_t n_inj = 0;
   // decision rows: users of each node, VAR nodes of each variable entry, nodes tie() reads
   const uint32_t *uoff = nullptr, *ulist = nullptr, *voff = nullptr, *vlist = nullptr;
   const uint8_t *tie_rel = nullptr;
@@ -645,9 +655,57 @@ struct Dom {
     return true;
   }
 
+  // x and y (nodes) have equal values: narrow nodes meet each other and their pair (if any)
+  // becomes {=}; wide Concat trees of matching shape are equated piecewise
+  MGP_RD bool equate(int32_t x0, int32_t y0) {
+    const mgp_node *o = orig ? orig : nd;
+    int32_t st[16];
+    int ns = 0;
+    st[ns++] = x0;
+    st[ns++] = y0;
+    while (ns >= 2) {
+      const int32_t y = st[--ns], x = st[--ns];
+      if (x == y || x < 0 || y < 0) continue;
+      const uint32_t w = o[x].width;
+      if (w != o[y].width || isb[x] || isb[y]) continue;
+      if (w <= MGP_MAX_WIDTH && nd[x].width == w && nd[y].width == w) {
+        const AV ax = av[x], ay = av[y];
+        if (!meet(x, ay) || !meet(y, ax)) return false;
+        const int32_t pi = pair_find(((uint64_t)(uint32_t)(x < y ? x : y) << 32) | (uint32_t)(x < y ? y : x));
+        if (pi >= 0 && !set_order(pairs[pi], 2, OEQ)) return false;
+        continue;
+      }
+      if (o[x].op == MGP_OP_CONCAT && o[y].op == MGP_OP_CONCAT && o[o[x].b].width == o[o[y].b].width &&
+          ns + 4 <= 16) {
+        st[ns++] = o[x].a;
+        st[ns++] = o[y].a;
+        st[ns++] = o[x].b;
+        st[ns++] = o[y].b;
+      }
+    }
+    return true;
+  }
+  MGP_RD bool injective() {
+    for (uint32_t i = 0; i < n_inj; ++i) {
+      if (bs[inj[i].eq] != BT) continue;
+      for (uint32_t j = i + 1; j < n_inj && inj[j].fn == inj[i].fn; ++j) {
+        if (bs[inj[j].eq] != BT) continue;
+        const int32_t x = inj[i].u, y = inj[j].u;
+        bool same = is_exact(av[x]) && is_exact(av[y]) && EQV(av[x].lo, av[y].lo);
+        if (!same) {
+          const int32_t pi = pair_find(((uint64_t)(uint32_t)(x < y ? x : y) << 32) | (uint32_t)(x < y ? y : x));
+          same = pi >= 0 && pairs[pi].u == OEQ;
+        }
+        if (same && !equate(inj[i].arg, inj[j].arg)) return false;
+      }
+    }
+    return true;
+  }
+
   MGP_RD bool tie() {
     for (uint32_t k = 0; k < n_og; ++k)
       if (!or_hull(og[k])) return false;
+    if (n_inj && !injective()) return false;
     if (n_pairs == 0 && n_ufs == 0 && n_arel == 0) return true;
     for (int sweep = 0; sweep < 2; ++sweep)
       for (uint32_t i = 0; i < n; ++i) {
@@ -1410,8 +1468,11 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
     const uint32_t k = (drow & 1) ? P.n_slot - 1 - kk : kk;  // odd rows decide in reverse order
     const uint64_t key = fe_mix64(seed ^ fe_mix64(tag ^ ((uint64_t)c << 12) ^ P.slot[k]));
     const int32_t nk = P.node[k];
-    const bool ufapp = d.nd[nk].op == MGP_OP_UFAPP;
-    const uint32_t fn = d.nd[nk].p0;
+    // (on the original DAG: an application with a wide argument is a fresh variable in the
+    // relaxed one the domain runs on)
+    const mgp_node &on = (d.orig ? d.orig : d.nd)[nk];
+    const bool ufapp = on.op == MGP_OP_UFAPP;
+    const uint32_t fn = on.p0;
     if (EQV(d.av[nk].lo, d.av[nk].hi)) {  // already one value: nothing to decide
       put(P.slot[k], d.av[nk].lo);
       if (ufapp && n_seen < kSeenUf) {

@@ -66,6 +66,7 @@ struct State {
   std::vector<UfApp> ufs;
   std::vector<int32_t> cong;  // pairs of structurally matching operand nodes (Dom::cong)
   std::vector<ArithRel> arel;  // ADD / SUB nodes whose wrap status orders a compare pair (Dom::arel)
+  std::vector<InjApp> inj;     // applications with an asserted inverse (Dom::injective)
   std::vector<OrGroup> og;     // disjunctive hulls (Dom::or_hull)
   std::vector<OrDis> odis;
   std::vector<int32_t> oatom, otgt;
@@ -102,6 +103,8 @@ struct State {
     d.n_cong = (uint32_t)cong.size();
     d.arel = arel.data();
     d.n_arel = (uint32_t)arel.size();
+    d.inj = inj.data();
+    d.n_inj = (uint32_t)inj.size();
     d.og = og.data();
     d.n_og = (uint32_t)og.size();
     d.odis = odis.data();
@@ -276,6 +279,22 @@ struct State {
       }
     }
     build_or_groups();
+    // injectivity: EQ(UFINV(u), arg) with u = UFAPP(arg), on the original DAG
+    inj.clear();
+    for (uint32_t e = 0; e < n; ++e) {
+      if (o[e].op != MGP_OP_EQ) continue;
+      for (int side = 0; side < 2; ++side) {
+        const int32_t iv = side ? o[e].b : o[e].a, other = side ? o[e].a : o[e].b;
+        if (iv < 0 || o[iv].op != MGP_OP_UFINV) continue;
+        const int32_t u = o[iv].a;
+        if (u < 0 || o[u].op != MGP_OP_UFAPP || o[u].a != other || o[u].p0 != o[iv].p0) continue;
+        if (o[u].width > MGP_MAX_WIDTH || nd[u].width != o[u].width) continue;
+        inj.push_back(InjApp{u, other, (int32_t)e, o[u].p0});
+        break;
+      }
+    }
+    std::stable_sort(inj.begin(), inj.end(), [](const InjApp &x, const InjApp &y) { return x.fn < y.fn; });
+    if (inj.size() > 4u * kUfGroup) inj.resize(4u * kUfGroup);
     // the pair lookup as a sorted array (the view's binary search, host and device)
     pair_keys.clear();
     pair_idx.clear();
@@ -405,6 +424,7 @@ struct State {
       tie_rel[e.r] = tie_rel[e.a] = tie_rel[e.b] = 1;
       if (e.flag >= 0) tie_rel[e.flag] = 1;
     }
+    for (const InjApp &a : inj) tie_rel[a.u] = tie_rel[a.eq] = 1;
     for (const OrGroup &g : og) {
       tie_rel[g.root] = 1;
       for (uint32_t k = g.d0; k < g.d1; ++k) tie_rel[odis[k].node] = 1;
@@ -975,6 +995,8 @@ extern "C" int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes,
     h.n_arel = (uint32_t)S.arel.size();
     h.og = B.put(S.og);
     h.n_og = (uint32_t)S.og.size();
+    h.inj = B.put(S.inj);
+    h.n_inj = (uint32_t)S.inj.size();
     h.odis = B.put(S.odis);
     h.oatom = B.put(S.oatom);
     h.otgt = B.put(S.otgt);

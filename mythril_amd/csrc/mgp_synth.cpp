@@ -14,6 +14,7 @@
 // at a random candidate index by mgp_plant_candidates_dev.  Evaluating at x*
 // uses the same 256-bit helpers as the kernel (mgp_bv.h) — this is workload
 // construction, not verification; parity is checked against oracle/.
+#include <atomic>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -24,6 +25,15 @@
 #include "mgp_bv.h"
 
 namespace {
+std::atomic<int> g_ablate{-1};
+int synth_ablate_mode() {
+  int m = g_ablate.load(std::memory_order_relaxed);
+  if (m >= 0) return m;
+  const char *e = getenv("MGP_SYNTH_ABLATE");
+  m = !e ? 0 : !strcmp(e, "nodiv") ? 1 : !strcmp(e, "nomul") ? 2 : !strcmp(e, "nodivmul") ? 3 : 0;
+  g_ablate.store(m, std::memory_order_relaxed);
+  return m;
+}
 
 constexpr uint32_t kSynthVars = 6;
 constexpr uint32_t kFreeVars = 4;
@@ -216,17 +226,12 @@ struct Gen {
     }
     return MGP_OP_ADD;
   }
-  // ablation knob for kernel studies (never set by the benchmark):
-  // MGP_SYNTH_ABLATE=nodiv|nomul|nodivmul replaces those ops by ADD
+  // ablation knob for kernel studies: MGP_SYNTH_ABLATE=nodiv|nomul|nodivmul (or
+  // mgp_synth_set_ablate 1 / 2 / 3) replaces those ops by ADD.  The same random stream
+  // draws the same DAGs otherwise, so the benchmark's division split (bench.py
+  // roofline.div_share) times the same states with every division turned into an ADD.
   static uint8_t ablate(uint8_t op) {
-    static const int mode = [] {
-      const char *e = getenv("MGP_SYNTH_ABLATE");
-      if (!e) return 0;
-      if (!strcmp(e, "nodiv")) return 1;
-      if (!strcmp(e, "nomul")) return 2;
-      if (!strcmp(e, "nodivmul")) return 3;
-      return 0;
-    }();
+    const int mode = synth_ablate_mode();
     const bool div = op >= MGP_OP_UDIV && op <= MGP_OP_SMOD;
     if (((mode & 1) && div) || ((mode & 2) && op == MGP_OP_MUL)) return MGP_OP_ADD;
     return op;
@@ -465,5 +470,11 @@ extern "C" int mgp_nominal_ops(const mgp_node *nodes, const uint64_t *node_offse
     }
     out_ops[s] = t;
   }
+  return MGP_OK;
+}
+
+extern "C" int mgp_synth_set_ablate(int mode) {
+  if (mode < 0 || mode > 3) return MGP_E_ARG;
+  g_ablate.store(mode, std::memory_order_relaxed);
   return MGP_OK;
 }

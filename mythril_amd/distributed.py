@@ -116,3 +116,50 @@ def run_sharded(state_ids: Sequence[int], evaluate: Callable[[np.ndarray], np.nd
         idx = local_indices(state_ids, rank, world)
     first = evaluate(idx) if len(idx) else np.zeros(0, dtype=np.int32)
     return gather_first_sat(idx, first, len(state_ids), dst=dst, device=device)
+
+
+def gather_witnesses(ids, first, wit, dst: int = 0):
+    """Gather the SAT states' (global id, first-SAT index, witness words) to rank `dst` -- the
+    second half of SURVEY.md §8e's exchange step (first-SAT words for every state, witness
+    words only for the SAT ones).
+
+    ids (int64 [n]), first (int32 [n]) and wit (int32 [n, n_vars * 8]) are this rank's
+    states as torch tensors on the process group's device (CUDA for "nccl" = RCCL, CPU for
+    gloo).  Only rows with first >= 0 travel: the counts are exchanged, every rank pads to
+    the largest count, one gather of the index / first pairs and one of the witness rows
+    follow.  -> on dst (ids np.int64 [k], first np.int32 [k], witness np.int32 [k, n_vars*8],
+    bytes received), None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    sat = torch.nonzero(first >= 0).flatten()
+    k_local = torch.tensor([int(sat.numel())], dtype=torch.int64, device=first.device)
+    counts = [torch.zeros_like(k_local) for _ in range(world)]
+    dist.all_gather(counts, k_local)
+    cap = max(1, max(int(c.item()) for c in counts))
+    width = int(wit.shape[1]) if wit.dim() == 2 else 0
+    head = torch.full((2, cap), -1, dtype=torch.int64, device=first.device)
+    rows = torch.zeros((cap, max(width, 1)), dtype=torch.int32, device=first.device)
+    n = int(sat.numel())
+    if n:
+        head[0, :n] = ids[sat].to(torch.int64)
+        head[1, :n] = first[sat].to(torch.int64)
+        if width:
+            rows[:n, :width] = wit[sat]
+    h_recv = [torch.empty_like(head) for _ in range(world)] if rank == dst else None
+    r_recv = [torch.empty_like(rows) for _ in range(world)] if rank == dst else None
+    dist.gather(head, h_recv, dst=dst)
+    dist.gather(rows, r_recv, dst=dst)
+    if rank != dst:
+        return None
+    out_ids, out_first, out_rows = [], [], []
+    for r in range(world):
+        k = int(counts[r].item())
+        a = h_recv[r].cpu().numpy()
+        out_ids.append(a[0, :k])
+        out_first.append(a[1, :k])
+        out_rows.append(r_recv[r].cpu().numpy()[:k, :width])
+    nbytes = sum((head.numel() * 8 + rows.numel() * 4) for _ in range(world))
+    return (np.concatenate(out_ids), np.concatenate(out_first).astype(np.int32),
+            np.concatenate(out_rows).astype(np.int32), nbytes)

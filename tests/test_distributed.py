@@ -63,6 +63,51 @@ def _worker(rank, world, port, out_path, balanced=False):
     dist.destroy_process_group()
 
 
+def _wit_worker(rank, world, port, out_path):
+    """Each rank evaluates its hash shard, then rank 0 gathers the SAT states' first-SAT
+    index and witness words (distributed.gather_witnesses, the §8e exchange step)."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, cands = _batch()
+    ids = np.arange(len(b["planted"])) + 10_000
+    idx = D.local_indices(ids, rank, world)
+    first = coracle.first_sat(*_slice(b, cands, idx)) if len(idx) else np.zeros(0, np.int32)
+    n_vars = cands.shape[2]
+    wit = np.zeros((len(idx), n_vars * 8), np.int32)
+    for k, s in enumerate(idx):
+        if first[k] >= 0:
+            wit[k] = cands[s, first[k]].reshape(-1).view(np.int32)
+    res = D.gather_witnesses(torch.as_tensor(ids[idx].astype(np.int64)), torch.as_tensor(first.astype(np.int32)),
+                             torch.as_tensor(wit), dst=0)
+    if rank == 0:
+        np.savez(out_path, ids=res[0], first=res[1], rows=res[2], nbytes=res[3])
+    else:
+        assert res is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_two_rank_witness_gather_matches_single_process(tmp_path):
+    """The gathered witnesses are the single-process witnesses: every SAT state once, with
+    its lowest satisfying candidate row (the witness the kernel writes)."""
+    out = str(tmp_path / "wit.npz")
+    mp.spawn(_wit_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    b, cands = _batch()
+    want = coracle.first_sat(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], cands)
+    sat = np.nonzero(want >= 0)[0]
+    order = np.argsort(got["ids"])
+    assert np.array_equal(got["ids"][order] - 10_000, sat)
+    assert np.array_equal(got["first"][order], want[sat])
+    rows = got["rows"][order].view(np.uint32).reshape(len(sat), cands.shape[2], 8)
+    assert np.array_equal(rows, cands[sat, want[sat]])
+    assert int(got["nbytes"]) > 0
+
+
 def test_hash_sharding_is_a_partition():
     ids = np.arange(10_000)
     for world in (1, 2, 4, 8):

@@ -617,6 +617,64 @@ def test_structural_congruence_exhaustive_soundness():
     assert refuted[0] > 0.8 * n_form[0] and refuted[1] > 0.8 * n_form[1], (refuted, n_form)
 
 
+def test_injectivity_exhaustive_soundness():
+    """Applications f(a) with their inverse asserted (inv(f(a)) == a, as the keccak manager
+    asserts for every application) -- direct, and through Concat(x, c) arguments of twice the
+    width -- with compares between the values and between the arguments: no refuted state
+    has a model over all 8^5 assignments of the variables and fresh values (C oracle), and
+    the injectivity rule (Dom::injective) refutes `f(a) == f(b) and a != b`."""
+    rng = np.random.default_rng(0x1A1)
+    w = 3
+    states = []
+    for _ in range(240):
+        nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
+        cl = [int(rng.integers(0, 8)) for _ in range(2)]
+        nl += [[S.CONST, w, -1, -1, -1, 0, 0], [S.CONST, w, -1, -1, -1, 1, 0]]
+        bools, apps = [], []
+        wide = rng.random() < 0.5
+        for k in range(2):
+            a = int(rng.choice([0, 1, 2, 3]))
+            if wide:
+                nl.append([S.CONCAT, 2 * w, a, 2, -1, 0, 0])
+                a = len(nl) - 1
+            nl.append([S.UFAPP, w, a, -1, -1, 7 if wide else 5, 2 + k])
+            u = len(nl) - 1
+            if rng.random() < 0.85:      # the manager's inv(f(x)) == x
+                nl.append([S.UFINV, 2 * w if wide else w, u, -1, -1, 7 if wide else 5, 4 + k])
+                nl.append([S.EQ, 1, len(nl) - 1, a, -1, 0, 0])
+                bools.append(len(nl) - 1)
+            apps.append((u, a))
+        (u0, a0), (u1, a1) = apps
+        nl.append([S.EQ, 1, u0, u1, -1, 0, 0])
+        bools.append(len(nl) - 1)
+        if rng.random() < 0.6:          # the arguments differ
+            nl.append([S.EQ, 1, a0, a1, -1, 0, 0])
+            nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+            bools.append(len(nl) - 1)
+        if rng.random() < 0.5:
+            nl.append([[S.ULT, S.EQ, S.UGT][int(rng.integers(3))], 1, int(rng.choice([0, 1])), 3, -1, 0, 0])
+            bools.append(len(nl) - 1)
+        root = bools[0]
+        for b in bools[1:]:
+            nl.append([S.BAND, 1, root, b, -1, 0, 0])
+            root = len(nl) - 1
+        states.append((nl, cl))
+    verdict = _refute(states)
+    n_vars = 6
+    grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
+    cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    refuted = 0
+    for (nl, cl), r in zip(states, verdict):
+        assert r in (0, 1)
+        if r != 1:
+            continue
+        refuted += 1
+        nodes, noff, consts, coff = pack_states([(nl, cl)])
+        assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
+    assert refuted > 40, refuted
+
+
 def _wrap_or_state(rng, w=3):
     """Random DAGs over three w-bit variables mixing ADD / SUB results compared with their
     operands (the wrap-ordering rule), BVAddNoOverflow / BVSubNoUnderflow flags on the same

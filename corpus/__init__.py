@@ -37,7 +37,7 @@ from __future__ import annotations
 import copy
 from typing import List, Optional, Tuple
 
-from mythril_amd.keccak import KeccakFunctionManager
+from .keccak_manager import KeccakFunctionManager
 from mythril_amd.smt import (And, Array, BVMulNoOverflow, BVSubNoUnderflow, Concat, Extract, If, Not, Or, UDiv, UGE,
                              UGT, ULE, ULT, symbol_factory)
 

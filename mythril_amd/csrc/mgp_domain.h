@@ -462,6 +462,19 @@ struct Dom {
     return true;
   }
   // would meeting s into node i leave it non-empty?
+  // ITE node i is narrowed past the hull of its branches (a requirement from above that
+  // one branch may not meet): some value either branch could take is excluded
+  // and the chain's fall-through (the else-branches followed past conditions not known
+  // true, to the first non-ITE) cannot supply it: a draw alone cannot meet the requirement
+  MGP_RD bool ite_required(uint32_t i) const {
+    const AV &r = av[i], &b = av[nd[i].b], &e = av[nd[i].c];
+    const V hz = AND(b.z, e.z), ho = AND(b.o, e.o), hlo = MIN(b.lo, e.lo), hhi = MAX(b.hi, e.hi);
+    if (EQV(AND(r.z, hz), r.z) && EQV(AND(r.o, ho), r.o) && !LT(hlo, r.lo) && !LT(r.hi, hhi)) return false;
+    int32_t j = (int32_t)i;
+    for (uint32_t hop = 0; hop < n && nd[j].op == MGP_OP_ITE && nd[j].a >= 0 && bs[nd[j].a] != BT; ++hop) j = nd[j].c;
+    return nd[j].op == MGP_OP_ITE ? false : !compatible(j, r);
+  }
+
   MGP_RD bool compatible(int32_t i, const AV &s) const {
     AV t = av[i];
     t.z = OR(t.z, s.z);
@@ -1370,8 +1383,10 @@ MGP_RD bool inside_av(const AV &a, const V &v) {
   return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
 }
 
-// rows whose decisions start with the Or case split (bit r: row r)
+// rows whose decisions start with the Or case split and the ITE branch split (bit r: row r)
 constexpr uint32_t kOrRowsDefault = 0xAu;
+// the split row whose ITE branch split always tries the then-branch first
+constexpr uint32_t kIteGreedyRow = 1u;
 
 // Decision row `row` of a prepared state on `d`, a private copy of the state's base
 // analysis (heur set, undo log and work list attached): each variable slot in turn is
@@ -1440,6 +1455,34 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
         const uint32_t mark = undo_log.size();
         work.clear();
         if (d.meetb(pick, BT) && d.run_from((uint32_t)pick, budget) == 0 && !undo_log.over) {
+          undo_log.clear();
+          break;
+        }
+        if (undo_log.over) return;
+        d.rollback(mark);
+      }
+    }
+  }
+  // Branch split of required selects (round 4): an ITE whose value the analysis has
+  // narrowed past the hull of its two branches (a storage read required non-zero, a
+  // balance read required >= a bound) with its condition open is a disjunction over the
+  // branches that can supply the value.  From the root down, such an ITE takes its
+  // then-branch (condition true: the read address equals that store's address, so the
+  // keys are equated and, through the keccak inverse, their preimages) or its else-branch;
+  // row kIteGreedyRow takes the first then-branch that propagates, the other split rows
+  // choose per node by the row's stream, and either way a choice that empties a domain
+  // is rolled back and the other side taken.  Without it a read of m_ownerIndex[k] after
+  // m_ownerIndex[sender] = 1 needs k == sender, which no independent draw of k gives.
+  if (row < 32u && ((or_rows >> row) & 1u)) {
+    for (uint32_t i = d.n; i-- > 0;) {
+      const mgp_node &x = d.nd[i];
+      if (x.op != MGP_OP_ITE || x.a < 0 || d.bs[x.a] != BB || !d.ite_required(i)) continue;
+      const bool then_first = row == kIteGreedyRow || ((fe_mix64(seed ^ fe_mix64(tag ^ i ^ ((uint64_t)row << 40))) >> 17) & 1u);
+      for (int side = 0; side < 2; ++side) {
+        const uint8_t want = (side == 0) == then_first ? BT : BF;
+        const uint32_t mark = undo_log.size();
+        work.clear();
+        if (d.meetb(x.a, want) && d.run_from((uint32_t)x.a, budget) == 0 && !undo_log.over) {
           undo_log.clear();
           break;
         }

@@ -5,8 +5,9 @@
 //
 // An abstract value is known bits (z = known-zero mask, o = known-one mask) x an
 // unsigned interval [lo, hi] (mgp_refute.cpp).  Row 0 takes lo, row 1 hi, row 2 lo + 1;
-// later rows a draw inside the interval (a full-width draw when the interval spans more
-// than 64 bits) with the known bits forced when that stays inside.
+// later rows a draw inside the interval (for a span of more than 64 bits: a full-width
+// draw when the interval covers half the values or more, else lo plus a draw below the
+// span) with the known bits forced when that stays inside.
 #pragma once
 #include <stdint.h>
 
@@ -44,10 +45,30 @@ MGP_HD U256 fe_sample_domain(const U256 &z, const U256 &o, const U256 &lo, const
     x = bv_add(lo, kk, nullptr);
     if (bv_ult(hi, x)) x = hi;
   } else {
-    x = v;  // wide interval: a full-width draw
+    // wide interval: a full-width draw when the interval covers at least half the width's
+    // values; else lo + a draw below the span (round 4: a narrow interval high in the range,
+    // e.g. a keccak manager interval of 2^123 values near 2^256, used to get lo or hi here,
+    // neither of which keeps the interval's alignment)
+    const uint32_t bl = bv_bitlen(span);
+    if (bl >= w) {
+      x = v;
+    } else {
+      U256 d = bv_mask(v, bl);
+      if (bv_ult(span, d)) d = bv_mask(v, bl - 1u);
+      x = bv_add(lo, d, nullptr);
+    }
   }
-  const U256 yw = bv_mask(bv_or(bv_and(x, bv_not(z)), o), w);
+  U256 yw = bv_mask(bv_or(bv_and(x, bv_not(z)), o), w);
   if (!bv_ult(yw, lo) && !bv_ult(hi, yw)) return yw;
+  if (!small && bv_ult(yw, lo)) {
+    // forcing known-zero low bits (an alignment) dropped below lo: one alignment step up
+    uint32_t a = 0;
+    while (a < w && ((z.w[a >> 5] >> (a & 31)) & 1u)) ++a;
+    if (a > 0 && a < w) {
+      const U256 up = bv_mask(bv_or(bv_and(bv_add(yw, bv_shl(bv_small(1u), a), nullptr), bv_not(z)), o), w);
+      if (!bv_ult(up, lo) && !bv_ult(hi, up)) return up;
+    }
+  }
   return (small || (!bv_ult(x, lo) && !bv_ult(hi, x))) ? x : ((row & 1) ? hi : lo);
 }
 

@@ -1,19 +1,11 @@
-"""KeccakFunctionManager mirror + batched concrete Keccak-256 on the GPU.
+"""Batched concrete Keccak-256 on the GPU: the product side of the keccak path.
 
-Mirrors mythril/laser/ethereum/keccak_function_manager.py:21-149 (same
-method names, constants and constraint shapes):
-
-  find_concrete_keccak(data)      40-54   concrete hash of data.size()//8 big-endian bytes
-  get_function(length)            56-69   UF pair keccak256_<n> / keccak256_<n>-1
-  get_empty_keccak_hash()         71-78
-  create_keccak(data)             80-98   (hash term, condition)
-  get_concrete_hash_data(model)   100-116
-  _create_condition(func_input)   118-146 interval [index*PART, index*PART+PART), %64 == 0,
-                                          OR over the concrete hashes seen so far
-
-The concrete hashes go through the HIP Keccak kernel (libmgp.so,
-mgp_keccak256_batch) — one launch for a whole batch via
-`find_concrete_keccak_batch` — instead of pyethereum's utils.sha3.
+`find_concrete_keccak` replaces the pyethereum utils.sha3 call of
+mythril/laser/ethereum/keccak_function_manager.py:40-54 with the HIP Keccak
+kernel (libmgp.so, mgp_keccak256_batch); `find_concrete_keccak_batch` hashes a
+whole batch in one launch.  The manager's UF modelling itself (get_function,
+create_keccak, _create_condition) stays the reference's; its restatement for
+the corpus and the tests is corpus/keccak_manager.py.
 `get_code_hash` / `get_code_hashes` mirror support/support_utils.py:29-41
 (pysha3 keccak_256 of the bytecode) on the same kernel, and
 `replace_with_actual_sha` mirrors the report-time substitution of
@@ -25,11 +17,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .smt import And, BitVec, Bool, Function, Or, ULE, ULT, URem, symbol_factory
+from .smt import BitVec, symbol_factory
 
-TOTAL_PARTS = 10 ** 40
-PART = (2 ** 256 - 1) // TOTAL_PARTS
-INTERVAL_DIFFERENCE = 10 ** 30
 hash_matcher = "fffffff"
 
 _ctx = None
@@ -88,95 +77,18 @@ def get_code_hash(code: str) -> str:
     return get_code_hashes([code])[0]
 
 
-class KeccakFunctionManager:
-    def __init__(self):
-        self.store_function: Dict[int, Tuple[Function, Function]] = {}
-        self.interval_hook_for_size: Dict[int, int] = {}
-        self._index_counter = TOTAL_PARTS - 34534
-        self.hash_result_store: Dict[int, List[BitVec]] = {}
-        self.quick_inverse: Dict[BitVec, BitVec] = {}
-        self.concrete_hashes: Dict[BitVec, BitVec] = {}
-
-    @staticmethod
-    def find_concrete_keccak(data: BitVec) -> BitVec:
-        digest = keccak256(data.value.to_bytes(data.size() // 8, byteorder="big"))
-        return symbol_factory.BitVecVal(int.from_bytes(digest, "big"), 256)
-
-    @staticmethod
-    def find_concrete_keccak_batch(datas: Sequence[BitVec]) -> List[BitVec]:
-        digs = keccak256_batch([d.value.to_bytes(d.size() // 8, byteorder="big") for d in datas])
-        return [symbol_factory.BitVecVal(int.from_bytes(h, "big"), 256) for h in digs]
-
-    def get_function(self, length: int) -> Tuple[Function, Function]:
-        try:
-            func, inverse = self.store_function[length]
-        except KeyError:
-            func = Function("keccak256_{}".format(length), length, 256)
-            inverse = Function("keccak256_{}-1".format(length), 256, length, inverse_of=func)
-            self.store_function[length] = (func, inverse)
-            self.hash_result_store[length] = []
-        return func, inverse
-
-    @staticmethod
-    def get_empty_keccak_hash() -> BitVec:
-        val = 89477152217924674838424037953991966239322087453347756267410168184682657981552
-        return symbol_factory.BitVecVal(val, 256)
-
-    def create_keccak(self, data: BitVec) -> Tuple[BitVec, Bool]:
-        length = data.size()
-        func, inverse = self.get_function(length)
-        if data.symbolic is False:
-            concrete_hash = self.find_concrete_keccak(data)
-            self.concrete_hashes[data] = concrete_hash
-            condition = And(func(data) == concrete_hash, inverse(func(data)) == data)
-            return concrete_hash, condition
-        condition = self._create_condition(func_input=data)
-        self.hash_result_store[length].append(func(data))
-        return func(data), condition
-
-    def get_concrete_hash_data(self, model) -> Dict[int, List[Optional[int]]]:
-        concrete_hashes: Dict[int, List[Optional[int]]] = {}
-        for size in self.hash_result_store:
-            concrete_hashes[size] = []
-            for val in self.hash_result_store[size]:
-                v = _as_int(model.eval(val.raw))
-                if v is not None:
-                    concrete_hashes[size].append(v)
-        return concrete_hashes
-
-    def _create_condition(self, func_input: BitVec) -> Bool:
-        length = func_input.size()
-        func, inv = self.get_function(length)
-        try:
-            index = self.interval_hook_for_size[length]
-        except KeyError:
-            self.interval_hook_for_size[length] = self._index_counter
-            index = self._index_counter
-            self._index_counter -= INTERVAL_DIFFERENCE
-        lower_bound = index * PART
-        upper_bound = lower_bound + PART
-        cond = And(
-            inv(func(func_input)) == func_input,
-            ULE(symbol_factory.BitVecVal(lower_bound, 256), func(func_input)),
-            ULT(func(func_input), symbol_factory.BitVecVal(upper_bound, 256)),
-            URem(func(func_input), symbol_factory.BitVecVal(64, 256)) == 0,
-        )
-        concrete_cond = symbol_factory.Bool(False)
-        for key, keccak in self.concrete_hashes.items():
-            hash_eq = And(func(func_input) == keccak, key == func_input)
-            concrete_cond = Or(concrete_cond, hash_eq)
-        return And(inv(func(func_input)) == func_input, Or(cond, concrete_cond))
-
-    def interval_values(self, length: int, k: int = 4) -> List[int]:
-        """Candidate hash values for keccak256_<length>: aligned points of its interval."""
-        if length not in self.interval_hook_for_size:
-            return []
-        lo = self.interval_hook_for_size[length] * PART
-        lo += (-lo) % 64
-        return [lo + 64 * j for j in range(k)]
+def find_concrete_keccak(data: BitVec) -> BitVec:
+    """keccak_function_manager.py:40-54 (`KeccakFunctionManager.find_concrete_keccak`): the
+    Keccak-256 of data.size()//8 big-endian bytes, as a 256-bit value.  The one method of the
+    reference's manager that LASER swaps for this."""
+    digest = keccak256(data.value.to_bytes(data.size() // 8, byteorder="big"))
+    return symbol_factory.BitVecVal(int.from_bytes(digest, "big"), 256)
 
 
-keccak_function_manager = KeccakFunctionManager()
+def find_concrete_keccak_batch(datas: Sequence[BitVec]) -> List[BitVec]:
+    """find_concrete_keccak over many values, one GPU launch per distinct length."""
+    digs = keccak256_batch([d.value.to_bytes(d.size() // 8, byteorder="big") for d in datas])
+    return [symbol_factory.BitVecVal(int.from_bytes(h, "big"), 256) for h in digs]
 
 
 def _as_int(v) -> Optional[int]:
@@ -214,7 +126,7 @@ def _hash_substitutions(tx_input: str, s_index: int, concrete_hashes, manager, m
 
 
 def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, code=None,
-                            manager: Optional[KeccakFunctionManager] = None, hasher=None) -> None:
+                            manager=None, hasher=None) -> None:
     """analysis/solver.py:159-192 (`_replace_with_actual_sha`): every 64-hex-digit window of a
     transaction's input that contains `hash_matcher` and equals a hash value of the model is
     replaced by the real Keccak-256 of the preimage the model gives its inverse.
@@ -224,9 +136,12 @@ def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, 
     over the unmodified inputs collects every preimage and hashes them in one launch
     (`hasher`: list of BitVec -> list of BitVec, default the GPU kernel); the exact
     sequential pass then reads that table and hashes the rare preimage it did not predict.
+    `manager` is the keccak function manager whose UF pairs the model speaks about (its
+    `store_function` and `get_concrete_hash_data`); by default LASER's singleton.
     """
-    manager = manager or keccak_function_manager
-    hasher = hasher or KeccakFunctionManager.find_concrete_keccak_batch
+    if manager is None:  # LASER's module-level singleton (keccak_function_manager.py:149)
+        from mythril.laser.ethereum.keccak_function_manager import keccak_function_manager as manager
+    hasher = hasher or find_concrete_keccak_batch
     concrete_hashes = manager.get_concrete_hash_data(model)
 
     def start(tx) -> Optional[int]:

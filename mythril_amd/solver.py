@@ -552,12 +552,15 @@ class Prefilter:
             B.close()
             res: List = [None] * len(states)
             refuted: List[int] = []
+            profs: List[dict] = []
             for grp in self._groups(nv, self.n_cand):
                 sub, sub_ref = self._check_native(ctx, [states[k] for k in grp],
                                                   None if parents is None else [parents[k] for k in grp])
                 for k, r in zip(grp, sub):
                     res[k] = r
                 refuted.extend(grp[k] for k in sub_ref)
+                profs.append(self.last_profile or {})
+            self.last_profile = _sum_profiles(profs)
             return res, sorted(refuted)
         prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
         first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute)
@@ -677,6 +680,28 @@ class Prefilter:
         prof["decide_states"] = len(retry)
         prof["retry_sat"] = found
         SolverStatistics().gpu_retry += len(retry)
+
+
+def _sum_profiles(profs: List[dict]) -> dict:
+    """Stage profile of a batch run as sub-batches: numeric stages summed (nested dicts
+    too), flags OR-ed, and the sub-batch count recorded."""
+    out: dict = {"groups": len(profs)}
+    for p in profs:
+        for k, v in p.items():
+            if isinstance(v, dict):
+                out[k] = _sum_profiles_into(out.get(k, {}), v)
+            elif isinstance(v, bool):
+                out[k] = bool(out.get(k, False)) or v
+            elif isinstance(v, (int, float)):
+                out[k] = out.get(k, 0) + v
+    return out
+
+
+def _sum_profiles_into(acc: dict, p: dict) -> dict:
+    for k, v in p.items():
+        if isinstance(v, (int, float)) and not isinstance(v, bool):
+            acc[k] = acc.get(k, 0) + v
+    return acc
 
 
 _prefilter: Optional[Prefilter] = None

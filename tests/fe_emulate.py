@@ -90,3 +90,96 @@ def run(n: int = 1024, seed: int = 0x4D595448, decide_rows: int = 4, n2: int = 2
 
 if __name__ == "__main__":
     run(int(sys.argv[1]) if len(sys.argv) > 1 else 1024)
+
+
+def suite_answers(queries, seed: int = 0x4D595448, decide_rows: int = 4, n2: int = 256, seed_rows: int = 0x3,
+                  witnesses: bool = False):
+    """The product policy over corpus.suite() queries on the CPU, level by level along the
+    parent links as corpus.answer feeds the GPU Prefilter: first round (parent witness in
+    row 0, device mixture with domain rows), host pre-check, second round with (parent-
+    seeded) decision rows.  -> list of 'sat' / 'unsat' / 'undecided' (test infrastructure:
+    the C oracle evaluates the candidates)."""
+    from mythril_amd import solver as SV
+
+    n = len(queries)
+    depth = [0] * n
+    for i, q in enumerate(queries):
+        depth[i] = depth[q[5]] + 1 if q[5] >= 0 else 0
+    ans = ["undecided"] * n
+    wit = [None] * n     # (slot keys, values) of a SAT query's witness
+    levels = collections.defaultdict(list)
+    for i, d in enumerate(depth):
+        levels[d].append(i)
+    fake = type("P", (), {"decide_rows": decide_rows, "decide_max_units": SV.Prefilter.DECIDE_MAX_UNITS,
+                          "DECIDE_MIN_ROWS": SV.Prefilter.DECIDE_MIN_ROWS})()
+    for d in sorted(levels):
+        idx = levels[d]
+        B = F.Batch([list(queries[i][3]) for i in idx])
+        par = [wit[queries[i][5]] if queries[i][5] >= 0 else None for i in idx]
+        ref, dom = N.refute_domains(*B.packed(), B.var_off)
+        nv = max(1, B.n_vars())
+        has = np.array([p is not None for p in par], np.uint8)
+        c = N.make_candidates(256, nv, seed, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off, B.aliases,
+                              B.const_off, B.consts, D._FIXED_LIMBS, has, var_kind=B.var_kind, dom=dom,
+                              state_keys=B.state_key)
+        sv, sm = F.seed_arrays(B, [None if p is None else dict_to_witness(p) for p in par])
+        for s in range(B.n_states):
+            m = sm[s].astype(bool)
+            c[s, 0, m] = sv[s, m]
+        _, _, status = N.lower(*B.packed(gpu=True))
+        f1 = coracle.first_sat(*B.packed(gpu=True), c)
+        f1[status != 0] = -2
+        f1[(B.flags & F.FE_SAT_UNSAFE) != 0] = -1
+        open_ = [k for k in range(len(idx)) if f1[k] < 0 and ref[k] != 1]
+        rows = None
+        if open_:
+            SB = F.Batch([list(queries[idx[k]][3]) for k in open_])
+            rps = SV.Prefilter.rows_per_state(fake, SB)
+            spar = [par[k] for k in open_]
+            seeds = F.seed_arrays(SB, [None if p is None else dict_to_witness(p) for p in spar]) \
+                if any(p is not None for p in spar) else None
+            seed2 = seed + 0x7F4A7C15
+            rows, mask, _ = N.decision_rows(*SB.packed(decide=True), max(1, SB.n_vars()), seed2, decide_rows, rps,
+                                            state_keys=SB.state_key, seeds=seeds, seed_rows=seed_rows)
+            _, dom2 = N.refute_domains(*SB.packed(), SB.var_off)
+            nv2 = max(1, SB.n_vars())
+            c2 = N.make_candidates(n2, nv2, seed2, SB.var_off, SB.var_width, SB.hint_off, SB.hints, SB.alias_off,
+                                   SB.aliases, SB.const_off, SB.consts, D._FIXED_LIMBS, np.zeros(SB.n_states, np.uint8),
+                                   var_kind=SB.var_kind, dom=dom2, state_keys=SB.state_key)
+            apply_xrows(SB, c2, rows, mask)
+            _, _, st2 = N.lower(*SB.packed(gpu=True))
+            f2 = coracle.first_sat(*SB.packed(gpu=True), c2)
+            f2[st2 != 0] = -2
+            f2[(SB.flags & F.FE_SAT_UNSAFE) != 0] = -1
+            for j, k in enumerate(open_):
+                if f2[j] >= 0:
+                    i = idx[k]
+                    ans[i] = "sat"
+                    v0, v1 = int(SB.var_off[j]), int(SB.var_off[j + 1])
+                    wit[i] = (np.array(SB.var_key[v0:v1]), c2[j, f2[j], : v1 - v0].copy())
+            SB.close()
+        for k, i in enumerate(idx):
+            if f1[k] >= 0:
+                ans[i] = "sat"
+                v0, v1 = int(B.var_off[k]), int(B.var_off[k + 1])
+                wit[i] = (np.array(B.var_key[v0:v1]), c[k, f1[k], : v1 - v0].copy())
+            elif ref[k] == 1:
+                ans[i] = "unsat"
+        B.close()
+    return (ans, wit) if witnesses else ans
+
+
+class dict_to_witness:
+    """A (slot keys, values) pair in the shape front.parent_arrays accepts."""
+
+    def __init__(self, kv):
+        self.kv = kv
+
+
+def _parent_arrays_kv(p, _orig=F.parent_arrays):
+    if isinstance(p, dict_to_witness):
+        return np.asarray(p.kv[0], np.uint64), np.ascontiguousarray(p.kv[1], np.uint32).reshape(-1, 8)
+    return _orig(p)
+
+
+F.parent_arrays = _parent_arrays_kv

@@ -7,7 +7,7 @@ import pytest
 
 from mythril_amd import dag as D
 from mythril_amd import front as F
-from mythril_amd.keccak import KeccakFunctionManager
+from corpus.keccak_manager import KeccakFunctionManager
 from mythril_amd.smt import (Array, And, BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow, Concat, Extract, Function,
                              If, K, LShR, Not, Or, SRem, UDiv, UGE, UGT, ULE, ULT, URem, Xor, symbol_factory)
 

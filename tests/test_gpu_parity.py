@@ -584,6 +584,54 @@ def _band4n_states(rng, n, late_vars: int = 0):
     return out
 
 
+def _mul_after_shift_states(rng, n):
+    """A per-lane shift (its handler leaves v6 = 32 - amount, or all-ones for amounts >=
+    256) and then MULs whose products' high limbs decide a compare.  The r3n defect: the
+    MUL handler's Comba column 0 moved v6 into the accumulator's high word instead of 0,
+    so a product read whatever the previous handler left in v6."""
+    w = 256
+    shifts = [S.LSHR, S.SHL, S.ASHR]
+    cmps = [S.ULT, S.UGT, S.SLT]
+    out = []
+    for _ in range(n):
+        nl = [[S.VAR, w, -1, -1, -1, k, 0] for k in range(3)]
+        cl = [int(rng.integers(1, 2 ** 62)) << 192, int(rng.integers(0, 2 ** 32))]
+        nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(2)]                  # 3, 4
+        nl.append([shifts[int(rng.integers(3))], w, 2, int(rng.integers(0, 2)), -1, 0, 0])  # 5
+        nl.append([S.MUL, w, 0, 1, -1, 0, 0])                                      # 6
+        nl.append([cmps[int(rng.integers(3))], 1, 6, 3, -1, 0, 0])                 # 7
+        nl.append([S.EQ, 1, 5, 4, -1, 0, 0])                                       # 8
+        nl.append([S.BNOT, 1, 8, -1, -1, 0, 0])                                    # 9
+        nl.append([S.BAND, 1, 7, 9, -1, 0, 0])                                     # 10
+        if rng.random() < 0.5:   # a second product after another shift
+            nl.append([shifts[int(rng.integers(3))], w, 5, 1, -1, 0, 0])           # 11
+            nl.append([S.MUL, w, 11, 2, -1, 0, 0])                                 # 12
+            nl.append([S.ULT, 1, 12, 3, -1, 0, 0])                                 # 13
+            nl.append([S.BAND, 1, 10, 13, -1, 0, 0])
+        out.append((nl, cl))
+    return out
+
+
+def test_mul_after_shift_scratch_vs_oracle(mgp_ctx):
+    """MUL after a handler that leaves scratch register v6 non-zero, against the C oracle on
+    every candidate (both engines).  Fails on the r3n MUL (column 0 reading a stale v6),
+    which the full-size test caught as 39 339 asm/HIP disagreements."""
+    rng = np.random.default_rng(2026)
+    states = _mul_after_shift_states(rng, 512)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = random_cands(rng, len(states), 256, 3, interesting_frac=0.3)
+    small = rng.random((len(states), 256)) < 0.4   # shift amounts < 256 as well as >= 256
+    cands[small, 1, 1:] = 0
+    cands[small, 1, 0] &= 0xFF
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    bad = np.nonzero(first != ref)[0]
+    assert bad.size == 0, f"{bad.size} states differ, e.g. {bad[:5]}"
+    assert (ref > 0).sum() > 100   # witnesses past candidate 0: earlier products were read
+
+
 def test_band4n_then_hbm_variables_vs_oracle(mgp_ctx):
     """Compares on variables 6.. (HBM loads, not the register bank) after folded BAND4N
     chains, against the C oracle on every candidate (both engines)."""

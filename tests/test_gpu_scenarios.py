@@ -22,7 +22,7 @@ reading") and check what the GPU-first front end answers and how many fallback
 import pytest
 
 from mythril_amd import dag as D
-from mythril_amd.keccak import KeccakFunctionManager
+from corpus.keccak_manager import KeccakFunctionManager
 from mythril_amd import solver as SV
 from mythril_amd.smt import (And, Array, BVMulNoOverflow, BVSubNoUnderflow, Concat, Extract, If, Not, UGE, UGT,
                              ULE, ULT, symbol_factory)

@@ -13,7 +13,8 @@ import pytest
 
 from mythril_amd import dag as D
 from mythril_amd import solver as SV
-from mythril_amd.keccak import KeccakFunctionManager, get_code_hash, get_code_hashes, keccak256_batch
+from corpus.keccak_manager import KeccakFunctionManager
+from mythril_amd.keccak import get_code_hash, get_code_hashes, keccak256_batch
 from mythril_amd.smt import And, Not, symbol_factory
 from oracle import bvsem as S
 from oracle.keccak_ref import keccak256 as keccak_py

@@ -6,6 +6,7 @@ the hasher (the product default is the GPU kernel); the GPU test runs the kernel
 """
 import pytest
 
+from corpus.keccak_manager import KeccakFunctionManager
 from mythril_amd import keccak as K
 from mythril_amd.smt import Concat, symbol_factory
 from oracle import keccak_ref
@@ -55,7 +56,7 @@ def reference_replace(concrete_transactions, model, manager, code=None):
 
 
 def _setup():
-    m = K.KeccakFunctionManager()
+    m = KeccakFunctionManager()
     key, other = BVS("key", 256), BVS("other", 256)
     h1, _ = m.create_keccak(Concat(key, BVV(0, 256)))
     h2, _ = m.create_keccak(Concat(other, BVV(1, 256)))

@@ -471,7 +471,7 @@ def test_c_oracle_contract_states_match_python_oracle():
     import corpus
     from mythril_amd import dag as D
     from mythril_amd import front as F
-    from mythril_amd.keccak import KeccakFunctionManager
+    from corpus.keccak_manager import KeccakFunctionManager
     from oracle import coracle
 
     kfm = KeccakFunctionManager()

@@ -113,7 +113,7 @@ def test_wide_mapping_preimage_state_lowers_and_candidates_satisfy():
     the 512-bit preimage and inverse lower to narrow pieces, and the candidates (hints plus
     domain-guided rows) include a model (checked with the CPU uop interpreter, no GPU)."""
     from mythril_amd import _native as N
-    from mythril_amd.keccak import KeccakFunctionManager
+    from corpus.keccak_manager import KeccakFunctionManager
     from mythril_amd.smt import Concat, ULT, symbol_factory
     from oracle import bvsem as S
     from oracle import uop_ref as UR

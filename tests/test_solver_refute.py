@@ -174,7 +174,7 @@ def test_decision_rows_per_state_rule():
 
     import corpus
     from mythril_amd.front import Batch
-    from mythril_amd.keccak import KeccakFunctionManager
+    from corpus.keccak_manager import KeccakFunctionManager
 
     kfm = KeccakFunctionManager()
     states = [list(t) for _, t, _ in corpus.wallet_states(0, kfm)[:4]]

@@ -540,6 +540,19 @@ def main():
         pf.core_async = False
         frontend["core_async"] = {"seconds": dta, "states_per_s": len(cs) / dta,
                                   "same_answers": [r[0] for r in res_a] == kinds}
+        # A/B: the candidate-memory cap of one witness round (batches past it run as
+        # sub-batches one after another), the default against 4x it
+        keep_cb = pf.cand_bytes
+        for tag, cb in (("cand_cap_x4", 4 * keep_cb), ("cand_cap_default", keep_cb)):
+            SV.unsat_cores().reset()
+            pf._N.program_cache_clear()
+            pf.cand_bytes = cb
+            tf = time.perf_counter()
+            res_c = pf.check_states(cs)
+            dtc = time.perf_counter() - tf
+            frontend[tag] = {"cand_bytes": cb, "seconds": dtc, "states_per_s": len(cs) / dtc,
+                             "same_answers": [r[0] for r in res_c] == kinds, "stages_ms": pf.last_profile}
+        pf.cand_bytes = keep_cb
         pf.ctx.close()
         log(f"frontend: {frontend}")
 

@@ -11,8 +11,9 @@ struct mgp_dec_state {
   // propagation graph and the decision slots
   uint64_t nd, orig, consts, av, bs, isb, vtie, vars, pairs, cmp_pair, cmp_dom, cmp_t, pair_keys, pair_idx, ufs;
   uint64_t uoff, ulist, voff, vlist, tie_rel, slot, width, node, eqh_off, eqh, cong, arel, og, odis, oatom, otgt, inj;
+  uint64_t tien, ufp;
   uint64_t n_consts;
-  uint32_t n, n_vt, n_pairs, n_ufs, n_slot, ucap, wcap, n_cong, n_arel, n_og, n_inj, pad;
+  uint32_t n, n_vt, n_pairs, n_ufs, n_slot, ucap, wcap, n_cong, n_arel, n_og, n_inj, n_cmpn, n_borp, n_ufp;
   // workspace of one task of this state: private node values, variable values, pair
   // orderings, truth sets, undo log, work list
   uint64_t ws_av, ws_vars, ws_pairs, ws_bs, ws_undo, ws_work, ws_bytes;

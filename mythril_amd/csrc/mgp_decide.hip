@@ -98,6 +98,11 @@ __global__ __launch_bounds__(64) void mgp_decide_kernel(const uint8_t *__restric
   d.pair_idx = at<int32_t>(blob, S.pair_idx);
   d.ufs = at<UfApp>(blob, S.ufs);
   d.n_ufs = S.n_ufs;
+  d.tien = at<int32_t>(blob, S.tien);
+  d.n_cmpn = S.n_cmpn;
+  d.n_borp = S.n_borp;
+  d.ufp = at<uint32_t>(blob, S.ufp);
+  d.n_ufp = S.n_ufp;
   d.cong = at<int32_t>(blob, S.cong);
   d.n_cong = S.n_cong;
   d.arel = at<ArithRel>(blob, S.arel);

@@ -95,6 +95,15 @@ MGP_RD AV exact(V v, uint32_t w) {
   return a;
 }
 MGP_RD bool is_exact(const AV &a) { return EQV(a.lo, a.hi); }
+// no bit known and the full interval: a backward transfer from it narrows nothing
+MGP_RD bool is_top(const AV &a, uint32_t w) {
+  const uint32_t li = w ? (w - 1u) >> 5 : 0u;
+  for (uint32_t i = 0; i <= li && i < 8; ++i) {
+    const uint32_t m = bv_limb_mask(w, (int)i);
+    if ((a.z.w[i] & m) || (a.o.w[i] & m) || a.lo.w[i] || a.hi.w[i] != m) return false;
+  }
+  return true;
+}
 
 // Re-establish the invariants (bits above w known zero, interval within the
 // bits' range, common high prefix of lo/hi as known bits).  false = empty.
@@ -371,6 +380,14 @@ struct Dom {
   // read in tx 2 against the write in tx 1 when both senders are equal)
   const UfApp *ufs = nullptr;
   uint32_t n_ufs = 0;
+  // what tie() visits, fixed per state (mgp_refute.cpp build_atoms): the compare nodes with
+  // a pair, then the BOR nodes whose operands are compares of one pair (tien, n_cmpn +
+  // n_borp entries), and the pairs (i, j) of ufs entries of one function whose arguments
+  // can be equal (ufp, 2 * n_ufp entries: two constants that differ never are)
+  const int32_t *tien = nullptr;
+  uint32_t n_cmpn = 0, n_borp = 0;
+  const uint32_t *ufp = nullptr;
+  uint32_t n_ufp = 0;
   // Structural congruence (round 4): pairs whose two operand nodes apply the same
   // operator with the same parameters (on the original DAG).  Once arg_equal proves their
   // operands equal -- a pair known equal, equal exact values, recursively -- the pair is
@@ -721,9 +738,9 @@ struct Dom {
     if (n_inj && !injective()) return false;
     if (n_pairs == 0 && n_ufs == 0 && n_arel == 0) return true;
     for (int sweep = 0; sweep < 2; ++sweep)
-      for (uint32_t i = 0; i < n; ++i) {
+      for (uint32_t q = 0; q < n_cmpn; ++q) {
+        const uint32_t i = (uint32_t)tien[q];
         const int32_t pi = cmp_pair[i];
-        if (pi < 0) continue;
         Pair &p = pairs[pi];
         const uint8_t t = cmp_t[i], f = (uint8_t)(OALL & ~t);
         if (bs[i] == BT && !set_order(p, cmp_dom[i], t)) return false;
@@ -733,11 +750,11 @@ struct Dom {
       }
     // a true Or of two compares on one operand pair (the Or(ULT, ==) expansion of ULE /
     // UGE, bitvec_helper.py:53-80) allows only the union of their orderings
-    for (uint32_t i = 0; i < n; ++i) {
-      if (nd[i].op != MGP_OP_BOR || bs[i] != BT) continue;
+    for (uint32_t q = n_cmpn; q < n_cmpn + n_borp; ++q) {
+      const int32_t i = tien[q];
+      if (bs[i] != BT) continue;
       const int32_t a = nd[i].a, b = nd[i].b;
-      const int32_t pa = cmp_pair[a], pb = cmp_pair[b];
-      if (pa < 0 || pa != pb) continue;
+      const int32_t pa = cmp_pair[a];
       const uint8_t da = cmp_dom[a], db = cmp_dom[b];
       if (da != db && da != 2 && db != 2) continue;  // signed with unsigned: no common set
       const uint8_t dom = da == 2 ? db : da;
@@ -775,15 +792,15 @@ struct Dom {
       }
       if (!meet(lo_n, a) || !meet(hi_n, b)) return false;
     }
-    for (uint32_t i = 0; i < n_ufs; ++i)
-      for (uint32_t j = i + 1; j < n_ufs && ufs[j].fn == ufs[i].fn && ufs[j].op == ufs[i].op; ++j) {
-        if (!arg_equal(ufs[i].arg, ufs[j].arg, 3)) continue;
-        const int32_t x = ufs[i].node, y = ufs[j].node;
-        const AV ax = av[x], ay = av[y];
-        if (!meet(x, ay) || !meet(y, ax)) return false;
-        const int32_t pi = pair_find(((uint64_t)(uint32_t)(x < y ? x : y) << 32) | (uint32_t)(x < y ? y : x));
-        if (pi >= 0 && !set_order(pairs[pi], 2, OEQ)) return false;
-      }
+    for (uint32_t q = 0; q < n_ufp; ++q) {
+      const uint32_t i = ufp[2 * q], j = ufp[2 * q + 1];
+      if (!arg_equal(ufs[i].arg, ufs[j].arg, 3)) continue;
+      const int32_t x = ufs[i].node, y = ufs[j].node;
+      const AV ax = av[x], ay = av[y];
+      if (!meet(x, ay) || !meet(y, ax)) return false;
+      const int32_t pi = pair_find(((uint64_t)(uint32_t)(x < y ? x : y) << 32) | (uint32_t)(x < y ? y : x));
+      if (pi >= 0 && !set_order(pairs[pi], 2, OEQ)) return false;
+    }
     return true;
   }
 
@@ -989,7 +1006,8 @@ struct Dom {
 
   // -------------------------------------------------------------- backward
   MGP_RD bool narrow_ult(int32_t a, int32_t b, bool strict) {  // require a < b (strict) or a <= b
-    const AV A = av[a], B = av[b];
+    const AV &A = av[a], &B = av[b];
+    if (strict ? LT(A.hi, B.lo) : !LT(B.lo, A.hi)) return true;  // holds already: nothing narrows
     AV ta = top(W(a)), tb = top(W(b));
     if (strict) {
       if (Z(B.hi) || EQV(A.lo, M(W(a)))) return false;
@@ -1005,6 +1023,7 @@ struct Dom {
   MGP_RD bool narrow_slt(int32_t a, int32_t b, bool strict) {
     const uint32_t w = W(a);
     AV fa = flip(av[a], w), fb = flip(av[b], w);
+    if (strict ? LT(fa.hi, fb.lo) : !LT(fb.lo, fa.hi)) return true;  // holds already
     if (strict) {
       if (Z(fb.hi) || EQV(fa.lo, M(w))) return false;
       fa.hi = MIN(fa.hi, SUBV(fb.hi, ONE()));
@@ -1155,10 +1174,12 @@ struct Dom {
       }
       case MGP_OP_ADD: {
         const AV A = av[x.a], B = av[x.b];
+        if ((is_exact(A) && is_exact(B)) || is_top(R, w)) return true;  // nothing to narrow
         return meet(x.a, av_sub(R, B, w)) && meet(x.b, av_sub(R, A, w));
       }
       case MGP_OP_SUB: {
         const AV A = av[x.a], B = av[x.b];
+        if ((is_exact(A) && is_exact(B)) || is_top(R, w)) return true;
         return meet(x.a, av_add(R, B, w)) && meet(x.b, av_sub(A, R, w));
       }
       case MGP_OP_XOR: {
@@ -1260,6 +1281,7 @@ struct Dom {
       }
       case MGP_OP_CONCAT: {
         const uint32_t wa = W(x.a), wb = W(x.b);
+        if ((is_exact(av[x.a]) && is_exact(av[x.b])) || is_top(R, w)) return true;
         AV ta = top(wa), tb = top(wb);
         ta.z = OR(ta.z, SHR(AND(R.z, M(w)), wb));
         ta.o = SHR(R.o, wb);
@@ -1337,8 +1359,13 @@ struct Dom {
         need_tie |= tie_rel[t] != 0;
         if ((work += 2u * (uoff[t + 1] - uoff[t]) + 1u) > budget) return 0;
         if (!backward(t)) return 1;
-        for (uint32_t k = uoff[t]; k < uoff[t + 1]; ++k)
-          if (!forward(ulist[k]) || !backward(ulist[k])) return 1;
+        // a user whose value the forward step changed is on the work list now, and its
+        // backward step runs when it is reached: only the unchanged ones need it here
+        for (uint32_t k = uoff[t]; k < uoff[t + 1]; ++k) {
+          const size_t before = T.size();
+          if (!forward(ulist[k])) return 1;
+          if (T.size() == before && !backward(ulist[k])) return 1;
+        }
       }
       const size_t before = T.size();
       if (!meetb((int32_t)n - 1, BT)) return 1;
@@ -1491,10 +1518,11 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
       }
     }
   }
-  // Fresh values of one function's applications are drawn pairwise distinct (round 4).
-  // keccak is injective on the formula's models (inv(f(x)) == x,
+  // Fresh values of one injective function's applications are drawn pairwise distinct
+  // (round 4). keccak is injective on the formula's models (inv(f(x)) == x,
   // keccak_function_manager.py:118-146), so two applications with different arguments need
-  // different values; the lo / hi schedules used to give every application of a keccak
+  // different values (other functions -- calldata bytes, balances -- are not injective and
+  // draw freely: two calldata bytes are often both 0); the lo / hi schedules used to give every application of a keccak
   // interval the same bound, and the inverse then read the first application's argument
   // (WalletLibrary's m_ownerIndex[owner] next to m_ownerIndex[sender]).  Applications with
   // equal arguments lose nothing: the evaluation gives a later one the earlier one's value.
@@ -1514,8 +1542,10 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
     // (on the original DAG: an application with a wide argument is a fresh variable in the
     // relaxed one the domain runs on)
     const mgp_node &on = (d.orig ? d.orig : d.nd)[nk];
-    const bool ufapp = on.op == MGP_OP_UFAPP;
     const uint32_t fn = on.p0;
+    bool ufapp = false;  // an application of a function with an asserted inverse
+    if (on.op == MGP_OP_UFAPP)
+      for (uint32_t j = 0; j < d.n_inj && !ufapp; ++j) ufapp = d.inj[j].fn == fn;
     if (EQV(d.av[nk].lo, d.av[nk].hi)) {  // already one value: nothing to decide
       put(P.slot[k], d.av[nk].lo);
       if (ufapp && n_seen < kSeenUf) {

@@ -64,6 +64,9 @@ struct State {
   std::vector<uint8_t> cmp_dom;   // 0 unsigned, 1 signed, 2 both (EQ)
   std::vector<uint8_t> cmp_t;     // orderings (x vs y) under which the node is true
   std::vector<UfApp> ufs;
+  std::vector<int32_t> tien;  // compare nodes with a pair, then BORs of one pair (Dom::tien)
+  uint32_t n_cmpn = 0, n_borp = 0;
+  std::vector<uint32_t> ufp;  // ufs index pairs whose arguments can be equal (Dom::ufp)
   std::vector<int32_t> cong;  // pairs of structurally matching operand nodes (Dom::cong)
   std::vector<ArithRel> arel;  // ADD / SUB nodes whose wrap status orders a compare pair (Dom::arel)
   std::vector<InjApp> inj;     // applications with an asserted inverse (Dom::injective)
@@ -99,6 +102,11 @@ struct State {
     d.pair_idx = pair_idx.data();
     d.ufs = ufs.data();
     d.n_ufs = (uint32_t)ufs.size();
+    d.tien = tien.data();
+    d.n_cmpn = n_cmpn;
+    d.n_borp = n_borp;
+    d.ufp = ufp.data();
+    d.n_ufp = (uint32_t)(ufp.size() / 2);
     d.cong = cong.data();
     d.n_cong = (uint32_t)cong.size();
     d.arel = arel.data();
@@ -241,6 +249,33 @@ struct State {
       i = j;
     }
     ufs.swap(keep);
+    tien.clear();
+    for (uint32_t i = 0; i < n; ++i)
+      if (cmp_pair[i] >= 0) tien.push_back((int32_t)i);
+    n_cmpn = (uint32_t)tien.size();
+    for (uint32_t i = 0; i < n; ++i) {
+      if (nd[i].op != MGP_OP_BOR || nd[i].a < 0 || nd[i].b < 0) continue;
+      const int32_t pa = cmp_pair[nd[i].a];
+      if (pa >= 0 && pa == cmp_pair[nd[i].b]) tien.push_back((int32_t)i);
+    }
+    n_borp = (uint32_t)tien.size() - n_cmpn;
+    // UF application pairs tie() compares: one function and operator; arguments that are
+    // two different constants never become equal (calldata bytes at fixed offsets)
+    ufp.clear();
+    auto const_arg = [&](int32_t a, const uint32_t *&c) {
+      if (a < 0 || o[a].op != MGP_OP_CONST || o[a].width > MGP_MAX_WIDTH) return false;
+      c = consts + 8u * (size_t)o[a].p0;
+      return true;
+    };
+    for (uint32_t i = 0; i < ufs.size(); ++i)
+      for (uint32_t j = i + 1; j < ufs.size() && ufs[j].fn == ufs[i].fn && ufs[j].op == ufs[i].op; ++j) {
+        const uint32_t *ci, *cj;
+        if (const_arg(ufs[i].arg, ci) && const_arg(ufs[j].arg, cj) && o[ufs[i].arg].width == o[ufs[j].arg].width &&
+            memcmp(ci, cj, 32) != 0)
+          continue;
+        ufp.push_back(i);
+        ufp.push_back(j);
+      }
     // structural congruence candidates: both operands of the pair apply one operator with
     // the same parameters and width (leaves excluded: one variable is one node's value
     // already, two constants are compared exactly)
@@ -984,6 +1019,11 @@ extern "C" int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes,
     h.pair_keys = B.put(S.pair_keys);
     h.pair_idx = B.put(S.pair_idx);
     h.ufs = B.put(S.ufs);
+    h.tien = B.put(S.tien);
+    h.ufp = B.put(S.ufp);
+    h.n_cmpn = S.n_cmpn;
+    h.n_borp = S.n_borp;
+    h.n_ufp = (uint32_t)(S.ufp.size() / 2);
     h.uoff = B.put(S.uoff);
     h.ulist = B.put(S.ulist);
     h.voff = B.put(S.voff);

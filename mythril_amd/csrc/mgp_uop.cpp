@@ -248,6 +248,56 @@ inline bool v1_live_after(const uint32_t *ins, uint32_t n, uint32_t from, uint32
   return false;
 }
 
+// Per Bool bit, the positions of the v1 instructions that read it and that write it
+// (ascending): v1_live_after and the writer / reader queries of the BAND4N fold as binary
+// searches instead of scans (WalletLibrary's programs run to 12 k instructions).
+struct BitIndex {
+  std::vector<std::vector<uint32_t>> rd, wr;
+  void build(const uint32_t *ins, uint32_t n) {
+    // Bool bits are 8-bit destinations; a read field past 255 names no Bool
+    rd.assign(256, {});
+    wr.assign(256, {});
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint32_t *I = ins + (size_t)k * MGP_INS_WORDS;
+      const uint32_t cand[3] = {I[1] & 0xFFFFu, I[1] >> 16, I[2] & 0xFFFFu};
+      for (int c = 0; c < 3; ++c) {
+        const uint32_t b = cand[c];
+        if (b < 256u && (c == 0 || cand[0] != b) && (c < 2 || cand[1] != b) && v1_reads_bool(I, b)) rd[b].push_back(k);
+      }
+      const uint32_t d = (I[0] >> 16) & 0xFFu;
+      if (v1_writes_bool(I, d)) wr[d].push_back(k);
+    }
+  }
+  static uint32_t first_at_or_after(const std::vector<uint32_t> &v, uint32_t k) {
+    const auto it = std::lower_bound(v.begin(), v.end(), k);
+    return it == v.end() ? 0xFFFFFFFFu : *it;
+  }
+  // v1_live_after: read at or after `from` before a (static) write; a read and a write in one
+  // instruction count as a read
+  bool live_after(uint32_t from, uint32_t bit) const {
+    if (bit == MGP_BOOL_TRUE || bit == MGP_BOOL_FALSE) return true;
+    if (bit >= rd.size()) return false;
+    const uint32_t r = first_at_or_after(rd[bit], from);
+    return r != 0xFFFFFFFFu && r <= first_at_or_after(wr[bit], from);
+  }
+  // instructions in [a, b) reading bit
+  uint32_t reads_in(uint32_t bit, uint32_t a, uint32_t b) const {
+    if (bit >= rd.size() || a >= b) return 0;
+    return (uint32_t)(std::lower_bound(rd[bit].begin(), rd[bit].end(), b) - std::lower_bound(rd[bit].begin(), rd[bit].end(), a));
+  }
+  // the last static writer of bit before q (-1: none)
+  int64_t last_write_before(uint32_t bit, uint32_t q) const {
+    if (bit >= wr.size()) return -1;
+    const auto it = std::lower_bound(wr[bit].begin(), wr[bit].end(), q);
+    return it == wr[bit].begin() ? -1 : (int64_t)*(it - 1);
+  }
+  bool writes_in(uint32_t bit, uint32_t a, uint32_t b) const {
+    if (bit >= wr.size() || a >= b) return false;
+    const uint32_t w = first_at_or_after(wr[bit], a);
+    return w != 0xFFFFFFFFu && w < b;
+  }
+};
+
 struct BoolPlan {
   std::vector<uint8_t> dead;                  // instruction folded into a neighbour
   std::vector<uint8_t> inv;                   // compare: toggle INVERT
@@ -268,12 +318,14 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
   P.andn.assign(n, 0);
   P.merged.assign(n, 0);
   P.neg.assign(n, 0);
+  BitIndex X;
+  X.build(ins, n);
   for (uint32_t pc = 0; pc + 1 < n; ++pc) {
     const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS, *J = I + MGP_INS_WORDS;
     const uint32_t op = v1_op(I), d = (I[0] >> 16) & 0xFFu;
     if (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF && v1_op(J) == MGP_OP_BNOT && (J[1] & 0xFFFFu) == d) {
       const uint32_t e = (J[0] >> 16) & 0xFFu;
-      if (e == d || !v1_live_after(ins, n, pc + 2, d)) {
+      if (e == d || !X.live_after(pc + 2, d)) {
         P.inv[pc] = 1;
         P.dst[pc] = e;
         P.dead[pc + 1] = 1;
@@ -291,7 +343,7 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
     const uint32_t t = (I[0] >> 16) & 0xFFu, ja = J[1] & 0xFFFFu, jb = J[1] >> 16;
     if ((ja == t) == (jb == t)) continue;  // J must read t exactly once
     const bool j_redefines_t = ((J[0] >> 16) & 0xFFu) == t;
-    if (P.andops[pc].size() + 1 > 4 || (!j_redefines_t && v1_live_after(ins, n, pc + 2, t))) continue;
+    if (P.andops[pc].size() + 1 > 4 || (!j_redefines_t && X.live_after(pc + 2, t))) continue;
     std::vector<uint32_t> ops = P.andops[pc];
     ops.push_back(ja == t ? jb : ja);
     P.andops[pc + 1] = ops;
@@ -315,7 +367,7 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
     if ((ja == t) == (jb == t)) return 0xFFFFFFFFu;
     if (t == MGP_BOOL_TRUE || t == MGP_BOOL_FALSE) return 0xFFFFFFFFu;
     const bool redefines = ((J[0] >> 16) & 0xFFu) == t;
-    if (!redefines && v1_live_after(ins, n, q + 1, t)) return 0xFFFFFFFFu;
+    if (!redefines && X.live_after(q + 1, t)) return 0xFFFFFFFFu;
     return ja == t ? jb : ja;
   };
   // a compare whose result only feeds the next BAND / BOR: the compare combines it (BCOMB)
@@ -350,8 +402,32 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
   // stream with folded instructions included, so every reader counts: x (the BNOT's result)
   // is read exactly once before q, inside the chain, and is not live after q; s (its
   // source) is not written between the BNOT and q.
-  auto writes = [&](uint32_t r, uint32_t bit) {
-    return v1_writes_bool(ins + (size_t)r * MGP_INS_WORDS, bit) || (!P.dead[r] && P.dst[r] == bit);
+  // destination overrides of the earlier folds (compare -> BNOT, BCOMB), per bit: with the
+  // static writers they are every instruction that writes a bit
+  std::vector<std::vector<uint32_t>> dpos(X.wr.size());
+  for (uint32_t r = 0; r < n; ++r)
+    if (P.dst[r] != 0xFFFFFFFFu) {
+      if (P.dst[r] >= dpos.size()) dpos.resize(P.dst[r] + 1);
+      dpos[P.dst[r]].push_back(r);
+    }
+  auto last_writer = [&](uint32_t bit, uint32_t q) -> int64_t {  // the last r < q writing bit
+    int64_t p = X.last_write_before(bit, q);
+    if (bit < dpos.size()) {
+      const auto &v = dpos[bit];
+      for (auto it = std::lower_bound(v.begin(), v.end(), q); it != v.begin();) {
+        --it;
+        if ((int64_t)*it <= p) break;
+        if (!P.dead[*it]) { p = *it; break; }
+      }
+    }
+    return p;
+  };
+  auto written_in = [&](uint32_t bit, uint32_t a, uint32_t b) {  // some r in [a, b) writes bit
+    if (X.writes_in(bit, a, b)) return true;
+    if (bit >= dpos.size()) return false;
+    for (auto it = std::lower_bound(dpos[bit].begin(), dpos[bit].end(), a); it != dpos[bit].end() && *it < b; ++it)
+      if (!P.dead[*it]) return true;
+    return false;
   };
   for (uint32_t q = 0; q < n; ++q) {
     if (P.dead[q] || v1_op(ins + (size_t)q * MGP_INS_WORDS) != MGP_OP_BAND || P.andn[q]) continue;
@@ -361,24 +437,16 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
     for (size_t j = 0; j < ops.size(); ++j) {
       const uint32_t x = ops[j];
       if (x == MGP_BOOL_TRUE || x == MGP_BOOL_FALSE || std::count(ops.begin(), ops.end(), x) != 1) continue;
-      int64_t p = -1;
-      for (int64_t r = (int64_t)q - 1; r >= 0; --r)
-        if (writes((uint32_t)r, x)) { p = r; break; }
+      const int64_t p = last_writer(x, q);
       if (p < 0 || (uint32_t)p >= lo || P.dead[p]) continue;
       const uint32_t *B = ins + (size_t)p * MGP_INS_WORDS;
       const uint32_t sx = B[1] & 0xFFFFu;
       if (v1_op(B) != MGP_OP_BNOT || P.dst[p] != 0xFFFFFFFFu) continue;  // in place (sx == x) too
-      uint32_t reads = 0, reads_in_chain = 0;
-      bool s_written = false;
-      for (uint32_t r = (uint32_t)p + 1; r <= q; ++r) {
-        if (v1_reads_bool(ins + (size_t)r * MGP_INS_WORDS, x)) {
-          ++reads;
-          reads_in_chain += r >= lo;
-        }
-        s_written |= writes(r, sx) && r < q;
-      }
+      const uint32_t reads = X.reads_in(x, (uint32_t)p + 1, q + 1);
+      const uint32_t reads_in_chain = X.reads_in(x, std::max((uint32_t)p + 1, lo), q + 1);
+      const bool s_written = written_in(sx, (uint32_t)p + 1, q);
       const bool q_redefines = v1_writes_bool(ins + (size_t)q * MGP_INS_WORDS, x);
-      if (reads != 1 || reads_in_chain != 1 || s_written || (!q_redefines && v1_live_after(ins, n, q + 1, x)))
+      if (reads != 1 || reads_in_chain != 1 || s_written || (!q_redefines && X.live_after(q + 1, x)))
         continue;
       ops[j] = sx;
       P.neg[q] |= (uint8_t)(1u << j);

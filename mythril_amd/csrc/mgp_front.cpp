@@ -177,6 +177,13 @@ inline uint64_t slot_key(uint32_t name, uint8_t kind, uint32_t aux, uint32_t j) 
               : ((uint64_t)(name & 0x7FFFFFFFu) << 32) | (j & 0xFFFFFFFFu);
 }
 
+inline uint64_t uf_slot_key(uint32_t name, uint32_t tid, uint32_t j) {
+  uint64_t z = ((uint64_t)name << 40) ^ ((uint64_t)tid << 8) ^ j ^ 0x5546A7E1ull;  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (1ull << 63) | ((z ^ (z >> 31)) >> 1);
+}
+
 template <typename IsPadded>
 void strengthen_padded(StateOut &S, IsPadded is_padded_eq);
 void pin_constants(StateOut &S);
@@ -197,7 +204,11 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
       S.var_name.push_back(name);
       S.var_aux.push_back(kind == 0 ? j : aux);
       S.var_kind.push_back(kind);
-      S.var_key.push_back(slot_key(name, kind, aux, j));
+      // a UF application's slot is keyed by its term (the arena hash-conses terms, so a
+      // child's constraint list names its parent's applications by the same ids): keying it
+      // by DAG position matched a parent's keccak256_512(sender, slot) value to the child's
+      // keccak256_512(to, slot) whenever the child's DAG ordered its applications differently
+      S.var_key.push_back(kind == 1 && tid >= 0 ? uf_slot_key(name, (uint32_t)tid, j) : slot_key(name, kind, aux, j));
     }
     return first;
   };

@@ -152,7 +152,7 @@ typedef struct mgp_node {
  * MGP_PROG_VARS includes).  Slot numbers of a spilling program are ordered by access
  * count, so the most used values stay in LDS. */
 #define MGP_LDS_SLOTS 32u
-#define MGP_MAX_SLOTS 255u
+#define MGP_MAX_SLOTS 4095u  /* BV destination: 8 bits in word 0 (bits 16..23), the high bits in word 3 */
 #define MGP_SPILL_BASE(max_var) ((max_var) > 8u ? (max_var) : 8u)
 #define MGP_PROG_VARS(h)                                                                        \
   ((h)[2] >= MGP_LDS_SLOTS ? MGP_SPILL_BASE((h)[3] >> 8) + (h)[2] - MGP_LDS_SLOTS + 1u : ((h)[3] >> 8))

@@ -259,15 +259,16 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
   // software-pipelined instruction fetch: the scalar loads of instruction
   // pc+1 are in flight while instruction pc executes (mgp_lower pads every
   // program with one zero instruction after RET)
-  uint32_t n0 = uni(ins[0]), n1 = uni(ins[1]), n2 = uni(ins[2]);
+  uint32_t n0 = uni(ins[0]), n1 = uni(ins[1]), n2 = uni(ins[2]), n3 = uni(ins[3]);
   for (uint32_t pc = 0; pc < n_ins; ++pc) {
-    const uint32_t w0 = n0, w1 = n1, w2 = n2;
+    const uint32_t w0 = n0, w1 = n1, w2 = n2, w3 = n3;
     n0 = uni(ins[pc * 4u + 4u]);
     n1 = uni(ins[pc * 4u + 5u]);
     n2 = uni(ins[pc * 4u + 6u]);
+    n3 = uni(ins[pc * 4u + 7u]);
     const uint32_t op = w0 & 0xFFu;
     const uint32_t width = ((w0 >> 8) & 0xFFu) + 1u;
-    const uint32_t dst = (w0 >> 16) & 0xFFu;
+    const uint32_t dst = ((w0 >> 16) & 0xFFu) | ((w3 & 0xFFu) << 8);  // BV slots past 255: high bits in w3
     const uint32_t flags = w0 >> 24;
     const uint32_t oa = w1 & 0xFFFFu, ob = w1 >> 16, oc = w2 & 0xFFFFu, imm = w2 >> 16;
 

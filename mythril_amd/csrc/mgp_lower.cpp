@@ -552,7 +552,7 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
     out.push_back((uint32_t)I.op | (width_field << 8) | (dst << 16) | (flags << 24));
     out.push_back((oa & 0xFFFFu) | (ob << 16));
     out.push_back((oc & 0xFFFFu) | ((I.imm & 0xFFFFu) << 16));
-    out.push_back(0u);
+    out.push_back(dst >> 8);  // a BV destination past slot 255 (WalletLibrary's input-order programs)
     ++n_emit;
   }
   // RET
@@ -567,7 +567,8 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
   static const bool norenum_dbg = getenv("MGP_LOWER_NORENUM") != nullptr;
   if (slots_used > MGP_LDS_SLOTS && slot_cap == MGP_LDS_SLOTS && !norenum_dbg) {
     auto field = [&](const std::pair<uint32_t, uint32_t> &f) -> uint32_t {
-      return f.first % 4u == 0u ? (out[f.first] >> 16) & 0xFFu : (out[f.first] >> f.second) & 0x3FFFu;
+      return f.first % 4u == 0u ? ((out[f.first] >> 16) & 0xFFu) | ((out[f.first + 3] & 0xFFu) << 8)
+                                : (out[f.first] >> f.second) & 0x3FFFu;
     };
     std::vector<uint32_t> cnt(slots_used, 0), by(slots_used), rank(slots_used);
     for (const auto &f : slot_fields) cnt[field(f)]++;
@@ -576,8 +577,10 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
     for (uint32_t r = 0; r < slots_used; ++r) rank[by[r]] = r;
     for (const auto &f : slot_fields) {
       const uint32_t nw = rank[field(f)];
-      if (f.first % 4u == 0u) out[f.first] = (out[f.first] & ~(0xFFu << 16)) | (nw << 16);
-      else out[f.first] = (out[f.first] & ~(0x3FFFu << f.second)) | (nw << f.second);
+      if (f.first % 4u == 0u) {
+        out[f.first] = (out[f.first] & ~(0xFFu << 16)) | ((nw & 0xFFu) << 16);
+        out[f.first + 3] = nw >> 8;
+      } else out[f.first] = (out[f.first] & ~(0x3FFFu << f.second)) | (nw << f.second);
     }
   }
 

@@ -489,7 +489,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       if (BP.dead[pc]) continue;
       const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS;
       const uint32_t op = I[0] & 0xFFu, width = ((I[0] >> 8) & 0xFFu) + 1u;
-      const uint32_t dst = BP.dst[pc] != 0xFFFFFFFFu ? BP.dst[pc] : (I[0] >> 16) & 0xFFu;
+      const uint32_t dst = BP.dst[pc] != 0xFFFFFFFFu ? BP.dst[pc] : ((I[0] >> 16) & 0xFFu) | ((I[3] & 0xFFu) << 8);
       const bool store = ((I[0] >> 24) & MGP_INS_STORE) != 0;
       const uint32_t oa = I[1] & 0xFFFFu, ob = I[1] >> 16, oc = I[2] & 0xFFFFu, imm = I[2] >> 16;
       const bool narrow = width < 256u;

@@ -57,10 +57,10 @@ def run_program(words: Sequence[int], off: int, xs: Sequence[int]):
         return bool((bools >> o) & 1)
 
     for pc in range(n_ins):
-        w0, w1, w2 = (int(words[ins0 + 4 * pc + k]) for k in range(3))
+        w0, w1, w2, w3 = (int(words[ins0 + 4 * pc + k]) for k in range(4))
         op = w0 & 0xFF
         width = ((w0 >> 8) & 0xFF) + 1
-        dst = (w0 >> 16) & 0xFF
+        dst = ((w0 >> 16) & 0xFF) | ((w3 & 0xFF) << 8)   # BV slots past 255: high bits in w3
         store = (w0 >> 24) & 1
         oa, ob, oc, imm = w1 & 0xFFFF, w1 >> 16, w2 & 0xFFFF, w2 >> 16
         if op == OP_RET:

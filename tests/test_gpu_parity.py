@@ -706,13 +706,14 @@ def test_back_to_back_batches_same_context(mgp_ctx):
 
 def test_spilled_values_and_demoted_bools(mgp_ctx):
     """Programs past the LDS slots (BV values spilled to candidate rows past the state's
-    variables), past the 17 Bool registers (demoted Bools) and past 64 constants, in one
+    variables, past slot 255 too), past the 17 Bool registers (demoted Bools) and past 64 constants, in one
     batch with ordinary states: the C ABI pads the candidate rows, both engines agree
     with the oracle, and the witness rows of the variables come back unchanged."""
     from .test_lowering import _bool_fan, _live_chain
 
     rng = np.random.default_rng(77)
-    states = [(_live_chain(n), []) for n in (36, 90, 200)] + [_bool_fan(n) for n in (24, 60)]
+    # 300 live values: destinations past slot 255 (high bits in instruction word 3)
+    states = [(_live_chain(n), []) for n in (36, 90, 200, 300)] + [_bool_fan(n) for n in (24, 60)]
     nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]
     pool = [(k * 0x9E3779B97F4A7C15 + 1) % 2 ** 256 for k in range(150)]
     acc = 0

@@ -190,16 +190,18 @@ def test_many_live_values_spill_to_candidate_rows():
     (include/mgp_ir.h): a 4-slot cap, 40 and 200 live values all lower and agree with the
     DAG in both encodings (the reference interpreters assert that no spill row is a
     variable the program reads, and that every row is written before it is read);
-    past MGP_MAX_SLOTS the state is unsupported, never wrong."""
+    300 live values need destinations past slot 255 (high bits in instruction word 3,
+    round 4: WalletLibrary's input-order programs need up to 326); past MGP_MAX_SLOTS the
+    state is unsupported, never wrong."""
     rows = [[3, 5], [INTERESTING[3], INTERESTING[4]], [0, 2 ** 256 - 1]]
-    for n, cap in ((28, 4), (40, 0), (200, 0)):
+    for n, cap in ((28, 4), (40, 0), (200, 0), (300, 0)):
         nl = _live_chain(n)
         words, po, status = _check_states([(nl, [])], [rows], max_slots=cap)
         assert status[0] == N.ST_OK, (n, cap)
         h = _header(words, po, 0)
         assert h[2] >= 32 if (n > 32 or cap) else True
         assert N.prog_rows(words, po)[0] == (max(h[3] >> 8, 8) + h[2] - 31 if h[2] >= 32 else h[3] >> 8)
-    nl = _live_chain(300)
+    nl = _live_chain(4200)
     nodes, noff, consts, coff = pack_states([(nl, [])])
     words, po, status = N.lower(nodes, noff, consts, coff)
     assert status[0] == N.ST_UNSUPPORTED

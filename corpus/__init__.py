@@ -257,6 +257,12 @@ def suite(hasher=None, max_open: int = 6, contracts=None):
         base = len(out)
         out.extend((cls.name, kind, label, terms, exp, -1 if par < 0 else base + par)
                    for kind, label, terms, exp, par in run.queries)
+    # a query is asked on a state its parent query established: a "sat" read off the query's
+    # own constraint holds only if that state is reachable, so it stays "sat" only when the
+    # parent's expectation is "sat" (an "unsat" needs no such condition)
+    for k, (c, kind, label, terms, exp, par) in enumerate(out):
+        if exp == "sat" and par >= 0 and out[par][4] != "sat":
+            out[k] = (c, kind, label, terms, None, par)
     return out
 
 

@@ -178,6 +178,17 @@ int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets,
                uint32_t n_states, const uint32_t *consts,
                const uint64_t *const_offsets, uint32_t max_passes,
                int8_t *out);
+/* mgp_refute plus one level of case splitting for the states it leaves open: each open
+ * select condition (BV ITE / BITE, nearest the root first, at most max_splits per state)
+ * is assumed true and false in turn; both refuted -> 1; one refuted -> the other
+ * polarity is kept.  A 1 is a proof.  The product runs it on the states both witness
+ * rounds leave open (solver.Prefilter), before they go to the caller's solver:
+ * ether_thief's balance comparisons after a zero-value transfer whose recipient is open
+ * (mythril/analysis/module/modules/ether_thief.py:55-95). */
+int mgp_refute_split(const mgp_node *nodes, const uint64_t *node_offsets,
+                     uint32_t n_states, const uint32_t *consts,
+                     const uint64_t *const_offsets, uint32_t max_passes,
+                     uint32_t max_splits, int8_t *out);
 /* Diagnostic (tests): the refined abstract value of every node of ONE state,
  * 33 words per node: known-zero mask, known-one mask, lo, hi (8 u32 limbs
  * each) and the Bool truth set (bit0 = may be false, bit1 = may be true).

@@ -91,6 +91,7 @@ def _bind(lib):
         "mgp_set_thread_omp": (ctypes.c_int, [ctypes.c_int]),
         "mgp_set_eval_diag": (ctypes.c_int, [_P]),
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
+        "mgp_refute_split": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
         "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
         "mgp_guided_candidates_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P,
@@ -164,6 +165,7 @@ EXPORTED_SYMBOLS = (
     "mgp_set_thread_omp",
     "mgp_set_eval_diag",
     "mgp_refute",
+    "mgp_refute_split",
     "mgp_refute_trace",
     "mgp_guided_candidates",
     "mgp_guided_candidates_rows",
@@ -415,6 +417,22 @@ def refute(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, cons
     out = np.zeros(max(n_states, 1), dtype=np.int8)
     _check(lib().mgp_refute(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
                             max_passes, _ptr(out)))
+    return out[:n_states]
+
+
+def refute_split(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,
+                 max_splits: int = 8, max_passes: int = 0) -> np.ndarray:
+    """refute + one level of case splits on open select conditions (mgp_refute_split)."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    const_offsets = np.ascontiguousarray(const_offsets, dtype=np.uint64)
+    n_states = len(node_offsets) - 1
+    out = np.zeros(max(n_states, 1), dtype=np.int8)
+    _check(lib().mgp_refute_split(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
+                                  max_passes, max_splits, _ptr(out)))
     return out[:n_states]
 
 

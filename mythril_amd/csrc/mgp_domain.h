@@ -715,6 +715,43 @@ struct Dom {
     }
     return true;
   }
+  // the node whose value x is known to equal: through BV ITEs whose condition is decided
+  // and through x + 0, x - 0, x | 0, x ^ 0 (LASER's balance updates by a zero call value)
+  MGP_RD bool zero_exact(int32_t i) const { return i >= 0 && is_exact(av[i]) && Z(av[i].lo); }
+  MGP_RD int32_t resolve(int32_t x) const {
+    for (int hop = 0; hop < 64 && x >= 0; ++hop) {
+      const mgp_node &t = nd[x];
+      if (t.op == MGP_OP_ITE && t.a >= 0) {
+        if (bs[t.a] == BT) { x = t.b; continue; }
+        if (bs[t.a] == BF) { x = t.c; continue; }
+      } else if ((t.op == MGP_OP_ADD || t.op == MGP_OP_OR || t.op == MGP_OP_XOR) && t.a >= 0 && t.b >= 0) {
+        if (zero_exact(t.b)) { x = t.a; continue; }
+        if (zero_exact(t.a)) { x = t.b; continue; }
+      } else if (t.op == MGP_OP_SUB && t.b >= 0 && zero_exact(t.b)) {
+        x = t.a;
+        continue;
+      }
+      break;
+    }
+    return x;
+  }
+  // x and y have one value in every model the analysis admits: they resolve to one node,
+  // to one function's applications on arguments known equal (after resolving them too),
+  // or to operators arg_equal matches
+  MGP_RD bool same_value(int32_t x, int32_t y) const {
+    const int32_t rx = resolve(x), ry = resolve(y);
+    if (rx == ry) return true;
+    if (rx < 0 || ry < 0) return false;
+    const mgp_node *o = orig ? orig : nd;
+    const mgp_node &a = o[rx], &b = o[ry];
+    if (a.op == MGP_OP_UFAPP && b.op == MGP_OP_UFAPP && a.p0 == b.p0 && a.width == b.width) {
+      const int32_t ax = a.a >= 0 && o[a.a].width <= MGP_MAX_WIDTH ? resolve(a.a) : a.a;
+      const int32_t bx = b.a >= 0 && o[b.a].width <= MGP_MAX_WIDTH ? resolve(b.a) : b.a;
+      return arg_equal(ax, bx, kCongDepth);
+    }
+    return rx != x || ry != y ? arg_equal(rx, ry, kCongDepth) : false;
+  }
+
   MGP_RD bool injective() {
     for (uint32_t i = 0; i < n_inj; ++i) {
       if (bs[inj[i].eq] != BT) continue;
@@ -764,6 +801,14 @@ struct Dom {
       Pair &p = pairs[cong[k]];
       if (p.u != OEQ && arg_equal(p.x, p.y, kCongDepth) && !set_order(p, 2, OEQ)) return false;
     }
+    // value aliases (refutation only: the decision rows keep their propagation cost):
+    // a compare of a balance read through zero-value transfers and decided ITEs against
+    // the starting balance of the same account compares one value with itself
+    if (!heur)
+      for (uint32_t pj = 0; pj < n_pairs; ++pj) {
+        Pair &p = pairs[pj];
+        if (p.u != OEQ && same_value(p.x, p.y) && !set_order(p, 2, OEQ)) return false;
+      }
     for (uint32_t k = 0; k < n_arel; ++k)
       if (!arith_rel(arel[k])) return false;
     for (uint32_t pj = 0; pj < n_pairs; ++pj) {

@@ -535,7 +535,76 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
   return d.run(max_passes ? max_passes : 16u);
 }
 
+// refute_one, then one level of case splitting (failed-literal probing): each open
+// condition of a select (BV ITE / BITE), nearest the root first, at most max_splits of
+// them, is assumed true and false in turn on a copy of the analysis; both refuted -> the
+// state is refuted; one refuted -> the other polarity holds and is kept for the next
+// probes.  Sound: the two assumptions cover every model.
+int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t max_passes,
+                     uint32_t max_splits) {
+  State s;
+  const int r = refute_one(nd, n, consts, n_consts, max_passes, &s);
+  if (r != 0 || max_splits == 0) return r;
+  Dom d = s.view();
+  const uint32_t passes = max_passes ? max_passes : 16u;
+  std::vector<int32_t> atoms;
+  std::vector<uint8_t> seen(s.n, 0);
+  for (uint32_t i = s.n; i-- > 0 && atoms.size() < max_splits;) {
+    const mgp_node &x = s.nd[i];
+    if ((x.op != MGP_OP_ITE && x.op != MGP_OP_BITE) || x.a < 0 || seen[x.a] || s.bs[x.a] != BB) continue;
+    seen[x.a] = 1;
+    atoms.push_back(x.a);
+  }
+  const std::vector<AV> av0 = s.av, vars0 = s.vars;
+  const std::vector<uint8_t> bs0 = s.bs;
+  const std::vector<Pair> pairs0 = s.pairs;
+  auto snapshot = [&](std::vector<AV> &a, std::vector<AV> &v, std::vector<uint8_t> &b, std::vector<Pair> &p) {
+    a = s.av; v = s.vars; b = s.bs; p = s.pairs;
+  };
+  auto restore = [&](const std::vector<AV> &a, const std::vector<AV> &v, const std::vector<uint8_t> &b,
+                     const std::vector<Pair> &p) {
+    std::copy(a.begin(), a.end(), s.av.begin());
+    std::copy(v.begin(), v.end(), s.vars.begin());
+    std::copy(b.begin(), b.end(), s.bs.begin());
+    std::copy(p.begin(), p.end(), s.pairs.begin());
+  };
+  std::vector<AV> ca = av0, cv = vars0;
+  std::vector<uint8_t> cb = bs0;
+  std::vector<Pair> cp = pairs0;
+  for (int32_t a : atoms) {
+    if (s.bs[a] != BB) continue;
+    snapshot(ca, cv, cb, cp);
+    const int rt = d.meetb(a, BT) ? d.run(passes) : 1;
+    restore(ca, cv, cb, cp);
+    const int rf = d.meetb(a, BF) ? d.run(passes) : 1;
+    restore(ca, cv, cb, cp);
+    if (rt == 1 && rf == 1) return 1;
+    if (rt == 1 || rf == 1) {  // the other polarity holds in every model
+      if (!d.meetb(a, rt == 1 ? BF : BT) || d.run(passes) == 1) return 1;
+    }
+  }
+  return 0;
+}
+
 }  // namespace
+
+extern "C" int mgp_refute_split(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                uint32_t max_splits, int8_t *out) {
+  if (!node_offsets || !out || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
+    const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
+    if (n1 < n0 || c1 < c0) {
+      out[s] = -1;
+      continue;
+    }
+    out[s] = (int8_t)refute_split_one(nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes,
+                                      max_splits);
+  }
+  return MGP_OK;
+}
 
 extern "C" int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
                           const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,

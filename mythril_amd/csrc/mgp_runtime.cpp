@@ -57,7 +57,7 @@ struct DevBuf {
 };
 
 // maximum program size accepted by the host-pointer entry point
-constexpr uint32_t kMaxSlotsHard = 255;
+constexpr uint32_t kMaxSlotsHard = MGP_MAX_SLOTS;
 
 }  // namespace
 
@@ -110,7 +110,7 @@ int64_t validate_programs(const uint32_t *w, const uint64_t *offs, uint32_t n_st
     bool has_ret = false;
     for (uint32_t i = 0; i < n_ins; ++i) {
       const uint32_t *I = w + o + MGP_HDR_WORDS + (uint64_t)i * MGP_INS_WORDS;
-      const uint32_t op = I[0] & 0xFFu, dst = (I[0] >> 16) & 0xFFu, fl = I[0] >> 24;
+      const uint32_t op = I[0] & 0xFFu, dst = ((I[0] >> 16) & 0xFFu) | ((I[3] & 0xFFu) << 8), fl = I[0] >> 24;
       const uint32_t opnds[3] = {I[1] & 0xFFFFu, I[1] >> 16, I[2] & 0xFFFFu};
       const bool bool_in = (op >= MGP_OP_BAND && op <= MGP_OP_BEQ) || op == MGP_OP_RET;
       const bool bool_out = (op >= MGP_OP_EQ && op <= MGP_OP_USUB_NOUDF) || (op >= MGP_OP_BAND && op <= MGP_OP_BEQ);

@@ -417,6 +417,10 @@ class Prefilter:
     # decision rows seeded with the parent witness (bit mask of rows; states without a parent
     # witness decide every row unseeded)
     SEED_ROWS = 0x3
+    # the states both witness rounds leave open get one level of case splits on their open
+    # select conditions (mgp_refute_split) before they go to the fallback: at most this many
+    # per state (0 = off)
+    SPLIT_REFUTE = 8
 
     def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,
                  devices: Optional[Sequence[int]] = None):
@@ -436,6 +440,7 @@ class Prefilter:
         self.decide_max_units = self.DECIDE_MAX_UNITS
         self.decide_on_gpu = "never"  # "never" (host), "auto" (>= DECIDE_GPU_MIN open states) or "always"
         self.seed_rows = self.SEED_ROWS
+        self.split_refute = self.SPLIT_REFUTE
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # refuted constraint lists wait in the core cache and are shrunk to cores together
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
@@ -577,6 +582,17 @@ class Prefilter:
                               None if parents is None else [parents[i] for i in retry])
         prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["retry_states"] = len(retry)
+        left = [i for i in range(len(states)) if first[i] < 0 and proven[i] != 1]
+        if left and self.refute and self.split_refute > 0:
+            ts = time.perf_counter()
+            LB = Batch([states[i] for i in left])
+            rs = self._N.refute_split(*LB.packed()[:4], max_splits=self.split_refute)
+            LB.close()
+            for k, i in enumerate(left):
+                if rs[k] == 1:
+                    proven[i] = 1
+            prof["split_ms"] = 1e3 * (time.perf_counter() - ts)
+            prof["split_refuted"] = int((rs == 1).sum())
         tr = time.perf_counter()
         out: List[Tuple[str, Optional[object]]] = []
         refuted = []

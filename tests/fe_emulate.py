@@ -80,6 +80,11 @@ def run(n: int = 1024, seed: int = 0x4D595448, decide_rows: int = 4, n2: int = 2
     f2 = host_round(SB, n2, seed2, dom=dom2, xrows=(rows, mask))
     SB.close()
     open2 = [i for k, i in enumerate(open_) if f2[k] < 0]
+    if open2:  # the product's case-split refutation of what both rounds leave open
+        LB = F.Batch([states[i] for i in open2])
+        rs = N.refute_split(*LB.packed()[:4], max_splits=SV.Prefilter.SPLIT_REFUTE)
+        LB.close()
+        open2 = [i for k, i in enumerate(open2) if rs[k] != 1]
     print(f"second round: +{len(open_) - len(open2)} open {len(open2)} (decisions {td:.2f}s, "
           f"{time.time() - t:.1f}s)")
     cnt = collections.Counter(C[i][0] for i in open2)
@@ -165,6 +170,14 @@ def suite_answers(queries, seed: int = 0x4D595448, decide_rows: int = 4, n2: int
                 wit[i] = (np.array(B.var_key[v0:v1]), c[k, f1[k], : v1 - v0].copy())
             elif ref[k] == 1:
                 ans[i] = "unsat"
+        left = [i for i in idx if ans[i] == "undecided"]
+        if left:  # the product's case-split refutation of what both rounds leave open
+            LB = F.Batch([list(queries[i][3]) for i in left])
+            rs = N.refute_split(*LB.packed()[:4], max_splits=SV.Prefilter.SPLIT_REFUTE)
+            LB.close()
+            for k, i in enumerate(left):
+                if rs[k] == 1:
+                    ans[i] = "unsat"
         B.close()
     return (ans, wit) if witnesses else ans
 

@@ -949,3 +949,73 @@ def test_exhaustive_soundness_store_chains():
         nodes, noff, consts, coff = pack_states([(nl, cl)])
         assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
     assert refuted > 40, refuted
+
+
+def _alias_state(rng, w=3):
+    """Random w-bit DAGs of the shapes the value-alias rule (Dom::same_value) and the case
+    split (mgp_refute_split) reason about: select chains on equalities of variables,
+    x + 0 / x - 0 / x | 0 / x ^ 0, applications of one function on selected arguments,
+    and compares between selected values and applications (ether_thief.py:55-95 in small:
+    a balance read through a zero-value transfer against the starting balance)."""
+    nl = [[S.VAR, w, -1, -1, -1, k, 0] for k in range(3)]
+    cl = [0] + [int(x) for x in rng.integers(0, 1 << w, size=2)]
+    nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(3)]   # 3: zero, 4, 5
+    vals, conds, bools = [0, 1, 2, 4, 5], [], []
+    for _ in range(int(rng.integers(2, 4))):
+        nl.append([S.EQ, 1, int(rng.integers(0, 3)), int(rng.choice([0, 1, 2, 4, 5])), -1, 0, 0])
+        conds.append(len(nl) - 1)
+    apps = []
+    for _ in range(int(rng.integers(6, 11))):
+        k = rng.random()
+        if k < 0.35:
+            nl.append([S.ITE, w, int(rng.choice(conds)), int(rng.choice(vals)), int(rng.choice(vals)), 0, 0])
+        elif k < 0.6:
+            nl.append([[S.ADD, S.SUB, S.OR, S.XOR][int(rng.integers(4))], w, int(rng.choice(vals)), 3, -1, 0, 0])
+        elif len(apps) < 2:
+            nl.append([S.UFAPP, w, int(rng.choice(vals)), -1, -1, 9, 3 + len(apps)])
+            apps.append(len(nl) - 1)
+        else:
+            nl.append([S.ITE, w, int(rng.choice(conds)), int(rng.choice(apps)), int(rng.choice(vals)), 0, 0])
+        vals.append(len(nl) - 1)
+    for _ in range(int(rng.integers(1, 3))):
+        a, b = int(rng.choice(vals[5:] or vals)), int(rng.choice(apps or vals))
+        op = [S.UGT, S.ULT, S.EQ][int(rng.integers(3))]
+        nl.append([op, 1, a, b, -1, 0, 0])
+        if op == S.EQ and rng.random() < 0.5:
+            nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+        bools.append(len(nl) - 1)
+    for c in conds:
+        if rng.random() < 0.4:
+            bools.append(c if rng.random() < 0.5 else (nl.append([S.BNOT, 1, c, -1, -1, 0, 0]) or len(nl) - 1))
+    root = bools[0]
+    for b in bools[1:]:
+        nl.append([S.BAND, 1, root, b, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl
+
+
+def test_value_alias_and_case_split_exhaustive_soundness():
+    """The value-alias rule and one level of case splitting (round 4, mgp_refute_split): every
+    state either refutes is checked over all 8^5 assignments of its three 3-bit variables and
+    two application values (C oracle, which gives applications with equal arguments one
+    value); the split must refute strictly more than the plain analysis."""
+    rng = np.random.default_rng(0xE7E)
+    states = [_alias_state(rng) for _ in range(700)]
+    nodes, noff, consts, coff = pack_states(states)
+    plain = N.refute(nodes, noff, consts, coff)
+    split = N.refute_split(nodes, noff, consts, coff, max_splits=8)
+    n_vars = 5
+    grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
+    cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    n_plain = n_split = 0
+    for st, p, s in zip(states, plain, split):
+        assert p in (0, 1) and s in (0, 1)
+        assert not (p == 1 and s != 1), "the split lost a plain refutation"
+        if s != 1:
+            continue
+        n_plain += p == 1
+        n_split += 1
+        nodes, noff, consts, coff = pack_states([st])
+        assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
+    assert n_plain > 50 and n_split > n_plain, (n_plain, n_split)

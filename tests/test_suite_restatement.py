@@ -1,0 +1,50 @@
+"""The product policy over restated `myth analyze` queries, on the CPU (no GPU): the LASER
+restatement of two solidity_examples contracts (corpus.laser, corpus.contracts) answered
+by tests/fe_emulate.py's CPU restatement of Prefilter (first round, pre-check, seeded
+decision rows, case-split refutation), counted as corpus.account counts z3 calls.
+
+The held-out contracts (corpus.held_out) are not used here: no policy knob is checked
+against them.
+"""
+import collections
+
+from oracle.keccak_ref import keccak256
+
+import corpus
+from mythril_amd import _native as N
+from mythril_amd import front as F
+from tests import fe_emulate as E
+
+
+def _queries(names):
+    return corpus.suite(hasher=keccak256, contracts=set(names))
+
+
+def test_calls_and_returnvalue_restatement_no_contradiction():
+    """calls.sol / returnvalue.sol: no answer contradicts a by-reading expectation, and the
+    z3 calls stay at the round-4 level (ether_thief's balance comparisons after zero-value
+    transfers are refuted by the case split, ether_thief.py:55-95)."""
+    qs = _queries(["calls", "returnvalue"])
+    assert not set(q[0] for q in qs) & corpus.held_out()
+    ans = E.suite_answers(qs)
+    acc = corpus.account(qs, ans)
+    assert acc["all"]["contradicted"] == 0
+    assert acc["all"]["z3_calls"] <= 33, acc["by_contract"]
+    thief = collections.Counter(a for q, a in zip(qs, ans) if "ether_thief" in q[2] and q[4] == "unsat")
+    assert thief["unsat"] >= 8 and thief["sat"] == 0, thief
+
+
+def test_case_split_refutes_what_plain_analysis_leaves():
+    """mgp_refute_split on the expected-unsat ether_thief queries: strictly more refuted than
+    mgp_refute, and it never refutes an expected-sat query of the two contracts."""
+    qs = _queries(["calls", "returnvalue"])
+    B = F.Batch([list(q[3]) for q in qs])
+    packed = B.packed()[:4]
+    plain = N.refute(*packed)
+    split = N.refute_split(*packed, max_splits=8)
+    B.close()
+    assert ((plain == 1) & (split != 1)).sum() == 0
+    exp = [q[4] for q in qs]
+    assert not any(s == 1 and e == "sat" for s, e in zip(split, exp))
+    thief = [k for k, q in enumerate(qs) if "ether_thief" in q[2] and q[4] == "unsat"]
+    assert sum(split[k] == 1 for k in thief) > sum(plain[k] == 1 for k in thief)

@@ -1,0 +1,11 @@
+# One GPU call: the gpu-marked suite, the r3n regression test against the defect's library
+# (expected to fail there), and a rocprofv3 kernel trace of a short bench run.
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r4c_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r4c_tests.log; exit 1; }
+tail -2 gpurun_out/r4c_tests.log
+MGP_LIB_PATH=mutants/d/libmgp.so timeout -k 10 120 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -k mul_after_shift --timeout 60 --timeout-method thread > gpurun_out/r4c_mutd.log 2>&1; rc=$?; echo "mutant d rc=$rc" >> gpurun_out/r4c_mutd.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "mutant step abnormal rc=$rc"; tail -20 gpurun_out/r4c_mutd.log; exit 1; fi
+grep -E "passed|failed|differ" gpurun_out/r4c_mutd.log | tail -4
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r4c -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --frontend 0 --suite 0 --no-cpu --refute-sample 0 --guided-sample 0 --keccak 0 --div-split 0 > gpurun_out/r4c_prof_bench.json 2> gpurun_out/r4c_prof_bench.err || { echo "rocprof run failed"; tail -5 gpurun_out/r4c_prof_bench.err; exit 1; }
+find gpurun_out/prof_r4c -name "*stats*"

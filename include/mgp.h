@@ -388,6 +388,10 @@ void mgp_fe_free(mgp_fe_batch *batch);
  * Replaces, for one batch, the z3
  * checks of Constraints.is_possible (constraints.py:34-51) and the SAT-only get_model
  * calls (analysis/solver.py:27-61) it can decide. */
+/* Size mgp_check_batch's pinned host staging buffer and device candidate block of ctx
+ * up front (they otherwise grow on the first large batch: pinning ~200 MB of host memory
+ * takes tens of ms).  solver.Prefilter reserves its cand_bytes at construction. */
+int mgp_pipeline_reserve(mgp_ctx *ctx, uint64_t host_bytes, uint64_t cand_bytes);
 #define MGP_CHECK_NO_REFUTE 0x1u   /* skip the host pre-check (and the domain rows) */
 #define MGP_CHECK_NO_DOMAINS 0x2u  /* plain mixture rows only (A/B)                    */
 int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint64_t seed,

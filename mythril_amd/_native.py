@@ -110,6 +110,7 @@ def _bind(lib):
                                             ctypes.POINTER(_P)]),
         "mgp_fe_get": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
         "mgp_fe_free": (None, [_P]),
+        "mgp_pipeline_reserve": (ctypes.c_int, [_P, _U64, _U64]),
         "mgp_check_batch": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _U32, _U32,
                                            _P, _P, _P, _P, _P]),
         "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _U32, _U32, _P]),
@@ -179,6 +180,7 @@ EXPORTED_SYMBOLS = (
     "mgp_fe_get",
     "mgp_fe_free",
     "mgp_check_batch",
+    "mgp_pipeline_reserve",
     "mgp_fe_candidates",
     "mgp_program_cache_clear",
 )
@@ -488,6 +490,10 @@ class Context:
         )
         _check(rc, self._h)
         return first, wit
+
+    def reserve(self, host_bytes: int, cand_bytes: int) -> None:
+        """mgp_pipeline_reserve: size the pipeline's pinned staging and candidate block now."""
+        _check(lib().mgp_pipeline_reserve(self._h, int(host_bytes), int(cand_bytes)), self._h)
 
     def check_batch(self, batch, n_cand: int, seed: int, parents=None, refute: bool = True, xrows=None):
         """A front-end batch (mythril_amd.front.Batch) through mgp_check_batch."""

@@ -1191,9 +1191,14 @@ static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32
     const char *e = getenv("MGP_LOWER_SCHED");
     return (e && e[0] >= '0' && e[0] <= '3' && e[1] == 0) ? e[0] - '0' : 1;
   }();
-  // few states (LASER's JUMPI forks): states in turn, each state's schedules in parallel
+  // few states (LASER's JUMPI forks): states in turn, each state's schedules in parallel --
+  // unless every state is large (WalletLibrary's: more than kBigNodes nodes), whose programs
+  // keep input order alone (lower_one), so the states themselves run in parallel
   const bool few = (int64_t)n_states * 2 < (int64_t)omp_get_max_threads();
-#pragma omp parallel for schedule(dynamic, 1) if (!few)
+  constexpr uint64_t kBigNodes = 600;
+  bool all_big = n_states > 1;
+  for (uint32_t s = 0; s < n_states && all_big; ++s) all_big = node_offsets[s + 1] - node_offsets[s] > kBigNodes;
+#pragma omp parallel for schedule(dynamic, 1) if (!few || all_big)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
     const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];

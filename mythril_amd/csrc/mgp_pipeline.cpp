@@ -336,6 +336,14 @@ void mgp_pipeline_release(mgp_ctx *ctx) {
   if (b->host) (void)hipHostFree(b->host);
 }
 
+int mgp_pipeline_reserve(mgp_ctx *ctx, uint64_t host_bytes, uint64_t cand_bytes) {
+  if (!ctx) return MGP_E_ARG;
+  PipeBufs &D = bufs_of(ctx);
+  hipError_t e = D.ensure_host((size_t)host_bytes);
+  if (e == hipSuccess && cand_bytes) e = D.ensure(B_CANDS, (size_t)cand_bytes);
+  return e == hipSuccess ? MGP_OK : mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+}
+
 int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64_t seed, const uint32_t *fixed_pool,
                     uint32_t n_fixed, const uint64_t *parent_keys, const uint32_t *parent_vals,
                     const uint64_t *parent_off, const uint64_t *slot_keys, const uint32_t *xrows,

@@ -421,6 +421,9 @@ class Prefilter:
     # select conditions (mgp_refute_split) before they go to the fallback: at most this many
     # per state (0 = off)
     SPLIT_REFUTE = 8
+    # pinned host staging of mgp_check_batch reserved per context (programs + tables of one
+    # batch go up through it: WalletLibrary's lowered programs are ~0.45 MB each)
+    HOST_STAGING = 256 << 20
 
     def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,
                  devices: Optional[Sequence[int]] = None):
@@ -442,6 +445,10 @@ class Prefilter:
         self.seed_rows = self.SEED_ROWS
         self.split_refute = self.SPLIT_REFUTE
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
+        # the pipeline's pinned host staging and candidate block, sized once here instead of
+        # on the first large batch (pinning a few hundred MB of host memory takes tens of ms)
+        for c in self.ctxs:
+            c.reserve(self.HOST_STAGING, self.cand_bytes)
         # refuted constraint lists wait in the core cache and are shrunk to cores together
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
         # one per call keeps the deletion trials off the latency of small calls

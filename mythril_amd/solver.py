@@ -448,7 +448,9 @@ class Prefilter:
         # the pipeline's pinned host staging and candidate block, sized once here instead of
         # on the first large batch (pinning a few hundred MB of host memory takes tens of ms)
         for c in self.ctxs:
-            c.reserve(self.HOST_STAGING, self.cand_bytes)
+            reserve = getattr(c, "reserve", None)  # (test doubles of the context have none)
+            if reserve is not None:
+                reserve(self.HOST_STAGING, self.cand_bytes)
         # refuted constraint lists wait in the core cache and are shrunk to cores together
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
         # one per call keeps the deletion trials off the latency of small calls

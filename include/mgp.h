@@ -178,10 +178,11 @@ int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets,
                uint32_t n_states, const uint32_t *consts,
                const uint64_t *const_offsets, uint32_t max_passes,
                int8_t *out);
-/* mgp_refute plus one level of case splitting for the states it leaves open: each open
- * select condition (BV ITE / BITE, nearest the root first, at most max_splits per state)
- * is assumed true and false in turn; both refuted -> 1; one refuted -> the other
- * polarity is kept.  A 1 is a proof.  The product runs it on the states both witness
+/* mgp_refute plus case splitting for the states it leaves open: each open select
+ * condition (BV ITE / BITE, nearest the root first; max_splits bits 0..15 = at most this
+ * many per state) is assumed true and false in turn, and each branch is split again on
+ * the others up to (max_splits >> 16) & 15 levels (0 = 1); both branches refuted -> 1;
+ * one refuted -> the other polarity is kept.  A 1 is a proof.  The product runs it on the states both witness
  * rounds leave open (solver.Prefilter), before they go to the caller's solver:
  * ether_thief's balance comparisons after a zero-value transfer whose recipient is open
  * (mythril/analysis/module/modules/ether_thief.py:55-95). */

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <functional>
 #include <iterator>
 #include <memory>
 #include <unordered_map>
@@ -542,48 +543,53 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
 // probes.  Sound: the two assumptions cover every model.
 int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t max_passes,
                      uint32_t max_splits) {
+  // max_splits: atoms per level in bits 0..15, levels in bits 16..19 (0 = 1)
+  const uint32_t n_atoms = max_splits & 0xFFFFu, depth = std::max<uint32_t>(1u, (max_splits >> 16) & 0xFu);
   State s;
   const int r = refute_one(nd, n, consts, n_consts, max_passes, &s);
-  if (r != 0 || max_splits == 0) return r;
+  if (r != 0 || n_atoms == 0) return r;
   Dom d = s.view();
   const uint32_t passes = max_passes ? max_passes : 16u;
   std::vector<int32_t> atoms;
   std::vector<uint8_t> seen(s.n, 0);
-  for (uint32_t i = s.n; i-- > 0 && atoms.size() < max_splits;) {
+  for (uint32_t i = s.n; i-- > 0 && atoms.size() < n_atoms;) {
     const mgp_node &x = s.nd[i];
     if ((x.op != MGP_OP_ITE && x.op != MGP_OP_BITE) || x.a < 0 || seen[x.a] || s.bs[x.a] != BB) continue;
     seen[x.a] = 1;
     atoms.push_back(x.a);
   }
-  const std::vector<AV> av0 = s.av, vars0 = s.vars;
-  const std::vector<uint8_t> bs0 = s.bs;
-  const std::vector<Pair> pairs0 = s.pairs;
-  auto snapshot = [&](std::vector<AV> &a, std::vector<AV> &v, std::vector<uint8_t> &b, std::vector<Pair> &p) {
-    a = s.av; v = s.vars; b = s.bs; p = s.pairs;
+  struct Snap {
+    std::vector<AV> av, vars;
+    std::vector<uint8_t> bs;
+    std::vector<Pair> pairs;
   };
-  auto restore = [&](const std::vector<AV> &a, const std::vector<AV> &v, const std::vector<uint8_t> &b,
-                     const std::vector<Pair> &p) {
-    std::copy(a.begin(), a.end(), s.av.begin());
-    std::copy(v.begin(), v.end(), s.vars.begin());
-    std::copy(b.begin(), b.end(), s.bs.begin());
-    std::copy(p.begin(), p.end(), s.pairs.begin());
+  auto take = [&](Snap &c) { c.av = s.av; c.vars = s.vars; c.bs = s.bs; c.pairs = s.pairs; };
+  auto put = [&](const Snap &c) {
+    std::copy(c.av.begin(), c.av.end(), s.av.begin());
+    std::copy(c.vars.begin(), c.vars.end(), s.vars.begin());
+    std::copy(c.bs.begin(), c.bs.end(), s.bs.begin());
+    std::copy(c.pairs.begin(), c.pairs.end(), s.pairs.begin());
   };
-  std::vector<AV> ca = av0, cv = vars0;
-  std::vector<uint8_t> cb = bs0;
-  std::vector<Pair> cp = pairs0;
-  for (int32_t a : atoms) {
-    if (s.bs[a] != BB) continue;
-    snapshot(ca, cv, cb, cp);
-    const int rt = d.meetb(a, BT) ? d.run(passes) : 1;
-    restore(ca, cv, cb, cp);
-    const int rf = d.meetb(a, BF) ? d.run(passes) : 1;
-    restore(ca, cv, cb, cp);
-    if (rt == 1 && rf == 1) return 1;
-    if (rt == 1 || rf == 1) {  // the other polarity holds in every model
-      if (!d.meetb(a, rt == 1 ? BF : BT) || d.run(passes) == 1) return 1;
+  std::vector<Snap> snaps(depth);
+  // true = the analysis as it stands (propagated) is refuted by splits `level` deep
+  std::function<bool(uint32_t)> probe = [&](uint32_t level) -> bool {
+    if (level == 0) return false;
+    Snap &c = snaps[level - 1];
+    for (int32_t a : atoms) {
+      if (s.bs[a] != BB) continue;
+      take(c);
+      const bool rt = !d.meetb(a, BT) || d.run(passes) == 1 || probe(level - 1);
+      put(c);
+      const bool rf = !d.meetb(a, BF) || d.run(passes) == 1 || probe(level - 1);
+      put(c);
+      if (rt && rf) return true;
+      if (rt || rf) {  // the other polarity holds in every model of this branch
+        if (!d.meetb(a, rt ? BF : BT) || d.run(passes) == 1) return true;
+      }
     }
-  }
-  return 0;
+    return false;
+  };
+  return probe(depth) ? 1 : 0;
 }
 
 }  // namespace

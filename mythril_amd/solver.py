@@ -417,10 +417,13 @@ class Prefilter:
     # decision rows seeded with the parent witness (bit mask of rows; states without a parent
     # witness decide every row unseeded)
     SEED_ROWS = 0x3
-    # the states both witness rounds leave open get one level of case splits on their open
-    # select conditions (mgp_refute_split) before they go to the fallback: at most this many
-    # per state (0 = off)
+    # the states both witness rounds leave open get case splits on their open select
+    # conditions (mgp_refute_split) before they go to the fallback: at most SPLIT_REFUTE of
+    # them per state (0 = off), nested SPLIT_DEPTH levels.  Depth 2 refutes 11 more of the
+    # tuned contracts' ether_thief / etherstore queries than depth 1 (calls.sol 32 -> 21 z3
+    # calls) and costs ~7x the split time of the states that reach it
     SPLIT_REFUTE = 8
+    SPLIT_DEPTH = 2
     # pinned host staging of mgp_check_batch reserved per context (programs + tables of one
     # batch go up through it: WalletLibrary's lowered programs are ~0.45 MB each)
     HOST_STAGING = 256 << 20
@@ -444,6 +447,7 @@ class Prefilter:
         self.decide_on_gpu = "never"  # "never" (host), "auto" (>= DECIDE_GPU_MIN open states) or "always"
         self.seed_rows = self.SEED_ROWS
         self.split_refute = self.SPLIT_REFUTE
+        self.split_depth = self.SPLIT_DEPTH
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # the pipeline's pinned host staging and candidate block, sized once here instead of
         # on the first large batch (pinning a few hundred MB of host memory takes tens of ms)
@@ -595,7 +599,7 @@ class Prefilter:
         if left and self.refute and self.split_refute > 0:
             ts = time.perf_counter()
             LB = Batch([states[i] for i in left])
-            rs = self._N.refute_split(*LB.packed()[:4], max_splits=self.split_refute)
+            rs = self._N.refute_split(*LB.packed()[:4], max_splits=self.split_refute, depth=self.split_depth)
             LB.close()
             for k, i in enumerate(left):
                 if rs[k] == 1:

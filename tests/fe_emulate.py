@@ -82,7 +82,8 @@ def run(n: int = 1024, seed: int = 0x4D595448, decide_rows: int = 4, n2: int = 2
     open2 = [i for k, i in enumerate(open_) if f2[k] < 0]
     if open2:  # the product's case-split refutation of what both rounds leave open
         LB = F.Batch([states[i] for i in open2])
-        rs = N.refute_split(*LB.packed()[:4], max_splits=SV.Prefilter.SPLIT_REFUTE)
+        rs = N.refute_split(*LB.packed()[:4], max_splits=SV.Prefilter.SPLIT_REFUTE,
+                                depth=SV.Prefilter.SPLIT_DEPTH)
         LB.close()
         open2 = [i for k, i in enumerate(open2) if rs[k] != 1]
     print(f"second round: +{len(open_) - len(open2)} open {len(open2)} (decisions {td:.2f}s, "
@@ -173,7 +174,8 @@ def suite_answers(queries, seed: int = 0x4D595448, decide_rows: int = 4, n2: int
         left = [i for i in idx if ans[i] == "undecided"]
         if left:  # the product's case-split refutation of what both rounds leave open
             LB = F.Batch([list(queries[i][3]) for i in left])
-            rs = N.refute_split(*LB.packed()[:4], max_splits=SV.Prefilter.SPLIT_REFUTE)
+            rs = N.refute_split(*LB.packed()[:4], max_splits=SV.Prefilter.SPLIT_REFUTE,
+                                depth=SV.Prefilter.SPLIT_DEPTH)
             LB.close()
             for k, i in enumerate(left):
                 if rs[k] == 1:

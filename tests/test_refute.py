@@ -995,27 +995,75 @@ def _alias_state(rng, w=3):
 
 
 def test_value_alias_and_case_split_exhaustive_soundness():
-    """The value-alias rule and one level of case splitting (round 4, mgp_refute_split): every
-    state either refutes is checked over all 8^5 assignments of its three 3-bit variables and
-    two application values (C oracle, which gives applications with equal arguments one
-    value); the split must refute strictly more than the plain analysis."""
+    """The value-alias rule and one and two levels of case splitting (round 4,
+    mgp_refute_split): every state either refutes is checked over all 8^5 assignments of its
+    three 3-bit variables and two application values (C oracle, which gives applications
+    with equal arguments one value); one level must refute strictly more than the plain
+    analysis, and two levels at least what one does."""
     rng = np.random.default_rng(0xE7E)
     states = [_alias_state(rng) for _ in range(700)]
     nodes, noff, consts, coff = pack_states(states)
     plain = N.refute(nodes, noff, consts, coff)
     split = N.refute_split(nodes, noff, consts, coff, max_splits=8)
+    split2 = N.refute_split(nodes, noff, consts, coff, max_splits=8, depth=2)
     n_vars = 5
     grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
     cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
     cands[0, :, :, 0] = grid
-    n_plain = n_split = 0
-    for st, p, s in zip(states, plain, split):
-        assert p in (0, 1) and s in (0, 1)
+    n_plain = n_split = n_split2 = 0
+    for st, p, s, s2 in zip(states, plain, split, split2):
+        assert p in (0, 1) and s in (0, 1) and s2 in (0, 1)
         assert not (p == 1 and s != 1), "the split lost a plain refutation"
-        if s != 1:
+        assert not (s == 1 and s2 != 1), "two levels lost a one-level refutation"
+        if s2 != 1:
             continue
         n_plain += p == 1
-        n_split += 1
+        n_split += s == 1
+        n_split2 += 1
         nodes, noff, consts, coff = pack_states([st])
         assert coracle.first_sat(nodes, noff, consts, coff, cands)[0] < 0, "refuted a satisfiable state"
-    assert n_plain > 50 and n_split > n_plain, (n_plain, n_split)
+    assert n_plain > 50 and n_split > n_plain and n_split2 >= n_split, (n_plain, n_split, n_split2)
+
+
+def _transfer_chain_state(rng, w=3):
+    """A balance passed through 2-3 conditional transfers (select on an equality of
+    addresses between the balance and the balance minus / plus / or / xor an amount that is
+    mostly zero) and compared with its start: ether_thief.py:55-95's balance comparisons
+    after a run of zero-value transfers, which need one split per transfer."""
+    nl = [[S.VAR, w, -1, -1, -1, k, 0] for k in range(4)]
+    cl = [0] + [int(x) for x in rng.integers(0, 1 << w, size=2)]
+    nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(3)]   # 4: zero, 5, 6
+    cur = 0
+    for _ in range(int(rng.integers(2, 4))):
+        a, b = (int(x) for x in rng.choice([1, 2, 3, 5, 6], 2, replace=False))
+        nl.append([S.EQ, 1, a, b, -1, 0, 0])
+        c = len(nl) - 1
+        op = [S.SUB, S.ADD, S.OR, S.XOR][int(rng.integers(4))]
+        nl.append([op, w, cur, 4 if rng.random() < 0.85 else int(rng.choice([5, 6])), -1, 0, 0])
+        t = len(nl) - 1
+        nl.append([S.ITE, w, c, t, cur, 0, 0] if rng.random() < 0.5 else [S.ITE, w, c, cur, t, 0, 0])
+        cur = len(nl) - 1
+    op = [S.UGT, S.ULT][int(rng.integers(2))]
+    nl.append([op, 1, cur, 0, -1, 0, 0] if rng.random() < 0.5 else [op, 1, 0, cur, -1, 0, 0])
+    return nl, cl
+
+
+def test_case_split_depth_exhaustive_soundness():
+    """Nested case splits (mgp_refute_split, depth 1..3) on transfer chains: each level
+    refutes a superset of the last and strictly more in total, and every refuted state is
+    checked over all 8^4 assignments of its four 3-bit variables (C oracle)."""
+    rng = np.random.default_rng(0x5917)
+    states = [_transfer_chain_state(rng) for _ in range(600)]
+    packed = pack_states(states)
+    levels = [N.refute(*packed)] + [N.refute_split(*packed, max_splits=8, depth=d) for d in (1, 2, 3)]
+    counts = [int((r == 1).sum()) for r in levels]
+    for lo, hi in zip(levels, levels[1:]):
+        assert ((lo == 1) & (hi != 1)).sum() == 0, "a deeper split lost a refutation"
+    assert counts[0] < counts[1] < counts[2] <= counts[3], counts
+    n_vars = 4
+    grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
+    cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    for st, r in zip(states, levels[3]):
+        if r == 1:
+            assert coracle.first_sat(*pack_states([st]), cands)[0] < 0, "refuted a satisfiable state"

@@ -122,8 +122,16 @@ struct Piece {
 };
 typedef std::vector<Piece> Pieces;
 
+// a piece of an argument as base term + constant offset (sum_form in lower_one)
+struct SumForm {
+  Ref r, base;
+  uint32_t w;
+  uint32_t off[8];
+};
+
 struct UFApp {
   Pieces arg, val, fresh;  // argument, value, the application's own fresh variable(s)
+  std::vector<SumForm> form;  // of arg, piece by piece (f applications only)
 };
 
 // MGP_LOWER_WHY=1: name the source line of every "unsupported" verdict (diagnostics)
@@ -708,6 +716,32 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     }
     return all ? 1 : -1;
   };
+  // known_eq on sum forms computed once per application: the f-application chains compare
+  // every new argument with every earlier one (WalletLibrary's states: ~6 500 comparisons)
+  auto forms_of = [&](const Pieces &p) {
+    std::vector<SumForm> f(p.size());
+    for (size_t k = 0; k < p.size(); ++k) {
+      f[k].r = p[k].r;
+      f[k].w = p[k].w;
+      sum_form(p[k].r, p[k].w, &f[k].base, f[k].off);
+    }
+    return f;
+  };
+  auto known_eq_forms = [](const std::vector<SumForm> &p, const std::vector<SumForm> &q) -> int {
+    if (p.size() != q.size()) return -1;
+    bool all = true;
+    for (size_t k = 0; k < p.size(); ++k) {
+      if (p[k].w != q[k].w) return -1;
+      if (p[k].r == q[k].r) continue;
+      if (p[k].r.k == R_CONST && q[k].r.k == R_CONST) return 0;
+      if (p[k].base == q[k].base) {
+        if (memcmp(p[k].off, q[k].off, sizeof(p[k].off)) != 0) return 0;
+        continue;
+      }
+      all = false;
+    }
+    return all ? 1 : -1;
+  };
   auto ite_pieces = [&](Ref c, const Pieces &p, const Pieces &q) -> Pieces {
     if (p.size() == 1 && q.size() == 1) return Pieces{Piece{S.add(MGP_OP_ITE, (uint16_t)p[0].w, false, c, p[0].r, q[0].r), p[0].w}};
     Pieces pa, qa, out;
@@ -1049,16 +1083,23 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         // chaining on fresh variables (free reads) instead of earlier chain results keeps
         // no earlier value live (calldata words are 32 selects of one array each).
         const Pieces arg = pieces_of(nd.a);
+        std::vector<SumForm> form = forms_of(arg);
         const Pieces fresh = var_pieces(nd.p1, w);
         Pieces v = fresh;
         std::vector<UFApp> &fl = fapps[nd.p0];
         for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
           if (wid_of(it->arg) != wid[nd.a] || wid_of(it->val) != w) return unsupported();
-          const int ke = known_eq(arg, it->arg);
+          const int ke = known_eq_forms(form, it->form);
           if (ke == 0) continue;
+          if (ke == -1 && arg.size() == 1 && it->arg.size() == 1 && v.size() == 1 && it->fresh.size() == 1) {
+            // the one-piece case of the line below, without piece-list temporaries
+            const Ref e = S.add(MGP_OP_EQ, (uint16_t)arg[0].w, true, arg[0].r, it->arg[0].r);
+            v[0].r = S.add(MGP_OP_ITE, (uint16_t)v[0].w, false, e, it->fresh[0].r, v[0].r);
+            continue;
+          }
           v = (ke == 1) ? it->fresh : ite_pieces(eq_pieces(arg, it->arg), it->fresh, v);
         }
-        fl.push_back(UFApp{arg, v, fresh});
+        fl.push_back(UFApp{arg, v, fresh, std::move(form)});
         set_val(i, v);
         break;
       }
@@ -1083,7 +1124,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           if (ke == 0) continue;
           v = (ke == 1) ? it->val : ite_pieces(eq_pieces(arg, it->arg), it->val, v);
         }
-        il.push_back(UFApp{arg, v, var_pieces(nd.p1, w)});
+        il.push_back(UFApp{arg, v, var_pieces(nd.p1, w), {}});
         set_val(i, v);
         break;
       }

@@ -424,6 +424,12 @@ class Prefilter:
     # calls) and costs ~7x the split time of the states that reach it
     SPLIT_REFUTE = 8
     SPLIT_DEPTH = 2
+    # a batch of at most this many states computes the decision rows of all its states on a
+    # host thread while its first round runs (the host is idle during the GPU wait of a
+    # small batch); the retry round then takes the rows of its open states from them.  Rows
+    # are a function of the state alone (content-keyed seeds, per-state caps), so the
+    # answers are those of the sequential policy (tests/test_determinism.py)
+    SPECULATE_ROWS_MAX = 16
     # pinned host staging of mgp_check_batch reserved per context (programs + tables of one
     # batch go up through it: WalletLibrary's lowered programs are ~0.45 MB each)
     HOST_STAGING = 256 << 20
@@ -448,6 +454,7 @@ class Prefilter:
         self.seed_rows = self.SEED_ROWS
         self.split_refute = self.SPLIT_REFUTE
         self.split_depth = self.SPLIT_DEPTH
+        self.speculate_rows_max = self.SPECULATE_ROWS_MAX
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # the pipeline's pinned host staging and candidate block, sized once here instead of
         # on the first large batch (pinning a few hundred MB of host memory takes tens of ms)
@@ -581,7 +588,12 @@ class Prefilter:
             self.last_profile = _sum_profiles(profs)
             return res, sorted(refuted)
         prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
-        first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute)
+        spec = self._speculate_rows(B, parents)
+        try:
+            first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute)
+        finally:
+            if spec is not None:
+                spec["thread"].join()
         self.last_times = times
         for k, name in enumerate(("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")):
             prof[name] = float(times[k])
@@ -592,7 +604,7 @@ class Prefilter:
         retry = [i for i in range(len(states)) if first[i] == -1 and proven[i] != 1]
         if retry and self.retry_cand > 0:
             self._retry_round(ctx, states, retry, first, witnesses, prof,
-                              None if parents is None else [parents[i] for i in retry])
+                              None if parents is None else [parents[i] for i in retry], spec=spec)
         prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["retry_states"] = len(retry)
         left = [i for i in range(len(states)) if first[i] < 0 and proven[i] != 1]
@@ -654,14 +666,54 @@ class Prefilter:
                         np.where(units * self.DECIDE_MIN_ROWS <= self.decide_max_units, self.DECIDE_MIN_ROWS, 0))
         return rows.astype(np.uint8)
 
-    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None, parents=None) -> None:
+    def _decide_on_gpu(self, n: int) -> bool:
+        return self.decide_on_gpu == "always" or (self.decide_on_gpu == "auto" and n >= self.DECIDE_GPU_MIN)
+
+    def _decision_rows(self, GB, parents, seed2, ctx=None):
+        """mgp_decision_rows of batch GB (parent-seeded rows when a parent witness is given)."""
+        from .front import seed_arrays
+
+        gv = max(1, GB.n_vars())
+        seeds = seed_arrays(GB, parents) if parents is not None and any(p is not None for p in parents) else None
+        if seeds is not None and seeds[0].shape[1] != gv:
+            seeds = None
+        rows, mask, _ = self._N.decision_rows(*GB.packed(decide=True), gv, seed2, self.decide_rows,
+                                              self.rows_per_state(GB), state_keys=GB.state_key, ctx=ctx,
+                                              seeds=seeds, seed_rows=self.seed_rows)
+        return rows, mask
+
+    def _speculate_rows(self, B, parents):
+        """Start the decision rows of every state of a small batch on a host thread (joined
+        before the batch's results are read); None when the batch does not qualify."""
+        n = B.n_states
+        if not (0 < n <= self.speculate_rows_max and self.retry_cand > 0 and self.decide_rows > 0
+                and not self._decide_on_gpu(n)):
+            return None
+        import threading
+
+        seed2 = (self.seed + 0x7F4A7C15) & (2 ** 64 - 1)
+        spec: dict = {}
+
+        def work():
+            t = time.perf_counter()
+            try:
+                spec["rows"] = self._decision_rows(B, parents, seed2)
+            except BaseException as e:  # re-raised by the retry round that needs the rows
+                spec["error"] = e
+            spec["ms"] = 1e3 * (time.perf_counter() - t)
+
+        spec["thread"] = threading.Thread(target=work, name="mgp-speculative-rows", daemon=True)
+        spec["thread"].start()
+        return spec
+
+    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None, parents=None, spec=None) -> None:
         """The second witness round for the open states: host decision rows
         (mgp_decision_rows, each variable fixed in turn and the analysis re-propagated)
         placed in the first mixture rows of a device-generated round with a new seed.  A
         state with a parent witness gets SEED_ROWS of its rows seeded with the parent's
         values (mgp_decision_rows_seeded): the draws then only decide what the child's new
         constraint brought in."""
-        from .front import FE_SAT_UNSAFE, Batch, seed_arrays
+        from .front import FE_SAT_UNSAFE, Batch
 
         prof = {} if prof is None else prof
         n2 = max(64, self.retry_cand // 64 * 64)
@@ -680,17 +732,18 @@ class Prefilter:
             # one group (the usual case): the batch built for the grouping is the round's batch
             GB = SB if len(groups) == 1 else Batch([states[retry[k]] for k in grp])
             gv = max(1, GB.n_vars())
-            rps = self.rows_per_state(GB)
             td = time.perf_counter()
-            on_gpu = self.decide_on_gpu == "always" or (self.decide_on_gpu == "auto" and
-                                                        len(grp) >= self.DECIDE_GPU_MIN)
+            on_gpu = self._decide_on_gpu(len(grp))
             par = None if parents is None else [parents[j] for j in grp]
-            seeds = seed_arrays(GB, par) if par is not None and any(p is not None for p in par) else None
-            if seeds is not None and seeds[0].shape[1] != gv:
-                seeds = None
-            rows, mask, _ = self._N.decision_rows(*GB.packed(decide=True), gv, seed2, self.decide_rows, rps,
-                                                  state_keys=GB.state_key, ctx=ctx if on_gpu else None,
-                                                  seeds=seeds, seed_rows=self.seed_rows)
+            if spec is not None and "error" in spec:
+                raise spec["error"]
+            if spec is not None and "rows" in spec:
+                # the speculative rows of the whole batch: this group's states, its variables
+                sel = [retry[j] for j in grp]
+                rows, mask = (np.ascontiguousarray(a[sel][:, :, :gv]) for a in spec["rows"])
+                prof["decide_speculative_ms"] = spec["ms"]
+            else:
+                rows, mask = self._decision_rows(GB, par, seed2, ctx=ctx if on_gpu else None)
             dec_ms += 1e3 * (time.perf_counter() - td)
             prof["decide_on_gpu"] = bool(on_gpu)
             f2, w2, _, st2 = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))

@@ -29,9 +29,11 @@ answer is `unknown`, which each caller maps exactly as the reference does.
 """
 from __future__ import annotations
 
-import threading
+import atexit
 import os
+import threading
 import time
+import weakref
 from functools import lru_cache
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple, Union
 
@@ -474,6 +476,7 @@ class Prefilter:
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
     def close(self) -> None:
+        _join_speculative()
         for c in self.ctxs:
             c.close()
 
@@ -589,11 +592,7 @@ class Prefilter:
             return res, sorted(refuted)
         prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
         spec = self._speculate_rows(B, parents)
-        try:
-            first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute)
-        finally:
-            if spec is not None:
-                spec["thread"].join()
+        first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute)
         self.last_times = times
         for k, name in enumerate(("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")):
             prof[name] = float(times[k])
@@ -669,41 +668,51 @@ class Prefilter:
     def _decide_on_gpu(self, n: int) -> bool:
         return self.decide_on_gpu == "always" or (self.decide_on_gpu == "auto" and n >= self.DECIDE_GPU_MIN)
 
-    def _decision_rows(self, GB, parents, seed2, ctx=None):
-        """mgp_decision_rows of batch GB (parent-seeded rows when a parent witness is given)."""
+    def _rows_args(self, GB, parents, copy=False):
+        """The inputs of mgp_decision_rows for batch GB (parent-seeded rows when a parent
+        witness is given); copy=True detaches them from GB's native arrays."""
         from .front import seed_arrays
 
         gv = max(1, GB.n_vars())
         seeds = seed_arrays(GB, parents) if parents is not None and any(p is not None for p in parents) else None
         if seeds is not None and seeds[0].shape[1] != gv:
             seeds = None
-        rows, mask, _ = self._N.decision_rows(*GB.packed(decide=True), gv, seed2, self.decide_rows,
-                                              self.rows_per_state(GB), state_keys=GB.state_key, ctx=ctx,
+        packed = [np.array(a, copy=True) for a in GB.packed(decide=True)] if copy else list(GB.packed(decide=True))
+        keys = np.array(GB.state_key, copy=True) if copy else GB.state_key
+        if copy and seeds is not None:
+            seeds = tuple(np.array(a, copy=True) for a in seeds)
+        return packed, gv, self.rows_per_state(GB), keys, seeds
+
+    def _decision_rows(self, args, seed2, ctx=None):
+        packed, gv, rps, keys, seeds = args
+        rows, mask, _ = self._N.decision_rows(*packed, gv, seed2, self.decide_rows, rps, state_keys=keys, ctx=ctx,
                                               seeds=seeds, seed_rows=self.seed_rows)
         return rows, mask
 
     def _speculate_rows(self, B, parents):
-        """Start the decision rows of every state of a small batch on a host thread (joined
-        before the batch's results are read); None when the batch does not qualify."""
+        """Start the decision rows of every state of a small batch on a host thread, on
+        copies of B's arrays (the thread never touches B, so a batch whose first round
+        decides everything returns without waiting for it); None when the batch does not
+        qualify."""
         n = B.n_states
         if not (0 < n <= self.speculate_rows_max and self.retry_cand > 0 and self.decide_rows > 0
                 and not self._decide_on_gpu(n)):
             return None
-        import threading
-
         seed2 = (self.seed + 0x7F4A7C15) & (2 ** 64 - 1)
         spec: dict = {}
+        args = self._rows_args(B, parents, copy=True)
 
         def work():
             t = time.perf_counter()
             try:
-                spec["rows"] = self._decision_rows(B, parents, seed2)
+                spec["rows"] = self._decision_rows(args, seed2)
             except BaseException as e:  # re-raised by the retry round that needs the rows
                 spec["error"] = e
             spec["ms"] = 1e3 * (time.perf_counter() - t)
 
         spec["thread"] = threading.Thread(target=work, name="mgp-speculative-rows", daemon=True)
         spec["thread"].start()
+        _SPECULATIVE.add(spec["thread"])
         return spec
 
     def _retry_round(self, ctx, states, retry, first, witnesses, prof=None, parents=None, spec=None) -> None:
@@ -735,15 +744,17 @@ class Prefilter:
             td = time.perf_counter()
             on_gpu = self._decide_on_gpu(len(grp))
             par = None if parents is None else [parents[j] for j in grp]
-            if spec is not None and "error" in spec:
-                raise spec["error"]
+            if spec is not None:
+                spec["thread"].join()
+                if "error" in spec:
+                    raise spec["error"]
             if spec is not None and "rows" in spec:
                 # the speculative rows of the whole batch: this group's states, its variables
                 sel = [retry[j] for j in grp]
                 rows, mask = (np.ascontiguousarray(a[sel][:, :, :gv]) for a in spec["rows"])
                 prof["decide_speculative_ms"] = spec["ms"]
             else:
-                rows, mask = self._decision_rows(GB, par, seed2, ctx=ctx if on_gpu else None)
+                rows, mask = self._decision_rows(self._rows_args(GB, par), seed2, ctx=ctx if on_gpu else None)
             dec_ms += 1e3 * (time.perf_counter() - td)
             prof["decide_on_gpu"] = bool(on_gpu)
             f2, w2, _, st2 = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
@@ -762,6 +773,17 @@ class Prefilter:
         prof["decide_states"] = len(retry)
         prof["retry_sat"] = found
         SolverStatistics().gpu_retry += len(retry)
+
+
+# speculative decision-row threads still running (a batch decided in its first round does
+# not wait for its own): joined at exit, so none is inside libmgp while the process ends
+_SPECULATIVE: "weakref.WeakSet" = weakref.WeakSet()
+
+
+@atexit.register
+def _join_speculative() -> None:
+    for t in list(_SPECULATIVE):
+        t.join()
 
 
 def _sum_profiles(profs: List[dict]) -> dict:

@@ -432,6 +432,13 @@ class Prefilter:
     # are a function of the state alone (content-keyed seeds, per-state caps), so the
     # answers are those of the sequential policy (tests/test_determinism.py)
     SPECULATE_ROWS_MAX = 16
+    # a state of more than this many DAG nodes gets its decision rows in the FIRST round
+    # (seed ROWS_FIRST_SEED; the retry round draws new ones): large contract states
+    # (WalletLibrary's 600-1 500 nodes) are rarely decided by the mixture alone (148 of the
+    # corpus' 344), and their rows cost less than a second GPU round on 12-30 k-instruction
+    # programs.  A rule on the state alone (tests/fe_emulate.py restates it)
+    ROWS_FIRST_NODES = 600
+    ROWS_FIRST_SEED = 0x3C6EF372
     # pinned host staging of mgp_check_batch reserved per context (programs + tables of one
     # batch go up through it: WalletLibrary's lowered programs are ~0.45 MB each)
     HOST_STAGING = 256 << 20
@@ -457,6 +464,7 @@ class Prefilter:
         self.split_refute = self.SPLIT_REFUTE
         self.split_depth = self.SPLIT_DEPTH
         self.speculate_rows_max = self.SPECULATE_ROWS_MAX
+        self.rows_first_nodes = self.ROWS_FIRST_NODES
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # the pipeline's pinned host staging and candidate block, sized once here instead of
         # on the first large batch (pinning a few hundred MB of host memory takes tens of ms)
@@ -591,8 +599,12 @@ class Prefilter:
             self.last_profile = _sum_profiles(profs)
             return res, sorted(refuted)
         prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
+        td = time.perf_counter()
+        xrows = self._first_round_rows(B, parents, ctx)
+        if xrows is not None:
+            prof["rows_first_ms"] = 1e3 * (time.perf_counter() - td)
         spec = self._speculate_rows(B, parents)
-        first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute)
+        first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute, xrows=xrows)
         self.last_times = times
         for k, name in enumerate(("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")):
             prof[name] = float(times[k])
@@ -688,6 +700,20 @@ class Prefilter:
         rows, mask, _ = self._N.decision_rows(*packed, gv, seed2, self.decide_rows, rps, state_keys=keys, ctx=ctx,
                                               seeds=seeds, seed_rows=self.seed_rows)
         return rows, mask
+
+    def _first_round_rows(self, B, parents, ctx):
+        """Decision rows of B's states above rows_first_nodes nodes (None if there are none),
+        for the first round's mixture rows."""
+        if self.decide_rows <= 0 or self.rows_first_nodes <= 0 or B.n_states == 0:
+            return None
+        big = np.diff(B.node_off) > self.rows_first_nodes
+        if not big.any():
+            return None
+        packed, gv, rps, keys, seeds = self._rows_args(B, parents)
+        rps = np.where(big, rps, 0).astype(np.uint8)
+        seed1 = (self.seed + self.ROWS_FIRST_SEED) & (2 ** 64 - 1)
+        on_gpu = self._decide_on_gpu(int(big.sum()))
+        return self._decision_rows((packed, gv, rps, keys, seeds), seed1, ctx=ctx if on_gpu else None)
 
     def _speculate_rows(self, B, parents):
         """Start the decision rows of every state of a small batch on a host thread, on

@@ -35,6 +35,28 @@ def host_round(B, n_cand, seed, dom=None, xrows=None):
     return f
 
 
+def first_round_rows(B, seed, parents=None, decide_rows: int = 4, seed_rows: int = 0x3):
+    """Prefilter._first_round_rows restated: decision rows (seed + ROWS_FIRST_SEED) of the
+    states above ROWS_FIRST_NODES nodes, parent-seeded like the retry round's; None if none."""
+    from mythril_amd import solver as SV
+
+    big = np.diff(B.node_off) > SV.Prefilter.ROWS_FIRST_NODES
+    if not big.any():
+        return None
+    fake = type("P", (), {"decide_rows": decide_rows, "decide_max_units": SV.Prefilter.DECIDE_MAX_UNITS,
+                          "DECIDE_MIN_ROWS": SV.Prefilter.DECIDE_MIN_ROWS})()
+    rps = np.where(big, SV.Prefilter.rows_per_state(fake, B), 0).astype(np.uint8)
+    gv = max(1, B.n_vars())
+    seeds = None
+    if parents is not None and any(p is not None for p in parents):
+        seeds = F.seed_arrays(B, parents)
+        if seeds[0].shape[1] != gv:
+            seeds = None
+    rows, mask, _ = N.decision_rows(*B.packed(decide=True), gv, (seed + SV.Prefilter.ROWS_FIRST_SEED) & (2 ** 64 - 1),
+                                    decide_rows, rps, state_keys=B.state_key, seeds=seeds, seed_rows=seed_rows)
+    return rows, mask
+
+
 def apply_xrows(B, cands, rows, mask, first_row=2):
     """Host restatement of mgp_fe_cands_kernel's explicit rows: mixture row k (candidate
     first_row + k) takes the masked slots of row k; pinned constants stay."""
@@ -61,7 +83,7 @@ def run(n: int = 1024, seed: int = 0x4D595448, decide_rows: int = 4, n2: int = 2
     t = time.time()
     B = F.Batch(states)
     ref, dom = N.refute_domains(*B.packed(), B.var_off)
-    f1 = host_round(B, 256, seed, dom=dom)
+    f1 = host_round(B, 256, seed, dom=dom, xrows=first_round_rows(B, seed, decide_rows=decide_rows))
     B.close()
     open_ = [i for i in range(n) if f1[i] < 0 and ref[i] != 1]
     print(f"first round: sat {int((f1 >= 0).sum())} refuted {int((ref == 1).sum())} open {len(open_)} "
@@ -128,10 +150,14 @@ def suite_answers(queries, seed: int = 0x4D595448, decide_rows: int = 4, n2: int
         c = N.make_candidates(256, nv, seed, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off, B.aliases,
                               B.const_off, B.consts, D._FIXED_LIMBS, has, var_kind=B.var_kind, dom=dom,
                               state_keys=B.state_key)
-        sv, sm = F.seed_arrays(B, [None if p is None else dict_to_witness(p) for p in par])
+        pw = [None if p is None else dict_to_witness(p) for p in par]
+        sv, sm = F.seed_arrays(B, pw)
         for s in range(B.n_states):
             m = sm[s].astype(bool)
             c[s, 0, m] = sv[s, m]
+        xr = first_round_rows(B, seed, pw, decide_rows=decide_rows, seed_rows=seed_rows)
+        if xr is not None:
+            apply_xrows(B, c, *xr)
         _, _, status = N.lower(*B.packed(gpu=True))
         f1 = coracle.first_sat(*B.packed(gpu=True), c)
         f1[status != 0] = -2

@@ -406,6 +406,11 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, ui
  * oldest first out): a retry round or a repeated query skips the lowering.  This
  * empties it (cold measurements, tests); returns the number of programs dropped. */
 uint64_t mgp_program_cache_clear(void);
+/* Lower the GPU programs of `batch` into that cache (no device work): a caller that has
+ * host work of its own before mgp_check_batch (the first-round decision rows of large
+ * states, solver.Prefilter) runs it on another thread meanwhile, and the check then finds
+ * every program lowered.  MGP_OK or the lowering's error. */
+int mgp_program_cache_warm(const mgp_fe_batch *batch);
 /* Test hook: the candidates mgp_check_batch would evaluate (no parents), device layout
  * [state][var][half][cand] of 16-byte groups, n_vars >= the batch's widest state. */
 int mgp_fe_candidates(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint32_t n_vars, uint64_t seed,

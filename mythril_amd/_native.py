@@ -115,6 +115,7 @@ def _bind(lib):
                                            _P, _P, _P, _P, _P]),
         "mgp_fe_candidates": (ctypes.c_int, [_P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _U32, _U32, _P]),
         "mgp_program_cache_clear": (_U64, []),
+        "mgp_program_cache_warm": (ctypes.c_int, [_P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -183,7 +184,13 @@ EXPORTED_SYMBOLS = (
     "mgp_pipeline_reserve",
     "mgp_fe_candidates",
     "mgp_program_cache_clear",
+    "mgp_program_cache_warm",
 )
+
+
+def program_cache_warm(batch_handle) -> None:
+    """Lower a native front-end batch's GPU programs into the program cache (host only)."""
+    _check(lib().mgp_program_cache_warm(batch_handle))
 
 
 def program_cache_clear() -> int:

@@ -320,6 +320,20 @@ uint64_t mgp_program_cache_clear(void) {
   return n;
 }
 
+int mgp_program_cache_warm(const mgp_fe_batch *B) {
+  if (!B) return MGP_E_ARG;
+  const Arr gnodes = get(B, MGP_FE_GPU_NODES), gnoff = get(B, MGP_FE_GPU_NODE_OFF), consts = get(B, MGP_FE_CONSTS),
+            coff = get(B, MGP_FE_CONST_OFF);
+  const uint32_t n_states = (uint32_t)(gnoff.n ? gnoff.n - 1 : 0);
+  if (n_states == 0) return MGP_OK;
+  static const uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  U32Buf words;
+  std::vector<uint64_t> offs;
+  std::vector<uint8_t> status;
+  return lower_cached((const mgp_node *)gnodes.p, (const uint64_t *)gnoff.p, n_states,
+                      consts.n ? (const uint32_t *)consts.p : zero8, (const uint64_t *)coff.p, words, offs, status);
+}
+
 void mgp_pipeline_release(mgp_ctx *ctx) {
   std::unique_ptr<PipeBufs> b;
   {

@@ -713,7 +713,25 @@ class Prefilter:
         rps = np.where(big, rps, 0).astype(np.uint8)
         seed1 = (self.seed + self.ROWS_FIRST_SEED) & (2 ** 64 - 1)
         on_gpu = self._decide_on_gpu(int(big.sum()))
-        return self._decision_rows((packed, gv, rps, keys, seeds), seed1, ctx=ctx if on_gpu else None)
+        out: dict = {}
+
+        def work():
+            try:
+                out["rows"] = self._decision_rows((packed, gv, rps, keys, seeds), seed1, ctx=ctx if on_gpu else None)
+            except BaseException as e:
+                out["error"] = e
+
+        # the rows on a host thread while this one lowers the batch's programs into the
+        # program cache (mgp_program_cache_warm): mgp_check_batch then finds them lowered
+        t = threading.Thread(target=work, name="mgp-first-round-rows", daemon=True)
+        t.start()
+        try:
+            self._N.program_cache_warm(B._h)
+        finally:
+            t.join()
+        if "error" in out:
+            raise out["error"]
+        return out["rows"]
 
     def _speculate_rows(self, B, parents):
         """Start the decision rows of every state of a small batch on a host thread, on

@@ -73,3 +73,21 @@ def test_product_has_no_oracle_dependency():
                 src = open(os.path.join(dirpath, f)).read()
                 assert "from oracle" not in src and "import oracle" not in src, f
                 assert "liboracle" not in src, f
+
+
+def test_program_cache_warm_lowers_each_distinct_program_once():
+    """mgp_program_cache_warm (host only) puts one program per distinct GPU node list in the
+    cache that mgp_check_batch reads; a second warm of the same batch adds none."""
+    import corpus
+    from mythril_amd import _native as N
+    from mythril_amd import front as F
+
+    cs = [c[1] for c in corpus.corpus(48)]
+    B = F.Batch(cs + cs[:5])
+    n, no, c, co = B.packed(gpu=True)
+    distinct = {bytes(n[no[i]:no[i + 1]].tobytes()) + bytes(c[co[i]:co[i + 1]].tobytes()) for i in range(len(no) - 1)}
+    N.program_cache_clear()
+    N.program_cache_warm(B._h)
+    N.program_cache_warm(B._h)
+    assert N.program_cache_clear() == len(distinct)
+    B.close()

@@ -426,12 +426,15 @@ class Prefilter:
     # calls) and costs ~7x the split time of the states that reach it
     SPLIT_REFUTE = 8
     SPLIT_DEPTH = 2
-    # a batch of at most this many states computes the decision rows of all its states on a
-    # host thread while its first round runs (the host is idle during the GPU wait of a
-    # small batch); the retry round then takes the rows of its open states from them.  Rows
-    # are a function of the state alone (content-keyed seeds, per-state caps), so the
-    # answers are those of the sequential policy (tests/test_determinism.py)
-    SPECULATE_ROWS_MAX = 16
+    # a batch of at most this many states can compute the decision rows of all its states
+    # on a host thread while its first round runs; the retry round then takes the rows of
+    # its open states from them.  Rows are a function of the state alone, so the answers
+    # are those of the sequential policy.  Off by default: once large states get their rows
+    # in the first round, the thread's unused rows compete with the next call (A/B in one
+    # process, profiles/fe_spec_ab_r4.json: 1-state calls 0.93 -> 1.66 ms, 2 WalletLibrary
+    # states 7.96 -> 7.05 ms)
+    SPECULATE_ROWS_MAX = 0
+    SMALL_BATCH = 16   # at most this many states: the first-round rows overlap the lowering
     # a state of more than this many DAG nodes gets its decision rows in the FIRST round
     # (seed ROWS_FIRST_SEED; the retry round draws new ones): large contract states
     # (WalletLibrary's 600-1 500 nodes) are rarely decided by the mixture alone (148 of the
@@ -721,14 +724,22 @@ class Prefilter:
             except BaseException as e:
                 out["error"] = e
 
-        # the rows on a host thread while this one lowers the batch's programs into the
-        # program cache (mgp_program_cache_warm): mgp_check_batch then finds them lowered
+        if B.n_states > self.SMALL_BATCH:
+            # a large batch keeps every host thread busy in either stage: run them in turn
+            # (two OpenMP teams on the same cores slowed the 128-state call 36 -> 75 ms)
+            return work() or self._rows_or_raise(out)
+        # a small batch: the rows on a host thread while this one lowers the batch's programs
+        # into the program cache (mgp_program_cache_warm); mgp_check_batch then finds them
         t = threading.Thread(target=work, name="mgp-first-round-rows", daemon=True)
         t.start()
         try:
             self._N.program_cache_warm(B._h)
         finally:
             t.join()
+        return self._rows_or_raise(out)
+
+    @staticmethod
+    def _rows_or_raise(out: dict):
         if "error" in out:
             raise out["error"]
         return out["rows"]

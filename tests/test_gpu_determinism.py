@@ -88,8 +88,8 @@ def test_answers_do_not_depend_on_the_batch(clean):
 
 
 def test_speculative_rows_answer_like_sequential(clean):
-    """Batches of <= SPECULATE_ROWS_MAX states compute every state's decision rows on a
-    host thread while the first round runs; the retry round takes its open states' rows
+    """With speculate_rows_max = 16 (off by default), batches of <= 16 states compute every
+    state's decision rows on a host thread while the first round runs; the retry round takes its open states' rows
     from them.  The answers and witnesses equal the sequential policy's, on small batches
     whose states need the retry round (WalletLibrary) and on mixed ones, with and without
     parent witnesses."""
@@ -97,7 +97,7 @@ def test_speculative_rows_answer_like_sequential(clean):
     wal = [c[1] for c in C if c[0].startswith("wallet")][:12]
     mixed = [c[1] for c in C[:16]]
     on, off = SV.Prefilter(0), SV.Prefilter(0)
-    off.speculate_rows_max = 0
+    on.speculate_rows_max, off.speculate_rows_max = 16, 0
     try:
         for batch in (wal[:2], wal, mixed, mixed[:5]):
             SV.unsat_cores().reset()

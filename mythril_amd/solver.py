@@ -442,6 +442,10 @@ class Prefilter:
     # programs.  A rule on the state alone (tests/fe_emulate.py restates it)
     ROWS_FIRST_NODES = 600
     ROWS_FIRST_SEED = 0x3C6EF372
+    # rows per large state in the first round: rows 0 and 1 (parent-seeded, the second the
+    # greedy select-branch row) decide all 344 large corpus states, as four do, for 60 % of
+    # the time; the retry round still gets DECIDE_ROWS
+    ROWS_FIRST_ROWS = 2
     # pinned host staging of mgp_check_batch reserved per context (programs + tables of one
     # batch go up through it: WalletLibrary's lowered programs are ~0.45 MB each)
     HOST_STAGING = 256 << 20
@@ -698,10 +702,11 @@ class Prefilter:
             seeds = tuple(np.array(a, copy=True) for a in seeds)
         return packed, gv, self.rows_per_state(GB), keys, seeds
 
-    def _decision_rows(self, args, seed2, ctx=None):
+    def _decision_rows(self, args, seed2, ctx=None, n_rows=None):
         packed, gv, rps, keys, seeds = args
-        rows, mask, _ = self._N.decision_rows(*packed, gv, seed2, self.decide_rows, rps, state_keys=keys, ctx=ctx,
-                                              seeds=seeds, seed_rows=self.seed_rows)
+        n_rows = self.decide_rows if n_rows is None else n_rows
+        rows, mask, _ = self._N.decision_rows(*packed, gv, seed2, n_rows, np.minimum(rps, n_rows).astype(np.uint8),
+                                              state_keys=keys, ctx=ctx, seeds=seeds, seed_rows=self.seed_rows)
         return rows, mask
 
     def _first_round_rows(self, B, parents, ctx):
@@ -720,7 +725,8 @@ class Prefilter:
 
         def work():
             try:
-                out["rows"] = self._decision_rows((packed, gv, rps, keys, seeds), seed1, ctx=ctx if on_gpu else None)
+                out["rows"] = self._decision_rows((packed, gv, rps, keys, seeds), seed1, ctx=ctx if on_gpu else None,
+                                                  n_rows=min(self.decide_rows, self.ROWS_FIRST_ROWS))
             except BaseException as e:
                 out["error"] = e
 

@@ -536,11 +536,12 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
   return d.run(max_passes ? max_passes : 16u);
 }
 
-// refute_one, then one level of case splitting (failed-literal probing): each open
-// condition of a select (BV ITE / BITE), nearest the root first, at most max_splits of
-// them, is assumed true and false in turn on a copy of the analysis; both refuted -> the
-// state is refuted; one refuted -> the other polarity holds and is kept for the next
-// probes.  Sound: the two assumptions cover every model.
+// refute_one, then case splitting (failed-literal probing, nested): each open condition of
+// a select (BV ITE / BITE), nearest the root first, at most max_splits of them, is assumed
+// true and false in turn on a copy of the analysis, and each branch is probed again on the
+// others down to `depth` levels; both branches refuted -> refuted; one refuted -> the other
+// polarity holds and is kept for the next probes at that level.  Sound: the two assumptions
+// cover every model of the state they split.
 int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t max_passes,
                      uint32_t max_splits) {
   // max_splits: atoms per level in bits 0..15, levels in bits 16..19 (0 = 1)

@@ -1197,8 +1197,12 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
   }
   // the schedules are independent: in parallel when the caller runs few states
   std::vector<Lowered> tried(n_scheds);
-#pragma omp parallel for schedule(dynamic, 1) if (par_scheds && n_scheds > 1)
-  for (int k = 0; k < n_scheds; ++k) tried[k] = finish_one(S, root, max_slots, scheds[k]);
+  if (n_scheds == 1) {
+    tried[0] = finish_one(std::move(S), root, max_slots, scheds[0]);  // S is not read again
+  } else {
+#pragma omp parallel for schedule(dynamic, 1) if (par_scheds)
+    for (int k = 0; k < n_scheds; ++k) tried[k] = finish_one(S, root, max_slots, scheds[k]);
+  }
   Lowered best;
   bool have = false;
   for (int k = 0; k < n_scheds; ++k) {

@@ -17,6 +17,7 @@ import numpy as np
 from mythril_amd import _native as N
 from mythril_amd import dag as D
 from mythril_amd import front as F
+from mythril_amd import solver as SV
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -103,3 +104,27 @@ def test_rows_do_not_depend_on_thread_count(tmp_path):
         got.append(np.load(out))
     for name in ("k", "s", "r", "m", "c"):
         assert np.array_equal(got[0][name], got[1][name]), name
+
+
+def test_first_round_rows_are_a_function_of_the_state():
+    """Prefilter._first_round_rows (restated by tests/fe_emulate.first_round_rows): the
+    decision rows a large state gets in the first round are the same in any batch that
+    holds it, and small states get none (their mask rows are empty)."""
+    import corpus
+    from tests import fe_emulate as E
+
+    C = corpus.corpus(96)
+    cs = [c[1] for c in C]
+    B = F.Batch(cs)
+    rows, mask = E.first_round_rows(B, 0x4D595448)
+    big = np.diff(B.node_off) > SV.Prefilter.ROWS_FIRST_NODES
+    assert big.any() and (~big).any()
+    assert not mask[~big].any() and mask[big].any()
+    sub = [i for i in range(96) if i % 5 in (1, 3)]
+    SB = F.Batch([cs[i] for i in sub])
+    rows2, mask2 = E.first_round_rows(SB, 0x4D595448)
+    gv = rows2.shape[2]
+    assert np.array_equal(rows[sub][:, :, :gv], rows2) and np.array_equal(mask[sub][:, :, :gv], mask2)
+    assert not mask[sub][:, :, gv:].any()
+    B.close()
+    SB.close()

@@ -799,6 +799,12 @@ struct RowBuf {
   }
 };
 
+// A state given zero decision rows (rows_per_state; the first round's rows go to large
+// states only) is not analysed at all: its status is 0 and it takes no task.
+inline bool skip_prep(const uint8_t *rows_per_state, uint32_t n_decide, uint32_t st) {
+  return rows_per_state && n_decide && rows_per_state[st] == 0;
+}
+
 // Host run of mgpd::decision_row on a private copy of P's base analysis.
 template <typename Put>
 void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, Put &put,
@@ -929,6 +935,11 @@ extern "C" int mgp_decision_rows_seeded(const mgp_node *nodes, const uint64_t *n
     std::vector<Prep> prep(ce - cs);
 #pragma omp parallel for schedule(dynamic, 1)
     for (int64_t st = cs; st < (int64_t)ce; ++st) {
+      if (skip_prep(rows_per_state, n_decide, (uint32_t)st)) {  // no rows: not analysed
+        prep[st - cs].r = 0;
+        out[st] = 0;
+        continue;
+      }
       const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
       const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
       prep_state(prep[st - cs], nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes,
@@ -1061,6 +1072,11 @@ extern "C" int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes,
   std::vector<Prep> prep(n_states);
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    if (skip_prep(rows_per_state, n_decide, (uint32_t)s)) {  // as the host path
+      prep[s].r = 0;
+      out[s] = 0;
+      continue;
+    }
     const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
     const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
     prep_state(prep[s], nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, n_vars);

@@ -1067,3 +1067,15 @@ def test_case_split_depth_exhaustive_soundness():
     for st, r in zip(states, levels[3]):
         if r == 1:
             assert coracle.first_sat(*pack_states([st]), cands)[0] < 0, "refuted a satisfiable state"
+
+
+def test_refute_split_argument_range():
+    """refute_split packs the atom count (bits 0..15) and the depth (bits 16..19) into one
+    C argument: values outside them are refused before the call."""
+    import pytest
+
+    nodes, noff, consts, coff = pack_states([_transfer_chain_state(np.random.default_rng(1))])
+    for kw in ({"depth": 0}, {"depth": 16}, {"max_splits": 1 << 16}, {"max_splits": -1}):
+        with pytest.raises(ValueError):
+            N.refute_split(nodes, noff, consts, coff, **kw)
+    assert N.refute_split(nodes, noff, consts, coff, max_splits=0).tolist() == N.refute(nodes, noff, consts, coff).tolist()

@@ -730,10 +730,32 @@ class Prefilter:
             except BaseException as e:
                 out["error"] = e
 
-        if B.n_states > self.SMALL_BATCH:
+        # rows_overlap_split (A/B knob, off): a large batch's two stages concurrently on half
+        # the threads each; they tie with running in turn (profiles/fe_overlap_ab_r4.json)
+        split = getattr(self, "rows_overlap_split", False)
+        if B.n_states > self.SMALL_BATCH and not split:
             # a large batch keeps every host thread busy in either stage: run them in turn
             # (two OpenMP teams on the same cores slowed the 128-state call 36 -> 75 ms)
             return work() or self._rows_or_raise(out)
+        if B.n_states > self.SMALL_BATCH:
+            # A/B knob: the two stages concurrently on half the threads each
+            lib = self._N.lib()
+            full = lib.mgp_set_thread_omp(0)
+            half = max(1, full // 2)
+
+            def work_half():
+                lib.mgp_set_thread_omp(half)
+                work()
+
+            t = threading.Thread(target=work_half, name="mgp-first-round-rows", daemon=True)
+            t.start()
+            prev = lib.mgp_set_thread_omp(half)
+            try:
+                self._N.program_cache_warm(B._h)
+            finally:
+                lib.mgp_set_thread_omp(prev)
+                t.join()
+            return self._rows_or_raise(out)
         # a small batch: the rows on a host thread while this one lowers the batch's programs
         # into the program cache (mgp_program_cache_warm); mgp_check_batch then finds them
         t = threading.Thread(target=work, name="mgp-first-round-rows", daemon=True)

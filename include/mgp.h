@@ -250,18 +250,7 @@ int mgp_decision_rows(const mgp_node *nodes, const uint64_t *node_offsets, uint3
                       uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
                       const uint8_t *rows_per_state, uint32_t *out_rows, uint8_t *out_mask, int8_t *out);
 
-/* mgp_decision_rows with the rows computed on ctx's GPU (mgp_decide.hip: one wave per
- * (state, row) task running the same propagation code, mgp_domain.h): the states are
- * prepared on the host (base analysis, propagation graph, decision slots), packed into
- * one blob and uploaded; rows and mask come back into the host arrays.  Bit-identical
- * outputs to mgp_decision_rows (out_rows of unset slots are zeroed).  Synchronous on
- * ctx's stream. */
-int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
-                          const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
-                          uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
-                          const uint8_t *rows_per_state, uint32_t *out_rows, uint8_t *out_mask, int8_t *out);
-
-/* mgp_decision_rows / mgp_decision_rows_dev with parent seeds: seed_vals u32[n_states *
+/* mgp_decision_rows with parent seeds: seed_vals u32[n_states *
  * n_vars * 8] and seed_mask u8[n_states * n_vars] give, per variable slot, the parent
  * state's witness value (matched by slot key); decision row r with bit r of seed_rows set
  * first fixes every seeded slot to it (rolled back where the child's constraints reject
@@ -272,13 +261,6 @@ int mgp_decision_rows_seeded(const mgp_node *nodes, const uint64_t *node_offsets
                              uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
                              const uint8_t *rows_per_state, const uint32_t *seed_vals, const uint8_t *seed_mask,
                              uint32_t seed_rows, uint32_t *out_rows, uint8_t *out_mask, int8_t *out);
-int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
-                                 uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
-                                 uint32_t max_passes, uint32_t n_vars, uint64_t seed, const uint64_t *state_keys,
-                                 uint32_t n_decide, const uint8_t *rows_per_state, const uint32_t *seed_vals,
-                                 const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
-                                 uint8_t *out_mask, int8_t *out);
-
 /* Candidate assignments for the first witness round (host, OpenMP over states):
  * per state, row 0 is left for the parent witness when has_parent[s], then the
  * first hint of every variable, that row with the x == y aliases applied, then

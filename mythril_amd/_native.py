@@ -101,10 +101,6 @@ def _bind(lib):
         "mgp_decision_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _P]),
         "mgp_decision_rows_seeded": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P,
                                                     _U32, _P, _P, _P]),
-        "mgp_decision_rows_seeded_dev": (ctypes.c_int, [_P, _P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P,
-                                                        _P, _P, _U32, _P, _P, _P]),
-        "mgp_decision_rows_dev": (ctypes.c_int, [_P, _P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P,
-                                                 _P]),
         "mgp_refute_domains": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
         "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, _P, _U64,
                                             ctypes.POINTER(_P)]),
@@ -173,9 +169,7 @@ EXPORTED_SYMBOLS = (
     "mgp_guided_candidates_rows",
     "mgp_make_candidates",
     "mgp_decision_rows",
-    "mgp_decision_rows_dev",
     "mgp_decision_rows_seeded",
-    "mgp_decision_rows_seeded_dev",
     "mgp_refute_domains",
     "mgp_build_states",
     "mgp_fe_get",
@@ -314,9 +308,9 @@ def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hin
 
 def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed: int, n_decide: int,
                   rows_per_state: Optional[np.ndarray] = None, state_keys: Optional[np.ndarray] = None,
-                  max_passes: int = 0, ctx: Optional["Context"] = None, seeds=None, seed_rows: int = 0):
+                  max_passes: int = 0, seeds=None, seed_rows: int = 0):
     """mgp_decision_rows -> (rows u32 [n, n_decide, n_vars, 8], mask u8 [n, n_decide, n_vars], status i8[n]);
-    with `ctx`, mgp_decision_rows_dev: the same rows computed on ctx's GPU.  seeds = (vals u32
+    seeds = (vals u32
     [n, n_vars, 8], mask u8 [n, n_vars]): parent values the rows in `seed_rows` (a bit mask)
     fix first (mgp_decision_rows_seeded)."""
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
@@ -346,21 +340,9 @@ def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed:
         if sv.shape != (n_states, n_vars, 8) or sm.shape != (n_states, n_vars):
             raise ValueError("seeds must be (vals u32 [n_states, n_vars, 8], mask u8 [n_states, n_vars])")
         sargs = args[:11] + (_ptr(sv), _ptr(sm), seed_rows) + args[11:]
-        if ctx is not None:
-            rc = lib().mgp_decision_rows_seeded_dev(ctx._h, *sargs)
-            if rc != 0:
-                msg = lib().mgp_last_error(ctx._h)
-                raise MgpError(rc, msg.decode() if msg else "")
-        else:
-            _check(lib().mgp_decision_rows_seeded(*sargs))
+        _check(lib().mgp_decision_rows_seeded(*sargs))
         return rows, mask, out[:n_states]
-    if ctx is not None:
-        rc = lib().mgp_decision_rows_dev(ctx._h, *args)
-        if rc != 0:
-            msg = lib().mgp_last_error(ctx._h)
-            raise MgpError(rc, msg.decode() if msg else "")
-    else:
-        _check(lib().mgp_decision_rows(*args))
+    _check(lib().mgp_decision_rows(*args))
     return rows, mask, out[:n_states]
 
 

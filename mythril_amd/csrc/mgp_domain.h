@@ -1,5 +1,5 @@
-// mgp_domain.h — the abstract domain of the UNSAT pre-check and the decision rows,
-// shared by the host (mgp_refute.cpp) and the device (mgp_decide.hip).
+// mgp_domain.h — the abstract domain of the UNSAT pre-check and the decision rows
+// (host code, mgp_refute.cpp).
 //
 // Known bits x unsigned interval per BV node, truth sets per Bool node, operand-pair
 // orderings and UF congruence (DESIGN.md §4 "mgp_refute").  Everything the propagation
@@ -7,9 +7,8 @@
 // with std::vector storage (mgp_refute.cpp State::setup / build_atoms / build_graph) and
 // views it; a decision row works on its own copy of the mutable arrays (node values,
 // truth sets, variable values, pair orderings) with a bounded undo log and work list
-// (`Stack`).  The same code compiles for gfx950, so the device decision rows
-// (mgp_decide.hip, one lane per (state, row)) are bit-identical to the host's by
-// construction, not by a second implementation.
+// (`Stack`).  (Round 5: the device build of this code, one lane per (state, row), ran
+// 7x slower than 16 host threads and was removed)
 #pragma once
 #include <stdint.h>
 #include <string.h>
@@ -1485,7 +1484,7 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
   constexpr uint32_t kTries = 4;
   Stack<UndoRec> &undo_log = *d.undo;
   Stack<uint32_t> &work = *d.touched;
-  const uint32_t budget = 4u * d.n + 64u;
+    const uint32_t budget = 4u * d.n + 64u;
   if (sv && sm && row < 32u && ((seed_rows >> row) & 1u)) {
     for (uint32_t k = 0; k < P.n_slot; ++k) {
       if (!sm[P.slot[k]]) continue;

@@ -975,251 +975,3 @@ extern "C" int mgp_guided_candidates(const mgp_node *nodes, const uint64_t *node
   return mgp_guided_candidates_rows(nodes, node_offsets, n_states, consts, const_offsets, max_passes, n_cand, n_vars,
                                     seed, every, n_decide, nullptr, cands, out);
 }
-
-// ------------------------------------------------- decision rows on the device
-// mgp_decision_rows with the rows computed by mgp_decide.hip: the states are prepared
-// here (base analysis, propagation graph, decision slots: the same prep_state), packed
-// into one read-only blob, and every (state, row) task runs mgpd::decision_row on the
-// GPU in a workspace of its own.  Same outputs as mgp_decision_rows, bit for bit.
-#include <map>
-#include <mutex>
-
-#include "mgp_decide.h"
-
-extern "C" int mgp_ctx_stream(mgp_ctx *ctx, void **stream, int *device);
-extern "C" int mgp_ctx_fail(mgp_ctx *ctx, int code, const char *msg);
-
-namespace {
-
-struct ByteBlob {
-  std::vector<uint8_t> b;
-  uint64_t put(const void *p, size_t bytes) {
-    const uint64_t off = (b.size() + 15u) / 16u * 16u;
-    b.resize(off + ((bytes + 15u) / 16u) * 16u + 16u, 0);  // padded: 16-B copies never read past
-    if (bytes) memcpy(b.data() + off, p, bytes);
-    return off;
-  }
-  template <typename T>
-  uint64_t put(const std::vector<T> &v) { return put(v.data(), v.size() * sizeof(T)); }
-};
-
-struct DevGrow {
-  void *p = nullptr;
-  size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    const size_t want = std::max<size_t>(bytes + bytes / 4u, 1u << 20);
-    const hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) cap = want;
-    return e;
-  }
-};
-struct DecBufs {
-  std::mutex mu;  // held across one call's upload, launches and synchronize
-  DevGrow blob, states, tasks, ws, rows, mask, svals, smask;
-};
-std::mutex g_dec_mu;                              // guards the map only
-std::map<std::pair<int, void *>, DecBufs> g_dec;  // per (device, stream); entries never move
-
-inline uint64_t up16(uint64_t x) { return (x + 15u) / 16u * 16u; }
-
-// workspace bytes a task may take before the tasks are split over several launches
-constexpr uint64_t kWsLaunchBytes = 4ull << 30;
-
-}  // namespace
-
-extern "C" int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
-                                            uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
-                                            uint32_t max_passes, uint32_t n_vars, uint64_t seed,
-                                            const uint64_t *state_keys, uint32_t n_decide,
-                                            const uint8_t *rows_per_state, const uint32_t *seed_vals,
-                                            const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
-                                            uint8_t *out_mask, int8_t *out);
-
-extern "C" int mgp_decision_rows_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
-                                     uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
-                                     uint32_t max_passes, uint32_t n_vars, uint64_t seed, const uint64_t *state_keys,
-                                     uint32_t n_decide, const uint8_t *rows_per_state, uint32_t *out_rows,
-                                     uint8_t *out_mask, int8_t *out) {
-  return mgp_decision_rows_seeded_dev(ctx, nodes, node_offsets, n_states, consts, const_offsets, max_passes, n_vars,
-                                      seed, state_keys, n_decide, rows_per_state, nullptr, nullptr, 0u, out_rows,
-                                      out_mask, out);
-}
-
-extern "C" int mgp_decision_rows_seeded_dev(mgp_ctx *ctx, const mgp_node *nodes, const uint64_t *node_offsets,
-                                            uint32_t n_states, const uint32_t *consts, const uint64_t *const_offsets,
-                                            uint32_t max_passes, uint32_t n_vars, uint64_t seed,
-                                            const uint64_t *state_keys, uint32_t n_decide,
-                                            const uint8_t *rows_per_state, const uint32_t *seed_vals,
-                                            const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
-                                            uint8_t *out_mask, int8_t *out) {
-  if (!ctx || !node_offsets || !out || (n_states && (!nodes || !const_offsets)) ||
-      (n_states && n_decide && (!out_rows || !out_mask)) || ((seed_vals == nullptr) != (seed_mask == nullptr)))
-    return MGP_E_ARG;
-  void *stp = nullptr;
-  int dev = 0;
-  int rc = mgp_ctx_stream(ctx, &stp, &dev);
-  if (rc != MGP_OK) return rc;
-  hipStream_t st = (hipStream_t)stp;
-  const size_t rows_bytes = (size_t)n_states * n_decide * n_vars * 32u, mask_bytes = (size_t)n_states * n_decide * n_vars;
-  if (n_states && n_decide) {
-    memset(out_mask, 0, mask_bytes);
-    memset(out_rows, 0, rows_bytes);
-  }
-  std::vector<Prep> prep(n_states);
-#pragma omp parallel for schedule(dynamic, 1)
-  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
-    if (skip_prep(rows_per_state, n_decide, (uint32_t)s)) {  // as the host path
-      prep[s].r = 0;
-      out[s] = 0;
-      continue;
-    }
-    const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
-    const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
-    prep_state(prep[s], nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, n_vars);
-    out[s] = (int8_t)prep[s].r;
-  }
-  if (!n_decide || !n_states) return MGP_OK;
-  // pack the prepared states and list the tasks
-  ByteBlob B;
-  std::vector<mgp_dec_state> hdr;
-  std::vector<mgp_dec_task> tasks;
-  std::vector<uint64_t> task_ws;  // workspace bytes of each task
-  for (uint32_t s = 0; s < n_states; ++s) {
-    const Prep &P = prep[s];
-    const uint32_t rs = rows_per_state ? std::min<uint32_t>(rows_per_state[s], n_decide) : n_decide;
-    if (P.r != 0 || rs == 0) continue;
-    const State &S = P.s;
-    mgp_dec_state h;
-    memset(&h, 0, sizeof h);
-    h.nd = B.put(S.nd, (size_t)S.n * sizeof(mgp_node));
-    h.orig = (S.orig && S.orig != S.nd) ? B.put(S.orig, (size_t)S.n * sizeof(mgp_node)) : h.nd;
-    h.consts = B.put(S.consts, (size_t)S.n_consts * 32u);
-    h.n_consts = S.n_consts;
-    h.av = B.put(S.av);
-    h.bs = B.put(S.bs);
-    h.isb = B.put(S.isb);
-    h.vtie = B.put(S.vtie);
-    h.vars = B.put(S.vars);
-    h.pairs = B.put(S.pairs);
-    h.cmp_pair = B.put(S.cmp_pair);
-    h.cmp_dom = B.put(S.cmp_dom);
-    h.cmp_t = B.put(S.cmp_t);
-    h.pair_keys = B.put(S.pair_keys);
-    h.pair_idx = B.put(S.pair_idx);
-    h.ufs = B.put(S.ufs);
-    h.tien = B.put(S.tien);
-    h.ufp = B.put(S.ufp);
-    h.n_cmpn = S.n_cmpn;
-    h.n_borp = S.n_borp;
-    h.n_ufp = (uint32_t)(S.ufp.size() / 2);
-    h.uoff = B.put(S.uoff);
-    h.ulist = B.put(S.ulist);
-    h.voff = B.put(S.voff);
-    h.vlist = B.put(S.vlist);
-    h.tie_rel = B.put(S.tie_rel);
-    h.cong = B.put(S.cong);
-    h.n_cong = (uint32_t)S.cong.size();
-    h.arel = B.put(S.arel);
-    h.n_arel = (uint32_t)S.arel.size();
-    h.og = B.put(S.og);
-    h.n_og = (uint32_t)S.og.size();
-    h.inj = B.put(S.inj);
-    h.n_inj = (uint32_t)S.inj.size();
-    h.odis = B.put(S.odis);
-    h.oatom = B.put(S.oatom);
-    h.otgt = B.put(S.otgt);
-    h.slot = B.put(P.slot);
-    h.width = B.put(P.width);
-    h.node = B.put(P.node);
-    h.eqh_off = B.put(P.eqh_off);
-    h.eqh = B.put(P.eqh);
-    h.n = S.n;
-    h.n_vt = (uint32_t)S.vars.size();
-    h.n_pairs = (uint32_t)S.pairs.size();
-    h.n_ufs = (uint32_t)S.ufs.size();
-    h.n_slot = (uint32_t)P.slot.size();
-    h.ucap = undo_cap(h.n, h.n_pairs, h.n_ufs);
-    h.wcap = work_cap(h.n, h.n_pairs, h.n_ufs);
-    uint64_t o = 0;
-    h.ws_av = o;
-    o = up16(o + (uint64_t)h.n * sizeof(AV));
-    h.ws_vars = o;
-    o = up16(o + (uint64_t)h.n_vt * sizeof(AV));
-    h.ws_pairs = o;
-    o = up16(o + (uint64_t)h.n_pairs * sizeof(Pair));
-    h.ws_bs = o;
-    o = up16(o + h.n);
-    h.ws_undo = o;
-    o = up16(o + (uint64_t)h.ucap * sizeof(UndoRec));
-    h.ws_work = o;
-    o = up16(o + (uint64_t)h.wcap * 4u);
-    h.ws_bytes = o;
-    const uint32_t si = (uint32_t)hdr.size();
-    hdr.push_back(h);
-    const uint64_t tag = state_keys ? state_keys[s] : (uint64_t)s << 32;
-    for (uint32_t row = 0; row < rs; ++row) {
-      tasks.push_back(mgp_dec_task{si, row, 0, tag, ((uint64_t)s * n_decide + row) * n_vars, (uint64_t)s * n_vars});
-      task_ws.push_back(h.ws_bytes);
-    }
-  }
-  if (tasks.empty()) return MGP_OK;
-  DecBufs *Dp;
-  {
-    std::lock_guard<std::mutex> lk(g_dec_mu);
-    Dp = &g_dec[{dev, stp}];
-  }
-  DecBufs &D = *Dp;
-  std::lock_guard<std::mutex> lk(D.mu);  // contexts on other devices / streams run concurrently
-  hipError_t e = hipSetDevice(dev);
-  // launches of at most kWsLaunchBytes of workspace each
-  std::vector<std::pair<size_t, size_t>> launches;
-  uint64_t ws_max = 0;
-  for (size_t a = 0; a < tasks.size();) {
-    uint64_t o = 0;
-    size_t b = a;
-    while (b < tasks.size() && (b == a || o + task_ws[b] <= kWsLaunchBytes)) {
-      tasks[b].ws = o;
-      o += task_ws[b];
-      ++b;
-    }
-    ws_max = std::max(ws_max, o);
-    launches.emplace_back(a, b);
-    a = b;
-  }
-  if (e == hipSuccess) e = D.blob.ensure(B.b.size());
-  if (e == hipSuccess) e = D.states.ensure(hdr.size() * sizeof(mgp_dec_state));
-  if (e == hipSuccess) e = D.tasks.ensure(tasks.size() * sizeof(mgp_dec_task));
-  if (e == hipSuccess) e = D.ws.ensure(ws_max);
-  if (e == hipSuccess) e = D.rows.ensure(rows_bytes);
-  if (e == hipSuccess) e = D.mask.ensure(mask_bytes);
-  if (e == hipSuccess) e = hipMemcpyAsync(D.blob.p, B.b.data(), B.b.size(), hipMemcpyHostToDevice, st);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(D.states.p, hdr.data(), hdr.size() * sizeof(mgp_dec_state), hipMemcpyHostToDevice, st);
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(D.tasks.p, tasks.data(), tasks.size() * sizeof(mgp_dec_task), hipMemcpyHostToDevice, st);
-  const size_t sv_bytes = seed_vals ? (size_t)n_states * n_vars * 32u : 0u, sm_bytes = seed_vals ? (size_t)n_states * n_vars : 0u;
-  if (e == hipSuccess && sv_bytes) e = D.svals.ensure(sv_bytes);
-  if (e == hipSuccess && sv_bytes) e = D.smask.ensure(sm_bytes);
-  if (e == hipSuccess && sv_bytes) e = hipMemcpyAsync(D.svals.p, seed_vals, sv_bytes, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess && sv_bytes) e = hipMemcpyAsync(D.smask.p, seed_mask, sm_bytes, hipMemcpyHostToDevice, st);
-  if (e == hipSuccess) e = hipMemsetAsync(D.rows.p, 0, rows_bytes, st);
-  if (e == hipSuccess) e = hipMemsetAsync(D.mask.p, 0, mask_bytes, st);
-  static const uint32_t or_rows = or_rows_mask();
-  for (const auto &L : launches) {
-    if (e != hipSuccess) break;
-    e = mgp_launch_decide((const uint8_t *)D.blob.p, (const mgp_dec_state *)D.states.p,
-                          (const mgp_dec_task *)D.tasks.p + L.first, (uint32_t)(L.second - L.first),
-                          (uint8_t *)D.ws.p, seed, or_rows, sv_bytes ? (const uint32_t *)D.svals.p : nullptr,
-                          sv_bytes ? (const uint8_t *)D.smask.p : nullptr, seed_rows, (uint32_t *)D.rows.p,
-                          (uint8_t *)D.mask.p, st);
-  }
-  if (e == hipSuccess) e = hipMemcpyAsync(out_rows, D.rows.p, rows_bytes, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(out_mask, D.mask.p, mask_bytes, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
-  return MGP_OK;
-}

@@ -29,11 +29,9 @@ answer is `unknown`, which each caller maps exactly as the reference does.
 """
 from __future__ import annotations
 
-import atexit
 import os
 import threading
 import time
-import weakref
 from functools import lru_cache
 from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple, Union
 
@@ -410,12 +408,6 @@ class Prefilter:
     # per-state work cap of the decision rows: variables x DAG nodes x rows (a deterministic
     # count; the largest WalletLibrary state of the corpus needs 1.8 M at four rows)
     DECIDE_MAX_UNITS = 1 << 25
-    # decision rows can run on the GPU (mgp_decision_rows_dev, bit-identical to the
-    # host's): decide_on_gpu="auto" sends a retry round of at least DECIDE_GPU_MIN open
-    # states there.  The default is the host: on the box the 1 024-state corpus' 4 096
-    # row tasks take 166 ms on 16 host threads and 1 138 ms on the GPU (one sequential
-    # propagation per lane, 128-B abstract values spilled to scratch)
-    DECIDE_GPU_MIN = 64
     # decision rows seeded with the parent witness (bit mask of rows; states without a parent
     # witness decide every row unseeded)
     SEED_ROWS = 0x3
@@ -426,14 +418,6 @@ class Prefilter:
     # calls) and costs ~7x the split time of the states that reach it
     SPLIT_REFUTE = 8
     SPLIT_DEPTH = 2
-    # a batch of at most this many states can compute the decision rows of all its states
-    # on a host thread while its first round runs; the retry round then takes the rows of
-    # its open states from them.  Rows are a function of the state alone, so the answers
-    # are those of the sequential policy.  Off by default: once large states get their rows
-    # in the first round, the thread's unused rows compete with the next call (A/B in one
-    # process, profiles/fe_spec_ab_r4.json: 1-state calls 0.93 -> 1.66 ms, 2 WalletLibrary
-    # states 7.96 -> 7.05 ms)
-    SPECULATE_ROWS_MAX = 0
     SMALL_BATCH = 16   # at most this many states: the first-round rows overlap the lowering
     # a state of more than this many DAG nodes gets its decision rows in the FIRST round
     # (seed ROWS_FIRST_SEED; the retry round draws new ones): large contract states
@@ -466,11 +450,9 @@ class Prefilter:
         self.retry_cand = self.RETRY_CAND  # 0 (or <= n_cand) = no second round
         self.decide_rows = self.DECIDE_ROWS
         self.decide_max_units = self.DECIDE_MAX_UNITS
-        self.decide_on_gpu = "never"  # "never" (host), "auto" (>= DECIDE_GPU_MIN open states) or "always"
         self.seed_rows = self.SEED_ROWS
         self.split_refute = self.SPLIT_REFUTE
         self.split_depth = self.SPLIT_DEPTH
-        self.speculate_rows_max = self.SPECULATE_ROWS_MAX
         self.rows_first_nodes = self.ROWS_FIRST_NODES
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # the pipeline's pinned host staging and candidate block, sized once here instead of
@@ -491,7 +473,6 @@ class Prefilter:
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
     def close(self) -> None:
-        _join_speculative()
         for c in self.ctxs:
             c.close()
 
@@ -610,7 +591,6 @@ class Prefilter:
         xrows = self._first_round_rows(B, parents, ctx)
         if xrows is not None:
             prof["rows_first_ms"] = 1e3 * (time.perf_counter() - td)
-        spec = self._speculate_rows(B, parents)
         first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute, xrows=xrows)
         self.last_times = times
         for k, name in enumerate(("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")):
@@ -622,7 +602,7 @@ class Prefilter:
         retry = [i for i in range(len(states)) if first[i] == -1 and proven[i] != 1]
         if retry and self.retry_cand > 0:
             self._retry_round(ctx, states, retry, first, witnesses, prof,
-                              None if parents is None else [parents[i] for i in retry], spec=spec)
+                              None if parents is None else [parents[i] for i in retry])
         prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["retry_states"] = len(retry)
         left = [i for i in range(len(states)) if first[i] < 0 and proven[i] != 1]
@@ -684,29 +664,22 @@ class Prefilter:
                         np.where(units * self.DECIDE_MIN_ROWS <= self.decide_max_units, self.DECIDE_MIN_ROWS, 0))
         return rows.astype(np.uint8)
 
-    def _decide_on_gpu(self, n: int) -> bool:
-        return self.decide_on_gpu == "always" or (self.decide_on_gpu == "auto" and n >= self.DECIDE_GPU_MIN)
-
-    def _rows_args(self, GB, parents, copy=False):
+    def _rows_args(self, GB, parents):
         """The inputs of mgp_decision_rows for batch GB (parent-seeded rows when a parent
-        witness is given); copy=True detaches them from GB's native arrays."""
+        witness is given)."""
         from .front import seed_arrays
 
         gv = max(1, GB.n_vars())
         seeds = seed_arrays(GB, parents) if parents is not None and any(p is not None for p in parents) else None
         if seeds is not None and seeds[0].shape[1] != gv:
             seeds = None
-        packed = [np.array(a, copy=True) for a in GB.packed(decide=True)] if copy else list(GB.packed(decide=True))
-        keys = np.array(GB.state_key, copy=True) if copy else GB.state_key
-        if copy and seeds is not None:
-            seeds = tuple(np.array(a, copy=True) for a in seeds)
-        return packed, gv, self.rows_per_state(GB), keys, seeds
+        return list(GB.packed(decide=True)), gv, self.rows_per_state(GB), GB.state_key, seeds
 
-    def _decision_rows(self, args, seed2, ctx=None, n_rows=None):
+    def _decision_rows(self, args, seed2, n_rows=None):
         packed, gv, rps, keys, seeds = args
         n_rows = self.decide_rows if n_rows is None else n_rows
         rows, mask, _ = self._N.decision_rows(*packed, gv, seed2, n_rows, np.minimum(rps, n_rows).astype(np.uint8),
-                                              state_keys=keys, ctx=ctx, seeds=seeds, seed_rows=self.seed_rows)
+                                              state_keys=keys, seeds=seeds, seed_rows=self.seed_rows)
         return rows, mask
 
     def _first_round_rows(self, B, parents, ctx):
@@ -720,42 +693,20 @@ class Prefilter:
         packed, gv, rps, keys, seeds = self._rows_args(B, parents)
         rps = np.where(big, rps, 0).astype(np.uint8)
         seed1 = (self.seed + self.ROWS_FIRST_SEED) & (2 ** 64 - 1)
-        on_gpu = self._decide_on_gpu(int(big.sum()))
         out: dict = {}
 
         def work():
             try:
-                out["rows"] = self._decision_rows((packed, gv, rps, keys, seeds), seed1, ctx=ctx if on_gpu else None,
+                out["rows"] = self._decision_rows((packed, gv, rps, keys, seeds), seed1,
                                                   n_rows=min(self.decide_rows, self.ROWS_FIRST_ROWS))
             except BaseException as e:
                 out["error"] = e
 
-        # rows_overlap_split (A/B knob, off): a large batch's two stages concurrently on half
-        # the threads each; they tie with running in turn (profiles/fe_overlap_ab_r4.json)
-        split = getattr(self, "rows_overlap_split", False)
-        if B.n_states > self.SMALL_BATCH and not split:
-            # a large batch keeps every host thread busy in either stage: run them in turn
-            # (two OpenMP teams on the same cores slowed the 128-state call 36 -> 75 ms)
-            return work() or self._rows_or_raise(out)
         if B.n_states > self.SMALL_BATCH:
-            # A/B knob: the two stages concurrently on half the threads each
-            lib = self._N.lib()
-            full = lib.mgp_set_thread_omp(0)
-            half = max(1, full // 2)
-
-            def work_half():
-                lib.mgp_set_thread_omp(half)
-                work()
-
-            t = threading.Thread(target=work_half, name="mgp-first-round-rows", daemon=True)
-            t.start()
-            prev = lib.mgp_set_thread_omp(half)
-            try:
-                self._N.program_cache_warm(B._h)
-            finally:
-                lib.mgp_set_thread_omp(prev)
-                t.join()
-            return self._rows_or_raise(out)
+            # a large batch keeps every host thread busy in either stage: run them in turn
+            # (two OpenMP teams on the same cores slowed the 128-state call 36 -> 75 ms; on half
+            # the threads each they tied with running in turn, profiles/fe_overlap_ab_r4.json)
+            return work() or self._rows_or_raise(out)
         # a small batch: the rows on a host thread while this one lowers the batch's programs
         # into the program cache (mgp_program_cache_warm); mgp_check_batch then finds them
         t = threading.Thread(target=work, name="mgp-first-round-rows", daemon=True)
@@ -772,33 +723,7 @@ class Prefilter:
             raise out["error"]
         return out["rows"]
 
-    def _speculate_rows(self, B, parents):
-        """Start the decision rows of every state of a small batch on a host thread, on
-        copies of B's arrays (the thread never touches B, so a batch whose first round
-        decides everything returns without waiting for it); None when the batch does not
-        qualify."""
-        n = B.n_states
-        if not (0 < n <= self.speculate_rows_max and self.retry_cand > 0 and self.decide_rows > 0
-                and not self._decide_on_gpu(n)):
-            return None
-        seed2 = (self.seed + 0x7F4A7C15) & (2 ** 64 - 1)
-        spec: dict = {}
-        args = self._rows_args(B, parents, copy=True)
-
-        def work():
-            t = time.perf_counter()
-            try:
-                spec["rows"] = self._decision_rows(args, seed2)
-            except BaseException as e:  # re-raised by the retry round that needs the rows
-                spec["error"] = e
-            spec["ms"] = 1e3 * (time.perf_counter() - t)
-
-        spec["thread"] = threading.Thread(target=work, name="mgp-speculative-rows", daemon=True)
-        spec["thread"].start()
-        _SPECULATIVE.add(spec["thread"])
-        return spec
-
-    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None, parents=None, spec=None) -> None:
+    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None, parents=None) -> None:
         """The second witness round for the open states: host decision rows
         (mgp_decision_rows, each variable fixed in turn and the analysis re-propagated)
         placed in the first mixture rows of a device-generated round with a new seed.  A
@@ -825,21 +750,9 @@ class Prefilter:
             GB = SB if len(groups) == 1 else Batch([states[retry[k]] for k in grp])
             gv = max(1, GB.n_vars())
             td = time.perf_counter()
-            on_gpu = self._decide_on_gpu(len(grp))
             par = None if parents is None else [parents[j] for j in grp]
-            if spec is not None:
-                spec["thread"].join()
-                if "error" in spec:
-                    raise spec["error"]
-            if spec is not None and "rows" in spec:
-                # the speculative rows of the whole batch: this group's states, its variables
-                sel = [retry[j] for j in grp]
-                rows, mask = (np.ascontiguousarray(a[sel][:, :, :gv]) for a in spec["rows"])
-                prof["decide_speculative_ms"] = spec["ms"]
-            else:
-                rows, mask = self._decision_rows(self._rows_args(GB, par), seed2, ctx=ctx if on_gpu else None)
+            rows, mask = self._decision_rows(self._rows_args(GB, par), seed2)
             dec_ms += 1e3 * (time.perf_counter() - td)
-            prof["decide_on_gpu"] = bool(on_gpu)
             f2, w2, _, st2 = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
             round2_ms = [a + float(b) for a, b in zip(round2_ms, st2)]
             unsafe = (GB.flags & FE_SAT_UNSAFE) != 0
@@ -856,17 +769,6 @@ class Prefilter:
         prof["decide_states"] = len(retry)
         prof["retry_sat"] = found
         SolverStatistics().gpu_retry += len(retry)
-
-
-# speculative decision-row threads still running (a batch decided in its first round does
-# not wait for its own): joined at exit, so none is inside libmgp while the process ends
-_SPECULATIVE: "weakref.WeakSet" = weakref.WeakSet()
-
-
-@atexit.register
-def _join_speculative() -> None:
-    for t in list(_SPECULATIVE):
-        t.join()
 
 
 def _sum_profiles(profs: List[dict]) -> dict:

@@ -87,37 +87,6 @@ def test_answers_do_not_depend_on_the_batch(clean):
         pf.close()
 
 
-def test_speculative_rows_answer_like_sequential(clean):
-    """With speculate_rows_max = 16 (off by default), batches of <= 16 states compute every
-    state's decision rows on a host thread while the first round runs; the retry round takes its open states' rows
-    from them.  The answers and witnesses equal the sequential policy's, on small batches
-    whose states need the retry round (WalletLibrary) and on mixed ones, with and without
-    parent witnesses."""
-    C = _corpus(96)
-    wal = [c[1] for c in C if c[0].startswith("wallet")][:12]
-    mixed = [c[1] for c in C[:16]]
-    on, off = SV.Prefilter(0), SV.Prefilter(0)
-    on.speculate_rows_max, off.speculate_rows_max = 16, 0
-    try:
-        for batch in (wal[:2], wal, mixed, mixed[:5]):
-            SV.unsat_cores().reset()
-            a = off.check_states(batch)
-            SV.unsat_cores().reset()
-            b = on.check_states(batch)
-            _same_answers(a, b)
-            if len(batch) <= on.speculate_rows_max and on.last_profile.get("retry_states"):
-                assert "decide_speculative_ms" in on.last_profile
-        # parent-seeded rows: the first batch's witnesses as parents of the same states
-        par = [w if k == SV.sat else None for k, w in off.check_states(wal[:4])]
-        SV.unsat_cores().reset()
-        a = off.check_states(wal[:4], par)
-        SV.unsat_cores().reset()
-        _same_answers(a, on.check_states(wal[:4], par))
-    finally:
-        on.close()
-        off.close()
-
-
 def test_two_contexts_answer_like_one(clean):
     """Prefilter(devices=[0, 0]): two contexts on one GPU, one host thread each, states
     hash-sharded by content key -- the same answers as Prefilter(0)."""

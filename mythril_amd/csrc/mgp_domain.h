@@ -12,18 +12,37 @@
 #pragma once
 #include <stdint.h>
 #include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "../../include/mgp.h"
 #include "mgp_bv.h"
 #include "mgp_fe_sample.h"
 
-#if defined(__HIPCC__)
-#define MGP_RD __host__ __device__ inline
-#else
 #define MGP_RD inline
-#endif
 
 namespace mgpd {
+
+// Study builds only (make EXTRA=-DMGPD_TRACE_ON OUT=... OBJDIR=..., loaded through
+// MGP_LIB_PATH): MGP_DECIDE_TRACE=1 makes decision rows print their steps to stderr
+#ifdef MGPD_TRACE_ON
+inline bool trace_on() {
+  static const int t = [] { const char *e = getenv("MGP_DECIDE_TRACE"); return e ? atoi(e) : 0; }();
+  return t != 0;
+}
+#define MGPD_TRACE(...) do { if (trace_on()) fprintf(stderr, __VA_ARGS__); } while (0)
+// MGP_DECIDE_TRACE=2 also prints every narrowing of a node in [MGP_TRACE_LO, MGP_TRACE_HI]
+inline bool trace_node(int32_t i) {
+  static const int lvl = [] { const char *e = getenv("MGP_DECIDE_TRACE"); return e ? atoi(e) : 0; }();
+  static const int lo = [] { const char *e = getenv("MGP_TRACE_LO"); return e ? atoi(e) : 0; }();
+  static const int hi = [] { const char *e = getenv("MGP_TRACE_HI"); return e ? atoi(e) : -1; }();
+  return lvl >= 2 && i >= lo && i <= hi;
+}
+#else
+inline bool trace_node(int32_t) { return false; }
+inline bool trace_on() { return false; }
+#define MGPD_TRACE(...) do { } while (0)
+#endif
 
 using V = U256;
 
@@ -426,12 +445,20 @@ struct Dom {
   // decision rows: users of each node, VAR nodes of each variable entry, nodes tie() reads
   const uint32_t *uoff = nullptr, *ulist = nullptr, *voff = nullptr, *vlist = nullptr;
   const uint8_t *tie_rel = nullptr;
+  // Equality substitution (round 5): once a pair is known equal, x == y, every ordering known
+  // between x and a third node z also holds between y and z (when a compare reads (y, z)).
+  // `h_to == h_r1` next to `h_to != h_s2` then decides `h_s2 == h_r1` false: three keccak
+  // values of one Store chain that no interval separates (pairs incident to each node: CSR)
+  const uint32_t *pinc_off = nullptr, *pinc = nullptr;
   bool changed = false;
   // decision mode (decision rows only, never a refutation): backward rules may also
   // narrow to the PREFERRED part of a solution set -- e.g. the non-wrapping preimages of
   // a product -- because a decision row is only a candidate that the GPU evaluation
   // checks.  Such narrowing is unsound for a proof, so run()/refute_one never enable it.
   bool heur = false;
+  // decision mode, wrap rows only: a product narrowed from above prefers its preimages
+  // that wrap once (c * a = 2^w + r) over the non-wrapping ones
+  bool wrap_pref = false;
   // decision rows: every change can go to an undo log (a failed draw rolls back instead
   // of copying the state) and the changed nodes to a work list (a decision propagates
   // from the decided node, run_from); variable entries are listed as kVarBit | entry
@@ -457,8 +484,14 @@ struct Dom {
     t.lo = MAX(t.lo, s.lo);
     t.hi = MIN(t.hi, s.hi);
     if (same(t, av[i])) return true;  // s adds nothing (stored values are normalised)
-    if (!normalize(t, w)) return false;
+    if (!normalize(t, w)) {
+      MGPD_TRACE("  empty: node %d (op %u)\n", i, nd[i].op);
+      return false;
+    }
     if (!same(t, av[i])) {
+      if (trace_node(i))
+        fprintf(stderr, "  node %d (op %u) -> [%08x..%08x, %08x..%08x]\n", i, nd[i].op, t.lo.w[7], t.lo.w[0], t.hi.w[7],
+                t.hi.w[0]);
       if (undo) undo->push_back(UndoRec{0, (uint32_t)i, av[i], 0, 0, 0});
       if (touched) touched->push_back((uint32_t)i);
       av[i] = t;
@@ -468,8 +501,12 @@ struct Dom {
   }
   MGP_RD bool meetb(int32_t i, uint8_t s) {
     const uint8_t t = bs[i] & s;
-    if (!t) return false;
+    if (!t) {
+      MGPD_TRACE("  empty: bool node %d (op %u)\n", i, nd[i].op);
+      return false;
+    }
     if (t != bs[i]) {
+      if (trace_node(i)) fprintf(stderr, "  bool %d (op %u) -> %u\n", i, nd[i].op, t);
       if (undo) undo->push_back(UndoRec{1, (uint32_t)i, AV(), bs[i], 0, 0});
       if (touched) touched->push_back((uint32_t)i);
       bs[i] = t;
@@ -768,6 +805,36 @@ struct Dom {
     return true;
   }
 
+  MGP_RD static uint8_t mirror_order(uint8_t m) {
+    return (uint8_t)((m & OEQ) | ((m & OLT) ? OGT : 0) | ((m & OGT) ? OLT : 0));
+  }
+  MGP_RD bool substitute() {
+    for (uint32_t pj = 0; pj < n_pairs; ++pj) {
+      if (pairs[pj].u != OEQ) continue;
+      for (int side = 0; side < 2; ++side) {
+        const int32_t a = side ? pairs[pj].y : pairs[pj].x, b = side ? pairs[pj].x : pairs[pj].y;
+        for (uint32_t k = pinc_off[a]; k < pinc_off[a + 1]; ++k) {
+          const uint32_t qk = pinc[k];
+          if (qk == pj) continue;
+          const Pair &q = pairs[qk];
+          const int32_t z = q.x == a ? q.y : q.x;
+          if (z == b) continue;
+          // orderings of a vs z (the pair stores x vs y)
+          const uint8_t mu = q.x == a ? q.u : mirror_order(q.u), ms = q.x == a ? q.s : mirror_order(q.s);
+          if (mu == OALL && ms == OALL) continue;
+          const int32_t lo = b < z ? b : z, hi = b < z ? z : b;
+          const int32_t pi = pair_find(((uint64_t)(uint32_t)lo << 32) | (uint32_t)hi);
+          if (pi < 0) continue;
+          Pair &t = pairs[pi];  // b vs z when t.x == b
+          const bool fw = t.x == b;
+          if (!set_order(t, 0, fw ? mu : mirror_order(mu)) || !set_order(t, 1, fw ? ms : mirror_order(ms)))
+            return false;
+        }
+      }
+    }
+    return true;
+  }
+
   MGP_RD bool tie() {
     for (uint32_t k = 0; k < n_og; ++k)
       if (!or_hull(og[k])) return false;
@@ -836,6 +903,7 @@ struct Dom {
       }
       if (!meet(lo_n, a) || !meet(hi_n, b)) return false;
     }
+    if (pinc_off && !substitute()) return false;
     for (uint32_t q = 0; q < n_ufp; ++q) {
       const uint32_t i = ufp[2 * q], j = ufp[2 * q + 1];
       if (!arg_equal(ufs[i].arg, ufs[j].arg, 3)) continue;
@@ -845,6 +913,10 @@ struct Dom {
       const int32_t pi = pair_find(((uint64_t)(uint32_t)(x < y ? x : y) << 32) | (uint32_t)(x < y ? y : x));
       if (pi >= 0 && !set_order(pairs[pi], 2, OEQ)) return false;
     }
+    // the pairs this call made equal (two keccak values required equal by a decided read)
+    // change no value when both are intervals, so no later round would revisit them:
+    // equate their preimages now
+    if (n_inj && !injective()) return false;
     return true;
   }
 
@@ -1255,6 +1327,26 @@ struct Dom {
             const AV B = av[q];
             if (!is_exact(B) || Z(B.lo) || is_exact(av[p])) continue;
             V lo, hi, rl, rh;
+            if (wrap_pref && LT(ONE(), B.lo) && LT(av[i].hi, SUBV(M(w), B.lo))) {
+              // a wrap row: the preimages that wrap once, c * a = 2^w + r (r in [R.lo, R.hi]),
+              // a = q0 + (r0 + 1 + r) / c with 2^w - 1 = q0 * c + r0
+              V q0, r0;
+              bv_udivrem(M(w), B.lo, &q0, &r0);
+              bv_udivrem(ADDV(ADDV(r0, ONE()), av[i].lo), B.lo, &lo, &rl);
+              if (!Z(rl)) lo = ADDV(lo, ONE());
+              bv_udivrem(ADDV(ADDV(r0, ONE()), av[i].hi), B.lo, &hi, &rh);
+              lo = ADDV(q0, lo);
+              hi = ADDV(q0, hi);
+              if (!LT(hi, lo) && !LT(M(w), hi)) {
+                AV t = top(w);
+                t.lo = lo;
+                t.hi = hi;
+                if (compatible(p, t)) {
+                  if (!meet(p, t)) return false;
+                  continue;
+                }
+              }
+            }
             bv_udivrem(av[i].lo, B.lo, &lo, &rl);
             if (!Z(rl)) lo = ADDV(lo, ONE());
             bv_udivrem(av[i].hi, B.lo, &hi, &rh);
@@ -1383,14 +1475,14 @@ struct Dom {
   // evaluations (a node with many users, e.g. calldatasize under every byte guard, counts
   // each of them).  1 = the decision empties a domain.  Only decision rows use it
   // (candidates, checked on the GPU); refutations run().
-  MGP_RD int run_from(uint32_t seed, uint32_t budget) {
+  MGP_RD int run_from(uint32_t seed, uint32_t budget, int rounds = 3) {
     Stack<uint32_t> &T = *touched;
     T.clear();
     T.push_back(seed);
     size_t head = 0;
     uint32_t work = 0;
     bool need_tie = false;
-    for (int round = 0; round < 3; ++round) {
+    for (int round = 0; round < rounds; ++round) {
       while (head < T.size()) {
         const uint32_t t = T[head++];
         if (t & kVarBit) {  // a variable's shared value changed: every VAR node of it
@@ -1459,6 +1551,16 @@ constexpr uint32_t kOrRowsDefault = 0xAu;
 // the split row whose ITE branch split always tries the then-branch first
 constexpr uint32_t kIteGreedyRow = 1u;
 
+// rows that start with the wrap decisions (bit r: row r)
+#ifndef MGP_WRAP_ROWS
+#define MGP_WRAP_ROWS 0xCu
+#endif
+constexpr uint32_t kWrapRows = MGP_WRAP_ROWS;
+constexpr int kSplitRounds = 8;
+#ifndef SPLIT_BUDGET_X
+#define SPLIT_BUDGET_X 16u
+#endif
+
 // Decision row `row` of a prepared state on `d`, a private copy of the state's base
 // analysis (heur set, undo log and work list attached): each variable slot in turn is
 // fixed to a draw from its current abstract value and the analysis re-propagated from
@@ -1482,9 +1584,14 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
                          uint32_t or_rows, Put &put, const uint32_t *sv = nullptr, const uint8_t *sm = nullptr,
                          uint32_t seed_rows = 0) {
   constexpr uint32_t kTries = 4;
+  MGPD_TRACE("=== row %u\n", row);
   Stack<UndoRec> &undo_log = *d.undo;
   Stack<uint32_t> &work = *d.touched;
     const uint32_t budget = 4u * d.n + 64u;
+  // the case splits (wrap pairs, Or and ITE branches) are few and steer the whole row: a
+  // split whose consequences are cut short by the budget leaves a contradiction that every
+  // later draw runs into, so they propagate further
+  const uint32_t split_budget = SPLIT_BUDGET_X * d.n + 64u;
   if (sv && sm && row < 32u && ((seed_rows >> row) & 1u)) {
     for (uint32_t k = 0; k < P.n_slot; ++k) {
       if (!sm[P.slot[k]]) continue;
@@ -1512,6 +1619,64 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
   // of the host time)
   const uint8_t kFirst8[8] = {0, 4, 6, 8, 2, 10, 12, 14};
   const uint32_t drow = row < 8u ? kFirst8[row] : row < 16u ? 2u * (row - 8u) + 1u : row;
+  // Wrap decisions (round 5).  A required wrap -- Not(BVAddNoOverflow(a, b)) or
+  // Not(BVMulNoOverflow(a, b)) (integer.py:141-160), or r = a + b ordered below an operand
+  // (SafeMath.add's assert(c >= a) failing, BECToken.sol:25-29) -- is met first by a wrapping
+  // pair of operand values: a + b = 2^w by (2^(w-1), 2^(w-1)) or by an operand's upper bound and
+  // its complement, a * b >= 2^w by (2, 2^(w-1)).  The choice propagates back through whatever
+  // supplies the operands: an exact 2^255 balance read excludes every store of a small constant
+  // from its Store chain, so the row aims at the state in which an earlier transaction's
+  // product wrapped (CVE-2018-10299: batchTransfer with cnt = 2, value = 2^255).  Random draws
+  // almost never produce such pairs.  A pair that empties a domain is rolled back.
+  if (row < 32u && ((kWrapRows >> row) & 1u)) {
+    bool over = false;
+    auto try_pair = [&](int32_t a, int32_t b, const V &va, const V &vb) -> bool {
+      const uint32_t w = d.W(a);
+      if (!inside_av(d.av[a], va) || !inside_av(d.av[b], vb)) return false;
+      const uint32_t mark = undo_log.size();
+      work.clear();
+      bool ok = d.meet(a, exact(va, w)) && d.run_from((uint32_t)a, split_budget, kSplitRounds) == 0 && !undo_log.over;
+      if (ok) {
+        work.clear();
+        ok = d.meet(b, exact(vb, w)) && d.run_from((uint32_t)b, split_budget, kSplitRounds) == 0 && !undo_log.over;
+      }
+      MGPD_TRACE("row %u wrap pair nodes %d %d (w %u): %s\n", row, a, b, w, ok ? "kept" : "rolled back");
+      if (ok) {
+        undo_log.clear();
+        d.wrap_pref = true;  // the row now aims at a wrapped state: products prefer wrapping
+        return true;
+      }
+      over = undo_log.over;
+      if (!over) d.rollback(mark);
+      return false;
+    };
+    auto wrap = [&](int32_t a, int32_t b, bool mul) {
+      if (a < 0 || b < 0 || is_exact(d.av[a]) || is_exact(d.av[b])) return;
+      const uint32_t w = d.W(a);
+      if (w < 2u || w != d.W(b)) return;
+      const V h = BIT(w - 1u), m = M(w);
+      if (mul) {
+        const V two = bv_small(2u);
+        if (try_pair(a, b, two, h) || over || try_pair(a, b, h, two)) return;
+        return;
+      }
+      if (try_pair(a, b, h, h) || over) return;
+      const V ah = d.av[a].hi, bh = d.av[b].hi;
+      if (!Z(ah) && (try_pair(a, b, ah, bv_mask(ADDV(SUBV(m, ah), ONE()), w)) || over)) return;
+      if (!Z(bh)) try_pair(a, b, bv_mask(ADDV(SUBV(m, bh), ONE()), w), bh);
+    };
+    for (uint32_t i = d.n; i-- > 0 && !over;) {
+      const mgp_node &x = d.nd[i];
+      if ((x.op == MGP_OP_UADD_NOOVF || x.op == MGP_OP_UMUL_NOOVF) && d.bs[i] == BF && !d.isb[x.a])
+        wrap(x.a, x.b, x.op == MGP_OP_UMUL_NOOVF);
+    }
+    for (uint32_t k = 0; k < d.n_arel && !over; ++k) {
+      const ArithRel &e = d.arel[k];
+      if (e.op == MGP_OP_ADD && (d.known_order(e.r, e.a) == OLT || d.known_order(e.r, e.b) == OLT))
+        wrap(e.a, e.b, false);
+    }
+    if (over) return;
+  }
   if (row < 32u && ((or_rows >> row) & 1u)) {
     // case split on the disjunctions the root requires: from the root down, a required Or
     // with both operands open takes its first operand (else its second) before any
@@ -1521,11 +1686,17 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
       if (d.nd[i].op != MGP_OP_BOR || d.bs[i] != BT) continue;
       const int32_t a = d.nd[i].a, b = d.nd[i].b;
       if (a < 0 || b < 0 || d.bs[a] != BB || d.bs[b] != BB) continue;
+      // a row aiming at a wrapped state leaves a ULE / UGE (Or(ULT, ==) on one operand pair,
+      // bitvec_helper.py:53-80) whole: splitting it would drop the boundary value (a transfer
+      // of a whole balance, value == bal, as the overflow witness needs); other rows split it
+      // too, and the strict side first bounds a balance read away from its zero default
+      if (d.wrap_pref && d.cmp_pair[a] >= 0 && d.cmp_pair[a] == d.cmp_pair[b]) continue;
       for (int side = 0; side < 2; ++side) {
         const int32_t pick = side ? b : a;
         const uint32_t mark = undo_log.size();
         work.clear();
-        if (d.meetb(pick, BT) && d.run_from((uint32_t)pick, budget) == 0 && !undo_log.over) {
+        if (d.meetb(pick, BT) && d.run_from((uint32_t)pick, split_budget, kSplitRounds) == 0 && !undo_log.over) {
+          MGPD_TRACE("row %u or node %u takes side %d\n", row, i, side);
           undo_log.clear();
           break;
         }
@@ -1544,19 +1715,27 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
   // choose per node by the row's stream, and either way a choice that empties a domain
   // is rolled back and the other side taken.  Without it a read of m_ownerIndex[k] after
   // m_ownerIndex[sender] = 1 needs k == sender, which no independent draw of k gives.
-  if (row < 32u && ((or_rows >> row) & 1u)) {
+  const bool wrap_row = row < 32u && ((kWrapRows >> row) & 1u);
+  if (row < 32u && (((or_rows >> row) & 1u) || wrap_row)) {
     for (uint32_t i = d.n; i-- > 0;) {
       const mgp_node &x = d.nd[i];
+      if (x.op == MGP_OP_ITE && x.a >= 0 && d.bs[x.a] == BB && trace_on() && !d.ite_required(i) && !is_top(d.av[i], x.width))
+        MGPD_TRACE("row %u ite node %u open, narrowed, not required (then %d else %d)\n", row, i, x.b, x.c);
       if (x.op != MGP_OP_ITE || x.a < 0 || d.bs[x.a] != BB || !d.ite_required(i)) continue;
-      const bool then_first = row == kIteGreedyRow || ((fe_mix64(seed ^ fe_mix64(tag ^ i ^ ((uint64_t)row << 40))) >> 17) & 1u);
+      // (a wrap row takes the latest store first: a value required past the old state comes
+      // from the writes of the transactions before, not from the initial storage)
+      const bool then_first = row == kIteGreedyRow || wrap_row ||
+                              ((fe_mix64(seed ^ fe_mix64(tag ^ i ^ ((uint64_t)row << 40))) >> 17) & 1u);
       for (int side = 0; side < 2; ++side) {
         const uint8_t want = (side == 0) == then_first ? BT : BF;
         const uint32_t mark = undo_log.size();
         work.clear();
-        if (d.meetb(x.a, want) && d.run_from((uint32_t)x.a, budget) == 0 && !undo_log.over) {
+        if (d.meetb(x.a, want) && d.run_from((uint32_t)x.a, split_budget, kSplitRounds) == 0 && !undo_log.over) {
+          MGPD_TRACE("row %u ite node %u takes %s\n", row, i, want == BT ? "then" : "else");
           undo_log.clear();
           break;
         }
+        MGPD_TRACE("row %u ite node %u: %s fails\n", row, i, want == BT ? "then" : "else");
         if (undo_log.over) return;
         d.rollback(mark);
       }
@@ -1600,6 +1779,7 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
     }
     V v = bv_zero();
     const uint32_t h0 = P.eqh_off[k], nh = P.eqh_off[k + 1] - h0;
+    MGPD_TRACE("row %u draw slot %u (node %d)\n", row, P.slot[k], nk);
     for (uint32_t t = 0; t < kTries + nh; ++t) {
       if (t < nh) {
         v = P.eqh[h0 + (t + drow + (drow < 8u ? 0u : (uint32_t)(key >> 40))) % nh];

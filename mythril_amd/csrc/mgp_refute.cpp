@@ -51,6 +51,8 @@ struct State {
   const mgp_node *nd;
   std::vector<mgp_node> relaxed;  // nd when the DAG holds wide values (relax_wide)
   const mgp_node *orig = nullptr;  // the DAG before relax_wide (UF arguments, congruence)
+  std::vector<mgp_node> origx;     // orig + the piece-expansion nodes relax_wide appended
+  std::vector<uint32_t> xconsts;   // the constant pool + the pieces' zero (when one is needed)
   uint32_t n;
   const uint32_t *consts;
   uint64_t n_consts;
@@ -79,6 +81,7 @@ struct State {
   std::vector<int32_t> pair_idx;
   std::vector<uint32_t> uoff, ulist, voff, vlist;  // users of each node; VAR nodes of each entry
   std::vector<uint8_t> tie_rel;  // nodes tie() reads: compares with a pair, BOR, pair operands
+  std::vector<uint32_t> pinc_off, pinc;  // pairs incident to each node (Dom::substitute)
 
   uint32_t W(int32_t i) const { return nd[i].width; }
 
@@ -124,6 +127,8 @@ struct State {
     d.voff = voff.data();
     d.vlist = vlist.data();
     d.tie_rel = tie_rel.data();
+    d.pinc_off = pinc_off.data();
+    d.pinc = pinc.data();
     return d;
   }
 
@@ -340,6 +345,21 @@ struct State {
       pair_keys.push_back(e.first);
       pair_idx.push_back(e.second);
     }
+    // pairs incident to each node, for equality substitution
+    pinc_off.assign(n + 1, 0u);
+    for (const Pair &p : pairs) {
+      pinc_off[p.x + 1]++;
+      pinc_off[p.y + 1]++;
+    }
+    for (uint32_t i = 0; i < n; ++i) pinc_off[i + 1] += pinc_off[i];
+    pinc.assign(pinc_off[n], 0u);
+    {
+      std::vector<uint32_t> at(pinc_off.begin(), pinc_off.end() - 1);
+      for (uint32_t k = 0; k < pairs.size(); ++k) {
+        pinc[at[pairs[k].x]++] = k;
+        pinc[at[pairs[k].y]++] = k;
+      }
+    }
   }
 
   // The BOR trees for Dom::or_hull: maximal BOR trees (a BOR that is no operand of another
@@ -480,7 +500,298 @@ inline bool op_bool_result(uint8_t op) {
          op == MGP_OP_TRUE || op == MGP_OP_FALSE;
 }
 
-bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out) {
+// Piece expansion (round 5).  The relaxation above loses every constraint that passes
+// through a wide value -- in particular the keccak manager's `key == func_input` between a
+// mapping access's 512-bit Concat(key, slot) and a concrete key (keccak_function_manager.py:
+// 146), so neither the refuter nor the decision rows could use a mapping key's equality
+// with a known key.  A wide value built from narrow parts (CONCAT, EXTRACT, ZEXT, ITE, a
+// wide constant's pool entries, a wide variable's or UF value's consecutive slots) is a
+// list of narrow pieces, low bits first; nodes appended after the original ones hold them:
+//   * a wide EQ e becomes BEQ(e, AND of the piece EQs), cut at the union of both sides'
+//     piece boundaries (EXTRACTs where a piece is split);
+//   * a narrow node that reads a wide value (an EXTRACT out of a Concat) becomes
+//     EQ(node, its value rebuilt from pieces);
+// and the root becomes the conjunction of the old root with these ties.  Each tie states
+// the node's exact meaning in the original DAG, so the expanded DAG is still a relaxation
+// of the original formula (UF values stay free): refutations stay sound.  The original
+// node indices are unchanged (the decision slots, the UF and injectivity tables and the
+// refuter's domain export read them); `orig` is extended by the appended nodes.
+namespace {
+struct Piece {
+  int32_t node;   // a narrow node (original or appended)
+  uint16_t lo, w; // bits [lo, lo + w) of that node
+};
+
+struct Expander {
+  const mgp_node *nd;
+  uint64_t n;
+  std::vector<mgp_node> &out;
+  std::vector<uint32_t> &xc;      // extended constant pool (limbs); empty = the original pool
+  const uint32_t *consts;
+  uint64_t n_consts;
+  std::vector<int8_t> state;      // per original node: 0 unknown, 1 expandable, -1 not
+  std::vector<std::vector<Piece>> memo;
+  int32_t zero_pool = -1;
+  std::unordered_map<uint64_t, int32_t> made;  // (op, a, params) of appended leaf / extract nodes
+  static constexpr size_t kMaxPieces = 64;
+
+  bool is_wide(int32_t j) const { return nd[j].width > MGP_MAX_WIDTH && !op_bool_result(nd[j].op); }
+
+  int32_t append(const mgp_node &x) {
+    out.push_back(x);
+    return (int32_t)out.size() - 1;
+  }
+  int32_t leaf(uint8_t op, uint16_t w, uint32_t p0) {
+    const uint64_t key = ((uint64_t)op << 56) ^ ((uint64_t)w << 40) ^ p0;
+    auto it = made.find(key);
+    if (it != made.end()) return it->second;
+    mgp_node x{};
+    x.op = op;
+    x.width = w;
+    x.a = x.b = x.c = -1;
+    x.p0 = p0;
+    return made[key] = append(x);
+  }
+  int32_t zero(uint16_t w) {
+    if (zero_pool < 0) {
+      if (xc.empty()) xc.assign(consts, consts + 8ull * n_consts);
+      zero_pool = (int32_t)(xc.size() / 8);
+      xc.insert(xc.end(), 8, 0u);
+    }
+    return leaf(MGP_OP_CONST, w, (uint32_t)zero_pool);
+  }
+  // the node holding piece p exactly (an EXTRACT when p is part of its node)
+  int32_t mat(const Piece &p) {
+    if (p.lo == 0 && p.w == out[p.node].width) return p.node;
+    const uint64_t key = (1ull << 63) ^ ((uint64_t)p.node << 24) ^ ((uint64_t)p.lo << 12) ^ p.w;
+    auto it = made.find(key);
+    if (it != made.end()) return it->second;
+    mgp_node x{};
+    x.op = MGP_OP_EXTRACT;
+    x.width = p.w;
+    x.a = p.node;
+    x.b = x.c = -1;
+    x.p0 = (uint32_t)(p.lo + p.w - 1u);
+    x.p1 = p.lo;
+    return made[key] = append(x);
+  }
+  // bits [lo, lo + w) of a piece list
+  static bool slice(const std::vector<Piece> &s, uint32_t lo, uint32_t w, std::vector<Piece> &r) {
+    uint32_t at = 0;
+    for (const Piece &p : s) {
+      const uint32_t a = std::max(at, lo), b = std::min(at + p.w, lo + w);
+      if (a < b) r.push_back(Piece{p.node, (uint16_t)(p.lo + (a - at)), (uint16_t)(b - a)});
+      at += p.w;
+    }
+    return r.size() <= kMaxPieces;
+  }
+  // two piece lists of one total width cut at the union of their boundaries
+  static void align(const std::vector<Piece> &x, const std::vector<Piece> &y, std::vector<Piece> &ax,
+                    std::vector<Piece> &ay) {
+    size_t i = 0, j = 0;
+    uint32_t ox = 0, oy = 0;  // offsets consumed within x[i], y[j]
+    while (i < x.size() && j < y.size()) {
+      const uint32_t w = std::min<uint32_t>(x[i].w - ox, y[j].w - oy);
+      ax.push_back(Piece{x[i].node, (uint16_t)(x[i].lo + ox), (uint16_t)w});
+      ay.push_back(Piece{y[j].node, (uint16_t)(y[j].lo + oy), (uint16_t)w});
+      ox += w;
+      oy += w;
+      if (ox == x[i].w) { ++i; ox = 0; }
+      if (oy == y[j].w) { ++j; oy = 0; }
+    }
+  }
+  // the pieces of original node j (low bits first); false = not built from narrow parts
+  bool pieces(int32_t j, std::vector<Piece> &r) {
+    if (j < 0 || (uint64_t)j >= n) return false;
+    if (state[j] == -1) return false;
+    if (state[j] == 1) {
+      r = memo[j];
+      return true;
+    }
+    state[j] = -1;
+    std::vector<Piece> s;
+    const mgp_node &x = nd[j];
+    bool ok = false;
+    if (!is_wide(j)) {
+      // a narrow node: itself, unless it reads a wide value (then relaxed in `out`; rebuilt)
+      const bool reads_wide = (x.a >= 0 && is_wide(x.a)) || (x.b >= 0 && is_wide(x.b)) || (x.c >= 0 && is_wide(x.c));
+      if (!reads_wide || x.op == MGP_OP_UFAPP || x.op == MGP_OP_UFINV) {
+        // (a narrow UF value read through a wide argument is its relaxed fresh value)
+        s.push_back(Piece{j, 0, x.width});
+        ok = true;
+      } else if (x.op == MGP_OP_EXTRACT) {
+        std::vector<Piece> a;
+        ok = pieces(x.a, a) && slice(a, x.p1, x.width, s);
+      }
+    } else {
+      const uint32_t w = x.width;
+      switch (x.op) {
+        case MGP_OP_CONCAT: {
+          std::vector<Piece> a, b;
+          ok = pieces(x.b, b) && pieces(x.a, a);
+          if (ok) {
+            s = b;
+            s.insert(s.end(), a.begin(), a.end());
+          }
+          break;
+        }
+        case MGP_OP_EXTRACT: {
+          std::vector<Piece> a;
+          ok = pieces(x.a, a) && slice(a, x.p1, w, s);
+          break;
+        }
+        case MGP_OP_ZEXT: {
+          ok = pieces(x.a, s);
+          for (uint32_t at = nd[x.a].width; ok && at < w; at += MGP_MAX_WIDTH)
+            s.push_back(Piece{zero((uint16_t)std::min<uint32_t>(MGP_MAX_WIDTH, w - at)), 0,
+                              (uint16_t)std::min<uint32_t>(MGP_MAX_WIDTH, w - at)});
+          break;
+        }
+        case MGP_OP_CONST:
+          if (x.p0 + (w + 255u) / 256u <= n_consts) {
+            for (uint32_t k = 0; k * 256u < w; ++k) {
+              const uint16_t pw = (uint16_t)std::min<uint32_t>(256u, w - 256u * k);
+              s.push_back(Piece{leaf(MGP_OP_CONST, pw, x.p0 + k), 0, pw});
+            }
+            ok = true;
+          }
+          break;
+        case MGP_OP_VAR: case MGP_OP_UFINV: case MGP_OP_UFAPP: {
+          // a wide variable or fresh UF value: consecutive slots from p0 (VAR) / p1 (UF)
+          const uint32_t base = x.op == MGP_OP_VAR ? x.p0 : x.p1;
+          for (uint32_t k = 0; k * 256u < w; ++k) {
+            const uint16_t pw = (uint16_t)std::min<uint32_t>(256u, w - 256u * k);
+            s.push_back(Piece{leaf(MGP_OP_VAR, pw, base + k), 0, pw});
+          }
+          ok = true;
+          break;
+        }
+        case MGP_OP_ITE: {
+          std::vector<Piece> b, c, ab, ac;
+          if (!(pieces(x.b, b) && pieces(x.c, c))) break;
+          align(b, c, ab, ac);
+          if (ab.size() > kMaxPieces) break;
+          for (size_t k = 0; k < ab.size(); ++k) {
+            mgp_node t{};
+            t.op = MGP_OP_ITE;
+            t.width = ab[k].w;
+            t.a = x.a;  // a narrow Bool condition (relaxed DAG: unchanged)
+            t.b = mat(ab[k]);
+            t.c = mat(ac[k]);
+            s.push_back(Piece{append(t), 0, ab[k].w});
+          }
+          ok = true;
+          break;
+        }
+        default: break;  // wide arithmetic: stays relaxed
+      }
+    }
+    if (!ok || s.size() > kMaxPieces) return false;
+    state[j] = 1;
+    memo[j] = s;
+    r = s;
+    return true;
+  }
+};
+}  // namespace
+
+bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out, const uint32_t *consts = nullptr,
+                uint64_t n_consts = 0, std::vector<mgp_node> *orig_out = nullptr,
+                std::vector<uint32_t> *xconsts = nullptr);
+
+bool relax_wide_narrow(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out);
+
+bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out, const uint32_t *consts,
+                uint64_t n_consts, std::vector<mgp_node> *orig_out, std::vector<uint32_t> *xconsts) {
+  if (!relax_wide_narrow(nd, n, out)) return false;
+  if (!orig_out || !xconsts) return true;
+  // piece expansion: ties appended after the relaxed DAG (see above)
+  std::vector<uint32_t> &xc = *xconsts;
+  xc.clear();
+  Expander E{nd, n, out, xc, consts, n_consts, std::vector<int8_t>(n, 0), std::vector<std::vector<Piece>>(n), -1, {}};
+  std::vector<int32_t> ties;
+  for (uint64_t i = 0; i < n; ++i) {
+    const mgp_node &x = nd[i];
+    const bool wa = x.a >= 0 && E.is_wide(x.a), wb = x.b >= 0 && E.is_wide(x.b);
+    if (x.op == MGP_OP_EQ && wa && wb && nd[x.a].width == nd[x.b].width) {
+      std::vector<Piece> pa, pb, aa, ab;
+      if (!E.pieces(x.a, pa) || !E.pieces(x.b, pb)) continue;
+      Expander::align(pa, pb, aa, ab);
+      if (aa.empty() || aa.size() > Expander::kMaxPieces) continue;
+      int32_t conj = -1;
+      for (size_t k = 0; k < aa.size(); ++k) {
+        const int32_t l = E.mat(aa[k]), r = E.mat(ab[k]);
+        mgp_node q{};
+        q.op = MGP_OP_EQ;
+        q.width = 1;
+        q.a = l;
+        q.b = r;
+        q.c = -1;
+        int32_t e = E.append(q);
+        if (conj >= 0) {
+          mgp_node t{};
+          t.op = MGP_OP_BAND;
+          t.width = 1;
+          t.a = conj;
+          t.b = e;
+          t.c = -1;
+          e = E.append(t);
+        }
+        conj = e;
+      }
+      mgp_node t{};
+      t.op = MGP_OP_BEQ;
+      t.width = 1;
+      t.a = (int32_t)i;
+      t.b = conj;
+      t.c = -1;
+      ties.push_back(E.append(t));
+    } else if (!E.is_wide((int32_t)i) && !op_bool_result(x.op) && x.op == MGP_OP_EXTRACT && wa) {
+      std::vector<Piece> p;
+      if (!E.pieces((int32_t)i, p) || p.empty() || p.size() > Expander::kMaxPieces) continue;
+      // rebuild the value: CONCAT of the pieces, high piece first
+      int32_t v = E.mat(p[0]);
+      uint32_t vw = p[0].w;
+      for (size_t k = 1; k < p.size(); ++k) {
+        mgp_node t{};
+        t.op = MGP_OP_CONCAT;
+        t.width = (uint16_t)(vw + p[k].w);
+        t.a = E.mat(p[k]);
+        t.b = v;
+        t.c = -1;
+        v = E.append(t);
+        vw += p[k].w;
+      }
+      mgp_node q{};
+      q.op = MGP_OP_EQ;
+      q.width = 1;
+      q.a = (int32_t)i;
+      q.b = v;
+      q.c = -1;
+      ties.push_back(E.append(q));
+    }
+  }
+  if (ties.empty()) {
+    out.resize(n);
+    xc.clear();
+    return true;
+  }
+  int32_t root = (int32_t)n - 1;
+  for (int32_t t : ties) {
+    mgp_node b{};
+    b.op = MGP_OP_BAND;
+    b.width = 1;
+    b.a = root;
+    b.b = t;
+    b.c = -1;
+    root = E.append(b);
+  }
+  orig_out->assign(nd, nd + n);
+  orig_out->insert(orig_out->end(), out.begin() + (int64_t)n, out.end());
+  return true;
+}
+
+bool relax_wide_narrow(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out) {
   auto wide = [&](int32_t j) { return j >= 0 && (uint64_t)j < n && nd[j].width > MGP_MAX_WIDTH &&
                                       !op_bool_result(nd[j].op); };
   bool any = false;
@@ -526,7 +837,15 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
   State st;
   State &s = keep ? *keep : st;
   s.orig = nd;
-  if (relax_wide(nd, n, s.relaxed)) nd = s.relaxed.data();
+  if (relax_wide(nd, n, s.relaxed, consts, n_consts, &s.origx, &s.xconsts)) {
+    nd = s.relaxed.data();
+    n = s.relaxed.size();
+    if (!s.origx.empty()) s.orig = s.origx.data();
+    if (!s.xconsts.empty()) {
+      consts = s.xconsts.data();
+      n_consts = s.xconsts.size() / 8u;
+    }
+  }
   s.nd = nd;
   s.n = (uint32_t)n;
   s.consts = consts;

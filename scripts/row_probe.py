@@ -116,8 +116,14 @@ def main():
     ref = N.refute(*B.packed())
     print("refute:", int(ref[0]), "decision status:", int(st[0]), "vars:", B.n_vars(0))
     st_dag = D.build_state(terms)
+    # the rows as mgp_check_batch places them (mixture rows 2.., pinned constants kept)
+    from tests import fe_emulate as E
+    cand = N.make_candidates(n_rows + 2, nv, 0x1234, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off,
+                             B.aliases, B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(1, np.uint8),
+                             var_kind=B.var_kind, state_keys=B.state_key)
+    E.apply_xrows(B, cand, rows, mask)
     for r in range(n_rows):
-        c = rows[0, r].copy()
+        c = cand[0, 2 + r].copy()
         ok = coracle.first_sat(*B.packed(gpu=True), c[None, None])[0]
         first_bad = None
         if ok != 0:
@@ -130,7 +136,7 @@ def main():
                 if not S.eval_root(sd.nodes, sd.consts, D.model_to_slots(sd, model)):
                     first_bad = k
                     break
-            if first_bad is not None and "--explain" in sys.argv and r == 0:
+            if first_bad is not None and "--explain" in sys.argv and r == int(os.environ.get("ROW", "0")):
                 vals = S.eval_dag(st_dag.nodes, st_dag.consts, D.model_to_slots(st_dag, model))
                 explain(terms, first_bad, vals, node_index(terms), depth=int(os.environ.get("DEPTH", "4")))
         print(f"row {r}: {'SAT' if ok == 0 else 'no'}  first violated conjunct {first_bad}  "

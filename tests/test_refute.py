@@ -163,8 +163,9 @@ def test_unsupported_and_empty():
 
 def test_wide_values_are_relaxed_soundly():
     """512-bit mapping preimages (include/mgp_ir.h "wide values") are relaxed to fresh
-    variables: the narrow contradiction next to them is still refuted, and nothing that
-    depends on the wide part is."""
+    variables and then tied back piecewise (mgp_refute.cpp piece expansion, round 5): the
+    narrow contradiction next to them is refuted, a contradiction that runs through the
+    pieces of a wide equality is refuted too, and the satisfiable case is not."""
     # Concat(x0, 0) as keccak256_512 argument, inverse result compared with the preimage
     mapping = [X0, X1, [S.CONST, 256, -1, -1, -1, 0, 0], [S.CONCAT, 512, 0, 2, -1, 0, 0],
                [S.UFAPP, 256, 3, -1, -1, 9, 2], [S.UFINV, 512, 4, -1, -1, 9, 3], [S.EQ, 1, 5, 3, -1, 0, 0],
@@ -175,11 +176,11 @@ def test_wide_values_are_relaxed_soundly():
     sat = mapping + [[S.CONST, 256, -1, -1, -1, 1, 0], [S.ULT, 1, 0, 9, -1, 0, 0],
                      [S.BAND, 1, 6, 10, -1, 0, 0], [S.BAND, 1, 11, 8, -1, 0, 0]]
     # contradictory only through the wide part (inv == Concat(x0, 0) but its high word
-    # != x0): the relaxation cannot see it, so it is left to the fallback solver
+    # != x0): the piece expansion equates inv's high piece with x0 and refutes it
     wide_only = mapping + [[S.EQ, 1, 7, 0, -1, 0, 0], [S.BNOT, 1, 9, -1, -1, 0, 0], [S.BAND, 1, 6, 10, -1, 0, 0]]
     out = _refute([(unsat, [0, 5]), (sat, [0, 5]), (wide_only, [0, 5]),
                    ([[S.VAR, 512, -1, -1, -1, 0, 0], [S.EQ, 1, 0, 0, -1, 0, 0]], [])])
-    assert list(out) == [1, 0, 0, 0]
+    assert list(out) == [1, 0, 1, 0]
     # sat: x0 = 1, x1 = x0 (the inverse returns the preimage), fresh values unused
     xs = [1, 1, 77, 0, 0, 0]
     assert S.eval_root(sat, [0, 5], xs)

@@ -320,7 +320,8 @@ MGP_RD AV flip(const AV &a, uint32_t w) {
 enum : uint8_t { OLT = 1, OEQ = 2, OGT = 4, OALL = 7 };
 constexpr uint32_t kVarBit = 0x80000000u;  // a work-list entry naming a variable-table entry
 constexpr uint32_t kUfGroup = 48;          // UF congruence: functions with at most this many applications
-constexpr int kCongDepth = 4;              // structural congruence: operator levels arg_equal looks through
+constexpr int kCongDepth = 4;
+constexpr int kChainBudget = 256;          // rel_under steps per pair (Dom::chain_orders)              // structural congruence: operator levels arg_equal looks through
 
 struct Pair { int32_t x, y; uint8_t u, s; };
 struct UfApp { int32_t node, arg; uint32_t fn; uint8_t op; };
@@ -788,6 +789,162 @@ struct Dom {
     return rx != x || ry != y ? arg_equal(rx, ry, kCongDepth) : false;
   }
 
+  // ---------------------------------------------------------- select-chain relation
+  // Path-sensitive ordering of x against z (round 5): the unsigned orderings {<, =, >} of x
+  // vs z that any model can give, following BV ITEs down both branches under the assumption
+  // their condition makes (an `a == b` condition: a and b equal on the then-path, different
+  // on the else-path), through x + 0, x - 0, x | 0, x ^ 0 and one function's applications
+  // on arguments equal under those assumptions.  A Store chain read of balances[ATTACKER]
+  // after zero-value transfers is then `=` to the starting balance on every path, which
+  // refutes ether_thief's `balance > starting` (ether_thief.py:55-95) however many
+  // transfers the chain holds -- the case split (refute_split) runs out of levels first.
+  struct Asm { int32_t p, q; uint8_t eq; };
+  static constexpr int kMaxAsm = 24;
+  // x's exact value, directly or through an assumed equality with an exact node
+  // the nodes assumed equal to x (x first), transitively over the equality assumptions
+  MGP_RD int eq_class(int32_t x, const Asm *as, int na, int32_t *cl) const {
+    int nc = 0;
+    cl[nc++] = x;
+    for (bool grew = true; grew;) {
+      grew = false;
+      for (int k = 0; k < na; ++k) {
+        if (!as[k].eq) continue;
+        bool hp = false, hq = false;
+        for (int j = 0; j < nc; ++j) {
+          hp |= cl[j] == as[k].p;
+          hq |= cl[j] == as[k].q;
+        }
+        if (hp != hq && nc < kMaxAsm + 1) {
+          cl[nc++] = hp ? as[k].q : as[k].p;
+          grew = true;
+        }
+      }
+    }
+    return nc;
+  }
+  MGP_RD bool value_under(int32_t x, const Asm *as, int na, V &v) const {
+    if (is_exact(av[x])) { v = av[x].lo; return true; }
+    int32_t cl[kMaxAsm + 1];
+    const int nc = eq_class(x, as, na, cl);
+    for (int j = 1; j < nc; ++j)
+      if (is_exact(av[cl[j]])) { v = av[cl[j]].lo; return true; }
+    return false;
+  }
+  // truth of p == q under the assumptions: BT, BF or BB
+  MGP_RD uint8_t eq_under(int32_t p, int32_t q, const Asm *as, int na, int depth) const {
+    if (p == q) return BT;
+    if (na) {
+      int32_t cp[kMaxAsm + 1], cq[kMaxAsm + 1];
+      const int np = eq_class(p, as, na, cp), nq = eq_class(q, as, na, cq);
+      for (int j = 1; j < np; ++j)
+        if (cp[j] == q) return BT;
+      for (int k = 0; k < na; ++k) {  // a disequality between the two classes
+        if (as[k].eq) continue;
+        bool ap = false, aq = false, bp = false, bq = false;
+        for (int j = 0; j < np; ++j) { ap |= cp[j] == as[k].p; bp |= cp[j] == as[k].q; }
+        for (int j = 0; j < nq; ++j) { aq |= cq[j] == as[k].p; bq |= cq[j] == as[k].q; }
+        if ((ap && bq) || (bp && aq)) return BF;
+      }
+    }
+    if (nd[p].width != nd[q].width || isb[p] || isb[q]) return BB;
+    V vp, vq;
+    const bool kp = value_under(p, as, na, vp), kq = value_under(q, as, na, vq);
+    if (kp && kq) return EQV(vp, vq) ? BT : BF;
+    if (kp && !inside_dom(av[q], vp)) return BF;
+    if (kq && !inside_dom(av[p], vq)) return BF;
+    const uint8_t o = known_order(p, q);
+    if (o == OEQ) return BT;
+    if (!(o & OEQ)) return BF;
+    if (depth > 0) {  // one function's applications on arguments equal under the assumptions
+      const mgp_node *og = orig ? orig : nd;
+      const mgp_node &a = og[p], &b = og[q];
+      if (a.op == MGP_OP_UFAPP && b.op == MGP_OP_UFAPP && a.p0 == b.p0 && a.a >= 0 && b.a >= 0 &&
+          og[a.a].width <= MGP_MAX_WIDTH && og[a.a].width == og[b.a].width &&
+          eq_under(a.a, b.a, as, na, depth - 1) == BT)
+        return BT;
+    }
+    return dec_eq(av[p], av[q]);
+  }
+  MGP_RD static bool inside_dom(const AV &a, const V &v) {
+    return !LT(v, a.lo) && !LT(a.hi, v) && Z(AND(v, a.z)) && EQV(AND(v, a.o), a.o);
+  }
+  MGP_RD uint8_t cond_under(int32_t c, const Asm *as, int na) const {
+    if (bs[c] == BT || bs[c] == BF) return bs[c];
+    if (nd[c].op == MGP_OP_EQ && !isb[nd[c].a]) {
+      const uint8_t r = eq_under(nd[c].a, nd[c].b, as, na, 2);
+      MGPD_TRACE("  cond %d = EQ(%d, %d) under %d assumptions: %u (exact %d %d)\n", c, nd[c].a, nd[c].b, na, r,
+                 (int)is_exact(av[nd[c].a]), (int)is_exact(av[nd[c].b]));
+      return r;
+    }
+    return BB;
+  }
+  MGP_RD bool zero_under(int32_t x, const Asm *as, int na) const {
+    V v;
+    return value_under(x, as, na, v) && Z(v);
+  }
+  MGP_RD uint8_t rel_under(int32_t x, int32_t z, Asm *as, int na, int &budget) const {
+    if (--budget < 0) return OALL;
+    for (int hop = 0; hop < 64; ++hop) {
+      if (x == z) return OEQ;
+      const mgp_node &t = nd[x];
+      if (t.op == MGP_OP_ITE && t.a >= 0) {
+        const uint8_t c = cond_under(t.a, as, na);
+        if (c == BT) { x = t.b; continue; }
+        if (c == BF) { x = t.c; continue; }
+        const bool eqc = nd[t.a].op == MGP_OP_EQ && !isb[nd[t.a].a] && na < kMaxAsm;
+        uint8_t r = 0;
+        for (int side = 0; side < 2; ++side) {
+          int m = na;
+          if (eqc) as[m++] = Asm{nd[t.a].a, nd[t.a].b, (uint8_t)(side == 0)};
+          r |= rel_under(side == 0 ? t.b : t.c, z, as, m, budget);
+          if (r == OALL) return OALL;
+        }
+        return r;
+      }
+      if ((t.op == MGP_OP_ADD || t.op == MGP_OP_OR || t.op == MGP_OP_XOR) && t.a >= 0 && t.b >= 0) {
+        if (zero_under(t.b, as, na)) { x = t.a; continue; }
+        if (zero_under(t.a, as, na)) { x = t.b; continue; }
+      } else if (t.op == MGP_OP_SUB && t.b >= 0 && zero_under(t.b, as, na)) {
+        x = t.a;
+        continue;
+      }
+      break;
+    }
+    if (x == z) return OEQ;
+    // a leaf: equal under the assumptions (a value, one function on equal arguments), else
+    // what the pair orderings and the intervals allow
+    const uint8_t e = nd[x].width == nd[z].width && !isb[x] && !isb[z] ? eq_under(x, z, as, na, 2) : BB;
+    if (e == BT) return OEQ;
+    uint8_t r = known_order(x, z);
+    if (e == BF) r &= (uint8_t)~OEQ;
+    const AV &X = av[x], &Zv = av[z];
+    if (!LT(X.lo, Zv.hi)) r &= (uint8_t)~OLT;  // x < z needs x.lo < z.hi
+    if (!LT(Zv.lo, X.hi)) r &= (uint8_t)~OGT;
+    if (LT(X.hi, Zv.lo) || LT(Zv.hi, X.lo)) r &= (uint8_t)~OEQ;
+    MGPD_TRACE("  rel leaf %d (op %u) vs %d: eq %u -> %u (assumptions %d)\n", x, nd[x].op, z, e, r, na);
+    return r;
+  }
+  // the pairs whose operand is an open select chain: their orderings from rel_under
+  MGP_RD bool chain_orders() {
+    for (uint32_t pj = 0; pj < n_pairs; ++pj) {
+      Pair &p = pairs[pj];
+      const bool cx = nd[p.x].op == MGP_OP_ITE && bs[nd[p.x].a] == BB;
+      const bool cy = nd[p.y].op == MGP_OP_ITE && bs[nd[p.y].a] == BB;
+      if (!cx && !cy) continue;
+      Asm as[kMaxAsm];
+      int budget = kChainBudget;
+      uint8_t r = OALL;  // each side that is a chain, walked against the other (both sound)
+      if (cx) r &= rel_under(p.x, p.y, as, 0, budget);
+      if (cy) {
+        budget = kChainBudget;
+        r &= mirror_order(rel_under(p.y, p.x, as, 0, budget));
+      }
+      MGPD_TRACE("chain pair %d %d: u %u -> rel %u (budget left %d)\n", p.x, p.y, p.u, r, budget);
+      if (r != OALL && !set_order(p, 0, r)) return false;
+    }
+    return true;
+  }
+
   MGP_RD bool injective() {
     for (uint32_t i = 0; i < n_inj; ++i) {
       if (bs[inj[i].eq] != BT) continue;
@@ -870,11 +1027,13 @@ struct Dom {
     // value aliases (refutation only: the decision rows keep their propagation cost):
     // a compare of a balance read through zero-value transfers and decided ITEs against
     // the starting balance of the same account compares one value with itself
-    if (!heur)
+    if (!heur) {
       for (uint32_t pj = 0; pj < n_pairs; ++pj) {
         Pair &p = pairs[pj];
         if (p.u != OEQ && same_value(p.x, p.y) && !set_order(p, 2, OEQ)) return false;
       }
+      if (!chain_orders()) return false;
+    }
     for (uint32_t k = 0; k < n_arel; ++k)
       if (!arith_rel(arel[k])) return false;
     for (uint32_t pj = 0; pj < n_pairs; ++pj) {

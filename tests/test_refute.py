@@ -1080,3 +1080,54 @@ def test_refute_split_argument_range():
         with pytest.raises(ValueError):
             N.refute_split(nodes, noff, consts, coff, **kw)
     assert N.refute_split(nodes, noff, consts, coff, max_splits=0).tolist() == N.refute(nodes, noff, consts, coff).tolist()
+
+
+def _balance_chain_state(rng, w=2):
+    """A balances array through 3-5 transfers (corpus.laser's transfer_ether on the laser.smt
+    mirror: Store chains of `b[to] = b[to] + v`, `b[from] = b[from] - v`, values mostly 0)
+    and ether_thief's `b[a] > start[a]` (ether_thief.py:55-95) or its `==` / `<` variants,
+    on w-bit addresses: the shapes Dom::chain_orders walks."""
+    from mythril_amd import smt
+    from mythril_amd.dag import build_state
+
+    sym = smt.symbol_factory
+    addrs = [sym.BitVecSym(f"a{k}", w) for k in range(3)]
+    zero = sym.BitVecVal(0, w)
+    amt = sym.BitVecSym("amt", w)
+    bal = smt.Array("bal", w, w)
+    start = __import__("copy").copy(bal)
+    cons = []
+    for _ in range(int(rng.integers(3, 6))):
+        frm, to = (addrs[int(i)] for i in rng.choice(3, 2, replace=False))
+        v = zero if rng.random() < 0.8 else amt
+        bal[to] = bal[to] + v
+        bal[frm] = bal[frm] - v
+        if rng.random() < 0.3:
+            cons.append(frm == addrs[int(rng.integers(3))])
+    a = addrs[int(rng.integers(3))]
+    op = int(rng.integers(3))
+    cons.append(smt.UGT(bal[a], start[a]) if op == 0 else (smt.ULT(bal[a], start[a]) if op == 1 else
+                                                              smt.Not(bal[a] == start[a])))
+    st = build_state([c.raw for c in cons])
+    return (st.nodes, st.consts), st.n_vars
+
+
+def test_chain_orders_exhaustive_soundness():
+    """Path-sensitive select-chain orderings (round 5, Dom::chain_orders): every state the
+    plain pre-check refutes is checked over all assignments of its addresses, amount and
+    base-read values (C oracle, equal reads of one array equal), and the plain pre-check
+    now refutes the zero-value transfer chains that needed a split per transfer."""
+    rng = np.random.default_rng(0xC4A1)
+    states = [_balance_chain_state(rng) for _ in range(160)]
+    verdict = _refute([s for s, _ in states])
+    refuted = 0
+    for ((nl, cl), n_vars), r in zip(states, verdict):
+        assert r in (0, 1)
+        if r != 1:
+            continue
+        refuted += 1
+        grid = np.array(np.meshgrid(*[np.arange(4)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
+        cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+        cands[0, :, :, 0] = grid
+        assert coracle.first_sat(*pack_states([(nl, cl)]), cands)[0] < 0, "refuted a satisfiable state"
+    assert refuted > 30, refuted

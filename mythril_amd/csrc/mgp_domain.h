@@ -639,7 +639,8 @@ struct Dom {
       if (wrap < 0) return true;
       if (e.flag >= 0 && !meetb(e.flag, wrap ? BF : BT)) return false;
       const uint8_t m = wrap ? (uint8_t)OLT : (uint8_t)(OGT | OEQ);
-      return order(e.r, e.a, m) && order(e.r, e.b, m);
+      if (!order(e.r, e.a, m) || !order(e.r, e.b, m)) return false;
+      return sum_bounds(e, wrap == 1);
     }
     int udf = -1;  // r = a - b underflows iff b >u a
     const uint8_t ab = known_order(e.a, e.b);
@@ -656,7 +657,51 @@ struct Dom {
     }
     if (udf < 0) return true;
     if (!order(e.a, e.b, udf ? (uint8_t)OLT : (uint8_t)(OGT | OEQ))) return false;
-    return order(e.r, e.a, udf ? (uint8_t)OGT : (uint8_t)(OLT | OEQ));
+    if (!order(e.r, e.a, udf ? (uint8_t)OGT : (uint8_t)(OLT | OEQ))) return false;
+    return sum_bounds(e, udf == 1);
+  }
+  // The interval of r = a + b (a - b) once its wrap status is known (round 5): without a wrap
+  // r lies in [a.lo + b.lo, a.hi + b.hi] ([a.lo - b.hi, a.hi - b.lo]), with one it is that
+  // range shifted by 2^w, where av_add / av_sub give up as soon as the operand ranges straddle
+  // the wrap.  SafeMath's asserts (BECToken.sol:20-29) fix the status, so a balance that went
+  // through `sub` and `add` keeps a bound and a later overflow test against it is decided.
+  MGP_RD bool sum_bounds(const ArithRel &e, bool wrapped) {
+    const uint32_t w = nd[e.r].width;
+    const AV &A = av[e.a], &B = av[e.b];
+    const V m = M(w);
+    V lo, hi;
+    if (e.op == MGP_OP_ADD) {
+      uint32_t c1 = 0, c2 = 0;
+      lo = bv_add(A.lo, B.lo, &c1);
+      hi = bv_add(A.hi, B.hi, &c2);
+      if (w < 256u) {  // carries out of bit w-1
+        c1 = !Z(AND(lo, NOT(m)));
+        c2 = !Z(AND(hi, NOT(m)));
+      }
+      if (!wrapped) {
+        if (c1) return false;             // even the smallest sum wraps
+        if (c2) hi = m;                   // the largest would: cap at 2^w - 1
+      } else {
+        if (!c2) return false;            // even the largest sum does not wrap
+        if (!c1) lo = bv_zero();          // the smallest would not: from 0
+      }
+    } else {
+      const bool b1 = LT(A.lo, B.hi), b2 = LT(A.hi, B.lo);  // borrows of lo - hi, hi - lo
+      lo = SUBV(A.lo, B.hi);
+      hi = SUBV(A.hi, B.lo);
+      if (!wrapped) {
+        if (b2) return false;
+        if (b1) lo = bv_zero();
+      } else {
+        if (!b1) return false;
+        if (!b2) hi = m;
+      }
+    }
+    AV t = top(w);
+    t.lo = bv_mask(lo, w);
+    t.hi = bv_mask(hi, w);
+    if (LT(t.hi, t.lo)) return true;  // (masking a capped bound: leave it to the other rules)
+    return meet(e.r, t);
   }
 
   // narrow [lo, hi] of node t by compare atom k (a compare of t with an exact node);
@@ -1162,7 +1207,12 @@ struct Dom {
         break;
       }
       case MGP_OP_ADD: r = av_add(*A, *B, w); break;
-      case MGP_OP_SUB: r = av_sub(*A, *B, w); break;
+      case MGP_OP_SUB:
+        // x - x = 0, also when the operands resolve to one node through decided selects (a
+        // balance minus the amount read from the same slot: `this.balance` sent in full)
+        r = (x.a == x.b || resolve(x.a) == resolve(x.b) || known_order(x.a, x.b) == OEQ) ? exact(bv_zero(), w)
+                                                                                          : av_sub(*A, *B, w);
+        break;
       case MGP_OP_NEG: r = av_sub(exact(bv_zero(), w), *A, w); break;
       case MGP_OP_MUL: r = av_mul(*A, *B, w); break;
       case MGP_OP_AND: r = av_and(*A, *B, w); break;

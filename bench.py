@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--refute-sample", type=int, default=1 << 17,
                     help="states of the rank-0 batch run through the host UNSAT pre-check (0 = skip)")
     ap.add_argument("--suite", type=int, default=1, help="the 13-contract solidity_examples suite (0 = skip)")
+    ap.add_argument("--suite-open-sweep", type=int, default=1,
+                    help="WalletLibrary -t 3 at max_open 6 / 12 / 24 open states between transactions (0 = skip)")
     ap.add_argument("--div-split", type=int, default=1, help="time the division-free twin batch (0 = skip)")
     ap.add_argument("--frontend", type=int, default=1024,
                     help="contract-shaped states through the full Prefilter front end (0 = skip)")
@@ -584,8 +586,28 @@ def main():
         suite = dict(acc, queries=len(qs), seconds=dt_all, queries_per_s=len(qs) / dt_all, generate_s=gen_s,
                      held_out_contracts=sorted(corpus.held_out()),
                      note="queries restated by reading the reference (corpus/laser.py, corpus/contracts.py); "
-                          "ref_calls = the reference's z3 calls (get_model lru-deduplicated), z3_calls = "
-                          "undecided prune/model queries + every tx-sequence query not refuted")
+                          "ref_calls = restated reference calls (the z3 calls the restated run makes, get_model "
+                          "lru-deduplicated), z3_calls = undecided prune/model/dep queries + every tx-sequence "
+                          "query not refuted; dep = DependencyPruner's get_model((loc == dep,))")
+        # WalletLibrary -t 3 (config 4, "state explosion") as the open states carried between
+        # transactions grow: max_open 6 (the suite's cap) / 12 / 24
+        if args.suite_open_sweep:
+            sweep = {}
+            for mo in (6, 12, 24):
+                tg = time.perf_counter()
+                wq = corpus.suite(max_open=mo, contracts={"wallet"})
+                g = time.perf_counter() - tg
+                SV.unsat_cores().reset()
+                pf._N.program_cache_clear()
+                t0 = time.perf_counter()
+                wa, _ = corpus.answer(pf, wq)
+                dt = time.perf_counter() - t0
+                wacc = corpus.account(wq, wa)["all"]
+                if wacc["contradicted"]:
+                    raise RuntimeError(f"wallet max_open={mo} contradicts the expectations: {wacc}")
+                sweep[str(mo)] = dict(wacc, seconds=dt, generate_s=g)
+                log(f"suite wallet max_open={mo}: {json.dumps(sweep[str(mo)])}")
+            suite["wallet_max_open"] = sweep
         pf.ctx.close()
         log(f"suite: {json.dumps(suite['all'])} held_out {json.dumps(suite['held_out'])}")
 

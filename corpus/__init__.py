@@ -233,7 +233,7 @@ def corpus(n: int) -> List[Tuple[str, tuple, Optional[str]]]:
 def suite(hasher=None, max_open: int = 6, contracts=None):
     """Every contract of solidity_examples/ through the LASER restatement (corpus.laser,
     corpus.contracts): -> list of (contract, kind, label, terms, expected) queries in the
-    order a `myth analyze <contract> -t N` run asks them (kind: prune / model / txseq).
+    order a `myth analyze <contract> -t N` run asks them (kind: prune / model / dep / txseq).
     The last field is the index of the query's parent (the prune query that established the
     asking state; -1 for none): the plugin hands a child its parent's witness.
 
@@ -260,10 +260,15 @@ def suite(hasher=None, max_open: int = 6, contracts=None):
     # a query is asked on a state its parent query established: a "sat" read off the query's
     # own constraint holds only if that state is reachable, so it stays "sat" only when the
     # parent's expectation is "sat" (an "unsat" needs no such condition)
+    # (such a dropped expectation stays visible: its label ends in SAT_IF_REACHABLE and
+    # account() reports how many there are)
     for k, (c, kind, label, terms, exp, par) in enumerate(out):
         if exp == "sat" and par >= 0 and out[par][4] != "sat":
-            out[k] = (c, kind, label, terms, None, par)
+            out[k] = (c, kind, label + SAT_IF_REACHABLE, terms, None, par)
     return out
+
+
+SAT_IF_REACHABLE = " [sat if its parent state is reachable]"
 
 
 def held_out() -> set:
@@ -276,9 +281,9 @@ def account(queries, answers, held=None) -> dict:
 
     answers[k] is the pre-filter's 'sat' (GPU witness) / 'unsat' (host refutation) /
     'undecided' for queries[k].  The reference makes one z3 call per query, except that
-    get_model is lru_cached (analysis/solver.py:27): a repeated SAT-only or tx-sequence
-    query with identical constraints is one call.  The pre-filter path makes:
-      prune / model: one fallback call when undecided;
+    get_model is lru_cached (analysis/solver.py:27): a repeated SAT-only, dependency or
+    tx-sequence query with identical constraints is one call.  The pre-filter path makes:
+      prune / model / dep: one fallback call when undecided;
       txseq: one z3 Optimize call unless refuted -- a GPU witness does not save it, the
       minimised model values go into the report (analysis/solver.py:88-136).
     A contradiction is a GPU witness on an expected-unsat query or a refutation of an
@@ -293,7 +298,7 @@ def account(queries, answers, held=None) -> dict:
                                       "undecided": 0, "contradicted": 0, "expected_sat": 0, "expected_sat_witness": 0,
                                       "expected_unsat": 0, "expected_unsat_refuted": 0,
                                       "by_kind": {k: {"queries": 0, "ref_calls": 0, "z3_calls": 0}
-                                                  for k in ("prune", "model", "txseq")}})
+                                                  for k in ("prune", "model", "dep", "txseq")}})
         c["queries"] += 1
         c[ans] += 1
         bk = c["by_kind"][kind]
@@ -319,6 +324,9 @@ def account(queries, answers, held=None) -> dict:
     for c in per.values():
         c["reduction"] = c["ref_calls"] / max(1, c["z3_calls"])
         c["held_out"] = False
+    dropped = collections.Counter(q[0] for q in queries if q[2].endswith(SAT_IF_REACHABLE))
+    for name, c in per.items():
+        c["sat_expectations_dropped"] = dropped.get(name, 0)
     for name in per:
         per[name]["held_out"] = name in held
 
@@ -327,7 +335,11 @@ def account(queries, answers, held=None) -> dict:
         z = sum(per[n]["z3_calls"] for n in names)
         return {"contracts": len(names), "queries": sum(per[n]["queries"] for n in names), "ref_calls": r,
                 "z3_calls": z, "reduction": r / max(1, z),
-                "contradicted": sum(per[n]["contradicted"] for n in names)}
+                "contradicted": sum(per[n]["contradicted"] for n in names),
+                "sat_expectations_dropped": sum(per[n]["sat_expectations_dropped"] for n in names),
+                "by_kind": {k: {f: sum(per[n]["by_kind"][k][f] for n in names) for f in ("queries", "ref_calls",
+                                                                                     "z3_calls")}
+                            for k in ("prune", "model", "dep", "txseq")}}
     names = list(per)
     return {"by_contract": dict(per), "all": total(names),
             "tuned": total([n for n in names if n not in held]),

@@ -13,6 +13,8 @@ on every contract of solidity_examples/ with each query tagged by how the refere
 * ``model``  -- a SAT-only get_model (analysis/solver.py:27-61): MutationPruner
   (mutation_pruner.py:55-83), the integer module's ostate check (integer.py:288-297),
   ether_thief (ether_thief.py:76-80), state_change_external_calls (120-145, 189-198);
+* ``dep``    -- DependencyPruner's `get_model((loc == dep,))` (below), a SAT-only get_model
+  on one equality of two storage locations, no path constraints;
 * ``txseq``  -- get_transaction_sequence (analysis/solver.py:88-136): get_model with the
   minimisation constraints (242-282) and minimize objectives, so a SAT answer is ONE z3
   Optimize call whatever the GPU finds (its model values go into the report); an UNSAT one
@@ -27,9 +29,13 @@ integer module's ostate sets; potential issues checked at transaction end,
 potential_issues.py:75-108), and MutationPruner's filter between transactions.
 What is approximated or left out, and why:
 
-* DependencyPruner's queries (dependency_pruner.py:134-187) are left out: they compare two
-  storage locations with no path constraints (mostly concrete slots), so counting them would
-  inflate the reduction;
+* DependencyPruner (dependency_pruner.py, loaded by default, analysis/symbolic.py:139-140) is
+  restated over the JUMPI successors as its basic blocks: from the second message call on, a
+  successor whose block this path saw before runs only if some storage location written in
+  the previous transaction can equal a location read on paths through the block -- one
+  ``dep`` query `get_model((loc == dep,))` per pair (dependency_pruner.py:134-187, lru-cached
+  like every get_model) -- and a pruned successor asks nothing more (PluginSkipState drops it
+  before the prune filter, svm.py:614-631);
 * compiler-internal arithmetic (memory pointers, ABI offsets) carries no integer-module
   annotation here; only source-level ADD / SUB / MUL / EXP do;
 * feasibility of every branch is decided by reading (`t=` / `f=` at each site), as the
@@ -102,6 +108,36 @@ class Tx:
         return Concat(BVV(0, 96), Extract(159, 0, self.arg(k)))
 
 
+class DepAnn:
+    """plugin_annotations.py:17-49 DependencyAnnotation: the blocks on this path, the storage
+    locations it read (this transaction) and wrote (per iteration), whether it made a call."""
+
+    def __init__(self):
+        self.loaded: list = []
+        self.written: Dict[int, list] = {}
+        self.has_call = False
+        self.path: list = [0]
+        self.seen: set = set()
+
+    def copy(self) -> "DepAnn":
+        d = DepAnn.__new__(DepAnn)
+        d.loaded = list(self.loaded)
+        d.written = {k: list(v) for k, v in self.written.items()}
+        d.has_call = self.has_call
+        d.path = list(self.path)
+        d.seen = set(self.seen)
+        return d
+
+
+def _same_term(a, b) -> bool:
+    return a.raw is b.raw
+
+
+def _add_loc(lst: list, loc) -> None:
+    if not any(_same_term(loc, x) for x in lst):
+        lst.append(loc)
+
+
 class World:
     """The world state a path carries: the contract's storage (one Store chain) and the
     balances (world_state.py:33); `starting` are the balances before any transaction."""
@@ -114,6 +150,7 @@ class World:
         self.txs: List[Tx] = []
         self.cons: list = []   # world_state.constraints: they carry over into the next transaction
         self.qid = -1          # the query that established the state this world was opened from
+        self.dep = DepAnn()    # DependencyAnnotation handed to the next transaction's states
 
     def fork(self) -> "World":
         w = World.__new__(World)
@@ -123,6 +160,7 @@ class World:
         w.txs = list(self.txs)
         w.cons = list(self.cons)
         w.qid = self.qid
+        w.dep = self.dep.copy()
         return w
 
 
@@ -144,6 +182,14 @@ class Analysis:
         self.next_tid = 1
         self.decide = refuter()
         self._decided: Dict[tuple, bool] = {}
+        # DependencyPruner (dependency_pruner.py:83-96): per block, the storage locations read
+        # and written on paths through it and whether a call was made; `iteration` counts the
+        # transactions as start_sym_trans does (the creation transaction is 1, reset to 0 when
+        # it ends, so message call k is iteration k)
+        self.dep_sloads: Dict[object, list] = {}
+        self.dep_sstores: Dict[object, list] = {}
+        self.dep_calls: set = set()
+        self.iteration = 0
 
     def tid(self) -> int:
         t = self.next_tid
@@ -219,9 +265,15 @@ class Path:
         self.mutated = False
         self.selfdestructed = False
         self.qid = -1   # the prune query that established this state (corpus parent links)
+        self.dep = world.dep.copy()
+        # dropped by DependencyPruner (PluginSkipState): the contract code still walks it
+        # (its successors are dead too) but it asks nothing and opens no world state
+        self.dead = False
 
     def _ask(self, kind: str, label: str, cons: Sequence, expected: Optional[str], establishes: bool = False,
              parent: Optional[int] = None) -> bool:
+        if self.dead:
+            return False
         i = len(self.run.queries)
         r = self.run.ask(kind, label, cons, expected, self.qid if parent is None else parent)
         if establishes:
@@ -238,6 +290,7 @@ class Path:
         p.call_sites = list(self.call_sites)
         p.sc_calls = list(self.sc_calls)
         p.potential = list(self.potential)
+        p.dep = self.dep.copy()
         return p
 
     # -------------------------------------------------------------- constraints
@@ -250,6 +303,8 @@ class Path:
                predictable: bool = False) -> Tuple[Optional["Path"], Optional["Path"]]:
         """JUMPI (instructions.py:1533-1610): the module pre-hooks, then both successors,
         each prune-checked; `t` / `f` say which one is feasible (by reading)."""
+        if self.dead:
+            return self.fork(), self.fork()
         self._sink(cond)
         if origin and not self.run.cached("origin", label) and \
                 self._ask("txseq", f"origin@{label}", self._txseq(self.cons), "sat"):
@@ -262,15 +317,109 @@ class Path:
             # (instructions.py:1556-1610), so it is still prune-checked once
             q = self.fork()
             q.cons.append(symbol_factory.Bool(True))
+            if not q._dep_block(f"{label}:{'T' if is_true(cond) else 'F'}"):
+                q.dead = True
             q._ask("prune", f"{label}:const", q.cons, "sat", establishes=True)
             return (q, None) if is_true(cond) else (None, q)
-        out = []
+        succ = []
         for want, ok in ((cond, t), (Not(cond), f)):
             q = self.fork()
             q.cons.append(want)
+            # the JUMPI post-hooks (DependencyPruner) run on both successors before the
+            # prune filter asks about either (svm.py:320-331, 251-255)
+            keep = q._dep_block(f"{label}:{'T' if want is cond else 'F'}")
+            succ.append((q, want, ok, keep))
+        out = []
+        for q, want, ok, keep in succ:
+            if not keep:  # PluginSkipState: no prune query, the state is gone
+                q.dead = True
+                out.append(q)
+                continue
             live = q._ask("prune", f"{label}:{'T' if want is cond else 'F'}", q.cons, _exp(ok), establishes=True)
             out.append(q if live else None)
         return out[0], out[1]
+
+    # -------------------------------------------------------------- DependencyPruner
+    def _dep_block(self, block) -> bool:
+        """jumpi_hook + _check_basic_block (dependency_pruner.py:202-221, 287-310): the block
+        joins this path; from iteration 2 on, a block this path has seen runs only if
+        wanna_execute says so.  False = PluginSkipState."""
+        run, d = self.run, self.dep
+        d.path.append(block)
+        if run.iteration < 2:
+            return True
+        if block not in d.seen:
+            d.seen.add(block)
+            return True
+        return self._wanna_execute(block)
+
+    def _wanna_execute(self, block) -> bool:
+        """dependency_pruner.py:134-187.  (Its storage_accessed_global branch compares block
+        offsets with storage locations and never matches; it is left out.)"""
+        run, d = self.run, self.dep
+        if block in run.dep_calls:
+            return True
+        if block not in run.dep_sloads:
+            return False
+        deps = run.dep_sloads[block]
+        for loc in d.written.get(run.iteration - 1, []):
+            for dep in list(deps) + list(d.loaded):
+                if self._dep_query(loc, dep, block):
+                    return True
+        return False
+
+    def _dep_query(self, loc, dep, block) -> bool:
+        """get_model((location == dependency,)): one SAT-only query on one unfolded equality
+        (z3 gets `loc == dep` as written, so distinct location pairs are distinct calls)."""
+        from mythril_amd import ir
+        from mythril_amd.smt import Bool, mk
+
+        eq = Bool(mk(ir.EQ, 0, (loc.raw, dep.raw)))
+        exp = None
+        if loc.raw.op == ir.CONST and dep.raw.op == ir.CONST:
+            exp = "sat" if loc.raw.params[0] == dep.raw.params[0] else "unsat"
+        elif loc.raw is dep.raw:
+            exp = "sat"
+        return self._ask("dep", f"dependency@{block}", [eq], exp)
+
+    def _dep_sload(self, key) -> None:
+        """sload_hook (dependency_pruner.py:247-259)."""
+        if self.dead:
+            return
+        run, d = self.run, self.dep
+        _add_loc(d.loaded, key)
+        for b in d.path:
+            _add_loc(run.dep_sloads.setdefault(b, []), key)
+
+    def _dep_sstore(self, key) -> None:
+        """sstore_hook (dependency_pruner.py:238-245)."""
+        if self.dead:
+            return
+        run, d = self.run, self.dep
+        for b in d.path:
+            _add_loc(run.dep_sstores.setdefault(b, []), key)
+        _add_loc(d.written.setdefault(run.iteration, []), key)
+
+    def _dep_call(self) -> None:
+        """call_hook (dependency_pruner.py:261-267)."""
+        if self.dead:
+            return
+        for b in self.dep.path:
+            if b in self.run.dep_sstores:
+                self.run.dep_calls.add(b)
+        self.dep.has_call = True
+
+    def _dep_end(self) -> None:
+        """_transaction_end at STOP / RETURN (dependency_pruner.py:269-285), then the
+        world-state hook: the annotation goes on with path [0] and nothing loaded
+        (dependency_pruner.py:312-330)."""
+        if self.dead:
+            return
+        for k in self.dep.loaded:
+            for b in self.dep.path:
+                _add_loc(self.run.dep_sloads.setdefault(b, []), k)
+        if self.dep.has_call:
+            self._dep_call()
 
     def require(self, cond, label: str, t: Optional[bool] = True, f: Optional[bool] = True, **kw) -> Optional["Path"]:
         """require(cond): the false successor reverts (nothing more is asked on it)."""
@@ -324,12 +473,14 @@ class Path:
 
     # -------------------------------------------------------------- storage
     def sload(self, key):
+        self._dep_sload(_bv(key))
         return self.world.storage[_bv(key)]
 
     def sstore(self, key, value) -> None:
         value = _bv(value)
         self._sink(value)
         self._state_access("sstore")
+        self._dep_sstore(_bv(key))
         self.world.storage[_bv(key)] = value
         self.mutated = True
 
@@ -370,6 +521,7 @@ class Path:
         `value_pos` / `thief` are the answers by reading."""
         to, value, gas = _bv(to), _bv(value), _bv(gas)
         run = self.run
+        self._dep_call()
         self._sink(value)
         self._state_access(f"call@{label}")
         # external_calls.py:83-110: gas > 2300 and to == attacker -> a potential issue
@@ -437,6 +589,8 @@ class Path:
         75-108), then add_world_state with MutationPruner's filter (mutation_pruner.py:55-83).
         Returns the path when its world state opens the next transaction."""
         run = self.run
+        if self.dead:
+            return None
         # unchecked_retval.py:80-110: one transaction sequence per recorded retval
         for site, rv, free in ([] if self.selfdestructed else self.retvals):
             if run.cached("unchecked_retval", site):
@@ -472,6 +626,10 @@ class Path:
                 run.found(module, site)
         self.world.cons = list(self.cons)   # the open world state keeps the path's constraints
         self.world.qid = self.qid
+        self._dep_end()
+        self.dep.path = [0]
+        self.dep.loaded = []
+        self.world.dep = self.dep
         if self.tx.creation:
             return self
         # MutationPruner: keep a world state that mutated, or whose callvalue can be > 0
@@ -504,6 +662,7 @@ def start_tx(run: Analysis, world: World, creation: bool = False, index: int = 0
     it can pay the value, the value moves (transaction_models.py:110-133)."""
     tx = Tx(run.tid(), creation)
     tx.index = index   # 0: the creation transaction, k: the k-th message call
+    run.iteration = 1 if creation else index   # start_sym_trans (the creation's is reset after it)
     w = world.fork()
     w.txs.append(tx)
     p = Path(run, w, tx, "constructor" if creation else "dispatcher")

@@ -891,16 +891,26 @@ int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uin
     std::copy(c.pairs.begin(), c.pairs.end(), s.pairs.begin());
   };
   std::vector<Snap> snaps(depth);
+  // work cap: at most kSplitWork node evaluations of propagation per state, so a
+  // WalletLibrary-size state (600-1 500 nodes) cannot spend a second in nested probes before
+  // the fallback; when it runs out the probes stop and the state is "not refuted" (sound)
+  constexpr uint64_t kSplitWork = 1ull << 23;
+  int64_t runs_left = (int64_t)std::max<uint64_t>(32u, kSplitWork / ((uint64_t)s.n * passes + 1u));
+  auto run_capped = [&]() -> int {
+    if (--runs_left < 0) return 0;
+    return d.run(passes);
+  };
   // true = the analysis as it stands (propagated) is refuted by splits `level` deep
   std::function<bool(uint32_t)> probe = [&](uint32_t level) -> bool {
-    if (level == 0) return false;
+    if (level == 0 || runs_left <= 0) return false;
     Snap &c = snaps[level - 1];
     for (int32_t a : atoms) {
       if (s.bs[a] != BB) continue;
+      if (runs_left <= 0) return false;
       take(c);
-      const bool rt = !d.meetb(a, BT) || d.run(passes) == 1 || probe(level - 1);
+      const bool rt = !d.meetb(a, BT) || run_capped() == 1 || probe(level - 1);
       put(c);
-      const bool rf = !d.meetb(a, BF) || d.run(passes) == 1 || probe(level - 1);
+      const bool rf = !d.meetb(a, BF) || run_capped() == 1 || probe(level - 1);
       put(c);
       if (rt && rf) return true;
       if (rt || rf) {  // the other polarity holds in every model of this branch

@@ -140,7 +140,11 @@ def replace_with_actual_sha(concrete_transactions: List[Dict[str, str]], model, 
     `store_function` and `get_concrete_hash_data`); by default LASER's singleton.
     """
     if manager is None:  # LASER's module-level singleton (keccak_function_manager.py:149)
-        from mythril.laser.ethereum.keccak_function_manager import keccak_function_manager as manager
+        try:
+            from mythril.laser.ethereum.keccak_function_manager import keccak_function_manager as manager
+        except ImportError as e:
+            raise ValueError("replace_with_actual_sha needs `manager` (the keccak function manager whose UF "
+                             "pairs the model speaks about) outside a LASER process") from e
     hasher = hasher or find_concrete_keccak_batch
     concrete_hashes = manager.get_concrete_hash_data(model)
 

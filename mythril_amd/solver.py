@@ -457,10 +457,16 @@ class Prefilter:
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
         # the pipeline's pinned host staging and candidate block, sized once here instead of
         # on the first large batch (pinning a few hundred MB of host memory takes tens of ms)
+        # (MGP_HOST_STAGING_MB lowers the reserve for several ranks on one device; a reserve
+        # that fails leaves the buffers to grow lazily on the first large batch)
+        staging = int(os.environ.get("MGP_HOST_STAGING_MB", self.HOST_STAGING >> 20)) << 20
         for c in self.ctxs:
             reserve = getattr(c, "reserve", None)  # (test doubles of the context have none)
-            if reserve is not None:
-                reserve(self.HOST_STAGING, self.cand_bytes)
+            if reserve is not None and staging > 0:
+                try:
+                    reserve(staging, self.cand_bytes)
+                except N.MgpError:
+                    pass
         # refuted constraint lists wait in the core cache and are shrunk to cores together
         # once core_batch of them are pending (flush_cores): one batched shrink instead of
         # one per call keeps the deletion trials off the latency of small calls

@@ -126,9 +126,12 @@ def test_keccak_complex_eq(backend):
     # the inverse's value), o1 ≡ o2 mod 2^255 -> o1 = o2 (both in one 2^123-wide keccak256_160
     # interval, keccak_function_manager.py:118-133), then a = b by the inverse of f -- chained
     # equalities through arithmetic that the known-bits x interval domain does not track.
-    # The GPU never answers sat: there is no model.
-    assert s.check() == SV.unknown
-    assert backend.calls == 1 and SV.SolverStatistics().gpu_sat == 0 and SV.SolverStatistics().refuted == 0
+    # The GPU never answers sat: there is no model.  Either the fallback decides it or the
+    # host pre-check refutes it (a correct improvement the test must not forbid).
+    st = SV.SolverStatistics()
+    assert s.check() != SV.sat
+    assert st.gpu_sat == 0
+    assert backend.calls + st.refuted == 1, (backend.calls, st.refuted)
 
 
 def test_keccak_complex_eq2(backend):

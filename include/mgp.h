@@ -190,6 +190,20 @@ int mgp_refute_split(const mgp_node *nodes, const uint64_t *node_offsets,
                      uint32_t n_states, const uint32_t *consts,
                      const uint64_t *const_offsets, uint32_t max_passes,
                      uint32_t max_splits, int8_t *out);
+/* UNSAT cores of refuted constraint lists (round 5; replaces rebuilding a DAG per deletion
+ * trial in the caller).  Each state is the DAG mgp_build_states builds from a list of
+ * n_roots[s] constraints (roots AND-chained at its tail).  Per state: up to `halvings`
+ * rounds keep the first or second half of the list when it alone is refuted, then (lists of
+ * at most max_single) greedy single deletions drop every constraint whose removal keeps the
+ * list refuted; each trial re-runs mgp_refute's analysis with only the kept constraints
+ * required.  keep (one byte per constraint, states concatenated): 1 = in the core.
+ * out[s]: 1 = core found (the kept set is refuted: a proof, the reference's z3 would answer
+ * unsat for it, analysis/solver.py:56-61), 0 = the list is not refuted (all kept),
+ * -1 = no root chain / malformed (all kept).  Host only (OpenMP over states). */
+int mgp_refute_cores(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                     const uint32_t *consts, const uint64_t *const_offsets, const uint32_t *n_roots,
+                     uint32_t max_passes, uint32_t halvings, uint32_t max_single, uint8_t *keep,
+                     int8_t *out);
 /* Diagnostic (tests): the refined abstract value of every node of ONE state,
  * 33 words per node: known-zero mask, known-one mask, lo, hi (8 u32 limbs
  * each) and the Bool truth set (bit0 = may be false, bit1 = may be true).

@@ -92,6 +92,7 @@ def _bind(lib):
         "mgp_set_eval_diag": (ctypes.c_int, [_P]),
         "mgp_refute": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _P]),
         "mgp_refute_split": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _P]),
+        "mgp_refute_cores": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _U32, _U32, _P, _P]),
         "mgp_refute_trace": (ctypes.c_int, [_P, _U64, _P, _U64, _U32, _P]),
         "mgp_guided_candidates": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P]),
         "mgp_guided_candidates_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U32, _U64, _U32, _U32, _P, _P,
@@ -164,6 +165,7 @@ EXPORTED_SYMBOLS = (
     "mgp_set_eval_diag",
     "mgp_refute",
     "mgp_refute_split",
+    "mgp_refute_cores",
     "mgp_refute_trace",
     "mgp_guided_candidates",
     "mgp_guided_candidates_rows",
@@ -428,6 +430,28 @@ def refute_split(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray
     _check(lib().mgp_refute_split(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
                                   max_passes, max_splits | (depth << 16), _ptr(out)))
     return out[:n_states]
+
+
+def refute_cores(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,
+                 n_roots: np.ndarray, max_passes: int = 0, halvings: int = 3, max_single: int = 32):
+    """mgp_refute_cores: the core of each refuted constraint list whose DAG these are (the
+    lists' constraint counts in n_roots) -> (list of u8 keep masks, status i8 [n])."""
+    nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
+    node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
+    consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
+    if consts.size == 0:
+        consts = np.zeros(8, dtype=np.uint32)
+    const_offsets = np.ascontiguousarray(const_offsets, dtype=np.uint64)
+    n_roots = np.ascontiguousarray(n_roots, dtype=np.uint32)
+    n_states = len(node_offsets) - 1
+    if n_roots.shape != (n_states,):
+        raise ValueError("n_roots must hold one count per state")
+    keep = np.zeros(max(int(n_roots.sum()), 1), dtype=np.uint8)
+    out = np.zeros(max(n_states, 1), dtype=np.int8)
+    _check(lib().mgp_refute_cores(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
+                                  _ptr(n_roots), max_passes, halvings, max_single, _ptr(keep), _ptr(out)))
+    off = np.concatenate([[0], np.cumsum(n_roots)]).astype(np.int64)
+    return [keep[off[k]:off[k + 1]] for k in range(n_states)], out[:n_states]
 
 
 def refute_trace(nodes: np.ndarray, consts: np.ndarray, max_passes: int = 0):

@@ -1724,13 +1724,23 @@ struct Dom {
   }
 
   // 1 = refuted (UNSAT), 0 = not refuted
+  // the nodes required true: the root, or (core trials, mgp_refute_cores) a chosen subset of
+  // the root conjuncts plus the piece-expansion ties
+  const int32_t *req = nullptr;
+  uint32_t n_req = 0;
+  MGP_RD bool require_root() {
+    if (!req) return meetb((int32_t)n - 1, BT);
+    for (uint32_t k = 0; k < n_req; ++k)
+      if (!meetb(req[k], BT)) return false;
+    return true;
+  }
   MGP_RD int run(uint32_t max_passes) {
-    if (!meetb((int32_t)n - 1, BT)) return 1;
+    if (!require_root()) return 1;
     for (uint32_t pass = 0; pass < max_passes; ++pass) {
       changed = false;
       for (uint32_t i = 0; i < n; ++i)
         if (!forward(i)) return 1;
-      if (!meetb((int32_t)n - 1, BT) || !tie()) return 1;
+      if (!require_root() || !tie()) return 1;
       for (uint32_t i = n; i-- > 0;)
         if (!backward(i)) return 1;
       if (!tie()) return 1;

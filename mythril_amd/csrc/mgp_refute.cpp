@@ -53,6 +53,7 @@ struct State {
   const mgp_node *orig = nullptr;  // the DAG before relax_wide (UF arguments, congruence)
   std::vector<mgp_node> origx;     // orig + the piece-expansion nodes relax_wide appended
   std::vector<uint32_t> xconsts;   // the constant pool + the pieces' zero (when one is needed)
+  std::vector<int32_t> ties;       // the piece-expansion ties (required with the root)
   uint32_t n;
   const uint32_t *consts;
   uint64_t n_consts;
@@ -697,12 +698,13 @@ struct Expander {
 
 bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out, const uint32_t *consts = nullptr,
                 uint64_t n_consts = 0, std::vector<mgp_node> *orig_out = nullptr,
-                std::vector<uint32_t> *xconsts = nullptr);
+                std::vector<uint32_t> *xconsts = nullptr, std::vector<int32_t> *ties_out = nullptr);
 
 bool relax_wide_narrow(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out);
 
 bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out, const uint32_t *consts,
-                uint64_t n_consts, std::vector<mgp_node> *orig_out, std::vector<uint32_t> *xconsts) {
+                uint64_t n_consts, std::vector<mgp_node> *orig_out, std::vector<uint32_t> *xconsts,
+                std::vector<int32_t> *ties_out) {
   if (!relax_wide_narrow(nd, n, out)) return false;
   if (!orig_out || !xconsts) return true;
   // piece expansion: ties appended after the relaxed DAG (see above)
@@ -788,6 +790,7 @@ bool relax_wide(const mgp_node *nd, uint64_t n, std::vector<mgp_node> &out, cons
   }
   orig_out->assign(nd, nd + n);
   orig_out->insert(orig_out->end(), out.begin() + (int64_t)n, out.end());
+  if (ties_out) *ties_out = ties;
   return true;
 }
 
@@ -837,7 +840,7 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
   State st;
   State &s = keep ? *keep : st;
   s.orig = nd;
-  if (relax_wide(nd, n, s.relaxed, consts, n_consts, &s.origx, &s.xconsts)) {
+  if (relax_wide(nd, n, s.relaxed, consts, n_consts, &s.origx, &s.xconsts, &s.ties)) {
     nd = s.relaxed.data();
     n = s.relaxed.size();
     if (!s.origx.empty()) s.orig = s.origx.data();
@@ -938,6 +941,125 @@ extern "C" int mgp_refute_split(const mgp_node *nodes, const uint64_t *node_offs
     }
     out[s] = (int8_t)refute_split_one(nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes,
                                       max_splits);
+  }
+  return MGP_OK;
+}
+
+namespace {
+// The root conjuncts of a DAG built by mgp_build_states from k constraints: the roots are
+// AND-chained into the last k - 1 nodes (mgp_front.cpp build_one); k = 1 is the last node
+// (or BAND(r, r) after it).  false = the tail is not such a chain.
+bool chain_roots(const mgp_node *nd, uint64_t n, uint32_t k, std::vector<int32_t> &roots) {
+  roots.clear();
+  if (k == 0 || n == 0) return false;
+  if (k == 1) {
+    const mgp_node &t = nd[n - 1];
+    roots.push_back(t.op == MGP_OP_BAND && t.a == t.b ? t.a : (int32_t)(n - 1));
+    return true;
+  }
+  if (n < k) return false;
+  const uint64_t c1 = n - (k - 1);  // first chain node: BAND(r0, r1)
+  roots.assign(k, -1);
+  for (uint32_t i = 1; i < k; ++i) {
+    const mgp_node &t = nd[c1 + i - 1];
+    if (t.op != MGP_OP_BAND || (i > 1 && t.a != (int32_t)(c1 + i - 2))) return false;
+    roots[i] = t.b;
+    if (i == 1) roots[0] = t.a;
+  }
+  return true;
+}
+
+// One refuted constraint list's core: the fewest root conjuncts (a minimal set under the
+// refuter, not a minimum) found by halving rounds and then greedy single deletions, every
+// trial re-running the analysis from the state's set-up values with only the kept conjuncts
+// (and the piece ties) required -- one DAG and one set-up per list, no rebuilding per trial.
+int core_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t k,
+             uint32_t max_passes, uint32_t halvings, uint32_t max_single, uint8_t *keep) {
+  std::vector<int32_t> roots;
+  for (uint32_t i = 0; i < k; ++i) keep[i] = 1;
+  if (!chain_roots(nd, n, k, roots)) return -1;
+  State s;
+  s.orig = nd;
+  const mgp_node *d0 = nd;
+  uint64_t nn = n;
+  if (relax_wide(nd, n, s.relaxed, consts, n_consts, &s.origx, &s.xconsts, &s.ties)) {
+    d0 = s.relaxed.data();
+    nn = s.relaxed.size();
+    if (!s.origx.empty()) s.orig = s.origx.data();
+    if (!s.xconsts.empty()) {
+      consts = s.xconsts.data();
+      n_consts = s.xconsts.size() / 8u;
+    }
+  }
+  s.nd = d0;
+  s.n = (uint32_t)nn;
+  s.consts = consts;
+  s.n_consts = n_consts;
+  if (!s.setup()) return -1;
+  const std::vector<AV> av0 = s.av, vars0 = s.vars;
+  const std::vector<uint8_t> bs0 = s.bs;
+  const std::vector<Pair> pairs0 = s.pairs;
+  const uint32_t passes = max_passes ? max_passes : 16u;
+  std::vector<int32_t> req;
+  auto refuted = [&](const std::vector<uint32_t> &sel) {
+    std::copy(av0.begin(), av0.end(), s.av.begin());
+    std::copy(vars0.begin(), vars0.end(), s.vars.begin());
+    std::copy(bs0.begin(), bs0.end(), s.bs.begin());
+    std::copy(pairs0.begin(), pairs0.end(), s.pairs.begin());
+    req.assign(s.ties.begin(), s.ties.end());
+    for (uint32_t i : sel) req.push_back(roots[i]);
+    Dom d = s.view();
+    d.req = req.data();
+    d.n_req = (uint32_t)req.size();
+    return d.run(passes) == 1;
+  };
+  std::vector<uint32_t> cur(k);
+  for (uint32_t i = 0; i < k; ++i) cur[i] = i;
+  if (!refuted(cur)) return 0;  // not refuted as a whole: keep everything
+  for (uint32_t h = 0; h < halvings && cur.size() >= 8; ++h) {
+    const size_t m = cur.size() / 2;
+    std::vector<uint32_t> lo(cur.begin(), cur.begin() + (int64_t)m), hi(cur.begin() + (int64_t)m, cur.end());
+    if (refuted(lo)) cur.swap(lo);
+    else if (refuted(hi)) cur.swap(hi);
+    else break;
+  }
+  if (cur.size() >= 2 && cur.size() <= max_single) {
+    for (size_t i = 0; i < cur.size() && cur.size() > 1;) {
+      std::vector<uint32_t> t(cur);
+      t.erase(t.begin() + (int64_t)i);
+      if (refuted(t)) cur.swap(t);  // conjunct i is not needed: drop it for good
+      else ++i;
+    }
+  }
+  for (uint32_t i = 0; i < k; ++i) keep[i] = 0;
+  for (uint32_t i : cur) keep[i] = 1;
+  return 1;
+}
+}  // namespace
+
+// UNSAT cores of refuted constraint lists (solver.UnsatCores.shrink_many, round 5): per
+// state, its DAG as mgp_build_states builds it from the list's `n_roots[s]` constraints;
+// keep (one byte per constraint, states concatenated) gets 1 for the constraints of the
+// core.  out[s]: 1 = core found (refuted), 0 = the whole list is not refuted (all kept),
+// -1 = not a root chain / malformed (all kept).
+extern "C" int mgp_refute_cores(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                const uint32_t *consts, const uint64_t *const_offsets, const uint32_t *n_roots,
+                                uint32_t max_passes, uint32_t halvings, uint32_t max_single, uint8_t *keep,
+                                int8_t *out) {
+  if (!node_offsets || !out || !n_roots || (n_states && (!nodes || !const_offsets || !keep))) return MGP_E_ARG;
+  std::vector<uint64_t> koff(n_states + 1, 0);
+  for (uint32_t s = 0; s < n_states; ++s) koff[s + 1] = koff[s] + n_roots[s];
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+    const uint64_t n0 = node_offsets[s], n1 = node_offsets[s + 1];
+    const uint64_t c0 = const_offsets[s], c1 = const_offsets[s + 1];
+    if (n1 < n0 || c1 < c0) {
+      out[s] = -1;
+      for (uint32_t i = 0; i < n_roots[s]; ++i) keep[koff[s] + i] = 1;
+      continue;
+    }
+    out[s] = (int8_t)core_one(nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, n_roots[s],
+                              max_passes, halvings, max_single, keep + koff[s]);
   }
   return MGP_OK;
 }

@@ -303,69 +303,27 @@ class UnsatCores:
 
     @staticmethod
     def shrink_many(N, lists: Sequence[Sequence[Term]], max_terms: int = 32, arena=None) -> List[List[Term]]:
-        """Deletion-based cores of many refuted constraint lists in a few batched native
-        calls (mgp_build_states + mgp_refute): up to HALVINGS rounds that keep the first or
-        second half of a list when it alone is refuted, then one batch with every
-        single-constraint deletion of every list; the constraints whose deletion breaks a
-        refutation form that list's core if a last batched refute confirms it alone.  Every
-        set returned is one the refuter refuted.  `arena`: the term arena to read
-        (a snapshot for a background shrink; default the live one)."""
-        from functools import partial
-
+        """Cores of many refuted constraint lists in one native call (mgp_build_states once
+        per list, then mgp_refute_cores): per list up to HALVINGS rounds keep the first or
+        second half when it alone is refuted, then greedy single deletions (lists of at most
+        max_terms) drop every constraint the refutation does not need; each trial re-runs
+        the analysis on the list's one DAG with only the kept constraints required.  Every
+        set returned is one the refuter refuted (a list it does not refute comes back
+        whole).  `arena`: the term arena to read (a snapshot for a background shrink;
+        default the live one)."""
         from .front import Batch
 
-        Batch = partial(Batch, arena=arena) if arena is not None else Batch
-
         lists = [list(dict.fromkeys(t)) for t in lists]
-        # halving first: a list whose first or second half alone is refuted has a core in
-        # that half, which then needs half the single-deletion trials (and a list that
-        # reaches its contradiction twice, where no single deletion matters, still shrinks)
-        for _ in range(UnsatCores.HALVINGS):
-            # any length: a path longer than max_terms, too long for single deletions,
-            # can halve into range
-            idx = [k for k, t in enumerate(lists) if len(t) >= UnsatCores.HALVE_MIN]
-            if not idx:
-                break
-            halves = []
-            for k in idx:
-                m = len(lists[k]) // 2
-                halves += [lists[k][:m], lists[k][m:]]
-            B = Batch(halves)
-            v = N.refute(*B.packed())
+        if not lists:
+            return []
+        B = Batch(lists, arena=arena) if arena is not None else Batch(lists)
+        try:
+            keep, status = N.refute_cores(*B.packed()[:4], np.array([len(t) for t in lists], np.uint32),
+                                          halvings=UnsatCores.HALVINGS, max_single=max_terms)
+        finally:
             B.close()
-            changed = False
-            for j, k in enumerate(idx):
-                if v[2 * j] == 1 or v[2 * j + 1] == 1:
-                    lists[k] = halves[2 * j] if v[2 * j] == 1 else halves[2 * j + 1]
-                    changed = True
-            if not changed:
-                break
-        trials, owner = [], []
-        for k, t in enumerate(lists):
-            if 2 <= len(t) <= max_terms:
-                trials.extend(t[:i] + t[i + 1:] for i in range(len(t)))
-                owner.extend([k] * len(t))
-        if not trials:
-            return lists
-        B = Batch(trials)
-        v = N.refute(*B.packed())
-        B.close()
-        need: Dict[int, List[Term]] = {}
-        pos = 0
-        for k, t in enumerate(lists):
-            if 2 <= len(t) <= max_terms:
-                need[k] = [t[i] for i in range(len(t)) if v[pos + i] != 1]
-                pos += len(t)
-        cand = [k for k, nd in need.items() if nd and len(nd) < len(lists[k])]
-        out = list(lists)
-        if cand:
-            B = Batch([need[k] for k in cand])
-            ok = N.refute(*B.packed())
-            B.close()
-            for k, r in zip(cand, ok):
-                if r == 1:
-                    out[k] = need[k]
-        return out
+        return [[t[i] for i in range(len(t)) if m[i]] if st == 1 else t
+                for t, m, st in zip(lists, keep, status)]
 
 
 class _ArenaSnapshot:

@@ -194,8 +194,10 @@ def test_decision_rows_per_state_rule():
 
 
 def test_core_shrink_halving_finds_a_core_of_a_redundant_list():
-    """A list reaching its contradiction twice (no single deletion matters) still shrinks:
-    a halving round keeps the half that is refuted alone (UnsatCores.shrink_many)."""
+    """A list reaching its contradiction twice (no single deletion alone breaks it) still
+    shrinks: a halving round keeps the half that is refuted alone, and without halvings the
+    greedy deletions (mgp_refute_cores, round 5: each deletion that keeps the list refuted is
+    kept) end on one of the two contradictions (UnsatCores.shrink_many)."""
     v = [BVS(f"h{i}", 256) for i in range(12)]
     x, y = BVS("hx", 256), BVS("hy", 256)
     # first half: one contradiction on x among fillers; second half: another on y
@@ -211,8 +213,9 @@ def test_core_shrink_halving_finds_a_core_of_a_redundant_list():
     B.close()
     old = SV.UnsatCores.HALVINGS
     try:
-        SV.UnsatCores.HALVINGS = 0  # single deletions alone: nothing is necessary, the list stays
-        assert SV.UnsatCores.shrink(N, terms) == terms
+        SV.UnsatCores.HALVINGS = 0  # greedy deletions alone: one of the two contradictions
+        greedy = set(SV.UnsatCores.shrink(N, terms))
+        assert greedy in ({first[1].raw, first[3].raw}, {second[1].raw, second[4].raw}), greedy
         SV.UnsatCores.HALVINGS = old
         core = SV.UnsatCores.shrink(N, terms)
     finally:

@@ -1289,6 +1289,157 @@ for _c in U.CMPS:
     HBODY[f"{_c}_RC"] = make_cmp(_c, VC)
 
 
+def make_eqsel(zk):
+    """EQSEL_<zk>: vA = (vC == vB) ? Z : vA, one select-chain step (uop_spec.EQSEL_OPS).  The
+    fetch handler brought the compared operands into vC / vB; Z's read (parameter w3[31:16],
+    moved to where fetch_one reads operand B) is issued first and lands while the compare
+    runs; the selection is one VOP2 cndmask per limb on vcc (a bank operand indexed as
+    SRC1, no moves)."""
+    def body():
+        wait_operands()
+        A("s_mov_b32 s17, s19")
+        if zk in ("slot", "var"):
+            fetch_one(zk, VT, "B")
+        elif zk == "const":
+            const_issue("B")
+        for i in range(8):
+            A(f"v_xor_b32 {v(VC + i)}, {v(VC + i)}, {v(VB + i)}")
+        or_reduce(VC, range(VC, VC + 8))
+        A(f"v_cmp_eq_u32 vcc, 0, {v(VC)}")
+        if zk == "slot":
+            A("s_waitcnt lgkmcnt(0)")
+        elif zk == "var":
+            A("s_waitcnt vmcnt(0)")
+        elif zk == "const":
+            const_finish(VT, "B")
+        if zk == "rvar":
+            idx_on("B", "SRC1")
+            for i in range(8):
+                A(f"v_cndmask_b32 {v(VA + i)}, {v(VA + i)}, {v(RV + i)}, vcc")
+            A("s_set_gpr_idx_off")
+        else:
+            for i in range(8):
+                A(f"v_cndmask_b32 {v(VA + i)}, {v(VA + i)}, {v(VT + i)}, vcc")
+        bv_epilogue()
+    return body
+
+
+for _x in U.EQSEL_OPS:
+    HBODY[_x] = make_eqsel(_x[6:])
+
+
+@handler("TSEL")
+def h_tsel():
+    """vA = z_i where q == k_i over the uop's table of (k_i, z_i) u32 pairs (uop_spec TSEL;
+    keys distinct, so at most one entry matches a lane).  q (vC) matches only where its
+    limbs 1-7 are zero (s[50:51]); 8 entries per s_load_dwordx16; an entry's two row loads
+    are issued under exec = the lanes whose q equals its key (skipped when none does), so
+    the loads of a chain overlap instead of running one per uop."""
+    wait_operands()
+    lp, ld = A.fresh("tsel"), A.fresh("tseld")
+    A("s_and_b32 s55, s19, 0xffff",
+      "s_lshr_b32 s54, s19, 16",
+      "s_lshl_b32 s54, s54, 3",
+      "s_mov_b64 s[48:49], exec")
+    or_reduce(4, range(VC + 1, VC + 8))
+    A("v_cmp_eq_u32 s[50:51], 0, v4",
+      "s_and_b64 s[50:51], s[50:51], exec")
+    A.label(lp)
+    A("s_load_dwordx16 s[24:39], s[14:15], s54",
+      "s_waitcnt lgkmcnt(0)")
+    for e in range(8):
+        skip = A.fresh("tskip")
+        if e:
+            A(f"s_cmp_le_u32 s55, {e}", f"s_cbranch_scc1 {ld}")
+        A(f"v_cmp_eq_u32 vcc, s{24 + 2 * e}, {v(VC)}",
+          "s_and_b64 exec, vcc, s[50:51]",
+          f"s_cbranch_execz {skip}")
+        tsel_row_load(e)
+        A.label(skip)
+        A("s_mov_b64 exec, s[48:49]")
+    A("s_add_u32 s54, s54, 64",
+      "s_sub_u32 s55, s55, 8",
+      "s_cmp_gt_i32 s55, 0",
+      f"s_cbranch_scc1 {lp}")
+    A.label(ld)
+    A("s_mov_b64 exec, s[48:49]",
+      "s_waitcnt vmcnt(0)")
+    bv_epilogue()
+
+
+def tsel_row_load(e):
+    """Entry e's z row (variable index s[25+2e], clamped like fetch_one) into vA under exec."""
+    A(f"s_min_u32 s53, s{25 + 2 * e}, s9",
+      "s_mul_i32 s53, s53, s8",
+      "s_add_u32 s52, s6, s53",
+      "s_addc_u32 s53, s7, 0",
+      f"global_load_dwordx4 {vr(VA, 4)}, v2, s[52:53]",
+      f"global_load_dwordx4 {vr(VA + 4, 4)}, v3, s[52:53]")
+
+
+@handler("TSELS")
+def h_tsels():
+    """TSEL with keys in LDS slots (entries (slot byte offset, z_i), chain order): q (vC)
+    is compared with all 256 bits of each key; the key of entry e+1 is read into the other
+    of two buffers (T, vB) while entry e is compared.  Overlapping matches resolve as in the
+    chain: one wave's row loads return in issue order, so a lane's last match lands last."""
+    wait_operands()
+    lp, ld = A.fresh("tsels"), A.fresh("tselsd")
+    A("s_and_b32 s55, s19, 0xffff",
+      "s_lshr_b32 s54, s19, 16",
+      "s_lshl_b32 s54, s54, 3",
+      "s_mov_b64 s[48:49], exec")
+    A.label(lp)
+    A("s_load_dwordx16 s[24:39], s[14:15], s54",
+      "s_waitcnt lgkmcnt(0)")
+    bufs = (VT, VB)
+
+    def issue(e):
+        # a bank key's word has no LDS offset in [15:0]: its read is of slot 0, unused
+        A(f"s_and_b32 s53, s{24 + 2 * e}, 0xffff",
+          "v_add_u32 v4, s53, v1",
+          f"ds_read_b128 {vr(bufs[e % 2], 4)}, v4",
+          f"ds_read_b128 {vr(bufs[e % 2] + 4, 4)}, v4 offset:1024")
+    issue(0)
+    for e in range(8):
+        buf, skip = bufs[e % 2], A.fresh("tsskip")
+        lbank, lcmp = A.fresh("tsbank"), A.fresh("tscmp")
+        if e:
+            A(f"s_cmp_le_u32 s55, {e}", f"s_cbranch_scc1 {ld}")
+        if e < 7:
+            issue(e + 1)
+            A("s_waitcnt lgkmcnt(2)")
+        else:
+            A("s_waitcnt lgkmcnt(0)")
+        A(f"s_bitcmp1_b32 s{24 + 2 * e}, 31", f"s_cbranch_scc1 {lbank}")
+        for i in range(8):
+            A(f"v_xor_b32 {v(buf + i)}, {v(buf + i)}, {v(VC + i)}")
+        A(f"s_branch {lcmp}")
+        A.label(lbank)
+        # key in register-bank position w[23:16]/8: read as the indexed SRC0
+        A(f"s_bfe_u32 s53, s{24 + 2 * e}, {(8 << 16) | 16:#x}",
+          "s_set_gpr_idx_on s53, gpr_idx(SRC0)")
+        for i in range(8):
+            A(f"v_xor_b32 {v(buf + i)}, {v(RV + i)}, {v(VC + i)}")
+        A("s_set_gpr_idx_off")
+        A.label(lcmp)
+        or_reduce(buf, range(buf, buf + 8))
+        A(f"v_cmp_eq_u32 vcc, 0, {v(buf)}",
+          "s_and_b64 exec, vcc, s[48:49]",
+          f"s_cbranch_execz {skip}")
+        tsel_row_load(e)
+        A.label(skip)
+        A("s_mov_b64 exec, s[48:49]")
+    A("s_add_u32 s54, s54, 64",
+      "s_sub_u32 s55, s55, 8",
+      "s_cmp_gt_i32 s55, 0",
+      f"s_cbranch_scc1 {lp}")
+    A.label(ld)
+    A("s_mov_b64 exec, s[48:49]",
+      "s_waitcnt vmcnt(0) lgkmcnt(0)")
+    bv_epilogue()
+
+
 # ---- division (Knuth D, 32-bit digits)
 # The 16-limb working dividend u is vA (u[0..7]) : vC (u[8..15]); quotient digit J is stored
 # into u[J+8].  The normalised divisor is formed in place in vB (the single-digit path keeps

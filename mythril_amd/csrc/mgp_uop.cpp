@@ -71,7 +71,37 @@ struct Translator {
   std::vector<Opnd> slot_map;
   uint32_t n_lds = 0;                // LDS slots the program uses
   std::map<uint32_t, uint32_t> mask_c, sign_c;  // width -> pool index
+  std::vector<uint32_t> tables;                 // TSEL tables (behind the pool)
+  std::map<std::vector<uint32_t>, uint32_t> table_at;  // table -> word offset in `tables`
   bool bad = false;
+
+  // v1 constant operand o with zero limbs above the first: its low limb
+  bool small_const(uint32_t o, uint32_t *lo) const {
+    const uint32_t *c = &v1pool[(size_t)(o & 0x3FFFu) * 8];
+    for (int l = 1; l < 8; ++l)
+      if (c[l]) return false;
+    *lo = c[0];
+    return true;
+  }
+  // a TSEL / TSELS table, padded to 8-entry blocks; returns its word offset, stored once
+  // per distinct table.  Constant keys are made distinct (a key's last entry wins, as in
+  // the chain); slot keys are per-lane values and stay in chain order.
+  uint32_t add_table(const std::vector<std::pair<uint32_t, uint32_t>> &ent, bool dedupe, uint32_t *n_out) {
+    std::vector<uint32_t> t;
+    for (size_t i = 0; i < ent.size(); ++i) {
+      bool later = false;
+      for (size_t j = i + 1; dedupe && j < ent.size() && !later; ++j) later = ent[j].first == ent[i].first;
+      if (!later) { t.push_back(ent[i].first); t.push_back(ent[i].second); }
+    }
+    *n_out = (uint32_t)(t.size() / 2);
+    while (t.size() % 16) t.push_back(0u);
+    auto it = table_at.find(t);
+    if (it != table_at.end()) return it->second;
+    const uint32_t off = (uint32_t)tables.size();
+    tables.insert(tables.end(), t.begin(), t.end());
+    table_at.emplace(std::move(t), off);
+    return off;
+  }
 
   uint32_t add_ms(const uint32_t w[8]) {
     const uint32_t idx = (uint32_t)(ms.size() / 8);
@@ -307,6 +337,7 @@ struct BoolPlan {
   std::vector<uint32_t> andn;                 // BAND: 1 + negated bit (folded BNOT), andops[0] the other
   std::vector<uint8_t> merged;                // BAND merged into the next BAND of its AND chain
   std::vector<uint8_t> neg;                   // BAND: andops negated (bit j = andops[j]; BAND4N)
+  std::vector<uint8_t> eqsel;                 // ITE: condition from the folded EQ just before it
 };
 
 void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
@@ -453,6 +484,24 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
       P.dead[p] = 1;
     }
   }
+  // select chains (a Select over a Store chain, a calldata byte table): `EQ x y -> t` then
+  // `ITE(t, z, acc)` with t read nowhere else -> one EQSEL uop.  The compared operands and
+  // z must not be the accumulator (it holds the chain's running value).
+  P.eqsel.assign(n, 0);
+  auto not_acc = [](uint32_t o) { return (o >> 14) != MGP_K_ACC; };
+  for (uint32_t pc = 0; pc + 1 < n; ++pc) {
+    const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS, *J = I + MGP_INS_WORDS;
+    if (P.dead[pc] || P.dead[pc + 1] || v1_op(I) != MGP_OP_EQ || v1_op(J) != MGP_OP_ITE) continue;
+    if (P.inv[pc] || P.comb[pc] || P.dst[pc] != 0xFFFFFFFFu) continue;
+    const uint32_t t = (I[0] >> 16) & 0xFFu;
+    if (t == MGP_BOOL_TRUE || t == MGP_BOOL_FALSE || (J[1] & 0xFFFFu) != t) continue;
+    if (!not_acc(I[1] & 0xFFFFu) || !not_acc(I[1] >> 16) || !not_acc(J[1] >> 16) || not_acc(J[2] & 0xFFFFu))
+      continue;
+    if (X.live_after(pc + 2, t)) continue;
+    P.dead[pc] = 1;
+    P.eqsel[pc + 1] = 1;
+    ++pc;
+  }
 }
 
 // w0 = first-handler offset | op-handler offset << 16.  A uop dispatched straight to its
@@ -582,6 +631,90 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         emit(w0_of(first, opid), (ra ? 0u : a.param) | (b.param << 16), w2 | flags, w3);
         continue;
       }
+      // the slot a BV result is stored to: a register slot, an LDS slot, or a spill row (the
+      // op keeps its result in vA; a VST uop behind it writes the row)
+      auto store_to = [&](uint32_t d_slot, uint32_t &flags, uint32_t &w2, int32_t &vst_row) {
+        const Opnd d = T.bv(MGP_OPND(MGP_K_SLOT, d_slot));
+        if (d.kind == KRVAR) {
+          flags |= MGP_UF_STORE | MGP_UF_REGST;
+          w2 |= d.param;
+        } else if (d.kind == KVAR) {
+          vst_row = (int32_t)d.param;
+        } else {
+          flags |= MGP_UF_STORE;
+          w2 |= d.param;
+        }
+      };
+      if (op == MGP_OP_ITE && BP.eqsel[pc] && pc + 2 < T.n_ins && BP.eqsel[pc + 2]) {
+        // a run of select steps comparing one operand q against keys that are all 32-bit
+        // constants (TSEL) or all LDS slots (TSELS), each selecting an HBM variable (a
+        // calldata / memory byte table): one uop over a table behind the pool
+        auto eq_ops = [&](uint32_t p, uint32_t *x, uint32_t *y) {
+          const uint32_t *E = ins + (size_t)(p - 1) * MGP_INS_WORDS;
+          *x = E[1] & 0xFFFFu;
+          *y = E[1] >> 16;
+        };
+        struct Run {
+          std::vector<std::pair<uint32_t, uint32_t>> ent;
+          int cls = 0;  // 1: constant keys (TSEL), 2: slot keys, LDS or bank (TSELS)
+          uint32_t end = 0;
+        };
+        // the steps from pc on that compare qraw with a key of one class and select a variable
+        auto collect = [&](uint32_t qraw) {
+          Run r;
+          r.end = pc;
+          for (uint32_t p = pc; p < T.n_ins && BP.eqsel[p]; p += 2) {
+            const uint32_t *J = ins + (size_t)p * MGP_INS_WORDS;
+            uint32_t x, y;
+            eq_ops(p, &x, &y);
+            if (x != qraw && y != qraw) break;
+            const uint32_t key = x == qraw ? y : x;
+            uint32_t kv = 0;
+            int c = 0;
+            if ((key >> 14) == MGP_K_CONST) {
+              if (T.small_const(key, &kv)) c = 1;
+            } else if ((key >> 14) != MGP_K_ACC) {
+              const Opnd k = T.bv(key);
+              // TSELS key word: LDS byte offset, or bit 31 + bank offset 8p in [23:16]
+              if (k.kind == KSLOT) { c = 2; kv = k.param; }
+              else if (k.kind == KRVAR) { c = 2; kv = 0x80000000u | (k.param << 16); }
+            }
+            const Opnd z = T.bv(J[1] >> 16);
+            if (!c || (r.cls && c != r.cls) || z.kind != KVAR) break;
+            r.cls = c;
+            r.ent.emplace_back(kv, z.param);
+            r.end = p;
+            if ((J[0] >> 24) & MGP_INS_STORE) break;  // a stored step ends the run
+          }
+          return r;
+        };
+        uint32_t a0, b0;
+        eq_ops(pc, &a0, &b0);
+        Run ra = collect(a0), rb = a0 == b0 ? Run() : collect(b0);
+        const bool use_a = ra.ent.size() >= rb.ent.size();
+        const uint32_t qraw = use_a ? a0 : b0;
+        const Run &run = use_a ? ra : rb;
+        const std::vector<std::pair<uint32_t, uint32_t>> &ent = run.ent;
+        const int cls = run.cls;
+        const uint32_t end = run.end;
+        const uint32_t n_pool = (uint32_t)((T.ms.size() + T.v1pool.size()) / 8);
+        const uint32_t tpos = n_pool * 4u + (uint32_t)(T.tables.size() / 2);  // (pool bytes + table bytes) / 8
+        const Opnd q = T.bv(qraw);
+        if (ent.size() >= MGP_U_TSEL_MIN && tpos + ent.size() + 8 < 0xFFFFu && q.kind != KACC &&
+            !(cls == 1 && q.kind == KCONST)) {
+          uint32_t n_ent;
+          const uint32_t toff = T.add_table(ent, cls == 1, &n_ent);
+          const uint32_t *J = ins + (size_t)end * MGP_INS_WORDS;
+          uint32_t flags = 0, w2 = 0;
+          int32_t vst_row = -1;
+          if ((J[0] >> 24) & MGP_INS_STORE) store_to(((J[0] >> 16) & 0xFFu) | ((J[3] & 0xFFu) << 8), flags, w2, vst_row);
+          emit(w0_of(fetch_id(q.kind, KNONE, true), cls == 1 ? MGP_U_TSEL : MGP_U_TSELS), q.param, w2 | flags,
+               n_ent | ((n_pool * 4u + toff / 2u) << 16));
+          if (vst_row >= 0) emit(w0_of(MGP_U_VST, MGP_U_VST), 0u, (uint32_t)vst_row, 0u);
+          pc = end;
+          continue;
+        }
+      }
       // ---- BV-producing
       uint32_t flags = 0, w2 = 0, w3 = 0, opid = 0;
       Opnd a = {KNONE, 0}, b = {KNONE, 0};
@@ -655,6 +788,14 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
           break;
         case MGP_OP_ITE:
+          if (BP.eqsel[pc]) {  // the folded EQ's operands are fetched (x -> vC, y -> vB)
+            const uint32_t *E = I - MGP_INS_WORDS;
+            const Opnd z = T.bv(ob);
+            a = T.bv(E[1] & 0xFFFFu); b = T.bv(E[1] >> 16);
+            opid = MGP_U_EQSEL_FIRST + (uint32_t)(z.kind - KSLOT);
+            w3 |= z.param << 16;
+            break;
+          }
           a = T.bv(ob); b = T.bv(oc); opid = MGP_U_ITE;
           w3 |= T.boolslot(oa) << 16;
           break;
@@ -666,20 +807,12 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         flags |= MGP_UF_MASK;
         w2 |= T.mask_off(width) << 16;
       }
-      // the slot the result is stored to: a register slot, an LDS slot, or a spill row
-      // (the op keeps its result in vA; a VST uop behind it writes the row)
       int32_t vst_row = -1;
-      if (store) {
-        const Opnd d = T.bv(MGP_OPND(MGP_K_SLOT, dst));
-        if (d.kind == KRVAR) {
-          flags |= MGP_UF_STORE | MGP_UF_REGST;
-          w2 |= d.param;
-        } else if (d.kind == KVAR) {
-          vst_row = (int32_t)d.param;
-        } else {
-          flags |= MGP_UF_STORE;
-          w2 |= d.param;
-        }
+      if (store) store_to(dst, flags, w2, vst_row);
+      if (op == MGP_OP_ITE && BP.eqsel[pc]) {
+        emit(w0_of(fetch_id(a.kind, b.kind, true), opid), a.param | (b.param << 16), w2 | flags, w3);
+        if (vst_row >= 0) emit(w0_of(MGP_U_VST, MGP_U_VST), 0u, (uint32_t)vst_row, 0u);
+        continue;
       }
       opid = epi_variant(opid, (flags & MGP_UF_STORE) != 0, (flags & MGP_UF_MASK) != 0,
                          (flags & MGP_UF_REGST) != 0);
@@ -714,6 +847,8 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     T.ms_base = (uint32_t)(T.ms.size() / 8);
     const size_t n_ms = T.ms.size();
     uops.clear();
+    T.tables.clear();
+    T.table_at.clear();
     translate();
     if (T.ms.size() != n_ms) T.bad = true;  // pass 2 found a constant pass 1 did not
   }
@@ -749,5 +884,6 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   out[base + 3] = (uint32_t)n_pool | (T.var_mask << 8) | (T.n_lds << 16);
   out.insert(out.end(), T.ms.begin(), T.ms.end());
   out.insert(out.end(), T.v1pool.begin(), T.v1pool.end());
+  out.insert(out.end(), T.tables.begin(), T.tables.end());
   return 0;
 }

@@ -18,6 +18,8 @@ at word offset align4(4 + 4*n_ins + 8*n_consts) + 4 from the program start):
   pool     n_pool <= 255 constants, 8 little-endian u32 limbs each: the width masks
            2^w-1 and sign constants 2^(w-1) the uops use first (their index fields
            are 6 bits), then the v1 pool; handlers read an entry with one scalar load
+  tables   the TSEL tables: (key, variable index) u32 pairs, 8-entry blocks (scalar
+           loads of 64 B), identical tables stored once
 
 uop words:
   w0 [15:0]  entry offset / 4 (from the kernel entry) of the FIRST handler: a fetch
@@ -47,7 +49,8 @@ uop words:
   VST: w2 [15:0] candidate variable row the lane's vA is stored to (a spill slot)
   w3 [5:0]  sign-constant pool index, [12:8] uniform shift bits (SHLI/LSHRI/ASHRI/CONCAT),
      [15:8] compares with BCOMB: the other Bool operand * 2,
-     [31:16] Bool destination * 2 (compares, Bool ops) or ITE condition * 2
+     [31:16] Bool destination * 2 (compares, Bool ops) or ITE condition * 2, or the
+             EQSEL_<kind> select operand's parameter
 
 Registers of the interpreter: vA (accumulator / operand A), vB (operand B),
 vC (operand A of a compare that is not the accumulator); Bool slots are
@@ -119,8 +122,26 @@ XV_LIST = [("acc", "rvar", "A", o) for o in ("MUL", "ITE", "ITE_R", "SLT_RA")] +
           [("rvar", "none", "A", o) for o in ("NOT", "NOT_R") + tuple(f"LSHRI{k}" for k in range(8))]
 XV_OPS = [f"XV_{ka}_{kb}_{t}_{o}" for ka, kb, t, o in XV_LIST]
 
+# one step of a select chain (Select over a Store chain, calldata byte tables, lowered as
+# `EQ key k_i` + `ITE(that, v_i, acc)`): vA = (vC == vB) ? Z : vA, with the compared
+# operands fetched by F_<kx>_<ky>_C and Z (operand kind <zk>, parameter w3[31:16]) read by
+# the op handler while the compare runs.  The translator fuses an EQ whose Bool result only
+# the next ITE reads (as its condition, the else operand being the accumulator).
+EQSEL_OPS = [f"EQSEL_{k}" for k in KINDS[1:]]
+
+# a run of select-chain steps over one key q (fetched into vC by F_<kq>_none_C) against
+# 32-bit constants k_i, selecting HBM variables z_i: one TSEL uop over a table of (k_i, z_i)
+# u32 pairs behind the pool (w3[15:0] entries, w3[31:16] = the table's byte offset from the
+# pool / 8, keys distinct, padded to 8 entries).  vA = z_i where q == k_i (the last i in
+# chain order), else vA unchanged; the handler compares q against 8 keys per scalar load
+# and issues each z_i row load under the lanes that match it.  TSELS: the same with keys in
+# LDS slots (pairs (slot byte offset, z_i), chain order kept: a lane's last match wins, as
+# the row loads of one wave return in issue order) -- a Store chain at symbolic indices read
+# at one index.
+TSEL_MIN = 3     # shorter runs stay EQSEL uops
+
 OPS = BOOL_OPS + MEM_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + \
-    XS_OPS + XC_OPS + XV_OPS
+    XS_OPS + XC_OPS + XV_OPS + EQSEL_OPS + ["TSEL", "TSELS"]
 # handler 0 stops the wave with MGP_UNDECIDED: an all-zero uop (the prefetch pad) or any
 # id past the table ends the program instead of running off into memory
 HANDLERS = ["INVALID"] + FETCH + OPS
@@ -174,6 +195,8 @@ def c_header() -> str:
     lines.append(f"#define MGP_U_XS_FIRST {ID[XS_OPS[0]]}")
     lines.append("static const unsigned short kXsBase[%d] = {%s};" % (len(XS_BASE), ", ".join(
         f"MGP_U_{o}" for o in XS_BASE)))
+    lines.append(f"#define MGP_U_EQSEL_FIRST {ID[EQSEL_OPS[0]]}")
+    lines.append(f"#define MGP_U_TSEL_MIN {TSEL_MIN}")
     lines.append(f"#define MGP_U_XC_FIRST {ID[XC_OPS[0]]}")
     lines.append("static const unsigned short kXcBase[%d] = {%s};" % (len(XC_BASE), ", ".join(
         f"MGP_U_{o}" for o in XC_BASE)))

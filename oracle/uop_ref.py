@@ -214,6 +214,24 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
         # BV-producing
         if op == "ITE":
             vA = vA if bools[w3 >> 17] else vB
+        elif op.startswith("EQSEL_"):   # select-chain step: vA = (vC == vB) ? Z : vA
+            z = load(op[6:], w3 >> 16)
+            vA = z if vC == vB else vA
+        elif op == "TSEL":              # table of (key, variable) pairs behind the pool
+            t0 = pool0 + 2 * (w3 >> 16)
+            n_ent = w3 & 0xFFFF
+            keys = [int(words[t0 + 2 * i]) for i in range(n_ent)]
+            assert len(set(keys)) == n_ent, "TSEL keys must be distinct"
+            for i in range(n_ent):
+                if vC == keys[i]:
+                    vA = load("var", int(words[t0 + 2 * i + 1]))
+        elif op == "TSELS":             # keys in LDS / bank slots, chain order
+            t0 = pool0 + 2 * (w3 >> 16)
+            for i in range(w3 & 0xFFFF):
+                kw = int(words[t0 + 2 * i])
+                key = bank[((kw >> 16) & 0xFF) // 8] if kw >> 31 else lds[kw & 0xFFFF]
+                if vC == key:
+                    vA = load("var", int(words[t0 + 2 * i + 1]))
         elif op in ("ADD", "SUB", "MUL", "AND", "OR", "XOR"):
             vA = {"ADD": vA + vB, "SUB": vA - vB, "MUL": vA * vB, "AND": vA & vB,
                   "OR": vA | vB, "XOR": vA ^ vB}[op] & M256

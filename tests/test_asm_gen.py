@@ -51,9 +51,18 @@ def test_branches_are_forward(asm):
         assert tgt in pos, f"undefined label {tgt}"
         if pos[tgt] > i:
             continue
+        n_back += 1
+        if re.match(r"\.Ltsels?_\d+$", tgt):
+            # the TSEL / TSELS table loop: 8 entries per pass, bounded by the entry count
+            # s55, which every pass decrements before the loop test
+            assert lines[i - 1].strip() == "s_cmp_gt_i32 s55, 0", lines[i - 1]
+            assert lines[i - 2].strip() == "s_sub_u32 s55, s55, 8", lines[i - 2]
+            assert l.strip().startswith("s_cbranch_scc1")
+            assert not any("s55" in x and not x.strip().startswith(("s_cmp", "s_sub_u32 s55", "s_and_b32 s55"))
+                           for x in lines[pos[tgt]:i]), "the loop counter is only decremented"
+            continue
         # a return from an out-of-line block: must land right after the forward branch
         # that entered this block (so it cannot loop)
-        n_back += 1
         assert re.match(r"\.L(km|kh)back_\d+$", tgt), f"backward branch at line {i}: {l.strip()}"
         enter = lines[pos[tgt] - 1].strip()
         assert enter.startswith("s_cbranch_scc1"), enter

@@ -584,6 +584,90 @@ def _band4n_states(rng, n, late_vars: int = 0):
     return out
 
 
+def _select_chain_states(rng, n):
+    """Select chains as LASER's arrays lower (a Select over a Store chain, calldata.py /
+    array.py: `EQ q k_i` + `ITE(that, z_i, acc)` pairs): per state two or three chains over
+    one set of keys, each chain comparing its q (a bank variable, a computed slot or a
+    constant) against keys that are small constants (repeated, some with high limbs set)
+    or computed slots (x + i, shared by the chains, and x & 3, which several lanes match
+    at once), selecting HBM variables, the bank variable 5 or a computed byte.  Root:
+    some chain == T.  The translator's EQSEL, TSEL and TSELS fusions all fire on these
+    (tests/test_lowering.py counts them)."""
+    out = []
+    for _ in range(n):
+        m = int(rng.integers(8, 40))
+        nl = [[S.VAR, 256, -1, -1, -1, k, 0] for k in range(5)]     # 0-4
+        nl.append([S.VAR, 256, -1, -1, -1, 5, 0])                    # 5: base / bank value
+        cl = []
+
+        def add(row):
+            nl.append(row)
+            return len(nl) - 1
+
+        def const(val):
+            cl.append(val)
+            return add([S.CONST, 256, -1, -1, -1, len(cl) - 1, 0])
+
+        zs = [add([S.VAR, 256, -1, -1, -1, 6 + i, 0]) for i in range(m)]
+        t = add([S.VAR, 256, -1, -1, -1, 6 + m, 0])
+        byte = add([S.AND, 256, 2, const(0xFF), -1, 0, 0])
+        slot_keys = [add([S.ADD, 256, 1, const(i), -1, 0, 0]) for i in range(int(rng.integers(4, 20)))]
+        slot_keys += [add([S.AND, 256, 2 + int(rng.integers(3)), const(3), -1, 0, 0]) for _ in range(3)]
+        masked = add([S.AND, 256, 0, const(0x3F), -1, 0, 0])
+        eqs = []
+        for _c in range(int(rng.integers(2, 4))):
+            qk = int(rng.integers(3))
+            q = 0 if qk == 0 else masked if qk == 1 else const(int(rng.integers(0, 24)))
+            acc = 5
+            for i in range(int(rng.integers(3, m + 1))):
+                r = rng.random()
+                if qk == 2 or r < 0.3:
+                    key = slot_keys[int(rng.integers(len(slot_keys)))]
+                elif r < 0.85:
+                    key = const(int(rng.integers(0, 48)))
+                else:
+                    key = const((int(rng.integers(1, 4)) << int(rng.choice([32, 100, 255]))) + int(rng.integers(0, 48)))
+                r = rng.random()
+                z = zs[i % m] if r < 0.85 else 5 if r < 0.92 else byte
+                c = add([S.EQ, 1, q, key, -1, 0, 0] if rng.random() < 0.5 else [S.EQ, 1, key, q, -1, 0, 0])
+                acc = add([S.ITE, 256, c, z, acc, 0, 0])
+            eqs.append(add([S.EQ, 1, acc, t, -1, 0, 0]))
+        root = eqs[0]
+        for e in eqs[1:]:
+            root = add([S.BOR, 1, root, e, -1, 0, 0])
+        out.append((nl, cl))
+    return out
+
+
+def _select_chain_cands(rng, states, n_cand):
+    """Candidates for _select_chain_states: variables 0-4 small (keys and q collide), a
+    tenth with high limbs set over a small low limb (TSEL must compare all 256 bits), the
+    selected values and T in 0..3 (the root holds often)."""
+    n_vars = max(max(r[5] for r in nl if r[0] == S.VAR) + 1 for nl, _ in states)
+    cands = np.zeros((len(states), n_cand, n_vars, 8), np.uint32)
+    cands[:, :, :, 0] = rng.integers(0, 4, size=(len(states), n_cand, n_vars))
+    cands[:, :, :5, 0] = rng.integers(0, 48, size=(len(states), n_cand, 5))
+    hi = rng.random((len(states), n_cand, 5)) < 0.1
+    cands[:, :, :5, int(rng.integers(1, 8))] = np.where(hi, 1, 0)
+    return cands
+
+
+def test_select_chain_fusions_vs_oracle(mgp_ctx):
+    """EQSEL / TSEL / TSELS (the select-chain uops of the gfx950 translation) against the C
+    oracle on every candidate (both engines; the HIP engine runs the v1 ITE chains)."""
+    rng = np.random.default_rng(515)
+    states = _select_chain_states(rng, 300)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = _select_chain_cands(rng, states, 256)
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    bad = np.nonzero(first != ref)[0]
+    assert bad.size == 0, f"{bad.size} states differ, e.g. {bad[:5]} gpu={first[bad[:5]]} ref={ref[bad[:5]]}"
+    assert (ref > 0).sum() > 50 and (ref < 0).sum() < len(states)
+
+
 def _mul_after_shift_states(rng, n):
     """A per-lane shift (its handler leaves v6 = 32 - amount, or all-ones for amounts >=
     256) and then MULs whose products' high limbs decide a compare.  The r3n defect: the

@@ -628,3 +628,64 @@ def test_band4n_then_hbm_variable_loads_uop_reference():
             seen |= nm.startswith("BAND4N")
             hit += seen and "_var_" in nm
     assert hit > 20, hit
+
+
+def test_select_chain_fusions_uop_reference_matches_oracle():
+    """Select chains (EQ + ITE pairs over one key) fused into EQSEL / TSEL / TSELS uops: the
+    uop reference interpreter agrees with the C oracle on every candidate, and each fusion
+    fires (CPU side of tests/test_gpu_parity.py::test_select_chain_fusions_vs_oracle)."""
+    from oracle import coracle
+
+    from .test_gpu_parity import _select_chain_cands, _select_chain_states
+
+    rng = np.random.default_rng(516)
+    states = _select_chain_states(rng, 60)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = _select_chain_cands(rng, states, 16)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    names = UR._names()
+    seen = {"EQSEL": 0, "TSEL": 0, "TSELS": 0}
+    for s in range(len(states)):
+        rows = [[S.limbs_to_int(cands[s, k, v]) for v in range(cands.shape[2])] for k in range(cands.shape[1])]
+        assert UR.first_sat_uops(words, int(po[s]), rows) == ref[s], s
+        u0 = UR.uop_offset(words, int(po[s]))
+        for k in range(int(words[u0])):
+            nm = names[int(words[u0 + 4 + 4 * k]) >> 16]
+            if nm.startswith("EQSEL"):
+                seen["EQSEL"] += 1
+            elif nm in seen:
+                seen[nm] += 1
+    assert all(v > 10 for v in seen.values()), seen
+    assert 0 < (ref >= 0).sum() < len(states) or (ref > 0).sum() > 5
+
+
+def test_contract_select_tables_uop_reference():
+    """WalletLibrary's calldata byte tables (TSEL) and symbolic-index Store chains (TSELS)
+    through the uop reference interpreter, against the C oracle."""
+    import corpus
+    from corpus.keccak_manager import KeccakFunctionManager
+    from mythril_amd import dag as D
+    from mythril_amd import front as F
+    from oracle import coracle
+
+    kfm = KeccakFunctionManager()
+    items = corpus.wallet_states(0, kfm)[:3]
+    B = F.Batch([list(c[1]) for c in items])
+    nv = B.n_vars()
+    _, dom = N.refute_domains(*B.packed(), B.var_off)
+    cands = N.make_candidates(8, nv, 7, B.var_off, B.var_width, B.hint_off, B.hints, B.alias_off, B.aliases,
+                              B.const_off, B.consts, D._FIXED_LIMBS, np.zeros(B.n_states, np.uint8),
+                              var_kind=B.var_kind, dom=dom)
+    nodes, noff, consts, coff = B.packed(gpu=True)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    words, po, status = N.lower(nodes, noff, consts, coff)
+    names = UR._names()
+    for s in range(B.n_states):
+        rows = [[S.limbs_to_int(cands[s, k, v]) for v in range(nv)] for k in range(8)]
+        assert UR.first_sat_uops(words, int(po[s]), rows) == ref[s], s
+        u0 = UR.uop_offset(words, int(po[s]))
+        ops = [names[int(words[u0 + 4 + 4 * k]) >> 16] for k in range(int(words[u0]))]
+        assert ops.count("TSEL") > 10 and ops.count("TSELS") > 10, s
+    B.close()

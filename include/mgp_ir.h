@@ -107,6 +107,10 @@ enum mgp_op {
 
   /* bytecode only */
   MGP_OP_MOV = 80,    /* dst = a masked to width */
+  /* one step of an f-application chain (UFAPP above; a Select over a Store chain, a
+   * calldata byte table): result = (a == b) ? c : ACC, the else value being the
+   * accumulator (the previous BV instruction's result); a, b, c never name ACC */
+  MGP_OP_EQSEL = 81,
   MGP_OP_RET = 90     /* root = Bool operand a   */
 };
 

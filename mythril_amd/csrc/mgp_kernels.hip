@@ -316,6 +316,9 @@ __global__ __launch_bounds__(MGP_WAVE) void mgp_eval_kernel(
       if (op == MGP_OP_ITE) {
         const bool cond = ((bools[c] >> oa) & 1ull) != 0ull;
         r = bv_sel(cond, fetch<CPL>(ob, acc[c], e, c, cand[c]), fetch<CPL>(oc, acc[c], e, c, cand[c]));
+      } else if (op == MGP_OP_EQSEL) {  // select-chain step: (a == b) ? c : acc
+        const bool hit = bv_eq(fetch<CPL>(oa, acc[c], e, c, cand[c]), fetch<CPL>(ob, acc[c], e, c, cand[c]));
+        r = bv_sel(hit, fetch<CPL>(oc, acc[c], e, c, cand[c]), acc[c]);
       } else if (is_unary_bv(op)) {
         r = eval_unary(op, fetch<CPL>(oa, acc[c], e, c, cand[c]), imm);
       } else {

@@ -50,6 +50,7 @@ struct VIns {
   bool is_bool;     // produces a Bool
   Ref a, b, c;
   uint32_t imm;
+  Ref d;            // EQSEL: the else value (emitted as the accumulator)
 };
 
 inline bool op_is_bool_result(uint8_t op) {
@@ -88,8 +89,9 @@ struct LowerState {
   std::unordered_map<ConstKey, uint32_t, ConstHash> pool_map;
   uint32_t max_var = 0;  // 1 + highest var index used
 
-  Ref add(uint8_t op, uint16_t width, bool is_bool, Ref a, Ref b = Ref(), Ref c = Ref(), uint32_t imm = 0) {
-    ins.push_back(VIns{op, width, is_bool, a, b, c, imm});
+  Ref add(uint8_t op, uint16_t width, bool is_bool, Ref a, Ref b = Ref(), Ref c = Ref(), uint32_t imm = 0,
+          Ref d = Ref()) {
+    ins.push_back(VIns{op, width, is_bool, a, b, c, imm, d});
     Ref r;
     r.k = R_INS;
     r.idx = (uint32_t)ins.size() - 1;
@@ -177,10 +179,10 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
   // The caller keeps whichever schedule needs the fewest LDS slots.
   if (sched != 0) {
     const uint32_t n0 = (uint32_t)S.ins.size();
-    auto kids = [&](uint32_t t, uint32_t out[3]) -> int {
+    auto kids = [&](uint32_t t, uint32_t out[4]) -> int {
       int k = 0;
       const VIns &I = S.ins[t];
-      for (const Ref *r : {&I.a, &I.b, &I.c})
+      for (const Ref *r : {&I.a, &I.b, &I.c, &I.d})
         if (r->k == R_INS) {
           bool dup = false;
           for (int j = 0; j < k; ++j) dup |= out[j] == r->idx;
@@ -193,9 +195,9 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
     if (sched == 1) {
       std::vector<uint32_t> need(n0, 1);
       for (uint32_t t = 0; t < n0; ++t) {
-        uint32_t ch[3];
+        uint32_t ch[4];
         const int k = kids(t, ch);
-        uint32_t nd[3] = {0, 0, 0};
+        uint32_t nd[4] = {0, 0, 0, 0};
         for (int i = 0; i < k; ++i) nd[i] = need[ch[i]];
         std::sort(nd, nd + k, [](uint32_t x, uint32_t y) { return x > y; });
         uint32_t m = 1;
@@ -210,7 +212,7 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
         if (state[t] == 2) { stack.pop_back(); continue; }
         if (state[t] == 1) { state[t] = 2; order.push_back(t); stack.pop_back(); continue; }
         state[t] = 1;
-        uint32_t ch[3];
+        uint32_t ch[4];
         const int k = kids(t, ch);
         std::sort(ch, ch + k, [&](uint32_t x, uint32_t y) { return need[x] < need[y]; });
         for (int i = 0; i < k; ++i)
@@ -223,7 +225,7 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
       std::vector<uint32_t> uses(n0, 0), pending(n0, 0);
       std::vector<std::vector<uint32_t>> users(n0);
       for (uint32_t t = 0; t < n0; ++t) {
-        uint32_t ch[3];
+        uint32_t ch[4];
         const int k = kids(t, ch);
         pending[t] = (uint32_t)k;
         for (int i = 0; i < k; ++i) {
@@ -240,7 +242,7 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
         int best_score = -1000, best_recent = -1;
         for (size_t r = 0; r < ready.size(); ++r) {
           const uint32_t t = ready[r];
-          uint32_t ch[3];
+          uint32_t ch[4];
           const int k = kids(t, ch);
           int score = 0, recent = 0;
           for (int i = 0; i < k; ++i) {
@@ -256,7 +258,7 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
         ready.erase(ready.begin() + (ptrdiff_t)best);
         order.push_back(t);
         last = t;
-        uint32_t ch[3];
+        uint32_t ch[4];
         const int k = kids(t, ch);
         for (int i = 0; i < k; ++i) uses[ch[i]]--;
         for (uint32_t u : users[t])
@@ -269,7 +271,7 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
       std::vector<VIns> re(n0);
       for (uint32_t i = 0; i < n0; ++i) {
         VIns I = S.ins[order[i]];
-        for (Ref *r : {&I.a, &I.b, &I.c})
+        for (Ref *r : {&I.a, &I.b, &I.c, &I.d})
           if (r->k == R_INS) r->idx = remap[r->idx];
         re[i] = I;
       }
@@ -390,7 +392,7 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
       std::vector<Ref> dref(n0);  // the 1-bit value of a demoted Bool
       for (uint32_t t = 0; t < n0; ++t) {
         VIns I = S.ins[t];
-        for (Ref *r : {&I.a, &I.b, &I.c})
+        for (Ref *r : {&I.a, &I.b, &I.c, &I.d})
           if (r->k == R_INS) r->idx = remap[r->idx];
         Ref *br[3], *nr[3];
         const int k = bool_refs(S.ins[t], br);
@@ -457,6 +459,14 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
       use(I.a, t, true); use(I.b, t, true); use(I.c, t, true);
     } else if (I.op == MGP_OP_ITE) {
       use(I.a, t, true); use(I.b, t, false); use(I.c, t, false);
+    } else if (I.op == MGP_OP_EQSEL) {
+      // a, b, c are read from slots (the accumulator holds the else value d; a d that
+      // is not the previous BV result is moved into it first, from its slot)
+      for (const Ref *r : {&I.a, &I.b, &I.c}) {
+        use(*r, t, false);
+        if (r->k == R_INS) needs_slot[r->idx] = 1;
+      }
+      use(I.d, t, false);
     } else {
       use(I.a, t, false); use(I.b, t, false); use(I.c, t, false);
     }
@@ -506,9 +516,27 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
   for (uint32_t t = 0; t < n; ++t) {
     const VIns &I = S.ins[t];
     uint32_t oa, ob = 0, oc = 0;
-    const uint32_t base = (uint32_t)out.size();
+    uint32_t base = (uint32_t)out.size();
     if (op_takes_bools(I.op)) {
       oa = bool_opnd(I.a); ob = bool_opnd(I.b); oc = bool_opnd(I.c);
+    } else if (I.op == MGP_OP_EQSEL) {
+      if (!(I.d.k == R_INS && prev_bv[t] == (int64_t)I.d.idx)) {
+        // the else value into the accumulator: MOV d (a variable, constant or slot)
+        out.push_back((uint32_t)MGP_OP_MOV | (((uint32_t)(I.width - 1) & 0xFFu) << 8));
+        out.push_back(bv_opnd(I.d, t) & 0xFFFFu);
+        out.push_back(0u);
+        out.push_back(0u);
+        if (in_slot(I.d, t)) slot_fields.push_back({base + 1, 0});
+        ++n_emit;
+      }
+      base = (uint32_t)out.size();  // this instruction's first word
+      auto no_acc = [&](const Ref &r) {
+        return r.k == R_INS ? MGP_OPND(MGP_K_SLOT, (uint32_t)loc[r.idx]) : bv_opnd(r, t);
+      };
+      oa = no_acc(I.a); ob = no_acc(I.b); oc = no_acc(I.c);
+      if (I.a.k == R_INS) slot_fields.push_back({base + 1, 0});
+      if (I.b.k == R_INS) slot_fields.push_back({base + 1, 16});
+      if (I.c.k == R_INS) slot_fields.push_back({base + 2, 0});
     } else if (I.op == MGP_OP_ITE) {
       oa = bool_opnd(I.a); ob = bv_opnd(I.b, t); oc = bv_opnd(I.c, t);
       if (in_slot(I.b, t)) slot_fields.push_back({base + 1, 16});
@@ -1092,9 +1120,9 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           const int ke = known_eq_forms(form, it->form);
           if (ke == 0) continue;
           if (ke == -1 && arg.size() == 1 && it->arg.size() == 1 && v.size() == 1 && it->fresh.size() == 1) {
-            // the one-piece case of the line below, without piece-list temporaries
-            const Ref e = S.add(MGP_OP_EQ, (uint16_t)arg[0].w, true, arg[0].r, it->arg[0].r);
-            v[0].r = S.add(MGP_OP_ITE, (uint16_t)v[0].w, false, e, it->fresh[0].r, v[0].r);
+            // the one-piece case of the line below as one EQSEL step (no Bool, one
+            // instruction instead of EQ + ITE)
+            v[0].r = S.add(MGP_OP_EQSEL, (uint16_t)v[0].w, false, arg[0].r, it->arg[0].r, it->fresh[0].r, 0, v[0].r);
             continue;
           }
           v = (ke == 1) ? it->fresh : ite_pieces(eq_pieces(arg, it->arg), it->fresh, v);
@@ -1143,7 +1171,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     for (int64_t t = (int64_t)n0 - 1; t >= 0; --t) {
       if (!live[t]) continue;
       const VIns &I = S.ins[t];
-      for (const Ref *r : {&I.a, &I.b, &I.c})
+      for (const Ref *r : {&I.a, &I.b, &I.c, &I.d})
         if (r->k == R_INS) live[r->idx] = 1;
     }
     std::vector<uint32_t> remap(n0, 0);
@@ -1153,7 +1181,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
       if (!live[t]) continue;
       remap[t] = (uint32_t)kept.size();
       VIns I = S.ins[t];
-      for (Ref *r : {&I.a, &I.b, &I.c})
+      for (Ref *r : {&I.a, &I.b, &I.c, &I.d})
         if (r->k == R_INS) r->idx = remap[r->idx];
       kept.push_back(I);
     }
@@ -1166,7 +1194,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     std::vector<int64_t> cmap(S.pool.size(), -1);
     std::vector<ConstKey> used;
     for (VIns &I : S.ins)
-      for (Ref *r : {&I.a, &I.b, &I.c})
+      for (Ref *r : {&I.a, &I.b, &I.c, &I.d})
         if (r->k == R_CONST) {
           if (cmap[r->idx] < 0) {
             cmap[r->idx] = (int64_t)used.size();

@@ -527,7 +527,11 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   const uint32_t *ins = v1 + MGP_HDR_WORDS;
   if (v1_ok) T.v1pool.assign(ins + (size_t)T.n_ins * MGP_INS_WORDS, ins + (size_t)T.n_ins * MGP_INS_WORDS + (size_t)T.n_c * 8);
   std::vector<uint32_t> uops;
+  // pass 1 only collects the register variables and the mask / sign constants: it emits
+  // nothing and looks for no TSEL runs (a run reads the operands its steps would)
+  bool pass2 = false;
   auto emit = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    if (!pass2) return;
     uops.push_back(w0); uops.push_back(w1); uops.push_back(w2); uops.push_back(w3);
   };
 
@@ -645,28 +649,43 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           w2 |= d.param;
         }
       };
-      if (op == MGP_OP_ITE && BP.eqsel[pc] && pc + 2 < T.n_ins && BP.eqsel[pc + 2]) {
+      // select-chain steps: a v1 EQSEL, or an ITE whose condition is the folded EQ before it
+      // (BoolPlan::eqsel); each compares x with y and selects z over the accumulator
+      auto is_step = [&](uint32_t p) {
+        return p < T.n_ins && (v1_op(ins + (size_t)p * MGP_INS_WORDS) == MGP_OP_EQSEL || BP.eqsel[p]);
+      };
+      auto step_ops = [&](uint32_t p, uint32_t *x, uint32_t *y, uint32_t *z) {
+        const uint32_t *J = ins + (size_t)p * MGP_INS_WORDS;
+        const uint32_t *E = v1_op(J) == MGP_OP_EQSEL ? J : J - MGP_INS_WORDS;
+        *x = E[1] & 0xFFFFu;
+        *y = E[1] >> 16;
+        *z = v1_op(J) == MGP_OP_EQSEL ? J[2] & 0xFFFFu : J[1] >> 16;
+      };
+      // the step right after the step at p (0xFFFFFFFF: none)
+      auto next_step = [&](uint32_t p) -> uint32_t {
+        if (p + 1 < T.n_ins && v1_op(ins + (size_t)(p + 1) * MGP_INS_WORDS) == MGP_OP_EQSEL) return p + 1;
+        if (p + 2 < T.n_ins && BP.eqsel[p + 2]) return p + 2;
+        return 0xFFFFFFFFu;
+      };
+      if (pass2 && is_step(pc) && next_step(pc) != 0xFFFFFFFFu) {
         // a run of select steps comparing one operand q against keys that are all 32-bit
-        // constants (TSEL) or all LDS slots (TSELS), each selecting an HBM variable (a
-        // calldata / memory byte table): one uop over a table behind the pool
-        auto eq_ops = [&](uint32_t p, uint32_t *x, uint32_t *y) {
-          const uint32_t *E = ins + (size_t)(p - 1) * MGP_INS_WORDS;
-          *x = E[1] & 0xFFFFu;
-          *y = E[1] >> 16;
-        };
+        // constants (TSEL) or all LDS / bank slots (TSELS), each selecting an HBM variable
+        // (a calldata / memory byte table): one uop over a table behind the pool
         struct Run {
-          std::vector<std::pair<uint32_t, uint32_t>> ent;
+          uint32_t n = 0;
           int cls = 0;  // 1: constant keys (TSEL), 2: slot keys, LDS or bank (TSELS)
           uint32_t end = 0;
         };
-        // the steps from pc on that compare qraw with a key of one class and select a variable
-        auto collect = [&](uint32_t qraw) {
+        // the steps from pc on that compare qraw with a key of one class and select a
+        // variable; with `ent`, their (key word, variable) table entries (no allocation
+        // while runs are only measured: this runs at every step of every chain)
+        auto collect = [&](uint32_t qraw, std::vector<std::pair<uint32_t, uint32_t>> *ent) {
           Run r;
           r.end = pc;
-          for (uint32_t p = pc; p < T.n_ins && BP.eqsel[p]; p += 2) {
+          for (uint32_t p = pc; p != 0xFFFFFFFFu; p = next_step(p)) {
             const uint32_t *J = ins + (size_t)p * MGP_INS_WORDS;
-            uint32_t x, y;
-            eq_ops(p, &x, &y);
+            uint32_t x, y, zo;
+            step_ops(p, &x, &y, &zo);
             if (x != qraw && y != qraw) break;
             const uint32_t key = x == qraw ? y : x;
             uint32_t kv = 0;
@@ -679,29 +698,32 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
               if (k.kind == KSLOT) { c = 2; kv = k.param; }
               else if (k.kind == KRVAR) { c = 2; kv = 0x80000000u | (k.param << 16); }
             }
-            const Opnd z = T.bv(J[1] >> 16);
+            const Opnd z = T.bv(zo);
             if (!c || (r.cls && c != r.cls) || z.kind != KVAR) break;
             r.cls = c;
-            r.ent.emplace_back(kv, z.param);
+            ++r.n;
+            if (ent) ent->emplace_back(kv, z.param);
             r.end = p;
             if ((J[0] >> 24) & MGP_INS_STORE) break;  // a stored step ends the run
           }
           return r;
         };
-        uint32_t a0, b0;
-        eq_ops(pc, &a0, &b0);
-        Run ra = collect(a0), rb = a0 == b0 ? Run() : collect(b0);
-        const bool use_a = ra.ent.size() >= rb.ent.size();
+        uint32_t a0, b0, z0;
+        step_ops(pc, &a0, &b0, &z0);
+        const Run ra = collect(a0, nullptr), rb = a0 == b0 ? Run() : collect(b0, nullptr);
+        const bool use_a = ra.n >= rb.n;
         const uint32_t qraw = use_a ? a0 : b0;
         const Run &run = use_a ? ra : rb;
-        const std::vector<std::pair<uint32_t, uint32_t>> &ent = run.ent;
         const int cls = run.cls;
         const uint32_t end = run.end;
         const uint32_t n_pool = (uint32_t)((T.ms.size() + T.v1pool.size()) / 8);
         const uint32_t tpos = n_pool * 4u + (uint32_t)(T.tables.size() / 2);  // (pool bytes + table bytes) / 8
         const Opnd q = T.bv(qraw);
-        if (ent.size() >= MGP_U_TSEL_MIN && tpos + ent.size() + 8 < 0xFFFFu && q.kind != KACC &&
+        if (run.n >= MGP_U_TSEL_MIN && tpos + run.n + 8 < 0xFFFFu && q.kind != KACC &&
             !(cls == 1 && q.kind == KCONST)) {
+          std::vector<std::pair<uint32_t, uint32_t>> ent;
+          ent.reserve(run.n);
+          collect(qraw, &ent);
           uint32_t n_ent;
           const uint32_t toff = T.add_table(ent, cls == 1, &n_ent);
           const uint32_t *J = ins + (size_t)end * MGP_INS_WORDS;
@@ -787,11 +809,14 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           opid = MGP_U_CONCAT0 + (imm >> 5);
           w3 |= (imm & 31u) << MGP_U_SHIFT_B_POS;
           break;
+        case MGP_OP_EQSEL:
         case MGP_OP_ITE:
-          if (BP.eqsel[pc]) {  // the folded EQ's operands are fetched (x -> vC, y -> vB)
-            const uint32_t *E = I - MGP_INS_WORDS;
-            const Opnd z = T.bv(ob);
-            a = T.bv(E[1] & 0xFFFFu); b = T.bv(E[1] >> 16);
+          if (op == MGP_OP_EQSEL || BP.eqsel[pc]) {  // the compared operands are fetched (x -> vC, y -> vB)
+            uint32_t x, y, zo;
+            step_ops(pc, &x, &y, &zo);
+            const Opnd z = T.bv(zo);
+            a = T.bv(x); b = T.bv(y);
+            if (a.kind == KACC || b.kind == KACC || z.kind == KACC) { T.bad = true; break; }
             opid = MGP_U_EQSEL_FIRST + (uint32_t)(z.kind - KSLOT);
             w3 |= z.param << 16;
             break;
@@ -809,7 +834,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       }
       int32_t vst_row = -1;
       if (store) store_to(dst, flags, w2, vst_row);
-      if (op == MGP_OP_ITE && BP.eqsel[pc]) {
+      if (op == MGP_OP_EQSEL || (op == MGP_OP_ITE && BP.eqsel[pc])) {
         emit(w0_of(fetch_id(a.kind, b.kind, true), opid), a.param | (b.param << 16), w2 | flags, w3);
         if (vst_row >= 0) emit(w0_of(MGP_U_VST, MGP_U_VST), 0u, (uint32_t)vst_row, 0u);
         continue;
@@ -849,6 +874,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     uops.clear();
     T.tables.clear();
     T.table_at.clear();
+    pass2 = true;
     translate();
     if (T.ms.size() != n_ms) T.bad = true;  // pass 2 found a constant pass 1 did not
   }

@@ -12,7 +12,7 @@ from typing import List, Sequence
 from . import bvsem as S
 
 K_SLOT, K_CONST, K_ACC, K_VAR = 0, 1, 2, 3
-OP_MOV, OP_RET = 80, 90
+OP_MOV, OP_EQSEL, OP_RET = 80, 81, 90
 BOOL_FALSE, BOOL_TRUE = 62, 63
 LDS_SLOTS = 32   # MGP_LDS_SLOTS
 
@@ -78,6 +78,9 @@ def run_program(words: Sequence[int], off: int, xs: Sequence[int]):
         m = S.mask(width)
         if op == S.ITE:
             r = bv(ob) if bl(oa) else bv(oc)
+        elif op == OP_EQSEL:   # select-chain step; operands never name the accumulator
+            assert K_ACC not in (oa >> 14, ob >> 14, oc >> 14)
+            r = bv(oc) if bv(oa) == bv(ob) else acc
         elif op in (OP_MOV, S.ZEXT):
             r = bv(oa)
         elif op == S.NOT:

@@ -1015,21 +1015,34 @@ int core_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_
   };
   std::vector<uint32_t> cur(k);
   for (uint32_t i = 0; i < k; ++i) cur[i] = i;
-  if (!refuted(cur)) return 0;  // not refuted as a whole: keep everything
+  // The lists come from refutations, so the whole list is not tested first: a refuted
+  // subset (the analysis is monotone in the required conjuncts) shows it, and only a list
+  // none of whose trials is refuted pays the whole-list test.  The newer half goes first: a
+  // path's older constraints are its parent's, which were satisfiable.
+  bool shown = false;
   for (uint32_t h = 0; h < halvings && cur.size() >= 8; ++h) {
     const size_t m = cur.size() / 2;
     std::vector<uint32_t> lo(cur.begin(), cur.begin() + (int64_t)m), hi(cur.begin() + (int64_t)m, cur.end());
-    if (refuted(lo)) cur.swap(lo);
-    else if (refuted(hi)) cur.swap(hi);
+    if (refuted(hi)) cur.swap(hi);
+    else if (refuted(lo)) cur.swap(lo);
     else break;
+    shown = true;
   }
   if (cur.size() >= 2 && cur.size() <= max_single) {
     for (size_t i = 0; i < cur.size() && cur.size() > 1;) {
       std::vector<uint32_t> t(cur);
       t.erase(t.begin() + (int64_t)i);
-      if (refuted(t)) cur.swap(t);  // conjunct i is not needed: drop it for good
-      else ++i;
+      if (refuted(t)) {  // conjunct i is not needed: drop it for good
+        cur.swap(t);
+        shown = true;
+      } else {
+        ++i;
+      }
     }
+  }
+  if (!shown && !refuted(cur)) {  // not refuted as a whole: keep everything
+    for (uint32_t i = 0; i < k; ++i) keep[i] = 1;
+    return 0;
   }
   for (uint32_t i = 0; i < k; ++i) keep[i] = 0;
   for (uint32_t i : cur) keep[i] = 1;

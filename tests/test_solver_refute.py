@@ -195,9 +195,10 @@ def test_decision_rows_per_state_rule():
 
 def test_core_shrink_halving_finds_a_core_of_a_redundant_list():
     """A list reaching its contradiction twice (no single deletion alone breaks it) still
-    shrinks: a halving round keeps the half that is refuted alone, and without halvings the
-    greedy deletions (mgp_refute_cores, round 5: each deletion that keeps the list refuted is
-    kept) end on one of the two contradictions (UnsatCores.shrink_many)."""
+    shrinks: a halving round keeps the half that is refuted alone (the newer half is tried
+    first: a path's older constraints are its parent's), and without halvings the greedy
+    deletions (mgp_refute_cores, round 5: each deletion that keeps the list refuted is kept)
+    end on one of the two contradictions (UnsatCores.shrink_many)."""
     v = [BVS(f"h{i}", 256) for i in range(12)]
     x, y = BVS("hx", 256), BVS("hy", 256)
     # first half: one contradiction on x among fillers; second half: another on y
@@ -220,7 +221,7 @@ def test_core_shrink_halving_finds_a_core_of_a_redundant_list():
         core = SV.UnsatCores.shrink(N, terms)
     finally:
         SV.UnsatCores.HALVINGS = old
-    assert set(core) == {first[1].raw, first[3].raw}
+    assert set(core) == {second[1].raw, second[4].raw}
 
 
 def test_retry_round_groups(fe):

@@ -234,6 +234,39 @@ MGP_RD AV av_xor(const AV &a, const AV &b, uint32_t w) {
   return r;
 }
 
+// x >> w of the 512-bit value (hi, lo), as (high part, low part)
+MGP_RD void shr512(const V &hi, const V &lo, uint32_t w, V *qh, V *ql) {
+  if (w >= 256u) {
+    *qh = bv_zero();
+    *ql = SHR(hi, w - 256u);
+    return;
+  }
+  *qh = SHR(hi, w);
+  *ql = w ? OR(SHR(lo, w), SHL(hi, 256u - w)) : lo;
+}
+
+// c * [lo, hi] for every c of a small range [c0, c1] (a loop count, a batch size): each
+// product interval that stays inside one multiple of 2^w is exact mod 2^w, and the result
+// is their hull -- a product that wraps for every c of the range still gets a bound
+// (cnt * value with value near 2^w is near 2^w, never small).  false: some c's products
+// straddle a multiple of 2^w.
+MGP_RD bool mul_small_range(const V &c0, uint32_t n_c, const V &lo, const V &hi, uint32_t w, V *rlo, V *rhi) {
+  bool any = false;
+  V c = c0;
+  for (uint32_t k = 0; k < n_c; ++k, c = ADDV(c, ONE())) {
+    V pl, ph, ql1, qh1, ql2, qh2;
+    const V hl = bv_mul_full(c, lo, &pl), hh = bv_mul_full(c, hi, &ph);
+    shr512(hl, pl, w, &qh1, &ql1);
+    shr512(hh, ph, w, &qh2, &ql2);
+    if (!EQV(qh1, qh2) || !EQV(ql1, ql2)) return false;
+    const V a = AND(pl, M(w)), b = AND(ph, M(w));
+    *rlo = any ? MIN(*rlo, a) : a;
+    *rhi = any ? MAX(*rhi, b) : b;
+    any = true;
+  }
+  return any;
+}
+
 MGP_RD AV av_mul(const AV &a, const AV &b, uint32_t w) {
   AV r = top(w);
   const uint32_t tz = ctz_ones(a.z) + ctz_ones(b.z);
@@ -243,6 +276,20 @@ MGP_RD AV av_mul(const AV &a, const AV &b, uint32_t w) {
   if (Z(hi) && (w == 256u || Z(AND(lo, NOT(M(w)))))) {
     r.hi = lo;
     r.lo = bv_mul(a.lo, b.lo);
+    return r;
+  }
+  // the product may wrap: an operand of at most 32 values bounds it per value
+  constexpr uint32_t kSmallRange = 32u;
+  for (int k = 0; k < 2; ++k) {
+    const AV &s = k ? b : a, &o = k ? a : b;
+    const V span = SUBV(s.hi, s.lo);
+    if (!LT(span, bv_small(kSmallRange))) continue;
+    V rl, rh;
+    if (mul_small_range(s.lo, span.w[0] + 1u, o.lo, o.hi, w, &rl, &rh)) {
+      r.lo = rl;
+      r.hi = rh;
+      break;
+    }
   }
   return r;
 }
@@ -700,8 +747,30 @@ struct Dom {
     AV t = top(w);
     t.lo = bv_mask(lo, w);
     t.hi = bv_mask(hi, w);
-    if (LT(t.hi, t.lo)) return true;  // (masking a capped bound: leave it to the other rules)
-    return meet(e.r, t);
+    if (!LT(t.hi, t.lo) && !meet(e.r, t)) return false;  // (a capped bound masked past: other rules)
+    return e.op == MGP_OP_ADD ? addend_bounds(e.a, e.b, e.r, wrapped) && addend_bounds(e.b, e.a, e.r, wrapped)
+                              : true;
+  }
+  // An addend y of r = x + y once the wrap status is known: y = r - x (+ 2^w if wrapped),
+  // so y lies in [r.lo - x.hi, r.hi - x.lo] (+ 2^w).  An overflow test that fails
+  // (SafeMath.add's assert, BECToken.sol:25-29) bounds the addend from below: y >= 2^w - x.hi.
+  MGP_RD bool addend_bounds(int32_t y, int32_t x, int32_t r, bool wrapped) {
+    const uint32_t w = nd[r].width;
+    const AV &X = av[x], &R = av[r];
+    AV t = top(w);
+    if (wrapped) {
+      // r = x + y - 2^w < x: r.lo < x.hi, y >= 2^w - (x.hi - r.lo); y <= 2^w - (x.lo - r.hi)
+      if (!LT(R.lo, X.hi)) return false;
+      t.lo = bv_mask(SUBV(bv_zero(), SUBV(X.hi, R.lo)), w);
+      if (LT(R.hi, X.lo)) t.hi = bv_mask(SUBV(bv_zero(), SUBV(X.lo, R.hi)), w);
+    } else {
+      // r = x + y >= x: y in [r.lo - x.hi, r.hi - x.lo]
+      if (LT(R.hi, X.lo)) return false;
+      t.hi = SUBV(R.hi, X.lo);
+      if (LT(X.hi, R.lo)) t.lo = SUBV(R.lo, X.hi);
+    }
+    if (LT(t.hi, t.lo)) return false;
+    return meet(y, t);
   }
 
   // narrow [lo, hi] of node t by compare atom k (a compare of t with an exact node);
@@ -1512,19 +1581,24 @@ struct Dom {
         return meet(x.a, av_xor(R, B, w)) && meet(x.b, av_xor(R, A, w));
       }
       case MGP_OP_MUL: {
-        // a * b = R (mod 2^w) with b exact and odd: b is invertible mod 2^k, so the k known
-        // low bits of R fix the k low bits of a = R * b^-1 (x * 5 == 1 pins x)
+        // a * b = R (mod 2^w) with b exact, b = d * 2^s, d odd: a * b = ((a * d) mod 2^(w-s))
+        // << s, and d is invertible mod 2^k, so the k known bits of R from bit s up fix the k
+        // low bits of a = (R >> s) * d^-1 (x * 5 == 1 pins x; cnt * 2^255 below 2^255 makes
+        // cnt even)
         for (int k = 0; k < 2; ++k) {
           const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
           const AV B = av[q];
-          if (!is_exact(B) || !(B.lo.w[0] & 1u)) continue;
-          uint32_t kn = ctz_ones(OR(R.z, R.o));
-          if (kn > w) kn = w;
+          if (!is_exact(B) || Z(B.lo)) continue;
+          const uint32_t s = ctz_ones(NOT(B.lo));
+          if (s >= w) continue;
+          const V d = SHR(B.lo, s);
+          uint32_t kn = ctz_ones(SHR(OR(R.z, R.o), s));
+          if (kn > w - s) kn = w - s;
           if (kn == 0) continue;
-          V inv = B.lo;  // Newton: b * b = 1 (mod 8), each step doubles the correct bits
-          for (int it = 0; it < 7; ++it) inv = bv_mul(inv, SUBV(bv_small(2u), bv_mul(B.lo, inv)));
+          V inv = d;  // Newton: d * d = 1 (mod 8), each step doubles the correct bits
+          for (int it = 0; it < 7; ++it) inv = bv_mul(inv, SUBV(bv_small(2u), bv_mul(d, inv)));
           const V lowm = M(kn);
-          const V al = AND(bv_mul(AND(R.o, lowm), inv), lowm);
+          const V al = AND(bv_mul(AND(SHR(R.o, s), lowm), inv), lowm);
           AV t = top(w);
           t.z = OR(t.z, AND(NOT(al), lowm));
           t.o = al;

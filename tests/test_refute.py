@@ -1131,3 +1131,79 @@ def test_chain_orders_exhaustive_soundness():
         cands[0, :, :, 0] = grid
         assert coracle.first_sat(*pack_states([(nl, cl)]), cands)[0] < 0, "refuted a satisfiable state"
     assert refuted > 30, refuted
+
+
+def _random_transfer_dag(rng, w):
+    """BECToken's batchTransfer shape (BECToken.sol:254-268, SafeMath.sol): cnt in a small
+    range, amount = cnt * value (may wrap), bal >= amount, a receiver balance x and
+    sum = x + value with its SafeMath.add overflow test taken either way (or as
+    BVAddNoOverflow), x sometimes bal - amount (the sender paying itself)."""
+    nl = [[S.VAR, w, -1, -1, -1, v, 0] for v in range(4)]          # cnt, value, bal, x0
+    cl = [int(rng.integers(1, 7)), 0, int(rng.integers(1, 1 << (w - 1))), int(rng.integers(0, 1 << w))]
+    nl += [[S.CONST, w, -1, -1, -1, c, 0] for c in range(4)]       # 4: cnt bound, 5: 0, 6: bal bound, 7: any
+    roots = [len(nl)]
+    nl.append([S.UGT, 1, 0, 5, -1, 0, 0])                           # cnt > 0
+    roots.append(len(nl))
+    nl.append([S.ULE if rng.random() < 0.5 else S.ULT, 1, 0, 4, -1, 0, 0])
+    nl.append([S.MUL, w, 0, 1, -1, 0, 0] if rng.random() < 0.5 else [S.MUL, w, 1, 0, -1, 0, 0])
+    amount = len(nl) - 1
+    roots.append(len(nl))
+    nl.append([S.UGE, 1, 2, amount, -1, 0, 0] if rng.random() < 0.5 else [S.ULE, 1, amount, 2, -1, 0, 0])
+    if rng.random() < 0.6:
+        roots.append(len(nl))
+        nl.append([S.ULT, 1, 2, 6, -1, 0, 0])                       # the sender's balance is bounded
+    if rng.random() < 0.4:                                          # the receiver is the sender
+        nl.append([S.SUB, w, 2, amount, -1, 0, 0])
+        x = len(nl) - 1
+    else:
+        x = 3
+        if rng.random() < 0.5:
+            roots.append(len(nl))
+            nl.append([S.ULT, 1, 3, 7, -1, 0, 0])
+    nl.append([S.ADD, w, x, 1, -1, 0, 0] if rng.random() < 0.5 else [S.ADD, w, 1, x, -1, 0, 0])
+    s = len(nl) - 1
+    k = rng.random()
+    if k < 0.4:
+        nl.append([S.UGE, 1, s, x, -1, 0, 0])                       # SafeMath.add: assert(c >= a)
+        nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])           # ... failing
+    elif k < 0.6:
+        nl.append([S.UGE, 1, s, x, -1, 0, 0])                       # ... holding
+    elif k < 0.8:
+        nl.append([S.UADD_NOOVF, 1, x, 1, -1, 0, 0])
+        nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+    else:
+        nl.append([S.ULT, 1, s, 7, -1, 0, 0])                       # a bound on the new balance
+    roots.append(len(nl) - 1)
+    if rng.random() < 0.3:
+        roots.append(len(nl))
+        nl.append([S.UGT, 1, 1, 7, -1, 0, 0])                       # value bounded below
+    r = roots[0]
+    for b in roots[1:]:
+        nl.append([S.BAND, 1, r, b, -1, 0, 0])
+        r = len(nl) - 1
+    return nl, cl
+
+
+@pytest.mark.parametrize("w", [4, 5])
+def test_exhaustive_soundness_transfer_shapes(w):
+    """Addend bounds once an addition's wrap status is known (a failing SafeMath.add assert
+    bounds the addend from below) and products with a small-range operand (cnt * value per
+    value of cnt): every refuted state has no model over ALL 2^(4w) assignments (C oracle),
+    and the rules refute states in numbers (BECToken's transaction-2 overflow queries)."""
+    rng = np.random.default_rng(0x7A5F + w)
+    n = {4: 300, 5: 120}[w]
+    states = [_random_transfer_dag(rng, w) for _ in range(n)]
+    verdict = _refute(states)
+    g = np.array(np.meshgrid(*[np.arange(1 << w)] * 4, indexing="ij")).reshape(4, -1).T
+    cands = np.zeros((1, g.shape[0], 4, 8), np.uint32)
+    cands[0, :, :, 0] = g
+    refuted = unsat = 0
+    for (nl, cl), r in zip(states, verdict):
+        assert r in (0, 1)
+        nodes, noff, consts, coff = pack_states([(nl, cl)])
+        has_model = coracle.first_sat(nodes, noff, consts, coff, cands)[0] >= 0
+        unsat += not has_model
+        if r == 1:
+            refuted += 1
+            assert not has_model, "refuted a satisfiable state"
+    assert refuted >= 0.8 * unsat, (refuted, unsat)  # 102 / 102 and 32 / 34 (72 and 18 before the rules)

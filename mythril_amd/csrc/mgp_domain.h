@@ -1589,6 +1589,10 @@ struct Dom {
           const int32_t p = k ? x.b : x.a, q = k ? x.a : x.b;
           const AV B = av[q];
           if (!is_exact(B) || Z(B.lo)) continue;
+          if (EQV(B.lo, ONE())) {  // a * 1 = a (a loop count narrowed to one transfer)
+            if (!meet(p, R)) return false;
+            continue;
+          }
           const uint32_t s = ctz_ones(NOT(B.lo));
           if (s >= w) continue;
           const V d = SHR(B.lo, s);

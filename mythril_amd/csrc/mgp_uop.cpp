@@ -710,7 +710,21 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
         };
         uint32_t a0, b0, z0;
         step_ops(pc, &a0, &b0, &z0);
-        const Run ra = collect(a0, nullptr), rb = a0 == b0 ? Run() : collect(b0, nullptr);
+        // an operand that the next MGP_U_TSEL_MIN - 1 steps all compare (raw operand
+        // fields, no kind lookups): most steps start no run, and this rejects them cheaply
+        auto shared = [&](uint32_t q) {
+          uint32_t p = pc;
+          for (uint32_t k = 1; k < MGP_U_TSEL_MIN; ++k) {
+            p = next_step(p);
+            if (p == 0xFFFFFFFFu) return false;
+            uint32_t x, y, z;
+            step_ops(p, &x, &y, &z);
+            if (x != q && y != q) return false;
+          }
+          return true;
+        };
+        const bool sa = shared(a0), sb = a0 != b0 && shared(b0);
+        const Run ra = sa ? collect(a0, nullptr) : Run(), rb = sb ? collect(b0, nullptr) : Run();
         const bool use_a = ra.n >= rb.n;
         const uint32_t qraw = use_a ? a0 : b0;
         const Run &run = use_a ? ra : rb;

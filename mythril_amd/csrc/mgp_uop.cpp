@@ -527,6 +527,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   const uint32_t *ins = v1 + MGP_HDR_WORDS;
   if (v1_ok) T.v1pool.assign(ins + (size_t)T.n_ins * MGP_INS_WORDS, ins + (size_t)T.n_ins * MGP_INS_WORDS + (size_t)T.n_c * 8);
   std::vector<uint32_t> uops;
+  uops.reserve((size_t)T.n_ins * MGP_U_UOP_WORDS + 64u);
   // pass 1 only collects the register variables and the mask / sign constants: it emits
   // nothing and looks for no TSEL runs (a run reads the operands its steps would)
   bool pass2 = false;
@@ -906,6 +907,8 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   }
   // pages of 64 uops: the last uop of every full page is PAGE (load the next page)
   const uint32_t n_real = (uint32_t)(uops.size() / MGP_U_UOP_WORDS);
+  out.reserve(out.size() + ((size_t)n_real + n_real / (MGP_U_PAGE_UOPS - 1) + 2u) * MGP_U_UOP_WORDS + T.ms.size() +
+              T.v1pool.size() + T.tables.size());
   uint32_t n_uops = 0;
   for (uint32_t i = 0; i < n_real; ++i) {
     if (n_uops % MGP_U_PAGE_UOPS == MGP_U_PAGE_UOPS - 1) {

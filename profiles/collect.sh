@@ -11,7 +11,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
-ARGS="--states ${PROF_STATES:-1048576} --steps 3 --warmup 1 --keccak 67108864 --keccak-chunk 67108864 --no-cpu --refute-sample 0 --frontend 0"
+ARGS="--states ${PROF_STATES:-1048576} --steps 3 --warmup 1 --keccak 67108864 --keccak-chunk 67108864 --no-cpu --refute-sample 0 --frontend 0 --suite 0 --suite-open-sweep 0 --div-split 0 --guided-sample 0"
 echo "[collect] kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
     python3 bench.py $ARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"

@@ -134,6 +134,7 @@ struct SumForm {
 struct UFApp {
   Pieces arg, val, fresh;  // argument, value, the application's own fresh variable(s)
   std::vector<SumForm> form;  // of arg, piece by piece (f applications only)
+  Ref raw;  // one-piece value: its fresh variable unmasked (EQSEL masks what it selects)
 };
 
 // MGP_LOWER_WHY=1: name the source line of every "unsupported" verdict (diagnostics)
@@ -1114,6 +1115,15 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
         std::vector<SumForm> form = forms_of(arg);
         const Pieces fresh = var_pieces(nd.p1, w);
         Pieces v = fresh;
+        // a one-piece value's fresh variable read as it is: an EQSEL step masks the value it
+        // selects to its width, so a narrow fresh value (a calldata byte) needs no masked
+        // copy held in a slot for every later chain that selects it
+        Ref raw;
+        if (w <= MGP_MAX_WIDTH) {
+          raw.k = R_VAR;
+          raw.idx = nd.p1;
+        }
+        Ref vraw = raw;  // v as an unmasked variable while v is one application's fresh value
         std::vector<UFApp> &fl = fapps[nd.p0];
         for (auto it = fl.rbegin(); it != fl.rend(); ++it) {
           if (wid_of(it->arg) != wid[nd.a] || wid_of(it->val) != w) return unsupported();
@@ -1122,12 +1132,21 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           if (ke == -1 && arg.size() == 1 && it->arg.size() == 1 && v.size() == 1 && it->fresh.size() == 1) {
             // the one-piece case of the line below as one EQSEL step (no Bool, one
             // instruction instead of EQ + ITE)
-            v[0].r = S.add(MGP_OP_EQSEL, (uint16_t)v[0].w, false, arg[0].r, it->arg[0].r, it->fresh[0].r, 0, v[0].r);
+            const Ref z = it->raw.k == R_VAR ? it->raw : it->fresh[0].r;
+            const Ref d = vraw.k == R_VAR ? vraw : v[0].r;
+            v[0].r = S.add(MGP_OP_EQSEL, (uint16_t)v[0].w, false, arg[0].r, it->arg[0].r, z, 0, d);
+            vraw = Ref();
             continue;
           }
-          v = (ke == 1) ? it->fresh : ite_pieces(eq_pieces(arg, it->arg), it->fresh, v);
+          if (ke == 1) {
+            v = it->fresh;
+            vraw = it->raw;
+          } else {
+            v = ite_pieces(eq_pieces(arg, it->arg), it->fresh, v);
+            vraw = Ref();
+          }
         }
-        fl.push_back(UFApp{arg, v, fresh, std::move(form)});
+        fl.push_back(UFApp{arg, v, fresh, std::move(form), raw});
         set_val(i, v);
         break;
       }
@@ -1152,7 +1171,7 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           if (ke == 0) continue;
           v = (ke == 1) ? it->val : ite_pieces(eq_pieces(arg, it->arg), it->val, v);
         }
-        il.push_back(UFApp{arg, v, var_pieces(nd.p1, w), {}});
+        il.push_back(UFApp{arg, v, var_pieces(nd.p1, w), {}, Ref()});
         set_val(i, v);
         break;
       }

@@ -700,7 +700,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
               else if (k.kind == KRVAR) { c = 2; kv = 0x80000000u | (k.param << 16); }
             }
             const Opnd z = T.bv(zo);
-            if (!c || (r.cls && c != r.cls) || z.kind != KVAR) break;
+            if (!c || (r.cls && c != r.cls) || z.kind != KVAR || ((J[0] >> 8) & 0xFFu) != ((I[0] >> 8) & 0xFFu)) break;
             r.cls = c;
             ++r.n;
             if (ent) ent->emplace_back(kv, z.param);
@@ -744,6 +744,10 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
           const uint32_t *J = ins + (size_t)end * MGP_INS_WORDS;
           uint32_t flags = 0, w2 = 0;
           int32_t vst_row = -1;
+          if (narrow && op == MGP_OP_EQSEL) {  // the selected variables are read unmasked (v1 EQSEL; pass 1 found its mask)
+            flags |= MGP_UF_MASK;
+            w2 |= T.mask_off(width) << 16;
+          }
           if ((J[0] >> 24) & MGP_INS_STORE) store_to(((J[0] >> 16) & 0xFFu) | ((J[3] & 0xFFu) << 8), flags, w2, vst_row);
           emit(w0_of(fetch_id(q.kind, KNONE, true), cls == 1 ? MGP_U_TSEL : MGP_U_TSELS), q.param, w2 | flags,
                n_ent | ((n_pool * 4u + toff / 2u) << 16));
@@ -834,6 +838,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
             if (a.kind == KACC || b.kind == KACC || z.kind == KACC) { T.bad = true; break; }
             opid = MGP_U_EQSEL_FIRST + (uint32_t)(z.kind - KSLOT);
             w3 |= z.param << 16;
+            need_mask = narrow && op == MGP_OP_EQSEL;  // a v1 EQSEL may select an unmasked variable
             break;
           }
           a = T.bv(ob); b = T.bv(oc); opid = MGP_U_ITE;

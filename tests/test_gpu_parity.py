@@ -668,6 +668,91 @@ def test_select_chain_fusions_vs_oracle(mgp_ctx):
     assert (ref > 0).sum() > 50 and (ref < 0).sum() < len(states)
 
 
+def _uf_byte_table_states(rng, n):
+    """Calldata-shaped UF applications (calldata.py:219-232, lowered as v1 EQSEL chains):
+    8-bit reads f(i) at constant indices, symbolic reads f(q), f(q + c), f(y) selecting
+    among them (TSEL over the constant keys, TSELS over the symbolic ones), and a second
+    function with 256-bit values; the fresh variables are read unmasked by the selects, so
+    candidates put garbage above bit 8 (the selects must mask what they pick).  Root: an Or
+    of equalities between reads, their concatenation and constants."""
+    out = []
+    for _ in range(n):
+        nl = [[S.VAR, 256, -1, -1, -1, 0, 0], [S.VAR, 256, -1, -1, -1, 1, 0]]   # q, y
+        cl = []
+
+        def add(row):
+            nl.append(row)
+            return len(nl) - 1
+
+        def const(v):
+            cl.append(v)
+            return add([S.CONST, 256, -1, -1, -1, len(cl) - 1, 0])
+
+        fresh = [10]
+
+        def app(arg, w=8, fid=5):
+            fresh[0] += 1
+            return add([S.UFAPP, w, arg, -1, -1, fid, fresh[0]])
+
+        k = int(rng.integers(4, 24))
+        const_reads = [app(const(i)) for i in range(k)]
+        sym = [app(0)]
+        for c in rng.choice(np.arange(1, 6), size=int(rng.integers(1, 4)), replace=False):
+            sym.append(app(add([S.ADD, 256, 0, const(int(c)), -1, 0, 0])))
+        sym.append(app(1))
+        wide = [app(const(int(rng.integers(0, 8))), 256, 6) for _ in range(3)] + [app(0, 256, 6)]
+        eqs = []
+        for _ in range(int(rng.integers(2, 5))):
+            r = rng.random()
+            a = int(rng.choice(sym))
+            if r < 0.4:
+                eqs.append(add([S.EQ, 1, a, int(rng.choice(const_reads)), -1, 0, 0]))
+            elif r < 0.6:
+                cc = add([S.CONST, 8, -1, -1, -1, len(cl), 0])
+                cl.append(int(rng.integers(0, 4)))
+                eqs.append(add([S.EQ, 1, a, cc, -1, 0, 0]))
+            elif r < 0.8:
+                cat = add([S.CONCAT, 16, a, int(rng.choice(sym)), -1, 0, 0])
+                cc = add([S.CONST, 16, -1, -1, -1, len(cl), 0])
+                cl.append(int(rng.integers(0, 4)) * 257)
+                eqs.append(add([S.EQ, 1, cat, cc, -1, 0, 0]))
+            else:
+                eqs.append(add([S.EQ, 1, wide[-1], int(rng.choice(wide[:-1])), -1, 0, 0]))
+        root = eqs[0]
+        for e in eqs[1:]:
+            root = add([S.BOR if rng.random() < 0.6 else S.BAND, 1, root, e, -1, 0, 0])
+        out.append((nl, cl))
+    return out
+
+
+def _uf_byte_table_cands(rng, states, n_cand):
+    """q, y near the constant indices; fresh values 0..3, half of them with garbage above
+    bit 8 (only the 8-bit reads ignore it; the 256-bit function's values use it)."""
+    n_vars = max(max(r[6] for r in nl if r[0] == S.UFAPP) + 1 for nl, _ in states)
+    cands = np.zeros((len(states), n_cand, n_vars, 8), np.uint32)
+    cands[:, :, 2:, 0] = rng.integers(0, 4, size=(len(states), n_cand, n_vars - 2))
+    junk = rng.random((len(states), n_cand, n_vars - 2)) < 0.5
+    cands[:, :, 2:, 0] |= np.where(junk, rng.integers(1, 1 << 20, size=junk.shape) << 8, 0).astype(np.uint32)
+    cands[:, :, :2, 0] = rng.integers(0, 28, size=(len(states), n_cand, 2))
+    return cands
+
+
+def test_uf_byte_tables_vs_oracle(mgp_ctx):
+    """UF chains as v1 EQSEL steps (narrow values selected from unmasked fresh variables,
+    masked by the step) through both engines: first-SAT equal to the C oracle's."""
+    rng = np.random.default_rng(919)
+    states = _uf_byte_table_states(rng, 300)
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    cands = _uf_byte_table_cands(rng, states, 256)
+    first, _ = mgp_ctx.eval_batch(words, po, cands)
+    ref = coracle.first_sat(nodes, noff, consts, coff, cands)
+    bad = np.nonzero(first != ref)[0]
+    assert bad.size == 0, f"{bad.size} states differ, e.g. {bad[:5]} gpu={first[bad[:5]]} ref={ref[bad[:5]]}"
+    assert (ref > 0).sum() > 30 and (ref < 0).sum() > 10
+
+
 def _mul_after_shift_states(rng, n):
     """A per-lane shift (its handler leaves v6 = 32 - amount, or all-ones for amounts >=
     256) and then MULs whose products' high limbs decide a compare.  The r3n defect: the

@@ -689,3 +689,27 @@ def test_contract_select_tables_uop_reference():
         ops = [names[int(words[u0 + 4 + 4 * k]) >> 16] for k in range(int(words[u0]))]
         assert ops.count("TSEL") > 10 and ops.count("TSELS") > 10, s
     B.close()
+
+
+def test_uf_byte_tables_both_references_match_oracle():
+    """UF chains lowered as v1 EQSEL steps whose selected fresh values are read unmasked
+    (EQSEL masks them): the bytecode and uop reference interpreters agree with the oracle on
+    candidates with garbage above the 8-bit values; TSEL and TSELS runs fire."""
+    from .test_gpu_parity import _uf_byte_table_cands, _uf_byte_table_states
+
+    rng = np.random.default_rng(920)
+    states = _uf_byte_table_states(rng, 40)
+    cands = _uf_byte_table_cands(rng, states, 12)
+    rows = [[[S.limbs_to_int(cands[s, k, v]) for v in range(cands.shape[2])] for k in range(cands.shape[1])]
+            for s in range(len(states))]
+    words, po, status = _check_states(states, rows)
+    assert (status == 0).all()
+    names = UR._names()
+    seen = set()
+    n_eqsel = 0
+    for s in range(len(states)):
+        o = int(po[s])
+        n_eqsel += sum(int(words[o + 4 + 4 * k]) & 0xFF == 81 for k in range(int(words[o])))
+        u0 = UR.uop_offset(words, o)
+        seen |= {names[int(words[u0 + 4 + 4 * k]) >> 16] for k in range(int(words[u0]))}
+    assert n_eqsel > 100 and {"TSEL", "TSELS"} <= seen, (n_eqsel, sorted(seen)[:20])

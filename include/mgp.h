@@ -275,6 +275,16 @@ int mgp_decision_rows_seeded(const mgp_node *nodes, const uint64_t *node_offsets
                              uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t n_decide,
                              const uint8_t *rows_per_state, const uint32_t *seed_vals, const uint8_t *seed_mask,
                              uint32_t seed_rows, uint32_t *out_rows, uint8_t *out_mask, int8_t *out);
+/* mgp_decision_rows_seeded for rows row0 .. row0 + n_decide - 1: output row k is decision
+ * row row0 + k (its schedule, case splits, draw stream and seed_rows bit are those of row
+ * row0 + k); rows_per_state counts rows from row0.  row0 = 0 is mgp_decision_rows_seeded.
+ * Prefilter's first round asks large states for row 1 alone (solver.py ROWS_FIRST_FROM). */
+int mgp_decision_rows_from(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                           const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                           uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t row0,
+                           uint32_t n_decide, const uint8_t *rows_per_state, const uint32_t *seed_vals,
+                           const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows, uint8_t *out_mask,
+                           int8_t *out);
 /* Candidate assignments for the first witness round (host, OpenMP over states):
  * per state, row 0 is left for the parent witness when has_parent[s], then the
  * first hint of every variable, that row with the x == y aliases applied, then

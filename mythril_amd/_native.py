@@ -102,6 +102,8 @@ def _bind(lib):
         "mgp_decision_rows": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P, _P]),
         "mgp_decision_rows_seeded": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _P, _P, _P,
                                                     _U32, _P, _P, _P]),
+        "mgp_decision_rows_from": (ctypes.c_int, [_P, _P, _U32, _P, _P, _U32, _U32, _U64, _P, _U32, _U32, _P, _P,
+                                                  _P, _U32, _P, _P, _P]),
         "mgp_refute_domains": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _U32, _P, _P]),
         "mgp_build_states": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64, _P, _P, _U32, _P, _U64,
                                             ctypes.POINTER(_P)]),
@@ -172,6 +174,7 @@ EXPORTED_SYMBOLS = (
     "mgp_make_candidates",
     "mgp_decision_rows",
     "mgp_decision_rows_seeded",
+    "mgp_decision_rows_from",
     "mgp_refute_domains",
     "mgp_build_states",
     "mgp_fe_get",
@@ -310,11 +313,12 @@ def make_candidates(n_cand: int, n_vars: int, seed: int, var_off, var_width, hin
 
 def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed: int, n_decide: int,
                   rows_per_state: Optional[np.ndarray] = None, state_keys: Optional[np.ndarray] = None,
-                  max_passes: int = 0, seeds=None, seed_rows: int = 0):
+                  max_passes: int = 0, seeds=None, seed_rows: int = 0, row0: int = 0):
     """mgp_decision_rows -> (rows u32 [n, n_decide, n_vars, 8], mask u8 [n, n_decide, n_vars], status i8[n]);
     seeds = (vals u32
     [n, n_vars, 8], mask u8 [n, n_vars]): parent values the rows in `seed_rows` (a bit mask)
-    fix first (mgp_decision_rows_seeded)."""
+    fix first (mgp_decision_rows_seeded); row0 > 0: output row k is decision row row0 + k
+    (mgp_decision_rows_from)."""
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
     node_offsets = np.ascontiguousarray(node_offsets, dtype=np.uint64)
     consts = np.ascontiguousarray(consts, dtype=np.uint32).reshape(-1)
@@ -336,13 +340,18 @@ def decision_rows(nodes, node_offsets, consts, const_offsets, n_vars: int, seed:
     args = (_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets), max_passes, n_vars,
             seed & (2 ** 64 - 1), _ptr(keys), n_decide, _ptr(rps), _ptr(rows) if rows.size else None,
             _ptr(mask) if mask.size else None, _ptr(out))
-    if seeds is not None:
-        sv = np.ascontiguousarray(seeds[0], dtype=np.uint32)
-        sm = np.ascontiguousarray(seeds[1], dtype=np.uint8)
-        if sv.shape != (n_states, n_vars, 8) or sm.shape != (n_states, n_vars):
-            raise ValueError("seeds must be (vals u32 [n_states, n_vars, 8], mask u8 [n_states, n_vars])")
-        sargs = args[:11] + (_ptr(sv), _ptr(sm), seed_rows) + args[11:]
-        _check(lib().mgp_decision_rows_seeded(*sargs))
+    if seeds is not None or row0:
+        sv = sm = None
+        if seeds is not None:
+            sv = np.ascontiguousarray(seeds[0], dtype=np.uint32)
+            sm = np.ascontiguousarray(seeds[1], dtype=np.uint8)
+            if sv.shape != (n_states, n_vars, 8) or sm.shape != (n_states, n_vars):
+                raise ValueError("seeds must be (vals u32 [n_states, n_vars, 8], mask u8 [n_states, n_vars])")
+        sa = (None if sv is None else _ptr(sv), None if sm is None else _ptr(sm), seed_rows)
+        if row0:
+            _check(lib().mgp_decision_rows_from(*(args[:9] + (int(row0),) + args[9:11] + sa + args[11:])))
+        else:
+            _check(lib().mgp_decision_rows_seeded(*(args[:11] + sa + args[11:])))
         return rows, mask, out[:n_states]
     _check(lib().mgp_decision_rows(*args))
     return rows, mask, out[:n_states]

@@ -1388,6 +1388,18 @@ extern "C" int mgp_decision_rows_seeded(const mgp_node *nodes, const uint64_t *n
                                         const uint8_t *rows_per_state, const uint32_t *seed_vals,
                                         const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
                                         uint8_t *out_mask, int8_t *out) {
+  return mgp_decision_rows_from(nodes, node_offsets, n_states, consts, const_offsets, max_passes, n_vars, seed,
+                                state_keys, 0u, n_decide, rows_per_state, seed_vals, seed_mask, seed_rows, out_rows,
+                                out_mask, out);
+}
+
+extern "C" int mgp_decision_rows_from(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t n_states,
+                                      const uint32_t *consts, const uint64_t *const_offsets, uint32_t max_passes,
+                                      uint32_t n_vars, uint64_t seed, const uint64_t *state_keys, uint32_t row0,
+                                      uint32_t n_decide, const uint8_t *rows_per_state, const uint32_t *seed_vals,
+                                      const uint8_t *seed_mask, uint32_t seed_rows, uint32_t *out_rows,
+                                      uint8_t *out_mask, int8_t *out) {
+  if (row0 > 255u) return MGP_E_ARG;
   if ((seed_vals == nullptr) != (seed_mask == nullptr)) return MGP_E_ARG;
   if (!node_offsets || !out || (n_states && (!nodes || !const_offsets)) ||
       (n_states && n_decide && (!out_rows || !out_mask)))
@@ -1425,7 +1437,8 @@ extern "C" int mgp_decision_rows_seeded(const mgp_node *nodes, const uint64_t *n
         out_mask[r0 + sl] = 1;
       };
       const uint64_t sb = (uint64_t)st * n_vars;
-      decision_row(P, row, 2u * row, seed, tag, put, seed_vals ? seed_vals + sb * 8u : nullptr,
+      const uint32_t ar = row0 + row;  // the absolute decision row
+      decision_row(P, ar, 2u * ar, seed, tag, put, seed_vals ? seed_vals + sb * 8u : nullptr,
                    seed_mask ? seed_mask + sb : nullptr, seed_rows);
     }
   }

@@ -391,10 +391,12 @@ class Prefilter:
     # programs.  A rule on the state alone (tests/fe_emulate.py restates it)
     ROWS_FIRST_NODES = 600
     ROWS_FIRST_SEED = 0x3C6EF372
-    # rows per large state in the first round: rows 0 and 1 (parent-seeded, the second the
-    # greedy select-branch row) decide all 344 large corpus states, as four do, for 60 % of
-    # the time; the retry round still gets DECIDE_ROWS
-    ROWS_FIRST_ROWS = 2
+    # rows per large state in the first round, from decision row ROWS_FIRST_FROM: row 1 (the
+    # greedy select-branch row, parent-seeded) decides all 344 large corpus states alone, as
+    # rows 0-1 and rows 0-3 do (row 0 alone: 148 stay open, tests/fe_emulate.py), at half the
+    # host time of two rows; the retry round still gets DECIDE_ROWS from row 0
+    ROWS_FIRST_FROM = 1
+    ROWS_FIRST_ROWS = 1
     # pinned host staging of mgp_check_batch reserved per context (programs + tables of one
     # batch go up through it: WalletLibrary's lowered programs are ~0.45 MB each)
     HOST_STAGING = 256 << 20
@@ -646,11 +648,11 @@ class Prefilter:
             seeds = None
         return list(GB.packed(decide=True)), gv, self.rows_per_state(GB), GB.state_key, seeds
 
-    def _decision_rows(self, args, seed2, n_rows=None):
+    def _decision_rows(self, args, seed2, n_rows=None, row0=0):
         packed, gv, rps, keys, seeds = args
         n_rows = self.decide_rows if n_rows is None else n_rows
         rows, mask, _ = self._N.decision_rows(*packed, gv, seed2, n_rows, np.minimum(rps, n_rows).astype(np.uint8),
-                                              state_keys=keys, seeds=seeds, seed_rows=self.seed_rows)
+                                              state_keys=keys, seeds=seeds, seed_rows=self.seed_rows, row0=row0)
         return rows, mask
 
     def _first_round_rows(self, B, parents, ctx):
@@ -666,10 +668,12 @@ class Prefilter:
         seed1 = (self.seed + self.ROWS_FIRST_SEED) & (2 ** 64 - 1)
         out: dict = {}
 
+        row0 = min(self.ROWS_FIRST_FROM, max(0, self.decide_rows - 1))
+
         def work():
             try:
                 out["rows"] = self._decision_rows((packed, gv, rps, keys, seeds), seed1,
-                                                  n_rows=min(self.decide_rows, self.ROWS_FIRST_ROWS))
+                                                  n_rows=min(self.decide_rows - row0, self.ROWS_FIRST_ROWS), row0=row0)
             except BaseException as e:
                 out["error"] = e
 

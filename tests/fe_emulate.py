@@ -45,7 +45,8 @@ def first_round_rows(B, seed, parents=None, decide_rows: int = 4, seed_rows: int
         return None
     fake = type("P", (), {"decide_rows": decide_rows, "decide_max_units": SV.Prefilter.DECIDE_MAX_UNITS,
                           "DECIDE_MIN_ROWS": SV.Prefilter.DECIDE_MIN_ROWS})()
-    n_rows = min(decide_rows, SV.Prefilter.ROWS_FIRST_ROWS)
+    row0 = min(SV.Prefilter.ROWS_FIRST_FROM, max(0, decide_rows - 1))
+    n_rows = min(decide_rows - row0, SV.Prefilter.ROWS_FIRST_ROWS)
     rps = np.where(big, np.minimum(SV.Prefilter.rows_per_state(fake, B), n_rows), 0).astype(np.uint8)
     gv = max(1, B.n_vars())
     seeds = None
@@ -54,7 +55,8 @@ def first_round_rows(B, seed, parents=None, decide_rows: int = 4, seed_rows: int
         if seeds[0].shape[1] != gv:
             seeds = None
     rows, mask, _ = N.decision_rows(*B.packed(decide=True), gv, (seed + SV.Prefilter.ROWS_FIRST_SEED) & (2 ** 64 - 1),
-                                    n_rows, rps, state_keys=B.state_key, seeds=seeds, seed_rows=seed_rows)
+                                    n_rows, rps, state_keys=B.state_key, seeds=seeds, seed_rows=seed_rows,
+                                    row0=row0)
     return rows, mask
 
 

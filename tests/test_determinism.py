@@ -128,3 +128,26 @@ def test_first_round_rows_are_a_function_of_the_state():
     assert not mask[sub][:, :, gv:].any()
     B.close()
     SB.close()
+
+
+def test_row_range_is_a_slice_of_the_full_rows():
+    """mgp_decision_rows_from (the first round's row 1 of large states): output row k is
+    decision row row0 + k of the full call, unseeded and parent-seeded, per state."""
+    import corpus
+
+    C = corpus.corpus(64)
+    cs = [c[1] for c in C if c[0].startswith("wallet")][:6] + [c[1] for c in C if c[0].startswith("bec")][:6]
+    B = F.Batch(cs)
+    nv = max(1, B.n_vars())
+    pk = B.packed(decide=True)
+    full, fmask, fst = N.decision_rows(*pk, nv, 21, 4, None, state_keys=B.state_key)
+    for row0, n in ((1, 1), (1, 3), (2, 2)):
+        r, m, st = N.decision_rows(*pk, nv, 21, n, None, state_keys=B.state_key, row0=row0)
+        assert np.array_equal(st, fst)
+        assert np.array_equal(r, full[:, row0:row0 + n]) and np.array_equal(m, fmask[:, row0:row0 + n])
+    # seeded: every slot of a parent witness offered (the states' own row 0 values)
+    seeds = (np.ascontiguousarray(full[:, 0]), np.ascontiguousarray(fmask[:, 0]))
+    sf, sm, _ = N.decision_rows(*pk, nv, 21, 3, None, state_keys=B.state_key, seeds=seeds, seed_rows=0x3)
+    s1, m1, _ = N.decision_rows(*pk, nv, 21, 2, None, state_keys=B.state_key, seeds=seeds, seed_rows=0x3, row0=1)
+    assert np.array_equal(s1, sf[:, 1:3]) and np.array_equal(m1, sm[:, 1:3])
+    B.close()

@@ -45,6 +45,7 @@
 #include <vector>
 
 #include "../../include/mgp.h"
+#include "mgp_buf.h"
 
 namespace {
 
@@ -558,14 +559,20 @@ void pin_constants(StateOut &S) {
 
 }  // namespace
 
+// The flat arrays are sized and then written in full by the per-state copy (in parallel):
+// no zero fill first (a 1 024-state batch is tens of MB of nodes, and a serial fill of them
+// cost more than building the states)
+template <typename T>
+using FeVec = std::vector<T, NoInitAlloc<T>>;
 struct mgp_fe_batch {
   uint32_t n_states = 0;
-  std::vector<mgp_node> nodes, gpu_nodes, dec_nodes;
+  FeVec<mgp_node> nodes, gpu_nodes, dec_nodes;
   std::vector<uint64_t> node_off, gpu_node_off, const_off, var_off, hint_off, alias_off;
-  std::vector<uint32_t> consts, var_width, var_full, var_name, var_aux, hints, aliases;
-  std::vector<uint8_t> var_kind, flags;
-  std::vector<uint64_t> var_key;
-  std::vector<int32_t> var_tid;
+  FeVec<uint32_t> consts, var_width, var_full, var_name, var_aux, hints, aliases;
+  FeVec<uint8_t> var_kind;
+  std::vector<uint8_t> flags;
+  FeVec<uint64_t> var_key;
+  FeVec<int32_t> var_tid;
   std::vector<uint64_t> state_key;
 };
 
@@ -694,9 +701,10 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
   bool any_ops = false;
   for (uint32_t s = 0; s < n_states; ++s) any_ops |= !res[s].gpu_ops.empty();
   if (any_ops) {  // the strengthened formula on the original node indices (decision rows)
-    B->dec_nodes = B->nodes;
+    B->dec_nodes.resize(nn);
 #pragma omp parallel for schedule(static)
     for (int64_t s = 0; s < (int64_t)n_states; ++s) {
+      std::copy(res[s].nodes.begin(), res[s].nodes.end(), B->dec_nodes.begin() + B->node_off[s]);
       const auto &ops = res[s].gpu_ops;
       for (size_t k = 0; k < ops.size(); k += 2) {
         mgp_node &nd = B->dec_nodes[B->node_off[s] + ops[k]];

@@ -472,14 +472,23 @@ def main():
         pf = SV.Prefilter(device=local)
         cs = _contract_states(args.frontend)
         pf.check_states(cs[:64])  # warm-up (kernels loaded, host pools touched)
-        SV.unsat_cores().reset()  # cold: no UNSAT core from the warm-up answers the timed run
-        pf._N.program_cache_clear()  # and no lowered program from it either
-        SV.SolverStatistics().reset()
-        tf = time.perf_counter()
-        res = pf.check_states(cs)
-        dtf = time.perf_counter() - tf
-        kinds = [r[0] for r in res]
-        st = SV.SolverStatistics()
+        # three cold calls (no UNSAT core and no lowered program from an earlier call answers
+        # any of them); the median is the reported rate, the first call is kept beside it,
+        # and every call must give the same answers
+        fe_calls = []
+        for rep in range(3):
+            SV.unsat_cores().reset()
+            pf._N.program_cache_clear()
+            SV.SolverStatistics().reset()
+            tf = time.perf_counter()
+            res = pf.check_states(cs)
+            fe_calls.append((time.perf_counter() - tf, [r[0] for r in res], pf.last_profile,
+                             SV.SolverStatistics().refuted, SV.SolverStatistics().core_hits))
+        kinds = fe_calls[0][1]
+        if any(c[1] != kinds for c in fe_calls):
+            raise RuntimeError("front end: cold calls on one batch gave different answers")
+        med_call = sorted(fe_calls, key=lambda c: c[0])[1]
+        dtf = med_call[0]
         import collections
 
         import corpus
@@ -505,12 +514,13 @@ def main():
         if expect["contradicted"]:
             raise RuntimeError(f"front end contradicts the corpus expectations: {expect}")
         frontend = {"states": len(cs), "seconds": dtf, "states_per_s": len(cs) / dtf,
+                    "calls_seconds": [round(c[0], 4) for c in fe_calls], "first_call_seconds": fe_calls[0][0],
                     "sat": kinds.count(SV.sat), "unsat": kinds.count(SV.unsat),
-                    "refuted": st.refuted, "core_hits": st.core_hits,
+                    "refuted": med_call[3], "core_hits": med_call[4],
                     "undecided": kinds.count("undecided"), "candidates": pf.n_cand,
                     "solver_call_reduction": len(cs) / max(1, kinds.count("undecided")), "expectations": expect,
                     "by_contract": {k: dict(v) for k, v in by_shape.items()},
-                    "stages_ms": pf.last_profile, "latency": frontend_latency(pf, SV, cs),
+                    "stages_ms": med_call[2], "latency": frontend_latency(pf, SV, cs),
                     "latency_2_by_contract": {
                         k: frontend_latency(pf, SV, [c for c, lab in zip(cs, labels) if lab.startswith(k)], sizes=(2,))
                         for k in ("suicide", "bectoken", "wallet")},

@@ -163,6 +163,14 @@ class Batch:
         v0, v1 = int(vt.var_off[s]), int(vt.var_off[s + 1])
         return SlotWitness(vt, v0, v1, words[: v1 - v0])
 
+    def witnesses(self, idx: Sequence[int], words: np.ndarray) -> List["SlotWitness"]:
+        """Witnesses of states idx (words [n, n_vars, 8] indexed by state): Batch.witness in
+        bulk, with the slot offsets read in one numpy gather (a 1 024-state answer list)."""
+        vt = self.var_tables()
+        ix = np.asarray(idx, dtype=np.int64)
+        v0s, v1s = vt.var_off[ix].tolist(), vt.var_off[ix + 1].tolist()
+        return [SlotWitness(vt, a, b, words[i, : b - a]) for i, a, b in zip(ix.tolist(), v0s, v1s)]
+
     def close(self) -> None:
         if self._h:
             N.lib().mgp_fe_free(self._h)

@@ -592,11 +592,13 @@ class Prefilter:
         tr = time.perf_counter()
         out: List[Tuple[str, Optional[object]]] = []
         refuted = []
+        first_round = [i for i in range(len(states)) if first[i] >= 0 and i not in witnesses]
+        witnesses.update(zip(first_round, B.witnesses(first_round, wit)))
         for i in range(len(states)):
             if first[i] >= 0:
                 if proven[i] == 1:  # a witness and an UNSAT proof cannot both hold
                     raise RuntimeError(f"mgp_refute refuted state {i} that has a GPU witness (soundness bug)")
-                out.append((sat, witnesses[i] if i in witnesses else B.witness(i, wit[i])))
+                out.append((sat, witnesses[i]))
             elif proven[i] == 1:
                 out.append((unsat, None))
                 refuted.append(i)

@@ -1379,10 +1379,13 @@ def tsel_row_load(e):
 
 @handler("TSELS")
 def h_tsels():
-    """TSEL with keys in LDS slots (entries (slot byte offset, z_i), chain order): q (vC)
-    is compared with all 256 bits of each key; the key of entry e+1 is read into the other
-    of two buffers (T, vB) while entry e is compared.  Overlapping matches resolve as in the
-    chain: one wave's row loads return in issue order, so a lane's last match lands last."""
+    """TSEL with keys in slots (entries (key word, z_i), chain order): q (vC) is compared
+    with all 256 bits of each key; an LDS key of entry e+1 is read into the other of two
+    buffers (T, vB) while entry e is compared, a bank key is read in place, and a
+    candidate-row key (an HBM variable or a spill row, word bit 30) is loaded into the
+    entry's buffer when its turn comes (its word's LDS offset is 0: the early read is of
+    slot 0, unused).  Overlapping matches resolve as in the chain: one wave's row loads
+    return in issue order, so a lane's last match lands last."""
     wait_operands()
     lp, ld = A.fresh("tsels"), A.fresh("tselsd")
     A("s_and_b32 s55, s19, 0xffff",
@@ -1411,6 +1414,18 @@ def h_tsels():
             A("s_waitcnt lgkmcnt(2)")
         else:
             A("s_waitcnt lgkmcnt(0)")
+        lrow = A.fresh("tsrow")
+        A(f"s_bitcmp1_b32 s{24 + 2 * e}, 30", f"s_cbranch_scc0 {lrow}")
+        # candidate-row key: variable w[29:16] (clamped like fetch_one) of this lane's row
+        A(f"s_bfe_u32 s53, s{24 + 2 * e}, {(14 << 16) | 16:#x}",
+          "s_min_u32 s53, s53, s9",
+          "s_mul_i32 s53, s53, s8",
+          "s_add_u32 s52, s6, s53",
+          "s_addc_u32 s53, s7, 0",
+          f"global_load_dwordx4 {vr(buf, 4)}, v2, s[52:53]",
+          f"global_load_dwordx4 {vr(buf + 4, 4)}, v3, s[52:53]",
+          "s_waitcnt vmcnt(0)")
+        A.label(lrow)
         A(f"s_bitcmp1_b32 s{24 + 2 * e}, 31", f"s_cbranch_scc1 {lbank}")
         for i in range(8):
             A(f"v_xor_b32 {v(buf + i)}, {v(buf + i)}, {v(VC + i)}")

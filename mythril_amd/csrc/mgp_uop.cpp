@@ -670,11 +670,11 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
       };
       if (pass2 && is_step(pc) && next_step(pc) != 0xFFFFFFFFu) {
         // a run of select steps comparing one operand q against keys that are all 32-bit
-        // constants (TSEL) or all LDS / bank slots (TSELS), each selecting an HBM variable
+        // constants (TSEL) or all values in LDS / bank / candidate rows (TSELS), each selecting an HBM variable
         // (a calldata / memory byte table): one uop over a table behind the pool
         struct Run {
           uint32_t n = 0;
-          int cls = 0;  // 1: constant keys (TSEL), 2: slot keys, LDS or bank (TSELS)
+          int cls = 0;  // 1: constant keys (TSEL), 2: value keys: LDS, bank or candidate row (TSELS)
           uint32_t end = 0;
         };
         // the steps from pc on that compare qraw with a key of one class and select a
@@ -695,9 +695,11 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
               if (T.small_const(key, &kv)) c = 1;
             } else if ((key >> 14) != MGP_K_ACC) {
               const Opnd k = T.bv(key);
-              // TSELS key word: LDS byte offset, or bit 31 + bank offset 8p in [23:16]
+              // TSELS key word: LDS byte offset, bit 31 + bank offset 8p in [23:16], or
+              // bit 30 + candidate-row variable in [29:16] (an HBM variable or a spill row)
               if (k.kind == KSLOT) { c = 2; kv = k.param; }
               else if (k.kind == KRVAR) { c = 2; kv = 0x80000000u | (k.param << 16); }
+              else if (k.kind == KVAR && k.param < 0x4000u) { c = 2; kv = 0x40000000u | (k.param << 16); }
             }
             const Opnd z = T.bv(zo);
             if (!c || (r.cls && c != r.cls) || z.kind != KVAR || ((J[0] >> 8) & 0xFFu) != ((I[0] >> 8) & 0xFFu)) break;

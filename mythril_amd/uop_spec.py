@@ -135,9 +135,13 @@ EQSEL_OPS = [f"EQSEL_{k}" for k in KINDS[1:]]
 # pool / 8, keys distinct, padded to 8 entries).  vA = z_i where q == k_i (the last i in
 # chain order), else vA unchanged; the handler compares q against 8 keys per scalar load
 # and issues each z_i row load under the lanes that match it.  TSELS: the same with keys in
-# LDS slots (pairs (slot byte offset, z_i), chain order kept: a lane's last match wins, as
-# the row loads of one wave return in issue order) -- a Store chain at symbolic indices read
-# at one index.
+# slots (pairs (key word, z_i), chain order kept: a lane's last match wins, as the row loads
+# of one wave return in issue order) -- a Store chain at symbolic indices read at one index.
+# Key word: an LDS slot's byte offset; bit 31 | 8p << 16: register-bank position p;
+# bit 30 | v << 16: candidate-row variable v (an HBM variable or a spill row, loaded by the
+# handler) -- WalletLibrary's long-lived symbolic offsets are mostly spilled.
+TSELS_KEY_BANK = 1 << 31
+TSELS_KEY_ROW = 1 << 30
 TSEL_MIN = 3     # shorter runs stay EQSEL uops
 
 OPS = BOOL_OPS + MEM_OPS + BV_BIN + BV_UN + SHIFT_I + CONCAT + ["ITE"] + CMP_VARIANTS + EPI_VARIANTS + XR_OPS + \

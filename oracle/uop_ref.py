@@ -225,11 +225,16 @@ def run_uops(words: Sequence[int], off: int, xs: Sequence[int]):
             for i in range(n_ent):
                 if vC == keys[i]:
                     vA = load("var", int(words[t0 + 2 * i + 1]))
-        elif op == "TSELS":             # keys in LDS / bank slots, chain order
+        elif op == "TSELS":             # keys in LDS / bank slots / candidate rows, chain order
             t0 = pool0 + 2 * (w3 >> 16)
             for i in range(w3 & 0xFFFF):
                 kw = int(words[t0 + 2 * i])
-                key = bank[((kw >> 16) & 0xFF) // 8] if kw >> 31 else lds[kw & 0xFFFF]
+                if kw >> 31:
+                    key = bank[((kw >> 16) & 0xFF) // 8]
+                elif kw >> 30 & 1:
+                    key = load("var", (kw >> 16) & 0x3FFF)
+                else:
+                    key = lds[kw & 0xFFFF]
                 if vC == key:
                     vA = load("var", int(words[t0 + 2 * i + 1]))
         elif op in ("ADD", "SUB", "MUL", "AND", "OR", "XOR"):

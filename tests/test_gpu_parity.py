@@ -590,7 +590,8 @@ def _select_chain_states(rng, n):
     one set of keys, each chain comparing its q (a bank variable, a computed slot or a
     constant) against keys that are small constants (repeated, some with high limbs set)
     or computed slots (x + i, shared by the chains, and x & 3, which several lanes match
-    at once), selecting HBM variables, the bank variable 5 or a computed byte.  Root:
+    at once) or HBM variables (TSELS keys read from the candidate row), selecting HBM
+    variables, the bank variable 5 or a computed byte.  Root:
     some chain == T.  The translator's EQSEL, TSEL and TSELS fusions all fire on these
     (tests/test_lowering.py counts them)."""
     out = []
@@ -613,6 +614,8 @@ def _select_chain_states(rng, n):
         byte = add([S.AND, 256, 2, const(0xFF), -1, 0, 0])
         slot_keys = [add([S.ADD, 256, 1, const(i), -1, 0, 0]) for i in range(int(rng.integers(4, 20)))]
         slot_keys += [add([S.AND, 256, 2 + int(rng.integers(3)), const(3), -1, 0, 0]) for _ in range(3)]
+        # keys that are HBM variables (index >= 6: TSELS candidate-row keys, as spilled slots are)
+        var_keys = [add([S.VAR, 256, -1, -1, -1, 7 + m + i, 0]) for i in range(4)]
         masked = add([S.AND, 256, 0, const(0x3F), -1, 0, 0])
         eqs = []
         for _c in range(int(rng.integers(2, 4))):
@@ -622,7 +625,8 @@ def _select_chain_states(rng, n):
             for i in range(int(rng.integers(3, m + 1))):
                 r = rng.random()
                 if qk == 2 or r < 0.3:
-                    key = slot_keys[int(rng.integers(len(slot_keys)))]
+                    key = slot_keys[int(rng.integers(len(slot_keys)))] if rng.random() < 0.7 else \
+                        var_keys[int(rng.integers(len(var_keys)))]
                 elif r < 0.85:
                     key = const(int(rng.integers(0, 48)))
                 else:

@@ -646,17 +646,22 @@ def test_select_chain_fusions_uop_reference_matches_oracle():
     cands = _select_chain_cands(rng, states, 16)
     ref = coracle.first_sat(nodes, noff, consts, coff, cands)
     names = UR._names()
-    seen = {"EQSEL": 0, "TSEL": 0, "TSELS": 0}
+    seen = {"EQSEL": 0, "TSEL": 0, "TSELS": 0, "row keys": 0}
     for s in range(len(states)):
         rows = [[S.limbs_to_int(cands[s, k, v]) for v in range(cands.shape[2])] for k in range(cands.shape[1])]
         assert UR.first_sat_uops(words, int(po[s]), rows) == ref[s], s
         u0 = UR.uop_offset(words, int(po[s]))
+        pool0 = u0 + int(words[u0 + 2]) // 4
         for k in range(int(words[u0])):
-            nm = names[int(words[u0 + 4 + 4 * k]) >> 16]
+            w0, w3 = int(words[u0 + 4 + 4 * k]), int(words[u0 + 7 + 4 * k])
+            nm = names[w0 >> 16]
             if nm.startswith("EQSEL"):
                 seen["EQSEL"] += 1
             elif nm in seen:
                 seen[nm] += 1
+            if nm == "TSELS":  # entries whose key is a candidate-row variable (word bit 30)
+                t0 = pool0 + 2 * (w3 >> 16)
+                seen["row keys"] += sum((int(words[t0 + 2 * i]) >> 30) == 1 for i in range(w3 & 0xFFFF))
     assert all(v > 10 for v in seen.values()), seen
     assert 0 < (ref >= 0).sum() < len(states) or (ref > 0).sum() > 5
 

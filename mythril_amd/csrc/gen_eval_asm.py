@@ -1380,12 +1380,15 @@ def tsel_row_load(e):
 @handler("TSELS")
 def h_tsels():
     """TSEL with keys in slots (entries (key word, z_i), chain order): q (vC) is compared
-    with all 256 bits of each key; an LDS key of entry e+1 is read into the other of two
-    buffers (T, vB) while entry e is compared, a bank key is read in place, and a
-    candidate-row key (an HBM variable or a spill row, word bit 30) is loaded into the
-    entry's buffer when its turn comes (its word's LDS offset is 0: the early read is of
-    slot 0, unused).  Overlapping matches resolve as in the chain: one wave's row loads
-    return in issue order, so a lane's last match lands last."""
+    with all 256 bits of each key.  The key of entry e+1 is fetched into the other of two
+    buffers (T, vB) while entry e is compared: an LDS key by two ds_reads, a candidate-row
+    key (an HBM variable or a spill row, word bit 30) by its two row loads; a bank key is
+    read in place when compared.  The waits follow the kinds of the two entries: an LDS key
+    waits for lgkmcnt(2) when the next key's reads are behind it, else lgkmcnt(0); a
+    candidate-row key waits for vmcnt(2) when the next key's two loads are behind it (the
+    row loads of entry e-1, issued before them, land first: loads return in order), else
+    vmcnt(0).  Overlapping matches resolve as in the chain: one wave's row loads return in
+    issue order, so a lane's last match lands last."""
     wait_operands()
     lp, ld = A.fresh("tsels"), A.fresh("tselsd")
     A("s_and_b32 s55, s19, 0xffff",
@@ -1399,33 +1402,45 @@ def h_tsels():
 
     def issue(e):
         # a bank key's word has no LDS offset in [15:0]: its read is of slot 0, unused
-        A(f"s_and_b32 s53, s{24 + 2 * e}, 0xffff",
+        lrow, ldone = A.fresh("tsirow"), A.fresh("tsidone")
+        A(f"s_bitcmp1_b32 s{24 + 2 * e}, 30", f"s_cbranch_scc1 {lrow}",
+          f"s_and_b32 s53, s{24 + 2 * e}, 0xffff",
           "v_add_u32 v4, s53, v1",
           f"ds_read_b128 {vr(bufs[e % 2], 4)}, v4",
-          f"ds_read_b128 {vr(bufs[e % 2] + 4, 4)}, v4 offset:1024")
-    issue(0)
-    for e in range(8):
-        buf, skip = bufs[e % 2], A.fresh("tsskip")
-        lbank, lcmp = A.fresh("tsbank"), A.fresh("tscmp")
-        if e:
-            A(f"s_cmp_le_u32 s55, {e}", f"s_cbranch_scc1 {ld}")
-        if e < 7:
-            issue(e + 1)
-            A("s_waitcnt lgkmcnt(2)")
-        else:
-            A("s_waitcnt lgkmcnt(0)")
-        lrow = A.fresh("tsrow")
-        A(f"s_bitcmp1_b32 s{24 + 2 * e}, 30", f"s_cbranch_scc0 {lrow}")
+          f"ds_read_b128 {vr(bufs[e % 2] + 4, 4)}, v4 offset:1024",
+          f"s_branch {ldone}")
+        A.label(lrow)
         # candidate-row key: variable w[29:16] (clamped like fetch_one) of this lane's row
         A(f"s_bfe_u32 s53, s{24 + 2 * e}, {(14 << 16) | 16:#x}",
           "s_min_u32 s53, s53, s9",
           "s_mul_i32 s53, s53, s8",
           "s_add_u32 s52, s6, s53",
           "s_addc_u32 s53, s7, 0",
-          f"global_load_dwordx4 {vr(buf, 4)}, v2, s[52:53]",
-          f"global_load_dwordx4 {vr(buf + 4, 4)}, v3, s[52:53]",
-          "s_waitcnt vmcnt(0)")
-        A.label(lrow)
+          f"global_load_dwordx4 {vr(bufs[e % 2], 4)}, v2, s[52:53]",
+          f"global_load_dwordx4 {vr(bufs[e % 2] + 4, 4)}, v3, s[52:53]")
+        A.label(ldone)
+
+    issue(0)
+    for e in range(8):
+        buf, skip = bufs[e % 2], A.fresh("tsskip")
+        lbank, lcmp, lwait = A.fresh("tsbank"), A.fresh("tscmp"), A.fresh("tswait")
+        if e:
+            A(f"s_cmp_le_u32 s55, {e}", f"s_cbranch_scc1 {ld}")
+        if e < 7:
+            lnext = A.fresh("tsnrow")
+            issue(e + 1)
+            A(f"s_bitcmp1_b32 s{24 + 2 * (e + 1)}, 30", f"s_cbranch_scc1 {lnext}",
+              "s_waitcnt lgkmcnt(2)",
+              f"s_bitcmp1_b32 s{24 + 2 * e}, 30", f"s_cbranch_scc0 {lwait}",
+              "s_waitcnt vmcnt(0)",
+              f"s_branch {lwait}")
+            A.label(lnext)
+            A("s_waitcnt lgkmcnt(0)",
+              f"s_bitcmp1_b32 s{24 + 2 * e}, 30", f"s_cbranch_scc0 {lwait}",
+              "s_waitcnt vmcnt(2)")
+            A.label(lwait)
+        else:
+            A("s_waitcnt vmcnt(0) lgkmcnt(0)")
         A(f"s_bitcmp1_b32 s{24 + 2 * e}, 31", f"s_cbranch_scc1 {lbank}")
         for i in range(8):
             A(f"v_xor_b32 {v(buf + i)}, {v(buf + i)}, {v(VC + i)}")

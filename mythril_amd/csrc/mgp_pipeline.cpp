@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <omp.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -206,6 +208,15 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
                  const uint64_t *coff, U32Buf &words, std::vector<uint64_t> &offs,
                  std::vector<uint8_t> &status) {
   ProgCache &C = prog_cache();
+  // MGP_FE_TIMING=1: the stages of this call on stderr (profiling aid)
+  static const bool timing = getenv("MGP_FE_TIMING") != nullptr;
+  double tt = omp_get_wtime();
+  auto stage = [&](const char *what) {
+    if (!timing) return;
+    const double now = omp_get_wtime();
+    fprintf(stderr, "[lower_cached] %u states: %s %.3f ms\n", n_states, what, 1e3 * (now - tt));
+    tt = now;
+  };
   std::vector<std::vector<uint8_t>> keys(n_states);
   std::vector<uint64_t> hs(n_states);
 #pragma omp parallel for schedule(dynamic, 8)
@@ -233,6 +244,7 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
       }
     }
   }
+  stage("keys + lookup");
   std::vector<mgp_node> mn;
   std::vector<uint32_t> mc;
   std::vector<uint64_t> mno(1, 0), mco(1, 0);
@@ -247,8 +259,10 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
   std::vector<uint8_t> mst;
   if (!miss.empty()) {
     if (mc.empty()) mc.assign(8, 0u);
+    stage("gather misses");
     const int rc = mgp_lower_vec(mn.data(), mno.data(), (uint32_t)miss.size(), mc.data(), mco.data(), 0, mw, mo, mst);
     if (rc != MGP_OK) return rc;
+    stage("lower");
   }
   offs.assign((size_t)n_states + 1, 0u);
   status.assign(n_states, 0u);
@@ -273,6 +287,7 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
       status[s] = hit_status[s];
     }
   }
+  stage("copy out + cache entries");
   if (!miss.empty()) {
     // insert the new programs, evicting the oldest past the byte budget
     std::lock_guard<std::mutex> lk(C.mu);
@@ -302,6 +317,7 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
       }
     }
   }
+  stage("insert");
   return MGP_OK;
 }
 

@@ -79,7 +79,8 @@ inline uint32_t limb_mask(uint32_t w, int l) {
 }
 
 struct Lowered {
-  std::vector<uint32_t> words;
+  std::vector<uint32_t> words;  // the v1 program
+  std::vector<uint32_t> uops;   // the gfx950 interpreter's translation, stored right behind it
   uint8_t status = MGP_ST_OK;
 };
 
@@ -120,12 +121,16 @@ struct LowerState {
 // threads: 25.3 -> 21.5 ms, page faults 28 -> 16 per state; one thread: 301 -> 290 ms).  A
 // list past 8 MB is not kept.
 thread_local std::vector<VIns> g_ins_pool;
-inline void ins_recycle(std::vector<VIns> &v) {
-  if (v.capacity() > g_ins_pool.capacity() && v.capacity() * sizeof(VIns) <= (8u << 20)) {
+// the same for the v1 program and the uop program of a state (recycled once copied out)
+thread_local std::vector<uint32_t> g_words_pool, g_uops_pool;
+template <typename T>
+inline void recycle(std::vector<T> &v, std::vector<T> &pool) {
+  if (v.capacity() > pool.capacity() && v.capacity() * sizeof(T) <= (8u << 20)) {
     v.clear();
-    g_ins_pool.swap(v);
+    pool.swap(v);
   }
 }
+inline void ins_recycle(std::vector<VIns> &v) { recycle(v, g_ins_pool); }
 
 // A value wider than one 256-bit slot (512-bit mapping preimages
 // Concat(key, slot), keccak256_512 / its inverse, 257-bit overflow sums) is a
@@ -506,6 +511,8 @@ Lowered finish_one(LowerState S, Ref root, uint32_t max_slots, int sched) {
   uint32_t slots_used = 0;
 
   std::vector<uint32_t> out;
+  out.swap(g_words_pool);
+  out.clear();
   out.reserve(4 + 4 * n + 8 * S.pool.size() + 4);
   out.resize(4, 0u);
 
@@ -1277,7 +1284,12 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
       if (spill ? b.words[0] >= best.words[0] : b.words[2] >= best.words[2]) continue;
     }
     std::vector<uint32_t> bu;
-    if (mgp_uop_translate(b.words.data(), bu) != 0) continue;
+    bu.swap(g_uops_pool);
+    bu.clear();
+    if (mgp_uop_translate(b.words.data(), bu) != 0) {
+      recycle(bu, g_uops_pool);
+      continue;
+    }
     best = std::move(b);
     uops->swap(bu);
     have = true;
@@ -1331,7 +1343,7 @@ static int lower_all(const mgp_node *nodes, const uint64_t *node_offsets, uint32
       uops.clear();
       mgp_uop_translate(a.words.data(), uops);
     }
-    a.words.insert(a.words.end(), uops.begin(), uops.end());
+    a.uops.swap(uops);
     res[s] = std::move(a);
   }
   return bad ? MGP_E_ARG : MGP_OK;
@@ -1345,13 +1357,16 @@ int mgp_lower_vec(const mgp_node *nodes, const uint64_t *node_offsets, uint32_t 
   const int rc = lower_all(nodes, node_offsets, n_states, consts, const_offsets, max_slots, res);
   if (rc != MGP_OK) return rc;
   offs.assign((size_t)n_states + 1, 0);
-  for (uint32_t s = 0; s < n_states; ++s) offs[s + 1] = offs[s] + res[s].words.size();
+  for (uint32_t s = 0; s < n_states; ++s) offs[s + 1] = offs[s] + res[s].words.size() + res[s].uops.size();
   words.resize(offs[n_states]);
   status.resize(n_states);
 #pragma omp parallel for schedule(static)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     memcpy(words.data() + offs[s], res[s].words.data(), res[s].words.size() * 4u);
+    memcpy(words.data() + offs[s] + res[s].words.size(), res[s].uops.data(), res[s].uops.size() * 4u);
     status[s] = res[s].status;
+    recycle(res[s].words, g_words_pool);
+    recycle(res[s].uops, g_uops_pool);
   }
   return MGP_OK;
 }
@@ -1366,7 +1381,7 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
   uint64_t total = 0;
   for (uint32_t s = 0; s < n_states; ++s) {
     out_prog_offsets[s] = total;
-    total += res[s].words.size();
+    total += res[s].words.size() + res[s].uops.size();
   }
   out_prog_offsets[n_states] = total;
   if (out_words_used) *out_words_used = total;
@@ -1374,7 +1389,10 @@ extern "C" int mgp_lower(const mgp_node *nodes, const uint64_t *node_offsets, ui
 #pragma omp parallel for schedule(static)
   for (int64_t s = 0; s < (int64_t)n_states; ++s) {
     memcpy(out_words + out_prog_offsets[s], res[s].words.data(), res[s].words.size() * 4u);
+    memcpy(out_words + out_prog_offsets[s] + res[s].words.size(), res[s].uops.data(), res[s].uops.size() * 4u);
     if (out_status) out_status[s] = res[s].status;
+    recycle(res[s].words, g_words_pool);
+    recycle(res[s].uops, g_uops_pool);
   }
   return MGP_OK;
 }

@@ -245,19 +245,23 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
     }
   }
   stage("keys + lookup");
-  std::vector<mgp_node> mn;
-  std::vector<uint32_t> mc;
-  std::vector<uint64_t> mno(1, 0), mco(1, 0);
-  for (uint32_t s : miss) {
-    mn.insert(mn.end(), nodes + noff[s], nodes + noff[s + 1]);
-    mc.insert(mc.end(), consts + coff[s] * 8u, consts + coff[s + 1] * 8u);
-    mno.push_back(mn.size());
-    mco.push_back(mc.size() / 8u);
-  }
   U32Buf mw;
   std::vector<uint64_t> mo;
   std::vector<uint8_t> mst;
-  if (!miss.empty()) {
+  if (miss.size() == n_states) {  // a cold batch: its own node lists, no gathered copy
+    const int rc = mgp_lower_vec(nodes, noff, n_states, consts, coff, 0, mw, mo, mst);
+    if (rc != MGP_OK) return rc;
+    stage("lower");
+  } else if (!miss.empty()) {
+    std::vector<mgp_node> mn;
+    std::vector<uint32_t> mc;
+    std::vector<uint64_t> mno(1, 0), mco(1, 0);
+    for (uint32_t s : miss) {
+      mn.insert(mn.end(), nodes + noff[s], nodes + noff[s + 1]);
+      mc.insert(mc.end(), consts + coff[s] * 8u, consts + coff[s + 1] * 8u);
+      mno.push_back(mn.size());
+      mco.push_back(mc.size() / 8u);
+    }
     if (mc.empty()) mc.assign(8, 0u);
     stage("gather misses");
     const int rc = mgp_lower_vec(mn.data(), mno.data(), (uint32_t)miss.size(), mc.data(), mco.data(), 0, mw, mo, mst);

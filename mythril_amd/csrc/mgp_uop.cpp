@@ -349,7 +349,7 @@ void plan_bools(const uint32_t *ins, uint32_t n, BoolPlan &P) {
   P.andn.assign(n, 0);
   P.merged.assign(n, 0);
   P.neg.assign(n, 0);
-  BitIndex X;
+  static thread_local BitIndex X;  // build() re-assigns it, keeping the per-bit lists' capacity
   X.build(ins, n);
   for (uint32_t pc = 0; pc + 1 < n; ++pc) {
     const uint32_t *I = ins + (size_t)pc * MGP_INS_WORDS, *J = I + MGP_INS_WORDS;
@@ -526,7 +526,10 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
   const bool v1_ok = (v1[3] & 0xFFu) == MGP_ST_OK;
   const uint32_t *ins = v1 + MGP_HDR_WORDS;
   if (v1_ok) T.v1pool.assign(ins + (size_t)T.n_ins * MGP_INS_WORDS, ins + (size_t)T.n_ins * MGP_INS_WORDS + (size_t)T.n_c * 8);
-  std::vector<uint32_t> uops;
+  // per-thread scratch reused across calls (a WalletLibrary program reserves ~120 KB here;
+  // fresh memory per call is page faults that a batch's threads take in turn)
+  static thread_local std::vector<uint32_t> uops;
+  uops.clear();
   uops.reserve((size_t)T.n_ins * MGP_U_UOP_WORDS + 64u);
   // pass 1 only collects the register variables and the mask / sign constants: it emits
   // nothing and looks for no TSEL runs (a run reads the operands its steps would)
@@ -536,7 +539,7 @@ int mgp_uop_translate(const uint32_t *v1, std::vector<uint32_t> &out) {
     uops.push_back(w0); uops.push_back(w1); uops.push_back(w2); uops.push_back(w3);
   };
 
-  BoolPlan BP;
+  static thread_local BoolPlan BP;  // every field is re-assigned by plan_bools (read only when v1_ok)
   if (v1_ok) plan_bools(ins, T.n_ins, BP);
   auto translate = [&]() {
     for (uint32_t pc = 0; v1_ok && pc < T.n_ins && !T.bad; ++pc) {

@@ -77,6 +77,7 @@ Arr get(const mgp_fe_batch *B, int f) {
 struct PipeBufs {
   void *p[16] = {};
   size_t cap[16] = {};
+  U32Buf words;          // the batch's lowered programs (host), reused across calls
   void *host = nullptr;  // pinned staging: one upload and one download per call (pageable
   size_t hcap = 0;       // hipMemcpyAsync is a blocking staged copy, ~0.4 ms each)
   hipError_t ensure_host(size_t bytes) {
@@ -245,7 +246,11 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
     }
   }
   stage("keys + lookup");
-  U32Buf mw;
+  // the lowered misses, in a per-thread buffer kept across calls: a cold 1 024-state batch
+  // is ~60 MB of programs, and releasing that every call showed as ~10 ms on the call's path
+  static thread_local U32Buf mw_keep;
+  U32Buf &mw = mw_keep;
+  mw.clear();
   std::vector<uint64_t> mo;
   std::vector<uint8_t> mst;
   if (miss.size() == n_states) {  // a cold batch: its own node lists, no gathered copy
@@ -323,7 +328,7 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
   }
   stage("insert");
   return MGP_OK;
-}
+}  // (the batch's key copies and gathered programs are released here)
 
 }  // namespace
 
@@ -409,12 +414,17 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   const uint32_t *cp = consts.n ? (const uint32_t *)consts.p : zero8;
 
   // 1. lower the GPU programs (programs lowered by an earlier call come from the cache)
-  U32Buf words;
+  // the batch's programs, in the context's kept buffer (the same ~60 MB every call)
+  PipeBufs &D0 = bufs_of(ctx);
+  U32Buf &words = D0.words;
+  words.clear();
   std::vector<uint64_t> offs;
   std::vector<uint8_t> status;
   int rc = lower_cached((const mgp_node *)gnodes.p, (const uint64_t *)gnoff.p, n_states, cp,
                         (const uint64_t *)coff.p, words, offs, status);
   if (rc != MGP_OK) return mgp_ctx_fail(ctx, rc, "lowering failed");
+  static const bool timing = getenv("MGP_FE_TIMING") != nullptr;
+  if (timing) fprintf(stderr, "[check_batch] %u states: lowered at %.3f ms\n", n_states, 1e3 * (omp_get_wtime() - t));
   std::vector<uint32_t> order(n_states), bounds(257), bslots(256);
   const int nb = mgp_plan_buckets(words.data(), offs.data(), n_states, order.data(), bounds.data(), bslots.data(),
                                   256);
@@ -457,6 +467,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
       }
     }
   }
+  if (timing) fprintf(stderr, "[check_batch] %u states: step 1 done at %.3f ms\n", n_states, 1e3 * (omp_get_wtime() - t));
   lap(0);
 
   // 2. host UNSAT pre-check + variable domains

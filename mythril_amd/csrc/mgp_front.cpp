@@ -42,6 +42,7 @@
 #include <algorithm>
 #include <new>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/mgp.h"
@@ -577,6 +578,33 @@ struct mgp_fe_batch {
 };
 
 namespace {
+// Released batches, kept for the next mgp_build_states (their arrays keep their capacity):
+// a 1 024-state batch is ~50 MB, and returning it to the system on every call cost several
+// ms in the caller's result stage.  At most two are kept.
+std::mutex &fe_pool_mu() {
+  static std::mutex m;
+  return m;
+}
+std::vector<mgp_fe_batch *> &fe_pool() {
+  static std::vector<mgp_fe_batch *> p;
+  return p;
+}
+mgp_fe_batch *fe_take() {
+  {
+    std::lock_guard<std::mutex> lk(fe_pool_mu());
+    if (!fe_pool().empty()) {
+      mgp_fe_batch *B = fe_pool().back();
+      fe_pool().pop_back();
+      // the arrays a build may leave unset
+      B->gpu_nodes.clear();
+      B->dec_nodes.clear();
+      B->gpu_node_off.clear();
+      return B;
+    }
+  }
+  return new (std::nothrow) mgp_fe_batch();
+}
+
 inline uint64_t key_mix(uint64_t h, uint64_t x) {
   h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
   h *= 0xBF58476D1CE4E5B9ull;
@@ -644,7 +672,7 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
   }
   if (getenv("MGP_FE_TIMING")) fprintf(stderr, "[fe] build %.3f ms\n", 1e3 * omp_get_wtime() - 1e3 * t_start);
   if (bad) return MGP_E_ARG;
-  mgp_fe_batch *B = new (std::nothrow) mgp_fe_batch();
+  mgp_fe_batch *B = fe_take();
   if (!B) return MGP_E_NOMEM;
   B->n_states = n_states;
   B->node_off.assign(n_states + 1, 0);
@@ -765,6 +793,16 @@ int mgp_fe_get(const mgp_fe_batch *B, int field, const void **ptr, uint64_t *cou
   }
 }
 
-void mgp_fe_free(mgp_fe_batch *B) { delete B; }
+void mgp_fe_free(mgp_fe_batch *B) {
+  if (!B) return;
+  {
+    std::lock_guard<std::mutex> lk(fe_pool_mu());
+    if (fe_pool().size() < 2) {
+      fe_pool().push_back(B);
+      return;
+    }
+  }
+  delete B;
+}
 
 }  // extern "C"

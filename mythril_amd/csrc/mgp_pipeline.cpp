@@ -78,6 +78,7 @@ struct PipeBufs {
   void *p[16] = {};
   size_t cap[16] = {};
   U32Buf words;          // the batch's lowered programs (host), reused across calls
+  U32Buf dom;            // the batch's variable domains (host), reused across calls
   void *host = nullptr;  // pinned staging: one upload and one download per call (pageable
   size_t hcap = 0;       // hipMemcpyAsync is a blocking staged copy, ~0.4 ms each)
   hipError_t ensure_host(size_t bytes) {
@@ -471,12 +472,13 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   lap(0);
 
   // 2. host UNSAT pre-check + variable domains
-  std::vector<uint32_t> dom;
+  U32Buf &dom = D0.dom;  // kept across calls; mgp_refute_domains zeroes what it writes
+  dom.clear();
   if (flags & MGP_CHECK_NO_REFUTE) {
     memset(out_refuted, 0, n_states);
   } else {
     const bool want_dom = !(flags & MGP_CHECK_NO_DOMAINS);
-    if (want_dom) dom.assign((size_t)vo[n_states] * 33u, 0u);
+    if (want_dom) dom.resize((size_t)vo[n_states] * 33u);
     rc = want_dom ? mgp_refute_domains((const mgp_node *)nodes.p, (const uint64_t *)noff.p, n_states, cp,
                                        (const uint64_t *)coff.p, vo, 0, out_refuted, dom.data())
                   : mgp_refute((const mgp_node *)nodes.p, (const uint64_t *)noff.p, n_states, cp,

@@ -1106,9 +1106,12 @@ extern "C" int mgp_refute_domains(const mgp_node *nodes, const uint64_t *node_of
   // literal False, tests/laser/state/calldata_test.py:41-55 after folding)
   if (!node_offsets || !out || !var_off || (n_states && (!nodes || !const_offsets))) return MGP_E_ARG;
   if (!out_dom && var_off[n_states] > 0) return MGP_E_ARG;
-  if (out_dom) memset(out_dom, 0, (size_t)var_off[n_states] * 33u * 4u);
+  // zeroed per state by the threads (a 1 024-state batch's domains are ~20 MB)
+  if (out_dom && var_off[0]) memset(out_dom, 0, (size_t)var_off[0] * 33u * 4u);
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t st = 0; st < (int64_t)n_states; ++st) {
+    if (out_dom && var_off[st + 1] > var_off[st])
+      memset(out_dom + var_off[st] * 33u, 0, (size_t)(var_off[st + 1] - var_off[st]) * 33u * 4u);
     const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
     const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
     if (n1 < n0 || c1 < c0) {
@@ -1274,9 +1277,16 @@ template <typename Put>
 void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64_t tag, Put &put,
                   const uint32_t *sv = nullptr, const uint8_t *sm = nullptr, uint32_t seed_rows = 0) {
   const State &s = P.s;
-  std::vector<AV> av(s.av), vars(s.vars);
-  std::vector<uint8_t> bs(s.bs);
-  std::vector<Pair> pairs(s.pairs);
+  // the row's private copy of the base analysis, in per-thread vectors that keep their
+  // capacity across rows (fresh ~150 KB copies per row were page faults the threads of a
+  // large batch take in turn)
+  static thread_local std::vector<AV> av, vars;
+  static thread_local std::vector<uint8_t> bs;
+  static thread_local std::vector<Pair> pairs;
+  av.assign(s.av.begin(), s.av.end());
+  vars.assign(s.vars.begin(), s.vars.end());
+  bs.assign(s.bs.begin(), s.bs.end());
+  pairs.assign(s.pairs.begin(), s.pairs.end());
   // the undo log and work list live in per-thread buffers reused across rows (only the
   // first `cap` entries of each are addressable, as on the device); allocated without a
   // zero fill, and released after a row of a large state so that one big state does not
@@ -1303,6 +1313,11 @@ void decision_row(const Prep &P, uint32_t row, uint32_t c, uint64_t seed, uint64
   mgpd::decision_row(pv, d, row, c, seed, tag, or_rows_mask(), put, sv, sm, seed_rows);
   undo_buf.trim();
   work_buf.trim();
+  if (av.capacity() * sizeof(AV) > RowBuf<AV>::kKeepBytes) {  // (as the undo log: no big state pinned)
+    std::vector<AV>().swap(av);
+    std::vector<AV>().swap(vars);
+    std::vector<Pair>().swap(pairs);
+  }
 }
 }  // namespace
 

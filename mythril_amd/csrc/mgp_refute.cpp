@@ -1420,6 +1420,35 @@ extern "C" int mgp_decision_rows_from(const mgp_node *nodes, const uint64_t *nod
       (n_states && n_decide && (!out_rows || !out_mask)))
     return MGP_E_ARG;
   if (n_states && n_decide) memset(out_mask, 0, (size_t)n_states * n_decide * n_vars);
+  // one row per state (the first round's row of large states): a state's analysis and its
+  // row are one task, so the threads stay busy to the end instead of meeting at a barrier
+  // between the analyses and the rows of every 256-state chunk (the same rows)
+  if (n_decide == 1) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t st = 0; st < (int64_t)n_states; ++st) {
+      if (skip_prep(rows_per_state, n_decide, (uint32_t)st)) {
+        out[st] = 0;
+        continue;
+      }
+      const uint64_t n0 = node_offsets[st], n1 = node_offsets[st + 1];
+      const uint64_t c0 = const_offsets[st], c1 = const_offsets[st + 1];
+      Prep P;
+      prep_state(P, nodes + n0, n1 - n0, consts ? consts + 8ull * c0 : nullptr, c1 - c0, max_passes, n_vars);
+      out[st] = (int8_t)P.r;
+      const uint32_t rs = rows_per_state ? std::min<uint32_t>(rows_per_state[st], 1u) : 1u;
+      if (P.r != 0 || rs == 0) continue;
+      const uint64_t tag = state_keys ? state_keys[st] : (uint64_t)st << 32;
+      const uint64_t r0 = (uint64_t)st * n_vars;
+      auto put = [&](uint32_t sl, const V &v) {
+        memcpy(out_rows + (r0 + sl) * 8ull, v.w, 32);
+        out_mask[r0 + sl] = 1;
+      };
+      const uint64_t sb = (uint64_t)st * n_vars;
+      decision_row(P, row0, 2u * row0, seed, tag, put, seed_vals ? seed_vals + sb * 8u : nullptr,
+                   seed_mask ? seed_mask + sb : nullptr, seed_rows);
+    }
+    return MGP_OK;
+  }
   constexpr uint32_t kChunk = 256;
   for (uint32_t cs = 0; cs < n_states; cs += kChunk) {
     const uint32_t ce = std::min<uint32_t>(n_states, cs + kChunk);

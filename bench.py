@@ -106,6 +106,8 @@ def main():
                     help="open states of that sample given the domain-guided second witness round")
     ap.add_argument("--keccak-sample-every", type=int, default=1 << 20,
                     help="beyond the first 65 536, check one digest in this many against the oracle")
+    ap.add_argument("--detail", default=None,
+                    help="path of the full JSON record (default profiles/bench_detail_r6.json)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks run the shard plumbing on CPU and rank 0 prints one line")
     args = ap.parse_args()
@@ -676,9 +678,75 @@ def main():
             "suite": suite,
             "gather": gather,
         }
-        print(json.dumps(line), flush=True)
+        # the full record (suite by contract, wallet sweep, latency and stage splits, A/B legs)
+        # goes to a side file; stdout carries the headline line the driver parses (< 12 KB)
+        detail = args.detail or os.path.join(ROOT, "profiles", "bench_detail_r6.json")
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(line, f, indent=1)
+        except OSError as e:
+            log(f"detail file {detail} not written: {e}")
+            detail = None
+        head = headline(line, detail)
+        text = json.dumps(head)
+        if len(text) > HEADLINE_MAX_BYTES:
+            raise RuntimeError(f"headline JSON line is {len(text)} bytes (> {HEADLINE_MAX_BYTES})")
+        print(text, flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+HEADLINE_MAX_BYTES = 12000
+_SUITE_KEYS = ("contracts", "queries", "ref_calls", "z3_calls", "reduction", "contradicted")
+
+
+def _pick(d, keys):
+    return None if d is None else {k: d[k] for k in keys if k in d}
+
+
+def headline(line: dict, detail_path) -> dict:
+    """The driver's one-line record: the contract keys, the eval kernel's roofline and CPU
+    baseline, and one level of the Keccak / front-end / suite results.  Everything else
+    stays in the detail file whose path it names."""
+    head = {k: line[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+    rf = dict(line["roofline"])
+    rf.pop("div_split", None)
+    head["roofline"] = rf
+    head["roofline_hbm"] = line["roofline_hbm"]
+    head["valu_busy"] = line["valu_busy"]
+    head["cpu_baseline"] = line["cpu_baseline"]
+    head["results"] = line["results"]
+    k = line.get("keccak")
+    if k is not None:
+        krf = {x: k["roofline"][x] for x in ("bound", "achieved", "peak", "unit", "frac", "traffic", "ops",
+                                             "kernel", "launch_ms", "hashes_per_launch")}
+        head["keccak"] = {"metric": k["metric"], "value": k["value"], "unit": k["unit"],
+                          "hashes_per_gpu": k["hashes_per_gpu"], "roofline": krf,
+                          "verified_mismatches": k["verified"]["mismatches"],
+                          "verified_checked": k["verified"]["checked"],
+                          "cpu_baseline": _pick(k.get("cpu_baseline"), ("value", "unit", "cores", "kind", "sample"))}
+    fe = line.get("frontend")
+    if fe is not None:
+        head["frontend"] = {**_pick(fe, ("states", "seconds", "states_per_s", "first_call_seconds", "sat", "unsat",
+                                         "undecided", "solver_call_reduction")),
+                            "contradicted": fe["expectations"]["contradicted"],
+                            "gpu_wait_ms": fe["stages_ms"].get("gpu_wait_ms"),
+                            "latency_ms": {str(r["states"]): round(r["ms_per_call"], 3) for r in fe["latency"]}}
+    pf = line.get("prefilter")
+    if pf is not None:
+        head["prefilter"] = _pick(pf, ("sample_states", "gpu_sat", "refuted", "fallback", "solver_call_reduction"))
+    su = line.get("suite")
+    if su is not None:
+        head["suite"] = {part: _pick(su.get(part), _SUITE_KEYS) for part in ("all", "tuned", "held_out")}
+        head["suite"]["seconds"] = su.get("seconds")
+        for extra in ("soundness", "frozen"):
+            if extra in su:
+                head["suite"][extra] = su[extra]
+    head["gather"] = line.get("gather")
+    head["detail"] = None if detail_path is None else os.path.relpath(detail_path, ROOT)
+    return head
 
 
 def measure_valu_peak(N, torch, dev, stream, sh) -> float:

@@ -258,17 +258,34 @@ def suite(hasher=None, max_open: int = 6, contracts=None):
         out.extend((cls.name, kind, label, terms, exp, -1 if par < 0 else base + par)
                    for kind, label, terms, exp, par in run.queries)
     # a query is asked on a state its parent query established: a "sat" read off the query's
-    # own constraint holds only if that state is reachable, so it stays "sat" only when the
-    # parent's expectation is "sat" (an "unsat" needs no such condition)
-    # (such a dropped expectation stays visible: its label ends in SAT_IF_REACHABLE and
-    # account() reports how many there are)
+    # own constraint holds only if that state is reachable.  Under a parent expected "unsat"
+    # it is dropped (the label ends in UNDER_UNSAT_PARENT).  Under an ancestor whose
+    # expectation reading leaves open it stays "sat" with the label suffix SAT_IF_REACHABLE:
+    # account() then counts a refutation of it as a contradiction unless an ancestor of it is
+    # refuted as well (an unsound refutation must not hide behind an unlabelled
+    # parent)
     for k, (c, kind, label, terms, exp, par) in enumerate(out):
-        if exp == "sat" and par >= 0 and out[par][4] != "sat":
-            out[k] = (c, kind, label + SAT_IF_REACHABLE, terms, None, par)
+        if exp != "sat" or par < 0:
+            continue
+        if out[par][4] == "unsat":
+            out[k] = (c, kind, label + UNDER_UNSAT_PARENT, terms, None, par)
+        elif out[par][4] is None or out[par][2].endswith(SAT_IF_REACHABLE):
+            out[k] = (c, kind, label + SAT_IF_REACHABLE, terms, exp, par)
     return out
 
 
 SAT_IF_REACHABLE = " [sat if its parent state is reachable]"
+UNDER_UNSAT_PARENT = " [parent expected unsat]"
+
+
+def ancestors(queries, k):
+    """Indices of query k's ancestors along the parent links, nearest first."""
+    out = []
+    p = queries[k][5]
+    while p >= 0:
+        out.append(p)
+        p = queries[p][5]
+    return out
 
 
 def held_out() -> set:
@@ -293,16 +310,26 @@ def account(queries, answers, held=None) -> dict:
 
     per = collections.OrderedDict()
     seen = set()
-    for (contract, kind, label, terms, exp, _parent), ans in zip(queries, answers):
+    for qi, ((contract, kind, label, terms, exp, _parent), ans) in enumerate(zip(queries, answers)):
         c = per.setdefault(contract, {"queries": 0, "ref_calls": 0, "z3_calls": 0, "sat": 0, "unsat": 0,
                                       "undecided": 0, "contradicted": 0, "expected_sat": 0, "expected_sat_witness": 0,
-                                      "expected_unsat": 0, "expected_unsat_refuted": 0,
+                                      "expected_unsat": 0, "expected_unsat_refuted": 0, "sat_if_reachable": 0,
+                                      "refuted_with_sat_expectation_if_reachable": 0,
+                                      "refuted_if_reachable_ancestor_refuted": 0,
                                       "by_kind": {k: {"queries": 0, "ref_calls": 0, "z3_calls": 0}
                                                   for k in ("prune", "model", "dep", "txseq")}})
         c["queries"] += 1
         c[ans] += 1
         bk = c["by_kind"][kind]
         bk["queries"] += 1
+        if exp == "sat" and label.endswith(SAT_IF_REACHABLE):
+            # (every occurrence, not only the lru-distinct ones counted below)
+            c["sat_if_reachable"] += 1
+            if ans == "unsat":
+                if any(answers[a] == "unsat" for a in ancestors(queries, qi)):
+                    c["refuted_if_reachable_ancestor_refuted"] += 1
+                else:
+                    c["refuted_with_sat_expectation_if_reachable"] += 1
         if kind != "prune":
             key = (contract, kind, terms)
             if key in seen:
@@ -320,11 +347,14 @@ def account(queries, answers, held=None) -> dict:
         elif exp == "sat":
             c["expected_sat"] += 1
             c["expected_sat_witness"] += ans == "sat"
-            c["contradicted"] += ans == "unsat"
+            if ans == "unsat":
+                # a refuted sat-if-reachable query is consistent only under a refuted ancestor
+                c["contradicted"] += not (label.endswith(SAT_IF_REACHABLE) and
+                                          any(answers[a] == "unsat" for a in ancestors(queries, qi)))
     for c in per.values():
         c["reduction"] = c["ref_calls"] / max(1, c["z3_calls"])
         c["held_out"] = False
-    dropped = collections.Counter(q[0] for q in queries if q[2].endswith(SAT_IF_REACHABLE))
+    dropped = collections.Counter(q[0] for q in queries if q[2].endswith(UNDER_UNSAT_PARENT))
     for name, c in per.items():
         c["sat_expectations_dropped"] = dropped.get(name, 0)
     for name in per:
@@ -337,6 +367,9 @@ def account(queries, answers, held=None) -> dict:
                 "z3_calls": z, "reduction": r / max(1, z),
                 "contradicted": sum(per[n]["contradicted"] for n in names),
                 "sat_expectations_dropped": sum(per[n]["sat_expectations_dropped"] for n in names),
+                **{f: sum(per[n][f] for n in names) for f in (
+                    "sat_if_reachable", "refuted_with_sat_expectation_if_reachable",
+                    "refuted_if_reachable_ancestor_refuted")},
                 "by_kind": {k: {f: sum(per[n]["by_kind"][k][f] for n in names) for f in ("queries", "ref_calls",
                                                                                      "z3_calls")}
                             for k in ("prune", "model", "dep", "txseq")}}

@@ -52,6 +52,8 @@ from __future__ import annotations
 
 import copy
 import itertools
+import json
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from mythril_amd.smt import (And, Array, BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow, Concat, Extract, If,
@@ -224,18 +226,83 @@ class Analysis:
 
 
 def refuter():
-    """The host UNSAT pre-check (mgp_refute, CPU code) as a decider for branches and module
-    queries that reading leaves open: terms -> refuted?"""
+    """The host UNSAT pre-check as a decider for branches and module queries that reading
+    leaves open: terms -> refuted?  It is the product's strongest setting (mgp_refute_split
+    with Prefilter's case splits and interval bisection, CPU code): a refutation is a proof,
+    so z3 answers unsat there and LASER drops the state -- a weaker decider would follow
+    branches the reference never reaches and count their queries on both sides."""
     from mythril_amd import _native as N
     from mythril_amd.front import Batch
+    from mythril_amd.solver import Prefilter
+
+    cache = refute_cache()
 
     def decide(terms: tuple) -> bool:
         B = Batch([list(terms)])
         try:
-            return int(N.refute(*B.packed())[0]) == 1
+            key = f"{int(B.state_key[0]):016x}"
+            r = cache.get(key)
+            if r is None:
+                r = cache[key] = int(N.refute_split(*B.packed()[:4], max_splits=Prefilter.SPLIT_REFUTE,
+                                                    depth=Prefilter.SPLIT_DEPTH)[0]) == 1
+            return r
         finally:
             B.close()
     return decide
+
+
+# The stream generator's refutations, by state content key (mgp_build_states
+# MGP_FE_STATE_KEY), computed by the refuter itself and kept in corpus/refute_cache.json so
+# that a suite() call does not re-run a minute of case splits on states it has decided before
+# (`python -m corpus.laser` rewrites it).  The file carries a hash of the refuter's sources and
+# settings: after any change to them it is ignored and every decision is recomputed live.
+_CACHE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "refute_cache.json")
+_CACHE: Optional[Dict[str, bool]] = None
+
+
+def _refuter_version() -> str:
+    import hashlib
+
+    from mythril_amd.solver import Prefilter
+
+    h = hashlib.sha256(f"{Prefilter.SPLIT_REFUTE}/{Prefilter.SPLIT_DEPTH}".encode())
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mythril_amd", "csrc")
+    for f in ("mgp_refute.cpp", "mgp_domain.h", "mgp_bv.h", "mgp_front.cpp"):
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:32]
+
+
+def refute_cache() -> Dict[str, bool]:
+    global _CACHE
+    if _CACHE is None:
+        _CACHE = {}
+        try:
+            with open(_CACHE_PATH) as f:
+                blob = json.load(f)
+            if blob.get("version") == _refuter_version():
+                _CACHE = {k: bool(v) for k, v in blob["decisions"].items()}
+        except (OSError, ValueError, KeyError):
+            pass
+    return _CACHE
+
+
+def save_refute_cache() -> int:
+    with open(_CACHE_PATH, "w") as f:
+        json.dump({"version": _refuter_version(), "decisions": {k: int(v) for k, v in sorted(refute_cache().items())}},
+                  f, separators=(",", ":"))
+    return len(refute_cache())
+
+
+if __name__ == "__main__":
+    import corpus
+    from corpus import laser as _L  # the module suite() uses (this file runs as __main__)
+
+    from oracle.keccak_ref import keccak256  # CPU Keccak for the manager's concrete hashes
+
+    for mo in (6, 12, 24):
+        corpus.suite(hasher=keccak256, max_open=mo, contracts=None if mo == 6 else {"wallet"})
+    print(f"{_L.save_refute_cache()} decisions -> {_L._CACHE_PATH}")
 
 
 class OverflowAnn:

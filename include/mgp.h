@@ -182,10 +182,14 @@ int mgp_refute(const mgp_node *nodes, const uint64_t *node_offsets,
  * condition (BV ITE / BITE, nearest the root first; max_splits bits 0..15 = at most this
  * many per state) is assumed true and false in turn, and each branch is split again on
  * the others up to (max_splits >> 16) & 15 levels (0 = 1); both branches refuted -> 1;
- * one refuted -> the other polarity is kept.  A 1 is a proof.  The product runs it on the states both witness
- * rounds leave open (solver.Prefilter), before they go to the caller's solver:
- * ether_thief's balance comparisons after a zero-value transfer whose recipient is open
- * (mythril/analysis/module/modules/ether_thief.py:55-95). */
+ * one refuted -> the other polarity is kept.  Then (round 6; max_splits bit 20 clear)
+ * interval bisection: a variable whose interval the analysis bounded is split in halves,
+ * 8 levels deep, each half propagated; every leaf refuted -> 1 (rubixi.sol:130-151:
+ * value * 90 / 100 > value * 300 / 100 between two require()s on value).  A 1 is a proof.
+ * The product runs it on the states both witness rounds leave open (solver.Prefilter),
+ * before they go to the caller's solver: ether_thief's balance comparisons after a
+ * zero-value transfer whose recipient is open (mythril/analysis/module/modules/
+ * ether_thief.py:55-95). */
 int mgp_refute_split(const mgp_node *nodes, const uint64_t *node_offsets,
                      uint32_t n_states, const uint32_t *consts,
                      const uint64_t *const_offsets, uint32_t max_passes,

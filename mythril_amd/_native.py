@@ -423,9 +423,10 @@ def refute(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, cons
 
 
 def refute_split(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray, const_offsets: np.ndarray,
-                 max_splits: int = 8, max_passes: int = 0, depth: int = 1) -> np.ndarray:
+                 max_splits: int = 8, max_passes: int = 0, depth: int = 1, bisect: bool = True) -> np.ndarray:
     """refute + case splits on open select conditions (mgp_refute_split): at most
-    max_splits conditions per state, nested `depth` levels (1..15)."""
+    max_splits conditions per state, nested `depth` levels (1..15); then (bisect) interval
+    bisection of bounded variables."""
     if not 0 <= max_splits < (1 << 16) or not 1 <= depth <= 15:
         raise ValueError(f"refute_split: max_splits {max_splits} / depth {depth} out of range")
     nodes = np.ascontiguousarray(nodes, dtype=NODE_DTYPE)
@@ -437,7 +438,7 @@ def refute_split(nodes: np.ndarray, node_offsets: np.ndarray, consts: np.ndarray
     n_states = len(node_offsets) - 1
     out = np.zeros(max(n_states, 1), dtype=np.int8)
     _check(lib().mgp_refute_split(_ptr(nodes), _ptr(node_offsets), n_states, _ptr(consts), _ptr(const_offsets),
-                                  max_passes, max_splits | (depth << 16), _ptr(out)))
+                                  max_passes, max_splits | (depth << 16) | (0 if bisect else 1 << 20), _ptr(out)))
     return out[:n_states]
 
 

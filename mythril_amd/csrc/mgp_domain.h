@@ -367,8 +367,8 @@ MGP_RD AV flip(const AV &a, uint32_t w) {
 enum : uint8_t { OLT = 1, OEQ = 2, OGT = 4, OALL = 7 };
 constexpr uint32_t kVarBit = 0x80000000u;  // a work-list entry naming a variable-table entry
 constexpr uint32_t kUfGroup = 48;          // UF congruence: functions with at most this many applications
-constexpr int kCongDepth = 4;
-constexpr int kChainBudget = 256;          // rel_under steps per pair (Dom::chain_orders)              // structural congruence: operator levels arg_equal looks through
+constexpr int kCongDepth = 4;    // structural congruence: operator levels arg_equal looks through
+constexpr int kChainBudget = 256;  // rel_under steps per pair (Dom::chain_orders)
 
 struct Pair { int32_t x, y; uint8_t u, s; };
 struct UfApp { int32_t node, arg; uint32_t fn; uint8_t op; };
@@ -1884,7 +1884,7 @@ MGP_RD void decision_row(const PrepView &P, Dom &d, uint32_t row, uint32_t c, ui
   MGPD_TRACE("=== row %u\n", row);
   Stack<UndoRec> &undo_log = *d.undo;
   Stack<uint32_t> &work = *d.touched;
-    const uint32_t budget = 4u * d.n + 64u;
+  const uint32_t budget = 4u * d.n + 64u;
   // the case splits (wrap pairs, Or and ITE branches) are few and steer the whole row: a
   // split whose consequences are cut short by the budget leaves a contradiction that every
   // later draw runs into, so they propagate further

@@ -47,6 +47,7 @@
 
 #include "../../include/mgp.h"
 #include "mgp_buf.h"
+#include "mgp_bv.h"
 
 namespace {
 
@@ -364,8 +365,31 @@ void build_one(const Arena &A, const int32_t *roots, uint64_t n_roots, StateOut 
     if (n.op == MGP_OP_UFAPP || n.op == MGP_OP_UFINV) return n.p1;
     return -1;
   };
+  // wrap hints: x * c (and BVMulNoOverflow(x, c)) with a constant c >= 2 -> the largest x
+  // that does not wrap and the smallest that does, floor((2^w-1)/c) and +1.  Paths whose
+  // feasibility rests on an overflowing product (rubixi's payout = value * multiplier / 100
+  // against the balance share, the integer module's Not(BVMulNoOverflow)) have their
+  // witnesses right past that boundary, where neither uniform nor small values land.
+  auto wrap_hints = [&](int64_t vi, int32_t cnode, uint32_t w) {
+    if (vi < 0 || S.nodes[cnode].op != MGP_OP_CONST || w > 256 || w < 2) return;
+    U256 c, q, r;
+    memcpy(c.w, &S.consts[8u * S.nodes[cnode].p0], 32);
+    c = bv_mask(c, w);
+    if (bv_ult(c, bv_small(2))) return;
+    bv_udivrem(bv_mask(bv_ones(), w), c, &q, &r);
+    U256 q1 = bv_mask(bv_add(q, bv_small(1), nullptr), w);
+    auto &H = S.hints[vi];
+    H.insert(H.end(), q.w, q.w + 8);
+    H.insert(H.end(), q1.w, q1.w + 8);
+  };
   for (const mgp_node &n : S.nodes) {
-    if (n.op < MGP_OP_EQ || n.op > MGP_OP_USUB_NOUDF || n.a < 0 || n.b < 0) continue;
+    if (n.a < 0 || n.b < 0) continue;
+    if (n.op == MGP_OP_MUL || n.op == MGP_OP_UMUL_NOOVF) {
+      const uint32_t w = S.nodes[n.a].width;
+      wrap_hints(var_of(n.a), n.b, w);
+      wrap_hints(var_of(n.b), n.a, w);
+    }
+    if (n.op < MGP_OP_EQ || n.op > MGP_OP_USUB_NOUDF) continue;
     const int64_t va = var_of(n.a), vb = var_of(n.b);
     if (n.op == MGP_OP_EQ && va >= 0 && vb >= 0 && va != vb) {
       S.aliases.push_back((uint32_t)va);

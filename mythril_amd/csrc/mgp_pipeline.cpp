@@ -249,7 +249,11 @@ int lower_cached(const mgp_node *nodes, const uint64_t *noff, uint32_t n_states,
   stage("keys + lookup");
   // the lowered misses, in a per-thread buffer kept across calls: a cold 1 024-state batch
   // is ~60 MB of programs, and releasing that every call showed as ~10 ms on the call's path
+  // (capped, ADVICE r5: a buffer past kKeepWords -- a batch larger than the 1 024-state bench
+  // call -- is released here rather than pinned by this thread for the life of the process)
   static thread_local U32Buf mw_keep;
+  constexpr size_t kKeepWords = (size_t)32 << 20;  // 128 MB
+  if (mw_keep.capacity() > kKeepWords) U32Buf().swap(mw_keep);
   U32Buf &mw = mw_keep;
   mw.clear();
   std::vector<uint64_t> mo;

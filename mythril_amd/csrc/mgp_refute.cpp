@@ -866,8 +866,10 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
 // cover every model of the state they split.
 int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t max_passes,
                      uint32_t max_splits) {
-  // max_splits: atoms per level in bits 0..15, levels in bits 16..19 (0 = 1)
+  // max_splits: atoms per level in bits 0..15, levels in bits 16..19 (0 = 1), bit 20 set =
+  // no interval bisection
   const uint32_t n_atoms = max_splits & 0xFFFFu, depth = std::max<uint32_t>(1u, (max_splits >> 16) & 0xFu);
+  const bool bisection = ((max_splits >> 20) & 1u) == 0u;
   State s;
   const int r = refute_one(nd, n, consts, n_consts, max_passes, &s);
   if (r != 0 || n_atoms == 0) return r;
@@ -922,7 +924,51 @@ int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uin
     }
     return false;
   };
-  return probe(depth) ? 1 : 0;
+  if (probe(depth)) return 1;
+  if (!bisection) return 0;
+  // Interval bisection (round 6): a variable whose interval the analysis bounded (a call
+  // value between two require()s, a balance below a cap) is split in two halves, each
+  // half propagated and split again, kBisectDepth levels; every leaf refuted -> refuted.
+  // Intervals lose the relation between two terms computed from one variable (rubixi.sol
+  // addPayout: value * 90 / 100 > value * 300 / 100 for 1 ether <= value < 50 ether holds
+  // for no value, yet the two quotients' intervals overlap); on a narrow enough piece of the
+  // variable's range they no longer do.  Sound: the halves cover the interval.  Split points
+  // follow the bit lengths first (a ratio test needs pieces within a constant factor), then
+  // the arithmetic midpoint.
+  constexpr uint32_t kBisectVars = 6, kBisectDepth = 8;
+  std::vector<int32_t> bvars;
+  for (uint32_t i = s.n; i-- > 0 && bvars.size() < kBisectVars;) {
+    const mgp_node &x = s.nd[i];
+    if (x.op != MGP_OP_VAR && x.op != MGP_OP_UFAPP && x.op != MGP_OP_UFINV) continue;
+    if (x.width < 2u || x.width > 256u) continue;
+    const AV &a = s.av[i];
+    if (is_exact(a) || (Z(a.lo) && EQV(a.hi, M(x.width)))) continue;  // one value, or unbounded
+    bvars.push_back((int32_t)i);
+  }
+  std::vector<Snap> bsnaps(kBisectDepth);
+  std::function<bool(int32_t, uint32_t)> bisect = [&](int32_t v, uint32_t level) -> bool {
+    if (level == 0 || runs_left <= 0) return false;
+    const AV a = s.av[v];
+    if (is_exact(a)) return false;
+    const uint32_t w = s.nd[v].width, lb = bv_bitlen(a.lo), hb = bv_bitlen(a.hi);
+    V mid = hb > lb + 1u ? SUBV(SHL(ONE(), (lb + hb) / 2u), ONE())
+                         : ADDV(a.lo, SHR(SUBV(a.hi, a.lo), 1u));
+    if (LT(mid, a.lo) || !LT(mid, a.hi)) mid = ADDV(a.lo, SHR(SUBV(a.hi, a.lo), 1u));
+    Snap &c = bsnaps[level - 1];
+    take(c);
+    for (int side = 0; side < 2; ++side) {
+      AV t = top(w);
+      t.lo = side ? ADDV(mid, ONE()) : a.lo;
+      t.hi = side ? a.hi : mid;
+      const bool r = !d.meet(v, t) || run_capped() == 1 || bisect(v, level - 1);
+      put(c);
+      if (!r) return false;
+    }
+    return true;
+  };
+  for (int32_t v : bvars)
+    if (bisect(v, kBisectDepth)) return 1;
+  return 0;
 }
 
 }  // namespace
@@ -1226,6 +1272,31 @@ void prep_state(Prep &P, const mgp_node *nodes, uint64_t n, const uint32_t *cons
       V c;
       memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
       eqh[k].push_back(bv_mask(c, P.width[k]));
+    }
+  }
+  // ... then the smallest value whose product with a constant c >= 2 wraps,
+  // floor((2^w-1)/c) + 1 (x * c and BVMulNoOverflow(x, c)): an interval holding the
+  // variable's bounds says nothing about where x * c wraps, so a draw from it almost never
+  // lands past that boundary (rubixi.sol:130-151: payout = value * multiplier / 100 above
+  // the balance share only once value * multiplier wraps)
+  for (uint32_t i = 0; i < s.n; ++i) {
+    const mgp_node &x = s.nd[i];
+    if ((x.op != MGP_OP_MUL && x.op != MGP_OP_UMUL_NOOVF) || x.a < 0 || x.b < 0) continue;
+    for (int side = 0; side < 2; ++side) {
+      const int32_t me = side ? x.b : x.a, other = side ? x.a : x.b;
+      const int32_t k = kof[me];
+      if (k < 0 || s.nd[other].op != MGP_OP_CONST || s.nd[other].p0 >= s.n_consts) continue;
+      const uint32_t w = P.width[k];
+      if (w < 2u || w > 256u || eqh[k].size() >= 16) continue;
+      V c, q, r;
+      memcpy(c.w, s.consts + 8ull * s.nd[other].p0, 32);
+      c = bv_mask(c, w);
+      if (bv_ult(c, bv_small(2u))) continue;
+      bv_udivrem(bv_mask(bv_ones(), w), c, &q, &r);
+      const V b = bv_mask(bv_add(q, bv_small(1u), nullptr), w);
+      bool dup = false;
+      for (const V &e : eqh[k]) dup |= bv_eq(e, b);
+      if (!dup) eqh[k].push_back(b);
     }
   }
   P.eqh_off.assign(1, 0u);

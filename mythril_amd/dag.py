@@ -258,7 +258,22 @@ def _harvest_hints(d: StateDag) -> None:
     intervals, keccak_function_manager.py:135-140) ; x == y -> alias pair."""
     nodes = d.nodes
     for (op, w, a, b, c, p0, p1) in nodes:
-        if op < ir.EQ or op > ir.USUB_NOUDF or a < 0 or b < 0:
+        if a < 0 or b < 0:
+            continue
+        if op in (ir.MUL, ir.UMUL_NOOVF):
+            # wrap hints: x * c -> floor((2^w-1)/c) and +1 (csrc/mgp_front.cpp wrap_hints)
+            wa = nodes[a][1]
+            for x, y in ((a, b), (b, a)):
+                vi = _var_of(nodes, x)
+                if vi < 0 or nodes[y][0] != ir.CONST or wa > 256 or wa < 2:
+                    continue
+                m = (1 << wa) - 1
+                cv = d.consts[nodes[y][5]] & m
+                if cv < 2:
+                    continue
+                q = m // cv
+                d.hints.setdefault(vi, []).extend([q, (q + 1) & m])
+        if op < ir.EQ or op > ir.USUB_NOUDF:
             continue
         va, vb = _var_of(nodes, a), _var_of(nodes, b)
         if op == ir.EQ and va >= 0 and vb >= 0 and va != vb:

@@ -12,7 +12,12 @@ Per contract it checks:
   C oracle does not take, by oracle.bvsem;
 * no answer contradicts a by-reading expectation (corpus.account);
 * the z3 calls left (undecided prune / model queries + every tx-sequence query that is not
-  refuted, corpus.account) stay within the ceiling measured at the last round's close.
+  refuted, corpus.account) stay within the ceiling measured at the last round's close;
+* the UNSAT side is sound on every contract shape the suite has: no
+  query that got a GPU witness -- a model, checked above -- is refuted by mgp_refute, by
+  mgp_refute_split at the product's settings (case splits + interval bisection), or covered
+  by a stored UNSAT core; and no refuted query whose "sat" expectation holds once its state
+  is reachable lacks a refuted ancestor (corpus.account counts that as a contradiction).
 
 Issue-level parity with the reference stays unpinned."""
 import numpy as np
@@ -20,7 +25,9 @@ import pytest
 
 import corpus
 from corpus import contracts as C
+from mythril_amd import _native as N
 from mythril_amd import dag as D
+from mythril_amd import front as F
 from mythril_amd import solver as SV
 from oracle import bvsem as S
 from oracle import coracle
@@ -64,6 +71,23 @@ def witnesses_hold(items):
     return ok
 
 
+def refuted_witnessed(qs, sat):
+    """Labels of witnessed queries (indices `sat`) that the refuter or the core cache calls UNSAT."""
+    if not sat:
+        return []
+    B = F.Batch([list(qs[k][3]) for k in sat])
+    try:
+        packed = B.packed()[:4]
+        plain = N.refute(*packed)
+        split = N.refute_split(*packed, max_splits=SV.Prefilter.SPLIT_REFUTE, depth=SV.Prefilter.SPLIT_DEPTH)
+    finally:
+        B.close()
+    SV.unsat_cores().flush(N)   # pending refuted lists -> cores, then no core may cover a model
+    cores = SV.unsat_cores()
+    return [(qs[k][2], int(p), int(r), bool(cores.covered(qs[k][3])))
+            for k, p, r in zip(sat, plain, split) if p == 1 or r == 1 or cores.covered(qs[k][3])]
+
+
 @pytest.fixture(scope="module")
 def prefilter(mgp_ctx):
     SV.enable_gpu(True)
@@ -85,6 +109,9 @@ def test_suite_contract_witnesses_and_calls(prefilter, name):
     held = witnesses_hold([(qs[k][3], wits[k]) for k in sat])
     bad = [qs[k][2] for k, h in zip(sat, held) if not h]
     assert not bad, f"{len(bad)} GPU witnesses are not models of their constraints: {bad[:5]}"
+    unsound = refuted_witnessed(qs, sat)
+    assert not unsound, f"refuter claims UNSAT for {len(unsound)} witnessed queries: {unsound[:5]}"
+    assert c["refuted_with_sat_expectation_if_reachable"] == 0, c
     print(f"{name}: {len(qs)} queries, {len(sat)} GPU witnesses checked, z3 calls {c['z3_calls']} "
           f"of {c['ref_calls']} restated reference calls ({c['by_kind']})")
     assert c["z3_calls"] <= CEILING[name], c

@@ -1056,7 +1056,10 @@ def test_case_split_depth_exhaustive_soundness():
     rng = np.random.default_rng(0x5917)
     states = [_transfer_chain_state(rng) for _ in range(600)]
     packed = pack_states(states)
-    levels = [N.refute(*packed)] + [N.refute_split(*packed, max_splits=8, depth=d) for d in (1, 2, 3)]
+    # (without the interval bisection: on 3-bit variables it enumerates every value, so one
+    # level with it refutes what three levels of case splits do; its soundness is checked
+    # below and in test_bisection_exhaustive_soundness)
+    levels = [N.refute(*packed)] + [N.refute_split(*packed, max_splits=8, depth=d, bisect=False) for d in (1, 2, 3)]
     counts = [int((r == 1).sum()) for r in levels]
     for lo, hi in zip(levels, levels[1:]):
         assert ((lo == 1) & (hi != 1)).sum() == 0, "a deeper split lost a refutation"
@@ -1068,6 +1071,56 @@ def test_case_split_depth_exhaustive_soundness():
     for st, r in zip(states, levels[3]):
         if r == 1:
             assert coracle.first_sat(*pack_states([st]), cands)[0] < 0, "refuted a satisfiable state"
+    withb = N.refute_split(*packed, max_splits=8, depth=2)
+    assert ((levels[2] == 1) & (withb != 1)).sum() == 0
+    for st, r in zip(states, withb):
+        if r == 1:
+            assert coracle.first_sat(*pack_states([st]), cands)[0] < 0, "bisection refuted a satisfiable state"
+
+
+def _ratio_state(rng, w=8):
+    """x bounded by two constants, then two products of x with constants (wrapping or not)
+    divided and compared -- rubixi.sol's payout against the balance share (130-151) -- next
+    to a second, free variable in an addition."""
+    lo, hi = sorted(int(v) for v in rng.integers(0, 1 << w, size=2))
+    c1, c2, d = (int(v) for v in rng.integers(1, 1 << (w // 2), size=3))
+    cl = [lo, hi, c1, c2, d]
+    nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
+    nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(5)]                     # 2..6
+    nl.append([S.UGE, 1, 0, 2, -1, 0, 0])                                         # 7: x >= lo
+    nl.append([S.ULE, 1, 0, 3, -1, 0, 0])                                         # 8: x <= hi
+    nl.append([S.MUL, w, 0, 4, -1, 0, 0])                                         # 9
+    nl.append([S.MUL, w, 0, 5, -1, 0, 0])                                         # 10
+    nl.append([S.UDIV, w, 9, 6, -1, 0, 0])                                        # 11
+    nl.append([S.UDIV, w, 10, 6, -1, 0, 0])                                       # 12
+    nl.append([S.ADD, w, 11, 1, -1, 0, 0] if rng.random() < 0.3 else [S.ADD, w, 11, 2, -1, 0, 0])  # 13
+    nl.append([[S.UGT, S.ULT, S.EQ][int(rng.integers(3))], 1, 13, 12, -1, 0, 0])  # 14
+    nl.append([S.BAND, 1, 7, 8, -1, 0, 0])
+    nl.append([S.BAND, 1, 15, 14, -1, 0, 0])
+    return nl, cl
+
+
+def test_bisection_exhaustive_soundness():
+    """Interval bisection (mgp_refute_split, round 6) on bounded-variable ratio tests over
+    8-bit values: it refutes states the case splits alone leave open, and every state it
+    refutes has no model over all 2^16 assignments of its two variables (C oracle)."""
+    rng = np.random.default_rng(0xB15E)
+    states = [_ratio_state(rng) for _ in range(400)]
+    packed = pack_states(states)
+    nob = N.refute_split(*packed, max_splits=8, depth=2, bisect=False)
+    withb = N.refute_split(*packed, max_splits=8, depth=2)
+    assert ((nob == 1) & (withb != 1)).sum() == 0
+    assert int((withb == 1).sum()) > int((nob == 1).sum()), (int((nob == 1).sum()), int((withb == 1).sum()))
+    grid = np.array(np.meshgrid(np.arange(256), np.arange(256), indexing="ij")).reshape(2, -1).T
+    cands = np.zeros((1, grid.shape[0], 2, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    n_unsat = 0
+    for st, r in zip(states, withb):
+        unsat = coracle.first_sat(*pack_states([st]), cands)[0] < 0
+        n_unsat += unsat
+        assert unsat or r != 1, "bisection refuted a satisfiable state"
+    # (on this shape it is also complete: 149 of 149 UNSAT states, 137 without it)
+    assert int((withb == 1).sum()) == n_unsat, (int((withb == 1).sum()), n_unsat)
 
 
 def test_refute_split_argument_range():

@@ -52,3 +52,27 @@ def test_case_split_refutes_what_plain_analysis_leaves():
     thief = [k for k, q in enumerate(qs) if "ether_thief" in q[2] and q[4] == "unsat"]
     n0, n1, n2 = (sum(r[k] == 1 for k in thief) for r in (plain, split, split2))
     assert n0 < n1 < n2, (n0, n1, n2)
+
+
+def test_no_refutation_of_a_witnessed_query():
+    """The UNSAT side on real contract shapes, on the CPU: every query of
+    calls.sol / returnvalue.sol / etherstore.sol that the CPU restatement of the witness
+    rounds answers with a model (checked by the C oracle there) is refuted neither by
+    mgp_refute nor by mgp_refute_split at the product's settings (case splits and interval
+    bisection); and every refuted query's sat-if-reachable expectation has a refuted ancestor."""
+    from mythril_amd import solver as SV
+
+    qs = _queries(["calls", "returnvalue", "etherstore"])
+    ans, _ = E.suite_answers(qs, witnesses=True)
+    sat = [k for k, a in enumerate(ans) if a == "sat"]
+    assert len(sat) > 100
+    B = F.Batch([list(qs[k][3]) for k in sat])
+    packed = B.packed()[:4]
+    plain = N.refute(*packed)
+    split = N.refute_split(*packed, max_splits=SV.Prefilter.SPLIT_REFUTE, depth=SV.Prefilter.SPLIT_DEPTH)
+    B.close()
+    bad = [qs[k][2] for k, p, r in zip(sat, plain, split) if p == 1 or r == 1]
+    assert not bad, bad[:5]
+    acc = corpus.account(qs, ans)
+    assert acc["all"]["refuted_with_sat_expectation_if_reachable"] == 0, acc["all"]
+    assert acc["all"]["contradicted"] == 0 and acc["all"]["sat_expectations_dropped"] == 0, acc["all"]

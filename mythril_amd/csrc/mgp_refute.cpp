@@ -858,6 +858,179 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
   return d.run(max_passes ? max_passes : 16u);
 }
 
+// Linear forms (round 6).  Under the analysis' decided select conditions and exact values,
+// every BV node of width <= 256 gets a linear form sum(coef * atom) + k mod 2^w over atoms:
+// variables, UF applications keyed by (function, exact argument) -- congruent applications
+// share one atom -- and any other node as itself.  A required compare whose two operands'
+// forms differ by a constant k (a = b + k) is then a condition on b alone: a >u b iff
+// k != 0 and b + k does not wrap (b <= 2^w-1-k); a == b iff k == 0.  Balance arithmetic
+// across a transfer is such a case: ether_thief.py:55-95 compares the attacker's balance
+// after (start - value) + refund with start, and refund = value - price cancels value
+// (weak_random.sol:18-35), which intervals cannot see.  Each derived condition is an
+// equivalence, so meeting it is sound.  true = refuted.
+namespace lin {
+constexpr uint32_t kMax = 6;
+struct Form {
+  uint8_t n = 0;
+  bool ok = true;  // false: more atoms than kMax (the node is its own atom instead)
+  uint64_t atom[kMax];
+  V coef[kMax];
+  V k;
+};
+inline uint64_t mix(uint64_t a, uint64_t b) {
+  uint64_t z = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull + (a << 6) + (a >> 2));
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  return z ^ (z >> 31);
+}
+inline Form of_const(const V &k) {
+  Form f;
+  f.k = k;
+  return f;
+}
+inline Form of_atom(uint64_t a) {
+  Form f;
+  f.k = bv_zero();
+  f.n = 1;
+  f.atom[0] = a;
+  f.coef[0] = bv_small(1u);
+  return f;
+}
+// r = x + s * y (mod 2^w); false if the atoms do not fit
+inline bool axpy(Form &r, const Form &x, const V &sc, const Form &y, uint32_t w) {
+  r = x;
+  r.k = bv_mask(ADDV(x.k, bv_mul(sc, y.k)), w);
+  for (uint32_t j = 0; j < y.n; ++j) {
+    const V c = bv_mask(bv_mul(sc, y.coef[j]), w);
+    uint32_t t = 0;
+    while (t < r.n && r.atom[t] != y.atom[j]) ++t;
+    if (t == r.n) {
+      if (r.n == kMax) return false;
+      r.atom[r.n] = y.atom[j];
+      r.coef[r.n++] = c;
+    } else {
+      r.coef[t] = bv_mask(ADDV(r.coef[t], c), w);
+    }
+  }
+  uint32_t o = 0;  // drop cancelled atoms
+  for (uint32_t t = 0; t < r.n; ++t)
+    if (!Z(r.coef[t])) {
+      r.atom[o] = r.atom[t];
+      r.coef[o++] = r.coef[t];
+    }
+  r.n = (uint8_t)o;
+  return true;
+}
+}  // namespace lin
+
+bool linear_refute(State &s, Dom &d, uint32_t passes) {
+  using lin::Form;
+  const uint32_t n = s.n;
+  std::vector<Form> F(n);
+  const V minus1 = bv_ones();
+  for (int round = 0; round < 3; ++round) {
+    for (uint32_t i = 0; i < n; ++i) {
+      const mgp_node &x = s.nd[i];
+      const uint32_t w = x.width;
+      Form &f = F[i];
+      f = Form();
+      if (s.isb[i] || w == 0u || w > 256u) continue;
+      const AV &a = s.av[i];
+      if (is_exact(a)) {
+        f = lin::of_const(a.lo);
+        continue;
+      }
+      const uint64_t self = lin::mix(0x4E4F4445ull, i);
+      auto ok_bv = [&](int32_t j) { return j >= 0 && !s.isb[j] && s.nd[j].width == w; };
+      bool done = false;
+      switch (x.op) {
+        case MGP_OP_VAR:
+          f = lin::of_atom(lin::mix(0x564152ull, ((uint64_t)x.p0 << 16) | w));
+          done = true;
+          break;
+        case MGP_OP_UFAPP: case MGP_OP_UFINV:
+          if (x.a >= 0 && s.nd[x.a].width <= 256u && is_exact(s.av[x.a])) {
+            uint64_t h = lin::mix(0x5546ull + x.op, ((uint64_t)x.p0 << 16) | w);
+            for (int l = 0; l < 8; ++l) h = lin::mix(h, s.av[x.a].lo.w[l]);
+            f = lin::of_atom(h);
+            done = true;
+          }
+          break;
+        case MGP_OP_ADD: case MGP_OP_SUB:
+          if (ok_bv(x.a) && ok_bv(x.b) && F[x.a].ok && F[x.b].ok)
+            done = lin::axpy(f, F[x.a], x.op == MGP_OP_ADD ? bv_small(1u) : minus1, F[x.b], w);
+          break;
+        case MGP_OP_NEG:
+          if (ok_bv(x.a) && F[x.a].ok) done = lin::axpy(f, lin::of_const(bv_zero()), minus1, F[x.a], w);
+          break;
+        case MGP_OP_MUL:
+          if (ok_bv(x.a) && ok_bv(x.b)) {
+            if (is_exact(s.av[x.a]) && F[x.b].ok) done = lin::axpy(f, lin::of_const(bv_zero()), s.av[x.a].lo, F[x.b], w);
+            else if (is_exact(s.av[x.b]) && F[x.a].ok) done = lin::axpy(f, lin::of_const(bv_zero()), s.av[x.b].lo, F[x.a], w);
+          }
+          break;
+        case MGP_OP_ITE:
+          if (x.a >= 0 && s.bs[x.a] != BB) {
+            const int32_t br = s.bs[x.a] == BT ? x.b : x.c;
+            if (ok_bv(br) && F[br].ok) {
+              f = F[br];
+              done = true;
+            }
+          }
+          break;
+        default:
+          break;
+      }
+      if (!done) f = lin::of_atom(self);
+    }
+    // the required compares whose operands differ by a constant
+    bool narrowed = false;
+    for (uint32_t i = 0; i < n; ++i) {
+      const mgp_node &x = s.nd[i];
+      if (x.op != MGP_OP_EQ && x.op != MGP_OP_ULT && x.op != MGP_OP_ULE && x.op != MGP_OP_UGT && x.op != MGP_OP_UGE)
+        continue;
+      if (s.bs[i] == BB || x.a < 0 || x.b < 0 || s.isb[x.a]) continue;
+      const uint32_t w = s.nd[x.a].width;
+      if (w == 0u || w > 256u || s.nd[x.b].width != w) continue;
+      Form dlt;
+      if (!lin::axpy(dlt, F[x.a], minus1, F[x.b], w) || dlt.n != 0) continue;
+      const V k = bv_mask(dlt.k, w);  // a = b + k
+      bool truth = s.bs[i] == BT;
+      if (x.op == MGP_OP_EQ) {
+        if (Z(k) != truth) return true;
+        continue;
+      }
+      // normalise to "a >u b" (UGT) or "a >=u b" (UGE) with the required truth
+      bool strict = x.op == MGP_OP_UGT || x.op == MGP_OP_ULE;
+      if (x.op == MGP_OP_ULT || x.op == MGP_OP_ULE) truth = !truth;  // ULT = !UGE, ULE = !UGT
+      if (Z(k)) {  // a == b: UGT false, UGE true
+        if (truth == strict) return true;
+        continue;
+      }
+      // k != 0: a >u b and a >=u b both hold iff b <= 2^w-1-k
+      const V lim = SUBV(M(w), k);
+      AV t = top(w);
+      if (truth) t.hi = lim;
+      else t.lo = ADDV(lim, ONE());
+      // on b and on every node whose form is exactly b's (a congruent UF application)
+      for (uint32_t j = 0; j < n; ++j) {
+        if (j != (uint32_t)x.b) {
+          const Form &g = F[j], &h = F[x.b];
+          if (s.isb[j] || s.nd[j].width != w || g.n != h.n || !EQV(g.k, h.k)) continue;
+          bool same = true;
+          for (uint32_t q = 0; q < g.n && same; ++q) same = g.atom[q] == h.atom[q] && EQV(g.coef[q], h.coef[q]);
+          if (!same) continue;
+        }
+        const AV before = s.av[j];
+        if (!d.meet((int32_t)j, t)) return true;
+        narrowed |= !(EQV(before.lo, s.av[j].lo) && EQV(before.hi, s.av[j].hi));
+      }
+    }
+    if (!narrowed) return false;
+    if (d.run(passes) == 1) return true;
+  }
+  return false;
+}
+
 // refute_one, then case splitting (failed-literal probing, nested): each open condition of
 // a select (BV ITE / BITE), nearest the root first, at most max_splits of them, is assumed
 // true and false in turn on a copy of the analysis, and each branch is probed again on the
@@ -867,7 +1040,7 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
 int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t n_consts, uint32_t max_passes,
                      uint32_t max_splits) {
   // max_splits: atoms per level in bits 0..15, levels in bits 16..19 (0 = 1), bit 20 set =
-  // no interval bisection
+  // no linear forms and no interval bisection (the round-6 stages)
   const uint32_t n_atoms = max_splits & 0xFFFFu, depth = std::max<uint32_t>(1u, (max_splits >> 16) & 0xFu);
   const bool bisection = ((max_splits >> 20) & 1u) == 0u;
   State s;
@@ -913,9 +1086,14 @@ int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uin
       if (s.bs[a] != BB) continue;
       if (runs_left <= 0) return false;
       take(c);
-      const bool rt = !d.meetb(a, BT) || run_capped() == 1 || probe(level - 1);
+      // (each branch also gets the linear-form pass: a select condition decided by the
+      // branch -- sender == ATTACKER in an earlier transaction -- resolves the balance
+      // selects whose forms then cancel)
+      const bool rt = !d.meetb(a, BT) || run_capped() == 1 || (bisection && linear_refute(s, d, passes)) ||
+                      probe(level - 1);
       put(c);
-      const bool rf = !d.meetb(a, BF) || run_capped() == 1 || probe(level - 1);
+      const bool rf = !d.meetb(a, BF) || run_capped() == 1 || (bisection && linear_refute(s, d, passes)) ||
+                      probe(level - 1);
       put(c);
       if (rt && rf) return true;
       if (rt || rf) {  // the other polarity holds in every model of this branch
@@ -926,6 +1104,7 @@ int refute_split_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uin
   };
   if (probe(depth)) return 1;
   if (!bisection) return 0;
+  if (linear_refute(s, d, passes)) return 1;
   // Interval bisection (round 6): a variable whose interval the analysis bounded (a call
   // value between two require()s, a balance below a cap) is split in two halves, each
   // half propagated and split again, kBisectDepth levels; every leaf refuted -> refuted.

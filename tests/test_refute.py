@@ -1123,6 +1123,53 @@ def test_bisection_exhaustive_soundness():
     assert int((withb == 1).sum()) == n_unsat, (int((withb == 1).sum()), n_unsat)
 
 
+def _refund_state(rng, w=3):
+    """A balance after a payment and a refund compared with the starting balance, over
+    applications of one balance function at a symbolic sender and at a constant address
+    (weak_random.sol:18-35 / ether_thief.py:55-95 in small): the sender pays v, gets back
+    v - p (or v, or v + p) and the attacker's balance is compared with its start."""
+    nl = [[S.VAR, w, -1, -1, -1, k, 0] for k in range(2)]                          # 0 sender, 1 value
+    cl = [int(x) for x in rng.integers(0, 1 << w, size=2)]
+    nl += [[S.CONST, w, -1, -1, -1, k, 0] for k in range(2)]                       # 2 attacker, 3 price
+    nl.append([S.UFAPP, w, 0, -1, -1, 9, 2])                                       # 4 bal(sender)
+    nl.append([S.UFAPP, w, 2, -1, -1, 9, 3])                                       # 5 bal(attacker)
+    nl.append([S.SUB, w, 4, 1, -1, 0, 0])                                          # 6 bal - v
+    refund = int(rng.integers(3))
+    nl.append([[S.SUB, S.ADD, S.ADD][refund], w, 1, 3 if refund < 2 else 1, -1, 0, 0])  # 7 v -/+ p (or v + v)
+    nl.append([S.ADD, w, 6, 7, -1, 0, 0])                                          # 8 after
+    nl.append([S.EQ, 1, 0, 2, -1, 0, 0])                                           # 9 sender == attacker
+    nl.append([S.ITE, w, 9, 8, 5, 0, 0])                                           # 10 attacker's balance
+    nl.append([[S.UGT, S.ULT, S.EQ][int(rng.integers(3))], 1, 10, 5, -1, 0, 0])    # 11 vs start
+    nl.append([S.UGE, 1, 4, 1, -1, 0, 0] if rng.random() < 0.7 else [S.ULT, 1, 1, 4, -1, 0, 0])  # 12
+    nl.append([S.UGE, 1, 1, 3, -1, 0, 0])                                          # 13 v >= p
+    root = 11
+    for extra in (12, 13) + ((9,) if rng.random() < 0.6 else ()):
+        nl.append([S.BAND, 1, root, extra, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl
+
+
+def test_linear_forms_exhaustive_soundness():
+    """The linear-form pass (mgp_refute_split, round 6) on payment-and-refund states: it
+    refutes states the case splits alone leave open, and every refuted state has no model
+    over all 8^4 assignments of its two variables and two application values (C oracle;
+    applications with equal arguments get one value)."""
+    rng = np.random.default_rng(0x11AE)
+    states = [_refund_state(rng) for _ in range(500)]
+    packed = pack_states(states)
+    nob = N.refute_split(*packed, max_splits=8, depth=2, bisect=False)
+    withb = N.refute_split(*packed, max_splits=8, depth=2)
+    assert ((nob == 1) & (withb != 1)).sum() == 0
+    assert int((withb == 1).sum()) > int((nob == 1).sum()), (int((nob == 1).sum()), int((withb == 1).sum()))
+    n_vars = 4
+    grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
+    cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
+    cands[0, :, :, 0] = grid
+    for st, r in zip(states, withb):
+        if r == 1:
+            assert coracle.first_sat(*pack_states([st]), cands)[0] < 0, "linear pass refuted a satisfiable state"
+
+
 def test_refute_split_argument_range():
     """refute_split packs the atom count (bits 0..15) and the depth (bits 16..19) into one
     C argument: values outside them are refused before the call."""

@@ -924,6 +924,24 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     else val[i] = p.size() == 1 ? p[0].r : join(p);
   };
 
+  // (round 6) bits 256.. of a piece list are constant zero: a zero-extended narrow value, a
+  // Concat under zero constant pieces.  Division, right shifts and signed compares of such
+  // values are the 256-bit ops on their low pieces (a zero sign bit makes ASHR a LSHR and a
+  // signed compare an unsigned one); any other wide operand of them stays unsupported.
+  auto high_zero = [&](const Pieces &p) -> bool {
+    uint32_t off = 0;
+    for (const Piece &q : p) {
+      const uint32_t end = off + q.w;
+      if (end > MGP_MAX_WIDTH) {
+        if (q.r.k != R_CONST) return false;
+        const ConstKey &c = S.pool[q.r.idx];
+        for (uint32_t b = off >= MGP_MAX_WIDTH ? 0u : MGP_MAX_WIDTH - off; b < q.w; ++b)
+          if ((c.w[b >> 5] >> (b & 31u)) & 1u) return false;
+      }
+      off = end;
+    }
+    return true;
+  };
   for (uint64_t i = 0; i < n_nodes; ++i) {
     const mgp_node &nd = nodes[i];
     const uint8_t op = nd.op;
@@ -997,6 +1015,26 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
           for (const Piece &q : wide[nd.a]) wide[i].push_back(Piece{S.add(MGP_OP_NOT, (uint16_t)q.w, false, q.r), q.w});
           break;
         }
+        case MGP_OP_UDIV: case MGP_OP_UREM: case MGP_OP_LSHR: case MGP_OP_ASHR: {
+          if (!opnd(nd.a) || !opnd(nd.b) || isb[nd.a] || isb[nd.b] || wid[nd.a] != w || wid[nd.b] != w)
+            return unsupported();
+          const Pieces &pa = wide[nd.a], &pb = wide[nd.b];
+          if (!high_zero(pa) || !high_zero(pb)) return unsupported();
+          const Ref la = join(slice(pa, 0, MGP_MAX_WIDTH)), lb = join(slice(pb, 0, MGP_MAX_WIDTH));
+          wide[i].push_back(Piece{S.add(op == MGP_OP_ASHR ? MGP_OP_LSHR : op, MGP_MAX_WIDTH, false, la, lb),
+                                  MGP_MAX_WIDTH});
+          // a w-bit x / 0 is 2^w - 1 (z3 bvudiv): the high pieces are ones then, else zero
+          Ref by0;
+          if (op == MGP_OP_UDIV) by0 = S.add(MGP_OP_EQ, MGP_MAX_WIDTH, true, lb, const_small(0, MGP_MAX_WIDTH));
+          for (uint32_t off = MGP_MAX_WIDTH; off < w;) {
+            const uint32_t pw = std::min<uint32_t>(MGP_MAX_WIDTH, w - off);
+            const Ref z = const_small(0, pw);
+            wide[i].push_back(Piece{op == MGP_OP_UDIV ? S.add(MGP_OP_ITE, (uint16_t)pw, false, by0, const_ones(pw), z) : z,
+                                    pw});
+            off += pw;
+          }
+          break;
+        }
         case MGP_OP_UFAPP:
         case MGP_OP_UFINV:
           break;  // below, shared with narrow results
@@ -1007,9 +1045,12 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
     }
     // narrow results: a wide operand is only legal where the case below says so
     if (is_wide(nd.a) || is_wide(nd.b) || is_wide(nd.c)) {
+      const bool sgn = op == MGP_OP_SLT || op == MGP_OP_SLE || op == MGP_OP_SGT || op == MGP_OP_SGE;
       const bool ok = op == MGP_OP_EXTRACT || op == MGP_OP_UFAPP || op == MGP_OP_UFINV ||
                       ((op == MGP_OP_EQ || op == MGP_OP_ULT || op == MGP_OP_ULE || op == MGP_OP_UGT ||
-                        op == MGP_OP_UGE) && !isb[nd.a] && !isb[nd.b]);
+                        op == MGP_OP_UGE) && !isb[nd.a] && !isb[nd.b]) ||
+                      (sgn && opnd(nd.a) && opnd(nd.b) && !isb[nd.a] && !isb[nd.b] && wid[nd.a] == wid[nd.b] &&
+                       high_zero(wide[nd.a]) && high_zero(wide[nd.b]));
       if (!ok) return unsupported();
     }
     switch (op) {
@@ -1103,6 +1144,11 @@ Lowered lower_one(const mgp_node *nodes, uint64_t n_nodes, const uint32_t *const
             case MGP_OP_UGT: val[i] = ult_pieces(y, x); break;
             case MGP_OP_ULE: val[i] = S.add(MGP_OP_BNOT, 1, true, ult_pieces(y, x)); break;
             case MGP_OP_UGE: val[i] = S.add(MGP_OP_BNOT, 1, true, ult_pieces(x, y)); break;
+            // signed compares of zero-extended values (checked above): the unsigned ones
+            case MGP_OP_SLT: val[i] = ult_pieces(x, y); break;
+            case MGP_OP_SGT: val[i] = ult_pieces(y, x); break;
+            case MGP_OP_SLE: val[i] = S.add(MGP_OP_BNOT, 1, true, ult_pieces(y, x)); break;
+            case MGP_OP_SGE: val[i] = S.add(MGP_OP_BNOT, 1, true, ult_pieces(x, y)); break;
             default: return unsupported();
           }
           break;

@@ -179,6 +179,21 @@ def test_wide_values_parity(mgp_ctx):
     assert 0 in want and -1 in want
 
 
+def test_wide_zext_division_shift_signed_parity(mgp_ctx):
+    """257..776-bit zero-extended UDIV / UREM / LSHR / ASHR and signed compares (round 6;
+    CREATE2's salt-padded 776-bit preimage shape, instructions.py:1707-1721): first-SAT over
+    each state's candidate rows vs oracle.bvsem, x / 0 included."""
+    from .test_lowering import wide_zext_cases
+    states, rows = wide_zext_cases()
+    nodes, noff, consts, coff = pack_states(states)
+    words, po, status = _lower(nodes, noff, consts, coff)
+    assert (status == 0).all()
+    first, _ = mgp_ctx.eval_batch(words, po, cands_from_ints(rows))
+    want = [S.first_sat(nl, cl, r) for (nl, cl), r in zip(states, rows)]
+    assert list(first) == want
+    assert any(x >= 0 for x in want) and any(x < 0 for x in want)
+
+
 def test_wide_arith_parity(mgp_ctx):
     """257..776-bit ADD / SUB carry chains, bitwise ops and unsigned compares: first-SAT
     over each state's candidate rows vs the oracle."""

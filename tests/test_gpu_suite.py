@@ -39,7 +39,7 @@ pytestmark = pytest.mark.gpu
 # mgp_refute decided); the ceilings only move down as the pre-filter decides more
 CEILING = {"suicide": 1, "bectoken": 5, "wallet": 9, "calls": 13, "etherstore": 9, "exceptions": 4,
            "hashforether": 1, "origin": 1, "returnvalue": 1, "rubixi": 24, "timelock": 6, "token": 2,
-           "weak_random": 42}
+           "weak_random": 8}
 
 
 def _limbs(vals, n_vars):

@@ -333,6 +333,64 @@ def test_wide_ops_left_unsupported():
         assert status[0] == N.ST_UNSUPPORTED, op
 
 
+def wide_zext_cases():
+    """UDIV / UREM / LSHR / ASHR and signed compares on 257..776-bit values whose bits from
+    256 up are zero (round 6): ZeroExt of a 256-bit variable, or Concat(0, x) -- the salt
+    padding of CREATE2's 776-bit preimage (instructions.py:1707-1721) -- against a divisor /
+    shift amount that is zero, one, small, the dividend or anything, with the result's low
+    and high halves checked.  -> (states, candidate rows)."""
+    states, rows = [], []
+    rng = np.random.default_rng(0x776)
+    edge = [0, 1, 2, 255, 256, 257, 775, 776, (1 << 256) - 1, 1 << 255, 5]
+    for w in (257, 300, 512, 776):
+        for op in (S.UDIV, S.UREM, S.LSHR, S.ASHR, S.SLT, S.SLE, S.SGT, S.SGE):
+            for shape in range(2):
+                nl = [[S.VAR, 256, -1, -1, -1, k, 0] for k in range(4)]                      # 0..3
+                nl.append([S.CONST, w - 256, -1, -1, -1, 0, 0])                               # 4: zero pad
+                nl.append([S.CONCAT, w, 4, 0, -1, 0, 0] if shape else [S.ZEXT, w, 0, -1, -1, 0, 0])  # 5: a
+                nl.append([S.ZEXT, w, 1, -1, -1, 0, 0])                                       # 6: b
+                if op in (S.SLT, S.SLE, S.SGT, S.SGE):
+                    nl.append([op, 1, 5, 6, -1, 0, 0])                                        # 7
+                    nl.append([S.EQ, 1, 2, 3, -1, 0, 0])                                      # 8
+                    nl.append([S.BXOR, 1, 7, 8, -1, 0, 0])                                    # 9
+                else:
+                    nl.append([op, w, 5, 6, -1, 0, 0])                                        # 7: r
+                    nl.append([S.EXTRACT, 256, 7, -1, -1, 255, 0])                            # 8: low
+                    nl.append([S.EXTRACT, w - 256, 7, -1, -1, w - 1, 256])                    # 9: high
+                    nl.append([S.ZEXT, 256, 9, -1, -1, 0, 0] if w - 256 < 256 else [S.EXTRACT, 256, 9, -1, -1, 255, 0])  # 10
+                    nl.append([S.EQ, 1, 8, 2, -1, 0, 0])                                      # 11
+                    nl.append([S.ULT, 1, 10, 3, -1, 0, 0])                                    # 12
+                    nl.append([S.BAND, 1, 11, 12, -1, 0, 0])                                  # 13
+                states.append((nl, [0, 0, 0]))
+                r = []
+                for _ in range(8):
+                    xs = [edge[int(rng.integers(0, len(edge)))] if rng.random() < 0.5 else
+                          int(rng.integers(0, 2 ** 62)) << int(rng.integers(0, 194)) for _ in range(4)]
+                    r.append(xs)
+                # make the root true on some rows: the low result and a bound above the high half
+                for xs in list(r[:4]):
+                    vals = S.eval_dag(nl, [0, 0, 0], xs)
+                    ys = list(xs)
+                    if op in (S.SLT, S.SLE, S.SGT, S.SGE):
+                        ys[3] = ys[2] if not vals[7] else ys[2] ^ 1
+                    else:
+                        ys[2] = vals[8]
+                        ys[3] = (vals[10] + 1) & ((1 << 256) - 1)
+                    r.append(ys)
+                rows.append(r)
+    return states, rows
+
+
+def test_wide_zero_extended_division_shifts_signed():
+    """Wide zero-extended division, right shifts and signed compares lower (round 6) and
+    match the DAG semantics (oracle.bvsem) in the bytecode and uop reference interpreters,
+    x / 0 = 2^w - 1 in the high pieces included."""
+    states, rows = wide_zext_cases()
+    _, _, status = _check_states(states, rows)
+    assert (status == 0).all()
+    assert sum(S.eval_root(nl, cl, xs) for (nl, cl), r in zip(states, rows) for xs in r) > 100
+
+
 def test_wide_mul_no_overflow_expansion():
     # z3's expansion of BVMulNoOverflow(a, b, False) (bitvec_helper.py:188-199):
     # Extract(511, 256, ZeroExt(256, a) * ZeroExt(256, b)) == 0, against UMUL_NOOVF itself

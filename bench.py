@@ -568,6 +568,26 @@ def main():
                              "same_answers": [r[0] for r in res_c] == kinds, "stages_ms": pf.last_profile}
         pf.cand_bytes = keep_cb
         pf.ctx.close()
+        # two pipelines on the one GPU (Prefilter(pipelines=2)): the batch hash-sharded over two
+        # contexts, each on its own host thread with half the OpenMP threads, so that one
+        # shard's GPU round overlaps the other's host stages; GPU busy =
+        # the sum of the two shards' GPU waits and launch stages over the call's wall time
+        pf2 = SV.Prefilter(devices=[local], pipelines=2)
+        pf2.check_states(cs[:256])
+        p2 = []
+        for rep in range(3):
+            SV.unsat_cores().reset()
+            pf2._N.program_cache_clear()
+            tf = time.perf_counter()
+            res2 = pf2.check_states(cs)
+            p2.append((time.perf_counter() - tf, [r[0] for r in res2], pf2.last_profile))
+        pf2.close()
+        med2 = sorted(p2, key=lambda c: c[0])[1]
+        frontend["pipelines2"] = {"seconds": med2[0], "states_per_s": len(cs) / med2[0],
+                                  "calls_seconds": [round(c[0], 4) for c in p2],
+                                  "same_answers": all(c[1] == kinds for c in p2), "stages_ms": med2[2]}
+        if not frontend["pipelines2"]["same_answers"]:
+            raise RuntimeError("front end: two pipelines gave other answers than one")
         log(f"frontend: {frontend}")
 
     # ------------------------------------ the 13 solidity_examples contracts (configs 1, 2, 4 + 10 more)
@@ -763,6 +783,9 @@ def headline(line: dict, detail_path) -> dict:
                                          "undecided", "solver_call_reduction")),
                             "contradicted": fe["expectations"]["contradicted"],
                             "gpu_wait_ms": fe["stages_ms"].get("gpu_wait_ms"),
+                            **({"pipelines2_seconds": fe["pipelines2"]["seconds"],
+                                "pipelines2_states_per_s": fe["pipelines2"]["states_per_s"]}
+                               if "pipelines2" in fe else {}),
                             "latency_ms": {str(r["states"]): round(r["ms_per_call"], 3) for r in fe["latency"]}}
     pf = line.get("prefilter")
     if pf is not None:

@@ -401,15 +401,25 @@ class Prefilter:
     # batch go up through it: WalletLibrary's lowered programs are ~0.45 MB each)
     HOST_STAGING = 256 << 20
 
+    # pipelines > 1: that many contexts per device, each with its own host thread and a share
+    # of the OpenMP threads; a batch of at least PIPELINE_MIN states is hash-sharded over them
+    # (as over devices), so one shard's GPU rounds run while another's host stages (DAG build,
+    # decision rows, lowering, pre-check) run -- the answers are the single pipeline's, every
+    # state's being a function of its content
+    PIPELINE_MIN = 128
+
     def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,
-                 devices: Optional[Sequence[int]] = None):
+                 devices: Optional[Sequence[int]] = None, pipelines: int = 1):
         from . import _native as N
 
         self._N = N
         self.devices = list(devices) if devices is not None else [device]
         if not self.devices:
             raise ValueError("Prefilter needs at least one device")
-        self.ctxs = [N.Context(d) for d in self.devices]
+        if pipelines < 1:
+            raise ValueError("Prefilter needs at least one pipeline per device")
+        self.pipelines = pipelines
+        self.ctxs = [N.Context(d) for d in self.devices for _ in range(pipelines)]
         self.ctx = self.ctxs[0]
         self.n_cand = n_cand
         self.seed = seed
@@ -442,6 +452,7 @@ class Prefilter:
         # the host idle between calls: back to back, its OpenMP team competes with the next
         # call's (the bench's first-round pass fell from 3 850 to 2 680 states/s with it on)
         self.core_async = False
+        self._tls = threading.local()  # per-thread stage profile (sharded batches)
         self.last_times = None     # mgp_check_batch stage times (ms) of the last batch
         self.last_profile = None   # host + GPU stage split of the last batch (bench frontend_latency)
 
@@ -469,7 +480,7 @@ class Prefilter:
             rest_par = None if parents is None else [p for p, h in zip(parents, hit) if not h]
             sub = iter(self.check_states(rest, rest_par) if rest else [])
             return [(unsat, None) if h else next(sub) for h in hit]
-        if len(self.ctxs) > 1 and len(states) > 1:
+        if len(self.ctxs) > 1 and len(states) > 1 and (len(self.devices) > 1 or len(states) >= self.PIPELINE_MIN):
             out, refuted = self._check_sharded(states, parents)
         else:
             out, refuted = self._check_native(self.ctx, states, parents)
@@ -504,13 +515,22 @@ class Prefilter:
         owner = self.shard(states)
         parts = [np.nonzero(owner == g)[0] for g in range(len(self.ctxs))]
         results: List = [None] * len(self.ctxs)
+        profs: List = [None] * len(self.ctxs)
         errors: List = []
+        # several pipelines on one host: each thread's OpenMP team gets its share of the cores
+        # (one full team per thread oversubscribes them)
+        lib = self._N.lib()
+        share = max(1, lib.mgp_set_thread_omp(0) * len(self.devices) // len(self.ctxs)) \
+            if self.pipelines > 1 else 0
 
         def work(g):
             idx = parts[g]
             try:
+                if share:
+                    lib.mgp_set_thread_omp(share)
                 results[g] = self._check_native(self.ctxs[g], [states[i] for i in idx],
                                                 None if parents is None else [parents[i] for i in idx])
+                profs[g] = getattr(self._tls, "profile", None)
             except BaseException as e:  # re-raised on the caller's thread
                 errors.append(e)
 
@@ -522,6 +542,7 @@ class Prefilter:
             t.join()
         if errors:
             raise errors[0]
+        self.last_profile = dict(_sum_profiles([p for p in profs if p]), shards=sum(1 for p in parts if len(p)))
         out: List = [None] * len(states)
         refuted: List[int] = []
         for g, idx in enumerate(parts):
@@ -556,8 +577,8 @@ class Prefilter:
                 for k, r in zip(grp, sub):
                     res[k] = r
                 refuted.extend(grp[k] for k in sub_ref)
-                profs.append(self.last_profile or {})
-            self.last_profile = _sum_profiles(profs)
+                profs.append(getattr(self._tls, "profile", None) or {})
+            self.last_profile = self._tls.profile = _sum_profiles(profs)
             return res, sorted(refuted)
         prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
         td = time.perf_counter()
@@ -608,6 +629,7 @@ class Prefilter:
         prof["results_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["cores_ms"] = 0.0
         self.last_profile = prof
+        self._tls.profile = prof
         return out, refuted
 
     def flush_cores(self) -> None:

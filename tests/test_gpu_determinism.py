@@ -104,6 +104,26 @@ def test_two_contexts_answer_like_one(clean):
         two.close()
 
 
+def test_two_pipelines_answer_like_one(clean):
+    """Prefilter(pipelines=2): two contexts on one GPU with half the OpenMP threads each, a
+    batch of >= PIPELINE_MIN states hash-sharded over them, a smaller one on the first --
+    the same answers and witnesses as one pipeline, both ways."""
+    one, two = SV.Prefilter(0), SV.Prefilter(0, pipelines=2)
+    try:
+        assert len(two.ctxs) == 2
+        for n in (300, 40):
+            cs = [c[1] for c in _corpus(n)]
+            SV.unsat_cores().reset()
+            a = one.check_states(cs)
+            SV.unsat_cores().reset()
+            b = two.check_states(cs)
+            _same_answers(a, b)
+            assert (two.last_profile or {}).get("shards", 1) == (2 if n >= two.PIPELINE_MIN else 1)
+    finally:
+        one.close()
+        two.close()
+
+
 def test_corpus_undecided_equals_cpu_restatement(clean):
     """The 1024-state mixed corpus through the product Prefilter (two rounds, decision rows)
     leaves exactly the states the CPU restatement of the same rounds leaves."""

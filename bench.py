@@ -631,14 +631,24 @@ def main():
         finally:
             SB.close()
         SV.unsat_cores().flush(N)
+        # ... and every refutation audited by a wider witness search (1 024 candidates per state
+        # from another seed, no pre-check): a model it finds would make that refutation unsound
+        unsat_idx = [k for k, a in enumerate(answers) if a == "unsat"]
+        auditor = SV.Prefilter(device=local, n_cand=1024, seed=0xA0D17)
+        auditor.refute, auditor.retry_cand, auditor.rows_first_nodes, auditor.split_refute = False, 0, 0, 0
+        audit = auditor.check_states([list(qs[k][3]) for k in unsat_idx]) if unsat_idx else []
+        auditor.close()
         soundness = {"witnessed": len(sat_idx), "refuted_plain": int((r_plain == 1).sum()),
+                     "refutations_audited": len(unsat_idx), "audit_candidates": 1024,
+                     "audit_models_found": sum(1 for a, _ in audit if a == "sat"),
                      "refuted_split": int((r_split == 1).sum()),
                      "core_covered": int(sum(SV.unsat_cores().covered(qs[k][3]) for k in sat_idx)),
                      **{f: acc["all"][f] for f in ("sat_if_reachable", "refuted_with_sat_expectation_if_reachable",
                                                    "sat_expectations_dropped")},
                      "seconds": time.perf_counter() - ts}
         log(f"suite soundness: {soundness}")
-        if soundness["refuted_plain"] or soundness["refuted_split"] or soundness["core_covered"]:
+        if (soundness["refuted_plain"] or soundness["refuted_split"] or soundness["core_covered"]
+                or soundness["audit_models_found"]):
             raise RuntimeError(f"the refuter claims UNSAT for witnessed suite queries: {soundness}")
         suite = dict(acc, queries=len(qs), seconds=dt_all, queries_per_s=len(qs) / dt_all, generate_s=gen_s,
                      soundness=soundness,

@@ -17,7 +17,9 @@ Per contract it checks:
   query that got a GPU witness -- a model, checked above -- is refuted by mgp_refute, by
   mgp_refute_split at the product's settings (case splits + interval bisection), or covered
   by a stored UNSAT core; and no refuted query whose "sat" expectation holds once its state
-  is reachable lacks a refuted ancestor (corpus.account counts that as a contradiction).
+  is reachable lacks a refuted ancestor (corpus.account counts that as a contradiction);
+* every refutation is audited by a wider witness search (AUDIT_CAND candidates per state from
+  another seed, no pre-check): it must find no model.
 
 Issue-level parity with the reference stays unpinned."""
 import numpy as np
@@ -88,6 +90,32 @@ def refuted_witnessed(qs, sat):
             for k, p, r in zip(sat, plain, split) if p == 1 or r == 1 or cores.covered(qs[k][3])]
 
 
+def audit_refutations(auditor, qs, answers):
+    """Labels of refuted queries (answer "unsat") for which a wider GPU witness search -- AUDIT_CAND
+    candidates per state from another seed, no pre-check -- finds a model: a refutation the
+    search contradicts is unsound.  Evidence by search, not a proof; it covers every UNSAT
+    claim of the suite (a SAT claim gets a witness check, an UNSAT claim none)."""
+    idx = [k for k, a in enumerate(answers) if a == "unsat"]
+    if not idx:
+        return [], 0
+    res = auditor.check_states([list(qs[k][3]) for k in idx])
+    return [qs[k][2] for k, (a, _) in zip(idx, res) if a == "sat"], len(idx)
+
+
+AUDIT_CAND = 1024
+
+
+@pytest.fixture(scope="module")
+def auditor(mgp_ctx):
+    a = SV.Prefilter(device=0, n_cand=AUDIT_CAND, seed=0xA0D17)
+    a.refute = False          # the search alone: a witness or nothing
+    a.retry_cand = 0
+    a.rows_first_nodes = 0
+    a.split_refute = 0
+    yield a
+    a.close()
+
+
 @pytest.fixture(scope="module")
 def prefilter(mgp_ctx):
     SV.enable_gpu(True)
@@ -97,7 +125,7 @@ def prefilter(mgp_ctx):
 
 
 @pytest.mark.parametrize("name", [c.name for c in C.ALL])
-def test_suite_contract_witnesses_and_calls(prefilter, name):
+def test_suite_contract_witnesses_and_calls(prefilter, auditor, name):
     qs = corpus.suite(contracts={name})
     assert qs and all(q[0] == name for q in qs)
     SV.unsat_cores().reset()
@@ -112,6 +140,9 @@ def test_suite_contract_witnesses_and_calls(prefilter, name):
     unsound = refuted_witnessed(qs, sat)
     assert not unsound, f"refuter claims UNSAT for {len(unsound)} witnessed queries: {unsound[:5]}"
     assert c["refuted_with_sat_expectation_if_reachable"] == 0, c
-    print(f"{name}: {len(qs)} queries, {len(sat)} GPU witnesses checked, z3 calls {c['z3_calls']} "
+    found, n_refuted = audit_refutations(auditor, qs, answers)
+    assert not found, f"a wider witness search finds models for {len(found)} refuted queries: {found[:5]}"
+    print(f"{name}: {len(qs)} queries, {len(sat)} GPU witnesses checked, {n_refuted} refutations audited, "
+          f"z3 calls {c['z3_calls']} "
           f"of {c['ref_calls']} restated reference calls ({c['by_kind']})")
     assert c["z3_calls"] <= CEILING[name], c

@@ -534,7 +534,7 @@ class Prefilter:
             except BaseException as e:  # re-raised on the caller's thread
                 errors.append(e)
 
-        threads = [threading.Thread(target=work, args=(g,), name=f"mgp-dev{self.devices[g]}")
+        threads = [threading.Thread(target=work, args=(g,), name=f"mgp-ctx{g}")
                    for g in range(len(self.ctxs)) if len(parts[g])]
         for t in threads:
             t.start()

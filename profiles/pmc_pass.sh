@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_${TAG}
 mkdir -p "$OUT"
-ARGS="--states ${PROF_STATES:-262144} --steps 2 --warmup 1 --keccak 0 --no-cpu --refute-sample 0 --frontend 0"
+ARGS="--states ${PROF_STATES:-262144} --steps 2 --warmup 1 --keccak 0 --no-cpu --refute-sample 0 --frontend 0 --suite 0 --suite-open-sweep 0 --div-split 0 --guided-sample 0"
 timeout -s KILL 150 rocprofv3 --pmc $COUNTERS -d "$OUT/pmc" -o run --output-format csv -- \
     python3 bench.py $ARGS > "$OUT/bench.json" 2> "$OUT/bench.err"
 python3 - "$OUT" <<'PY'

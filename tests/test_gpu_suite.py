@@ -124,6 +124,17 @@ def prefilter(mgp_ctx):
     pf.ctx.close()
 
 
+# The issues SURVEY §8d expects by reading for the three `myth analyze` configs, as the txseq
+# query of the module that reports them: the product must answer at least one of them with a
+# GPU witness (the state exists, so the reference's z3 call finds its transaction sequence and
+# the issue is reported by both), and refute none that reading calls sat.
+CONFIG_ISSUES = {
+    "suicide": ["suicide:suicide@kill:selfdestruct"],                  # config 1: SWC-106 in kill(address)
+    "bectoken": ["bectoken:overflow_issue@batchTransfer:mul"],         # config 2: SWC-101 in batchTransfer
+    "wallet": ["wallet:suicide_attacker@kill:selfdestruct"],           # config 4: SWC-106 via initWallet -> kill
+}
+
+
 @pytest.mark.parametrize("name", [c.name for c in C.ALL])
 def test_suite_contract_witnesses_and_calls(prefilter, auditor, name):
     qs = corpus.suite(contracts={name})
@@ -140,6 +151,9 @@ def test_suite_contract_witnesses_and_calls(prefilter, auditor, name):
     unsound = refuted_witnessed(qs, sat)
     assert not unsound, f"refuter claims UNSAT for {len(unsound)} witnessed queries: {unsound[:5]}"
     assert c["refuted_with_sat_expectation_if_reachable"] == 0, c
+    for lab in CONFIG_ISSUES.get(name, ()):
+        got = [a for q, a in zip(qs, answers) if q[2].startswith(lab)]
+        assert "sat" in got, (lab, got)
     found, n_refuted = audit_refutations(auditor, qs, answers)
     assert not found, f"a wider witness search finds models for {len(found)} refuted queries: {found[:5]}"
     print(f"{name}: {len(qs)} queries, {len(sat)} GPU witnesses checked, {n_refuted} refutations audited, "

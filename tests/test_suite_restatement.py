@@ -76,3 +76,33 @@ def test_no_refutation_of_a_witnessed_query():
     acc = corpus.account(qs, ans)
     assert acc["all"]["refuted_with_sat_expectation_if_reachable"] == 0, acc["all"]
     assert acc["all"]["contradicted"] == 0 and acc["all"]["sat_expectations_dropped"] == 0, acc["all"]
+
+
+def test_refute_cache_matches_the_refuter():
+    """corpus/refute_cache.json (the stream generator's refutations by state content key) was
+    written by the refuter as it is now: its version is the hash of the refuter's sources and
+    settings, and a stale file would make every suite() run (GPU tests, bench) recompute its
+    decisions live.  A sample of its entries must agree with a live mgp_refute_split run."""
+    import json
+
+    from corpus import laser as L
+
+    with open(L._CACHE_PATH) as f:
+        blob = json.load(f)
+    assert blob["version"] == L._refuter_version(), "stale corpus/refute_cache.json: run python -m corpus.laser"
+    assert len(blob["decisions"]) > 1000
+    # live agreement on the queries of two small contracts (keys recomputed from their terms)
+    qs = _queries(["suicide", "origin", "calls"])
+    from mythril_amd.solver import Prefilter
+
+    seen = 0
+    for q in qs:
+        B = F.Batch([list(q[3])])
+        key = f"{int(B.state_key[0]):016x}"
+        if key in blob["decisions"]:
+            live = int(N.refute_split(*B.packed()[:4], max_splits=Prefilter.SPLIT_REFUTE,
+                                      depth=Prefilter.SPLIT_DEPTH)[0]) == 1
+            assert live == bool(blob["decisions"][key]), q[2]
+            seen += 1
+        B.close()
+    assert seen >= 5, seen

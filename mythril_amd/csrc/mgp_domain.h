@@ -369,6 +369,7 @@ constexpr uint32_t kVarBit = 0x80000000u;  // a work-list entry naming a variabl
 constexpr uint32_t kUfGroup = 48;          // UF congruence: functions with at most this many applications
 constexpr int kCongDepth = 4;    // structural congruence: operator levels arg_equal looks through
 constexpr int kChainBudget = 256;  // rel_under steps per pair (Dom::chain_orders)
+constexpr int kChainTotal = 1 << 16;  // rel_under steps per chain_orders call, all pairs
 
 struct Pair { int32_t x, y; uint8_t u, s; };
 struct UfApp { int32_t node, arg; uint32_t fn; uint8_t op; };
@@ -1039,8 +1040,13 @@ struct Dom {
     return r;
   }
   // the pairs whose operand is an open select chain: their orderings from rel_under
+  // (every call also has a total of kChainTotal steps over all its pairs, so a
+  // state with thousands of chain pairs cannot make one tie() unbounded; the corpus never
+  // reaches it -- the suite's refutations are unchanged -- and stopping early only leaves
+  // orderings unknown, which is sound)
   MGP_RD bool chain_orders() {
-    for (uint32_t pj = 0; pj < n_pairs; ++pj) {
+    int total = kChainTotal;
+    for (uint32_t pj = 0; pj < n_pairs && total > 0; ++pj) {
       Pair &p = pairs[pj];
       const bool cx = nd[p.x].op == MGP_OP_ITE && bs[nd[p.x].a] == BB;
       const bool cy = nd[p.y].op == MGP_OP_ITE && bs[nd[p.y].a] == BB;
@@ -1049,9 +1055,11 @@ struct Dom {
       int budget = kChainBudget;
       uint8_t r = OALL;  // each side that is a chain, walked against the other (both sound)
       if (cx) r &= rel_under(p.x, p.y, as, 0, budget);
+      total -= kChainBudget - budget;
       if (cy) {
         budget = kChainBudget;
         r &= mirror_order(rel_under(p.y, p.x, as, 0, budget));
+        total -= kChainBudget - budget;
       }
       MGPD_TRACE("chain pair %d %d: u %u -> rel %u (budget left %d)\n", p.x, p.y, p.u, r, budget);
       if (r != OALL && !set_order(p, 0, r)) return false;

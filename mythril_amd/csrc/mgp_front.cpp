@@ -655,7 +655,9 @@ uint64_t state_key_of(const StateOut &S, const uint64_t *name_hash, uint64_t n_n
   for (const mgp_node &n : S.gpu_nodes) node(n);
   for (uint32_t c : S.consts) h = key_mix(h, c);
   for (size_t v = 0; v < S.var_width.size(); ++v) {
-    h = key_mix(h, nh(S.var_name[v]));
+    // (a pinned constant's slot has no name -- var_name 0 is whatever name the arena interned
+    // first in this process, so hashing it made the key depend on the process' history)
+    h = key_mix(h, S.var_kind[v] == 2u ? 0x50494E4E4544ull : nh(S.var_name[v]));
     h = key_mix(h, ((uint64_t)S.var_width[v] << 40) ^ ((uint64_t)S.var_kind[v] << 32) ^ S.var_aux[v]);
     h = key_mix(h, S.var_full[v]);
   }

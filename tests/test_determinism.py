@@ -151,3 +151,32 @@ def test_row_range_is_a_slice_of_the_full_rows():
     s1, m1, _ = N.decision_rows(*pk, nv, 21, 2, None, state_keys=B.state_key, seeds=seeds, seed_rows=0x3, row0=1)
     assert np.array_equal(s1, sf[:, 1:3]) and np.array_equal(m1, sm[:, 1:3])
     B.close()
+
+
+def test_content_keys_do_not_depend_on_the_process_history():
+    """A state's content key is the same in a process that interned other names first
+    (round 6: a pinned constant's slot hashed the arena's name 0, whatever name that was):
+    two subprocesses build the same calls.sol query, one after creating an unrelated symbol."""
+    import subprocess
+    import sys
+
+    code = (
+        "import sys; sys.path.insert(0, {root!r})\n"
+        "{pre}"
+        "import corpus\n"
+        "from oracle.keccak_ref import keccak256\n"
+        "from mythril_amd import front as F\n"
+        "qs = corpus.suite(hasher=keccak256, contracts={{'calls'}})\n"
+        "keys = []\n"
+        "for q in qs[:60]:\n"
+        "    B = F.Batch([list(q[3])]); keys.append(int(B.state_key[0])); B.close()\n"
+        "print(keys)\n")
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for pre in ("", "from mythril_amd.smt import symbol_factory; _z = symbol_factory.BitVecSym('zz_first', 256)\n"):
+        r = subprocess.run([sys.executable, "-c", code.format(root=root, pre=pre)], capture_output=True, text=True,
+                           timeout=300, check=True)
+        outs.append(r.stdout.strip().splitlines()[-1])
+    assert outs[0] == outs[1]

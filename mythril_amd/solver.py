@@ -405,7 +405,9 @@ class Prefilter:
     # of the OpenMP threads; a batch of at least PIPELINE_MIN states is hash-sharded over them
     # (as over devices), so one shard's GPU rounds run while another's host stages (DAG build,
     # decision rows, lowering, pre-check) run -- the answers are the single pipeline's, every
-    # state's being a function of its content
+    # state's being a function of its content.  Off by default: on a
+    # 16-thread host the two half teams cost more than the overlap hides (the 1 024-state call
+    # 119 -> 221-272 ms, bench frontend.pipelines2)
     PIPELINE_MIN = 128
 
     def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,

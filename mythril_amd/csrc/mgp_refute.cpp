@@ -870,18 +870,16 @@ int refute_one(const mgp_node *nd, uint64_t n, const uint32_t *consts, uint64_t 
 // equivalence, so meeting it is sound.  true = refuted.
 namespace lin {
 constexpr uint32_t kMax = 6;
+// atoms are exact identities, never hashes: a variable (slot, width), or a node index -- the
+// node itself, or for a UF application the first node applying the same function to the
+// same exact argument value
+constexpr uint64_t kVarAtom = 1ull << 62, kNodeAtom = 2ull << 62;
 struct Form {
   uint8_t n = 0;
-  bool ok = true;  // false: more atoms than kMax (the node is its own atom instead)
   uint64_t atom[kMax];
   V coef[kMax];
   V k;
 };
-inline uint64_t mix(uint64_t a, uint64_t b) {
-  uint64_t z = a * 0x9E3779B97F4A7C15ull ^ (b + 0x632BE59BD9B4E019ull + (a << 6) + (a >> 2));
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  return z ^ (z >> 31);
-}
 inline Form of_const(const V &k) {
   Form f;
   f.k = k;
@@ -927,7 +925,15 @@ bool linear_refute(State &s, Dom &d, uint32_t passes) {
   const uint32_t n = s.n;
   std::vector<Form> F(n);
   const V minus1 = bv_ones();
+  struct UfRep {
+    uint8_t op;
+    uint32_t fn, w;
+    V arg;
+    uint32_t node;
+  };
+  std::vector<UfRep> reps;
   for (int round = 0; round < 3; ++round) {
+    reps.clear();
     for (uint32_t i = 0; i < n; ++i) {
       const mgp_node &x = s.nd[i];
       const uint32_t w = x.width;
@@ -939,39 +945,45 @@ bool linear_refute(State &s, Dom &d, uint32_t passes) {
         f = lin::of_const(a.lo);
         continue;
       }
-      const uint64_t self = lin::mix(0x4E4F4445ull, i);
+      const uint64_t self = lin::kNodeAtom | i;
       auto ok_bv = [&](int32_t j) { return j >= 0 && !s.isb[j] && s.nd[j].width == w; };
       bool done = false;
       switch (x.op) {
         case MGP_OP_VAR:
-          f = lin::of_atom(lin::mix(0x564152ull, ((uint64_t)x.p0 << 16) | w));
+          f = lin::of_atom(lin::kVarAtom | ((uint64_t)x.p0 << 16) | w);
           done = true;
           break;
         case MGP_OP_UFAPP: case MGP_OP_UFINV:
           if (x.a >= 0 && s.nd[x.a].width <= 256u && is_exact(s.av[x.a])) {
-            uint64_t h = lin::mix(0x5546ull + x.op, ((uint64_t)x.p0 << 16) | w);
-            for (int l = 0; l < 8; ++l) h = lin::mix(h, s.av[x.a].lo.w[l]);
-            f = lin::of_atom(h);
+            const V &arg = s.av[x.a].lo;
+            uint32_t rep = i;
+            for (const UfRep &r : reps)
+              if (r.op == x.op && r.fn == x.p0 && r.w == w && EQV(r.arg, arg)) {
+                rep = r.node;
+                break;
+              }
+            if (rep == i) reps.push_back(UfRep{x.op, x.p0, w, arg, i});
+            f = lin::of_atom(lin::kNodeAtom | rep);
             done = true;
           }
           break;
         case MGP_OP_ADD: case MGP_OP_SUB:
-          if (ok_bv(x.a) && ok_bv(x.b) && F[x.a].ok && F[x.b].ok)
+          if (ok_bv(x.a) && ok_bv(x.b))
             done = lin::axpy(f, F[x.a], x.op == MGP_OP_ADD ? bv_small(1u) : minus1, F[x.b], w);
           break;
         case MGP_OP_NEG:
-          if (ok_bv(x.a) && F[x.a].ok) done = lin::axpy(f, lin::of_const(bv_zero()), minus1, F[x.a], w);
+          if (ok_bv(x.a)) done = lin::axpy(f, lin::of_const(bv_zero()), minus1, F[x.a], w);
           break;
         case MGP_OP_MUL:
           if (ok_bv(x.a) && ok_bv(x.b)) {
-            if (is_exact(s.av[x.a]) && F[x.b].ok) done = lin::axpy(f, lin::of_const(bv_zero()), s.av[x.a].lo, F[x.b], w);
-            else if (is_exact(s.av[x.b]) && F[x.a].ok) done = lin::axpy(f, lin::of_const(bv_zero()), s.av[x.b].lo, F[x.a], w);
+            if (is_exact(s.av[x.a])) done = lin::axpy(f, lin::of_const(bv_zero()), s.av[x.a].lo, F[x.b], w);
+            else if (is_exact(s.av[x.b])) done = lin::axpy(f, lin::of_const(bv_zero()), s.av[x.b].lo, F[x.a], w);
           }
           break;
         case MGP_OP_ITE:
           if (x.a >= 0 && s.bs[x.a] != BB) {
             const int32_t br = s.bs[x.a] == BT ? x.b : x.c;
-            if (ok_bv(br) && F[br].ok) {
+            if (ok_bv(br)) {
               f = F[br];
               done = true;
             }

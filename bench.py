@@ -430,6 +430,17 @@ def main():
         sat_s, ref_s = first[:ns] >= 0, ver == 1
         if (sat_s & ref_s).any():
             raise RuntimeError("mgp_refute refuted a state with a GPU witness (soundness bug)")
+        # the split refuter (case splits, linear forms, bisection) against the GPU witnesses of
+        # the first 32 768 states: a 256-bit soundness check on random DAGs
+        ns2 = min(ns, 1 << 15)
+        ts2 = time.perf_counter()
+        ver2 = N.refute_split(b["nodes"][: int(b["node_offsets"][ns2])], b["node_offsets"][: ns2 + 1], b["consts"],
+                              b["const_offsets"][: ns2 + 1], max_splits=8, depth=2)
+        split_check = {"states": ns2, "refuted": int((ver2 == 1).sum()),
+                       "refuted_with_gpu_witness": int(((ver2 == 1) & (first[:ns2] >= 0)).sum()),
+                       "seconds": time.perf_counter() - ts2}
+        if split_check["refuted_with_gpu_witness"]:
+            raise RuntimeError(f"mgp_refute_split refuted states with a GPU witness: {split_check}")
         fallback = int(ns - sat_s.sum() - ref_s.sum())
         # second witness round on the states still open: candidates drawn from the pre-check's
         # refined domains, 32 rows by decisions (mgp_guided_candidates), the rest uniform
@@ -458,7 +469,7 @@ def main():
         prefilter = {"sample_states": ns, "gpu_sat": int(sat_s.sum()), "refuted": int(ref_s.sum()),
                      "fallback": fallback, "solver_call_reduction": ns / max(1, fallback),
                      "refute_states_per_s": ns / dtr, "refute_threads": _threads(),
-                     "guided_round": guided,
+                     "guided_round": guided, "split_check": split_check,
                      "note": "synthetic DAGs (random ops), not solidity_examples; reduction = states / states "
                              "left for z3 after GPU witnesses and host refutations (guided_round: after the "
                              "second, domain-guided witness round as well)"}
@@ -806,6 +817,8 @@ def headline(line: dict, detail_path) -> dict:
     pf = line.get("prefilter")
     if pf is not None:
         head["prefilter"] = _pick(pf, ("sample_states", "gpu_sat", "refuted", "fallback", "solver_call_reduction"))
+        if pf.get("split_check"):
+            head["prefilter"]["split_check"] = _pick(pf["split_check"], ("states", "refuted", "refuted_with_gpu_witness"))
     su = line.get("suite")
     if su is not None:
         head["suite"] = {part: _pick(su.get(part), _SUITE_KEYS) for part in ("all", "tuned", "held_out")}

@@ -10,7 +10,8 @@ checks are size-independent properties plus oracle checks on samples:
 * sampled SAT states: the reported witness equals the candidate at first_sat and
   the oracle confirms it satisfies the state; sampled states' first_sat equals the
   oracle's first-SAT scan over all 256 of their device candidates;
-* the host UNSAT pre-check refutes no state that has a GPU witness.
+* the host UNSAT pre-check (plain, and the split refuter on 32 768 states) refutes no state
+  that has a GPU witness.
 """
 import numpy as np
 import pytest
@@ -107,3 +108,10 @@ def test_bench_workload_full_size(mgp_ctx):
     verdict = N.refute(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"])
     assert not ((verdict == 1) & (first >= 0)).any()
     assert (verdict[first < 0] == 1).any()
+    # the split refuter (case splits, linear forms, interval bisection) on the first 32 768
+    # states: no GPU-witnessed state refuted, and more refuted than by the plain analysis
+    k = 1 << 15
+    v2 = N.refute_split(b["nodes"][: int(b["node_offsets"][k])], b["node_offsets"][: k + 1], b["consts"],
+                        b["const_offsets"][: k + 1], max_splits=8, depth=2)
+    assert not ((v2 == 1) & (first[:k] >= 0)).any()
+    assert int((v2 == 1).sum()) > int((verdict[:k] == 1).sum())

@@ -1307,3 +1307,24 @@ def test_exhaustive_soundness_transfer_shapes(w):
             refuted += 1
             assert not has_model, "refuted a satisfiable state"
     assert refuted >= 0.8 * unsat, (refuted, unsat)  # 102 / 102 and 32 / 34 (72 and 18 before the rules)
+
+
+def test_split_never_refutes_a_planted_synthetic_state():
+    """256-bit soundness on random DAGs (the bench's generator, SURVEY §8d op mix): a state with
+    a planted satisfying assignment -- checked here by the C oracle -- is never refuted by
+    mgp_refute_split at the product's settings (case splits, linear forms, bisection), while
+    the split refuter refutes hundreds of the other states."""
+    b = N.synth_generate(0x4D595448, 3 << 20, 4096, 64, 256)
+    r = N.refute_split(b["nodes"], b["node_offsets"], b["consts"], b["const_offsets"], max_splits=8, depth=2)
+    planted = np.nonzero(b["planted"])[0]
+    assert len(planted) > 1500 and int((r == 1).sum()) > 500
+    # the plants are models (one candidate row per planted state)
+    sub = planted[:512]
+    no, co = b["node_offsets"].astype(np.int64), b["const_offsets"].astype(np.int64)
+    nodes = np.concatenate([b["nodes"][no[i]:no[i + 1]] for i in sub])
+    consts = np.concatenate([b["consts"][co[i]:co[i + 1]] for i in sub]).reshape(-1, 8)
+    noff = np.concatenate([[0], np.cumsum([no[i + 1] - no[i] for i in sub])]).astype(np.uint64)
+    coff = np.concatenate([[0], np.cumsum([co[i + 1] - co[i] for i in sub])]).astype(np.uint64)
+    cands = np.ascontiguousarray(b["plant_words"][sub][:, None])
+    assert (coracle.first_sat(nodes, noff, consts, coff, cands) == 0).all()
+    assert int((r[planted] == 1).sum()) == 0

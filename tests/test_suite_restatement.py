@@ -106,3 +106,36 @@ def test_refute_cache_matches_the_refuter():
             seen += 1
         B.close()
     assert seen >= 5, seen
+
+
+def test_account_counts_a_refuted_sat_if_reachable_query():
+    """corpus.account: a child expected sat under an unlabelled parent keeps
+    its expectation (label suffix SAT_IF_REACHABLE); its refutation is a contradiction unless
+    an ancestor is refuted too; under a parent expected unsat the expectation is dropped."""
+    T = (object(),)
+    R = corpus.SAT_IF_REACHABLE
+    qs = [("c", "prune", "c:root", T, None, -1),              # 0 unlabelled
+          ("c", "prune", "c:child" + R, T, "sat", 0),         # 1 sat if 0 is reachable
+          ("c", "prune", "c:grandchild" + R, T, "sat", 1),    # 2 sat if 1 is reachable
+          ("c", "prune", "c:bad", T, "unsat", -1),            # 3
+          ("c", "prune", "c:under unsat" + corpus.UNDER_UNSAT_PARENT, T, None, 3)]
+    # 1 refuted under an undecided root: a contradiction; 2 refuted under refuted 1: consistent
+    acc = corpus.account(qs, ["undecided", "unsat", "unsat", "unsat", "undecided"])
+    c = acc["by_contract"]["c"]
+    assert c["contradicted"] == 1 and c["refuted_with_sat_expectation_if_reachable"] == 1
+    assert c["refuted_if_reachable_ancestor_refuted"] == 1 and c["sat_expectations_dropped"] == 1
+    # the root refuted as well: no contradiction left
+    acc = corpus.account(qs, ["unsat", "unsat", "unsat", "unsat", "undecided"])
+    assert acc["by_contract"]["c"]["contradicted"] == 0
+
+
+def test_suite_marks_expectations_by_parent():
+    """corpus.suite(): no sat expectation is dropped (the stream never follows a parent
+    expected unsat); children of unlabelled parents carry the SAT_IF_REACHABLE suffix."""
+    qs = _queries(["bectoken"])
+    assert not any(q[2].endswith(corpus.UNDER_UNSAT_PARENT) for q in qs)
+    marked = [k for k, q in enumerate(qs) if q[2].endswith(corpus.SAT_IF_REACHABLE)]
+    assert marked and all(qs[k][4] == "sat" for k in marked)
+    for k in marked:   # the parent is unlabelled or itself sat-if-reachable
+        p = qs[k][5]
+        assert qs[p][4] is None or qs[p][2].endswith(corpus.SAT_IF_REACHABLE)

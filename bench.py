@@ -578,6 +578,27 @@ def main():
             frontend[tag] = {"cand_bytes": cb, "seconds": dtc, "states_per_s": len(cs) / dtc,
                              "same_answers": [r[0] for r in res_c] == kinds, "stages_ms": pf.last_profile}
         pf.cand_bytes = keep_cb
+        # A/B: the call cut into at least 2 / 4 groups (Prefilter.min_groups), so that more of
+        # each GPU round overlaps the next group's host stages; medians of 3 cold calls
+        keep_mg = pf.min_groups
+        frontend["min_groups"] = {}
+        for mg in (2, 4):
+            pf.min_groups = mg
+            runs = []
+            for rep in range(3):
+                SV.unsat_cores().reset()
+                pf._N.program_cache_clear()
+                tf = time.perf_counter()
+                res_g = pf.check_states(cs)
+                runs.append((time.perf_counter() - tf, [r[0] for r in res_g], pf.last_profile))
+            medg = sorted(runs, key=lambda c: c[0])[1]
+            frontend["min_groups"][str(mg)] = {"seconds": medg[0], "states_per_s": len(cs) / medg[0],
+                                               "calls_seconds": [round(c[0], 4) for c in runs],
+                                               "same_answers": all(c[1] == kinds for c in runs),
+                                               "stages_ms": medg[2]}
+            if not frontend["min_groups"][str(mg)]["same_answers"]:
+                raise RuntimeError(f"front end: min_groups={mg} gave other answers")
+        pf.min_groups = keep_mg
         pf.ctx.close()
         # two pipelines on the one GPU (Prefilter(pipelines=2)): the batch hash-sharded over two
         # contexts, each on its own host thread with half the OpenMP threads, so that one

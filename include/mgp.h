@@ -380,11 +380,17 @@ int mgp_build_states(const uint8_t *t_op, const uint32_t *t_width, const int32_t
                      uint64_t n_names, mgp_fe_batch **out);
 int mgp_fe_get(const mgp_fe_batch *batch, int field, const void **ptr, uint64_t *count);
 void mgp_fe_free(mgp_fe_batch *batch);
+/* States idx[0..n) of a built batch (indices < its n_states, any order, repeats allowed) as a
+ * new batch, free with mgp_fe_free: every field equals what mgp_build_states gives for those
+ * states' roots, without walking the term arena again.  solver.Prefilter cuts its
+ * candidate-memory groups and retry rounds out of the call's one build this way. */
+int mgp_fe_select(const mgp_fe_batch *batch, const uint32_t *idx, uint32_t n, mgp_fe_batch **out);
 
 /* One batch through the whole pre-filter (mgp_pipeline.cpp): lower the GPU programs,
- * generate n_cand candidates per state ON THE GPU (the mgp_make_candidates mixture,
- * bit-identical, from the batch's hints/aliases/constants + fixed_pool), evaluate, and
- * run mgp_refute on the host while the GPU works.  Parent witnesses (optional):
+ * run the host pre-check (mgp_refute_domains: refutations + the variable domains the
+ * candidates draw from), generate n_cand candidates per state ON THE GPU (the
+ * mgp_make_candidates mixture, bit-identical, from the batch's hints/aliases/constants +
+ * fixed_pool) and evaluate them.  Parent witnesses (optional):
  * parent_keys/parent_vals[parent_off[s] .. parent_off[s+1]) are (slot key, 8 limbs)
  * pairs of state s's parent witness; slot_keys = the batch's MGP_FE_VAR_KEY; a state
  * with a parent gets those values in candidate row 0.  Outputs: out_first[s] as
@@ -405,12 +411,33 @@ void mgp_fe_free(mgp_fe_batch *batch);
 int mgp_pipeline_reserve(mgp_ctx *ctx, uint64_t host_bytes, uint64_t cand_bytes);
 #define MGP_CHECK_NO_REFUTE 0x1u   /* skip the host pre-check (and the domain rows) */
 #define MGP_CHECK_NO_DOMAINS 0x2u  /* plain mixture rows only (A/B)                    */
+#define MGP_CHECK_NO_WITNESS 0x4u  /* mgp_check_submit: first-SAT words only, no witness download */
 int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint64_t seed,
                     const uint32_t *fixed_pool, uint32_t n_fixed, const uint64_t *parent_keys,
                     const uint32_t *parent_vals, const uint64_t *parent_off, const uint64_t *slot_keys,
                     const uint32_t *xrows, const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars,
                     uint32_t flags, int32_t *out_first, uint32_t *out_witness, int8_t *out_refuted,
                     uint32_t *out_n_vars, double *out_times);
+/* mgp_check_batch in two halves, so that a caller overlaps one batch's GPU round with the
+ * next batch's host stages.  mgp_check_submit does the host stages (lowering, pre-check,
+ * staging into one of the context's two pinned buffers), enqueues the upload, kernels and
+ * download on the context's stream, and returns without waiting: out_refuted and
+ * *out_n_vars are final, out_times gets 3 stage times (lower, refute, upload+launch),
+ * *out_ticket names the batch (-1 for an empty one).  At most two batches are in flight
+ * per context (a third submit fails with MGP_E_ARG).  mgp_check_finish waits for the
+ * ticket's batch and writes out_first / out_witness as mgp_check_batch does (out_witness
+ * NULL, or a submit with MGP_CHECK_NO_WITNESS: none); out_times gets 2 (GPU wait,
+ * copy-back).  Batches run on the device in submit order; the batch object and the
+ * explicit rows need to live only until mgp_check_submit returns.  Answers are those of
+ * mgp_check_batch on the same arguments. */
+int mgp_check_submit(mgp_ctx *ctx, const mgp_fe_batch *batch, uint32_t n_cand, uint64_t seed,
+                     const uint32_t *fixed_pool, uint32_t n_fixed, const uint64_t *parent_keys,
+                     const uint32_t *parent_vals, const uint64_t *parent_off, const uint64_t *slot_keys,
+                     const uint32_t *xrows, const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars,
+                     uint32_t flags, int8_t *out_refuted, uint32_t *out_n_vars, double *out_times,
+                     int32_t *out_ticket);
+int mgp_check_finish(mgp_ctx *ctx, int32_t ticket, int32_t *out_first, uint32_t *out_witness,
+                     double *out_times);
 /* mgp_check_batch keeps the programs it lowers in a process-wide cache keyed by the
  * exact node list and constants of each state (compared in full on a hit; 256 MiB,
  * oldest first out): a retry round or a repeated query skips the lowering.  This

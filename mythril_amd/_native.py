@@ -109,6 +109,10 @@ def _bind(lib):
                                             ctypes.POINTER(_P)]),
         "mgp_fe_get": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(_U64)]),
         "mgp_fe_free": (None, [_P]),
+        "mgp_fe_select": (ctypes.c_int, [_P, _P, _U32, ctypes.POINTER(_P)]),
+        "mgp_check_submit": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _U32, _U32,
+                                            _P, _P, _P, _P]),
+        "mgp_check_finish": (ctypes.c_int, [_P, _I32, _P, _P, _P]),
         "mgp_pipeline_reserve": (ctypes.c_int, [_P, _U64, _U64]),
         "mgp_check_batch": (ctypes.c_int, [_P, _P, _U32, _U64, _P, _U32, _P, _P, _P, _P, _P, _P, _U32, _U32, _U32,
                                            _P, _P, _P, _P, _P]),
@@ -179,7 +183,10 @@ EXPORTED_SYMBOLS = (
     "mgp_build_states",
     "mgp_fe_get",
     "mgp_fe_free",
+    "mgp_fe_select",
     "mgp_check_batch",
+    "mgp_check_submit",
+    "mgp_check_finish",
     "mgp_pipeline_reserve",
     "mgp_fe_candidates",
     "mgp_program_cache_clear",
@@ -524,6 +531,11 @@ class Context:
     def check_batch(self, batch, n_cand: int, seed: int, parents=None, refute: bool = True, xrows=None):
         """A front-end batch (mythril_amd.front.Batch) through mgp_check_batch."""
         return batch._check_native(self, n_cand, seed, parents, refute, xrows)
+
+    def submit_batch(self, batch, n_cand: int, seed: int, parents=None, refute: bool = True, xrows=None):
+        """mgp_check_submit: the host stages of check_batch now, the GPU round enqueued; ->
+        front.PendingRound (finish() = mgp_check_finish).  At most two in flight."""
+        return batch._submit_native(self, n_cand, seed, parents, refute, xrows)
 
     def keccak256(self, data: np.ndarray, length: int, stride: int) -> np.ndarray:
         data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)

@@ -819,6 +819,78 @@ int mgp_fe_get(const mgp_fe_batch *B, int field, const void **ptr, uint64_t *cou
   }
 }
 
+// The states idx[0..n) of a built batch as a batch of their own, in that order: every
+// per-state array sliced and concatenated (node, constant, slot and alias references are
+// local to their state, so slices need no renumbering).  The same arrays a build of those
+// states' roots would give, without walking the term arena again (solver.Prefilter splits a
+// batch into candidate-memory groups and retry rounds this way).
+int mgp_fe_select(const mgp_fe_batch *B, const uint32_t *idx, uint32_t n, mgp_fe_batch **out) {
+  if (!B || !out || (n && !idx)) return MGP_E_ARG;
+  *out = nullptr;
+  for (uint32_t k = 0; k < n; ++k)
+    if (idx[k] >= B->n_states) return MGP_E_ARG;
+  mgp_fe_batch *S = fe_take();
+  if (!S) return MGP_E_NOMEM;
+  S->n_states = n;
+  const bool gpu = !B->gpu_nodes.empty(), dec = !B->dec_nodes.empty();
+  auto offsets = [&](const std::vector<uint64_t> &src, std::vector<uint64_t> &dst) {
+    dst.assign((size_t)n + 1, 0);
+    for (uint32_t k = 0; k < n; ++k) dst[k + 1] = dst[k] + (src[idx[k] + 1] - src[idx[k]]);
+  };
+  offsets(B->node_off, S->node_off);
+  offsets(B->const_off, S->const_off);
+  offsets(B->var_off, S->var_off);
+  offsets(B->alias_off, S->alias_off);
+  if (gpu) offsets(B->gpu_node_off, S->gpu_node_off);
+  const uint64_t nv = S->var_off[n];
+  S->hint_off.assign(nv + 1, 0);
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint64_t v0 = B->var_off[idx[k]], d0 = S->var_off[k], V = S->var_off[k + 1] - d0;
+    for (uint64_t v = 0; v < V; ++v) S->hint_off[d0 + v + 1] = B->hint_off[v0 + v + 1] - B->hint_off[v0 + v];
+  }
+  for (uint64_t v = 0; v < nv; ++v) S->hint_off[v + 1] += S->hint_off[v];
+  S->nodes.resize(S->node_off[n]);
+  if (dec) S->dec_nodes.resize(S->node_off[n]);
+  if (gpu) S->gpu_nodes.resize(S->gpu_node_off[n]);
+  S->consts.resize(S->const_off[n] * 8);
+  S->var_width.resize(nv);
+  S->var_full.resize(nv);
+  S->var_name.resize(nv);
+  S->var_aux.resize(nv);
+  S->var_kind.resize(nv);
+  S->var_key.resize(nv);
+  S->var_tid.resize(nv);
+  S->hints.resize(S->hint_off[nv] * 8);
+  S->aliases.resize(S->alias_off[n] * 2);
+  S->flags.assign(n, 0);
+  S->state_key.assign(n, 0);
+#pragma omp parallel for schedule(static) if (n > 64)
+  for (int64_t k = 0; k < (int64_t)n; ++k) {
+    const uint32_t s = idx[k];
+    auto slice = [&](const auto &src, auto &dst, uint64_t from, uint64_t to, uint64_t at) {
+      std::copy(src.begin() + from, src.begin() + to, dst.begin() + at);
+    };
+    slice(B->nodes, S->nodes, B->node_off[s], B->node_off[s + 1], S->node_off[k]);
+    if (dec) slice(B->dec_nodes, S->dec_nodes, B->node_off[s], B->node_off[s + 1], S->node_off[k]);
+    if (gpu) slice(B->gpu_nodes, S->gpu_nodes, B->gpu_node_off[s], B->gpu_node_off[s + 1], S->gpu_node_off[k]);
+    slice(B->consts, S->consts, B->const_off[s] * 8, B->const_off[s + 1] * 8, S->const_off[k] * 8);
+    const uint64_t v0 = B->var_off[s], v1 = B->var_off[s + 1], d0 = S->var_off[k];
+    slice(B->var_width, S->var_width, v0, v1, d0);
+    slice(B->var_full, S->var_full, v0, v1, d0);
+    slice(B->var_name, S->var_name, v0, v1, d0);
+    slice(B->var_aux, S->var_aux, v0, v1, d0);
+    slice(B->var_kind, S->var_kind, v0, v1, d0);
+    slice(B->var_key, S->var_key, v0, v1, d0);
+    slice(B->var_tid, S->var_tid, v0, v1, d0);
+    slice(B->hints, S->hints, B->hint_off[v0] * 8, B->hint_off[v1] * 8, S->hint_off[d0] * 8);
+    slice(B->aliases, S->aliases, B->alias_off[s] * 2, B->alias_off[s + 1] * 2, S->alias_off[k] * 2);
+    S->flags[k] = B->flags[s];
+    S->state_key[k] = B->state_key[s];
+  }
+  *out = S;
+  return MGP_OK;
+}
+
 void mgp_fe_free(mgp_fe_batch *B) {
   if (!B) return;
   {

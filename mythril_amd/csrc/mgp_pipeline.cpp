@@ -1,5 +1,7 @@
-// mgp_pipeline.cpp — one call per batch of states: lower, generate candidates on the
-// GPU, evaluate, and run the host UNSAT pre-check while the GPU works.
+// mgp_pipeline.cpp — one call per batch of states: lower, pre-check on the host,
+// generate candidates on the GPU and evaluate (the pre-check runs before the upload: its
+// domains feed the candidates).  A caller overlaps one batch's GPU round with the next
+// batch's host stages through mgp_check_submit / mgp_check_finish.
 //
 // This is the native body of Prefilter.check_states (mythril_amd/solver.py), i.e. of
 // the batched prune filter at LaserEVM.exec (mythril/laser/ethereum/svm.py:251-255)
@@ -73,14 +75,20 @@ Arr get(const mgp_fe_batch *B, int f) {
   return a;
 }
 
-// device buffers of the pipeline, one set per (context); grown on demand
-struct PipeBufs {
-  void *p[16] = {};
-  size_t cap[16] = {};
-  U32Buf words;          // the batch's lowered programs (host), reused across calls
-  U32Buf dom;            // the batch's variable domains (host), reused across calls
-  void *host = nullptr;  // pinned staging: one upload and one download per call (pageable
-  size_t hcap = 0;       // hipMemcpyAsync is a blocking staged copy, ~0.4 ms each)
+// One submitted batch: its pinned staging buffer (one upload and one download per batch;
+// pageable hipMemcpyAsync is a blocking staged copy, ~0.4 ms each), the event recorded
+// after its download, and what mgp_check_finish needs to unpack the download.  Two slots
+// per context: a caller submits the next batch -- lowering, pre-check and staging on the
+// host -- while the previous one runs on the GPU (solver.Prefilter's group pipeline).
+struct Slot {
+  void *host = nullptr;
+  size_t hcap = 0;
+  hipEvent_t done = nullptr;
+  bool busy = false;
+  bool want_witness = false;
+  uint32_t n_states = 0, n_vars = 0, user_vars = 0;
+  size_t first_bytes = 0;
+  std::vector<uint8_t> status;
   hipError_t ensure_host(size_t bytes) {
     if (bytes <= hcap) return hipSuccess;
     if (host) (void)hipHostFree(host);
@@ -91,6 +99,16 @@ struct PipeBufs {
     if (e == hipSuccess) hcap = want;
     return e;
   }
+};
+
+// device buffers of the pipeline, one set per (context); grown on demand.  Every batch's
+// device work is in order on the context's stream, so two submitted batches share them.
+struct PipeBufs {
+  void *p[16] = {};
+  size_t cap[16] = {};
+  U32Buf words;          // the batch's lowered programs (host), reused across calls
+  U32Buf dom;            // the batch's variable domains (host), reused across calls
+  Slot slot[2];
   hipError_t ensure(int i, size_t bytes) {
     if (bytes <= cap[i]) return hipSuccess;
     if (p[i]) (void)hipFree(p[i]);
@@ -375,26 +393,34 @@ void mgp_pipeline_release(mgp_ctx *ctx) {
     m.erase(it);
   }
   if (!b) return;
+  for (Slot &s : b->slot)
+    if (s.busy && s.done) (void)hipEventSynchronize(s.done);  // nothing in flight reads what is freed
   for (int i = 0; i < 16; ++i)
     if (b->p[i]) (void)hipFree(b->p[i]);
-  if (b->host) (void)hipHostFree(b->host);
+  for (Slot &s : b->slot) {
+    if (s.host) (void)hipHostFree(s.host);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
 }
 
 int mgp_pipeline_reserve(mgp_ctx *ctx, uint64_t host_bytes, uint64_t cand_bytes) {
   if (!ctx) return MGP_E_ARG;
   PipeBufs &D = bufs_of(ctx);
-  hipError_t e = D.ensure_host((size_t)host_bytes);
+  hipError_t e = hipSuccess;
+  for (Slot &s : D.slot)
+    if (e == hipSuccess && !s.busy) e = s.ensure_host((size_t)host_bytes);
   if (e == hipSuccess && cand_bytes) e = D.ensure(B_CANDS, (size_t)cand_bytes);
   return e == hipSuccess ? MGP_OK : mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
 }
 
-int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64_t seed, const uint32_t *fixed_pool,
-                    uint32_t n_fixed, const uint64_t *parent_keys, const uint32_t *parent_vals,
-                    const uint64_t *parent_off, const uint64_t *slot_keys, const uint32_t *xrows,
-                    const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars, uint32_t flags, int32_t *out_first,
-                    uint32_t *out_witness, int8_t *out_refuted, uint32_t *out_n_vars, double *out_times) {
-  if (!ctx || !B || !out_first || !out_refuted || n_cand == 0 || (n_fixed && !fixed_pool))
-    return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument to mgp_check_batch");
+int mgp_check_submit(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64_t seed, const uint32_t *fixed_pool,
+                     uint32_t n_fixed, const uint64_t *parent_keys, const uint32_t *parent_vals,
+                     const uint64_t *parent_off, const uint64_t *slot_keys, const uint32_t *xrows,
+                     const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars, uint32_t flags, int8_t *out_refuted,
+                     uint32_t *out_n_vars, double *out_times, int32_t *out_ticket) {
+  if (!ctx || !B || !out_refuted || !out_ticket || n_cand == 0 || (n_fixed && !fixed_pool))
+    return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument to mgp_check_submit");
+  *out_ticket = -1;
   double t = omp_get_wtime();
   auto lap = [&](int k) {
     const double now = omp_get_wtime();
@@ -408,9 +434,14 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
             aoff = get(B, MGP_FE_ALIAS_OFF), aliases = get(B, MGP_FE_ALIASES), vkind = get(B, MGP_FE_VAR_KIND),
             skey = get(B, MGP_FE_STATE_KEY);
   const uint32_t n_states = (uint32_t)(noff.n ? noff.n - 1 : 0);
-  if (n_states == 0) return MGP_OK;
+  if (out_n_vars) *out_n_vars = 1;
+  if (n_states == 0) return MGP_OK;  // ticket -1: nothing to finish
   if (n_xrows && (!xrows || !xmask || n_xvars == 0))
     return mgp_ctx_fail(ctx, MGP_E_ARG, "explicit rows need xrows, xmask and n_xvars");
+  PipeBufs &D0 = bufs_of(ctx);
+  const int ticket = !D0.slot[0].busy ? 0 : (!D0.slot[1].busy ? 1 : -1);
+  if (ticket < 0) return mgp_ctx_fail(ctx, MGP_E_ARG, "two batches in flight on this context: finish one first");
+  Slot &SL = D0.slot[ticket];
   const uint64_t *vo = (const uint64_t *)voff.p;
   uint32_t n_vars = 1;
   for (uint32_t s = 0; s < n_states; ++s) n_vars = std::max<uint32_t>(n_vars, (uint32_t)(vo[s + 1] - vo[s]));
@@ -419,8 +450,8 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   const uint32_t *cp = consts.n ? (const uint32_t *)consts.p : zero8;
 
   // 1. lower the GPU programs (programs lowered by an earlier call come from the cache)
-  // the batch's programs, in the context's kept buffer (the same ~60 MB every call)
-  PipeBufs &D0 = bufs_of(ctx);
+  // the batch's programs, in the context's kept buffer (the same ~60 MB every call; a
+  // batch still in flight has its copy in its own staging buffer)
   U32Buf &words = D0.words;
   words.clear();
   std::vector<uint64_t> offs;
@@ -497,7 +528,7 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   mgp_ctx_stream(ctx, &stp, &dev);
   hipStream_t st = (hipStream_t)stp;
   hipError_t e = hipSetDevice(dev);
-  PipeBufs &D = bufs_of(ctx);
+  PipeBufs &D = D0;
   const size_t cand_bytes = (size_t)n_states * n_cand * n_vars * 32u;
   const uint32_t n_chunks = (n_cand + 63u) / 64u;
   // one table buffer: var_off | var_width | hint_off | hints | alias_off | aliases | const_off | consts |
@@ -523,9 +554,11 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   for (int i = 0; i < 21; ++i) at[i + 4] = (at[i + 3] + sizes[i] + 255) & ~(size_t)255;
   const size_t up = at[24];
   const size_t wit_bytes = (size_t)n_states * n_vars * 32u, first_bytes = ((size_t)n_states * 4u + 255) & ~(size_t)255;
-  if (e == hipSuccess) e = D.ensure_host(std::max(up, first_bytes + (out_witness ? wit_bytes : 0)));
+  const bool want_witness = !(flags & MGP_CHECK_NO_WITNESS);
+  if (e == hipSuccess) e = SL.ensure_host(std::max(up, first_bytes + (want_witness ? wit_bytes : 0)));
+  if (e == hipSuccess && !SL.done) e = hipEventCreateWithFlags(&SL.done, hipEventDisableTiming);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
-  uint8_t *H = (uint8_t *)D.host;
+  uint8_t *H = (uint8_t *)SL.host;
   {  // the programs (hundreds of MB for contract states): copied in 4-MiB pieces in parallel
     const size_t piece = (size_t)4 << 20, n_pieces = (pre[0] + piece - 1) / piece;
     const uint8_t *src = (const uint8_t *)words.data();
@@ -539,11 +572,14 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
   memcpy(H + at[2], order.data(), pre[2]);
   for (int i = 0; i < 21; ++i)
     if (sizes[i] && srcs[i]) memcpy(H + at[i + 3], srcs[i], sizes[i]);
-  if (e == hipSuccess) e = D.ensure(B_CANDS, cand_bytes);
-  if (e == hipSuccess) e = D.ensure(B_FIRST, (size_t)n_states * 4u);
-  if (e == hipSuccess) e = D.ensure(B_WIT, wit_bytes);
-  if (e == hipSuccess) e = D.ensure(B_PART, (size_t)n_states * n_chunks * 4u);
-  if (e == hipSuccess) e = D.ensure(B_TABLES, up);
+  // a device buffer that must grow is freed and reallocated: let the other slot's batch,
+  // which may still read it, drain first
+  const size_t need[5] = {cand_bytes, (size_t)n_states * 4u, wit_bytes, (size_t)n_states * n_chunks * 4u, up};
+  const int which[5] = {B_CANDS, B_FIRST, B_WIT, B_PART, B_TABLES};
+  bool grow = false;
+  for (int i = 0; i < 5; ++i) grow |= need[i] > D.cap[which[i]];
+  if (grow && D.slot[1 - ticket].busy && e == hipSuccess) e = hipStreamSynchronize(st);
+  for (int i = 0; i < 5 && e == hipSuccess; ++i) e = D.ensure(which[i], need[i]);
   if (e == hipSuccess) e = hipMemcpyAsync(D.p[B_TABLES], H, up, hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
   const uint8_t *base = (const uint8_t *)D.p[B_TABLES], *tb = base + at[3];
@@ -563,27 +599,70 @@ int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64
                         (const uint32_t *)D.p[B_CANDS], n_cand, n_vars, max_slots, (int32_t *)D.p[B_FIRST],
                         (uint32_t *)D.p[B_WIT], (int32_t *)D.p[B_PART], (const uint32_t *)(base + at[2]),
                         bounds.data(), bslots.data(), (uint32_t)nb, st);
-  // one download into the pinned buffer (the upload has been consumed by then: same stream)
+  // one download into the slot's pinned buffer (the upload has been consumed by then: same stream)
   if (e == hipSuccess) e = hipMemcpyAsync(H, D.p[B_FIRST], (size_t)n_states * 4u, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess && out_witness)
+  if (e == hipSuccess && want_witness)
     e = hipMemcpyAsync(H + first_bytes, D.p[B_WIT], wit_bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipEventRecord(SL.done, st);
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
+  SL.busy = true;
+  SL.want_witness = want_witness;
+  SL.n_states = n_states;
+  SL.n_vars = n_vars;
+  SL.user_vars = user_vars;
+  SL.first_bytes = first_bytes;
+  SL.status.swap(status);
+  *out_ticket = ticket;
   lap(2);
-  e = hipStreamSynchronize(st);
+  return MGP_OK;
+}
+
+int mgp_check_finish(mgp_ctx *ctx, int32_t ticket, int32_t *out_first, uint32_t *out_witness, double *out_times) {
+  if (!ctx) return MGP_E_ARG;
+  if (ticket < 0) return MGP_OK;  // an empty batch
+  PipeBufs &D = bufs_of(ctx);
+  if (ticket > 1 || !D.slot[ticket].busy) return mgp_ctx_fail(ctx, MGP_E_ARG, "mgp_check_finish: no such batch in flight");
+  Slot &SL = D.slot[ticket];
+  if (!out_first || (out_witness && !SL.want_witness)) return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument to mgp_check_finish");
+  double t = omp_get_wtime();
+  hipError_t e = hipEventSynchronize(SL.done);
+  SL.busy = false;  // the slot is free again whatever happened to its batch
   if (e != hipSuccess) return mgp_ctx_fail(ctx, MGP_E_HIP, hipGetErrorString(e));
-  lap(3);
+  double now = omp_get_wtime();
+  if (out_times) out_times[0] = 1e3 * (now - t);
+  t = now;
   // 5. first-SAT words and the witnesses of the SAT states
+  const uint8_t *H = (const uint8_t *)SL.host;
+  const uint32_t n_states = SL.n_states;
   memcpy(out_first, H, (size_t)n_states * 4u);
   if (out_witness) {
-    const uint32_t *w = (const uint32_t *)(H + first_bytes);
+    const uint32_t *w = (const uint32_t *)(H + SL.first_bytes);
     for (uint32_t s = 0; s < n_states; ++s)
-      if (out_first[s] >= 0) memcpy(out_witness + (size_t)s * user_vars * 8u, w + (size_t)s * n_vars * 8u,
-                                    (size_t)user_vars * 32u);
+      if (out_first[s] >= 0) memcpy(out_witness + (size_t)s * SL.user_vars * 8u, w + (size_t)s * SL.n_vars * 8u,
+                                    (size_t)SL.user_vars * 32u);
   }
   for (uint32_t s = 0; s < n_states; ++s)
-    if (status[s] != MGP_ST_OK && out_first[s] >= 0) out_first[s] = MGP_UNDECIDED;  // never expected
-  lap(4);
+    if (SL.status[s] != MGP_ST_OK && out_first[s] >= 0) out_first[s] = MGP_UNDECIDED;  // never expected
+  if (out_times) out_times[1] = 1e3 * (omp_get_wtime() - t);
   return MGP_OK;
+}
+
+int mgp_check_batch(mgp_ctx *ctx, const mgp_fe_batch *B, uint32_t n_cand, uint64_t seed, const uint32_t *fixed_pool,
+                    uint32_t n_fixed, const uint64_t *parent_keys, const uint32_t *parent_vals,
+                    const uint64_t *parent_off, const uint64_t *slot_keys, const uint32_t *xrows,
+                    const uint8_t *xmask, uint32_t n_xrows, uint32_t n_xvars, uint32_t flags, int32_t *out_first,
+                    uint32_t *out_witness, int8_t *out_refuted, uint32_t *out_n_vars, double *out_times) {
+  if (!ctx || !B || !out_first || !out_refuted || n_cand == 0 || (n_fixed && !fixed_pool))
+    return mgp_ctx_fail(ctx, MGP_E_ARG, "bad argument to mgp_check_batch");
+  int32_t ticket = -1;
+  double tm[5] = {0, 0, 0, 0, 0};
+  int rc = mgp_check_submit(ctx, B, n_cand, seed, fixed_pool, n_fixed, parent_keys, parent_vals, parent_off,
+                            slot_keys, xrows, xmask, n_xrows, n_xvars,
+                            out_witness ? (flags & ~MGP_CHECK_NO_WITNESS) : (flags | MGP_CHECK_NO_WITNESS),
+                            out_refuted, out_n_vars, tm, &ticket);
+  if (rc == MGP_OK) rc = mgp_check_finish(ctx, ticket, out_first, out_witness, tm + 3);
+  if (out_times) memcpy(out_times, tm, sizeof(tm));
+  return rc;
 }
 
 // Test hook: the candidates mgp_check_batch evaluates, copied back in the device layout

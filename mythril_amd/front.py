@@ -63,6 +63,22 @@ class Batch:
                                 self.n_states, _arena_ptr(A.name_hash) if len(A.name_hash) else None,
                                 len(A.name_hash), ctypes.byref(self._h))
         N._check(rc)
+        self._load_fields()
+
+    def select(self, idx: Sequence[int]) -> "Batch":
+        """States idx of this batch as a batch of their own (mgp_fe_select: the arrays a
+        build of those states would give, without walking the term arena again)."""
+        ix = np.ascontiguousarray(np.asarray(idx, dtype=np.uint32).reshape(-1))
+        out = Batch.__new__(Batch)
+        out.n_states = int(ix.size)
+        out._vt = None
+        out._h = ctypes.c_void_p()
+        N._check(N.lib().mgp_fe_select(self._h, N._ptr(ix) if ix.size else None, ix.size, ctypes.byref(out._h)))
+        out._load_fields()
+        return out
+
+    def _load_fields(self) -> None:
+        L = N.lib()
         for name, (idx, dt, per) in _FIELDS.items():
             p, n = ctypes.c_void_p(), ctypes.c_uint64()
             N._check(L.mgp_fe_get(self._h, idx, ctypes.byref(p), ctypes.byref(n)))
@@ -89,21 +105,24 @@ class Batch:
         nv, 8], mask u8 [n, k, nv]): explicit rows placed in the first k mixture rows."""
         return ctx.check_batch(self, n_cand, seed, parents, refute, xrows)
 
-    def _check_native(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True,
-                      xrows=None):
-        """mgp_check_batch on libmgp context `ctx`."""
+    def submit(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True,
+               xrows=None):
+        """The host half of check (mgp_check_submit on a libmgp context): lowering, pre-check
+        and staging now, the GPU round enqueued; -> a pending round whose finish() returns
+        check's tuple.  A context without submit_batch (a test double) answers at once."""
+        sub = getattr(ctx, "submit_batch", None)
+        if sub is None:
+            return _Answered(ctx.check_batch(self, n_cand, seed, parents, refute, xrows))
+        return sub(self, n_cand, seed, parents, refute, xrows)
+
+    def _native_args(self, n_cand: int, seed: int, parents, xrows):
+        """The batch-side arguments of mgp_check_batch / mgp_check_submit."""
         global FIXED_POOL_LIMBS
         if FIXED_POOL_LIMBS is None:
             from .dag import _FIXED_LIMBS
 
             FIXED_POOL_LIMBS = np.ascontiguousarray(_FIXED_LIMBS, dtype=np.uint32)
         n = self.n_states
-        n_vars = max(1, self.n_vars())
-        first = np.full(n, N.MGP_NO_SAT, np.int32)
-        wit = np.zeros((n, n_vars, 8), np.uint32)
-        ref = np.zeros(max(n, 1), np.int8)
-        times = np.zeros(5, np.float64)
-        nv = ctypes.c_uint32(0)
         pk = pv = po = None
         if parents is not None and any(p is not None for p in parents):
             ks, vs, cnt = [], [], []
@@ -119,14 +138,42 @@ class Batch:
             if pk.size == 0:
                 pk, pv = np.zeros(1, np.uint64), np.zeros((1, 8), np.uint32)
         xr, xm, nx, nxv = self._xrows(xrows)
-        rc = N.lib().mgp_check_batch(ctx._h, self._h, n_cand, seed & (2 ** 64 - 1), N._ptr(FIXED_POOL_LIMBS),
-                                     len(FIXED_POOL_LIMBS), N._ptr(pk), N._ptr(pv), N._ptr(po),
-                                     N._ptr(self.var_key) if pk is not None else None,
-                                     N._ptr(xr), N._ptr(xm), nx, nxv,
-                                     0 if refute else 1, N._ptr(first), N._ptr(wit), N._ptr(ref),
+        # (the arrays stay referenced by the caller until the native call returns)
+        return (pk, pv, po, xr, xm), (self._h, n_cand, seed & (2 ** 64 - 1), N._ptr(FIXED_POOL_LIMBS),
+                                      len(FIXED_POOL_LIMBS), N._ptr(pk), N._ptr(pv), N._ptr(po),
+                                      N._ptr(self.var_key) if pk is not None else None,
+                                      N._ptr(xr), N._ptr(xm), nx, nxv)
+
+    def _check_native(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True,
+                      xrows=None):
+        """mgp_check_batch on libmgp context `ctx`."""
+        n = self.n_states
+        n_vars = max(1, self.n_vars())
+        first = np.full(n, N.MGP_NO_SAT, np.int32)
+        wit = np.zeros((n, n_vars, 8), np.uint32)
+        ref = np.zeros(max(n, 1), np.int8)
+        times = np.zeros(5, np.float64)
+        nv = ctypes.c_uint32(0)
+        keep, args = self._native_args(n_cand, seed, parents, xrows)
+        rc = N.lib().mgp_check_batch(ctx._h, *args, 0 if refute else 1, N._ptr(first), N._ptr(wit), N._ptr(ref),
                                      ctypes.byref(nv), N._ptr(times))
         N._check(rc, ctx._h)
         return first, wit, ref[:n], times
+
+    def _submit_native(self, ctx, n_cand: int, seed: int, parents: Optional[Sequence] = None, refute: bool = True,
+                       xrows=None) -> "PendingRound":
+        """mgp_check_submit on libmgp context `ctx`."""
+        n = self.n_states
+        ref = np.zeros(max(n, 1), np.int8)
+        times = np.zeros(5, np.float64)
+        nv = ctypes.c_uint32(0)
+        ticket = ctypes.c_int32(-1)
+        keep, args = self._native_args(n_cand, seed, parents, xrows)
+        rc = N.lib().mgp_check_submit(ctx._h, *args, 0 if refute else 1, N._ptr(ref), ctypes.byref(nv),
+                                      N._ptr(times), ctypes.byref(ticket))
+        N._check(rc, ctx._h)
+        del keep
+        return PendingRound(ctx, ticket.value, n, max(1, self.n_vars()), ref[:n], times)
 
     def _xrows(self, xrows):
         if xrows is None:
@@ -224,6 +271,36 @@ class Batch:
         w = np.ascontiguousarray(words[: v1 - v0], dtype=np.uint32)
         vals = [int.from_bytes(w[i].tobytes(), "little") for i in range(v1 - v0)]
         return _decode(self.var_width, self.var_full, self.var_name, self.var_aux, self.var_kind, v0, v1, vals)
+
+
+class PendingRound:
+    """A witness round submitted with mgp_check_submit; finish() waits for its GPU work and
+    returns (first_sat, witness, refuted, stage ms[5]) as Batch.check does."""
+
+    def __init__(self, ctx, ticket: int, n: int, n_vars: int, refuted: np.ndarray, times: np.ndarray):
+        self.ctx, self.ticket, self.n, self.n_vars = ctx, ticket, n, n_vars
+        self.refuted, self.times = refuted, times
+        self._out = None
+
+    def finish(self):
+        if self._out is None:
+            first = np.full(self.n, N.MGP_NO_SAT, np.int32)
+            wit = np.zeros((self.n, self.n_vars, 8), np.uint32)
+            N._check(N.lib().mgp_check_finish(self.ctx._h, self.ticket, N._ptr(first), N._ptr(wit),
+                                              N._ptr(self.times[3:])), self.ctx._h)
+            self._out = (first, wit, self.refuted, self.times)
+        return self._out
+
+
+class _Answered:
+    """A round answered at submission (a context without mgp_check_submit)."""
+
+    def __init__(self, out):
+        self._out = out
+        self.times = out[3]
+
+    def finish(self):
+        return self._out
 
 
 class VarTables:

@@ -29,6 +29,7 @@ answer is `unknown`, which each caller maps exactly as the reference does.
 """
 from __future__ import annotations
 
+import collections
 import os
 import threading
 import time
@@ -409,6 +410,8 @@ class Prefilter:
     # 16-thread host the two half teams cost more than the overlap hides (the 1 024-state call
     # 119 -> 221-272 ms, bench frontend.pipelines2)
     PIPELINE_MIN = 128
+    MIN_GROUPS = 1
+    GROUP_MIN_STATES = 256
 
     def __init__(self, device: int = 0, n_cand: int = 256, seed: int = 0x4D595448,
                  devices: Optional[Sequence[int]] = None, pipelines: int = 1):
@@ -434,6 +437,9 @@ class Prefilter:
         self.split_depth = self.SPLIT_DEPTH
         self.rows_first_nodes = self.ROWS_FIRST_NODES
         self.cand_bytes = 1 << 30  # candidate memory of one witness round (larger batches are split)
+        # a call of >= GROUP_MIN_STATES states runs as at least min_groups groups, so that the
+        # pipeline has a next round's host stages to overlap with each GPU round
+        self.min_groups = self.MIN_GROUPS
         # the pipeline's pinned host staging and candidate block, sized once here instead of
         # on the first large batch (pinning a few hundred MB of host memory takes tens of ms)
         # (MGP_HOST_STAGING_MB lowers the reserve for several ranks on one device; a reserve
@@ -557,54 +563,53 @@ class Prefilter:
         return out, sorted(refuted)
 
     def _check_native(self, ctx, states, parents):
-        """One native front-end batch (mgp_build_states) through mgp_check_batch on `ctx`:
-        GPU witnesses, host refutations overlapped with the GPU; the second witness round
-        for what is left.  -> (results, indices of the refuted states).  A batch whose
-        candidate block would pass `cand_bytes` is split into sub-batches of similar
-        variable counts (the answers do not change: candidates are keyed by content)."""
-        from .front import FE_SAT_UNSAFE, Batch
+        """One native front-end batch (mgp_build_states) through the witness rounds on `ctx`
+        (GPU witnesses; host refutations) and the split refuter for what is left.  ->
+        (results, indices of the refuted states).  A batch whose candidate block would pass
+        `cand_bytes` runs as groups of similar variable counts, cut out of the one build
+        (Batch.select).  The rounds are pipelined (mgp_check_submit / mgp_check_finish, two in
+        flight): a round's host stages -- decision rows, lowering, pre-check, staging -- run
+        while the previous round is on the GPU, and a group's second round is queued when its
+        first round finishes.  The answers do not change: candidates are keyed by content."""
+        from .front import Batch
 
         tb = time.perf_counter()
         B = Batch(states)
+        n = len(states)
+        prof = {"states": n, "build_ms": 1e3 * (time.perf_counter() - tb)}
         nv = np.diff(B.var_off).astype(np.int64)
         n_vars = max(1, int(nv.max()) if len(nv) else 1)
-        if len(states) > 1 and len(states) * self.n_cand * n_vars * 32 > self.cand_bytes:
-            B.close()
-            res: List = [None] * len(states)
-            refuted: List[int] = []
-            profs: List[dict] = []
-            for grp in self._groups(nv, self.n_cand):
-                sub, sub_ref = self._check_native(ctx, [states[k] for k in grp],
-                                                  None if parents is None else [parents[k] for k in grp])
-                for k, r in zip(grp, sub):
-                    res[k] = r
-                refuted.extend(grp[k] for k in sub_ref)
-                profs.append(getattr(self._tls, "profile", None) or {})
-            self.last_profile = self._tls.profile = _sum_profiles(profs)
-            return res, sorted(refuted)
-        prof = {"states": len(states), "build_ms": 1e3 * (time.perf_counter() - tb)}
-        td = time.perf_counter()
-        xrows = self._first_round_rows(B, parents, ctx)
-        if xrows is not None:
-            prof["rows_first_ms"] = 1e3 * (time.perf_counter() - td)
-        first, wit, proven, times = B.check(ctx, self.n_cand, self.seed, parents, refute=self.refute, xrows=xrows)
-        self.last_times = times
-        for k, name in enumerate(("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")):
-            prof[name] = float(times[k])
-        tr = time.perf_counter()
-        unsafe = (B.flags & FE_SAT_UNSAFE) != 0
-        first[unsafe & (first >= 0)] = -1  # no GPU SAT answer for those (mgp_front.cpp)
+        parts = self.min_groups if n >= self.GROUP_MIN_STATES else 1
+        groups = self._groups(nv, self.n_cand, -(-n // parts) if parts > 1 else 0) \
+            if n > 1 and (parts > 1 or n * self.n_cand * n_vars * 32 > self.cand_bytes) else [list(range(n))]
+        first = np.full(n, -1, np.int32)
+        proven = np.zeros(n, np.int8)
         witnesses: Dict[int, object] = {}
-        retry = [i for i in range(len(states)) if first[i] == -1 and proven[i] != 1]
-        if retry and self.retry_cand > 0:
-            self._retry_round(ctx, states, retry, first, witnesses, prof,
-                              None if parents is None else [parents[i] for i in retry])
-        prof["retry_ms"] = 1e3 * (time.perf_counter() - tr)
-        prof["retry_states"] = len(retry)
-        left = [i for i in range(len(states)) if first[i] < 0 and proven[i] != 1]
+        jobs = collections.deque(_Round("first", grp, B if len(groups) == 1 else B.select(grp), len(groups) > 1,
+                                        None if parents is None else [parents[i] for i in grp])
+                                 for grp in groups)
+        inflight: collections.deque = collections.deque()
+        try:
+            while jobs or inflight:
+                if jobs and len(inflight) < 2:
+                    job = jobs.popleft()
+                    self._submit_round(ctx, job, prof)
+                    inflight.append(job)
+                    continue
+                job = inflight.popleft()
+                jobs.extend(self._finish_round(job, first, proven, witnesses, prof))
+        finally:
+            for job in inflight:  # an error: drain what is in flight before the batches go
+                try:
+                    job.pending.finish()
+                except Exception:
+                    pass
+            for job in list(jobs) + list(inflight):
+                job.close()
+        left = [i for i in range(n) if first[i] < 0 and proven[i] != 1]
         if left and self.refute and self.split_refute > 0:
             ts = time.perf_counter()
-            LB = Batch([states[i] for i in left])
+            LB = B.select(left)
             rs = self._N.refute_split(*LB.packed()[:4], max_splits=self.split_refute, depth=self.split_depth)
             LB.close()
             for k, i in enumerate(left):
@@ -615,9 +620,7 @@ class Prefilter:
         tr = time.perf_counter()
         out: List[Tuple[str, Optional[object]]] = []
         refuted = []
-        first_round = [i for i in range(len(states)) if first[i] >= 0 and i not in witnesses]
-        witnesses.update(zip(first_round, B.witnesses(first_round, wit)))
-        for i in range(len(states)):
+        for i in range(n):
             if first[i] >= 0:
                 if proven[i] == 1:  # a witness and an UNSAT proof cannot both hold
                     raise RuntimeError(f"mgp_refute refuted state {i} that has a GPU witness (soundness bug)")
@@ -630,23 +633,122 @@ class Prefilter:
         B.close()
         prof["results_ms"] = 1e3 * (time.perf_counter() - tr)
         prof["cores_ms"] = 0.0
+        if len(groups) > 1:
+            prof["groups"] = len(groups)
         self.last_profile = prof
         self._tls.profile = prof
         return out, refuted
+
+    _STAGES = ("lower_ms", "refute_ms", "upload_launch_ms", "gpu_wait_ms", "copy_back_ms")
+
+    def _submit_round(self, ctx, job: "_Round", prof: dict) -> None:
+        """Host half of a witness round: its explicit rows (the first round's decision rows of
+        large states; the second round's decision rows), then mgp_check_submit."""
+        td = time.perf_counter()
+        if job.kind == "first":
+            xrows = self._first_round_rows(job.batch, job.parents, ctx)
+            if xrows is not None:
+                prof["rows_first_ms"] = prof.get("rows_first_ms", 0.0) + 1e3 * (time.perf_counter() - td)
+            job.pending = job.batch.submit(ctx, self.n_cand, self.seed, job.parents, refute=self.refute, xrows=xrows)
+            for name, t in zip(self._STAGES[:3], job.pending.times[:3]):
+                prof[name] = prof.get(name, 0.0) + float(t)
+        else:
+            rows, mask = self._decision_rows(self._rows_args(job.batch, job.parents), self._seed2())
+            prof["decide_host_ms"] = prof.get("decide_host_ms", 0.0) + 1e3 * (time.perf_counter() - td)
+            # (the second round's candidates carry no parent row: its decision rows are seeded
+            # with the parents' values instead, mgp_decision_rows_seeded)
+            job.pending = job.batch.submit(ctx, self._n2(), self._seed2(), refute=self.refute, xrows=(rows, mask))
+            r2 = prof.setdefault("round2_stages", {})
+            for name, t in zip(("lower", "refute", "upload_launch"), job.pending.times[:3]):
+                r2[name] = r2.get(name, 0.0) + float(t)
+        prof["pipelined_rounds"] = prof.get("pipelined_rounds", 0) + 1
+
+    def _finish_round(self, job: "_Round", first, proven, witnesses, prof) -> List["_Round"]:
+        """Collect a round's answers into first / proven / witnesses; a first round returns the
+        second round(s) for its open states (none when retry_cand is 0)."""
+        from .front import FE_SAT_UNSAFE
+
+        f, w, ref, times = job.pending.finish()
+        if job.kind == "first":
+            for name, t in zip(self._STAGES[3:], times[3:5]):
+                prof[name] = prof.get(name, 0.0) + float(t)
+        else:
+            r2 = prof.setdefault("round2_stages", {})
+            for name, t in zip(("gpu_wait", "copy_back"), times[3:5]):
+                r2[name] = r2.get(name, 0.0) + float(t)
+        tr = time.perf_counter()
+        unsafe = (job.batch.flags & FE_SAT_UNSAFE) != 0
+        G = job.idx
+        follow: List[_Round] = []
+        if job.kind == "first":
+            f = f.copy()
+            f[unsafe & (f >= 0)] = -1  # no GPU SAT answer for those (mgp_front.cpp)
+            for k, i in enumerate(G):
+                first[i] = f[k]
+                if ref[k] == 1:
+                    proven[i] = 1
+            sat_k = [k for k in range(len(G)) if f[k] >= 0]
+            for k, wt in zip(sat_k, job.batch.witnesses(sat_k, w)):
+                witnesses[G[k]] = wt
+            retry = [k for k in range(len(G)) if f[k] == -1 and ref[k] != 1]
+            prof["retry_states"] = prof.get("retry_states", 0) + len(retry)
+            if retry and self.retry_cand > 0:
+                SolverStatistics().gpu_retry += len(retry)
+                follow = self._retry_rounds(job, retry)
+        else:
+            found = 0
+            for k, i in enumerate(G):
+                if f[k] >= 0 and not unsafe[k]:
+                    first[i] = f[k]
+                    witnesses[i] = job.batch.witness(k, w[k])
+                    found += 1
+            prof["retry_sat"] = prof.get("retry_sat", 0) + found
+        job.close()
+        prof["collect_ms"] = prof.get("collect_ms", 0.0) + 1e3 * (time.perf_counter() - tr)
+        return follow
+
+    def _n2(self) -> int:
+        return max(64, self.retry_cand // 64 * 64)
+
+    def _seed2(self) -> int:
+        return (self.seed + 0x7F4A7C15) & (2 ** 64 - 1)
+
+    def _retry_rounds(self, job: "_Round", retry: List[int]) -> List["_Round"]:
+        """The second witness round of a first round's open states (local indices `retry`):
+        host decision rows (mgp_decision_rows, each variable fixed in turn and the analysis
+        re-propagated) placed in the first mixture rows of a device-generated round with a
+        new seed, one round per candidate-memory group.  A state with a parent witness gets
+        SEED_ROWS of its rows seeded with the parent's values (mgp_decision_rows_seeded):
+        the draws then only decide what the child's new constraint brought in."""
+        n2 = self._n2()
+        SB = job.batch.select(retry)
+        nv = np.diff(SB.var_off).astype(np.int64)
+        groups = self._groups(nv, n2) if len(retry) * n2 * max(1, int(nv.max())) * 32 > self.cand_bytes \
+            else [list(range(len(retry)))]
+        par = job.parents
+        out = []
+        for grp in groups:
+            GB = SB if len(groups) == 1 else SB.select(grp)
+            out.append(_Round("retry", [job.idx[retry[k]] for k in grp], GB, True,
+                              None if par is None else [par[retry[k]] for k in grp]))
+        if len(groups) > 1:
+            SB.close()
+        return out
 
     def flush_cores(self) -> None:
         """Shrink the pending refuted constraint lists to cores and store them (waits for
         a background shrink first)."""
         _cores.flush(self._N)
 
-    def _groups(self, nv: np.ndarray, n_cand: int) -> List[List[int]]:
-        """Indices grouped by variable count so that each group's candidate block fits cand_bytes."""
+    def _groups(self, nv: np.ndarray, n_cand: int, max_len: int = 0) -> List[List[int]]:
+        """Indices grouped by variable count so that each group's candidate block fits cand_bytes
+        (and, max_len > 0, each group holds at most max_len states)."""
         order = sorted(range(len(nv)), key=lambda i: (int(nv[i]), i))
         groups: List[List[int]] = []
         grp: List[int] = []
         for i in order:
             w = max(1, int(nv[i]))
-            if grp and (len(grp) + 1) * n_cand * w * 32 > self.cand_bytes:
+            if grp and ((len(grp) + 1) * n_cand * w * 32 > self.cand_bytes or 0 < max_len <= len(grp)):
                 groups.append(grp)
                 grp = []
             grp.append(i)
@@ -724,52 +826,20 @@ class Prefilter:
             raise out["error"]
         return out["rows"]
 
-    def _retry_round(self, ctx, states, retry, first, witnesses, prof=None, parents=None) -> None:
-        """The second witness round for the open states: host decision rows
-        (mgp_decision_rows, each variable fixed in turn and the analysis re-propagated)
-        placed in the first mixture rows of a device-generated round with a new seed.  A
-        state with a parent witness gets SEED_ROWS of its rows seeded with the parent's
-        values (mgp_decision_rows_seeded): the draws then only decide what the child's new
-        constraint brought in."""
-        from .front import FE_SAT_UNSAFE, Batch
 
-        prof = {} if prof is None else prof
-        n2 = max(64, self.retry_cand // 64 * 64)
-        seed2 = (self.seed + 0x7F4A7C15) & (2 ** 64 - 1)
-        SB = Batch([states[i] for i in retry])
-        nv = np.diff(SB.var_off).astype(np.int64)
-        groups = self._groups(nv, n2) if len(retry) * n2 * max(1, int(nv.max())) * 32 > self.cand_bytes \
-            else [list(range(len(retry)))]
-        if len(groups) > 1:
-            SB.close()
-        t_dec = time.perf_counter()
-        dec_ms = 0.0
-        found = 0
-        round2_ms = [0.0] * 5  # the second round's check_batch stages (lower, refute, upload, GPU, copy)
-        for grp in groups:
-            # one group (the usual case): the batch built for the grouping is the round's batch
-            GB = SB if len(groups) == 1 else Batch([states[retry[k]] for k in grp])
-            gv = max(1, GB.n_vars())
-            td = time.perf_counter()
-            par = None if parents is None else [parents[j] for j in grp]
-            rows, mask = self._decision_rows(self._rows_args(GB, par), seed2)
-            dec_ms += 1e3 * (time.perf_counter() - td)
-            f2, w2, _, st2 = GB.check(ctx, n2, seed2, refute=self.refute, xrows=(rows, mask))
-            round2_ms = [a + float(b) for a, b in zip(round2_ms, st2)]
-            unsafe = (GB.flags & FE_SAT_UNSAFE) != 0
-            for k, j in enumerate(grp):
-                i = retry[j]
-                if f2[k] >= 0 and not unsafe[k]:
-                    first[i] = f2[k]
-                    witnesses[i] = GB.witness(k, w2[k])
-                    found += 1
-            GB.close()
-        prof["decide_host_ms"] = dec_ms
-        prof["round2_stages"] = dict(zip(("lower", "refute", "upload_launch", "gpu_wait", "copy_back"), round2_ms))
-        prof["decide_ms"] = 1e3 * (time.perf_counter() - t_dec)  # host decision rows + their GPU round
-        prof["decide_states"] = len(retry)
-        prof["retry_sat"] = found
-        SolverStatistics().gpu_retry += len(retry)
+class _Round:
+    """One witness round of a Prefilter batch: the global indices of its states, their
+    batch (owned: closed once the round is collected), their parent witnesses and, once
+    submitted, the pending GPU round."""
+
+    def __init__(self, kind: str, idx: List[int], batch, owned: bool, parents):
+        self.kind, self.idx, self.batch, self.owned, self.parents = kind, idx, batch, owned, parents
+        self.pending = None
+
+    def close(self) -> None:
+        if self.owned and self.batch is not None:
+            self.batch.close()
+        self.batch = None
 
 
 def _sum_profiles(profs: List[dict]) -> dict:

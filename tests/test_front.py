@@ -5,6 +5,7 @@ strengthening and witness decoding must be identical (CPU only)."""
 import numpy as np
 import pytest
 
+from mythril_amd import _native as N
 from mythril_amd import dag as D
 from mythril_amd import front as F
 from corpus.keccak_manager import KeccakFunctionManager
@@ -117,3 +118,32 @@ def test_mixed_corpus_with_pinned_constants():
         if d.gpu_nodes is not None and d.flags & 4:
             front = [n for n in d.gpu_nodes[: len(d.gpu_nodes) - len(d.nodes)]]
             assert all(n[0] == 1 for n in front) and {n[5] for n in front} <= set(d.pinned)
+
+
+def test_select_equals_a_build_of_the_selected_states():
+    """Batch.select (mgp_fe_select, how Prefilter cuts its candidate-memory groups and retry
+    rounds out of one build): every field equals a fresh build of the selected states --
+    permuted, repeated and pinned states, an empty selection, a select of a select."""
+    import corpus
+
+    cs = [c[1] for c in corpus.corpus(96)]
+    B = F.Batch(cs)
+    assert (B.flags & 4).any() and not (B.flags & 4).all()  # pinned and unpinned states
+    picks = [list(range(0, 96, 3)), [95, 2, 2, 40, 7], [int(i) for i in np.random.default_rng(3).permutation(96)],
+             [], [i for i in range(96) if not B.flags[i] & 6]]
+    for idx in picks:
+        S, R = B.select(idx), F.Batch([cs[i] for i in idx])
+        for name in F._FIELDS:
+            assert np.array_equal(getattr(S, name), getattr(R, name)), (name, idx[:6])
+        if idx:
+            sub = list(range(len(idx)))[::-2]
+            S2, R2 = S.select(sub), F.Batch([cs[idx[k]] for k in sub])
+            for name in F._FIELDS:
+                assert np.array_equal(getattr(S2, name), getattr(R2, name)), name
+            S2.close()
+            R2.close()
+        S.close()
+        R.close()
+    with pytest.raises(N.MgpError):
+        B.select([96])
+    B.close()

@@ -144,3 +144,44 @@ def test_corpus_undecided_equals_cpu_restatement(clean):
         assert not (exp == "unsat" and k == SV.sat) and not (exp == "sat" and k == SV.unsat), lab
     assert sum(1 for (_, _, e), k in zip(C, kinds) if e == "unsat" and k == SV.unsat) == \
         sum(1 for _, _, e in C if e == "unsat")
+
+
+def test_submit_finish_equals_check_batch(mgp_ctx):
+    """mgp_check_submit / mgp_check_finish (two rounds in flight on one context, finished in
+    order) give what mgp_check_batch gives for each batch; a third submit is refused while
+    two are in flight, and the context works on afterwards."""
+    cs = [c[1] for c in _corpus(200)]
+    B1, B2 = F.Batch(cs[:120]), F.Batch(cs[120:])
+    want = [B.check(mgp_ctx, 256, 99) for B in (B1, B2)]
+    p1 = B1.submit(mgp_ctx, 256, 99)
+    p2 = B2.submit(mgp_ctx, 256, 99)
+    with pytest.raises(N.MgpError):
+        B1.submit(mgp_ctx, 256, 99)
+    got = [p1.finish(), p2.finish()]
+    for (f, w, r, _), (gf, gw, gr, _) in zip(want, got):
+        assert np.array_equal(f, gf) and np.array_equal(r, gr)
+        sat = f >= 0
+        assert np.array_equal(w[sat], gw[sat])
+    f3 = B2.check(mgp_ctx, 256, 99)[0]
+    assert np.array_equal(f3, want[1][0])
+    B1.close()
+    B2.close()
+
+
+def test_grouped_pipelined_call_answers_like_one_group(clean):
+    """A call cut into several candidate-memory groups (Batch.select of the one build), their
+    first and second rounds pipelined two in flight: the same answers and witnesses as the
+    call in one group."""
+    pf = SV.Prefilter(0)
+    try:
+        cs = [c[1] for c in _corpus(300)]
+        a = pf.check_states(cs)
+        assert pf.last_profile.get("groups", 1) == 1
+        SV.unsat_cores().reset()
+        pf.cand_bytes = 48 * pf.n_cand * 64 * 32
+        b = pf.check_states(cs)
+        assert pf.last_profile.get("groups", 1) >= 3
+        assert pf.last_profile["pipelined_rounds"] > pf.last_profile["groups"]
+        _same_answers(a, b)
+    finally:
+        pf.close()

@@ -187,6 +187,7 @@ class Checker:
         self.budget = budget
         self.steps = 0
         self.creep: Dict[int, int] = {}
+        self.atom_node: Dict = {}
         self.av: List = [None] * self.n
         self.pairs: List[int] = [OALL] * len(self.pair_xy)
         for i, t in enumerate(order):
@@ -700,6 +701,7 @@ class Checker:
         other node is an atom of its own.  None for Bool nodes."""
         forms: List = [None] * self.n
         av = self.av
+        self.atom_node: Dict = {}
         # a compared pair known equal: the later node takes the earlier one's form
         rep: Dict[int, int] = {}
         for p, (x, y, _) in enumerate(self.pair_xy):
@@ -730,7 +732,9 @@ class Checker:
                         break
             elif op in (S.UFAPP, S.UFINV):
                 fa = forms[ar[0]]
-                f = (0, {("u", op, repr(t.params), _form_key(fa) if fa is not None else ("n", ar[0])): 1})
+                key = ("u", op, repr(t.params), _form_key(fa) if fa is not None else ("n", ar[0]))
+                self.atom_node.setdefault(key, i)
+                f = (0, {key: 1})
             if f is None or len(f[1]) > 24:
                 f = (0, {("n", i): 1})
             j = rep.get(i)
@@ -742,12 +746,35 @@ class Checker:
             forms[i] = f
         return forms
 
+    def _diff_range(self, d, m: int):
+        """The integer range of a difference form d = k + sum(c * atom) with every atom in its
+        interval (a coefficient above m / 2 counts as negative), or None if it leaves [0, m]."""
+        lo = hi = d[0]
+        for key, c in d[1].items():
+            i = key[1] if key[0] == "n" else self.atom_node.get(key)
+            if i is None:
+                return None
+            a = self.av[i]
+            if c <= m // 2:
+                lo += c * a[0]
+                hi += c * a[1]
+            else:
+                c = m + 1 - c
+                lo -= c * a[1]
+                hi -= c * a[0]
+        if lo < 0 or hi > m:
+            return None
+        return lo, hi
+
     def linear(self, work: List[int]) -> None:
         """Compares whose operands' forms differ by a constant k: x = y + k mod 2^w, so x > y
         iff k != 0 and y + k does not wrap (y <= 2^w - 1 - k), x < y iff it wraps, x == y iff
         k == 0.  That bounds the pair's orderings (and so the compare's truth, open or not) by
         y's interval; a compare required true or false narrows y's interval to the side it
-        needs (or empties the branch)."""
+        needs (or empties the branch).  A difference that is not constant but whose atoms'
+        intervals keep it inside [lo, hi] within [0, 2^w - 1] (x = y + D, D in [lo, hi]) bounds
+        the orderings the same way: "=" only if lo == 0, ">" if y + max(lo, 1) can stay below
+        2^w, "<" only if y + hi can wrap (either operand order)."""
         forms = self._forms()
         av = self.av
         for i, (p, sw, signed) in self.cmp_pair.items():
@@ -758,22 +785,39 @@ class Checker:
             w = self.w[x]
             m = _mask(w)
             d = _lin_add(fx, fy, -1, m)
-            if d[1]:
-                continue
-            k = d[0]
-            if k == 0:
-                poss = OEQ
+            k = None
+            if not d[1]:
+                k = d[0]
+                if k == 0:
+                    poss = OEQ
+                elif signed:
+                    poss = OLT | OGT
+                else:
+                    yv = av[y]
+                    poss = (OGT if yv[0] <= m - k else 0) | (OLT if yv[1] > m - k else 0)
             elif signed:
-                poss = OLT | OGT
+                continue
             else:
-                yv = av[y]
-                poss = (OGT if yv[0] <= m - k else 0) | (OLT if yv[1] > m - k else 0)
+                r = self._diff_range(d, m)
+                flip = False
+                if r is None:
+                    r = self._diff_range(_lin_scale(d, m, m), m)   # y - x
+                    flip = True
+                    if r is None:
+                        continue
+                lo, hi = r
+                b = av[x] if flip else av[y]   # the operand D is added to
+                poss = (OEQ if lo == 0 else 0) | \
+                    (OGT if hi > 0 and b[0] + max(lo, 1) <= m else 0) | \
+                    (OLT if b[1] + hi > m else 0)
+                if flip:
+                    poss = _swap(poss)
             self._set_pair(p, _swap(poss) if sw else poss, work)
             op = self.t[i].op
             t_ord = OGT | OEQ if op == S.USUB_NOUDF else _TRUE_ORD[op]
             self._set(i, (BT if poss & t_ord else 0) | (BF if poss & ~t_ord & OALL else 0), work)
             v = av[i]
-            if k == 0 or signed or v not in (BT, BF):
+            if k is None or k == 0 or signed or v not in (BT, BF):
                 continue
             want = (t_ord if v == BT else OALL & ~t_ord) & (OLT | OGT)
             if want == OGT:      # y + k must not wrap

@@ -1,6 +1,6 @@
 """Replay every refutation of the restated suite with the independent checker.
 
-    python scripts/replay_refutations.py [out.json] [--workers N]
+    python scripts/replay_refutations.py [out.json] [--workers N] [--tier1]
 
 For every query of corpus.suite() (all 13 contracts) that the product's split refuter refutes
 at the product's settings (mgp_refute_split, Prefilter.SPLIT_REFUTE / SPLIT_DEPTH), the
@@ -32,19 +32,24 @@ _Q = None
 _CORES = None
 
 
+_TIERS = None
+
+
 def _one(k):
     t = time.perf_counter()
-    ok = RC.refute(_CORES[k])
+    ok = RC.refute(_CORES[k], tiers=_TIERS)
     return k, bool(ok), time.perf_counter() - t
 
 
 def main():
-    global _Q, _CORES
+    global _Q, _CORES, _TIERS
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     out_path = args[0] if args else "profiles/refute_replay_r6.json"
     workers = 7
     if "--workers" in sys.argv:
         workers = int(sys.argv[sys.argv.index("--workers") + 1])
+    if "--tier1" in sys.argv:   # the cheap search alone (a quick look)
+        _TIERS = RC.TIERS[:1]
     t0 = time.perf_counter()
     qs = corpus.suite(hasher=keccak256)
     B = F.Batch([list(q[3]) for q in qs])
@@ -74,7 +79,7 @@ def main():
     tot = {"queries": len(qs), "refuted": len(refuted), "replayed": sum(ok for _, ok, _ in res),
            "core_constraints_mean": float(np.mean([len(cores[k]) for k in refuted])) if refuted else 0.0,
            "suite_seconds": round(t_suite, 1), "replay_seconds": round(time.perf_counter() - t1, 1),
-           "workers": workers, "tiers": [list(t) for t in RC.TIERS],
+           "workers": workers, "tiers": [list(t) for t in (_TIERS or RC.TIERS)],
            "state_seconds_max": round(max(secs), 2) if secs else 0.0}
     blob = {"all": tot, "by_contract": {c: {**v, "unreplayed_kinds": dict(collections.Counter(
         lab.split(":")[1].split("@")[0] for lab in v["unreplayed"]))} for c, v in sorted(by.items())}}

@@ -184,6 +184,19 @@ class Checker:
             if 1 < len(apps) <= 64:
                 for i in apps:
                     self.uf_peers[i] = [j for j in apps if j != i]
+        # injective applications: f(x) with the keccak manager's inverse axiom
+        # f^-1(f(x)) == x among the constraints (keccak_function_manager.py:102-146); while
+        # the axiom node holds, f(x) == f(y) implies x == y
+        self.inj: Dict[object, List[Tuple[int, int]]] = {}
+        for e, t in enumerate(order):
+            if t.op != S.EQ or len(self.args[e]) != 2:
+                continue
+            for u, x in (self.args[e], self.args[e][::-1]):
+                tu = order[u]
+                if tu.op == S.UFINV and order[self.args[u][0]].op == S.UFAPP:
+                    a = self.args[u][0]
+                    if self.args[a][0] == x and order[a].params[0] == tu.params[0]:
+                        self.inj.setdefault(tu.params[0], []).append((a, e))
         self.budget = budget
         self.steps = 0
         self.creep: Dict[int, int] = {}
@@ -777,6 +790,7 @@ class Checker:
         2^w, "<" only if y + hi can wrap (either operand order)."""
         forms = self._forms()
         av = self.av
+        self._injective(forms, work)
         for i, (p, sw, signed) in self.cmp_pair.items():
             x, y = self.args[i]
             fx, fy = forms[x], forms[y]
@@ -826,6 +840,51 @@ class Checker:
                 self._set(y, (m - k + 1, m, 0, 0), work)
             elif not want:
                 raise Empty
+
+    def _differ(self, a: int, b: int, forms) -> bool:
+        """Nodes a and b can never be equal: their forms differ by a non-zero constant, their
+        compared pair excludes "=", or their abstract values cannot meet."""
+        if a == b:
+            return False
+        fa, fb = forms[a], forms[b]
+        if fa is not None and fb is not None:
+            d = _lin_add(fa, fb, -1, _mask(self.w[a]))
+            if not d[1]:
+                return d[0] != 0
+        if not self._pair_ord(a, b) & OEQ:
+            return True
+        return not self._orders(self.av[a], self.av[b], self.w[a], False) & OEQ
+
+    def _injective(self, forms, work: List[int]) -> None:
+        """Two applications of an injective function (inverse axiom required true): equal
+        values with different arguments empty the branch; different arguments exclude "=" from
+        every compare of one application with a value the other is known to equal; equal
+        values make the arguments equal."""
+        av = self.av
+        for apps in self.inj.values():
+            live = [a for a, e in apps if av[e] == BT]
+            for x in range(len(live)):
+                for y in range(x + 1, len(live)):
+                    i, j = live[x], live[y]
+                    ai, aj = self.args[i][0], self.args[j][0]
+                    same_val = (_is_exact(av[i]) and av[i] == av[j]) or self._pair_ord(i, j) == OEQ
+                    if self._differ(ai, aj, forms):
+                        if same_val:
+                            raise Empty
+                        for k, o in ((i, j), (j, i)):
+                            if not _is_exact(av[o]):
+                                continue
+                            for c in self.users[k]:
+                                cp = self.cmp_pair.get(c)
+                                if cp is None:
+                                    continue
+                                other = [z for z in self.args[c] if z != k]
+                                if other and _is_exact(av[other[0]]) and av[other[0]][0] == av[o][0]:
+                                    pp, sw, _ = cp
+                                    self._set_pair(pp, OALL & ~OEQ, work)
+                    elif same_val and self.w[ai] == self.w[aj]:
+                        self._set(ai, av[aj], work)
+                        self._set(aj, av[ai], work)
 
     def saturate(self, seeds: Optional[List[int]] = None, rounds: int = 4) -> None:
         """propagate, then the linear pass and propagation again while it narrows something."""

@@ -618,6 +618,45 @@ def test_structural_congruence_exhaustive_soundness():
     assert refuted[0] > 0.8 * n_form[0] and refuted[1] > 0.8 * n_form[1], (refuted, n_form)
 
 
+def _injective_state(rng, w=3):
+    """Applications f(a) with their inverse asserted (inv(f(a)) == a, as the keccak manager
+    asserts) -- direct or through Concat(x, c) arguments of twice the width -- with compares
+    between the values and between the arguments (six variables: two w-bit variables, two
+    application values, two inverse values)."""
+    nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
+    cl = [int(rng.integers(0, 8)) for _ in range(2)]
+    nl += [[S.CONST, w, -1, -1, -1, 0, 0], [S.CONST, w, -1, -1, -1, 1, 0]]
+    bools, apps = [], []
+    wide = rng.random() < 0.5
+    for k in range(2):
+        a = int(rng.choice([0, 1, 2, 3]))
+        if wide:
+            nl.append([S.CONCAT, 2 * w, a, 2, -1, 0, 0])
+            a = len(nl) - 1
+        nl.append([S.UFAPP, w, a, -1, -1, 7 if wide else 5, 2 + k])
+        u = len(nl) - 1
+        if rng.random() < 0.85:      # the manager's inv(f(x)) == x
+            nl.append([S.UFINV, 2 * w if wide else w, u, -1, -1, 7 if wide else 5, 4 + k])
+            nl.append([S.EQ, 1, len(nl) - 1, a, -1, 0, 0])
+            bools.append(len(nl) - 1)
+        apps.append((u, a))
+    (u0, a0), (u1, a1) = apps
+    nl.append([S.EQ, 1, u0, u1, -1, 0, 0])
+    bools.append(len(nl) - 1)
+    if rng.random() < 0.6:          # the arguments differ
+        nl.append([S.EQ, 1, a0, a1, -1, 0, 0])
+        nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+        bools.append(len(nl) - 1)
+    if rng.random() < 0.5:
+        nl.append([[S.ULT, S.EQ, S.UGT][int(rng.integers(3))], 1, int(rng.choice([0, 1])), 3, -1, 0, 0])
+        bools.append(len(nl) - 1)
+    root = bools[0]
+    for b in bools[1:]:
+        nl.append([S.BAND, 1, root, b, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl
+
+
 def test_injectivity_exhaustive_soundness():
     """Applications f(a) with their inverse asserted (inv(f(a)) == a, as the keccak manager
     asserts for every application) -- direct, and through Concat(x, c) arguments of twice the
@@ -626,40 +665,7 @@ def test_injectivity_exhaustive_soundness():
     the injectivity rule (Dom::injective) refutes `f(a) == f(b) and a != b`."""
     rng = np.random.default_rng(0x1A1)
     w = 3
-    states = []
-    for _ in range(240):
-        nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
-        cl = [int(rng.integers(0, 8)) for _ in range(2)]
-        nl += [[S.CONST, w, -1, -1, -1, 0, 0], [S.CONST, w, -1, -1, -1, 1, 0]]
-        bools, apps = [], []
-        wide = rng.random() < 0.5
-        for k in range(2):
-            a = int(rng.choice([0, 1, 2, 3]))
-            if wide:
-                nl.append([S.CONCAT, 2 * w, a, 2, -1, 0, 0])
-                a = len(nl) - 1
-            nl.append([S.UFAPP, w, a, -1, -1, 7 if wide else 5, 2 + k])
-            u = len(nl) - 1
-            if rng.random() < 0.85:      # the manager's inv(f(x)) == x
-                nl.append([S.UFINV, 2 * w if wide else w, u, -1, -1, 7 if wide else 5, 4 + k])
-                nl.append([S.EQ, 1, len(nl) - 1, a, -1, 0, 0])
-                bools.append(len(nl) - 1)
-            apps.append((u, a))
-        (u0, a0), (u1, a1) = apps
-        nl.append([S.EQ, 1, u0, u1, -1, 0, 0])
-        bools.append(len(nl) - 1)
-        if rng.random() < 0.6:          # the arguments differ
-            nl.append([S.EQ, 1, a0, a1, -1, 0, 0])
-            nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
-            bools.append(len(nl) - 1)
-        if rng.random() < 0.5:
-            nl.append([[S.ULT, S.EQ, S.UGT][int(rng.integers(3))], 1, int(rng.choice([0, 1])), 3, -1, 0, 0])
-            bools.append(len(nl) - 1)
-        root = bools[0]
-        for b in bools[1:]:
-            nl.append([S.BAND, 1, root, b, -1, 0, 0])
-            root = len(nl) - 1
-        states.append((nl, cl))
+    states = [_injective_state(rng, w) for _ in range(240)]
     verdict = _refute(states)
     n_vars = 6
     grid = np.array(np.meshgrid(*[np.arange(8)] * n_vars, indexing="ij")).reshape(n_vars, -1).T

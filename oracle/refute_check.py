@@ -715,6 +715,7 @@ class Checker:
         forms: List = [None] * self.n
         av = self.av
         self.atom_node: Dict = {}
+        self.steps += self.n // 4   # a pass over the DAG counts against the step budget
         # a compared pair known equal: the later node takes the earlier one's form
         rep: Dict[int, int] = {}
         for p, (x, y, _) in enumerate(self.pair_xy):
@@ -1021,7 +1022,7 @@ def _order_bounds(a, b, want: int):
     return None, None
 
 
-TIERS = ((2, 8, 20000), (3, 8, 300000))   # (split depth, atoms per level, step budget)
+TIERS = ((2, 8, 60000), (3, 8, 600000))   # (split depth, atoms per level, step budget)
 
 
 def refute(roots: Sequence, depth: int = 0, max_atoms: int = 8, budget: int = 0, tiers=None) -> bool:

@@ -94,15 +94,15 @@ def _suite(names):
 
 
 def test_checker_never_refutes_a_witnessed_suite_query():
-    """Queries of calls.sol / returnvalue.sol that the CPU restatement of the witness rounds
-    answers with a model (C-oracle checked) are never re-proved UNSAT by the checker."""
+    """Queries of returnvalue.sol that the CPU restatement of the witness rounds answers with a
+    model (C-oracle checked) are never re-proved UNSAT by the checker."""
     from tests import fe_emulate as E
 
-    qs = _suite(["calls", "returnvalue"])
+    qs = _suite(["returnvalue"])
     ans, _ = E.suite_answers(qs, witnesses=True)
     sat = [k for k, a in enumerate(ans) if a == "sat"]
-    assert len(sat) > 50
-    for k in sat[::max(1, len(sat) // 60)]:
+    assert len(sat) > 30
+    for k in sat[::max(1, len(sat) // 40)]:
         assert not RC.refute(list(qs[k][3]), tiers=((2, 8, 5000),)), qs[k][2]
 
 

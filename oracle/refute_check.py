@@ -528,14 +528,12 @@ class Checker:
             return
         if op == S.CONCAT:
             wb = self.w[ar[1]]
-            wa = self.w[ar[0]]
             mb = _mask(wb)
             self._set(ar[0], (v[0] >> wb, v[1] >> wb, v[2] >> wb, v[3] >> wb), work)
             if (v[0] >> wb) == (v[1] >> wb):
                 self._set(ar[1], (v[0] & mb, v[1] & mb, v[2] & mb, v[3] & mb), work)
             else:
                 self._set(ar[1], (0, mb, v[2] & mb, v[3] & mb), work)
-            del wa
             return
         if len(ar) < 2:
             return

@@ -28,10 +28,7 @@ from mythril_amd.solver import Prefilter  # noqa: E402
 from oracle import refute_check as RC  # noqa: E402
 from oracle.keccak_ref import keccak256  # noqa: E402
 
-_Q = None
-_CORES = None
-
-
+_CORES = None   # refuted query index -> its core (inherited by the forked workers)
 _TIERS = None
 
 
@@ -42,7 +39,7 @@ def _one(k):
 
 
 def main():
-    global _Q, _CORES, _TIERS
+    global _CORES, _TIERS
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     out_path = args[0] if args else "profiles/refute_replay_r6.json"
     workers = 7
@@ -62,7 +59,7 @@ def main():
     for k in refuted:
         cs = list(qs[k][3])
         cores[k] = [c for c, m in zip(cs, keep[k]) if m] if st[k] == 1 else cs
-    _Q, _CORES = qs, cores
+    _CORES = cores
     t_suite = time.perf_counter() - t0
     t1 = time.perf_counter()
     with mp.get_context("fork").Pool(workers) as pool:

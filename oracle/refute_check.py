@@ -1049,7 +1049,8 @@ def _refute_once(roots: Sequence, depth: int, max_atoms: int, budget: int) -> bo
     if _split(C, depth, max_atoms):
         return True
     C.restore(base)
-    return C.steps <= C.budget and _bisect(C, BISECT_LEVELS)
+    C.steps = 0   # the bisection gets a budget of its own
+    return _bisect(C, BISECT_LEVELS)
 
 
 BISECT_LEVELS = 8

@@ -587,11 +587,28 @@ class Checker:
             else:  # r = a << s: a's bits 0..w-s are r's bits s..
                 self._set(ar[0], (0, m, v[2] >> s, v[3] >> s), work)
             return
-        if op == S.MUL and _is_exact(b) and b[0] > 0 and v[1] < m:
-            # a * c = r with r < 2^w: if a * c never wraps below r's ceiling, a <= r.hi / c
-            c = b[0]
-            if a[1] * c <= m:
-                self._set(ar[0], ((v[0] + c - 1) // c, v[1] // c, 0, 0), work)
+        if op == S.MUL:
+            # x * c = r (mod 2^w) with c exact: x * c = j * 2^w + r for some wrap count j, so
+            # x lies in the union over j of [(j * 2^w + r.lo) / c, (j * 2^w + r.hi) / c]
+            # (rounded inwards) within x's interval; x gets the hull of the non-empty pieces
+            for x, y in ((0, 1), (1, 0)):
+                o = av[ar[y]]
+                if not _is_exact(o) or o[0] == 0:
+                    continue
+                c, xv = o[0], av[ar[x]]
+                j0, j1 = xv[0] * c >> w, xv[1] * c >> w
+                if j1 - j0 > 64:
+                    continue
+                lo = hi = None
+                for j in range(j0, j1 + 1):
+                    plo = max(xv[0], -(-((j << w) + v[0]) // c))
+                    phi = min(xv[1], ((j << w) + v[1]) // c)
+                    if plo <= phi:
+                        lo = plo if lo is None else lo
+                        hi = phi
+                if lo is None:
+                    raise Empty
+                self._set(ar[x], (lo, hi, 0, 0), work)
             return
 
     def _or_of_compares(self, ar, work: List[int]) -> None:
@@ -1056,19 +1073,19 @@ def _refute_once(roots: Sequence, depth: int, max_atoms: int, budget: int) -> bo
 BISECT_LEVELS = 8
 
 
-def _bisect(C: Checker, levels: int, max_vars: int = 3) -> bool:
-    """Interval bisection: a variable whose interval the propagation bounded is cut in
-    halves, each half propagated (with the linear pass), `levels` deep; refuted when every
+def _bisect(C: Checker, levels: int, max_vars: int = 4) -> bool:
+    """Interval bisection: a node (a variable, a calldata word, ...) whose interval the
+    propagation bounded is cut in halves, each half propagated (with the linear pass), `levels` deep; refuted when every
     leaf empties.  Bit-length midpoints first (a range over several orders of magnitude), then
     arithmetic ones."""
     cands = []
     for i in range(C.n):
-        if C.t[i].op == S.VAR and not C.isb[i]:
+        if C.t[i].op not in (S.CONST, S.ITE) and not C.isb[i]:
             lo, hi = C.av[i][0], C.av[i][1]
             if lo != hi and (lo > 0 or hi < _mask(C.w[i])):
-                cands.append((hi - lo, i))
+                cands.append((C.t[i].op != S.VAR, hi - lo, i))   # variables first
     base = C.snapshot()
-    for _, i in sorted(cands)[:max_vars]:
+    for _, _, i in sorted(cands)[:max_vars]:
         if _halves(C, i, levels):
             return True
         C.restore(base)

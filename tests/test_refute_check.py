@@ -13,7 +13,7 @@ from oracle import coracle
 from oracle import refute_check as RC
 
 from ._util import pack_states
-from .test_refute import _injective_state, _random_small_dag, _ratio_state, _refund_state, _transfer_chain_state
+from .test_refute import _injective_state, _random_mul_dag, _random_small_dag, _ratio_state, _refund_state, _transfer_chain_state
 
 
 def _terms(nodes, consts):
@@ -47,11 +47,11 @@ def _no_model(state, n_vars, w):
     return coracle.first_sat(*pack_states([state]), cands)[0] < 0
 
 
-@pytest.mark.parametrize("shape", ["random", "transfer", "refund", "ratio", "injective"])
+@pytest.mark.parametrize("shape", ["random", "transfer", "refund", "ratio", "injective", "mul"])
 def test_checker_is_sound_exhaustively(shape):
     """Every state the checker re-proves UNSAT has no model over all assignments of its
     variables (and UF application values), and it re-proves a real share of them."""
-    rng = np.random.default_rng({"random": 0xC4EC, "transfer": 0x7A5F, "refund": 0x4EF0, "ratio": 0x2A71, "injective": 0x1A1}[shape])
+    rng = np.random.default_rng({"random": 0xC4EC, "transfer": 0x7A5F, "refund": 0x4EF0, "ratio": 0x2A71, "injective": 0x1A1, "mul": 0x30DE}[shape])
     if shape == "random":
         states = [(_random_small_dag(rng, w=4, n_ops=int(rng.integers(4, 14))), 2, 4) for _ in range(300)]
     elif shape == "transfer":
@@ -60,8 +60,10 @@ def test_checker_is_sound_exhaustively(shape):
         states = [(_refund_state(rng), 4, 3) for _ in range(300)]
     elif shape == "ratio":   # rubixi.sol's payout ratios (interval bisection)
         states = [(_ratio_state(rng), 2, 8) for _ in range(150)]
-    else:   # keccak applications with the manager's inverse axiom (injectivity)
+    elif shape == "injective":   # keccak applications with the manager's inverse axiom
         states = [(_injective_state(rng), 6, 3) for _ in range(150)]
+    else:   # products by constants, wrapping (BECToken's cnt * value)
+        states = [(_random_mul_dag(rng, 6), 2, 6) for _ in range(300)]
     proved = 0
     for st, n_vars, w in states:
         if RC.refute([_terms(*st)], tiers=((2, 8, 20000),)):

@@ -184,6 +184,12 @@ class Checker:
             if 1 < len(apps) <= 64:
                 for i in apps:
                     self.uf_peers[i] = [j for j in apps if j != i]
+        # BVAddNoOverflow nodes by their (unordered) operand pair
+        self.noovf: Dict[Tuple[int, int], int] = {}
+        for i, t in enumerate(order):
+            if t.op == S.UADD_NOOVF and len(self.args[i]) == 2:
+                a, b = self.args[i]
+                self.noovf[(min(a, b), max(a, b))] = i
         # injective applications: f(x) with the keccak manager's inverse axiom
         # f^-1(f(x)) == x among the constraints (keccak_function_manager.py:102-146); while
         # the axiom node holds, f(x) == f(y) implies x == y
@@ -836,10 +842,22 @@ class Checker:
                     if r is None:
                         continue
                 lo, hi = r
-                b = av[x] if flip else av[y]   # the operand D is added to
+                base = x if flip else y   # the operand D is added to
+                b = av[base]
                 poss = (OEQ if lo == 0 else 0) | \
                     (OGT if hi > 0 and b[0] + max(lo, 1) <= m else 0) | \
                     (OLT if b[1] + hi > m else 0)
+                # D is one node d and BVAddNoOverflow(base, d) is decided: the sum wraps (x < y)
+                # or it does not (x >= y) -- bitvec_helper.py's SafeMath-style overflow checks
+                dd = _lin_scale(d, m, m) if flip else d
+                if dd[0] == 0 and len(dd[1]) == 1:
+                    (key, coef), = dd[1].items()
+                    if coef == 1 and key[0] == "n":
+                        t = self.noovf.get((min(base, key[1]), max(base, key[1])))
+                        if t is not None and av[t] == BT:
+                            poss &= OGT | OEQ
+                        elif t is not None and av[t] == BF:
+                            poss &= OLT
                 if flip:
                     poss = _swap(poss)
             self._set_pair(p, _swap(poss) if sw else poss, work)

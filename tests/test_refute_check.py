@@ -40,6 +40,32 @@ def _terms(nodes, consts):
     return out[-1]
 
 
+def _safemath_state(rng, w=4):
+    """SafeMath.add's shapes (BECToken.sol): s = a + b (either operand order) compared with one
+    of its operands, next to BVAddNoOverflow(a, b) or its negation and a bound on b."""
+    nl = [[S.VAR, w, -1, -1, -1, 0, 0], [S.VAR, w, -1, -1, -1, 1, 0]]
+    cl = [int(rng.integers(0, 1 << w)) for _ in range(2)]
+    nl += [[S.CONST, w, -1, -1, -1, 0, 0], [S.CONST, w, -1, -1, -1, 1, 0]]        # 2, 3
+    nl.append([S.ADD, w, 0, 1, -1, 0, 0] if rng.random() < 0.5 else [S.ADD, w, 1, 0, -1, 0, 0])  # 4
+    bools = []
+    nl.append([S.UADD_NOOVF, 1, 0, 1, -1, 0, 0] if rng.random() < 0.5 else [S.UADD_NOOVF, 1, 1, 0, -1, 0, 0])
+    bools.append(len(nl) - 1)
+    if rng.random() < 0.5:
+        nl.append([S.BNOT, 1, len(nl) - 1, -1, -1, 0, 0])
+        bools.append(len(nl) - 1)
+    op = [S.UGE, S.UGT, S.ULT, S.ULE, S.EQ][int(rng.integers(5))]
+    nl.append([op, 1, 4, int(rng.choice([0, 1])), -1, 0, 0])
+    bools.append(len(nl) - 1)
+    if rng.random() < 0.5:
+        nl.append([[S.ULT, S.UGT, S.EQ][int(rng.integers(3))], 1, 1, int(rng.choice([2, 3])), -1, 0, 0])
+        bools.append(len(nl) - 1)
+    root = bools[-1]
+    for b in bools[-4:-1][::-1]:
+        nl.append([S.BAND, 1, root, b, -1, 0, 0])
+        root = len(nl) - 1
+    return nl, cl
+
+
 def _no_model(state, n_vars, w):
     grid = np.array(np.meshgrid(*[np.arange(1 << w)] * n_vars, indexing="ij")).reshape(n_vars, -1).T
     cands = np.zeros((1, grid.shape[0], n_vars, 8), np.uint32)
@@ -47,11 +73,11 @@ def _no_model(state, n_vars, w):
     return coracle.first_sat(*pack_states([state]), cands)[0] < 0
 
 
-@pytest.mark.parametrize("shape", ["random", "transfer", "refund", "ratio", "injective", "mul"])
+@pytest.mark.parametrize("shape", ["random", "transfer", "refund", "ratio", "injective", "mul", "safemath"])
 def test_checker_is_sound_exhaustively(shape):
     """Every state the checker re-proves UNSAT has no model over all assignments of its
     variables (and UF application values), and it re-proves a real share of them."""
-    rng = np.random.default_rng({"random": 0xC4EC, "transfer": 0x7A5F, "refund": 0x4EF0, "ratio": 0x2A71, "injective": 0x1A1, "mul": 0x30DE}[shape])
+    rng = np.random.default_rng({"random": 0xC4EC, "transfer": 0x7A5F, "refund": 0x4EF0, "ratio": 0x2A71, "injective": 0x1A1, "mul": 0x30DE, "safemath": 0x5AFE}[shape])
     if shape == "random":
         states = [(_random_small_dag(rng, w=4, n_ops=int(rng.integers(4, 14))), 2, 4) for _ in range(300)]
     elif shape == "transfer":
@@ -62,8 +88,10 @@ def test_checker_is_sound_exhaustively(shape):
         states = [(_ratio_state(rng), 2, 8) for _ in range(150)]
     elif shape == "injective":   # keccak applications with the manager's inverse axiom
         states = [(_injective_state(rng), 6, 3) for _ in range(150)]
-    else:   # products by constants, wrapping (BECToken's cnt * value)
+    elif shape == "mul":   # products by constants, wrapping (BECToken's cnt * value)
         states = [(_random_mul_dag(rng, 6), 2, 6) for _ in range(300)]
+    else:
+        states = [(_safemath_state(rng), 2, 4) for _ in range(300)]
     proved = 0
     for st, n_vars, w in states:
         if RC.refute([_terms(*st)], tiers=((2, 8, 20000),)):

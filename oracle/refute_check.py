@@ -340,6 +340,9 @@ class Checker:
                 return (a[0] // b[1], a[1] // b[0], 0, 0)
             return _top(w)
         if op == S.UREM:
+            if _is_exact(b) and b[0] and not b[0] & (b[0] - 1):   # x % 2^k = x & (2^k - 1)
+                k = b[0] - 1
+                return (0, min(a[1], k), (a[2] & k) | (m & ~k), a[3] & k)
             if b[0] > 0:
                 return (0, min(a[1], b[1] - 1), 0, 0)
             return (0, a[1], 0, 0)
@@ -572,6 +575,10 @@ class Checker:
             for x, y in ((0, 1), (1, 0)):
                 o = av[ar[y]]
                 self._set(ar[x], (v[0], m, v[2] & o[3], v[3]), work)
+            return
+        if op == S.UREM and _is_exact(b) and b[0] and not b[0] & (b[0] - 1):
+            k = b[0] - 1   # x % 2^k: the low k bits of x are the result's
+            self._set(ar[0], (0, m, v[2] & k, v[3] & k), work)
             return
         if op == S.OR:
             for x, y in ((0, 1), (1, 0)):

@@ -1,6 +1,6 @@
 """Replay every refutation of the restated suite with the independent checker.
 
-    python scripts/replay_refutations.py [out.json] [--workers N] [--tier1]
+    python scripts/replay_refutations.py [out.json] [--workers N] [--tier1] [--contracts a,b]
 
 For every query of corpus.suite() (all 13 contracts) that the product's split refuter refutes
 at the product's settings (mgp_refute_split, Prefilter.SPLIT_REFUTE / SPLIT_DEPTH), the
@@ -40,7 +40,8 @@ def _one(k):
 
 def main():
     global _CORES, _TIERS
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    args = [a for k, a in enumerate(sys.argv[1:]) if not a.startswith("--")
+            and sys.argv[k] not in ("--workers", "--contracts")]
     out_path = args[0] if args else "profiles/refute_replay_r6.json"
     workers = 7
     if "--workers" in sys.argv:
@@ -48,7 +49,10 @@ def main():
     if "--tier1" in sys.argv:   # the cheap search alone (a quick look)
         _TIERS = RC.TIERS[:1]
     t0 = time.perf_counter()
-    qs = corpus.suite(hasher=keccak256)
+    names = None
+    if "--contracts" in sys.argv:   # a subset of the suite (a quick look)
+        names = set(sys.argv[sys.argv.index("--contracts") + 1].split(","))
+    qs = corpus.suite(hasher=keccak256, contracts=names)
     B = F.Batch([list(q[3]) for q in qs])
     p = B.packed()[:4]
     split = N.refute_split(*p, max_splits=Prefilter.SPLIT_REFUTE, depth=Prefilter.SPLIT_DEPTH)

@@ -52,6 +52,9 @@ NVGPR = (VD + 1 + 7) // 8 * 8   # 128 with the 10-position bank (4 waves/SIMD); 
 POOL_PREFETCH_LINES = int(os.environ.get("MGP_POOL_PF", "4"))
 POOL_PREFETCH_CHUNK = bool(int(os.environ.get("MGP_POOL_PF_CHUNK", "0")))   # again at each chunk
 HALIGN = int(os.environ.get("MGP_HALIGN", "2"))   # log2 byte alignment of handler entries
+# diagnostic builds only (A/B of the VALU cost of the dispatch reads): extra v_readlane per uop
+# dispatch into the dead temporary s48; 0 in every shipped build
+EXTRA_READLANES = int(os.environ.get("MGP_EXTRA_RL", "0"))
 # division registers inside T
 D_FA, D_FB = 32, 34          # f64 pairs: dividend / reciprocal, divisor / estimate
 D_M = 36                     # v36 carry into the next product, v37 = 0 (64-bit mad addend)
@@ -166,6 +169,8 @@ def first_fields():
 def tail():
     """Make the prefetched uop current (s21 = its lane, s17 = its w1) and jump to its first
     handler."""
+    for _ in range(EXTRA_READLANES):
+        A(f"v_readlane_b32 s48, {v(PG + 2)}, s3")
     A("s_mov_b32 s21, s3",
       "s_mov_b32 s17, s16",
       "s_setpc_b64 s[0:1]")
